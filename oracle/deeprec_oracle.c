@@ -1,0 +1,980 @@
+/*
+ * deeprec_oracle.c -- CPU restatement of DeepRec's CPU EmbeddingVariable hot
+ * path.  TEST INFRASTRUCTURE ONLY: it is the parity checker for the HIP
+ * engine and the timed "cpu_baseline" leg of bench.py (kind "port").  Nothing
+ * in the shipped engine (deeprec-1_amd/) may link, load or call this file.
+ *
+ * Parity pinning: the reference (a TensorFlow 1.15 fork built with Bazel and
+ * network-fetched deps) cannot be compiled or imported in this container
+ * (SURVEY.md section 8c), so this restatement is pinned against the
+ * reference's own golden vectors / KATs committed under tests/golden/
+ * (fused_embedding_local_ops_test.cc, segment_reduction_ali_ops_test.cc,
+ * fused_embedding_ops_test.cc, embedding_variable_ops_test.py).
+ *
+ * Every function cites the reference file:line whose semantics it restates
+ * (paths relative to the reference root).  Association order of fp32 sums is
+ * replayed exactly where the reference fixes it, so the HIP engine can be
+ * checked bit-exactly.
+ *
+ * Build: see oracle/Makefile (gcc -O2 -ffp-contract=off -fPIC -shared -pthread).
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORC_OK 0
+#define ORC_INVALID_ARGUMENT 3
+#define ORC_NOT_FOUND 5
+#define ORC_RESOURCE_EXHAUSTED 8
+
+/* ------------------------------------------------------------------------ */
+/* Unique with first-occurrence order.                                       */
+/* unique_ali_op_util.h:192-222 (SerialComputeV1): y[j] = j-th distinct key  */
+/* in order of first appearance, idx[i] = position of x[i] in y.  Counts are */
+/* UniqueWithCounts (unique_ali_op.cc:137-180).                              */
+/* ------------------------------------------------------------------------ */
+static uint64_t orc_mix64(uint64_t k) {
+  k ^= k >> 33; k *= 0xff51afd7ed558ccdULL;
+  k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ULL;
+  k ^= k >> 33;
+  return k;
+}
+
+int64_t orc_unique(const int64_t* x, int64_t n, int64_t* y, int32_t* idx,
+                   int32_t* counts) {
+  if (n <= 0) return 0;
+  int64_t cap = 16;
+  while (cap < 2 * n) cap <<= 1;
+  int64_t* slot = (int64_t*)malloc(sizeof(int64_t) * cap); /* -> y index */
+  for (int64_t s = 0; s < cap; ++s) slot[s] = -1;
+  int64_t u = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    uint64_t h = orc_mix64((uint64_t)x[i]) & (uint64_t)(cap - 1);
+    for (;;) {
+      int64_t j = slot[h];
+      if (j < 0) {
+        slot[h] = u;
+        y[u] = x[i];
+        if (counts) counts[u] = 0;
+        j = u++;
+      }
+      if (y[j] == x[i]) {
+        idx[i] = (int32_t)j;
+        if (counts) counts[j] += 1;
+        break;
+      }
+      h = (h + 1) & (uint64_t)(cap - 1);
+    }
+  }
+  free(slot);
+  return u;
+}
+
+/* ------------------------------------------------------------------------ */
+/* SparseSegment{Sum,Mean,SqrtN}[WithNumSegments], CPU ali kernel.           */
+/* segment_reduction_ali_ops_util.h:30-177 (Reduce driver) and :193-318      */
+/* (row reducer).  Association order per output row, num = bag length:      */
+/*   num == 1 : out = L0                                                     */
+/*   else     : r = num % 8 (0 -> 8, 1 -> 9);                                 */
+/*              out = (((L0 + L1) + L2) ... + L_{r-1}) / m                   */
+/*              (m = num, sqrt(num) for mean/sqrtn when num < 10, else 1)     */
+/*              then for each further group of 8:                            */
+/*              out += (((L_r + L_{r+1}) + ...) + L_{r+7})                   */
+/*              then out /= num (or sqrt(num)) when num >= 10.               */
+/* Missing segments are filled with 0 (default_value).                       */
+/* combiner: 0 sum, 1 mean, 2 sqrtn.                                          */
+/* ------------------------------------------------------------------------ */
+static void orc_reduce_bag(const float* data, int64_t D, const int32_t* idx,
+                           int64_t start, int64_t num, int combiner,
+                           float* out) {
+  if (num == 1) {
+    memcpy(out, data + (int64_t)idx[start] * D, sizeof(float) * D);
+    return;
+  }
+  int64_t r = num % 8;
+  if (r == 0) r = 8;
+  if (r == 1) r = 9;
+  float m = 1.0f;
+  if (combiner == 1 && num < 10) m = (float)num;
+  if (combiner == 2 && num < 10) m = (float)sqrt((double)num);
+  for (int64_t d = 0; d < D; ++d) {
+    float s = data[(int64_t)idx[start] * D + d];
+    for (int64_t k = 1; k < r; ++k) s = s + data[(int64_t)idx[start + k] * D + d];
+    out[d] = s / m;
+  }
+  for (int64_t g = r; g < num; g += 8) {
+    for (int64_t d = 0; d < D; ++d) {
+      float s = data[(int64_t)idx[start + g] * D + d];
+      for (int64_t k = 1; k < 8; ++k) s = s + data[(int64_t)idx[start + g + k] * D + d];
+      out[d] = out[d] + s;
+    }
+  }
+  if (num >= 10) {
+    float q = 1.0f;
+    if (combiner == 1) q = (float)num;
+    if (combiner == 2) q = (float)sqrt((double)num);
+    if (combiner != 0)
+      for (int64_t d = 0; d < D; ++d) out[d] = out[d] / q;
+  }
+}
+
+int orc_sparse_segment_reduce(const float* data, int64_t data_rows, int64_t D,
+                              const int32_t* idx, const int32_t* seg, int64_t n,
+                              int64_t num_segments, int combiner, float* out,
+                              int64_t* out_rows) {
+  int64_t last_plus_one = n > 0 ? (int64_t)seg[n - 1] + 1 : 0;
+  int64_t rows = num_segments >= 0 ? num_segments : last_plus_one;
+  if (num_segments >= 0 && rows < last_plus_one) return ORC_INVALID_ARGUMENT;
+  if (out_rows) *out_rows = rows;
+  if (!out) return ORC_OK;
+  memset(out, 0, sizeof(float) * rows * D);
+  int64_t start = 0;
+  while (start < n) {
+    int32_t s = seg[start];
+    if (s < 0 || s >= rows) return ORC_INVALID_ARGUMENT;
+    int64_t end = start + 1;
+    while (end < n && seg[end] == s) ++end;
+    if (end < n && seg[end] < s) return ORC_INVALID_ARGUMENT; /* not increasing */
+    for (int64_t k = start; k < end; ++k)
+      if (idx[k] < 0 || idx[k] >= data_rows) return ORC_INVALID_ARGUMENT;
+    orc_reduce_bag(data, D, idx, start, end - start, combiner, out + (int64_t)s * D);
+    start = end;
+  }
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* SparseSegment{Mean,SqrtN}Grad CPU: segment_reduction_ali_ops_util.h:331-458 */
+/* out[idx[i]] (=|+=) grad[seg[i]] * scale, i ascending, scale =             */
+/* float(1/double(cnt)) or float(1/sqrt(double(cnt))); cnt==1 -> no scale.    */
+/* is_sqrtn: 0 mean, 1 sqrtn.  (Sum grad = unsorted_segment_sum of the        */
+/* gathered grad, math_grad.py:321-327; see orc_sparse_segment_sum_grad.)    */
+/* ------------------------------------------------------------------------ */
+int orc_sparse_segment_reduce_grad(const float* grad, int64_t grad_rows,
+                                   int64_t D, const int32_t* idx,
+                                   const int32_t* seg, int64_t n,
+                                   int64_t out_rows, int is_sqrtn, float* out) {
+  memset(out, 0, sizeof(float) * out_rows * D);
+  if (out_rows == 0 || n == 0) return ORC_OK;
+  if ((int64_t)seg[n - 1] + 1 > grad_rows) return ORC_INVALID_ARGUMENT;
+  int32_t* cnt = (int32_t*)calloc((size_t)n, sizeof(int32_t));
+  unsigned char* touched = (unsigned char*)calloc((size_t)out_rows, 1);
+  int64_t start = 0;
+  while (start < n) {
+    int64_t end = start + 1;
+    while (end < n && seg[end] == seg[start]) ++end;
+    if (seg[start] < 0 || seg[start] >= grad_rows) { free(cnt); free(touched); return ORC_INVALID_ARGUMENT; }
+    for (int64_t k = start; k < end; ++k) cnt[k] = (int32_t)(end - start);
+    start = end;
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    int32_t o = idx[i];
+    if (o < 0 || o >= out_rows) { free(cnt); free(touched); return ORC_INVALID_ARGUMENT; }
+    const float* g = grad + (int64_t)seg[i] * D;
+    float* dst = out + (int64_t)o * D;
+    if (cnt[i] == 1) {
+      if (touched[o]) for (int64_t d = 0; d < D; ++d) dst[d] = dst[d] + g[d];
+      else memcpy(dst, g, sizeof(float) * D);
+    } else {
+      float scale = is_sqrtn ? (float)(1.0 / sqrt((double)cnt[i]))
+                             : (float)(1.0 / (double)cnt[i]);
+      if (touched[o]) for (int64_t d = 0; d < D; ++d) { float p = g[d] * scale; dst[d] = dst[d] + p; }
+      else for (int64_t d = 0; d < D; ++d) dst[d] = g[d] * scale;
+    }
+    touched[o] = 1;
+  }
+  free(cnt);
+  free(touched);
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* UnsortedSegmentSum CPU: segment_reduction_ops.cc:377-405.  out = 0, then  */
+/* out[seg[i]] += data[i] for i ascending; seg < 0 is skipped.               */
+/* ------------------------------------------------------------------------ */
+int orc_unsorted_segment_sum(const float* data, int64_t n, int64_t D,
+                             const int32_t* seg, int64_t num_segments,
+                             float* out) {
+  memset(out, 0, sizeof(float) * num_segments * D);
+  for (int64_t i = 0; i < n; ++i) {
+    int32_t j = seg[i];
+    if (j < 0) continue;
+    if (j >= num_segments) return ORC_INVALID_ARGUMENT;
+    for (int64_t d = 0; d < D; ++d) out[(int64_t)j * D + d] = out[(int64_t)j * D + d] + data[i * D + d];
+  }
+  return ORC_OK;
+}
+
+/* Sum grad: unsorted_segment_sum(gather(grad, seg), idx, U)                 */
+/* (python/ops/math_grad.py:321-327), fused without materialising the gather. */
+int orc_sparse_segment_sum_grad(const float* grad, int64_t grad_rows, int64_t D,
+                                const int32_t* idx, const int32_t* seg,
+                                int64_t n, int64_t out_rows, float* out) {
+  memset(out, 0, sizeof(float) * out_rows * D);
+  for (int64_t i = 0; i < n; ++i) {
+    int32_t j = idx[i];
+    if (j < 0) continue;
+    if (j >= out_rows || seg[i] < 0 || seg[i] >= grad_rows) return ORC_INVALID_ARGUMENT;
+    for (int64_t d = 0; d < D; ++d)
+      out[(int64_t)j * D + d] = out[(int64_t)j * D + d] + grad[(int64_t)seg[i] * D + d];
+  }
+  return ORC_OK;
+}
+
+/* Weighted path of embedding_lookup_sparse (embedding_ops.py:609-651):      */
+/* gather(emb, idx) * w then SegmentSum; mean divides by the segment sum of  */
+/* weights, sqrtn by sqrt(segment sum of w^2).  Sequential left-to-right sum  */
+/* (the reference's Eigen reduction order is not pinned: tolerance-checked). */
+int orc_weighted_segment_reduce(const float* emb, int64_t D, const int32_t* idx,
+                                const float* w, const int32_t* seg, int64_t n,
+                                int64_t num_segments, int combiner, float* out) {
+  memset(out, 0, sizeof(float) * num_segments * D);
+  float* wsum = (float*)calloc((size_t)(num_segments > 0 ? num_segments : 1), sizeof(float));
+  for (int64_t i = 0; i < n; ++i) {
+    int32_t s = seg[i];
+    if (s < 0 || s >= num_segments) { free(wsum); return ORC_INVALID_ARGUMENT; }
+    float wi = w[i];
+    for (int64_t d = 0; d < D; ++d) {
+      float p = emb[(int64_t)idx[i] * D + d] * wi;
+      out[(int64_t)s * D + d] = out[(int64_t)s * D + d] + p;
+    }
+    wsum[s] = wsum[s] + (combiner == 2 ? wi * wi : wi);
+  }
+  if (combiner != 0) {
+    for (int64_t s = 0; s < num_segments; ++s) {
+      float q = combiner == 2 ? sqrtf(wsum[s]) : wsum[s];
+      for (int64_t d = 0; d < D; ++d) out[s * D + d] = out[s * D + d] / q;
+    }
+  }
+  free(wsum);
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Dense-table gather (GatherFunctorCPU / HandleCopies, gather_functor.h:36- */
+/* 115): out[i] = table[idx[i]]; an out-of-range index is an error.          */
+/* ------------------------------------------------------------------------ */
+int orc_gather(const float* table, int64_t rows, int64_t D, const int64_t* idx,
+               int64_t n, float* out) {
+  for (int64_t i = 0; i < n; ++i) {
+    if (idx[i] < 0 || idx[i] >= rows) return ORC_INVALID_ARGUMENT;
+    memcpy(out + i * D, table + idx[i] * D, sizeof(float) * D);
+  }
+  return ORC_OK;
+}
+
+/* clip_by_norm as used by embedding_ops._clip (embedding_ops.py:42-91 ->    */
+/* clip_ops.clip_by_norm): x * max_norm / max(l2norm, max_norm).             */
+void orc_clip_rows(float* rows, int64_t n, int64_t D, float max_norm) {
+  for (int64_t i = 0; i < n; ++i) {
+    float* r = rows + i * D;
+    float l2sum = 0.0f;
+    for (int64_t d = 0; d < D; ++d) l2sum = l2sum + r[d] * r[d];
+    float l2norm = l2sum > 0.0f ? sqrtf(l2sum) : l2sum;
+    float den = l2norm > max_norm ? l2norm : max_norm;
+    for (int64_t d = 0; d < D; ++d) { float t = r[d] * max_norm; r[d] = t / den; }
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* FusedEmbeddingLocalSparseLookUp (fused_embedding_local_ops_gpu.cu.cc:41-84 */
+/* + combiner fused_embedding_common.cu.h:11-53): per bag, sequential sum of */
+/* rows (each clipped by max_norm/l2 when max_norm >= 0 and l2 > max_norm),  */
+/* then sqrtn: /sqrtf(n), mean: /n.  offsets = first nnz of each bag.         */
+/* Bags are given by row ids (sp_indices[:,0]) sorted ascending.             */
+/* ------------------------------------------------------------------------ */
+int orc_fused_local_lookup(const float* table, int64_t rows, int64_t D,
+                           const int64_t* values, const int64_t* row_ids,
+                           int64_t nnz, int64_t batch, int combiner,
+                           float max_norm, float* out, int32_t* offsets) {
+  for (int64_t b = 0; b < batch; ++b) offsets[b] = 0x7fffffff;
+  for (int64_t i = nnz - 1; i >= 0; --i) {
+    if (row_ids[i] < 0 || row_ids[i] >= batch) return ORC_INVALID_ARGUMENT;
+    offsets[row_ids[i]] = (int32_t)i;
+  }
+  float* e = (float*)malloc(sizeof(float) * (D > 0 ? D : 1));
+  for (int64_t b = 0; b < batch; ++b) {
+    int64_t off = offsets[b];
+    int64_t cnt = (b == batch - 1 ? nnz : offsets[b + 1]) - off;
+    for (int64_t d = 0; d < D; ++d) out[b * D + d] = 0.0f;
+    for (int64_t k = 0; k < cnt; ++k) {
+      int64_t v = values[off + k];
+      if (v < 0 || v >= rows) { free(e); return ORC_INVALID_ARGUMENT; }
+      memcpy(e, table + v * D, sizeof(float) * D);
+      if (max_norm >= 0.0f) {
+        float l2 = 0.0f;
+        for (int64_t d = 0; d < D; ++d) l2 = l2 + e[d] * e[d];
+        l2 = sqrtf(l2);
+        if (l2 > max_norm) for (int64_t d = 0; d < D; ++d) e[d] = e[d] * (max_norm / l2);
+      }
+      for (int64_t d = 0; d < D; ++d) out[b * D + d] = out[b * D + d] + e[d];
+    }
+    for (int64_t d = 0; d < D; ++d) {
+      if (combiner == 2) out[b * D + d] = out[b * D + d] / sqrtf((float)cnt);
+      else if (combiner == 1) out[b * D + d] = out[b * D + d] / (float)cnt;
+    }
+  }
+  free(e);
+  return ORC_OK;
+}
+
+/* FusedEmbeddingLocalSparseLookUpGrad (fused_embedding_local_ops_gpu.cu.cc: */
+/* 86-122): grad[nnz,D], row k of bag b = top_grad[b] combined (/sqrtf(n),   */
+/* /n), scaled by max_norm/l2 when max_norm > 0 and l2 > max_norm.           */
+int orc_fused_local_lookup_grad(const float* top_grad, const float* table,
+                                int64_t rows, int64_t D, const int64_t* values,
+                                const int32_t* offsets, int64_t nnz,
+                                int64_t batch, int combiner, float max_norm,
+                                float* grad_out) {
+  for (int64_t b = 0; b < batch; ++b) {
+    int64_t off = offsets[b];
+    int64_t cnt = (b == batch - 1 ? nnz : offsets[b + 1]) - off;
+    for (int64_t k = 0; k < cnt; ++k) {
+      int64_t v = values[off + k];
+      if (v < 0 || v >= rows) return ORC_INVALID_ARGUMENT;
+      float scale_clip = 1.0f;
+      int clip = 0;
+      if (max_norm > 0.0f) {
+        float l2 = 0.0f;
+        for (int64_t d = 0; d < D; ++d) l2 = l2 + table[v * D + d] * table[v * D + d];
+        l2 = sqrtf(l2);
+        if (l2 > max_norm) { clip = 1; scale_clip = max_norm / l2; }
+      }
+      for (int64_t d = 0; d < D; ++d) {
+        float g = top_grad[b * D + d];
+        if (combiner == 2) g = g / sqrtf((float)cnt);
+        else if (combiner == 1) g = g / (float)cnt;
+        if (clip) g = g * scale_clip;
+        grad_out[(off + k) * D + d] = g;
+      }
+    }
+  }
+  return ORC_OK;
+}
+
+/* FusedEmbeddingSparsePreLookUp partition step (fused_embedding_ops_gpus.  */
+/* cu.cc:158-310, "div" over partition_shapes): ids are stably sorted, then  */
+/* split by the cumulative row ranges of the partitions and rebased.  Writes */
+/* out_values (rebased ids) / out_pos (original nnz position) in partition   */
+/* order and part_sizes[num_partitions].                                      */
+int orc_fused_pre_lookup(const int64_t* values, int64_t nnz,
+                         const int64_t* part_rows, int64_t num_parts,
+                         int64_t* out_values, int64_t* out_pos,
+                         int64_t* part_sizes) {
+  int64_t* order = (int64_t*)malloc(sizeof(int64_t) * (nnz > 0 ? nnz : 1));
+  for (int64_t i = 0; i < nnz; ++i) order[i] = i;
+  /* stable insertion/merge sort by id */
+  for (int64_t w = 1; w < nnz; w *= 2) {
+    int64_t* tmp = (int64_t*)malloc(sizeof(int64_t) * nnz);
+    for (int64_t lo = 0; lo < nnz; lo += 2 * w) {
+      int64_t mid = lo + w < nnz ? lo + w : nnz;
+      int64_t hi = lo + 2 * w < nnz ? lo + 2 * w : nnz;
+      int64_t a = lo, b = mid, o = lo;
+      while (a < mid && b < hi) tmp[o++] = (values[order[b]] < values[order[a]]) ? order[b++] : order[a++];
+      while (a < mid) tmp[o++] = order[a++];
+      while (b < hi) tmp[o++] = order[b++];
+    }
+    memcpy(order, tmp, sizeof(int64_t) * nnz);
+    free(tmp);
+  }
+  int64_t base = 0, k = 0;
+  for (int64_t p = 0; p < num_parts; ++p) {
+    int64_t lim = base + part_rows[p];
+    int64_t c = 0;
+    while (k < nnz && values[order[k]] < lim) {
+      if (values[order[k]] < base) { free(order); return ORC_INVALID_ARGUMENT; }
+      out_values[k] = values[order[k]] - base;
+      out_pos[k] = order[k];
+      ++k; ++c;
+    }
+    part_sizes[p] = c;
+    base = lim;
+  }
+  free(order);
+  return k == nnz ? ORC_OK : ORC_INVALID_ARGUMENT;
+}
+
+/* ------------------------------------------------------------------------ */
+/* EmbeddingVariable.                                                        */
+/*  - key -> ValuePtr map shared by primary and slot EVs                     */
+/*    (kernels/kv_variable_ops.cc:232-238, embedding_var.h:320-339)          */
+/*  - per key: version, freq, one row per emb_index allocated on first touch */
+/*    by copying the caller's default (value_ptr.h:145-170)                  */
+/*  - filters: Nullable / Counter / Bloom (embedding_filter.h:27-396)        */
+/* ------------------------------------------------------------------------ */
+#define ORC_MAX_COLS 8
+
+typedef struct {
+  int64_t key;
+  int64_t version;
+  int64_t freq;
+  float* rows[ORC_MAX_COLS];
+} orc_entry;
+
+typedef struct {
+  int64_t cap;       /* hash slots, power of two */
+  int64_t* slot;     /* -> entry index, -1 empty */
+  orc_entry* ent;
+  int64_t n_ent, ent_cap;
+  int refs;
+} orc_map;
+
+typedef struct {
+  orc_map* map;
+  int64_t dim;
+  int emb_index;
+  int primary;
+  float* default_value;
+  int64_t filter_freq, steps_to_live;
+  /* bloom */
+  int64_t k_hash, num_counter;
+  int counter_bits;
+  void* bloom;
+  int64_t seeds[64];
+} orc_ev;
+
+static orc_map* orc_map_new(void) {
+  orc_map* m = (orc_map*)calloc(1, sizeof(orc_map));
+  m->cap = 1024;
+  m->slot = (int64_t*)malloc(sizeof(int64_t) * m->cap);
+  for (int64_t i = 0; i < m->cap; ++i) m->slot[i] = -1;
+  m->ent_cap = 512;
+  m->ent = (orc_entry*)calloc((size_t)m->ent_cap, sizeof(orc_entry));
+  m->refs = 1;
+  return m;
+}
+
+static int64_t orc_map_find(orc_map* m, int64_t key) {
+  uint64_t h = orc_mix64((uint64_t)key) & (uint64_t)(m->cap - 1);
+  for (;;) {
+    int64_t e = m->slot[h];
+    if (e < 0) return -1;
+    if (m->ent[e].key == key) return e;
+    h = (h + 1) & (uint64_t)(m->cap - 1);
+  }
+}
+
+static void orc_map_grow(orc_map* m) {
+  int64_t ncap = m->cap * 2;
+  int64_t* ns = (int64_t*)malloc(sizeof(int64_t) * ncap);
+  for (int64_t i = 0; i < ncap; ++i) ns[i] = -1;
+  for (int64_t e = 0; e < m->n_ent; ++e) {
+    if (m->ent[e].key == INT64_MIN && m->ent[e].version == INT64_MIN) continue; /* removed */
+    uint64_t h = orc_mix64((uint64_t)m->ent[e].key) & (uint64_t)(ncap - 1);
+    while (ns[h] >= 0) h = (h + 1) & (uint64_t)(ncap - 1);
+    ns[h] = e;
+  }
+  free(m->slot);
+  m->slot = ns;
+  m->cap = ncap;
+}
+
+/* LookupOrCreateKeyInternal (embedding_var.h:320-339) */
+static int64_t orc_map_lookup_or_create(orc_map* m, int64_t key) {
+  int64_t e = orc_map_find(m, key);
+  if (e >= 0) return e;
+  if (2 * (m->n_ent + 1) > m->cap) orc_map_grow(m);
+  if (m->n_ent == m->ent_cap) {
+    m->ent_cap *= 2;
+    m->ent = (orc_entry*)realloc(m->ent, sizeof(orc_entry) * m->ent_cap);
+  }
+  e = m->n_ent++;
+  memset(&m->ent[e], 0, sizeof(orc_entry));
+  m->ent[e].key = key;
+  uint64_t h = orc_mix64((uint64_t)key) & (uint64_t)(m->cap - 1);
+  while (m->slot[h] >= 0) h = (h + 1) & (uint64_t)(m->cap - 1);
+  m->slot[h] = e;
+  return e;
+}
+
+/* BloomFilter::GenerateSeed (embedding_filter.h:252-279) */
+static void orc_bloom_seeds(orc_ev* ev) {
+  static const int64_t defaults[25] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41,
+                                       43, 47, 53, 59, 61, 67, 71, 73, 79, 83, 89, 97};
+  int64_t k = ev->k_hash > 64 ? 64 : ev->k_hash;
+  if (k < 25) {
+    for (int64_t i = 0; i < k; ++i) ev->seeds[i] = defaults[i];
+  } else {
+    for (int64_t i = 0; i < 25; ++i) ev->seeds[i] = defaults[i];
+    int64_t last = 98;
+    for (int64_t i = 25; i < k; ++i) {
+      for (int64_t j = last;; ++j) {
+        if (j % 2 == 0) continue;
+        int prime = 1;
+        /* the reference loop starts at k = 0 (j % 0 is UB); effectively it  */
+        /* tests divisors 2..sqrt(j)+1 -- restated that way.                 */
+        for (int64_t q = 2; q <= (int64_t)sqrt((double)j) + 1; ++q)
+          if (j % q == 0) { prime = 0; break; }
+        if (prime) { ev->seeds[i] = j; last = j; break; }
+      }
+    }
+  }
+}
+
+/* BloomFilter::FastHash64 (embedding_filter.h:134-148) */
+uint64_t orc_fasthash64(int64_t key, uint64_t seed) {
+  const uint64_t m = 0x880355f21e6d1965ULL;
+  uint64_t h = seed ^ (8 * m);
+  uint64_t v = (uint64_t)key;
+  v ^= v >> 23; v *= 0x2127599bf4325c37ULL; v ^= v >> 47;
+  h ^= v; h *= m;
+  v = 0;
+  v ^= v >> 23; v *= 0x2127599bf4325c37ULL; v ^= v >> 47;
+  h ^= v; h *= m;
+  h ^= h >> 23; h *= 0x2127599bf4325c37ULL; h ^= h >> 47;
+  return h;
+}
+
+static uint64_t orc_bloom_get(orc_ev* ev, int64_t c) {
+  switch (ev->counter_bits) {
+    case 8: return ((uint8_t*)ev->bloom)[c];
+    case 16: return ((uint16_t*)ev->bloom)[c];
+    case 32: return ((uint32_t*)ev->bloom)[c];
+    default: return ((uint64_t*)ev->bloom)[c];
+  }
+}
+static void orc_bloom_add(orc_ev* ev, int64_t c, int64_t count) {
+  switch (ev->counter_bits) {
+    case 8: ((uint8_t*)ev->bloom)[c] += (uint8_t)count; break;
+    case 16: ((uint16_t*)ev->bloom)[c] += (uint16_t)count; break;
+    case 32: ((uint32_t*)ev->bloom)[c] += (uint32_t)count; break;
+    default: ((uint64_t*)ev->bloom)[c] += (uint64_t)count; break;
+  }
+}
+/* GetBloomFreq (embedding_filter.h:103-127): min over the k counters */
+int64_t orc_bloom_freq(orc_ev* ev, int64_t key) {
+  uint64_t mn = 0;
+  for (int64_t i = 0; i < ev->k_hash; ++i) {
+    int64_t c = (int64_t)(orc_fasthash64(key, (uint64_t)ev->seeds[i]) % (uint64_t)ev->num_counter);
+    uint64_t v = orc_bloom_get(ev, c);
+    if (i == 0 || v < mn) mn = v;
+  }
+  return (int64_t)mn;
+}
+/* AddFreq (embedding_filter.h:190-250): each counter below filter_freq += count */
+static void orc_bloom_addfreq(orc_ev* ev, int64_t key, int64_t count) {
+  for (int64_t i = 0; i < ev->k_hash; ++i) {
+    int64_t c = (int64_t)(orc_fasthash64(key, (uint64_t)ev->seeds[i]) % (uint64_t)ev->num_counter);
+    if ((int64_t)orc_bloom_get(ev, c) < ev->filter_freq) orc_bloom_add(ev, c, count);
+  }
+}
+
+/* EmbeddingConfig::calc_num_hash_func / calc_num_counter (embedding_config.h:63-70) */
+static void orc_bloom_params(int64_t max_element_size, float fpp, int64_t* k, int64_t* nc) {
+  float loghpp = fabsf((float)(log(fpp) / log(2)));
+  *k = (int64_t)ceil(loghpp);
+  float loghpp2 = fabsf((float)log(fpp));
+  float factor = (float)(log(2) * log(2));
+  *nc = (int64_t)ceil(loghpp2 / factor * max_element_size);
+}
+
+/* InitializeKvVariableOp primary branch (kernels/kv_variable_ops.cc:173-193). */
+orc_ev* orc_ev_create(int64_t dim, const float* default_row, int64_t filter_freq,
+                      int64_t steps_to_live, int64_t max_element_size,
+                      float false_positive_probability, int counter_bits) {
+  orc_ev* ev = (orc_ev*)calloc(1, sizeof(orc_ev));
+  ev->map = orc_map_new();
+  ev->dim = dim;
+  ev->emb_index = 0;
+  ev->primary = 1;
+  ev->default_value = (float*)malloc(sizeof(float) * dim);
+  memcpy(ev->default_value, default_row, sizeof(float) * dim);
+  ev->filter_freq = filter_freq < 0 ? 0 : filter_freq;
+  ev->steps_to_live = steps_to_live;
+  if (ev->filter_freq > 0 && max_element_size != 0 && false_positive_probability != -1.0f) {
+    orc_bloom_params(max_element_size, false_positive_probability, &ev->k_hash, &ev->num_counter);
+    ev->counter_bits = counter_bits ? counter_bits : 64;
+    ev->bloom = calloc((size_t)ev->num_counter, (size_t)(ev->counter_bits / 8));
+    orc_bloom_seeds(ev);
+  }
+  return ev;
+}
+
+/* Slot EV sharing the primary's key map (kernels/kv_variable_ops.cc:212-226): */
+/* emb_index = slot_index (block_num == 1), no filter of its own.             */
+orc_ev* orc_ev_create_slot(orc_ev* primary, int slot_index, const float* default_row) {
+  if (slot_index <= 0 || slot_index >= ORC_MAX_COLS) return NULL;
+  orc_ev* ev = (orc_ev*)calloc(1, sizeof(orc_ev));
+  ev->map = primary->map;
+  ev->map->refs++;
+  ev->dim = primary->dim;
+  ev->emb_index = slot_index;
+  ev->primary = 0;
+  ev->default_value = (float*)malloc(sizeof(float) * ev->dim);
+  memcpy(ev->default_value, default_row, sizeof(float) * ev->dim);
+  ev->steps_to_live = primary->steps_to_live;
+  return ev;
+}
+
+void orc_ev_free(orc_ev* ev) {
+  if (!ev) return;
+  if (--ev->map->refs == 0) {
+    for (int64_t e = 0; e < ev->map->n_ent; ++e)
+      for (int c = 0; c < ORC_MAX_COLS; ++c) free(ev->map->ent[e].rows[c]);
+    free(ev->map->ent);
+    free(ev->map->slot);
+    free(ev->map);
+  }
+  free(ev->bloom);
+  free(ev->default_value);
+  free(ev);
+}
+
+/* ValuePtr::GetOrAllocate (value_ptr.h:145-170) */
+static float* orc_get_or_alloc(orc_ev* ev, int64_t e, const float* default_v) {
+  orc_entry* en = &ev->map->ent[e];
+  if (!en->rows[ev->emb_index]) {
+    en->rows[ev->emb_index] = (float*)malloc(sizeof(float) * ev->dim);
+    memcpy(en->rows[ev->emb_index], default_v, sizeof(float) * ev->dim);
+  }
+  return en->rows[ev->emb_index];
+}
+
+/* KvResourceGather / KvResourceGatherV1 (kernels/kv_variable_ops.cc:314-449) */
+/* -> EmbeddingVar::LookupOrCreate -> filter_->LookupOrCreate                 */
+/* (Nullable :348-353, Counter :296-320, Bloom :56-82).                       */
+/* defaults: [n,D] per-index rows, or NULL for the EV's own default_value_.   */
+/* counts: NULL for V0 (count 1).                                             */
+int orc_ev_gather(orc_ev* ev, const int64_t* keys, int64_t n,
+                  const float* defaults, const int32_t* counts, float* out) {
+  const int64_t D = ev->dim;
+  for (int64_t i = 0; i < n; ++i) {
+    const float* dv = defaults ? defaults + i * D : ev->default_value;
+    int64_t cnt = counts ? counts[i] : 1;
+    if (ev->filter_freq == 0) {                      /* NullableFilter */
+      int64_t e = orc_map_lookup_or_create(ev->map, keys[i]);
+      memcpy(out + i * D, orc_get_or_alloc(ev, e, dv), sizeof(float) * D);
+    } else if (ev->k_hash == 0) {                    /* CounterFilter */
+      int64_t e = orc_map_lookup_or_create(ev->map, keys[i]);
+      orc_entry* en = &ev->map->ent[e];
+      if (en->freq >= ev->filter_freq) {
+        memcpy(out + i * D, orc_get_or_alloc(ev, e, dv), sizeof(float) * D);
+      } else {
+        en->freq += cnt;
+        memcpy(out + i * D, dv, sizeof(float) * D);
+      }
+    } else {                                         /* BloomFilter */
+      if (orc_bloom_freq(ev, keys[i]) >= ev->filter_freq) {
+        int64_t e = orc_map_lookup_or_create(ev->map, keys[i]);
+        memcpy(out + i * D, orc_get_or_alloc(ev, e, dv), sizeof(float) * D);
+      } else {
+        orc_bloom_addfreq(ev, keys[i], cnt);
+        memcpy(out + i * D, dv, sizeof(float) * D);
+      }
+    }
+  }
+  return ORC_OK;
+}
+
+/* EmbeddingVar::Import (embedding_var.h:187-219), the semantics the build   */
+/* gives KvResourceInsert / KvResourceImportV2.  partition_num <= 0 disables */
+/* the `key % bucket_num % partition_num == partition_id` filter.            */
+int orc_ev_import(orc_ev* ev, const int64_t* keys, int64_t n, const float* values,
+                  const int64_t* versions, const int64_t* freqs,
+                  int64_t bucket_num, int64_t partition_id, int64_t partition_num) {
+  const int64_t D = ev->dim;
+  for (int64_t i = 0; i < n; ++i) {
+    if (partition_num > 0 && keys[i] % bucket_num % partition_num != partition_id) continue;
+    int64_t e = orc_map_lookup_or_create(ev->map, keys[i]);
+    orc_entry* en = &ev->map->ent[e];
+    if (ev->primary) {
+      if (ev->filter_freq != 0) {
+        int64_t f = freqs ? freqs[i] : 0;
+        en->freq = f <= ev->filter_freq ? ev->filter_freq : f;
+      }
+      if (ev->steps_to_live != 0) en->version = versions ? versions[i] : 0;
+    }
+    orc_get_or_alloc(ev, e, values + i * D);
+  }
+  return ORC_OK;
+}
+
+int64_t orc_ev_size(orc_ev* ev) { return ev->map->n_ent; }
+
+/* EmbeddingVar::GetSnapshot (embedding_var.h:221-243) -> KvResourceExport:  */
+/* keys whose own row and primary row exist; freqs if filter_freq != 0,      */
+/* versions if steps_to_live != 0.  Iteration order of the reference's hash  */
+/* map is unpinned; this restatement emits keys in ascending order.          */
+int64_t orc_ev_export(orc_ev* ev, int64_t* keys, float* values, int64_t* versions,
+                      int64_t* freqs) {
+  orc_map* m = ev->map;
+  int64_t* order = (int64_t*)malloc(sizeof(int64_t) * (m->n_ent > 0 ? m->n_ent : 1));
+  int64_t k = 0;
+  for (int64_t e = 0; e < m->n_ent; ++e)
+    if (m->ent[e].rows[ev->emb_index] && m->ent[e].rows[0]) order[k++] = e;
+  /* insertion sort is fine for test sizes; use qsort-like shell sort */
+  for (int64_t gap = k / 2; gap > 0; gap /= 2)
+    for (int64_t i = gap; i < k; ++i)
+      for (int64_t j = i; j >= gap && m->ent[order[j - gap]].key > m->ent[order[j]].key; j -= gap) {
+        int64_t t = order[j]; order[j] = order[j - gap]; order[j - gap] = t;
+      }
+  for (int64_t i = 0; i < k; ++i) {
+    orc_entry* en = &m->ent[order[i]];
+    if (keys) keys[i] = en->key;
+    if (values) memcpy(values + i * ev->dim, en->rows[ev->emb_index], sizeof(float) * ev->dim);
+    if (versions) versions[i] = en->version;
+    if (freqs) freqs[i] = ev->k_hash ? orc_bloom_freq(ev, en->key) : en->freq;
+  }
+  free(order);
+  return k;
+}
+
+int64_t orc_ev_freq(orc_ev* ev, int64_t key) {
+  if (ev->k_hash) return orc_bloom_freq(ev, key);
+  int64_t e = orc_map_find(ev->map, key);
+  return e < 0 ? 0 : ev->map->ent[e].freq;
+}
+int64_t orc_ev_version(orc_ev* ev, int64_t key) {
+  int64_t e = orc_map_find(ev->map, key);
+  return e < 0 ? -1 : ev->map->ent[e].version;
+}
+int orc_ev_has_row(orc_ev* ev, int64_t key) {
+  int64_t e = orc_map_find(ev->map, key);
+  return e >= 0 && ev->map->ent[e].rows[ev->emb_index] != NULL;
+}
+
+/* filter_->LookupOrCreateKey with update_version (embedding_var.h:109-121,  */
+/* embedding_filter.h:322-326,355-359,84-93).  Returns the entry or -1 when  */
+/* filtered (is_filter == false).                                             */
+static int64_t orc_apply_key(orc_ev* var, int64_t key, int64_t gs) {
+  if (var->k_hash) {
+    if (orc_bloom_freq(var, key) < var->filter_freq) return -1;
+  }
+  int64_t e = orc_map_lookup_or_create(var->map, key);
+  if (var->primary && var->steps_to_live != 0 && gs != -1) var->map->ent[e].version = gs;
+  if (!var->k_hash && var->filter_freq > 0 && var->map->ent[e].freq < var->filter_freq) return -1;
+  return e;
+}
+
+/* KvResourceSparseApplyGradientDescent (training_ali_ops.cc:1597-1678):     */
+/* v -= lr * g                                                                */
+int orc_ev_apply_sgd(orc_ev* var, float lr, const float* grad, const int64_t* keys,
+                     int64_t n, int64_t gs) {
+  const int64_t D = var->dim;
+  for (int64_t i = 0; i < n; ++i) {
+    int64_t e = orc_apply_key(var, keys[i], gs);
+    if (e < 0) continue;
+    float* v = orc_get_or_alloc(var, e, var->default_value);
+    for (int64_t d = 0; d < D; ++d) { float p = lr * grad[i * D + d]; v[d] = v[d] - p; }
+  }
+  return ORC_OK;
+}
+
+/* KvSparseApplyAdagrad (training_ali_ops.cc:61-145):                        */
+/* a += g*g; v -= (lr * g) * rsqrt(a)                                         */
+int orc_ev_apply_adagrad(orc_ev* var, orc_ev* accum, float lr, const float* grad,
+                         const int64_t* keys, int64_t n, int64_t gs) {
+  const int64_t D = var->dim;
+  for (int64_t i = 0; i < n; ++i) {
+    int64_t e = orc_apply_key(var, keys[i], gs);
+    if (e < 0) continue;
+    float* a = orc_get_or_alloc(accum, e, accum->default_value);
+    float* v = orc_get_or_alloc(var, e, var->default_value);
+    for (int64_t d = 0; d < D; ++d) {
+      float g = grad[i * D + d];
+      float g2 = g * g;
+      a[d] = a[d] + g2;
+      float lg = lr * g;
+      float rs = 1.0f / sqrtf(a[d]);
+      float up = lg * rs;
+      v[d] = v[d] - up;
+    }
+  }
+  return ORC_OK;
+}
+
+/* KvSparseApplyAdam (training_ali_ops.cc:848-975):                          */
+/* alpha = lr*sqrt(1-b2^t)/(1-b1^t); m += (g-m)(1-b1); v += (g^2-v)(1-b2);     */
+/* var -= (m*alpha)/(sqrt(v)+eps)                                             */
+int orc_ev_apply_adam(orc_ev* var, orc_ev* m_ev, orc_ev* v_ev, float beta1_power,
+                      float beta2_power, float lr, float beta1, float beta2,
+                      float eps, const float* grad, const int64_t* keys, int64_t n,
+                      int64_t gs) {
+  const int64_t D = var->dim;
+  const float alpha = lr * sqrtf(1.0f - beta2_power) / (1.0f - beta1_power);
+  for (int64_t i = 0; i < n; ++i) {
+    int64_t e = orc_apply_key(var, keys[i], gs);
+    if (e < 0) continue;
+    float* w = orc_get_or_alloc(var, e, var->default_value);
+    float* m = orc_get_or_alloc(m_ev, e, m_ev->default_value);
+    float* v = orc_get_or_alloc(v_ev, e, v_ev->default_value);
+    for (int64_t d = 0; d < D; ++d) {
+      float g = grad[i * D + d];
+      float t1 = g - m[d]; t1 = t1 * (1.0f - beta1); m[d] = m[d] + t1;
+      float t2 = g * g; t2 = t2 - v[d]; t2 = t2 * (1.0f - beta2); v[d] = v[d] + t2;
+      float num = m[d] * alpha;
+      float den = sqrtf(v[d]) + eps;
+      w[d] = w[d] - num / den;
+    }
+  }
+  return ORC_OK;
+}
+
+/* Dense-variable counterparts (ResourceSparseApply*, training_ops.cc),      */
+/* used by the EV == dense 5-step equality idiom                              */
+/* (embedding_variable_ops_test.py:825-997).  Rows indexed directly.          */
+int orc_dense_apply_sgd(float* table, int64_t D, float lr, const float* grad,
+                        const int64_t* idx, int64_t n) {
+  for (int64_t i = 0; i < n; ++i)
+    for (int64_t d = 0; d < D; ++d) { float p = grad[i * D + d] * lr; table[idx[i] * D + d] -= p; }
+  return ORC_OK;
+}
+int orc_dense_apply_adagrad(float* table, float* accum, int64_t D, float lr,
+                            const float* grad, const int64_t* idx, int64_t n) {
+  for (int64_t i = 0; i < n; ++i)
+    for (int64_t d = 0; d < D; ++d) {
+      float g = grad[i * D + d];
+      float g2 = g * g;
+      accum[idx[i] * D + d] += g2;
+      float lg = g * lr;
+      float rs = 1.0f / sqrtf(accum[idx[i] * D + d]);
+      float up = lg * rs;
+      table[idx[i] * D + d] -= up;
+    }
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Interactions (callers of the path).                                       */
+/* ------------------------------------------------------------------------ */
+/* FM 2nd order (modelzoo/DeepFM/train.py:205-209):                          */
+/* out[b,d] = 0.5 * ((sum_f e)^2 - sum_f e^2), accumulated in double.         */
+void orc_fm2(const float* emb, int64_t B, int64_t F, int64_t D, float* out) {
+  for (int64_t b = 0; b < B; ++b)
+    for (int64_t d = 0; d < D; ++d) {
+      double s = 0.0, q = 0.0;
+      for (int64_t f = 0; f < F; ++f) {
+        double e = emb[(b * F + f) * D + d];
+        s += e; q += e * e;
+      }
+      out[b * D + d] = (float)(0.5 * (s * s - q));
+    }
+}
+
+/* DLRM dot interaction (modelzoo/DLRM/train.py:150-163): strictly-lower    */
+/* triangle of X X^T in row-major (i>j) order, X = [B, F, D]; double accum.  */
+void orc_dot_interaction(const float* x, int64_t B, int64_t F, int64_t D, float* out) {
+  int64_t P = F * (F - 1) / 2;
+  for (int64_t b = 0; b < B; ++b) {
+    int64_t p = 0;
+    for (int64_t i = 0; i < F; ++i)
+      for (int64_t j = 0; j < i; ++j) {
+        double s = 0.0;
+        for (int64_t d = 0; d < D; ++d) s += (double)x[(b * F + i) * D + d] * (double)x[(b * F + j) * D + d];
+        out[b * P + p++] = (float)s;
+      }
+  }
+}
+
+/* DCN-v2 CrossNet layer (absent from the reference; build-defined spec):    */
+/* x_{l+1} = x0 * (W x_l + b) + x_l, W [d, d] row-major (out, in); double.    */
+void orc_crossnet_layer(const float* x0, const float* xl, const float* W, const float* bias,
+                        int64_t B, int64_t d, float* out) {
+  for (int64_t r = 0; r < B; ++r)
+    for (int64_t o = 0; o < d; ++o) {
+      double s = bias ? bias[o] : 0.0;
+      for (int64_t k = 0; k < d; ++k) s += (double)W[o * d + k] * (double)xl[r * d + k];
+      out[r * d + o] = (float)((double)x0[r * d + o] * s + (double)xl[r * d + o]);
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Threaded CPU pipeline for bench.py's cpu_baseline leg: the DeepRec CPU    */
+/* composition of embedding_lookup_sparse over an EV (embedding_ops.py:      */
+/* 587-664): Unique (serial) -> KvResourceGather (Shard over all threads,    */
+/* kv_variable_ops.cc:360-362) -> SparseSegmentReduction (Shard over         */
+/* threads-1 over output rows, segment_reduction_ali_ops_util.h:173-174).    */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  orc_ev* ev;
+  const int64_t* keys;
+  float* out;
+  int64_t lo, hi;
+  const float* data; const int32_t* idx; const int32_t* seg_off; int combiner;
+  const float* table; const int64_t* rows;
+} orc_task;
+
+static void* orc_gather_worker(void* p) {
+  orc_task* t = (orc_task*)p;
+  const int64_t D = t->ev->dim;
+  for (int64_t i = t->lo; i < t->hi; ++i) {
+    int64_t e = orc_map_find(t->ev->map, t->keys[i]);
+    const float* src = (e >= 0 && t->ev->map->ent[e].rows[0]) ? t->ev->map->ent[e].rows[0] : t->ev->default_value;
+    memcpy(t->out + i * D, src, sizeof(float) * D);
+  }
+  return NULL;
+}
+static void* orc_dense_gather_worker(void* p) {
+  orc_task* t = (orc_task*)p;
+  const int64_t D = t->combiner; /* reused field: D */
+  for (int64_t i = t->lo; i < t->hi; ++i)
+    memcpy(t->out + i * D, t->table + t->rows[i] * D, sizeof(float) * D);
+  return NULL;
+}
+static void* orc_reduce_worker(void* p) {
+  orc_task* t = (orc_task*)p;
+  const int64_t D = t->ev ? t->ev->dim : (int64_t)t->rows[0];
+  for (int64_t s = t->lo; s < t->hi; ++s) {
+    int64_t a = t->seg_off[s], b = t->seg_off[s + 1];
+    if (b > a) orc_reduce_bag(t->data, D, t->idx, a, b - a, t->combiner & 3, t->out + s * D);
+    else memset(t->out + s * D, 0, sizeof(float) * D);
+  }
+  return NULL;
+}
+
+static void orc_run_sharded(void* (*fn)(void*), orc_task* proto, int64_t total, int threads) {
+  if (threads < 1) threads = 1;
+  pthread_t th[256];
+  orc_task tk[256];
+  if (threads > 256) threads = 256;
+  for (int t = 0; t < threads; ++t) {
+    tk[t] = *proto;
+    tk[t].lo = total * t / threads;
+    tk[t].hi = total * (t + 1) / threads;
+    pthread_create(&th[t], NULL, fn, &tk[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+}
+
+/* Per-feature embedding_lookup_sparse over an EV; bags given by seg_off     */
+/* (CSR offsets over the batch, length B+1).  Workspace allocated inside.    */
+int orc_pipeline_ev_lookup_sparse(orc_ev* ev, const int64_t* ids, int64_t nnz,
+                                  const int32_t* seg_off, int64_t B, int combiner,
+                                  int threads, float* out) {
+  const int64_t D = ev->dim;
+  int64_t* uniq = (int64_t*)malloc(sizeof(int64_t) * (nnz > 0 ? nnz : 1));
+  int32_t* idx = (int32_t*)malloc(sizeof(int32_t) * (nnz > 0 ? nnz : 1));
+  int64_t U = orc_unique(ids, nnz, uniq, idx, NULL);
+  float* emb = (float*)malloc(sizeof(float) * (U > 0 ? U : 1) * D);
+  orc_task p;
+  memset(&p, 0, sizeof(p));
+  p.ev = ev; p.keys = uniq; p.out = emb;
+  orc_run_sharded(orc_gather_worker, &p, U, threads);
+  memset(&p, 0, sizeof(p));
+  p.ev = ev; p.data = emb; p.idx = idx; p.seg_off = seg_off; p.combiner = combiner; p.out = out;
+  orc_run_sharded(orc_reduce_worker, &p, B, threads > 1 ? threads - 1 : 1);
+  free(uniq); free(idx); free(emb);
+  return ORC_OK;
+}
+
+/* Same over a dense table (ResourceGather HandleCopies + ali reduce).       */
+int orc_pipeline_dense_lookup_sparse(const float* table, int64_t D, const int64_t* ids,
+                                     int64_t nnz, const int32_t* seg_off, int64_t B,
+                                     int combiner, int threads, float* out) {
+  int64_t* uniq = (int64_t*)malloc(sizeof(int64_t) * (nnz > 0 ? nnz : 1));
+  int32_t* idx = (int32_t*)malloc(sizeof(int32_t) * (nnz > 0 ? nnz : 1));
+  int64_t U = orc_unique(ids, nnz, uniq, idx, NULL);
+  float* emb = (float*)malloc(sizeof(float) * (U > 0 ? U : 1) * D);
+  orc_task p;
+  memset(&p, 0, sizeof(p));
+  p.table = table; p.rows = uniq; p.out = emb; p.combiner = (int)D;
+  orc_run_sharded(orc_dense_gather_worker, &p, U, threads);
+  int64_t dd = D;
+  memset(&p, 0, sizeof(p));
+  p.rows = &dd; p.data = emb; p.idx = idx; p.seg_off = seg_off; p.combiner = combiner; p.out = out;
+  orc_run_sharded(orc_reduce_worker, &p, B, threads > 1 ? threads - 1 : 1);
+  free(uniq); free(idx); free(emb);
+  return ORC_OK;
+}
