@@ -1,0 +1,100 @@
+// core.hip -- error reporting, device status word, synthetic table fill.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include <mutex>
+
+#include "dr_common.h"
+
+__device__ int g_dr_status;
+
+namespace dr {
+
+static thread_local char t_err[1024];
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(t_err, sizeof(t_err), fmt, ap);
+  va_end(ap);
+}
+
+int* status_word() {
+  static std::mutex mu;
+  static int* cache[64] = {nullptr};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  if (!cache[dev]) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_dr_status)) != hipSuccess) return nullptr;
+    cache[dev] = static_cast<int*>(p);
+  }
+  return cache[dev];
+}
+
+__global__ void fill_synth_kernel(float* __restrict__ t, int64_t rows, int dim, uint64_t seed) {
+  const int64_t total4 = rows * dim / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += stride) {
+    const int64_t e = i * 4;
+    float4 v;
+    v.x = synth(seed, (e + 0) / dim, (e + 0) % dim);
+    v.y = synth(seed, (e + 1) / dim, (e + 1) % dim);
+    v.z = synth(seed, (e + 2) / dim, (e + 2) % dim);
+    v.w = synth(seed, (e + 3) / dim, (e + 3) % dim);
+    reinterpret_cast<float4*>(t)[i] = v;
+  }
+}
+
+__global__ void fill_synth_tail_kernel(float* __restrict__ t, int64_t begin, int64_t end,
+                                       int dim, uint64_t seed) {
+  const int64_t e = begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < end) t[e] = synth(seed, e / dim, e % dim);
+}
+
+}  // namespace dr
+
+extern "C" {
+
+int dr_abi_version(void) { return 1; }
+
+const char* dr_last_error(void) { return dr::t_err; }
+
+int dr_status_check(void* stream) {
+  int* st = dr::status_word();
+  DR_REQUIRE(st != nullptr, DR_INTERNAL, "no device status word");
+  DR_HIP(hipStreamSynchronize(dr::S(stream)));
+  int v = 0;
+  DR_HIP(hipMemcpy(&v, st, sizeof(int), hipMemcpyDeviceToHost));
+  if (v != 0) {
+    int z = 0;
+    DR_HIP(hipMemcpy(st, &z, sizeof(int), hipMemcpyHostToDevice));
+    dr::set_error("device kernel latched status %d", v);
+  }
+  return v;
+}
+
+int dr_fill_synthetic(float* table, int64_t rows, int dim, uint64_t seed, void* stream) {
+  DR_REQUIRE(rows >= 0 && dim > 0, DR_INVALID_ARGUMENT, "bad table shape");
+  DR_REQUIRE(((uintptr_t)table & 15) == 0, DR_INVALID_ARGUMENT, "table must be 16B aligned");
+  const int64_t total = rows * dim;
+  const int64_t total4 = total / 4;
+  if (total4 > 0) {
+    int64_t blocks = dr::ceil_div(total4, 256);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(dr::fill_synth_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                       dr::S(stream), table, rows, dim, seed);
+    DR_LAUNCH_CHECK();
+  }
+  if (total4 * 4 < total) {
+    hipLaunchKernelGGL(dr::fill_synth_tail_kernel, dim3(1), dim3(256), 0, dr::S(stream), table,
+                       total4 * 4, total, dim, seed);
+    DR_LAUNCH_CHECK();
+  }
+  return DR_OK;
+}
+
+float dr_synth_value(uint64_t seed, int64_t row, int64_t col) { return dr::synth(seed, row, col); }
+
+}  // extern "C"

@@ -1,0 +1,108 @@
+// dr_common.h -- shared helpers of the MI355X engine (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "deeprec_amd.h"
+
+namespace dr {
+
+void set_error(const char* fmt, ...);
+// Device status word of the current device (latched by kernels).
+int* status_word();
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+#define DR_HIP(x)                                                              \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      ::dr::set_error("%s failed: %s", #x, hipGetErrorString(e_));            \
+      return DR_INTERNAL;                                                      \
+    }                                                                          \
+  } while (0)
+
+#define DR_REQUIRE(cond, code, ...)                                            \
+  do {                                                                         \
+    if (!(cond)) {                                                             \
+      ::dr::set_error(__VA_ARGS__);                                            \
+      return code;                                                             \
+    }                                                                          \
+  } while (0)
+
+#define DR_LAUNCH_CHECK()                                                      \
+  do {                                                                         \
+    hipError_t e_ = hipGetLastError();                                         \
+    if (e_ != hipSuccess) {                                                    \
+      ::dr::set_error("kernel launch failed: %s", hipGetErrorString(e_));     \
+      return DR_INTERNAL;                                                      \
+    }                                                                          \
+  } while (0)
+
+// Latch the first error code into the device status word.
+__device__ __forceinline__ void latch(int* st, int code) { atomicCAS(st, 0, code); }
+
+// Workspace carving: every piece 256-byte aligned.
+struct Carver {
+  char* p;
+  size_t used;
+  explicit Carver(void* base) : p(static_cast<char*>(base)), used(0) {}
+  template <class T>
+  T* take(size_t n) {
+    size_t off = (used + 255) & ~size_t(255);
+    used = off + n * sizeof(T);
+    return p ? reinterpret_cast<T*>(p + off) : nullptr;
+  }
+};
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline int64_t next_pow2(int64_t x) {
+  int64_t c = 1;
+  while (c < x) c <<= 1;
+  return c;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdULL;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ULL;
+  k ^= k >> 33;
+  return k;
+}
+
+// SplitMix64 of (seed, row, col) -> uniform [-1, 1).  Host and device share it
+// (synthetic tables: dr_fill_synthetic, dr_ev_insert_synthetic).
+__host__ __device__ __forceinline__ float synth(uint64_t seed, int64_t row, int64_t col) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ULL + (uint64_t)row * 0xBF58476D1CE4E5B9ULL +
+               (uint64_t)col * 0x94D049BB133111EBULL;
+  z ^= z >> 30;
+  z *= 0xBF58476D1CE4E5B9ULL;
+  z ^= z >> 27;
+  z *= 0x94D049BB133111EBULL;
+  z ^= z >> 31;
+  return (float)(int32_t)(uint32_t)(z >> 32) * (1.0f / 2147483648.0f);
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  const int l = __lane_id();
+  return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+// Effective element count: min(n, *n_dev) when a device count is supplied.
+__device__ __forceinline__ int64_t eff_n(int64_t n, const int64_t* n_dev) {
+  if (!n_dev) return n;
+  int64_t m = *n_dev;
+  return m < n ? m : n;
+}
+
+// ---- scan / sort primitives (scan_sort.hip) --------------------------------
+size_t scan_ws_bytes(int64_t n);
+// Exclusive scan of int32 values into int32 out; *total (device int64) = sum.
+int scan_exclusive_i32(const int32_t* in, int32_t* out, int64_t n, const int64_t* n_dev,
+                       int64_t* total, void* ws, hipStream_t st);
+
+}  // namespace dr

@@ -1,0 +1,1262 @@
+// ev.hip -- GPU EmbeddingVariable: open-addressing key -> row table in HBM,
+// value pools per column (primary + optimizer slots), DeepRec filters,
+// insert-on-miss resolve, import/export and sparse-apply optimizers.
+//
+// Reference semantics (paths relative to the DeepRec root):
+//   EmbeddingVar            core/framework/embedding/embedding_var.h:50-363
+//   LookupOrCreateKeyInternal  embedding_var.h:320-339
+//   ValuePtr::GetOrAllocate value_ptr.h:145-170 (per-column default copy)
+//   Nullable/Counter/Bloom  embedding_filter.h:27-396
+//   KvResourceGather[V1]    core/kernels/kv_variable_ops.cc:314-449
+//   Import / GetSnapshot    embedding_var.h:187-243
+//   KvSparseApply*          core/kernels/training_ali_ops.cc
+//
+// HBM layout (one key space shared by a primary EV and its slot EVs, as the
+// reference shares kv_ between them, kv_variable_ops.cc:232-238):
+//   slots[cap + 1]  16 B {key, rc}: rc = row (bits 0..47) | column-init
+//                   bitset (bits 48..63); key -1 lives in slots[cap].
+//   pool[c]         [row_cap, dim] fp32 rows of column c (0 = primary).
+//   freq/version    [row_cap] int64, only when filter / steps_to_live on.
+// A key owns one row id for all columns; a column's row is initialised from
+// that column's default the first time it is touched, exactly like the
+// reference's lazily allocated per-emb_index rows.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "dr_common.h"
+
+namespace dr {
+
+static constexpr int kMaxCols = 16;
+static constexpr uint64_t kEmptyKey = ~0ull;
+static constexpr uint64_t kUnset = ~0ull;
+static constexpr uint64_t kRowMask = (1ull << 48) - 1;
+static constexpr uint64_t kRowDead = kRowMask;  // allocation failed
+
+struct __attribute__((aligned(16))) Slot {
+  uint64_t key;
+  uint64_t rc;
+};
+
+struct EvShared {
+  std::atomic<int> refs{1};
+  int device = 0;
+  int64_t dim = 0;
+  int64_t filter_freq = 0, steps_to_live = 0;
+  int64_t k_hash = 0, num_counter = 0;
+  int counter_bits = 64;
+  Slot* slots = nullptr;
+  int64_t cap = 0;  // power of two (+1 special slot allocated)
+  int64_t* top = nullptr;
+  int64_t row_cap = 0;
+  int64_t* freq = nullptr;
+  int64_t* version = nullptr;
+  float* pools[kMaxCols] = {nullptr};
+  float* defaults[kMaxCols] = {nullptr};
+  void* bloom = nullptr;
+  uint64_t* seeds = nullptr;
+  // host-side capacity accounting (no sync on the steady-state path)
+  std::mutex mu;
+  int64_t known = 0, adds_since_known = 0, adds_since_copy = 0;
+  bool copy_pending = false;
+  hipEvent_t copy_ev = nullptr;
+  int64_t* pinned_top = nullptr;
+};
+
+}  // namespace dr
+
+struct dr_ev {
+  dr::EvShared* sh;
+  int col;
+  std::atomic<int> refs{1};
+};
+
+namespace dr {
+
+// Per-table view passed to kernels by value.
+struct EvDesc {
+  Slot* slots;
+  int64_t cap;
+  int64_t* top;
+  int64_t row_cap;
+  int64_t* freq;
+  int64_t* version;
+  void* bloom;
+  const uint64_t* seeds;
+  int64_t filter_freq;
+  int64_t num_counter;
+  int32_t k_hash;
+  int32_t counter_bits;
+  int32_t col;
+  int32_t primary;
+};
+
+static EvDesc make_desc(const dr_ev* ev) {
+  const EvShared* s = ev->sh;
+  EvDesc d;
+  d.slots = s->slots;
+  d.cap = s->cap;
+  d.top = s->top;
+  d.row_cap = s->row_cap;
+  d.freq = s->freq;
+  d.version = s->version;
+  d.bloom = s->bloom;
+  d.seeds = s->seeds;
+  d.filter_freq = s->filter_freq;
+  d.num_counter = s->num_counter;
+  d.k_hash = (int32_t)s->k_hash;
+  d.counter_bits = s->counter_bits;
+  d.col = ev->col;
+  d.primary = ev->col == 0;
+  return d;
+}
+
+// ---- device helpers --------------------------------------------------------
+__device__ __forceinline__ uint64_t atomic_read_u64(uint64_t* p) {
+  return __hip_atomic_fetch_or(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Find (or, with insert, create) the slot of `key`.  Returns nullptr when not
+// found (insert == false).  *rc receives the published rc word.
+__device__ Slot* ev_find(const EvDesc& e, uint64_t key, bool insert, bool* created,
+                         uint64_t* rc, int* st) {
+  *created = false;
+  Slot* s = nullptr;
+  if (key == kEmptyKey) {
+    s = e.slots + e.cap;
+    uint64_t cur = s->key;
+    if (cur != 0ull) {
+      if (!insert) {
+        cur = atomic_read_u64(&s->key);
+        if (cur != 0ull) return nullptr;
+      } else {
+        uint64_t old = atomicCAS((unsigned long long*)&s->key, (unsigned long long)kEmptyKey, 0ull);
+        if (old == kEmptyKey) *created = true;
+      }
+    }
+  } else {
+    const uint64_t mask = (uint64_t)e.cap - 1;
+    uint64_t h = mix64(key) & mask;
+    for (int64_t probes = 0;; ++probes) {
+      if (probes > e.cap) {
+        latch(st, DR_RESOURCE_EXHAUSTED);
+        return nullptr;
+      }
+      Slot* c = e.slots + h;
+      uint64_t cur = c->key;
+      if (cur == key) {
+        s = c;
+        break;
+      }
+      if (cur == kEmptyKey) {
+        if (!insert) {
+          cur = atomic_read_u64(&c->key);  // rule out a stale empty
+          if (cur == kEmptyKey) return nullptr;
+          if (cur == key) {
+            s = c;
+            break;
+          }
+        } else {
+          uint64_t old =
+              atomicCAS((unsigned long long*)&c->key, (unsigned long long)kEmptyKey,
+                        (unsigned long long)key);
+          if (old == kEmptyKey) {
+            s = c;
+            *created = true;
+            break;
+          }
+          if (old == key) {
+            s = c;
+            break;
+          }
+        }
+      }
+      h = (h + 1) & mask;
+    }
+  }
+  if (*created) {
+    const int64_t row = (int64_t)atomicAdd((unsigned long long*)e.top, 1ull);
+    uint64_t v;
+    if (row >= e.row_cap) {
+      latch(st, DR_RESOURCE_EXHAUSTED);
+      v = kRowDead;
+    } else {
+      v = (uint64_t)row;  // freq/version rows were zeroed at allocation
+    }
+    __hip_atomic_store(&s->rc, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *rc = v;
+    return s;
+  }
+  uint64_t v = s->rc;
+  if (v == kUnset) {
+    for (int spin = 0; spin < (1 << 22); ++spin) {
+      v = atomic_read_u64(&s->rc);
+      if (v != kUnset) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (v == kUnset) {
+      latch(st, DR_INTERNAL);
+      v = kRowDead;
+    }
+  }
+  *rc = v;
+  return s;
+}
+
+// ---- Bloom counters (embedding_filter.h:97-250) -----------------------------
+__device__ __forceinline__ uint64_t fasthash64(uint64_t key, uint64_t seed) {
+  const uint64_t m = 0x880355f21e6d1965ULL;
+  uint64_t h = seed ^ (8 * m);
+  uint64_t v = key;
+  v ^= v >> 23;
+  v *= 0x2127599bf4325c37ULL;
+  v ^= v >> 47;
+  h ^= v;
+  h *= m;
+  v = 0;
+  v ^= v >> 23;
+  v *= 0x2127599bf4325c37ULL;
+  v ^= v >> 47;
+  h ^= v;
+  h *= m;
+  h ^= h >> 23;
+  h *= 0x2127599bf4325c37ULL;
+  h ^= h >> 47;
+  return h;
+}
+
+__device__ __forceinline__ uint64_t bloom_get(const EvDesc& e, int64_t c) {
+  switch (e.counter_bits) {
+    case 8: return ((const uint8_t*)e.bloom)[c];
+    case 16: return ((const uint16_t*)e.bloom)[c];
+    case 32: return ((const uint32_t*)e.bloom)[c];
+    default: return ((const uint64_t*)e.bloom)[c];
+  }
+}
+
+__device__ __forceinline__ void bloom_add(const EvDesc& e, int64_t c, uint64_t cnt) {
+  if (e.counter_bits == 64) {
+    atomicAdd((unsigned long long*)e.bloom + c, (unsigned long long)cnt);
+  } else if (e.counter_bits == 32) {
+    atomicAdd((unsigned int*)e.bloom + c, (unsigned int)cnt);
+  } else {
+    // 8/16-bit counters: add into the containing aligned 32-bit word (wraps
+    // in-field like the reference's __sync_fetch_and_add on uint8/16).
+    const int bytes = e.counter_bits / 8;
+    char* base = (char*)e.bloom + c * bytes;
+    unsigned int* w = (unsigned int*)((uintptr_t)base & ~(uintptr_t)3);
+    const int sh = (int)(((uintptr_t)base & 3) * 8);
+    const unsigned int fmask = (bytes == 1 ? 0xFFu : 0xFFFFu) << sh;
+    unsigned int old = *w, assumed;
+    do {
+      assumed = old;
+      unsigned int f = ((assumed & fmask) >> sh) + (unsigned int)cnt;
+      unsigned int nv = (assumed & ~fmask) | ((f << sh) & fmask);
+      old = atomicCAS(w, assumed, nv);
+    } while (old != assumed);
+  }
+}
+
+__device__ int64_t bloom_min_freq(const EvDesc& e, uint64_t key) {
+  uint64_t mn = 0;
+  for (int i = 0; i < e.k_hash; ++i) {
+    const int64_t c = (int64_t)(fasthash64(key, e.seeds[i]) % (uint64_t)e.num_counter);
+    const uint64_t v = bloom_get(e, c);
+    if (i == 0 || v < mn) mn = v;
+  }
+  return (int64_t)mn;
+}
+
+__device__ void bloom_addfreq(const EvDesc& e, uint64_t key, int64_t cnt) {
+  for (int i = 0; i < e.k_hash; ++i) {
+    const int64_t c = (int64_t)(fasthash64(key, e.seeds[i]) % (uint64_t)e.num_counter);
+    if ((int64_t)bloom_get(e, c) < e.filter_freq) bloom_add(e, c, (uint64_t)cnt);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Resolve (gather): lane per key.  rows_out[i] = row or -(i+1) (default);
+// init[i] = 1 when this lane claimed the column's first touch of the row;
+// badd[i] = count to add to Bloom counters in the follow-up pass.
+// Grouped over tables: table t owns keys [koff[t], koff[t+1]) and the device
+// count n_dev[t] (nullable) bounds it.
+// ---------------------------------------------------------------------------
+struct EvGroup {
+  EvDesc e[DR_MAX_GROUP];
+  int64_t koff[DR_MAX_GROUP + 1];
+  const int64_t* n_dev[DR_MAX_GROUP];
+};
+
+__device__ __forceinline__ int table_of(const EvGroup& g, int T, int64_t i) {
+  int t = 0;
+  while (t + 1 < T && i >= g.koff[t + 1]) ++t;
+  return t;
+}
+
+__global__ void ev_resolve_kernel(EvGroup g, int T, const int64_t* __restrict__ keys,
+                                  const int32_t* __restrict__ counts, int64_t* __restrict__ rows_out,
+                                  uint8_t* __restrict__ init, int32_t* __restrict__ badd, int* st) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.koff[T]) return;
+  const int t = table_of(g, T, i);
+  const EvDesc& e = g.e[t];
+  const int64_t li = i - g.koff[t];
+  if (g.n_dev[t] && li >= *g.n_dev[t]) return;
+  init[i] = 0;
+  badd[i] = 0;
+  const uint64_t key = (uint64_t)keys[i];
+  const int64_t cnt = counts ? counts[i] : 1;
+  if (e.k_hash > 0) {  // BloomFilter::LookupOrCreate (embedding_filter.h:56-82)
+    if (bloom_min_freq(e, key) < e.filter_freq) {
+      badd[i] = (int32_t)cnt;
+      rows_out[i] = -(li + 1);
+      return;
+    }
+  }
+  bool created;
+  uint64_t rc;
+  Slot* s = ev_find(e, key, true, &created, &rc, st);
+  if (!s || (rc & kRowMask) == kRowDead) {
+    rows_out[i] = -(li + 1);
+    return;
+  }
+  const int64_t row = (int64_t)(rc & kRowMask);
+  if (e.filter_freq > 0 && e.k_hash == 0) {  // CounterFilter (embedding_filter.h:296-320)
+    unsigned long long* f = (unsigned long long*)(e.freq + row);
+    unsigned long long old = __hip_atomic_fetch_add(f, 0ull, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+    bool admitted = false;
+    for (;;) {
+      if ((int64_t)old >= e.filter_freq) {
+        admitted = true;
+        break;
+      }
+      unsigned long long prev = atomicCAS(f, old, old + (unsigned long long)cnt);
+      if (prev == old) break;
+      old = prev;
+    }
+    if (!admitted) {
+      rows_out[i] = -(li + 1);
+      return;
+    }
+  }
+  const uint64_t bit = 1ull << (48 + e.col);
+  if (!(rc & bit)) {
+    const uint64_t old = atomicOr((unsigned long long*)&s->rc, (unsigned long long)bit);
+    if (!(old & bit)) init[i] = 1;
+  }
+  rows_out[i] = row;
+}
+
+__global__ void ev_bloom_add_kernel(EvGroup g, int T, const int64_t* __restrict__ keys,
+                                    const int32_t* __restrict__ badd) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.koff[T]) return;
+  const int t = table_of(g, T, i);
+  const int64_t li = i - g.koff[t];
+  if (g.n_dev[t] && li >= *g.n_dev[t]) return;
+  if (badd[i] > 0) bloom_addfreq(g.e[t], (uint64_t)keys[i], badd[i]);
+}
+
+// Copy the first-touch rows: pool[col][row_i] = src(i), group of 64 lanes
+// per key, lane-strided floats.  src(i) = src_rows[li*dim] or src_default.
+struct InitGroup {
+  float* pool[DR_MAX_GROUP];
+  const float* src[DR_MAX_GROUP];      // per-key rows ([n,dim]) or nullptr
+  const float* dflt[DR_MAX_GROUP];     // column default (dim)
+  int64_t koff[DR_MAX_GROUP + 1];
+  const int64_t* n_dev[DR_MAX_GROUP];
+};
+
+__global__ void ev_init_rows_kernel(InitGroup g, int T, int64_t dim,
+                                    const int64_t* __restrict__ rows,
+                                    const uint8_t* __restrict__ init) {
+  const int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  if (i >= g.koff[T]) return;
+  int t = 0;
+  while (t + 1 < T && i >= g.koff[t + 1]) ++t;
+  const int64_t li = i - g.koff[t];
+  if (g.n_dev[t] && li >= *g.n_dev[t]) return;
+  if (!init[i]) return;
+  const int64_t row = rows[i];
+  const float* src = g.src[t] ? g.src[t] + li * dim : g.dflt[t];
+  float* dst = g.pool[t] + row * dim;
+  for (int64_t c = threadIdx.x % 64; c < dim; c += 64) dst[c] = src[c];
+}
+
+// Copy-out for dr_ev_gather: out[i] = row >= 0 ? pool[row] : default(i).
+__global__ void ev_copy_out_kernel(const float* __restrict__ pool, int64_t dim,
+                                   const int64_t* __restrict__ rows, const float* __restrict__ defaults,
+                                   const float* __restrict__ dflt, int64_t n, const int64_t* n_dev,
+                                   float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  if (i >= eff_n(n, n_dev)) return;
+  const int64_t r = rows[i];
+  const float* src = r >= 0 ? pool + r * dim : (defaults ? defaults + i * dim : dflt);
+  for (int64_t c = threadIdx.x % 64; c < dim; c += 64) out[i * dim + c] = src[c];
+}
+
+// ---------------------------------------------------------------------------
+// Import (EmbeddingVar::Import, embedding_var.h:187-219).
+// ---------------------------------------------------------------------------
+__global__ void ev_import_kernel(EvDesc e, const int64_t* __restrict__ keys, int64_t n,
+                                 const int64_t* __restrict__ versions,
+                                 const int64_t* __restrict__ freqs, int64_t partition_id,
+                                 int64_t partition_num, int64_t steps_to_live,
+                                 int64_t* __restrict__ rows_out, uint8_t* __restrict__ init,
+                                 int* st) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  init[i] = 0;
+  rows_out[i] = -1;
+  const int64_t key = keys[i];
+  if (partition_num > 0 && key % 1000 % partition_num != partition_id) return;
+  bool created;
+  uint64_t rc;
+  Slot* s = ev_find(e, (uint64_t)key, true, &created, &rc, st);
+  if (!s || (rc & kRowMask) == kRowDead) return;
+  const int64_t row = (int64_t)(rc & kRowMask);
+  if (e.primary) {
+    if (e.filter_freq != 0 && e.freq) {
+      const int64_t f = freqs ? freqs[i] : 0;
+      e.freq[row] = f <= e.filter_freq ? e.filter_freq : f;
+    }
+    if (steps_to_live != 0 && e.version) e.version[row] = versions ? versions[i] : 0;
+  }
+  const uint64_t bit = 1ull << (48 + e.col);
+  if (!(rc & bit)) {
+    const uint64_t old = atomicOr((unsigned long long*)&s->rc, (unsigned long long)bit);
+    if (!(old & bit)) init[i] = 1;
+  }
+  rows_out[i] = row;
+}
+
+// Synthetic bulk insert of keys [begin, begin + n) (bench / test tables):
+// rows are filled with synth(seed, key, col) by ev_synth_rows_kernel.
+__global__ void ev_insert_range_kernel(EvDesc e, int64_t begin, int64_t n,
+                                       int64_t* __restrict__ rows_out, uint8_t* __restrict__ init,
+                                       int* st) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  init[i] = 0;
+  rows_out[i] = -1;
+  bool created;
+  uint64_t rc;
+  Slot* s = ev_find(e, (uint64_t)(begin + i), true, &created, &rc, st);
+  if (!s || (rc & kRowMask) == kRowDead) return;
+  const uint64_t bit = 1ull << (48 + e.col);
+  if (!(rc & bit)) {
+    const uint64_t old = atomicOr((unsigned long long*)&s->rc, (unsigned long long)bit);
+    if (!(old & bit)) init[i] = 1;
+  }
+  rows_out[i] = (int64_t)(rc & kRowMask);
+}
+
+__global__ void ev_synth_rows_kernel(float* __restrict__ pool, int64_t dim, int64_t begin,
+                                     int64_t n, const int64_t* __restrict__ rows,
+                                     const uint8_t* __restrict__ init, uint64_t seed) {
+  const int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  if (i >= n || !init[i]) return;
+  float* dst = pool + rows[i] * dim;
+  for (int64_t c = threadIdx.x % 64; c < dim; c += 64) dst[c] = synth(seed, begin + i, c);
+}
+
+// Lookup without insert (export helpers / key_meta).
+__global__ void ev_lookup_kernel(EvDesc e, const int64_t* __restrict__ keys, int64_t n,
+                                 int64_t* __restrict__ rows_out, uint64_t* __restrict__ rc_out,
+                                 int* st) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  bool created;
+  uint64_t rc = kUnset;
+  Slot* s = ev_find(e, (uint64_t)keys[i], false, &created, &rc, st);
+  rows_out[i] = s ? (int64_t)(rc & kRowMask) : -1;
+  rc_out[i] = s ? rc : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Sparse apply: group of G lanes per key; the leader probes, sets version
+// and column bits, the group initialises first-touch rows from the column
+// defaults (var->flat / accum->flat in training_ali_ops.cc) and updates.
+// ---------------------------------------------------------------------------
+struct ApplyCols {
+  float* pool[3];
+  const float* dflt[3];
+  int ncol;
+  int cols[3];
+};
+
+enum { OPT_SGD = 0, OPT_ADAGRAD = 1, OPT_ADAM = 2 };
+
+struct OptScalars {
+  float lr, beta1, beta2, eps, alpha;
+};
+
+template <int G, int OPT>
+__global__ __launch_bounds__(256) void ev_apply_kernel(EvDesc e, ApplyCols cols, int64_t dim,
+                                                       const int64_t* __restrict__ keys,
+                                                       const float* __restrict__ grad, int64_t n,
+                                                       const int64_t* n_dev, int64_t gs,
+                                                       int64_t steps_to_live, OptScalars sc,
+                                                       int* st) {
+  const int64_t i = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G;
+  const bool live = i < eff_n(n, n_dev);
+  const int lane = threadIdx.x & 63;
+  const int leader = lane & ~(G - 1);
+  const int lg = lane & (G - 1);
+  int64_t row = -1;
+  int initmask = 0;
+  if (live && lg == 0) {
+    const uint64_t key = (uint64_t)keys[i];
+    bool ok = true;
+    if (e.k_hash > 0 && bloom_min_freq(e, key) < e.filter_freq) ok = false;
+    if (ok) {
+      bool created;
+      uint64_t rc;
+      Slot* s = ev_find(e, key, true, &created, &rc, st);
+      if (s && (rc & kRowMask) != kRowDead) {
+        row = (int64_t)(rc & kRowMask);
+        if (steps_to_live != 0 && gs != -1 && e.version) e.version[row] = gs;
+        if (e.filter_freq > 0 && e.k_hash == 0) {
+          const int64_t f = (int64_t)__hip_atomic_fetch_add(
+              (unsigned long long*)(e.freq + row), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (f < e.filter_freq) row = -1;
+        }
+        if (row >= 0) {
+          uint64_t bits = 0;
+          for (int c = 0; c < cols.ncol; ++c) bits |= 1ull << (48 + cols.cols[c]);
+          if ((rc & bits) != bits) {
+            const uint64_t old = atomicOr((unsigned long long*)&s->rc, (unsigned long long)bits);
+            for (int c = 0; c < cols.ncol; ++c)
+              if (!(old & (1ull << (48 + cols.cols[c])))) initmask |= 1 << c;
+          }
+        }
+      }
+    }
+  }
+  row = __shfl(row, leader, 64);
+  initmask = __shfl(initmask, leader, 64);
+  if (!live || row < 0) return;
+  float* v0 = cols.pool[0] + row * dim;
+  float* v1 = cols.ncol > 1 ? cols.pool[1] + row * dim : nullptr;
+  float* v2 = cols.ncol > 2 ? cols.pool[2] + row * dim : nullptr;
+  const float* g = grad + i * dim;
+  for (int64_t c = lg; c < dim; c += G) {
+    const float gv = g[c];
+    float w = (initmask & 1) ? cols.dflt[0][c] : v0[c];
+    if (OPT == OPT_SGD) {
+      const float p = sc.lr * gv;  // v -= lr * g  (training_ali_ops.cc:1663)
+      w = w - p;
+    } else if (OPT == OPT_ADAGRAD) {  // training_ali_ops.cc:131-132
+      float a = (initmask & 2) ? cols.dflt[1][c] : v1[c];
+      const float g2 = gv * gv;
+      a = a + g2;
+      const float lg_ = sc.lr * gv;
+      const float rs = 1.0f / sqrtf(a);
+      const float up = lg_ * rs;
+      w = w - up;
+      v1[c] = a;
+    } else {  // OPT_ADAM, training_ali_ops.cc:952-958
+      float m = (initmask & 2) ? cols.dflt[1][c] : v1[c];
+      float v = (initmask & 4) ? cols.dflt[2][c] : v2[c];
+      float t1 = gv - m;
+      t1 = t1 * (1.0f - sc.beta1);
+      m = m + t1;
+      float t2 = gv * gv;
+      t2 = t2 - v;
+      t2 = t2 * (1.0f - sc.beta2);
+      v = v + t2;
+      const float num = m * sc.alpha;
+      const float den = sqrtf(v) + sc.eps;
+      w = w - num / den;
+      v1[c] = m;
+      v2[c] = v;
+    }
+    v0[c] = w;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Rehash into a larger slot table (growth).
+// ---------------------------------------------------------------------------
+__global__ void ev_rehash_kernel(const Slot* __restrict__ old_slots, int64_t old_cap,
+                                 Slot* __restrict__ new_slots, int64_t new_cap) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= old_cap) return;
+  const Slot s = old_slots[i];
+  if (s.key == kEmptyKey) return;
+  const uint64_t mask = (uint64_t)new_cap - 1;
+  uint64_t h = mix64(s.key) & mask;
+  for (;;) {
+    uint64_t old = atomicCAS((unsigned long long*)&new_slots[h].key, (unsigned long long)kEmptyKey,
+                             (unsigned long long)s.key);
+    if (old == kEmptyKey) {
+      new_slots[h].rc = s.rc;
+      return;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+// ---- host helpers ------------------------------------------------------------
+static void bloom_params(int64_t max_element_size, float fpp, int64_t* k, int64_t* nc) {
+  // EmbeddingConfig::calc_num_hash_func / calc_num_counter (embedding_config.h:63-70)
+  float loghpp = fabsf((float)(log(fpp) / log(2)));
+  *k = (int64_t)ceil(loghpp);
+  float loghpp2 = fabsf((float)log(fpp));
+  float factor = (float)(log(2) * log(2));
+  *nc = (int64_t)ceil(loghpp2 / factor * max_element_size);
+}
+
+static void bloom_seeds(int64_t k, std::vector<uint64_t>* out) {
+  // BloomFilter::GenerateSeed (embedding_filter.h:252-279)
+  static const int64_t defaults[25] = {2,  3,  5,  7,  11, 13, 17, 19, 23, 29, 31, 37, 41,
+                                       43, 47, 53, 59, 61, 67, 71, 73, 79, 83, 89, 97};
+  out->clear();
+  for (int64_t i = 0; i < k && i < 25; ++i) out->push_back((uint64_t)defaults[i]);
+  int64_t last = 98;
+  for (int64_t i = 25; i < k; ++i) {
+    for (int64_t j = last;; ++j) {
+      if (j % 2 == 0) continue;
+      bool prime = true;
+      for (int64_t q = 2; q <= (int64_t)std::sqrt((double)j) + 1; ++q)
+        if (j % q == 0) {
+          prime = false;
+          break;
+        }
+      if (prime) {
+        out->push_back((uint64_t)j);
+        last = j;
+        break;
+      }
+    }
+  }
+}
+
+static int alloc_pool(EvShared* s, int col, const float* default_row_host) {
+  DR_HIP(hipMalloc(&s->pools[col], (size_t)s->row_cap * s->dim * sizeof(float)));
+  DR_HIP(hipMalloc(&s->defaults[col], (size_t)s->dim * sizeof(float)));
+  DR_HIP(hipMemcpy(s->defaults[col], default_row_host, s->dim * sizeof(float),
+                   hipMemcpyHostToDevice));
+  return DR_OK;
+}
+
+static void free_shared(EvShared* s) {
+  (void)hipFree(s->slots);
+  (void)hipFree(s->top);
+  (void)hipFree(s->freq);
+  (void)hipFree(s->version);
+  for (int c = 0; c < kMaxCols; ++c) {
+    (void)hipFree(s->pools[c]);
+    (void)hipFree(s->defaults[c]);
+  }
+  (void)hipFree(s->bloom);
+  (void)hipFree(s->seeds);
+  if (s->copy_ev) (void)hipEventDestroy(s->copy_ev);
+  if (s->pinned_top) (void)hipHostFree(s->pinned_top);
+  delete s;
+}
+
+// Grow the slot table and/or the row arrays so that `need` keys fit.
+static int grow(EvShared* s, int64_t need, hipStream_t st) {
+  if (need > s->cap * 3 / 4) {
+    int64_t ncap = next_pow2(need * 2);
+    Slot* ns = nullptr;
+    DR_HIP(hipMalloc(&ns, (size_t)(ncap + 1) * sizeof(Slot)));
+    DR_HIP(hipMemsetAsync(ns, 0xFF, (size_t)(ncap + 1) * sizeof(Slot), st));
+    hipLaunchKernelGGL(ev_rehash_kernel, dim3((unsigned)ceil_div(s->cap, 256)), dim3(256), 0, st,
+                       s->slots, s->cap, ns, ncap);
+    DR_LAUNCH_CHECK();
+    DR_HIP(hipMemcpyAsync(ns + ncap, s->slots + s->cap, sizeof(Slot), hipMemcpyDeviceToDevice, st));
+    DR_HIP(hipStreamSynchronize(st));
+    DR_HIP(hipFree(s->slots));
+    s->slots = ns;
+    s->cap = ncap;
+  }
+  if (need > s->row_cap) {
+    int64_t nrc = std::max(need, s->row_cap * 2);
+    for (int c = 0; c < kMaxCols; ++c) {
+      if (!s->pools[c]) continue;
+      float* np = nullptr;
+      DR_HIP(hipMalloc(&np, (size_t)nrc * s->dim * sizeof(float)));
+      DR_HIP(hipMemcpyAsync(np, s->pools[c], (size_t)s->row_cap * s->dim * sizeof(float),
+                            hipMemcpyDeviceToDevice, st));
+      DR_HIP(hipStreamSynchronize(st));
+      DR_HIP(hipFree(s->pools[c]));
+      s->pools[c] = np;
+    }
+    int64_t** arrs[2] = {&s->freq, &s->version};
+    for (auto a : arrs) {
+      if (!*a) continue;
+      int64_t* np = nullptr;
+      DR_HIP(hipMalloc(&np, (size_t)nrc * sizeof(int64_t)));
+      DR_HIP(hipMemsetAsync(np, 0, (size_t)nrc * sizeof(int64_t), st));
+      DR_HIP(hipMemcpyAsync(np, *a, (size_t)s->row_cap * sizeof(int64_t), hipMemcpyDeviceToDevice,
+                            st));
+      DR_HIP(hipStreamSynchronize(st));
+      DR_HIP(hipFree(*a));
+      *a = np;
+    }
+    s->row_cap = nrc;
+  }
+  return DR_OK;
+}
+
+// Make sure `n` more keys fit.  Steady state: no host sync (the device key
+// count is mirrored asynchronously into pinned memory after every call).
+static int reserve(EvShared* s, int64_t n, hipStream_t st) {
+  std::lock_guard<std::mutex> g(s->mu);
+  if (s->copy_pending && hipEventQuery(s->copy_ev) == hipSuccess) {
+    s->known = *s->pinned_top;
+    s->adds_since_known = s->adds_since_copy;
+    s->copy_pending = false;
+  }
+  const int64_t limit = std::min(s->row_cap, s->cap * 3 / 4);
+  if (s->known + s->adds_since_known + n > limit) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cs);
+    DR_REQUIRE(cs == hipStreamCaptureStatusNone, DR_RESOURCE_EXHAUSTED,
+               "EV capacity may be exceeded inside stream capture; dr_ev_reserve first");
+    DR_HIP(hipStreamSynchronize(st));
+    int64_t actual = 0;
+    DR_HIP(hipMemcpy(&actual, s->top, sizeof(int64_t), hipMemcpyDeviceToHost));
+    s->known = actual;
+    s->adds_since_known = 0;
+    s->copy_pending = false;
+    if (actual + n > limit) {
+      int rc = grow(s, actual + n, st);
+      if (rc) return rc;
+    }
+  }
+  s->adds_since_known += n;
+  if (s->copy_pending) s->adds_since_copy += n;
+  return DR_OK;
+}
+
+static void post_call(EvShared* s, hipStream_t st) {
+  std::lock_guard<std::mutex> g(s->mu);
+  if (s->copy_pending) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(st, &cs);
+  if (cs != hipStreamCaptureStatusNone) return;
+  if (hipMemcpyAsync(s->pinned_top, s->top, sizeof(int64_t), hipMemcpyDeviceToHost, st) !=
+      hipSuccess)
+    return;
+  if (hipEventRecord(s->copy_ev, st) != hipSuccess) return;
+  s->copy_pending = true;
+  s->adds_since_copy = 0;
+}
+
+struct ResolveWs {
+  uint8_t* init;
+  int32_t* badd;
+};
+static ResolveWs carve_resolve(void* ws, int64_t n, size_t* used) {
+  Carver c(ws);
+  ResolveWs w;
+  w.init = c.take<uint8_t>(n > 0 ? n : 1);
+  w.badd = c.take<int32_t>(n > 0 ? n : 1);
+  if (used) *used = c.used + 256;
+  return w;
+}
+
+static int resolve_grouped(dr_ev* const* evs, int T, const int64_t* keys, const int64_t* koff,
+                           const int64_t* const* n_dev, const float* const* defaults,
+                           const int32_t* counts, int64_t* rows_out, void* ws, size_t ws_bytes,
+                           hipStream_t st) {
+  DR_REQUIRE(T >= 1 && T <= DR_MAX_GROUP, DR_INVALID_ARGUMENT, "bad table count");
+  const int64_t total = koff[T];
+  size_t need = 0;
+  carve_resolve(nullptr, total, &need);
+  DR_REQUIRE(ws_bytes >= need, DR_INVALID_ARGUMENT, "resolve workspace too small");
+  if (total == 0) return DR_OK;
+  int* stw = status_word();
+  DR_REQUIRE(stw, DR_INTERNAL, "status word unavailable");
+  for (int t = 0; t < T; ++t) {
+    int rc = reserve(evs[t]->sh, koff[t + 1] - koff[t], st);
+    if (rc) return rc;
+  }
+  ResolveWs w = carve_resolve(ws, total, nullptr);
+  EvGroup g;
+  memset(&g, 0, sizeof(g));
+  InitGroup ig;
+  memset(&ig, 0, sizeof(ig));
+  bool any_bloom = false;
+  for (int t = 0; t < T; ++t) {
+    g.e[t] = make_desc(evs[t]);
+    g.koff[t] = koff[t];
+    g.n_dev[t] = n_dev ? n_dev[t] : nullptr;
+    ig.pool[t] = evs[t]->sh->pools[evs[t]->col];
+    ig.src[t] = defaults ? defaults[t] : nullptr;
+    ig.dflt[t] = evs[t]->sh->defaults[evs[t]->col];
+    ig.koff[t] = koff[t];
+    ig.n_dev[t] = g.n_dev[t];
+    any_bloom |= g.e[t].k_hash > 0;
+    DR_REQUIRE(evs[t]->sh->dim == evs[0]->sh->dim, DR_INVALID_ARGUMENT,
+               "grouped EVs must share dim");
+  }
+  g.koff[T] = total;
+  ig.koff[T] = total;
+  const unsigned blocks = (unsigned)ceil_div(total, 256);
+  hipLaunchKernelGGL(ev_resolve_kernel, dim3(blocks), dim3(256), 0, st, g, T, keys, counts,
+                     rows_out, w.init, w.badd, stw);
+  if (any_bloom)
+    hipLaunchKernelGGL(ev_bloom_add_kernel, dim3(blocks), dim3(256), 0, st, g, T, keys, w.badd);
+  hipLaunchKernelGGL(ev_init_rows_kernel, dim3((unsigned)ceil_div(total, 4)), dim3(256), 0, st, ig,
+                     T, evs[0]->sh->dim, rows_out, w.init);
+  DR_LAUNCH_CHECK();
+  for (int t = 0; t < T; ++t) post_call(evs[t]->sh, st);
+  return DR_OK;
+}
+
+static int apply_common(int opt, dr_ev* var, dr_ev* s1, dr_ev* s2, OptScalars sc,
+                        const float* grad, const int64_t* keys, int64_t n, const int64_t* n_dev,
+                        int64_t gs, hipStream_t st) {
+  DR_REQUIRE(var && var->col == 0, DR_INVALID_ARGUMENT, "var must be a primary EV");
+  if (n == 0) return DR_OK;
+  EvShared* s = var->sh;
+  DR_REQUIRE(!s1 || s1->sh == s, DR_INVALID_ARGUMENT, "slot EV must share the primary's keys");
+  DR_REQUIRE(!s2 || s2->sh == s, DR_INVALID_ARGUMENT, "slot EV must share the primary's keys");
+  int rc = reserve(s, n, st);
+  if (rc) return rc;
+  int* stw = status_word();
+  ApplyCols cols;
+  memset(&cols, 0, sizeof(cols));
+  dr_ev* evs[3] = {var, s1, s2};
+  cols.ncol = opt == OPT_SGD ? 1 : (opt == OPT_ADAGRAD ? 2 : 3);
+  for (int c = 0; c < cols.ncol; ++c) {
+    DR_REQUIRE(evs[c], DR_INVALID_ARGUMENT, "missing slot EV");
+    cols.cols[c] = evs[c]->col;
+    cols.pool[c] = s->pools[evs[c]->col];
+    cols.dflt[c] = s->defaults[evs[c]->col];
+  }
+  EvDesc e = make_desc(var);
+  constexpr int G = 64;
+  const unsigned blocks = (unsigned)ceil_div(n, 256 / G);
+  if (opt == OPT_SGD)
+    hipLaunchKernelGGL((ev_apply_kernel<G, OPT_SGD>), dim3(blocks), dim3(256), 0, st, e, cols,
+                       s->dim, keys, grad, n, n_dev, gs, s->steps_to_live, sc, stw);
+  else if (opt == OPT_ADAGRAD)
+    hipLaunchKernelGGL((ev_apply_kernel<G, OPT_ADAGRAD>), dim3(blocks), dim3(256), 0, st, e, cols,
+                       s->dim, keys, grad, n, n_dev, gs, s->steps_to_live, sc, stw);
+  else
+    hipLaunchKernelGGL((ev_apply_kernel<G, OPT_ADAM>), dim3(blocks), dim3(256), 0, st, e, cols,
+                       s->dim, keys, grad, n, n_dev, gs, s->steps_to_live, sc, stw);
+  DR_LAUNCH_CHECK();
+  post_call(s, st);
+  return DR_OK;
+}
+
+}  // namespace dr
+
+// ===========================================================================
+extern "C" {
+
+int dr_ev_create(const dr_ev_config* cfg, const float* default_row_host, dr_ev** out) {
+  using namespace dr;
+  DR_REQUIRE(cfg && out && default_row_host, DR_INVALID_ARGUMENT, "null argument");
+  DR_REQUIRE(cfg->dim > 0, DR_INVALID_ARGUMENT, "dim must be > 0");
+  DR_REQUIRE(cfg->steps_to_live >= 0, DR_INVALID_ARGUMENT, "steps_to_live must >= 0");
+  EvShared* s = new (std::nothrow) EvShared();
+  DR_REQUIRE(s, DR_RESOURCE_EXHAUSTED, "host allocation failed");
+  (void)hipGetDevice(&s->device);
+  s->dim = cfg->dim;
+  s->filter_freq = cfg->filter_freq < 0 ? 0 : cfg->filter_freq;
+  s->steps_to_live = cfg->steps_to_live;
+  const int64_t capacity = cfg->capacity > 0 ? cfg->capacity : 1024;
+  s->cap = next_pow2(std::max<int64_t>(1024, capacity * 2));
+  s->row_cap = std::max<int64_t>(1024, capacity);
+  int rc = DR_OK;
+#define DR_TRY(x)                        \
+  do {                                   \
+    if ((x) != hipSuccess) {             \
+      set_error("%s failed", #x);        \
+      free_shared(s);                    \
+      return DR_RESOURCE_EXHAUSTED;      \
+    }                                    \
+  } while (0)
+  DR_TRY(hipMalloc(&s->slots, (size_t)(s->cap + 1) * sizeof(Slot)));
+  DR_TRY(hipMemset(s->slots, 0xFF, (size_t)(s->cap + 1) * sizeof(Slot)));
+  DR_TRY(hipMalloc(&s->top, sizeof(int64_t)));
+  DR_TRY(hipMemset(s->top, 0, sizeof(int64_t)));
+  if (s->filter_freq > 0) {
+    DR_TRY(hipMalloc(&s->freq, (size_t)s->row_cap * sizeof(int64_t)));
+    DR_TRY(hipMemset(s->freq, 0, (size_t)s->row_cap * sizeof(int64_t)));
+  }
+  if (s->steps_to_live != 0) {
+    DR_TRY(hipMalloc(&s->version, (size_t)s->row_cap * sizeof(int64_t)));
+    DR_TRY(hipMemset(s->version, 0, (size_t)s->row_cap * sizeof(int64_t)));
+  }
+  if (s->filter_freq > 0 && cfg->max_element_size != 0 && cfg->false_positive_probability != -1.0f) {
+    bloom_params(cfg->max_element_size, cfg->false_positive_probability, &s->k_hash,
+                 &s->num_counter);
+    s->counter_bits = cfg->counter_bits ? cfg->counter_bits : 64;
+    if (s->counter_bits != 8 && s->counter_bits != 16 && s->counter_bits != 32)
+      s->counter_bits = 64;
+    const size_t bytes = ((size_t)s->num_counter * (s->counter_bits / 8) + 7) & ~(size_t)7;
+    DR_TRY(hipMalloc(&s->bloom, bytes));
+    DR_TRY(hipMemset(s->bloom, 0, bytes));
+    std::vector<uint64_t> seeds;
+    bloom_seeds(s->k_hash, &seeds);
+    DR_TRY(hipMalloc(&s->seeds, seeds.size() * sizeof(uint64_t) + 8));
+    DR_TRY(hipMemcpy(s->seeds, seeds.data(), seeds.size() * sizeof(uint64_t),
+                     hipMemcpyHostToDevice));
+  }
+  DR_TRY(hipEventCreateWithFlags(&s->copy_ev, hipEventDisableTiming));
+  DR_TRY(hipHostMalloc(&s->pinned_top, sizeof(int64_t)));
+#undef DR_TRY
+  rc = alloc_pool(s, 0, default_row_host);
+  if (rc) {
+    free_shared(s);
+    return rc;
+  }
+  dr_ev* ev = new dr_ev();
+  ev->sh = s;
+  ev->col = 0;
+  *out = ev;
+  return DR_OK;
+}
+
+int dr_ev_create_slot(dr_ev* primary, int slot_index, const float* default_row_host, dr_ev** out) {
+  using namespace dr;
+  DR_REQUIRE(primary && out && default_row_host, DR_INVALID_ARGUMENT, "null argument");
+  DR_REQUIRE(primary->col == 0, DR_INVALID_ARGUMENT, "slots attach to a primary EV");
+  DR_REQUIRE(slot_index >= 1 && slot_index < kMaxCols, DR_INVALID_ARGUMENT,
+             "slot_index must be in [1, %d)", kMaxCols);
+  EvShared* s = primary->sh;
+  std::lock_guard<std::mutex> g(s->mu);
+  DR_REQUIRE(!s->pools[slot_index], DR_ALREADY_EXISTS, "slot %d already exists", slot_index);
+  int rc = alloc_pool(s, slot_index, default_row_host);
+  if (rc) return rc;
+  s->refs.fetch_add(1);
+  dr_ev* ev = new dr_ev();
+  ev->sh = s;
+  ev->col = slot_index;
+  *out = ev;
+  return DR_OK;
+}
+
+int dr_ev_retain(dr_ev* ev) {
+  DR_REQUIRE(ev, DR_INVALID_ARGUMENT, "null ev");
+  ev->refs.fetch_add(1);
+  return DR_OK;
+}
+
+int dr_ev_release(dr_ev* ev) {
+  DR_REQUIRE(ev, DR_INVALID_ARGUMENT, "null ev");
+  if (ev->refs.fetch_sub(1) == 1) {
+    dr::EvShared* s = ev->sh;
+    if (s->refs.fetch_sub(1) == 1) dr::free_shared(s);
+    delete ev;
+  }
+  return DR_OK;
+}
+
+int64_t dr_ev_dim(dr_ev* ev) { return ev ? ev->sh->dim : -1; }
+
+const float* dr_ev_pool(dr_ev* ev) { return ev ? ev->sh->pools[ev->col] : nullptr; }
+
+int dr_ev_size(dr_ev* ev, int64_t* size_host, void* stream) {
+  DR_REQUIRE(ev && size_host, DR_INVALID_ARGUMENT, "null argument");
+  DR_HIP(hipStreamSynchronize(dr::S(stream)));
+  DR_HIP(hipMemcpy(size_host, ev->sh->top, sizeof(int64_t), hipMemcpyDeviceToHost));
+  return DR_OK;
+}
+
+int dr_ev_reserve(dr_ev* ev, int64_t extra, void* stream) {
+  DR_REQUIRE(ev && extra >= 0, DR_INVALID_ARGUMENT, "bad argument");
+  dr::EvShared* s = ev->sh;
+  hipStream_t st = dr::S(stream);
+  std::lock_guard<std::mutex> g(s->mu);
+  DR_HIP(hipStreamSynchronize(st));
+  int64_t actual = 0;
+  DR_HIP(hipMemcpy(&actual, s->top, sizeof(int64_t), hipMemcpyDeviceToHost));
+  s->known = actual;
+  s->adds_since_known = 0;
+  s->copy_pending = false;
+  return dr::grow(s, actual + extra, st);
+}
+
+size_t dr_ev_resolve_workspace_size(int64_t n) {
+  size_t used = 0;
+  dr::carve_resolve(nullptr, n, &used);
+  return used;
+}
+
+int dr_ev_resolve(dr_ev* ev, const int64_t* keys, int64_t n, const int64_t* n_dev,
+                  const float* defaults, const int32_t* counts, int64_t* rows_out, void* ws,
+                  size_t ws_bytes, void* stream) {
+  DR_REQUIRE(ev && n >= 0, DR_INVALID_ARGUMENT, "bad argument");
+  int64_t koff[2] = {0, n};
+  const int64_t* nd[1] = {n_dev};
+  const float* df[1] = {defaults};
+  return dr::resolve_grouped(&ev, 1, keys, koff, nd, defaults ? df : nullptr, counts, rows_out, ws,
+                             ws_bytes, dr::S(stream));
+}
+
+// Grouped resolve over T EVs (one per feature); keys/counts/rows_out are
+// concatenated with table t at [koff_host[t], koff_host[t+1]).
+int dr_ev_resolve_grouped(dr_ev* const* evs, int num_tables, const int64_t* keys,
+                          const int64_t* koff_host, const int64_t* const* n_dev_per_table,
+                          const int32_t* counts, int64_t* rows_out, void* ws, size_t ws_bytes,
+                          void* stream) {
+  return dr::resolve_grouped(evs, num_tables, keys, koff_host, n_dev_per_table, nullptr, counts,
+                             rows_out, ws, ws_bytes, dr::S(stream));
+}
+
+int dr_ev_gather(dr_ev* ev, const int64_t* keys, int64_t n, const float* defaults,
+                 const int32_t* counts, float* out, void* ws, size_t ws_bytes, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(ev && n >= 0, DR_INVALID_ARGUMENT, "bad argument");
+  if (n == 0) return DR_OK;
+  Carver c(ws);
+  int64_t* rows = c.take<int64_t>(n);
+  size_t rneed = dr_ev_resolve_workspace_size(n);
+  void* rws = c.take<char>(rneed);
+  DR_REQUIRE(ws_bytes >= c.used, DR_INVALID_ARGUMENT, "workspace too small");
+  int rc = dr_ev_resolve(ev, keys, n, nullptr, defaults, counts, rows, rws, rneed, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(ev_copy_out_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, S(stream),
+                     ev->sh->pools[ev->col], ev->sh->dim, rows, defaults,
+                     ev->sh->defaults[ev->col], n, nullptr, out);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+size_t dr_ev_gather_workspace_size(int64_t n) {
+  dr::Carver c(nullptr);
+  c.take<int64_t>(n > 0 ? n : 1);
+  c.take<char>(dr_ev_resolve_workspace_size(n));
+  return c.used + 256;
+}
+
+int dr_ev_insert(dr_ev* ev, const int64_t* keys, int64_t n, const float* values,
+                 const int64_t* versions, const int64_t* freqs, int64_t partition_id,
+                 int64_t partition_num, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(ev && n >= 0, DR_INVALID_ARGUMENT, "bad argument");
+  if (n == 0) return DR_OK;
+  hipStream_t st = S(stream);
+  int rc = reserve(ev->sh, n, st);
+  if (rc) return rc;
+  int64_t* rows = nullptr;
+  uint8_t* init = nullptr;
+  DR_HIP(hipMallocAsync((void**)&rows, n * sizeof(int64_t), st));
+  DR_HIP(hipMallocAsync((void**)&init, n, st));
+  EvDesc e = make_desc(ev);
+  const unsigned blocks = (unsigned)ceil_div(n, 256);
+  hipLaunchKernelGGL(ev_import_kernel, dim3(blocks), dim3(256), 0, st, e, keys, n, versions, freqs,
+                     partition_id, partition_num, ev->sh->steps_to_live, rows, init,
+                     status_word());
+  InitGroup ig;
+  memset(&ig, 0, sizeof(ig));
+  ig.pool[0] = ev->sh->pools[ev->col];
+  ig.src[0] = values;
+  ig.dflt[0] = ev->sh->defaults[ev->col];
+  ig.koff[0] = 0;
+  ig.koff[1] = n;
+  hipLaunchKernelGGL(ev_init_rows_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, ig, 1,
+                     ev->sh->dim, rows, init);
+  DR_LAUNCH_CHECK();
+  DR_HIP(hipFreeAsync(rows, st));
+  DR_HIP(hipFreeAsync(init, st));
+  post_call(ev->sh, st);
+  return DR_OK;
+}
+
+// Bulk insert of keys [key_begin, key_begin + n) with synthetic rows
+// synth(seed, key, col) -- populates bench/test tables without a host copy.
+int dr_ev_insert_synthetic(dr_ev* ev, int64_t key_begin, int64_t n, uint64_t seed,
+                           void* stream) {
+  using namespace dr;
+  DR_REQUIRE(ev && n >= 0, DR_INVALID_ARGUMENT, "bad argument");
+  if (n == 0) return DR_OK;
+  hipStream_t st = S(stream);
+  int rc = reserve(ev->sh, n, st);
+  if (rc) return rc;
+  const int64_t chunk = std::min<int64_t>(n, 1 << 24);
+  int64_t* rows = nullptr;
+  uint8_t* init = nullptr;
+  DR_HIP(hipMallocAsync((void**)&rows, chunk * sizeof(int64_t), st));
+  DR_HIP(hipMallocAsync((void**)&init, chunk, st));
+  EvDesc e = make_desc(ev);
+  for (int64_t b = 0; b < n; b += chunk) {
+    const int64_t m = std::min(chunk, n - b);
+    hipLaunchKernelGGL(ev_insert_range_kernel, dim3((unsigned)ceil_div(m, 256)), dim3(256), 0, st,
+                       e, key_begin + b, m, rows, init, status_word());
+    hipLaunchKernelGGL(ev_synth_rows_kernel, dim3((unsigned)ceil_div(m, 4)), dim3(256), 0, st,
+                       ev->sh->pools[ev->col], ev->sh->dim, key_begin + b, m, rows, init, seed);
+    DR_LAUNCH_CHECK();
+  }
+  DR_HIP(hipFreeAsync(rows, st));
+  DR_HIP(hipFreeAsync(init, st));
+  post_call(ev->sh, st);
+  return DR_OK;
+}
+
+// Export: keys whose own column and primary rows exist (GetSnapshot,
+// embedding_var.h:221-243), ascending key order.
+int dr_ev_export(dr_ev* ev, int64_t* keys_out, float* values_out, int64_t* versions_out,
+                 int64_t* freqs_out, int64_t capacity, int64_t* m_host, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(ev && m_host, DR_INVALID_ARGUMENT, "null argument");
+  hipStream_t st = S(stream);
+  EvShared* s = ev->sh;
+  DR_HIP(hipStreamSynchronize(st));
+  std::vector<Slot> slots((size_t)s->cap + 1);
+  DR_HIP(hipMemcpy(slots.data(), s->slots, slots.size() * sizeof(Slot), hipMemcpyDeviceToHost));
+  const uint64_t need = (1ull << 48) | (1ull << (48 + ev->col));
+  std::vector<std::pair<int64_t, int64_t>> kr;  // (key, row)
+  for (size_t i = 0; i < slots.size(); ++i) {
+    const Slot& x = slots[i];
+    const bool occupied = (i < (size_t)s->cap) ? x.key != kEmptyKey : x.key == 0ull;
+    if (!occupied || x.rc == kUnset || (x.rc & kRowMask) == kRowDead) continue;
+    if ((x.rc & need) != need) continue;
+    const int64_t key = i < (size_t)s->cap ? (int64_t)x.key : -1;
+    kr.emplace_back(key, (int64_t)(x.rc & kRowMask));
+  }
+  std::sort(kr.begin(), kr.end());
+  const int64_t m = (int64_t)kr.size();
+  *m_host = m;
+  if (!keys_out && !values_out && !versions_out && !freqs_out) return DR_OK;
+  DR_REQUIRE(capacity >= m, DR_INVALID_ARGUMENT, "export capacity %lld < %lld",
+             (long long)capacity, (long long)m);
+  if (m == 0) return DR_OK;
+  std::vector<int64_t> keys(m), rows(m), vers(m, 0), frqs(m, 0);
+  for (int64_t i = 0; i < m; ++i) {
+    keys[i] = kr[i].first;
+    rows[i] = kr[i].second;
+  }
+  int64_t top = 0;
+  DR_HIP(hipMemcpy(&top, s->top, sizeof(int64_t), hipMemcpyDeviceToHost));
+  if ((versions_out && s->version) || (freqs_out && s->freq)) {
+    std::vector<int64_t> hv(top > 0 ? top : 1), hf(top > 0 ? top : 1);
+    if (s->version && top > 0)
+      DR_HIP(hipMemcpy(hv.data(), s->version, top * sizeof(int64_t), hipMemcpyDeviceToHost));
+    if (s->freq && top > 0)
+      DR_HIP(hipMemcpy(hf.data(), s->freq, top * sizeof(int64_t), hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < m; ++i) {
+      if (s->version) vers[i] = hv[rows[i]];
+      if (s->freq) frqs[i] = hf[rows[i]];
+    }
+  }
+  if (keys_out) DR_HIP(hipMemcpy(keys_out, keys.data(), m * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (versions_out)
+    DR_HIP(hipMemcpy(versions_out, vers.data(), m * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (freqs_out) {
+    if (s->k_hash > 0) {
+      // Bloom: freq is the counters' minimum (GetFreq -> GetBloomFreq)
+      const size_t bytes = ((size_t)s->num_counter * (s->counter_bits / 8) + 7) & ~(size_t)7;
+      std::vector<uint8_t> hb(bytes);
+      DR_HIP(hipMemcpy(hb.data(), s->bloom, bytes, hipMemcpyDeviceToHost));
+      std::vector<uint64_t> seeds;
+      bloom_seeds(s->k_hash, &seeds);
+      for (int64_t i = 0; i < m; ++i) {
+        uint64_t mn = 0;
+        for (int64_t h = 0; h < s->k_hash; ++h) {
+          uint64_t key = (uint64_t)keys[i];
+          const uint64_t mm = 0x880355f21e6d1965ULL;
+          uint64_t hh = seeds[h] ^ (8 * mm), v = key;
+          v ^= v >> 23; v *= 0x2127599bf4325c37ULL; v ^= v >> 47; hh ^= v; hh *= mm;
+          v = 0; v ^= v >> 23; v *= 0x2127599bf4325c37ULL; v ^= v >> 47; hh ^= v; hh *= mm;
+          hh ^= hh >> 23; hh *= 0x2127599bf4325c37ULL; hh ^= hh >> 47;
+          const int64_t c = (int64_t)(hh % (uint64_t)s->num_counter);
+          uint64_t val = 0;
+          switch (s->counter_bits) {
+            case 8: val = hb[c]; break;
+            case 16: val = ((uint16_t*)hb.data())[c]; break;
+            case 32: val = ((uint32_t*)hb.data())[c]; break;
+            default: val = ((uint64_t*)hb.data())[c]; break;
+          }
+          if (h == 0 || val < mn) mn = val;
+        }
+        frqs[i] = (int64_t)mn;
+      }
+    }
+    DR_HIP(hipMemcpy(freqs_out, frqs.data(), m * sizeof(int64_t), hipMemcpyHostToDevice));
+  }
+  if (values_out) {
+    int64_t* drows = nullptr;
+    DR_HIP(hipMalloc(&drows, m * sizeof(int64_t)));
+    DR_HIP(hipMemcpy(drows, rows.data(), m * sizeof(int64_t), hipMemcpyHostToDevice));
+    int rc = dr_gather(s->pools[ev->col], top, s->dim, drows, m, values_out, stream);
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(drows);
+    if (rc) return rc;
+  }
+  return DR_OK;
+}
+
+int dr_ev_key_meta(dr_ev* ev, const int64_t* keys_host, int64_t n, int64_t* freq_host,
+                   int64_t* version_host, int32_t* has_row_host, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(ev && keys_host && n >= 0, DR_INVALID_ARGUMENT, "bad argument");
+  if (n == 0) return DR_OK;
+  hipStream_t st = S(stream);
+  EvShared* s = ev->sh;
+  int64_t *dk = nullptr, *dr_ = nullptr;
+  uint64_t* drc = nullptr;
+  DR_HIP(hipMalloc(&dk, n * sizeof(int64_t)));
+  DR_HIP(hipMalloc(&dr_, n * sizeof(int64_t)));
+  DR_HIP(hipMalloc(&drc, n * sizeof(uint64_t)));
+  DR_HIP(hipMemcpy(dk, keys_host, n * sizeof(int64_t), hipMemcpyHostToDevice));
+  EvDesc e = make_desc(ev);
+  hipLaunchKernelGGL(ev_lookup_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, e, dk,
+                     n, dr_, drc, status_word());
+  DR_HIP(hipStreamSynchronize(st));
+  std::vector<int64_t> rows(n);
+  std::vector<uint64_t> rcs(n);
+  DR_HIP(hipMemcpy(rows.data(), dr_, n * sizeof(int64_t), hipMemcpyDeviceToHost));
+  DR_HIP(hipMemcpy(rcs.data(), drc, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  (void)hipFree(dk);
+  (void)hipFree(dr_);
+  (void)hipFree(drc);
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t r = rows[i];
+    if (freq_host) {
+      freq_host[i] = 0;
+      if (r >= 0 && s->freq) DR_HIP(hipMemcpy(&freq_host[i], s->freq + r, 8, hipMemcpyDeviceToHost));
+    }
+    if (version_host) {
+      version_host[i] = r >= 0 ? 0 : -1;
+      if (r >= 0 && s->version)
+        DR_HIP(hipMemcpy(&version_host[i], s->version + r, 8, hipMemcpyDeviceToHost));
+    }
+    if (has_row_host) has_row_host[i] = r >= 0 && ((rcs[i] >> (48 + ev->col)) & 1);
+  }
+  return DR_OK;
+}
+
+int dr_ev_apply_sgd(dr_ev* var, float lr, const float* grad, const int64_t* keys, int64_t n,
+                    const int64_t* n_dev, int64_t global_step, void* stream) {
+  dr::OptScalars sc = {lr, 0, 0, 0, 0};
+  return dr::apply_common(dr::OPT_SGD, var, nullptr, nullptr, sc, grad, keys, n, n_dev,
+                          global_step, dr::S(stream));
+}
+
+int dr_ev_apply_adagrad(dr_ev* var, dr_ev* accum, float lr, const float* grad,
+                        const int64_t* keys, int64_t n, const int64_t* n_dev, int64_t global_step,
+                        void* stream) {
+  dr::OptScalars sc = {lr, 0, 0, 0, 0};
+  return dr::apply_common(dr::OPT_ADAGRAD, var, accum, nullptr, sc, grad, keys, n, n_dev,
+                          global_step, dr::S(stream));
+}
+
+int dr_ev_apply_adam(dr_ev* var, dr_ev* m, dr_ev* v, float beta1_power, float beta2_power,
+                     float lr, float beta1, float beta2, float epsilon, const float* grad,
+                     const int64_t* keys, int64_t n, const int64_t* n_dev, int64_t global_step,
+                     void* stream) {
+  // alpha = lr * sqrt(1 - beta2^t) / (1 - beta1^t)  (training_ali_ops.cc:935-937)
+  const float alpha = lr * sqrtf(1.0f - beta2_power) / (1.0f - beta1_power);
+  dr::OptScalars sc = {lr, beta1, beta2, epsilon, alpha};
+  return dr::apply_common(dr::OPT_ADAM, var, m, v, sc, grad, keys, n, n_dev, global_step,
+                          dr::S(stream));
+}
+
+}  // extern "C"

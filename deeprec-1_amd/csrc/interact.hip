@@ -1,0 +1,216 @@
+// interact.hip -- feature interactions fed by the pooled embeddings.
+//   FM second order   modelzoo/DeepFM/train.py:205-209   (HBM-bound)
+//   DLRM dot          modelzoo/DLRM/train.py:150-163     (LDS-tiled, per sample)
+//   DCN-v2 CrossNet   (absent from the reference)        (bf16 MFMA GEMM)
+#include "dr_common.h"
+
+namespace dr {
+
+// out[b, d] = 0.5 * ((sum_f e)^2 - sum_f e^2); thread per (b, 4 columns).
+__global__ void fm2_kernel(const float* __restrict__ emb, int64_t B, int F, int D,
+                           float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int D4 = D / 4;
+  if (t >= B * D4) return;
+  const int64_t b = t / D4;
+  const int c = (int)(t % D4);
+  const float4* p = reinterpret_cast<const float4*>(emb + b * (int64_t)F * D) + c;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
+  for (int f = 0; f < F; ++f) {
+    const float4 e = p[(int64_t)f * D4];
+    s.x += e.x; s.y += e.y; s.z += e.z; s.w += e.w;
+    q.x += e.x * e.x; q.y += e.y * e.y; q.z += e.z * e.z; q.w += e.w * e.w;
+  }
+  float4 o;
+  o.x = 0.5f * (s.x * s.x - q.x);
+  o.y = 0.5f * (s.y * s.y - q.y);
+  o.z = 0.5f * (s.z * s.z - q.z);
+  o.w = 0.5f * (s.w * s.w - q.w);
+  reinterpret_cast<float4*>(out + b * (int64_t)D)[c] = o;
+}
+
+// d fm / d e_f = (sum_f' e_f' - e_f) * g
+__global__ void fm2_grad_kernel(const float* __restrict__ emb, const float* __restrict__ g,
+                                int64_t B, int F, int D, float* __restrict__ ge) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * D) return;
+  const int64_t b = t / D;
+  const int d = (int)(t % D);
+  const float* p = emb + b * (int64_t)F * D + d;
+  float s = 0.f;
+  for (int f = 0; f < F; ++f) s += p[(int64_t)f * D];
+  const float gv = g[b * D + d];
+  for (int f = 0; f < F; ++f) ge[b * (int64_t)F * D + (int64_t)f * D + d] = (s - p[(int64_t)f * D]) * gv;
+}
+
+// One block per sample: X [F, D] staged in LDS (row stride D+1 to break bank
+// conflicts), thread per lower-triangle pair (i > j), row-major pair order.
+__global__ void dot_kernel(const float* __restrict__ x, int F, int D, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  const int64_t b = blockIdx.x;
+  const int ld = D + 1;
+  const float* src = x + b * (int64_t)F * D;
+  for (int e = threadIdx.x; e < F * D; e += blockDim.x) xs[(e / D) * ld + e % D] = src[e];
+  __syncthreads();
+  const int P = F * (F - 1) / 2;
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    // invert p = i(i-1)/2 + j
+    int i = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)p)) * 0.5f);
+    while (i * (i - 1) / 2 > p) --i;
+    while ((i + 1) * i / 2 <= p) ++i;
+    const int j = p - i * (i - 1) / 2;
+    const float* a = xs + i * ld;
+    const float* c = xs + j * ld;
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) s += a[d] * c[d];
+    out[b * (int64_t)P + p] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// CrossNet layer: out[b,o] = x0[b,o] * (sum_k xl[b,k] W[o,k] + bias[o]) + xl[b,o]
+// bf16 operands, fp32 accumulate, v_mfma_f32_16x16x32_bf16.
+// Block tile 128 (rows of the batch) x 128 (output features), 4 waves as
+// 2x2, each wave 64x64 = 4x4 MFMA tiles; K step 32 staged through LDS with
+// rows padded to 80 B.  A = xl [B, d] and W [d, d] are both K-contiguous,
+// so every fragment is one 16-B LDS read (lane l: row l&15, k 8(l>>4)..+7).
+// ---------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  // round-to-nearest-even; NaN stays NaN
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffff) > 0x7f800000) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fff + ((u >> 16) & 1);
+  return (uint16_t)(u >> 16);
+}
+
+static constexpr int CN_BM = 128, CN_BN = 128, CN_BK = 32, CN_LDS_ROW = 40;  // 40 shorts = 80 B
+
+__global__ __launch_bounds__(256) void crossnet_kernel(const uint16_t* __restrict__ x0,
+                                                       const uint16_t* __restrict__ xl,
+                                                       const uint16_t* __restrict__ W,
+                                                       const float* __restrict__ bias, int64_t M,
+                                                       int d, uint16_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint16_t sA[CN_BM * CN_LDS_ROW];
+  __shared__ __attribute__((aligned(16))) uint16_t sB[CN_BN * CN_LDS_ROW];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t m0 = (int64_t)blockIdx.y * CN_BM;
+  const int n0 = blockIdx.x * CN_BN;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < d; k0 += CN_BK) {
+    // stage: 128 rows x 4 chunks of 8 bf16 per operand = 512 chunks, 2 per thread
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int c = tid + r * 256;
+      const int row = c >> 2, kc = (c & 3) * 8;
+      bf16x8 va = bf16x8{0, 0, 0, 0, 0, 0, 0, 0}, vb = va;
+      const int64_t gm = m0 + row;
+      const int gn = n0 + row;
+      const int gk = k0 + kc;
+      if (gm < M && gk < d) va = *reinterpret_cast<const bf16x8*>(xl + gm * d + gk);
+      if (gn < d && gk < d) vb = *reinterpret_cast<const bf16x8*>(W + (int64_t)gn * d + gk);
+      *reinterpret_cast<bf16x8*>(sA + row * CN_LDS_ROW + kc) = va;
+      *reinterpret_cast<bf16x8*>(sB + row * CN_LDS_ROW + kc) = vb;
+    }
+    __syncthreads();
+    bf16x8 fa[4], fb[4];
+    const int fr = lane & 15, fk = (lane >> 4) * 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      fa[i] = *reinterpret_cast<const bf16x8*>(sA + (wm * 64 + i * 16 + fr) * CN_LDS_ROW + fk);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      fb[j] = *reinterpret_cast<const bf16x8*>(sB + (wn * 64 + j * 16 + fr) * CN_LDS_ROW + fk);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    __syncthreads();
+  }
+  // epilogue: C/D map col = lane&15, row = (lane>>4)*4 + reg
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wn * 64 + j * 16 + (lane & 15);
+      if (col >= d) continue;
+      const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        if (row >= M) continue;
+        const float lin = acc[i][j][r] + bv;
+        const float v = bf2f(x0[row * d + col]) * lin + bf2f(xl[row * d + col]);
+        out[row * d + col] = f2bf(v);
+      }
+    }
+}
+
+}  // namespace dr
+
+extern "C" {
+
+int dr_fm2(const float* emb, int64_t batch, int fields, int dim, float* out, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && fields > 0 && dim > 0 && dim % 4 == 0, DR_INVALID_ARGUMENT,
+             "dr_fm2: dim must be a multiple of 4");
+  if (batch == 0) return DR_OK;
+  const int64_t n = batch * (dim / 4);
+  hipLaunchKernelGGL(fm2_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, S(stream), emb,
+                     batch, fields, dim, out);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_fm2_grad(const float* emb, const float* top_grad, int64_t batch, int fields, int dim,
+                float* grad_emb, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && fields > 0 && dim > 0, DR_INVALID_ARGUMENT, "bad shape");
+  if (batch == 0) return DR_OK;
+  const int64_t n = batch * dim;
+  hipLaunchKernelGGL(fm2_grad_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, S(stream),
+                     emb, top_grad, batch, fields, dim, grad_emb);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_dot_interaction(const float* x, int64_t batch, int fields, int dim, float* out,
+                       void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && fields > 1 && dim > 0, DR_INVALID_ARGUMENT, "bad shape");
+  const size_t lds = (size_t)fields * (dim + 1) * sizeof(float);
+  DR_REQUIRE(lds <= 64 * 1024, DR_INVALID_ARGUMENT, "fields*dim too large for one block");
+  if (batch == 0) return DR_OK;
+  hipLaunchKernelGGL(dot_kernel, dim3((unsigned)batch), dim3(256), lds, S(stream), x, fields, dim,
+                     out);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_crossnet_layer_bf16(const uint16_t* x0, const uint16_t* xl, const uint16_t* W,
+                           const float* bias, int64_t batch, int d, uint16_t* out, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && d > 0 && d % 8 == 0, DR_INVALID_ARGUMENT,
+             "dr_crossnet_layer_bf16: d must be a multiple of 8 (pad features)");
+  DR_REQUIRE(((uintptr_t)x0 | (uintptr_t)xl | (uintptr_t)W) % 16 == 0, DR_INVALID_ARGUMENT,
+             "operands must be 16B aligned");
+  if (batch == 0) return DR_OK;
+  dim3 grid((unsigned)ceil_div(d, CN_BN), (unsigned)ceil_div(batch, CN_BM));
+  hipLaunchKernelGGL(crossnet_kernel, grid, dim3(256), 0, S(stream), x0, xl, W, bias, batch, d,
+                     out);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,741 @@
+// pool.hip -- the hot path: grouped fused lookup + segment pooling, dense row
+// gather, CSR bag offsets, deterministic segment-sum backward.
+//
+// Layout: a row of `dim` fp32 values is covered by a lane group of G lanes,
+// each lane owning CPL chunks of VEC (4 -> dwordx4) consecutive floats, so a
+// wave64 moves 64 x 16 B = 1 KiB per load instruction.  D=128 fp32: G=32,
+// CPL=1 (two rows per wave instruction); D=64: G=16 (four rows).  A group
+// owns NB consecutive bags of one table and issues all their row loads
+// before the first store (memory-level parallelism for the random row
+// reads, which are the HBM-bound part: SURVEY.md section 8d "row gather").
+//
+// Pooling replays the reference association order exactly:
+//  ORDER_ALI: SparseSegmentReduction::Reduce
+//             (core/kernels/segment_reduction_ali_ops_util.h:193-318)
+//  ORDER_SEQ: FusedEmbeddingLocalSparseLookUp EmbeddingLookUp
+//             (core/kernels/fused_embedding/fused_embedding_local_ops_gpu.cu.cc:41-84)
+// fp32 adds are separate roundings (built with -ffp-contract=off).
+#include "dr_common.h"
+
+namespace dr {
+
+struct PoolArgs {
+  dr_pool_desc d[DR_MAX_GROUP];
+};
+
+template <int VEC>
+struct VecT;
+template <>
+struct VecT<4> {
+  using T = float4;
+};
+template <>
+struct VecT<1> {
+  using T = float;
+};
+
+__device__ __forceinline__ float4 vadd(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float vadd(float a, float b) { return a + b; }
+__device__ __forceinline__ float4 vdiv(float4 a, float q) {
+  return make_float4(a.x / q, a.y / q, a.z / q, a.w / q);
+}
+__device__ __forceinline__ float vdiv(float a, float q) { return a / q; }
+__device__ __forceinline__ float4 vmul(float4 a, float q) {
+  return make_float4(a.x * q, a.y * q, a.z * q, a.w * q);
+}
+__device__ __forceinline__ float vmul(float a, float q) { return a * q; }
+__device__ __forceinline__ float vdot(float4 a) { return a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w; }
+__device__ __forceinline__ float vdot(float a) { return a * a; }
+template <class V>
+__device__ __forceinline__ V vzero();
+template <>
+__device__ __forceinline__ float4 vzero<float4>() {
+  return make_float4(0.f, 0.f, 0.f, 0.f);
+}
+template <>
+__device__ __forceinline__ float vzero<float>() {
+  return 0.f;
+}
+
+// Sum over the G lanes of a group (xor butterfly stays inside the group).
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Pointer to the row selected by nnz position k (nullptr -> zero row).
+__device__ __forceinline__ const float* select_row(const dr_pool_desc& d, int64_t k, int dim,
+                                                   int* st) {
+  int64_t r;
+  if (d.ids) {
+    r = d.ids[k];
+  } else if (!d.rows) {
+    r = d.idx[k];
+  } else {
+    r = d.rows[d.idx[k]];
+    if (r < 0) return d.default_rows + (-r - 1) * d.default_stride;
+    return d.pool + r * (int64_t)dim;
+  }
+  if (r < 0 || r >= d.pool_rows) {
+    latch(st, DR_INVALID_ARGUMENT);
+    return nullptr;
+  }
+  return d.pool + r * (int64_t)dim;
+}
+
+template <int VEC, int G, int CPL>
+struct Row {
+  typename VecT<VEC>::T v[CPL];
+};
+
+template <int VEC, int G, int CPL>
+__device__ __forceinline__ void load_row(Row<VEC, G, CPL>& x, const float* p, int lg, int dv) {
+  using V = typename VecT<VEC>::T;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = lg + c * G;
+    x.v[c] = (p && col < dv) ? reinterpret_cast<const V*>(p)[col] : vzero<V>();
+  }
+}
+
+template <int VEC, int G, int CPL>
+__device__ __forceinline__ void store_row(const Row<VEC, G, CPL>& x, float* p, int lg, int dv) {
+  using V = typename VecT<VEC>::T;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = lg + c * G;
+    if (col < dv) reinterpret_cast<V*>(p)[col] = x.v[c];
+  }
+}
+
+// clip_by_norm (embedding_ops._clip -> clip_ops.clip_by_norm) for ORDER_ALI,
+// and the fused kernel's `emb *= max_norm / l2` (fused_embedding_local_ops_gpu.
+// cu.cc:59-71) for ORDER_SEQ.  Enabled iff max_norm >= 0.
+template <int VEC, int G, int CPL, int ORDER>
+__device__ __forceinline__ void clip_row(Row<VEC, G, CPL>& x, float max_norm) {
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) s += vdot(x.v[c]);
+  s = group_sum<G>(s);
+  if (ORDER == DR_ORDER_ALI) {
+    const float l2 = s > 0.f ? sqrtf(s) : s;
+    const float den = l2 > max_norm ? l2 : max_norm;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) x.v[c] = vdiv(vmul(x.v[c], max_norm), den);
+  } else {
+    const float l2 = sqrtf(s);
+    if (l2 > max_norm) {
+      const float f = max_norm / l2;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) x.v[c] = vmul(x.v[c], f);
+    }
+  }
+}
+
+template <int VEC, int G, int CPL>
+__device__ __forceinline__ void acc_add(Row<VEC, G, CPL>& a, const Row<VEC, G, CPL>& b) {
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) a.v[c] = vadd(a.v[c], b.v[c]);
+}
+
+template <int VEC, int G, int CPL, int ORDER>
+__device__ __forceinline__ void fetch(Row<VEC, G, CPL>& x, const dr_pool_desc& d, int64_t k,
+                                      int dim, int lg, int dv, int* st) {
+  load_row<VEC, G, CPL>(x, select_row(d, k, dim, st), lg, dv);
+  if (d.max_norm >= 0.f) clip_row<VEC, G, CPL, ORDER>(x, d.max_norm);
+}
+
+// One bag, general length, in the reference association order.
+template <int VEC, int G, int CPL, int ORDER>
+__device__ void pool_bag(const dr_pool_desc& d, int64_t b, int dim, int lg, int dv, int* st) {
+  using R = Row<VEC, G, CPL>;
+  const int64_t k0 = d.bag_off[b];
+  const int64_t num = (int64_t)d.bag_off[b + 1] - k0;
+  float* out = d.out + b * d.out_stride;
+  R acc;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<typename VecT<VEC>::T>();
+  if (num <= 0) {
+    store_row<VEC, G, CPL>(acc, out, lg, dv);
+    return;
+  }
+  if (d.weights) {
+    // embedding_ops.py:609-651: gather * w, segment_sum, / sum(w) or sqrt(sum(w^2))
+    float wsum = 0.f;
+    for (int64_t k = 0; k < num; ++k) {
+      R x;
+      fetch<VEC, G, CPL, ORDER>(x, d, k0 + k, dim, lg, dv, st);
+      const float w = d.weights[k0 + k];
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) acc.v[c] = vadd(acc.v[c], vmul(x.v[c], w));
+      wsum = wsum + (d.combiner == DR_COMBINER_SQRTN ? w * w : w);
+    }
+    if (d.combiner != DR_COMBINER_SUM) {
+      const float q = d.combiner == DR_COMBINER_SQRTN ? sqrtf(wsum) : wsum;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) acc.v[c] = vdiv(acc.v[c], q);
+    }
+    store_row<VEC, G, CPL>(acc, out, lg, dv);
+    return;
+  }
+  if (ORDER == DR_ORDER_SEQ) {
+    // out = 0; out += e_k ...; Combine: / sqrtf(n) or / n
+    int64_t k = 0;
+    for (; k + 4 <= num; k += 4) {
+      R x0, x1, x2, x3;
+      fetch<VEC, G, CPL, ORDER>(x0, d, k0 + k, dim, lg, dv, st);
+      fetch<VEC, G, CPL, ORDER>(x1, d, k0 + k + 1, dim, lg, dv, st);
+      fetch<VEC, G, CPL, ORDER>(x2, d, k0 + k + 2, dim, lg, dv, st);
+      fetch<VEC, G, CPL, ORDER>(x3, d, k0 + k + 3, dim, lg, dv, st);
+      acc_add(acc, x0);
+      acc_add(acc, x1);
+      acc_add(acc, x2);
+      acc_add(acc, x3);
+    }
+    for (; k < num; ++k) {
+      R x;
+      fetch<VEC, G, CPL, ORDER>(x, d, k0 + k, dim, lg, dv, st);
+      acc_add(acc, x);
+    }
+    if (d.combiner != DR_COMBINER_SUM) {
+      const float q = d.combiner == DR_COMBINER_SQRTN ? sqrtf((float)num) : (float)num;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) acc.v[c] = vdiv(acc.v[c], q);
+    }
+    store_row<VEC, G, CPL>(acc, out, lg, dv);
+    return;
+  }
+  // ORDER_ALI
+  if (num == 1) {
+    fetch<VEC, G, CPL, ORDER>(acc, d, k0, dim, lg, dv, st);
+    store_row<VEC, G, CPL>(acc, out, lg, dv);
+    return;
+  }
+  int64_t r = num % 8;
+  if (r == 0) r = 8;
+  if (r == 1) r = 9;
+  {
+    R x[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j)
+      if (j < r) fetch<VEC, G, CPL, ORDER>(x[j], d, k0 + j, dim, lg, dv, st);
+    acc = x[0];
+#pragma unroll
+    for (int j = 1; j < 9; ++j)
+      if (j < r) acc_add(acc, x[j]);
+  }
+  if (num < 10 && d.combiner != DR_COMBINER_SUM) {
+    const float m = d.combiner == DR_COMBINER_MEAN ? (float)num : (float)sqrt((double)num);
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) acc.v[c] = vdiv(acc.v[c], m);
+  }
+  for (int64_t g = r; g < num; g += 8) {
+    R x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fetch<VEC, G, CPL, ORDER>(x[j], d, k0 + g + j, dim, lg, dv, st);
+    R s = x[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) acc_add(s, x[j]);
+    acc_add(acc, s);
+  }
+  if (num >= 10 && d.combiner != DR_COMBINER_SUM) {
+    const float q = d.combiner == DR_COMBINER_MEAN ? (float)num : (float)sqrt((double)num);
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) acc.v[c] = vdiv(acc.v[c], q);
+  }
+  store_row<VEC, G, CPL>(acc, out, lg, dv);
+}
+
+// Grid: one group of G lanes per (table, chunk of NB bags).
+template <int VEC, int G, int CPL, int ORDER, int NB>
+__global__ __launch_bounds__(256) void pool_grouped_kernel(PoolArgs args, int T, int64_t B,
+                                                           int dim, int64_t chunks_per_table,
+                                                           int* st) {
+  constexpr int GPB = 256 / G;
+  const int64_t item = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+  if (item >= (int64_t)T * chunks_per_table) return;
+  const int t = (int)(item / chunks_per_table);
+  const int64_t b0 = (item - (int64_t)t * chunks_per_table) * NB;
+  const int lg = threadIdx.x % G;
+  const int dv = dim / VEC;
+  const dr_pool_desc& d = args.d[t];
+  int64_t nbag = B - b0;
+  if (nbag > NB) nbag = NB;
+  // Fast path: every bag holds exactly one id, no weights, no clipping ->
+  // NB independent row loads in flight, then NB stores (pure row copy).
+  int off[NB + 1];
+#pragma unroll
+  for (int j = 0; j <= NB; ++j) off[j] = (j <= nbag) ? d.bag_off[b0 + j] : 0;
+  bool fast = nbag == NB && !d.weights && d.max_norm < 0.f;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) fast = fast && (off[j + 1] - off[j] == 1);
+  if (fast) {
+    Row<VEC, G, CPL> x[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) load_row<VEC, G, CPL>(x[j], select_row(d, off[j], dim, st), lg, dv);
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+      store_row<VEC, G, CPL>(x[j], d.out + (b0 + j) * d.out_stride, lg, dv);
+    return;
+  }
+  for (int j = 0; j < nbag; ++j) pool_bag<VEC, G, CPL, ORDER>(d, b0 + j, dim, lg, dv, st);
+}
+
+template <int VEC, int G, int CPL, int ORDER>
+static int launch_pool(const PoolArgs& a, int T, int64_t B, int dim, hipStream_t s, int* st) {
+  constexpr int NB = 4;
+  const int64_t cpt = ceil_div(B, NB);
+  const int64_t items = (int64_t)T * cpt;
+  const int64_t blocks = ceil_div(items, 256 / G);
+  hipLaunchKernelGGL((pool_grouped_kernel<VEC, G, CPL, ORDER, NB>), dim3((unsigned)blocks),
+                     dim3(256), 0, s, a, T, B, dim, cpt, st);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+template <int ORDER>
+static int dispatch_pool(const PoolArgs& a, int T, int64_t B, int dim, hipStream_t s, int* st) {
+  if (dim % 4 == 0) {
+    const int d4 = dim / 4;
+    if (d4 <= 1) return launch_pool<4, 1, 1, ORDER>(a, T, B, dim, s, st);
+    if (d4 <= 2) return launch_pool<4, 2, 1, ORDER>(a, T, B, dim, s, st);
+    if (d4 <= 4) return launch_pool<4, 4, 1, ORDER>(a, T, B, dim, s, st);
+    if (d4 <= 8) return launch_pool<4, 8, 1, ORDER>(a, T, B, dim, s, st);
+    if (d4 <= 16) return launch_pool<4, 16, 1, ORDER>(a, T, B, dim, s, st);
+    if (d4 <= 32) return launch_pool<4, 32, 1, ORDER>(a, T, B, dim, s, st);
+    if (d4 <= 64) return launch_pool<4, 64, 1, ORDER>(a, T, B, dim, s, st);
+    if (d4 <= 128) return launch_pool<4, 64, 2, ORDER>(a, T, B, dim, s, st);
+    if (d4 <= 256) return launch_pool<4, 64, 4, ORDER>(a, T, B, dim, s, st);
+  } else {
+    if (dim <= 4) return launch_pool<1, 4, 1, ORDER>(a, T, B, dim, s, st);
+    if (dim <= 8) return launch_pool<1, 8, 1, ORDER>(a, T, B, dim, s, st);
+    if (dim <= 16) return launch_pool<1, 16, 1, ORDER>(a, T, B, dim, s, st);
+    if (dim <= 32) return launch_pool<1, 32, 1, ORDER>(a, T, B, dim, s, st);
+    if (dim <= 64) return launch_pool<1, 64, 1, ORDER>(a, T, B, dim, s, st);
+    if (dim <= 256) return launch_pool<1, 64, 4, ORDER>(a, T, B, dim, s, st);
+  }
+  set_error("dim %d unsupported (max 1024 fp32 / 256 unaligned)", dim);
+  return DR_INVALID_ARGUMENT;
+}
+
+// ---------------------------------------------------------------------------
+// CSR bag offsets from sorted segment ids.
+// ---------------------------------------------------------------------------
+template <class TI>
+__global__ void bag_offsets_kernel(const TI* __restrict__ seg, int64_t stride, int64_t n,
+                                   const int64_t* n_dev, int64_t B, int32_t* __restrict__ off,
+                                   int* st) {
+  const int64_t ne = eff_n(n, n_dev);
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > ne) return;
+  if (ne == 0) {
+    for (int64_t r = 0; r <= B; ++r) off[r] = 0;
+    return;
+  }
+  if (k == ne) return;
+  int64_t s = (int64_t)seg[k * stride];
+  const int64_t prev = k > 0 ? (int64_t)seg[(k - 1) * stride] : -1;
+  if (s < prev || s < 0 || s >= B) {
+    latch(st, DR_INVALID_ARGUMENT);
+    s = s < 0 ? 0 : (s >= B ? B - 1 : s);
+    if (s < prev) return;
+  }
+  for (int64_t r = prev + 1; r <= s; ++r) off[r] = (int32_t)k;
+  if (k == ne - 1)
+    for (int64_t r = s + 1; r <= B; ++r) off[r] = (int32_t)ne;
+}
+
+template <class TI>
+static int launch_bag_offsets(const TI* seg, int64_t stride, int64_t n, const int64_t* n_dev,
+                              int64_t B, int32_t* off, hipStream_t s) {
+  int* st = status_word();
+  DR_REQUIRE(st, DR_INTERNAL, "status word unavailable");
+  const unsigned blocks = (unsigned)ceil_div(n + 1, 256);
+  hipLaunchKernelGGL(bag_offsets_kernel<TI>, dim3(blocks), dim3(256), 0, s, seg, stride, n, n_dev,
+                     B, off, st);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Row gather (ResourceGather): group per index, NB indices per group.
+// ---------------------------------------------------------------------------
+template <int VEC, int G, int CPL>
+__global__ __launch_bounds__(256) void gather_kernel(const float* __restrict__ table, int64_t rows,
+                                                     int dim, const int64_t* __restrict__ ids,
+                                                     int64_t n, float* __restrict__ out, int* st) {
+  constexpr int GPB = 256 / G;
+  constexpr int NB = 4;
+  const int64_t i0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * NB;
+  const int lg = threadIdx.x % G;
+  const int dv = dim / VEC;
+  Row<VEC, G, CPL> x[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const float* p = nullptr;
+    if (i0 + j < n) {
+      const int64_t r = ids[i0 + j];
+      if (r >= 0 && r < rows)
+        p = table + r * (int64_t)dim;
+      else
+        latch(st, DR_INVALID_ARGUMENT);
+    }
+    load_row<VEC, G, CPL>(x[j], p, lg, dv);
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+    if (i0 + j < n) store_row<VEC, G, CPL>(x[j], out + (i0 + j) * (int64_t)dim, lg, dv);
+}
+
+template <int VEC, int G, int CPL>
+static int launch_gather(const float* table, int64_t rows, int dim, const int64_t* ids,
+                         int64_t n, float* out, hipStream_t s, int* st) {
+  const int64_t blocks = ceil_div(ceil_div(n, 4), 256 / G);
+  hipLaunchKernelGGL((gather_kernel<VEC, G, CPL>), dim3((unsigned)blocks), dim3(256), 0, s, table,
+                     rows, dim, ids, n, out, st);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic CSR segment sum: out[u] = init + sum_{j in [off[u],off[u+1])}
+// src[srow(j)] * scale(j), j ascending.  Used for SparseSegment*Grad,
+// UnsortedSegmentSum and the pooled-lookup backward.
+//   mode 0: sum from 0.0f             (UnsortedSegmentSum, Sum grad)
+//   mode 1: ali mean grad (first assigns, scale = float(1/double(cnt)))
+//   mode 2: ali sqrtn grad (scale = float(1/sqrt(double(cnt))))
+// srow(j) = seg_of_pos ? seg_of_pos[perm[j]] : perm[j]; cnt from bag_off.
+// ---------------------------------------------------------------------------
+template <int VEC, int G, int CPL>
+__global__ __launch_bounds__(256) void csr_sum_kernel(
+    const float* __restrict__ src, int64_t src_stride, int64_t src_rows,
+    const int32_t* __restrict__ perm, const int32_t* __restrict__ seg_of_pos,
+    const int32_t* __restrict__ off, const int32_t* __restrict__ bag_off, int64_t U,
+    const int64_t* U_dev, int dim, int mode, float* __restrict__ out, int* st) {
+  constexpr int GPB = 256 / G;
+  const int64_t u = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+  const int64_t ue = eff_n(U, U_dev);
+  if (u >= ue) return;
+  const int lg = threadIdx.x % G;
+  const int dv = dim / VEC;
+  using R = Row<VEC, G, CPL>;
+  using V = typename VecT<VEC>::T;
+  R acc;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<V>();
+  const int32_t j0 = off[u], j1 = off[u + 1];
+  bool first = true;
+  for (int32_t j = j0; j < j1; ++j) {
+    const int32_t p = perm[j];
+    const int64_t r = seg_of_pos ? (int64_t)seg_of_pos[p] : (int64_t)p;
+    R x;
+    const float* rp = nullptr;
+    if (r >= 0 && r < src_rows)
+      rp = src + r * src_stride;
+    else
+      latch(st, DR_INVALID_ARGUMENT);
+    load_row<VEC, G, CPL>(x, rp, lg, dv);
+    if (mode == 0) {
+      acc_add(acc, x);
+    } else {
+      const int32_t cnt = (rp && bag_off) ? bag_off[r + 1] - bag_off[r] : 1;
+      if (cnt != 1) {
+        const float sc = mode == 2 ? (float)(1.0 / sqrt((double)cnt)) : (float)(1.0 / (double)cnt);
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) x.v[c] = vmul(x.v[c], sc);
+      }
+      if (first)
+        acc = x;
+      else
+        acc_add(acc, x);
+    }
+    first = false;
+  }
+  store_row<VEC, G, CPL>(acc, out + u * (int64_t)dim, lg, dv);
+}
+
+template <int VEC, int G, int CPL>
+static int launch_csr_sum(const float* src, int64_t src_stride, int64_t src_rows,
+                          const int32_t* perm, const int32_t* seg_of_pos, const int32_t* off,
+                          const int32_t* bag_off, int64_t U, const int64_t* U_dev, int dim,
+                          int mode, float* out, hipStream_t s, int* st) {
+  const int64_t blocks = ceil_div(U > 0 ? U : 1, 256 / G);
+  hipLaunchKernelGGL((csr_sum_kernel<VEC, G, CPL>), dim3((unsigned)blocks), dim3(256), 0, s, src,
+                     src_stride, src_rows, perm, seg_of_pos, off, bag_off, U, U_dev, dim, mode,
+                     out, st);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+static int dispatch_csr_sum(const float* src, int64_t src_stride, int64_t src_rows,
+                            const int32_t* perm, const int32_t* seg_of_pos, const int32_t* off,
+                            const int32_t* bag_off, int64_t U, const int64_t* U_dev, int dim,
+                            int mode, float* out, hipStream_t s, int* st) {
+#define DR_CSR(V, G, C) \
+  return launch_csr_sum<V, G, C>(src, src_stride, src_rows, perm, seg_of_pos, off, bag_off, U, U_dev, dim, mode, out, s, st)
+  if (dim % 4 == 0 && (src_stride % 4) == 0) {
+    const int d4 = dim / 4;
+    if (d4 <= 2) DR_CSR(4, 2, 1);
+    if (d4 <= 4) DR_CSR(4, 4, 1);
+    if (d4 <= 8) DR_CSR(4, 8, 1);
+    if (d4 <= 16) DR_CSR(4, 16, 1);
+    if (d4 <= 32) DR_CSR(4, 32, 1);
+    if (d4 <= 64) DR_CSR(4, 64, 1);
+    if (d4 <= 256) DR_CSR(4, 64, 4);
+  } else {
+    if (dim <= 8) DR_CSR(1, 8, 1);
+    if (dim <= 32) DR_CSR(1, 32, 1);
+    if (dim <= 64) DR_CSR(1, 64, 1);
+    if (dim <= 256) DR_CSR(1, 64, 4);
+  }
+#undef DR_CSR
+  set_error("dim %d unsupported", dim);
+  return DR_INVALID_ARGUMENT;
+}
+
+// seg (int32) -> sort keys; negatives go to a sentinel bucket past `limit`.
+__global__ void keys_from_i32_kernel(const int32_t* __restrict__ seg, int64_t n, int64_t limit,
+                                     uint64_t* __restrict__ keys, int32_t* __restrict__ vals,
+                                     int* st) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int64_t s = seg[i];
+  if (s >= limit) {
+    latch(st, DR_INVALID_ARGUMENT);
+    s = limit;
+  }
+  keys[i] = (uint64_t)(s < 0 ? limit : s);
+  vals[i] = (int32_t)i;
+}
+
+static int bits_for(int64_t x) {
+  int b = 0;
+  while (b < 63 && ((int64_t)1 << b) <= x) ++b;
+  return b;
+}
+
+struct SegSumWs {
+  uint64_t* kin;
+  int32_t* vin;
+  uint64_t* kout;
+  int32_t* perm;
+  int32_t* off;
+  void* sort_ws;
+  size_t sort_bytes;
+};
+
+static SegSumWs carve_segsum(void* ws, int64_t n, int64_t num_out, size_t* used) {
+  Carver c(ws);
+  SegSumWs w;
+  const int64_t nn = n > 0 ? n : 1;
+  w.kin = c.take<uint64_t>(nn);
+  w.vin = c.take<int32_t>(nn);
+  w.kout = c.take<uint64_t>(nn);
+  w.perm = c.take<int32_t>(nn);
+  w.off = c.take<int32_t>(num_out + 2);
+  w.sort_bytes = dr_sort_pairs_workspace_size(n);
+  w.sort_ws = c.take<char>(w.sort_bytes);
+  if (used) *used = c.used + 256;
+  return w;
+}
+
+// Shared driver: group positions by seg (stable), then CSR-sum.
+static int segsum_driver(const int32_t* keyseg, int64_t n, int64_t num_out, const int64_t* U_dev,
+                         const float* src, int64_t src_stride, int64_t src_rows,
+                         const int32_t* seg_of_pos, const int32_t* bag_off, int dim, int mode,
+                         float* out, void* ws, hipStream_t s) {
+  int* st = status_word();
+  DR_REQUIRE(st, DR_INTERNAL, "status word unavailable");
+  size_t used = 0;
+  SegSumWs w = carve_segsum(ws, n, num_out, &used);
+  if (num_out == 0) return DR_OK;
+  if (n == 0) {
+    DR_HIP(hipMemsetAsync(out, 0, (size_t)num_out * dim * sizeof(float), s));
+    return DR_OK;
+  }
+  hipLaunchKernelGGL(keys_from_i32_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
+                     keyseg, n, num_out, w.kin, w.vin, st);
+  DR_LAUNCH_CHECK();
+  int rc = dr_sort_pairs(w.kin, w.vin, w.kout, w.perm, n, 0, bits_for(num_out), w.sort_ws,
+                         w.sort_bytes, s);
+  if (rc) return rc;
+  // offsets over num_out + 1 buckets (the last one collects skipped positions)
+  rc = launch_bag_offsets<uint64_t>(w.kout, 1, n, nullptr, num_out + 1, w.off, s);
+  if (rc) return rc;
+  return dispatch_csr_sum(src, src_stride, src_rows, w.perm, seg_of_pos, w.off, bag_off, num_out,
+                          U_dev, dim, mode, out, s, st);
+}
+
+}  // namespace dr
+
+// ===========================================================================
+extern "C" {
+
+int dr_pool_grouped(const dr_pool_desc* descs_host, int num_tables, int64_t batch, int dim,
+                    int order, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(num_tables >= 1 && num_tables <= DR_MAX_GROUP, DR_INVALID_ARGUMENT,
+             "num_tables must be in [1, %d]", DR_MAX_GROUP);
+  DR_REQUIRE(batch >= 0 && dim > 0, DR_INVALID_ARGUMENT, "bad batch/dim");
+  if (batch == 0) return DR_OK;
+  PoolArgs a;
+  memset(&a, 0, sizeof(a));
+  for (int t = 0; t < num_tables; ++t) {
+    const dr_pool_desc& d = descs_host[t];
+    DR_REQUIRE(d.pool && d.bag_off && d.out && (d.ids || d.idx), DR_INVALID_ARGUMENT,
+               "table %d: missing pointers", t);
+    if (dim % 4 == 0)
+      DR_REQUIRE(((uintptr_t)d.pool & 15) == 0 && ((uintptr_t)d.out & 15) == 0 &&
+                     d.out_stride % 4 == 0 &&
+                     (!d.default_rows || ((uintptr_t)d.default_rows & 15) == 0),
+                 DR_INVALID_ARGUMENT, "table %d: pool/out must be 16B aligned with stride %% 4", t);
+    a.d[t] = d;
+  }
+  int* st = status_word();
+  DR_REQUIRE(st, DR_INTERNAL, "status word unavailable");
+  hipStream_t s = S(stream);
+  if (order == DR_ORDER_SEQ) return dispatch_pool<DR_ORDER_SEQ>(a, num_tables, batch, dim, s, st);
+  return dispatch_pool<DR_ORDER_ALI>(a, num_tables, batch, dim, s, st);
+}
+
+int dr_bag_offsets(const int64_t* seg, int64_t n, int64_t batch, int32_t* bag_off,
+                   void* stream) {
+  return dr::launch_bag_offsets<int64_t>(seg, 1, n, nullptr, batch, bag_off, dr::S(stream));
+}
+
+int dr_bag_offsets_i32(const int32_t* seg, int64_t n, int64_t batch, int32_t* bag_off,
+                       void* stream) {
+  return dr::launch_bag_offsets<int32_t>(seg, 1, n, nullptr, batch, bag_off, dr::S(stream));
+}
+
+// Strided variant for sp_indices[:, 0] (stride 2), used by the fused ops.
+int dr_bag_offsets_strided(const int64_t* seg, int64_t stride, int64_t n, int64_t batch,
+                           int32_t* bag_off, void* stream) {
+  return dr::launch_bag_offsets<int64_t>(seg, stride, n, nullptr, batch, bag_off, dr::S(stream));
+}
+
+int dr_gather(const float* table, int64_t rows, int64_t dim, const int64_t* ids, int64_t n,
+              float* out, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(n >= 0 && dim > 0 && dim <= 1024, DR_INVALID_ARGUMENT, "bad gather shape");
+  if (n == 0) return DR_OK;
+  int* st = status_word();
+  hipStream_t s = S(stream);
+  const int d = (int)dim;
+  const bool al = ((uintptr_t)table & 15) == 0 && ((uintptr_t)out & 15) == 0;
+  if (d % 4 == 0 && al) {
+    const int d4 = d / 4;
+    if (d4 <= 4) return launch_gather<4, 4, 1>(table, rows, d, ids, n, out, s, st);
+    if (d4 <= 8) return launch_gather<4, 8, 1>(table, rows, d, ids, n, out, s, st);
+    if (d4 <= 16) return launch_gather<4, 16, 1>(table, rows, d, ids, n, out, s, st);
+    if (d4 <= 32) return launch_gather<4, 32, 1>(table, rows, d, ids, n, out, s, st);
+    if (d4 <= 64) return launch_gather<4, 64, 1>(table, rows, d, ids, n, out, s, st);
+    return launch_gather<4, 64, 4>(table, rows, d, ids, n, out, s, st);
+  }
+  if (d <= 8) return launch_gather<1, 8, 1>(table, rows, d, ids, n, out, s, st);
+  if (d <= 32) return launch_gather<1, 32, 1>(table, rows, d, ids, n, out, s, st);
+  if (d <= 64) return launch_gather<1, 64, 1>(table, rows, d, ids, n, out, s, st);
+  if (d <= 256) return launch_gather<1, 64, 4>(table, rows, d, ids, n, out, s, st);
+  set_error("dim %d unsupported", d);
+  return DR_INVALID_ARGUMENT;
+}
+
+size_t dr_segment_workspace_size(int64_t num_segments) {
+  return (size_t)(num_segments + 2) * sizeof(int32_t) + 512;
+}
+
+int dr_sparse_segment_reduce(const float* data, int64_t data_rows, int64_t dim,
+                             const int32_t* idx, const int32_t* seg, int64_t n,
+                             int64_t num_segments, int combiner, float* out, void* ws,
+                             size_t ws_bytes, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(ws_bytes >= dr_segment_workspace_size(num_segments), DR_INVALID_ARGUMENT,
+             "workspace too small");
+  DR_REQUIRE(num_segments >= 0 && dim > 0, DR_INVALID_ARGUMENT, "bad shape");
+  if (num_segments == 0) return DR_OK;
+  int32_t* off = static_cast<int32_t*>(ws);
+  int rc = launch_bag_offsets<int32_t>(seg, 1, n, nullptr, num_segments, off, S(stream));
+  if (rc) return rc;
+  dr_pool_desc d;
+  memset(&d, 0, sizeof(d));
+  d.pool = data;
+  d.pool_rows = data_rows;
+  d.idx = idx;
+  d.bag_off = off;
+  d.out = out;
+  d.out_stride = dim;
+  d.combiner = combiner;
+  d.max_norm = -1.0f;
+  return dr_pool_grouped(&d, 1, num_segments, (int)dim, DR_ORDER_ALI, stream);
+}
+
+size_t dr_segment_grad_workspace_size(int64_t n, int64_t grad_rows, int64_t out_rows) {
+  size_t used = 0;
+  dr::carve_segsum(nullptr, n, out_rows, &used);
+  return used + (size_t)(grad_rows + 2) * sizeof(int32_t) + 512;
+}
+
+int dr_sparse_segment_reduce_grad(const float* grad, int64_t grad_rows, int64_t dim,
+                                  const int32_t* idx, const int32_t* seg, int64_t n,
+                                  int64_t out_rows, int combiner, float* out, void* ws,
+                                  size_t ws_bytes, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(ws_bytes >= dr_segment_grad_workspace_size(n, grad_rows, out_rows),
+             DR_INVALID_ARGUMENT, "workspace too small");
+  size_t used = 0;
+  carve_segsum(nullptr, n, out_rows, &used);
+  int32_t* bag_off = reinterpret_cast<int32_t*>(static_cast<char*>(ws) + ((used + 255) & ~255ul));
+  int rc = DR_OK;
+  if (combiner != DR_COMBINER_SUM) {
+    rc = launch_bag_offsets<int32_t>(seg, 1, n, nullptr, grad_rows, bag_off, S(stream));
+    if (rc) return rc;
+  }
+  const int mode = combiner == DR_COMBINER_SUM ? 0 : (combiner == DR_COMBINER_MEAN ? 1 : 2);
+  return segsum_driver(idx, n, out_rows, nullptr, grad, dim, grad_rows, seg,
+                       combiner == DR_COMBINER_SUM ? nullptr : bag_off, (int)dim, mode, out, ws,
+                       S(stream));
+}
+
+size_t dr_unsorted_segment_sum_workspace_size(int64_t n, int64_t num_segments) {
+  size_t used = 0;
+  dr::carve_segsum(nullptr, n, num_segments, &used);
+  return used;
+}
+
+int dr_unsorted_segment_sum(const float* data, int64_t n, int64_t dim, const int32_t* seg,
+                            int64_t num_segments, float* out, void* ws, size_t ws_bytes,
+                            void* stream) {
+  using namespace dr;
+  DR_REQUIRE(ws_bytes >= dr_unsorted_segment_sum_workspace_size(n, num_segments),
+             DR_INVALID_ARGUMENT, "workspace too small");
+  return segsum_driver(seg, n, num_segments, nullptr, data, dim, n, nullptr, nullptr, (int)dim, 0,
+                       out, ws, S(stream));
+}
+
+size_t dr_pool_grad_workspace_size(int64_t n) {
+  size_t used = 0;
+  dr::carve_segsum(nullptr, n, n, &used);
+  return used;
+}
+
+// Backward of dr_pool_grouped (ORDER_ALI / TF grad semantics) for one table:
+// gradient per unique row, deterministic.  seg[k] = bag of position k,
+// idx[k] = unique position; rows past *num_unique are not written.
+int dr_pool_grad(const float* top_grad, int64_t top_stride, int64_t batch, int dim,
+                 const int32_t* bag_off, const int32_t* seg, const int32_t* idx, int64_t n,
+                 const int64_t* num_unique, int combiner, float* grad_unique, void* ws,
+                 size_t ws_bytes, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(ws_bytes >= dr_pool_grad_workspace_size(n), DR_INVALID_ARGUMENT,
+             "workspace too small");
+  const int mode = combiner == DR_COMBINER_SUM ? 0 : (combiner == DR_COMBINER_MEAN ? 1 : 2);
+  return segsum_driver(idx, n, n, num_unique, top_grad, top_stride, batch, seg,
+                       combiner == DR_COMBINER_SUM ? nullptr : bag_off, dim, mode, grad_unique,
+                       ws, S(stream));
+}
+
+}  // extern "C"

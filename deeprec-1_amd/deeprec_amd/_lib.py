@@ -1,0 +1,175 @@
+"""ctypes binding of the engine's C ABI (include/deeprec_amd.h).
+
+The shared library is built in-tree by `make -C deeprec-1_amd` (or
+__graft_entry__.build()).  There is deliberately no CPU fallback: if the
+library is missing, or no GPU is visible, every op raises.
+"""
+import ctypes as C
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdeeprec_amd.so")
+
+# TF error::Code values (include/deeprec_amd.h)
+OK, INVALID_ARGUMENT, NOT_FOUND, ALREADY_EXISTS, RESOURCE_EXHAUSTED, INTERNAL = 0, 3, 5, 6, 8, 13
+_CODE_NAMES = {3: "InvalidArgument", 5: "NotFound", 6: "AlreadyExists", 8: "ResourceExhausted",
+               13: "Internal"}
+
+COMBINERS = {"sum": 0, "mean": 1, "sqrtn": 2}
+ORDER_ALI, ORDER_SEQ = 0, 1
+MAX_GROUP = 32
+
+
+class DeepRecError(RuntimeError):
+    """Raised for a non-OK status (mirrors tf.errors.*Error by code)."""
+
+    def __init__(self, code, msg):
+        super().__init__("%s (%d): %s" % (_CODE_NAMES.get(code, "Error"), code, msg))
+        self.code = code
+
+
+class InvalidArgumentError(DeepRecError, ValueError):
+    pass
+
+
+class DrPoolDesc(C.Structure):
+    _fields_ = [
+        ("pool", C.c_void_p), ("pool_rows", C.c_int64), ("ids", C.c_void_p), ("idx", C.c_void_p),
+        ("rows", C.c_void_p), ("default_rows", C.c_void_p), ("default_stride", C.c_int64),
+        ("bag_off", C.c_void_p),
+        ("weights", C.c_void_p), ("out", C.c_void_p), ("out_stride", C.c_int64),
+        ("combiner", C.c_int32), ("max_norm", C.c_float),
+    ]
+
+
+class DrEvConfig(C.Structure):
+    _fields_ = [
+        ("dim", C.c_int64), ("capacity", C.c_int64), ("steps_to_live", C.c_int64),
+        ("filter_freq", C.c_int64), ("max_element_size", C.c_int64),
+        ("false_positive_probability", C.c_float), ("counter_bits", C.c_int32),
+        ("layout", C.c_int32),
+    ]
+
+
+_P, _I64, _I32, _F32, _SZ, _U64 = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_size_t, C.c_uint64
+
+# name -> (restype, argtypes); must match include/deeprec_amd.h
+SIGNATURES = {
+    "dr_abi_version": (_I32, []),
+    "dr_last_error": (C.c_char_p, []),
+    "dr_status_check": (_I32, [_P]),
+    "dr_unique_workspace_size": (_SZ, [_I64]),
+    "dr_unique": (_I32, [_P, _I64, _P, _P, _P, _P, _P, _SZ, _P]),
+    "dr_sort_pairs_workspace_size": (_SZ, [_I64]),
+    "dr_sort_pairs": (_I32, [_P, _P, _P, _P, _I64, _I32, _I32, _P, _SZ, _P]),
+    "dr_gather": (_I32, [_P, _I64, _I64, _P, _I64, _P, _P]),
+    "dr_segment_workspace_size": (_SZ, [_I64]),
+    "dr_sparse_segment_reduce": (_I32, [_P, _I64, _I64, _P, _P, _I64, _I64, _I32, _P, _P, _SZ, _P]),
+    "dr_segment_grad_workspace_size": (_SZ, [_I64, _I64, _I64]),
+    "dr_sparse_segment_reduce_grad": (_I32, [_P, _I64, _I64, _P, _P, _I64, _I64, _I32, _P, _P, _SZ,
+                                             _P]),
+    "dr_unsorted_segment_sum_workspace_size": (_SZ, [_I64, _I64]),
+    "dr_unsorted_segment_sum": (_I32, [_P, _I64, _I64, _P, _I64, _P, _P, _SZ, _P]),
+    "dr_pool_grouped": (_I32, [_P, _I32, _I64, _I32, _I32, _P]),
+    "dr_bag_offsets": (_I32, [_P, _I64, _I64, _P, _P]),
+    "dr_bag_offsets_i32": (_I32, [_P, _I64, _I64, _P, _P]),
+    "dr_bag_offsets_strided": (_I32, [_P, _I64, _I64, _I64, _P, _P]),
+    "dr_pool_grad_workspace_size": (_SZ, [_I64]),
+    "dr_pool_grad": (_I32, [_P, _I64, _I64, _I32, _P, _P, _P, _I64, _P, _I32, _P, _P, _SZ, _P]),
+    "dr_ev_create": (_I32, [_P, _P, _P]),
+    "dr_ev_create_slot": (_I32, [_P, _I32, _P, _P]),
+    "dr_ev_retain": (_I32, [_P]),
+    "dr_ev_release": (_I32, [_P]),
+    "dr_ev_size": (_I32, [_P, _P, _P]),
+    "dr_ev_dim": (_I64, [_P]),
+    "dr_ev_reserve": (_I32, [_P, _I64, _P]),
+    "dr_ev_resolve_workspace_size": (_SZ, [_I64]),
+    "dr_ev_resolve": (_I32, [_P, _P, _I64, _P, _P, _P, _P, _P, _SZ, _P]),
+    "dr_ev_resolve_grouped": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "dr_ev_pool": (_P, [_P]),
+    "dr_ev_gather_workspace_size": (_SZ, [_I64]),
+    "dr_ev_gather": (_I32, [_P, _P, _I64, _P, _P, _P, _P, _SZ, _P]),
+    "dr_ev_insert": (_I32, [_P, _P, _I64, _P, _P, _P, _I64, _I64, _P]),
+    "dr_ev_insert_synthetic": (_I32, [_P, _I64, _I64, _U64, _P]),
+    "dr_ev_export": (_I32, [_P, _P, _P, _P, _P, _I64, _P, _P]),
+    "dr_ev_key_meta": (_I32, [_P, _P, _I64, _P, _P, _P, _P]),
+    "dr_ev_apply_sgd": (_I32, [_P, _F32, _P, _P, _I64, _P, _I64, _P]),
+    "dr_ev_apply_adagrad": (_I32, [_P, _P, _F32, _P, _P, _I64, _P, _I64, _P]),
+    "dr_ev_apply_adam": (_I32, [_P, _P, _P, _F32, _F32, _F32, _F32, _F32, _F32, _P, _P, _I64, _P,
+                                _I64, _P]),
+    "dr_fused_local_workspace_size": (_SZ, [_I64]),
+    "dr_fused_local_lookup": (_I32, [_P, _I64, _I32, _P, _P, _I64, _I64, _I32, _F32, _P, _P, _P,
+                                     _SZ, _P]),
+    "dr_fused_local_lookup_grad": (_I32, [_P, _P, _I64, _I32, _P, _P, _I64, _I64, _I32, _F32, _P,
+                                          _P]),
+    "dr_partition_workspace_size": (_SZ, [_I64]),
+    "dr_partition_by_owner": (_I32, [_P, _I64, _P, _I32, _P, _P, _P, _P, _SZ, _P]),
+    "dr_rows_scatter": (_I32, [_P, _P, _I64, _P, _I32, _P, _P]),
+    "dr_rows_pack": (_I32, [_P, _P, _I64, _P, _I32, _P, _P]),
+    "dr_fm2": (_I32, [_P, _I64, _I32, _I32, _P, _P]),
+    "dr_fm2_grad": (_I32, [_P, _P, _I64, _I32, _I32, _P, _P]),
+    "dr_dot_interaction": (_I32, [_P, _I64, _I32, _I32, _P, _P]),
+    "dr_crossnet_layer_bf16": (_I32, [_P, _P, _P, _P, _I64, _I32, _P, _P]),
+    "dr_fill_synthetic": (_I32, [_P, _I64, _I32, _U64, _P]),
+    "dr_synth_value": (_F32, [_U64, _I64, _I64]),
+}
+
+_lib = None
+
+
+def load():
+    """Load the HIP library (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DeepRecError(INTERNAL, "HIP extension %s not built; run "
+                                         "`make -C deeprec-1_amd` or __graft_entry__.build()"
+                               % LIB_PATH)
+        lib = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def lib():
+    return _lib if _lib is not None else load()
+
+
+def check(rc):
+    if rc != OK:
+        msg = lib().dr_last_error()
+        msg = msg.decode() if msg else ""
+        if rc == INVALID_ARGUMENT:
+            raise InvalidArgumentError(rc, msg)
+        raise DeepRecError(rc, msg)
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise DeepRecError(INTERNAL, "deeprec_amd ops need an MI355X (no GPU visible); "
+                                     "there is no CPU fallback")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None passes through as NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def workspace(nbytes, device):
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+def status_check(device=None):
+    """Synchronise and raise if a kernel latched an error (OP_REQUIRES)."""
+    check(lib().dr_status_check(stream_handle(device)))

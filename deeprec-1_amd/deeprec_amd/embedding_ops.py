@@ -1,0 +1,380 @@
+"""embedding_lookup / embedding_lookup_sparse / safe_embedding_lookup_sparse /
+fused_embedding_lookup_sparse with DeepRec's argument semantics
+(python/ops/embedding_ops.py:94-675,1209-1344; python/ops/fused_embedding_ops.py:18-97),
+executed by the HIP engine.
+
+The sparse lookup is fused on the GPU: dedup (first-occurrence unique) ->
+EV insert-on-miss resolve -> one grouped gather+pool kernel that reads the
+table rows directly and reduces them in the reference's CPU association
+order, so the [U, D] intermediate of the reference composition is never
+materialised.  Backward produces IndexedSlices per unique id through the
+deterministic segment-grad kernels and hands them to the optimizers
+(training.py) via `pending_grads`, like TF's sparse gradient path.
+"""
+import torch
+
+from . import _lib, ops
+from ._lib import COMBINERS, ORDER_ALI, ORDER_SEQ, DrPoolDesc, check, lib, ptr, stream_handle, workspace
+from .kv_variable_ops import EmbeddingVariable, IndexedSlices
+
+
+class SparseTensor(object):
+    """indices [nnz, 2] int64 (row-major canonical), values [nnz], dense_shape."""
+
+    def __init__(self, indices, values, dense_shape):
+        self.indices = indices
+        self.values = values
+        self.dense_shape = tuple(int(x) for x in dense_shape)
+
+    @property
+    def device(self):
+        return self.values.device
+
+
+class DenseTable(object):
+    """A plain [rows, dim] embedding table (tf.Variable of a hash_bucket column;
+    ResourceGather path, resource_variable_ops.cc:628).  Sparse gradients are
+    queued in pending_grads as IndexedSlices (row ids)."""
+
+    def __init__(self, weight):
+        self.weight = weight.to(torch.float32).contiguous()
+        self.dim = self.weight.shape[1]
+        self.device = self.weight.device
+        self.pending_grads = []
+
+    def get_shape(self):
+        return tuple(self.weight.shape)
+
+
+def _anchor(holder):
+    a = getattr(holder, "_anchor", None)
+    if a is None:
+        a = torch.zeros(1, device=holder.device, requires_grad=True)
+        holder._anchor = a
+    return a
+
+
+def _ev_default_dev(ev):
+    d = getattr(ev, "_default_dev", None)
+    if d is None:
+        d = ev.default_value.contiguous()
+        ev._default_dev = d
+    return d
+
+
+class _Feature(object):
+    """One feature's prepared lookup (everything the pool kernel needs)."""
+
+    def __init__(self, params, values, seg, batch, weights, combiner, max_norm):
+        self.params = params
+        self.values = values
+        self.seg = seg
+        self.batch = batch
+        self.weights = weights
+        self.combiner = combiner
+        self.max_norm = max_norm
+        self.uniq = self.idx = self.U = self.rows = None
+        self.defaults = None
+
+
+def _prepare(f, need_unique):
+    dev = f.values.device
+    f.bag_off = ops.bag_offsets(f.seg, f.batch)
+    p = f.params
+    if isinstance(p, EmbeddingVariable):
+        with_counts = p.filter_freq != 0          # embedding_ops.py:592-596
+        f.uniq, f.idx, cnt, f.U = ops.unique_device(f.values, with_counts)
+        f.defaults = p._defaults_for(f.uniq.numel(), None)
+        f.rows = p.resolve(f.uniq, n_dev=f.U, counts=cnt, defaults=f.defaults)
+    elif need_unique:
+        f.uniq, f.idx, _, f.U = ops.unique_device(f.values)
+
+
+def _desc(f, out, out_stride):
+    d = DrPoolDesc()
+    p = f.params
+    if isinstance(p, EmbeddingVariable):
+        d.pool = p.pool()
+        d.pool_rows = 0
+        d.idx = ptr(f.idx)
+        d.rows = ptr(f.rows)
+        if f.defaults is not None:
+            d.default_rows = ptr(f.defaults)
+            d.default_stride = p.dim
+        else:
+            d.default_rows = ptr(_ev_default_dev(p))
+            d.default_stride = 0
+    else:
+        t = p.weight if isinstance(p, DenseTable) else p
+        d.pool = ptr(t)
+        d.pool_rows = t.shape[0]
+        d.ids = ptr(f.values)
+    d.bag_off = ptr(f.bag_off)
+    d.weights = ptr(f.weights)
+    d.out = out.data_ptr()
+    d.out_stride = out_stride
+    d.combiner = COMBINERS[f.combiner]
+    d.max_norm = -1.0 if f.max_norm is None else float(f.max_norm)
+    return d
+
+
+def _grad_to_slices(f, g, top_stride):
+    """Pooled grad [B, D] (stride) -> IndexedSlices over the unique ids."""
+    if f.weights is not None or f.max_norm is not None:
+        raise NotImplementedError("backward of weighted / max_norm lookups is not implemented")
+    if f.uniq is None:
+        f.uniq, f.idx, _, f.U = ops.unique_device(f.values)
+    dev = g.device
+    n = f.values.numel()
+    D = f.params.dim if not torch.is_tensor(f.params) else f.params.shape[1]
+    gu = torch.empty((n, D), dtype=torch.float32, device=dev)
+    seg32 = f.seg.to(torch.int32).contiguous()
+    wsb = lib().dr_pool_grad_workspace_size(n)
+    ws = workspace(wsb, dev)
+    check(lib().dr_pool_grad(ptr(g), top_stride, f.batch, D, ptr(f.bag_off), ptr(seg32),
+                             ptr(f.idx), n, ptr(f.U), COMBINERS[f.combiner], ptr(gu), ptr(ws), wsb,
+                             stream_handle(dev)))
+    ops._post(dev)
+    return IndexedSlices(gu, f.uniq, f.U)
+
+
+class _LookupFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, feats, order):
+        ctx.feats = feats
+        return _pool_all(feats, order)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        g = grad_out.contiguous()
+        D = None
+        col = 0
+        for f in ctx.feats:
+            D = f.params.dim if not torch.is_tensor(f.params) else f.params.shape[1]
+            gf = g[:, col:col + D]
+            col += D
+            holder = f.params
+            if torch.is_tensor(holder):
+                continue
+            sl = _grad_to_slices(f, gf.contiguous(), D)
+            holder.pending_grads.append(sl)
+        return None, None, None
+
+
+def _run(feats, order=ORDER_ALI, need_grad=None):
+    """Grouped pooled lookup of features sharing the batch -> [B, sum(D_t)]."""
+    if need_grad is None:
+        need_grad = torch.is_grad_enabled() and any(not torch.is_tensor(f.params) for f in feats)
+    for f in feats:
+        _prepare(f, need_unique=False)
+    if need_grad:
+        anchor = [_anchor(f.params) for f in feats if not torch.is_tensor(f.params)][0]
+        return _LookupFn.apply(anchor, feats, order)
+    return _pool_all(feats, order)
+
+
+def _pool_all(feats, order):
+    dev = feats[0].values.device
+    B = feats[0].batch
+    dims = [f.params.dim if not torch.is_tensor(f.params) else f.params.shape[1] for f in feats]
+    total = sum(dims)
+    out = torch.empty((B, total), dtype=torch.float32, device=dev)
+    # group consecutive features of equal dim into <= 32-table launches
+    col = 0
+    i = 0
+    while i < len(feats):
+        j = i
+        while j < len(feats) and dims[j] == dims[i] and j - i < _lib.MAX_GROUP:
+            j += 1
+        descs = []
+        c = col
+        for f in feats[i:j]:
+            descs.append(_desc(f, out[:, c:], total))
+            c += dims[i]
+        ops.pool_grouped(descs, B, dims[i], order, dev)
+        col = c
+        i = j
+    return out
+
+
+def _seg_of(sp_ids):
+    # segment_ids = sp_ids.indices[:, 0] cast to int32 (embedding_ops.py:587-589)
+    return sp_ids.indices[:, 0].to(torch.int32).contiguous()
+
+
+def embedding_lookup_sparse(params, sp_ids, sp_weights=None, partition_strategy="mod", name=None,
+                            combiner=None, max_norm=None):
+    """tf.nn.embedding_lookup_sparse (embedding_ops.py:480-675), 2-D sp_ids."""
+    if combiner is None:
+        combiner = "mean"
+    if combiner not in ("mean", "sqrtn", "sum"):
+        raise ValueError("combiner must be one of 'mean', 'sqrtn' or 'sum'")
+    if isinstance(params, (list, tuple)):
+        if len(params) == 1:
+            params = params[0]
+        else:
+            return _partitioned_lookup_sparse(params, sp_ids, sp_weights, partition_strategy,
+                                              combiner, max_norm)
+    values = sp_ids.values.to(torch.int64).contiguous()
+    w = None if sp_weights is None else sp_weights.values.to(torch.float32).contiguous()
+    f = _Feature(params, values, _seg_of(sp_ids), sp_ids.dense_shape[0], w, combiner, max_norm)
+    return _run([f])
+
+
+def embedding_lookup_sparse_multi(params_list, sp_ids_list, combiner="mean", max_norm=None):
+    """Grouped lookup of several features (one pooled launch per 32 tables);
+    returns the input_layer concatenation [B, sum(D_t)]."""
+    feats = []
+    for p, sp in zip(params_list, sp_ids_list):
+        feats.append(_Feature(p, sp.values.to(torch.int64).contiguous(), _seg_of(sp),
+                              sp.dense_shape[0], None, combiner, max_norm))
+    return _run(feats)
+
+
+def embedding_lookup(params, ids, partition_strategy="mod", name=None, max_norm=None,
+                     ev_init_value=None, counts=None):
+    """tf.nn.embedding_lookup (embedding_ops.py:94-342, 346)."""
+    if isinstance(params, (list, tuple)) and len(params) == 1:
+        params = params[0]
+    if isinstance(params, (list, tuple)):
+        flat = ids.reshape(-1).to(torch.int64)
+        np_ = len(params)
+        if isinstance(params[0], EmbeddingVariable):
+            p_assign = flat % 1000 % np_           # embedding_ops.py:207-209
+            new_ids = flat
+        elif partition_strategy == "mod":
+            p_assign = flat % np_
+            new_ids = flat // np_
+        else:  # "div"
+            sizes = [p.get_shape()[0] if not torch.is_tensor(p) else p.shape[0] for p in params]
+            total = sum(sizes)
+            ipp, extras = total // np_, total % np_
+            p_assign = torch.maximum(flat // (ipp + 1), (flat - extras) // ipp)
+            new_ids = torch.where(p_assign < extras, flat % (ipp + 1), (flat - extras) % ipp)
+        D = params[0].dim if not torch.is_tensor(params[0]) else params[0].shape[1]
+        out = torch.empty((flat.numel(), D), dtype=torch.float32, device=flat.device)
+        for p in range(np_):
+            sel = torch.nonzero(p_assign == p).reshape(-1)
+            if sel.numel() == 0:
+                continue
+            out[sel] = embedding_lookup(params[p], new_ids[sel], ev_init_value=None)
+        res = out.reshape(tuple(ids.shape) + (D,))
+    elif isinstance(params, EmbeddingVariable):
+        res = params.sparse_read(ids, counts=counts, ev_init_value=ev_init_value)
+    else:
+        t = params.weight if isinstance(params, DenseTable) else params
+        res = ops.gather(t, ids)
+    if max_norm is not None:
+        r2 = res.reshape(-1, res.shape[-1])
+        l2 = torch.sqrt((r2 * r2).sum(1, keepdim=True))
+        r2 = r2 * max_norm / torch.maximum(l2, torch.tensor(max_norm, device=r2.device))
+        res = r2.reshape(res.shape)
+    return res
+
+
+def _partitioned_lookup_sparse(params, sp_ids, sp_weights, partition_strategy, combiner,
+                               max_norm):
+    values = sp_ids.values.to(torch.int64)
+    seg = _seg_of(sp_ids)
+    B = sp_ids.dense_shape[0]
+    if isinstance(params[0], EmbeddingVariable) and params[0].filter_freq == 0:
+        uniq, idx = ops.unique(values)
+        counts = None
+    else:
+        uniq, idx, counts = ops.unique_with_counts(values)
+    emb = embedding_lookup(params, uniq, partition_strategy, counts=counts)
+    if max_norm is not None:
+        l2 = torch.sqrt((emb * emb).sum(1, keepdim=True))
+        emb = emb * max_norm / torch.maximum(l2, torch.tensor(max_norm, device=emb.device))
+    if sp_weights is None:
+        fn = {"sum": ops.sparse_segment_sum, "mean": ops.sparse_segment_mean,
+              "sqrtn": ops.sparse_segment_sqrt_n}[combiner]
+        return fn(emb, idx, seg, num_segments=B)
+    f = _Feature(emb, idx.to(torch.int64), seg, B, sp_weights.values.to(torch.float32),
+                 combiner, None)
+    return _run([f], need_grad=False)
+
+
+# ---------------------------------------------------------------------------
+# safe_embedding_lookup_sparse (embedding_ops.py:1209-1344)
+# ---------------------------------------------------------------------------
+def _prune_and_fill(sp_ids, sp_weights, combiner, default_id, prune):
+    ind = sp_ids.indices.to(torch.int64)
+    val = sp_ids.values.to(torch.int64)
+    w = None if sp_weights is None else sp_weights.values.to(torch.float32)
+    B = sp_ids.dense_shape[0]
+    if prune:
+        keep = val >= 0                                       # _prune_invalid_ids
+        if w is not None and combiner != "sum":
+            keep = keep & (w > 0)                             # _prune_invalid_weights
+        ind, val = ind[keep], val[keep]
+        if w is not None:
+            w = w[keep]
+    present = torch.zeros(B, dtype=torch.bool, device=val.device)
+    present[ind[:, 0]] = True
+    empty = ~present
+    fill = torch.nonzero(empty).reshape(-1)
+    if fill.numel():                                          # sparse_fill_empty_rows
+        add_ind = torch.stack([fill, torch.zeros_like(fill)], 1)
+        ind = torch.cat([ind, add_ind])
+        val = torch.cat([val, torch.full((fill.numel(),), int(default_id or 0),
+                                         dtype=torch.int64, device=val.device)])
+        if w is not None:
+            w = torch.cat([w, torch.ones(fill.numel(), dtype=torch.float32, device=w.device)])
+        key = ind[:, 0] * (sp_ids.dense_shape[1] + 1) + ind[:, 1]
+        order = torch.sort(key, stable=True).indices
+        ind, val = ind[order], val[order]
+        if w is not None:
+            w = w[order]
+    sp = SparseTensor(ind, val, sp_ids.dense_shape)
+    spw = None if w is None else SparseTensor(ind, w, sp_ids.dense_shape)
+    return sp, spw, empty
+
+
+def safe_embedding_lookup_sparse(embedding_weights, sparse_ids, sparse_weights=None,
+                                 combiner="mean", default_id=None, name=None,
+                                 partition_strategy="div", max_norm=None, prune=True):
+    if embedding_weights is None:
+        raise ValueError("Missing embedding_weights %s." % embedding_weights)
+    sp, spw, empty = _prune_and_fill(sparse_ids, sparse_weights, combiner, default_id, prune)
+    res = embedding_lookup_sparse(embedding_weights, sp, spw, partition_strategy=partition_strategy,
+                                  combiner=combiner, max_norm=max_norm)
+    if default_id is None:
+        res = torch.where(empty[:, None], torch.zeros_like(res), res)
+    return res
+
+
+# ---------------------------------------------------------------------------
+# fused_embedding_lookup_sparse (python/ops/fused_embedding_ops.py:18-72),
+# local variant: FusedEmbeddingLocalSparseLookUp semantics (sequential sum,
+# then combiner; max_norm per row).
+# ---------------------------------------------------------------------------
+class _FusedLocalFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, table, sp_values, sp_indices, batch, combiner, max_norm):
+        out, vo = ops.fused_embedding_local_sparse_look_up(sp_values, sp_indices, (batch, 0),
+                                                           table, combiner, max_norm)
+        ctx.save_for_backward(table, sp_values, vo)
+        ctx.combiner, ctx.max_norm = combiner, max_norm
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        table, sp_values, vo = ctx.saved_tensors
+        grad_vals = ops.fused_embedding_local_sparse_look_up_grad(
+            g.contiguous(), table, sp_values, vo, ctx.combiner, ctx.max_norm)
+        dense = torch.zeros_like(table)
+        dense.index_add_(0, sp_values.to(torch.int64), grad_vals)
+        return dense, None, None, None, None, None
+
+
+def fused_embedding_lookup_sparse(embedding_weights, sparse_ids, combiner="mean", max_norm=None,
+                                  name=None):
+    table = embedding_weights[0] if isinstance(embedding_weights, (list, tuple)) \
+        else embedding_weights
+    if isinstance(table, DenseTable):
+        table = table.weight
+    mn = -1.0 if max_norm is None else float(max_norm)
+    return _FusedLocalFn.apply(table, sparse_ids.values.to(torch.int64).contiguous(),
+                               sparse_ids.indices.to(torch.int64).contiguous(),
+                               sparse_ids.dense_shape[0], combiner, mn)

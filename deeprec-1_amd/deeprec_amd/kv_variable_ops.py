@@ -1,0 +1,288 @@
+"""EmbeddingVariable -- the GPU-resident counterpart of DeepRec's
+python/ops/kv_variable_ops.py:44-765 (class EmbeddingVariable) and
+python/ops/variables.py:238-330 (EmbeddingVariableOption / CounterFilter /
+CBFFilter).  Storage and the insert-on-miss lookup run in HIP kernels through
+the C ABI (dr_ev_*); this module only holds the handle and the Python-level
+argument semantics.
+"""
+import ctypes as C
+import threading
+
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr, stream_handle, workspace
+
+
+# ---------------------------------------------------------------------------
+# Options (variables.py:238-330)
+# ---------------------------------------------------------------------------
+class CounterFilter(object):
+    def __init__(self, filter_freq=0):
+        self.filter_freq = filter_freq
+
+
+class CBFFilter(object):
+    """Counting Bloom filter admission (embedding_filter.h:27-286)."""
+
+    def __init__(self, filter_freq=0, max_element_size=0, false_positive_probability=-1.0,
+                 counter_type=torch.int64):
+        self.filter_freq = filter_freq
+        self.max_element_size = max_element_size
+        self.false_positive_probability = false_positive_probability
+        bits = {torch.uint8: 8, torch.int8: 8, torch.int16: 16, torch.int32: 32,
+                torch.int64: 64}
+        self.counter_bits = bits.get(counter_type, 64) if not isinstance(counter_type, int) \
+            else counter_type
+
+
+class GlobalStepEvict(object):
+    def __init__(self, steps_to_live=None):
+        self.steps_to_live = steps_to_live
+
+
+class EmbeddingVariableOption(object):
+    def __init__(self, ht_type="", ht_partition_num=1000, evict_option=None, filter_option=None):
+        self.ht_type = ht_type
+        self.ht_partition_num = ht_partition_num
+        self.evict_option = evict_option
+        self.filter_option = filter_option
+
+
+def _default_row(initializer, dim, device):
+    """EV default_value_ (InitializeKvVariableOp input 2, a [dim] tensor)."""
+    if initializer is None:
+        initializer = 0.0
+    if callable(initializer):
+        v = initializer((dim,))
+        v = torch.as_tensor(v, dtype=torch.float32).reshape(dim)
+    else:
+        v = torch.full((dim,), float(initializer), dtype=torch.float32)
+    return v.cpu().contiguous()
+
+
+class IndexedSlices(object):
+    """values [N, D] for rows `indices` [N] (tf.IndexedSlices)."""
+
+    def __init__(self, values, indices, num_valid=None):
+        self.values = values
+        self.indices = indices
+        self.num_valid = num_valid  # optional device int64[1] (<= N)
+
+
+class EmbeddingVariable(object):
+    """Hash-keyed embedding table resident in HBM.
+
+    initializer: float constant, or callable(shape) -> tensor (e.g.
+    lambda s: torch.randn(s) * 0.01).  As in the reference, a callable
+    initializer draws a fresh [N, D] default block per sparse_read call
+    (kv_variable_ops.py:651-654); a constant uses the EV's own default row.
+    """
+
+    def __init__(self, name, embedding_dim, initializer=None, steps_to_live=0, ev_option=None,
+                 capacity=1 << 16, device=None, _primary=None, _slot_index=0):
+        _lib.require_gpu()
+        self.name = name
+        self.dim = int(embedding_dim)
+        self.device = torch.device(device) if device is not None else \
+            torch.device("cuda", torch.cuda.current_device())
+        self.initializer = initializer
+        self._primary = _primary
+        self._slot_index = _slot_index
+        self._lock = threading.Lock()
+        self.pending_grads = []
+        opt = ev_option or EmbeddingVariableOption()
+        f = opt.filter_option
+        self.filter_freq = int(getattr(f, "filter_freq", 0) or 0)
+        if opt.evict_option is not None and opt.evict_option.steps_to_live:
+            steps_to_live = opt.evict_option.steps_to_live
+        self.steps_to_live = int(steps_to_live or 0)
+        default = _default_row(initializer, self.dim, self.device)
+        self._default_host = default
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            if _primary is None:
+                cfg = _lib.DrEvConfig()
+                cfg.dim = self.dim
+                cfg.capacity = int(capacity)
+                cfg.steps_to_live = self.steps_to_live
+                cfg.filter_freq = self.filter_freq
+                cfg.max_element_size = int(getattr(f, "max_element_size", 0) or 0)
+                cfg.false_positive_probability = float(
+                    getattr(f, "false_positive_probability", -1.0))
+                cfg.counter_bits = int(getattr(f, "counter_bits", 64) or 64)
+                cfg.layout = 1 if (self.filter_freq or self.steps_to_live) else 0
+                check(lib().dr_ev_create(C.byref(cfg), default.data_ptr(), C.byref(h)))
+            else:
+                check(lib().dr_ev_create_slot(_primary._h, _slot_index, default.data_ptr(),
+                                              C.byref(h)))
+        self._h = h
+        self._slots = {}
+        self._next_slot = 1
+
+    # -- lifecycle ---------------------------------------------------------
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None):
+                lib().dr_ev_release(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def is_primary(self):
+        return self._primary is None
+
+    def slot(self, name, initializer):
+        """Slot EV sharing this EV's key space (slot_creator.py:82-117)."""
+        if name not in self._slots:
+            idx = self._next_slot
+            self._next_slot += 1
+            self._slots[name] = EmbeddingVariable(self.name + "/" + name, self.dim, initializer,
+                                                  device=self.device, _primary=self,
+                                                  _slot_index=idx)
+        return self._slots[name]
+
+    def get_shape(self):
+        return (None, self.dim)
+
+    @property
+    def default_value(self):
+        return self._default_host.to(self.device)
+
+    def pool(self):
+        """Base pointer of this EV's value rows (device)."""
+        return lib().dr_ev_pool(self._h)
+
+    # -- ops -----------------------------------------------------------------
+    def _defaults_for(self, n, ev_init_value):
+        if ev_init_value is not None:
+            return torch.as_tensor(ev_init_value, dtype=torch.float32,
+                                   device=self.device).expand(n, self.dim).contiguous()
+        if callable(self.initializer):
+            v = self.initializer((n, self.dim))
+            return torch.as_tensor(v, dtype=torch.float32, device=self.device).reshape(
+                n, self.dim).contiguous()
+        return None
+
+    def sparse_read(self, indices, counts=None, ev_init_value=None, name=None):
+        """KvResourceGather / KvResourceGatherV1 (kv_variable_ops.py:644-664)."""
+        ids = indices.reshape(-1).to(torch.int64).contiguous()
+        n = ids.numel()
+        out = torch.empty((n, self.dim), dtype=torch.float32, device=self.device)
+        if n == 0:
+            return out.reshape(tuple(indices.shape) + (self.dim,))
+        dflt = self._defaults_for(n, ev_init_value)
+        cnt = None if counts is None else counts.reshape(-1).to(torch.int32).contiguous()
+        wsb = lib().dr_ev_gather_workspace_size(n)
+        ws = workspace(wsb, self.device)
+        check(lib().dr_ev_gather(self._h, ptr(ids), n, ptr(dflt), ptr(cnt), ptr(out), ptr(ws), wsb,
+                                 stream_handle(self.device)))
+        from .ops import _post
+        _post(self.device)
+        return out.reshape(tuple(indices.shape) + (self.dim,))
+
+    def resolve(self, keys, n_dev=None, counts=None, defaults=None):
+        """Insert-on-miss resolve of (unique) keys to rows; -(i+1) = default row i."""
+        keys = keys.reshape(-1).to(torch.int64).contiguous()
+        n = keys.numel()
+        rows = torch.empty(n, dtype=torch.int64, device=self.device)
+        wsb = lib().dr_ev_resolve_workspace_size(n)
+        ws = workspace(wsb, self.device)
+        check(lib().dr_ev_resolve(self._h, ptr(keys), n, ptr(n_dev), ptr(defaults), ptr(counts),
+                                  ptr(rows), ptr(ws), wsb, stream_handle(self.device)))
+        return rows
+
+    def insert(self, keys, values, versions=None, freqs=None):
+        """KvResourceInsert (core/ops/kv_variable_ops.cc:478-492) with
+        EmbeddingVar::Import semantics: existing rows are kept."""
+        return self._import(keys, values, versions, freqs, 0, 0)
+
+    def import_partitioned(self, keys, values, versions, freqs, partition_id, partition_num):
+        """KvResourceImportV2 restore filter key % 1000 % partition_num == id."""
+        return self._import(keys, values, versions, freqs, partition_id, partition_num)
+
+    def _import(self, keys, values, versions, freqs, pid, pnum):
+        k = keys.reshape(-1).to(device=self.device, dtype=torch.int64).contiguous()
+        v = values.reshape(k.numel(), self.dim).to(device=self.device,
+                                                   dtype=torch.float32).contiguous()
+        ver = None if versions is None else versions.to(device=self.device,
+                                                        dtype=torch.int64).contiguous()
+        fr = None if freqs is None else freqs.to(device=self.device, dtype=torch.int64).contiguous()
+        check(lib().dr_ev_insert(self._h, ptr(k), k.numel(), ptr(v), ptr(ver), ptr(fr), pid, pnum,
+                                 stream_handle(self.device)))
+
+    def insert_synthetic(self, key_begin, n, seed):
+        """Insert keys [key_begin, key_begin+n) with rows synth(seed, key, col)."""
+        check(lib().dr_ev_insert_synthetic(self._h, int(key_begin), int(n), int(seed),
+                                           stream_handle(self.device)))
+
+    def total_count(self):
+        """KvVariableShape: [num keys, dim]."""
+        n = C.c_int64(0)
+        check(lib().dr_ev_size(self._h, C.byref(n), stream_handle(self.device)))
+        return torch.tensor([n.value, self.dim], dtype=torch.int64)
+
+    def export(self):
+        """KvResourceExport -> (keys, values, versions, freqs), keys ascending."""
+        m = C.c_int64(0)
+        st = stream_handle(self.device)
+        check(lib().dr_ev_export(self._h, None, None, None, None, 0, C.byref(m), st))
+        M = m.value
+        keys = torch.empty(M, dtype=torch.int64, device=self.device)
+        vals = torch.empty((M, self.dim), dtype=torch.float32, device=self.device)
+        vers = torch.empty(M, dtype=torch.int64, device=self.device)
+        frqs = torch.empty(M, dtype=torch.int64, device=self.device)
+        check(lib().dr_ev_export(self._h, ptr(keys), ptr(vals), ptr(vers), ptr(frqs), M,
+                                 C.byref(m), st))
+        n = m.value
+        if self.steps_to_live == 0:
+            vers = vers[:0]
+        if self.filter_freq == 0:
+            frqs = frqs[:0]
+        return keys[:n], vals[:n], vers, frqs
+
+    def key_meta(self, keys):
+        """(freq, version, has_row) of keys, host numpy (tests/debug)."""
+        import numpy as np
+        k = np.ascontiguousarray(keys, dtype=np.int64)
+        n = k.shape[0]
+        fr = np.zeros(n, np.int64)
+        ve = np.zeros(n, np.int64)
+        hr = np.zeros(n, np.int32)
+        check(lib().dr_ev_key_meta(self._h, k.ctypes.data, n, fr.ctypes.data, ve.ctypes.data,
+                                   hr.ctypes.data, stream_handle(self.device)))
+        return fr, ve, hr.astype(bool)
+
+    def reserve(self, extra):
+        check(lib().dr_ev_reserve(self._h, int(extra), stream_handle(self.device)))
+
+
+_EV_REGISTRY = {}
+
+
+def get_embedding_variable(name, embedding_dim, key_dtype=torch.int64, initializer=None,
+                           steps_to_live=0, ev_option=None, capacity=1 << 16, device=None,
+                           partitioner=None):
+    """tf.get_embedding_variable (variable_scope.py:2142-2197).
+
+    With `partitioner=n` (fixed_size_partitioner(num_shards=n)) returns a list
+    of n EVs; lookups route key -> shard by key % 1000 % n
+    (embedding_ops.py:207-209)."""
+    if partitioner is not None and int(partitioner) > 1:
+        return [get_embedding_variable("%s/part_%d" % (name, p), embedding_dim, key_dtype,
+                                       initializer, steps_to_live, ev_option, capacity, device)
+                for p in range(int(partitioner))]
+    if name in _EV_REGISTRY:
+        return _EV_REGISTRY[name]
+    ev = EmbeddingVariable(name, embedding_dim, initializer, steps_to_live, ev_option, capacity,
+                           device)
+    _EV_REGISTRY[name] = ev
+    return ev
+
+
+def reset_registry():
+    _EV_REGISTRY.clear()

@@ -1,0 +1,362 @@
+"""Functional GPU ops with DeepRec/TF op names, on torch device tensors.
+
+Each op calls the HIP C ABI (include/deeprec_amd.h) on torch's current stream.
+Data-dependent errors (OP_REQUIRES in the reference) are latched on the
+device; call `status_check()` or enable `set_validate(True)` to have every op
+synchronise and raise, which is what the parity tests do.
+"""
+import os
+
+import torch
+
+from . import _lib
+from ._lib import COMBINERS, ORDER_ALI, ORDER_SEQ, check, lib, ptr, stream_handle, workspace
+
+_VALIDATE = os.environ.get("DEEPREC_AMD_VALIDATE", "0") == "1"
+
+
+def set_validate(on):
+    global _VALIDATE
+    _VALIDATE = bool(on)
+
+
+def _post(device):
+    if _VALIDATE:
+        _lib.status_check(device)
+
+
+def status_check(device=None):
+    _lib.status_check(device)
+
+
+def _dev(t):
+    if not t.is_cuda:
+        raise _lib.DeepRecError(_lib.INVALID_ARGUMENT,
+                                "deeprec_amd ops take device tensors (got %s)" % t.device)
+    return t.device
+
+
+def _c(t, dtype):
+    return t.to(dtype).contiguous()
+
+
+# ---------------------------------------------------------------------------
+# Unique (UniqueAliOp, core/kernels/unique_ali_op.cc:46-180)
+# ---------------------------------------------------------------------------
+def unique_device(x, with_counts=False):
+    """First-occurrence unique with NO host sync.
+
+    Returns (y [n], idx [n] int32, counts [n] int32 or None, num_unique int64[1]);
+    only y[:num_unique] / counts[:num_unique] are meaningful."""
+    dev = _dev(x)
+    x = _c(x.reshape(-1), torch.int64)
+    n = x.numel()
+    y = torch.empty(n, dtype=torch.int64, device=dev)
+    idx = torch.empty(n, dtype=torch.int32, device=dev)
+    cnt = torch.empty(n, dtype=torch.int32, device=dev) if with_counts else None
+    u = torch.empty(1, dtype=torch.int64, device=dev)
+    wsb = lib().dr_unique_workspace_size(n)
+    ws = workspace(wsb, dev)
+    check(lib().dr_unique(ptr(x), n, ptr(y), ptr(idx), ptr(cnt), ptr(u), ptr(ws), wsb,
+                          stream_handle(dev)))
+    _post(dev)
+    return y, idx, cnt, u
+
+
+def unique(x, out_idx=torch.int32):
+    """tf.unique: (y, idx), y in first-occurrence order (syncs for |y|)."""
+    y, idx, _, u = unique_device(x)
+    k = int(u.item())
+    return y[:k], idx.to(out_idx)
+
+
+def unique_with_counts(x, out_idx=torch.int32):
+    y, idx, cnt, u = unique_device(x, with_counts=True)
+    k = int(u.item())
+    return y[:k], idx.to(out_idx), cnt[:k]
+
+
+# ---------------------------------------------------------------------------
+# Gather / segment reductions
+# ---------------------------------------------------------------------------
+def gather(params, indices):
+    """ResourceGather on a dense [R, D] table (gather_functor.h:36-115)."""
+    dev = _dev(params)
+    params = _c(params, torch.float32)
+    idx = _c(indices.reshape(-1), torch.int64)
+    D = params.shape[1]
+    out = torch.empty((idx.numel(), D), dtype=torch.float32, device=dev)
+    check(lib().dr_gather(ptr(params), params.shape[0], D, ptr(idx), idx.numel(), ptr(out),
+                          stream_handle(dev)))
+    _post(dev)
+    return out.reshape(tuple(indices.shape) + (D,))
+
+
+def _segment_reduce(data, indices, segment_ids, num_segments, combiner):
+    dev = _dev(data)
+    data = _c(data, torch.float32)
+    data2 = data.reshape(data.shape[0], -1)
+    idx = _c(indices, torch.int32)
+    seg = _c(segment_ids, torch.int32)
+    if num_segments is None:  # output rows = last segment id + 1 (reference CPU)
+        num_segments = int(seg[-1].item()) + 1 if seg.numel() else 0
+    D = data2.shape[1]
+    out = torch.empty((num_segments, D), dtype=torch.float32, device=dev)
+    wsb = lib().dr_segment_workspace_size(num_segments)
+    ws = workspace(wsb, dev)
+    check(lib().dr_sparse_segment_reduce(ptr(data2), data2.shape[0], D, ptr(idx), ptr(seg),
+                                         idx.numel(), num_segments, COMBINERS[combiner], ptr(out),
+                                         ptr(ws), wsb, stream_handle(dev)))
+    _post(dev)
+    return out.reshape((num_segments,) + tuple(data.shape[1:]))
+
+
+def sparse_segment_sum(data, indices, segment_ids, num_segments=None):
+    return _segment_reduce(data, indices, segment_ids, num_segments, "sum")
+
+
+def sparse_segment_mean(data, indices, segment_ids, num_segments=None):
+    return _segment_reduce(data, indices, segment_ids, num_segments, "mean")
+
+
+def sparse_segment_sqrt_n(data, indices, segment_ids, num_segments=None):
+    return _segment_reduce(data, indices, segment_ids, num_segments, "sqrtn")
+
+
+def _segment_grad(grad, indices, segment_ids, output_dim0, combiner):
+    dev = _dev(grad)
+    grad = _c(grad, torch.float32)
+    g2 = grad.reshape(grad.shape[0], -1)
+    idx = _c(indices, torch.int32)
+    seg = _c(segment_ids, torch.int32)
+    D = g2.shape[1]
+    out = torch.empty((output_dim0, D), dtype=torch.float32, device=dev)
+    wsb = lib().dr_segment_grad_workspace_size(idx.numel(), g2.shape[0], output_dim0)
+    ws = workspace(wsb, dev)
+    check(lib().dr_sparse_segment_reduce_grad(ptr(g2), g2.shape[0], D, ptr(idx), ptr(seg),
+                                              idx.numel(), output_dim0, COMBINERS[combiner],
+                                              ptr(out), ptr(ws), wsb, stream_handle(dev)))
+    _post(dev)
+    return out.reshape((output_dim0,) + tuple(grad.shape[1:]))
+
+
+def sparse_segment_sum_grad(grad, indices, segment_ids, output_dim0):
+    """Grad of SparseSegmentSum = unsorted_segment_sum(gather(grad, seg), idx, dim0)
+    (math_grad.py:321-327), deterministic CPU order."""
+    return _segment_grad(grad, indices, segment_ids, output_dim0, "sum")
+
+
+def sparse_segment_mean_grad(grad, indices, segment_ids, output_dim0):
+    return _segment_grad(grad, indices, segment_ids, output_dim0, "mean")
+
+
+def sparse_segment_sqrt_n_grad(grad, indices, segment_ids, output_dim0):
+    return _segment_grad(grad, indices, segment_ids, output_dim0, "sqrtn")
+
+
+def unsorted_segment_sum(data, segment_ids, num_segments):
+    """UnsortedSegmentSum (segment_reduction_ops.cc:377-405): serial order, seg<0 skipped."""
+    dev = _dev(data)
+    data = _c(data, torch.float32)
+    d2 = data.reshape(data.shape[0], -1)
+    seg = _c(segment_ids, torch.int32)
+    D = d2.shape[1]
+    out = torch.empty((num_segments, D), dtype=torch.float32, device=dev)
+    wsb = lib().dr_unsorted_segment_sum_workspace_size(seg.numel(), num_segments)
+    ws = workspace(wsb, dev)
+    check(lib().dr_unsorted_segment_sum(ptr(d2), d2.shape[0], D, ptr(seg), num_segments, ptr(out),
+                                        ptr(ws), wsb, stream_handle(dev)))
+    _post(dev)
+    return out.reshape((num_segments,) + tuple(data.shape[1:]))
+
+
+def bag_offsets(segment_ids, batch):
+    """CSR offsets [batch+1] of sorted segment ids (int32 or int64)."""
+    dev = _dev(segment_ids)
+    off = torch.empty(batch + 1, dtype=torch.int32, device=dev)
+    if segment_ids.dtype == torch.int32:
+        s = segment_ids.contiguous()
+        check(lib().dr_bag_offsets_i32(ptr(s), s.numel(), batch, ptr(off), stream_handle(dev)))
+    else:
+        s = _c(segment_ids, torch.int64)
+        check(lib().dr_bag_offsets(ptr(s), s.numel(), batch, ptr(off), stream_handle(dev)))
+    _post(dev)
+    return off
+
+
+def pool_grouped(descs, batch, dim, order=ORDER_ALI, device=None):
+    """Launch dr_pool_grouped on a list of _lib.DrPoolDesc (<= 32 tables)."""
+    arr = (_lib.DrPoolDesc * len(descs))(*descs)
+    check(lib().dr_pool_grouped(arr, len(descs), batch, dim, order, stream_handle(device)))
+    _post(device)
+
+
+def sort_pairs(keys, vals, bit_hi, bit_lo=0):
+    """Stable LSD radix sort of (uint64 key, int32 value) pairs."""
+    dev = _dev(keys)
+    k = _c(keys, torch.int64)
+    v = _c(vals, torch.int32)
+    ko = torch.empty_like(k)
+    vo = torch.empty_like(v)
+    wsb = lib().dr_sort_pairs_workspace_size(k.numel())
+    ws = workspace(wsb, dev)
+    check(lib().dr_sort_pairs(ptr(k), ptr(v), ptr(ko), ptr(vo), k.numel(), bit_lo, bit_hi, ptr(ws),
+                              wsb, stream_handle(dev)))
+    _post(dev)
+    return ko, vo
+
+
+# ---------------------------------------------------------------------------
+# Fused embedding ops (core/ops/fused_embedding_ops.cc:12-58)
+# ---------------------------------------------------------------------------
+def fused_embedding_local_sparse_look_up(sp_values, sp_indices, sp_dense_shape, emb_variable,
+                                         combiner="mean", max_norm=-1.0):
+    dev = _dev(emb_variable)
+    table = _c(emb_variable, torch.float32)
+    vals = _c(sp_values, torch.int64)
+    ind = _c(sp_indices, torch.int64)
+    B = int(sp_dense_shape[0])
+    D = table.shape[1]
+    out = torch.empty((B, D), dtype=torch.float32, device=dev)
+    vo = torch.empty(B, dtype=torch.int32, device=dev)
+    wsb = lib().dr_fused_local_workspace_size(B)
+    ws = workspace(wsb, dev)
+    check(lib().dr_fused_local_lookup(ptr(table), table.shape[0], D, ptr(vals), ptr(ind),
+                                      vals.numel(), B, COMBINERS[combiner], float(max_norm),
+                                      ptr(out), ptr(vo), ptr(ws), wsb, stream_handle(dev)))
+    _post(dev)
+    return out, vo
+
+
+def fused_embedding_local_sparse_look_up_grad(top_grad, emb_variable, sp_values,
+                                              sp_values_offset, combiner="mean", max_norm=-1.0):
+    dev = _dev(top_grad)
+    tg = _c(top_grad, torch.float32)
+    table = _c(emb_variable, torch.float32)
+    vals = _c(sp_values, torch.int64)
+    vo = _c(sp_values_offset, torch.int32)
+    D = tg.shape[1]
+    out = torch.empty((vals.numel(), D), dtype=torch.float32, device=dev)
+    check(lib().dr_fused_local_lookup_grad(ptr(tg), ptr(table), table.shape[0], D, ptr(vals),
+                                           ptr(vo), vals.numel(), tg.shape[0],
+                                           COMBINERS[combiner], float(max_norm), ptr(out),
+                                           stream_handle(dev)))
+    _post(dev)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Interactions
+# ---------------------------------------------------------------------------
+def fm_second_order(emb):
+    """0.5 * ((sum_f e)^2 - sum_f e^2) over [B, F, D] (DeepFM train.py:205-209)."""
+    dev = _dev(emb)
+    e = _c(emb, torch.float32)
+    B, F, D = e.shape
+    out = torch.empty((B, D), dtype=torch.float32, device=dev)
+    check(lib().dr_fm2(ptr(e), B, F, D, ptr(out), stream_handle(dev)))
+    _post(dev)
+    return out
+
+
+def fm_second_order_grad(emb, top_grad):
+    dev = _dev(emb)
+    e = _c(emb, torch.float32)
+    g = _c(top_grad, torch.float32)
+    B, F, D = e.shape
+    out = torch.empty_like(e)
+    check(lib().dr_fm2_grad(ptr(e), ptr(g), B, F, D, ptr(out), stream_handle(dev)))
+    _post(dev)
+    return out
+
+
+def dot_interaction(x):
+    """DLRM dot_op (DLRM train.py:150-163): strictly-lower triangle of X X^T."""
+    dev = _dev(x)
+    x = _c(x, torch.float32)
+    B, F, D = x.shape
+    out = torch.empty((B, F * (F - 1) // 2), dtype=torch.float32, device=dev)
+    check(lib().dr_dot_interaction(ptr(x), B, F, D, ptr(out), stream_handle(dev)))
+    _post(dev)
+    return out
+
+
+def crossnet_layer(x0, xl, weight, bias=None):
+    """DCN-v2 cross layer x0 * (xl W^T + b) + xl, bf16 MFMA, fp32 accumulate.
+
+    Feature dims that are not a multiple of 8 are zero-padded (exact)."""
+    dev = _dev(x0)
+    B, d = x0.shape
+    dp = (d + 7) // 8 * 8
+
+    def pad2(t, rows, cols):
+        t = t.to(torch.bfloat16)
+        if t.shape[1] == cols and t.shape[0] == rows:
+            return t.contiguous()
+        o = torch.zeros((rows, cols), dtype=torch.bfloat16, device=dev)
+        o[:t.shape[0], :t.shape[1]] = t
+        return o
+
+    a0 = pad2(x0, B, dp)
+    al = pad2(xl, B, dp)
+    w = pad2(weight, dp, dp)
+    b = None
+    if bias is not None:
+        b = torch.zeros(dp, dtype=torch.float32, device=dev)
+        b[:d] = bias.float()
+    out = torch.empty((B, dp), dtype=torch.bfloat16, device=dev)
+    check(lib().dr_crossnet_layer_bf16(ptr(a0), ptr(al), ptr(w), ptr(b), B, dp, ptr(out),
+                                       stream_handle(dev)))
+    _post(dev)
+    return out[:, :d]
+
+
+# ---------------------------------------------------------------------------
+# Row-sharded exchange helpers
+# ---------------------------------------------------------------------------
+def partition_by_owner(keys, world, n_dev=None):
+    """Stable bucket of keys by owner = key % world (SOK selectKernel,
+    all2all_input_dispatcher.cu:36-126; EV rule embedding_ops.py:207-209).
+    Returns (keys_sorted, perm, send_counts[world] int64)."""
+    dev = _dev(keys)
+    k = _c(keys, torch.int64)
+    n = k.numel()
+    ko = torch.empty_like(k)
+    perm = torch.empty(n, dtype=torch.int32, device=dev)
+    counts = torch.empty(world, dtype=torch.int64, device=dev)
+    wsb = lib().dr_partition_workspace_size(n)
+    ws = workspace(wsb, dev)
+    check(lib().dr_partition_by_owner(ptr(k), n, ptr(n_dev), world, ptr(ko), ptr(perm),
+                                      ptr(counts), ptr(ws), wsb, stream_handle(dev)))
+    _post(dev)
+    return ko, perm, counts
+
+
+def rows_scatter(src, perm, out, n_dev=None):
+    """out[perm[j]] = src[j]"""
+    dev = _dev(src)
+    check(lib().dr_rows_scatter(ptr(src), ptr(perm), perm.numel(), ptr(n_dev), src.shape[1],
+                                ptr(out), stream_handle(dev)))
+    _post(dev)
+    return out
+
+
+def rows_pack(src, perm, out, n_dev=None):
+    """out[j] = src[perm[j]]"""
+    dev = _dev(src)
+    check(lib().dr_rows_pack(ptr(src), ptr(perm), perm.numel(), ptr(n_dev), src.shape[1],
+                             ptr(out), stream_handle(dev)))
+    _post(dev)
+    return out
+
+
+def fill_synthetic(table, seed):
+    """table[r, c] = hash(seed, r, c) in [-1, 1) (regenerable: synth_value)."""
+    dev = _dev(table)
+    check(lib().dr_fill_synthetic(ptr(table), table.shape[0], table.shape[1], seed,
+                                  stream_handle(dev)))
+    return table
+
+
+def synth_value(seed, row, col):
+    return lib().dr_synth_value(seed, row, col)

@@ -1,0 +1,321 @@
+/*
+ * deeprec_amd.h -- C ABI of the MI355X-native sharded-embedding engine.
+ *
+ * This is the drop-in boundary for DeepRec's EmbeddingVariable /
+ * embedding_lookup_sparse hot path.  Each entry point
+ * names the reference op/kernel it replaces (paths relative to the DeepRec
+ * reference root).  Conventions:
+ *   - every buffer argument is a caller-owned DEVICE pointer unless its name
+ *     ends in `_host`; `stream` is a hipStream_t passed as void*;
+ *   - EmbeddingVariables are library-owned, refcounted opaque handles
+ *     (ResourceMgr + core::ScopedUnref in the reference);
+ *   - return value is a TF error::Code (DR_OK == 0); dr_last_error() returns
+ *     a thread-local message for the last failure on this thread;
+ *   - data-dependent errors found on the device (index out of range,
+ *     unsorted segment ids, table full) are latched in a device status word
+ *     and reported by dr_status_check() (which synchronises the stream), so
+ *     that the hot entry points never block the host;
+ *   - no call aborts the process;
+ *   - entry points taking `ws`/`ws_bytes` need a device workspace of at least
+ *     the size returned by the matching *_workspace_size() query;
+ *   - nothing here allocates device memory or synchronises except the
+ *     functions documented as such (create/reserve/size/export/status), so
+ *     the per-step calls can be captured into a hipGraph.
+ */
+#ifndef DEEPREC_AMD_H_
+#define DEEPREC_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* TF error::Code values (tensorflow/core/lib/core/error_codes.proto). */
+enum {
+  DR_OK = 0,
+  DR_INVALID_ARGUMENT = 3,
+  DR_NOT_FOUND = 5,
+  DR_ALREADY_EXISTS = 6,
+  DR_RESOURCE_EXHAUSTED = 8,
+  DR_INTERNAL = 13
+};
+
+/* Combiners of embedding_lookup_sparse / SparseSegment{Sum,Mean,SqrtN}. */
+enum { DR_COMBINER_SUM = 0, DR_COMBINER_MEAN = 1, DR_COMBINER_SQRTN = 2 };
+
+/* Pooling association order.
+ * DR_ORDER_ALI  : SparseSegmentReduction::Reduce CPU order
+ *                 (core/kernels/segment_reduction_ali_ops_util.h:193-318)
+ * DR_ORDER_SEQ  : left-to-right then combiner, FusedEmbeddingLocalSparseLookUp
+ *                 (core/kernels/fused_embedding/fused_embedding_local_ops_gpu.cu.cc:41-84) */
+enum { DR_ORDER_ALI = 0, DR_ORDER_SEQ = 1 };
+
+int dr_abi_version(void);
+const char* dr_last_error(void);
+/* Synchronises `stream`, returns and clears the device status word
+ * (DR_OK or the first DR_* code latched by a kernel since the last check). */
+int dr_status_check(void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Unique / UniqueWithCounts, first-occurrence order.                        */
+/* Replaces UniqueAliOp (core/kernels/unique_ali_op.cc:46-180,               */
+/* unique_ali_op_util.h:192-222).  num_unique is a DEVICE int64.             */
+/* ------------------------------------------------------------------------ */
+size_t dr_unique_workspace_size(int64_t n);
+int dr_unique(const int64_t* keys, int64_t n, int64_t* uniq_out, int32_t* idx_out,
+              int32_t* counts_out /* nullable */, int64_t* num_unique,
+              void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Stable radix sort of (uint64 key, int32 value) pairs on bits [lo, hi).    */
+/* Replaces cub::DeviceRadixSort::SortPairs in FusedEmbeddingSparsePreLookUp */
+/* (core/kernels/fused_embedding/fused_embedding_ops_gpus.cu.cc:192-212).    */
+/* ------------------------------------------------------------------------ */
+size_t dr_sort_pairs_workspace_size(int64_t n);
+int dr_sort_pairs(const uint64_t* keys_in, const int32_t* vals_in, uint64_t* keys_out,
+                  int32_t* vals_out, int64_t n, int bit_lo, int bit_hi,
+                  void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Dense-table row gather: ResourceGather / GatherV2                         */
+/* (core/kernels/resource_variable_ops.cc:628, gather_functor.h:36-115).     */
+/* Out-of-range ids latch DR_INVALID_ARGUMENT and write zeros.               */
+/* ------------------------------------------------------------------------ */
+int dr_gather(const float* table, int64_t rows, int64_t dim, const int64_t* ids,
+              int64_t n, float* out, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* SparseSegment{Sum,Mean,SqrtN}[WithNumSegments] over a materialised       */
+/* [data_rows, dim] input (segment_reduction_ali_ops.cc:141-250).  seg must */
+/* be sorted; missing segments are 0.                                        */
+/* ------------------------------------------------------------------------ */
+size_t dr_segment_workspace_size(int64_t num_segments);
+int dr_sparse_segment_reduce(const float* data, int64_t data_rows, int64_t dim,
+                             const int32_t* idx, const int32_t* seg, int64_t n,
+                             int64_t num_segments, int combiner, float* out,
+                             void* ws, size_t ws_bytes, void* stream);
+
+/* SparseSegment{Sum,Mean,SqrtN}Grad in the CPU order (ascending i per       */
+/* output row; segment_reduction_ali_ops_util.h:331-458, and for Sum the    */
+/* math_grad.py:321-327 unsorted_segment_sum composition).  Deterministic.   */
+size_t dr_segment_grad_workspace_size(int64_t n, int64_t grad_rows, int64_t out_rows);
+int dr_sparse_segment_reduce_grad(const float* grad, int64_t grad_rows, int64_t dim,
+                                  const int32_t* idx, const int32_t* seg, int64_t n,
+                                  int64_t out_rows, int combiner, float* out,
+                                  void* ws, size_t ws_bytes, void* stream);
+
+/* UnsortedSegmentSum (segment_reduction_ops.cc:377-405): serial ascending-i */
+/* order per output row, seg < 0 skipped.  Deterministic (no float atomics). */
+size_t dr_unsorted_segment_sum_workspace_size(int64_t n, int64_t num_segments);
+int dr_unsorted_segment_sum(const float* data, int64_t n, int64_t dim, const int32_t* seg,
+                            int64_t num_segments, float* out, void* ws, size_t ws_bytes,
+                            void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Grouped fused lookup + pooling: one launch for up to DR_MAX_GROUP tables  */
+/* (features).  For table t, bag b of batch B: rows L_k = pool[row(k)] for   */
+/* k in [bag_off[b], bag_off[b+1]), reduced in `order` with `combiner` (and */
+/* per-row clip_by_norm when max_norm > 0), written to                       */
+/* out[b * out_stride + d].  Row selection per nnz k:                        */
+/*   idx == NULL : row = ids[k]              (dense table, bounds-checked)   */
+/*   idx != NULL : row = rows[idx[k]]        (EV resolved unique rows);      */
+/*                 row < 0 -> default_rows[-row-1] (filtered / not admitted) */
+/* Empty bags are 0 (gap fill), or zero_empty==0 keeps the same.             */
+/* This is the fused embedding_lookup_sparse forward                        */
+/* (python/ops/embedding_ops.py:480-675) minus the dedup/resolve steps.      */
+/* ------------------------------------------------------------------------ */
+#define DR_MAX_GROUP 32
+typedef struct {
+  const float* pool;          /* table or EV value pool base, [rows, dim]  */
+  int64_t pool_rows;          /* bounds for dense ids                       */
+  const int64_t* ids;         /* dense: [nnz] row ids                       */
+  const int32_t* idx;         /* EV: [nnz] -> unique position (or NULL)     */
+  const int64_t* rows;        /* EV: [U] resolved row per unique key        */
+  const float* default_rows;  /* EV: rows for negative selections           */
+  int64_t default_stride;     /* elements between default rows (0: one row) */
+  const int32_t* bag_off;     /* [B+1] CSR offsets of the bags              */
+  const float* weights;       /* [nnz] sp_weights or NULL                   */
+  float* out;                 /* [B, out_stride] output                     */
+  int64_t out_stride;
+  int32_t combiner;
+  float max_norm;             /* >= 0: clip rows (clip_by_norm for ALI order,
+                                 fused `*= max_norm/l2` for SEQ); -1: off     */
+} dr_pool_desc;
+
+int dr_pool_grouped(const dr_pool_desc* descs_host, int num_tables, int64_t batch,
+                    int dim, int order, void* stream);
+
+/* CSR bag offsets from sorted segment ids (sp_indices[:,0]):               */
+/* bag_off[s] = first k with seg[k] >= s, bag_off[B] = n.  Unsorted or out  */
+/* of range ids latch DR_INVALID_ARGUMENT.                                   */
+int dr_bag_offsets(const int64_t* seg, int64_t n, int64_t batch, int32_t* bag_off,
+                   void* stream);
+int dr_bag_offsets_i32(const int32_t* seg, int64_t n, int64_t batch, int32_t* bag_off,
+                       void* stream);
+/* Same over sp_indices[:, 0] read with a stride (2 for [nnz, 2] indices).   */
+int dr_bag_offsets_strided(const int64_t* seg, int64_t stride, int64_t n, int64_t batch,
+                           int32_t* bag_off, void* stream);
+
+/* Backward of the grouped pooling for one table, deterministic:             */
+/* grad_unique[u] = sum over k with idx[k]==u (ascending k) of               */
+/*   top_grad[bag(k)] * scale(bag)  (scale: 1, 1/n, 1/sqrt(n) as the         */
+/* reference grad kernels compute it).  = SparseSegment*Grad on the unique  */
+/* rows.  num_unique is a DEVICE int64 (upper bound n).                      */
+size_t dr_pool_grad_workspace_size(int64_t n);
+int dr_pool_grad(const float* top_grad, int64_t top_stride, int64_t batch, int dim,
+                 const int32_t* bag_off, const int32_t* seg, const int32_t* idx, int64_t n,
+                 const int64_t* num_unique, int combiner, float* grad_unique,
+                 void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* EmbeddingVariable (core/framework/embedding/embedding_var.h:50-363).      */
+/* ------------------------------------------------------------------------ */
+typedef struct dr_ev dr_ev;
+
+typedef struct {
+  int64_t dim;                       /* value_len                           */
+  int64_t capacity;                  /* initial key capacity (grows)        */
+  int64_t steps_to_live;             /* >0: versions kept                   */
+  int64_t filter_freq;               /* >0: Counter (or Bloom) admission    */
+  int64_t max_element_size;          /* Bloom sizing (with fpp)             */
+  float false_positive_probability;  /* -1: Counter filter                  */
+  int32_t counter_bits;              /* Bloom counter width 8/16/32/64      */
+  int32_t layout;                    /* 0 light, 1 normal (informational)   */
+} dr_ev_config;
+
+/* InitializeKvVariableOp primary branch (kernels/kv_variable_ops.cc:173-193). */
+int dr_ev_create(const dr_ev_config* cfg, const float* default_row_host, dr_ev** out);
+/* Slot EV sharing the primary's key space (kv_variable_ops.cc:212-226).    */
+int dr_ev_create_slot(dr_ev* primary, int slot_index, const float* default_row_host,
+                      dr_ev** out);
+int dr_ev_retain(dr_ev* ev);
+int dr_ev_release(dr_ev* ev);
+/* KvVariableShapeOp (kv_variable_ops.cc:58-75): number of keys.  Syncs.   */
+int dr_ev_size(dr_ev* ev, int64_t* size_host, void* stream);
+int64_t dr_ev_dim(dr_ev* ev);
+/* Ensures room for `extra` new keys (may rehash/grow; syncs when it must). */
+int dr_ev_reserve(dr_ev* ev, int64_t extra, void* stream);
+
+/* Resolve keys to value-pool rows with insert-on-miss and the filter,       */
+/* initialising first-touch rows from `defaults` ([n,dim], or NULL = the EV */
+/* default).  rows_out[i] = row, or -(i+1) when the key is filtered (the    */
+/* caller then reads defaults[i]).  n_dev: optional DEVICE count <= n.       */
+/* This is the per-key part of KvResourceGather[V1]                          */
+/* (kv_variable_ops.cc:314-449 -> EmbeddingVar::LookupOrCreate).             */
+size_t dr_ev_resolve_workspace_size(int64_t n);
+int dr_ev_resolve(dr_ev* ev, const int64_t* keys, int64_t n, const int64_t* n_dev,
+                  const float* defaults, const int32_t* counts, int64_t* rows_out,
+                  void* ws, size_t ws_bytes, void* stream);
+/* Grouped resolve over T EVs of equal dim (one per feature) in one launch: */
+/* keys/counts/rows_out concatenated, table t at [koff_host[t],             */
+/* koff_host[t+1]), optional per-table DEVICE counts; defaults = EV default. */
+int dr_ev_resolve_grouped(dr_ev* const* evs, int num_tables, const int64_t* keys,
+                          const int64_t* koff_host, const int64_t* const* n_dev_per_table,
+                          const int32_t* counts, int64_t* rows_out, void* ws, size_t ws_bytes,
+                          void* stream);
+/* Value-pool base of this EV's column (primary or slot).                   */
+const float* dr_ev_pool(dr_ev* ev);
+
+/* KvResourceGather (counts == NULL) / KvResourceGatherV1.                   */
+size_t dr_ev_gather_workspace_size(int64_t n);
+int dr_ev_gather(dr_ev* ev, const int64_t* keys, int64_t n, const float* defaults,
+                 const int32_t* counts, float* out, void* ws, size_t ws_bytes,
+                 void* stream);
+
+/* KvResourceInsert / KvResourceImportV2 with EmbeddingVar::Import semantics */
+/* (embedding_var.h:187-219): partition_num <= 0 disables the               */
+/* key % 1000 % partition_num == partition_id filter.                        */
+int dr_ev_insert(dr_ev* ev, const int64_t* keys, int64_t n, const float* values,
+                 const int64_t* versions, const int64_t* freqs, int64_t partition_id,
+                 int64_t partition_num, void* stream);
+
+/* Bulk insert of keys [key_begin, key_begin + n) whose rows are            */
+/* synth(seed, key, col) (dr_synth_value): populates synthetic tables.      */
+int dr_ev_insert_synthetic(dr_ev* ev, int64_t key_begin, int64_t n, uint64_t seed,
+                           void* stream);
+
+/* KvResourceExport (kv_variable_ops.cc:786-835), keys ascending.  Syncs.   */
+/* Pass NULL outputs to query the count into *m_host first.                 */
+int dr_ev_export(dr_ev* ev, int64_t* keys_out, float* values_out, int64_t* versions_out,
+                 int64_t* freqs_out, int64_t capacity, int64_t* m_host, void* stream);
+
+/* Per-key freq / version of the primary, host-side, syncs (tests/debug).   */
+int dr_ev_key_meta(dr_ev* ev, const int64_t* keys_host, int64_t n, int64_t* freq_host,
+                   int64_t* version_host, int32_t* has_row_host, void* stream);
+
+/* KvResourceSparseApplyGradientDescent (training_ali_ops.cc:1597-1678).     */
+int dr_ev_apply_sgd(dr_ev* var, float lr, const float* grad, const int64_t* keys,
+                    int64_t n, const int64_t* n_dev, int64_t global_step, void* stream);
+/* KvSparseApplyAdagrad (training_ali_ops.cc:61-145).                        */
+int dr_ev_apply_adagrad(dr_ev* var, dr_ev* accum, float lr, const float* grad,
+                        const int64_t* keys, int64_t n, const int64_t* n_dev,
+                        int64_t global_step, void* stream);
+/* KvSparseApplyAdam (training_ali_ops.cc:848-975).                          */
+int dr_ev_apply_adam(dr_ev* var, dr_ev* m, dr_ev* v, float beta1_power, float beta2_power,
+                     float lr, float beta1, float beta2, float epsilon, const float* grad,
+                     const int64_t* keys, int64_t n, const int64_t* n_dev,
+                     int64_t global_step, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* FusedEmbeddingLocalSparseLookUp[Grad]                                     */
+/* (core/ops/fused_embedding_ops.cc:12-58, kernels in                        */
+/* fused_embedding_local_ops_gpu.cu.cc:18-122).  sp_indices [nnz,2].         */
+/* ------------------------------------------------------------------------ */
+size_t dr_fused_local_workspace_size(int64_t batch);
+int dr_fused_local_lookup(const float* table, int64_t rows, int dim, const int64_t* sp_values,
+                          const int64_t* sp_indices, int64_t nnz, int64_t batch,
+                          int combiner, float max_norm, float* out, int32_t* values_offset,
+                          void* ws, size_t ws_bytes, void* stream);
+int dr_fused_local_lookup_grad(const float* top_grad, const float* table, int64_t rows,
+                               int dim, const int64_t* sp_values, const int32_t* values_offset,
+                               int64_t nnz, int64_t batch, int combiner, float max_norm,
+                               float* grad_out, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Owner partition for the row-sharded all-to-all (SOK selectKernel,         */
+/* sparse_operation_kit/.../all2all_input_dispatcher.cu:36-126, and the EV   */
+/* partition rule embedding_ops.py:207-209): stable bucket of keys by        */
+/* owner = key % world; perm_out[j] = source position; send_counts[world]   */
+/* (device int64).                                                           */
+/* ------------------------------------------------------------------------ */
+size_t dr_partition_workspace_size(int64_t n);
+int dr_partition_by_owner(const int64_t* keys, int64_t n, const int64_t* n_dev, int world,
+                          int64_t* keys_out, int32_t* perm_out, int64_t* send_counts,
+                          void* ws, size_t ws_bytes, void* stream);
+/* Row exchange helpers: dst[perm[j]] = src[j] (scatter back) / dst[j] =     */
+/* src[perm[j]] (pack), rows of `dim` floats; n_dev optional.                */
+int dr_rows_scatter(const float* src, const int32_t* perm, int64_t n, const int64_t* n_dev,
+                    int dim, float* dst, void* stream);
+int dr_rows_pack(const float* src, const int32_t* perm, int64_t n, const int64_t* n_dev,
+                 int dim, float* dst, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Interactions (callers of the path).                                       */
+/* ------------------------------------------------------------------------ */
+/* FM 2nd order (modelzoo/DeepFM/train.py:205-209): emb [B,F,D] -> [B,D].   */
+int dr_fm2(const float* emb, int64_t batch, int fields, int dim, float* out, void* stream);
+int dr_fm2_grad(const float* emb, const float* top_grad, int64_t batch, int fields, int dim,
+                float* grad_emb, void* stream);
+/* DLRM dot (modelzoo/DLRM/train.py:150-163): X [B,F,D] -> [B, F(F-1)/2].   */
+int dr_dot_interaction(const float* x, int64_t batch, int fields, int dim, float* out,
+                       void* stream);
+/* DCN-v2 cross layer (absent in the reference): out = x0 * (xl W^T + b) + xl */
+/* x0/xl/out [B,d] bf16 (uint16 storage), W [d,d] bf16 row-major (out,in),   */
+/* b [d] f32; bf16 MFMA with fp32 accumulation.                              */
+int dr_crossnet_layer_bf16(const uint16_t* x0, const uint16_t* xl, const uint16_t* W,
+                           const float* bias, int64_t batch, int d, uint16_t* out,
+                           void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Synthetic data (bench/tests): table[r, c] = hash-derived uniform [-1, 1)  */
+/* of (seed, r, c), regenerable on host (dr_synth_value).                     */
+/* ------------------------------------------------------------------------ */
+int dr_fill_synthetic(float* table, int64_t rows, int dim, uint64_t seed, void* stream);
+float dr_synth_value(uint64_t seed, int64_t row, int64_t col);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DEEPREC_AMD_H_ */

@@ -1,0 +1,464 @@
+"""GPU parity: the HIP engine through its C ABI vs the CPU restatement (oracle/)
+and the reference's golden vectors.  Integer/index work must be bit-exact;
+fp32 pooling replays the reference association order and is checked
+bit-exact as well (the north_star bound is 1e-5 relative); optimizer updates
+with rsqrt/sqrt are checked at 1e-5 relative.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+RTOL = 1e-5
+
+
+def load(name):
+    with open(os.path.join(GOLD, name + ".json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def dr():
+    import deeprec_amd
+    deeprec_amd.load()
+    deeprec_amd.set_validate(True)
+    assert torch.cuda.is_available()
+    return deeprec_amd
+
+
+@pytest.fixture(scope="module")
+def ops(dr):
+    from deeprec_amd import ops
+    return ops
+
+
+DEV = "cuda:0"
+
+
+def T(x, dtype=None):
+    return torch.as_tensor(np.asarray(x), device=DEV, dtype=dtype)
+
+
+def H(t):
+    return t.detach().cpu().numpy()
+
+
+# ---------------------------------------------------------------------------
+def test_native_library_is_loaded(dr):
+    from deeprec_amd import _lib
+    assert _lib.lib().dr_abi_version() == 1
+    maps = open("/proc/self/maps").read()
+    assert "libdeeprec_amd.so" in maps
+
+
+@pytest.mark.parametrize("case", ["sqrtn", "mean", "sum", "sqrtn_maxnorm200"])
+def test_fused_local_forward_golden(ops, orc, case):
+    g = load("fused_local")
+    c = g["forward"][case]
+    comb = c.get("combiner", case)
+    table = np.asarray(g["table"], np.float32).reshape(g["bucket"], g["dim"])
+    ind = np.asarray(g["sp_indices"], np.int64).reshape(-1, 2)
+    out, vo = ops.fused_embedding_local_sparse_look_up(T(g["sp_values"]), T(ind), (g["batch"], 8),
+                                                       T(table), comb, c["max_norm"])
+    np.testing.assert_allclose(H(out).ravel(), c["expected"], atol=g["tolerance"], rtol=0)
+    assert H(vo).tolist() == g["offsets_expected"]
+    ref, _ = orc.fused_local_lookup(table, g["sp_values"], ind[:, 0], g["batch"], comb,
+                                    c["max_norm"])
+    if c["max_norm"] < 0:
+        np.testing.assert_array_equal(H(out), ref)
+    else:
+        np.testing.assert_allclose(H(out), ref, rtol=RTOL)
+
+
+@pytest.mark.parametrize("case", ["sqrtn", "mean", "sum", "mean_maxnorm100"])
+def test_fused_local_grad_golden(ops, orc, case):
+    g = load("fused_local")
+    c = g["grad"][case]
+    comb = c.get("combiner", case)
+    table = np.asarray(g["table"], np.float32).reshape(g["bucket"], g["dim"])
+    top = np.asarray(g["top_grad"], np.float32).reshape(g["batch"], g["dim"])
+    out = ops.fused_embedding_local_sparse_look_up_grad(T(top), T(table), T(g["sp_values"]),
+                                                        T(g["offsets_expected"], torch.int32),
+                                                        comb, c["max_norm"])
+    np.testing.assert_allclose(H(out).ravel(), c["expected"], atol=g["tolerance"], rtol=0)
+    ref = orc.fused_local_lookup_grad(top, table, g["sp_values"], g["offsets_expected"], comb,
+                                      c["max_norm"])
+    np.testing.assert_allclose(H(out), ref, rtol=RTOL, atol=1e-7)
+
+
+@pytest.mark.parametrize("comb", ["sum", "mean", "sqrtn"])
+def test_segment_formula_kat(ops, orc, comb):
+    g = load("segment_formula")
+    rows, D, n = g["rows"], g["dim"], g["n"]
+    data = np.repeat(np.arange(rows, dtype=np.float32)[:, None], D, 1)
+    i = np.arange(n)
+    idx, seg = (2 * i).astype(np.int32), (i // 2).astype(np.int32)
+    fn = {"sum": ops.sparse_segment_sum, "mean": ops.sparse_segment_mean,
+          "sqrtn": ops.sparse_segment_sqrt_n}[comb]
+    out = H(fn(T(data), T(idx), T(seg)))
+    np.testing.assert_array_equal(out, orc.sparse_segment_reduce(data, idx, seg, comb))
+
+
+@pytest.mark.parametrize("D", [1, 3, 8, 18, 64, 128])
+@pytest.mark.parametrize("comb", ["sum", "mean", "sqrtn"])
+def test_segment_reduce_random_bitexact(ops, orc, D, comb):
+    rng = np.random.default_rng(D * 7 + len(comb))
+    R = 500
+    data = rng.standard_normal((R, D)).astype(np.float32) * 10
+    lens = rng.integers(0, 30, 64)
+    lens[:12] = np.arange(12)           # every num % 8 branch incl. 0 (gap) and 1
+    seg = np.repeat(np.arange(64), lens).astype(np.int32)
+    idx = rng.integers(0, R, seg.shape[0]).astype(np.int32)
+    fn = {"sum": ops.sparse_segment_sum, "mean": ops.sparse_segment_mean,
+          "sqrtn": ops.sparse_segment_sqrt_n}[comb]
+    out = H(fn(T(data), T(idx), T(seg), num_segments=70))
+    ref = orc.sparse_segment_reduce(data, idx, seg, comb, num_segments=70)
+    np.testing.assert_array_equal(out, ref)
+
+
+def test_segment_reduce_errors_latched(dr, ops):
+    data = T(np.ones((4, 2), np.float32))
+    with pytest.raises(dr.DeepRecError):
+        ops.sparse_segment_sum(data, T([0, 9], torch.int32), T([0, 1], torch.int32))
+    with pytest.raises(dr.DeepRecError):
+        ops.sparse_segment_sum(data, T([0, 1], torch.int32), T([1, 0], torch.int32),
+                               num_segments=2)
+
+
+@pytest.mark.parametrize("n,lo,hi", [(0, 0, 1), (1, 0, 1), (1000, 0, 10), (200000, -5, 100000),
+                                     (300000, 0, 1 << 40)])
+def test_unique_bitexact(ops, orc, n, lo, hi):
+    rng = np.random.default_rng(n)
+    x = rng.integers(lo, hi, n).astype(np.int64)
+    if n > 10:
+        x[5] = -1                      # the table's empty pattern is handled
+        x[7] = -1
+    y, idx, cnt = ops.unique_with_counts(T(x))
+    ry, ridx, rcnt = orc.unique(x, with_counts=True)
+    np.testing.assert_array_equal(H(y), ry)
+    np.testing.assert_array_equal(H(idx), ridx)
+    np.testing.assert_array_equal(H(cnt), rcnt)
+
+
+def test_sort_pairs_stable(ops):
+    rng = np.random.default_rng(3)
+    n = 100003
+    keys = rng.integers(0, 1 << 20, n).astype(np.int64)
+    vals = np.arange(n, dtype=np.int32)
+    ko, vo = ops.sort_pairs(T(keys), T(vals), 20)
+    order = np.argsort(keys, kind="stable")
+    np.testing.assert_array_equal(H(ko), keys[order])
+    np.testing.assert_array_equal(H(vo), vals[order])
+
+
+def test_unsorted_segment_sum_bitexact(ops, orc):
+    rng = np.random.default_rng(11)
+    n, D, S = 20000, 24, 700
+    data = (rng.standard_normal((n, D)) * 100).astype(np.float32)
+    seg = rng.integers(-3, S, n).astype(np.int32)
+    out = H(ops.unsorted_segment_sum(T(data), T(seg), S))
+    np.testing.assert_array_equal(out, orc.unsorted_segment_sum(data, seg, S))
+
+
+@pytest.mark.parametrize("comb", ["sum", "mean", "sqrtn"])
+def test_segment_grad_bitexact(ops, orc, comb):
+    rng = np.random.default_rng(5)
+    B, D, U = 300, 16, 120
+    lens = rng.integers(1, 12, B)
+    seg = np.repeat(np.arange(B), lens).astype(np.int32)
+    idx = rng.integers(0, U, seg.shape[0]).astype(np.int32)
+    grad = rng.standard_normal((B, D)).astype(np.float32)
+    fn = {"sum": ops.sparse_segment_sum_grad, "mean": ops.sparse_segment_mean_grad,
+          "sqrtn": ops.sparse_segment_sqrt_n_grad}[comb]
+    out = H(fn(T(grad), T(idx), T(seg), U))
+    np.testing.assert_array_equal(out, orc.sparse_segment_reduce_grad(grad, idx, seg, U, comb))
+
+
+def test_gather_and_oob(dr, ops):
+    t = np.arange(40, dtype=np.float32).reshape(10, 4)
+    out = H(ops.gather(T(t), T([3, 0, 9])))
+    np.testing.assert_array_equal(out, t[[3, 0, 9]])
+    with pytest.raises(dr.DeepRecError):
+        ops.gather(T(t), T([10]))
+
+
+# ---------------------------------------------------------------------------
+# EmbeddingVariable
+# ---------------------------------------------------------------------------
+def test_ev_export_kat(dr, orc):
+    k = load("ev")["export"]
+    ev = dr.EmbeddingVariable("exp", k["dim"], k["init"],
+                              ev_option=dr.EmbeddingVariableOption(
+                                  filter_option=dr.CounterFilter(k["filter_freq"]),
+                                  evict_option=dr.GlobalStepEvict(k["steps_to_live"])))
+    from deeprec_amd import ops
+    for _ in range(k["runs"]):
+        u, idx, cnt = ops.unique_with_counts(T(k["lookup"]))
+        ev.sparse_read(u, counts=cnt)
+    keys, vals, vers, frqs = ev.export()
+    assert H(keys).tolist() == k["keys"]
+    assert H(vals).tolist() == k["values"]
+    assert H(vers).tolist() == k["versions"]
+    assert H(frqs).tolist() == k["freqs"]
+
+
+def test_ev_shape_kat(dr):
+    k = load("ev")["shape"]
+    ev = dr.EmbeddingVariable("shape", k["dim"], 1.0)
+    ev.sparse_read(T(k["lookup"]))
+    assert ev.total_count().tolist() == k["expected"]
+
+
+def test_ev_counter_filter_timeline(dr, ops):
+    k = load("ev")["counter_filter_gd"]
+    ev = dr.EmbeddingVariable("cf", k["dim"], 1.0,
+                              ev_option=dr.EmbeddingVariableOption(
+                                  filter_option=dr.CounterFilter(k["filter_freq"])))
+    opt = dr.GradientDescentOptimizer(k["lr"])
+    seen = []
+    for step in range(4):
+        u, idx, cnt = ops.unique_with_counts(T([k["key"]]))
+        seen.append(H(ev.sparse_read(u, counts=cnt)))
+        ev.pending_grads.append(dr.IndexedSlices(
+            T(np.full((1, k["dim"]), k["loss_scale"], np.float32)), u))
+        opt.apply_gradients([ev], global_step=step)
+    assert all((s == 1.0).all() for s in seen[:3])
+    assert (seen[3] != 1.0).all()
+
+
+def test_ev_gather_matches_oracle(dr, orc):
+    rng = np.random.default_rng(9)
+    D = 16
+    ev = dr.EmbeddingVariable("g", D, 0.5, capacity=64)      # forces growth
+    oev = orc.EV(D, 0.5)
+    for step in range(5):
+        keys = np.unique(rng.integers(-10, 400, 150)).astype(np.int64)
+        rng.shuffle(keys)
+        dflt = rng.standard_normal((keys.shape[0], D)).astype(np.float32)
+        out = H(ev.sparse_read(T(keys), ev_init_value=T(dflt)))
+        ref = oev.gather(keys, dflt)
+        np.testing.assert_array_equal(out, ref)
+    assert int(ev.total_count()[0]) == oev.size()
+    k1, v1, _, _ = ev.export()
+    k2, v2, _, _ = oev.export()
+    np.testing.assert_array_equal(H(k1), k2)
+    np.testing.assert_array_equal(H(v1), v2)
+
+
+def test_ev_insert_import_semantics(dr, orc):
+    ev = dr.EmbeddingVariable("imp", 2, 0.0, steps_to_live=5,
+                              ev_option=dr.EmbeddingVariableOption(
+                                  filter_option=dr.CounterFilter(2)))
+    keys = np.arange(20, dtype=np.int64)
+    vals = np.repeat(keys[:, None], 2, 1).astype(np.float32)
+    ev.import_partitioned(T(keys), T(vals), T(keys * 10), T(np.ones(20, np.int64)), 1, 4)
+    k, v, ver, fr = ev.export()
+    assert H(k).tolist() == [x for x in range(20) if x % 4 == 1]
+    assert (H(fr) == 2).all()
+    assert H(ver).tolist() == [x * 10 for x in H(k)]
+    # existing rows are kept by insert (Import semantics)
+    ev.insert(T(np.array([1], np.int64)), T(np.array([[7.0, 7.0]], np.float32)))
+    k, v, _, _ = ev.export()
+    assert H(v)[0].tolist() == [1.0, 1.0]
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adagrad", "adam"])
+def test_ev_equals_dense_5step(dr, orc, opt):
+    k = load("ev")["ev_equals_dense"]
+    D, ids, lr = k["dim"], np.asarray(k["ids"], np.int64), np.float32(k["lr"])
+    ev = dr.EmbeddingVariable("eq_" + opt, D, 1.0)
+    oev = orc.EV(D, 1.0)
+    if opt == "sgd":
+        o = dr.GradientDescentOptimizer(lr)
+    elif opt == "adagrad":
+        o = dr.AdagradOptimizer(lr, k["adagrad_initial_accumulator"])
+        oacc = oev.create_slot(1, k["adagrad_initial_accumulator"])
+    else:
+        a = k["adam"]
+        o = dr.AdamOptimizer(lr, a["beta1"], a["beta2"], a["epsilon"])
+        om, ov = oev.create_slot(1, 0.0), oev.create_slot(2, 0.0)
+    g = np.full((len(ids), D), k["loss_scale"], np.float32)
+    for step in range(k["steps"]):
+        r = H(ev.sparse_read(T(ids)))
+        np.testing.assert_allclose(r, oev.gather(ids), rtol=RTOL)
+        ev.pending_grads.append(dr.IndexedSlices(T(g), T(ids)))
+        o.apply_gradients([ev], global_step=step)
+        if opt == "sgd":
+            oev.apply_sgd(lr, g, ids, step)
+        elif opt == "adagrad":
+            oev.apply_adagrad(oacc, lr, g, ids, step)
+        else:
+            b1p = np.float32(a["beta1"]) ** (step + 1)
+            b2p = np.float32(a["beta2"]) ** (step + 1)
+            oev.apply_adam(om, ov, b1p, b2p, lr, a["beta1"], a["beta2"], a["epsilon"], g, ids,
+                           step)
+    final = H(ev.sparse_read(T(ids)))
+    if opt == "sgd":
+        np.testing.assert_array_equal(final, oev.gather(ids))
+    else:
+        np.testing.assert_allclose(final, oev.gather(ids), rtol=RTOL)
+
+
+def test_ev_bloom_filter_sequential(dr, orc):
+    f = dr.CBFFilter(filter_freq=3, max_element_size=1000, false_positive_probability=0.01,
+                     counter_type=16)
+    ev = dr.EmbeddingVariable("bloom", 4, 0.5, ev_option=dr.EmbeddingVariableOption(
+        filter_option=f))
+    oev = orc.EV(4, 0.5, filter_freq=3, max_element_size=1000, false_positive_probability=0.01,
+                 counter_bits=16)
+    for rep in range(5):
+        for key in range(12):
+            a = H(ev.sparse_read(T([key])))
+            b = oev.gather(np.array([key], np.int64))
+            np.testing.assert_array_equal(a, b)
+    assert int(ev.total_count()[0]) == oev.size()
+    _, _, _, f1 = ev.export()
+    _, _, _, f2 = oev.export()
+    np.testing.assert_array_equal(H(f1), f2)
+
+
+# ---------------------------------------------------------------------------
+# embedding_lookup_sparse composition
+# ---------------------------------------------------------------------------
+def _random_sparse(rng, B, max_h, vocab, allow_empty=False):
+    lens = rng.integers(0 if allow_empty else 1, max_h + 1, B)
+    rows = np.repeat(np.arange(B), lens)
+    cols = np.concatenate([np.arange(l) for l in lens]) if lens.sum() else np.zeros(0, np.int64)
+    ind = np.stack([rows, cols], 1).astype(np.int64)
+    vals = rng.integers(0, vocab, rows.shape[0]).astype(np.int64)
+    return ind, vals
+
+
+@pytest.mark.parametrize("comb", ["sum", "mean", "sqrtn"])
+@pytest.mark.parametrize("D", [8, 64, 128])
+def test_ev_lookup_sparse_bitexact(dr, orc, comb, D):
+    rng = np.random.default_rng(D + 3)
+    B = 257
+    ev = dr.EmbeddingVariable("els_%s_%d" % (comb, D), D, 0.25)
+    oev = orc.EV(D, 0.25)
+    # pre-populate part of the key space with distinct rows
+    keys = np.arange(0, 300, dtype=np.int64)
+    vals = rng.standard_normal((300, D)).astype(np.float32)
+    ev.insert(T(keys), T(vals))
+    oev.insert(keys, vals)
+    ind, v = _random_sparse(rng, B, 20, 600)
+    out = H(dr.embedding_lookup_sparse(ev, dr.SparseTensor(T(ind), T(v), (B, 20)),
+                                       combiner=comb))
+    ref = orc.embedding_lookup_sparse(oev, ind, v, B, combiner=comb)
+    np.testing.assert_array_equal(out, ref)
+    assert int(ev.total_count()[0]) == oev.size()
+
+
+@pytest.mark.parametrize("comb", ["sum", "mean", "sqrtn"])
+def test_dense_lookup_sparse_bitexact(dr, orc, comb):
+    rng = np.random.default_rng(17)
+    B, D, R = 1000, 32, 5000
+    table = rng.standard_normal((R, D)).astype(np.float32)
+    ind, v = _random_sparse(rng, B, 15, R)
+    out = H(dr.embedding_lookup_sparse(T(table), dr.SparseTensor(T(ind), T(v), (B, 15)),
+                                       combiner=comb))
+    np.testing.assert_array_equal(out, orc.embedding_lookup_sparse(table, ind, v, B,
+                                                                   combiner=comb))
+
+
+def test_weighted_and_max_norm_lookup(dr, orc):
+    rng = np.random.default_rng(21)
+    B, D, R = 200, 16, 800
+    table = rng.standard_normal((R, D)).astype(np.float32)
+    ind, v = _random_sparse(rng, B, 6, R)
+    w = rng.uniform(0.1, 2.0, v.shape[0]).astype(np.float32)
+    sp = dr.SparseTensor(T(ind), T(v), (B, 6))
+    for comb in ("sum", "mean", "sqrtn"):
+        out = H(dr.embedding_lookup_sparse(T(table), sp, dr.SparseTensor(T(ind), T(w), (B, 6)),
+                                           combiner=comb))
+        ref = orc.embedding_lookup_sparse(table, ind, v, B, weights=w, combiner=comb)
+        np.testing.assert_allclose(out, ref, rtol=RTOL, atol=1e-6)
+        out = H(dr.embedding_lookup_sparse(T(table), sp, combiner=comb, max_norm=1.5))
+        ref = orc.embedding_lookup_sparse(table, ind, v, B, combiner=comb, max_norm=1.5)
+        np.testing.assert_allclose(out, ref, rtol=RTOL, atol=1e-6)
+
+
+def test_safe_lookup_prune_and_empty_rows(dr, orc):
+    rng = np.random.default_rng(23)
+    B, D = 100, 8
+    ev = dr.EmbeddingVariable("safe", D, 0.5)
+    oev = orc.EV(D, 0.5)
+    ind, v = _random_sparse(rng, B, 5, 50, allow_empty=True)
+    v[::7] = -3                                  # pruned ids
+    sp = dr.SparseTensor(T(ind), T(v), (B, 5))
+    for default_id in (None, 4):
+        out = H(dr.safe_embedding_lookup_sparse(ev, sp, combiner="mean", default_id=default_id))
+        ref = orc.safe_embedding_lookup_sparse(oev, ind, v, (B, 5), combiner="mean",
+                                               default_id=default_id)
+        np.testing.assert_array_equal(out, ref)
+    assert int(ev.total_count()[0]) == oev.size()
+
+
+def test_lookup_backward_matches_segment_grad(dr, orc):
+    rng = np.random.default_rng(29)
+    B, D = 64, 8
+    for comb in ("sum", "mean", "sqrtn"):
+        ev = dr.EmbeddingVariable("bw_" + comb, D, 0.1)
+        ind, v = _random_sparse(rng, B, 7, 40)
+        out = dr.embedding_lookup_sparse(ev, dr.SparseTensor(T(ind), T(v), (B, 7)),
+                                         combiner=comb)
+        g = rng.standard_normal((B, D)).astype(np.float32)
+        out.backward(T(g))
+        sl = ev.pending_grads.pop()
+        U = int(sl.num_valid.item())
+        uids, idx = orc.unique(v)
+        assert H(sl.indices[:U]).tolist() == uids.tolist()
+        ref = orc.sparse_segment_reduce_grad(g, idx, ind[:, 0].astype(np.int32), U, comb)
+        np.testing.assert_array_equal(H(sl.values[:U]), ref)
+
+
+# ---------------------------------------------------------------------------
+# interactions / exchange helpers
+# ---------------------------------------------------------------------------
+def test_fm2(ops, orc):
+    rng = np.random.default_rng(31)
+    e = rng.standard_normal((300, 26, 64)).astype(np.float32)
+    out = H(ops.fm_second_order(T(e)))
+    ref = orc.fm2(e)
+    scale = 0.5 * (np.abs(e).sum(1) ** 2 + (e * e).sum(1))
+    assert (np.abs(out - ref) <= 1e-5 * scale + 1e-6).all()
+
+
+def test_dot_interaction(ops, orc):
+    rng = np.random.default_rng(37)
+    x = rng.standard_normal((50, 27, 128)).astype(np.float32)
+    out = H(ops.dot_interaction(T(x)))
+    ref = orc.dot_interaction(x)
+    scale = np.abs(x).sum(2).max() ** 2 / 27
+    np.testing.assert_allclose(out, ref, rtol=1e-4, atol=1e-5 * scale)
+
+
+def test_crossnet_bf16(ops, orc):
+    rng = np.random.default_rng(41)
+    B, d = 200, 200
+    bf = lambda a: torch.as_tensor(a, device=DEV).to(torch.bfloat16)
+    x0 = bf(rng.standard_normal((B, d)).astype(np.float32))
+    xl = bf(rng.standard_normal((B, d)).astype(np.float32))
+    W = bf((rng.standard_normal((d, d)) / np.sqrt(d)).astype(np.float32))
+    b = torch.as_tensor(rng.standard_normal(d).astype(np.float32), device=DEV)
+    out = ops.crossnet_layer(x0, xl, W, b).float()
+    ref = orc.crossnet_layer(H(x0.float()), H(xl.float()), H(W.float()), H(b))
+    err = np.abs(H(out) - ref)
+    assert err.max() <= 2e-2 * np.abs(ref).max() + 1e-2
+
+
+def test_partition_by_owner(ops):
+    rng = np.random.default_rng(43)
+    keys = rng.integers(0, 10 ** 9, 50000).astype(np.int64)
+    for world in (1, 2, 4, 8):
+        ko, perm, counts = ops.partition_by_owner(T(keys), world)
+        owner = keys % world
+        order = np.argsort(owner, kind="stable")
+        np.testing.assert_array_equal(H(perm), order)
+        np.testing.assert_array_equal(H(ko), keys[order])
+        np.testing.assert_array_equal(H(counts), np.bincount(owner, minlength=world))
