@@ -1,0 +1,275 @@
+#!/usr/bin/env python3
+"""bench.py -- embedding lookups/s on the DLRM Criteo-Terabyte shape.
+
+One step = one pass of the north_star hot path over one batch: for each of
+the 26 sparse features, first-occurrence dedup -> EmbeddingVariable
+insert-on-miss resolve -> fused gather + sum pooling into the [B, 26*128]
+input_layer output (embedding_lookup_sparse, combiner "sum", hotness 1).
+At N GPUs the tables are row-sharded (owner = key % N) and every step runs
+the index all-to-all -> owner resolve + gather -> row all-to-all exchange
+over RCCL (deeprec_amd/sharded.py); per-GPU work is fixed (weak scaling).
+
+Timing: W untimed warmup steps, then exactly K steps bracketed by a barrier
+and torch.cuda.synchronize(); max over ranks; rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "deeprec-1_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--tables", type=int, default=26)
+    p.add_argument("--rows", type=int, default=12_500_000, help="rows per table per GPU")
+    p.add_argument("--dim", type=int, default=128)
+    p.add_argument("--batch", type=int, default=65536, help="per-GPU batch (B_local)")
+    p.add_argument("--zipf", type=float, default=0.0, help="0 = uniform keys")
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-rows", type=int, default=2_000_000)
+    p.add_argument("--kernel-iters", type=int, default=20)
+    return p.parse_args()
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def make_batches(nb, tables, batch, keyspace, zipf, seed, device):
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    out = []
+    for _ in range(nb):
+        if zipf > 0:
+            rng = np.random.default_rng(seed)
+            k = (rng.zipf(zipf, size=(tables, batch)) - 1) % keyspace
+            ids = torch.as_tensor(k, dtype=torch.int64, device=device)
+        else:
+            ids = torch.randint(0, keyspace, (tables, batch), generator=g, device=device,
+                                dtype=torch.int64)
+        out.append(ids)
+        seed += 1
+    return out
+
+
+def cpu_baseline(args, n_lookups_target=None):
+    """DeepRec-CPU-semantics restatement (oracle/) timed on the host cores:
+    Unique -> KvResourceGather (EV hash lookup + row memcpy, Shard over
+    threads) -> SparseSegmentSum, per feature, h = 1."""
+    from oracle import oracle as orc
+    threads = min(16, os.cpu_count() or 1)
+    D, R = args.dim, args.cpu_rows
+    rng = np.random.default_rng(2021)
+    ev = orc.EV(D, 0.0)
+    chunk = 1 << 18
+    for b in range(0, R, chunk):
+        keys = np.arange(b, min(R, b + chunk), dtype=np.int64)
+        ev.insert(keys, rng.standard_normal((keys.shape[0], D)).astype(np.float32))
+    B = args.batch
+    seg_off = np.arange(B + 1, dtype=np.int32)
+    out = np.empty((B, D), np.float32)
+    L = orc.lib()
+    done, t0 = 0, time.perf_counter()
+    while True:
+        ids = rng.integers(0, R, B).astype(np.int64)
+        rc = L.orc_pipeline_ev_lookup_sparse(ev._h, orc._p(ids), B, orc._p(seg_off), B, 0,
+                                             threads, orc._p(out))
+        assert rc == 0
+        done += B
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds:
+            break
+    return {"value": done / el, "unit": "lookups/s", "cores": threads, "kind": "port",
+            "sample": "%d lookups (features of B=%d ids, h=1) over a %d-key x %d-dim fp32 EV, "
+                      "%.1f s, oracle/deeprec_oracle.c orc_pipeline_ev_lookup_sparse "
+                      "(serial Unique + sharded KvResourceGather + ali SparseSegmentSum)"
+                      % (done, B, R, D, el)}
+
+
+def main():
+    args = parse()
+    import deeprec_amd as dr
+    from deeprec_amd import _lib, ops
+    from deeprec_amd.embedding_ops import SparseTensor
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    dr.load()
+    T, D, B, R = args.tables, args.dim, args.batch, args.rows
+    torch.cuda.synchronize()
+
+    # ---- tables: T EVs, keys [0, R) resident with synthetic rows ---------
+    t0 = time.perf_counter()
+    evs = []
+    for t in range(T):
+        ev = dr.EmbeddingVariable("table%d" % t, D, 0.0, capacity=R + (1 << 19), device=dev)
+        ev.insert_synthetic(0, R, seed=1000 + t)
+        evs.append(ev)
+    torch.cuda.synchronize()
+    log("populated %d EVs x %d rows x %d dim in %.1fs" % (T, R, D, time.perf_counter() - t0))
+
+    if world > 1:
+        from deeprec_amd.sharded import ShardedLookup
+        engine = ShardedLookup(evs, world, rank, B, dev)
+        keyspace = R * world
+    else:
+        engine = None
+        keyspace = R
+    batches = make_batches(4, T, B, keyspace, args.zipf, 2021 + 7919 * rank, dev)
+    seg = torch.arange(B, dtype=torch.int32, device=dev)
+    ind = torch.stack([torch.arange(B, device=dev), torch.zeros(B, dtype=torch.int64, device=dev)], 1)
+    static_ids = torch.empty((T, B), dtype=torch.int64, device=dev)
+    sps = [SparseTensor(ind, static_ids[t], (B, 1)) for t in range(T)]
+
+    def step():
+        if engine is not None:
+            return engine.forward(static_ids)
+        return dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum")
+
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        for w in range(max(args.warmup, 2)):
+            static_ids.copy_(batches[w % len(batches)])
+            out = step()
+            torch.cuda.synchronize()
+            log("eager warmup step %d ok" % w)
+        dr.status_check(dev)
+        graph = None
+        if not args.no_graph and engine is None:
+            graph = torch.cuda.CUDAGraph()
+            static_ids.copy_(batches[0])
+            with torch.cuda.graph(graph):
+                out = step()
+            log("graph captured")
+            graph.replay()
+            torch.cuda.synchronize()
+            log("graph replay ok")
+
+        debug = os.environ.get("DR_BENCH_DEBUG") == "1"
+
+        def run_step(i):
+            static_ids.copy_(batches[i % len(batches)])
+            if debug:
+                torch.cuda.synchronize()
+                log("step %d: input copied" % i)
+            if graph is not None:
+                graph.replay()
+            else:
+                step()
+            if debug:
+                torch.cuda.synchronize()
+                log("step %d: done" % i)
+
+        for w in range(args.warmup):
+            run_step(w)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            run_step(i)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        log("timed %d steps in %.3fs" % (args.steps, el))
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    lookups = T * B * args.steps * world
+    value = lookups / el
+    ms = el / args.steps * 1e3
+    dr.status_check(dev)
+
+    # ---- dominant kernel: the grouped gather+pool launch, timed alone -----
+    from deeprec_amd.embedding_ops import _Feature, _prepare_group, _pool_all
+    static_ids.copy_(batches[0])
+    with torch.no_grad():
+        feats = [_Feature(evs[t], static_ids[t], seg, B, None, "sum", None) for t in range(T)]
+        _prepare_group(feats)
+        _pool_all(feats, _lib.ORDER_ALI)
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.kernel_iters):
+            _pool_all(feats, _lib.ORDER_ALI)
+        e1.record()
+        torch.cuda.synchronize()
+    k_ms = e0.elapsed_time(e1) / args.kernel_iters
+    per_lookup = 8 + 4 + D * 4 + D * 4      # nnz(8+4+Ds) + B*Ds, h = 1
+    bytes_launch = T * B * per_lookup
+    achieved = bytes_launch / (k_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+            "kernel": "dr::pool_grouped_kernel<4,32,1,ALI,4>", "kernel_ms": round(k_ms, 4),
+            "bytes_per_launch": bytes_launch, "bytes_per_lookup": per_lookup}
+    pmc = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            roof["traffic"] = json.load(open(pmc)).get("pool_bytes_per_launch")
+        except Exception:
+            pass
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        with open(os.path.join(ROOT, "BASELINE.json")) as f:
+            metric = json.load(f)["metric"]
+        line = {
+            "metric": metric,
+            "value": round(value, 1),
+            "unit": "lookups/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (uniform keys%s, hash-derived table rows)" % (
+                "" if args.zipf <= 0 else ", zipf %.2f" % args.zipf),
+            "config": {"workload": "DLRM Criteo-TB shape: %d EV tables x %d rows/GPU x %d fp32, "
+                                   "B_local=%d, hotness 1, embedding_lookup_sparse(sum) forward "
+                                   "(unique -> EV resolve -> fused gather+pool)%s"
+                                   % (T, R, D, B, "; row-sharded all-to-all" if world > 1 else ""),
+                       "global_batch": B * world, "tables": T, "rows_per_gpu": R, "dim": D,
+                       "parallelism": "row-sharded tables x%d, data-parallel batch" % world},
+            "samples_per_s": round(value / T, 1),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -33,6 +33,40 @@ int* status_word() {
   return cache[dev];
 }
 
+__global__ void fill_u32_kernel(uint32_t* __restrict__ p, int64_t n4, uint32_t v) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) p[i] = v;
+}
+
+__global__ void fill_u8_kernel(unsigned char* __restrict__ p, int64_t n, unsigned char v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+int fill_bytes(void* p, unsigned char value, size_t bytes, hipStream_t st) {
+  if (bytes == 0) return DR_OK;
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t v4 = 0x01010101u * value;
+  if ((a & 3) == 0) {
+    const int64_t n4 = (int64_t)(bytes / 4);
+    if (n4 > 0) {
+      int64_t blocks = ceil_div(n4, 256);
+      if (blocks > 4096) blocks = 4096;
+      hipLaunchKernelGGL(fill_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                         static_cast<uint32_t*>(p), n4, v4);
+    }
+    const int64_t tail = (int64_t)(bytes - (size_t)n4 * 4);
+    if (tail > 0)
+      hipLaunchKernelGGL(fill_u8_kernel, dim3(1), dim3(256), 0, st,
+                         static_cast<unsigned char*>(p) + n4 * 4, tail, value);
+  } else {
+    hipLaunchKernelGGL(fill_u8_kernel, dim3((unsigned)ceil_div((int64_t)bytes, 256)), dim3(256), 0,
+                       st, static_cast<unsigned char*>(p), (int64_t)bytes, value);
+  }
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
 __global__ void fill_synth_kernel(float* __restrict__ t, int64_t rows, int dim, uint64_t seed) {
   const int64_t total4 = rows * dim / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;

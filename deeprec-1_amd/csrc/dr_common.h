@@ -99,6 +99,12 @@ __device__ __forceinline__ int64_t eff_n(int64_t n, const int64_t* n_dev) {
   return m < n ? m : n;
 }
 
+// Byte-pattern fill by a kernel (stream-ordered, graph-capturable).  Used
+// instead of hipMemsetAsync for workspace state that later kernels probe:
+// a captured memset node is serviced by a DMA engine and in hipGraph replay
+// the next kernel may still see the previous contents in another XCD's L2.
+int fill_bytes(void* p, unsigned char value, size_t bytes, hipStream_t st);
+
 // ---- scan / sort primitives (scan_sort.hip) --------------------------------
 size_t scan_ws_bytes(int64_t n);
 // Exclusive scan of int32 values into int32 out; *total (device int64) = sum.

@@ -287,30 +287,47 @@ __device__ void bloom_addfreq(const EvDesc& e, uint64_t key, int64_t cnt) {
 // Grouped over tables: table t owns keys [koff[t], koff[t+1]) and the device
 // count n_dev[t] (nullable) bounds it.
 // ---------------------------------------------------------------------------
+// Tagged mode (tags != nullptr): one array holds keys of all T tables with a
+// per-key table id tags[i]; n_dev[0] bounds it.  This is the owner side of
+// the sharded exchange, where keys of every feature arrive interleaved.
 struct EvGroup {
   EvDesc e[DR_MAX_GROUP];
   int64_t koff[DR_MAX_GROUP + 1];
   const int64_t* n_dev[DR_MAX_GROUP];
+  const int32_t* tags;
 };
 
-__device__ __forceinline__ int table_of(const EvGroup& g, int T, int64_t i) {
-  int t = 0;
-  while (t + 1 < T && i >= g.koff[t + 1]) ++t;
-  return t;
+__device__ __forceinline__ bool locate(const EvGroup& g, int T, int64_t i,
+                                       const int64_t* __restrict__ keys, int* t, int64_t* li,
+                                       uint64_t* key) {
+  if (i >= g.koff[T]) return false;
+  if (g.tags) {
+    if (g.n_dev[0] && i >= *g.n_dev[0]) return false;
+    *t = g.tags[i];
+    *key = (uint64_t)keys[i];
+    *li = i;
+    return true;
+  }
+  int tt = 0;
+  while (tt + 1 < T && i >= g.koff[tt + 1]) ++tt;
+  *t = tt;
+  *li = i - g.koff[tt];
+  if (g.n_dev[tt] && *li >= *g.n_dev[tt]) return false;
+  *key = (uint64_t)keys[i];
+  return true;
 }
 
 __global__ void ev_resolve_kernel(EvGroup g, int T, const int64_t* __restrict__ keys,
                                   const int32_t* __restrict__ counts, int64_t* __restrict__ rows_out,
                                   uint8_t* __restrict__ init, int32_t* __restrict__ badd, int* st) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= g.koff[T]) return;
-  const int t = table_of(g, T, i);
+  int t;
+  int64_t li;
+  uint64_t key;
+  if (!locate(g, T, i, keys, &t, &li, &key)) return;
   const EvDesc& e = g.e[t];
-  const int64_t li = i - g.koff[t];
-  if (g.n_dev[t] && li >= *g.n_dev[t]) return;
   init[i] = 0;
   badd[i] = 0;
-  const uint64_t key = (uint64_t)keys[i];
   const int64_t cnt = counts ? counts[i] : 1;
   if (e.k_hash > 0) {  // BloomFilter::LookupOrCreate (embedding_filter.h:56-82)
     if (bloom_min_freq(e, key) < e.filter_freq) {
@@ -357,11 +374,11 @@ __global__ void ev_resolve_kernel(EvGroup g, int T, const int64_t* __restrict__ 
 __global__ void ev_bloom_add_kernel(EvGroup g, int T, const int64_t* __restrict__ keys,
                                     const int32_t* __restrict__ badd) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= g.koff[T]) return;
-  const int t = table_of(g, T, i);
-  const int64_t li = i - g.koff[t];
-  if (g.n_dev[t] && li >= *g.n_dev[t]) return;
-  if (badd[i] > 0) bloom_addfreq(g.e[t], (uint64_t)keys[i], badd[i]);
+  int t;
+  int64_t li;
+  uint64_t key;
+  if (!locate(g, T, i, keys, &t, &li, &key)) return;
+  if (badd[i] > 0) bloom_addfreq(g.e[t], key, badd[i]);
 }
 
 // Copy the first-touch rows: pool[col][row_i] = src(i), group of 64 lanes
@@ -372,6 +389,7 @@ struct InitGroup {
   const float* dflt[DR_MAX_GROUP];     // column default (dim)
   int64_t koff[DR_MAX_GROUP + 1];
   const int64_t* n_dev[DR_MAX_GROUP];
+  const int32_t* tags;
 };
 
 __global__ void ev_init_rows_kernel(InitGroup g, int T, int64_t dim,
@@ -380,9 +398,15 @@ __global__ void ev_init_rows_kernel(InitGroup g, int T, int64_t dim,
   const int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
   if (i >= g.koff[T]) return;
   int t = 0;
-  while (t + 1 < T && i >= g.koff[t + 1]) ++t;
-  const int64_t li = i - g.koff[t];
-  if (g.n_dev[t] && li >= *g.n_dev[t]) return;
+  int64_t li = i;
+  if (g.tags) {
+    if (g.n_dev[0] && i >= *g.n_dev[0]) return;
+    t = g.tags[i];
+  } else {
+    while (t + 1 < T && i >= g.koff[t + 1]) ++t;
+    li = i - g.koff[t];
+    if (g.n_dev[t] && li >= *g.n_dev[t]) return;
+  }
   if (!init[i]) return;
   const int64_t row = rows[i];
   const float* src = g.src[t] ? g.src[t] + li * dim : g.dflt[t];
@@ -400,6 +424,32 @@ __global__ void ev_copy_out_kernel(const float* __restrict__ pool, int64_t dim,
   const int64_t r = rows[i];
   const float* src = r >= 0 ? pool + r * dim : (defaults ? defaults + i * dim : dflt);
   for (int64_t c = threadIdx.x % 64; c < dim; c += 64) out[i * dim + c] = src[c];
+}
+
+// Owner-side row pack of the sharded exchange: out[i] = pool_t[row_i] (or the
+// table's default row when filtered), t from the composite key.  G lanes per
+// row, dwordx4.
+struct PoolGroup {
+  const float* pool[DR_MAX_GROUP];
+  const float* dflt[DR_MAX_GROUP];
+};
+
+template <int G>
+__global__ __launch_bounds__(256) void ev_gather_tagged_kernel(
+    PoolGroup pg, int T, int64_t dim, const int32_t* __restrict__ tags,
+    const int64_t* __restrict__ rows, int64_t n, const int64_t* n_dev, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G;
+  if (i >= eff_n(n, n_dev)) return;
+  const int t = tags[i];
+  const int64_t r = rows[i];
+  const float* src = r >= 0 ? pg.pool[t] + r * dim : pg.dflt[t];
+  const int lg = threadIdx.x % G;
+  if ((dim & 3) == 0) {
+    for (int64_t c = lg; c < dim / 4; c += G)
+      reinterpret_cast<float4*>(out + i * dim)[c] = reinterpret_cast<const float4*>(src)[c];
+  } else {
+    for (int64_t c = lg; c < dim; c += G) out[i * dim + c] = src[c];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -669,7 +719,8 @@ static int grow(EvShared* s, int64_t need, hipStream_t st) {
     int64_t ncap = next_pow2(need * 2);
     Slot* ns = nullptr;
     DR_HIP(hipMalloc(&ns, (size_t)(ncap + 1) * sizeof(Slot)));
-    DR_HIP(hipMemsetAsync(ns, 0xFF, (size_t)(ncap + 1) * sizeof(Slot), st));
+    int frc = fill_bytes(ns, 0xFF, (size_t)(ncap + 1) * sizeof(Slot), st);
+    if (frc) return frc;
     hipLaunchKernelGGL(ev_rehash_kernel, dim3((unsigned)ceil_div(s->cap, 256)), dim3(256), 0, st,
                        s->slots, s->cap, ns, ncap);
     DR_LAUNCH_CHECK();
@@ -696,7 +747,8 @@ static int grow(EvShared* s, int64_t need, hipStream_t st) {
       if (!*a) continue;
       int64_t* np = nullptr;
       DR_HIP(hipMalloc(&np, (size_t)nrc * sizeof(int64_t)));
-      DR_HIP(hipMemsetAsync(np, 0, (size_t)nrc * sizeof(int64_t), st));
+      int frc = fill_bytes(np, 0, (size_t)nrc * sizeof(int64_t), st);
+      if (frc) return frc;
       DR_HIP(hipMemcpyAsync(np, *a, (size_t)s->row_cap * sizeof(int64_t), hipMemcpyDeviceToDevice,
                             st));
       DR_HIP(hipStreamSynchronize(st));
@@ -712,16 +764,18 @@ static int grow(EvShared* s, int64_t need, hipStream_t st) {
 // count is mirrored asynchronously into pinned memory after every call).
 static int reserve(EvShared* s, int64_t n, hipStream_t st) {
   std::lock_guard<std::mutex> g(s->mu);
-  if (s->copy_pending && hipEventQuery(s->copy_ev) == hipSuccess) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(st, &cs);
+  const bool capturing = cs != hipStreamCaptureStatusNone;
+  // (event queries are illegal while a global-mode capture is open)
+  if (!capturing && s->copy_pending && hipEventQuery(s->copy_ev) == hipSuccess) {
     s->known = *s->pinned_top;
     s->adds_since_known = s->adds_since_copy;
     s->copy_pending = false;
   }
   const int64_t limit = std::min(s->row_cap, s->cap * 3 / 4);
   if (s->known + s->adds_since_known + n > limit) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(st, &cs);
-    DR_REQUIRE(cs == hipStreamCaptureStatusNone, DR_RESOURCE_EXHAUSTED,
+    DR_REQUIRE(!capturing, DR_RESOURCE_EXHAUSTED,
                "EV capacity may be exceeded inside stream capture; dr_ev_reserve first");
     DR_HIP(hipStreamSynchronize(st));
     int64_t actual = 0;
@@ -740,6 +794,8 @@ static int reserve(EvShared* s, int64_t n, hipStream_t st) {
 }
 
 static void post_call(EvShared* s, hipStream_t st) {
+  static const bool no_mirror = getenv("DR_NO_MIRROR") != nullptr;
+  if (no_mirror) return;
   std::lock_guard<std::mutex> g(s->mu);
   if (s->copy_pending) return;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -769,7 +825,8 @@ static ResolveWs carve_resolve(void* ws, int64_t n, size_t* used) {
 static int resolve_grouped(dr_ev* const* evs, int T, const int64_t* keys, const int64_t* koff,
                            const int64_t* const* n_dev, const float* const* defaults,
                            const int32_t* counts, int64_t* rows_out, void* ws, size_t ws_bytes,
-                           hipStream_t st) {
+                           hipStream_t st, const int32_t* tags = nullptr) {
+  const bool composite = tags != nullptr;
   DR_REQUIRE(T >= 1 && T <= DR_MAX_GROUP, DR_INVALID_ARGUMENT, "bad table count");
   const int64_t total = koff[T];
   size_t need = 0;
@@ -779,7 +836,7 @@ static int resolve_grouped(dr_ev* const* evs, int T, const int64_t* keys, const 
   int* stw = status_word();
   DR_REQUIRE(stw, DR_INTERNAL, "status word unavailable");
   for (int t = 0; t < T; ++t) {
-    int rc = reserve(evs[t]->sh, koff[t + 1] - koff[t], st);
+    int rc = reserve(evs[t]->sh, composite ? total : koff[t + 1] - koff[t], st);
     if (rc) return rc;
   }
   ResolveWs w = carve_resolve(ws, total, nullptr);
@@ -788,14 +845,16 @@ static int resolve_grouped(dr_ev* const* evs, int T, const int64_t* keys, const 
   InitGroup ig;
   memset(&ig, 0, sizeof(ig));
   bool any_bloom = false;
+  g.tags = tags;
+  ig.tags = tags;
   for (int t = 0; t < T; ++t) {
     g.e[t] = make_desc(evs[t]);
-    g.koff[t] = koff[t];
-    g.n_dev[t] = n_dev ? n_dev[t] : nullptr;
+    g.koff[t] = composite ? 0 : koff[t];
+    g.n_dev[t] = n_dev ? n_dev[composite ? 0 : t] : nullptr;
     ig.pool[t] = evs[t]->sh->pools[evs[t]->col];
     ig.src[t] = defaults ? defaults[t] : nullptr;
     ig.dflt[t] = evs[t]->sh->defaults[evs[t]->col];
-    ig.koff[t] = koff[t];
+    ig.koff[t] = g.koff[t];
     ig.n_dev[t] = g.n_dev[t];
     any_bloom |= g.e[t].k_hash > 0;
     DR_REQUIRE(evs[t]->sh->dim == evs[0]->sh->dim, DR_INVALID_ARGUMENT,
@@ -1008,6 +1067,52 @@ int dr_ev_resolve_grouped(dr_ev* const* evs, int num_tables, const int64_t* keys
                           void* stream) {
   return dr::resolve_grouped(evs, num_tables, keys, koff_host, n_dev_per_table, nullptr, counts,
                              rows_out, ws, ws_bytes, dr::S(stream));
+}
+
+// Tagged resolve: keys of all T tables in one array, table of key i =
+// tags[i] (n_dev: optional DEVICE count).  Filtered keys give -(i+1) and
+// read table t's EV default.
+int dr_ev_resolve_tagged(dr_ev* const* evs, int num_tables, const int64_t* keys,
+                         const int32_t* tags, int64_t n, const int64_t* n_dev,
+                         const int32_t* counts, int64_t* rows_out, void* ws, size_t ws_bytes,
+                         void* stream) {
+  DR_REQUIRE(num_tables >= 1 && num_tables <= DR_MAX_GROUP, DR_INVALID_ARGUMENT,
+             "bad table count");
+  int64_t koff[DR_MAX_GROUP + 1];
+  for (int t = 0; t < num_tables; ++t) koff[t] = 0;
+  koff[num_tables] = n;
+  const int64_t* nd[1] = {n_dev};
+  DR_REQUIRE(tags, DR_INVALID_ARGUMENT, "tags required");
+  return dr::resolve_grouped(evs, num_tables, keys, koff, nd, nullptr, counts, rows_out, ws,
+                             ws_bytes, dr::S(stream), tags);
+}
+
+// Owner-side pack for the row exchange: out[i] = resolved row of key i of
+// table tags[i] (table default when filtered).
+int dr_ev_gather_tagged(dr_ev* const* evs, int num_tables, const int32_t* tags,
+                        const int64_t* rows, int64_t n, const int64_t* n_dev, float* out,
+                        void* stream) {
+  using namespace dr;
+  DR_REQUIRE(num_tables >= 1 && num_tables <= DR_MAX_GROUP, DR_INVALID_ARGUMENT,
+             "bad table count");
+  if (n == 0) return DR_OK;
+  PoolGroup pg;
+  memset(&pg, 0, sizeof(pg));
+  const int64_t dim = evs[0]->sh->dim;
+  for (int t = 0; t < num_tables; ++t) {
+    DR_REQUIRE(evs[t]->sh->dim == dim, DR_INVALID_ARGUMENT, "tables must share dim");
+    pg.pool[t] = evs[t]->sh->pools[evs[t]->col];
+    pg.dflt[t] = evs[t]->sh->defaults[evs[t]->col];
+  }
+  constexpr int G = 32;
+  hipLaunchKernelGGL(ev_gather_tagged_kernel<G>, dim3((unsigned)ceil_div(n, 256 / G)),
+                     dim3(256), 0, S(stream), pg, num_tables, dim, tags, rows, n, n_dev, out);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+const float* dr_ev_default_row(dr_ev* ev) {
+  return ev ? ev->sh->defaults[ev->col] : nullptr;
 }
 
 int dr_ev_gather(dr_ev* ev, const int64_t* keys, int64_t n, const float* defaults,

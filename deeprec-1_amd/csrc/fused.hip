@@ -105,9 +105,92 @@ __global__ void rows_move_kernel(const float* __restrict__ src, const int32_t* _
   }
 }
 
+struct RouteGroup {
+  int64_t koff[DR_MAX_GROUP + 1];
+};
+
+// sort key = owner * T + feature for valid uniques, world * T otherwise.
+__global__ void route_keys_kernel(RouteGroup g, int T, const int64_t* __restrict__ uniq,
+                                  const int64_t* __restrict__ num_unique, int world,
+                                  uint64_t* __restrict__ skey, int32_t* __restrict__ pos,
+                                  unsigned long long* __restrict__ counts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.koff[T]) return;
+  int t = 0;
+  while (t + 1 < T && i >= g.koff[t + 1]) ++t;
+  uint64_t k = (uint64_t)world * T;
+  if (i - g.koff[t] < num_unique[t]) {
+    int64_t o = uniq[i] % world;
+    if (o < 0) o += world;
+    k = (uint64_t)o * T + t;
+    atomicAdd(&counts[k], 1ull);
+  }
+  skey[i] = k;
+  pos[i] = (int32_t)i;
+}
+
+__global__ void route_emit_kernel(const int64_t* __restrict__ uniq, const uint64_t* __restrict__ skey,
+                                  const int32_t* __restrict__ perm, int64_t n, int T, int world,
+                                  int64_t* __restrict__ keys_out, int32_t* __restrict__ tags_out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint64_t k = skey[j];
+  if (k >= (uint64_t)world * T) return;
+  keys_out[j] = uniq[perm[j]];
+  tags_out[j] = (int32_t)(k % (uint64_t)T);
+}
+
 }  // namespace dr
 
 extern "C" {
+
+size_t dr_route_workspace_size(int64_t n, int world, int num_tables) {
+  (void)world;
+  (void)num_tables;
+  dr::Carver c(nullptr);
+  c.take<uint64_t>(n > 0 ? n : 1);
+  c.take<int32_t>(n > 0 ? n : 1);
+  c.take<uint64_t>(n > 0 ? n : 1);
+  c.take<char>(dr_sort_pairs_workspace_size(n));
+  return c.used + 256;
+}
+
+int dr_route_by_owner(const int64_t* uniq, const int64_t* koff_host, int num_tables,
+                      const int64_t* num_unique, int world, int64_t* keys_out, int32_t* tags_out,
+                      int32_t* perm_out, int64_t* counts, void* ws, size_t ws_bytes,
+                      void* stream) {
+  using namespace dr;
+  const int T = num_tables;
+  DR_REQUIRE(T >= 1 && T <= DR_MAX_GROUP && world >= 1 && world <= 1024, DR_INVALID_ARGUMENT,
+             "dr_route_by_owner: bad T/world");
+  const int64_t n = koff_host[T];
+  DR_REQUIRE(ws_bytes >= dr_route_workspace_size(n, world, T), DR_INVALID_ARGUMENT,
+             "workspace too small");
+  hipStream_t st = S(stream);
+  int frc = fill_bytes(counts, 0, (size_t)world * T * sizeof(int64_t), st);
+  if (frc) return frc;
+  if (n == 0) return DR_OK;
+  RouteGroup g;
+  for (int t = 0; t <= T; ++t) g.koff[t] = koff_host[t];
+  Carver c(ws);
+  uint64_t* skey = c.take<uint64_t>(n);
+  int32_t* pos = c.take<int32_t>(n);
+  uint64_t* skey2 = c.take<uint64_t>(n);
+  const size_t sb = dr_sort_pairs_workspace_size(n);
+  void* sws = c.take<char>(sb);
+  const unsigned blocks = (unsigned)ceil_div(n, 256);
+  hipLaunchKernelGGL(route_keys_kernel, dim3(blocks), dim3(256), 0, st, g, T, uniq, num_unique,
+                     world, skey, pos, (unsigned long long*)counts);
+  DR_LAUNCH_CHECK();
+  int bits = 0;
+  while (((int64_t)1 << bits) <= (int64_t)world * T) ++bits;
+  int rc = dr_sort_pairs(skey, pos, skey2, perm_out, n, 0, bits, sws, sb, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(route_emit_kernel, dim3(blocks), dim3(256), 0, st, uniq, skey2, perm_out, n,
+                     T, world, keys_out, tags_out);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
 
 size_t dr_fused_local_workspace_size(int64_t batch) {
   return (size_t)(batch + 2) * sizeof(int32_t) + 256;
@@ -170,7 +253,8 @@ int dr_partition_by_owner(const int64_t* keys, int64_t n, const int64_t* n_dev, 
   DR_REQUIRE(ws_bytes >= dr_partition_workspace_size(n), DR_INVALID_ARGUMENT,
              "workspace too small");
   hipStream_t st = S(stream);
-  DR_HIP(hipMemsetAsync(send_counts, 0, world * sizeof(int64_t), st));
+  int frc = fill_bytes(send_counts, 0, world * sizeof(int64_t), st);
+  if (frc) return frc;
   if (n == 0) return DR_OK;
   Carver c(ws);
   uint64_t* okey = c.take<uint64_t>(n);

@@ -554,7 +554,7 @@ static int segsum_driver(const int32_t* keyseg, int64_t n, int64_t num_out, cons
   SegSumWs w = carve_segsum(ws, n, num_out, &used);
   if (num_out == 0) return DR_OK;
   if (n == 0) {
-    DR_HIP(hipMemsetAsync(out, 0, (size_t)num_out * dim * sizeof(float), s));
+    return fill_bytes(out, 0, (size_t)num_out * dim * sizeof(float), s);
     return DR_OK;
   }
   hipLaunchKernelGGL(keys_from_i32_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,

@@ -95,7 +95,7 @@ size_t scan_ws_bytes(int64_t n) {
 int scan_exclusive_i32(const int32_t* in, int32_t* out, int64_t n, const int64_t* n_dev,
                        int64_t* total, void* ws, hipStream_t st) {
   if (n <= 0) {
-    if (total) DR_HIP(hipMemsetAsync(total, 0, sizeof(int64_t), st));
+    if (total) return fill_bytes(total, 0, sizeof(int64_t), st);
     return DR_OK;
   }
   const int64_t nb = ceil_div(n, kScanTile);

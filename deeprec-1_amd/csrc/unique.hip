@@ -1,71 +1,103 @@
-// unique.hip -- Unique / UniqueWithCounts in first-occurrence order.
+// unique.hip -- Unique / UniqueWithCounts in first-occurrence order, for one
+// table or for all T tables of a step in one pass (grouped).
 //
 // Replaces UniqueAliOp (core/kernels/unique_ali_op.cc:46-180); the order
 // contract is SerialComputeV1 (unique_ali_op_util.h:192-222): y lists keys
 // in order of first appearance, idx[i] = position of x[i] in y.
 //
 // GPU algorithm (no host sync, integer-exact):
-//   1. open-addressing table (capacity pow2 >= 2n) in the workspace; each
-//      position i CAS-inserts its key and atomicMin's its position into the
-//      slot -> slot holds the FIRST position of that key;
-//   2. flag[i] = (slot.minpos == i); exclusive scan of flags gives the
-//      unique id of every first occurrence (= first-occurrence order);
+//   1. open-addressing table per feature (capacity pow2 >= 2 n_t) in the
+//      workspace; each position i CAS-inserts its key and atomicMin's its
+//      position into the slot -> the slot holds the FIRST position of the key;
+//   2. flag[i] = (slot.minpos == i); one exclusive scan over all features;
+//      the local unique id is prefix[i] - prefix[first position of table t]
+//      (a table's first position is always a first occurrence);
 //   3. idx[i] = uid(slot(i)); counts by integer atomics (order-free, exact).
-// Key -1 is the table's empty pattern; it is routed to a dedicated slot.
+// Key -1 is the hash's empty pattern; each table routes it to a spare slot.
+// Outputs keep the input layout: table t's uniques / counts sit at
+// [koff[t], koff[t] + U_t) and U_t goes to num_unique[t] (device int64).
 #include "dr_common.h"
 
 namespace dr {
 
 static constexpr uint64_t kEmpty = ~0ull;
 
-struct UniqueWs {
-  uint64_t* tkeys;   // [cap]
-  uint32_t* minpos;  // [cap + 1]
-  int32_t* tuid;     // [cap + 1]
-  int32_t* slot_of;  // [n]
-  int32_t* flags;    // [n] scan output
-  void* scan_ws;
-  int64_t cap;
+struct UniqGroup {
+  int64_t koff[DR_MAX_GROUP + 1];   // input offsets
+  int64_t hbase[DR_MAX_GROUP];      // hash region base (slots)
+  int64_t hcap[DR_MAX_GROUP];       // region capacity (pow2), spare slot at hbase + hcap
 };
 
-static UniqueWs carve_unique(void* ws, int64_t n, size_t* used = nullptr) {
+struct UniqueWs {
+  uint64_t* tkeys;   // [hash_total]
+  uint32_t* minpos;  // [hash_total]
+  int32_t* tuid;     // [hash_total]
+  int32_t* slot_of;  // [n]
+  int32_t* flags;    // [n] scan output
+  int64_t* total;    // [1]
+  void* scan_ws;
+};
+
+static int64_t build_group(const int64_t* koff, int T, UniqGroup* g) {
+  int64_t base = 0;
+  for (int t = 0; t < T; ++t) {
+    const int64_t n = koff[t + 1] - koff[t];
+    g->koff[t] = koff[t];
+    g->hbase[t] = base;
+    g->hcap[t] = next_pow2(2 * (n > 32 ? n : 32));
+    base += g->hcap[t] + 1;
+  }
+  g->koff[T] = koff[T];
+  return base;
+}
+
+static UniqueWs carve_unique(void* ws, int64_t n, int64_t hash_total, size_t* used) {
   Carver c(ws);
   UniqueWs u;
-  u.cap = next_pow2(2 * (n > 32 ? n : 32));
-  u.tkeys = c.take<uint64_t>(u.cap);
-  u.minpos = c.take<uint32_t>(u.cap + 1);
-  u.tuid = c.take<int32_t>(u.cap + 1);
+  u.tkeys = c.take<uint64_t>(hash_total);
+  u.minpos = c.take<uint32_t>(hash_total);
+  u.tuid = c.take<int32_t>(hash_total);
   u.slot_of = c.take<int32_t>(n > 0 ? n : 1);
   u.flags = c.take<int32_t>(n > 0 ? n : 1);
+  u.total = c.take<int64_t>(1);
   u.scan_ws = c.take<char>(scan_ws_bytes(n));
-  if (used) *used = c.used;
+  if (used) *used = c.used + 256;
   return u;
 }
 
-__global__ void unique_insert_kernel(const int64_t* __restrict__ keys, int64_t n,
+__device__ __forceinline__ int group_table(const UniqGroup& g, int T, int64_t i) {
+  int t = 0;
+  while (t + 1 < T && i >= g.koff[t + 1]) ++t;
+  return t;
+}
+
+__global__ void unique_insert_kernel(UniqGroup g, int T, const int64_t* __restrict__ keys,
                                      uint64_t* __restrict__ tkeys, uint32_t* __restrict__ minpos,
-                                     int32_t* __restrict__ slot_of, int64_t cap) {
+                                     int32_t* __restrict__ slot_of) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= g.koff[T]) return;
+  const int t = group_table(g, T, i);
   const uint64_t k = (uint64_t)keys[i];
+  const int64_t cap = g.hcap[t];
+  uint64_t* tk = tkeys + g.hbase[t];
   int64_t s;
   if (k == kEmpty) {
     s = cap;
   } else {
     const uint64_t mask = (uint64_t)cap - 1;
     uint64_t h = mix64(k) & mask;
-    for (;;) {
-      uint64_t cur = tkeys[h];
-      if (cur == k) break;
-      if (cur == kEmpty) {
-        uint64_t old = atomicCAS((unsigned long long*)&tkeys[h], (unsigned long long)kEmpty,
-                                 (unsigned long long)k);
-        if (old == kEmpty || old == k) break;
-      }
+    // The CAS result (performed at the memory side) is the only truth used to
+    // skip a slot, so a stale cached line can never make the probe run past
+    // every slot (the table holds at most half its capacity).
+    for (int64_t probes = 0; probes <= cap; ++probes) {
+      uint64_t old = atomicCAS((unsigned long long*)&tk[h], (unsigned long long)kEmpty,
+                               (unsigned long long)k);
+      if (old == kEmpty || old == k) break;
       h = (h + 1) & mask;
     }
     s = (int64_t)h;
   }
+  s += g.hbase[t];
   atomicMin(&minpos[s], (uint32_t)i);
   slot_of[i] = (int32_t)s;
 }
@@ -79,67 +111,109 @@ __global__ void unique_flag_kernel(int64_t n, const uint32_t* __restrict__ minpo
 }
 
 // After the scan flags[] holds exclusive prefix sums.
-__global__ void unique_emit_kernel(const int64_t* __restrict__ keys, int64_t n,
+__global__ void unique_emit_kernel(UniqGroup g, int T, const int64_t* __restrict__ keys,
                                    const uint32_t* __restrict__ minpos,
                                    const int32_t* __restrict__ slot_of,
                                    const int32_t* __restrict__ prefix, int64_t* __restrict__ uniq,
                                    int32_t* __restrict__ tuid) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= g.koff[T]) return;
   const int32_t s = slot_of[i];
   if (minpos[s] == (uint32_t)i) {
-    const int32_t u = prefix[i];
-    uniq[u] = keys[i];
+    const int t = group_table(g, T, i);
+    const int32_t u = prefix[i] - prefix[g.koff[t]];
+    uniq[g.koff[t] + u] = keys[i];
     tuid[s] = u;
   }
 }
 
-__global__ void unique_expand_kernel(int64_t n, const int32_t* __restrict__ slot_of,
+__global__ void unique_expand_kernel(UniqGroup g, int T, const int32_t* __restrict__ slot_of,
                                      const int32_t* __restrict__ tuid, int32_t* __restrict__ idx,
                                      int32_t* __restrict__ counts) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= g.koff[T]) return;
   const int32_t u = tuid[slot_of[i]];
   idx[i] = u;
-  if (counts) atomicAdd(&counts[u], 1);
+  if (counts) {
+    const int t = group_table(g, T, i);
+    atomicAdd(&counts[g.koff[t] + u], 1);
+  }
+}
+
+__global__ void unique_counts_kernel(UniqGroup g, int T, const int32_t* __restrict__ prefix,
+                                     const int64_t* __restrict__ total,
+                                     int64_t* __restrict__ num_unique) {
+  const int t = threadIdx.x;
+  if (t >= T) return;
+  const int64_t n = g.koff[T];
+  const int64_t a = g.koff[t] < n ? prefix[g.koff[t]] : *total;
+  const int64_t b = g.koff[t + 1] < n ? prefix[g.koff[t + 1]] : *total;
+  num_unique[t] = g.koff[t + 1] > g.koff[t] ? b - a : 0;
 }
 
 }  // namespace dr
 
-extern "C" size_t dr_unique_workspace_size(int64_t n) {
+extern "C" size_t dr_unique_grouped_workspace_size(const int64_t* koff_host, int num_tables) {
+  if (num_tables < 1 || num_tables > DR_MAX_GROUP) return 0;
+  dr::UniqGroup g;
+  const int64_t ht = dr::build_group(koff_host, num_tables, &g);
   size_t used = 0;
-  dr::carve_unique(nullptr, n, &used);
-  return used + 256;
+  dr::carve_unique(nullptr, koff_host[num_tables], ht, &used);
+  return used;
+}
+
+extern "C" int dr_unique_grouped(const int64_t* keys, const int64_t* koff_host, int num_tables,
+                                 int64_t* uniq_out, int32_t* idx_out, int32_t* counts_out,
+                                 int64_t* num_unique, void* ws, size_t ws_bytes, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(num_tables >= 1 && num_tables <= DR_MAX_GROUP, DR_INVALID_ARGUMENT,
+             "dr_unique_grouped: 1..%d tables", DR_MAX_GROUP);
+  const int T = num_tables;
+  const int64_t n = koff_host[T];
+  DR_REQUIRE(n >= 0 && n < (int64_t)0x7fffffff, DR_INVALID_ARGUMENT, "dr_unique: bad n");
+  for (int t = 0; t < T; ++t)
+    DR_REQUIRE(koff_host[t + 1] >= koff_host[t], DR_INVALID_ARGUMENT, "koff must be sorted");
+  DR_REQUIRE(ws_bytes >= dr_unique_grouped_workspace_size(koff_host, T), DR_INVALID_ARGUMENT,
+             "dr_unique: workspace too small");
+  hipStream_t st = S(stream);
+  if (n == 0) {
+    return fill_bytes(num_unique, 0, T * sizeof(int64_t), st);
+    return DR_OK;
+  }
+  UniqGroup g;
+  const int64_t ht = build_group(koff_host, T, &g);
+  UniqueWs u = carve_unique(ws, n, ht, nullptr);
+  int frc = fill_bytes(u.tkeys, 0xFF, ht * sizeof(uint64_t), st);
+  if (!frc) frc = fill_bytes(u.minpos, 0xFF, ht * sizeof(uint32_t), st);
+  if (!frc && counts_out) frc = fill_bytes(counts_out, 0, n * sizeof(int32_t), st);
+  if (frc) return frc;
+  const unsigned blocks = (unsigned)ceil_div(n, 256);
+  hipLaunchKernelGGL(unique_insert_kernel, dim3(blocks), dim3(256), 0, st, g, T, keys, u.tkeys,
+                     u.minpos, u.slot_of);
+  hipLaunchKernelGGL(unique_flag_kernel, dim3(blocks), dim3(256), 0, st, n, u.minpos, u.slot_of,
+                     u.flags);
+  DR_LAUNCH_CHECK();
+  int rc = scan_exclusive_i32(u.flags, u.flags, n, nullptr, u.total, u.scan_ws, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(unique_emit_kernel, dim3(blocks), dim3(256), 0, st, g, T, keys, u.minpos,
+                     u.slot_of, u.flags, uniq_out, u.tuid);
+  hipLaunchKernelGGL(unique_expand_kernel, dim3(blocks), dim3(256), 0, st, g, T, u.slot_of, u.tuid,
+                     idx_out, counts_out);
+  hipLaunchKernelGGL(unique_counts_kernel, dim3(1), dim3(64), 0, st, g, T, u.flags, u.total,
+                     num_unique);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+extern "C" size_t dr_unique_workspace_size(int64_t n) {
+  const int64_t koff[2] = {0, n > 0 ? n : 0};
+  return dr_unique_grouped_workspace_size(koff, 1);
 }
 
 extern "C" int dr_unique(const int64_t* keys, int64_t n, int64_t* uniq_out, int32_t* idx_out,
                          int32_t* counts_out, int64_t* num_unique, void* ws, size_t ws_bytes,
                          void* stream) {
-  using namespace dr;
-  DR_REQUIRE(n >= 0 && n < (int64_t)0x7fffffff, DR_INVALID_ARGUMENT, "dr_unique: bad n");
-  DR_REQUIRE(ws_bytes >= dr_unique_workspace_size(n), DR_INVALID_ARGUMENT,
-             "dr_unique: workspace too small");
-  hipStream_t st = S(stream);
-  if (n == 0) {
-    DR_HIP(hipMemsetAsync(num_unique, 0, sizeof(int64_t), st));
-    return DR_OK;
-  }
-  UniqueWs u = carve_unique(ws, n);
-  DR_HIP(hipMemsetAsync(u.tkeys, 0xFF, u.cap * sizeof(uint64_t), st));
-  DR_HIP(hipMemsetAsync(u.minpos, 0xFF, (u.cap + 1) * sizeof(uint32_t), st));
-  if (counts_out) DR_HIP(hipMemsetAsync(counts_out, 0, n * sizeof(int32_t), st));
-  const unsigned blocks = (unsigned)ceil_div(n, 256);
-  hipLaunchKernelGGL(unique_insert_kernel, dim3(blocks), dim3(256), 0, st, keys, n, u.tkeys,
-                     u.minpos, u.slot_of, u.cap);
-  hipLaunchKernelGGL(unique_flag_kernel, dim3(blocks), dim3(256), 0, st, n, u.minpos, u.slot_of,
-                     u.flags);
-  DR_LAUNCH_CHECK();
-  int rc = scan_exclusive_i32(u.flags, u.flags, n, nullptr, num_unique, u.scan_ws, st);
-  if (rc) return rc;
-  hipLaunchKernelGGL(unique_emit_kernel, dim3(blocks), dim3(256), 0, st, keys, n, u.minpos,
-                     u.slot_of, u.flags, uniq_out, u.tuid);
-  hipLaunchKernelGGL(unique_expand_kernel, dim3(blocks), dim3(256), 0, st, n, u.slot_of, u.tuid,
-                     idx_out, counts_out);
-  DR_LAUNCH_CHECK();
-  return DR_OK;
+  const int64_t koff[2] = {0, n};
+  return dr_unique_grouped(keys, koff, 1, uniq_out, idx_out, counts_out, num_unique, ws, ws_bytes,
+                           stream);
 }

@@ -62,6 +62,10 @@ SIGNATURES = {
     "dr_status_check": (_I32, [_P]),
     "dr_unique_workspace_size": (_SZ, [_I64]),
     "dr_unique": (_I32, [_P, _I64, _P, _P, _P, _P, _P, _SZ, _P]),
+    "dr_unique_grouped_workspace_size": (_SZ, [_P, _I32]),
+    "dr_unique_grouped": (_I32, [_P, _P, _I32, _P, _P, _P, _P, _P, _SZ, _P]),
+    "dr_route_workspace_size": (_SZ, [_I64, _I32, _I32]),
+    "dr_route_by_owner": (_I32, [_P, _P, _I32, _P, _I32, _P, _P, _P, _P, _P, _SZ, _P]),
     "dr_sort_pairs_workspace_size": (_SZ, [_I64]),
     "dr_sort_pairs": (_I32, [_P, _P, _P, _P, _I64, _I32, _I32, _P, _SZ, _P]),
     "dr_gather": (_I32, [_P, _I64, _I64, _P, _I64, _P, _P]),
@@ -88,7 +92,10 @@ SIGNATURES = {
     "dr_ev_resolve_workspace_size": (_SZ, [_I64]),
     "dr_ev_resolve": (_I32, [_P, _P, _I64, _P, _P, _P, _P, _P, _SZ, _P]),
     "dr_ev_resolve_grouped": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "dr_ev_resolve_tagged": (_I32, [_P, _I32, _P, _P, _I64, _P, _P, _P, _P, _SZ, _P]),
+    "dr_ev_gather_tagged": (_I32, [_P, _I32, _P, _P, _I64, _P, _P, _P]),
     "dr_ev_pool": (_P, [_P]),
+    "dr_ev_default_row": (_P, [_P]),
     "dr_ev_gather_workspace_size": (_SZ, [_I64]),
     "dr_ev_gather": (_I32, [_P, _P, _I64, _P, _P, _P, _P, _SZ, _P]),
     "dr_ev_insert": (_I32, [_P, _P, _I64, _P, _P, _P, _I64, _I64, _P]),

@@ -161,12 +161,51 @@ class _LookupFn(torch.autograd.Function):
         return None, None, None
 
 
+def _groupable(feats):
+    p0 = feats[0].params
+    return (len(feats) > 1 and len(feats) <= _lib.MAX_GROUP
+            and all(isinstance(f.params, EmbeddingVariable) and not callable(f.params.initializer)
+                    and f.params.dim == p0.dim and f.params.device == p0.device for f in feats))
+
+
+def _prepare_group(feats):
+    """All features of a step at once: one grouped unique, one grouped EV
+    resolve (insert-on-miss + filters), then per-feature bag offsets."""
+    import ctypes as C
+    dev = feats[0].values.device
+    T = len(feats)
+    koff = [0]
+    for f in feats:
+        koff.append(koff[-1] + f.values.numel())
+    vals = torch.cat([f.values for f in feats])
+    with_counts = any(f.params.filter_freq != 0 for f in feats)
+    uniq, idx, cnt, U = ops.unique_grouped(vals, koff, with_counts)
+    rows = torch.empty(koff[-1], dtype=torch.int64, device=dev)
+    handles = (C.c_void_p * T)(*[f.params.handle.value for f in feats])
+    ndev = (C.c_void_p * T)(*[U.data_ptr() + 8 * t for t in range(T)])
+    wsb = lib().dr_ev_resolve_workspace_size(koff[-1])
+    ws = workspace(wsb, dev)
+    check(lib().dr_ev_resolve_grouped(handles, T, ptr(uniq), ops._koff_array(koff), ndev, ptr(cnt),
+                                      ptr(rows), ptr(ws), wsb, stream_handle(dev)))
+    ops._post(dev)
+    for t, f in enumerate(feats):
+        f.bag_off = ops.bag_offsets(f.seg, f.batch)
+        f.uniq = uniq[koff[t]:koff[t + 1]]
+        f.idx = idx[koff[t]:koff[t + 1]]
+        f.rows = rows[koff[t]:koff[t + 1]]
+        f.U = U[t:t + 1]
+        f.defaults = None
+
+
 def _run(feats, order=ORDER_ALI, need_grad=None):
     """Grouped pooled lookup of features sharing the batch -> [B, sum(D_t)]."""
     if need_grad is None:
         need_grad = torch.is_grad_enabled() and any(not torch.is_tensor(f.params) for f in feats)
-    for f in feats:
-        _prepare(f, need_unique=False)
+    if _groupable(feats):
+        _prepare_group(feats)
+    else:
+        for f in feats:
+            _prepare(f, need_unique=False)
     if need_grad:
         anchor = [_anchor(f.params) for f in feats if not torch.is_tensor(f.params)][0]
         return _LookupFn.apply(anchor, feats, order)

@@ -63,6 +63,54 @@ def unique_device(x, with_counts=False):
     return y, idx, cnt, u
 
 
+def _koff_array(koff):
+    import ctypes as C
+    return (C.c_int64 * len(koff))(*[int(k) for k in koff])
+
+
+def unique_grouped(keys, koff, with_counts=False):
+    """Grouped first-occurrence unique of T features in one pass.
+
+    keys: concatenated [sum n_t] int64; koff: host offsets (T+1).  Returns
+    (uniq, idx, counts or None, num_unique[T] int64 device); feature t's
+    uniques are uniq[koff[t] : koff[t] + num_unique[t]], idx is feature-local."""
+    dev = _dev(keys)
+    k = _c(keys, torch.int64)
+    n = k.numel()
+    T = len(koff) - 1
+    ka = _koff_array(koff)
+    y = torch.empty(n, dtype=torch.int64, device=dev)
+    idx = torch.empty(n, dtype=torch.int32, device=dev)
+    cnt = torch.empty(n, dtype=torch.int32, device=dev) if with_counts else None
+    u = torch.empty(T, dtype=torch.int64, device=dev)
+    wsb = lib().dr_unique_grouped_workspace_size(ka, T)
+    ws = workspace(wsb, dev)
+    check(lib().dr_unique_grouped(ptr(k), ka, T, ptr(y), ptr(idx), ptr(cnt), ptr(u), ptr(ws), wsb,
+                                  stream_handle(dev)))
+    _post(dev)
+    return y, idx, cnt, u
+
+
+def route_by_owner(uniq, koff, num_unique, world):
+    """(owner, feature)-blocked send order of a grouped unique: returns
+    (keys_send, tags_send, perm, counts[world, T]) with only the first
+    counts.sum() entries meaningful."""
+    dev = _dev(uniq)
+    n = uniq.numel()
+    T = len(koff) - 1
+    ka = _koff_array(koff)
+    keys = torch.empty(n, dtype=torch.int64, device=dev)
+    tags = torch.empty(n, dtype=torch.int32, device=dev)
+    perm = torch.empty(n, dtype=torch.int32, device=dev)
+    counts = torch.empty((world, T), dtype=torch.int64, device=dev)
+    wsb = lib().dr_route_workspace_size(n, world, T)
+    ws = workspace(wsb, dev)
+    check(lib().dr_route_by_owner(ptr(uniq), ka, T, ptr(num_unique), world, ptr(keys), ptr(tags),
+                                  ptr(perm), ptr(counts), ptr(ws), wsb, stream_handle(dev)))
+    _post(dev)
+    return keys, tags, perm, counts
+
+
 def unique(x, out_idx=torch.int32):
     """tf.unique: (y, idx), y in first-occurrence order (syncs for |y|)."""
     y, idx, _, u = unique_device(x)

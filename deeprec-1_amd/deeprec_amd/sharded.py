@@ -1,0 +1,142 @@
+"""Row-sharded embedding lookup across the GPUs of one node.
+
+Every rank holds, for each of the T features, the EV shard of the keys it
+owns (owner = key % world, the reference's EV partition rule
+key % 1000 % world for world | 1000, embedding_ops.py:207-209, and SOK's
+key % G, all2all_input_dispatcher.cu:74).  One forward step:
+
+  1. grouped first-occurrence dedup of the local batch (all features, one pass)
+  2. route: stable (owner, feature)-blocked ordering of the uniques
+  3. counts all-to-all (world x T int64), one host read of the split sizes
+     (SOK syncs here too, all2all_input_dispatcher.cu:256-268)
+  4. keys all-to-all (int64)                         -- RCCL over xGMI
+  5. owner: tagged insert-on-miss resolve + row pack of the received keys
+  6. rows all-to-all back (D fp32 per unique key)     -- RCCL over xGMI
+  7. requester: fused gather+pool straight from the received rows
+     (rowsel[perm[j]] = j), reference association order
+
+Parity: the per-bag reduction order is fixed by position within the bag,
+never by arrival rank, so the G-GPU output equals the 1-GPU output bit for
+bit.  The local steps go through a backend object so the exchange protocol
+can be exercised on CPU with world_size-2 gloo (tests/); the product
+backend is HipLocal (HIP kernels through the C ABI).
+"""
+import ctypes as C
+
+import torch
+import torch.distributed as dist
+
+from . import _lib, ops
+from ._lib import COMBINERS, ORDER_ALI, DrPoolDesc, check, lib, ptr, stream_handle, workspace
+
+
+class HipLocal(object):
+    """Local engine steps on the GPU (the product backend)."""
+
+    def __init__(self, evs, device):
+        self.evs = evs
+        self.device = device
+        self.T = len(evs)
+        self.dim = evs[0].dim
+        self.handles = (C.c_void_p * self.T)(*[e.handle.value for e in evs])
+        self.filter = any(e.filter_freq != 0 for e in evs)
+
+    def unique_grouped(self, vals, koff):
+        return ops.unique_grouped(vals, koff, self.filter)
+
+    def route(self, uniq, koff, num_unique, world):
+        return ops.route_by_owner(uniq, koff, num_unique, world)
+
+    def resolve_pack(self, keys, tags, n):
+        """Owner side: insert-on-miss resolve + row pack of n received keys."""
+        rows = torch.empty(n, dtype=torch.int64, device=self.device)
+        out = torch.empty((n, self.dim), dtype=torch.float32, device=self.device)
+        if n == 0:
+            return out
+        wsb = lib().dr_ev_resolve_workspace_size(n)
+        ws = workspace(wsb, self.device)
+        st = stream_handle(self.device)
+        check(lib().dr_ev_resolve_tagged(self.handles, self.T, ptr(keys), ptr(tags), n, None, None,
+                                         ptr(rows), ptr(ws), wsb, st))
+        check(lib().dr_ev_gather_tagged(self.handles, self.T, ptr(tags), ptr(rows), n, None,
+                                        ptr(out), st))
+        ops._post(self.device)
+        return out
+
+    def pool(self, rows_recv, rowsel, idx, koff, bag_offs, batch, combiner):
+        T, D = self.T, self.dim
+        out = torch.empty((batch, T * D), dtype=torch.float32, device=self.device)
+        descs = []
+        for t in range(T):
+            d = DrPoolDesc()
+            d.pool = rows_recv.data_ptr()
+            d.idx = idx.data_ptr() + 4 * koff[t]
+            d.rows = rowsel.data_ptr() + 8 * koff[t]
+            d.default_rows = rows_recv.data_ptr()
+            d.default_stride = 0
+            d.bag_off = bag_offs[t].data_ptr()
+            d.out = out.data_ptr() + 4 * t * D
+            d.out_stride = T * D
+            d.combiner = COMBINERS[combiner]
+            d.max_norm = -1.0
+            descs.append(d)
+        ops.pool_grouped(descs, batch, D, ORDER_ALI, self.device)
+        return out
+
+
+class ShardedLookup(object):
+    """All-to-all row-sharded embedding_lookup_sparse over T features."""
+
+    def __init__(self, evs, world, rank, batch, device, backend=None, group=None):
+        self.evs = evs
+        self.world = world
+        self.rank = rank
+        self.batch = batch
+        self.device = device
+        self.T = len(evs)
+        self.dim = evs[0].dim if evs else 0
+        self.group = group
+        self.backend = backend or HipLocal(evs, device)
+        self.last_stats = {}
+
+    def _a2a(self, out, inp, out_splits=None, in_splits=None):
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+        return out
+
+    def forward(self, ids, bag_offs=None, combiner="sum"):
+        """ids: [T, nnz] keys (hotness 1 when bag_offs is None: bag b = id b)."""
+        T, G, be = self.T, self.world, self.backend
+        dev = ids.device
+        nnz = ids.shape[1]
+        vals = ids.reshape(-1)
+        koff = [t * nnz for t in range(T + 1)]
+        uniq, idx, _cnt, U = be.unique_grouped(vals, koff)
+        keys_s, tags_s, perm, counts = be.route(uniq, koff, U, G)
+        # 3. counts exchange (peer-major [G, T]) and one host read of the splits
+        recv_counts = torch.empty_like(counts)
+        self._a2a(recv_counts.view(-1), counts.view(-1))
+        both = torch.cat([counts.view(-1), recv_counts.view(-1)]).cpu()
+        sc = both[:G * T].view(G, T)
+        rc = both[G * T:].view(G, T)
+        send_splits = sc.sum(1).tolist()
+        recv_splits = rc.sum(1).tolist()
+        S, R = int(sum(send_splits)), int(sum(recv_splits))
+        # 4. keys all-to-all
+        keys_r = torch.empty(R, dtype=torch.int64, device=dev)
+        self._a2a(keys_r, keys_s[:S], recv_splits, send_splits)
+        tags_r = torch.repeat_interleave(
+            torch.arange(T, dtype=torch.int32, device=dev).repeat(G),
+            recv_counts.view(-1), output_size=R)
+        # 5. owner resolve + pack, 6. rows all-to-all back
+        rows_s = be.resolve_pack(keys_r, tags_r, R)
+        rows_r = torch.empty((S, self.dim), dtype=torch.float32, device=dev)
+        self._a2a(rows_r, rows_s, send_splits, recv_splits)
+        # 7. requester: unique position -> row in the received buffer, pool
+        rowsel = torch.zeros(T * nnz, dtype=torch.int64, device=dev)
+        rowsel[perm[:S].to(torch.int64)] = torch.arange(S, dtype=torch.int64, device=dev)
+        if bag_offs is None:
+            off = torch.arange(self.batch + 1, dtype=torch.int32, device=dev)
+            bag_offs = [off] * T
+        out = be.pool(rows_r, rowsel, idx, koff, bag_offs, self.batch, combiner)
+        self.last_stats = {"sent_keys": S, "recv_keys": R}
+        return out

@@ -67,6 +67,13 @@ size_t dr_unique_workspace_size(int64_t n);
 int dr_unique(const int64_t* keys, int64_t n, int64_t* uniq_out, int32_t* idx_out,
               int32_t* counts_out /* nullable */, int64_t* num_unique,
               void* ws, size_t ws_bytes, void* stream);
+/* The same for T features in one pass: feature t owns keys                 */
+/* [koff_host[t], koff_host[t+1]); its uniques / counts are written at the  */
+/* same offset, idx is feature-local, num_unique[t] (DEVICE) = U_t.         */
+size_t dr_unique_grouped_workspace_size(const int64_t* koff_host, int num_tables);
+int dr_unique_grouped(const int64_t* keys, const int64_t* koff_host, int num_tables,
+                      int64_t* uniq_out, int32_t* idx_out, int32_t* counts_out,
+                      int64_t* num_unique, void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Stable radix sort of (uint64 key, int32 value) pairs on bits [lo, hi).    */
@@ -215,8 +222,22 @@ int dr_ev_resolve_grouped(dr_ev* const* evs, int num_tables, const int64_t* keys
                           const int64_t* koff_host, const int64_t* const* n_dev_per_table,
                           const int32_t* counts, int64_t* rows_out, void* ws, size_t ws_bytes,
                           void* stream);
+/* Tagged resolve (owner side of the sharded exchange): keys of all T EVs  */
+/* (equal dim) in one array, table of key i = tags[i]; n_dev: optional      */
+/* DEVICE count.  Filtered keys give -(i+1) (read table t's default row).   */
+int dr_ev_resolve_tagged(dr_ev* const* evs, int num_tables, const int64_t* keys,
+                         const int32_t* tags, int64_t n, const int64_t* n_dev,
+                         const int32_t* counts, int64_t* rows_out, void* ws, size_t ws_bytes,
+                         void* stream);
+/* Owner-side row pack: out[i] = resolved row of key i of table tags[i]     */
+/* (the table's default row when filtered).                                  */
+int dr_ev_gather_tagged(dr_ev* const* evs, int num_tables, const int32_t* tags,
+                        const int64_t* rows, int64_t n, const int64_t* n_dev, float* out,
+                        void* stream);
 /* Value-pool base of this EV's column (primary or slot).                   */
 const float* dr_ev_pool(dr_ev* ev);
+/* Device pointer of this EV's default row (dim floats).                    */
+const float* dr_ev_default_row(dr_ev* ev);
 
 /* KvResourceGather (counts == NULL) / KvResourceGatherV1.                   */
 size_t dr_ev_gather_workspace_size(int64_t n);
@@ -284,6 +305,16 @@ size_t dr_partition_workspace_size(int64_t n);
 int dr_partition_by_owner(const int64_t* keys, int64_t n, const int64_t* n_dev, int world,
                           int64_t* keys_out, int32_t* perm_out, int64_t* send_counts,
                           void* ws, size_t ws_bytes, void* stream);
+/* Request routing of a grouped unique (dr_unique_grouped layout): the      */
+/* valid uniques of all T features are stably ordered by (owner, feature),  */
+/* owner = key % world, giving the [peer][feature]-blocked send buffer of    */
+/* the key all-to-all: keys_out/tags_out (feature id)/perm_out (source      */
+/* position) and counts[world * T] (DEVICE int64, peer-major).               */
+size_t dr_route_workspace_size(int64_t n, int world, int num_tables);
+int dr_route_by_owner(const int64_t* uniq, const int64_t* koff_host, int num_tables,
+                      const int64_t* num_unique, int world, int64_t* keys_out,
+                      int32_t* tags_out, int32_t* perm_out, int64_t* counts, void* ws,
+                      size_t ws_bytes, void* stream);
 /* Row exchange helpers: dst[perm[j]] = src[j] (scatter back) / dst[j] =     */
 /* src[perm[j]] (pack), rows of `dim` floats; n_dev optional.                */
 int dr_rows_scatter(const float* src, const int32_t* perm, int64_t n, const int64_t* n_dev,

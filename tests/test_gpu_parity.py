@@ -145,6 +145,67 @@ def test_unique_bitexact(ops, orc, n, lo, hi):
     np.testing.assert_array_equal(H(cnt), rcnt)
 
 
+def test_unique_grouped_bitexact(ops, orc):
+    rng = np.random.default_rng(77)
+    sizes = [0, 1, 500, 3000, 17, 40000]
+    parts = [rng.integers(-2, 50 + 7 * s, s).astype(np.int64) for s in sizes]
+    koff = np.concatenate([[0], np.cumsum(sizes)]).tolist()
+    y, idx, cnt, U = ops.unique_grouped(T(np.concatenate(parts)), koff, with_counts=True)
+    y, idx, cnt, U = H(y), H(idx), H(cnt), H(U)
+    for t, x in enumerate(parts):
+        ry, ridx, rcnt = orc.unique(x, with_counts=True)
+        assert U[t] == ry.shape[0]
+        a = koff[t]
+        np.testing.assert_array_equal(y[a:a + U[t]], ry)
+        np.testing.assert_array_equal(idx[a:koff[t + 1]], ridx)
+        np.testing.assert_array_equal(cnt[a:a + U[t]], rcnt)
+
+
+def test_route_by_owner(ops):
+    rng = np.random.default_rng(78)
+    sizes = [1000, 0, 2500, 300]
+    parts = [rng.integers(0, 10 ** 6, s).astype(np.int64) for s in sizes]
+    koff = np.concatenate([[0], np.cumsum(sizes)]).tolist()
+    y, idx, cnt, U = ops.unique_grouped(T(np.concatenate(parts)), koff)
+    for world in (1, 2, 8):
+        keys, tags, perm, counts = ops.route_by_owner(y, koff, U, world)
+        counts = H(counts)
+        exp_k, exp_t = [], []
+        Uh, yh = H(U), H(y)
+        for p in range(world):
+            for t in range(len(sizes)):
+                u = yh[koff[t]:koff[t] + Uh[t]]
+                sel = u[u % world == p]
+                assert counts[p, t] == sel.shape[0]
+                exp_k.append(sel)
+                exp_t.append(np.full(sel.shape[0], t))
+        m = int(counts.sum())
+        np.testing.assert_array_equal(H(keys)[:m], np.concatenate(exp_k))
+        np.testing.assert_array_equal(H(tags)[:m], np.concatenate(exp_t))
+        np.testing.assert_array_equal(yh[H(perm)[:m]], np.concatenate(exp_k))
+
+
+def test_multi_feature_grouped_lookup(dr, orc):
+    rng = np.random.default_rng(79)
+    B, D, F = 300, 32, 5
+    evs, oevs, sps, raw = [], [], [], []
+    for f in range(F):
+        evs.append(dr.EmbeddingVariable("mf%d" % f, D, 0.1 * (f + 1)))
+        oevs.append(orc.EV(D, 0.1 * (f + 1)))
+        keys = np.arange(100 * f, 100 * f + 80, dtype=np.int64)
+        vals = rng.standard_normal((80, D)).astype(np.float32)
+        evs[-1].insert(T(keys), T(vals))
+        oevs[-1].insert(keys, vals)
+        ind, v = _random_sparse(rng, B, 4, 100 * f + 160)
+        sps.append(dr.SparseTensor(T(ind), T(v), (B, 4)))
+        raw.append((ind, v))
+    out = H(dr.embedding_lookup_sparse_multi(evs, sps, combiner="mean"))
+    for f in range(F):
+        ref = orc.embedding_lookup_sparse(oevs[f], raw[f][0], raw[f][1], B, combiner="mean")
+        np.testing.assert_array_equal(out[:, f * D:(f + 1) * D], ref)
+        assert int(evs[f].total_count()[0]) == oevs[f].size()
+
+
 def test_sort_pairs_stable(ops):
     rng = np.random.default_rng(3)
     n = 100003
