@@ -392,26 +392,41 @@ struct InitGroup {
   const int32_t* tags;
 };
 
+// Wave-cooperative: each lane tests one key's flag, the wave ballots and then
+// copies every flagged row with all 64 lanes.  In steady state (no new keys)
+// this is one coalesced byte load per key.
 __global__ void ev_init_rows_kernel(InitGroup g, int T, int64_t dim,
                                     const int64_t* __restrict__ rows,
                                     const uint8_t* __restrict__ init) {
-  const int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
-  if (i >= g.koff[T]) return;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  bool need = false;
   int t = 0;
   int64_t li = i;
-  if (g.tags) {
-    if (g.n_dev[0] && i >= *g.n_dev[0]) return;
-    t = g.tags[i];
-  } else {
-    while (t + 1 < T && i >= g.koff[t + 1]) ++t;
-    li = i - g.koff[t];
-    if (g.n_dev[t] && li >= *g.n_dev[t]) return;
+  if (i < g.koff[T]) {
+    bool live = true;
+    if (g.tags) {
+      if (g.n_dev[0] && i >= *g.n_dev[0]) live = false;
+      else t = g.tags[i];
+    } else {
+      while (t + 1 < T && i >= g.koff[t + 1]) ++t;
+      li = i - g.koff[t];
+      if (g.n_dev[t] && li >= *g.n_dev[t]) live = false;
+    }
+    need = live && init[i];
   }
-  if (!init[i]) return;
-  const int64_t row = rows[i];
-  const float* src = g.src[t] ? g.src[t] + li * dim : g.dflt[t];
-  float* dst = g.pool[t] + row * dim;
-  for (int64_t c = threadIdx.x % 64; c < dim; c += 64) dst[c] = src[c];
+  uint64_t mask = __ballot(need);
+  while (mask) {
+    const int src_lane = __ffsll((unsigned long long)mask) - 1;
+    mask &= mask - 1;
+    const int tt = __shfl(t, src_lane, 64);
+    const int64_t ll = __shfl(li, src_lane, 64);
+    const int64_t ii = __shfl(i, src_lane, 64);
+    const int64_t row = rows[ii];
+    const float* src = g.src[tt] ? g.src[tt] + ll * dim : g.dflt[tt];
+    float* dst = g.pool[tt] + row * dim;
+    for (int64_t c = lane; c < dim; c += 64) dst[c] = src[c];
+  }
 }
 
 // Copy-out for dr_ev_gather: out[i] = row >= 0 ? pool[row] : default(i).
@@ -867,7 +882,7 @@ static int resolve_grouped(dr_ev* const* evs, int T, const int64_t* keys, const 
                      rows_out, w.init, w.badd, stw);
   if (any_bloom)
     hipLaunchKernelGGL(ev_bloom_add_kernel, dim3(blocks), dim3(256), 0, st, g, T, keys, w.badd);
-  hipLaunchKernelGGL(ev_init_rows_kernel, dim3((unsigned)ceil_div(total, 4)), dim3(256), 0, st, ig,
+  hipLaunchKernelGGL(ev_init_rows_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, st, ig,
                      T, evs[0]->sh->dim, rows_out, w.init);
   DR_LAUNCH_CHECK();
   for (int t = 0; t < T; ++t) post_call(evs[t]->sh, st);
@@ -1166,7 +1181,7 @@ int dr_ev_insert(dr_ev* ev, const int64_t* keys, int64_t n, const float* values,
   ig.dflt[0] = ev->sh->defaults[ev->col];
   ig.koff[0] = 0;
   ig.koff[1] = n;
-  hipLaunchKernelGGL(ev_init_rows_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, ig, 1,
+  hipLaunchKernelGGL(ev_init_rows_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, ig, 1,
                      ev->sh->dim, rows, init);
   DR_LAUNCH_CHECK();
   DR_HIP(hipFreeAsync(rows, st));

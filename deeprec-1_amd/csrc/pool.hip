@@ -73,6 +73,8 @@ __device__ __forceinline__ const float* select_row(const dr_pool_desc& d, int64_
   int64_t r;
   if (d.ids) {
     r = d.ids[k];
+    // pre-resolved EV rows (dr_rows_per_nnz): negative = filtered -> default
+    if (r < 0 && d.default_rows) return d.default_rows + (-r - 1) * d.default_stride;
   } else if (!d.rows) {
     r = d.idx[k];
   } else {
@@ -349,6 +351,55 @@ __global__ void bag_offsets_kernel(const TI* __restrict__ seg, int64_t stride, i
     for (int64_t r = s + 1; r <= B; ++r) off[r] = (int32_t)ne;
 }
 
+// Grouped form: blockIdx.y = feature.
+struct BagGroup {
+  const int64_t* seg[DR_MAX_GROUP];
+  int64_t stride[DR_MAX_GROUP];
+  int64_t n[DR_MAX_GROUP];
+  int32_t* off[DR_MAX_GROUP];
+};
+
+__global__ void bag_offsets_grouped_kernel(BagGroup g, int64_t B, int* st) {
+  const int t = blockIdx.y;
+  const int64_t ne = g.n[t];
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > ne) return;
+  const int64_t* seg = g.seg[t];
+  const int64_t stride = g.stride[t];
+  int32_t* off = g.off[t];
+  if (ne == 0) {
+    for (int64_t r = k; r <= B; r += blockDim.x) off[r] = 0;
+    return;
+  }
+  if (k == ne) return;
+  int64_t s = seg[k * stride];
+  const int64_t prev = k > 0 ? seg[(k - 1) * stride] : -1;
+  if (s < prev || s < 0 || s >= B) {
+    latch(st, DR_INVALID_ARGUMENT);
+    s = s < 0 ? 0 : (s >= B ? B - 1 : s);
+    if (s < prev) return;
+  }
+  for (int64_t r = prev + 1; r <= s; ++r) off[r] = (int32_t)k;
+  if (k == ne - 1)
+    for (int64_t r = s + 1; r <= B; ++r) off[r] = (int32_t)ne;
+}
+
+// rowsel[i] = rows[koff[t] + idx[i]] for i in feature t: the EV row of every
+// nnz, resolved once so the pool kernel's load chain is bag_off -> row id ->
+// row data (one dependent load fewer).
+struct KoffGroup {
+  int64_t koff[DR_MAX_GROUP + 1];
+};
+
+__global__ void rows_per_nnz_kernel(KoffGroup g, int T, const int64_t* __restrict__ rows,
+                                    const int32_t* __restrict__ idx, int64_t* __restrict__ rowsel) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.koff[T]) return;
+  int t = 0;
+  while (t + 1 < T && i >= g.koff[t + 1]) ++t;
+  rowsel[i] = rows[g.koff[t] + idx[i]];
+}
+
 template <class TI>
 static int launch_bag_offsets(const TI* seg, int64_t stride, int64_t n, const int64_t* n_dev,
                               int64_t B, int32_t* off, hipStream_t s) {
@@ -610,6 +661,45 @@ int dr_bag_offsets(const int64_t* seg, int64_t n, int64_t batch, int32_t* bag_of
 int dr_bag_offsets_i32(const int32_t* seg, int64_t n, int64_t batch, int32_t* bag_off,
                        void* stream) {
   return dr::launch_bag_offsets<int32_t>(seg, 1, n, nullptr, batch, bag_off, dr::S(stream));
+}
+
+int dr_bag_offsets_grouped(const int64_t* const* seg, const int64_t* stride,
+                           const int64_t* n, int num_tables, int64_t batch,
+                           int32_t* const* bag_off, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(num_tables >= 1 && num_tables <= DR_MAX_GROUP, DR_INVALID_ARGUMENT,
+             "bad table count");
+  int* st = status_word();
+  DR_REQUIRE(st, DR_INTERNAL, "status word unavailable");
+  BagGroup g;
+  memset(&g, 0, sizeof(g));
+  int64_t mx = 0;
+  for (int t = 0; t < num_tables; ++t) {
+    g.seg[t] = seg[t];
+    g.stride[t] = stride[t];
+    g.n[t] = n[t];
+    g.off[t] = bag_off[t];
+    mx = n[t] > mx ? n[t] : mx;
+  }
+  dim3 grid((unsigned)ceil_div(mx + 1, 256), (unsigned)num_tables);
+  hipLaunchKernelGGL(bag_offsets_grouped_kernel, grid, dim3(256), 0, S(stream), g, batch, st);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_rows_per_nnz(const int64_t* rows, const int32_t* idx, const int64_t* koff_host,
+                    int num_tables, int64_t* rowsel, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(num_tables >= 1 && num_tables <= DR_MAX_GROUP, DR_INVALID_ARGUMENT,
+             "bad table count");
+  KoffGroup g;
+  for (int t = 0; t <= num_tables; ++t) g.koff[t] = koff_host[t];
+  const int64_t n = koff_host[num_tables];
+  if (n == 0) return DR_OK;
+  hipLaunchKernelGGL(rows_per_nnz_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0,
+                     S(stream), g, num_tables, rows, idx, rowsel);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
 }
 
 // Strided variant for sp_indices[:, 0] (stride 2), used by the fused ops.

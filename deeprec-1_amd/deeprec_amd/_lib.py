@@ -80,6 +80,8 @@ SIGNATURES = {
     "dr_bag_offsets": (_I32, [_P, _I64, _I64, _P, _P]),
     "dr_bag_offsets_i32": (_I32, [_P, _I64, _I64, _P, _P]),
     "dr_bag_offsets_strided": (_I32, [_P, _I64, _I64, _I64, _P, _P]),
+    "dr_bag_offsets_grouped": (_I32, [_P, _P, _P, _I32, _I64, _P, _P]),
+    "dr_rows_per_nnz": (_I32, [_P, _P, _P, _I32, _P, _P]),
     "dr_pool_grad_workspace_size": (_SZ, [_I64]),
     "dr_pool_grad": (_I32, [_P, _I64, _I64, _I32, _P, _P, _P, _I64, _P, _I32, _P, _P, _SZ, _P]),
     "dr_ev_create": (_I32, [_P, _P, _P]),

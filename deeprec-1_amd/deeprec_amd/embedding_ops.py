@@ -63,23 +63,61 @@ def _ev_default_dev(ev):
 
 
 class _Feature(object):
-    """One feature's prepared lookup (everything the pool kernel needs)."""
+    """One feature's prepared lookup (everything the pool kernel needs).
+
+    seg: sorted segment ids -- an int32/int64 vector, or the [nnz, 2] int64
+    sp_ids.indices (read in place, stride 2: no per-step conversion)."""
 
     def __init__(self, params, values, seg, batch, weights, combiner, max_norm):
         self.params = params
         self.values = values
-        self.seg = seg
+        if seg.dim() == 2:
+            self.seg64, self.seg_stride = seg.contiguous(), seg.shape[1]
+        elif seg.dtype == torch.int64:
+            self.seg64, self.seg_stride = seg.contiguous(), 1
+        else:
+            self.seg64, self.seg_stride = seg.to(torch.int64).contiguous(), 1
+        self._seg32 = seg if seg.dim() == 1 and seg.dtype == torch.int32 else None
         self.batch = batch
         self.weights = weights
         self.combiner = combiner
         self.max_norm = max_norm
-        self.uniq = self.idx = self.U = self.rows = None
+        self.uniq = self.idx = self.U = self.rows = self.rowsel = None
         self.defaults = None
+
+    @property
+    def seg(self):
+        """int32 segment ids (embedding_ops.py:587-589), built on demand."""
+        if self._seg32 is None:
+            s = self.seg64 if self.seg_stride == 1 else self.seg64[:, 0]
+            self._seg32 = s.to(torch.int32).contiguous()
+        return self._seg32
+
+
+def _bag_offsets_all(feats):
+    """CSR bag offsets of every feature in one launch."""
+    import ctypes as C
+    T = len(feats)
+    dev = feats[0].values.device
+    offs = [torch.empty(f.batch + 1, dtype=torch.int32, device=dev) for f in feats]
+    B = feats[0].batch
+    if any(f.batch != B for f in feats) or T > _lib.MAX_GROUP:
+        for f, o in zip(feats, offs):
+            f.bag_off = ops.bag_offsets(f.seg64 if f.seg_stride == 1 else f.seg, f.batch)
+        return
+    segs = (C.c_void_p * T)(*[f.seg64.data_ptr() for f in feats])
+    strides = (C.c_int64 * T)(*[f.seg_stride for f in feats])
+    ns = (C.c_int64 * T)(*[f.values.numel() for f in feats])
+    outs = (C.c_void_p * T)(*[o.data_ptr() for o in offs])
+    check(lib().dr_bag_offsets_grouped(segs, strides, ns, T, B, outs, stream_handle(dev)))
+    ops._post(dev)
+    for f, o in zip(feats, offs):
+        f.bag_off = o
 
 
 def _prepare(f, need_unique):
     dev = f.values.device
-    f.bag_off = ops.bag_offsets(f.seg, f.batch)
+    _bag_offsets_all([f])
     p = f.params
     if isinstance(p, EmbeddingVariable):
         with_counts = p.filter_freq != 0          # embedding_ops.py:592-596
@@ -93,7 +131,13 @@ def _prepare(f, need_unique):
 def _desc(f, out, out_stride):
     d = DrPoolDesc()
     p = f.params
-    if isinstance(p, EmbeddingVariable):
+    if isinstance(p, EmbeddingVariable) and f.rowsel is not None:
+        d.pool = p.pool()
+        d.pool_rows = 1 << 62
+        d.ids = ptr(f.rowsel)                      # pre-resolved row per nnz
+        d.default_rows = ptr(_ev_default_dev(p))
+        d.default_stride = 0
+    elif isinstance(p, EmbeddingVariable):
         d.pool = p.pool()
         d.pool_rows = 0
         d.idx = ptr(f.idx)
@@ -187,12 +231,16 @@ def _prepare_group(feats):
     ws = workspace(wsb, dev)
     check(lib().dr_ev_resolve_grouped(handles, T, ptr(uniq), ops._koff_array(koff), ndev, ptr(cnt),
                                       ptr(rows), ptr(ws), wsb, stream_handle(dev)))
+    rowsel = torch.empty(koff[-1], dtype=torch.int64, device=dev)
+    check(lib().dr_rows_per_nnz(ptr(rows), ptr(idx), ops._koff_array(koff), T, ptr(rowsel),
+                                stream_handle(dev)))
     ops._post(dev)
+    _bag_offsets_all(feats)
     for t, f in enumerate(feats):
-        f.bag_off = ops.bag_offsets(f.seg, f.batch)
         f.uniq = uniq[koff[t]:koff[t + 1]]
         f.idx = idx[koff[t]:koff[t + 1]]
         f.rows = rows[koff[t]:koff[t + 1]]
+        f.rowsel = rowsel[koff[t]:koff[t + 1]]
         f.U = U[t:t + 1]
         f.defaults = None
 
@@ -237,8 +285,12 @@ def _pool_all(feats, order):
 
 
 def _seg_of(sp_ids):
-    # segment_ids = sp_ids.indices[:, 0] cast to int32 (embedding_ops.py:587-589)
-    return sp_ids.indices[:, 0].to(torch.int32).contiguous()
+    # segment_ids = sp_ids.indices[:, 0] (embedding_ops.py:587-589), read in
+    # place from the [nnz, 2] indices; the int32 cast happens on demand.
+    ind = sp_ids.indices
+    if ind.dtype != torch.int64:
+        ind = ind.to(torch.int64)
+    return ind.contiguous()
 
 
 def embedding_lookup_sparse(params, sp_ids, sp_weights=None, partition_strategy="mod", name=None,
@@ -314,7 +366,7 @@ def embedding_lookup(params, ids, partition_strategy="mod", name=None, max_norm=
 def _partitioned_lookup_sparse(params, sp_ids, sp_weights, partition_strategy, combiner,
                                max_norm):
     values = sp_ids.values.to(torch.int64)
-    seg = _seg_of(sp_ids)
+    seg = sp_ids.indices[:, 0].to(torch.int32).contiguous()
     B = sp_ids.dense_shape[0]
     if isinstance(params[0], EmbeddingVariable) and params[0].filter_freq == 0:
         uniq, idx = ops.unique(values)

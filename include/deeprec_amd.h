@@ -161,6 +161,15 @@ int dr_bag_offsets(const int64_t* seg, int64_t n, int64_t batch, int32_t* bag_of
                    void* stream);
 int dr_bag_offsets_i32(const int32_t* seg, int64_t n, int64_t batch, int32_t* bag_off,
                        void* stream);
+/* Grouped over T features in one launch (seg[t] read with stride[t]).      */
+int dr_bag_offsets_grouped(const int64_t* const* seg, const int64_t* stride,
+                           const int64_t* n, int num_tables, int64_t batch,
+                           int32_t* const* bag_off, void* stream);
+/* rowsel[i] = rows[koff[t] + idx[i]] for nnz i of feature t (grouped-unique */
+/* layout): pre-resolves every nnz to its EV row for dr_pool_grouped (set   */
+/* desc.ids = rowsel, desc.default_rows for negative = filtered rows).       */
+int dr_rows_per_nnz(const int64_t* rows, const int32_t* idx, const int64_t* koff_host,
+                    int num_tables, int64_t* rowsel, void* stream);
 /* Same over sp_indices[:, 0] read with a stride (2 for [nnz, 2] indices).   */
 int dr_bag_offsets_strided(const int64_t* seg, int64_t stride, int64_t n, int64_t batch,
                            int32_t* bag_off, void* stream);
