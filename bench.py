@@ -208,8 +208,9 @@ def main():
     from deeprec_amd.embedding_ops import _Feature, _prepare_group, _pool_all
     static_ids.copy_(batches[0])
     with torch.no_grad():
-        feats = [_Feature(evs[t], static_ids[t], seg, B, None, "sum", None) for t in range(T)]
-        _prepare_group(feats)
+        feats = [_Feature(evs[t], static_ids[t], seg, B, None, "sum", None, onehot=True)
+                 for t in range(T)]
+        _prepare_group(feats, need_grad=False)
         _pool_all(feats, _lib.ORDER_ALI)
         torch.cuda.synchronize()
         e0 = torch.cuda.Event(enable_timing=True)
@@ -225,7 +226,7 @@ def main():
     achieved = bytes_launch / (k_ms * 1e-3) / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
-            "kernel": "dr::pool_grouped_kernel<4,32,1,ALI,4>", "kernel_ms": round(k_ms, 4),
+            "kernel": "dr::pool_onehot_kernel<4,32,1,ALI,4>", "kernel_ms": round(k_ms, 4),
             "bytes_per_launch": bytes_launch, "bytes_per_lookup": per_lookup}
     pmc = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
     if os.path.exists(pmc):

@@ -56,7 +56,7 @@ struct Carver {
   }
 };
 
-inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline int64_t next_pow2(int64_t x) {
   int64_t c = 1;
   while (c < x) c <<= 1;

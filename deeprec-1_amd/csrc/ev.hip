@@ -180,6 +180,11 @@ __device__ Slot* ev_find(const EvDesc& e, uint64_t key, bool insert, bool* creat
       h = (h + 1) & mask;
     }
   }
+  // The creator publishes the row BEFORE any lane waits for one: with
+  // duplicate keys in one call, creator and waiter can share a wavefront,
+  // and a divergent spin ahead of the creator's store would never end
+  // (lanes of a wave do not progress independently).  Two sequential ifs
+  // reconverge in between, so the store is issued first.
   if (*created) {
     const int64_t row = (int64_t)atomicAdd((unsigned long long*)e.top, 1ull);
     uint64_t v;
@@ -191,8 +196,9 @@ __device__ Slot* ev_find(const EvDesc& e, uint64_t key, bool insert, bool* creat
     }
     __hip_atomic_store(&s->rc, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *rc = v;
-    return s;
   }
+  __builtin_amdgcn_wave_barrier();  // convergent: keeps the two ifs apart
+  if (*created) return s;
   uint64_t v = s->rc;
   if (v == kUnset) {
     for (int spin = 0; spin < (1 << 22); ++spin) {

@@ -104,6 +104,40 @@ __device__ __forceinline__ void load_row(Row<VEC, G, CPL>& x, const float* p, in
   }
 }
 
+// Rows read exactly once per launch: nontemporal hint (no L2 retention).
+typedef float nf4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 nt_load(const float4* p) {
+  const nf4 v = __builtin_nontemporal_load(reinterpret_cast<const nf4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float nt_load(const float* p) { return __builtin_nontemporal_load(p); }
+
+template <int VEC, int G, int CPL>
+__device__ __forceinline__ void load_row_nt(Row<VEC, G, CPL>& x, const float* p, int lg, int dv) {
+  using V = typename VecT<VEC>::T;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = lg + c * G;
+    x.v[c] = (p && col < dv) ? nt_load(reinterpret_cast<const V*>(p) + col) : vzero<V>();
+  }
+}
+
+__device__ __forceinline__ void nt_store(float4 v, float4* p) {
+  nf4 w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<nf4*>(p));
+}
+__device__ __forceinline__ void nt_store(float v, float* p) { __builtin_nontemporal_store(v, p); }
+
+template <int VEC, int G, int CPL>
+__device__ __forceinline__ void store_row_nt(const Row<VEC, G, CPL>& x, float* p, int lg, int dv) {
+  using V = typename VecT<VEC>::T;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = lg + c * G;
+    if (col < dv) nt_store(x.v[c], reinterpret_cast<V*>(p) + col);
+  }
+}
+
 template <int VEC, int G, int CPL>
 __device__ __forceinline__ void store_row(const Row<VEC, G, CPL>& x, float* p, int lg, int dv) {
   using V = typename VecT<VEC>::T;
@@ -252,9 +286,96 @@ __device__ void pool_bag(const dr_pool_desc& d, int64_t b, int dim, int lg, int 
   store_row<VEC, G, CPL>(acc, out, lg, dv);
 }
 
-// Grid: one group of G lanes per (table, chunk of NB bags).
+// Pooling kernels:
+//  * pool_onehot_kernel (DR_POOL_ONEHOT: bag b is nnz b): a pure row copy in
+//    OUTPUT order -- group g covers slots j = g*NB .. g*NB+NB-1 of the [B, T]
+//    slot grid (slot j = bag j / T of table j % T), so consecutive groups
+//    write consecutive NB*D-float pieces of the [B, T*D] concat; row reads
+//    are random.  Nontemporal loads and stores (each row byte is touched once
+//    per launch).  Measured on MI355X (tools/pool_probe.py): this
+//    shape 5.08 TB/s vs 4.25 for table-major NB=8 default-policy copies.
+//  * pool_fast_kernel: without the one-hot guarantee, chunks of NB bags of one
+//    table whose bags each hold exactly one id, with no weights / clipping.
+//  * pool_general_kernel: every other chunk (multi-hot bags, weights,
+//    max_norm), replaying the reference association order.  It skips the
+//    chunks the fast kernel took, by the same predicate.
+template <int NB>
+__device__ __forceinline__ bool chunk_is_fast(const dr_pool_desc& d, int64_t b0, int64_t B,
+                                              int (&off)[NB + 1]) {
+  if (b0 + NB > B || d.weights || d.max_norm >= 0.f) return false;
+#pragma unroll
+  for (int j = 0; j <= NB; ++j) off[j] = d.bag_off[b0 + j];
+  bool fast = true;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) fast = fast && (off[j + 1] - off[j] == 1);
+  return fast;
+}
+
+template <int VEC, int G, int CPL, int ORDER>
+__device__ __forceinline__ void seq_zero_add(Row<VEC, G, CPL>& x) {
+  // fused op (ORDER_SEQ): out = 0 + e, which turns -0.0 into +0.0 exactly
+  if (ORDER == DR_ORDER_SEQ) {
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) x.v[c] = vadd(vzero<typename VecT<VEC>::T>(), x.v[c]);
+  }
+}
+
 template <int VEC, int G, int CPL, int ORDER, int NB>
-__global__ __launch_bounds__(256) void pool_grouped_kernel(PoolArgs args, int T, int64_t B,
+__global__ __launch_bounds__(256) void pool_onehot_kernel(PoolArgs args, int T, int64_t B, int dim,
+                                                          int* st) {
+  constexpr int GPB = 256 / G;
+  const int64_t slots = (int64_t)T * B;
+  const int64_t s0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * NB;
+  if (s0 >= slots) return;
+  const int lg = threadIdx.x % G;
+  const int dv = dim / VEC;
+  Row<VEC, G, CPL> x[NB];
+  float* o[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int64_t s = s0 + j;
+    const float* p = nullptr;
+    o[j] = nullptr;
+    if (s < slots) {
+      const int64_t b = s / T;
+      const dr_pool_desc& d = args.d[(int)(s - b * T)];
+      p = select_row(d, b, dim, st);
+      o[j] = d.out + b * d.out_stride;
+    }
+    load_row_nt<VEC, G, CPL>(x[j], p, lg, dv);
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    seq_zero_add<VEC, G, CPL, ORDER>(x[j]);
+    if (o[j]) store_row_nt<VEC, G, CPL>(x[j], o[j], lg, dv);
+  }
+}
+
+template <int VEC, int G, int CPL, int ORDER, int NB>
+__global__ __launch_bounds__(256) void pool_fast_kernel(PoolArgs args, int T, int64_t B, int dim,
+                                                        int64_t chunks_per_table, int* st) {
+  constexpr int GPB = 256 / G;
+  const int64_t item = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+  if (item >= (int64_t)T * chunks_per_table) return;
+  const int t = (int)(item / chunks_per_table);
+  const int64_t b0 = (item - (int64_t)t * chunks_per_table) * NB;
+  const int lg = threadIdx.x % G;
+  const int dv = dim / VEC;
+  const dr_pool_desc& d = args.d[t];
+  int off[NB + 1];
+  if (!chunk_is_fast<NB>(d, b0, B, off)) return;
+  Row<VEC, G, CPL> x[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) load_row_nt<VEC, G, CPL>(x[j], select_row(d, off[j], dim, st), lg, dv);
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    seq_zero_add<VEC, G, CPL, ORDER>(x[j]);
+    store_row_nt<VEC, G, CPL>(x[j], d.out + (b0 + j) * d.out_stride, lg, dv);
+  }
+}
+
+template <int VEC, int G, int CPL, int ORDER, int NB>
+__global__ __launch_bounds__(256) void pool_general_kernel(PoolArgs args, int T, int64_t B,
                                                            int dim, int64_t chunks_per_table,
                                                            int* st) {
   constexpr int GPB = 256 / G;
@@ -265,61 +386,61 @@ __global__ __launch_bounds__(256) void pool_grouped_kernel(PoolArgs args, int T,
   const int lg = threadIdx.x % G;
   const int dv = dim / VEC;
   const dr_pool_desc& d = args.d[t];
+  int off[NB + 1];
+  if (chunk_is_fast<NB>(d, b0, B, off)) return;  // taken by pool_fast_kernel
   int64_t nbag = B - b0;
   if (nbag > NB) nbag = NB;
-  // Fast path: every bag holds exactly one id, no weights, no clipping ->
-  // NB independent row loads in flight, then NB stores (pure row copy).
-  int off[NB + 1];
-#pragma unroll
-  for (int j = 0; j <= NB; ++j) off[j] = (j <= nbag) ? d.bag_off[b0 + j] : 0;
-  bool fast = nbag == NB && !d.weights && d.max_norm < 0.f;
-#pragma unroll
-  for (int j = 0; j < NB; ++j) fast = fast && (off[j + 1] - off[j] == 1);
-  if (fast) {
-    Row<VEC, G, CPL> x[NB];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) load_row<VEC, G, CPL>(x[j], select_row(d, off[j], dim, st), lg, dv);
-#pragma unroll
-    for (int j = 0; j < NB; ++j)
-      store_row<VEC, G, CPL>(x[j], d.out + (b0 + j) * d.out_stride, lg, dv);
-    return;
-  }
   for (int j = 0; j < nbag; ++j) pool_bag<VEC, G, CPL, ORDER>(d, b0 + j, dim, lg, dv, st);
 }
 
+enum { POOL_ONEHOT = 1 };
+static constexpr int kOneHotNB = 4;  // rows in flight per lane group (probe optimum)
+static constexpr int kChunkNB = 8;   // bags per chunk, fast/general split
+
 template <int VEC, int G, int CPL, int ORDER>
-static int launch_pool(const PoolArgs& a, int T, int64_t B, int dim, hipStream_t s, int* st) {
-  constexpr int NB = 4;
-  const int64_t cpt = ceil_div(B, NB);
-  const int64_t items = (int64_t)T * cpt;
-  const int64_t blocks = ceil_div(items, 256 / G);
-  hipLaunchKernelGGL((pool_grouped_kernel<VEC, G, CPL, ORDER, NB>), dim3((unsigned)blocks),
-                     dim3(256), 0, s, a, T, B, dim, cpt, st);
+static int launch_pool(const PoolArgs& a, int T, int64_t B, int dim, int flags, hipStream_t s,
+                       int* st) {
+  if (flags & POOL_ONEHOT) {
+    const int64_t items = ceil_div((int64_t)T * B, kOneHotNB);
+    hipLaunchKernelGGL((pool_onehot_kernel<VEC, G, CPL, ORDER, kOneHotNB>),
+                       dim3((unsigned)ceil_div(items, 256 / G)), dim3(256), 0, s, a, T, B, dim,
+                       st);
+  } else {
+    const int64_t cpt = ceil_div(B, kChunkNB);
+    const unsigned blocks = (unsigned)ceil_div((int64_t)T * cpt, 256 / G);
+    hipLaunchKernelGGL((pool_fast_kernel<VEC, G, CPL, ORDER, kChunkNB>), dim3(blocks), dim3(256),
+                       0, s, a, T, B, dim, cpt, st);
+    hipLaunchKernelGGL((pool_general_kernel<VEC, G, CPL, ORDER, kChunkNB>), dim3(blocks),
+                       dim3(256), 0, s, a, T, B, dim, cpt, st);
+  }
   DR_LAUNCH_CHECK();
   return DR_OK;
 }
 
 template <int ORDER>
-static int dispatch_pool(const PoolArgs& a, int T, int64_t B, int dim, hipStream_t s, int* st) {
+static int dispatch_pool(const PoolArgs& a, int T, int64_t B, int dim, int flags, hipStream_t s,
+                         int* st) {
+#define DR_POOL(V, G, C) return launch_pool<V, G, C, ORDER>(a, T, B, dim, flags, s, st)
   if (dim % 4 == 0) {
     const int d4 = dim / 4;
-    if (d4 <= 1) return launch_pool<4, 1, 1, ORDER>(a, T, B, dim, s, st);
-    if (d4 <= 2) return launch_pool<4, 2, 1, ORDER>(a, T, B, dim, s, st);
-    if (d4 <= 4) return launch_pool<4, 4, 1, ORDER>(a, T, B, dim, s, st);
-    if (d4 <= 8) return launch_pool<4, 8, 1, ORDER>(a, T, B, dim, s, st);
-    if (d4 <= 16) return launch_pool<4, 16, 1, ORDER>(a, T, B, dim, s, st);
-    if (d4 <= 32) return launch_pool<4, 32, 1, ORDER>(a, T, B, dim, s, st);
-    if (d4 <= 64) return launch_pool<4, 64, 1, ORDER>(a, T, B, dim, s, st);
-    if (d4 <= 128) return launch_pool<4, 64, 2, ORDER>(a, T, B, dim, s, st);
-    if (d4 <= 256) return launch_pool<4, 64, 4, ORDER>(a, T, B, dim, s, st);
+    if (d4 <= 1) DR_POOL(4, 1, 1);
+    if (d4 <= 2) DR_POOL(4, 2, 1);
+    if (d4 <= 4) DR_POOL(4, 4, 1);
+    if (d4 <= 8) DR_POOL(4, 8, 1);
+    if (d4 <= 16) DR_POOL(4, 16, 1);
+    if (d4 <= 32) DR_POOL(4, 32, 1);
+    if (d4 <= 64) DR_POOL(4, 64, 1);
+    if (d4 <= 128) DR_POOL(4, 64, 2);
+    if (d4 <= 256) DR_POOL(4, 64, 4);
   } else {
-    if (dim <= 4) return launch_pool<1, 4, 1, ORDER>(a, T, B, dim, s, st);
-    if (dim <= 8) return launch_pool<1, 8, 1, ORDER>(a, T, B, dim, s, st);
-    if (dim <= 16) return launch_pool<1, 16, 1, ORDER>(a, T, B, dim, s, st);
-    if (dim <= 32) return launch_pool<1, 32, 1, ORDER>(a, T, B, dim, s, st);
-    if (dim <= 64) return launch_pool<1, 64, 1, ORDER>(a, T, B, dim, s, st);
-    if (dim <= 256) return launch_pool<1, 64, 4, ORDER>(a, T, B, dim, s, st);
+    if (dim <= 4) DR_POOL(1, 4, 1);
+    if (dim <= 8) DR_POOL(1, 8, 1);
+    if (dim <= 16) DR_POOL(1, 16, 1);
+    if (dim <= 32) DR_POOL(1, 32, 1);
+    if (dim <= 64) DR_POOL(1, 64, 1);
+    if (dim <= 256) DR_POOL(1, 64, 4);
   }
+#undef DR_POOL
   set_error("dim %d unsupported (max 1024 fp32 / 256 unaligned)", dim);
   return DR_INVALID_ARGUMENT;
 }
@@ -435,11 +556,11 @@ __global__ __launch_bounds__(256) void gather_kernel(const float* __restrict__ t
       else
         latch(st, DR_INVALID_ARGUMENT);
     }
-    load_row<VEC, G, CPL>(x[j], p, lg, dv);
+    load_row_nt<VEC, G, CPL>(x[j], p, lg, dv);
   }
 #pragma unroll
   for (int j = 0; j < NB; ++j)
-    if (i0 + j < n) store_row<VEC, G, CPL>(x[j], out + (i0 + j) * (int64_t)dim, lg, dv);
+    if (i0 + j < n) store_row_nt<VEC, G, CPL>(x[j], out + (i0 + j) * (int64_t)dim, lg, dv);
 }
 
 template <int VEC, int G, int CPL>
@@ -628,17 +749,26 @@ extern "C" {
 
 int dr_pool_grouped(const dr_pool_desc* descs_host, int num_tables, int64_t batch, int dim,
                     int order, void* stream) {
+  return dr_pool_grouped_ex(descs_host, num_tables, batch, dim, order, 0, stream);
+}
+
+int dr_pool_grouped_ex(const dr_pool_desc* descs_host, int num_tables, int64_t batch, int dim,
+                       int order, int flags, void* stream) {
   using namespace dr;
   DR_REQUIRE(num_tables >= 1 && num_tables <= DR_MAX_GROUP, DR_INVALID_ARGUMENT,
              "num_tables must be in [1, %d]", DR_MAX_GROUP);
   DR_REQUIRE(batch >= 0 && dim > 0, DR_INVALID_ARGUMENT, "bad batch/dim");
+  DR_REQUIRE((flags & ~DR_POOL_ONEHOT) == 0, DR_INVALID_ARGUMENT, "unknown flags 0x%x", flags);
   if (batch == 0) return DR_OK;
+  const bool onehot = flags & DR_POOL_ONEHOT;
   PoolArgs a;
   memset(&a, 0, sizeof(a));
   for (int t = 0; t < num_tables; ++t) {
     const dr_pool_desc& d = descs_host[t];
-    DR_REQUIRE(d.pool && d.bag_off && d.out && (d.ids || d.idx), DR_INVALID_ARGUMENT,
-               "table %d: missing pointers", t);
+    DR_REQUIRE(d.pool && (d.bag_off || onehot) && d.out && (d.ids || d.idx),
+               DR_INVALID_ARGUMENT, "table %d: missing pointers", t);
+    DR_REQUIRE(!onehot || (!d.weights && d.max_norm < 0.f), DR_INVALID_ARGUMENT,
+               "table %d: DR_POOL_ONEHOT excludes weights and max_norm", t);
     if (dim % 4 == 0)
       DR_REQUIRE(((uintptr_t)d.pool & 15) == 0 && ((uintptr_t)d.out & 15) == 0 &&
                      d.out_stride % 4 == 0 &&
@@ -649,8 +779,9 @@ int dr_pool_grouped(const dr_pool_desc* descs_host, int num_tables, int64_t batc
   int* st = status_word();
   DR_REQUIRE(st, DR_INTERNAL, "status word unavailable");
   hipStream_t s = S(stream);
-  if (order == DR_ORDER_SEQ) return dispatch_pool<DR_ORDER_SEQ>(a, num_tables, batch, dim, s, st);
-  return dispatch_pool<DR_ORDER_ALI>(a, num_tables, batch, dim, s, st);
+  if (order == DR_ORDER_SEQ)
+    return dispatch_pool<DR_ORDER_SEQ>(a, num_tables, batch, dim, flags, s, st);
+  return dispatch_pool<DR_ORDER_ALI>(a, num_tables, batch, dim, flags, s, st);
 }
 
 int dr_bag_offsets(const int64_t* seg, int64_t n, int64_t batch, int32_t* bag_off,

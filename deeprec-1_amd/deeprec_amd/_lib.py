@@ -20,6 +20,7 @@ _CODE_NAMES = {3: "InvalidArgument", 5: "NotFound", 6: "AlreadyExists", 8: "Reso
 COMBINERS = {"sum": 0, "mean": 1, "sqrtn": 2}
 ORDER_ALI, ORDER_SEQ = 0, 1
 MAX_GROUP = 32
+POOL_ONEHOT = 1
 
 
 class DeepRecError(RuntimeError):
@@ -77,6 +78,7 @@ SIGNATURES = {
     "dr_unsorted_segment_sum_workspace_size": (_SZ, [_I64, _I64]),
     "dr_unsorted_segment_sum": (_I32, [_P, _I64, _I64, _P, _I64, _P, _P, _SZ, _P]),
     "dr_pool_grouped": (_I32, [_P, _I32, _I64, _I32, _I32, _P]),
+    "dr_pool_grouped_ex": (_I32, [_P, _I32, _I64, _I32, _I32, _I32, _P]),
     "dr_bag_offsets": (_I32, [_P, _I64, _I64, _P, _P]),
     "dr_bag_offsets_i32": (_I32, [_P, _I64, _I64, _P, _P]),
     "dr_bag_offsets_strided": (_I32, [_P, _I64, _I64, _I64, _P, _P]),

@@ -68,8 +68,12 @@ class _Feature(object):
     seg: sorted segment ids -- an int32/int64 vector, or the [nnz, 2] int64
     sp_ids.indices (read in place, stride 2: no per-step conversion)."""
 
-    def __init__(self, params, values, seg, batch, weights, combiner, max_norm):
+    def __init__(self, params, values, seg, batch, weights, combiner, max_norm, onehot=False):
         self.params = params
+        # one id per row (a valid [B, 1] SparseTensor with nnz == B): bag b is
+        # nnz b, so the pool kernel needs no bag offsets (DR_POOL_ONEHOT).
+        self.onehot = bool(onehot) and weights is None and max_norm is None
+        self.bag_off = None
         self.values = values
         if seg.dim() == 2:
             self.seg64, self.seg_stride = seg.contiguous(), seg.shape[1]
@@ -94,9 +98,17 @@ class _Feature(object):
         return self._seg32
 
 
-def _bag_offsets_all(feats):
+def _is_onehot(sp_ids, nnz):
+    return len(sp_ids.dense_shape) == 2 and sp_ids.dense_shape[1] == 1 and \
+        nnz == sp_ids.dense_shape[0]
+
+
+def _bag_offsets_all(feats, skip_onehot=False):
     """CSR bag offsets of every feature in one launch."""
     import ctypes as C
+    feats = [f for f in feats if f.bag_off is None and not (skip_onehot and f.onehot)]
+    if not feats:
+        return
     T = len(feats)
     dev = feats[0].values.device
     offs = [torch.empty(f.batch + 1, dtype=torch.int32, device=dev) for f in feats]
@@ -117,7 +129,7 @@ def _bag_offsets_all(feats):
 
 def _prepare(f, need_unique):
     dev = f.values.device
-    _bag_offsets_all([f])
+    _bag_offsets_all([f], skip_onehot=True)
     p = f.params
     if isinstance(p, EmbeddingVariable):
         with_counts = p.filter_freq != 0          # embedding_ops.py:592-596
@@ -153,7 +165,7 @@ def _desc(f, out, out_stride):
         d.pool = ptr(t)
         d.pool_rows = t.shape[0]
         d.ids = ptr(f.values)
-    d.bag_off = ptr(f.bag_off)
+    d.bag_off = None if f.bag_off is None else ptr(f.bag_off)
     d.weights = ptr(f.weights)
     d.out = out.data_ptr()
     d.out_stride = out_stride
@@ -169,6 +181,7 @@ def _grad_to_slices(f, g, top_stride):
     if f.uniq is None:
         f.uniq, f.idx, _, f.U = ops.unique_device(f.values)
     dev = g.device
+    _bag_offsets_all([f])
     n = f.values.numel()
     D = f.params.dim if not torch.is_tensor(f.params) else f.params.shape[1]
     gu = torch.empty((n, D), dtype=torch.float32, device=dev)
@@ -212,17 +225,48 @@ def _groupable(feats):
                     and f.params.dim == p0.dim and f.params.device == p0.device for f in feats))
 
 
-def _prepare_group(feats):
+def _concat_values(feats, koff):
+    """The features' ids as one vector; a view when they already sit back to
+    back in one buffer (e.g. rows of a [T, nnz] id matrix), else a copy."""
+    v0 = feats[0].values
+    if all(f.values.dtype == torch.int64 and f.values.is_contiguous()
+           and f.values.untyped_storage().data_ptr() == v0.untyped_storage().data_ptr()
+           and f.values.data_ptr() == v0.data_ptr() + 8 * koff[t] for t, f in enumerate(feats)):
+        return torch.as_strided(v0, (koff[-1],), (1,))
+    return torch.cat([f.values for f in feats])
+
+
+def _prepare_group(feats, need_grad=True):
     """All features of a step at once: one grouped unique, one grouped EV
-    resolve (insert-on-miss + filters), then per-feature bag offsets."""
+    resolve (insert-on-miss + filters), then per-feature bag offsets.
+
+    Forward-only lookups of filter-free EVs skip the Unique: every nnz is
+    resolved straight into the EV's hash table, whose CAS insert is itself
+    the dedup (LookupOrCreate is idempotent, embedding_var.h:320-339), so
+    the outputs and the EV contents equal the unique -> gather pipeline's.
+    Unique is still built when counts feed a Counter/Bloom filter or when a
+    gradient needs the unique ids (embedding_ops.py:592-596)."""
     import ctypes as C
     dev = feats[0].values.device
     T = len(feats)
     koff = [0]
     for f in feats:
         koff.append(koff[-1] + f.values.numel())
-    vals = torch.cat([f.values for f in feats])
+    vals = _concat_values(feats, koff)
     with_counts = any(f.params.filter_freq != 0 for f in feats)
+    if not with_counts and not need_grad:
+        rowsel = torch.empty(koff[-1], dtype=torch.int64, device=dev)
+        handles = (C.c_void_p * T)(*[f.params.handle.value for f in feats])
+        wsb = lib().dr_ev_resolve_workspace_size(koff[-1])
+        ws = workspace(wsb, dev)
+        check(lib().dr_ev_resolve_grouped(handles, T, ptr(vals), ops._koff_array(koff), None, None,
+                                          ptr(rowsel), ptr(ws), wsb, stream_handle(dev)))
+        ops._post(dev)
+        _bag_offsets_all(feats, skip_onehot=True)
+        for t, f in enumerate(feats):
+            f.uniq = f.idx = f.rows = f.U = f.defaults = None
+            f.rowsel = rowsel[koff[t]:koff[t + 1]]
+        return
     uniq, idx, cnt, U = ops.unique_grouped(vals, koff, with_counts)
     rows = torch.empty(koff[-1], dtype=torch.int64, device=dev)
     handles = (C.c_void_p * T)(*[f.params.handle.value for f in feats])
@@ -235,7 +279,7 @@ def _prepare_group(feats):
     check(lib().dr_rows_per_nnz(ptr(rows), ptr(idx), ops._koff_array(koff), T, ptr(rowsel),
                                 stream_handle(dev)))
     ops._post(dev)
-    _bag_offsets_all(feats)
+    _bag_offsets_all(feats, skip_onehot=True)
     for t, f in enumerate(feats):
         f.uniq = uniq[koff[t]:koff[t + 1]]
         f.idx = idx[koff[t]:koff[t + 1]]
@@ -250,7 +294,7 @@ def _run(feats, order=ORDER_ALI, need_grad=None):
     if need_grad is None:
         need_grad = torch.is_grad_enabled() and any(not torch.is_tensor(f.params) for f in feats)
     if _groupable(feats):
-        _prepare_group(feats)
+        _prepare_group(feats, need_grad)
     else:
         for f in feats:
             _prepare(f, need_unique=False)
@@ -273,12 +317,15 @@ def _pool_all(feats, order):
         j = i
         while j < len(feats) and dims[j] == dims[i] and j - i < _lib.MAX_GROUP:
             j += 1
+        onehot = all(f.onehot for f in feats[i:j])
+        if not onehot:
+            _bag_offsets_all(feats[i:j])
         descs = []
         c = col
         for f in feats[i:j]:
             descs.append(_desc(f, out[:, c:], total))
             c += dims[i]
-        ops.pool_grouped(descs, B, dims[i], order, dev)
+        ops.pool_grouped(descs, B, dims[i], order, dev, onehot=onehot)
         col = c
         i = j
     return out
@@ -308,7 +355,8 @@ def embedding_lookup_sparse(params, sp_ids, sp_weights=None, partition_strategy=
                                               combiner, max_norm)
     values = sp_ids.values.to(torch.int64).contiguous()
     w = None if sp_weights is None else sp_weights.values.to(torch.float32).contiguous()
-    f = _Feature(params, values, _seg_of(sp_ids), sp_ids.dense_shape[0], w, combiner, max_norm)
+    f = _Feature(params, values, _seg_of(sp_ids), sp_ids.dense_shape[0], w, combiner, max_norm,
+                 onehot=_is_onehot(sp_ids, values.numel()))
     return _run([f])
 
 
@@ -317,8 +365,9 @@ def embedding_lookup_sparse_multi(params_list, sp_ids_list, combiner="mean", max
     returns the input_layer concatenation [B, sum(D_t)]."""
     feats = []
     for p, sp in zip(params_list, sp_ids_list):
-        feats.append(_Feature(p, sp.values.to(torch.int64).contiguous(), _seg_of(sp),
-                              sp.dense_shape[0], None, combiner, max_norm))
+        v = sp.values.to(torch.int64).contiguous()
+        feats.append(_Feature(p, v, _seg_of(sp), sp.dense_shape[0], None, combiner, max_norm,
+                              onehot=_is_onehot(sp, v.numel())))
     return _run(feats)
 
 

@@ -232,10 +232,13 @@ def bag_offsets(segment_ids, batch):
     return off
 
 
-def pool_grouped(descs, batch, dim, order=ORDER_ALI, device=None):
-    """Launch dr_pool_grouped on a list of _lib.DrPoolDesc (<= 32 tables)."""
+def pool_grouped(descs, batch, dim, order=ORDER_ALI, device=None, onehot=False):
+    """Launch dr_pool_grouped_ex on a list of _lib.DrPoolDesc (<= 32 tables).
+    onehot: every bag b holds exactly nnz b (bag_off not read)."""
     arr = (_lib.DrPoolDesc * len(descs))(*descs)
-    check(lib().dr_pool_grouped(arr, len(descs), batch, dim, order, stream_handle(device)))
+    flags = _lib.POOL_ONEHOT if onehot else 0
+    check(lib().dr_pool_grouped_ex(arr, len(descs), batch, dim, order, flags,
+                                   stream_handle(device)))
     _post(device)
 
 

@@ -74,13 +74,13 @@ class HipLocal(object):
             d.rows = rowsel.data_ptr() + 8 * koff[t]
             d.default_rows = rows_recv.data_ptr()
             d.default_stride = 0
-            d.bag_off = bag_offs[t].data_ptr()
+            d.bag_off = None if bag_offs is None else bag_offs[t].data_ptr()
             d.out = out.data_ptr() + 4 * t * D
             d.out_stride = T * D
             d.combiner = COMBINERS[combiner]
             d.max_norm = -1.0
             descs.append(d)
-        ops.pool_grouped(descs, batch, D, ORDER_ALI, self.device)
+        ops.pool_grouped(descs, batch, D, ORDER_ALI, self.device, onehot=bag_offs is None)
         return out
 
 
@@ -134,9 +134,8 @@ class ShardedLookup(object):
         # 7. requester: unique position -> row in the received buffer, pool
         rowsel = torch.zeros(T * nnz, dtype=torch.int64, device=dev)
         rowsel[perm[:S].to(torch.int64)] = torch.arange(S, dtype=torch.int64, device=dev)
-        if bag_offs is None:
-            off = torch.arange(self.batch + 1, dtype=torch.int32, device=dev)
-            bag_offs = [off] * T
+        if bag_offs is None and nnz != self.batch:
+            raise ValueError("one-hot ids need nnz == batch (%d != %d)" % (nnz, self.batch))
         out = be.pool(rows_r, rowsel, idx, koff, bag_offs, self.batch, combiner)
         self.last_stats = {"sent_keys": S, "recv_keys": R}
         return out

@@ -153,6 +153,13 @@ typedef struct {
 
 int dr_pool_grouped(const dr_pool_desc* descs_host, int num_tables, int64_t batch,
                     int dim, int order, void* stream);
+/* Same with flags.  DR_POOL_ONEHOT: the caller guarantees bag b holds      */
+/* exactly nnz b (one id per row, nnz == batch, e.g. Criteo categorical      */
+/* features); bag_off may be NULL and is not read; weights must be NULL and  */
+/* max_norm < 0.  Results are identical to dr_pool_grouped on such input.    */
+#define DR_POOL_ONEHOT 1
+int dr_pool_grouped_ex(const dr_pool_desc* descs_host, int num_tables, int64_t batch,
+                       int dim, int order, int flags, void* stream);
 
 /* CSR bag offsets from sorted segment ids (sp_indices[:,0]):               */
 /* bag_off[s] = first k with seg[k] >= s, bag_off[B] = n.  Unsorted or out  */

@@ -185,12 +185,15 @@ def test_route_by_owner(ops):
         np.testing.assert_array_equal(yh[H(perm)[:m]], np.concatenate(exp_k))
 
 
-def test_multi_feature_grouped_lookup(dr, orc):
+@pytest.mark.parametrize("grad", [True, False])
+def test_multi_feature_grouped_lookup(dr, orc, grad):
+    """grad=False exercises the forward-only direct resolve (no Unique):
+    outputs, key counts and exported keys must equal the unique path's."""
     rng = np.random.default_rng(79)
     B, D, F = 300, 32, 5
     evs, oevs, sps, raw = [], [], [], []
     for f in range(F):
-        evs.append(dr.EmbeddingVariable("mf%d" % f, D, 0.1 * (f + 1)))
+        evs.append(dr.EmbeddingVariable("mf%d_%d" % (f, grad), D, 0.1 * (f + 1)))
         oevs.append(orc.EV(D, 0.1 * (f + 1)))
         keys = np.arange(100 * f, 100 * f + 80, dtype=np.int64)
         vals = rng.standard_normal((80, D)).astype(np.float32)
@@ -199,11 +202,16 @@ def test_multi_feature_grouped_lookup(dr, orc):
         ind, v = _random_sparse(rng, B, 4, 100 * f + 160)
         sps.append(dr.SparseTensor(T(ind), T(v), (B, 4)))
         raw.append((ind, v))
-    out = H(dr.embedding_lookup_sparse_multi(evs, sps, combiner="mean"))
+    with torch.set_grad_enabled(grad):
+        out = H(dr.embedding_lookup_sparse_multi(evs, sps, combiner="mean"))
     for f in range(F):
         ref = orc.embedding_lookup_sparse(oevs[f], raw[f][0], raw[f][1], B, combiner="mean")
         np.testing.assert_array_equal(out[:, f * D:(f + 1) * D], ref)
         assert int(evs[f].total_count()[0]) == oevs[f].size()
+        k, v = evs[f].export()[:2]
+        ok, ov = oevs[f].export()[:2]
+        np.testing.assert_array_equal(H(k), ok)
+        np.testing.assert_array_equal(H(v), ov)
 
 
 def test_sort_pairs_stable(ops):
@@ -413,6 +421,66 @@ def test_ev_lookup_sparse_bitexact(dr, orc, comb, D):
     ref = orc.embedding_lookup_sparse(oev, ind, v, B, combiner=comb)
     np.testing.assert_array_equal(out, ref)
     assert int(ev.total_count()[0]) == oev.size()
+
+
+@pytest.mark.parametrize("B", [1, 7, 8, 1003])
+def test_onehot_and_mostly_onehot_pooling(dr, orc, B):
+    """Pool kernel split: all-singleton chunks go to the lean copy kernel
+    (DR_POOL_ONEHOT when the SparseTensor is [B, 1] with nnz == B), mixed
+    chunks to the general kernel -- both bit-exact to the oracle."""
+    rng = np.random.default_rng(B + 11)
+    D, R = 64, 4000
+    table = rng.standard_normal((R, D)).astype(np.float32)
+    table[5] = -0.0                      # SEQ order must turn -0.0 into +0.0
+    # one-hot [B, 1]
+    ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1).astype(np.int64)
+    v = rng.integers(0, R, B).astype(np.int64)
+    v[0] = 5
+    for comb in ("sum", "mean", "sqrtn"):
+        out = H(dr.embedding_lookup_sparse(T(table), dr.SparseTensor(T(ind), T(v), (B, 1)),
+                                           combiner=comb))
+        np.testing.assert_array_equal(out, orc.embedding_lookup_sparse(table, ind, v, B,
+                                                                       combiner=comb))
+    # mostly one-hot: ~5% of bags hold 2-3 ids, some chunks fast, some general
+    lens = np.where(rng.random(B) < 0.05, rng.integers(2, 4, B), 1)
+    rows = np.repeat(np.arange(B), lens)
+    cols = np.concatenate([np.arange(l) for l in lens])
+    ind2 = np.stack([rows, cols], 1).astype(np.int64)
+    v2 = rng.integers(0, R, rows.shape[0]).astype(np.int64)
+    for comb in ("sum", "mean", "sqrtn"):
+        out = H(dr.embedding_lookup_sparse(T(table), dr.SparseTensor(T(ind2), T(v2), (B, 3)),
+                                           combiner=comb))
+        np.testing.assert_array_equal(out, orc.embedding_lookup_sparse(table, ind2, v2, B,
+                                                                       combiner=comb))
+    # grouped EV features, one-hot
+    evs, oevs, sps, raw = [], [], [], []
+    for f in range(3):
+        evs.append(dr.EmbeddingVariable("oh%d_%d" % (B, f), D, 0.5))
+        oevs.append(orc.EV(D, 0.5))
+        keys = np.arange(0, 50, dtype=np.int64)
+        vals = rng.standard_normal((50, D)).astype(np.float32)
+        evs[-1].insert(T(keys), T(vals))
+        oevs[-1].insert(keys, vals)
+        vf = rng.integers(0, 100, B).astype(np.int64)
+        sps.append(dr.SparseTensor(T(ind), T(vf), (B, 1)))
+        raw.append(vf)
+    out = H(dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum"))
+    for f in range(3):
+        ref = orc.embedding_lookup_sparse(oevs[f], ind, raw[f], B, combiner="sum")
+        np.testing.assert_array_equal(out[:, f * D:(f + 1) * D], ref)
+
+
+def test_pool_onehot_flag_rejects_weights(dr, ops):
+    from deeprec_amd import _lib
+    t = torch.zeros((4, 8), device=DEV)
+    ids = torch.arange(4, device=DEV)
+    w = torch.ones(4, device=DEV)
+    out = torch.empty((4, 8), device=DEV)
+    d = _lib.DrPoolDesc()
+    d.pool, d.pool_rows, d.ids, d.weights = t.data_ptr(), 4, ids.data_ptr(), w.data_ptr()
+    d.out, d.out_stride, d.combiner, d.max_norm = out.data_ptr(), 8, 0, -1.0
+    with pytest.raises(_lib.InvalidArgumentError):
+        ops.pool_grouped([d], 4, 8, onehot=True)
 
 
 @pytest.mark.parametrize("comb", ["sum", "mean", "sqrtn"])
