@@ -110,12 +110,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DR_BENCH_GLOO_STAGED=1: rehearsal of the N>1 path with every rank on
+    # cuda:0 and the all-to-alls staged through host memory over gloo (a
+    # 1-GPU box cannot host two RCCL ranks).  Never used for reported numbers.
+    staged = world > 1 and os.environ.get("DR_BENCH_GLOO_STAGED") == "1"
+    if staged:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if staged:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     dr.load()
     T, D, B, R = args.tables, args.dim, args.batch, args.rows
     torch.cuda.synchronize()
@@ -125,7 +134,8 @@ def main():
     evs = []
     for t in range(T):
         ev = dr.EmbeddingVariable("table%d" % t, D, 0.0, capacity=R + (1 << 19), device=dev)
-        ev.insert_synthetic(0, R, seed=1000 + t)
+        # rank r owns keys k % world == r of the keyspace [0, R * world)
+        ev.insert_synthetic(rank, R, seed=1000 + t, key_stride=world)
         evs.append(ev)
     torch.cuda.synchronize()
     log("populated %d EVs x %d rows x %d dim in %.1fs" % (T, R, D, time.perf_counter() - t0))
@@ -134,6 +144,13 @@ def main():
         from deeprec_amd.sharded import ShardedLookup
         engine = ShardedLookup(evs, world, rank, B, dev)
         keyspace = R * world
+        if staged:
+            def staged_a2a(out, inp, out_splits=None, in_splits=None):
+                o = torch.empty(out.shape, dtype=out.dtype)
+                dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits)
+                out.copy_(o)
+                return out
+            engine._a2a = staged_a2a
     else:
         engine = None
         keyspace = R
@@ -196,7 +213,7 @@ def main():
         el = time.perf_counter() - t0
         log("timed %d steps in %.3fs" % (args.steps, el))
     if dist is not None:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device="cpu" if staged else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     lookups = T * B * args.steps * world
@@ -206,7 +223,8 @@ def main():
 
     # ---- dominant kernel: the grouped gather+pool launch, timed alone -----
     from deeprec_amd.embedding_ops import _Feature, _prepare_group, _pool_all
-    static_ids.copy_(batches[0])
+    # keys this rank owns (all keys at N=1): the local gather+pool kernel
+    static_ids.copy_((batches[0] % R) * world + rank)
     with torch.no_grad():
         feats = [_Feature(evs[t], static_ids[t], seg, B, None, "sum", None, onehot=True)
                  for t in range(T)]
@@ -258,8 +276,10 @@ def main():
                 "" if args.zipf <= 0 else ", zipf %.2f" % args.zipf),
             "config": {"workload": "DLRM Criteo-TB shape: %d EV tables x %d rows/GPU x %d fp32, "
                                    "B_local=%d, hotness 1, embedding_lookup_sparse(sum) forward "
-                                   "(unique -> EV resolve -> fused gather+pool)%s"
-                                   % (T, R, D, B, "; row-sharded all-to-all" if world > 1 else ""),
+                                   "(EV insert-on-miss resolve of every id -> fused gather+pool; "
+                                   "forward-only filter-free one-hot needs no Unique)%s"
+                                   % (T, R, D, B, "; keys all-to-all -> owner resolve+pack -> "
+                                      "rows all-to-all (RCCL)" if world > 1 else ""),
                        "global_batch": B * world, "tables": T, "rows_per_gpu": R, "dim": D,
                        "parallelism": "row-sharded tables x%d, data-parallel batch" % world},
             "samples_per_s": round(value / T, 1),

@@ -510,7 +510,7 @@ __global__ void ev_import_kernel(EvDesc e, const int64_t* __restrict__ keys, int
 
 // Synthetic bulk insert of keys [begin, begin + n) (bench / test tables):
 // rows are filled with synth(seed, key, col) by ev_synth_rows_kernel.
-__global__ void ev_insert_range_kernel(EvDesc e, int64_t begin, int64_t n,
+__global__ void ev_insert_range_kernel(EvDesc e, int64_t begin, int64_t stride, int64_t n,
                                        int64_t* __restrict__ rows_out, uint8_t* __restrict__ init,
                                        int* st) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -519,7 +519,7 @@ __global__ void ev_insert_range_kernel(EvDesc e, int64_t begin, int64_t n,
   rows_out[i] = -1;
   bool created;
   uint64_t rc;
-  Slot* s = ev_find(e, (uint64_t)(begin + i), true, &created, &rc, st);
+  Slot* s = ev_find(e, (uint64_t)(begin + i * stride), true, &created, &rc, st);
   if (!s || (rc & kRowMask) == kRowDead) return;
   const uint64_t bit = 1ull << (48 + e.col);
   if (!(rc & bit)) {
@@ -530,12 +530,13 @@ __global__ void ev_insert_range_kernel(EvDesc e, int64_t begin, int64_t n,
 }
 
 __global__ void ev_synth_rows_kernel(float* __restrict__ pool, int64_t dim, int64_t begin,
-                                     int64_t n, const int64_t* __restrict__ rows,
+                                     int64_t stride, int64_t n, const int64_t* __restrict__ rows,
                                      const uint8_t* __restrict__ init, uint64_t seed) {
   const int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
   if (i >= n || !init[i]) return;
   float* dst = pool + rows[i] * dim;
-  for (int64_t c = threadIdx.x % 64; c < dim; c += 64) dst[c] = synth(seed, begin + i, c);
+  const int64_t key = begin + i * stride;
+  for (int64_t c = threadIdx.x % 64; c < dim; c += 64) dst[c] = synth(seed, key, c);
 }
 
 // Lookup without insert (export helpers / key_meta).
@@ -846,7 +847,8 @@ static ResolveWs carve_resolve(void* ws, int64_t n, size_t* used) {
 static int resolve_grouped(dr_ev* const* evs, int T, const int64_t* keys, const int64_t* koff,
                            const int64_t* const* n_dev, const float* const* defaults,
                            const int32_t* counts, int64_t* rows_out, void* ws, size_t ws_bytes,
-                           hipStream_t st, const int32_t* tags = nullptr) {
+                           hipStream_t st, const int32_t* tags = nullptr,
+                           const int64_t* per_table_host = nullptr) {
   const bool composite = tags != nullptr;
   DR_REQUIRE(T >= 1 && T <= DR_MAX_GROUP, DR_INVALID_ARGUMENT, "bad table count");
   const int64_t total = koff[T];
@@ -857,7 +859,9 @@ static int resolve_grouped(dr_ev* const* evs, int T, const int64_t* keys, const 
   int* stw = status_word();
   DR_REQUIRE(stw, DR_INTERNAL, "status word unavailable");
   for (int t = 0; t < T; ++t) {
-    int rc = reserve(evs[t]->sh, composite ? total : koff[t + 1] - koff[t], st);
+    const int64_t nt = composite ? (per_table_host ? per_table_host[t] : total)
+                                 : koff[t + 1] - koff[t];
+    int rc = reserve(evs[t]->sh, nt, st);
     if (rc) return rc;
   }
   ResolveWs w = carve_resolve(ws, total, nullptr);
@@ -1095,8 +1099,8 @@ int dr_ev_resolve_grouped(dr_ev* const* evs, int num_tables, const int64_t* keys
 // read table t's EV default.
 int dr_ev_resolve_tagged(dr_ev* const* evs, int num_tables, const int64_t* keys,
                          const int32_t* tags, int64_t n, const int64_t* n_dev,
-                         const int32_t* counts, int64_t* rows_out, void* ws, size_t ws_bytes,
-                         void* stream) {
+                         const int64_t* per_table_host, const int32_t* counts,
+                         int64_t* rows_out, void* ws, size_t ws_bytes, void* stream) {
   DR_REQUIRE(num_tables >= 1 && num_tables <= DR_MAX_GROUP, DR_INVALID_ARGUMENT,
              "bad table count");
   int64_t koff[DR_MAX_GROUP + 1];
@@ -1105,7 +1109,7 @@ int dr_ev_resolve_tagged(dr_ev* const* evs, int num_tables, const int64_t* keys,
   const int64_t* nd[1] = {n_dev};
   DR_REQUIRE(tags, DR_INVALID_ARGUMENT, "tags required");
   return dr::resolve_grouped(evs, num_tables, keys, koff, nd, nullptr, counts, rows_out, ws,
-                             ws_bytes, dr::S(stream), tags);
+                             ws_bytes, dr::S(stream), tags, per_table_host);
 }
 
 // Owner-side pack for the row exchange: out[i] = resolved row of key i of
@@ -1198,10 +1202,10 @@ int dr_ev_insert(dr_ev* ev, const int64_t* keys, int64_t n, const float* values,
 
 // Bulk insert of keys [key_begin, key_begin + n) with synthetic rows
 // synth(seed, key, col) -- populates bench/test tables without a host copy.
-int dr_ev_insert_synthetic(dr_ev* ev, int64_t key_begin, int64_t n, uint64_t seed,
-                           void* stream) {
+int dr_ev_insert_synthetic(dr_ev* ev, int64_t key_begin, int64_t key_stride, int64_t n,
+                           uint64_t seed, void* stream) {
   using namespace dr;
-  DR_REQUIRE(ev && n >= 0, DR_INVALID_ARGUMENT, "bad argument");
+  DR_REQUIRE(ev && n >= 0 && key_stride >= 1, DR_INVALID_ARGUMENT, "bad argument");
   if (n == 0) return DR_OK;
   hipStream_t st = S(stream);
   int rc = reserve(ev->sh, n, st);
@@ -1215,9 +1219,10 @@ int dr_ev_insert_synthetic(dr_ev* ev, int64_t key_begin, int64_t n, uint64_t see
   for (int64_t b = 0; b < n; b += chunk) {
     const int64_t m = std::min(chunk, n - b);
     hipLaunchKernelGGL(ev_insert_range_kernel, dim3((unsigned)ceil_div(m, 256)), dim3(256), 0, st,
-                       e, key_begin + b, m, rows, init, status_word());
+                       e, key_begin + b * key_stride, key_stride, m, rows, init, status_word());
     hipLaunchKernelGGL(ev_synth_rows_kernel, dim3((unsigned)ceil_div(m, 4)), dim3(256), 0, st,
-                       ev->sh->pools[ev->col], ev->sh->dim, key_begin + b, m, rows, init, seed);
+                       ev->sh->pools[ev->col], ev->sh->dim, key_begin + b * key_stride,
+                       key_stride, m, rows, init, seed);
     DR_LAUNCH_CHECK();
   }
   DR_HIP(hipFreeAsync(rows, st));

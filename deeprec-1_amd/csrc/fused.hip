@@ -110,23 +110,43 @@ struct RouteGroup {
 };
 
 // sort key = owner * T + feature for valid uniques, world * T otherwise.
-__global__ void route_keys_kernel(RouteGroup g, int T, const int64_t* __restrict__ uniq,
-                                  const int64_t* __restrict__ num_unique, int world,
-                                  uint64_t* __restrict__ skey, int32_t* __restrict__ pos,
-                                  unsigned long long* __restrict__ counts) {
+// num_unique == nullptr: every key of a feature is valid (raw ids, no dedup).
+// The [world*T] histogram is built in LDS per block (one global atomic per
+// bin per block instead of one per key onto ~200 hot addresses).
+constexpr int kRouteLdsBins = 4096;
+__global__ __launch_bounds__(256) void route_keys_kernel(RouteGroup g, int T,
+                                                         const int64_t* __restrict__ uniq,
+                                                         const int64_t* __restrict__ num_unique,
+                                                         int world, uint64_t* __restrict__ skey,
+                                                         int32_t* __restrict__ pos,
+                                                         unsigned long long* __restrict__ counts) {
+  __shared__ unsigned int hist[kRouteLdsBins];
+  const int bins = world * T;
+  const bool lds = bins <= kRouteLdsBins;
+  if (lds)
+    for (int b = threadIdx.x; b < bins; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= g.koff[T]) return;
-  int t = 0;
-  while (t + 1 < T && i >= g.koff[t + 1]) ++t;
-  uint64_t k = (uint64_t)world * T;
-  if (i - g.koff[t] < num_unique[t]) {
-    int64_t o = uniq[i] % world;
-    if (o < 0) o += world;
-    k = (uint64_t)o * T + t;
-    atomicAdd(&counts[k], 1ull);
+  if (i < g.koff[T]) {
+    int t = 0;
+    while (t + 1 < T && i >= g.koff[t + 1]) ++t;
+    uint64_t k = (uint64_t)bins;
+    if (!num_unique || i - g.koff[t] < num_unique[t]) {
+      int64_t o = uniq[i] % world;
+      if (o < 0) o += world;
+      k = (uint64_t)o * T + t;
+      if (lds)
+        atomicAdd(&hist[k], 1u);
+      else
+        atomicAdd(&counts[k], 1ull);
+    }
+    skey[i] = k;
+    pos[i] = (int32_t)i;
   }
-  skey[i] = k;
-  pos[i] = (int32_t)i;
+  if (!lds) return;
+  __syncthreads();
+  for (int b = threadIdx.x; b < bins; b += blockDim.x)
+    if (hist[b]) atomicAdd(&counts[b], (unsigned long long)hist[b]);
 }
 
 __global__ void route_emit_kernel(const int64_t* __restrict__ uniq, const uint64_t* __restrict__ skey,

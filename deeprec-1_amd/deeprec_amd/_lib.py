@@ -96,14 +96,14 @@ SIGNATURES = {
     "dr_ev_resolve_workspace_size": (_SZ, [_I64]),
     "dr_ev_resolve": (_I32, [_P, _P, _I64, _P, _P, _P, _P, _P, _SZ, _P]),
     "dr_ev_resolve_grouped": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P, _SZ, _P]),
-    "dr_ev_resolve_tagged": (_I32, [_P, _I32, _P, _P, _I64, _P, _P, _P, _P, _SZ, _P]),
+    "dr_ev_resolve_tagged": (_I32, [_P, _I32, _P, _P, _I64, _P, _P, _P, _P, _P, _SZ, _P]),
     "dr_ev_gather_tagged": (_I32, [_P, _I32, _P, _P, _I64, _P, _P, _P]),
     "dr_ev_pool": (_P, [_P]),
     "dr_ev_default_row": (_P, [_P]),
     "dr_ev_gather_workspace_size": (_SZ, [_I64]),
     "dr_ev_gather": (_I32, [_P, _P, _I64, _P, _P, _P, _P, _SZ, _P]),
     "dr_ev_insert": (_I32, [_P, _P, _I64, _P, _P, _P, _I64, _I64, _P]),
-    "dr_ev_insert_synthetic": (_I32, [_P, _I64, _I64, _U64, _P]),
+    "dr_ev_insert_synthetic": (_I32, [_P, _I64, _I64, _I64, _U64, _P]),
     "dr_ev_export": (_I32, [_P, _P, _P, _P, _P, _I64, _P, _P]),
     "dr_ev_key_meta": (_I32, [_P, _P, _I64, _P, _P, _P, _P]),
     "dr_ev_apply_sgd": (_I32, [_P, _F32, _P, _P, _I64, _P, _I64, _P]),

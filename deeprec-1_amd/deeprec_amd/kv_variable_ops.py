@@ -215,10 +215,10 @@ class EmbeddingVariable(object):
         check(lib().dr_ev_insert(self._h, ptr(k), k.numel(), ptr(v), ptr(ver), ptr(fr), pid, pnum,
                                  stream_handle(self.device)))
 
-    def insert_synthetic(self, key_begin, n, seed):
-        """Insert keys [key_begin, key_begin+n) with rows synth(seed, key, col)."""
-        check(lib().dr_ev_insert_synthetic(self._h, int(key_begin), int(n), int(seed),
-                                           stream_handle(self.device)))
+    def insert_synthetic(self, key_begin, n, seed, key_stride=1):
+        """Insert keys key_begin + i*key_stride, i < n, rows synth(seed, key, col)."""
+        check(lib().dr_ev_insert_synthetic(self._h, int(key_begin), int(key_stride), int(n),
+                                           int(seed), stream_handle(self.device)))
 
     def total_count(self):
         """KvVariableShape: [num keys, dim]."""

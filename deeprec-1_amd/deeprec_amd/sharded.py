@@ -47,8 +47,9 @@ class HipLocal(object):
     def route(self, uniq, koff, num_unique, world):
         return ops.route_by_owner(uniq, koff, num_unique, world)
 
-    def resolve_pack(self, keys, tags, n):
-        """Owner side: insert-on-miss resolve + row pack of n received keys."""
+    def resolve_pack(self, keys, tags, n, per_table):
+        """Owner side: insert-on-miss resolve + row pack of n received keys
+        (per_table: host list of how many of them belong to each table)."""
         rows = torch.empty(n, dtype=torch.int64, device=self.device)
         out = torch.empty((n, self.dim), dtype=torch.float32, device=self.device)
         if n == 0:
@@ -56,22 +57,30 @@ class HipLocal(object):
         wsb = lib().dr_ev_resolve_workspace_size(n)
         ws = workspace(wsb, self.device)
         st = stream_handle(self.device)
-        check(lib().dr_ev_resolve_tagged(self.handles, self.T, ptr(keys), ptr(tags), n, None, None,
-                                         ptr(rows), ptr(ws), wsb, st))
+        pt = (C.c_int64 * self.T)(*[int(x) for x in per_table])
+        check(lib().dr_ev_resolve_tagged(self.handles, self.T, ptr(keys), ptr(tags), n, None, pt,
+                                         None, ptr(rows), ptr(ws), wsb, st))
         check(lib().dr_ev_gather_tagged(self.handles, self.T, ptr(tags), ptr(rows), n, None,
                                         ptr(out), st))
         ops._post(self.device)
         return out
 
     def pool(self, rows_recv, rowsel, idx, koff, bag_offs, batch, combiner):
+        """Requester: pooled [batch, T*D] from the received rows.  rowsel[u]
+        is the received row of unique u (idx given: nnz -> unique) or of nnz
+        u directly (idx None, the direct one-hot mode)."""
         T, D = self.T, self.dim
         out = torch.empty((batch, T * D), dtype=torch.float32, device=self.device)
         descs = []
         for t in range(T):
             d = DrPoolDesc()
             d.pool = rows_recv.data_ptr()
-            d.idx = idx.data_ptr() + 4 * koff[t]
-            d.rows = rowsel.data_ptr() + 8 * koff[t]
+            if idx is None:
+                d.ids = rowsel.data_ptr() + 8 * koff[t]
+                d.pool_rows = max(int(rows_recv.shape[0]), 1)
+            else:
+                d.idx = idx.data_ptr() + 4 * koff[t]
+                d.rows = rowsel.data_ptr() + 8 * koff[t]
             d.default_rows = rows_recv.data_ptr()
             d.default_stride = 0
             d.bag_off = None if bag_offs is None else bag_offs[t].data_ptr()
@@ -93,24 +102,34 @@ class ShardedLookup(object):
         self.rank = rank
         self.batch = batch
         self.device = device
-        self.T = len(evs)
-        self.dim = evs[0].dim if evs else 0
         self.group = group
         self.backend = backend or HipLocal(evs, device)
+        self.T = self.backend.T
+        self.dim = self.backend.dim
         self.last_stats = {}
 
     def _a2a(self, out, inp, out_splits=None, in_splits=None):
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
         return out
 
-    def forward(self, ids, bag_offs=None, combiner="sum"):
-        """ids: [T, nnz] keys (hotness 1 when bag_offs is None: bag b = id b)."""
+    def forward(self, ids, bag_offs=None, combiner="sum", need_grad=False):
+        """ids: [T, nnz] keys (hotness 1 when bag_offs is None: bag b = id b).
+
+        Forward-only one-hot lookups of filter-free EVs route the raw ids
+        (no Unique): the owner's insert-on-miss resolve dedups, exactly as
+        in the single-GPU direct mode (embedding_ops._prepare_group)."""
         T, G, be = self.T, self.world, self.backend
         dev = ids.device
         nnz = ids.shape[1]
+        if bag_offs is None and nnz != self.batch:
+            raise ValueError("one-hot ids need nnz == batch (%d != %d)" % (nnz, self.batch))
         vals = ids.reshape(-1)
         koff = [t * nnz for t in range(T + 1)]
-        uniq, idx, _cnt, U = be.unique_grouped(vals, koff)
+        direct = bag_offs is None and not need_grad and not be.filter
+        if direct:
+            uniq, idx, U = vals, None, None
+        else:
+            uniq, idx, _cnt, U = be.unique_grouped(vals, koff)
         keys_s, tags_s, perm, counts = be.route(uniq, koff, U, G)
         # 3. counts exchange (peer-major [G, T]) and one host read of the splits
         recv_counts = torch.empty_like(counts)
@@ -128,14 +147,12 @@ class ShardedLookup(object):
             torch.arange(T, dtype=torch.int32, device=dev).repeat(G),
             recv_counts.view(-1), output_size=R)
         # 5. owner resolve + pack, 6. rows all-to-all back
-        rows_s = be.resolve_pack(keys_r, tags_r, R)
+        rows_s = be.resolve_pack(keys_r, tags_r, R, rc.sum(0).tolist())
         rows_r = torch.empty((S, self.dim), dtype=torch.float32, device=dev)
         self._a2a(rows_r, rows_s, send_splits, recv_splits)
-        # 7. requester: unique position -> row in the received buffer, pool
+        # 7. requester: (unique | nnz) position -> row in the received buffer
         rowsel = torch.zeros(T * nnz, dtype=torch.int64, device=dev)
         rowsel[perm[:S].to(torch.int64)] = torch.arange(S, dtype=torch.int64, device=dev)
-        if bag_offs is None and nnz != self.batch:
-            raise ValueError("one-hot ids need nnz == batch (%d != %d)" % (nnz, self.batch))
         out = be.pool(rows_r, rowsel, idx, koff, bag_offs, self.batch, combiner)
-        self.last_stats = {"sent_keys": S, "recv_keys": R}
+        self.last_stats = {"sent_keys": S, "recv_keys": R, "direct": direct}
         return out

@@ -241,10 +241,12 @@ int dr_ev_resolve_grouped(dr_ev* const* evs, int num_tables, const int64_t* keys
 /* Tagged resolve (owner side of the sharded exchange): keys of all T EVs  */
 /* (equal dim) in one array, table of key i = tags[i]; n_dev: optional      */
 /* DEVICE count.  Filtered keys give -(i+1) (read table t's default row).   */
+/* per_table_host: optional HOST count of keys per table (capacity          */
+/* accounting; NULL assumes all n keys may be new to every table).          */
 int dr_ev_resolve_tagged(dr_ev* const* evs, int num_tables, const int64_t* keys,
                          const int32_t* tags, int64_t n, const int64_t* n_dev,
-                         const int32_t* counts, int64_t* rows_out, void* ws, size_t ws_bytes,
-                         void* stream);
+                         const int64_t* per_table_host, const int32_t* counts,
+                         int64_t* rows_out, void* ws, size_t ws_bytes, void* stream);
 /* Owner-side row pack: out[i] = resolved row of key i of table tags[i]     */
 /* (the table's default row when filtered).                                  */
 int dr_ev_gather_tagged(dr_ev* const* evs, int num_tables, const int32_t* tags,
@@ -268,9 +270,11 @@ int dr_ev_insert(dr_ev* ev, const int64_t* keys, int64_t n, const float* values,
                  const int64_t* versions, const int64_t* freqs, int64_t partition_id,
                  int64_t partition_num, void* stream);
 
-/* Bulk insert of keys [key_begin, key_begin + n) whose rows are            */
-/* synth(seed, key, col) (dr_synth_value): populates synthetic tables.      */
-int dr_ev_insert_synthetic(dr_ev* ev, int64_t key_begin, int64_t n, uint64_t seed,
+/* Bulk insert of keys key_begin + i * key_stride, i in [0, n), whose rows  */
+/* are synth(seed, key, col) (dr_synth_value): populates synthetic tables   */
+/* (stride = world for the key % world shard a rank owns).                   */
+int dr_ev_insert_synthetic(dr_ev* ev, int64_t key_begin, int64_t key_stride, int64_t n,
+                           uint64_t seed,
                            void* stream);
 
 /* KvResourceExport (kv_variable_ops.cc:786-835), keys ascending.  Syncs.   */
@@ -326,6 +330,8 @@ int dr_partition_by_owner(const int64_t* keys, int64_t n, const int64_t* n_dev, 
 /* owner = key % world, giving the [peer][feature]-blocked send buffer of    */
 /* the key all-to-all: keys_out/tags_out (feature id)/perm_out (source      */
 /* position) and counts[world * T] (DEVICE int64, peer-major).               */
+/* num_unique == NULL routes every key (raw ids of a forward-only one-hot   */
+/* lookup: the owner's insert-on-miss dedups, SOK all2all_input_dispatcher).*/
 size_t dr_route_workspace_size(int64_t n, int world, int num_tables);
 int dr_route_by_owner(const int64_t* uniq, const int64_t* koff_host, int num_tables,
                       const int64_t* num_unique, int world, int64_t* keys_out,

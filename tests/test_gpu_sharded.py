@@ -1,0 +1,133 @@
+"""Row-sharded engine with the HIP backend (HipLocal) on one GPU.
+
+World sizes 1 and 2 are emulated inside one process: every rank is a thread
+with its own ShardedLookup and its own EV shards, and the all-to-all is an
+in-memory exchange between the threads (same device, same stream order), so
+routing, tagged owner resolve, row pack and requester pooling all run as
+HIP kernels through the C ABI.  The RCCL transport itself is not under test
+here (the driver's multi-GPU run exercises it); the CPU gloo test covers the
+protocol over a real process group.  Outputs must equal the single-process
+oracle bit for bit.
+"""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+T, D, B = 4, 64, 512
+KEYSPACE = 3000
+DEFAULT = 0.5
+
+
+def _vals(t, keys):
+    k = np.asarray(keys, np.float64)[:, None]
+    return np.cos(0.013 * k + 0.7 * t + 0.05 * np.arange(D)[None, :]).astype(np.float32)
+
+
+class _Exchange(object):
+    """all_to_all_single between threads of one process."""
+
+    def __init__(self, world):
+        self.world = world
+        self.bar = threading.Barrier(world)
+        self.box = [None] * world
+
+    def a2a(self, rank, out, inp, out_splits, in_splits):
+        W = self.world
+        if in_splits is None:
+            in_splits = [inp.shape[0] // W] * W
+        if out_splits is None:
+            out_splits = [out.shape[0] // W] * W
+        self.box[rank] = list(torch.split(inp, list(in_splits)))
+        self.bar.wait()
+        pieces = [self.box[p][rank] for p in range(W)]
+        assert [x.shape[0] for x in pieces] == list(out_splits)
+        if out.shape[0]:
+            torch.cat(pieces, out=out)
+        self.bar.wait()
+        return out
+
+
+def _run_world(world, onehot, combiner):
+    import deeprec_amd as dr
+    from oracle import oracle as orc
+    from deeprec_amd.sharded import ShardedLookup
+    dr.load()
+    ex = _Exchange(world)
+    engines, batches = [], []
+    rng = np.random.default_rng(5 + world)
+    for r in range(world):
+        evs = []
+        own = np.arange(r, KEYSPACE // 2, world, dtype=np.int64)
+        for t in range(T):
+            ev = dr.EmbeddingVariable("sh%d_%d_%d_%d" % (world, int(onehot), r, t), D, DEFAULT,
+                                      device=DEV)
+            ev.insert(torch.as_tensor(own, device=DEV), torch.as_tensor(_vals(t, own), device=DEV))
+            evs.append(ev)
+        eng = ShardedLookup(evs, world, r, B, torch.device(DEV))
+        eng._a2a = (lambda rr: (lambda out, inp, os_=None, is_=None:
+                                ex.a2a(rr, out, inp, os_, is_)))(r)
+        engines.append(eng)
+        if onehot:
+            lens = np.ones(B, np.int64)
+        else:
+            lens = rng.integers(0, 5, B)
+            lens[3] = 0
+        nnz = int(lens.sum())
+        ids = rng.integers(0, KEYSPACE, (T, nnz)).astype(np.int64)
+        ids[:, :4] = 11                       # duplicates inside the batch
+        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+        batches.append((ids, off))
+    outs = [None] * world
+    errs = []
+
+    def run(r):
+        try:
+            ids, off = batches[r]
+            bo = None if onehot else [torch.as_tensor(off, device=DEV)] * T
+            with torch.no_grad():
+                outs[r] = engines[r].forward(torch.as_tensor(ids, device=DEV), bag_offs=bo,
+                                             combiner=combiner).cpu().numpy()
+        except Exception as e:  # surfaced below
+            errs.append(e)
+            ex.bar.abort()
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(120)
+    if errs:
+        raise errs[0]
+    dr.status_check()
+    allk = np.arange(0, KEYSPACE // 2, dtype=np.int64)
+    for r in range(world):
+        ids, off = batches[r]
+        assert engines[r].last_stats["direct"] == onehot
+        seg = np.repeat(np.arange(B), np.diff(off))
+        ind = np.stack([seg, np.zeros_like(seg)], 1)
+        for t in range(T):
+            ref_ev = orc.EV(D, DEFAULT)
+            ref_ev.insert(allk, _vals(t, allk))
+            ref = orc.embedding_lookup_sparse(ref_ev, ind, ids[t], B, combiner=combiner)
+            np.testing.assert_array_equal(outs[r][:, t * D:(t + 1) * D], ref)
+    # each shard holds only its own keys
+    for r in range(world):
+        for ev in engines[r].evs:
+            k = ev.export()[0].cpu().numpy()
+            assert np.all(k % world == r)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_sharded_onehot_direct(world):
+    _run_world(world, True, "sum")
+
+
+@pytest.mark.parametrize("world", [1, 2])
+@pytest.mark.parametrize("combiner", ["sum", "mean"])
+def test_sharded_multihot_unique(world, combiner):
+    _run_world(world, False, combiner)
