@@ -42,6 +42,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--cpu-rows", type=int, default=2_000_000)
     p.add_argument("--kernel-iters", type=int, default=20)
+    p.add_argument("--engine", default="auto", choices=["auto", "local", "xgmi", "a2a"],
+                   help="auto: local lookup at N=1, xgmi peer-write (RCCL all-to-all "
+                        "fallback) at N>1; xgmi/a2a at N=1 run the sharded engine on itself")
     return p.parse_args()
 
 
@@ -140,17 +143,49 @@ def main():
     torch.cuda.synchronize()
     log("populated %d EVs x %d rows x %d dim in %.1fs" % (T, R, D, time.perf_counter() - t0))
 
-    if world > 1:
-        from deeprec_amd.sharded import ShardedLookup
-        engine = ShardedLookup(evs, world, rank, B, dev)
+    engine_kind = "local"
+    want = args.engine if args.engine != "auto" else ("local" if world == 1 else "xgmi")
+    if want != "local":
+        from deeprec_amd.sharded import ShardedLookup, XgmiShardedLookup
         keyspace = R * world
-        if staged:
-            def staged_a2a(out, inp, out_splits=None, in_splits=None):
-                o = torch.empty(out.shape, dtype=out.dtype)
-                dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits)
-                out.copy_(o)
-                return out
-            engine._a2a = staged_a2a
+        engine = None
+        if want == "xgmi" and world == 1:
+            engine = XgmiShardedLookup(evs, 1, 0, B, dev)
+            engine_kind = "xgmi peer-write"
+        elif want == "xgmi":
+            # peer writes over xGMI; every rank must succeed or all fall back
+            ok, err = 1, ""
+            try:
+                barrier = None
+                if staged:
+                    def barrier():
+                        torch.cuda.synchronize()
+                        dist.barrier()
+                engine = XgmiShardedLookup(evs, world, rank, B, dev, barrier=barrier)
+            except Exception as e:  # IPC mapping unavailable
+                ok, err = 0, str(e)
+            flag = torch.tensor([ok], dtype=torch.int32, device="cpu" if staged else dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if int(flag.item()) == 1:
+                engine_kind = "xgmi peer-write"
+            else:
+                log("xgmi engine unavailable on some rank (%s); RCCL all-to-all engine" % err)
+                if engine is not None:
+                    engine.close()
+                engine = None
+        if engine is None:
+            engine = ShardedLookup(evs, world, rank, B, dev)
+            engine_kind = "RCCL all-to-all"
+            if staged:
+                def staged_a2a(out, inp, out_splits=None, in_splits=None):
+                    o = torch.empty(out.shape, dtype=out.dtype)
+                    dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits)
+                    out.copy_(o)
+                    return out
+                engine._a2a = staged_a2a
+            elif world == 1:
+                engine._a2a = lambda out, inp, os_=None, is_=None: out.copy_(inp)
+        log("sharded engine: %s" % engine_kind)
     else:
         engine = None
         keyspace = R
@@ -278,9 +313,11 @@ def main():
                                    "B_local=%d, hotness 1, embedding_lookup_sparse(sum) forward "
                                    "(EV insert-on-miss resolve of every id -> fused gather+pool; "
                                    "forward-only filter-free one-hot needs no Unique)%s"
-                                   % (T, R, D, B, "; keys all-to-all -> owner resolve+pack -> "
-                                      "rows all-to-all (RCCL)" if world > 1 else ""),
+                                   % (T, R, D, B, "; %s exchange: ids to owners (key %% N), "
+                                      "owner resolve, rows back" % engine_kind
+                                      if world > 1 else ""),
                        "global_batch": B * world, "tables": T, "rows_per_gpu": R, "dim": D,
+                       "engine": engine_kind,
                        "parallelism": "row-sharded tables x%d, data-parallel batch" % world},
             "samples_per_s": round(value / T, 1),
             "roofline": roof,

@@ -1391,3 +1391,225 @@ int dr_ev_apply_adam(dr_ev* var, dr_ev* m, dr_ev* v, float beta1_power, float be
 }
 
 }  // extern "C"
+
+// ===========================================================================
+// Owner side of the peer-mapped sharded lookup (dr_xgmi_serve).
+// The inbox region of requester src holds cnt[src] (key, slot) pairs written
+// over xGMI by src's dr_xgmi_route; a cross-rank barrier separates the two.
+// Three launches, each a (grid.x, grid.y = src) grid-stride loop:
+//   resolve: insert-on-miss of every inbox key in EV (slot % T)
+//   init   : first-touch default rows (kernel boundary: before any read)
+//   emit   : row -> out[src][slot * dim] of the requester, over xGMI
+// ===========================================================================
+namespace dr {
+
+struct XgmiResolveArgs {
+  EvDesc e[DR_MAX_GROUP];
+  const int64_t* keys;  // local inbox [world][cap]
+  const int32_t* slot;
+  const int64_t* cnt;   // local [world], written by the requesters
+  int64_t cap;
+  int T;
+};
+
+__device__ __forceinline__ int64_t inbox_count(const int64_t* cnt, int src) {
+  return __hip_atomic_load(cnt + src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(256) void xgmi_resolve_kernel(XgmiResolveArgs a,
+                                                           int64_t* __restrict__ rows,
+                                                           uint8_t* __restrict__ init, int* st) {
+  const int src = blockIdx.y;
+  const int64_t n = inbox_count(a.cnt, src);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t j = (int64_t)src * a.cap + i;
+    const uint64_t key = (uint64_t)a.keys[j];
+    const int t = a.slot[j] % a.T;
+    const EvDesc& e = a.e[t];
+    bool created;
+    uint64_t rc;
+    Slot* s = ev_find(e, key, true, &created, &rc, st);
+    uint8_t flag = 0;
+    int64_t row = -1;
+    if (s && (rc & kRowMask) != kRowDead) {
+      row = (int64_t)(rc & kRowMask);
+      const uint64_t bit = 1ull << (48 + e.col);
+      if (!(rc & bit)) {
+        const uint64_t old = atomicOr((unsigned long long*)&s->rc, (unsigned long long)bit);
+        if (!(old & bit)) flag = 1;
+      }
+    }
+    rows[j] = row;
+    init[j] = flag;
+  }
+}
+
+struct XgmiRowArgs {
+  float* pool[DR_MAX_GROUP];
+  const float* dflt[DR_MAX_GROUP];
+  float* out[DR_MAX_PEERS];   // requesters' outputs (peer-mapped)
+  const int32_t* slot;
+  const int64_t* cnt;
+  int64_t cap;
+  int64_t dim;
+  int T;
+};
+
+// Wave-cooperative first-touch copy (steady state: one byte per key).
+__global__ __launch_bounds__(256) void xgmi_init_kernel(XgmiRowArgs a,
+                                                        const int64_t* __restrict__ rows,
+                                                        const uint8_t* __restrict__ init) {
+  const int src = blockIdx.y;
+  const int64_t n = inbox_count(a.cnt, src);
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t base = wave * 64; base < n; base += waves * 64) {
+    const int64_t i = base + lane;
+    const int64_t j = (int64_t)src * a.cap + i;
+    const bool need = i < n && init[j];
+    uint64_t mask = __ballot(need);
+    while (mask) {
+      const int l = __ffsll((unsigned long long)mask) - 1;
+      mask &= mask - 1;
+      const int64_t jj = __shfl(j, l, 64);
+      const int t = a.slot[jj] % a.T;
+      float* dst = a.pool[t] + rows[jj] * a.dim;
+      const float* src_row = a.dflt[t];
+      for (int64_t c = lane; c < a.dim; c += 64) dst[c] = src_row[c];
+    }
+  }
+}
+
+typedef float xf4 __attribute__((ext_vector_type(4)));
+
+// G lanes per row (dim/4 <= G), NB rows in flight per group, nontemporal
+// (each row byte crosses once); the stores land in the requester's HBM.
+template <int G, int NB>
+__global__ __launch_bounds__(256) void xgmi_emit_kernel(XgmiRowArgs a,
+                                                        const int64_t* __restrict__ rows) {
+  const int src = blockIdx.y;
+  const int64_t n = inbox_count(a.cnt, src);
+  constexpr int GPB = 256 / G;
+  const int lg = threadIdx.x % G;
+  const int dv = (int)(a.dim / 4);
+  const int64_t grp = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+  const int64_t ngrp = (int64_t)gridDim.x * GPB;
+  float* out = a.out[src];
+  for (int64_t i0 = grp * NB; i0 < n; i0 += ngrp * NB) {
+    xf4 x[NB];
+    float* dst[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      dst[k] = nullptr;
+      x[k] = xf4{0.f, 0.f, 0.f, 0.f};
+      const int64_t i = i0 + k;
+      if (i < n && lg < dv) {
+        const int64_t j = (int64_t)src * a.cap + i;
+        const int32_t sl = a.slot[j];
+        const int t = sl % a.T;
+        const int64_t r = rows[j];
+        const float* row = r >= 0 ? a.pool[t] + r * a.dim : a.dflt[t];
+        x[k] = __builtin_nontemporal_load(reinterpret_cast<const xf4*>(row) + lg);
+        dst[k] = out + (int64_t)sl * a.dim;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+      if (dst[k]) __builtin_nontemporal_store(x[k], reinterpret_cast<xf4*>(dst[k]) + lg);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) __threadfence_system();  // remote stores performed before the end
+}
+
+struct XgmiWs {
+  int64_t* rows;
+  uint8_t* init;
+};
+static XgmiWs carve_xgmi(void* ws, int world, int64_t cap, size_t* used) {
+  Carver c(ws);
+  XgmiWs w;
+  w.rows = c.take<int64_t>((int64_t)world * cap);
+  w.init = c.take<uint8_t>((int64_t)world * cap);
+  if (used) *used = c.used + 256;
+  return w;
+}
+
+}  // namespace dr
+
+extern "C" {
+
+size_t dr_xgmi_serve_workspace_size(int world, int64_t cap) {
+  size_t used = 0;
+  dr::carve_xgmi(nullptr, world > 0 ? world : 1, cap > 0 ? cap : 1, &used);
+  return used;
+}
+
+int dr_xgmi_serve(const dr_xgmi_peers* peers, dr_ev* const* evs, int num_tables,
+                  int64_t batch, void* ws, size_t ws_bytes, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(peers && evs && num_tables >= 1 && num_tables <= DR_MAX_GROUP && batch >= 0,
+             DR_INVALID_ARGUMENT, "bad argument");
+  const int W = peers->world;
+  const int r = peers->rank;
+  DR_REQUIRE(W >= 1 && W <= DR_MAX_PEERS && r >= 0 && r < W && peers->cap > 0,
+             DR_INVALID_ARGUMENT, "bad world/rank/cap");
+  DR_REQUIRE(ws_bytes >= dr_xgmi_serve_workspace_size(W, peers->cap), DR_INVALID_ARGUMENT,
+             "serve workspace too small");
+  const int64_t dim = evs[0]->sh->dim;
+  DR_REQUIRE(dim % 4 == 0 && dim <= 256, DR_INVALID_ARGUMENT,
+             "xgmi serve needs dim %% 4 == 0 and dim <= 256 (got %lld)", (long long)dim);
+  XgmiResolveArgs ra;
+  memset(&ra, 0, sizeof(ra));
+  XgmiRowArgs wa;
+  memset(&wa, 0, sizeof(wa));
+  for (int t = 0; t < num_tables; ++t) {
+    const EvShared* s = evs[t]->sh;
+    DR_REQUIRE(s->dim == dim, DR_INVALID_ARGUMENT, "tables must share dim");
+    DR_REQUIRE(s->filter_freq == 0 && s->k_hash == 0, DR_INVALID_ARGUMENT,
+               "table %d: xgmi serve is for filter-free EVs", t);
+    ra.e[t] = make_desc(evs[t]);
+    wa.pool[t] = s->pools[evs[t]->col];
+    wa.dflt[t] = s->defaults[evs[t]->col];
+  }
+  DR_REQUIRE(peers->inbox_keys[r] && peers->inbox_slot[r] && peers->inbox_cnt[r],
+             DR_INVALID_ARGUMENT, "own inbox not set");
+  ra.keys = peers->inbox_keys[r];
+  ra.slot = peers->inbox_slot[r];
+  ra.cnt = peers->inbox_cnt[r];
+  ra.cap = peers->cap;
+  ra.T = num_tables;
+  for (int p = 0; p < W; ++p) {
+    DR_REQUIRE(peers->out[p], DR_INVALID_ARGUMENT, "peer %d output not mapped", p);
+    wa.out[p] = peers->out[p];
+  }
+  wa.slot = ra.slot;
+  wa.cnt = ra.cnt;
+  wa.cap = peers->cap;
+  wa.dim = dim;
+  wa.T = num_tables;
+  XgmiWs w = carve_xgmi(ws, W, peers->cap, nullptr);
+  int* stw = status_word();
+  DR_REQUIRE(stw, DR_INTERNAL, "status word unavailable");
+  hipStream_t st = S(stream);
+  // expected keys per source ~ T*B / W; a few hundred blocks per source
+  const int64_t per_src = std::max<int64_t>(1, (int64_t)num_tables * batch / W);
+  const unsigned gx = (unsigned)std::min<int64_t>(1024, std::max<int64_t>(1, ceil_div(per_src, 1024)));
+  hipLaunchKernelGGL(xgmi_resolve_kernel, dim3(gx, W), dim3(256), 0, st, ra, w.rows, w.init, stw);
+  hipLaunchKernelGGL(xgmi_init_kernel, dim3(gx, W), dim3(256), 0, st, wa, w.rows, w.init);
+  const int dv = (int)(dim / 4);
+  const unsigned ge = (unsigned)std::min<int64_t>(2048, std::max<int64_t>(1, ceil_div(per_src, 64)));
+  if (dv <= 8)
+    hipLaunchKernelGGL((xgmi_emit_kernel<8, 4>), dim3(ge, W), dim3(256), 0, st, wa, w.rows);
+  else if (dv <= 16)
+    hipLaunchKernelGGL((xgmi_emit_kernel<16, 4>), dim3(ge, W), dim3(256), 0, st, wa, w.rows);
+  else if (dv <= 32)
+    hipLaunchKernelGGL((xgmi_emit_kernel<32, 4>), dim3(ge, W), dim3(256), 0, st, wa, w.rows);
+  else
+    hipLaunchKernelGGL((xgmi_emit_kernel<64, 4>), dim3(ge, W), dim3(256), 0, st, wa, w.rows);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+}  // extern "C"

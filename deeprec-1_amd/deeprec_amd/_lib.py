@@ -54,6 +54,18 @@ class DrEvConfig(C.Structure):
     ]
 
 
+MAX_PEERS = 16
+IPC_HANDLE_BYTES = 64
+
+
+class DrXgmiPeers(C.Structure):
+    _fields_ = [
+        ("world", C.c_int32), ("rank", C.c_int32), ("cap", C.c_int64),
+        ("inbox_keys", C.c_void_p * MAX_PEERS), ("inbox_slot", C.c_void_p * MAX_PEERS),
+        ("inbox_cnt", C.c_void_p * MAX_PEERS), ("out", C.c_void_p * MAX_PEERS),
+    ]
+
+
 _P, _I64, _I32, _F32, _SZ, _U64 = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_size_t, C.c_uint64
 
 # name -> (restype, argtypes); must match include/deeprec_amd.h
@@ -119,6 +131,12 @@ SIGNATURES = {
     "dr_partition_by_owner": (_I32, [_P, _I64, _P, _I32, _P, _P, _P, _P, _SZ, _P]),
     "dr_rows_scatter": (_I32, [_P, _P, _I64, _P, _I32, _P, _P]),
     "dr_rows_pack": (_I32, [_P, _P, _I64, _P, _I32, _P, _P]),
+    "dr_ipc_export": (_I32, [_P, _P, _P]),
+    "dr_ipc_import": (_I32, [_P, _I64, _P, _P]),
+    "dr_ipc_close": (_I32, [_P]),
+    "dr_xgmi_route": (_I32, [_P, _P, _I32, _I64, _P, _P]),
+    "dr_xgmi_serve_workspace_size": (_SZ, [_I32, _I64]),
+    "dr_xgmi_serve": (_I32, [_P, _P, _I32, _I64, _P, _SZ, _P]),
     "dr_fm2": (_I32, [_P, _I64, _I32, _I32, _P, _P]),
     "dr_fm2_grad": (_I32, [_P, _P, _I64, _I32, _I32, _P, _P]),
     "dr_dot_interaction": (_I32, [_P, _I64, _I32, _I32, _P, _P]),

@@ -156,3 +156,122 @@ class ShardedLookup(object):
         out = be.pool(rows_r, rowsel, idx, koff, bag_offs, self.batch, combiner)
         self.last_stats = {"sent_keys": S, "recv_keys": R, "direct": direct}
         return out
+
+
+class XgmiBuffers(object):
+    """One rank's exchange buffers for XgmiShardedLookup (torch allocations
+    shared with the peers through HIP IPC): the inbox that requesters write
+    (key, slot) pairs into, and the [B, T*D] output that owners write rows
+    into."""
+
+    def __init__(self, world, T, batch, dim, device):
+        self.cap = T * batch
+        self.inbox_keys = torch.empty((world, self.cap), dtype=torch.int64, device=device)
+        self.inbox_slot = torch.empty((world, self.cap), dtype=torch.int32, device=device)
+        self.inbox_cnt = torch.zeros(world, dtype=torch.int64, device=device)
+        self.out = torch.empty((batch, T * dim), dtype=torch.float32, device=device)
+
+    def tensors(self):
+        return [self.inbox_keys, self.inbox_slot, self.inbox_cnt, self.out]
+
+
+class XgmiShardedLookup(object):
+    """Row-sharded one-hot embedding_lookup_sparse(sum) over xGMI peer writes.
+
+    Same partitioning and results as ShardedLookup (owner = key % world,
+    outputs bit-identical to one GPU), without staging copies: requesters
+    write (key, slot) pairs straight into the owners' inboxes and owners
+    write rows straight into the requesters' outputs (dr_xgmi_route /
+    dr_xgmi_serve).  Two stream-ordered cross-rank barriers (a one-element
+    RCCL all_reduce each) separate the phases; there is no host sync.
+
+    forward() returns this rank's persistent output buffer: it is rewritten
+    by the next forward(), so consume it (on the same stream) first.
+    peer_buffers / barrier let tests run several ranks in one process."""
+
+    def __init__(self, evs, world, rank, batch, device, group=None, peer_buffers=None,
+                 barrier=None, buffers=None):
+        if world > _lib.MAX_PEERS:
+            raise ValueError("world %d > %d" % (world, _lib.MAX_PEERS))
+        for e in evs:
+            if e.filter_freq != 0:
+                raise ValueError("XgmiShardedLookup needs filter-free EVs")
+        self.evs = evs
+        self.world, self.rank, self.batch = world, rank, batch
+        self.device = device
+        self.group = group
+        self.T = len(evs)
+        self.dim = evs[0].dim
+        self.handles = (C.c_void_p * self.T)(*[e.handle.value for e in evs])
+        self.bufs = buffers or XgmiBuffers(world, self.T, batch, self.dim, device)
+        self._bases = []
+        if world == 1 and peer_buffers is None:
+            peer_buffers = [self.bufs]
+            barrier = barrier or (lambda: None)
+        if peer_buffers is None:
+            peer_ptrs = self._exchange_ipc()
+        else:
+            peer_ptrs = [[t.data_ptr() for t in b.tensors()] for b in peer_buffers]
+        p = _lib.DrXgmiPeers()
+        p.world, p.rank, p.cap = world, rank, self.bufs.cap
+        for q in range(world):
+            p.inbox_keys[q], p.inbox_slot[q], p.inbox_cnt[q], p.out[q] = peer_ptrs[q]
+        self.peers = p
+        self.cnt_ws = torch.zeros(world, dtype=torch.int64, device=device)
+        self.wsb = lib().dr_xgmi_serve_workspace_size(world, self.bufs.cap)
+        self.ws = workspace(self.wsb, device)
+        self.flag = torch.zeros(1, dtype=torch.float32, device=device)
+        self._barrier = barrier or self._rccl_barrier
+
+    def _exchange_ipc(self):
+        mine = []
+        for t in self.bufs.tensors():
+            h = (C.c_char * _lib.IPC_HANDLE_BYTES)()
+            off = C.c_int64(0)
+            check(lib().dr_ipc_export(t.data_ptr(), h, C.byref(off)))
+            mine.append((bytes(h), off.value))
+        everyone = [None] * self.world
+        dist.all_gather_object(everyone, mine, group=self.group)
+        ptrs = []
+        for q in range(self.world):
+            if q == self.rank:
+                ptrs.append([t.data_ptr() for t in self.bufs.tensors()])
+                continue
+            row = []
+            for hb, off in everyone[q]:
+                h = (C.c_char * _lib.IPC_HANDLE_BYTES).from_buffer_copy(hb)
+                pp, base = C.c_void_p(), C.c_void_p()
+                check(lib().dr_ipc_import(h, off, C.byref(pp), C.byref(base)))
+                self._bases.append(base.value)
+                row.append(pp.value)
+            ptrs.append(row)
+        return ptrs
+
+    def _rccl_barrier(self):
+        dist.all_reduce(self.flag, group=self.group)
+
+    def route(self, ids):
+        check(lib().dr_xgmi_route(C.byref(self.peers), ptr(ids), self.T, self.batch,
+                                  ptr(self.cnt_ws), stream_handle(self.device)))
+        ops._post(self.device)
+
+    def serve(self):
+        check(lib().dr_xgmi_serve(C.byref(self.peers), self.handles, self.T, self.batch,
+                                  ptr(self.ws), self.wsb, stream_handle(self.device)))
+        ops._post(self.device)
+
+    def forward(self, ids):
+        """ids: [T, B] int64 keys (hotness 1) -> [B, T*D] pooled (sum)."""
+        if tuple(ids.shape) != (self.T, self.batch) or ids.dtype != torch.int64:
+            raise ValueError("ids must be int64 [%d, %d]" % (self.T, self.batch))
+        ids = ids.contiguous()
+        self.route(ids)
+        self._barrier()
+        self.serve()
+        self._barrier()
+        return self.bufs.out
+
+    def close(self):
+        for b in self._bases:
+            lib().dr_ipc_close(b)
+        self._bases = []

@@ -345,6 +345,48 @@ int dr_rows_pack(const float* src, const int32_t* perm, int64_t n, const int64_t
                  int dim, float* dst, void* stream);
 
 /* ------------------------------------------------------------------------ */
+/* Peer-mapped sharded one-hot lookup over xGMI (no staging copies).         */
+/* The reference's SOK all2all dispatcher moves keys to owners and rows     */
+/* back through NCCL buffers (all2all_input_dispatcher.cu:74,256-268,       */
+/* forward_functions.cuh); here every rank exposes, once, through HIP IPC:  */
+/*   inbox_keys [world][cap] int64, inbox_slot [world][cap] int32,          */
+/*   inbox_cnt [world] int64 (region src is written by requester src),      */
+/*   out [B, T*dim] fp32 (the pooled one-hot result, written by owners).    */
+/* A step is dr_xgmi_route (requester: owner = key % world; writes           */
+/* (key, slot = b*T + t) straight into the owner's inbox over xGMI) ->       */
+/* a cross-rank barrier on the stream -> dr_xgmi_serve (owner: insert-on-    */
+/* miss resolve of its inbox in its EVs, then writes each row straight into  */
+/* out[slot] of the requester) -> barrier.  Filter-free EVs, forward only.   */
+/* Outputs are position-addressed, so they equal the single-GPU lookup bit   */
+/* for bit.  EVs are not grown by serve: dr_ev_reserve beforehand; overflow  */
+/* latches DR_RESOURCE_EXHAUSTED.                                             */
+/* ------------------------------------------------------------------------ */
+#define DR_MAX_PEERS 16
+#define DR_IPC_HANDLE_BYTES 64
+/* handle of the allocation holding ptr (+ ptr's offset in it).              */
+int dr_ipc_export(const void* ptr, void* handle_out, int64_t* offset_out);
+/* maps a peer's allocation; *ptr_out = base + offset, *base_out for close.  */
+int dr_ipc_import(const void* handle, int64_t offset, void** ptr_out, void** base_out);
+int dr_ipc_close(void* base);
+
+typedef struct {
+  int32_t world, rank;
+  int64_t cap;                        /* keys per (requester, owner) region */
+  int64_t* inbox_keys[DR_MAX_PEERS];  /* rank p's inbox, mapped here         */
+  int32_t* inbox_slot[DR_MAX_PEERS];
+  int64_t* inbox_cnt[DR_MAX_PEERS];
+  float* out[DR_MAX_PEERS];           /* rank p's [B, T*dim] output          */
+} dr_xgmi_peers;
+
+/* keys [T, B] int64 (feature-major, bag b of feature t = keys[t*B + b]);   */
+/* cnt_ws: DEVICE int64[world] scratch.  Requires T*B <= cap.                */
+int dr_xgmi_route(const dr_xgmi_peers* peers, const int64_t* keys, int num_tables,
+                  int64_t batch, int64_t* cnt_ws, void* stream);
+size_t dr_xgmi_serve_workspace_size(int world, int64_t cap);
+int dr_xgmi_serve(const dr_xgmi_peers* peers, dr_ev* const* evs, int num_tables,
+                  int64_t batch, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------ */
 /* Interactions (callers of the path).                                       */
 /* ------------------------------------------------------------------------ */
 /* FM 2nd order (modelzoo/DeepFM/train.py:205-209): emb [B,F,D] -> [B,D].   */

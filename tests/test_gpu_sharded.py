@@ -131,3 +131,70 @@ def test_sharded_onehot_direct(world):
 @pytest.mark.parametrize("combiner", ["sum", "mean"])
 def test_sharded_multihot_unique(world, combiner):
     _run_world(world, False, combiner)
+
+
+# ---------------------------------------------------------------------------
+# Peer-write engine (dr_xgmi_route / dr_xgmi_serve), ranks as threads sharing
+# one GPU: "peer" buffers are plain same-device allocations here (the IPC
+# mapping is exercised by tools/xgmi_ipc_check.py as separate processes).
+# ---------------------------------------------------------------------------
+def _run_xgmi(world, steps=2):
+    import deeprec_amd as dr
+    from oracle import oracle as orc
+    from deeprec_amd.sharded import XgmiBuffers, XgmiShardedLookup
+    dr.load()
+    rng = np.random.default_rng(17 + world)
+    evs_all, bufs = [], []
+    for r in range(world):
+        own = np.arange(r, KEYSPACE // 2, world, dtype=np.int64)
+        evs = []
+        for t in range(T):
+            ev = dr.EmbeddingVariable("xg%d_%d_%d" % (world, r, t), D, DEFAULT, device=DEV)
+            ev.insert(torch.as_tensor(own, device=DEV), torch.as_tensor(_vals(t, own), device=DEV))
+            evs.append(ev)
+        evs_all.append(evs)
+        bufs.append(XgmiBuffers(world, T, B, D, DEV))
+    bar = threading.Barrier(world)
+    engines = [XgmiShardedLookup(evs_all[r], world, r, B, torch.device(DEV), peer_buffers=bufs,
+                                 barrier=bar.wait, buffers=bufs[r]) for r in range(world)]
+    allk = np.arange(0, KEYSPACE // 2, dtype=np.int64)
+    ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+    for step in range(steps):
+        ids = [rng.integers(0, KEYSPACE, (T, B)).astype(np.int64) for _ in range(world)]
+        for r in range(world):
+            ids[r][:, :5] = 13 + step                 # duplicates across ranks and rows
+        outs = [None] * world
+        errs = []
+
+        def run(r):
+            try:
+                o = engines[r].forward(torch.as_tensor(ids[r], device=DEV))
+                bar.wait()                           # every owner has written every output
+                outs[r] = o.cpu().numpy()
+            except Exception as e:
+                errs.append(e)
+                bar.abort()
+
+        th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(120)
+        if errs:
+            raise errs[0]
+        dr.status_check()
+        for r in range(world):
+            for t in range(T):
+                ref_ev = orc.EV(D, DEFAULT)
+                ref_ev.insert(allk, _vals(t, allk))
+                ref = orc.embedding_lookup_sparse(ref_ev, ind, ids[r][t], B, combiner="sum")
+                np.testing.assert_array_equal(outs[r][:, t * D:(t + 1) * D], ref)
+    for r in range(world):
+        for ev in evs_all[r]:
+            k = ev.export()[0].cpu().numpy()
+            assert np.all(k % world == r)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_xgmi_peer_write_engine(world):
+    _run_xgmi(world)
