@@ -173,23 +173,39 @@ def main():
                 if engine is not None:
                     engine.close()
                 engine = None
+        a2a = ShardedLookup(evs, world, rank, B, dev)
+        if staged:
+            def staged_a2a(out, inp, out_splits=None, in_splits=None):
+                o = torch.empty(out.shape, dtype=out.dtype)
+                dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits)
+                out.copy_(o)
+                return out
+            a2a._a2a = staged_a2a
+        elif world == 1:
+            a2a._a2a = lambda out, inp, os_=None, is_=None: out.copy_(inp)
         if engine is None:
-            engine = ShardedLookup(evs, world, rank, B, dev)
+            engine = a2a
             engine_kind = "RCCL all-to-all"
-            if staged:
-                def staged_a2a(out, inp, out_splits=None, in_splits=None):
-                    o = torch.empty(out.shape, dtype=out.dtype)
-                    dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits)
-                    out.copy_(o)
-                    return out
-                engine._a2a = staged_a2a
-            elif world == 1:
-                engine._a2a = lambda out, inp, os_=None, is_=None: out.copy_(inp)
         log("sharded engine: %s" % engine_kind)
     else:
         engine = None
         keyspace = R
     batches = make_batches(4, T, B, keyspace, args.zipf, 2021 + 7919 * rank, dev)
+    engine_check = None
+    if engine is not None and engine is not a2a:
+        # the peer-write engine must reproduce the all-to-all engine bit for bit
+        with torch.no_grad():
+            ref = a2a.forward(batches[0]).clone()
+            same = int(torch.equal(engine.forward(batches[0]), ref))
+        if world > 1:
+            flag = torch.tensor([same], dtype=torch.int32, device="cpu" if staged else dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            same = int(flag.item())
+        engine_check = "xgmi output == all-to-all output, step 0, all ranks: %s" % bool(same)
+        log(engine_check)
+        if not same:
+            engine.close()
+            engine, engine_kind = a2a, "RCCL all-to-all (xgmi check failed)"
     seg = torch.arange(B, dtype=torch.int32, device=dev)
     ind = torch.stack([torch.arange(B, device=dev), torch.zeros(B, dtype=torch.int64, device=dev)], 1)
     static_ids = torch.empty((T, B), dtype=torch.int64, device=dev)
@@ -317,7 +333,7 @@ def main():
                                       "owner resolve, rows back" % engine_kind
                                       if world > 1 else ""),
                        "global_batch": B * world, "tables": T, "rows_per_gpu": R, "dim": D,
-                       "engine": engine_kind,
+                       "engine": engine_kind, "engine_check": engine_check,
                        "parallelism": "row-sharded tables x%d, data-parallel batch" % world},
             "samples_per_s": round(value / T, 1),
             "roofline": roof,
