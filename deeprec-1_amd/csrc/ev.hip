@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <atomic>
 #include <cmath>
 #include <mutex>
@@ -396,6 +397,8 @@ struct InitGroup {
   int64_t koff[DR_MAX_GROUP + 1];
   const int64_t* n_dev[DR_MAX_GROUP];
   const int32_t* tags;
+  int64_t* mtop[DR_MAX_GROUP];  // row counters to mirror (nullptr: none)
+  int64_t* mdst[DR_MAX_GROUP];  // pinned host mirrors
 };
 
 // Wave-cooperative: each lane tests one key's flag, the wave ballots and then
@@ -406,6 +409,12 @@ __global__ void ev_init_rows_kernel(InitGroup g, int T, int64_t dim,
                                     const uint8_t* __restrict__ init) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
+  if (blockIdx.x == 0 && threadIdx.x < T && g.mdst[threadIdx.x]) {
+    // the resolve kernel before this one has finished: the counter is final
+    const int64_t top = __hip_atomic_load(g.mtop[threadIdx.x], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(g.mdst[threadIdx.x], top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   bool need = false;
   int t = 0;
   int64_t li = i;
@@ -570,21 +579,76 @@ struct OptScalars {
   float lr, beta1, beta2, eps, alpha;
 };
 
-template <int G, int OPT>
-__global__ __launch_bounds__(256) void ev_apply_kernel(EvDesc e, ApplyCols cols, int64_t dim,
-                                                       const int64_t* __restrict__ keys,
-                                                       const float* __restrict__ grad, int64_t n,
-                                                       const int64_t* n_dev, int64_t gs,
-                                                       int64_t steps_to_live, OptScalars sc,
-                                                       int* st) {
-  const int64_t i = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G;
-  const bool live = i < eff_n(n, n_dev);
+// Two phases per wave of 64 keys.  Phase 1, lane per key: LookupOrCreate
+// with the global step / filter admission / first-touch column mask (the
+// dependent hash probes of 64 keys overlap).  Phase 2: groups of G lanes
+// update 64/G rows at a time with VEC-wide loads/stores; every element is
+// the reference's scalar formula with separate fp32 roundings.
+template <int OPT, int VEC, int G>
+__device__ __forceinline__ float apply_one(float gv, float w, float* a1, float* a2,
+                                           const OptScalars& sc) {
+  if (OPT == OPT_SGD) {
+    const float p = sc.lr * gv;  // v -= lr * g  (training_ali_ops.cc:1663)
+    return w - p;
+  } else if (OPT == OPT_ADAGRAD) {  // training_ali_ops.cc:131-132
+    float a = *a1;
+    const float g2 = gv * gv;
+    a = a + g2;
+    const float lg_ = sc.lr * gv;
+    const float rs = 1.0f / sqrtf(a);
+    const float up = lg_ * rs;
+    *a1 = a;
+    return w - up;
+  } else {  // OPT_ADAM, training_ali_ops.cc:952-958
+    float m = *a1;
+    float v = *a2;
+    float t1 = gv - m;
+    t1 = t1 * (1.0f - sc.beta1);
+    m = m + t1;
+    float t2 = gv * gv;
+    t2 = t2 - v;
+    t2 = t2 * (1.0f - sc.beta2);
+    v = v + t2;
+    const float num = m * sc.alpha;
+    const float den = sqrtf(v) + sc.eps;
+    *a1 = m;
+    *a2 = v;
+    return w - num / den;
+  }
+}
+
+// One table of a grouped apply launch (blockIdx.y selects it).
+struct ApplyTable {
+  EvDesc e;
+  ApplyCols cols;
+  const int64_t* keys;
+  const float* grad;
+  int64_t n;
+  const int64_t* n_dev;
+  int64_t steps_to_live;
+};
+static constexpr int kApplyGroup = 16;  // keeps the kernel arguments < 4 KiB
+struct ApplyGroup {
+  ApplyTable t[kApplyGroup];
+};
+
+template <int OPT, int VEC, int G>
+__global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t dim, int64_t gs,
+                                                       OptScalars sc, int* st) {
+  const ApplyTable& at = ag.t[blockIdx.y];
+  const EvDesc& e = at.e;
+  const ApplyCols& cols = at.cols;
+  const int64_t* __restrict__ keys = at.keys;
+  const float* __restrict__ grad = at.grad;
+  const int64_t steps_to_live = at.steps_to_live;
   const int lane = threadIdx.x & 63;
-  const int leader = lane & ~(G - 1);
-  const int lg = lane & (G - 1);
+  const int64_t base = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63);
+  const int64_t ne = eff_n(at.n, at.n_dev);
+  if (base >= ne) return;  // wave-uniform
+  const int64_t i = base + lane;
   int64_t row = -1;
   int initmask = 0;
-  if (live && lg == 0) {
+  if (i < ne) {
     const uint64_t key = (uint64_t)keys[i];
     bool ok = true;
     if (e.k_hash > 0 && bloom_min_freq(e, key) < e.filter_freq) ok = false;
@@ -612,45 +676,56 @@ __global__ __launch_bounds__(256) void ev_apply_kernel(EvDesc e, ApplyCols cols,
       }
     }
   }
-  row = __shfl(row, leader, 64);
-  initmask = __shfl(initmask, leader, 64);
-  if (!live || row < 0) return;
-  float* v0 = cols.pool[0] + row * dim;
-  float* v1 = cols.ncol > 1 ? cols.pool[1] + row * dim : nullptr;
-  float* v2 = cols.ncol > 2 ? cols.pool[2] + row * dim : nullptr;
-  const float* g = grad + i * dim;
-  for (int64_t c = lg; c < dim; c += G) {
-    const float gv = g[c];
-    float w = (initmask & 1) ? cols.dflt[0][c] : v0[c];
-    if (OPT == OPT_SGD) {
-      const float p = sc.lr * gv;  // v -= lr * g  (training_ali_ops.cc:1663)
-      w = w - p;
-    } else if (OPT == OPT_ADAGRAD) {  // training_ali_ops.cc:131-132
-      float a = (initmask & 2) ? cols.dflt[1][c] : v1[c];
-      const float g2 = gv * gv;
-      a = a + g2;
-      const float lg_ = sc.lr * gv;
-      const float rs = 1.0f / sqrtf(a);
-      const float up = lg_ * rs;
-      w = w - up;
-      v1[c] = a;
-    } else {  // OPT_ADAM, training_ali_ops.cc:952-958
-      float m = (initmask & 2) ? cols.dflt[1][c] : v1[c];
-      float v = (initmask & 4) ? cols.dflt[2][c] : v2[c];
-      float t1 = gv - m;
-      t1 = t1 * (1.0f - sc.beta1);
-      m = m + t1;
-      float t2 = gv * gv;
-      t2 = t2 - v;
-      t2 = t2 * (1.0f - sc.beta2);
-      v = v + t2;
-      const float num = m * sc.alpha;
-      const float den = sqrtf(v) + sc.eps;
-      w = w - num / den;
-      v1[c] = m;
-      v2[c] = v;
+  constexpr int P = 64 / G;                          // rows updated together
+  constexpr int U = OPT == OPT_ADAM ? 2 : 4;          // row batches in flight
+  const int sub = lane / G;
+  const int lg = lane % G;
+  const int64_t dv = dim / VEC;
+  using V = typename std::conditional<VEC == 4, float4, float>::type;
+  const V* d0 = reinterpret_cast<const V*>(cols.dflt[0]);
+  const V* d1 = reinterpret_cast<const V*>(cols.dflt[1]);
+  const V* d2 = reinterpret_cast<const V*>(cols.dflt[2]);
+  for (int k0 = 0; k0 < 64; k0 += P * U) {
+    // cross-lane reads with every lane active (a disabled source lane reads 0)
+    int64_t rr[U];
+    int imq[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int k = k0 + q * P + sub;
+      rr[q] = __shfl(row, k, 64);
+      imq[q] = __shfl(initmask, k, 64);
+      if (base + k >= ne) rr[q] = -1;
     }
-    v0[c] = w;
+    for (int64_t c = lg; c < dv; c += G) {
+      V gv[U], w[U], a1[U], a2[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q) {  // all loads of U rows first
+        const int k = k0 + q * P + sub;
+        const int im = imq[q];
+        if (rr[q] < 0) continue;
+        gv[q] = reinterpret_cast<const V*>(grad + (base + k) * dim)[c];
+        w[q] = (im & 1) ? d0[c] : reinterpret_cast<const V*>(cols.pool[0] + rr[q] * dim)[c];
+        if (OPT != OPT_SGD)
+          a1[q] = (im & 2) ? d1[c] : reinterpret_cast<const V*>(cols.pool[1] + rr[q] * dim)[c];
+        if (OPT == OPT_ADAM)
+          a2[q] = (im & 4) ? d2[c] : reinterpret_cast<const V*>(cols.pool[2] + rr[q] * dim)[c];
+      }
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        if (rr[q] < 0) continue;
+        if constexpr (VEC == 4) {
+          w[q].x = apply_one<OPT, VEC, G>(gv[q].x, w[q].x, &a1[q].x, &a2[q].x, sc);
+          w[q].y = apply_one<OPT, VEC, G>(gv[q].y, w[q].y, &a1[q].y, &a2[q].y, sc);
+          w[q].z = apply_one<OPT, VEC, G>(gv[q].z, w[q].z, &a1[q].z, &a2[q].z, sc);
+          w[q].w = apply_one<OPT, VEC, G>(gv[q].w, w[q].w, &a1[q].w, &a2[q].w, sc);
+        } else {
+          w[q] = apply_one<OPT, VEC, G>(gv[q], w[q], &a1[q], &a2[q], sc);
+        }
+        if (OPT != OPT_SGD) reinterpret_cast<V*>(cols.pool[1] + rr[q] * dim)[c] = a1[q];
+        if (OPT == OPT_ADAM) reinterpret_cast<V*>(cols.pool[2] + rr[q] * dim)[c] = a2[q];
+        reinterpret_cast<V*>(cols.pool[0] + rr[q] * dim)[c] = w[q];
+      }
+    }
   }
 }
 
@@ -815,20 +890,31 @@ static int reserve(EvShared* s, int64_t n, hipStream_t st) {
   return DR_OK;
 }
 
-static void post_call(EvShared* s, hipStream_t st) {
+// Mirror of the device row counter into pinned host memory (capacity
+// accounting without syncs).  want_mirror() says whether a fresh copy should
+// be issued now; the copy is either a DMA (post_call) or written by the
+// stream's next init kernel (resolve paths), followed by mirrored().
+static bool want_mirror(EvShared* s, hipStream_t st) {
   static const bool no_mirror = getenv("DR_NO_MIRROR") != nullptr;
-  if (no_mirror) return;
-  std::lock_guard<std::mutex> g(s->mu);
-  if (s->copy_pending) return;
+  if (no_mirror || s->copy_pending) return false;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   (void)hipStreamIsCapturing(st, &cs);
-  if (cs != hipStreamCaptureStatusNone) return;
-  if (hipMemcpyAsync(s->pinned_top, s->top, sizeof(int64_t), hipMemcpyDeviceToHost, st) !=
-      hipSuccess)
-    return;
+  return cs == hipStreamCaptureStatusNone;
+}
+
+static void mirrored(EvShared* s, hipStream_t st) {
   if (hipEventRecord(s->copy_ev, st) != hipSuccess) return;
   s->copy_pending = true;
   s->adds_since_copy = 0;
+}
+
+static void post_call(EvShared* s, hipStream_t st) {
+  std::lock_guard<std::mutex> g(s->mu);
+  if (!want_mirror(s, st)) return;
+  if (hipMemcpyAsync(s->pinned_top, s->top, sizeof(int64_t), hipMemcpyDeviceToHost, st) !=
+      hipSuccess)
+    return;
+  mirrored(s, st);
 }
 
 struct ResolveWs {
@@ -892,10 +978,113 @@ static int resolve_grouped(dr_ev* const* evs, int T, const int64_t* keys, const 
                      rows_out, w.init, w.badd, stw);
   if (any_bloom)
     hipLaunchKernelGGL(ev_bloom_add_kernel, dim3(blocks), dim3(256), 0, st, g, T, keys, w.badd);
+  // counter mirrors ride on the init kernel (no extra copy launches)
+  EvShared* mir[DR_MAX_GROUP];
+  int nmir = 0;
+  for (int t = 0; t < T; ++t) {
+    EvShared* sh = evs[t]->sh;
+    bool seen = false;
+    for (int q = 0; q < nmir; ++q) seen = seen || mir[q] == sh;
+    if (seen) continue;
+    sh->mu.lock();
+    if (want_mirror(sh, st)) {
+      ig.mtop[t] = sh->top;
+      ig.mdst[t] = sh->pinned_top;
+      mir[nmir++] = sh;
+    } else {
+      sh->mu.unlock();
+    }
+  }
   hipLaunchKernelGGL(ev_init_rows_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, st, ig,
                      T, evs[0]->sh->dim, rows_out, w.init);
-  DR_LAUNCH_CHECK();
-  for (int t = 0; t < T; ++t) post_call(evs[t]->sh, st);
+  const hipError_t le = hipGetLastError();
+  for (int q = 0; q < nmir; ++q) {
+    if (le == hipSuccess) mirrored(mir[q], st);
+    mir[q]->mu.unlock();
+  }
+  if (le != hipSuccess) {
+    set_error("kernel launch failed: %s", hipGetErrorString(le));
+    return DR_INTERNAL;
+  }
+  return DR_OK;
+}
+
+// Grouped sparse apply: T tables (same dim) per launch, blockIdx.y = table,
+// in chunks of kApplyGroup.  A single-table apply is a group of one.
+static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* const* s2, int T,
+                         OptScalars sc, const float* const* grads, const int64_t* const* keys,
+                         const int64_t* n_host, const int64_t* const* n_dev, int64_t gs,
+                         hipStream_t st) {
+  DR_REQUIRE(T >= 1 && vars && grads && keys && n_host, DR_INVALID_ARGUMENT, "bad argument");
+  int* stw = status_word();
+  DR_REQUIRE(stw, DR_INTERNAL, "status word unavailable");
+  const int64_t dim = vars[0] ? vars[0]->sh->dim : 0;
+  const int ncol = opt == OPT_SGD ? 1 : (opt == OPT_ADAGRAD ? 2 : 3);
+  for (int c0 = 0; c0 < T; c0 += kApplyGroup) {
+    const int tn = std::min(kApplyGroup, T - c0);
+    ApplyGroup ag;
+    memset(&ag, 0, sizeof(ag));
+    int64_t nmax = 0;
+    bool aligned = dim % 4 == 0;
+    for (int j = 0; j < tn; ++j) {
+      const int t = c0 + j;
+      dr_ev* var = vars[t];
+      DR_REQUIRE(var && var->col == 0, DR_INVALID_ARGUMENT, "table %d: var must be a primary EV",
+                 t);
+      EvShared* s = var->sh;
+      DR_REQUIRE(s->dim == dim, DR_INVALID_ARGUMENT, "grouped apply needs equal dims");
+      dr_ev* cv[3] = {var, s1 ? s1[t] : nullptr, s2 ? s2[t] : nullptr};
+      ApplyTable& a = ag.t[j];
+      a.cols.ncol = ncol;
+      for (int c = 0; c < ncol; ++c) {
+        DR_REQUIRE(cv[c] && cv[c]->sh == s, DR_INVALID_ARGUMENT,
+                   "table %d: slot EV missing or not sharing the primary's keys", t);
+        a.cols.cols[c] = cv[c]->col;
+        a.cols.pool[c] = s->pools[cv[c]->col];
+        a.cols.dflt[c] = s->defaults[cv[c]->col];
+        aligned = aligned && ((((uintptr_t)a.cols.pool[c]) | ((uintptr_t)a.cols.dflt[c])) & 15) == 0;
+      }
+      aligned = aligned && (((uintptr_t)grads[t]) & 15) == 0;
+      a.e = make_desc(var);
+      a.keys = keys[t];
+      a.grad = grads[t];
+      a.n = n_host[t];
+      a.n_dev = n_dev ? n_dev[t] : nullptr;
+      a.steps_to_live = s->steps_to_live;
+      if (a.n > 0) {
+        int rc = reserve(s, a.n, st);
+        if (rc) return rc;
+      }
+      nmax = std::max(nmax, a.n);
+    }
+    if (nmax == 0) continue;
+    const dim3 grid((unsigned)ceil_div(nmax, 256), (unsigned)tn);
+#define DR_APPLY(VEC, G)                                                                    \
+  do {                                                                                     \
+    if (opt == OPT_SGD)                                                                    \
+      hipLaunchKernelGGL((ev_apply_kernel<OPT_SGD, VEC, G>), grid, dim3(256), 0, st, ag,    \
+                         dim, gs, sc, stw);                                                 \
+    else if (opt == OPT_ADAGRAD)                                                           \
+      hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAGRAD, VEC, G>), grid, dim3(256), 0, st, ag,\
+                         dim, gs, sc, stw);                                                 \
+    else                                                                                   \
+      hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAM, VEC, G>), grid, dim3(256), 0, st, ag,   \
+                         dim, gs, sc, stw);                                                 \
+  } while (0)
+    if (aligned && dim / 4 <= 8)
+      DR_APPLY(4, 8);
+    else if (aligned && dim / 4 <= 16)
+      DR_APPLY(4, 16);
+    else if (aligned && dim / 4 <= 32)
+      DR_APPLY(4, 32);
+    else if (aligned)
+      DR_APPLY(4, 64);
+    else
+      DR_APPLY(1, 64);
+#undef DR_APPLY
+    DR_LAUNCH_CHECK();
+  }
+  // no counter mirror here: the step's next resolve refreshes it
   return DR_OK;
 }
 
@@ -904,37 +1093,14 @@ static int apply_common(int opt, dr_ev* var, dr_ev* s1, dr_ev* s2, OptScalars sc
                         int64_t gs, hipStream_t st) {
   DR_REQUIRE(var && var->col == 0, DR_INVALID_ARGUMENT, "var must be a primary EV");
   if (n == 0) return DR_OK;
-  EvShared* s = var->sh;
-  DR_REQUIRE(!s1 || s1->sh == s, DR_INVALID_ARGUMENT, "slot EV must share the primary's keys");
-  DR_REQUIRE(!s2 || s2->sh == s, DR_INVALID_ARGUMENT, "slot EV must share the primary's keys");
-  int rc = reserve(s, n, st);
-  if (rc) return rc;
-  int* stw = status_word();
-  ApplyCols cols;
-  memset(&cols, 0, sizeof(cols));
-  dr_ev* evs[3] = {var, s1, s2};
-  cols.ncol = opt == OPT_SGD ? 1 : (opt == OPT_ADAGRAD ? 2 : 3);
-  for (int c = 0; c < cols.ncol; ++c) {
-    DR_REQUIRE(evs[c], DR_INVALID_ARGUMENT, "missing slot EV");
-    cols.cols[c] = evs[c]->col;
-    cols.pool[c] = s->pools[evs[c]->col];
-    cols.dflt[c] = s->defaults[evs[c]->col];
-  }
-  EvDesc e = make_desc(var);
-  constexpr int G = 64;
-  const unsigned blocks = (unsigned)ceil_div(n, 256 / G);
-  if (opt == OPT_SGD)
-    hipLaunchKernelGGL((ev_apply_kernel<G, OPT_SGD>), dim3(blocks), dim3(256), 0, st, e, cols,
-                       s->dim, keys, grad, n, n_dev, gs, s->steps_to_live, sc, stw);
-  else if (opt == OPT_ADAGRAD)
-    hipLaunchKernelGGL((ev_apply_kernel<G, OPT_ADAGRAD>), dim3(blocks), dim3(256), 0, st, e, cols,
-                       s->dim, keys, grad, n, n_dev, gs, s->steps_to_live, sc, stw);
-  else
-    hipLaunchKernelGGL((ev_apply_kernel<G, OPT_ADAM>), dim3(blocks), dim3(256), 0, st, e, cols,
-                       s->dim, keys, grad, n, n_dev, gs, s->steps_to_live, sc, stw);
-  DR_LAUNCH_CHECK();
-  post_call(s, st);
-  return DR_OK;
+  dr_ev* v[1] = {var};
+  dr_ev* a[1] = {s1};
+  dr_ev* b[1] = {s2};
+  const float* g[1] = {grad};
+  const int64_t* k[1] = {keys};
+  const int64_t nh[1] = {n};
+  const int64_t* nd[1] = {n_dev};
+  return apply_grouped(opt, v, a, b, 1, sc, g, k, nh, nd, gs, st);
 }
 
 }  // namespace dr
@@ -1377,6 +1543,23 @@ int dr_ev_apply_adagrad(dr_ev* var, dr_ev* accum, float lr, const float* grad,
   dr::OptScalars sc = {lr, 0, 0, 0, 0};
   return dr::apply_common(dr::OPT_ADAGRAD, var, accum, nullptr, sc, grad, keys, n, n_dev,
                           global_step, dr::S(stream));
+}
+
+int dr_ev_apply_grouped(int optimizer, dr_ev* const* vars, dr_ev* const* slot1,
+                        dr_ev* const* slot2, int num_tables, const float* const* grads,
+                        const int64_t* const* keys, const int64_t* n_host,
+                        const int64_t* const* n_dev, float lr, float beta1_power,
+                        float beta2_power, float beta1, float beta2, float epsilon,
+                        int64_t global_step, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(optimizer >= DR_OPT_SGD && optimizer <= DR_OPT_ADAM, DR_INVALID_ARGUMENT,
+             "unknown optimizer %d", optimizer);
+  OptScalars sc = {lr, beta1, beta2, epsilon, 0.f};
+  if (optimizer == DR_OPT_ADAM) sc.alpha = lr * sqrtf(1.0f - beta2_power) / (1.0f - beta1_power);
+  const int opt = optimizer == DR_OPT_SGD ? OPT_SGD
+                                          : (optimizer == DR_OPT_ADAGRAD ? OPT_ADAGRAD : OPT_ADAM);
+  return apply_grouped(opt, vars, slot1, slot2, num_tables, sc, grads, keys, n_host, n_dev,
+                       global_step, S(stream));
 }
 
 int dr_ev_apply_adam(dr_ev* var, dr_ev* m, dr_ev* v, float beta1_power, float beta2_power,

@@ -742,6 +742,139 @@ static int segsum_driver(const int32_t* keyseg, int64_t n, int64_t num_out, cons
                           U_dev, dim, mode, out, s, st);
 }
 
+// ---- grouped pooling backward (dr_pool_grad_grouped) -----------------------
+// One stable radix sort of all features' nnz by global unique row
+// (koff[t] + idx[k]) replaces T per-feature sorts; one CSR pass sums them.
+struct GradGroup {
+  dr_pool_grad_desc d[DR_MAX_GROUP];
+  int64_t koff[DR_MAX_GROUP + 1];
+};
+
+__device__ __forceinline__ int grad_table(const GradGroup& g, int T, int64_t i) {
+  int t = 0;
+  while (t + 1 < T && i >= g.koff[t + 1]) ++t;
+  return t;
+}
+
+__global__ void grad_keys_kernel(GradGroup g, int T, uint64_t* __restrict__ kin,
+                                 int32_t* __restrict__ vin, int* st) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.koff[T]) return;
+  const int t = grad_table(g, T, i);
+  const int64_t k = i - g.koff[t];
+  int64_t u = g.d[t].idx[k];
+  if (u < 0 || u >= g.d[t].nnz) {
+    latch(st, DR_INVALID_ARGUMENT);
+    u = g.koff[T] - g.koff[t];  // sentinel bucket past the end
+  }
+  kin[i] = (uint64_t)(g.koff[t] + u);
+  vin[i] = (int32_t)i;
+}
+
+// A group owns NB consecutive unique rows and issues the first element's
+// row load of all NB before summing (most rows of one-hot features have a
+// single element: NB loads in flight instead of one dependent chain each).
+template <int VEC, int G, int CPL, int NB>
+__global__ __launch_bounds__(256) void grad_csr_grouped_kernel(GradGroup g, int T, int64_t B,
+                                                               const int32_t* __restrict__ perm,
+                                                               const int32_t* __restrict__ off,
+                                                               int dim, float* __restrict__ out,
+                                                               int* st) {
+  constexpr int GPB = 256 / G;
+  const int64_t u0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * NB;
+  const int64_t N = g.koff[T];
+  if (u0 >= N) return;
+  const int lg = threadIdx.x % G;
+  const int dv = dim / VEC;
+  using R = Row<VEC, G, CPL>;
+  using V = typename VecT<VEC>::T;
+  R x[NB];
+  int tq[NB];
+  int32_t j0[NB], j1[NB];
+  const float* rp0[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    const int64_t u = u0 + q;
+    j0[q] = j1[q] = 0;
+    rp0[q] = nullptr;
+    tq[q] = 0;
+    if (u < N) {
+      const int t = grad_table(g, T, u);
+      tq[q] = t;
+      const dr_pool_grad_desc& d = g.d[t];
+      if (u - g.koff[t] < *d.num_unique) {
+        j0[q] = off[u];
+        j1[q] = off[u + 1];
+        if (j1[q] > j0[q]) {
+          const int64_t k = (int64_t)perm[j0[q]] - g.koff[t];
+          const int64_t r = d.seg ? d.seg[k * d.seg_stride] : k;
+          if (r >= 0 && r < B)
+            rp0[q] = d.top_grad + r * d.top_stride;
+          else
+            latch(st, DR_INVALID_ARGUMENT);
+        }
+      } else {
+        j0[q] = j1[q] = -1;  // past U_t: not written
+      }
+    } else {
+      j0[q] = j1[q] = -1;
+    }
+    load_row<VEC, G, CPL>(x[q], rp0[q], lg, dv);
+  }
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    if (j0[q] < 0) continue;
+    const dr_pool_grad_desc& d = g.d[tq[q]];
+    const int mode = d.combiner == DR_COMBINER_SUM ? 0 : (d.combiner == DR_COMBINER_MEAN ? 1 : 2);
+    R acc;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<V>();
+    for (int32_t j = j0[q]; j < j1[q]; ++j) {
+      R y;
+      int64_t r = -1;
+      if (j == j0[q]) {
+        y = x[q];
+        if (rp0[q]) r = (rp0[q] - d.top_grad) / d.top_stride;
+      } else {
+        const int64_t k = (int64_t)perm[j] - g.koff[tq[q]];
+        r = d.seg ? d.seg[k * d.seg_stride] : k;
+        const float* rp = nullptr;
+        if (r >= 0 && r < B)
+          rp = d.top_grad + r * d.top_stride;
+        else
+          latch(st, DR_INVALID_ARGUMENT);
+        load_row<VEC, G, CPL>(y, rp, lg, dv);
+        if (!rp) r = -1;
+      }
+      if (mode == 0) {
+        acc_add(acc, y);  // UnsortedSegmentSum order: 0 + x_0 + x_1 ...
+      } else {
+        const int32_t cnt = (r >= 0 && d.bag_off) ? d.bag_off[r + 1] - d.bag_off[r] : 1;
+        if (cnt != 1) {
+          const float sc =
+              mode == 2 ? (float)(1.0 / sqrt((double)cnt)) : (float)(1.0 / (double)cnt);
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) y.v[c] = vmul(y.v[c], sc);
+        }
+        if (j == j0[q])
+          acc = y;
+        else
+          acc_add(acc, y);
+      }
+    }
+    store_row<VEC, G, CPL>(acc, out + (u0 + q) * (int64_t)dim, lg, dv);
+  }
+}
+
+template <int VEC, int G, int CPL>
+static void launch_grad_csr(const GradGroup& g, int T, int64_t B, const int32_t* perm,
+                            const int32_t* off, int dim, float* out, hipStream_t s, int* st) {
+  constexpr int NB = 4;
+  const int64_t blocks = ceil_div(ceil_div(g.koff[T] > 0 ? g.koff[T] : 1, NB), 256 / G);
+  hipLaunchKernelGGL((grad_csr_grouped_kernel<VEC, G, CPL, NB>), dim3((unsigned)blocks),
+                     dim3(256), 0, s, g, T, B, perm, off, dim, out, st);
+}
+
 }  // namespace dr
 
 // ===========================================================================
@@ -941,6 +1074,73 @@ size_t dr_pool_grad_workspace_size(int64_t n) {
   size_t used = 0;
   dr::carve_segsum(nullptr, n, n, &used);
   return used;
+}
+
+size_t dr_pool_grad_grouped_workspace_size(int64_t total_nnz) {
+  return dr_pool_grad_workspace_size(total_nnz);
+}
+
+int dr_pool_grad_grouped(const dr_pool_grad_desc* descs_host, int num_tables, int64_t batch,
+                         int dim, float* grad_unique, void* ws, size_t ws_bytes, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(descs_host && num_tables >= 1 && num_tables <= DR_MAX_GROUP && dim > 0 &&
+                 batch >= 0 && grad_unique,
+             DR_INVALID_ARGUMENT, "bad argument");
+  GradGroup g;
+  memset(&g, 0, sizeof(g));
+  g.koff[0] = 0;
+  bool aligned = dim % 4 == 0 && ((uintptr_t)grad_unique & 15) == 0;
+  for (int t = 0; t < num_tables; ++t) {
+    const dr_pool_grad_desc& d = descs_host[t];
+    DR_REQUIRE(d.top_grad && d.idx && d.num_unique && d.nnz >= 0, DR_INVALID_ARGUMENT,
+               "table %d: missing pointers", t);
+    DR_REQUIRE(d.combiner == DR_COMBINER_SUM || d.bag_off || !d.seg, DR_INVALID_ARGUMENT,
+               "table %d: mean/sqrtn of multi-hot bags need bag_off", t);
+    g.d[t] = d;
+    g.koff[t + 1] = g.koff[t] + d.nnz;
+    aligned = aligned && ((uintptr_t)d.top_grad & 15) == 0 && d.top_stride % 4 == 0;
+  }
+  const int64_t n = g.koff[num_tables];
+  DR_REQUIRE(n < (1ll << 31), DR_INVALID_ARGUMENT, "too many nnz");
+  DR_REQUIRE(ws_bytes >= dr_pool_grad_grouped_workspace_size(n), DR_INVALID_ARGUMENT,
+             "workspace too small");
+  if (n == 0) return DR_OK;
+  int* st = status_word();
+  DR_REQUIRE(st, DR_INTERNAL, "status word unavailable");
+  hipStream_t s = S(stream);
+  SegSumWs w = carve_segsum(ws, n, n, nullptr);
+  hipLaunchKernelGGL(grad_keys_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, g,
+                     num_tables, w.kin, w.vin, st);
+  DR_LAUNCH_CHECK();
+  int rc = dr_sort_pairs(w.kin, w.vin, w.kout, w.perm, n, 0, bits_for(n), w.sort_ws,
+                         w.sort_bytes, stream);
+  if (rc) return rc;
+  rc = launch_bag_offsets<uint64_t>(w.kout, 1, n, nullptr, n + 1, w.off, s);
+  if (rc) return rc;
+  if (aligned) {
+    const int d4 = dim / 4;
+    if (d4 <= 8)
+      launch_grad_csr<4, 8, 1>(g, num_tables, batch, w.perm, w.off, dim, grad_unique, s, st);
+    else if (d4 <= 16)
+      launch_grad_csr<4, 16, 1>(g, num_tables, batch, w.perm, w.off, dim, grad_unique, s, st);
+    else if (d4 <= 32)
+      launch_grad_csr<4, 32, 1>(g, num_tables, batch, w.perm, w.off, dim, grad_unique, s, st);
+    else if (d4 <= 64)
+      launch_grad_csr<4, 64, 1>(g, num_tables, batch, w.perm, w.off, dim, grad_unique, s, st);
+    else if (d4 <= 256)
+      launch_grad_csr<4, 64, 4>(g, num_tables, batch, w.perm, w.off, dim, grad_unique, s, st);
+    else
+      DR_REQUIRE(false, DR_INVALID_ARGUMENT, "dim %d unsupported", dim);
+  } else {
+    if (dim <= 64)
+      launch_grad_csr<1, 64, 1>(g, num_tables, batch, w.perm, w.off, dim, grad_unique, s, st);
+    else if (dim <= 256)
+      launch_grad_csr<1, 64, 4>(g, num_tables, batch, w.perm, w.off, dim, grad_unique, s, st);
+    else
+      DR_REQUIRE(false, DR_INVALID_ARGUMENT, "dim %d unsupported", dim);
+  }
+  DR_LAUNCH_CHECK();
+  return DR_OK;
 }
 
 // Backward of dr_pool_grouped (ORDER_ALI / TF grad semantics) for one table:

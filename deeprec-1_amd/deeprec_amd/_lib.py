@@ -45,6 +45,14 @@ class DrPoolDesc(C.Structure):
     ]
 
 
+class DrPoolGradDesc(C.Structure):
+    _fields_ = [
+        ("top_grad", C.c_void_p), ("top_stride", C.c_int64), ("bag_off", C.c_void_p),
+        ("seg", C.c_void_p), ("seg_stride", C.c_int64), ("idx", C.c_void_p), ("nnz", C.c_int64),
+        ("num_unique", C.c_void_p), ("combiner", C.c_int32),
+    ]
+
+
 class DrEvConfig(C.Structure):
     _fields_ = [
         ("dim", C.c_int64), ("capacity", C.c_int64), ("steps_to_live", C.c_int64),
@@ -97,6 +105,8 @@ SIGNATURES = {
     "dr_bag_offsets_grouped": (_I32, [_P, _P, _P, _I32, _I64, _P, _P]),
     "dr_rows_per_nnz": (_I32, [_P, _P, _P, _I32, _P, _P]),
     "dr_pool_grad_workspace_size": (_SZ, [_I64]),
+    "dr_pool_grad_grouped_workspace_size": (_SZ, [_I64]),
+    "dr_pool_grad_grouped": (_I32, [_P, _I32, _I64, _I32, _P, _P, _SZ, _P]),
     "dr_pool_grad": (_I32, [_P, _I64, _I64, _I32, _P, _P, _P, _I64, _P, _I32, _P, _P, _SZ, _P]),
     "dr_ev_create": (_I32, [_P, _P, _P]),
     "dr_ev_create_slot": (_I32, [_P, _I32, _P, _P]),
@@ -122,6 +132,8 @@ SIGNATURES = {
     "dr_ev_apply_adagrad": (_I32, [_P, _P, _F32, _P, _P, _I64, _P, _I64, _P]),
     "dr_ev_apply_adam": (_I32, [_P, _P, _P, _F32, _F32, _F32, _F32, _F32, _F32, _P, _P, _I64, _P,
                                 _I64, _P]),
+    "dr_ev_apply_grouped": (_I32, [_I32, _P, _P, _P, _I32, _P, _P, _P, _P, _F32, _F32, _F32,
+                                   _F32, _F32, _F32, _I64, _P]),
     "dr_fused_local_workspace_size": (_SZ, [_I64]),
     "dr_fused_local_lookup": (_I32, [_P, _I64, _I32, _P, _P, _I64, _I64, _I32, _F32, _P, _P, _P,
                                      _SZ, _P]),

@@ -74,6 +74,7 @@ class _Feature(object):
         # nnz b, so the pool kernel needs no bag offsets (DR_POOL_ONEHOT).
         self.onehot = bool(onehot) and weights is None and max_norm is None
         self.bag_off = None
+        self.group = None
         self.values = values
         if seg.dim() == 2:
             self.seg64, self.seg_stride = seg.contiguous(), seg.shape[1]
@@ -192,7 +193,7 @@ def _grad_to_slices(f, g, top_stride):
                              ptr(f.idx), n, ptr(f.U), COMBINERS[f.combiner], ptr(gu), ptr(ws), wsb,
                              stream_handle(dev)))
     ops._post(dev)
-    return IndexedSlices(gu, f.uniq, f.U)
+    return IndexedSlices(gu, f.uniq, f.U, unique=True)
 
 
 class _LookupFn(torch.autograd.Function):
@@ -204,16 +205,28 @@ class _LookupFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out):
         g = grad_out.contiguous()
-        D = None
-        col = 0
+        total = g.shape[1]
+        cols, col = [], 0
         for f in ctx.feats:
-            D = f.params.dim if not torch.is_tensor(f.params) else f.params.shape[1]
-            gf = g[:, col:col + D]
-            col += D
+            cols.append(col)
+            col += f.params.dim if not torch.is_tensor(f.params) else f.params.shape[1]
+        done = set()
+        for i, f in enumerate(ctx.feats):
             holder = f.params
             if torch.is_tensor(holder):
                 continue
-            sl = _grad_to_slices(f, gf.contiguous(), D)
+            grp = getattr(f, "group", None)
+            if grp is not None:
+                if id(grp) in done:
+                    continue
+                done.add(id(grp))
+                pos = {id(x): j for j, x in enumerate(ctx.feats)}
+                sls = grp.grads(g, [cols[pos[id(x)]] for x in grp.feats], total)
+                for x, sl in zip(grp.feats, sls):
+                    x.params.pending_grads.append(sl)
+                continue
+            D = holder.dim if not torch.is_tensor(holder) else holder.shape[1]
+            sl = _grad_to_slices(f, g[:, cols[i]:cols[i] + D].contiguous(), D)
             holder.pending_grads.append(sl)
         return None, None, None
 
@@ -264,7 +277,7 @@ def _prepare_group(feats, need_grad=True):
         ops._post(dev)
         _bag_offsets_all(feats, skip_onehot=True)
         for t, f in enumerate(feats):
-            f.uniq = f.idx = f.rows = f.U = f.defaults = None
+            f.uniq = f.idx = f.rows = f.U = f.defaults = f.group = None
             f.rowsel = rowsel[koff[t]:koff[t + 1]]
         return
     uniq, idx, cnt, U = ops.unique_grouped(vals, koff, with_counts)
@@ -287,6 +300,55 @@ def _prepare_group(feats, need_grad=True):
         f.rowsel = rowsel[koff[t]:koff[t + 1]]
         f.U = U[t:t + 1]
         f.defaults = None
+    group = _UniqueGroup(feats, uniq, U, koff)
+    for f in feats:
+        f.group = group
+
+
+class _UniqueGroup(object):
+    """Features that went through one dr_unique_grouped call: their backward
+    runs as one dr_pool_grad_grouped (one sort for all features)."""
+
+    def __init__(self, feats, uniq, U, koff):
+        self.feats = feats
+        self.uniq = uniq
+        self.U = U
+        self.koff = koff
+
+    def grads(self, g, cols, top_stride):
+        """g: the pooled grad (base tensor), cols[t]: column of feature t.
+        Returns one IndexedSlices per feature."""
+        dev = g.device
+        D = self.feats[0].params.dim
+        descs = (_lib.DrPoolGradDesc * len(self.feats))()
+        for t, f in enumerate(self.feats):
+            if f.weights is not None or f.max_norm is not None:
+                raise NotImplementedError("backward of weighted / max_norm lookups is not "
+                                          "implemented")
+            d = descs[t]
+            d.top_grad = g.data_ptr() + 4 * cols[t]
+            d.top_stride = top_stride
+            if f.onehot:
+                d.bag_off, d.seg, d.seg_stride = None, None, 0
+            else:
+                _bag_offsets_all([f])
+                d.bag_off = ptr(f.bag_off)
+                d.seg = ptr(f.seg64)
+                d.seg_stride = f.seg_stride
+            d.idx = ptr(f.idx)
+            d.nnz = f.values.numel()
+            d.num_unique = ptr(f.U)
+            d.combiner = COMBINERS[f.combiner]
+        n = self.koff[-1]
+        gu = torch.empty((max(n, 1), D), dtype=torch.float32, device=dev)
+        wsb = lib().dr_pool_grad_grouped_workspace_size(n)
+        ws = workspace(wsb, dev)
+        check(lib().dr_pool_grad_grouped(descs, len(self.feats), self.feats[0].batch, D, ptr(gu),
+                                         ptr(ws), wsb, stream_handle(dev)))
+        ops._post(dev)
+        k = self.koff
+        return [IndexedSlices(gu[k[t]:k[t + 1]], self.uniq[k[t]:k[t + 1]], self.U[t:t + 1], True)
+                for t in range(len(self.feats))]
 
 
 def _run(feats, order=ORDER_ALI, need_grad=None):

@@ -64,10 +64,11 @@ def _default_row(initializer, dim, device):
 class IndexedSlices(object):
     """values [N, D] for rows `indices` [N] (tf.IndexedSlices)."""
 
-    def __init__(self, values, indices, num_valid=None):
+    def __init__(self, values, indices, num_valid=None, unique=False):
         self.values = values
         self.indices = indices
         self.num_valid = num_valid  # optional device int64[1] (<= N)
+        self.unique = unique        # indices known distinct (a lookup's backward)
 
 
 class EmbeddingVariable(object):

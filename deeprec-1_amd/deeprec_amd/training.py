@@ -15,39 +15,116 @@ from .embedding_ops import DenseTable
 from .kv_variable_ops import EmbeddingVariable, IndexedSlices
 
 
-def _dedup(slices):
-    if len(slices) == 1:
-        return slices[0]           # one lookup's slices are already unique ids
+def _concat(slices):
     vals, idxs = [], []
     for s in slices:
         n = s.indices.numel() if s.num_valid is None else int(s.num_valid.item())
         vals.append(s.values[:n])
         idxs.append(s.indices[:n])
-    v = torch.cat(vals)
-    i = torch.cat(idxs)
+    return torch.cat(vals), torch.cat(idxs)
+
+
+def _dedup(slices):
+    """_deduplicate_indexed_slices (optimizer.py:68-83): unique + sum."""
+    if len(slices) == 1 and slices[0].unique:
+        return slices[0]           # one lookup's backward: ids already distinct
+    v, i = _concat(slices)
     u, pos = ops.unique(i)
     summed = ops.unsorted_segment_sum(v, pos, u.numel())
-    return IndexedSlices(summed, u)
+    return IndexedSlices(summed, u, unique=True)
+
+
+def _rounds(slices):
+    """Split possibly repeated indices into rounds of distinct ids, round r
+    holding every id's r-th occurrence (in index order).  Applying the rounds
+    in order replays a kernel that walks the indices sequentially."""
+    if len(slices) == 1 and slices[0].unique:
+        return slices
+    v, i = _concat(slices)
+    if i.numel() == 0:
+        return []
+    _, pos = ops.unique(i)
+    pos = pos.to(torch.int64)
+    order = torch.sort(pos, stable=True).indices
+    sp = pos[order]
+    start = torch.ones_like(sp, dtype=torch.bool)
+    start[1:] = sp[1:] != sp[:-1]
+    first = torch.cummax(torch.where(start, torch.arange(sp.numel(), device=sp.device),
+                                     torch.zeros_like(sp)), 0).values
+    rank = torch.empty_like(sp)
+    rank[order] = torch.arange(sp.numel(), device=sp.device) - first
+    out = []
+    for r in range(int(rank.max().item()) + 1):
+        m = rank == r
+        out.append(IndexedSlices(v[m], i[m], unique=True))
+    return out
 
 
 class _Optimizer(object):
+    _opt = None   # DR_OPT_* code of the EV apply kernel
+
     def __init__(self, learning_rate):
         self.lr = float(learning_rate)
 
+    # How repeated indices reach the EV apply kernel: summed first (the
+    # default _resource_apply_sparse_duplicate_indices, optimizer.py:1060-1083)
+    # or applied one after another (GradientDescent overrides it and hands
+    # the raw indices to KvResourceSparseApplyGradientDescent,
+    # gradient_descent.py:71-76, whose kernel walks them in order).
+    _ev_duplicates = "sum"
+
     def apply_gradients(self, var_list, global_step=None):
         gs = -1 if global_step is None else int(global_step)
+        rounds = []   # rounds[r] = [(var, slices)] applied in one grouped launch
         for var in var_list:
             if not var.pending_grads:
                 continue
-            sl = _dedup(var.pending_grads)
+            pending = var.pending_grads
             var.pending_grads = []
             if isinstance(var, EmbeddingVariable):
-                self._apply_ev(var, sl, gs)
+                sls = (_rounds(pending) if self._ev_duplicates == "sequential"
+                       else [_dedup(pending)])
+                for r, sl in enumerate(sls):
+                    if r == len(rounds):
+                        rounds.append([])
+                    rounds[r].append((var, sl))
             elif isinstance(var, DenseTable):
-                self._apply_dense(var, sl)
+                self._apply_dense(var, _dedup(pending))
             else:
                 raise TypeError("unsupported variable %r" % (var,))
+        for items in rounds:
+            self._apply_ev_batch(items, gs)
         self._finish()
+
+    def _slots(self, var):
+        return None, None
+
+    def _scalars(self):
+        return (0.0, 0.0, 0.0, 0.0, 0.0)
+
+    def _apply_ev_batch(self, items, gs):
+        """One dr_ev_apply_grouped per (device, dim) group of variables."""
+        import ctypes as C
+        groups = {}
+        for var, sl in items:
+            groups.setdefault((str(var.device), var.dim), []).append((var, sl))
+        b1p, b2p, b1, b2, eps = self._scalars()
+        for (_, _), grp in groups.items():
+            T = len(grp)
+            dev = grp[0][0].device
+            vals = [sl.values.contiguous() for _, sl in grp]
+            idxs = [sl.indices.contiguous() for _, sl in grp]
+            slots = [self._slots(var) for var, _ in grp]
+            P = C.c_void_p * T
+            s1 = P(*[a.handle.value if a is not None else None for a, _ in slots])
+            s2 = P(*[b.handle.value if b is not None else None for _, b in slots])
+            check(lib().dr_ev_apply_grouped(
+                self._opt, P(*[var.handle.value for var, _ in grp]), s1, s2, T,
+                P(*[v.data_ptr() for v in vals]), P(*[i.data_ptr() for i in idxs]),
+                (C.c_int64 * T)(*[i.numel() for i in idxs]),
+                P(*[ptr(sl.num_valid) for _, sl in grp]), self.lr, b1p, b2p, b1, b2, eps, gs,
+                stream_handle(dev)))
+            ops._post(dev)
 
     def _finish(self):
         pass
@@ -60,12 +137,8 @@ class _Optimizer(object):
 class GradientDescentOptimizer(_Optimizer):
     """KvResourceSparseApplyGradientDescent (training_ali_ops.cc:1597-1678)."""
 
-    def _apply_ev(self, var, sl, gs):
-        dev = var.device
-        check(lib().dr_ev_apply_sgd(var.handle, self.lr, ptr(sl.values.contiguous()),
-                                    ptr(sl.indices.contiguous()), sl.indices.numel(),
-                                    ptr(sl.num_valid), gs, stream_handle(dev)))
-        ops._post(dev)
+    _opt = 0
+    _ev_duplicates = "sequential"
 
     def _dense_update(self, var, idx, g):
         var.weight.index_add_(0, idx, g * (-self.lr))
@@ -74,19 +147,15 @@ class GradientDescentOptimizer(_Optimizer):
 class AdagradOptimizer(_Optimizer):
     """KvSparseApplyAdagrad (training_ali_ops.cc:61-145)."""
 
+    _opt = 1
+
     def __init__(self, learning_rate, initial_accumulator_value=0.1):
         super().__init__(learning_rate)
         self.init_acc = float(initial_accumulator_value)
         self._dense_acc = {}
 
-    def _apply_ev(self, var, sl, gs):
-        acc = var.slot("Adagrad", self.init_acc)
-        dev = var.device
-        check(lib().dr_ev_apply_adagrad(var.handle, acc.handle, self.lr,
-                                        ptr(sl.values.contiguous()), ptr(sl.indices.contiguous()),
-                                        sl.indices.numel(), ptr(sl.num_valid), gs,
-                                        stream_handle(dev)))
-        ops._post(dev)
+    def _slots(self, var):
+        return var.slot("Adagrad", self.init_acc), None
 
     def _dense_update(self, var, idx, g):
         acc = self._dense_acc.setdefault(id(var), torch.full_like(var.weight, self.init_acc))
@@ -99,22 +168,19 @@ class AdamOptimizer(_Optimizer):
     """KvSparseApplyAdam (training_ali_ops.cc:848-975); beta powers advance
     once per apply_gradients like the optimizer's non-slot variables."""
 
+    _opt = 2
+
     def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8):
         super().__init__(learning_rate)
         self.beta1, self.beta2, self.eps = float(beta1), float(beta2), float(epsilon)
         self.b1p = torch.tensor(self.beta1, dtype=torch.float32).item()
         self.b2p = torch.tensor(self.beta2, dtype=torch.float32).item()
 
-    def _apply_ev(self, var, sl, gs):
-        m = var.slot("Adam", 0.0)
-        v = var.slot("Adam_1", 0.0)
-        dev = var.device
-        check(lib().dr_ev_apply_adam(var.handle, m.handle, v.handle, self.b1p, self.b2p, self.lr,
-                                     self.beta1, self.beta2, self.eps,
-                                     ptr(sl.values.contiguous()), ptr(sl.indices.contiguous()),
-                                     sl.indices.numel(), ptr(sl.num_valid), gs,
-                                     stream_handle(dev)))
-        ops._post(dev)
+    def _slots(self, var):
+        return var.slot("Adam", 0.0), var.slot("Adam_1", 0.0)
+
+    def _scalars(self):
+        return (self.b1p, self.b2p, self.beta1, self.beta2, self.eps)
 
     def _finish(self):
         f32 = lambda x: torch.tensor(x, dtype=torch.float32)

@@ -181,6 +181,28 @@ int dr_rows_per_nnz(const int64_t* rows, const int32_t* idx, const int64_t* koff
 int dr_bag_offsets_strided(const int64_t* seg, int64_t stride, int64_t n, int64_t batch,
                            int32_t* bag_off, void* stream);
 
+/* Backward of dr_pool_grouped over T features in one pass (the features of */
+/* one dr_unique_grouped call): grad_unique row koff[t] + u (koff = prefix  */
+/* sums of nnz) = sum over nnz k of feature t with idx[k] == u, ascending k, */
+/* of top_grad_t[bag(k)] scaled like dr_pool_grad.  bag(k) = seg[k *         */
+/* seg_stride] (sp_indices[:, 0] read in place), or k when seg == NULL       */
+/* (one-hot).  Rows u >= num_unique[t] are not written.  Deterministic; the  */
+/* per-feature math equals dr_pool_grad / SparseSegment*Grad.                */
+typedef struct {
+  const float* top_grad;      /* feature t's [B, dim] slice of the pooled grad */
+  int64_t top_stride;
+  const int32_t* bag_off;     /* [B+1]; NULL for one-hot                      */
+  const int64_t* seg;         /* NULL for one-hot                             */
+  int64_t seg_stride;
+  const int32_t* idx;         /* [nnz] feature-local unique position          */
+  int64_t nnz;
+  const int64_t* num_unique;  /* DEVICE U_t                                   */
+  int32_t combiner;
+} dr_pool_grad_desc;
+size_t dr_pool_grad_grouped_workspace_size(int64_t total_nnz);
+int dr_pool_grad_grouped(const dr_pool_grad_desc* descs_host, int num_tables, int64_t batch,
+                         int dim, float* grad_unique, void* ws, size_t ws_bytes, void* stream);
+
 /* Backward of the grouped pooling for one table, deterministic:             */
 /* grad_unique[u] = sum over k with idx[k]==u (ascending k) of               */
 /*   top_grad[bag(k)] * scale(bag)  (scale: 1, 1/n, 1/sqrt(n) as the         */
@@ -286,6 +308,10 @@ int dr_ev_export(dr_ev* ev, int64_t* keys_out, float* values_out, int64_t* versi
 int dr_ev_key_meta(dr_ev* ev, const int64_t* keys_host, int64_t n, int64_t* freq_host,
                    int64_t* version_host, int32_t* has_row_host, void* stream);
 
+/* Sparse applies: keys must be distinct within one call (rows are updated   */
+/* in parallel).  Repeated indices are handled by the caller the way DeepRec */
+/* does: summed first (optimizer.py:68-83), or for GradientDescent applied  */
+/* one occurrence-round after another (gradient_descent.py:71-76).          */
 /* KvResourceSparseApplyGradientDescent (training_ali_ops.cc:1597-1678).     */
 int dr_ev_apply_sgd(dr_ev* var, float lr, const float* grad, const int64_t* keys,
                     int64_t n, const int64_t* n_dev, int64_t global_step, void* stream);
@@ -298,6 +324,17 @@ int dr_ev_apply_adam(dr_ev* var, dr_ev* m, dr_ev* v, float beta1_power, float be
                      float lr, float beta1, float beta2, float epsilon, const float* grad,
                      const int64_t* keys, int64_t n, const int64_t* n_dev,
                      int64_t global_step, void* stream);
+/* The same applies over T EVs of equal dim in few launches (16 tables per  */
+/* launch): table t gets grads[t] [n_host[t], dim] for keys[t], optional     */
+/* DEVICE count n_dev[t]; slot1/slot2: Adagrad accumulator / Adam m, v (or  */
+/* NULL).  Scalars as in the single-table calls.                             */
+enum { DR_OPT_SGD = 0, DR_OPT_ADAGRAD = 1, DR_OPT_ADAM = 2 };
+int dr_ev_apply_grouped(int optimizer, dr_ev* const* vars, dr_ev* const* slot1,
+                        dr_ev* const* slot2, int num_tables, const float* const* grads,
+                        const int64_t* const* keys, const int64_t* n_host,
+                        const int64_t* const* n_dev, float lr, float beta1_power,
+                        float beta2_power, float beta1, float beta2, float epsilon,
+                        int64_t global_step, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* FusedEmbeddingLocalSparseLookUp[Grad]                                     */

@@ -546,6 +546,111 @@ def test_lookup_backward_matches_segment_grad(dr, orc):
         np.testing.assert_array_equal(H(sl.values[:U]), ref)
 
 
+@pytest.mark.parametrize("onehot", [True, False])
+@pytest.mark.parametrize("comb", ["sum", "mean", "sqrtn"])
+def test_grouped_backward_matches_segment_grad(dr, orc, onehot, comb):
+    """Grouped features (one dr_unique_grouped) -> one dr_pool_grad_grouped:
+    each feature's IndexedSlices equal the reference SparseSegment*Grad."""
+    rng = np.random.default_rng(31 + int(onehot))
+    B, D, F = 300, 32, 4
+    evs, sps, raw = [], [], []
+    for f in range(F):
+        evs.append(dr.EmbeddingVariable("gbw_%d_%s_%d" % (int(onehot), comb, f), D, 0.1))
+        if onehot:
+            ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+            v = rng.integers(0, 120, B).astype(np.int64)
+            shape = (B, 1)
+        else:
+            ind, v = _random_sparse(rng, B, 5, 120, allow_empty=True)
+            shape = (B, 5)
+        sps.append(dr.SparseTensor(T(ind), T(v), shape))
+        raw.append((ind, v))
+    out = dr.embedding_lookup_sparse_multi(evs, sps, combiner=comb)
+    g = rng.standard_normal((B, F * D)).astype(np.float32)
+    out.backward(T(g))
+    for f in range(F):
+        sl = evs[f].pending_grads.pop()
+        U = int(sl.num_valid.item())
+        uids, idx = orc.unique(raw[f][1])
+        assert H(sl.indices[:U]).tolist() == uids.tolist()
+        ref = orc.sparse_segment_reduce_grad(np.ascontiguousarray(g[:, f * D:(f + 1) * D]), idx,
+                                             raw[f][0][:, 0].astype(np.int32), U, comb)
+        np.testing.assert_array_equal(H(sl.values[:U]), ref)
+
+
+def test_optimizers_with_repeated_indices(dr, orc):
+    """SGD hands raw repeated indices to the KV kernel, which walks them in
+    order (gradient_descent.py:71-76); Adagrad sums them first
+    (_deduplicate_indexed_slices, optimizer.py:68-83)."""
+    rng = np.random.default_rng(3)
+    D = 40
+    keys = np.array([5, 9, 5, 5, 2, 9, 100, 5] * 20, np.int64)   # ranks up to 80
+    g = rng.standard_normal((keys.shape[0], D)).astype(np.float32)
+    # SGD: sequential application
+    ev = dr.EmbeddingVariable("dup_sgd", D, 0.5)
+    oev = orc.EV(D, 0.5)
+    ev.pending_grads.append(dr.IndexedSlices(T(g), T(keys)))
+    dr.GradientDescentOptimizer(0.1).apply_gradients([ev], global_step=0)
+    oev.apply_sgd(np.float32(0.1), g, keys, 0)
+    k, v = ev.export()[:2]
+    ok, ov = oev.export()[:2]
+    np.testing.assert_array_equal(H(k), ok)
+    np.testing.assert_array_equal(H(v), ov)
+    # Adagrad: dedup (unique + unsorted_segment_sum) then one update per key
+    ev2 = dr.EmbeddingVariable("dup_ada", D, 0.5)
+    oev2 = orc.EV(D, 0.5)
+    oacc = oev2.create_slot(1, 0.1)
+    ev2.pending_grads.append(dr.IndexedSlices(T(g), T(keys)))
+    dr.AdagradOptimizer(0.1, 0.1).apply_gradients([ev2], global_step=0)
+    u, pos = orc.unique(keys)
+    gs = orc.unsorted_segment_sum(g, pos, u.shape[0])
+    oev2.apply_adagrad(oacc, np.float32(0.1), gs, u, 0)
+    k, v = ev2.export()[:2]
+    ok, ov = oev2.export()[:2]
+    np.testing.assert_array_equal(H(k), ok)
+    np.testing.assert_array_equal(H(v), ov)
+
+
+def test_grouped_train_step_matches_oracle(dr, orc):
+    """fwd -> grouped bwd -> KV SGD / Adagrad apply over 3 steps equals the
+    oracle EV updated with the reference formulas."""
+    rng = np.random.default_rng(77)
+    B, D, F = 256, 64, 3
+    for opt_name in ("sgd", "adagrad"):
+        evs, oevs, oacc = [], [], []
+        for f in range(F):
+            evs.append(dr.EmbeddingVariable("gts_%s_%d" % (opt_name, f), D, 0.05))
+            oevs.append(orc.EV(D, 0.05))
+            if opt_name == "adagrad":
+                oacc.append(oevs[-1].create_slot(1, 0.1))
+        opt = dr.GradientDescentOptimizer(0.3) if opt_name == "sgd" else dr.AdagradOptimizer(0.3)
+        for step in range(3):
+            ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+            vals = [rng.integers(0, 200, B).astype(np.int64) for _ in range(F)]
+            sps = [dr.SparseTensor(T(ind), T(v), (B, 1)) for v in vals]
+            out = dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum")
+            g = rng.standard_normal((B, F * D)).astype(np.float32)
+            for f in range(F):
+                ref = orc.embedding_lookup_sparse(oevs[f], ind, vals[f], B, combiner="sum")
+                np.testing.assert_array_equal(H(out)[:, f * D:(f + 1) * D], ref)
+            out.backward(T(g))
+            opt.apply_gradients(evs)
+            for f in range(F):
+                uids, idx = orc.unique(vals[f])
+                gu = orc.sparse_segment_reduce_grad(np.ascontiguousarray(g[:, f * D:(f + 1) * D]),
+                                                    idx, np.arange(B, dtype=np.int32),
+                                                    uids.shape[0], "sum")
+                if opt_name == "sgd":
+                    oevs[f].apply_sgd(0.3, gu, uids)
+                else:
+                    oevs[f].apply_adagrad(oacc[f], 0.3, gu, uids)
+        for f in range(F):
+            k, v = evs[f].export()[:2]
+            ok, ov = oevs[f].export()[:2]
+            np.testing.assert_array_equal(H(k), ok)
+            np.testing.assert_array_equal(H(v), ov)
+
+
 # ---------------------------------------------------------------------------
 # interactions / exchange helpers
 # ---------------------------------------------------------------------------
