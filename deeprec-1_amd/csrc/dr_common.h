@@ -99,6 +99,26 @@ __device__ __forceinline__ int64_t eff_n(int64_t n, const int64_t* n_dev) {
   return m < n ? m : n;
 }
 
+// Table holding element i of a grouped launch (koff: T+1 prefix offsets in
+// kernel-argument memory).  The binary search for the block's first element
+// is uniform (scalar loads); each lane then steps over the few table
+// boundaries inside its block.  A per-lane linear walk over koff would be up
+// to T dependent loads per element.
+__device__ __forceinline__ int table_of(const int64_t* koff, int T, int64_t i,
+                                        int64_t block_first) {
+  int lo = 0, hi = T - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (koff[mid] <= block_first)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  int t = lo;
+  while (t + 1 < T && i >= koff[t + 1]) ++t;
+  return t;
+}
+
 // Byte-pattern fill by a kernel (stream-ordered, graph-capturable).  Used
 // instead of hipMemsetAsync for workspace state that later kernels probe:
 // a captured memset node is serviced by a DMA engine and in hipGraph replay

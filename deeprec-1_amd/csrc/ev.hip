@@ -315,8 +315,7 @@ __device__ __forceinline__ bool locate(const EvGroup& g, int T, int64_t i,
     *li = i;
     return true;
   }
-  int tt = 0;
-  while (tt + 1 < T && i >= g.koff[tt + 1]) ++tt;
+  const int tt = table_of(g.koff, T, i, (int64_t)blockIdx.x * blockDim.x);
   *t = tt;
   *li = i - g.koff[tt];
   if (g.n_dev[tt] && *li >= *g.n_dev[tt]) return false;
@@ -424,7 +423,7 @@ __global__ void ev_init_rows_kernel(InitGroup g, int T, int64_t dim,
       if (g.n_dev[0] && i >= *g.n_dev[0]) live = false;
       else t = g.tags[i];
     } else {
-      while (t + 1 < T && i >= g.koff[t + 1]) ++t;
+      t = table_of(g.koff, T, i, (int64_t)blockIdx.x * blockDim.x);
       li = i - g.koff[t];
       if (g.n_dev[t] && li >= *g.n_dev[t]) live = false;
     }

@@ -128,8 +128,7 @@ __global__ __launch_bounds__(256) void route_keys_kernel(RouteGroup g, int T,
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < g.koff[T]) {
-    int t = 0;
-    while (t + 1 < T && i >= g.koff[t + 1]) ++t;
+    const int t = table_of(g.koff, T, i, (int64_t)blockIdx.x * blockDim.x);
     uint64_t k = (uint64_t)bins;
     if (!num_unique || i - g.koff[t] < num_unique[t]) {
       int64_t o = uniq[i] % world;

@@ -516,8 +516,7 @@ __global__ void rows_per_nnz_kernel(KoffGroup g, int T, const int64_t* __restric
                                     const int32_t* __restrict__ idx, int64_t* __restrict__ rowsel) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= g.koff[T]) return;
-  int t = 0;
-  while (t + 1 < T && i >= g.koff[t + 1]) ++t;
+  const int t = table_of(g.koff, T, i, (int64_t)blockIdx.x * blockDim.x);
   rowsel[i] = rows[g.koff[t] + idx[i]];
 }
 
@@ -750,17 +749,16 @@ struct GradGroup {
   int64_t koff[DR_MAX_GROUP + 1];
 };
 
-__device__ __forceinline__ int grad_table(const GradGroup& g, int T, int64_t i) {
-  int t = 0;
-  while (t + 1 < T && i >= g.koff[t + 1]) ++t;
-  return t;
+__device__ __forceinline__ int grad_table(const GradGroup& g, int T, int64_t i,
+                                          int64_t block_first) {
+  return table_of(g.koff, T, i, block_first);
 }
 
 __global__ void grad_keys_kernel(GradGroup g, int T, uint64_t* __restrict__ kin,
                                  int32_t* __restrict__ vin, int* st) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= g.koff[T]) return;
-  const int t = grad_table(g, T, i);
+  const int t = grad_table(g, T, i, (int64_t)blockIdx.x * blockDim.x);
   const int64_t k = i - g.koff[t];
   int64_t u = g.d[t].idx[k];
   if (u < 0 || u >= g.d[t].nnz) {
@@ -771,72 +769,80 @@ __global__ void grad_keys_kernel(GradGroup g, int T, uint64_t* __restrict__ kin,
   vin[i] = (int32_t)i;
 }
 
-// A group owns NB consecutive unique rows and issues the first element's
-// row load of all NB before summing (most rows of one-hot features have a
-// single element: NB loads in flight instead of one dependent chain each).
+// Position-driven over the sorted (global unique row, nnz) pairs: a group
+// owns NB consecutive sorted positions.  A position that starts its row's
+// run sums the run (in ascending nnz order -- the sort is stable); others
+// are skipped.  The common one-element run costs two independent sequential
+// loads (key, nnz) and one row load, with no offsets table.
 template <int VEC, int G, int CPL, int NB>
-__global__ __launch_bounds__(256) void grad_csr_grouped_kernel(GradGroup g, int T, int64_t B,
-                                                               const int32_t* __restrict__ perm,
-                                                               const int32_t* __restrict__ off,
-                                                               int dim, float* __restrict__ out,
-                                                               int* st) {
+__global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64_t B,
+                                                       const uint64_t* __restrict__ skey,
+                                                       const int32_t* __restrict__ perm,
+                                                       int dim, float* __restrict__ out,
+                                                       int* st) {
   constexpr int GPB = 256 / G;
-  const int64_t u0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * NB;
   const int64_t N = g.koff[T];
-  if (u0 >= N) return;
+  const int64_t p0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * NB;
+  if (p0 >= N) return;
+  const int64_t pf = (int64_t)blockIdx.x * GPB * NB;  // block's first position
+  const int64_t ufirst = (int64_t)skey[pf];           // uniform: its row, for table_of
   const int lg = threadIdx.x % G;
   const int dv = dim / VEC;
   using R = Row<VEC, G, CPL>;
   using V = typename VecT<VEC>::T;
   R x[NB];
+  int64_t uq[NB], rq[NB];
   int tq[NB];
-  int32_t j0[NB], j1[NB];
-  const float* rp0[NB];
+  bool head[NB], single[NB];
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
-    const int64_t u = u0 + q;
-    j0[q] = j1[q] = 0;
-    rp0[q] = nullptr;
+    const int64_t p = p0 + q;
+    head[q] = single[q] = false;
+    uq[q] = -1;
+    rq[q] = -1;
     tq[q] = 0;
-    if (u < N) {
-      const int t = grad_table(g, T, u);
-      tq[q] = t;
-      const dr_pool_grad_desc& d = g.d[t];
-      if (u - g.koff[t] < *d.num_unique) {
-        j0[q] = off[u];
-        j1[q] = off[u + 1];
-        if (j1[q] > j0[q]) {
-          const int64_t k = (int64_t)perm[j0[q]] - g.koff[t];
-          const int64_t r = d.seg ? d.seg[k * d.seg_stride] : k;
-          if (r >= 0 && r < B)
-            rp0[q] = d.top_grad + r * d.top_stride;
-          else
-            latch(st, DR_INVALID_ARGUMENT);
+    const float* rp = nullptr;
+    if (p < N) {
+      const int64_t u = (int64_t)skey[p];
+      const int64_t prev = p > 0 ? (int64_t)skey[p - 1] : -1;
+      const int64_t next = p + 1 < N ? (int64_t)skey[p + 1] : -1;
+      if (u < N && u != prev) {  // u == N: sentinel for out-of-range idx
+        const int t = table_of(g.koff, T, u, ufirst < N ? ufirst : 0);
+        const dr_pool_grad_desc& d = g.d[t];
+        head[q] = true;
+        single[q] = u != next;
+        uq[q] = u;
+        tq[q] = t;
+        const int64_t k = (int64_t)perm[p] - g.koff[t];
+        const int64_t r = d.seg ? d.seg[k * d.seg_stride] : k;
+        if (r >= 0 && r < B) {
+          rp = d.top_grad + r * d.top_stride;
+          rq[q] = r;
+        } else {
+          latch(st, DR_INVALID_ARGUMENT);
         }
-      } else {
-        j0[q] = j1[q] = -1;  // past U_t: not written
       }
-    } else {
-      j0[q] = j1[q] = -1;
     }
-    load_row<VEC, G, CPL>(x[q], rp0[q], lg, dv);
+    load_row<VEC, G, CPL>(x[q], rp, lg, dv);
   }
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
-    if (j0[q] < 0) continue;
+    if (!head[q]) continue;
     const dr_pool_grad_desc& d = g.d[tq[q]];
     const int mode = d.combiner == DR_COMBINER_SUM ? 0 : (d.combiner == DR_COMBINER_MEAN ? 1 : 2);
     R acc;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<V>();
-    for (int32_t j = j0[q]; j < j1[q]; ++j) {
+    int64_t p = p0 + q;
+    for (bool first = true;; first = false) {
       R y;
-      int64_t r = -1;
-      if (j == j0[q]) {
+      int64_t r;
+      if (first) {
         y = x[q];
-        if (rp0[q]) r = (rp0[q] - d.top_grad) / d.top_stride;
+        r = rq[q];
       } else {
-        const int64_t k = (int64_t)perm[j] - g.koff[tq[q]];
+        if (p >= N || (int64_t)skey[p] != uq[q]) break;
+        const int64_t k = (int64_t)perm[p] - g.koff[tq[q]];
         r = d.seg ? d.seg[k * d.seg_stride] : k;
         const float* rp = nullptr;
         if (r >= 0 && r < B)
@@ -856,23 +862,25 @@ __global__ __launch_bounds__(256) void grad_csr_grouped_kernel(GradGroup g, int 
 #pragma unroll
           for (int c = 0; c < CPL; ++c) y.v[c] = vmul(y.v[c], sc);
         }
-        if (j == j0[q])
+        if (first)
           acc = y;
         else
           acc_add(acc, y);
       }
+      ++p;
+      if (single[q]) break;
     }
-    store_row<VEC, G, CPL>(acc, out + (u0 + q) * (int64_t)dim, lg, dv);
+    store_row<VEC, G, CPL>(acc, out + uq[q] * (int64_t)dim, lg, dv);
   }
 }
 
 template <int VEC, int G, int CPL>
-static void launch_grad_csr(const GradGroup& g, int T, int64_t B, const int32_t* perm,
-                            const int32_t* off, int dim, float* out, hipStream_t s, int* st) {
+static void launch_grad_csr(const GradGroup& g, int T, int64_t B, const uint64_t* skey,
+                            const int32_t* perm, int dim, float* out, hipStream_t s, int* st) {
   constexpr int NB = 4;
   const int64_t blocks = ceil_div(ceil_div(g.koff[T] > 0 ? g.koff[T] : 1, NB), 256 / G);
-  hipLaunchKernelGGL((grad_csr_grouped_kernel<VEC, G, CPL, NB>), dim3((unsigned)blocks),
-                     dim3(256), 0, s, g, T, B, perm, off, dim, out, st);
+  hipLaunchKernelGGL((grad_seg_kernel<VEC, G, CPL, NB>), dim3((unsigned)blocks), dim3(256), 0, s,
+                     g, T, B, skey, perm, dim, out, st);
 }
 
 }  // namespace dr
@@ -1115,27 +1123,25 @@ int dr_pool_grad_grouped(const dr_pool_grad_desc* descs_host, int num_tables, in
   int rc = dr_sort_pairs(w.kin, w.vin, w.kout, w.perm, n, 0, bits_for(n), w.sort_ws,
                          w.sort_bytes, stream);
   if (rc) return rc;
-  rc = launch_bag_offsets<uint64_t>(w.kout, 1, n, nullptr, n + 1, w.off, s);
-  if (rc) return rc;
   if (aligned) {
     const int d4 = dim / 4;
     if (d4 <= 8)
-      launch_grad_csr<4, 8, 1>(g, num_tables, batch, w.perm, w.off, dim, grad_unique, s, st);
+      launch_grad_csr<4, 8, 1>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, s, st);
     else if (d4 <= 16)
-      launch_grad_csr<4, 16, 1>(g, num_tables, batch, w.perm, w.off, dim, grad_unique, s, st);
+      launch_grad_csr<4, 16, 1>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, s, st);
     else if (d4 <= 32)
-      launch_grad_csr<4, 32, 1>(g, num_tables, batch, w.perm, w.off, dim, grad_unique, s, st);
+      launch_grad_csr<4, 32, 1>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, s, st);
     else if (d4 <= 64)
-      launch_grad_csr<4, 64, 1>(g, num_tables, batch, w.perm, w.off, dim, grad_unique, s, st);
+      launch_grad_csr<4, 64, 1>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, s, st);
     else if (d4 <= 256)
-      launch_grad_csr<4, 64, 4>(g, num_tables, batch, w.perm, w.off, dim, grad_unique, s, st);
+      launch_grad_csr<4, 64, 4>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, s, st);
     else
       DR_REQUIRE(false, DR_INVALID_ARGUMENT, "dim %d unsupported", dim);
   } else {
     if (dim <= 64)
-      launch_grad_csr<1, 64, 1>(g, num_tables, batch, w.perm, w.off, dim, grad_unique, s, st);
+      launch_grad_csr<1, 64, 1>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, s, st);
     else if (dim <= 256)
-      launch_grad_csr<1, 64, 4>(g, num_tables, batch, w.perm, w.off, dim, grad_unique, s, st);
+      launch_grad_csr<1, 64, 4>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, s, st);
     else
       DR_REQUIRE(false, DR_INVALID_ARGUMENT, "dim %d unsupported", dim);
   }

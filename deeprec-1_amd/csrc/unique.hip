@@ -65,10 +65,9 @@ static UniqueWs carve_unique(void* ws, int64_t n, int64_t hash_total, size_t* us
   return u;
 }
 
+// (all callers index elements as blockIdx.x * blockDim.x + threadIdx.x)
 __device__ __forceinline__ int group_table(const UniqGroup& g, int T, int64_t i) {
-  int t = 0;
-  while (t + 1 < T && i >= g.koff[t + 1]) ++t;
-  return t;
+  return table_of(g.koff, T, i, (int64_t)blockIdx.x * blockDim.x);
 }
 
 __global__ void unique_insert_kernel(UniqGroup g, int T, const int64_t* __restrict__ keys,
