@@ -129,6 +129,7 @@ __device__ Slot* ev_find(const EvDesc& e, uint64_t key, bool insert, bool* creat
                          uint64_t* rc, int* st) {
   *created = false;
   Slot* s = nullptr;
+  uint64_t rc_seen = kUnset;  // rc read together with a matching key
   if (key == kEmptyKey) {
     s = e.slots + e.cap;
     uint64_t cur = s->key;
@@ -150,9 +151,13 @@ __device__ Slot* ev_find(const EvDesc& e, uint64_t key, bool insert, bool* creat
         return nullptr;
       }
       Slot* c = e.slots + h;
-      uint64_t cur = c->key;
+      // one 16-byte load brings key and rc: a hit needs no second round trip
+      typedef unsigned long long slot_v __attribute__((ext_vector_type(2)));
+      const slot_v sv = *reinterpret_cast<const slot_v*>(c);
+      uint64_t cur = sv.x;
       if (cur == key) {
         s = c;
+        rc_seen = sv.y;
         break;
       }
       if (cur == kEmptyKey) {
@@ -200,7 +205,7 @@ __device__ Slot* ev_find(const EvDesc& e, uint64_t key, bool insert, bool* creat
   }
   __builtin_amdgcn_wave_barrier();  // convergent: keeps the two ifs apart
   if (*created) return s;
-  uint64_t v = s->rc;
+  uint64_t v = rc_seen != kUnset ? rc_seen : s->rc;
   if (v == kUnset) {
     for (int spin = 0; spin < (1 << 22); ++spin) {
       v = atomic_read_u64(&s->rc);

@@ -470,6 +470,32 @@ def test_onehot_and_mostly_onehot_pooling(dr, orc, B):
         np.testing.assert_array_equal(out[:, f * D:(f + 1) * D], ref)
 
 
+def test_many_feature_forward_matches_oracle(dr, orc):
+    """11 one-hot filter-free EV features without grad (direct resolve, one
+    grouped pool launch); outputs and EV contents must equal the oracle
+    (insert-on-miss included)."""
+    rng = np.random.default_rng(123)
+    B, D, F = 700, 32, 11
+    ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+    evs, oevs, sps, vals = [], [], [], []
+    for f in range(F):
+        evs.append(dr.EmbeddingVariable("pipe%d" % f, D, 0.25 + f))
+        oevs.append(orc.EV(D, 0.25 + f))
+        keys = np.arange(0, 300, dtype=np.int64)
+        rows = rng.standard_normal((300, D)).astype(np.float32)
+        evs[-1].insert(T(keys), T(rows))
+        oevs[-1].insert(keys, rows)
+        v = rng.integers(0, 600, B).astype(np.int64)
+        vals.append(v)
+        sps.append(dr.SparseTensor(T(ind), T(v), (B, 1)))
+    with torch.no_grad():
+        out = H(dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum"))
+    for f in range(F):
+        ref = orc.embedding_lookup_sparse(oevs[f], ind, vals[f], B, combiner="sum")
+        np.testing.assert_array_equal(out[:, f * D:(f + 1) * D], ref)
+        assert int(evs[f].total_count()[0]) == oevs[f].size()
+
+
 def test_pool_onehot_flag_rejects_weights(dr, ops):
     from deeprec_amd import _lib
     t = torch.zeros((4, 8), device=DEV)
