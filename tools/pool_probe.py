@@ -44,15 +44,21 @@ def main():
     spans = [1 << int(s) for s in args.spans.split(",") if s] + [rows]
     for span in spans:
         span = min(span, rows)
-        for mode in ("random", "sequential"):
-            if mode == "sequential" and span != rows:
+        for mode in ("random", "sequential", "slot-sequential", "random-runs8"):
+            if mode != "random" and span != rows:
                 continue
             sel = []
             for t in range(T):
                 if mode == "random":
                     sel.append(torch.randint(0, span, (B,), generator=g, device=dev))
-                else:
+                elif mode == "sequential":      # table-major rows
                     sel.append(torch.arange(t * B, (t + 1) * B, device=dev) % rows)
+                elif mode == "slot-sequential":  # row = output slot: a plain copy
+                    sel.append((torch.arange(B, device=dev) * T + t) % rows)
+                else:                            # random 4 KiB runs of 8 rows
+                    base = torch.randint(0, span // 8, (B // 8 + 1,), generator=g, device=dev)
+                    r = (base[:, None] * 8 + torch.arange(8, device=dev)[None, :]).reshape(-1)
+                    sel.append(r[:B] % rows)
             descs = []
             for t in range(T):
                 d = _lib.DrPoolDesc()
