@@ -331,14 +331,18 @@ __device__ __forceinline__ bool locate(const EvGroup& g, int T, int64_t i,
 __global__ void ev_resolve_kernel(EvGroup g, int T, const int64_t* __restrict__ keys,
                                   const int32_t* __restrict__ counts, int64_t* __restrict__ rows_out,
                                   uint8_t* __restrict__ init, int32_t* __restrict__ badd, int* st) {
+  // per-lane table index: descriptors staged in LDS (see pool_onehot_kernel)
+  __shared__ EvDesc se[DR_MAX_GROUP];
+  if (threadIdx.x < T) se[threadIdx.x] = g.e[threadIdx.x];
+  __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int t;
   int64_t li;
   uint64_t key;
   if (!locate(g, T, i, keys, &t, &li, &key)) return;
-  const EvDesc& e = g.e[t];
+  const EvDesc& e = se[t];
   init[i] = 0;
-  badd[i] = 0;
+  if (badd) badd[i] = 0;
   const int64_t cnt = counts ? counts[i] : 1;
   if (e.k_hash > 0) {  // BloomFilter::LookupOrCreate (embedding_filter.h:56-82)
     if (bloom_min_freq(e, key) < e.filter_freq) {
@@ -979,7 +983,7 @@ static int resolve_grouped(dr_ev* const* evs, int T, const int64_t* keys, const 
   ig.koff[T] = total;
   const unsigned blocks = (unsigned)ceil_div(total, 256);
   hipLaunchKernelGGL(ev_resolve_kernel, dim3(blocks), dim3(256), 0, st, g, T, keys, counts,
-                     rows_out, w.init, w.badd, stw);
+                     rows_out, w.init, any_bloom ? w.badd : nullptr, stw);
   if (any_bloom)
     hipLaunchKernelGGL(ev_bloom_add_kernel, dim3(blocks), dim3(256), 0, st, g, T, keys, w.badd);
   // counter mirrors ride on the init kernel (no extra copy launches)
@@ -1606,6 +1610,9 @@ __device__ __forceinline__ int64_t inbox_count(const int64_t* cnt, int src) {
 __global__ __launch_bounds__(256) void xgmi_resolve_kernel(XgmiResolveArgs a,
                                                            int64_t* __restrict__ rows,
                                                            uint8_t* __restrict__ init, int* st) {
+  __shared__ EvDesc se[DR_MAX_GROUP];  // per-lane table index: stage in LDS
+  if (threadIdx.x < a.T) se[threadIdx.x] = a.e[threadIdx.x];
+  __syncthreads();
   const int src = blockIdx.y;
   const int64_t n = inbox_count(a.cnt, src);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -1613,7 +1620,7 @@ __global__ __launch_bounds__(256) void xgmi_resolve_kernel(XgmiResolveArgs a,
     const int64_t j = (int64_t)src * a.cap + i;
     const uint64_t key = (uint64_t)a.keys[j];
     const int t = a.slot[j] % a.T;
-    const EvDesc& e = a.e[t];
+    const EvDesc& e = se[t];
     bool created;
     uint64_t rc;
     Slot* s = ev_find(e, key, true, &created, &rc, st);
@@ -1676,6 +1683,13 @@ typedef float xf4 __attribute__((ext_vector_type(4)));
 template <int G, int NB>
 __global__ __launch_bounds__(256) void xgmi_emit_kernel(XgmiRowArgs a,
                                                         const int64_t* __restrict__ rows) {
+  __shared__ const float* spool[DR_MAX_GROUP];  // per-lane table index: stage in LDS
+  __shared__ const float* sdflt[DR_MAX_GROUP];
+  if (threadIdx.x < a.T) {
+    spool[threadIdx.x] = a.pool[threadIdx.x];
+    sdflt[threadIdx.x] = a.dflt[threadIdx.x];
+  }
+  __syncthreads();
   const int src = blockIdx.y;
   const int64_t n = inbox_count(a.cnt, src);
   constexpr int GPB = 256 / G;
@@ -1697,7 +1711,7 @@ __global__ __launch_bounds__(256) void xgmi_emit_kernel(XgmiRowArgs a,
         const int32_t sl = a.slot[j];
         const int t = sl % a.T;
         const int64_t r = rows[j];
-        const float* row = r >= 0 ? a.pool[t] + r * a.dim : a.dflt[t];
+        const float* row = r >= 0 ? spool[t] + r * a.dim : sdflt[t];
         x[k] = __builtin_nontemporal_load(reinterpret_cast<const xf4*>(row) + lg);
         dst[k] = out + (int64_t)sl * a.dim;
       }

@@ -788,6 +788,9 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
                                                        const int32_t* __restrict__ perm,
                                                        int dim, float* __restrict__ out,
                                                        int* st) {
+  __shared__ dr_pool_grad_desc sd[DR_MAX_GROUP];  // per-lane table index: stage in LDS
+  if (threadIdx.x < T) sd[threadIdx.x] = g.d[threadIdx.x];
+  __syncthreads();
   constexpr int GPB = 256 / G;
   const int64_t N = g.koff[T];
   const int64_t p0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * NB;
@@ -816,7 +819,7 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
       const int64_t next = p + 1 < N ? (int64_t)skey[p + 1] : -1;
       if (u < N && u != prev) {  // u == N: sentinel for out-of-range idx
         const int t = table_of(g.koff, T, u, ufirst < N ? ufirst : 0);
-        const dr_pool_grad_desc& d = g.d[t];
+        const dr_pool_grad_desc& d = sd[t];
         head[q] = true;
         single[q] = u != next;
         uq[q] = u;
@@ -836,7 +839,7 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
     if (!head[q]) continue;
-    const dr_pool_grad_desc& d = g.d[tq[q]];
+    const dr_pool_grad_desc& d = sd[tq[q]];
     const int mode = d.combiner == DR_COMBINER_SUM ? 0 : (d.combiner == DR_COMBINER_MEAN ? 1 : 2);
     R acc;
 #pragma unroll
