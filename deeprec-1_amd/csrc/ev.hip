@@ -1720,9 +1720,13 @@ __global__ __launch_bounds__(256) void xgmi_emit_kernel(XgmiRowArgs a,
     for (int k = 0; k < NB; ++k)
       if (dst[k]) __builtin_nontemporal_store(x[k], reinterpret_cast<xf4*>(dst[k]) + lg);
   }
-  __syncthreads();
-  if (threadIdx.x == 0) __threadfence_system();  // remote stores performed before the end
+  // no per-block system fence here: xgmi_flush_kernel follows the launch
 }
+
+// System-scope release on every XCD (blocks are dispatched round-robin over
+// the 8 XCDs; 64 blocks cover each several times): writes back whatever the
+// previous kernel left in the XCDs' L2 for the peers' memory.
+__global__ void xgmi_flush_kernel() { __threadfence_system(); }
 
 struct XgmiWs {
   int64_t* rows;
@@ -1794,21 +1798,26 @@ int dr_xgmi_serve(const dr_xgmi_peers* peers, dr_ev* const* evs, int num_tables,
   int* stw = status_word();
   DR_REQUIRE(stw, DR_INTERNAL, "status word unavailable");
   hipStream_t st = S(stream);
-  // expected keys per source ~ T*B / W; a few hundred blocks per source
+  // One-shot grids sized for 1.25x the keys a source sends on average
+  // (T*B / W for keys spread over owners); the kernels' grid-stride loops
+  // take any excess (skewed keys) in a second pass.  Small grids with long
+  // grid-stride loops measured ~30% slower on the emit.
   const int64_t per_src = std::max<int64_t>(1, (int64_t)num_tables * batch / W);
-  const unsigned gx = (unsigned)std::min<int64_t>(1024, std::max<int64_t>(1, ceil_div(per_src, 1024)));
+  const int64_t expect = per_src + per_src / 4 + 256;
+  const unsigned gx = (unsigned)ceil_div(expect, 256);
   hipLaunchKernelGGL(xgmi_resolve_kernel, dim3(gx, W), dim3(256), 0, st, ra, w.rows, w.init, stw);
   hipLaunchKernelGGL(xgmi_init_kernel, dim3(gx, W), dim3(256), 0, st, wa, w.rows, w.init);
   const int dv = (int)(dim / 4);
-  const unsigned ge = (unsigned)std::min<int64_t>(2048, std::max<int64_t>(1, ceil_div(per_src, 64)));
+  auto ge = [&](int G) { return dim3((unsigned)ceil_div(expect, (256 / G) * 4), W); };
   if (dv <= 8)
-    hipLaunchKernelGGL((xgmi_emit_kernel<8, 4>), dim3(ge, W), dim3(256), 0, st, wa, w.rows);
+    hipLaunchKernelGGL((xgmi_emit_kernel<8, 4>), ge(8), dim3(256), 0, st, wa, w.rows);
   else if (dv <= 16)
-    hipLaunchKernelGGL((xgmi_emit_kernel<16, 4>), dim3(ge, W), dim3(256), 0, st, wa, w.rows);
+    hipLaunchKernelGGL((xgmi_emit_kernel<16, 4>), ge(16), dim3(256), 0, st, wa, w.rows);
   else if (dv <= 32)
-    hipLaunchKernelGGL((xgmi_emit_kernel<32, 4>), dim3(ge, W), dim3(256), 0, st, wa, w.rows);
+    hipLaunchKernelGGL((xgmi_emit_kernel<32, 4>), ge(32), dim3(256), 0, st, wa, w.rows);
   else
-    hipLaunchKernelGGL((xgmi_emit_kernel<64, 4>), dim3(ge, W), dim3(256), 0, st, wa, w.rows);
+    hipLaunchKernelGGL((xgmi_emit_kernel<64, 4>), ge(64), dim3(256), 0, st, wa, w.rows);
+  hipLaunchKernelGGL(xgmi_flush_kernel, dim3(64), dim3(64), 0, st);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

@@ -77,13 +77,17 @@ __global__ __launch_bounds__(256) void xgmi_route_kernel(XgmiArgs a, const int64
     __builtin_nontemporal_store(keys[(int64_t)t * B + b], a.inbox_keys[o] + at);
     __builtin_nontemporal_store((int32_t)j, a.inbox_slot[o] + at);
   }
-  __syncthreads();
-  if (threadIdx.x == 0) __threadfence_system();  // remote stores performed before the end
+  // no per-block system fence (one per block cost more than the kernel):
+  // xgmi_counts_kernel flushes every XCD's L2 right after this launch
 }
 
+// Runs after the route kernel: every block issues a system-scope release
+// (L2 write-back of the XCD it runs on; 64 blocks cover the 8 XCDs), and
+// block 0 publishes this rank's per-owner counts.
 __global__ void xgmi_counts_kernel(XgmiArgs a, const unsigned long long* __restrict__ cnt) {
+  __threadfence_system();
   const int p = threadIdx.x;
-  if (p < a.world) {
+  if (blockIdx.x == 0 && p < a.world) {
     __hip_atomic_store(a.inbox_cnt[p] + a.rank, (int64_t)cnt[p], __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -157,7 +161,7 @@ int dr_xgmi_route(const dr_xgmi_peers* peers, const int64_t* keys, int num_table
     hipLaunchKernelGGL(xgmi_route_kernel, dim3((unsigned)ceil_div(n, 256 * RT_ITEMS)), dim3(256),
                        0, st, a, keys, num_tables, batch, (unsigned long long*)cnt_ws);
   }
-  hipLaunchKernelGGL(xgmi_counts_kernel, dim3(1), dim3(64), 0, st, a,
+  hipLaunchKernelGGL(xgmi_counts_kernel, dim3(64), dim3(64), 0, st, a,
                      (const unsigned long long*)cnt_ws);
   DR_LAUNCH_CHECK();
   return DR_OK;
