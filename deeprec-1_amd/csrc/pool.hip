@@ -362,6 +362,9 @@ __global__ __launch_bounds__(256) void pool_onehot_kernel(PoolArgs args, int T, 
 template <int VEC, int G, int CPL, int ORDER, int NB>
 __global__ __launch_bounds__(256) void pool_fast_kernel(PoolArgs args, int T, int64_t B, int dim,
                                                         int64_t chunks_per_table, int* st) {
+  __shared__ dr_pool_desc sd[DR_MAX_GROUP];  // per-group table index: stage in LDS
+  if (threadIdx.x < T) sd[threadIdx.x] = args.d[threadIdx.x];
+  __syncthreads();
   constexpr int GPB = 256 / G;
   const int64_t item = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
   if (item >= (int64_t)T * chunks_per_table) return;
@@ -369,7 +372,7 @@ __global__ __launch_bounds__(256) void pool_fast_kernel(PoolArgs args, int T, in
   const int64_t b0 = (item - (int64_t)t * chunks_per_table) * NB;
   const int lg = threadIdx.x % G;
   const int dv = dim / VEC;
-  const dr_pool_desc& d = args.d[t];
+  const dr_pool_desc& d = sd[t];
   int off[NB + 1];
   if (!chunk_is_fast<NB>(d, b0, B, off)) return;
   Row<VEC, G, CPL> x[NB];
@@ -386,6 +389,9 @@ template <int VEC, int G, int CPL, int ORDER, int NB>
 __global__ __launch_bounds__(256) void pool_general_kernel(PoolArgs args, int T, int64_t B,
                                                            int dim, int64_t chunks_per_table,
                                                            int* st) {
+  __shared__ dr_pool_desc sd[DR_MAX_GROUP];  // per-group table index: stage in LDS
+  if (threadIdx.x < T) sd[threadIdx.x] = args.d[threadIdx.x];
+  __syncthreads();
   constexpr int GPB = 256 / G;
   const int64_t item = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
   if (item >= (int64_t)T * chunks_per_table) return;
@@ -393,7 +399,7 @@ __global__ __launch_bounds__(256) void pool_general_kernel(PoolArgs args, int T,
   const int64_t b0 = (item - (int64_t)t * chunks_per_table) * NB;
   const int lg = threadIdx.x % G;
   const int dv = dim / VEC;
-  const dr_pool_desc& d = args.d[t];
+  const dr_pool_desc& d = sd[t];
   int off[NB + 1];
   if (chunk_is_fast<NB>(d, b0, B, off)) return;  // taken by pool_fast_kernel
   int64_t nbag = B - b0;

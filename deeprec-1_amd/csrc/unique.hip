@@ -73,12 +73,18 @@ __device__ __forceinline__ int group_table(const UniqGroup& g, int T, int64_t i)
 __global__ void unique_insert_kernel(UniqGroup g, int T, const int64_t* __restrict__ keys,
                                      uint64_t* __restrict__ tkeys, uint32_t* __restrict__ minpos,
                                      int32_t* __restrict__ slot_of) {
+  __shared__ int64_t shcap[DR_MAX_GROUP], shbase[DR_MAX_GROUP];  // per-lane table: LDS
+  if (threadIdx.x < T) {
+    shcap[threadIdx.x] = g.hcap[threadIdx.x];
+    shbase[threadIdx.x] = g.hbase[threadIdx.x];
+  }
+  __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= g.koff[T]) return;
   const int t = group_table(g, T, i);
   const uint64_t k = (uint64_t)keys[i];
-  const int64_t cap = g.hcap[t];
-  uint64_t* tk = tkeys + g.hbase[t];
+  const int64_t cap = shcap[t];
+  uint64_t* tk = tkeys + shbase[t];
   int64_t s;
   if (k == kEmpty) {
     s = cap;
@@ -96,7 +102,7 @@ __global__ void unique_insert_kernel(UniqGroup g, int T, const int64_t* __restri
     }
     s = (int64_t)h;
   }
-  s += g.hbase[t];
+  s += shbase[t];
   atomicMin(&minpos[s], (uint32_t)i);
   slot_of[i] = (int32_t)s;
 }
