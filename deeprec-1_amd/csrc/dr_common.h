@@ -8,11 +8,29 @@
 
 namespace dr {
 
+// Nontemporal (stream-once) loads / stores of float / float4.
+typedef float nf4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 nt_load(const float4* p) {
+  const nf4 v = __builtin_nontemporal_load(reinterpret_cast<const nf4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float nt_load(const float* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void nt_store(float4 v, float4* p) {
+  nf4 w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<nf4*>(p));
+}
+__device__ __forceinline__ void nt_store(float v, float* p) { __builtin_nontemporal_store(v, p); }
+
 void set_error(const char* fmt, ...);
 // Device status word of the current device (latched by kernels).
 int* status_word();
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// pool.hip: EV copy-out, out[i] = rows[i] >= 0 ? pool[rows[i]] : (defaults ?
+// defaults[i] : dflt); the gather-copy kernel (dwordx4, nontemporal).
+int gather_ev_rows(const float* pool, int64_t dim, const int64_t* rows, int64_t n,
+                   const float* defaults, const float* dflt, float* out, hipStream_t s);
 
 #define DR_HIP(x)                                                              \
   do {                                                                         \

@@ -452,18 +452,6 @@ __global__ void ev_init_rows_kernel(InitGroup g, int T, int64_t dim,
   }
 }
 
-// Copy-out for dr_ev_gather: out[i] = row >= 0 ? pool[row] : default(i).
-__global__ void ev_copy_out_kernel(const float* __restrict__ pool, int64_t dim,
-                                   const int64_t* __restrict__ rows, const float* __restrict__ defaults,
-                                   const float* __restrict__ dflt, int64_t n, const int64_t* n_dev,
-                                   float* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
-  if (i >= eff_n(n, n_dev)) return;
-  const int64_t r = rows[i];
-  const float* src = r >= 0 ? pool + r * dim : (defaults ? defaults + i * dim : dflt);
-  for (int64_t c = threadIdx.x % 64; c < dim; c += 64) out[i * dim + c] = src[c];
-}
-
 // Owner-side row pack of the sharded exchange: out[i] = pool_t[row_i] (or the
 // table's default row when filtered), t from the composite key.  G lanes per
 // row, dwordx4.
@@ -1028,6 +1016,16 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
   DR_REQUIRE(stw, DR_INTERNAL, "status word unavailable");
   const int64_t dim = vars[0] ? vars[0]->sh->dim : 0;
   const int ncol = opt == OPT_SGD ? 1 : (opt == OPT_ADAGRAD ? 2 : 3);
+  // Capacity first: a reserve may grow (reallocate) the slot table and the
+  // row pools, so no pointer may be read into a descriptor before it.
+  for (int t = 0; t < T; ++t) {
+    DR_REQUIRE(vars[t] && vars[t]->col == 0, DR_INVALID_ARGUMENT,
+               "table %d: var must be a primary EV", t);
+    if (n_host[t] > 0) {
+      int rc = reserve(vars[t]->sh, n_host[t], st);
+      if (rc) return rc;
+    }
+  }
   for (int c0 = 0; c0 < T; c0 += kApplyGroup) {
     const int tn = std::min(kApplyGroup, T - c0);
     ApplyGroup ag;
@@ -1037,8 +1035,6 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
     for (int j = 0; j < tn; ++j) {
       const int t = c0 + j;
       dr_ev* var = vars[t];
-      DR_REQUIRE(var && var->col == 0, DR_INVALID_ARGUMENT, "table %d: var must be a primary EV",
-                 t);
       EvShared* s = var->sh;
       DR_REQUIRE(s->dim == dim, DR_INVALID_ARGUMENT, "grouped apply needs equal dims");
       dr_ev* cv[3] = {var, s1 ? s1[t] : nullptr, s2 ? s2[t] : nullptr};
@@ -1059,10 +1055,6 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
       a.n = n_host[t];
       a.n_dev = n_dev ? n_dev[t] : nullptr;
       a.steps_to_live = s->steps_to_live;
-      if (a.n > 0) {
-        int rc = reserve(s, a.n, st);
-        if (rc) return rc;
-      }
       nmax = std::max(nmax, a.n);
     }
     if (nmax == 0) continue;
@@ -1326,11 +1318,8 @@ int dr_ev_gather(dr_ev* ev, const int64_t* keys, int64_t n, const float* default
   DR_REQUIRE(ws_bytes >= c.used, DR_INVALID_ARGUMENT, "workspace too small");
   int rc = dr_ev_resolve(ev, keys, n, nullptr, defaults, counts, rows, rws, rneed, stream);
   if (rc) return rc;
-  hipLaunchKernelGGL(ev_copy_out_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, S(stream),
-                     ev->sh->pools[ev->col], ev->sh->dim, rows, defaults,
-                     ev->sh->defaults[ev->col], n, nullptr, out);
-  DR_LAUNCH_CHECK();
-  return DR_OK;
+  return gather_ev_rows(ev->sh->pools[ev->col], ev->sh->dim, rows, n, defaults,
+                        ev->sh->defaults[ev->col], out, S(stream));
 }
 
 size_t dr_ev_gather_workspace_size(int64_t n) {

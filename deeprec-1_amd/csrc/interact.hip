@@ -29,9 +29,46 @@ __global__ void fm2_kernel(const float* __restrict__ emb, int64_t B, int F, int 
   reinterpret_cast<float4*>(out + b * (int64_t)D)[c] = o;
 }
 
-// d fm / d e_f = (sum_f' e_f' - e_f) * g
-__global__ void fm2_grad_kernel(const float* __restrict__ emb, const float* __restrict__ g,
-                                int64_t B, int F, int D, float* __restrict__ ge) {
+// d fm / d e_f = (sum_f' e_f' - e_f) * g.  Thread per (b, 4 columns); the F
+// field vectors stay in registers between the sum and the write (a second
+// read pass went back to HBM: the in-flight working set outgrows L2).
+template <int FM>
+__global__ __launch_bounds__(256) void fm2_grad_kernel(const float* __restrict__ emb,
+                                                       const float* __restrict__ g, int64_t B,
+                                                       int F, int D, float* __restrict__ ge) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int D4 = D / 4;
+  if (t >= B * D4) return;
+  const int64_t b = t / D4;
+  const int c = (int)(t - b * D4);
+  const float4* p = reinterpret_cast<const float4*>(emb + b * (int64_t)F * D) + c;
+  float4 e[FM];
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int f = 0; f < FM; ++f)
+    if (f < F) e[f] = nt_load(p + (int64_t)f * D4);
+#pragma unroll
+  for (int f = 0; f < FM; ++f)
+    if (f < F) {
+      s.x += e[f].x; s.y += e[f].y; s.z += e[f].z; s.w += e[f].w;
+    }
+  const float4 gv = reinterpret_cast<const float4*>(g + b * (int64_t)D)[c];
+  float4* q = reinterpret_cast<float4*>(ge + b * (int64_t)F * D) + c;
+#pragma unroll
+  for (int f = 0; f < FM; ++f)
+    if (f < F) {
+      float4 o;
+      o.x = (s.x - e[f].x) * gv.x;
+      o.y = (s.y - e[f].y) * gv.y;
+      o.z = (s.z - e[f].z) * gv.z;
+      o.w = (s.w - e[f].w) * gv.w;
+      nt_store(o, q + (int64_t)f * D4);
+    }
+}
+
+// Any shape: scalar, two passes.
+__global__ void fm2_grad_any_kernel(const float* __restrict__ emb, const float* __restrict__ g,
+                                    int64_t B, int F, int D, float* __restrict__ ge) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= B * D) return;
   const int64_t b = t / D;
@@ -43,7 +80,14 @@ __global__ void fm2_grad_kernel(const float* __restrict__ emb, const float* __re
   for (int f = 0; f < F; ++f) ge[b * (int64_t)F * D + (int64_t)f * D + d] = (s - p[(int64_t)f * D]) * gv;
 }
 
-// One block per sample: X [F, D] staged in LDS (row stride D+1 to break bank
+// DLRM dot, register-tiled: one wave per sample, X [F, D] staged in LDS
+// (rows padded to a multiple of 4, row stride D+4 floats).  The lower
+// triangle of X X^T is cut into 4x4 tiles (nb = ceil(F/4) row blocks,
+// nb(nb+1)/2 <= 32 tiles); lane = 2*tile + khalf accumulates its tile's 16
+// dot products over alternate 4-float K slices with dwordx4 LDS reads (8
+// reads per 64 FMAs), and one xor-shuffle adds the two partial sums.  LDS traffic per sample ~ tiles x 8
+// rows x D floats instead of 2 rows x D per pair.
+// Any shape: one block per sample: X [F, D] staged in LDS (row stride D+1 to break bank
 // conflicts), thread per lower-triangle pair (i > j), row-major pair order.
 __global__ void dot_kernel(const float* __restrict__ x, int F, int D, float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) float xs[];
@@ -65,6 +109,91 @@ __global__ void dot_kernel(const float* __restrict__ x, int F, int D, float* __r
     for (int d = 0; d < D; ++d) s += a[d] * c[d];
     out[b * (int64_t)P + p] = s;
   }
+}
+
+static constexpr int DOT_WAVES = 4;
+static constexpr int DOT_MAXE = 16;  // float4 per lane when staging: F_pad * D / 4 <= 1024
+
+__global__ __launch_bounds__(256) void dot_tile_kernel(const float* __restrict__ x, int64_t B,
+                                                       int F, int D, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float xs_all[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * DOT_WAVES + wave;
+  const int Fp = (F + 3) & ~3;
+  const int ld = D + 4;
+  float* xs = xs_all + (size_t)wave * Fp * ld;
+  if (b < B) {
+    // all of the lane's loads first (a load -> LDS store loop would wait out
+    // one HBM latency per iteration)
+    const float4* src = reinterpret_cast<const float4*>(x + b * (int64_t)F * D);
+    const int D4 = D / 4;
+    const int n4 = Fp * D4, nv = F * D4;
+    float4 v[DOT_MAXE];
+#pragma unroll
+    for (int q = 0; q < DOT_MAXE; ++q) {
+      const int e = lane + q * 64;
+      v[q] = e < nv ? nt_load(src + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < DOT_MAXE; ++q) {
+      const int e = lane + q * 64;
+      if (e < n4) {
+        const int r = e / D4, c = e - r * D4;
+        *reinterpret_cast<float4*>(xs + r * ld + c * 4) = v[q];
+      }
+    }
+  }
+  __syncthreads();
+  if (b >= B) return;
+  const int nb = Fp / 4;
+  const int tiles = nb * (nb + 1) / 2;
+  const int tile = lane >> 1, kh = lane & 1;
+  int bi = 0, bj = 0;
+  if (tile < tiles) {
+    // tile -> (bi >= bj), row-major over the lower block triangle
+    while ((bi + 1) * (bi + 2) / 2 <= tile) ++bi;
+    bj = tile - bi * (bi + 1) / 2;
+  }
+  float acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  if (tile < tiles) {
+    const float* A = xs + (bi * 4) * ld;
+    const float* Bm = xs + (bj * 4) * ld;
+    // lanes 2t, 2t+1 take alternate 4-float slices of K (adjacent banks)
+    for (int k = kh * 4; k < D; k += 8) {
+      float4 a[4], c[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const float4*>(A + i * ld + k);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c[j] = *reinterpret_cast<const float4*>(Bm + j * ld + k);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[i][j] = fmaf(a[i].x, c[j].x, acc[i][j]);
+          acc[i][j] = fmaf(a[i].y, c[j].y, acc[i][j]);
+          acc[i][j] = fmaf(a[i].z, c[j].z, acc[i][j]);
+          acc[i][j] = fmaf(a[i].w, c[j].w, acc[i][j]);
+        }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] += __shfl_xor(acc[i][j], 1, 64);
+  if (tile >= tiles || kh) return;
+  const int64_t P = (int64_t)F * (F - 1) / 2;
+  float* o = out + b * P;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int gi = bi * 4 + i, gj = bj * 4 + j;
+      if (gi < F && gj < gi) o[gi * (gi - 1) / 2 + gj] = acc[i][j];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -178,9 +307,22 @@ int dr_fm2_grad(const float* emb, const float* top_grad, int64_t batch, int fiel
   using namespace dr;
   DR_REQUIRE(batch >= 0 && fields > 0 && dim > 0, DR_INVALID_ARGUMENT, "bad shape");
   if (batch == 0) return DR_OK;
-  const int64_t n = batch * dim;
-  hipLaunchKernelGGL(fm2_grad_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, S(stream),
-                     emb, top_grad, batch, fields, dim, grad_emb);
+  const bool al = ((((uintptr_t)emb) | ((uintptr_t)top_grad) | ((uintptr_t)grad_emb)) & 15) == 0;
+  if (dim % 4 == 0 && al && fields <= 32) {
+    const unsigned blocks = (unsigned)ceil_div(batch * (dim / 4), 256);
+    if (fields <= 8)
+      hipLaunchKernelGGL(fm2_grad_kernel<8>, dim3(blocks), dim3(256), 0, S(stream), emb, top_grad,
+                         batch, fields, dim, grad_emb);
+    else if (fields <= 16)
+      hipLaunchKernelGGL(fm2_grad_kernel<16>, dim3(blocks), dim3(256), 0, S(stream), emb,
+                         top_grad, batch, fields, dim, grad_emb);
+    else
+      hipLaunchKernelGGL(fm2_grad_kernel<32>, dim3(blocks), dim3(256), 0, S(stream), emb,
+                         top_grad, batch, fields, dim, grad_emb);
+  } else {
+    hipLaunchKernelGGL(fm2_grad_any_kernel, dim3((unsigned)ceil_div(batch * dim, 256)), dim3(256),
+                       0, S(stream), emb, top_grad, batch, fields, dim, grad_emb);
+  }
   DR_LAUNCH_CHECK();
   return DR_OK;
 }
@@ -192,6 +334,15 @@ int dr_dot_interaction(const float* x, int64_t batch, int fields, int dim, float
   const size_t lds = (size_t)fields * (dim + 1) * sizeof(float);
   DR_REQUIRE(lds <= 64 * 1024, DR_INVALID_ARGUMENT, "fields*dim too large for one block");
   if (batch == 0) return DR_OK;
+  const int nb = (fields + 3) / 4;
+  const size_t tlds = (size_t)DOT_WAVES * nb * 4 * (dim + 4) * sizeof(float);
+  if (nb * (nb + 1) / 2 <= 32 && dim % 8 == 0 && ((uintptr_t)x & 15) == 0 && tlds <= 64 * 1024 &&
+      nb * 4 * (dim / 4) <= DOT_MAXE * 64) {
+    hipLaunchKernelGGL(dot_tile_kernel, dim3((unsigned)ceil_div(batch, DOT_WAVES)), dim3(256), tlds,
+                       S(stream), x, batch, fields, dim, out);
+    DR_LAUNCH_CHECK();
+    return DR_OK;
+  }
   hipLaunchKernelGGL(dot_kernel, dim3((unsigned)batch), dim3(256), lds, S(stream), x, fields, dim,
                      out);
   DR_LAUNCH_CHECK();

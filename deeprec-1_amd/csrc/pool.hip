@@ -105,12 +105,6 @@ __device__ __forceinline__ void load_row(Row<VEC, G, CPL>& x, const float* p, in
 }
 
 // Rows read exactly once per launch: nontemporal hint (no L2 retention).
-typedef float nf4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 nt_load(const float4* p) {
-  const nf4 v = __builtin_nontemporal_load(reinterpret_cast<const nf4*>(p));
-  return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ float nt_load(const float* p) { return __builtin_nontemporal_load(p); }
 
 template <int VEC, int G, int CPL>
 __device__ __forceinline__ void load_row_nt(Row<VEC, G, CPL>& x, const float* p, int lg, int dv) {
@@ -122,11 +116,6 @@ __device__ __forceinline__ void load_row_nt(Row<VEC, G, CPL>& x, const float* p,
   }
 }
 
-__device__ __forceinline__ void nt_store(float4 v, float4* p) {
-  nf4 w = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(w, reinterpret_cast<nf4*>(p));
-}
-__device__ __forceinline__ void nt_store(float v, float* p) { __builtin_nontemporal_store(v, p); }
 
 template <int VEC, int G, int CPL>
 __device__ __forceinline__ void store_row_nt(const Row<VEC, G, CPL>& x, float* p, int lg, int dv) {
@@ -185,22 +174,128 @@ __device__ __forceinline__ void fetch(Row<VEC, G, CPL>& x, const dr_pool_desc& d
   if (d.max_norm >= 0.f) clip_row<VEC, G, CPL, ORDER>(x, d.max_norm);
 }
 
-// One bag, general length, in the reference association order.
+template <int VEC, int G, int CPL, int ORDER>
+__device__ __forceinline__ void fetch_p(Row<VEC, G, CPL>& x, const float* p, float max_norm,
+                                        int lg, int dv) {
+  load_row<VEC, G, CPL>(x, p, lg, dv);
+  if (max_norm >= 0.f) clip_row<VEC, G, CPL, ORDER>(x, max_norm);
+}
+
+// Row pointers of up to 4G bag positions, one per lane and window, fetched
+// in parallel by the G lanes of a group before any row load (the idx -> row
+// chain is paid once per bag instead of once per 8-row chunk); position k is
+// read back with a shuffle inside the group.
+template <int G>
+struct BagPtrs {
+  const float* p[4];
+  int base;  // first lane of the group
+  __device__ __forceinline__ const float* at(int64_t k) const {
+    const int w = (int)(k / G), j = (int)(k % G);
+    const float* q = w == 0 ? p[0] : (w == 1 ? p[1] : (w == 2 ? p[2] : p[3]));
+    const uint64_t u = (uint64_t)(uintptr_t)q;
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)u, base + j, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(u >> 32), base + j, 64);
+    return reinterpret_cast<const float*>((uintptr_t)(((uint64_t)hi << 32) | lo));
+  }
+};
+
+// Unweighted bag of `num` rows, P(k) = row pointer of position k, summed in
+// the reference association order.
+template <int VEC, int G, int CPL, int ORDER, class PtrAt>
+__device__ __forceinline__ void pool_bag_rows(const dr_pool_desc& d, int64_t num, float* out,
+                                              int lg, int dv, const PtrAt& P) {
+  using R = Row<VEC, G, CPL>;
+  R acc;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<typename VecT<VEC>::T>();
+  if (ORDER == DR_ORDER_SEQ) {
+    // out = 0; out += e_k ...; Combine: / sqrtf(n) or / n
+    int64_t k = 0;
+    for (; k + 4 <= num; k += 4) {
+      R x0, x1, x2, x3;
+      fetch_p<VEC, G, CPL, ORDER>(x0, P(k), d.max_norm, lg, dv);
+      fetch_p<VEC, G, CPL, ORDER>(x1, P(k + 1), d.max_norm, lg, dv);
+      fetch_p<VEC, G, CPL, ORDER>(x2, P(k + 2), d.max_norm, lg, dv);
+      fetch_p<VEC, G, CPL, ORDER>(x3, P(k + 3), d.max_norm, lg, dv);
+      acc_add(acc, x0);
+      acc_add(acc, x1);
+      acc_add(acc, x2);
+      acc_add(acc, x3);
+    }
+    for (; k < num; ++k) {
+      R x;
+      fetch_p<VEC, G, CPL, ORDER>(x, P(k), d.max_norm, lg, dv);
+      acc_add(acc, x);
+    }
+    if (d.combiner != DR_COMBINER_SUM) {
+      const float q = d.combiner == DR_COMBINER_SQRTN ? sqrtf((float)num) : (float)num;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) acc.v[c] = vdiv(acc.v[c], q);
+    }
+    store_row<VEC, G, CPL>(acc, out, lg, dv);
+    return;
+  }
+  // ORDER_ALI
+  if (num == 1) {
+    fetch_p<VEC, G, CPL, ORDER>(acc, P(0), d.max_norm, lg, dv);
+    store_row<VEC, G, CPL>(acc, out, lg, dv);
+    return;
+  }
+  int64_t r = num % 8;
+  if (r == 0) r = 8;
+  if (r == 1) r = 9;
+  {
+    R x[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j)
+      if (j < r) fetch_p<VEC, G, CPL, ORDER>(x[j], P(j), d.max_norm, lg, dv);
+    acc = x[0];
+#pragma unroll
+    for (int j = 1; j < 9; ++j)
+      if (j < r) acc_add(acc, x[j]);
+  }
+  if (num < 10 && d.combiner != DR_COMBINER_SUM) {
+    const float m = d.combiner == DR_COMBINER_MEAN ? (float)num : (float)sqrt((double)num);
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) acc.v[c] = vdiv(acc.v[c], m);
+  }
+  for (int64_t g = r; g < num; g += 8) {
+    R x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fetch_p<VEC, G, CPL, ORDER>(x[j], P(g + j), d.max_norm, lg, dv);
+    R s = x[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) acc_add(s, x[j]);
+    acc_add(acc, s);
+  }
+  if (num >= 10 && d.combiner != DR_COMBINER_SUM) {
+    const float q = d.combiner == DR_COMBINER_MEAN ? (float)num : (float)sqrt((double)num);
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) acc.v[c] = vdiv(acc.v[c], q);
+  }
+  store_row<VEC, G, CPL>(acc, out, lg, dv);
+}
+
+// One bag, general length, in the reference association order.  Called by
+// every lane of a group together (the shuffles of BagPtrs need that).
 template <int VEC, int G, int CPL, int ORDER>
 __device__ void pool_bag(const dr_pool_desc& d, int64_t b, int dim, int lg, int dv, int* st) {
   using R = Row<VEC, G, CPL>;
   const int64_t k0 = d.bag_off[b];
   const int64_t num = (int64_t)d.bag_off[b + 1] - k0;
   float* out = d.out + b * d.out_stride;
-  R acc;
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<typename VecT<VEC>::T>();
   if (num <= 0) {
-    store_row<VEC, G, CPL>(acc, out, lg, dv);
+    R z;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) z.v[c] = vzero<typename VecT<VEC>::T>();
+    store_row<VEC, G, CPL>(z, out, lg, dv);
     return;
   }
   if (d.weights) {
     // embedding_ops.py:609-651: gather * w, segment_sum, / sum(w) or sqrt(sum(w^2))
+    R acc;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<typename VecT<VEC>::T>();
     float wsum = 0.f;
     for (int64_t k = 0; k < num; ++k) {
       R x;
@@ -218,72 +313,20 @@ __device__ void pool_bag(const dr_pool_desc& d, int64_t b, int dim, int lg, int 
     store_row<VEC, G, CPL>(acc, out, lg, dv);
     return;
   }
-  if (ORDER == DR_ORDER_SEQ) {
-    // out = 0; out += e_k ...; Combine: / sqrtf(n) or / n
-    int64_t k = 0;
-    for (; k + 4 <= num; k += 4) {
-      R x0, x1, x2, x3;
-      fetch<VEC, G, CPL, ORDER>(x0, d, k0 + k, dim, lg, dv, st);
-      fetch<VEC, G, CPL, ORDER>(x1, d, k0 + k + 1, dim, lg, dv, st);
-      fetch<VEC, G, CPL, ORDER>(x2, d, k0 + k + 2, dim, lg, dv, st);
-      fetch<VEC, G, CPL, ORDER>(x3, d, k0 + k + 3, dim, lg, dv, st);
-      acc_add(acc, x0);
-      acc_add(acc, x1);
-      acc_add(acc, x2);
-      acc_add(acc, x3);
-    }
-    for (; k < num; ++k) {
-      R x;
-      fetch<VEC, G, CPL, ORDER>(x, d, k0 + k, dim, lg, dv, st);
-      acc_add(acc, x);
-    }
-    if (d.combiner != DR_COMBINER_SUM) {
-      const float q = d.combiner == DR_COMBINER_SQRTN ? sqrtf((float)num) : (float)num;
+  if (G >= 8 && num <= 4 * G) {
+    BagPtrs<G> bp;
+    bp.base = (int)(threadIdx.x % 64) - lg;
 #pragma unroll
-      for (int c = 0; c < CPL; ++c) acc.v[c] = vdiv(acc.v[c], q);
+    for (int w = 0; w < 4; ++w) {
+      const int64_t k = (int64_t)w * G + lg;
+      bp.p[w] = k < num ? select_row(d, k0 + k, dim, st) : nullptr;
     }
-    store_row<VEC, G, CPL>(acc, out, lg, dv);
+    pool_bag_rows<VEC, G, CPL, ORDER>(d, num, out, lg, dv,
+                                      [&](int64_t k) { return bp.at(k); });
     return;
   }
-  // ORDER_ALI
-  if (num == 1) {
-    fetch<VEC, G, CPL, ORDER>(acc, d, k0, dim, lg, dv, st);
-    store_row<VEC, G, CPL>(acc, out, lg, dv);
-    return;
-  }
-  int64_t r = num % 8;
-  if (r == 0) r = 8;
-  if (r == 1) r = 9;
-  {
-    R x[9];
-#pragma unroll
-    for (int j = 0; j < 9; ++j)
-      if (j < r) fetch<VEC, G, CPL, ORDER>(x[j], d, k0 + j, dim, lg, dv, st);
-    acc = x[0];
-#pragma unroll
-    for (int j = 1; j < 9; ++j)
-      if (j < r) acc_add(acc, x[j]);
-  }
-  if (num < 10 && d.combiner != DR_COMBINER_SUM) {
-    const float m = d.combiner == DR_COMBINER_MEAN ? (float)num : (float)sqrt((double)num);
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) acc.v[c] = vdiv(acc.v[c], m);
-  }
-  for (int64_t g = r; g < num; g += 8) {
-    R x[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) fetch<VEC, G, CPL, ORDER>(x[j], d, k0 + g + j, dim, lg, dv, st);
-    R s = x[0];
-#pragma unroll
-    for (int j = 1; j < 8; ++j) acc_add(s, x[j]);
-    acc_add(acc, s);
-  }
-  if (num >= 10 && d.combiner != DR_COMBINER_SUM) {
-    const float q = d.combiner == DR_COMBINER_MEAN ? (float)num : (float)sqrt((double)num);
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) acc.v[c] = vdiv(acc.v[c], q);
-  }
-  store_row<VEC, G, CPL>(acc, out, lg, dv);
+  pool_bag_rows<VEC, G, CPL, ORDER>(d, num, out, lg, dv,
+                                    [&](int64_t k) { return select_row(d, k0 + k, dim, st); });
 }
 
 // Pooling kernels:
@@ -385,31 +428,35 @@ __global__ __launch_bounds__(256) void pool_fast_kernel(PoolArgs args, int T, in
   }
 }
 
+// One bag per lane group (multi-hot bags need the parallelism: a group per
+// chunk of NB bags left most of the chip idle), over a capped grid that
+// strides through the bags so the per-block descriptor staging and the
+// early exits of fast chunks stay cheap.
 template <int VEC, int G, int CPL, int ORDER, int NB>
 __global__ __launch_bounds__(256) void pool_general_kernel(PoolArgs args, int T, int64_t B,
-                                                           int dim, int64_t chunks_per_table,
-                                                           int* st) {
+                                                           int dim, int* st) {
   __shared__ dr_pool_desc sd[DR_MAX_GROUP];  // per-group table index: stage in LDS
   if (threadIdx.x < T) sd[threadIdx.x] = args.d[threadIdx.x];
   __syncthreads();
   constexpr int GPB = 256 / G;
-  const int64_t item = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
-  if (item >= (int64_t)T * chunks_per_table) return;
-  const int t = (int)(item / chunks_per_table);
-  const int64_t b0 = (item - (int64_t)t * chunks_per_table) * NB;
   const int lg = threadIdx.x % G;
   const int dv = dim / VEC;
-  const dr_pool_desc& d = sd[t];
-  int off[NB + 1];
-  if (chunk_is_fast<NB>(d, b0, B, off)) return;  // taken by pool_fast_kernel
-  int64_t nbag = B - b0;
-  if (nbag > NB) nbag = NB;
-  for (int j = 0; j < nbag; ++j) pool_bag<VEC, G, CPL, ORDER>(d, b0 + j, dim, lg, dv, st);
+  const int64_t total = (int64_t)T * B;
+  for (int64_t item = (int64_t)blockIdx.x * GPB + threadIdx.x / G; item < total;
+       item += (int64_t)gridDim.x * GPB) {
+    const int t = (int)(item / B);
+    const int64_t b = item - (int64_t)t * B;
+    const dr_pool_desc& d = sd[t];
+    int off[NB + 1];
+    if (chunk_is_fast<NB>(d, b - b % NB, B, off)) continue;  // taken by pool_fast_kernel
+    pool_bag<VEC, G, CPL, ORDER>(d, b, dim, lg, dv, st);
+  }
 }
 
 enum { POOL_ONEHOT = 1 };
 static constexpr int kOneHotNB = 4;  // rows in flight per lane group (probe optimum)
 static constexpr int kChunkNB = 8;   // bags per chunk, fast/general split
+static constexpr int64_t kGeneralBlocks = 256 * 16;  // general-kernel grid cap (16 per CU)
 
 template <int VEC, int G, int CPL, int ORDER>
 static int launch_pool(const PoolArgs& a, int T, int64_t B, int dim, int flags, hipStream_t s,
@@ -424,8 +471,9 @@ static int launch_pool(const PoolArgs& a, int T, int64_t B, int dim, int flags, 
     const unsigned blocks = (unsigned)ceil_div((int64_t)T * cpt, 256 / G);
     hipLaunchKernelGGL((pool_fast_kernel<VEC, G, CPL, ORDER, kChunkNB>), dim3(blocks), dim3(256),
                        0, s, a, T, B, dim, cpt, st);
-    hipLaunchKernelGGL((pool_general_kernel<VEC, G, CPL, ORDER, kChunkNB>), dim3(blocks),
-                       dim3(256), 0, s, a, T, B, dim, cpt, st);
+    const int64_t gblocks = std::min<int64_t>(ceil_div((int64_t)T * B, 256 / G), kGeneralBlocks);
+    hipLaunchKernelGGL((pool_general_kernel<VEC, G, CPL, ORDER, kChunkNB>), dim3((unsigned)gblocks),
+                       dim3(256), 0, s, a, T, B, dim, st);
   }
   DR_LAUNCH_CHECK();
   return DR_OK;
@@ -549,10 +597,14 @@ static int launch_bag_offsets(const TI* seg, int64_t stride, int64_t n, const in
 // ---------------------------------------------------------------------------
 // Row gather (ResourceGather): group per index, NB indices per group.
 // ---------------------------------------------------------------------------
-template <int VEC, int G, int CPL>
+// EV mode (dr_ev_gather copy-out): ids are resolved rows, a negative row
+// takes default row i of `defaults` [n, dim] or, without it, the EV default.
+template <int VEC, int G, int CPL, bool EV>
 __global__ __launch_bounds__(256) void gather_kernel(const float* __restrict__ table, int64_t rows,
                                                      int dim, const int64_t* __restrict__ ids,
-                                                     int64_t n, float* __restrict__ out, int* st) {
+                                                     int64_t n, float* __restrict__ out, int* st,
+                                                     const float* __restrict__ defaults,
+                                                     const float* __restrict__ dflt) {
   constexpr int GPB = 256 / G;
   constexpr int NB = 4;
   const int64_t i0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * NB;
@@ -564,7 +616,9 @@ __global__ __launch_bounds__(256) void gather_kernel(const float* __restrict__ t
     const float* p = nullptr;
     if (i0 + j < n) {
       const int64_t r = ids[i0 + j];
-      if (r >= 0 && r < rows)
+      if (EV)
+        p = r >= 0 ? table + r * (int64_t)dim : (defaults ? defaults + (i0 + j) * dim : dflt);
+      else if (r >= 0 && r < rows)
         p = table + r * (int64_t)dim;
       else
         latch(st, DR_INVALID_ARGUMENT);
@@ -576,14 +630,50 @@ __global__ __launch_bounds__(256) void gather_kernel(const float* __restrict__ t
     if (i0 + j < n) store_row_nt<VEC, G, CPL>(x[j], out + (i0 + j) * (int64_t)dim, lg, dv);
 }
 
-template <int VEC, int G, int CPL>
+template <int VEC, int G, int CPL, bool EV>
 static int launch_gather(const float* table, int64_t rows, int dim, const int64_t* ids,
-                         int64_t n, float* out, hipStream_t s, int* st) {
+                         int64_t n, float* out, hipStream_t s, int* st, const float* defaults,
+                         const float* dflt) {
   const int64_t blocks = ceil_div(ceil_div(n, 4), 256 / G);
-  hipLaunchKernelGGL((gather_kernel<VEC, G, CPL>), dim3((unsigned)blocks), dim3(256), 0, s, table,
-                     rows, dim, ids, n, out, st);
+  hipLaunchKernelGGL((gather_kernel<VEC, G, CPL, EV>), dim3((unsigned)blocks), dim3(256), 0, s,
+                     table, rows, dim, ids, n, out, st, defaults, dflt);
   DR_LAUNCH_CHECK();
   return DR_OK;
+}
+
+template <bool EV>
+static int gather_dispatch(const float* table, int64_t rows, int d, const int64_t* ids, int64_t n,
+                           float* out, hipStream_t s, int* st, const float* defaults,
+                           const float* dflt) {
+  const bool al = ((((uintptr_t)table) | ((uintptr_t)out) | ((uintptr_t)defaults) |
+                    ((uintptr_t)dflt)) & 15) == 0;
+#define DR_G(VEC, G, CPL) \
+  return launch_gather<VEC, G, CPL, EV>(table, rows, d, ids, n, out, s, st, defaults, dflt)
+  if (d % 4 == 0 && al) {
+    const int d4 = d / 4;
+    if (d4 <= 4) DR_G(4, 4, 1);
+    if (d4 <= 8) DR_G(4, 8, 1);
+    if (d4 <= 16) DR_G(4, 16, 1);
+    if (d4 <= 32) DR_G(4, 32, 1);
+    if (d4 <= 64) DR_G(4, 64, 1);
+    DR_G(4, 64, 4);
+  }
+  if (d <= 8) DR_G(1, 8, 1);
+  if (d <= 32) DR_G(1, 32, 1);
+  if (d <= 64) DR_G(1, 64, 1);
+  if (d <= 256) DR_G(1, 64, 4);
+#undef DR_G
+  set_error("dim %d unsupported", d);
+  return DR_INVALID_ARGUMENT;
+}
+
+// dr_ev_gather's copy-out (ev.hip): out[i] = rows[i] >= 0 ? pool[rows[i]]
+// : (defaults ? defaults[i] : dflt).
+int gather_ev_rows(const float* pool, int64_t dim, const int64_t* rows, int64_t n,
+                   const float* defaults, const float* dflt, float* out, hipStream_t s) {
+  DR_REQUIRE(dim > 0 && dim <= 1024, DR_INVALID_ARGUMENT, "bad gather dim");
+  if (n == 0) return DR_OK;
+  return gather_dispatch<true>(pool, 0, (int)dim, rows, n, out, s, status_word(), defaults, dflt);
 }
 
 // ---------------------------------------------------------------------------
@@ -613,34 +703,46 @@ __global__ __launch_bounds__(256) void csr_sum_kernel(
 #pragma unroll
   for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<V>();
   const int32_t j0 = off[u], j1 = off[u + 1];
-  bool first = true;
-  for (int32_t j = j0; j < j1; ++j) {
-    const int32_t p = perm[j];
-    const int64_t r = seg_of_pos ? (int64_t)seg_of_pos[p] : (int64_t)p;
-    R x;
-    const float* rp = nullptr;
-    if (r >= 0 && r < src_rows)
-      rp = src + r * src_stride;
-    else
-      latch(st, DR_INVALID_ARGUMENT);
-    load_row<VEC, G, CPL>(x, rp, lg, dv);
-    if (mode == 0) {
-      acc_add(acc, x);
-    } else {
-      const int32_t cnt = (rp && bag_off) ? bag_off[r + 1] - bag_off[r] : 1;
-      if (cnt != 1) {
-        const float sc = mode == 2 ? (float)(1.0 / sqrt((double)cnt)) : (float)(1.0 / (double)cnt);
+  constexpr int NB = 4;  // rows in flight; summed strictly in ascending j
+  for (int32_t jb = j0; jb < j1; jb += NB) {
+    R x[NB];
+    int64_t rr[NB];
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) x.v[c] = vmul(x.v[c], sc);
+    for (int q = 0; q < NB; ++q) {
+      const float* rp = nullptr;
+      rr[q] = -1;
+      if (jb + q < j1) {
+        const int32_t p = perm[jb + q];
+        const int64_t r = seg_of_pos ? (int64_t)seg_of_pos[p] : (int64_t)p;
+        if (r >= 0 && r < src_rows) {
+          rp = src + r * src_stride;
+          rr[q] = r;
+        } else {
+          latch(st, DR_INVALID_ARGUMENT);
+        }
       }
-      if (first)
-        acc = x;
-      else
-        acc_add(acc, x);
+      load_row<VEC, G, CPL>(x[q], rp, lg, dv);
     }
-    first = false;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      if (jb + q >= j1) break;
+      if (mode == 0) {
+        acc_add(acc, x[q]);
+      } else {
+        const int32_t cnt = (rr[q] >= 0 && bag_off) ? bag_off[rr[q] + 1] - bag_off[rr[q]] : 1;
+        if (cnt != 1) {
+          const float sc = mode == 2 ? (float)(1.0 / sqrt((double)cnt)) : (float)(1.0 / (double)cnt);
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) x[q].v[c] = vmul(x[q].v[c], sc);
+        }
+        if (jb + q == j0)
+          acc = x[q];
+        else
+          acc_add(acc, x[q]);
+      }
+    }
   }
-  store_row<VEC, G, CPL>(acc, out + u * (int64_t)dim, lg, dv);
+  store_row_nt<VEC, G, CPL>(acc, out + u * (int64_t)dim, lg, dv);
 }
 
 template <int VEC, int G, int CPL>
@@ -1004,25 +1106,8 @@ int dr_gather(const float* table, int64_t rows, int64_t dim, const int64_t* ids,
   using namespace dr;
   DR_REQUIRE(n >= 0 && dim > 0 && dim <= 1024, DR_INVALID_ARGUMENT, "bad gather shape");
   if (n == 0) return DR_OK;
-  int* st = status_word();
-  hipStream_t s = S(stream);
-  const int d = (int)dim;
-  const bool al = ((uintptr_t)table & 15) == 0 && ((uintptr_t)out & 15) == 0;
-  if (d % 4 == 0 && al) {
-    const int d4 = d / 4;
-    if (d4 <= 4) return launch_gather<4, 4, 1>(table, rows, d, ids, n, out, s, st);
-    if (d4 <= 8) return launch_gather<4, 8, 1>(table, rows, d, ids, n, out, s, st);
-    if (d4 <= 16) return launch_gather<4, 16, 1>(table, rows, d, ids, n, out, s, st);
-    if (d4 <= 32) return launch_gather<4, 32, 1>(table, rows, d, ids, n, out, s, st);
-    if (d4 <= 64) return launch_gather<4, 64, 1>(table, rows, d, ids, n, out, s, st);
-    return launch_gather<4, 64, 4>(table, rows, d, ids, n, out, s, st);
-  }
-  if (d <= 8) return launch_gather<1, 8, 1>(table, rows, d, ids, n, out, s, st);
-  if (d <= 32) return launch_gather<1, 32, 1>(table, rows, d, ids, n, out, s, st);
-  if (d <= 64) return launch_gather<1, 64, 1>(table, rows, d, ids, n, out, s, st);
-  if (d <= 256) return launch_gather<1, 64, 4>(table, rows, d, ids, n, out, s, st);
-  set_error("dim %d unsupported", d);
-  return DR_INVALID_ARGUMENT;
+  return gather_dispatch<false>(table, rows, (int)dim, ids, n, out, S(stream), status_word(),
+                                nullptr, nullptr);
 }
 
 size_t dr_segment_workspace_size(int64_t num_segments) {

@@ -225,9 +225,9 @@ def test_sort_pairs_stable(ops):
     np.testing.assert_array_equal(H(vo), vals[order])
 
 
-def test_unsorted_segment_sum_bitexact(ops, orc):
+@pytest.mark.parametrize("n,D,S", [(20000, 24, 700), (5000, 128, 40), (3000, 3, 2500)])
+def test_unsorted_segment_sum_bitexact(ops, orc, n, D, S):
     rng = np.random.default_rng(11)
-    n, D, S = 20000, 24, 700
     data = (rng.standard_normal((n, D)) * 100).astype(np.float32)
     seg = rng.integers(-3, S, n).astype(np.int32)
     out = H(ops.unsorted_segment_sum(T(data), T(seg), S))
@@ -317,6 +317,26 @@ def test_ev_gather_matches_oracle(dr, orc):
     k2, v2, _, _ = oev.export()
     np.testing.assert_array_equal(H(k1), k2)
     np.testing.assert_array_equal(H(v1), v2)
+
+
+@pytest.mark.parametrize("D", [3, 128])
+def test_ev_gather_wide_and_odd_dims(dr, orc, D):
+    # dwordx4 copy-out (D % 4 == 0) and the scalar one; EV default row and
+    # per-key defaults
+    rng = np.random.default_rng(19)
+    ev = dr.EmbeddingVariable("gw%d" % D, D, 0.25, capacity=256)
+    oev = orc.EV(D, 0.25)
+    for step in range(3):
+        keys = np.unique(rng.integers(0, 3000, 700)).astype(np.int64)
+        rng.shuffle(keys)
+        if step == 1:
+            dflt = rng.standard_normal((keys.shape[0], D)).astype(np.float32)
+            out = H(ev.sparse_read(T(keys), ev_init_value=T(dflt)))
+            ref = oev.gather(keys, dflt)
+        else:
+            out = H(ev.sparse_read(T(keys)))
+            ref = oev.gather(keys, np.full((keys.shape[0], D), 0.25, np.float32))
+        np.testing.assert_array_equal(out, ref)
 
 
 def test_ev_insert_import_semantics(dr, orc):
@@ -689,12 +709,27 @@ def test_fm2(ops, orc):
     assert (np.abs(out - ref) <= 1e-5 * scale + 1e-6).all()
 
 
-def test_dot_interaction(ops, orc):
+@pytest.mark.parametrize("F,D", [(5, 64), (26, 64), (40, 8), (3, 6)])
+def test_fm2_grad(ops, orc, F, D):
+    # register-resident kernel (F <= 8 / 32) and the scalar fallback (F > 32, D % 4)
+    rng = np.random.default_rng(33)
+    e = rng.standard_normal((97, F, D)).astype(np.float32)
+    g = rng.standard_normal((97, D)).astype(np.float32)
+    out = H(ops.fm_second_order_grad(T(e), T(g)))
+    ref = (e.astype(np.float64).sum(1, keepdims=True) - e) * g[:, None, :]
+    scale = np.abs(e).sum(1, keepdims=True) * np.abs(g)[:, None, :]
+    assert (np.abs(out - ref) <= 1e-5 * scale + 1e-6).all()
+
+
+@pytest.mark.parametrize("B,F,D", [(50, 27, 128), (9, 5, 16), (7, 2, 8), (5, 30, 64),
+                                   (6, 27, 12)])
+def test_dot_interaction(ops, orc, B, F, D):
+    # tiled kernel: nb(nb+1)/2 <= 32 tiles, D % 8 == 0; others: per-pair kernel
     rng = np.random.default_rng(37)
-    x = rng.standard_normal((50, 27, 128)).astype(np.float32)
+    x = rng.standard_normal((B, F, D)).astype(np.float32)
     out = H(ops.dot_interaction(T(x)))
     ref = orc.dot_interaction(x)
-    scale = np.abs(x).sum(2).max() ** 2 / 27
+    scale = np.abs(x).sum(2).max() ** 2 / F
     np.testing.assert_allclose(out, ref, rtol=1e-4, atol=1e-5 * scale)
 
 
