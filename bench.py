@@ -209,55 +209,58 @@ def main():
     seg = torch.arange(B, dtype=torch.int32, device=dev)
     ind = torch.stack([torch.arange(B, device=dev), torch.zeros(B, dtype=torch.int64, device=dev)], 1)
     static_ids = torch.empty((T, B), dtype=torch.int64, device=dev)
-    sps = [SparseTensor(ind, static_ids[t], (B, 1)) for t in range(T)]
+    # the id batches are resident in HBM (value counts no host->device input
+    # traffic); step k reads batch k % 4 in place
+    batch_sps = [[SparseTensor(ind, ids[t], (B, 1)) for t in range(T)] for ids in batches]
 
-    def step():
+    def step(k):
         if engine is not None:
-            return engine.forward(static_ids)
-        return dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum")
+            return engine.forward(batches[k])
+        return dr.embedding_lookup_sparse_multi(evs, batch_sps[k], combiner="sum")
 
+    NBATCH = len(batches)
     torch.cuda.synchronize()
     with torch.no_grad():
         for w in range(max(args.warmup, 2)):
-            static_ids.copy_(batches[w % len(batches)])
-            out = step()
+            out = step(w % NBATCH)
             torch.cuda.synchronize()
             log("eager warmup step %d ok" % w)
         dr.status_check(dev)
-        graph = None
+        graph_all = None
         if not args.no_graph and engine is None:
-            graph = torch.cuda.CUDAGraph()
-            static_ids.copy_(batches[0])
-            with torch.cuda.graph(graph):
-                out = step()
-            log("graph captured")
-            graph.replay()
+            # one graph of the NBATCH steps in a row (a graph launch costs
+            # ~10 us between replays; hipGraph-captured inner loop with every
+            # step's full work inside); leftover steps run eagerly
+            graph_all = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph_all):
+                for k in range(NBATCH):
+                    out = step(k)
+            log("graphs captured")
+            graph_all.replay()
             torch.cuda.synchronize()
             log("graph replay ok")
 
         debug = os.environ.get("DR_BENCH_DEBUG") == "1"
 
-        def run_step(i):
-            static_ids.copy_(batches[i % len(batches)])
-            if debug:
-                torch.cuda.synchronize()
-                log("step %d: input copied" % i)
-            if graph is not None:
-                graph.replay()
-            else:
-                step()
-            if debug:
-                torch.cuda.synchronize()
-                log("step %d: done" % i)
+        def run_steps(i0, n):
+            i = i0
+            while i < i0 + n:
+                if graph_all is not None and i % NBATCH == 0 and i + NBATCH <= i0 + n:
+                    graph_all.replay()
+                    i += NBATCH
+                    continue
+                step(i % NBATCH)
+                if debug:
+                    torch.cuda.synchronize()
+                    log("step %d: done" % i)
+                i += 1
 
-        for w in range(args.warmup):
-            run_step(w)
+        run_steps(0, args.warmup)
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for i in range(args.steps):
-            run_step(i)
+        run_steps(0, args.steps)
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
@@ -272,35 +275,53 @@ def main():
     ms = el / args.steps * 1e3
     dr.status_check(dev)
 
-    # ---- dominant kernel: the grouped gather+pool launch, timed alone -----
-    from deeprec_amd.embedding_ops import _Feature, _prepare_group, _pool_all
-    # keys this rank owns (all keys at N=1): the local gather+pool kernel
+    # ---- dominant kernel: the fused one-hot EV lookup, timed alone --------
+    # dr_ev_lookup_onehot on keys this rank owns (all keys at N=1): the
+    # probe + row-copy kernel and its three miss-list kernels (empty here: all
+    # keys exist), timed with HIP events on the stream they run on.
+    from deeprec_amd.embedding_ops import _Feature, _fused_onehot
     static_ids.copy_((batches[0] % R) * world + rank)
     with torch.no_grad():
         feats = [_Feature(evs[t], static_ids[t], seg, B, None, "sum", None, onehot=True)
                  for t in range(T)]
-        _prepare_group(feats, need_grad=False)
-        _pool_all(feats, _lib.ORDER_ALI)
+        assert _fused_onehot(feats, _lib.ORDER_ALI) is not None
         torch.cuda.synchronize()
+        kg = None
+        if not args.no_graph:
+            # replayed graph of one call: no Python overhead between launches
+            kg = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(kg):
+                _fused_onehot(feats, _lib.ORDER_ALI)
+            kg.replay()
+            torch.cuda.synchronize()
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(args.kernel_iters):
-            _pool_all(feats, _lib.ORDER_ALI)
+        if kg is not None:
+            for _ in range(args.kernel_iters):
+                kg.replay()
+        else:
+            for _ in range(args.kernel_iters):
+                _fused_onehot(feats, _lib.ORDER_ALI)
         e1.record()
         torch.cuda.synchronize()
     k_ms = e0.elapsed_time(e1) / args.kernel_iters
-    per_lookup = 8 + 4 + D * 4 + D * 4      # nnz(8+4+Ds) + B*Ds, h = 1
+    # SURVEY 8(d) EV hashed gather (+ the pooled write): key 8 + slot 16 +
+    # row D*4 read + D*4 output write per lookup (h = 1)
+    per_lookup = 8 + 16 + D * 4 + D * 4
     bytes_launch = T * B * per_lookup
     achieved = bytes_launch / (k_ms * 1e-3) / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
-            "kernel": "dr::pool_onehot_kernel<4,32,1,ALI,4>", "kernel_ms": round(k_ms, 4),
+            "kernel": "dr::ev_lookup_onehot_kernel<4,32,1,ALI,4> (+ 3 miss-list kernels, empty)",
+            "kernel_ms": round(k_ms, 4),
             "bytes_per_launch": bytes_launch, "bytes_per_lookup": per_lookup}
     pmc = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
     if os.path.exists(pmc):
         try:
-            roof["traffic"] = json.load(open(pmc)).get("pool_bytes_per_launch")
+            j = json.load(open(pmc))
+            if j.get("kernel") == "ev_lookup_onehot_kernel":  # PMC of this same kernel only
+                roof["traffic"] = j.get("bytes_per_launch")
         except Exception:
             pass
 

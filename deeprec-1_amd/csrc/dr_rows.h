@@ -1,0 +1,98 @@
+// dr_rows.h -- one embedding row held by a group of G lanes (VEC floats per
+// lane per column chunk, CPL chunks): loads / stores (default or
+// nontemporal policy) and elementwise helpers shared by the pooling, gather
+// and EV kernels.
+#pragma once
+#include "dr_common.h"
+
+namespace dr {
+
+template <int VEC>
+struct VecT;
+template <>
+struct VecT<4> {
+  using T = float4;
+};
+template <>
+struct VecT<1> {
+  using T = float;
+};
+
+__device__ __forceinline__ float4 vadd(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float vadd(float a, float b) { return a + b; }
+__device__ __forceinline__ float4 vdiv(float4 a, float q) {
+  return make_float4(a.x / q, a.y / q, a.z / q, a.w / q);
+}
+__device__ __forceinline__ float vdiv(float a, float q) { return a / q; }
+__device__ __forceinline__ float4 vmul(float4 a, float q) {
+  return make_float4(a.x * q, a.y * q, a.z * q, a.w * q);
+}
+__device__ __forceinline__ float vmul(float a, float q) { return a * q; }
+__device__ __forceinline__ float vdot(float4 a) { return a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w; }
+__device__ __forceinline__ float vdot(float a) { return a * a; }
+template <class V>
+__device__ __forceinline__ V vzero();
+template <>
+__device__ __forceinline__ float4 vzero<float4>() {
+  return make_float4(0.f, 0.f, 0.f, 0.f);
+}
+template <>
+__device__ __forceinline__ float vzero<float>() {
+  return 0.f;
+}
+
+template <int VEC, int G, int CPL>
+struct Row {
+  typename VecT<VEC>::T v[CPL];
+};
+
+template <int VEC, int G, int CPL>
+__device__ __forceinline__ void load_row(Row<VEC, G, CPL>& x, const float* p, int lg, int dv) {
+  using V = typename VecT<VEC>::T;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = lg + c * G;
+    x.v[c] = (p && col < dv) ? reinterpret_cast<const V*>(p)[col] : vzero<V>();
+  }
+}
+
+// Rows read exactly once per launch: nontemporal hint (no L2 retention).
+template <int VEC, int G, int CPL>
+__device__ __forceinline__ void load_row_nt(Row<VEC, G, CPL>& x, const float* p, int lg, int dv) {
+  using V = typename VecT<VEC>::T;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = lg + c * G;
+    x.v[c] = (p && col < dv) ? nt_load(reinterpret_cast<const V*>(p) + col) : vzero<V>();
+  }
+}
+
+template <int VEC, int G, int CPL>
+__device__ __forceinline__ void store_row_nt(const Row<VEC, G, CPL>& x, float* p, int lg, int dv) {
+  using V = typename VecT<VEC>::T;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = lg + c * G;
+    if (col < dv) nt_store(x.v[c], reinterpret_cast<V*>(p) + col);
+  }
+}
+
+template <int VEC, int G, int CPL>
+__device__ __forceinline__ void store_row(const Row<VEC, G, CPL>& x, float* p, int lg, int dv) {
+  using V = typename VecT<VEC>::T;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = lg + c * G;
+    if (col < dv) reinterpret_cast<V*>(p)[col] = x.v[c];
+  }
+}
+
+template <int VEC, int G, int CPL>
+__device__ __forceinline__ void acc_add(Row<VEC, G, CPL>& a, const Row<VEC, G, CPL>& b) {
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) a.v[c] = vadd(a.v[c], b.v[c]);
+}
+
+}  // namespace dr

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "dr_common.h"
+#include "dr_rows.h"
 
 namespace dr {
 
@@ -1103,6 +1104,379 @@ static int apply_common(int opt, dr_ev* var, dr_ev* s1, dr_ev* s2, OptScalars sc
   return apply_grouped(opt, v, a, b, 1, sc, g, k, nh, nd, gs, st);
 }
 
+
+// ---------------------------------------------------------------------------
+// Fused one-hot forward lookup (dr_ev_lookup_onehot): filter-free EVs, bag b
+// of table t = id t*B + b, output [B, T*D] concat.  One kernel probes the key
+// table and copies the row straight into the output, in output-slot order
+// (slot j = b*T + t, the pool_onehot_kernel layout); the resolve pass and
+// its row-index array disappear from the step.  The probe is read-only: a
+// key that is absent, still being created, or whose column has not been
+// initialised is appended to a miss list, and one small kernel finishes
+// those slots exactly as resolve -> init -> copy would (insert-on-miss with
+// the creator-first protocol of ev_find, first-touch default row, copy).
+// In steady state the list is empty and it exits at once.
+// ---------------------------------------------------------------------------
+struct LkDesc {
+  const Slot* slots;
+  int64_t cap;
+  const float* pool;
+  uint64_t colbit;
+};
+
+struct LookupArgs {
+  LkDesc d[DR_MAX_GROUP];
+  const int64_t* keys;  // [T, B]
+  float* out;
+  int64_t out_stride;
+};
+
+// Row of `key` when present with this column initialised, else -1.
+__device__ __forceinline__ int64_t ev_probe_row(const LkDesc& e, uint64_t key) {
+  uint64_t rc;
+  typedef unsigned long long slot_v __attribute__((ext_vector_type(2)));
+  if (key == kEmptyKey) {
+    const slot_v sv = *reinterpret_cast<const slot_v*>(e.slots + e.cap);
+    if (sv.x != 0ull) return -1;
+    rc = sv.y;
+  } else {
+    const uint64_t mask = (uint64_t)e.cap - 1;
+    uint64_t h = mix64(key) & mask;
+    for (int64_t probes = 0;; ++probes) {
+      if (probes > e.cap) return -1;
+      const slot_v sv = *reinterpret_cast<const slot_v*>(e.slots + h);
+      if (sv.x == key) {
+        rc = sv.y;
+        break;
+      }
+      if (sv.x == kEmptyKey) return -1;  // (a stale empty only sends it to the miss path)
+      h = (h + 1) & mask;
+    }
+  }
+  if (rc == kUnset || !(rc & e.colbit)) return -1;
+  const int64_t row = (int64_t)(rc & kRowMask);
+  return row == (int64_t)kRowDead ? -1 : row;
+}
+
+template <int VEC, int G, int CPL, int ORDER, int NB>
+__global__ __launch_bounds__(256) void ev_lookup_onehot_kernel(LookupArgs a, int T, int64_t B,
+                                                               int dim, int32_t* __restrict__ mlist,
+                                                               unsigned long long* __restrict__ mcnt) {
+  __shared__ LkDesc sd[DR_MAX_GROUP];  // per-lane table index: stage in LDS
+  if (threadIdx.x < T) sd[threadIdx.x] = a.d[threadIdx.x];
+  __syncthreads();
+  constexpr int GPB = 256 / G;
+  const int64_t slots = (int64_t)T * B;
+  const int64_t s0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * NB;
+  if (s0 >= slots) return;
+  const int lg = threadIdx.x % G;
+  const int dv = dim / VEC;
+  const int base = (int)(threadIdx.x % 64) - lg;
+  // lanes 0..NB-1 of the group probe one slot each
+  const float* mine = nullptr;
+  bool missed = false;
+  if (lg < NB && s0 + lg < slots) {
+    const int64_t s = s0 + lg;
+    const int64_t b = (int64_t)((uint32_t)s / (uint32_t)T);  // slots < 2^31 (host check)
+    const int t = (int)(s - b * T);
+    const LkDesc& e = sd[t];
+    const int64_t row = ev_probe_row(e, (uint64_t)a.keys[(int64_t)t * B + b]);
+    if (row >= 0)
+      mine = e.pool + row * (int64_t)dim;
+    else
+      missed = true;
+  }
+  // wave-aggregated append of the misses
+  const uint64_t mm = __ballot(missed);
+  if (mm) {
+    const int lane = (int)(threadIdx.x % 64);
+    const int leader = __ffsll((unsigned long long)mm) - 1;
+    unsigned long long at = 0;
+    if (lane == leader) at = atomicAdd(mcnt, (unsigned long long)__popcll(mm));
+    at = __shfl(at, leader, 64);
+    if (missed) mlist[at + __popcll(mm & lanemask_lt())] = (int32_t)(s0 + lg);
+  }
+  Row<VEC, G, CPL> x[NB];
+  float* o[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    const uint64_t u = (uint64_t)(uintptr_t)mine;
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)u, base + q, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(u >> 32), base + q, 64);
+    const float* p = reinterpret_cast<const float*>((uintptr_t)(((uint64_t)hi << 32) | lo));
+    const int64_t s = s0 + q;
+    o[q] = nullptr;
+    if (p && s < slots) {
+      const int64_t b = (int64_t)((uint32_t)s / (uint32_t)T);
+      o[q] = a.out + b * a.out_stride + (s - b * T) * (int64_t)dim;
+    }
+    load_row_nt<VEC, G, CPL>(x[q], p, lg, dv);
+  }
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    if (ORDER == DR_ORDER_SEQ) {  // fused op: out = 0 + e (-0.0 -> +0.0)
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) x[q].v[c] = vadd(vzero<typename VecT<VEC>::T>(), x[q].v[c]);
+    }
+    if (o[q]) store_row_nt<VEC, G, CPL>(x[q], o[q], lg, dv);
+  }
+}
+
+struct MissArgs {
+  EvDesc e[DR_MAX_GROUP];
+  float* pool[DR_MAX_GROUP];
+  const float* dflt[DR_MAX_GROUP];
+  int64_t* mtop[DR_MAX_GROUP];  // row counters to mirror (nullptr: none)
+  int64_t* mdst[DR_MAX_GROUP];
+  const int64_t* keys;
+  float* out;
+  int64_t out_stride;
+};
+
+// Grid-wide barrier of the miss kernel.  The grid is small enough to be
+// co-resident (kMissBlocks, ~2 blocks per CU), the spin is bounded (latches
+// INTERNAL instead of hanging), and the agent-scope fences write back /
+// invalidate the XCD-local L2s around it.
+__device__ __forceinline__ void miss_grid_sync(unsigned* bar, unsigned target, int* st) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    atomicAdd(bar, 1u);
+    for (unsigned spin = 0;
+         __hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
+      if (spin > (1u << 24)) {
+        latch(st, DR_INTERNAL);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+    }
+    __threadfence();
+  }
+  __syncthreads();
+}
+
+// The listed slots, in three grid-synchronised phases (what resolve -> init
+// -> copy do in three launches): (1) insert-on-miss resolve, creator-first
+// (ev_find), claiming each row's first touch of the column; (2) default rows
+// for the claims, one wave per row, and block 0 refreshes the capacity
+// mirrors (the counter is final); (3) copy each slot's row (or the default
+// when allocation failed) into the output.  Steady state: the list is empty
+// and every block returns after one load.
+template <int ORDER>
+__global__ __launch_bounds__(256) void ev_miss_kernel(MissArgs a, int T, int64_t B, int64_t dim,
+                                                      const int32_t* __restrict__ mlist,
+                                                      const unsigned long long* __restrict__ mcnt,
+                                                      unsigned* __restrict__ bar,
+                                                      int64_t* __restrict__ mrow,
+                                                      uint8_t* __restrict__ minit, int* st) {
+  const int64_t n = (int64_t)*mcnt;
+  if (n == 0) return;  // uniform over the grid
+  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nthreads) {
+    const int64_t s = mlist[i];
+    const int64_t b = s / T;
+    const int t = (int)(s - b * T);
+    const EvDesc& e = a.e[t];
+    bool created;
+    uint64_t rc;
+    Slot* sl = ev_find(e, (uint64_t)a.keys[(int64_t)t * B + b], true, &created, &rc, st);
+    uint8_t claim = 0;
+    int64_t row = -1;
+    if (sl && (rc & kRowMask) != kRowDead) {
+      row = (int64_t)(rc & kRowMask);
+      const uint64_t bit = 1ull << (48 + e.col);
+      if (!(rc & bit)) {
+        const uint64_t old = atomicOr((unsigned long long*)&sl->rc, (unsigned long long)bit);
+        if (!(old & bit)) claim = 1;
+      }
+    }
+    mrow[i] = row;
+    minit[i] = claim;
+  }
+  miss_grid_sync(bar, gridDim.x, st);
+  if (blockIdx.x == 0 && threadIdx.x < T && a.mdst[threadIdx.x]) {
+    const int64_t top = __hip_atomic_load(a.mtop[threadIdx.x], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.mdst[threadIdx.x], top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / 64);
+  const int64_t w0 = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  for (int64_t i = w0; i < n; i += waves) {
+    if (!minit[i]) continue;
+    const int t = (int)(mlist[i] % T);
+    float* dst = a.pool[t] + mrow[i] * dim;
+    for (int64_t c = lane; c < dim; c += 64) dst[c] = a.dflt[t][c];
+  }
+  miss_grid_sync(bar, 2 * gridDim.x, st);
+  for (int64_t i = w0; i < n; i += waves) {
+    const int64_t s = mlist[i];
+    const int64_t b = s / T;
+    const int t = (int)(s - b * T);
+    const float* src = mrow[i] >= 0 ? a.pool[t] + mrow[i] * dim : a.dflt[t];
+    float* dst = a.out + b * a.out_stride + (int64_t)t * dim;
+    for (int64_t c = lane; c < dim; c += 64) dst[c] = ORDER == DR_ORDER_SEQ ? 0.f + src[c] : src[c];
+  }
+}
+
+// 2 blocks per CU of the current device: co-resident by construction
+static unsigned miss_blocks() {
+  static std::atomic<int> cached[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 64;
+  int cus = cached[dev].load(std::memory_order_relaxed);
+  if (cus <= 0) {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 32;
+    cached[dev].store(cus, std::memory_order_relaxed);
+  }
+  return (unsigned)(2 * cus);
+}
+
+struct LookupWs {
+  int32_t* mlist;
+  unsigned long long* mcnt;  // [2]: miss count, grid-barrier counter
+  int64_t* mrow;
+  uint8_t* minit;
+};
+static LookupWs carve_lookup(void* ws, int64_t n, size_t* used) {
+  Carver c(ws);
+  LookupWs w;
+  const int64_t nn = n > 0 ? n : 1;
+  w.mlist = c.take<int32_t>(nn);
+  w.mcnt = c.take<unsigned long long>(2);
+  w.mrow = c.take<int64_t>(nn);
+  w.minit = c.take<uint8_t>(nn);
+  if (used) *used = c.used + 256;
+  return w;
+}
+
+template <int VEC, int G, int CPL, int ORDER, int NB>
+static void launch_lookup_nb(const LookupArgs& a, int T, int64_t B, int dim, const LookupWs& w,
+                             hipStream_t st) {
+  const int64_t items = ceil_div((int64_t)T * B, NB);
+  hipLaunchKernelGGL((ev_lookup_onehot_kernel<VEC, G, CPL, ORDER, NB>),
+                     dim3((unsigned)ceil_div(items, 256 / G)), dim3(256), 0, st, a, T, B, dim,
+                     w.mlist, w.mcnt);
+}
+
+template <int VEC, int G, int CPL, int ORDER>
+static void launch_lookup_onehot(const LookupArgs& a, int T, int64_t B, int dim, const LookupWs& w,
+                                 hipStream_t st) {
+  static const int nb = getenv("DR_LOOKUP_NB") ? atoi(getenv("DR_LOOKUP_NB")) : 4;
+  if (nb == 8 && G >= 8)
+    launch_lookup_nb<VEC, G, CPL, ORDER, 8>(a, T, B, dim, w, st);
+  else if (nb == 2)
+    launch_lookup_nb<VEC, G, CPL, ORDER, 2>(a, T, B, dim, w, st);
+  else
+    launch_lookup_nb<VEC, G, CPL, ORDER, 4>(a, T, B, dim, w, st);
+}
+
+static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t B, float* out,
+                         int64_t out_stride, int order, void* ws, size_t ws_bytes, hipStream_t st) {
+  DR_REQUIRE(evs && T >= 1 && T <= DR_MAX_GROUP && B >= 0 && out_stride >= 0, DR_INVALID_ARGUMENT,
+             "bad argument");
+  DR_REQUIRE(order == DR_ORDER_ALI || order == DR_ORDER_SEQ, DR_INVALID_ARGUMENT, "bad order");
+  const int64_t n = (int64_t)T * B;
+  DR_REQUIRE(n < (1ll << 31), DR_INVALID_ARGUMENT, "T*B must be < 2^31");
+  size_t need = 0;
+  carve_lookup(nullptr, n, &need);
+  DR_REQUIRE(ws_bytes >= need, DR_INVALID_ARGUMENT, "lookup workspace too small");
+  const int64_t dim = evs[0]->sh->dim;
+  DR_REQUIRE(dim % 4 == 0 && dim <= 256, DR_INVALID_ARGUMENT,
+             "fused one-hot lookup needs dim %% 4 == 0 and dim <= 256");
+  DR_REQUIRE(out_stride >= (int64_t)T * dim && (out_stride % 4) == 0 &&
+                 ((uintptr_t)out & 15) == 0,
+             DR_INVALID_ARGUMENT, "out must be 16-B aligned with stride >= T*dim (multiple of 4)");
+  if (n == 0) return DR_OK;
+  int* stw = status_word();
+  DR_REQUIRE(stw, DR_INTERNAL, "status word unavailable");
+  for (int t = 0; t < T; ++t) {
+    const EvShared* s = evs[t]->sh;
+    DR_REQUIRE(s->dim == dim, DR_INVALID_ARGUMENT, "tables must share dim");
+    DR_REQUIRE(s->filter_freq == 0 && s->k_hash == 0, DR_INVALID_ARGUMENT,
+               "table %d: the fused lookup is for filter-free EVs", t);
+    DR_REQUIRE(((uintptr_t)s->pools[evs[t]->col] & 15) == 0, DR_INVALID_ARGUMENT,
+               "pool alignment");
+  }
+  // capacity before any pointer is read (a reserve may grow the tables)
+  for (int t = 0; t < T; ++t) {
+    int rc = reserve(evs[t]->sh, B, st);
+    if (rc) return rc;
+  }
+  LookupWs w = carve_lookup(ws, n, nullptr);
+  int rc = fill_bytes(w.mcnt, 0, 2 * sizeof(unsigned long long), st);
+  if (rc) return rc;
+  LookupArgs la;
+  memset(&la, 0, sizeof(la));
+  MissArgs ma;
+  memset(&ma, 0, sizeof(ma));
+  for (int t = 0; t < T; ++t) {
+    const EvShared* s = evs[t]->sh;
+    la.d[t].slots = s->slots;
+    la.d[t].cap = s->cap;
+    la.d[t].pool = s->pools[evs[t]->col];
+    la.d[t].colbit = 1ull << (48 + evs[t]->col);
+    ma.e[t] = make_desc(evs[t]);
+    ma.pool[t] = s->pools[evs[t]->col];
+    ma.dflt[t] = s->defaults[evs[t]->col];
+  }
+  la.keys = ma.keys = keys;
+  la.out = ma.out = out;
+  la.out_stride = ma.out_stride = out_stride;
+  const int d4 = (int)(dim / 4);
+#define DR_LK(G, C)                                                             \
+  do {                                                                          \
+    if (order == DR_ORDER_ALI)                                                  \
+      launch_lookup_onehot<4, G, C, DR_ORDER_ALI>(la, T, B, (int)dim, w, st);   \
+    else                                                                        \
+      launch_lookup_onehot<4, G, C, DR_ORDER_SEQ>(la, T, B, (int)dim, w, st);   \
+  } while (0)
+  if (d4 <= 4) DR_LK(4, 1);
+  else if (d4 <= 8) DR_LK(8, 1);
+  else if (d4 <= 16) DR_LK(16, 1);
+  else if (d4 <= 32) DR_LK(32, 1);
+  else DR_LK(64, 1);
+#undef DR_LK
+  // capacity mirrors ride on the miss kernel (as on resolve_grouped's init)
+  EvShared* mir[DR_MAX_GROUP];
+  int nmir = 0;
+  for (int t = 0; t < T; ++t) {
+    EvShared* sh = evs[t]->sh;
+    bool seen = false;
+    for (int q = 0; q < nmir; ++q) seen = seen || mir[q] == sh;
+    if (seen) continue;
+    sh->mu.lock();
+    if (want_mirror(sh, st)) {
+      ma.mtop[t] = sh->top;
+      ma.mdst[t] = sh->pinned_top;
+      mir[nmir++] = sh;
+    } else {
+      sh->mu.unlock();
+    }
+  }
+  unsigned* bar = reinterpret_cast<unsigned*>(w.mcnt + 1);
+  const unsigned kMissBlocks = miss_blocks();
+  if (order == DR_ORDER_ALI)
+    hipLaunchKernelGGL(ev_miss_kernel<DR_ORDER_ALI>, dim3(kMissBlocks), dim3(256), 0, st, ma, T, B,
+                       dim, w.mlist, w.mcnt, bar, w.mrow, w.minit, stw);
+  else
+    hipLaunchKernelGGL(ev_miss_kernel<DR_ORDER_SEQ>, dim3(kMissBlocks), dim3(256), 0, st, ma, T, B,
+                       dim, w.mlist, w.mcnt, bar, w.mrow, w.minit, stw);
+  const hipError_t le = hipGetLastError();
+  for (int q = 0; q < nmir; ++q) {
+    if (le == hipSuccess) mirrored(mir[q], st);
+    mir[q]->mu.unlock();
+  }
+  if (le != hipSuccess) {
+    set_error("kernel launch failed: %s", hipGetErrorString(le));
+    return DR_INTERNAL;
+  }
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
 }  // namespace dr
 
 // ===========================================================================
@@ -1258,6 +1632,20 @@ int dr_ev_resolve_grouped(dr_ev* const* evs, int num_tables, const int64_t* keys
                           void* stream) {
   return dr::resolve_grouped(evs, num_tables, keys, koff_host, n_dev_per_table, nullptr, counts,
                              rows_out, ws, ws_bytes, dr::S(stream));
+}
+
+// Fused one-hot forward lookup over T filter-free EVs (see lookup_onehot).
+size_t dr_ev_lookup_onehot_workspace_size(int num_tables, int64_t batch) {
+  size_t used = 0;
+  dr::carve_lookup(nullptr, (int64_t)num_tables * batch, &used);
+  return used;
+}
+
+int dr_ev_lookup_onehot(dr_ev* const* evs, int num_tables, const int64_t* keys, int64_t batch,
+                        float* out, int64_t out_stride, int order, void* ws, size_t ws_bytes,
+                        void* stream) {
+  return dr::lookup_onehot(evs, num_tables, keys, batch, out, out_stride, order, ws, ws_bytes,
+                           dr::S(stream));
 }
 
 // Tagged resolve: keys of all T tables in one array, table of key i =

@@ -4,6 +4,8 @@
 //   DCN-v2 CrossNet   (absent from the reference)        (bf16 MFMA GEMM)
 #include "dr_common.h"
 
+#include <algorithm>
+
 namespace dr {
 
 // out[b, d] = 0.5 * ((sum_f e)^2 - sum_f e^2); thread per (b, 4 columns).
@@ -114,37 +116,29 @@ __global__ void dot_kernel(const float* __restrict__ x, int F, int D, float* __r
 static constexpr int DOT_WAVES = 4;
 static constexpr int DOT_MAXE = 16;  // float4 per lane when staging: F_pad * D / 4 <= 1024
 
+__device__ __forceinline__ void dot_load(float4 (&v)[DOT_MAXE], const float* x, int64_t b,
+                                         int64_t B, int nv, int FD, int lane) {
+  const float4* src = reinterpret_cast<const float4*>(x + b * (int64_t)FD);
+#pragma unroll
+  for (int q = 0; q < DOT_MAXE; ++q) {
+    const int e = lane + q * 64;
+    v[q] = (b < B && e < nv) ? nt_load(src + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// Persistent: block i handles samples (i + it*grid)*DOT_WAVES + wave, and
+// the loads of a wave's next sample are issued before it computes the
+// current one (their registers are free once the sample sits in LDS), so
+// HBM latency hides behind the LDS/FMA work at 2 blocks per CU.
 __global__ __launch_bounds__(256) void dot_tile_kernel(const float* __restrict__ x, int64_t B,
                                                        int F, int D, float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) float xs_all[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * DOT_WAVES + wave;
   const int Fp = (F + 3) & ~3;
   const int ld = D + 4;
+  const int D4 = D / 4;
+  const int n4 = Fp * D4, nv = F * D4;
   float* xs = xs_all + (size_t)wave * Fp * ld;
-  if (b < B) {
-    // all of the lane's loads first (a load -> LDS store loop would wait out
-    // one HBM latency per iteration)
-    const float4* src = reinterpret_cast<const float4*>(x + b * (int64_t)F * D);
-    const int D4 = D / 4;
-    const int n4 = Fp * D4, nv = F * D4;
-    float4 v[DOT_MAXE];
-#pragma unroll
-    for (int q = 0; q < DOT_MAXE; ++q) {
-      const int e = lane + q * 64;
-      v[q] = e < nv ? nt_load(src + e) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int q = 0; q < DOT_MAXE; ++q) {
-      const int e = lane + q * 64;
-      if (e < n4) {
-        const int r = e / D4, c = e - r * D4;
-        *reinterpret_cast<float4*>(xs + r * ld + c * 4) = v[q];
-      }
-    }
-  }
-  __syncthreads();
-  if (b >= B) return;
   const int nb = Fp / 4;
   const int tiles = nb * (nb + 1) / 2;
   const int tile = lane >> 1, kh = lane & 1;
@@ -154,46 +148,66 @@ __global__ __launch_bounds__(256) void dot_tile_kernel(const float* __restrict__
     while ((bi + 1) * (bi + 2) / 2 <= tile) ++bi;
     bj = tile - bi * (bi + 1) / 2;
   }
-  float acc[4][4];
+  const int64_t P = (int64_t)F * (F - 1) / 2;
+  const int64_t step = (int64_t)gridDim.x * DOT_WAVES;
+  int64_t b = (int64_t)blockIdx.x * DOT_WAVES + wave;
+  const int64_t b_first_of_block = (int64_t)blockIdx.x * DOT_WAVES;
+  float4 v[DOT_MAXE];
+  dot_load(v, x, b, B, nv, F * D, lane);
+  for (int64_t bb = b_first_of_block; bb < B; bb += step, b += step) {
+    // (the trip count is uniform over the block: bb is the block's first sample)
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int q = 0; q < DOT_MAXE; ++q) {
+      const int e = lane + q * 64;
+      if (e < n4) {
+        const int r = e / D4, c = e - r * D4;
+        *reinterpret_cast<float4*>(xs + r * ld + c * 4) = v[q];
+      }
+    }
+    __syncthreads();
+    dot_load(v, x, b + step, B, nv, F * D, lane);  // next sample, in flight during compute
+    float acc[4][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
-  if (tile < tiles) {
-    const float* A = xs + (bi * 4) * ld;
-    const float* Bm = xs + (bj * 4) * ld;
-    // lanes 2t, 2t+1 take alternate 4-float slices of K (adjacent banks)
-    for (int k = kh * 4; k < D; k += 8) {
-      float4 a[4], c[4];
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const float4*>(A + i * ld + k);
+      for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+    if (tile < tiles) {
+      const float* A = xs + (bi * 4) * ld;
+      const float* Bm = xs + (bj * 4) * ld;
+      // lanes 2t, 2t+1 take alternate 4-float slices of K (adjacent banks)
+      for (int k = kh * 4; k < D; k += 8) {
+        float4 a4[4], c4[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) c[j] = *reinterpret_cast<const float4*>(Bm + j * ld + k);
+        for (int i = 0; i < 4; ++i) a4[i] = *reinterpret_cast<const float4*>(A + i * ld + k);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c4[j] = *reinterpret_cast<const float4*>(Bm + j * ld + k);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[i][j] = fmaf(a4[i].x, c4[j].x, acc[i][j]);
+            acc[i][j] = fmaf(a4[i].y, c4[j].y, acc[i][j]);
+            acc[i][j] = fmaf(a4[i].z, c4[j].z, acc[i][j]);
+            acc[i][j] = fmaf(a4[i].w, c4[j].w, acc[i][j]);
+          }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] += __shfl_xor(acc[i][j], 1, 64);
+    if (b < B && tile < tiles && !kh) {
+      float* o = out + b * P;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          acc[i][j] = fmaf(a[i].x, c[j].x, acc[i][j]);
-          acc[i][j] = fmaf(a[i].y, c[j].y, acc[i][j]);
-          acc[i][j] = fmaf(a[i].z, c[j].z, acc[i][j]);
-          acc[i][j] = fmaf(a[i].w, c[j].w, acc[i][j]);
+          const int gi = bi * 4 + i, gj = bj * 4 + j;
+          if (gi < F && gj < gi) o[gi * (gi - 1) / 2 + gj] = acc[i][j];
         }
     }
+    __syncthreads();  // LDS is rewritten next iteration
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] += __shfl_xor(acc[i][j], 1, 64);
-  if (tile >= tiles || kh) return;
-  const int64_t P = (int64_t)F * (F - 1) / 2;
-  float* o = out + b * P;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int gi = bi * 4 + i, gj = bj * 4 + j;
-      if (gi < F && gj < gi) o[gi * (gi - 1) / 2 + gj] = acc[i][j];
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -338,8 +352,11 @@ int dr_dot_interaction(const float* x, int64_t batch, int fields, int dim, float
   const size_t tlds = (size_t)DOT_WAVES * nb * 4 * (dim + 4) * sizeof(float);
   if (nb * (nb + 1) / 2 <= 32 && dim % 8 == 0 && ((uintptr_t)x & 15) == 0 && tlds <= 64 * 1024 &&
       nb * 4 * (dim / 4) <= DOT_MAXE * 64) {
-    hipLaunchKernelGGL(dot_tile_kernel, dim3((unsigned)ceil_div(batch, DOT_WAVES)), dim3(256), tlds,
-                       S(stream), x, batch, fields, dim, out);
+    // grid: what fits at once (LDS-limited blocks per CU x 256 CUs)
+    const int per_cu = std::max<int>(1, (int)((160 * 1024) / tlds));
+    const int64_t grid = std::min<int64_t>(ceil_div(batch, DOT_WAVES), (int64_t)per_cu * 256);
+    hipLaunchKernelGGL(dot_tile_kernel, dim3((unsigned)grid), dim3(256), tlds, S(stream), x, batch,
+                       fields, dim, out);
     DR_LAUNCH_CHECK();
     return DR_OK;
   }

@@ -16,48 +16,13 @@
 //             (core/kernels/fused_embedding/fused_embedding_local_ops_gpu.cu.cc:41-84)
 // fp32 adds are separate roundings (built with -ffp-contract=off).
 #include "dr_common.h"
+#include "dr_rows.h"
 
 namespace dr {
 
 struct PoolArgs {
   dr_pool_desc d[DR_MAX_GROUP];
 };
-
-template <int VEC>
-struct VecT;
-template <>
-struct VecT<4> {
-  using T = float4;
-};
-template <>
-struct VecT<1> {
-  using T = float;
-};
-
-__device__ __forceinline__ float4 vadd(float4 a, float4 b) {
-  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
-}
-__device__ __forceinline__ float vadd(float a, float b) { return a + b; }
-__device__ __forceinline__ float4 vdiv(float4 a, float q) {
-  return make_float4(a.x / q, a.y / q, a.z / q, a.w / q);
-}
-__device__ __forceinline__ float vdiv(float a, float q) { return a / q; }
-__device__ __forceinline__ float4 vmul(float4 a, float q) {
-  return make_float4(a.x * q, a.y * q, a.z * q, a.w * q);
-}
-__device__ __forceinline__ float vmul(float a, float q) { return a * q; }
-__device__ __forceinline__ float vdot(float4 a) { return a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w; }
-__device__ __forceinline__ float vdot(float a) { return a * a; }
-template <class V>
-__device__ __forceinline__ V vzero();
-template <>
-__device__ __forceinline__ float4 vzero<float4>() {
-  return make_float4(0.f, 0.f, 0.f, 0.f);
-}
-template <>
-__device__ __forceinline__ float vzero<float>() {
-  return 0.f;
-}
 
 // Sum over the G lanes of a group (xor butterfly stays inside the group).
 template <int G>
@@ -89,54 +54,6 @@ __device__ __forceinline__ const float* select_row(const dr_pool_desc& d, int64_
   return d.pool + r * (int64_t)dim;
 }
 
-template <int VEC, int G, int CPL>
-struct Row {
-  typename VecT<VEC>::T v[CPL];
-};
-
-template <int VEC, int G, int CPL>
-__device__ __forceinline__ void load_row(Row<VEC, G, CPL>& x, const float* p, int lg, int dv) {
-  using V = typename VecT<VEC>::T;
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) {
-    const int col = lg + c * G;
-    x.v[c] = (p && col < dv) ? reinterpret_cast<const V*>(p)[col] : vzero<V>();
-  }
-}
-
-// Rows read exactly once per launch: nontemporal hint (no L2 retention).
-
-template <int VEC, int G, int CPL>
-__device__ __forceinline__ void load_row_nt(Row<VEC, G, CPL>& x, const float* p, int lg, int dv) {
-  using V = typename VecT<VEC>::T;
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) {
-    const int col = lg + c * G;
-    x.v[c] = (p && col < dv) ? nt_load(reinterpret_cast<const V*>(p) + col) : vzero<V>();
-  }
-}
-
-
-template <int VEC, int G, int CPL>
-__device__ __forceinline__ void store_row_nt(const Row<VEC, G, CPL>& x, float* p, int lg, int dv) {
-  using V = typename VecT<VEC>::T;
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) {
-    const int col = lg + c * G;
-    if (col < dv) nt_store(x.v[c], reinterpret_cast<V*>(p) + col);
-  }
-}
-
-template <int VEC, int G, int CPL>
-__device__ __forceinline__ void store_row(const Row<VEC, G, CPL>& x, float* p, int lg, int dv) {
-  using V = typename VecT<VEC>::T;
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) {
-    const int col = lg + c * G;
-    if (col < dv) reinterpret_cast<V*>(p)[col] = x.v[c];
-  }
-}
-
 // clip_by_norm (embedding_ops._clip -> clip_ops.clip_by_norm) for ORDER_ALI,
 // and the fused kernel's `emb *= max_norm / l2` (fused_embedding_local_ops_gpu.
 // cu.cc:59-71) for ORDER_SEQ.  Enabled iff max_norm >= 0.
@@ -159,12 +76,6 @@ __device__ __forceinline__ void clip_row(Row<VEC, G, CPL>& x, float max_norm) {
       for (int c = 0; c < CPL; ++c) x.v[c] = vmul(x.v[c], f);
     }
   }
-}
-
-template <int VEC, int G, int CPL>
-__device__ __forceinline__ void acc_add(Row<VEC, G, CPL>& a, const Row<VEC, G, CPL>& b) {
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) a.v[c] = vadd(a.v[c], b.v[c]);
 }
 
 template <int VEC, int G, int CPL, int ORDER>

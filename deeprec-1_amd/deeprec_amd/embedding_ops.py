@@ -11,6 +11,8 @@ materialised.  Backward produces IndexedSlices per unique id through the
 deterministic segment-grad kernels and hands them to the optimizers
 (training.py) via `pending_grads`, like TF's sparse gradient path.
 """
+import os
+
 import torch
 
 from . import _lib, ops
@@ -52,6 +54,11 @@ def _anchor(holder):
         a = torch.zeros(1, device=holder.device, requires_grad=True)
         holder._anchor = a
     return a
+
+
+# DEEPREC_AMD_FUSED_ONEHOT=0 selects the resolve -> pool pipeline for
+# forward-only one-hot lookups (A/B measurement; both are HIP paths).
+_FUSED_ONEHOT = os.environ.get("DEEPREC_AMD_FUSED_ONEHOT", "1") != "0"
 
 
 def _ev_default_dev(ev):
@@ -351,10 +358,45 @@ class _UniqueGroup(object):
                 for t in range(len(self.feats))]
 
 
+def _fused_onehot(feats, order):
+    """Forward-only one-hot lookup of filter-free EVs in one fused launch
+    (dr_ev_lookup_onehot: probe + row copy, no resolve pass / row array).
+    Returns the [B, T*D] output, or None when the features do not qualify."""
+    import ctypes as C
+    p0 = feats[0].params
+    if not (len(feats) <= _lib.MAX_GROUP and isinstance(p0, EmbeddingVariable)):
+        return None
+    B = feats[0].batch
+    D = p0.dim
+    for f in feats:
+        p = f.params
+        if not (isinstance(p, EmbeddingVariable) and f.onehot and f.batch == B
+                and p.dim == D and p.device == p0.device and p.filter_freq == 0
+                and not callable(p.initializer) and f.values.numel() == B):
+            return None
+    if D % 4 != 0 or D > 256 or len(feats) * B >= (1 << 31):
+        return None
+    T = len(feats)
+    dev = feats[0].values.device
+    vals = _concat_values(feats, [t * B for t in range(T + 1)])
+    out = torch.empty((B, T * D), dtype=torch.float32, device=dev)
+    handles = (C.c_void_p * T)(*[f.params.handle.value for f in feats])
+    wsb = lib().dr_ev_lookup_onehot_workspace_size(T, B)
+    ws = workspace(wsb, dev)
+    check(lib().dr_ev_lookup_onehot(handles, T, ptr(vals), B, ptr(out), T * D, order, ptr(ws), wsb,
+                                    stream_handle(dev)))
+    ops._post(dev)
+    return out
+
+
 def _run(feats, order=ORDER_ALI, need_grad=None):
     """Grouped pooled lookup of features sharing the batch -> [B, sum(D_t)]."""
     if need_grad is None:
         need_grad = torch.is_grad_enabled() and any(not torch.is_tensor(f.params) for f in feats)
+    if not need_grad and _FUSED_ONEHOT:
+        out = _fused_onehot(feats, order)
+        if out is not None:
+            return out
     if _groupable(feats):
         _prepare_group(feats, need_grad)
     else:

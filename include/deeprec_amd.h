@@ -260,6 +260,18 @@ int dr_ev_resolve_grouped(dr_ev* const* evs, int num_tables, const int64_t* keys
                           const int64_t* koff_host, const int64_t* const* n_dev_per_table,
                           const int32_t* counts, int64_t* rows_out, void* ws, size_t ws_bytes,
                           void* stream);
+/* Fused one-hot forward lookup: KvResourceGather + SparseSegmentSum of     */
+/* embedding_lookup_sparse (embedding_ops.py:480-675, kv_variable_ops.cc:   */
+/* 314-366) for T filter-free EVs of equal dim when every bag holds exactly */
+/* one id (a [B, 1] SparseTensor per feature): keys [T, batch] (table t's   */
+/* id of bag b at t*batch + b) -> out[b*out_stride + t*dim + c].  Insert-on-*/
+/* miss with the EV default row, as resolve + pool.  order: DR_ORDER_ALI    */
+/* (embedding_lookup_sparse) or DR_ORDER_SEQ (fused op: 0 + e).  Requires   */
+/* dim % 4 == 0, dim <= 256, 16-B aligned out, T*batch < 2^31.              */
+size_t dr_ev_lookup_onehot_workspace_size(int num_tables, int64_t batch);
+int dr_ev_lookup_onehot(dr_ev* const* evs, int num_tables, const int64_t* keys, int64_t batch,
+                        float* out, int64_t out_stride, int order, void* ws, size_t ws_bytes,
+                        void* stream);
 /* Tagged resolve (owner side of the sharded exchange): keys of all T EVs  */
 /* (equal dim) in one array, table of key i = tags[i]; n_dev: optional      */
 /* DEVICE count.  Filtered keys give -(i+1) (read table t's default row).   */

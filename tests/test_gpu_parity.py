@@ -214,6 +214,77 @@ def test_multi_feature_grouped_lookup(dr, orc, grad):
         np.testing.assert_array_equal(H(v), ov)
 
 
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("D", [8, 128])
+def test_onehot_forward_lookup(dr, orc, fused, D):
+    """Forward-only one-hot lookup of filter-free EVs: the fused probe+copy
+    kernel (dr_ev_lookup_onehot) and the resolve -> pool pipeline must both
+    equal the oracle's unique -> gather -> pool, including misses (inserted
+    with the default row), duplicate new keys in one batch, key -1, and a
+    slot EV column whose rows exist but whose column was never touched."""
+    from deeprec_amd import embedding_ops as eo
+    rng = np.random.default_rng(83 + D)
+    B, F = 777, 3
+    saved = eo._FUSED_ONEHOT
+    eo._FUSED_ONEHOT = fused
+    try:
+        evs, oevs = [], []
+        for f in range(F):
+            evs.append(dr.EmbeddingVariable("oh%d_%d_%d" % (f, D, fused), D, 0.5 - f,
+                                            capacity=300))
+            oevs.append(orc.EV(D, 0.5 - f))
+            keys = np.arange(0, 400, 2, dtype=np.int64) + f
+            vals = rng.standard_normal((keys.shape[0], D)).astype(np.float32)
+            evs[-1].insert(T(keys), T(vals))
+            oevs[-1].insert(keys, vals)
+        for step in range(3):
+            ids = rng.integers(-1, 700, (F, B)).astype(np.int64)  # ~half new, dups, -1
+            flat = T(ids.reshape(-1))
+            ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+            sps = [dr.SparseTensor(T(ind), flat[f * B:(f + 1) * B], (B, 1)) for f in range(F)]
+            with torch.no_grad():
+                out = H(dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum"))
+            for f in range(F):
+                ref = orc.embedding_lookup_sparse(oevs[f], ind, ids[f], B, combiner="sum")
+                np.testing.assert_array_equal(out[:, f * D:(f + 1) * D], ref)
+        for f in range(F):
+            assert int(evs[f].total_count()[0]) == oevs[f].size()
+            k, v = evs[f].export()[:2]
+            ok, ov = oevs[f].export()[:2]
+            np.testing.assert_array_equal(H(k), ok)
+            np.testing.assert_array_equal(H(v), ov)
+    finally:
+        eo._FUSED_ONEHOT = saved
+
+
+def test_onehot_fused_abi_orders_and_slot_column(dr):
+    """dr_ev_lookup_onehot directly: SEQ order turns -0.0 into +0.0 (fused
+    op semantics), ALI keeps it; a slot EV (column 1) of existing keys is
+    initialised on first touch by the miss path."""
+    import ctypes as C
+    from deeprec_amd._lib import ORDER_ALI, ORDER_SEQ, check, lib, ptr, stream_handle, workspace
+    D, B = 4, 5
+    ev = dr.EmbeddingVariable("ohabi", D, 0.0, capacity=64)
+    ev.insert(T(np.array([1, 2], np.int64)), T(np.array([[-0.0] * D, [3.0] * D], np.float32)))
+    sl = ev.slot("acc", 0.25)
+    keys = T(np.array([1, 2, 2, 9, 1], np.int64))
+    for col_ev, order, want in ((ev, ORDER_ALI, None), (ev, ORDER_SEQ, None), (sl, ORDER_ALI, 0.25)):
+        out = torch.full((B, D), 7.0, device=DEV)
+        h = (C.c_void_p * 1)(col_ev.handle.value)
+        wsb = lib().dr_ev_lookup_onehot_workspace_size(1, B)
+        ws = workspace(wsb, DEV)
+        check(lib().dr_ev_lookup_onehot(h, 1, ptr(keys), B, ptr(out), D, order, ptr(ws), wsb,
+                                        stream_handle()))
+        o = H(out)
+        if want is not None:
+            assert (o == want).all()
+            continue
+        np.testing.assert_array_equal(o[1], [3.0] * D)
+        np.testing.assert_array_equal(o[3], [0.0] * D)  # new key 9: EV default
+        neg = np.signbit(o[0])
+        assert neg.all() if order == ORDER_ALI else (~neg).all()
+
+
 def test_sort_pairs_stable(ops):
     rng = np.random.default_rng(3)
     n = 100003

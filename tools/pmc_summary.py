@@ -1,6 +1,6 @@
 """Summarise rocprofv3 outputs of a bench run into profiles/.
 
-  python tools/pmc_summary.py <stats_dir> <fetch_dir> <write_dir> <round>
+  python tools/pmc_summary.py <stats_dir> <fetch_dir> <write_dir> <round> [kernel]
 
 * <stats_dir>/*_kernel_stats.csv   (rocprofv3 --kernel-trace --stats --output-format csv)
 * <fetch_dir>/*_counter_collection.csv (rocprofv3 --pmc FETCH_SIZE, own pass)
@@ -21,7 +21,7 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "pool_onehot_kernel"
+KERNEL = "ev_lookup_onehot_kernel"  # bench.py's dominant kernel (argv[5] overrides)
 
 
 def per_dispatch(d, counter):
@@ -32,7 +32,10 @@ def per_dispatch(d, counter):
 
 
 def main():
+    global KERNEL
     stats_dir, fetch_dir, write_dir, rnd = sys.argv[1:5]
+    if len(sys.argv) > 5:
+        KERNEL = sys.argv[5]
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     st = glob.glob(os.path.join(stats_dir, "*_kernel_stats.csv"))[0]
@@ -54,7 +57,7 @@ def main():
         "dispatches": [len(fetch), len(write)],
         "fetch_bytes_corrected": f_b,
         "write_bytes": w_b,
-        "pool_bytes_per_launch": f_b + w_b,
+        "bytes_per_launch": f_b + w_b,
         "kernel_avg_ns_rocprof": avg_ns,
     }
     json.dump(out, open(os.path.join(prof, "%s_pmc_traffic.json" % rnd), "w"), indent=1)
