@@ -15,6 +15,24 @@ key % G, all2all_input_dispatcher.cu:74).  One forward step:
   7. requester: fused gather+pool straight from the received rows
      (rowsel[perm[j]] = j), reference association order
 
+backward() (SURVEY.md 8e backward) runs the exchange in reverse:
+
+  1. requester: grouped segment grad per local unique id (SparseSegment*Grad
+     = unsorted_segment_sum over ascending nnz, math_grad.py:321-368)
+  2. rows packed into the forward's send order (owner, feature)
+  3. grad-rows all-to-all to the owners (the forward's splits, reversed)
+  4. owner: the received rows regrouped feature-major, source-rank-major
+     inside a feature, and queued on the EV as one IndexedSlices per feature
+
+The owner's slice for feature t is therefore the rank-order concatenation
+of every rank's (unique ids, partial grads) for the keys it owns -- what a
+data-parallel job hands the optimizer when the replicas' IndexedSlices are
+gathered (Horovod's allgather of IndexedSlices, in rank order) -- and the
+optimizer deduplicates it exactly as _deduplicate_indexed_slices does
+(optimizer.py:68-83; ascending position = ascending source rank), or, for
+SGD, applies repeated ids in order.  Deterministic, and equal bit for bit
+to the oracle applying the same concatenation.
+
 Parity: the per-bag reduction order is fixed by position within the bag,
 never by arrival rank, so the G-GPU output equals the 1-GPU output bit for
 bit.  The local steps go through a backend object so the exchange protocol
@@ -65,6 +83,47 @@ class HipLocal(object):
         ops._post(self.device)
         return out
 
+    def pool_grad(self, grad, idx, koff, num_unique, bag_offs, batch, combiner):
+        """Requester backward step 1: grad of every local unique id, in the
+        grouped-unique layout (row koff[t] + u), [koff[-1], D] fp32."""
+        T, D = self.T, self.dim
+        n = koff[-1]
+        descs = (_lib.DrPoolGradDesc * T)()
+        keep = []
+        for t in range(T):
+            d = descs[t]
+            d.top_grad = grad.data_ptr() + 4 * t * D
+            d.top_stride = T * D
+            if bag_offs is None:
+                d.bag_off, d.seg, d.seg_stride = None, None, 0
+            else:
+                nt = koff[t + 1] - koff[t]
+                seg = torch.repeat_interleave(
+                    torch.arange(batch, dtype=torch.int64, device=self.device),
+                    (bag_offs[t][1:] - bag_offs[t][:-1]).to(torch.int64), output_size=nt)
+                keep.append(seg)
+                d.bag_off = bag_offs[t].data_ptr()
+                d.seg = seg.data_ptr()
+                d.seg_stride = 1
+            d.idx = idx.data_ptr() + 4 * koff[t]
+            d.nnz = koff[t + 1] - koff[t]
+            d.num_unique = num_unique.data_ptr() + 8 * t
+            d.combiner = COMBINERS[combiner]
+        gu = torch.empty((max(n, 1), D), dtype=torch.float32, device=self.device)
+        wsb = lib().dr_pool_grad_grouped_workspace_size(n)
+        ws = workspace(wsb, self.device)
+        check(lib().dr_pool_grad_grouped(descs, T, batch, D, ptr(gu), ptr(ws), wsb,
+                                         stream_handle(self.device)))
+        ops._post(self.device)
+        return gu
+
+    def pack(self, src, perm):
+        """out[j] = src[perm[j]] (perm int32)."""
+        out = torch.empty((perm.numel(), self.dim), dtype=torch.float32, device=self.device)
+        if perm.numel():
+            ops.rows_pack(src, perm, out)
+        return out
+
     def pool(self, rows_recv, rowsel, idx, koff, bag_offs, batch, combiner):
         """Requester: pooled [batch, T*D] from the received rows.  rowsel[u]
         is the received row of unique u (idx given: nnz -> unique) or of nnz
@@ -107,6 +166,7 @@ class ShardedLookup(object):
         self.T = self.backend.T
         self.dim = self.backend.dim
         self.last_stats = {}
+        self._saved = None
 
     def _a2a(self, out, inp, out_splits=None, in_splits=None):
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
@@ -155,6 +215,66 @@ class ShardedLookup(object):
         rowsel[perm[:S].to(torch.int64)] = torch.arange(S, dtype=torch.int64, device=dev)
         out = be.pool(rows_r, rowsel, idx, koff, bag_offs, self.batch, combiner)
         self.last_stats = {"sent_keys": S, "recv_keys": R, "direct": direct}
+        self._saved = None
+        if need_grad:
+            self._saved = dict(idx=idx, koff=koff, U=U, perm=perm[:S], keys_r=keys_r, rc=rc,
+                               send=send_splits, recv=recv_splits, bag_offs=bag_offs,
+                               combiner=combiner)
+        return out
+
+    def backward(self, grad_out):
+        """grad_out: [B, T*D] gradient of the last forward(need_grad=True).
+
+        Returns, per feature t, the owner-side (keys [n_t], grads [n_t, D])
+        slice (source-rank-major), and queues it on evs[t].pending_grads as an
+        IndexedSlices for the optimizer (training.py)."""
+        sv = self._saved
+        if sv is None:
+            raise RuntimeError("backward() needs a forward(..., need_grad=True) first")
+        self._saved = None
+        T, G, D, be = self.T, self.world, self.dim, self.backend
+        g = grad_out.contiguous()
+        if tuple(g.shape) != (self.batch, T * D):
+            raise ValueError("grad must be [%d, %d]" % (self.batch, T * D))
+        # 1-2. per-unique grads, packed into the forward's send order
+        gu = be.pool_grad(g, sv["idx"], sv["koff"], sv["U"], sv["bag_offs"], self.batch,
+                          sv["combiner"])
+        grads_s = be.pack(gu, sv["perm"])
+        # 3. grad rows to the owners (reverse of the rows all-to-all)
+        R = int(sum(sv["recv"]))
+        grads_r = torch.empty((R, D), dtype=torch.float32, device=g.device)
+        self._a2a(grads_r, grads_s, sv["recv"], sv["send"])
+        # 4. regroup [source][feature] blocks feature-major: a block permutation
+        rc = sv["rc"]                                    # host [G, T]
+        n_t = rc.sum(0).tolist()
+        src_start = [[0] * T for _ in range(G)]
+        acc = 0
+        for p in range(G):
+            for t in range(T):
+                src_start[p][t] = acc
+                acc += int(rc[p, t])
+        blocks, starts, lens = [], [], []
+        acc = 0
+        for t in range(T):
+            for p in range(G):
+                blocks.append(src_start[p][t] - acc)
+                lens.append(int(rc[p, t]))
+                acc += int(rc[p, t])
+        dev = g.device
+        shift = torch.repeat_interleave(torch.tensor(blocks, dtype=torch.int64),
+                                        torch.tensor(lens, dtype=torch.int64)).to(dev)
+        perm_t = (torch.arange(R, dtype=torch.int64, device=dev) + shift).to(torch.int32)
+        keys_t = sv["keys_r"][perm_t.to(torch.int64)]
+        grads_t = be.pack(grads_r, perm_t)
+        out, off = [], 0
+        for t in range(T):
+            k = keys_t[off:off + n_t[t]]
+            v = grads_t[off:off + n_t[t]]
+            off += n_t[t]
+            out.append((k, v))
+            if self.evs is not None:
+                from .kv_variable_ops import IndexedSlices
+                self.evs[t].pending_grads.append(IndexedSlices(v, k, unique=False))
         return out
 
 

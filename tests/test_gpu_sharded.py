@@ -198,3 +198,104 @@ def _run_xgmi(world, steps=2):
 @pytest.mark.parametrize("world", [1, 2, 3])
 def test_xgmi_peer_write_engine(world):
     _run_xgmi(world)
+
+
+# ---------------------------------------------------------------------------
+# Sharded backward (ShardedLookup.backward): grad rows to the owners, then the
+# KV optimizer on each shard.  Reference: one EV per feature holding every
+# key, updated with the rank-order concatenation of each rank's (unique ids,
+# partial grads) -- deduplicated (Adagrad, optimizer.py:68-83) or applied in
+# order (SGD, gradient_descent.py:71-76).
+# ---------------------------------------------------------------------------
+def _run_sharded_train(world, onehot, opt_name, combiner):
+    import deeprec_amd as dr
+    from oracle import oracle as orc
+    from deeprec_amd.sharded import ShardedLookup
+    dr.load()
+    ex = _Exchange(world)
+    rng = np.random.default_rng(41 + world)
+    lr = np.float32(0.3)
+    engines, batches, grads = [], [], []
+    for r in range(world):
+        own = np.arange(r, KEYSPACE // 2, world, dtype=np.int64)
+        evs = []
+        for t in range(T):
+            ev = dr.EmbeddingVariable("tr%d_%d_%s_%s_%d_%d" % (world, int(onehot), opt_name,
+                                                              combiner, r, t), D, DEFAULT,
+                                      device=DEV)
+            ev.insert(torch.as_tensor(own, device=DEV), torch.as_tensor(_vals(t, own), device=DEV))
+            evs.append(ev)
+        eng = ShardedLookup(evs, world, r, B, torch.device(DEV))
+        eng._a2a = (lambda rr: (lambda out, inp, os_=None, is_=None:
+                                ex.a2a(rr, out, inp, os_, is_)))(r)
+        engines.append(eng)
+        lens = np.ones(B, np.int64) if onehot else rng.integers(0, 5, B)
+        if not onehot:
+            lens[3] = 0
+        nnz = int(lens.sum())
+        ids = rng.integers(0, KEYSPACE, (T, nnz)).astype(np.int64)
+        ids[:, :4] = 11 + r % 2                  # duplicates inside and across ranks
+        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+        batches.append((ids, off))
+        grads.append(rng.standard_normal((B, T * D)).astype(np.float32))
+    opts = [dr.GradientDescentOptimizer(lr) if opt_name == "sgd" else dr.AdagradOptimizer(lr, 0.1)
+            for _ in range(world)]
+    errs = []
+
+    def run(r):
+        try:
+            ids, off = batches[r]
+            bo = None if onehot else [torch.as_tensor(off, device=DEV)] * T
+            engines[r].forward(torch.as_tensor(ids, device=DEV), bag_offs=bo, combiner=combiner,
+                               need_grad=True)
+            engines[r].backward(torch.as_tensor(grads[r], device=DEV))
+            opts[r].apply_gradients(engines[r].evs, global_step=1)
+        except Exception as e:
+            errs.append(e)
+            ex.bar.abort()
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(120)
+    if errs:
+        raise errs[0]
+    dr.status_check()
+    allk = np.arange(0, KEYSPACE // 2, dtype=np.int64)
+    for t in range(T):
+        ref = orc.EV(D, DEFAULT)
+        ref.insert(allk, _vals(t, allk))
+        ks, gs = [], []
+        for p in range(world):
+            ids, off = batches[p]
+            u, idx = orc.unique(ids[t])
+            ref.gather(u)                                    # forward's insert-on-miss
+            seg = np.repeat(np.arange(B, dtype=np.int32), np.diff(off))
+            ks.append(u)
+            gs.append(orc.sparse_segment_reduce_grad(
+                np.ascontiguousarray(grads[p][:, t * D:(t + 1) * D]), idx, seg, u.shape[0],
+                combiner))
+        if opt_name == "sgd":
+            for k, g in zip(ks, gs):                          # repeated ids in order
+                ref.apply_sgd(lr, g, k, 1)
+        else:
+            acc = ref.create_slot(1, 0.1)
+            k, g = np.concatenate(ks), np.concatenate(gs)
+            u, pos = orc.unique(k)
+            ref.apply_adagrad(acc, lr, orc.unsorted_segment_sum(g, pos, u.shape[0]), u, 1)
+        rk, rv = ref.export()[:2]
+        for r in range(world):
+            k, v = [x.cpu().numpy() for x in engines[r].evs[t].export()[:2]]
+            o = np.argsort(k)
+            m = rk % world == r
+            ro = np.argsort(rk[m])
+            np.testing.assert_array_equal(k[o], rk[m][ro])
+            np.testing.assert_array_equal(v[o], rv[m][ro])
+
+
+@pytest.mark.parametrize("world", [1, 2])
+@pytest.mark.parametrize("opt_name", ["sgd", "adagrad"])
+@pytest.mark.parametrize("onehot,combiner", [(True, "sum"), (False, "mean")])
+def test_sharded_backward_apply(world, opt_name, onehot, combiner):
+    _run_sharded_train(world, onehot, opt_name, combiner)

@@ -85,6 +85,23 @@ class OracleLocal(object):
                 out[m] = self.evs[t].gather(k[m])
         return torch.from_numpy(out)
 
+    def pool_grad(self, grad, idx, koff, U, bag_offs, batch, combiner):
+        g = grad.numpy()
+        out = np.zeros((koff[-1], D), np.float32)
+        for t in range(self.T):
+            it = idx.numpy()[koff[t]:koff[t + 1]]
+            if bag_offs is None:
+                seg = np.arange(batch, dtype=np.int32)
+            else:
+                seg = np.repeat(np.arange(batch, dtype=np.int32), np.diff(bag_offs[t].numpy()))
+            u = int(U[t])
+            out[koff[t]:koff[t] + u] = self.orc.sparse_segment_reduce_grad(
+                np.ascontiguousarray(g[:, t * D:(t + 1) * D]), it, seg, u, combiner)
+        return torch.from_numpy(out)
+
+    def pack(self, src, perm):
+        return torch.from_numpy(np.ascontiguousarray(src.numpy()[perm.numpy().astype(np.int64)]))
+
     def pool(self, rows_recv, rowsel, idx, koff, bag_offs, batch, combiner):
         rr, rs = rows_recv.numpy(), rowsel.numpy()
         out = np.zeros((batch, self.T * D), np.float32)
@@ -98,7 +115,7 @@ class OracleLocal(object):
                 it = idx.numpy()[koff[t]:koff[t + 1]]
                 U = int(it.max()) + 1
                 emb = rr[rs[koff[t]:koff[t] + U]]
-                off = bag_offs[t].numpy()
+                off = (np.arange(batch + 1) if bag_offs is None else bag_offs[t].numpy())
                 seg = np.repeat(np.arange(batch, dtype=np.int32), np.diff(off))
                 pooled = self.orc.sparse_segment_reduce(emb, it, seg, combiner,
                                                         num_segments=batch)
@@ -165,6 +182,34 @@ def _worker(rank, world, port, outdir):
                     ind = np.stack([seg, np.zeros_like(seg)], 1)
                     ref = orc.embedding_lookup_sparse(ref_ev, ind, ids[t], B, combiner=combiner)
                     np.testing.assert_array_equal(out[:, t * D:(t + 1) * D], ref)
+        # backward: the owner receives, per feature, the rank-order
+        # concatenation of every rank's (unique ids it owns, partial grads)
+        for onehot in (True, False):
+            for combiner in (("sum",) if onehot else ("sum", "mean")):
+                allb = [_batches(p, onehot) for p in range(world)]
+                if not onehot:
+                    allb = [([b[0][0]] * T, [b[1][0]] * T) for b in allb]
+                grads = [np.random.default_rng(300 + p).standard_normal((B, T * D))
+                         .astype(np.float32) for p in range(world)]
+                ids, offs = allb[rank]
+                bo = None if onehot else [torch.from_numpy(o) for o in offs]
+                eng.forward(torch.from_numpy(np.stack(ids)), bag_offs=bo, combiner=combiner,
+                            need_grad=True)
+                got = eng.backward(torch.from_numpy(grads[rank]))
+                for t in range(T):
+                    ek, ev_ = [], []
+                    for p in range(world):
+                        pid, poff = allb[p]
+                        u, idx = orc.unique(pid[t])
+                        seg = np.repeat(np.arange(B, dtype=np.int32), np.diff(poff[t]))
+                        gu = orc.sparse_segment_reduce_grad(
+                            np.ascontiguousarray(grads[p][:, t * D:(t + 1) * D]), idx, seg,
+                            u.shape[0], combiner)
+                        m = u % world == rank
+                        ek.append(u[m])
+                        ev_.append(gu[m])
+                    np.testing.assert_array_equal(got[t][0].numpy(), np.concatenate(ek))
+                    np.testing.assert_array_equal(got[t][1].numpy(), np.concatenate(ev_))
         # every key looked up anywhere is now owned by exactly its owner shard
         for t in range(T):
             keys = sh_evs[t].export()[0]
