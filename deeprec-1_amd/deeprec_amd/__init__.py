@@ -15,6 +15,7 @@ from .embedding_ops import (DenseTable, SparseTensor, embedding_lookup, embeddin
 from .kv_variable_ops import (CBFFilter, CounterFilter, EmbeddingVariable, EmbeddingVariableOption,
                               GlobalStepEvict, IndexedSlices, get_embedding_variable)
 from .ops import set_validate, status_check
+from .string_ops import StringTensor, string_to_hash_bucket_fast
 from .training import AdagradOptimizer, AdamOptimizer, GradientDescentOptimizer
 
 __all__ = [
@@ -23,5 +24,6 @@ __all__ = [
     "fused_embedding_lookup_sparse", "safe_embedding_lookup_sparse", "CBFFilter",
     "CounterFilter", "EmbeddingVariable", "EmbeddingVariableOption", "GlobalStepEvict",
     "IndexedSlices", "get_embedding_variable", "set_validate", "status_check",
-    "AdagradOptimizer", "AdamOptimizer", "GradientDescentOptimizer",
+    "AdagradOptimizer", "AdamOptimizer", "GradientDescentOptimizer", "StringTensor",
+    "string_to_hash_bucket_fast",
 ]

@@ -453,6 +453,21 @@ int dr_crossnet_layer_bf16(const uint16_t* x0, const uint16_t* xl, const uint16_
                            void* stream);
 
 /* ------------------------------------------------------------------------ */
+/* String -> id, the step before the lookup.  Strings are one byte buffer    */
+/* plus int64 offsets[n+1] (string i = bytes[offsets[i] .. offsets[i+1])).   */
+/* ------------------------------------------------------------------------ */
+/* farmhash Fingerprint64 (core/platform/fingerprint.h:80-88; the Fingerprint */
+/* op's per-string value, core/kernels/fingerprint_op.cc:55-64).             */
+int dr_fingerprint64(const uint8_t* bytes, const int64_t* offsets, int64_t n, uint64_t* out,
+                     void* stream);
+/* StringToHashBucketFast (core/kernels/string_to_hash_bucket_ali_op.h:33-63, */
+/* op def core/ops/string_ops.cc:77): out[i] = Fingerprint64(s_i) %          */
+/* num_buckets.  EV string columns pass INT64_MAX                            */
+/* (python/feature_column/feature_column_v2.py:5954-5957).                   */
+int dr_string_to_hash_bucket_fast(const uint8_t* bytes, const int64_t* offsets, int64_t n,
+                                  int64_t num_buckets, int64_t* out, void* stream);
+
+/* ------------------------------------------------------------------------ */
 /* Synthetic data (bench/tests): table[r, c] = hash-derived uniform [-1, 1)  */
 /* of (seed, r, c), regenerable on host (dr_synth_value).                     */
 /* ------------------------------------------------------------------------ */

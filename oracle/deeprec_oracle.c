@@ -978,3 +978,143 @@ int orc_pipeline_dense_lookup_sparse(const float* table, int64_t D, const int64_
   free(uniq); free(idx); free(emb);
   return ORC_OK;
 }
+
+/* ------------------------------------------------------------------------ */
+/* String -> id: StringToHashBucketFast (string_to_hash_bucket_ali_op.h:     */
+/* 33-63: bucket = Fingerprint64(s) % num_buckets) and the EV column's       */
+/* num_buckets = INT64_MAX (feature_column_v2.py:5954-5957).                 */
+/* Fingerprint64 = farmhash::Fingerprint64 (tensorflow/core/platform/        */
+/* fingerprint.h:80-88), i.e. farmhashna::Hash64 of google/farmhash          */
+/* @816a4ae622e964763ca0862d9dbd19324a1eaf45 (tensorflow/workspace.bzl:      */
+/* 275-282; a network-fetched dependency absent from the reference tree).    */
+/* Restated from farmhash's published algorithm; pinned by the reference's   */
+/* golden values (fingerprint_test.cc:26-29, fingerprint_op_test.cc:64-106,  */
+/* string_to_hash_bucket_op_test.py:40-50) in tests/golden/.                 */
+/* ------------------------------------------------------------------------ */
+static const uint64_t orc_k0 = 0xc3a5c85c97cb3127ULL;
+static const uint64_t orc_k1 = 0xb492b66fbe98f273ULL;
+static const uint64_t orc_k2 = 0x9ae16a3b2f90404fULL;
+
+static uint64_t orc_fetch64(const uint8_t* p) {
+  uint64_t v;
+  memcpy(&v, p, 8);
+  return v; /* little-endian host */
+}
+static uint32_t orc_fetch32(const uint8_t* p) {
+  uint32_t v;
+  memcpy(&v, p, 4);
+  return v;
+}
+static uint64_t orc_rot64(uint64_t v, int s) { return s == 0 ? v : (v >> s) | (v << (64 - s)); }
+static uint64_t orc_shiftmix(uint64_t v) { return v ^ (v >> 47); }
+static uint64_t orc_hash_len16(uint64_t u, uint64_t v, uint64_t mul) {
+  uint64_t a = (u ^ v) * mul;
+  a ^= a >> 47;
+  uint64_t b = (v ^ a) * mul;
+  b ^= b >> 47;
+  return b * mul;
+}
+static uint64_t orc_hash_len0to16(const uint8_t* s, uint64_t len) {
+  if (len >= 8) {
+    uint64_t mul = orc_k2 + len * 2;
+    uint64_t a = orc_fetch64(s) + orc_k2;
+    uint64_t b = orc_fetch64(s + len - 8);
+    uint64_t c = orc_rot64(b, 37) * mul + a;
+    uint64_t d = (orc_rot64(a, 25) + b) * mul;
+    return orc_hash_len16(c, d, mul);
+  }
+  if (len >= 4) {
+    uint64_t mul = orc_k2 + len * 2;
+    uint64_t a = orc_fetch32(s);
+    return orc_hash_len16(len + (a << 3), orc_fetch32(s + len - 4), mul);
+  }
+  if (len > 0) {
+    uint8_t a = s[0], b = s[len >> 1], c = s[len - 1];
+    uint32_t y = (uint32_t)a + ((uint32_t)b << 8);
+    uint32_t z = (uint32_t)len + ((uint32_t)c << 2);
+    return orc_shiftmix(y * orc_k2 ^ z * orc_k0) * orc_k2;
+  }
+  return orc_k2;
+}
+static uint64_t orc_hash_len17to32(const uint8_t* s, uint64_t len) {
+  uint64_t mul = orc_k2 + len * 2;
+  uint64_t a = orc_fetch64(s) * orc_k1;
+  uint64_t b = orc_fetch64(s + 8);
+  uint64_t c = orc_fetch64(s + len - 8) * mul;
+  uint64_t d = orc_fetch64(s + len - 16) * orc_k2;
+  return orc_hash_len16(orc_rot64(a + b, 43) + orc_rot64(c, 30) + d,
+                        a + orc_rot64(b + orc_k2, 18) + c, mul);
+}
+static uint64_t orc_hash_len33to64(const uint8_t* s, uint64_t len) {
+  uint64_t mul = orc_k2 + len * 2;
+  uint64_t a = orc_fetch64(s) * orc_k2;
+  uint64_t b = orc_fetch64(s + 8);
+  uint64_t c = orc_fetch64(s + len - 8) * mul;
+  uint64_t d = orc_fetch64(s + len - 16) * orc_k2;
+  uint64_t y = orc_rot64(a + b, 43) + orc_rot64(c, 30) + d;
+  uint64_t z = orc_hash_len16(y, a + orc_rot64(b + orc_k2, 18) + c, mul);
+  uint64_t e = orc_fetch64(s + 16) * mul;
+  uint64_t f = orc_fetch64(s + 24);
+  uint64_t g = (y + orc_fetch64(s + len - 32)) * mul;
+  uint64_t h = (z + orc_fetch64(s + len - 24)) * mul;
+  return orc_hash_len16(orc_rot64(e + f, 43) + orc_rot64(g, 30) + h,
+                        e + orc_rot64(f + a, 18) + g, mul);
+}
+static void orc_weak32(const uint8_t* s, uint64_t a, uint64_t b, uint64_t* o1, uint64_t* o2) {
+  uint64_t w = orc_fetch64(s), x = orc_fetch64(s + 8), y = orc_fetch64(s + 16),
+           z = orc_fetch64(s + 24);
+  a += w;
+  b = orc_rot64(b + a + z, 21);
+  uint64_t c = a;
+  a += x;
+  a += y;
+  b += orc_rot64(a, 44);
+  *o1 = a + z;
+  *o2 = b + c;
+}
+
+uint64_t orc_fingerprint64(const uint8_t* s, uint64_t len) {
+  if (len <= 16) return orc_hash_len0to16(s, len);
+  if (len <= 32) return orc_hash_len17to32(s, len);
+  if (len <= 64) return orc_hash_len33to64(s, len);
+  const uint64_t seed = 81;
+  uint64_t x = seed, y = seed * orc_k1 + 113, z = orc_shiftmix(y * orc_k2 + 113) * orc_k2;
+  uint64_t v1 = 0, v2 = 0, w1 = 0, w2 = 0, t;
+  x = x * orc_k2 + orc_fetch64(s);
+  const uint8_t* end = s + ((len - 1) / 64) * 64;
+  const uint8_t* last64 = end + ((len - 1) & 63) - 63;
+  do {
+    x = orc_rot64(x + y + v1 + orc_fetch64(s + 8), 37) * orc_k1;
+    y = orc_rot64(y + v2 + orc_fetch64(s + 48), 42) * orc_k1;
+    x ^= w2;
+    y += v1 + orc_fetch64(s + 40);
+    z = orc_rot64(z + w1, 33) * orc_k1;
+    orc_weak32(s, v2 * orc_k1, x + w1, &v1, &v2);
+    orc_weak32(s + 32, z + w2, y + orc_fetch64(s + 16), &w1, &w2);
+    t = z; z = x; x = t;
+    s += 64;
+  } while (s != end);
+  uint64_t mul = orc_k1 + ((z & 0xff) << 1);
+  s = last64;
+  w1 += ((len - 1) & 63);
+  v1 += w1;
+  w1 += v1;
+  x = orc_rot64(x + y + v1 + orc_fetch64(s + 8), 37) * mul;
+  y = orc_rot64(y + v2 + orc_fetch64(s + 48), 42) * mul;
+  x ^= w2 * 9;
+  y += v1 * 9 + orc_fetch64(s + 40);
+  z = orc_rot64(z + w1, 33) * mul;
+  orc_weak32(s, v2 * mul, x + w1, &v1, &v2);
+  orc_weak32(s + 32, z + w2, y + orc_fetch64(s + 16), &w1, &w2);
+  t = z; z = x; x = t;
+  return orc_hash_len16(orc_hash_len16(v1, w1, mul) + orc_shiftmix(y) * orc_k0 + z,
+                        orc_hash_len16(v2, w2, mul) + x, mul);
+}
+
+/* StringToHashBucketFast over n strings in (offsets[n+1], bytes) layout. */
+void orc_string_to_hash_bucket_fast(const uint8_t* bytes, const int64_t* offsets, int64_t n,
+                                    int64_t num_buckets, int64_t* out) {
+  for (int64_t i = 0; i < n; ++i)
+    out[i] = (int64_t)(orc_fingerprint64(bytes + offsets[i], (uint64_t)(offsets[i + 1] - offsets[i])) %
+                       (uint64_t)num_buckets);
+}

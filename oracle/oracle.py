@@ -68,6 +68,8 @@ def lib():
             "orc_dot_interaction": (None, [p, i64, i64, i64, p]),
             "orc_crossnet_layer": (None, [p, p, p, p, i64, i64, p]),
             "orc_fasthash64": (C.c_uint64, [i64, C.c_uint64]),
+            "orc_fingerprint64": (C.c_uint64, [p, C.c_uint64]),
+            "orc_string_to_hash_bucket_fast": (None, [p, p, i64, i64, p]),
             "orc_pipeline_ev_lookup_sparse": (i32, [p, p, i64, p, i64, i32, i32, p]),
             "orc_pipeline_dense_lookup_sparse": (i32, [p, i64, p, i64, p, i64, i32, i32, p]),
         }
@@ -209,6 +211,29 @@ def fused_pre_lookup(values, part_rows):
 
 def fasthash64(key, seed):
     return lib().orc_fasthash64(int(key), int(seed))
+
+
+def fingerprint64(data):
+    """farmhash Fingerprint64 of a bytes object (fingerprint.h:80-88)."""
+    b = np.frombuffer(bytes(data) + b"\0", np.uint8)
+    return int(lib().orc_fingerprint64(_p(b), len(data)))
+
+
+def strings_to_arrays(strings):
+    """(offsets int64 [n+1], bytes uint8) layout of a list of str/bytes."""
+    enc = [s.encode() if isinstance(s, str) else bytes(s) for s in strings]
+    off = np.zeros(len(enc) + 1, np.int64)
+    off[1:] = np.cumsum([len(e) for e in enc])
+    return off, np.frombuffer(b"".join(enc) + b"\0", np.uint8)
+
+
+def string_to_hash_bucket_fast(strings, num_buckets):
+    """StringToHashBucketFast (string_to_hash_bucket_ali_op.h:33-63)."""
+    off, buf = strings_to_arrays(strings)
+    out = np.empty(len(strings), np.int64)
+    lib().orc_string_to_hash_bucket_fast(_p(buf), _p(off), len(strings), int(num_buckets),
+                                         _p(out))
+    return out
 
 
 def fm2(emb):

@@ -177,9 +177,38 @@ def ev_kats():
     )
 
 
+def fingerprint():
+    """Fingerprint64 / StringToHashBucketFast KATs.  Byte strings are stored
+    as generating rules (iota from a start byte, as the reference test builds
+    them) or as literal ASCII."""
+    return dict(
+        # core/platform/fingerprint_test.cc:26-29
+        fingerprint64=[dict(ascii="Hello", value=str(15404698994557526151)),
+                       dict(ascii="World", value=str(18308117990299812472))],
+        # python/kernel_tests/string_to_hash_bucket_op_test.py:40-50 (comments
+        # give the raw fingerprints; num_buckets 10 -> [9, 2, 2, 5])
+        fingerprint64_letters=[dict(ascii="a", value=str(12917804110809363939)),
+                               dict(ascii="b", value=str(11795596070477164822)),
+                               dict(ascii="c", value=str(11430444447143000872)),
+                               dict(ascii="d", value=str(4470636696479570465))],
+        hash_bucket_fast=dict(strings=["a", "b", "c", "d"], num_buckets=10,
+                              expected=[9, 2, 2, 5]),
+        # core/kernels/fingerprint_op_test.cc:64-74: uint8 [1, 3,4,5,6,7] iota
+        # from 47 (wrapping), one row of 2520 bytes -> little-endian bytes
+        op_bytes=dict(iota_start=47, length=2520, expected_le="2d90df0379363c43"),
+        # :78-106: strings of 10, 7, 0, 19 bytes, iota from 0, 7, 71, 41; per
+        # string fingerprints (shape {4}) and the fingerprint of their
+        # concatenated little-endian bytes (shape {1, 2, 2})
+        op_strings=dict(iota_starts=[0, 7, 71, 41], lengths=[10, 7, 0, 19],
+                        expected_each_le=["eaffd6b2b24d709b", "6e9ded21c64a6152",
+                                          "4f40902f3b6ae19a", "0d9b7f6323141cb8"],
+                        expected_combined_le="92432852a37c4818"),
+    )
+
+
 def main():
     out = dict(fused_local=fused_local(), pre_lookup_partition=pre_lookup_partition(),
-               segment_formula=segment_formula(), ev=ev_kats())
+               segment_formula=segment_formula(), ev=ev_kats(), fingerprint=fingerprint())
     for k, v in out.items():
         with open(os.path.join(HERE, k + ".json"), "w") as f:
             json.dump(v, f, indent=1)

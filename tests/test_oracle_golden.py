@@ -269,3 +269,34 @@ def test_ev_import_partition_filter(orc):
     assert k.tolist() == [x for x in range(20) if x % 1000 % 4 == 1]
     assert (fr == 2).all()               # clamped up to filter_freq (embedding_var.h:204-209)
     assert ver.tolist() == [x * 10 for x in k]
+
+
+# Fingerprint64 / StringToHashBucketFast: fingerprint_test.cc:26-29,
+# fingerprint_op_test.cc:64-106, string_to_hash_bucket_op_test.py:40-50 ------
+def _iota_bytes(start, n):
+    return ((np.arange(n) + start) % 256).astype(np.uint8).tobytes()
+
+
+def test_fingerprint64_kat(orc):
+    g = load("fingerprint")
+    for c in g["fingerprint64"] + g["fingerprint64_letters"]:
+        assert orc.fingerprint64(c["ascii"].encode()) == int(c["value"])
+    hb = g["hash_bucket_fast"]
+    np.testing.assert_array_equal(orc.string_to_hash_bucket_fast(hb["strings"], hb["num_buckets"]),
+                                  hb["expected"])
+    ob = g["op_bytes"]                                  # > 64 bytes: the long loop
+    fp = orc.fingerprint64(_iota_bytes(ob["iota_start"], ob["length"]))
+    assert fp.to_bytes(8, "little").hex() == ob["expected_le"]
+    os_ = g["op_strings"]                               # 0-16 and 17-32 bytes
+    each = [orc.fingerprint64(_iota_bytes(s, n)).to_bytes(8, "little")
+            for s, n in zip(os_["iota_starts"], os_["lengths"])]
+    assert [e.hex() for e in each] == os_["expected_each_le"]
+    assert orc.fingerprint64(b"".join(each)).to_bytes(8, "little").hex() == \
+        os_["expected_combined_le"]
+
+
+def test_hash_bucket_int64_max_for_ev_columns(orc):
+    # feature_column_v2.py:5954-5957: EV string columns hash into INT64_MAX buckets
+    ids = orc.string_to_hash_bucket_fast(["a", "Hello"], np.iinfo(np.int64).max)
+    assert ids[0] == 12917804110809363939 % (2 ** 63 - 1)
+    assert ids[1] == 15404698994557526151 % (2 ** 63 - 1)
