@@ -468,6 +468,13 @@ int dr_string_to_hash_bucket_fast(const uint8_t* bytes, const int64_t* offsets, 
                                   int64_t num_buckets, int64_t* out, void* stream);
 
 /* ------------------------------------------------------------------------ */
+/* Checkpoint support (host function, no device work): crc32c::Extend of    */
+/* core/lib/hash/crc32c.h, used for TensorBundle entry and SSTable block     */
+/* checksums (core/util/tensor_bundle/tensor_bundle.cc:435-455).             */
+/* ------------------------------------------------------------------------ */
+uint32_t dr_crc32c_extend(uint32_t init_crc, const void* data, size_t n);
+
+/* ------------------------------------------------------------------------ */
 /* Synthetic data (bench/tests): table[r, c] = hash-derived uniform [-1, 1)  */
 /* of (seed, r, c), regenerable on host (dr_synth_value).                     */
 /* ------------------------------------------------------------------------ */

@@ -236,6 +236,25 @@ def string_to_hash_bucket_fast(strings, num_buckets):
     return out
 
 
+def dump_embedding_values(keys, values, versions, freqs):
+    """DumpEmbeddingValues (kv_variable_ops.h:148-265): a snapshot's entries
+    grouped into 1000 sub-partitions by key % 1000 with C++ remainder
+    semantics (negative keys fall in no sub-partition and are dropped),
+    snapshot order kept inside a sub-partition.  versions / freqs may be
+    empty (steps_to_live == 0 / no filter).  Returns (partition_offset int32
+    [1001], keys, values, versions, freqs)."""
+    keys = np.asarray(keys, np.int64)
+    parts = [[] for _ in range(1000)]
+    for i, k in enumerate(keys.tolist()):
+        if k >= 0:
+            parts[k % 1000].append(i)
+    order = np.array([i for p in parts for i in p], np.int64)
+    offs = np.zeros(1001, np.int32)
+    offs[1:] = np.cumsum([len(p) for p in parts])
+    pick = lambda a: (np.asarray(a)[order] if len(a) else np.asarray(a))
+    return offs, keys[order], np.asarray(values)[order], pick(versions), pick(freqs)
+
+
 def fm2(emb):
     emb = np.ascontiguousarray(emb, np.float32)
     B, F, D = emb.shape
