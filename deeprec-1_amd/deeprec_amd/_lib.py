@@ -158,6 +158,9 @@ SIGNATURES = {
     "dr_fingerprint64": (_I32, [_P, _P, _I64, _P, _P]),
     "dr_string_to_hash_bucket_fast": (_I32, [_P, _P, _I64, _I64, _P, _P]),
     "dr_crc32c_extend": (C.c_uint32, [C.c_uint32, _P, _SZ]),
+    "dr_sparse_fill_workspace_size": (_SZ, [_I64, _I64]),
+    "dr_sparse_prune_fill": (_I32, [_P, _I32, _P, _P, _I64, _I64, _I32, _I64, _F32, _P, _P, _P,
+                                    _P, _P, _P, _P, _SZ, _P]),
     "dr_fill_synthetic": (_I32, [_P, _I64, _I32, _U64, _P]),
     "dr_synth_value": (_F32, [_U64, _I64, _I64]),
 }

@@ -542,36 +542,48 @@ def _partitioned_lookup_sparse(params, sp_ids, sp_weights, partition_strategy, c
 # ---------------------------------------------------------------------------
 # safe_embedding_lookup_sparse (embedding_ops.py:1209-1344)
 # ---------------------------------------------------------------------------
+def sparse_prune_fill(sp_ids, sp_weights=None, default_id=0, prune=0):
+    """_prune_invalid_ids / _prune_invalid_weights (prune 1 / 2) and
+    sparse_fill_empty_rows (embedding_ops.py:1299-1310) in one GPU call
+    (dr_sparse_prune_fill).  Returns (SparseTensor ids, SparseTensor weights
+    or None, is_row_empty bool [B], reverse_index_map int64 [nnz])."""
+    ind = sp_ids.indices.to(torch.int64).contiguous()
+    val = sp_ids.values.to(torch.int64).contiguous()
+    dev = val.device
+    w = None if sp_weights is None else sp_weights.values.to(torch.float32).contiguous()
+    n = val.numel()
+    rank = ind.shape[1] if ind.dim() == 2 else 2
+    B = int(sp_ids.dense_shape[0])
+    cap = n + B
+    oind = torch.empty((max(cap, 1), rank), dtype=torch.int64, device=dev)
+    oval = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+    ow = None if w is None else torch.empty(max(cap, 1), dtype=torch.float32, device=dev)
+    rev = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    empty = torch.empty(max(B, 1), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    wsb = lib().dr_sparse_fill_workspace_size(n, B)
+    ws = workspace(wsb, dev)
+    check(lib().dr_sparse_prune_fill(ptr(ind), rank, ptr(val), ptr(w), n, B, int(prune),
+                                     int(default_id or 0), 1.0, ptr(oind), ptr(oval), ptr(ow),
+                                     ptr(rev), ptr(empty), ptr(cnt), ptr(ws), wsb,
+                                     stream_handle(dev)))
+    ops._post(dev)
+    m = int(cnt.item())          # the output's size (SparseFillEmptyRows allocates it too)
+    sp = SparseTensor(oind[:m], oval[:m], sp_ids.dense_shape)
+    spw = None if ow is None else SparseTensor(oind[:m], ow[:m], sp_ids.dense_shape)
+    return sp, spw, empty[:B].to(torch.bool), rev[:n]
+
+
+def sparse_fill_empty_rows(sp_input, default_value, name=None):
+    """tf.sparse.fill_empty_rows (SparseFillEmptyRows) for int64 ids:
+    returns (filled SparseTensor, empty_row_indicator)."""
+    sp, _, empty, _ = sparse_prune_fill(sp_input, None, default_value, 0)
+    return sp, empty
+
+
 def _prune_and_fill(sp_ids, sp_weights, combiner, default_id, prune):
-    ind = sp_ids.indices.to(torch.int64)
-    val = sp_ids.values.to(torch.int64)
-    w = None if sp_weights is None else sp_weights.values.to(torch.float32)
-    B = sp_ids.dense_shape[0]
-    if prune:
-        keep = val >= 0                                       # _prune_invalid_ids
-        if w is not None and combiner != "sum":
-            keep = keep & (w > 0)                             # _prune_invalid_weights
-        ind, val = ind[keep], val[keep]
-        if w is not None:
-            w = w[keep]
-    present = torch.zeros(B, dtype=torch.bool, device=val.device)
-    present[ind[:, 0]] = True
-    empty = ~present
-    fill = torch.nonzero(empty).reshape(-1)
-    if fill.numel():                                          # sparse_fill_empty_rows
-        add_ind = torch.stack([fill, torch.zeros_like(fill)], 1)
-        ind = torch.cat([ind, add_ind])
-        val = torch.cat([val, torch.full((fill.numel(),), int(default_id or 0),
-                                         dtype=torch.int64, device=val.device)])
-        if w is not None:
-            w = torch.cat([w, torch.ones(fill.numel(), dtype=torch.float32, device=w.device)])
-        key = ind[:, 0] * (sp_ids.dense_shape[1] + 1) + ind[:, 1]
-        order = torch.sort(key, stable=True).indices
-        ind, val = ind[order], val[order]
-        if w is not None:
-            w = w[order]
-    sp = SparseTensor(ind, val, sp_ids.dense_shape)
-    spw = None if w is None else SparseTensor(ind, w, sp_ids.dense_shape)
+    mode = 0 if not prune else (2 if sp_weights is not None and combiner != "sum" else 1)
+    sp, spw, empty, _ = sparse_prune_fill(sp_ids, sp_weights, default_id, mode)
     return sp, spw, empty
 
 

@@ -467,6 +467,25 @@ int dr_fingerprint64(const uint8_t* bytes, const int64_t* offsets, int64_t n, ui
 int dr_string_to_hash_bucket_fast(const uint8_t* bytes, const int64_t* offsets, int64_t n,
                                   int64_t num_buckets, int64_t* out, void* stream);
 
+/* SparseTensor preparation of safe_embedding_lookup_sparse                  */
+/* (python/ops/embedding_ops.py:1289-1310) in one call: prune = 0 none,      */
+/* 1 _prune_invalid_ids (ids < 0), 2 also _prune_invalid_weights (w <= 0),   */
+/* then SparseFillEmptyRows (core/kernels/sparse_fill_empty_rows_op_util.h:  */
+/* 17-128): rows ascending, a row's entries in input order, each empty row   */
+/* one [row, 0..] entry = default_value (weight default_weight).  indices    */
+/* [nnz, rank]; outputs sized for nnz + dense_rows entries, the used count   */
+/* in *out_nnz (DEVICE int64).  reverse_index_map[i] = output position of    */
+/* input i or -1 when pruned (nullable); empty_row [dense_rows] (nullable).  */
+/* weights / out_weights both NULL or both set.  Rows out of range latch     */
+/* INVALID_ARGUMENT.                                                         */
+size_t dr_sparse_fill_workspace_size(int64_t nnz, int64_t dense_rows);
+int dr_sparse_prune_fill(const int64_t* indices, int rank, const int64_t* values,
+                         const float* weights, int64_t nnz, int64_t dense_rows, int prune,
+                         int64_t default_value, float default_weight, int64_t* out_indices,
+                         int64_t* out_values, float* out_weights, int64_t* reverse_index_map,
+                         uint8_t* empty_row, int64_t* out_nnz, void* ws, size_t ws_bytes,
+                         void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* Checkpoint support (host function, no device work): crc32c::Extend of    */
 /* core/lib/hash/crc32c.h, used for TensorBundle entry and SSTable block     */

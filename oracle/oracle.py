@@ -401,7 +401,7 @@ def prune_and_fill(indices, values, dense_shape, weights=None, combiner="mean", 
                    prune=True):
     """safe_embedding_lookup_sparse steps 1-3 (embedding_ops.py:1289-1310).
 
-    indices [nnz,2] int64 row-major canonical, values [nnz] int64.
+    indices [nnz,2] int64 (any order), values [nnz] int64.
     Returns (indices, values, weights, is_row_empty)."""
     indices = np.asarray(indices, np.int64).reshape(-1, 2)
     values = np.asarray(values, np.int64)
@@ -414,20 +414,53 @@ def prune_and_fill(indices, values, dense_shape, weights=None, combiner="mean", 
         if w is not None:
             w = w[keep]
     B = int(dense_shape[0])
-    present = np.zeros(B, bool)
-    present[indices[:, 0]] = True
-    empty = ~present
-    if empty.any():                                          # sparse_fill_empty_rows
-        fill_rows = np.nonzero(empty)[0]
-        add_idx = np.stack([fill_rows, np.zeros_like(fill_rows)], 1)
-        add_val = np.full(fill_rows.shape[0], default_id or 0, np.int64)
-        all_idx = np.concatenate([indices, add_idx])
-        order = np.lexsort((all_idx[:, 1], all_idx[:, 0]))  # stable row-major
-        indices = all_idx[order]
-        values = np.concatenate([values, add_val])[order]
-        if w is not None:
-            w = np.concatenate([w, np.ones(fill_rows.shape[0], np.float32)])[order]
+    indices, values, empty, rev = sparse_fill_empty_rows(indices, values, B, default_id or 0)
+    if w is not None:
+        w = _fill_like(rev, w, indices.shape[0], np.float32(1.0))   # fill weights with 1.0
     return indices, values, w, empty
+
+
+def sparse_fill_empty_rows(indices, values, dense_rows, default_value):
+    """SparseFillEmptyRows (core/kernels/sparse_fill_empty_rows_op_util.h:
+    17-128), serial: entry i goes to scratch[row-1] + filled_count[row]++
+    (rows ascending, input order inside a row); an empty row gets one entry
+    [row, 0, ...] = default_value.  Returns (indices, values,
+    empty_row_indicator, reverse_index_map)."""
+    indices = np.asarray(indices, np.int64)
+    rank = indices.shape[1] if indices.ndim == 2 else 2
+    indices = indices.reshape(-1, rank)
+    values = np.asarray(values)
+    n = indices.shape[0]
+    scratch = np.zeros(dense_rows, np.int64)
+    for i in range(n):
+        r = int(indices[i, 0])
+        if not 0 <= r < dense_rows:
+            raise OracleError("indices(%d, 0) is invalid: %d >= %d" % (i, r, dense_rows))
+        scratch[r] += 1
+    empty = scratch == 0
+    scratch = np.cumsum(np.maximum(scratch, 1))
+    n_full = int(scratch[-1]) if dense_rows else 0
+    out_i = np.zeros((n_full, rank), np.int64)
+    out_v = np.full(n_full, default_value, values.dtype if n else np.asarray(default_value).dtype)
+    filled = np.zeros(dense_rows, np.int64)
+    rev = np.zeros(n, np.int64)
+    for i in range(n):
+        r = int(indices[i, 0])
+        o = (0 if r == 0 else scratch[r - 1]) + filled[r]
+        filled[r] += 1
+        out_i[o] = indices[i]
+        out_v[o] = values[i]
+        rev[i] = o
+    for r in range(dense_rows):
+        if filled[r] == 0:
+            out_i[0 if r == 0 else scratch[r - 1], 0] = r
+    return out_i, out_v, empty, rev
+
+
+def _fill_like(rev, vals, n_full, default):
+    out = np.full(n_full, default, np.asarray(vals).dtype)
+    out[rev] = vals
+    return out
 
 
 def embedding_lookup_sparse(params, indices, values, batch, weights=None, combiner="mean",

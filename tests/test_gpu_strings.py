@@ -94,6 +94,6 @@ def test_bad_offsets_latch_invalid_argument():
     from deeprec_amd import string_ops as so
     data = torch.zeros(8, dtype=torch.uint8, device="cuda")
     offs = torch.as_tensor([0, 5, 2], dtype=torch.int64, device="cuda")
-    so.fingerprint64(so.StringTensor(data, offs))
-    with pytest.raises(dr.InvalidArgumentError):
+    with pytest.raises(dr.InvalidArgumentError):   # at the op (validate mode) or the check
+        so.fingerprint64(so.StringTensor(data, offs))
         dr.status_check()
