@@ -211,6 +211,53 @@ __global__ __launch_bounds__(256) void dot_tile_kernel(const float* __restrict__
 }
 
 // ---------------------------------------------------------------------------
+// Dot interaction backward: dX[b,i,:] = sum_{j != i} S[i,j] X[b,j,:] with S
+// the symmetric completion of the pair grads (S[i,j] = S[j,i] = g[b, p(i,j)],
+// p(i,j) = i(i-1)/2 + j for i > j) -- the autodiff of DLRM's dot_op
+// (modelzoo/DLRM/train.py:150-163: matmul(X, X^T) then the strictly-lower
+// boolean mask).  A half-wave owns one sample, a lane one float4 column:
+// the column of X stays in registers (F float4), the sample's pair grads sit
+// in LDS and are read as broadcasts.  HBM bound: X read + dX written once.
+// ---------------------------------------------------------------------------
+template <int FM>
+__global__ __launch_bounds__(256) void dot_grad_kernel(const float* __restrict__ x,
+                                                       const float* __restrict__ g, int64_t B,
+                                                       int F, int D, float* __restrict__ dx) {
+  extern __shared__ float gs_all[];
+  const int P = F * (F - 1) / 2;
+  const int half = threadIdx.x >> 5, hl = threadIdx.x & 31;
+  float* gs = gs_all + half * P;
+  const int64_t b = (int64_t)blockIdx.x * 8 + half;
+  const bool live = b < B;
+  if (live)
+    for (int p = hl; p < P; p += 32) gs[p] = g[b * P + p];
+  __syncthreads();
+  if (!live) return;
+  const int D4 = D / 4;
+  const float4* xb = reinterpret_cast<const float4*>(x + b * (int64_t)F * D);
+  float4* ob = reinterpret_cast<float4*>(dx + b * (int64_t)F * D);
+  for (int c = hl; c < D4; c += 32) {
+    float4 xr[FM];
+#pragma unroll
+    for (int j = 0; j < FM; ++j) xr[j] = j < F ? nt_load(xb + j * D4 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < F; ++i) {
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        if (j < F && j != i) {
+          const float sij = i > j ? gs[i * (i - 1) / 2 + j] : gs[j * (j - 1) / 2 + i];
+          acc.x = fmaf(sij, xr[j].x, acc.x);
+          acc.y = fmaf(sij, xr[j].y, acc.y);
+          acc.z = fmaf(sij, xr[j].z, acc.z);
+          acc.w = fmaf(sij, xr[j].w, acc.w);
+        }
+      }
+      nt_store(acc, ob + i * D4 + c);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // CrossNet layer: out[b,o] = x0[b,o] * (sum_k xl[b,k] W[o,k] + bias[o]) + xl[b,o]
 // bf16 operands, fp32 accumulate, v_mfma_f32_16x16x32_bf16.
 // Block tile 128 (rows of the batch) x 128 (output features), 4 waves as
@@ -362,6 +409,26 @@ int dr_dot_interaction(const float* x, int64_t batch, int fields, int dim, float
   }
   hipLaunchKernelGGL(dot_kernel, dim3((unsigned)batch), dim3(256), lds, S(stream), x, fields, dim,
                      out);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_dot_interaction_grad(const float* x, const float* top_grad, int64_t batch, int fields,
+                            int dim, float* grad_x, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && fields > 1 && fields <= 32 && dim > 0 && dim % 4 == 0,
+             DR_INVALID_ARGUMENT, "dr_dot_interaction_grad: need 2 <= fields <= 32, dim %% 4 == 0");
+  DR_REQUIRE((((uintptr_t)x) | ((uintptr_t)grad_x)) % 16 == 0, DR_INVALID_ARGUMENT,
+             "x / grad_x must be 16-B aligned");
+  if (batch == 0) return DR_OK;
+  const size_t lds = (size_t)8 * fields * (fields - 1) / 2 * sizeof(float);
+  const unsigned grid = (unsigned)ceil_div(batch, 8);
+  if (fields <= 16)
+    hipLaunchKernelGGL(dot_grad_kernel<16>, dim3(grid), dim3(256), lds, S(stream), x, top_grad,
+                       batch, fields, dim, grad_x);
+  else
+    hipLaunchKernelGGL(dot_grad_kernel<32>, dim3(grid), dim3(256), lds, S(stream), x, top_grad,
+                       batch, fields, dim, grad_x);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

@@ -154,6 +154,7 @@ SIGNATURES = {
     "dr_fm2": (_I32, [_P, _I64, _I32, _I32, _P, _P]),
     "dr_fm2_grad": (_I32, [_P, _P, _I64, _I32, _I32, _P, _P]),
     "dr_dot_interaction": (_I32, [_P, _I64, _I32, _I32, _P, _P]),
+    "dr_dot_interaction_grad": (_I32, [_P, _P, _I64, _I32, _I32, _P, _P]),
     "dr_crossnet_layer_bf16": (_I32, [_P, _P, _P, _P, _I64, _I32, _P, _P]),
     "dr_fingerprint64": (_I32, [_P, _P, _I64, _P, _P]),
     "dr_string_to_hash_bucket_fast": (_I32, [_P, _P, _I64, _I64, _P, _P]),

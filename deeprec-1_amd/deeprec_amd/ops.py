@@ -332,6 +332,18 @@ def dot_interaction(x):
     return out
 
 
+def dot_interaction_grad(x, top_grad):
+    """Backward of dot_interaction: [B, F, D] grad of X."""
+    dev = _dev(x)
+    x = _c(x, torch.float32)
+    g = _c(top_grad, torch.float32)
+    B, F, D = x.shape
+    out = torch.empty_like(x)
+    check(lib().dr_dot_interaction_grad(ptr(x), ptr(g), B, F, D, ptr(out), stream_handle(dev)))
+    _post(dev)
+    return out
+
+
 def crossnet_layer(x0, xl, weight, bias=None):
     """DCN-v2 cross layer x0 * (xl W^T + b) + xl, bf16 MFMA, fp32 accumulate.
 

@@ -445,6 +445,10 @@ int dr_fm2_grad(const float* emb, const float* top_grad, int64_t batch, int fiel
 /* DLRM dot (modelzoo/DLRM/train.py:150-163): X [B,F,D] -> [B, F(F-1)/2].   */
 int dr_dot_interaction(const float* x, int64_t batch, int fields, int dim, float* out,
                        void* stream);
+/* Its backward: grad_x [B,F,D] = S X with S the symmetric completion of    */
+/* top_grad [B, F(F-1)/2] (autodiff of the reference's matmul + mask).       */
+int dr_dot_interaction_grad(const float* x, const float* top_grad, int64_t batch, int fields,
+                            int dim, float* grad_x, void* stream);
 /* DCN-v2 cross layer (absent in the reference): out = x0 * (xl W^T + b) + xl */
 /* x0/xl/out [B,d] bf16 (uint16 storage), W [d,d] bf16 row-major (out,in),   */
 /* b [d] f32; bf16 MFMA with fp32 accumulation.                              */
