@@ -216,21 +216,29 @@ __global__ __launch_bounds__(256) void dot_tile_kernel(const float* __restrict__
 // p(i,j) = i(i-1)/2 + j for i > j) -- the autodiff of DLRM's dot_op
 // (modelzoo/DLRM/train.py:150-163: matmul(X, X^T) then the strictly-lower
 // boolean mask).  A half-wave owns one sample, a lane one float4 column:
-// the column of X stays in registers (F float4), the sample's pair grads sit
-// in LDS and are read as broadcasts.  HBM bound: X read + dX written once.
+// the column of X stays in registers (F float4), the sample's S sits in LDS
+// and is read as 16-B broadcasts.  HBM bound: X read + dX written once.
 // ---------------------------------------------------------------------------
 template <int FM>
 __global__ __launch_bounds__(256) void dot_grad_kernel(const float* __restrict__ x,
                                                        const float* __restrict__ g, int64_t B,
                                                        int F, int D, float* __restrict__ dx) {
-  extern __shared__ float gs_all[];
+  // S of the half-wave's sample, zero-padded to FM x FM (row i = the
+  // coefficients of dX[i]): no branches in the FMA loop, 16-B LDS reads.
+  __shared__ __attribute__((aligned(16))) float ss_all[8][FM * FM];
   const int P = F * (F - 1) / 2;
   const int half = threadIdx.x >> 5, hl = threadIdx.x & 31;
-  float* gs = gs_all + half * P;
+  float* ss = ss_all[half];
   const int64_t b = (int64_t)blockIdx.x * 8 + half;
   const bool live = b < B;
-  if (live)
-    for (int p = hl; p < P; p += 32) gs[p] = g[b * P + p];
+  const float* gb = g + b * (int64_t)P;
+  for (int e = hl; e < FM * FM; e += 32) {
+    const int i = e / FM, j = e - i * FM;
+    float v = 0.f;
+    if (live && i < F && j < F && i != j)
+      v = i > j ? gb[i * (i - 1) / 2 + j] : gb[j * (j - 1) / 2 + i];
+    ss[e] = v;
+  }
   __syncthreads();
   if (!live) return;
   const int D4 = D / 4;
@@ -239,17 +247,22 @@ __global__ __launch_bounds__(256) void dot_grad_kernel(const float* __restrict__
   for (int c = hl; c < D4; c += 32) {
     float4 xr[FM];
 #pragma unroll
-    for (int j = 0; j < FM; ++j) xr[j] = j < F ? nt_load(xb + j * D4 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j = 0; j < FM; ++j)
+      xr[j] = j < F ? nt_load(xb + j * D4 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     for (int i = 0; i < F; ++i) {
+      const float4* srow = reinterpret_cast<const float4*>(ss + i * FM);
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int j = 0; j < FM; ++j) {
-        if (j < F && j != i) {
-          const float sij = i > j ? gs[i * (i - 1) / 2 + j] : gs[j * (j - 1) / 2 + i];
-          acc.x = fmaf(sij, xr[j].x, acc.x);
-          acc.y = fmaf(sij, xr[j].y, acc.y);
-          acc.z = fmaf(sij, xr[j].z, acc.z);
-          acc.w = fmaf(sij, xr[j].w, acc.w);
+      for (int j4 = 0; j4 < FM / 4; ++j4) {
+        const float4 s4 = srow[j4];
+        const float sj[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 xv = xr[j4 * 4 + q];
+          acc.x = fmaf(sj[q], xv.x, acc.x);
+          acc.y = fmaf(sj[q], xv.y, acc.y);
+          acc.z = fmaf(sj[q], xv.z, acc.z);
+          acc.w = fmaf(sj[q], xv.w, acc.w);
         }
       }
       nt_store(acc, ob + i * D4 + c);
@@ -421,13 +434,15 @@ int dr_dot_interaction_grad(const float* x, const float* top_grad, int64_t batch
   DR_REQUIRE((((uintptr_t)x) | ((uintptr_t)grad_x)) % 16 == 0, DR_INVALID_ARGUMENT,
              "x / grad_x must be 16-B aligned");
   if (batch == 0) return DR_OK;
-  const size_t lds = (size_t)8 * fields * (fields - 1) / 2 * sizeof(float);
   const unsigned grid = (unsigned)ceil_div(batch, 8);
   if (fields <= 16)
-    hipLaunchKernelGGL(dot_grad_kernel<16>, dim3(grid), dim3(256), lds, S(stream), x, top_grad,
+    hipLaunchKernelGGL(dot_grad_kernel<16>, dim3(grid), dim3(256), 0, S(stream), x, top_grad,
+                       batch, fields, dim, grad_x);
+  else if (fields <= 28)
+    hipLaunchKernelGGL(dot_grad_kernel<28>, dim3(grid), dim3(256), 0, S(stream), x, top_grad,
                        batch, fields, dim, grad_x);
   else
-    hipLaunchKernelGGL(dot_grad_kernel<32>, dim3(grid), dim3(256), lds, S(stream), x, top_grad,
+    hipLaunchKernelGGL(dot_grad_kernel<32>, dim3(grid), dim3(256), 0, S(stream), x, top_grad,
                        batch, fields, dim, grad_x);
   DR_LAUNCH_CHECK();
   return DR_OK;

@@ -212,30 +212,76 @@ class _LookupFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out):
         g = grad_out.contiguous()
-        total = g.shape[1]
-        cols, col = [], 0
-        for f in ctx.feats:
-            cols.append(col)
-            col += f.params.dim if not torch.is_tensor(f.params) else f.params.shape[1]
-        done = set()
-        for i, f in enumerate(ctx.feats):
-            holder = f.params
-            if torch.is_tensor(holder):
-                continue
-            grp = getattr(f, "group", None)
-            if grp is not None:
-                if id(grp) in done:
-                    continue
-                done.add(id(grp))
-                pos = {id(x): j for j, x in enumerate(ctx.feats)}
-                sls = grp.grads(g, [cols[pos[id(x)]] for x in grp.feats], total)
-                for x, sl in zip(grp.feats, sls):
-                    x.params.pending_grads.append(sl)
-                continue
-            D = holder.dim if not torch.is_tensor(holder) else holder.shape[1]
-            sl = _grad_to_slices(f, g[:, cols[i]:cols[i] + D].contiguous(), D)
-            holder.pending_grads.append(sl)
+        _queue_grads(ctx.feats, g, 0, g.shape[1])
         return None, None, None
+
+
+def _queue_grads(feats, g, col0, total):
+    """Per-feature IndexedSlices from the pooled grad g (rows of `total`
+    floats, feature columns starting at col0), queued on the variables."""
+    cols, col = [], col0
+    for f in feats:
+        cols.append(col)
+        col += f.params.dim if not torch.is_tensor(f.params) else f.params.shape[1]
+    done = set()
+    for i, f in enumerate(feats):
+        holder = f.params
+        if torch.is_tensor(holder):
+            continue
+        grp = getattr(f, "group", None)
+        if grp is not None:
+            if id(grp) in done:
+                continue
+            done.add(id(grp))
+            pos = {id(x): j for j, x in enumerate(feats)}
+            sls = grp.grads(g, [cols[pos[id(x)]] for x in grp.feats], total)
+            for x, sl in zip(grp.feats, sls):
+                x.params.pending_grads.append(sl)
+            continue
+        D = holder.dim
+        sl = _grad_to_slices(f, g[:, cols[i]:cols[i] + D].contiguous(), D)
+        holder.pending_grads.append(sl)
+
+
+class _StackFn(torch.autograd.Function):
+    """[x0 | e_1 | ... | e_T] as one [B, 1+T, D] tensor: the pooling writes
+    straight into the interaction input (no concat copy) and the backward
+    reads the embeddings' grads in place with the row stride."""
+
+    @staticmethod
+    def forward(ctx, x0, anchor, feats, order):
+        B, D = x0.shape
+        T = len(feats)
+        X = torch.empty((B, 1 + T, D), dtype=torch.float32, device=x0.device)
+        X[:, 0].copy_(x0)
+        _pool_all(feats, order, out=X.view(B, (1 + T) * D)[:, D:])
+        ctx.feats = feats
+        return X
+
+    @staticmethod
+    def backward(ctx, gX):
+        g = gX.contiguous()
+        B, F, D = g.shape
+        _queue_grads(ctx.feats, g.view(B, F * D), D, F * D)
+        return g[:, 0], None, None, None
+
+
+def embedding_stack(x0, params_list, sp_ids_list, combiner="sum"):
+    """torch.stack([x0] + [embedding_lookup_sparse(p, sp) ...], 1) for EVs of
+    dim x0.shape[1] (DLRM's interaction input, modelzoo/DLRM/train.py:214-219)."""
+    feats = []
+    for p, sp in zip(params_list, sp_ids_list):
+        v = sp.values.to(torch.int64).contiguous()
+        feats.append(_Feature(p, v, _seg_of(sp), sp.dense_shape[0], None, combiner, None,
+                              onehot=_is_onehot(sp, v.numel())))
+    need_grad = torch.is_grad_enabled()
+    if _groupable(feats):
+        _prepare_group(feats, need_grad)
+    else:
+        for f in feats:
+            _prepare(f, need_unique=False)
+    anchor = [_anchor(f.params) for f in feats if not torch.is_tensor(f.params)][0]
+    return _StackFn.apply(x0, anchor, feats, ORDER_ALI)
 
 
 def _groupable(feats):
@@ -408,12 +454,16 @@ def _run(feats, order=ORDER_ALI, need_grad=None):
     return _pool_all(feats, order)
 
 
-def _pool_all(feats, order):
+def _pool_all(feats, order, out=None):
     dev = feats[0].values.device
     B = feats[0].batch
     dims = [f.params.dim if not torch.is_tensor(f.params) else f.params.shape[1] for f in feats]
     total = sum(dims)
-    out = torch.empty((B, total), dtype=torch.float32, device=dev)
+    if out is None:
+        out = torch.empty((B, total), dtype=torch.float32, device=dev)
+    elif out.shape[0] != B or out.stride(1) != 1 or out.shape[1] < total:
+        raise ValueError("out must be a [B, >= %d] view with unit column stride" % total)
+    stride = out.stride(0)
     # group consecutive features of equal dim into <= 32-table launches
     col = 0
     i = 0
@@ -427,7 +477,7 @@ def _pool_all(feats, order):
         descs = []
         c = col
         for f in feats[i:j]:
-            descs.append(_desc(f, out[:, c:], total))
+            descs.append(_desc(f, out[:, c:], stride))
             c += dims[i]
         ops.pool_grouped(descs, B, dims[i], order, dev, onehot=onehot)
         col = c

@@ -22,7 +22,7 @@ Inputs are one-hot ids ([T, B] int64, Criteo hotness 1) and dense features
 import torch
 
 from . import ops
-from .embedding_ops import SparseTensor, embedding_lookup_sparse_multi
+from .embedding_ops import SparseTensor, embedding_lookup_sparse_multi, embedding_stack
 
 
 class DotInteraction(torch.autograd.Function):
@@ -64,28 +64,50 @@ def _mlp(sizes, last_act=True):
 
 class _OneHotLookup(object):
     """T one-hot features -> [B, T*D] through embedding_lookup_sparse_multi
-    (grouped Unique -> EV resolve -> fused pooling; grads queued on the EVs)."""
+    (grouped Unique -> EV resolve -> fused pooling; grads queued on the EVs),
+    or stacked behind a dense row into [B, 1+T, D] (stack())."""
 
     def __init__(self, evs):
         self.evs = evs
         self._ind = {}
 
-    def __call__(self, ids):
+    def _sps(self, ids):
         T, B = ids.shape
         key = (B, ids.device)
         if key not in self._ind:
             r = torch.arange(B, device=ids.device)
             self._ind[key] = torch.stack([r, torch.zeros_like(r)], 1)
         ind = self._ind[key]
-        sps = [SparseTensor(ind, ids[t], (B, 1)) for t in range(T)]
-        return embedding_lookup_sparse_multi(self.evs, sps, combiner="sum")
+        return [SparseTensor(ind, ids[t], (B, 1)) for t in range(T)]
+
+    def __call__(self, ids):
+        return embedding_lookup_sparse_multi(self.evs, self._sps(ids), combiner="sum")
+
+    def stack(self, x0, ids):
+        return embedding_stack(x0, self.evs, self._sps(ids), combiner="sum")
+
+
+class _MaybeBF16(object):
+    """The reference's bf16 switch: MLPs run in bf16 on fp32 master weights
+    (variable_scope(...).keep_weights(), DLRM train.py:183-195), outputs
+    cast back to fp32."""
+
+    def __init__(self, on):
+        self.on = on
+
+    def __call__(self, mlp, x):
+        if not self.on:
+            return mlp(x)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            return mlp(x).float()
 
 
 class DLRM(torch.nn.Module):
     """modelzoo/DLRM/train.py DLRM with interaction_op='dot'."""
 
-    def __init__(self, evs, num_dense=13, mlp_bot=(512, 256), mlp_top=(512, 256)):
+    def __init__(self, evs, num_dense=13, mlp_bot=(512, 256), mlp_top=(512, 256), bf16=False):
         super().__init__()
+        self.bf16 = _MaybeBF16(bf16)
         self.evs = list(evs)
         self.dim = self.evs[0].dim
         self.T = len(self.evs)
@@ -98,13 +120,11 @@ class DLRM(torch.nn.Module):
         self.lookup = _OneHotLookup(self.evs)
 
     def forward(self, dense, ids):
-        B = dense.shape[0]
-        x0 = self.bottom(dense)
-        emb = self.lookup(ids)                                     # [B, T*D]
-        X = torch.cat([x0.unsqueeze(1), emb.view(B, self.T, self.dim)], 1)
+        x0 = self.bf16(self.bottom, dense)
+        X = self.lookup.stack(x0, ids)                             # [B, 1+T, D], no concat copy
         z = DotInteraction.apply(X)
-        net = self.top(torch.cat([x0, z], 1))
-        return torch.sigmoid(self.last(net)).squeeze(1)
+        net = self.bf16(self.top, torch.cat([x0, z], 1))
+        return torch.sigmoid(self.bf16(self.last, net)).squeeze(1)
 
 
 class DeepFM(torch.nn.Module):

@@ -1,0 +1,80 @@
+"""Full training step of a modelzoo model on the bench's table shape (N = 1):
+DLRM (modelzoo/DLRM/train.py) or DeepFM (modelzoo/DeepFM/train.py) forward,
+BCE loss, backward, dense SGD, KV SGD / Adagrad on every EV.  Prints one JSON
+line with samples/s and the per-phase split.  A measurement aid for
+SURVEY 8f #4; bench.py's headline metric is the forward lookup.
+
+  python tools/model_step.py [--model dlrm|deepfm] [--rows 12500000] [--dim 128]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "deeprec-1_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="dlrm", choices=["dlrm", "deepfm"])
+    ap.add_argument("--tables", type=int, default=26)
+    ap.add_argument("--rows", type=int, default=12_500_000)
+    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--opt", default="sgd", choices=["sgd", "adagrad"])
+    ap.add_argument("--bf16", action="store_true", help="MLPs in bf16 (the reference's --bf16)")
+    args = ap.parse_args()
+    import deeprec_amd as dr
+    from deeprec_amd import modelzoo as mz
+    dr.load()
+    dev = torch.device("cuda", 0)
+    T, D, B, R = args.tables, args.dim, args.batch, args.rows
+    t0 = time.perf_counter()
+    evs = []
+    for t in range(T):
+        ev = dr.EmbeddingVariable("ms%d" % t, D, 0.0, capacity=R + (1 << 19), device=dev)
+        ev.insert_synthetic(0, R, seed=1000 + t)
+        evs.append(ev)
+    if args.model == "dlrm":
+        model = mz.DLRM(evs, 13, (512, 256), (512, 256), bf16=args.bf16).to(dev)
+    else:
+        wide = []
+        for t in range(T):
+            ev = dr.EmbeddingVariable("msw%d" % t, 1, 0.0, capacity=R + (1 << 19), device=dev)
+            ev.insert_synthetic(0, R, seed=5000 + t)
+            wide.append(ev)
+        model = mz.DeepFM(evs, wide).to(dev)
+    torch.cuda.synchronize()
+    print("[model_step] tables ready in %.1fs" % (time.perf_counter() - t0), file=sys.stderr,
+          flush=True)
+    dopt = torch.optim.SGD(model.parameters(), lr=0.01)
+    eopt = dr.GradientDescentOptimizer(0.01) if args.opt == "sgd" else dr.AdagradOptimizer(0.01)
+    g = torch.Generator(device=dev)
+    g.manual_seed(2021)
+    batches = [(torch.randn(B, 13, generator=g, device=dev),
+                torch.randint(0, R, (T, B), generator=g, device=dev),
+                (torch.rand(B, generator=g, device=dev) > 0.5).float()) for _ in range(4)]
+    for i in range(args.warmup):
+        mz.train_step(model, *batches[i % 4][:2], batches[i % 4][2], dopt, eopt, i)
+    torch.cuda.synchronize()
+    print("[model_step] warmup ok", file=sys.stderr, flush=True)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = mz.train_step(model, *batches[i % 4][:2], batches[i % 4][2], dopt, eopt, i)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    dr.status_check(dev)
+    print(json.dumps({"model": args.model, "samples_per_s": round(B * args.steps / el, 1),
+                      "lookups_per_s": round(T * B * args.steps / el, 1),
+                      "ms_per_step": round(el / args.steps * 1e3, 3), "batch": B, "tables": T,
+                      "rows": R, "dim": D, "opt": args.opt, "bf16_mlp": args.bf16, "loss": float(loss)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
