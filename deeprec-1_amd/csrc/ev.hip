@@ -1968,6 +1968,7 @@ int dr_ev_apply_adam(dr_ev* var, dr_ev* m, dr_ev* v, float beta1_power, float be
 //   resolve: insert-on-miss of every inbox key in EV (slot % T)
 //   init   : first-touch default rows (kernel boundary: before any read)
 //   emit   : row -> out[src][slot * dim] of the requester, over xGMI
+//            (1-D grid, destinations interleaved block by block)
 // ===========================================================================
 namespace dr {
 
@@ -2025,6 +2026,7 @@ struct XgmiRowArgs {
   int64_t cap;
   int64_t dim;
   int T;
+  int world;
 };
 
 // Wave-cooperative first-touch copy (steady state: one byte per key).
@@ -2067,13 +2069,20 @@ __global__ __launch_bounds__(256) void xgmi_emit_kernel(XgmiRowArgs a,
     sdflt[threadIdx.x] = a.dflt[threadIdx.x];
   }
   __syncthreads();
-  const int src = blockIdx.y;
+  // Destinations interleaved over consecutive blocks (src = block % world):
+  // the blocks resident at any moment write to every peer at once, so all
+  // xGMI links carry rows together.  A src-major grid would keep most of
+  // the chip writing to one peer (one link) at a time.
+  const int W = a.world;
+  const int src = (int)(blockIdx.x % (unsigned)W);
+  const int64_t bx = blockIdx.x / (unsigned)W;
+  const int64_t nbx = gridDim.x / (unsigned)W;
   const int64_t n = inbox_count(a.cnt, src);
   constexpr int GPB = 256 / G;
   const int lg = threadIdx.x % G;
   const int dv = (int)(a.dim / 4);
-  const int64_t grp = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
-  const int64_t ngrp = (int64_t)gridDim.x * GPB;
+  const int64_t grp = bx * GPB + threadIdx.x / G;
+  const int64_t ngrp = nbx * GPB;
   float* out = a.out[src];
   for (int64_t i0 = grp * NB; i0 < n; i0 += ngrp * NB) {
     xf4 x[NB];
@@ -2171,6 +2180,7 @@ int dr_xgmi_serve(const dr_xgmi_peers* peers, dr_ev* const* evs, int num_tables,
   wa.cap = peers->cap;
   wa.dim = dim;
   wa.T = num_tables;
+  wa.world = W;
   XgmiWs w = carve_xgmi(ws, W, peers->cap, nullptr);
   int* stw = status_word();
   DR_REQUIRE(stw, DR_INTERNAL, "status word unavailable");
@@ -2185,7 +2195,7 @@ int dr_xgmi_serve(const dr_xgmi_peers* peers, dr_ev* const* evs, int num_tables,
   hipLaunchKernelGGL(xgmi_resolve_kernel, dim3(gx, W), dim3(256), 0, st, ra, w.rows, w.init, stw);
   hipLaunchKernelGGL(xgmi_init_kernel, dim3(gx, W), dim3(256), 0, st, wa, w.rows, w.init);
   const int dv = (int)(dim / 4);
-  auto ge = [&](int G) { return dim3((unsigned)ceil_div(expect, (256 / G) * 4), W); };
+  auto ge = [&](int G) { return dim3((unsigned)(ceil_div(expect, (256 / G) * 4) * W)); };
   if (dv <= 8)
     hipLaunchKernelGGL((xgmi_emit_kernel<8, 4>), ge(8), dim3(256), 0, st, wa, w.rows);
   else if (dv <= 16)
