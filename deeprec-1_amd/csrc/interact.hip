@@ -5,6 +5,7 @@
 #include "dr_common.h"
 
 #include <algorithm>
+#include <stdlib.h>
 
 namespace dr {
 
@@ -360,6 +361,160 @@ __global__ __launch_bounds__(256) void crossnet_kernel(const uint16_t* __restric
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// CrossNet layer, pipelined (d % 64 == 0): same 128 x 128 tile and 2 x 2 waves
+// of 4 x 4 v_mfma_f32_16x16x32_bf16, K step 64, operands staged global -> LDS
+// by global_load_lds_dwordx4 (no VGPR round trip) into two LDS buffers, so the
+// DMA of K tile k+1 is in flight while tile k is multiplied.  One counted
+// s_waitcnt vmcnt + one raw s_barrier per K step (a __syncthreads() would
+// drain the prefetch with a vmcnt(0)), one s_barrier before a buffer is
+// restaged.  LDS image: [128 rows][8 chunks of 16 B], chunk c of row r stored
+// at c ^ ((r >> 1) & 7) (the swizzle is applied to the per-lane global source
+// address; the DMA destination is wave base + lane * 16), so the 16 lanes of
+// a fragment read hit 16 distinct 16-B bank slots.  Blocks are remapped so
+// that the 8 XCDs each own a contiguous range of tiles (row tile major): the
+// 27+ column tiles of one xl row panel share an XCD's L2.
+// Optionally writes lin = xl W^T + b (bf16) for the backward pass.
+// ---------------------------------------------------------------------------
+static constexpr int CG_BM = 128, CG_BN = 128, CG_BK = 64;
+static constexpr int CG_TILE_BYTES = CG_BM * CG_BK * 2;  // 16 KB per operand per buffer
+
+__device__ __forceinline__ void cg_stage(const uint16_t* __restrict__ X, int64_t rows_valid,
+                                         int64_t row0, int d, int k0, char* lds_tile, int wave,
+                                         int lane) {
+  // 16 wave instructions of 8 rows x 128 B cover the 128-row tile; 4 per wave
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r0 = (wave * 4 + i) * 8;
+    const int r = r0 + (lane >> 3);
+    const int pc = lane & 7;
+    const int lc = pc ^ ((r >> 1) & 7);
+    int64_t gr = row0 + r;
+    if (gr >= rows_valid) gr = rows_valid - 1;  // rows past the end feed discarded outputs
+    const uint16_t* src = X + gr * (int64_t)d + k0 + lc * 8;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(lds_tile + r0 * 128),
+                                     16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 cg_frag(const char* lds_tile, int r, int lc) {
+  return *reinterpret_cast<const bf16x8*>(lds_tile + r * 128 + ((lc ^ ((r >> 1) & 7)) << 4));
+}
+
+__global__ __launch_bounds__(256, 2) void crossnet_glds_kernel(
+    const uint16_t* __restrict__ x0, const uint16_t* __restrict__ xl,
+    const uint16_t* __restrict__ W, const float* __restrict__ bias, int64_t M, int d,
+    uint16_t* __restrict__ out, uint16_t* __restrict__ lin_out) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * 2 * CG_TILE_BYTES];  // [buf][A|B]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  // XCD-contiguous tile order (bijective for any grid size)
+  const int64_t nwg = (int64_t)gridDim.x;
+  const int64_t orig = blockIdx.x;
+  const int64_t xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t tile = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int ntn = d / CG_BN + (d % CG_BN ? 1 : 0);
+  const int64_t m0 = (tile / ntn) * CG_BM;
+  const int n0 = (int)(tile % ntn) * CG_BN;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = d / CG_BK;
+  cg_stage(xl, M, m0, d, 0, lds, wave, lane);
+  cg_stage(W, d, n0, d, 0, lds + CG_TILE_BYTES, wave, lane);
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = lds + (kt & 1) * 2 * CG_TILE_BYTES;
+    if (kt + 1 < nk) {
+      char* nxt = lds + ((kt + 1) & 1) * 2 * CG_TILE_BYTES;
+      cg_stage(xl, M, m0, d, (kt + 1) * CG_BK, nxt, wave, lane);
+      cg_stage(W, d, n0, d, (kt + 1) * CG_BK, nxt + CG_TILE_BYTES, wave, lane);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's tile-kt DMAs landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // ... and every other wave's
+    asm volatile("" ::: "memory");
+    const char* sA = cur;
+    const char* sB = cur + CG_TILE_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[4], fb[4];
+      const int lc = kk * 4 + fq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = cg_frag(sA, wm * 64 + i * 16 + fr, lc);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = cg_frag(sB, wn * 64 + j * 16 + fr, lc);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // buffer kt&1 is restaged by iteration kt+1's DMA
+    asm volatile("" ::: "memory");
+  }
+  // Epilogue through LDS (free after the loop's last barrier): each wave puts
+  // its 64 x 64 fp32 accumulator tile into its own 16 KB region (C/D map col =
+  // lane&15, row = (lane>>4)*4 + reg; columns XOR-swizzled by (row>>2)&3 x 16
+  // so the four row groups of one store hit different banks), then reads it
+  // back 8 columns per lane: x0 / xl / out / lin move as 16-B vectors, 8
+  // lanes per 128-B row segment.
+  float* ct = reinterpret_cast<float*>(lds) + wave * 64 * 64;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i * 16 + fq * 4 + r;
+        const int col = (j * 16 + fr) ^ (((row >> 2) & 3) << 4);
+        ct[row * 64 + col] = acc[i][j][r];
+      }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int idx = it * 64 + lane;
+    const int row = idx >> 3, cc = (idx & 7) * 8;
+    const int64_t grow = m0 + wm * 64 + row;
+    const int gcol = n0 + wn * 64 + cc;
+    if (grow >= M || gcol >= d) continue;
+    const int pc = cc ^ (((row >> 2) & 3) << 4);
+    const float4 l0 = *reinterpret_cast<const float4*>(ct + row * 64 + pc);
+    const float4 l1 = *reinterpret_cast<const float4*>(ct + row * 64 + pc + 4);
+    float lin[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+    if (bias) {
+      const float4 b0 = *reinterpret_cast<const float4*>(bias + gcol);
+      const float4 b1 = *reinterpret_cast<const float4*>(bias + gcol + 4);
+      lin[0] += b0.x; lin[1] += b0.y; lin[2] += b0.z; lin[3] += b0.w;
+      lin[4] += b1.x; lin[5] += b1.y; lin[6] += b1.z; lin[7] += b1.w;
+    }
+    const int64_t o = grow * d + gcol;
+    const u32x4 a0 = *reinterpret_cast<const u32x4*>(x0 + o);
+    const u32x4 al = *reinterpret_cast<const u32x4*>(xl + o);
+    u32x4 ov, lv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t p0 = a0[e], pl = al[e];
+      const float v0 = bf2f((uint16_t)(p0 & 0xffff)) * lin[2 * e] + bf2f((uint16_t)(pl & 0xffff));
+      const float v1 = bf2f((uint16_t)(p0 >> 16)) * lin[2 * e + 1] + bf2f((uint16_t)(pl >> 16));
+      ov[e] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+      lv[e] = (uint32_t)f2bf(lin[2 * e]) | ((uint32_t)f2bf(lin[2 * e + 1]) << 16);
+    }
+    *reinterpret_cast<u32x4*>(out + o) = ov;
+    if (lin_out) *reinterpret_cast<u32x4*>(lin_out + o) = lv;
+  }
+}
+
 }  // namespace dr
 
 extern "C" {
@@ -448,19 +603,38 @@ int dr_dot_interaction_grad(const float* x, const float* top_grad, int64_t batch
   return DR_OK;
 }
 
-int dr_crossnet_layer_bf16(const uint16_t* x0, const uint16_t* xl, const uint16_t* W,
-                           const float* bias, int64_t batch, int d, uint16_t* out, void* stream) {
+int dr_crossnet_forward_bf16(const uint16_t* x0, const uint16_t* xl, const uint16_t* W,
+                             const float* bias, int64_t batch, int d, uint16_t* out,
+                             uint16_t* lin_out, void* stream) {
   using namespace dr;
   DR_REQUIRE(batch >= 0 && d > 0 && d % 8 == 0, DR_INVALID_ARGUMENT,
              "dr_crossnet_layer_bf16: d must be a multiple of 8 (pad features)");
   DR_REQUIRE(((uintptr_t)x0 | (uintptr_t)xl | (uintptr_t)W) % 16 == 0, DR_INVALID_ARGUMENT,
              "operands must be 16B aligned");
   if (batch == 0) return DR_OK;
+  static const bool legacy = getenv("DR_CROSSNET_LEGACY") != nullptr;
+  const bool al16 = (((uintptr_t)bias | (uintptr_t)out | (uintptr_t)lin_out) & 15) == 0;
+  if (d % CG_BK == 0 && !legacy && al16) {
+    const int64_t tiles = ceil_div(batch, CG_BM) * ceil_div(d, CG_BN);
+    DR_REQUIRE(tiles < (1ll << 31), DR_INVALID_ARGUMENT, "batch too large");
+    hipLaunchKernelGGL(crossnet_glds_kernel, dim3((unsigned)tiles), dim3(256), 0, S(stream), x0,
+                       xl, W, bias, batch, d, out, lin_out);
+    DR_LAUNCH_CHECK();
+    return DR_OK;
+  }
+  DR_REQUIRE(!lin_out, DR_INVALID_ARGUMENT,
+             "lin_out needs d %% 64 == 0 and 16-B aligned bias / out / lin_out");
   dim3 grid((unsigned)ceil_div(d, CN_BN), (unsigned)ceil_div(batch, CN_BM));
   hipLaunchKernelGGL(crossnet_kernel, grid, dim3(256), 0, S(stream), x0, xl, W, bias, batch, d,
                      out);
   DR_LAUNCH_CHECK();
   return DR_OK;
+}
+
+int dr_crossnet_layer_bf16(const uint16_t* x0, const uint16_t* xl, const uint16_t* W,
+                           const float* bias, int64_t batch, int d, uint16_t* out,
+                           void* stream) {
+  return dr_crossnet_forward_bf16(x0, xl, W, bias, batch, d, out, nullptr, stream);
 }
 
 }  // extern "C"

@@ -797,16 +797,56 @@ __global__ void grad_keys_kernel(GradGroup g, int T, uint64_t* __restrict__ kin,
 }
 
 // Position-driven over the sorted (global unique row, nnz) pairs: a group
-// owns NB consecutive sorted positions.  A position that starts its row's
-// run sums the run (in ascending nnz order -- the sort is stable); others
-// are skipped.  The common one-element run costs two independent sequential
-// loads (key, nnz) and one row load, with no offsets table.
+// owns NB consecutive sorted positions.  Runs (all nnz of one unique row)
+// are cut into chunks of kGradChunk positions counted from the run's start;
+// a position that starts a chunk sums it in ascending nnz order (the sort is
+// stable), every other position is skipped.  A run that fits one chunk --
+// every run in practice, and every run of the parity tests -- is therefore
+// summed exactly in the serial order of the reference's CPU loops
+// (UnsortedSegmentSum / SparseSegmentReductionGrad).  A longer run (a
+// padding id repeated over a whole DIN history batch, a hot Zipf key) is
+// the ordered sum of its chunk partials, ((c_0 + c_1) + c_2) + ...: fixed
+// association, deterministic run to run, no atomics, and no single wave
+// walking a run of 10^5 positions.  The common one-element run costs two
+// independent sequential loads (key, nnz) and one row load.
+static constexpr int64_t kGradChunk = 256;
+
+// Scratch of the chunked pass: run_start = the segsum workspace's off[0, n)
+// (unused by the grouped path), long-run count = off[n + 1]; the long-run
+// list (2 int32 per run) and the chunk partials (dim <= kGradMaxDim floats per
+// chunk) follow the segsum workspace (dr_pool_grad_grouped_workspace_size).
+static constexpr int64_t kGradMaxDim = 1024;
+static size_t grad_chunk_ws_bytes(int64_t n) {
+  const int64_t chunks = n / kGradChunk + 2;
+  return (size_t)(2 * chunks * sizeof(int32_t) + 256 + chunks * kGradMaxDim * sizeof(float) + 256);
+}
+struct GradWs {
+  int32_t* run_start;
+  int32_t* nlong;
+  int32_t* longs;
+  float* part;
+};
+static constexpr int kGradChain = 8;  // positions of a chunk fetched per step
+
+// run_start[u] = first sorted position of row u; clears the long-run count.
+__global__ void grad_run_start_kernel(const uint64_t* __restrict__ skey, int64_t N,
+                                      int32_t* __restrict__ run_start, int32_t* __restrict__ nlong) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p == 0) *nlong = 0;
+  if (p >= N) return;
+  const uint64_t u = skey[p];
+  if (u < (uint64_t)N && (p == 0 || skey[p - 1] != u)) run_start[u] = (int32_t)p;
+}
+
 template <int VEC, int G, int CPL, int NB>
 __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64_t B,
                                                        const uint64_t* __restrict__ skey,
                                                        const int32_t* __restrict__ perm,
+                                                       const int32_t* __restrict__ run_start,
                                                        int dim, float* __restrict__ out,
-                                                       int* st) {
+                                                       float* __restrict__ part,
+                                                       int32_t* __restrict__ longs,
+                                                       int32_t* __restrict__ nlong, int* st) {
   __shared__ dr_pool_grad_desc sd[DR_MAX_GROUP];  // per-lane table index: stage in LDS
   if (threadIdx.x < T) sd[threadIdx.x] = g.d[threadIdx.x];
   __syncthreads();
@@ -821,7 +861,7 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
   using R = Row<VEC, G, CPL>;
   using V = typename VecT<VEC>::T;
   R x[NB];
-  int64_t uq[NB], rq[NB];
+  int64_t uq[NB], rq[NB], sq[NB];
   int tq[NB];
   bool head[NB], single[NB];
 #pragma unroll
@@ -830,13 +870,19 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
     head[q] = single[q] = false;
     uq[q] = -1;
     rq[q] = -1;
+    sq[q] = p;
     tq[q] = 0;
     const float* rp = nullptr;
     if (p < N) {
       const int64_t u = (int64_t)skey[p];
       const int64_t prev = p > 0 ? (int64_t)skey[p - 1] : -1;
       const int64_t next = p + 1 < N ? (int64_t)skey[p + 1] : -1;
-      if (u < N && u != prev) {  // u == N: sentinel for out-of-range idx
+      bool chunk_head = u != prev;
+      if (u < N && !chunk_head) {
+        sq[q] = run_start[u];
+        chunk_head = (p - sq[q]) % kGradChunk == 0;
+      }
+      if (u < N && chunk_head) {  // u == N: sentinel for out-of-range idx
         const int t = table_of(g.koff, T, u, ufirst < N ? ufirst : 0);
         const dr_pool_grad_desc& d = sd[t];
         head[q] = true;
@@ -860,57 +906,137 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
     if (!head[q]) continue;
     const dr_pool_grad_desc& d = sd[tq[q]];
     const int mode = d.combiner == DR_COMBINER_SUM ? 0 : (d.combiner == DR_COMBINER_MEAN ? 1 : 2);
+    const int64_t u = uq[q];
+    const int64_t c0 = p0 + q;          // chunk's first position
+    const bool first_chunk = c0 == sq[q];
+    auto scaled = [&](R& y, int64_t r) {
+      if (mode == 0) return;
+      const int32_t cnt = (r >= 0 && d.bag_off) ? d.bag_off[r + 1] - d.bag_off[r] : 1;
+      if (cnt != 1) {
+        const float sc = mode == 2 ? (float)(1.0 / sqrt((double)cnt)) : (float)(1.0 / (double)cnt);
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) y.v[c] = vmul(y.v[c], sc);
+      }
+    };
     R acc;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<V>();
-    int64_t p = p0 + q;
-    for (bool first = true;; first = false) {
-      R y;
-      int64_t r;
-      if (first) {
-        y = x[q];
-        r = rq[q];
-      } else {
-        if (p >= N || (int64_t)skey[p] != uq[q]) break;
-        const int64_t k = (int64_t)perm[p] - g.koff[tq[q]];
-        r = d.seg ? d.seg[k * d.seg_stride] : k;
-        const float* rp = nullptr;
-        if (r >= 0 && r < B)
-          rp = d.top_grad + r * d.top_stride;
-        else
-          latch(st, DR_INVALID_ARGUMENT);
-        load_row<VEC, G, CPL>(y, rp, lg, dv);
-        if (!rp) r = -1;
-      }
-      if (mode == 0) {
-        acc_add(acc, y);  // UnsortedSegmentSum order: 0 + x_0 + x_1 ...
-      } else {
-        const int32_t cnt = (r >= 0 && d.bag_off) ? d.bag_off[r + 1] - d.bag_off[r] : 1;
-        if (cnt != 1) {
-          const float sc =
-              mode == 2 ? (float)(1.0 / sqrt((double)cnt)) : (float)(1.0 / (double)cnt);
+    // UnsortedSegmentSum order 0 + x_0 + x_1 ... (sum); x_0 * s + ... (mean/sqrtn);
+    // a later chunk's partial starts at its first element
+    bool fresh = !(first_chunk && mode == 0);
+    if (single[q]) {
+      scaled(x[q], rq[q]);
+      if (fresh)
+        acc = x[q];
+      else
+        acc_add(acc, x[q]);
+    } else {
+      const int64_t lim = c0 + kGradChunk < N ? c0 + kGradChunk : N;
+      for (int64_t p = c0; p < lim; p += kGradChain) {
+        R y[kGradChain];
+        int64_t ry[kGradChain];
+        bool ok[kGradChain];
 #pragma unroll
-          for (int c = 0; c < CPL; ++c) y.v[c] = vmul(y.v[c], sc);
+        for (int j = 0; j < kGradChain; ++j) {  // all key loads issued before any use
+          const int64_t kj = p + j < lim ? (int64_t)skey[p + j] : -1;
+          ok[j] = kj == u;  // monotone: sorted keys
         }
-        if (first)
-          acc = y;
-        else
-          acc_add(acc, y);
+#pragma unroll
+        for (int j = 0; j < kGradChain; ++j) {
+          const float* rp = nullptr;
+          ry[j] = -1;
+          if (ok[j]) {
+            const int64_t k = (int64_t)perm[p + j] - g.koff[tq[q]];
+            const int64_t r = d.seg ? d.seg[k * d.seg_stride] : k;
+            if (r >= 0 && r < B) {
+              rp = d.top_grad + r * d.top_stride;
+              ry[j] = r;
+            } else {
+              latch(st, DR_INVALID_ARGUMENT);
+            }
+          }
+          load_row<VEC, G, CPL>(y[j], rp, lg, dv);
+        }
+#pragma unroll
+        for (int j = 0; j < kGradChain; ++j) {
+          if (!ok[j]) break;
+          scaled(y[j], ry[j]);
+          if (fresh) {
+            acc = y[j];
+            fresh = false;
+          } else {
+            acc_add(acc, y[j]);
+          }
+        }
+        if (!ok[kGradChain - 1]) break;
       }
-      ++p;
-      if (single[q]) break;
     }
-    store_row<VEC, G, CPL>(acc, out + uq[q] * (int64_t)dim, lg, dv);
+    if (first_chunk) {
+      store_row<VEC, G, CPL>(acc, out + u * (int64_t)dim, lg, dv);
+      // a run longer than one chunk: queue it for grad_finish_kernel
+      if (lg == 0 && c0 + kGradChunk < N && (int64_t)skey[c0 + kGradChunk] == u) {
+        const int32_t at = atomicAdd(nlong, 1);
+        longs[2 * at] = (int32_t)u;
+        longs[2 * at + 1] = (int32_t)c0;
+      }
+    } else {
+      store_row<VEC, G, CPL>(acc, part + (c0 / kGradChunk) * (int64_t)dim, lg, dv);
+    }
+  }
+}
+
+// out[u] = ((c_0 + c_1) + c_2) + ... for the queued long runs: c_0 is already
+// in out[u]; c_k sits in part[start / chunk + k] (consecutive slots).
+template <int VEC, int G, int CPL>
+__global__ __launch_bounds__(256) void grad_finish_kernel(const uint64_t* __restrict__ skey,
+                                                          int64_t N, int dim,
+                                                          float* __restrict__ out,
+                                                          const float* __restrict__ part,
+                                                          const int32_t* __restrict__ longs,
+                                                          const int32_t* __restrict__ nlong) {
+  constexpr int GPB = 256 / G;
+  const int n = *nlong;
+  const int lg = threadIdx.x % G;
+  const int dv = dim / VEC;
+  using R = Row<VEC, G, CPL>;
+  for (int64_t i = (int64_t)blockIdx.x * GPB + threadIdx.x / G; i < n;
+       i += (int64_t)gridDim.x * GPB) {
+    const int64_t u = longs[2 * i], c0 = longs[2 * i + 1];
+    R acc;
+    load_row<VEC, G, CPL>(acc, out + u * (int64_t)dim, lg, dv);
+    for (int64_t c = c0 + kGradChunk; c < N; c += kGradChain * kGradChunk) {
+      R y[kGradChain];
+      bool ok[kGradChain];
+#pragma unroll
+      for (int j = 0; j < kGradChain; ++j) {
+        const int64_t cj = c + j * kGradChunk;
+        ok[j] = cj < N && (int64_t)skey[cj] == u;
+        load_row<VEC, G, CPL>(y[j], ok[j] ? part + (cj / kGradChunk) * (int64_t)dim : nullptr,
+                              lg, dv);
+      }
+#pragma unroll
+      for (int j = 0; j < kGradChain; ++j)
+        if (ok[j]) acc_add(acc, y[j]);
+      if (!ok[kGradChain - 1]) break;
+    }
+    store_row<VEC, G, CPL>(acc, out + u * (int64_t)dim, lg, dv);
   }
 }
 
 template <int VEC, int G, int CPL>
 static void launch_grad_csr(const GradGroup& g, int T, int64_t B, const uint64_t* skey,
-                            const int32_t* perm, int dim, float* out, hipStream_t s, int* st) {
+                            const int32_t* perm, int dim, float* out, const GradWs& w,
+                            hipStream_t s, int* st) {
   constexpr int NB = 4;
-  const int64_t blocks = ceil_div(ceil_div(g.koff[T] > 0 ? g.koff[T] : 1, NB), 256 / G);
+  const int64_t N = g.koff[T];
+  hipLaunchKernelGGL(grad_run_start_kernel, dim3((unsigned)ceil_div(N > 0 ? N : 1, 256)),
+                     dim3(256), 0, s, skey, N, w.run_start, w.nlong);
+  const int64_t blocks = ceil_div(ceil_div(N > 0 ? N : 1, NB), 256 / G);
   hipLaunchKernelGGL((grad_seg_kernel<VEC, G, CPL, NB>), dim3((unsigned)blocks), dim3(256), 0, s,
-                     g, T, B, skey, perm, dim, out, st);
+                     g, T, B, skey, perm, w.run_start, dim, out, w.part, w.longs, w.nlong, st);
+  if (N > kGradChunk)
+    hipLaunchKernelGGL((grad_finish_kernel<VEC, G, CPL>), dim3(64), dim3(256), 0, s, skey, N, dim,
+                       out, w.part, w.longs, w.nlong);
 }
 
 }  // namespace dr
@@ -1100,7 +1226,8 @@ size_t dr_pool_grad_workspace_size(int64_t n) {
 }
 
 size_t dr_pool_grad_grouped_workspace_size(int64_t total_nnz) {
-  return dr_pool_grad_workspace_size(total_nnz);
+  return ((dr_pool_grad_workspace_size(total_nnz) + 255) & ~size_t(255)) +
+         dr::grad_chunk_ws_bytes(total_nnz);
 }
 
 int dr_pool_grad_grouped(const dr_pool_grad_desc* descs_host, int num_tables, int64_t batch,
@@ -1132,6 +1259,18 @@ int dr_pool_grad_grouped(const dr_pool_grad_desc* descs_host, int num_tables, in
   DR_REQUIRE(st, DR_INTERNAL, "status word unavailable");
   hipStream_t s = S(stream);
   SegSumWs w = carve_segsum(ws, n, n, nullptr);
+  GradWs gw;
+  gw.run_start = w.off;
+  gw.nlong = w.off + n + 1;
+  {
+    size_t seg_used = 0;
+    carve_segsum(nullptr, n, n, &seg_used);
+    Carver c(static_cast<char*>(ws) + ((seg_used + 255) & ~size_t(255)));
+    const int64_t chunks = n / kGradChunk + 2;
+    gw.longs = c.take<int32_t>(2 * chunks);
+    gw.part = c.take<float>(chunks * kGradMaxDim);
+  }
+  DR_REQUIRE(dim <= kGradMaxDim, DR_INVALID_ARGUMENT, "dim %d unsupported", dim);
   hipLaunchKernelGGL(grad_keys_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, g,
                      num_tables, w.kin, w.vin, st);
   DR_LAUNCH_CHECK();
@@ -1141,22 +1280,29 @@ int dr_pool_grad_grouped(const dr_pool_grad_desc* descs_host, int num_tables, in
   if (aligned) {
     const int d4 = dim / 4;
     if (d4 <= 8)
-      launch_grad_csr<4, 8, 1>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, s, st);
+      launch_grad_csr<4, 8, 1>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, gw, s,
+                                st);
     else if (d4 <= 16)
-      launch_grad_csr<4, 16, 1>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, s, st);
+      launch_grad_csr<4, 16, 1>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, gw, s,
+                                st);
     else if (d4 <= 32)
-      launch_grad_csr<4, 32, 1>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, s, st);
+      launch_grad_csr<4, 32, 1>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, gw, s,
+                                st);
     else if (d4 <= 64)
-      launch_grad_csr<4, 64, 1>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, s, st);
+      launch_grad_csr<4, 64, 1>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, gw, s,
+                                st);
     else if (d4 <= 256)
-      launch_grad_csr<4, 64, 4>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, s, st);
+      launch_grad_csr<4, 64, 4>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, gw, s,
+                                st);
     else
       DR_REQUIRE(false, DR_INVALID_ARGUMENT, "dim %d unsupported", dim);
   } else {
     if (dim <= 64)
-      launch_grad_csr<1, 64, 1>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, s, st);
+      launch_grad_csr<1, 64, 1>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, gw, s,
+                                st);
     else if (dim <= 256)
-      launch_grad_csr<1, 64, 4>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, s, st);
+      launch_grad_csr<1, 64, 4>(g, num_tables, batch, w.kout, w.perm, dim, grad_unique, gw, s,
+                                st);
     else
       DR_REQUIRE(false, DR_INVALID_ARGUMENT, "dim %d unsupported", dim);
   }

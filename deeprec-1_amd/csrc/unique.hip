@@ -80,30 +80,46 @@ __global__ void unique_insert_kernel(UniqGroup g, int T, const int64_t* __restri
   }
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= g.koff[T]) return;
+  if (i >= g.koff[T]) return;  // (exited lanes are the wave's tail: never a run head)
   const int t = group_table(g, T, i);
   const uint64_t k = (uint64_t)keys[i];
-  const int64_t cap = shcap[t];
-  uint64_t* tk = tkeys + shbase[t];
-  int64_t s;
-  if (k == kEmpty) {
-    s = cap;
-  } else {
-    const uint64_t mask = (uint64_t)cap - 1;
-    uint64_t h = mix64(k) & mask;
-    // The CAS result (performed at the memory side) is the only truth used to
-    // skip a slot, so a stale cached line can never make the probe run past
-    // every slot (the table holds at most half its capacity).
-    for (int64_t probes = 0; probes <= cap; ++probes) {
-      uint64_t old = atomicCAS((unsigned long long*)&tk[h], (unsigned long long)kEmpty,
-                               (unsigned long long)k);
-      if (old == kEmpty || old == k) break;
-      h = (h + 1) & mask;
+  // Runs of one key in consecutive positions of a wave (a padded history
+  // batch, a hot id) insert once: only the run's first lane -- the smallest
+  // position -- touches the slot; the rest take its slot by a shuffle.  The
+  // hot slot then sees one CAS + one atomicMin per wave, not per position.
+  const int lane = __lane_id();
+  const uint32_t klo = (uint32_t)k, khi = (uint32_t)(k >> 32);
+  const uint32_t plo = (uint32_t)__shfl_up((int)klo, 1, 64);
+  const uint32_t phi = (uint32_t)__shfl_up((int)khi, 1, 64);
+  const int pt = __shfl_up(t, 1, 64);
+  const bool head = lane == 0 || plo != klo || phi != khi || pt != t;
+  const uint64_t heads = __ballot(head);
+  int64_t s = 0;
+  if (head) {
+    const int64_t cap = shcap[t];
+    uint64_t* tk = tkeys + shbase[t];
+    if (k == kEmpty) {
+      s = cap;
+    } else {
+      const uint64_t mask = (uint64_t)cap - 1;
+      uint64_t h = mix64(k) & mask;
+      // The CAS result (performed at the memory side) is the only truth used
+      // to skip a slot, so a stale cached line can never make the probe run
+      // past every slot (the table holds at most half its capacity).
+      for (int64_t probes = 0; probes <= cap; ++probes) {
+        uint64_t old = atomicCAS((unsigned long long*)&tk[h], (unsigned long long)kEmpty,
+                                 (unsigned long long)k);
+        if (old == kEmpty || old == k) break;
+        h = (h + 1) & mask;
+      }
+      s = (int64_t)h;
     }
-    s = (int64_t)h;
+    s += shbase[t];
+    atomicMin(&minpos[s], (uint32_t)i);
   }
-  s += shbase[t];
-  atomicMin(&minpos[s], (uint32_t)i);
+  const uint64_t le = heads & (lanemask_lt() | (1ull << lane));
+  const int src = 63 - __clzll((long long)le);
+  s = (int64_t)(uint32_t)__shfl((int)(uint32_t)s, src, 64);
   slot_of[i] = (int32_t)s;
 }
 

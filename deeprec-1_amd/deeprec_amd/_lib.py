@@ -156,6 +156,11 @@ SIGNATURES = {
     "dr_dot_interaction": (_I32, [_P, _I64, _I32, _I32, _P, _P]),
     "dr_dot_interaction_grad": (_I32, [_P, _P, _I64, _I32, _I32, _P, _P]),
     "dr_crossnet_layer_bf16": (_I32, [_P, _P, _P, _P, _I64, _I32, _P, _P]),
+    "dr_crossnet_forward_bf16": (_I32, [_P, _P, _P, _P, _I64, _I32, _P, _P, _P]),
+    "dr_din_attention_input": (_I32, [_P, _P, _I64, _I64, _I32, _P, _P]),
+    "dr_din_attention_input_grad": (_I32, [_P, _P, _P, _I64, _I64, _I32, _P, _P, _I32, _P]),
+    "dr_din_attention_pool": (_I32, [_P, _P, _P, _I64, _I64, _I32, _P, _P, _P, _P]),
+    "dr_din_attention_pool_grad": (_I32, [_P, _P, _P, _P, _P, _I64, _I64, _I32, _P, _P, _P]),
     "dr_fingerprint64": (_I32, [_P, _P, _I64, _P, _P]),
     "dr_string_to_hash_bucket_fast": (_I32, [_P, _P, _I64, _I64, _P, _P]),
     "dr_crc32c_extend": (C.c_uint32, [C.c_uint32, _P, _SZ]),

@@ -152,6 +152,185 @@ class DeepFM(torch.nn.Module):
         return torch.sigmoid(self.last(net)).squeeze(1)
 
 
+class DinAttentionInput(torch.autograd.Function):
+    """dr_din_attention_input / _grad: [q, f, q - f, q * f]."""
+
+    @staticmethod
+    def forward(ctx, query, facts):
+        ctx.save_for_backward(query, facts)
+        return ops.din_attention_input(query, facts)
+
+    @staticmethod
+    def backward(ctx, g):
+        query, facts = ctx.saved_tensors
+        return ops.din_attention_input_grad(query, facts, g)
+
+
+class DinAttentionPool(torch.autograd.Function):
+    """dr_din_attention_pool / _grad: masked softmax + weighted sum of the
+    history, and the plain history sum, from one pass over the facts."""
+
+    @staticmethod
+    def forward(ctx, scores, mask, facts):
+        att, his_sum, alphas = ops.din_attention_pool(scores, mask, facts)
+        ctx.save_for_backward(alphas, mask, facts)
+        return att, his_sum
+
+    @staticmethod
+    def backward(ctx, g_att, g_sum):
+        alphas, mask, facts = ctx.saved_tensors
+        if g_att is None:
+            g_att = torch.zeros(facts.shape[0], facts.shape[2], device=facts.device)
+        gs, gf = ops.din_attention_pool_grad(alphas, mask, facts, g_att, g_sum)
+        return gs, None, gf
+
+
+class CrossLayer(torch.autograd.Function):
+    """DCN-v2 cross layer x_{l+1} = x0 * (x_l W^T + b) + x_l (BASELINE
+    configs[4]; absent from the reference).  Forward: the
+    fused bf16 MFMA kernel (dr_crossnet_forward_bf16), which also hands back
+    lin = x_l W^T + b for the backward.  Backward (library GEMMs, fp32
+    accumulate): u = g * x0, dW = u^T x_l, db = sum u, dx_l = u W + g,
+    dx0 = g * lin."""
+
+    @staticmethod
+    def forward(ctx, x0, xl, weight, bias):
+        wb = weight.to(torch.bfloat16)
+        out, lin = ops.crossnet_forward(x0, xl, wb, bias, with_lin=True)
+        ctx.save_for_backward(x0, xl, wb, lin)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x0, xl, wb, lin = ctx.saved_tensors
+        g = g.to(torch.bfloat16)
+        u = g * x0
+        dW = torch.matmul(u.t(), xl).float()
+        db = u.float().sum(0)
+        dxl = torch.addmm(g, u, wb)
+        dx0 = g * lin
+        return dx0, dxl, dW, db
+
+
+class DCNv2(torch.nn.Module):
+    """DCN-v2 (stacked): x0 = [dense | e_1 .. e_T] zero-padded to a multiple
+    of 64 features, bf16; L cross layers on the MFMA kernel; a bf16 deep MLP
+    over x_L; one logit, sigmoid, BCE (as DLRM / DeepFM here).  Cross weights
+    are fp32 master copies cast to bf16 per step (the reference's bf16 +
+    keep_weights convention, modelzoo/DLRM/train.py:183-195)."""
+
+    def __init__(self, evs, num_dense=13, layers=3, deep=(1024, 512)):
+        super().__init__()
+        self.evs = list(evs)
+        self.dim = self.evs[0].dim
+        self.T = len(self.evs)
+        self.num_dense = num_dense
+        self.d = num_dense + self.T * self.dim
+        self.dp = (self.d + 63) // 64 * 64
+        dp = self.dp
+        ws = []
+        for _ in range(layers):
+            w = torch.zeros(dp, dp)
+            w[:self.d, :self.d] = torch.randn(self.d, self.d) / self.d ** 0.5
+            ws.append(torch.nn.Parameter(w))
+        self.cross_w = torch.nn.ParameterList(ws)
+        self.cross_b = torch.nn.ParameterList([torch.nn.Parameter(torch.zeros(dp))
+                                               for _ in range(layers)])
+        self.deep = _mlp([dp] + list(deep))
+        self.last = torch.nn.Linear(deep[-1], 1)
+        self.lookup = _OneHotLookup(self.evs)
+
+    def forward(self, dense, ids):
+        B = dense.shape[0]
+        emb = self.lookup(ids)                                     # [B, T*D] fp32
+        pad = torch.zeros(B, self.dp - self.d, device=dense.device, dtype=dense.dtype)
+        x0 = torch.cat([dense, emb, pad], 1).to(torch.bfloat16)
+        x = x0
+        for w, b in zip(self.cross_w, self.cross_b):
+            x = CrossLayer.apply(x0, x, w, b)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            net = self.last(self.deep(x)).float()
+        return torch.sigmoid(net).squeeze(1)
+
+
+class Dice(torch.nn.Module):
+    """dice() of modelzoo/DIN/script/utils.py:12-35 (batch statistics)."""
+
+    def __init__(self, n, epsilon=1e-9):
+        super().__init__()
+        self.alpha = torch.nn.Parameter(torch.zeros(n))
+        self.epsilon = epsilon
+
+    def forward(self, x):
+        mean = x.mean(0, keepdim=True)
+        std = torch.sqrt(((x - mean) ** 2 + self.epsilon).mean(0, keepdim=True))
+        xp = torch.sigmoid((x - mean) / (std + self.epsilon))
+        return self.alpha * (1.0 - xp) * x + xp * x
+
+
+class DIN(torch.nn.Module):
+    """modelzoo/DIN/script/model.py Model_DIN (use_negsampling=False) on EVs.
+
+    Embedding layer (model.py:61-98): uid / mid / cat EVs of dim D; item_eb =
+    [mid, cat] of the target, item_his_eb = [mid, cat] of every history
+    position ([B, T, 2D], padding positions look up id 0 like the reference's
+    zero-padded id matrix).  Attention (model.py:381-386, utils.py:264-309):
+    din_all -> 80 sigmoid -> 40 sigmoid -> 1 -> masked softmax -> weighted
+    sum.  FCN (model.py:118-138): batch_normalization in inference form
+    (moving mean 0 / variance 1, epsilon 1e-3, trainable gamma / beta), 200
+    Dice, 80 Dice, 2, softmax + 1e-8."""
+
+    def __init__(self, uid_ev, mid_ev, cat_ev):
+        super().__init__()
+        self.uid_ev, self.mid_ev, self.cat_ev = uid_ev, mid_ev, cat_ev
+        self.evs = [uid_ev, mid_ev, cat_ev]
+        D = mid_ev.dim
+        H = 2 * D
+        self.f1_att = torch.nn.Linear(4 * H, 80)
+        self.f2_att = torch.nn.Linear(80, 40)
+        self.f3_att = torch.nn.Linear(40, 1)
+        n_in = uid_ev.dim + 4 * H
+        self.bn1_gamma = torch.nn.Parameter(torch.ones(n_in))
+        self.bn1_beta = torch.nn.Parameter(torch.zeros(n_in))
+        self.dnn1 = torch.nn.Linear(n_in, 200)
+        self.dice_1 = Dice(200)
+        self.dnn2 = torch.nn.Linear(200, 80)
+        self.dice_2 = Dice(80)
+        self.dnn3 = torch.nn.Linear(80, 2)
+        self.uid_lookup = _OneHotLookup([uid_ev])
+        self.item_lookup = _OneHotLookup([mid_ev, cat_ev])
+
+    def forward(self, uids, mids, cats, mid_his, cat_his, mask):
+        B, T = mid_his.shape
+        uid_e = self.uid_lookup(uids.reshape(1, B))
+        item_eb = self.item_lookup(torch.stack([mids, cats]))                    # [B, 2D]
+        his = torch.stack([mid_his.reshape(-1), cat_his.reshape(-1)])
+        facts = self.item_lookup(his).view(B, T, -1)                              # [B, T, 2D]
+        din_all = DinAttentionInput.apply(item_eb, facts)                         # [B, T, 4H]
+        h = torch.sigmoid(self.f1_att(din_all))
+        h = torch.sigmoid(self.f2_att(h))
+        scores = self.f3_att(h).view(B, T)
+        att, his_sum = DinAttentionPool.apply(scores, mask, facts)
+        inp = torch.cat([uid_e, item_eb, his_sum, item_eb * his_sum, att], -1)
+        bn = inp * (1.0 / (1.0 + 1e-3) ** 0.5) * self.bn1_gamma + self.bn1_beta
+        x = self.dice_1(self.dnn1(bn))
+        x = self.dice_2(self.dnn2(x))
+        return torch.softmax(self.dnn3(x), -1) + 1e-8
+
+
+def din_train_step(model, batch, dense_opt, ev_opt, global_step=None):
+    """One DIN step: ctr_loss = -mean(log(y_hat) * target) (model.py:137),
+    backward, dense optimizer, KV optimizer on the uid / mid / cat EVs."""
+    uids, mids, cats, mid_his, cat_his, mask, target = batch
+    y_hat = model(uids, mids, cats, mid_his, cat_his, mask)
+    loss = -(torch.log(y_hat) * target).mean()
+    dense_opt.zero_grad(set_to_none=True)
+    loss.backward()
+    dense_opt.step()
+    ev_opt.apply_gradients(model.evs, global_step=global_step)
+    return loss
+
+
 def train_step(model, dense, ids, labels, dense_opt, ev_opt, global_step=None):
     """One step: forward, BCE loss (tf.keras BinaryCrossentropy on the
     sigmoid output), backward, dense optimizer, KV optimizer on every EV."""

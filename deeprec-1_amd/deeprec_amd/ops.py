@@ -347,10 +347,11 @@ def dot_interaction_grad(x, top_grad):
 def crossnet_layer(x0, xl, weight, bias=None):
     """DCN-v2 cross layer x0 * (xl W^T + b) + xl, bf16 MFMA, fp32 accumulate.
 
-    Feature dims that are not a multiple of 8 are zero-padded (exact)."""
+    Feature dims that are not a multiple of 64 are zero-padded (exact); a
+    caller that keeps its features padded (modelzoo.DCNv2) pays no copy."""
     dev = _dev(x0)
     B, d = x0.shape
-    dp = (d + 7) // 8 * 8
+    dp = (d + 63) // 64 * 64
 
     def pad2(t, rows, cols):
         t = t.to(torch.bfloat16)
@@ -367,11 +368,92 @@ def crossnet_layer(x0, xl, weight, bias=None):
     if bias is not None:
         b = torch.zeros(dp, dtype=torch.float32, device=dev)
         b[:d] = bias.float()
-    out = torch.empty((B, dp), dtype=torch.bfloat16, device=dev)
-    check(lib().dr_crossnet_layer_bf16(ptr(a0), ptr(al), ptr(w), ptr(b), B, dp, ptr(out),
-                                       stream_handle(dev)))
-    _post(dev)
+    out, _ = crossnet_forward(a0, al, w, b, with_lin=False)
     return out[:, :d]
+
+
+def crossnet_forward(x0, xl, weight, bias, with_lin=True):
+    """dr_crossnet_forward_bf16 on padded operands: x0 / xl [B, d] bf16,
+    weight [d, d] bf16 (out, in), bias [d] fp32 or None, d % 64 == 0.
+    Returns (out [B, d] bf16, lin = xl W^T + b [B, d] bf16 or None)."""
+    dev = _dev(x0)
+    B, d = x0.shape
+    if d % 64 or x0.dtype != torch.bfloat16 or xl.dtype != torch.bfloat16 \
+            or weight.dtype != torch.bfloat16 or tuple(weight.shape) != (d, d):
+        raise ValueError("crossnet_forward needs bf16 operands with d % 64 == 0")
+    x0, xl, weight = x0.contiguous(), xl.contiguous(), weight.contiguous()
+    b = None if bias is None else bias.to(torch.float32).contiguous()
+    out = torch.empty((B, d), dtype=torch.bfloat16, device=dev)
+    lin = torch.empty((B, d), dtype=torch.bfloat16, device=dev) if with_lin else None
+    check(lib().dr_crossnet_forward_bf16(ptr(x0), ptr(xl), ptr(weight), ptr(b), B, d, ptr(out),
+                                         ptr(lin), stream_handle(dev)))
+    _post(dev)
+    return out, lin
+
+
+# ---------------------------------------------------------------------------
+# DIN attention (modelzoo/DIN/script/utils.py:264-309, script/model.py:94-98)
+# ---------------------------------------------------------------------------
+def din_attention_input(query, facts):
+    """din_all = concat([q, f, q - f, q * f], -1): query [B, H], facts
+    [B, T, H] -> [B, T, 4H] (utils.py:280-282)."""
+    dev = _dev(facts)
+    B, T, H = facts.shape
+    q, f = _c(query, torch.float32), _c(facts, torch.float32)
+    out = torch.empty((B, T, 4 * H), dtype=torch.float32, device=dev)
+    check(lib().dr_din_attention_input(ptr(q), ptr(f), B, T, H, ptr(out), stream_handle(dev)))
+    _post(dev)
+    return out
+
+
+def din_attention_input_grad(query, facts, top_grad, grad_facts=None):
+    """Backward of din_attention_input -> (grad_query [B, H], grad_facts
+    [B, T, H]); when grad_facts is given it is accumulated into in place."""
+    dev = _dev(facts)
+    B, T, H = facts.shape
+    q, f, g = _c(query, torch.float32), _c(facts, torch.float32), _c(top_grad, torch.float32)
+    gq = torch.empty((B, H), dtype=torch.float32, device=dev)
+    acc = grad_facts is not None
+    if not acc:
+        grad_facts = torch.empty((B, T, H), dtype=torch.float32, device=dev)
+    elif not grad_facts.is_contiguous() or grad_facts.dtype != torch.float32:
+        raise ValueError("grad_facts must be a contiguous fp32 tensor")
+    check(lib().dr_din_attention_input_grad(ptr(q), ptr(f), ptr(g), B, T, H, ptr(gq),
+                                            ptr(grad_facts), int(acc), stream_handle(dev)))
+    _post(dev)
+    return gq, grad_facts
+
+
+def din_attention_pool(scores, mask, facts, with_sum=True):
+    """Masked softmax over the history + weighted sum (din_attention, mode
+    'SUM', utils.py:286-303) and the history sum (model.py:98) in one pass.
+    scores / mask [B, T], facts [B, T, H] -> (att [B, H], his_sum [B, H] or
+    None, alphas [B, T])."""
+    dev = _dev(facts)
+    B, T, H = facts.shape
+    s, m, f = _c(scores, torch.float32), _c(mask, torch.float32), _c(facts, torch.float32)
+    att = torch.empty((B, H), dtype=torch.float32, device=dev)
+    hs = torch.empty((B, H), dtype=torch.float32, device=dev) if with_sum else None
+    al = torch.empty((B, T), dtype=torch.float32, device=dev)
+    check(lib().dr_din_attention_pool(ptr(s), ptr(m), ptr(f), B, T, H, ptr(att), ptr(hs), ptr(al),
+                                      stream_handle(dev)))
+    _post(dev)
+    return att, hs, al
+
+
+def din_attention_pool_grad(alphas, mask, facts, grad_att, grad_sum=None):
+    """-> (grad_scores [B, T], grad_facts [B, T, H])."""
+    dev = _dev(facts)
+    B, T, H = facts.shape
+    a, m, f = _c(alphas, torch.float32), _c(mask, torch.float32), _c(facts, torch.float32)
+    ga = _c(grad_att, torch.float32)
+    gs = None if grad_sum is None else _c(grad_sum, torch.float32)
+    gsc = torch.empty((B, T), dtype=torch.float32, device=dev)
+    gf = torch.empty((B, T, H), dtype=torch.float32, device=dev)
+    check(lib().dr_din_attention_pool_grad(ptr(a), ptr(m), ptr(f), ptr(ga), ptr(gs), B, T, H,
+                                           ptr(gsc), ptr(gf), stream_handle(dev)))
+    _post(dev)
+    return gsc, gf
 
 
 # ---------------------------------------------------------------------------

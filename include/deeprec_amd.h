@@ -455,6 +455,38 @@ int dr_dot_interaction_grad(const float* x, const float* top_grad, int64_t batch
 int dr_crossnet_layer_bf16(const uint16_t* x0, const uint16_t* xl, const uint16_t* W,
                            const float* bias, int64_t batch, int d, uint16_t* out,
                            void* stream);
+/* Same layer, also writing lin_out = xl W^T + b (bf16, nullable; needs      */
+/* d % 64 == 0) for the backward pass.  d % 64 == 0 selects the pipelined    */
+/* kernel (global_load_lds staging, double-buffered K steps of 64).          */
+int dr_crossnet_forward_bf16(const uint16_t* x0, const uint16_t* xl, const uint16_t* W,
+                             const float* bias, int64_t batch, int d, uint16_t* out,
+                             uint16_t* lin_out, void* stream);
+
+/* DIN user-behaviour attention (modelzoo/DIN/script/utils.py:264-309,      */
+/* din_attention mode 'SUM'; script/model.py:94-98,381-390).  query [B,H],  */
+/* facts [B,T,H] (the gathered history, H = 2 x EMBEDDING_DIM), fp32.        */
+/* hidden <= 64, or a multiple of 4 <= 256 with 16-B aligned operands.       */
+/* din_all [B,T,4H] = [q, f, q - f, q * f] (utils.py:280-282).              */
+int dr_din_attention_input(const float* query, const float* facts, int64_t batch, int64_t seq_len,
+                           int hidden, float* out, void* stream);
+/* Its backward: grad_query [B,H] = sum over t; grad_facts [B,T,H] is        */
+/* written (accumulate = 0) or added to (accumulate = 1).                     */
+int dr_din_attention_input_grad(const float* query, const float* facts, const float* top_grad,
+                                int64_t batch, int64_t seq_len, int hidden, float* grad_query,
+                                float* grad_facts, int accumulate, void* stream);
+/* scores [B,T] (attention-MLP output), mask [B,T] (1.0 = valid,             */
+/* tf.equal(mask, 1)): s = mask ? scores : float(-2^32+1); alphas = softmax  */
+/* over t; att_out [B,H] = sum_t alpha_t f_t; sum_out [B,H] (nullable) =     */
+/* sum_t f_t over every position (item_his_eb_sum, model.py:98).             */
+int dr_din_attention_pool(const float* scores, const float* mask, const float* facts,
+                          int64_t batch, int64_t seq_len, int hidden, float* att_out,
+                          float* sum_out, float* alphas, void* stream);
+/* Its backward: grad_scores [B,T] (0 where masked), grad_facts [B,T,H] =    */
+/* alpha_t grad_att + grad_sum (grad_sum nullable).                          */
+int dr_din_attention_pool_grad(const float* alphas, const float* mask, const float* facts,
+                               const float* grad_att, const float* grad_sum, int64_t batch,
+                               int64_t seq_len, int hidden, float* grad_scores,
+                               float* grad_facts, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* String -> id, the step before the lookup.  Strings are one byte buffer    */

@@ -1,0 +1,119 @@
+"""DCN-v2 cross layer (BASELINE configs[4]) on the bf16 MFMA kernel against a
+plain PyTorch fp32 reference of x0 * (xl W^T + b) + xl computed from the same
+bf16 operands, its backward against torch autograd, and one DCNv2 training
+step against an fp32 torch model with dense tables.
+
+Tolerances are bf16 ones, stated per assertion: the kernel rounds its
+outputs to bf16 (relative step 2^-8) after an fp32-accumulated K sum, so
+outputs are compared at 1/64 of the reference's max magnitude."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _ref(x0, xl, W, b):
+    lin = xl.float() @ W.float().t() + b
+    return x0.float() * lin + xl.float(), lin
+
+
+def _close(got, want, frac=1.0 / 64):
+    err = (got.float() - want.float()).abs().max().item()
+    assert err <= frac * want.float().abs().max().item() + 1e-2, err
+
+
+@pytest.mark.parametrize("B,d", [(300, 192), (129, 3392), (64, 64)])
+def test_crossnet_forward_matches_torch(B, d):
+    from deeprec_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(B + d)
+    x0 = torch.randn(B, d, generator=g).to(DEV, torch.bfloat16)
+    xl = torch.randn(B, d, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(d, d, generator=g) / d ** 0.5).to(DEV, torch.bfloat16)
+    b = torch.randn(d, generator=g).to(DEV)
+    out, lin = ops.crossnet_forward(x0, xl, W, b)
+    want, wlin = _ref(x0, xl, W, b)
+    _close(out, want)
+    _close(lin, wlin)
+    out2, none = ops.crossnet_forward(x0, xl, W, None, with_lin=False)
+    assert none is None
+    _close(out2, _ref(x0, xl, W, torch.zeros(d, device=DEV))[0])
+
+
+def test_crossnet_layer_unpadded_d_matches_torch():
+    from deeprec_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(3)
+    B, d = 70, 13 + 26 * 16                       # 429: zero-padded to 448 inside
+    x0 = torch.randn(B, d, generator=g).to(DEV, torch.bfloat16)
+    xl = torch.randn(B, d, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(d, d, generator=g) / d ** 0.5).to(DEV, torch.bfloat16)
+    b = torch.randn(d, generator=g).to(DEV)
+    _close(ops.crossnet_layer(x0, xl, W, b), _ref(x0, xl, W, b)[0])
+
+
+def test_cross_layer_backward_matches_autograd():
+    from deeprec_amd.modelzoo import CrossLayer
+    g = torch.Generator(device="cpu").manual_seed(9)
+    B, d = 256, 128
+    x0 = torch.randn(B, d, generator=g).to(DEV, torch.bfloat16)
+    xl = torch.randn(B, d, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(d, d, generator=g) / d ** 0.5).to(DEV)
+    b = torch.randn(d, generator=g).to(DEV)
+    G = torch.randn(B, d, generator=g).to(DEV, torch.bfloat16)
+    a0, al = x0.clone().requires_grad_(True), xl.clone().requires_grad_(True)
+    w, bb = W.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    CrossLayer.apply(a0, al, w, bb).backward(G)
+    r0, rl = x0.float().requires_grad_(True), xl.float().requires_grad_(True)
+    rw, rb = W.to(torch.bfloat16).float().requires_grad_(True), b.clone().requires_grad_(True)
+    (r0 * (rl @ rw.t() + rb) + rl).backward(G.float())
+    for got, want in ((a0.grad, r0.grad), (al.grad, rl.grad), (w.grad, rw.grad), (bb.grad, rb.grad)):
+        _close(got, want, frac=1.0 / 32)
+
+
+def test_dcn_train_step_matches_torch_reference():
+    import deeprec_amd as dr
+    from deeprec_amd import modelzoo as mz
+    torch.manual_seed(13)
+    T, R, D, B, lr = 4, 50, 16, 256, 0.05
+    gen = torch.Generator(device="cpu").manual_seed(6)
+    tables = [torch.randn(R, D, generator=gen) * 0.1 for _ in range(T)]
+    evs = []
+    for t, w in enumerate(tables):
+        ev = dr.EmbeddingVariable("dcn_%d" % t, D, 0.0, device=DEV)
+        ev.insert(torch.arange(R, device=DEV), w.to(DEV))
+        evs.append(ev)
+    model = mz.DCNv2(evs, 13, layers=2, deep=(64, 32)).to(DEV)
+    ids = torch.randint(0, R, (T, B), device=DEV)
+    dense = torch.randn(B, 13, device=DEV)
+    labels = (torch.rand(B, device=DEV) > 0.5).float()
+    P = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    # fp32 torch reference of the same model (bf16 rounding of x0 and of the
+    # cross weights as in the kernel path; everything else fp32)
+    W = [t.to(DEV).clone().requires_grad_(True) for t in tables]
+    emb = torch.cat([torch.nn.functional.embedding(ids[t], W[t]) for t in range(T)], 1)
+    x0 = torch.cat([dense, emb, torch.zeros(B, model.dp - model.d, device=DEV)], 1)
+    x = x0
+    for i in range(2):
+        wi = P["cross_w.%d" % i].to(torch.bfloat16).float()
+        x = x0 * (x @ wi.t() + P["cross_b.%d" % i]) + x
+    h = x
+    for i in range(2):
+        h = torch.relu(h @ P["deep.%d.weight" % (2 * i)].t() + P["deep.%d.bias" % (2 * i)])
+    pred = torch.sigmoid(h @ P["last.weight"].t() + P["last.bias"]).squeeze(1)
+    p = pred.clamp(1e-7, 1 - 1e-7)
+    ref_loss = -(labels * torch.log(p) + (1 - labels) * torch.log(1 - p)).mean()
+    ref_loss.backward()
+    before = [_rows(ev, R) for ev in evs]
+    dopt = torch.optim.SGD(model.parameters(), lr=lr)
+    loss = mz.train_step(model, dense, ids, labels, dopt, dr.GradientDescentOptimizer(lr))
+    assert abs(loss.item() - ref_loss.item()) <= 2e-2 * abs(ref_loss.item())   # bf16 path
+    for t in range(T):
+        got = (before[t] - _rows(evs[t], R)) / lr                 # the applied EV gradient
+        _close(got, W[t].grad, frac=1.0 / 16)
+
+
+def _rows(ev, R):
+    k, v = ev.export()[:2]
+    out = torch.zeros(R, ev.dim, device=DEV)
+    out[k] = v
+    return out

@@ -1,0 +1,171 @@
+"""DIN user-behaviour attention (seq.hip) against plain PyTorch references of
+modelzoo/DIN/script/utils.py:264-309 (din_attention, mode 'SUM') and
+script/model.py:94-98,381-392, and one DIN training step (modelzoo.DIN)
+against a torch fp32 model with dense tables.
+
+Tolerances: the kernels vs an fp64 torch reference at rtol/atol 1e-5 (fp32
+sums of <= 150 terms); the model step at fp32 rtol 1e-5 / atol 1e-6 like the
+other model tests (north_star's 1e-5 rel)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+PAD = -4294967296.0     # float32(-2**32 + 1), utils.py:291
+
+
+def _ref_din_input(q, f):
+    T = f.shape[1]
+    qq = q.unsqueeze(1).expand(-1, T, -1)
+    return torch.cat([qq, f, qq - f, qq * f], -1)
+
+
+def _ref_pool(scores, mask, f):
+    s = torch.where(mask == 1, scores, torch.full_like(scores, PAD))
+    a = torch.softmax(s, -1)
+    return torch.bmm(a.unsqueeze(1), f).squeeze(1), f.sum(1), a
+
+
+def _case(B, T, H, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    q = torch.randn(B, H, generator=g, dtype=torch.float64)
+    f = torch.randn(B, T, H, generator=g, dtype=torch.float64)
+    lens = torch.randint(0, T + 1, (B,), generator=g)
+    lens[0] = T
+    if B > 1:
+        lens[1] = 0                       # every position masked: uniform softmax
+    mask = (torch.arange(T)[None, :] < lens[:, None]).double()
+    scores = torch.randn(B, T, generator=g, dtype=torch.float64) * 3
+    return [x.to(DEV) for x in (q, f, mask, scores)]
+
+
+SHAPES = [(64, 100, 36), (33, 1, 36), (17, 150, 18), (9, 7, 5), (5, 65, 256), (3, 9, 64)]
+
+
+@pytest.mark.parametrize("B,T,H", SHAPES)
+def test_din_attention_input_fwd_bwd(B, T, H):
+    from deeprec_amd import ops
+    q, f, _, _ = _case(B, T, H, B + T + H)
+    got = ops.din_attention_input(q.float(), f.float())
+    want = _ref_din_input(q.float(), f.float())
+    assert torch.equal(got, want)                       # pure copies / one op each: exact
+    g = torch.randn(B, T, 4 * H, device=DEV, dtype=torch.float64)
+    qr, fr = q.clone().requires_grad_(True), f.clone().requires_grad_(True)
+    _ref_din_input(qr, fr).backward(g)
+    gq, gf = ops.din_attention_input_grad(q.float(), f.float(), g.float())
+    torch.testing.assert_close(gq.double(), qr.grad, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gf.double(), fr.grad, rtol=1e-5, atol=1e-5)
+    # accumulate into an existing gradient
+    base = torch.randn(B, T, H, device=DEV)
+    acc = base.clone()
+    ops.din_attention_input_grad(q.float(), f.float(), g.float(), grad_facts=acc)
+    torch.testing.assert_close(acc.double(), base.double() + fr.grad, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("B,T,H", SHAPES)
+def test_din_attention_pool_fwd_bwd(B, T, H):
+    from deeprec_amd import ops
+    q, f, mask, scores = _case(B, T, H, 7 * B + T + H)
+    att, hs, al = ops.din_attention_pool(scores.float(), mask.float(), f.float())
+    w_att, w_hs, w_al = _ref_pool(scores, mask, f)
+    torch.testing.assert_close(al.double(), w_al, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(att.double(), w_att, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(hs.double(), w_hs, rtol=1e-5, atol=1e-5)
+    if B > 1:   # fully masked row -> 1/T each (softmax of equal paddings)
+        torch.testing.assert_close(al[1], torch.full((T,), 1.0 / T, device=DEV))
+    ga = torch.randn(B, H, device=DEV, dtype=torch.float64)
+    gs = torch.randn(B, H, device=DEV, dtype=torch.float64)
+    sr, fr = scores.clone().requires_grad_(True), f.clone().requires_grad_(True)
+    a_, s_, _ = _ref_pool(sr, mask, fr)
+    (a_ * ga).sum().add_((s_ * gs).sum()).backward()
+    gsc, gf = ops.din_attention_pool_grad(al, mask.float(), f.float(), ga.float(), gs.float())
+    torch.testing.assert_close(gsc.double(), sr.grad, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gf.double(), fr.grad, rtol=1e-5, atol=1e-5)
+    assert torch.all(gsc[mask == 0] == 0)
+
+
+def test_din_attention_rejects_bad_shapes():
+    from deeprec_amd import ops
+    from deeprec_amd._lib import DeepRecError
+    f = torch.zeros(2, 3, 300, device=DEV)                   # H > 256
+    with pytest.raises(DeepRecError):
+        ops.din_attention_input(torch.zeros(2, 300, device=DEV), f)
+    with pytest.raises(DeepRecError):                        # T == 0 has no softmax
+        ops.din_attention_pool(torch.zeros(2, 0, device=DEV), torch.zeros(2, 0, device=DEV),
+                               torch.zeros(2, 0, 8, device=DEV))
+
+
+def _evs(dr, name, tables):
+    evs = []
+    for t, w in enumerate(tables):
+        ev = dr.EmbeddingVariable("%s_%d" % (name, t), w.shape[1], 0.0, device=DEV)
+        ev.insert(torch.arange(w.shape[0], device=DEV), w.to(DEV))
+        evs.append(ev)
+    return evs
+
+
+def _ev_rows(ev, R):
+    k, v = ev.export()[:2]
+    out = torch.zeros(R, ev.dim, device=DEV)
+    out[k] = v
+    return out
+
+
+def test_din_train_step_matches_torch_reference():
+    import deeprec_amd as dr
+    from deeprec_amd import modelzoo as mz
+    torch.manual_seed(11)
+    D, B, T, lr = 18, 96, 23, 0.05
+    R = [40, 60, 12]                                    # uid, mid, cat vocab
+    g = torch.Generator(device="cpu").manual_seed(4)
+    tables = [torch.randn(r, D, generator=g) * 0.1 for r in R]
+    evs = _evs(dr, "din", tables)
+    model = mz.DIN(*evs).to(DEV)
+    uids = torch.randint(0, R[0], (B,), device=DEV)
+    mids = torch.randint(0, R[1], (B,), device=DEV)
+    cats = torch.randint(0, R[2], (B,), device=DEV)
+    lens = torch.randint(1, T + 1, (B,), device=DEV)
+    mask = (torch.arange(T, device=DEV)[None, :] < lens[:, None]).float()
+    mid_his = torch.randint(1, R[1], (B, T), device=DEV) * mask.long()     # zero padded
+    cat_his = torch.randint(1, R[2], (B, T), device=DEV) * mask.long()
+    lab = (torch.rand(B, device=DEV) > 0.5).long()
+    target = torch.stack([lab, 1 - lab], 1).float()
+
+    P = {k: v.detach().clone().requires_grad_(True) for k, v in model.state_dict().items()}
+    W = [t.to(DEV).clone().requires_grad_(True) for t in tables]
+
+    def lin(x, n):
+        return x @ P[n + ".weight"].t() + P[n + ".bias"]
+
+    def dice(x, n):
+        mean = x.mean(0, keepdim=True)
+        std = torch.sqrt(((x - mean) ** 2 + 1e-9).mean(0, keepdim=True))
+        xp = torch.sigmoid((x - mean) / (std + 1e-9))
+        return P[n + ".alpha"] * (1.0 - xp) * x + xp * x
+
+    emb = torch.nn.functional.embedding
+    uid_e = emb(uids, W[0])
+    item = torch.cat([emb(mids, W[1]), emb(cats, W[2])], 1)
+    facts = torch.cat([emb(mid_his, W[1]), emb(cat_his, W[2])], 2)
+    h = torch.sigmoid(lin(_ref_din_input(item, facts), "f1_att"))
+    h = torch.sigmoid(lin(h, "f2_att"))
+    scores = lin(h, "f3_att").view(B, T)
+    att, his_sum, _ = _ref_pool(scores, mask, facts)
+    inp = torch.cat([uid_e, item, his_sum, item * his_sum, att], -1)
+    bn = inp * (1.0 / (1.0 + 1e-3) ** 0.5) * P["bn1_gamma"] + P["bn1_beta"]
+    x = dice(lin(bn, "dnn1"), "dice_1")
+    x = dice(lin(x, "dnn2"), "dice_2")
+    y = torch.softmax(lin(x, "dnn3"), -1) + 1e-8
+    ref_loss = -(torch.log(y) * target).mean()
+    ref_loss.backward()
+
+    dopt = torch.optim.SGD(model.parameters(), lr=lr)
+    batch = (uids, mids, cats, mid_his, cat_his, mask, target)
+    loss = mz.din_train_step(model, batch, dopt, dr.GradientDescentOptimizer(lr))
+    torch.testing.assert_close(loss, ref_loss.detach(), rtol=1e-5, atol=1e-6)
+    for name, prm in model.named_parameters():
+        want = P[name] - lr * P[name].grad
+        torch.testing.assert_close(prm.detach(), want.detach(), rtol=1e-5, atol=1e-6)
+    for t in range(3):
+        want = W[t] - lr * W[t].grad
+        torch.testing.assert_close(_ev_rows(evs[t], R[t]), want.detach(), rtol=1e-5, atol=1e-6)

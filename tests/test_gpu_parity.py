@@ -695,6 +695,44 @@ def test_grouped_backward_matches_segment_grad(dr, orc, onehot, comb):
         np.testing.assert_array_equal(H(sl.values[:U]), ref)
 
 
+@pytest.mark.parametrize("comb", ["sum", "mean"])
+@pytest.mark.parametrize("D", [18, 32])
+def test_grouped_backward_long_runs(dr, orc, comb, D):
+    """Runs longer than one chunk (256 positions: a DIN padding id over a
+    whole history batch) are summed as ordered chunk partials.  Runs of
+    <= 256 positions -- here 256 exactly and 200 -- stay bit-exact to the
+    serial reference order; longer ones (257, 5000, 3 x 256) match it to
+    fp32 tolerance 1e-5 rel / 1e-3 abs (sums of up to 5000 N(0,1) terms, |S| ~ 70)."""
+    rng = np.random.default_rng(37)
+    runs = {0: 5000, 1: 256, 2: 257, 3: 768, 4: 200}
+    v = np.concatenate([np.full(n, k, np.int64) for k, n in runs.items()] +
+                       [rng.integers(5, 400, 3000).astype(np.int64)])
+    rng.shuffle(v)
+    B = v.size
+    evs, sps = [], []
+    for f in range(2):
+        evs.append(dr.EmbeddingVariable("lrun_%s_%d_%d" % (comb, D, f), D, 0.1))
+        ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+        sps.append(dr.SparseTensor(T(ind), T(v), (B, 1)))
+    out = dr.embedding_lookup_sparse_multi(evs, sps, combiner=comb)
+    g = rng.standard_normal((B, 2 * D)).astype(np.float32)
+    out.backward(T(g))
+    uids, idx = orc.unique(v)
+    seg = np.arange(B, dtype=np.int32)
+    for f in range(2):
+        sl = evs[f].pending_grads.pop()
+        U = int(sl.num_valid.item())
+        assert H(sl.indices[:U]).tolist() == uids.tolist()
+        ref = orc.sparse_segment_reduce_grad(np.ascontiguousarray(g[:, f * D:(f + 1) * D]), idx,
+                                             seg, U, comb)
+        got = H(sl.values[:U])
+        pos = {int(k): i for i, k in enumerate(uids)}
+        exact = [i for i in range(U) if int(uids[i]) not in (0, 2, 3)]
+        np.testing.assert_array_equal(got[exact], ref[exact])
+        for k in (0, 2, 3):
+            np.testing.assert_allclose(got[pos[k]], ref[pos[k]], rtol=1e-5, atol=1e-3)
+
+
 def test_optimizers_with_repeated_indices(dr, orc):
     """SGD hands raw repeated indices to the KV kernel, which walks them in
     order (gradient_descent.py:71-76); Adagrad sums them first

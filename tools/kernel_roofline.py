@@ -161,21 +161,32 @@ def main():
 
     # -- DCN-v2 CrossNet layer, bf16 MFMA: 2*B*d^2 flop ------------------------
     if want("crossnet"):
-        B, d = 16384, 13 + 26 * 128
-        dp = (d + 7) // 8 * 8
-        x0 = torch.randn((B, dp), generator=g, device=dev).to(torch.bfloat16)
-        w = (torch.randn((dp, dp), generator=g, device=dev) / dp ** 0.5).to(torch.bfloat16)
-        bias = torch.zeros(dp, device=dev)
-        out = torch.empty((B, dp), dtype=torch.bfloat16, device=dev)
+        for B in (16384, 65536):
+            d = 13 + 26 * 128
+            dp = (d + 63) // 64 * 64
+            x0 = torch.randn((B, dp), generator=g, device=dev).to(torch.bfloat16)
+            xl = torch.randn((B, dp), generator=g, device=dev).to(torch.bfloat16)
+            w = (torch.randn((dp, dp), generator=g, device=dev) / dp ** 0.5).to(torch.bfloat16)
+            bias = torch.zeros(dp, device=dev)
+            out = torch.empty((B, dp), dtype=torch.bfloat16, device=dev)
+            lin = torch.empty((B, dp), dtype=torch.bfloat16, device=dev)
 
-        def cross():
-            check(lib().dr_crossnet_layer_bf16(ptr(x0), ptr(x0), ptr(w), ptr(bias), B, dp,
-                                               ptr(out), stream_handle(dev)))
-        ms = timed(cross, it)
-        report("crossnet_layer_bf16", ms, flops=2 * B * dp * dp, shape="B %d, d %d" % (B, dp))
-        ms = timed(lambda: torch.matmul(x0, w.t()), it)
-        report("torch_matmul_bf16_same_shape", ms, flops=2 * B * dp * dp,
-               shape="B %d, d %d (hipBLASLt reference point)" % (B, dp))
+            def cross(lin_out=None):
+                check(lib().dr_crossnet_forward_bf16(ptr(x0), ptr(xl), ptr(w), ptr(bias), B, dp,
+                                                     ptr(out), lin_out, stream_handle(dev)))
+            ms = timed(cross, it)
+            report("crossnet_layer_bf16", ms, flops=2 * B * dp * dp,
+                   shape="B %d, d %d (glds pipelined, fused epilogue)" % (B, dp))
+            ms = timed(lambda: cross(ptr(lin)), it)
+            report("crossnet_forward_bf16_with_lin", ms, flops=2 * B * dp * dp,
+                   shape="B %d, d %d (+ lin output)" % (B, dp))
+            ms = timed(lambda: torch.matmul(xl, w.t()), it)
+            report("torch_matmul_bf16_same_shape", ms, flops=2 * B * dp * dp,
+                   shape="B %d, d %d (hipBLASLt GEMM alone, no epilogue)" % (B, dp))
+            ms = timed(lambda: torch.addcmul(xl, x0, torch.addmm(bias.to(torch.bfloat16), xl,
+                                                                  w.t())), it)
+            report("torch_crossnet_composed", ms, flops=2 * B * dp * dp,
+                   shape="B %d, d %d (hipBLASLt addmm + addcmul)" % (B, dp))
 
     # -- KV sparse apply: U*(24 + (1+2k)*D*4), k = columns touched -------------
     if want("apply"):
