@@ -570,10 +570,11 @@ struct ApplyCols {
   int cols[3];
 };
 
-enum { OPT_SGD = 0, OPT_ADAGRAD = 1, OPT_ADAM = 2 };
+enum { OPT_SGD = 0, OPT_ADAGRAD = 1, OPT_ADAM = 2, OPT_FTRL = 3 };
 
 struct OptScalars {
   float lr, beta1, beta2, eps, alpha;
+  float l1, l2, lr_power, l2_shrinkage;  // FTRL
 };
 
 // Two phases per wave of 64 keys.  Phase 1, lane per key: LookupOrCreate
@@ -629,20 +630,16 @@ struct ApplyGroup {
   ApplyTable t[kApplyGroup];
 };
 
-template <int OPT, int VEC, int G>
-__global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t dim, int64_t gs,
-                                                       OptScalars sc, int* st) {
-  const ApplyTable& at = ag.t[blockIdx.y];
+// Phase 1 of a sparse apply, lane per key: LookupOrCreate with the global
+// step / filter admission / first-touch column mask (training_ali_ops.cc
+// LookupOrCreateKey + is_filter).  row = -1 when not admitted.
+__device__ __forceinline__ void apply_probe(const ApplyTable& at, int64_t i, int64_t ne,
+                                            int64_t gs, int64_t* row_out, int* initmask_out,
+                                            int* st) {
   const EvDesc& e = at.e;
   const ApplyCols& cols = at.cols;
   const int64_t* __restrict__ keys = at.keys;
-  const float* __restrict__ grad = at.grad;
   const int64_t steps_to_live = at.steps_to_live;
-  const int lane = threadIdx.x & 63;
-  const int64_t base = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63);
-  const int64_t ne = eff_n(at.n, at.n_dev);
-  if (base >= ne) return;  // wave-uniform
-  const int64_t i = base + lane;
   int64_t row = -1;
   int initmask = 0;
   if (i < ne) {
@@ -673,6 +670,23 @@ __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t di
       }
     }
   }
+  *row_out = row;
+  *initmask_out = initmask;
+}
+
+template <int OPT, int VEC, int G>
+__global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t dim, int64_t gs,
+                                                       OptScalars sc, int* st) {
+  const ApplyTable& at = ag.t[blockIdx.y];
+  const ApplyCols& cols = at.cols;
+  const float* __restrict__ grad = at.grad;
+  const int lane = threadIdx.x & 63;
+  const int64_t base = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63);
+  const int64_t ne = eff_n(at.n, at.n_dev);
+  if (base >= ne) return;  // wave-uniform
+  int64_t row;
+  int initmask;
+  apply_probe(at, base + lane, ne, gs, &row, &initmask, st);
   constexpr int P = 64 / G;                          // rows updated together
   constexpr int U = OPT == OPT_ADAM ? 2 : 4;          // row batches in flight
   const int sub = lane / G;
@@ -722,6 +736,110 @@ __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t di
         if (OPT == OPT_ADAM) reinterpret_cast<V*>(cols.pool[2] + rr[q] * dim)[c] = a2[q];
         reinterpret_cast<V*>(cols.pool[0] + rr[q] * dim)[c] = w[q];
       }
+    }
+  }
+}
+
+// KvResourceSparseApplyFtrl[V2] (training_ali_ops.cc:167-331, COMPUTE_FTRL
+// :279-307).  Phase 1 as above (columns var, accum, linear).  Phase 2, G
+// lanes per row, two passes: (1) linear += gu - (new_accum^p - accum^p) / lr
+// * var, stored, with the row's sum of squares reduced over the group by
+// xor shuffles; (2) var = norm > l1 ? (l1 - norm) / ((new_accum^p / lr + 2
+// l2) norm) * linear : 0, accum += g^2 (plain g, :307).  gu = g + 2 l2_shr
+// var for V2.  p = 1/2 (sqrt) when lr_power == -0.5, else -lr_power (powf).
+template <int VEC, int G>
+__device__ __forceinline__ float ftrl_pow(float x, const OptScalars& sc) {
+  return sc.lr_power == -0.5f ? sqrtf(x) : powf(x, -sc.lr_power);
+}
+
+template <int VEC, int G>
+__global__ __launch_bounds__(256) void ev_apply_ftrl_kernel(ApplyGroup ag, int64_t dim,
+                                                            int64_t gs, OptScalars sc, int* st) {
+  const ApplyTable& at = ag.t[blockIdx.y];
+  const ApplyCols& cols = at.cols;
+  const float* __restrict__ grad = at.grad;
+  const int lane = threadIdx.x & 63;
+  const int64_t base = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63);
+  const int64_t ne = eff_n(at.n, at.n_dev);
+  if (base >= ne) return;  // wave-uniform
+  int64_t row;
+  int initmask;
+  apply_probe(at, base + lane, ne, gs, &row, &initmask, st);
+  constexpr int P = 64 / G;
+  const int sub = lane / G;
+  const int lg = lane % G;
+  const int64_t dv = dim / VEC;
+  using V = typename std::conditional<VEC == 4, float4, float>::type;
+  const bool shrink = sc.l2_shrinkage > 0.f;
+  for (int k0 = 0; k0 < 64; k0 += P) {
+    const int k = k0 + sub;
+    int64_t r = __shfl(row, k, 64);  // every lane active for the shuffles
+    const int im = __shfl(initmask, k, 64);
+    if (base + k >= ne) r = -1;
+    float ss = 0.f;
+    if (r >= 0) {
+      const V* gp = reinterpret_cast<const V*>(grad + (base + k) * dim);
+      V* wp = reinterpret_cast<V*>(cols.pool[0] + r * dim);
+      V* ap = reinterpret_cast<V*>(cols.pool[1] + r * dim);
+      V* lp = reinterpret_cast<V*>(cols.pool[2] + r * dim);
+      const V* d0 = reinterpret_cast<const V*>(cols.dflt[0]);
+      const V* d1 = reinterpret_cast<const V*>(cols.dflt[1]);
+      const V* d2 = reinterpret_cast<const V*>(cols.dflt[2]);
+      for (int64_t c = lg; c < dv; c += G) {
+        const V gv = gp[c];
+        const V w = (im & 1) ? d0[c] : wp[c];
+        const V a = (im & 2) ? d1[c] : ap[c];
+        V l = (im & 4) ? d2[c] : lp[c];
+        const float* gf = reinterpret_cast<const float*>(&gv);
+        const float* wf = reinterpret_cast<const float*>(&w);
+        const float* af = reinterpret_cast<const float*>(&a);
+        float* lf = reinterpret_cast<float*>(&l);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const float gu = shrink ? gf[j] + 2.0f * sc.l2_shrinkage * wf[j] : gf[j];
+          const float na = af[j] + gu * gu;
+          const float dp = ftrl_pow<VEC, G>(na, sc) - ftrl_pow<VEC, G>(af[j], sc);
+          const float t = dp / sc.lr * wf[j];
+          lf[j] = lf[j] + (gu - t);
+          ss += lf[j] * lf[j];
+        }
+        lp[c] = l;
+      }
+    }
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    if (r < 0) continue;
+    const float norm = sqrtf(ss);
+    const V* gp = reinterpret_cast<const V*>(grad + (base + k) * dim);
+    V* wp = reinterpret_cast<V*>(cols.pool[0] + r * dim);
+    V* ap = reinterpret_cast<V*>(cols.pool[1] + r * dim);
+    const V* lp = reinterpret_cast<const V*>(cols.pool[2] + r * dim);
+    const V* d0 = reinterpret_cast<const V*>(cols.dflt[0]);
+    const V* d1 = reinterpret_cast<const V*>(cols.dflt[1]);
+    for (int64_t c = lg; c < dv; c += G) {
+      const V gv = gp[c];
+      V w = (im & 1) ? d0[c] : wp[c];
+      V a = (im & 2) ? d1[c] : ap[c];
+      const V l = lp[c];
+      const float* gf = reinterpret_cast<const float*>(&gv);
+      float* wf = reinterpret_cast<float*>(&w);
+      float* af = reinterpret_cast<float*>(&a);
+      const float* lf = reinterpret_cast<const float*>(&l);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float gu = shrink ? gf[j] + 2.0f * sc.l2_shrinkage * wf[j] : gf[j];
+        const float na = af[j] + gu * gu;
+        if (norm > sc.l1) {
+          const float eta_rec = ftrl_pow<VEC, G>(na, sc) / sc.lr;
+          const float coef = (sc.l1 - norm) / ((eta_rec + 2.0f * sc.l2) * norm);
+          wf[j] = coef * lf[j];
+        } else {
+          wf[j] = 0.f;
+        }
+        af[j] = af[j] + gf[j] * gf[j];
+      }
+      wp[c] = w;
+      ap[c] = a;
     }
   }
 }
@@ -1068,6 +1186,9 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
     else if (opt == OPT_ADAGRAD)                                                           \
       hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAGRAD, VEC, G>), grid, dim3(256), 0, st, ag,\
                          dim, gs, sc, stw);                                                 \
+    else if (opt == OPT_FTRL)                                                              \
+      hipLaunchKernelGGL((ev_apply_ftrl_kernel<VEC, G>), grid, dim3(256), 0, st, ag, dim,   \
+                         gs, sc, stw);                                                      \
     else                                                                                   \
       hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAM, VEC, G>), grid, dim3(256), 0, st, ag,   \
                          dim, gs, sc, stw);                                                 \
@@ -1917,7 +2038,7 @@ int dr_ev_key_meta(dr_ev* ev, const int64_t* keys_host, int64_t n, int64_t* freq
 
 int dr_ev_apply_sgd(dr_ev* var, float lr, const float* grad, const int64_t* keys, int64_t n,
                     const int64_t* n_dev, int64_t global_step, void* stream) {
-  dr::OptScalars sc = {lr, 0, 0, 0, 0};
+  dr::OptScalars sc = {lr, 0, 0, 0, 0, 0, 0, 0, 0};
   return dr::apply_common(dr::OPT_SGD, var, nullptr, nullptr, sc, grad, keys, n, n_dev,
                           global_step, dr::S(stream));
 }
@@ -1925,7 +2046,7 @@ int dr_ev_apply_sgd(dr_ev* var, float lr, const float* grad, const int64_t* keys
 int dr_ev_apply_adagrad(dr_ev* var, dr_ev* accum, float lr, const float* grad,
                         const int64_t* keys, int64_t n, const int64_t* n_dev, int64_t global_step,
                         void* stream) {
-  dr::OptScalars sc = {lr, 0, 0, 0, 0};
+  dr::OptScalars sc = {lr, 0, 0, 0, 0, 0, 0, 0, 0};
   return dr::apply_common(dr::OPT_ADAGRAD, var, accum, nullptr, sc, grad, keys, n, n_dev,
                           global_step, dr::S(stream));
 }
@@ -1939,12 +2060,44 @@ int dr_ev_apply_grouped(int optimizer, dr_ev* const* vars, dr_ev* const* slot1,
   using namespace dr;
   DR_REQUIRE(optimizer >= DR_OPT_SGD && optimizer <= DR_OPT_ADAM, DR_INVALID_ARGUMENT,
              "unknown optimizer %d", optimizer);
-  OptScalars sc = {lr, beta1, beta2, epsilon, 0.f};
+  OptScalars sc = {lr, beta1, beta2, epsilon, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (optimizer == DR_OPT_ADAM) sc.alpha = lr * sqrtf(1.0f - beta2_power) / (1.0f - beta1_power);
   const int opt = optimizer == DR_OPT_SGD ? OPT_SGD
                                           : (optimizer == DR_OPT_ADAGRAD ? OPT_ADAGRAD : OPT_ADAM);
   return apply_grouped(opt, vars, slot1, slot2, num_tables, sc, grads, keys, n_host, n_dev,
                        global_step, S(stream));
+}
+
+int dr_ev_apply_ftrl_grouped(dr_ev* const* vars, dr_ev* const* accums, dr_ev* const* linears,
+                             int num_tables, const float* const* grads,
+                             const int64_t* const* keys, const int64_t* n_host,
+                             const int64_t* const* n_dev, float lr, float l1, float l2,
+                             float lr_power, float l2_shrinkage, int64_t global_step,
+                             void* stream) {
+  using namespace dr;
+  // the op's OP_REQUIRES (training_ali_ops.cc:189-246)
+  DR_REQUIRE(lr > 0.f, DR_INVALID_ARGUMENT, "lr is not a positive scalar");
+  DR_REQUIRE(l1 >= 0.f && l2 >= 0.f && l2_shrinkage >= 0.f, DR_INVALID_ARGUMENT,
+             "l1 / l2 / l2_shrinkage regularization strength must be non-negative");
+  DR_REQUIRE(lr_power <= 0.f, DR_INVALID_ARGUMENT, "lr_power is not a non-positive scalar");
+  OptScalars sc = {lr, 0.f, 0.f, 0.f, 0.f, l1, l2, lr_power, l2_shrinkage};
+  return apply_grouped(OPT_FTRL, vars, accums, linears, num_tables, sc, grads, keys, n_host,
+                       n_dev, global_step, S(stream));
+}
+
+int dr_ev_apply_ftrl(dr_ev* var, dr_ev* accum, dr_ev* linear, float lr, float l1, float l2,
+                     float lr_power, float l2_shrinkage, const float* grad, const int64_t* keys,
+                     int64_t n, const int64_t* n_dev, int64_t global_step, void* stream) {
+  if (n == 0) return DR_OK;
+  dr_ev* v[1] = {var};
+  dr_ev* a[1] = {accum};
+  dr_ev* l[1] = {linear};
+  const float* g[1] = {grad};
+  const int64_t* k[1] = {keys};
+  const int64_t nh[1] = {n};
+  const int64_t* nd[1] = {n_dev};
+  return dr_ev_apply_ftrl_grouped(v, a, l, 1, g, k, nh, nd, lr, l1, l2, lr_power, l2_shrinkage,
+                                  global_step, stream);
 }
 
 int dr_ev_apply_adam(dr_ev* var, dr_ev* m, dr_ev* v, float beta1_power, float beta2_power,
@@ -1953,7 +2106,7 @@ int dr_ev_apply_adam(dr_ev* var, dr_ev* m, dr_ev* v, float beta1_power, float be
                      void* stream) {
   // alpha = lr * sqrt(1 - beta2^t) / (1 - beta1^t)  (training_ali_ops.cc:935-937)
   const float alpha = lr * sqrtf(1.0f - beta2_power) / (1.0f - beta1_power);
-  dr::OptScalars sc = {lr, beta1, beta2, epsilon, alpha};
+  dr::OptScalars sc = {lr, beta1, beta2, epsilon, alpha, 0, 0, 0, 0};
   return dr::apply_common(dr::OPT_ADAM, var, m, v, sc, grad, keys, n, n_dev, global_step,
                           dr::S(stream));
 }

@@ -136,6 +136,10 @@ SIGNATURES = {
                                 _I64, _P]),
     "dr_ev_apply_grouped": (_I32, [_I32, _P, _P, _P, _I32, _P, _P, _P, _P, _F32, _F32, _F32,
                                    _F32, _F32, _F32, _I64, _P]),
+    "dr_ev_apply_ftrl": (_I32, [_P, _P, _P, _F32, _F32, _F32, _F32, _F32, _P, _P, _I64, _P, _I64,
+                                _P]),
+    "dr_ev_apply_ftrl_grouped": (_I32, [_P, _P, _P, _I32, _P, _P, _P, _P, _F32, _F32, _F32, _F32,
+                                        _F32, _I64, _P]),
     "dr_fused_local_workspace_size": (_SZ, [_I64]),
     "dr_fused_local_lookup": (_I32, [_P, _I64, _I32, _P, _P, _I64, _I64, _I32, _F32, _P, _P, _P,
                                      _SZ, _P]),

@@ -182,25 +182,17 @@ def _desc(f, out, out_stride):
     return d
 
 
-def _grad_to_slices(f, g, top_stride):
-    """Pooled grad [B, D] (stride) -> IndexedSlices over the unique ids."""
+def _grad_to_slices(f, g, col, top_stride):
+    """Pooled grad (feature columns from `col` of rows of `top_stride`
+    floats) -> IndexedSlices over the unique ids, through the grouped
+    backward kernel with one feature (chunked runs: a hot id does not
+    serialise one wave)."""
     if f.weights is not None or f.max_norm is not None:
         raise NotImplementedError("backward of weighted / max_norm lookups is not implemented")
     if f.uniq is None:
         f.uniq, f.idx, _, f.U = ops.unique_device(f.values)
-    dev = g.device
-    _bag_offsets_all([f])
-    n = f.values.numel()
-    D = f.params.dim if not torch.is_tensor(f.params) else f.params.shape[1]
-    gu = torch.empty((n, D), dtype=torch.float32, device=dev)
-    seg32 = f.seg.to(torch.int32).contiguous()
-    wsb = lib().dr_pool_grad_workspace_size(n)
-    ws = workspace(wsb, dev)
-    check(lib().dr_pool_grad(ptr(g), top_stride, f.batch, D, ptr(f.bag_off), ptr(seg32),
-                             ptr(f.idx), n, ptr(f.U), COMBINERS[f.combiner], ptr(gu), ptr(ws), wsb,
-                             stream_handle(dev)))
-    ops._post(dev)
-    return IndexedSlices(gu, f.uniq, f.U, unique=True)
+    grp = _UniqueGroup([f], f.uniq, f.U, [0, f.values.numel()])
+    return grp.grads(g, [col], top_stride)[0]
 
 
 class _LookupFn(torch.autograd.Function):
@@ -238,9 +230,7 @@ def _queue_grads(feats, g, col0, total):
             for x, sl in zip(grp.feats, sls):
                 x.params.pending_grads.append(sl)
             continue
-        D = holder.dim
-        sl = _grad_to_slices(f, g[:, cols[i]:cols[i] + D].contiguous(), D)
-        holder.pending_grads.append(sl)
+        holder.pending_grads.append(_grad_to_slices(f, g, cols[i], total))
 
 
 class _StackFn(torch.autograd.Function):

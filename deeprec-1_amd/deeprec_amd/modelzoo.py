@@ -185,6 +185,81 @@ class DinAttentionPool(torch.autograd.Function):
         return gs, None, gf
 
 
+class WDL(torch.nn.Module):
+    """modelzoo/WDL/train.py WDL (BASELINE configs[0]) on EVs.
+
+    Deep part (:238-281): tf.feature_column.input_layer over the embedding
+    columns (one EV per categorical column, combiner 'mean') and the 13
+    min-max normalised numeric columns, in input_layer's order -- columns
+    sorted by name ('C10_embedding' < 'C1_embedding' < ... < 'I1' < 'I10'
+    ...) -- then dnn [1024, 512, 256] ReLU and a 1-unit logits layer.  Wide
+    part (:283-295): linear_model with sparse_combiner 'sum' over the same
+    categorical ids (dim-1 EVs), one weight per numeric column, one bias.
+    logits = dnn_logits + linear_logits."""
+
+    def __init__(self, cat_names, deep_evs, wide_evs, num_names, hidden=(1024, 512, 256)):
+        super().__init__()
+        self.cat_names, self.num_names = list(cat_names), list(num_names)
+        self.deep_evs, self.wide_evs = list(deep_evs), list(wide_evs)
+        self.evs = self.deep_evs + self.wide_evs
+        dims = [ev.dim for ev in self.deep_evs]
+        # input_layer column order: sort by column name, then lay out
+        cols, off = {}, 0
+        for name, d in zip(self.cat_names, dims):
+            cols[name + "_embedding"] = list(range(off, off + d))
+            off += d
+        for j, name in enumerate(self.num_names):
+            cols[name] = [off + j]
+        perm = [c for name in sorted(cols) for c in cols[name]]
+        self.register_buffer("perm", torch.tensor(perm, dtype=torch.int64), persistent=False)
+        self.dnn = _mlp([off + len(self.num_names)] + list(hidden))
+        self.logits = torch.nn.Linear(hidden[-1], 1)
+        self.linear_num = torch.nn.Parameter(torch.zeros(len(self.num_names), 1))
+        self.linear_bias = torch.nn.Parameter(torch.zeros(1))
+        self.deep_lookup = _OneHotLookup(self.deep_evs)
+        self.wide_lookup = _OneHotLookup(self.wide_evs)
+
+    def deep_parameters(self):
+        return list(self.dnn.parameters()) + list(self.logits.parameters())
+
+    def wide_parameters(self):
+        return [self.linear_num, self.linear_bias]
+
+    def forward(self, dense, ids):
+        emb = embedding_lookup_sparse_multi(self.deep_evs, self.deep_lookup._sps(ids),
+                                            combiner="mean")
+        net = torch.cat([emb, dense], 1).index_select(1, self.perm)
+        dnn_logits = self.logits(self.dnn(net))
+        wide = self.wide_lookup(ids)                                # [B, T] (sum of dim-1 rows)
+        linear_logits = wide.sum(1, keepdim=True) + dense @ self.linear_num + self.linear_bias
+        return (dnn_logits + linear_logits).squeeze(1)
+
+
+def wdl_train_step(model, dense, ids, labels, deep_opt, deep_ev_opt, wide_opt, wide_ev_opt,
+                   global_step=None):
+    """One WDL step (modelzoo/WDL/train.py:302-335): sigmoid cross entropy
+    (mean over the batch); deep variables (dnn + embedding EVs) by deep_opt /
+    deep_ev_opt (the reference: Adagrad 0.01, accumulator 0.1), linear
+    variables by wide_opt / wide_ev_opt (the reference: Ftrl 0.2, l1 = l2 =
+    0).  A training.FtrlOptimizer as wide_opt updates the dense linear
+    weights elementwise (ApplyFtrl)."""
+    from .training import FtrlOptimizer
+    logits = model(dense, ids)
+    loss = torch.nn.functional.binary_cross_entropy_with_logits(logits, labels)
+    deep_opt.zero_grad(set_to_none=True)
+    for p in model.wide_parameters():
+        p.grad = None
+    loss.backward()
+    deep_opt.step()
+    if isinstance(wide_opt, FtrlOptimizer):
+        wide_opt.dense_step(model.wide_parameters())
+    else:
+        wide_opt.step()
+    deep_ev_opt.apply_gradients(model.deep_evs, global_step=global_step)
+    wide_ev_opt.apply_gradients(model.wide_evs, global_step=global_step)
+    return loss
+
+
 class CrossLayer(torch.autograd.Function):
     """DCN-v2 cross layer x_{l+1} = x0 * (x_l W^T + b) + x_l (BASELINE
     configs[4]; absent from the reference).  Forward: the

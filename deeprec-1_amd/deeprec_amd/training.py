@@ -189,3 +189,69 @@ class AdamOptimizer(_Optimizer):
 
     def _dense_update(self, var, idx, g):
         raise NotImplementedError("dense-table Adam: use an EmbeddingVariable")
+
+
+class FtrlOptimizer(_Optimizer):
+    """KvResourceSparseApplyFtrl[V2] (training_ali_ops.cc:167-331) on EVs:
+    slots accum (initial_accumulator_value) and linear (0); l2_shrinkage > 0
+    selects FtrlV2.  Dense tables use the elementwise ResourceSparseApplyFtrl
+    of training_ops.cc (per-element |linear| instead of the KV op's row norm)."""
+
+    _opt = 3
+
+    def __init__(self, learning_rate, learning_rate_power=-0.5, initial_accumulator_value=0.1,
+                 l1_regularization_strength=0.0, l2_regularization_strength=0.0,
+                 l2_shrinkage_regularization_strength=0.0):
+        super().__init__(learning_rate)
+        self.lr_power = float(learning_rate_power)
+        self.init_acc = float(initial_accumulator_value)
+        self.l1 = float(l1_regularization_strength)
+        self.l2 = float(l2_regularization_strength)
+        self.l2_shrinkage = float(l2_shrinkage_regularization_strength)
+        self._dense = {}
+
+    def _slots(self, var):
+        return var.slot("Ftrl", self.init_acc), var.slot("Ftrl_1", 0.0)
+
+    def _apply_ev_batch(self, items, gs):
+        import ctypes as C
+        groups = {}
+        for var, sl in items:
+            groups.setdefault((str(var.device), var.dim), []).append((var, sl))
+        for (_, _), grp in groups.items():
+            T = len(grp)
+            dev = grp[0][0].device
+            vals = [sl.values.contiguous() for _, sl in grp]
+            idxs = [sl.indices.contiguous() for _, sl in grp]
+            slots = [self._slots(var) for var, _ in grp]
+            P = C.c_void_p * T
+            check(lib().dr_ev_apply_ftrl_grouped(
+                P(*[var.handle.value for var, _ in grp]), P(*[a.handle.value for a, _ in slots]),
+                P(*[b.handle.value for _, b in slots]), T, P(*[v.data_ptr() for v in vals]),
+                P(*[i.data_ptr() for i in idxs]), (C.c_int64 * T)(*[i.numel() for i in idxs]),
+                P(*[ptr(sl.num_valid) for _, sl in grp]), self.lr, self.l1, self.l2,
+                self.lr_power, self.l2_shrinkage, gs, stream_handle(dev)))
+            ops._post(dev)
+
+    def dense_step(self, params):
+        """Elementwise FTRL (ApplyFtrl, training_ops.cc) on dense torch
+        parameters with .grad set (a WDL linear part's numeric weights / bias)."""
+        with torch.no_grad():
+            for p in params:
+                if p.grad is None:
+                    continue
+                acc, lin = self._dense.setdefault(
+                    id(p), (torch.full_like(p, self.init_acc), torch.zeros_like(p)))
+                g = p.grad
+                gu = g + 2.0 * self.l2_shrinkage * p if self.l2_shrinkage > 0 else g
+                na = acc + gu * gu
+                pw = -self.lr_power
+                lin.add_(gu - (na.pow(pw) - acc.pow(pw)) / self.lr * p)
+                quad = na.pow(pw) / self.lr + 2.0 * self.l2
+                p.copy_(torch.where(lin.abs() > self.l1,
+                                    (torch.sign(lin) * self.l1 - lin) / quad,
+                                    torch.zeros_like(p)))
+                acc.add_(g * g)
+
+    def _dense_update(self, var, idx, g):
+        raise NotImplementedError("dense-table FTRL: use an EmbeddingVariable")

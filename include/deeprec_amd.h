@@ -347,6 +347,19 @@ int dr_ev_apply_grouped(int optimizer, dr_ev* const* vars, dr_ev* const* slot1,
                         const int64_t* const* n_dev, float lr, float beta1_power,
                         float beta2_power, float beta1, float beta2, float epsilon,
                         int64_t global_step, void* stream);
+/* KvResourceSparseApplyFtrl / FtrlV2 (training_ali_ops.cc:167-331; op defs  */
+/* core/ops/training_ali_ops.cc): accum / linear are slot EVs of var;        */
+/* l2_shrinkage 0 = Ftrl, > 0 = FtrlV2.  The row norm of `linear` is an fp32 */
+/* reduction (Eigen's order is not reproducible: parity within 1e-5 rel).    */
+int dr_ev_apply_ftrl(dr_ev* var, dr_ev* accum, dr_ev* linear, float lr, float l1, float l2,
+                     float lr_power, float l2_shrinkage, const float* grad, const int64_t* keys,
+                     int64_t n, const int64_t* n_dev, int64_t global_step, void* stream);
+int dr_ev_apply_ftrl_grouped(dr_ev* const* vars, dr_ev* const* accums, dr_ev* const* linears,
+                             int num_tables, const float* const* grads,
+                             const int64_t* const* keys, const int64_t* n_host,
+                             const int64_t* const* n_dev, float lr, float l1, float l2,
+                             float lr_power, float l2_shrinkage, int64_t global_step,
+                             void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* FusedEmbeddingLocalSparseLookUp[Grad]                                     */

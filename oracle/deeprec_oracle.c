@@ -812,6 +812,58 @@ int orc_ev_apply_adam(orc_ev* var, orc_ev* m_ev, orc_ev* v_ev, float beta1_power
   return ORC_OK;
 }
 
+/* KvResourceSparseApplyFtrl[V2] (training_ali_ops.cc:167-331), the       */
+/* COMPUTE_FTRL macro (:279-307) per key with grad_to_use = g (+ 2 * l2_    */
+/* shrinkage * var for V2, :308-311):                                        */
+/*   new_accum = accum + gu^2                                                */
+/*   linear   += gu - (new_accum^p - accum^p) / lr * var    (p = -lr_power,  */
+/*               sqrt when lr_power == -0.5)                                 */
+/*   norm = sqrt(sum linear^2)  (a row reduction: Eigen's order is not       */
+/*          reproducible, ascending order here -> parity by tolerance)       */
+/*   var = norm > l1 ? (l1 - norm) / ((new_accum^p / lr + 2 l2) norm) linear */
+/*                   : 0                                                     */
+/*   accum += g^2   (the plain gradient, :307)                               */
+int orc_ev_apply_ftrl(orc_ev* var, orc_ev* accum_ev, orc_ev* linear_ev, float lr, float l1,
+                      float l2, float lr_power, float l2_shrinkage, const float* grad,
+                      const int64_t* keys, int64_t n, int64_t gs) {
+  const int64_t D = var->dim;
+  const int sq = lr_power == -0.5f;
+  float* gu = (float*)malloc(sizeof(float) * (size_t)(D > 0 ? D : 1));
+  if (!gu) return ORC_RESOURCE_EXHAUSTED;
+  for (int64_t i = 0; i < n; ++i) {
+    int64_t e = orc_apply_key(var, keys[i], gs);
+    if (e < 0) continue;
+    float* w = orc_get_or_alloc(var, e, var->default_value);
+    float* a = orc_get_or_alloc(accum_ev, e, accum_ev->default_value);
+    float* lin = orc_get_or_alloc(linear_ev, e, linear_ev->default_value);
+    float nsq = 0.f;
+    for (int64_t d = 0; d < D; ++d) {
+      float g = grad[i * D + d];
+      gu[d] = l2_shrinkage > 0.f ? g + 2.0f * l2_shrinkage * w[d] : g;
+      float na = a[d] + gu[d] * gu[d];
+      float dp = sq ? sqrtf(na) - sqrtf(a[d]) : powf(na, -lr_power) - powf(a[d], -lr_power);
+      float t = dp / lr * w[d];
+      lin[d] = lin[d] + (gu[d] - t);
+      nsq += lin[d] * lin[d];
+    }
+    float norm = sqrtf(nsq);
+    for (int64_t d = 0; d < D; ++d) {
+      float g = grad[i * D + d];
+      float na = a[d] + gu[d] * gu[d];
+      if (norm > l1) {
+        float eta_rec = (sq ? sqrtf(na) : powf(na, -lr_power)) / lr;
+        float coef = (l1 - norm) / ((eta_rec + 2.0f * l2) * norm);
+        w[d] = coef * lin[d];
+      } else {
+        w[d] = 0.f;
+      }
+      a[d] = a[d] + g * g;
+    }
+  }
+  free(gu);
+  return ORC_OK;
+}
+
 /* Dense-variable counterparts (ResourceSparseApply*, training_ops.cc),      */
 /* used by the EV == dense 5-step equality idiom                              */
 /* (embedding_variable_ops_test.py:825-997).  Rows indexed directly.          */

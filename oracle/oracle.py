@@ -62,6 +62,7 @@ def lib():
             "orc_ev_apply_sgd": (i32, [p, f32, p, p, i64, i64]),
             "orc_ev_apply_adagrad": (i32, [p, p, f32, p, p, i64, i64]),
             "orc_ev_apply_adam": (i32, [p, p, p, f32, f32, f32, f32, f32, f32, p, p, i64, i64]),
+            "orc_ev_apply_ftrl": (i32, [p, p, p, f32, f32, f32, f32, f32, p, p, i64, i64]),
             "orc_dense_apply_sgd": (i32, [p, i64, f32, p, p, i64]),
             "orc_dense_apply_adagrad": (i32, [p, p, i64, f32, p, p, i64]),
             "orc_fm2": (None, [p, i64, i64, i64, p]),
@@ -379,6 +380,13 @@ class EV(object):
         _check(lib().orc_ev_apply_adam(self._h, m._h, v._h, beta1_power, beta2_power, lr,
                                        beta1, beta2, eps, _p(grad), _p(keys), keys.shape[0],
                                        gs), "adam")
+
+    def apply_ftrl(self, accum, linear, lr, l1, l2, lr_power, l2_shrinkage, grad, keys, gs=-1):
+        grad = np.ascontiguousarray(grad, np.float32)
+        keys = np.ascontiguousarray(keys, np.int64)
+        _check(lib().orc_ev_apply_ftrl(self._h, accum._h, linear._h, lr, l1, l2, lr_power,
+                                       l2_shrinkage, _p(grad), _p(keys), keys.shape[0], gs),
+               "ftrl")
 
 
 def dense_apply_sgd(table, lr, grad, idx):
