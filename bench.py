@@ -2,12 +2,16 @@
 """bench.py -- embedding lookups/s on the DLRM Criteo-Terabyte shape.
 
 One step = one pass of the north_star hot path over one batch: for each of
-the 26 sparse features, first-occurrence dedup -> EmbeddingVariable
-insert-on-miss resolve -> fused gather + sum pooling into the [B, 26*128]
-input_layer output (embedding_lookup_sparse, combiner "sum", hotness 1).
-At N GPUs the tables are row-sharded (owner = key % N) and every step runs
-the index all-to-all -> owner resolve + gather -> row all-to-all exchange
-over RCCL (deeprec_amd/sharded.py); per-GPU work is fixed (weak scaling).
+the 26 sparse features, EmbeddingVariable insert-on-miss resolve of every id
+-> gather + sum pooling into the [B, 26*128] input_layer output
+(embedding_lookup_sparse, combiner "sum", hotness 1; forward-only lookups of
+filter-free EVs need no Unique), one fused kernel at N = 1.
+At N GPUs the tables are row-sharded (owner = key % N) and every step sends
+the ids to their owners, resolves them there and brings the rows back: over
+xGMI peer writes (XgmiShardedLookup), or the RCCL all-to-all engine
+(ShardedLookup) when IPC mapping is unavailable; per-GPU work is fixed
+(weak scaling).  The JSON line carries the roofline of the dominant kernel
+and, for the north_star's row-gather target, of the pre-resolved gather.
 
 Timing: W untimed warmup steps, then exactly K steps bracketed by a barrier
 and torch.cuda.synchronize(); max over ranks; rank 0 prints one JSON line.
@@ -306,6 +310,41 @@ def main():
         e1.record()
         torch.cuda.synchronize()
     k_ms = e0.elapsed_time(e1) / args.kernel_iters
+
+    # ---- the north_star's row-gather target: the same
+    # lookups on pre-resolved rows (dr_ev_resolve_grouped once, outside the
+    # timing), pool_onehot_kernel alone: 8 (row id) + D*4 read + D*4 write
+    from deeprec_amd.embedding_ops import _pool_all, _prepare_group
+    with torch.no_grad():
+        gfeats = [_Feature(evs[t], static_ids[t], seg, B, None, "sum", None, onehot=True)
+                  for t in range(T)]
+        _prepare_group(gfeats, need_grad=False)
+        _pool_all(gfeats, _lib.ORDER_ALI)
+        torch.cuda.synchronize()
+        pg = None
+        if not args.no_graph:
+            pg = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(pg):
+                _pool_all(gfeats, _lib.ORDER_ALI)
+            pg.replay()
+            torch.cuda.synchronize()
+        e0.record()
+        for _ in range(args.kernel_iters):
+            if pg is not None:
+                pg.replay()
+            else:
+                _pool_all(gfeats, _lib.ORDER_ALI)
+        e1.record()
+        torch.cuda.synchronize()
+    g_ms = e0.elapsed_time(e1) / args.kernel_iters
+    g_per = 8 + 2 * D * 4
+    g_ach = T * B * g_per / (g_ms * 1e-3) / 1e9
+    roof_gather = {"bound": "hbm", "achieved": round(g_ach, 1), "peak": PEAK_HBM_GBS,
+                   "unit": "GB/s", "frac": round(g_ach / PEAK_HBM_GBS, 4), "traffic": None,
+                   "kernel": "dr::pool_onehot_kernel<4,32,1,ALI,4> on pre-resolved rows "
+                             "(BASELINE.md row-gather target, >= 0.70)",
+                   "kernel_ms": round(g_ms, 4), "bytes_per_launch": T * B * g_per,
+                   "bytes_per_lookup": g_per}
     # SURVEY 8(d) EV hashed gather (+ the pooled write): key 8 + slot 16 +
     # row D*4 read + D*4 output write per lookup (h = 1)
     per_lookup = 8 + 16 + D * 4 + D * 4
@@ -358,6 +397,7 @@ def main():
                        "parallelism": "row-sharded tables x%d, data-parallel batch" % world},
             "samples_per_s": round(value / T, 1),
             "roofline": roof,
+            "roofline_row_gather": roof_gather,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

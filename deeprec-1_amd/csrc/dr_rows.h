@@ -95,4 +95,19 @@ __device__ __forceinline__ void acc_add(Row<VEC, G, CPL>& a, const Row<VEC, G, C
   for (int c = 0; c < CPL; ++c) a.v[c] = vadd(a.v[c], b.v[c]);
 }
 
+// Row load with an always-valid pointer (only the lane's column predicate):
+// a per-row "pointer or zero" select makes hipcc branch around every load
+// and wait for it before the next one, so batches of independent loads
+// serialise into dependent round trips.  Callers clamp indices instead and
+// discard invalid rows after the loads.
+template <int VEC, int G, int CPL>
+__device__ __forceinline__ void load_row_u(Row<VEC, G, CPL>& x, const float* p, int lg, int dv) {
+  using V = typename VecT<VEC>::T;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = lg + c * G;
+    x.v[c] = col < dv ? reinterpret_cast<const V*>(p)[col] : vzero<V>();
+  }
+}
+
 }  // namespace dr

@@ -69,6 +69,7 @@ struct EvShared {
   bool copy_pending = false;
   hipEvent_t copy_ev = nullptr;
   int64_t* pinned_top = nullptr;
+  int64_t removed = 0;  // keys removed by dr_ev_shrink (rows are not recycled)
 };
 
 }  // namespace dr
@@ -841,6 +842,71 @@ __global__ __launch_bounds__(256) void ev_apply_ftrl_kernel(ApplyGroup ag, int64
       wp[c] = w;
       ap[c] = a;
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Save-time eviction, EmbeddingVar::Shrink (embedding_var.h:264-313), called
+// by DumpEv before DumpEmbeddingValues (save_restore_v2_ops.cc:128-131):
+//   l2_weight_threshold != -1 : drop keys whose 0.5 * sum_j v_j^2 (primary
+//                               row, ascending j in fp32) < threshold
+//   else, steps_to_live > 0   : version == -1 -> version = gs; drop keys
+//                               with gs - version > steps_to_live
+// Marking is one thread per slot; the kept slots are rehashed into a fresh
+// table (linear probing has no tombstones).  Rows of dropped keys are not
+// recycled ("TODO memory recycle" in the reference too).
+// ---------------------------------------------------------------------------
+__global__ void ev_shrink_mark_kernel(Slot* __restrict__ slots, int64_t cap, const float* pool,
+                                      const float* dflt, int64_t dim, int64_t* __restrict__ version,
+                                      int mode, float l2_threshold, int64_t gs,
+                                      int64_t steps_to_live, uint8_t* __restrict__ keep,
+                                      unsigned long long* __restrict__ nremoved) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > cap) return;
+  const Slot sl = slots[i];
+  const bool occupied = i < cap ? sl.key != kEmptyKey : sl.key == 0ull;
+  uint8_t k = 1;
+  if (occupied && sl.rc != kUnset && (sl.rc & kRowMask) != kRowDead) {
+    const int64_t row = (int64_t)(sl.rc & kRowMask);
+    if (mode == 1) {
+      const float* v = (sl.rc & (1ull << 48)) ? pool + row * dim : dflt;
+      float l2 = 0.f;
+      for (int64_t j = 0; j < dim; ++j) l2 += v[j] * v[j];
+      l2 *= 0.5f;
+      if (l2 < l2_threshold) k = 0;
+    } else if (mode == 2 && version) {
+      const int64_t ver = version[row];
+      if (ver == -1)
+        version[row] = gs;
+      else if (gs - ver > steps_to_live)
+        k = 0;
+    }
+  }
+  keep[i] = k;
+  if (!k) atomicAdd(nremoved, 1ull);
+}
+
+__global__ void ev_rehash_kept_kernel(const Slot* __restrict__ old_slots, int64_t cap,
+                                      const uint8_t* __restrict__ keep,
+                                      Slot* __restrict__ new_slots) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > cap) return;
+  const Slot s = old_slots[i];
+  if (i == cap) {  // the key -1 slot
+    if (keep[i]) new_slots[cap] = s;
+    return;
+  }
+  if (s.key == kEmptyKey || !keep[i]) return;
+  const uint64_t mask = (uint64_t)cap - 1;
+  uint64_t h = mix64(s.key) & mask;
+  for (;;) {
+    uint64_t old = atomicCAS((unsigned long long*)&new_slots[h].key, (unsigned long long)kEmptyKey,
+                             (unsigned long long)s.key);
+    if (old == kEmptyKey) {
+      new_slots[h].rc = s.rc;
+      return;
+    }
+    h = (h + 1) & mask;
   }
 }
 
@@ -1711,6 +1777,59 @@ int dr_ev_size(dr_ev* ev, int64_t* size_host, void* stream) {
   DR_REQUIRE(ev && size_host, DR_INVALID_ARGUMENT, "null argument");
   DR_HIP(hipStreamSynchronize(dr::S(stream)));
   DR_HIP(hipMemcpy(size_host, ev->sh->top, sizeof(int64_t), hipMemcpyDeviceToHost));
+  *size_host -= ev->sh->removed;
+  return DR_OK;
+}
+
+int dr_ev_shrink(dr_ev* ev, int64_t global_step, float l2_weight_threshold,
+                 int64_t* removed_host, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(ev && ev->col == 0, DR_INVALID_ARGUMENT, "shrink needs a primary EV");
+  EvShared* s = ev->sh;
+  hipStream_t st = S(stream);
+  const int mode = l2_weight_threshold != -1.0f ? 1 : (s->steps_to_live > 0 ? 2 : 0);
+  if (removed_host) *removed_host = 0;
+  if (mode == 0) return DR_OK;
+  std::lock_guard<std::mutex> g(s->mu);
+  const int64_t n = s->cap + 1;
+  uint8_t* keep = nullptr;
+  unsigned long long* cnt = nullptr;
+  Slot* ns = nullptr;
+  DR_HIP(hipMalloc(&keep, (size_t)n));
+  if (hipMalloc(&cnt, sizeof(unsigned long long)) != hipSuccess) {
+    (void)hipFree(keep);
+    DR_REQUIRE(false, DR_RESOURCE_EXHAUSTED, "shrink: out of device memory");
+  }
+  if (hipMalloc(&ns, (size_t)n * sizeof(Slot)) != hipSuccess) {
+    (void)hipFree(keep);
+    (void)hipFree(cnt);
+    DR_REQUIRE(false, DR_RESOURCE_EXHAUSTED, "shrink: out of device memory");
+  }
+  int rc = fill_bytes(cnt, 0, sizeof(unsigned long long), st);
+  if (!rc) rc = fill_bytes(ns, 0xFF, (size_t)n * sizeof(Slot), st);
+  unsigned long long removed = 0;
+  if (!rc) {
+    const unsigned blocks = (unsigned)ceil_div(n, 256);
+    hipLaunchKernelGGL(ev_shrink_mark_kernel, dim3(blocks), dim3(256), 0, st, s->slots, s->cap,
+                       s->pools[0], s->defaults[0], s->dim, s->version, mode,
+                       l2_weight_threshold, global_step, s->steps_to_live, keep, cnt);
+    hipLaunchKernelGGL(ev_rehash_kept_kernel, dim3(blocks), dim3(256), 0, st, s->slots, s->cap,
+                       keep, ns);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess ||
+        hipMemcpy(&removed, cnt, sizeof(removed), hipMemcpyDeviceToHost) != hipSuccess)
+      rc = DR_INTERNAL;
+  }
+  (void)hipFree(keep);
+  (void)hipFree(cnt);
+  if (rc) {
+    (void)hipFree(ns);
+    set_error("dr_ev_shrink failed");
+    return rc;
+  }
+  (void)hipFree(s->slots);
+  s->slots = ns;
+  s->removed += (int64_t)removed;
+  if (removed_host) *removed_host = (int64_t)removed;
   return DR_OK;
 }
 

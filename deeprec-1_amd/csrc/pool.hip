@@ -619,21 +619,29 @@ __global__ __launch_bounds__(256) void csr_sum_kernel(
     R x[NB];
     int64_t rr[NB];
 #pragma unroll
-    for (int q = 0; q < NB; ++q) {
-      const float* rp = nullptr;
-      rr[q] = -1;
-      if (jb + q < j1) {
-        const int32_t p = perm[jb + q];
-        const int64_t r = seg_of_pos ? (int64_t)seg_of_pos[p] : (int64_t)p;
-        if (r >= 0 && r < src_rows) {
-          rp = src + r * src_stride;
-          rr[q] = r;
-        } else {
-          latch(st, DR_INVALID_ARGUMENT);
-        }
-      }
-      load_row<VEC, G, CPL>(x[q], rp, lg, dv);
+    for (int q = 0; q < NB; ++q) {  // unconditional, clamped loads (load_row_u)
+      const int32_t jq = jb + q < j1 ? jb + q : j1 - 1;
+      rr[q] = perm[jq];
     }
+    if (seg_of_pos) {
+#pragma unroll
+      for (int q = 0; q < NB; ++q) rr[q] = seg_of_pos[rr[q]];
+    }
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const bool okr = (rr[q] >= 0) & (rr[q] < src_rows);
+      bad |= (jb + q < j1) & !okr;
+      rr[q] = okr ? rr[q] : -1;
+      load_row_u<VEC, G, CPL>(x[q], src + (okr ? rr[q] : 0) * src_stride, lg, dv);
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q)
+      if (rr[q] < 0) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) x[q].v[c] = vzero<V>();
+      }
+    if (bad) latch(st, DR_INVALID_ARGUMENT);
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
       if (jb + q >= j1) break;
@@ -751,10 +759,9 @@ static int segsum_driver(const int32_t* keyseg, int64_t n, int64_t num_out, cons
   size_t used = 0;
   SegSumWs w = carve_segsum(ws, n, num_out, &used);
   if (num_out == 0) return DR_OK;
-  if (n == 0) {
-    return fill_bytes(out, 0, (size_t)num_out * dim * sizeof(float), s);
-    return DR_OK;
-  }
+  if (n == 0) return fill_bytes(out, 0, (size_t)num_out * dim * sizeof(float), s);
+  // (rows are loaded through clamped indices: a row 0 must exist)
+  DR_REQUIRE(src_rows > 0, DR_INVALID_ARGUMENT, "segment ids given for an empty data tensor");
   hipLaunchKernelGGL(keys_from_i32_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
                      keyseg, n, num_out, w.kin, w.vin, st);
   DR_LAUNCH_CHECK();
@@ -860,47 +867,66 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
   const int dv = dim / VEC;
   using R = Row<VEC, G, CPL>;
   using V = typename VecT<VEC>::T;
-  R x[NB];
-  int64_t uq[NB], rq[NB], sq[NB];
-  int tq[NB];
+  // -- keys of the NB positions and their neighbours: unconditional loads --
+  int64_t uk[NB + 2];
+#pragma unroll
+  for (int q = -1; q <= NB; ++q) {
+    int64_t pp = p0 + q;
+    pp = pp < 0 ? 0 : (pp >= N ? N - 1 : pp);
+    uk[q + 1] = (int64_t)skey[pp];
+  }
+  int64_t rsq[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    const int64_t u = uk[q + 1];
+    rsq[q] = run_start[u < N ? u : 0];
+  }
   bool head[NB], single[NB];
+  int64_t uq[NB], sq[NB];
+  int tq[NB];
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
     const int64_t p = p0 + q;
-    head[q] = single[q] = false;
-    uq[q] = -1;
-    rq[q] = -1;
-    sq[q] = p;
-    tq[q] = 0;
-    const float* rp = nullptr;
-    if (p < N) {
-      const int64_t u = (int64_t)skey[p];
-      const int64_t prev = p > 0 ? (int64_t)skey[p - 1] : -1;
-      const int64_t next = p + 1 < N ? (int64_t)skey[p + 1] : -1;
-      bool chunk_head = u != prev;
-      if (u < N && !chunk_head) {
-        sq[q] = run_start[u];
-        chunk_head = (p - sq[q]) % kGradChunk == 0;
-      }
-      if (u < N && chunk_head) {  // u == N: sentinel for out-of-range idx
-        const int t = table_of(g.koff, T, u, ufirst < N ? ufirst : 0);
-        const dr_pool_grad_desc& d = sd[t];
-        head[q] = true;
-        single[q] = u != next;
-        uq[q] = u;
-        tq[q] = t;
-        const int64_t k = (int64_t)perm[p] - g.koff[t];
-        const int64_t r = d.seg ? d.seg[k * d.seg_stride] : k;
-        if (r >= 0 && r < B) {
-          rp = d.top_grad + r * d.top_stride;
-          rq[q] = r;
-        } else {
-          latch(st, DR_INVALID_ARGUMENT);
-        }
-      }
-    }
-    load_row<VEC, G, CPL>(x[q], rp, lg, dv);
+    const int64_t u = uk[q + 1];
+    const bool in = p < N && u < N;  // u == N: sentinel for out-of-range idx
+    const bool rhead = p == 0 || uk[q] != u;
+    sq[q] = rhead ? p : rsq[q];
+    head[q] = in && (rhead || (p - sq[q]) % kGradChunk == 0);
+    single[q] = p + 1 >= N || uk[q + 2] != u;
+    uq[q] = u;
+    tq[q] = head[q] ? table_of(g.koff, T, u, ufirst < N ? ufirst : 0) : 0;
   }
+  // -- source rows of the head positions: one batch of unconditional loads --
+  int64_t rq[NB];
+  bool bad = false;
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    int64_t pp = p0 + q;
+    pp = pp >= N ? N - 1 : pp;
+    const int64_t k = (int64_t)perm[pp] - g.koff[tq[q]];
+    rq[q] = head[q] && k >= 0 && k < sd[tq[q]].nnz ? k : 0;
+  }
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    const int64_t* segp = sd[tq[q]].seg;
+    if (segp) rq[q] = segp[rq[q] * sd[tq[q]].seg_stride];
+  }
+  R x[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    const bool okr = rq[q] >= 0 && rq[q] < B;
+    bad |= head[q] && !okr;
+    if (!okr) rq[q] = -1;
+    load_row_u<VEC, G, CPL>(x[q], sd[tq[q]].top_grad + (okr ? rq[q] : 0) * sd[tq[q]].top_stride,
+                            lg, dv);
+  }
+#pragma unroll
+  for (int q = 0; q < NB; ++q)
+    if (rq[q] < 0) {
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) x[q].v[c] = vzero<V>();
+    }
+  if (bad) latch(st, DR_INVALID_ARGUMENT);
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
     if (!head[q]) continue;
@@ -932,34 +958,43 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
         acc_add(acc, x[q]);
     } else {
       const int64_t lim = c0 + kGradChunk < N ? c0 + kGradChunk : N;
+      const float* tg = d.top_grad;
+      const int64_t ts = d.top_stride;
+      const int64_t* segp = d.seg;
+      const int64_t sst = d.seg_stride;
+      const int64_t kt0 = g.koff[tq[q]];
+      const int64_t nnz_t = d.nnz;
+      bool cbad = false;
       for (int64_t p = c0; p < lim; p += kGradChain) {
         R y[kGradChain];
         int64_t ry[kGradChain];
         bool ok[kGradChain];
 #pragma unroll
-        for (int j = 0; j < kGradChain; ++j) {  // all key loads issued before any use
-          const int64_t kj = p + j < lim ? (int64_t)skey[p + j] : -1;
-          ok[j] = kj == u;  // monotone: sorted keys
+        for (int j = 0; j < kGradChain; ++j) {  // keys and sources: unconditional, clamped
+          const int64_t pj = p + j < N ? p + j : N - 1;
+          const int64_t kj = (int64_t)skey[pj];
+          ok[j] = (p + j < lim) & (kj == u);  // monotone: sorted keys
+          const int64_t k = (int64_t)perm[pj] - kt0;
+          ry[j] = ((k >= 0) & (k < nnz_t)) ? k : 0;
+        }
+        if (segp) {
+#pragma unroll
+          for (int j = 0; j < kGradChain; ++j) ry[j] = segp[ry[j] * sst];
         }
 #pragma unroll
         for (int j = 0; j < kGradChain; ++j) {
-          const float* rp = nullptr;
-          ry[j] = -1;
-          if (ok[j]) {
-            const int64_t k = (int64_t)perm[p + j] - g.koff[tq[q]];
-            const int64_t r = d.seg ? d.seg[k * d.seg_stride] : k;
-            if (r >= 0 && r < B) {
-              rp = d.top_grad + r * d.top_stride;
-              ry[j] = r;
-            } else {
-              latch(st, DR_INVALID_ARGUMENT);
-            }
-          }
-          load_row<VEC, G, CPL>(y[j], rp, lg, dv);
+          const bool okr = (ry[j] >= 0) & (ry[j] < B);
+          cbad |= ok[j] & !okr;
+          ry[j] = okr ? ry[j] : -1;
+          load_row_u<VEC, G, CPL>(y[j], tg + (okr ? ry[j] : 0) * ts, lg, dv);
         }
 #pragma unroll
         for (int j = 0; j < kGradChain; ++j) {
           if (!ok[j]) break;
+          if (ry[j] < 0) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) y[j].v[c] = vzero<V>();
+          }
           scaled(y[j], ry[j]);
           if (fresh) {
             acc = y[j];
@@ -970,6 +1005,7 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
         }
         if (!ok[kGradChain - 1]) break;
       }
+      if (cbad) latch(st, DR_INVALID_ARGUMENT);
     }
     if (first_chunk) {
       store_row<VEC, G, CPL>(acc, out + u * (int64_t)dim, lg, dv);
@@ -993,7 +1029,8 @@ __global__ __launch_bounds__(256) void grad_finish_kernel(const uint64_t* __rest
                                                           float* __restrict__ out,
                                                           const float* __restrict__ part,
                                                           const int32_t* __restrict__ longs,
-                                                          const int32_t* __restrict__ nlong) {
+                                                          const int32_t* __restrict__ nlong,
+                                                          int64_t nslots) {
   constexpr int GPB = 256 / G;
   const int n = *nlong;
   const int lg = threadIdx.x % G;
@@ -1003,16 +1040,19 @@ __global__ __launch_bounds__(256) void grad_finish_kernel(const uint64_t* __rest
        i += (int64_t)gridDim.x * GPB) {
     const int64_t u = longs[2 * i], c0 = longs[2 * i + 1];
     R acc;
-    load_row<VEC, G, CPL>(acc, out + u * (int64_t)dim, lg, dv);
+    load_row_u<VEC, G, CPL>(acc, out + u * (int64_t)dim, lg, dv);
+    const int64_t s0 = c0 / kGradChunk;  // c0's slot; chunk k of the run -> slot s0 + k
     for (int64_t c = c0 + kGradChunk; c < N; c += kGradChain * kGradChunk) {
       R y[kGradChain];
       bool ok[kGradChain];
 #pragma unroll
-      for (int j = 0; j < kGradChain; ++j) {
+      for (int j = 0; j < kGradChain; ++j) {  // unconditional, clamped loads
         const int64_t cj = c + j * kGradChunk;
-        ok[j] = cj < N && (int64_t)skey[cj] == u;
-        load_row<VEC, G, CPL>(y[j], ok[j] ? part + (cj / kGradChunk) * (int64_t)dim : nullptr,
-                              lg, dv);
+        const int64_t kj = (int64_t)skey[cj < N ? cj : N - 1];
+        ok[j] = (cj < N) & (kj == u);
+        int64_t sl = s0 + 1 + (c - c0 - kGradChunk) / kGradChunk + j;
+        sl = sl < nslots ? sl : nslots - 1;
+        load_row_u<VEC, G, CPL>(y[j], part + sl * (int64_t)dim, lg, dv);
       }
 #pragma unroll
       for (int j = 0; j < kGradChain; ++j)
@@ -1036,7 +1076,7 @@ static void launch_grad_csr(const GradGroup& g, int T, int64_t B, const uint64_t
                      g, T, B, skey, perm, w.run_start, dim, out, w.part, w.longs, w.nlong, st);
   if (N > kGradChunk)
     hipLaunchKernelGGL((grad_finish_kernel<VEC, G, CPL>), dim3(64), dim3(256), 0, s, skey, N, dim,
-                       out, w.part, w.longs, w.nlong);
+                       out, w.part, w.longs, w.nlong, N / kGradChunk + 2);
 }
 
 }  // namespace dr
@@ -1252,6 +1292,7 @@ int dr_pool_grad_grouped(const dr_pool_grad_desc* descs_host, int num_tables, in
   }
   const int64_t n = g.koff[num_tables];
   DR_REQUIRE(n < (1ll << 31), DR_INVALID_ARGUMENT, "too many nnz");
+  DR_REQUIRE(batch > 0 || n == 0, DR_INVALID_ARGUMENT, "nnz without a batch");
   DR_REQUIRE(ws_bytes >= dr_pool_grad_grouped_workspace_size(n), DR_INVALID_ARGUMENT,
              "workspace too small");
   if (n == 0) return DR_OK;

@@ -114,6 +114,7 @@ SIGNATURES = {
     "dr_ev_release": (_I32, [_P]),
     "dr_ev_size": (_I32, [_P, _P, _P]),
     "dr_ev_dim": (_I64, [_P]),
+    "dr_ev_shrink": (_I32, [_P, _I64, _F32, _P, _P]),
     "dr_ev_reserve": (_I32, [_P, _I64, _P]),
     "dr_ev_resolve_workspace_size": (_SZ, [_I64]),
     "dr_ev_resolve": (_I32, [_P, _P, _I64, _P, _P, _P, _P, _P, _SZ, _P]),

@@ -451,11 +451,20 @@ def write_ev_tensors(writer, tensor_key, offs, keys, vals, vers, frqs):
     writer.add(tensor_key + "-freqs", frqs)
 
 
-def save(prefix, variables):
-    """Saver.save for EVs: {tensor_key: EmbeddingVariable} -> one bundle."""
+def save(prefix, variables, global_step=None):
+    """Saver.save for EVs: {tensor_key: EmbeddingVariable} -> one bundle.
+
+    Like DumpEv (save_restore_v2_ops.cc:117-133), each variable's key space
+    is shrunk first (EmbeddingVar::Shrink: by L2 weight when the EV has an
+    l2_weight_threshold, else by global step when steps_to_live > 0), so
+    evicted keys are not written; global_step None skips the step eviction."""
     w = BundleWriter(prefix)
     for name in variables:
-        dump_embedding_values(variables[name], name, w)
+        ev = variables[name]
+        p = ev._primary or ev
+        if p.l2_weight_threshold != -1.0 or (global_step is not None and p.steps_to_live > 0):
+            ev.shrink(0 if global_step is None else global_step)
+        dump_embedding_values(ev, name, w)
     w.finish()
     return prefix
 

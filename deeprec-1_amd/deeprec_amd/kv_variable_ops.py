@@ -81,7 +81,8 @@ class EmbeddingVariable(object):
     """
 
     def __init__(self, name, embedding_dim, initializer=None, steps_to_live=0, ev_option=None,
-                 capacity=1 << 16, device=None, _primary=None, _slot_index=0):
+                 capacity=1 << 16, device=None, _primary=None, _slot_index=0,
+                 l2_weight_threshold=-1.0):
         _lib.require_gpu()
         self.name = name
         self.dim = int(embedding_dim)
@@ -98,6 +99,8 @@ class EmbeddingVariable(object):
         if opt.evict_option is not None and opt.evict_option.steps_to_live:
             steps_to_live = opt.evict_option.steps_to_live
         self.steps_to_live = int(steps_to_live or 0)
+        # EmbeddingConfig::l2_weight_threshold (embedding_config.h:17,28): -1 = off
+        self.l2_weight_threshold = float(l2_weight_threshold)
         default = _default_row(initializer, self.dim, self.device)
         self._default_host = default
         h = C.c_void_p()
@@ -261,13 +264,23 @@ class EmbeddingVariable(object):
     def reserve(self, extra):
         check(lib().dr_ev_reserve(self._h, int(extra), stream_handle(self.device)))
 
+    def shrink(self, global_step=0):
+        """EmbeddingVar::Shrink (embedding_var.h:264-313) on the key space this
+        EV shares with its slots: by L2 weight when l2_weight_threshold != -1,
+        else by global step when steps_to_live > 0.  Returns keys removed."""
+        p = self._primary or self
+        n = C.c_int64(0)
+        check(lib().dr_ev_shrink(p._h, int(global_step), p.l2_weight_threshold, C.byref(n),
+                                 stream_handle(self.device)))
+        return n.value
+
 
 _EV_REGISTRY = {}
 
 
 def get_embedding_variable(name, embedding_dim, key_dtype=torch.int64, initializer=None,
                            steps_to_live=0, ev_option=None, capacity=1 << 16, device=None,
-                           partitioner=None):
+                           partitioner=None, l2_weight_threshold=-1.0):
     """tf.get_embedding_variable (variable_scope.py:2142-2197).
 
     With `partitioner=n` (fixed_size_partitioner(num_shards=n)) returns a list
@@ -275,12 +288,13 @@ def get_embedding_variable(name, embedding_dim, key_dtype=torch.int64, initializ
     (embedding_ops.py:207-209)."""
     if partitioner is not None and int(partitioner) > 1:
         return [get_embedding_variable("%s/part_%d" % (name, p), embedding_dim, key_dtype,
-                                       initializer, steps_to_live, ev_option, capacity, device)
+                                       initializer, steps_to_live, ev_option, capacity, device,
+                                       l2_weight_threshold=l2_weight_threshold)
                 for p in range(int(partitioner))]
     if name in _EV_REGISTRY:
         return _EV_REGISTRY[name]
     ev = EmbeddingVariable(name, embedding_dim, initializer, steps_to_live, ev_option, capacity,
-                           device)
+                           device, l2_weight_threshold=l2_weight_threshold)
     _EV_REGISTRY[name] = ev
     return ev
 

@@ -1,10 +1,12 @@
-"""Model glue around the hot path: the DLRM and DeepFM
-training steps of DeepRec's modelzoo, built from this engine's ops.
+"""Model glue around the hot path: the DLRM, DeepFM, DIN
+and WDL training steps of DeepRec's modelzoo, and DCN-v2 (BASELINE
+configs[4]), built from this engine's ops.
 
 Only the embedding side and the interactions are this engine's kernels
 (EV lookup + pooled backward + KV optimizer, dot interaction fwd/bwd, FM
-second order fwd/bwd); the MLPs are plain library GEMMs (torch.nn.Linear ->
-hipBLASLt), as the north_star asks.
+second order fwd/bwd, DIN attention fwd/bwd, the bf16 MFMA cross layer);
+the MLPs are plain library GEMMs (torch.nn.Linear -> hipBLASLt), as the
+north_star asks.
 
 * DLRM: modelzoo/DLRM/train.py:105-290 -- bottom MLP over the 13 dense
   features (ReLU after every layer), `dot_op` over [bottom, e_1..e_26]
@@ -15,6 +17,9 @@ hipBLASLt), as the north_star asks.
   (dim-1) embeddings, FM second order over the field embeddings (:205-209),
   DNN over the concatenated embeddings, final DNN over [dnn, linear, fm],
   a last 1-unit layer, sigmoid.
+* DIN: modelzoo/DIN/script/model.py:11-150,368-392 (DIN class below).
+* WDL: modelzoo/WDL/train.py:182-335 (WDL class below).
+* DCN-v2: stacked cross network on the MFMA kernel (DCNv2 class below).
 
 Inputs are one-hot ids ([T, B] int64, Criteo hotness 1) and dense features
 [B, 13] fp32.
@@ -328,6 +333,48 @@ class DCNv2(torch.nn.Module):
         return torch.sigmoid(net).squeeze(1)
 
 
+class _SplitKLinearFn(torch.autograd.Function):
+    """y = x W^T + b whose weight gradient is a split-K GEMM: for the DIN
+    attention MLP x has B*T ~ 4e5 rows and W is 80 x 144, so dW = g^T x is a
+    K = 4e5 reduction onto a 1e4-element output, which one library GEMM runs
+    on ~15 workgroups (1 ms).  Here K is cut into S slices (a batched GEMM
+    with S x more workgroups) and the S partial products are summed."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, slices):
+        ctx.save_for_backward(x, weight)
+        ctx.slices = slices
+        return torch.nn.functional.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        gx = g @ weight
+        K = x.shape[0]
+        S = ctx.slices
+        while S > 1 and K % S:
+            S //= 2
+        if S > 1:
+            gw = torch.bmm(g.reshape(S, K // S, -1).transpose(1, 2),
+                           x.reshape(S, K // S, -1)).sum(0)
+        else:
+            gw = g.t() @ x
+        return gx, gw, g.sum(0), None
+
+
+class SplitKLinear(torch.nn.Linear):
+    """torch.nn.Linear with a split-K weight gradient for inputs of many rows."""
+
+    def __init__(self, n_in, n_out, slices=64):
+        super().__init__(n_in, n_out)
+        self.slices = slices
+
+    def forward(self, x):
+        shape = x.shape
+        y = _SplitKLinearFn.apply(x.reshape(-1, shape[-1]), self.weight, self.bias, self.slices)
+        return y.reshape(shape[:-1] + (self.out_features,))
+
+
 class Dice(torch.nn.Module):
     """dice() of modelzoo/DIN/script/utils.py:12-35 (batch statistics)."""
 
@@ -361,9 +408,9 @@ class DIN(torch.nn.Module):
         self.evs = [uid_ev, mid_ev, cat_ev]
         D = mid_ev.dim
         H = 2 * D
-        self.f1_att = torch.nn.Linear(4 * H, 80)
-        self.f2_att = torch.nn.Linear(80, 40)
-        self.f3_att = torch.nn.Linear(40, 1)
+        self.f1_att = SplitKLinear(4 * H, 80)
+        self.f2_att = SplitKLinear(80, 40)
+        self.f3_att = SplitKLinear(40, 1)
         n_in = uid_ev.dim + 4 * H
         self.bn1_gamma = torch.nn.Parameter(torch.ones(n_in))
         self.bn1_beta = torch.nn.Parameter(torch.zeros(n_in))

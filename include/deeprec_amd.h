@@ -239,6 +239,14 @@ int dr_ev_retain(dr_ev* ev);
 int dr_ev_release(dr_ev* ev);
 /* KvVariableShapeOp (kv_variable_ops.cc:58-75): number of keys.  Syncs.   */
 int dr_ev_size(dr_ev* ev, int64_t* size_host, void* stream);
+/* Save-time eviction EmbeddingVar::Shrink (embedding_var.h:264-313), as     */
+/* DumpEv runs it before a save (save_restore_v2_ops.cc:128-131):            */
+/* l2_weight_threshold != -1 drops keys with 0.5 * |row|^2 < threshold; else  */
+/* with steps_to_live > 0, version -1 becomes global_step and keys with      */
+/* global_step - version > steps_to_live are dropped.  Synchronises;         */
+/* *removed_host (nullable) = keys dropped.                                   */
+int dr_ev_shrink(dr_ev* ev, int64_t global_step, float l2_weight_threshold,
+                 int64_t* removed_host, void* stream);
 int64_t dr_ev_dim(dr_ev* ev);
 /* Ensures room for `extra` new keys (may rehash/grow; syncs when it must). */
 int dr_ev_reserve(dr_ev* ev, int64_t extra, void* stream);
