@@ -278,6 +278,118 @@ class ShardedLookup(object):
         return out
 
 
+class _ReduceScatterFn(torch.autograd.Function):
+    """out[B, C] = sum over ranks of their partial[rank's bags]; backward =
+    the all-gather of the gradient (every owner needs every rank's rows)."""
+
+    @staticmethod
+    def forward(ctx, partial, eng):
+        ctx.eng = eng
+        return eng._reduce_scatter(partial.contiguous())
+
+    @staticmethod
+    def backward(ctx, g):
+        return ctx.eng._all_gather_fixed(g.contiguous()), None
+
+
+class ReduceScatterShardedLookup(object):
+    """SOK's owner-side pooling for multi-hot bags (the DistributedEmbedding
+    of modelzoo/SOK: forward_functions.cuh:72-97 pools on the owner,
+    reduce_scatter_dispatcher.cu:45-52 sums the partial bags and scatters
+    the batch), over the same row sharding (owner = key % world):
+
+      1. all-gather the per-feature id counts, the ids (uneven sizes, one
+         all-to-all) and the CSR bag offsets of every rank;
+      2. owner: keep the ids it owns, pool them per global bag with the
+         fused lookup (combiner sum; bags without an owned id are 0) into a
+         [world * B, T * D] partial;
+      3. mean / sqrtn divide the partials by the global bag size, then
+         reduce-scatter (sum) -> this rank's [B, T * D].
+
+    Per bag the exchange carries T * D floats per rank pair instead of one
+    row per id: cheaper than the row all-to-all once bags hold more ids than
+    there are ranks.  Backward: the gradient is all-gathered and the owners'
+    lookups queue IndexedSlices of their own keys.  The per-bag sum is
+    associated per owner, then across owners, so results match the
+    single-GPU lookup to fp32 tolerance, not bit for bit.  _all_gather_fixed
+    / _all_gather_var / _reduce_scatter are torch.distributed collectives
+    (RCCL); tests replace them to run several ranks in one process."""
+
+    def __init__(self, evs, world, rank, batch, device, group=None):
+        self.evs = list(evs)
+        self.world, self.rank, self.batch = world, rank, batch
+        self.device = device
+        self.group = group
+        self.T = len(self.evs)
+        self.dim = self.evs[0].dim
+
+    # -- collectives -----------------------------------------------------
+    def _all_gather_fixed(self, t):
+        out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t, group=self.group)
+        return out.reshape((self.world * t.shape[0],) + tuple(t.shape[1:]))
+
+    def _all_gather_var(self, t, sizes):
+        out = torch.empty(int(sum(sizes)), dtype=t.dtype, device=t.device)
+        dist.all_to_all_single(out, t.repeat(self.world), list(sizes), [t.numel()] * self.world,
+                               group=self.group)
+        return out
+
+    def _reduce_scatter(self, t):
+        out = torch.empty((t.shape[0] // self.world,) + tuple(t.shape[1:]), dtype=t.dtype,
+                          device=t.device)
+        dist.reduce_scatter_tensor(out, t, group=self.group)
+        return out
+
+    # -- step ------------------------------------------------------------
+    def forward(self, ids, bag_offs, combiner="sum"):
+        """ids[t]: [nnz_t] int64 ids of feature t; bag_offs[t]: [B + 1] int32
+        CSR offsets of its bags.  Returns [B, T * D] (autograd-enabled: the
+        EVs receive their IndexedSlices on backward)."""
+        from .embedding_ops import SparseTensor, embedding_lookup_sparse_multi
+        if combiner not in ("sum", "mean", "sqrtn"):
+            raise ValueError("combiner must be one of 'sum', 'mean' or 'sqrtn'")
+        T, G, B, dev = self.T, self.world, self.batch, self.device
+        ids = [x.reshape(-1).to(torch.int64) for x in ids]
+        offs = torch.stack([o.to(torch.int64).reshape(-1) for o in bag_offs])       # [T, B+1]
+        if offs.shape != (T, B + 1):
+            raise ValueError("bag_offs must be T x [B + 1]")
+        nnz = torch.tensor([x.numel() for x in ids], dtype=torch.int64, device=dev)
+        sizes = self._all_gather_fixed(nnz).reshape(G, T).cpu()                      # host
+        per_rank = sizes.sum(1).tolist()
+        all_ids = self._all_gather_var(torch.cat(ids), per_rank)
+        all_offs = self._all_gather_fixed(offs).reshape(G, T, B + 1)
+        rank_base = [0]
+        for r in range(G):
+            rank_base.append(rank_base[-1] + int(per_rank[r]))
+        sps = []
+        for t in range(T):
+            vals, segs = [], []
+            for r in range(G):
+                a = rank_base[r] + int(sizes[r, :t].sum())
+                v = all_ids[a:a + int(sizes[r, t])]
+                o = all_offs[r, t]
+                seg = torch.repeat_interleave(torch.arange(B, device=dev) + r * B, o[1:] - o[:-1],
+                                              output_size=v.numel())
+                vals.append(v)
+                segs.append(seg)
+            v = torch.cat(vals)
+            seg = torch.cat(segs)
+            own = torch.nonzero(v % G == self.rank).reshape(-1)        # sizes: host sync
+            v, seg = v[own].contiguous(), seg[own]
+            ind = torch.stack([seg, torch.zeros_like(seg)], 1)
+            sps.append(SparseTensor(ind, v, (G * B, max(1, int(v.numel())))))
+        partial = embedding_lookup_sparse_multi(self.evs, sps, combiner="sum")   # [G*B, T*D]
+        if combiner != "sum":            # the global bag sizes are known to every owner
+            cnt = (all_offs[:, :, 1:] - all_offs[:, :, :-1]).permute(0, 2, 1)
+            cnt = cnt.reshape(G * B, T).to(torch.float32)
+            if combiner == "sqrtn":
+                cnt = torch.sqrt(cnt)
+            cnt = torch.where(cnt > 0, cnt, torch.ones_like(cnt))
+            partial = (partial.view(G * B, T, self.dim) / cnt[:, :, None]).reshape(G * B, -1)
+        return _ReduceScatterFn.apply(partial, self)                             # [B, T*D]
+
+
 class XgmiBuffers(object):
     """One rank's exchange buffers for XgmiShardedLookup (torch allocations
     shared with the peers through HIP IPC): the inbox that requesters write
