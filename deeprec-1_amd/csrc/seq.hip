@@ -288,6 +288,7 @@ int dr_din_attention_input(const float* query, const float* facts, int64_t batch
                            int hidden, float* out, void* stream) {
   using namespace dr;
   DR_REQUIRE(batch >= 0 && seq_len >= 0 && hidden > 0, DR_INVALID_ARGUMENT, "bad shape");
+  if (batch * seq_len == 0) return DR_OK;
   DR_REQUIRE(query && facts && out, DR_INVALID_ARGUMENT, "null operand");
   const int vec = seq_vec(hidden, (uintptr_t)query | (uintptr_t)facts | (uintptr_t)out);
   DR_REQUIRE(vec > 0, DR_INVALID_ARGUMENT,
@@ -311,13 +312,13 @@ int dr_din_attention_input_grad(const float* query, const float* facts, const fl
   using namespace dr;
   DR_REQUIRE(batch >= 0 && seq_len >= 0 && hidden > 0, DR_INVALID_ARGUMENT, "bad shape");
   DR_REQUIRE(batch < (1ll << 31), DR_INVALID_ARGUMENT, "batch must be < 2^31");
+  if (batch == 0) return DR_OK;
   DR_REQUIRE(query && facts && top_grad && grad_query && grad_facts, DR_INVALID_ARGUMENT,
              "null operand");
   const int vec = seq_vec(hidden, (uintptr_t)query | (uintptr_t)facts | (uintptr_t)top_grad |
                                       (uintptr_t)grad_facts);
   DR_REQUIRE(vec > 0, DR_INVALID_ARGUMENT,
              "dr_din_attention_input_grad: hidden must be <= 64, or a multiple of 4 <= 256");
-  if (batch == 0) return DR_OK;
   if (vec == 4)
     hipLaunchKernelGGL(din_input_grad_kernel<4>, dim3((unsigned)batch), dim3(64), 0, S(stream),
                        query, facts, top_grad, seq_len, hidden, grad_query, grad_facts,
@@ -338,11 +339,11 @@ int dr_din_attention_pool(const float* scores, const float* mask, const float* f
              "bad shape (seq_len must be >= 1)");
   DR_REQUIRE(batch < (1ll << 31) && seq_len <= 8192, DR_INVALID_ARGUMENT,
              "batch must be < 2^31 and seq_len <= 8192");
+  if (batch == 0) return DR_OK;
   DR_REQUIRE(scores && mask && facts && att_out && alphas, DR_INVALID_ARGUMENT, "null operand");
   const int vec = seq_vec(hidden, (uintptr_t)facts);
   DR_REQUIRE(vec > 0, DR_INVALID_ARGUMENT,
              "dr_din_attention_pool: hidden must be <= 64, or a multiple of 4 <= 256");
-  if (batch == 0) return DR_OK;
   const size_t lds = (size_t)(((seq_len + 3) & ~3ll) + 2 * 64 * vec) * sizeof(float);
   if (vec == 4)
     hipLaunchKernelGGL(din_pool_kernel<4>, dim3((unsigned)batch), dim3(64), lds, S(stream),
@@ -363,13 +364,13 @@ int dr_din_attention_pool_grad(const float* alphas, const float* mask, const flo
              "bad shape (seq_len must be >= 1)");
   DR_REQUIRE(batch < (1ll << 31) && seq_len <= 8192, DR_INVALID_ARGUMENT,
              "batch must be < 2^31 and seq_len <= 8192");
+  if (batch == 0) return DR_OK;
   DR_REQUIRE(alphas && mask && facts && grad_att && grad_scores && grad_facts,
              DR_INVALID_ARGUMENT, "null operand");
   const int vec = seq_vec(hidden, (uintptr_t)facts | (uintptr_t)grad_att | (uintptr_t)grad_sum |
                                       (uintptr_t)grad_facts);
   DR_REQUIRE(vec > 0, DR_INVALID_ARGUMENT,
              "dr_din_attention_pool_grad: hidden must be <= 64, or a multiple of 4 <= 256");
-  if (batch == 0) return DR_OK;
   const size_t lds = (size_t)(2 * ((seq_len + 3) & ~3ll) + 64) * sizeof(float);
   if (vec == 4)
     hipLaunchKernelGGL(din_pool_grad_kernel<4>, dim3((unsigned)batch), dim3(64), lds, S(stream),

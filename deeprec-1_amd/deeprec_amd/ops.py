@@ -40,6 +40,14 @@ def _c(t, dtype):
     return t.to(dtype).contiguous()
 
 
+def _inner(t):
+    """Elements per row of a [n, ...] tensor (also when n == 0)."""
+    k = 1
+    for x in t.shape[1:]:
+        k *= int(x)
+    return k
+
+
 # ---------------------------------------------------------------------------
 # Unique (UniqueAliOp, core/kernels/unique_ali_op.cc:46-180)
 # ---------------------------------------------------------------------------
@@ -143,7 +151,7 @@ def gather(params, indices):
 def _segment_reduce(data, indices, segment_ids, num_segments, combiner):
     dev = _dev(data)
     data = _c(data, torch.float32)
-    data2 = data.reshape(data.shape[0], -1)
+    data2 = data.reshape(data.shape[0], _inner(data))
     idx = _c(indices, torch.int32)
     seg = _c(segment_ids, torch.int32)
     if num_segments is None:  # output rows = last segment id + 1 (reference CPU)
@@ -174,7 +182,7 @@ def sparse_segment_sqrt_n(data, indices, segment_ids, num_segments=None):
 def _segment_grad(grad, indices, segment_ids, output_dim0, combiner):
     dev = _dev(grad)
     grad = _c(grad, torch.float32)
-    g2 = grad.reshape(grad.shape[0], -1)
+    g2 = grad.reshape(grad.shape[0], _inner(grad))
     idx = _c(indices, torch.int32)
     seg = _c(segment_ids, torch.int32)
     D = g2.shape[1]
@@ -206,7 +214,7 @@ def unsorted_segment_sum(data, segment_ids, num_segments):
     """UnsortedSegmentSum (segment_reduction_ops.cc:377-405): serial order, seg<0 skipped."""
     dev = _dev(data)
     data = _c(data, torch.float32)
-    d2 = data.reshape(data.shape[0], -1)
+    d2 = data.reshape(data.shape[0], _inner(data))
     seg = _c(segment_ids, torch.int32)
     D = d2.shape[1]
     out = torch.empty((num_segments, D), dtype=torch.float32, device=dev)

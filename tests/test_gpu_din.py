@@ -169,3 +169,18 @@ def test_din_train_step_matches_torch_reference():
     for t in range(3):
         want = W[t] - lr * W[t].grad
         torch.testing.assert_close(_ev_rows(evs[t], R[t]), want.detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_din_attention_empty_batch():
+    from deeprec_amd import ops
+    f = torch.zeros(0, 5, 36, device=DEV)
+    q = torch.zeros(0, 36, device=DEV)
+    assert ops.din_attention_input(q, f).shape == (0, 5, 144)
+    gq, gf = ops.din_attention_input_grad(q, f, torch.zeros(0, 5, 144, device=DEV))
+    assert gq.shape == (0, 36) and gf.shape == (0, 5, 36)
+    att, hs, al = ops.din_attention_pool(torch.zeros(0, 5, device=DEV),
+                                         torch.zeros(0, 5, device=DEV), f)
+    assert att.shape == (0, 36) and al.shape == (0, 5)
+    gs, gf = ops.din_attention_pool_grad(al, torch.zeros(0, 5, device=DEV), f,
+                                         torch.zeros(0, 36, device=DEV))
+    assert gs.shape == (0, 5)

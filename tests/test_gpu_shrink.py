@@ -98,3 +98,10 @@ def test_save_applies_shrink(dr, tmp_path):
     ck.save(prefix, {"emb": ev}, global_step=6)
     r = ck.BundleReader(prefix)
     assert sorted(r.lookup_rows("emb-keys", 0, 2).tolist()) == [2, 3]
+
+
+def test_shrink_empty_ev(dr):
+    ev = dr.EmbeddingVariable("shrink_empty", 4, 0.0, steps_to_live=3)
+    assert ev.shrink(10) == 0
+    assert int(ev.total_count()[0]) == 0
+    assert ev.export()[0].numel() == 0

@@ -151,3 +151,23 @@ def test_wdl_reference_optimizers_step():
     for ev, b in zip(model.evs, before):
         assert not torch.equal(_rows(ev, R), b)
     assert float(model.linear_bias.detach().abs()) > 0
+
+
+def test_ev_ftrl_empty_and_first_touch_slots(orc):
+    """n = 0 is a no-op; a key first seen by the apply starts from the
+    variable's and the slots' defaults (LookupOrCreateKey)."""
+    import deeprec_amd as dr
+    ev = dr.EmbeddingVariable("ftrl_edge", 4, 0.5)
+    opt = dr.FtrlOptimizer(0.1, l1_regularization_strength=0.0)
+    ev.pending_grads.append(dr.IndexedSlices(torch.zeros(0, 4, device=DEV),
+                                             torch.zeros(0, dtype=torch.int64, device=DEV)))
+    opt.apply_gradients([ev], global_step=0)
+    assert int(ev.total_count()[0]) == 0
+    g = np.full((1, 4), 0.25, np.float32)
+    ev.pending_grads.append(dr.IndexedSlices(T(g), T([42])))
+    opt.apply_gradients([ev], global_step=1)
+    oev = orc.EV(4, 0.5)
+    oacc, olin = oev.create_slot(1, 0.1), oev.create_slot(2, 0.0)
+    oev.apply_ftrl(oacc, olin, 0.1, 0.0, 0.0, -0.5, 0.0, g, np.array([42]), 1)
+    np.testing.assert_allclose(ev.sparse_read(T([42])).cpu().numpy(), oev.gather(np.array([42])),
+                               rtol=1e-6)

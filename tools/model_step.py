@@ -7,7 +7,7 @@ history lengths U[1, maxlen], Adam as in the reference).  Prints one JSON
 line with samples/s and the per-phase split.  A measurement aid for
 SURVEY 8f #4; bench.py's headline metric is the forward lookup.
 
-  python tools/model_step.py [--model dlrm|deepfm|din|dcn] [--rows 12500000] [--dim 128]
+  python tools/model_step.py [--model dlrm|deepfm|din|dcn|wdl] [--rows 12500000] [--dim 128]
 """
 import argparse
 import json
@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.join(ROOT, "deeprec-1_amd"))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="dlrm", choices=["dlrm", "deepfm", "din", "dcn"])
+    ap.add_argument("--model", default="dlrm", choices=["dlrm", "deepfm", "din", "dcn", "wdl"])
     ap.add_argument("--maxlen", type=int, default=100, help="DIN history length bound")
     ap.add_argument("--tables", type=int, default=26)
     ap.add_argument("--rows", type=int, default=12_500_000)
@@ -41,6 +41,9 @@ def main():
     if args.model == "din":
         args.batch = args.batch or 4096
         return din(args, dr, mz, dev)
+    if args.model == "wdl":
+        args.batch = args.batch or 65536
+        return wdl(args, dr, mz, dev)
     args.batch = args.batch or 65536
     T, D, B, R = args.tables, args.dim, args.batch, args.rows
     t0 = time.perf_counter()
@@ -84,6 +87,56 @@ def main():
                       "lookups_per_s": round(T * B * args.steps / el, 1),
                       "ms_per_step": round(el / args.steps * 1e3, 3), "batch": B, "tables": T,
                       "rows": R, "dim": D, "opt": args.opt, "bf16_mlp": args.bf16, "loss": float(loss)}), flush=True)
+
+
+# modelzoo/WDL/train.py:23-81: per-column hash buckets and embedding dims
+WDL_BUCKETS = [2500, 2000, 300000, 250000, 1000, 100, 20000, 4000, 20, 100000, 10000, 250000,
+               40000, 100, 100, 200000, 50, 10000, 4000, 20, 250000, 100, 100, 250000, 400, 100000]
+WDL_DIMS = [64, 64, 128, 128, 64, 64, 64, 64, 64, 128, 64, 128, 64, 64, 64, 128, 64, 64, 64, 64,
+            128, 64, 64, 128, 64, 128]
+
+
+def wdl(args, dr, mz, dev):
+    """WDL step (configs[0]'s model, here on the GPU): 26 categorical columns
+    with the reference's bucket sizes and dims, 13 numeric columns, dnn
+    [1024, 512, 256]; Adagrad 0.01 (deep) and FTRL 0.2 (linear) as
+    modelzoo/WDL/train.py:302-335."""
+    B = args.batch
+    cats = ["C%d" % (i + 1) for i in range(26)]
+    nums = ["I%d" % (i + 1) for i in range(13)]
+    deep, wide = [], []
+    for i, (r, d) in enumerate(zip(WDL_BUCKETS, WDL_DIMS)):
+        ev = dr.EmbeddingVariable("wdl_d%d" % i, d, 0.0, capacity=r + (1 << 16), device=dev)
+        ev.insert_synthetic(0, r, seed=900 + i)
+        deep.append(ev)
+        ew = dr.EmbeddingVariable("wdl_w%d" % i, 1, 0.0, capacity=r + (1 << 16), device=dev)
+        ew.insert_synthetic(0, r, seed=950 + i)
+        wide.append(ew)
+    model = mz.WDL(cats, deep, wide, nums).to(dev)
+    deep_opt = torch.optim.Adagrad(model.deep_parameters(), lr=0.01,
+                                   initial_accumulator_value=0.1)
+    ftrl = dr.FtrlOptimizer(0.2)
+    adagrad = dr.AdagradOptimizer(0.01)
+    g = torch.Generator(device=dev)
+    g.manual_seed(2021)
+    bk = torch.tensor(WDL_BUCKETS, device=dev)[:, None]
+    batches = [(torch.rand(B, 13, generator=g, device=dev),
+                (torch.rand(26, B, generator=g, device=dev) * bk).to(torch.int64),
+                (torch.rand(B, generator=g, device=dev) > 0.5).float()) for _ in range(4)]
+    for i in range(args.warmup):
+        mz.wdl_train_step(model, *batches[i % 4], deep_opt, adagrad, ftrl, ftrl, i)
+    torch.cuda.synchronize()
+    print("[model_step] warmup ok", file=sys.stderr, flush=True)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = mz.wdl_train_step(model, *batches[i % 4], deep_opt, adagrad, ftrl, ftrl, i)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    dr.status_check(dev)
+    print(json.dumps({"model": "wdl", "samples_per_s": round(B * args.steps / el, 1),
+                      "lookups_per_s": round(52 * B * args.steps / el, 1),
+                      "ms_per_step": round(el / args.steps * 1e3, 3), "batch": B,
+                      "opt": "adagrad+ftrl", "loss": float(loss.detach())}), flush=True)
 
 
 def din(args, dr, mz, dev):
