@@ -380,13 +380,14 @@ __global__ __launch_bounds__(256) void crossnet_kernel(const uint16_t* __restric
 static constexpr int CG_BM = 128, CG_BN = 128, CG_BK = 64;
 static constexpr int CG_TILE_BYTES = CG_BM * CG_BK * 2;  // 16 KB per operand per buffer
 
-__device__ __forceinline__ void cg_stage(const uint16_t* __restrict__ X, int64_t rows_valid,
-                                         int64_t row0, int d, int k0, char* lds_tile, int wave,
-                                         int lane) {
-  // 16 wave instructions of 8 rows x 128 B cover the 128-row tile; 4 per wave
+template <int NI>
+__device__ __forceinline__ void cg_stage_n(const uint16_t* __restrict__ X, int64_t rows_valid,
+                                           int64_t row0, int d, int k0, char* lds_tile, int wave,
+                                           int lane) {
+  // NI wave instructions of 8 rows x 128 B per wave cover waves * NI * 8 rows
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r0 = (wave * 4 + i) * 8;
+  for (int i = 0; i < NI; ++i) {
+    const int r0 = (wave * NI + i) * 8;
     const int r = r0 + (lane >> 3);
     const int pc = lane & 7;
     const int lc = pc ^ ((r >> 1) & 7);
@@ -397,6 +398,12 @@ __device__ __forceinline__ void cg_stage(const uint16_t* __restrict__ X, int64_t
                                      (__attribute__((address_space(3))) void*)(lds_tile + r0 * 128),
                                      16, 0, 0);
   }
+}
+
+__device__ __forceinline__ void cg_stage(const uint16_t* __restrict__ X, int64_t rows_valid,
+                                         int64_t row0, int d, int k0, char* lds_tile, int wave,
+                                         int lane) {
+  cg_stage_n<4>(X, rows_valid, row0, d, k0, lds_tile, wave, lane);
 }
 
 __device__ __forceinline__ bf16x8 cg_frag(const char* lds_tile, int r, int lc) {
@@ -467,6 +474,127 @@ __global__ __launch_bounds__(256, 2) void crossnet_glds_kernel(
   // so the four row groups of one store hit different banks), then reads it
   // back 8 columns per lane: x0 / xl / out / lin move as 16-B vectors, 8
   // lanes per 128-B row segment.
+  float* ct = reinterpret_cast<float*>(lds) + wave * 64 * 64;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i * 16 + fq * 4 + r;
+        const int col = (j * 16 + fr) ^ (((row >> 2) & 3) << 4);
+        ct[row * 64 + col] = acc[i][j][r];
+      }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int idx = it * 64 + lane;
+    const int row = idx >> 3, cc = (idx & 7) * 8;
+    const int64_t grow = m0 + wm * 64 + row;
+    const int gcol = n0 + wn * 64 + cc;
+    if (grow >= M || gcol >= d) continue;
+    const int pc = cc ^ (((row >> 2) & 3) << 4);
+    const float4 l0 = *reinterpret_cast<const float4*>(ct + row * 64 + pc);
+    const float4 l1 = *reinterpret_cast<const float4*>(ct + row * 64 + pc + 4);
+    float lin[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+    if (bias) {
+      const float4 b0 = *reinterpret_cast<const float4*>(bias + gcol);
+      const float4 b1 = *reinterpret_cast<const float4*>(bias + gcol + 4);
+      lin[0] += b0.x; lin[1] += b0.y; lin[2] += b0.z; lin[3] += b0.w;
+      lin[4] += b1.x; lin[5] += b1.y; lin[6] += b1.z; lin[7] += b1.w;
+    }
+    const int64_t o = grow * d + gcol;
+    const u32x4 a0 = *reinterpret_cast<const u32x4*>(x0 + o);
+    const u32x4 al = *reinterpret_cast<const u32x4*>(xl + o);
+    u32x4 ov, lv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t p0 = a0[e], pl = al[e];
+      const float v0 = bf2f((uint16_t)(p0 & 0xffff)) * lin[2 * e] + bf2f((uint16_t)(pl & 0xffff));
+      const float v1 = bf2f((uint16_t)(p0 >> 16)) * lin[2 * e + 1] + bf2f((uint16_t)(pl >> 16));
+      ov[e] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+      lv[e] = (uint32_t)f2bf(lin[2 * e]) | ((uint32_t)f2bf(lin[2 * e + 1]) << 16);
+    }
+    *reinterpret_cast<u32x4*>(out + o) = ov;
+    if (lin_out) *reinterpret_cast<u32x4*>(lin_out + o) = lv;
+  }
+}
+
+// The same layer with a 256 x 128 tile, 8 waves (4 x 2, each 64 x 64) and
+// three LDS stages (3 x 48 KB, one block per CU): two K tiles stay in
+// flight, and a K step needs ONE barrier -- wait for this wave's DMAs of
+// tile kt (vmcnt(6): tile kt+1's six may remain), s_barrier (every wave's
+// landed, and every wave is done reading tile kt-1's buffer), then issue
+// tile kt+2 into that buffer and multiply tile kt.
+static constexpr int C3_BM = 256, C3_BN = 128, C3_BK = 64;
+static constexpr int C3_A_BYTES = C3_BM * C3_BK * 2, C3_B_BYTES = C3_BN * C3_BK * 2;
+static constexpr int C3_STAGE = C3_A_BYTES + C3_B_BYTES;  // 48 KB
+
+__global__ __launch_bounds__(512, 1) void crossnet_glds3_kernel(
+    const uint16_t* __restrict__ x0, const uint16_t* __restrict__ xl,
+    const uint16_t* __restrict__ W, const float* __restrict__ bias, int64_t M, int d,
+    uint16_t* __restrict__ out, uint16_t* __restrict__ lin_out) {
+  __shared__ __attribute__((aligned(1024))) char lds[3 * C3_STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;  // 4 x 2 waves
+  const int64_t nwg = (int64_t)gridDim.x;
+  const int64_t orig = blockIdx.x;
+  const int64_t xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t tile = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int ntn = d / C3_BN + (d % C3_BN ? 1 : 0);
+  const int64_t m0 = (tile / ntn) * C3_BM;
+  const int n0 = (int)(tile % ntn) * C3_BN;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = d / C3_BK;
+  // prologue: tiles 0 and 1 in flight (6 DMAs per wave per tile)
+  cg_stage_n<4>(xl, M, m0, d, 0, lds, wave, lane);
+  cg_stage_n<2>(W, d, n0, d, 0, lds + C3_A_BYTES, wave, lane);
+  if (nk > 1) {
+    cg_stage_n<4>(xl, M, m0, d, C3_BK, lds + C3_STAGE, wave, lane);
+    cg_stage_n<2>(W, d, n0, d, C3_BK, lds + C3_STAGE + C3_A_BYTES, wave, lane);
+  }
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // tile kt landed (this wave)
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // ... every wave's, and tile kt-1's buffer is free
+    asm volatile("" ::: "memory");
+    if (kt + 2 < nk) {
+      char* nxt = lds + ((kt + 2) % 3) * C3_STAGE;
+      cg_stage_n<4>(xl, M, m0, d, (kt + 2) * C3_BK, nxt, wave, lane);
+      cg_stage_n<2>(W, d, n0, d, (kt + 2) * C3_BK, nxt + C3_A_BYTES, wave, lane);
+    }
+    const char* sA = lds + (kt % 3) * C3_STAGE;
+    const char* sB = sA + C3_A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[4], fb[4];
+      const int lc = kk * 4 + fq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = cg_frag(sA, wm * 64 + i * 16 + fr, lc);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = cg_frag(sB, wn * 64 + j * 16 + fr, lc);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // every wave done with the last tile before LDS is reused
+  asm volatile("" ::: "memory");
+  // epilogue through LDS, as crossnet_glds_kernel (a 16 KB region per wave)
   float* ct = reinterpret_cast<float*>(lds) + wave * 64 * 64;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -614,6 +742,16 @@ int dr_crossnet_forward_bf16(const uint16_t* x0, const uint16_t* xl, const uint1
   if (batch == 0) return DR_OK;
   static const bool legacy = getenv("DR_CROSSNET_LEGACY") != nullptr;
   const bool al16 = (((uintptr_t)bias | (uintptr_t)out | (uintptr_t)lin_out) & 15) == 0;
+  static const int variant = getenv("DR_CROSSNET_VARIANT") ? atoi(getenv("DR_CROSSNET_VARIANT"))
+                                                           : 3;
+  if (d % C3_BK == 0 && !legacy && al16 && variant == 3) {
+    const int64_t tiles = ceil_div(batch, C3_BM) * ceil_div(d, C3_BN);
+    DR_REQUIRE(tiles < (1ll << 31), DR_INVALID_ARGUMENT, "batch too large");
+    hipLaunchKernelGGL(crossnet_glds3_kernel, dim3((unsigned)tiles), dim3(512), 0, S(stream), x0,
+                       xl, W, bias, batch, d, out, lin_out);
+    DR_LAUNCH_CHECK();
+    return DR_OK;
+  }
   if (d % CG_BK == 0 && !legacy && al16) {
     const int64_t tiles = ceil_div(batch, CG_BM) * ceil_div(d, CG_BN);
     DR_REQUIRE(tiles < (1ll << 31), DR_INVALID_ARGUMENT, "batch too large");
