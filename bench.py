@@ -355,14 +355,17 @@ def main():
             "kernel": "dr::ev_lookup_onehot_kernel<4,32,1,ALI,4> (+ 3 miss-list kernels, empty)",
             "kernel_ms": round(k_ms, 4),
             "bytes_per_launch": bytes_launch, "bytes_per_lookup": per_lookup}
-    pmc = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            j = json.load(open(pmc))
-            if j.get("kernel") == "ev_lookup_onehot_kernel":  # PMC of this same kernel only
-                roof["traffic"] = j.get("bytes_per_launch")
-        except Exception:
-            pass
+    for obj, fname, kname in ((roof, "r01_pmc_traffic.json", "ev_lookup_onehot_kernel"),
+                              (roof_gather, "r01_pmc_traffic_row_gather.json",
+                               "pool_onehot_kernel")):
+        pmc = os.path.join(ROOT, "profiles", fname)
+        if os.path.exists(pmc):
+            try:
+                j = json.load(open(pmc))
+                if j.get("kernel") == kname:  # PMC of this same kernel only
+                    obj["traffic"] = j.get("bytes_per_launch")
+            except Exception:
+                pass
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 outputs of a bench run into profiles/.
 
-  python tools/pmc_summary.py <stats_dir> <fetch_dir> <write_dir> <round> [kernel]
+  python tools/pmc_summary.py <stats_dir> <fetch_dir> <write_dir> <round> [kernel] [tag]
 
 * <stats_dir>/*_kernel_stats.csv   (rocprofv3 --kernel-trace --stats --output-format csv)
 * <fetch_dir>/*_counter_collection.csv (rocprofv3 --pmc FETCH_SIZE, own pass)
@@ -9,8 +9,8 @@
 FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  gfx950 correction
 (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half the bytes of a
 wide (16 B/lane) coalesced read stream, so it is doubled; WRITE_SIZE is exact
-for 16 B/lane stores.  Writes profiles/<round>_pmc_traffic.json and copies
-the kernel stats CSV to profiles/<round>_bench_kernel_stats.csv.
+for 16 B/lane stores.  Writes profiles/<round>_pmc_traffic[_<tag>].json and
+copies the kernel stats CSV to profiles/<round>_bench_kernel_stats.csv.
 """
 import csv
 import glob
@@ -36,6 +36,7 @@ def main():
     stats_dir, fetch_dir, write_dir, rnd = sys.argv[1:5]
     if len(sys.argv) > 5:
         KERNEL = sys.argv[5]
+    tag = ("_" + sys.argv[6]) if len(sys.argv) > 6 else ""
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     st = glob.glob(os.path.join(stats_dir, "*_kernel_stats.csv"))[0]
@@ -60,7 +61,7 @@ def main():
         "bytes_per_launch": f_b + w_b,
         "kernel_avg_ns_rocprof": avg_ns,
     }
-    json.dump(out, open(os.path.join(prof, "%s_pmc_traffic.json" % rnd), "w"), indent=1)
+    json.dump(out, open(os.path.join(prof, "%s_pmc_traffic%s.json" % (rnd, tag)), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
