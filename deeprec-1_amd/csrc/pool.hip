@@ -833,7 +833,8 @@ struct GradWs {
   int32_t* longs;
   float* part;
 };
-static constexpr int kGradChain = 8;  // positions of a chunk fetched per step
+static constexpr int kGradChain = 8;         // positions of a chunk fetched per step
+static constexpr int kGradFinishChain = 32;  // chunk partials of a long run fetched per step
 
 // run_start[u] = first sorted position of row u; clears the long-run count.
 __global__ void grad_run_start_kernel(const uint64_t* __restrict__ skey, int64_t N,
@@ -1042,11 +1043,15 @@ __global__ __launch_bounds__(256) void grad_finish_kernel(const uint64_t* __rest
     R acc;
     load_row_u<VEC, G, CPL>(acc, out + u * (int64_t)dim, lg, dv);
     const int64_t s0 = c0 / kGradChunk;  // c0's slot; chunk k of the run -> slot s0 + k
-    for (int64_t c = c0 + kGradChunk; c < N; c += kGradChain * kGradChunk) {
-      R y[kGradChain];
-      bool ok[kGradChain];
+    // <= 128 floats of rows in flight per lane
+    constexpr int FC = 128 / (VEC * CPL) < 8 ? 8
+                       : (128 / (VEC * CPL) > kGradFinishChain ? kGradFinishChain
+                                                               : 128 / (VEC * CPL));
+    for (int64_t c = c0 + kGradChunk; c < N; c += FC * kGradChunk) {
+      R y[FC];
+      bool ok[FC];
 #pragma unroll
-      for (int j = 0; j < kGradChain; ++j) {  // unconditional, clamped loads
+      for (int j = 0; j < FC; ++j) {  // unconditional, clamped loads
         const int64_t cj = c + j * kGradChunk;
         const int64_t kj = (int64_t)skey[cj < N ? cj : N - 1];
         ok[j] = (cj < N) & (kj == u);
@@ -1055,9 +1060,9 @@ __global__ __launch_bounds__(256) void grad_finish_kernel(const uint64_t* __rest
         load_row_u<VEC, G, CPL>(y[j], part + sl * (int64_t)dim, lg, dv);
       }
 #pragma unroll
-      for (int j = 0; j < kGradChain; ++j)
+      for (int j = 0; j < FC; ++j)
         if (ok[j]) acc_add(acc, y[j]);
-      if (!ok[kGradChain - 1]) break;
+      if (!ok[FC - 1]) break;
     }
     store_row<VEC, G, CPL>(acc, out + u * (int64_t)dim, lg, dv);
   }
