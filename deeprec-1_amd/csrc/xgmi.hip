@@ -94,6 +94,82 @@ __global__ void xgmi_counts_kernel(XgmiArgs a, const unsigned long long* __restr
   __threadfence_system();
 }
 
+
+// ---- backward (owner side): pull the requesters' gradient rows ---------------
+// The inbox entries of source s (positions [0, cnt[s]) of region s) are
+// compacted to e = prefix[s] + i, sorted by (table, source, slot) -- slot is
+// unique per source, so the order is canonical whatever order the route
+// kernel's atomics placed them in -- and each sorted entry copies its key and
+// the requester's gradient row gin[s][slot] (read over xGMI) into the output.
+struct XgmiPullArgs {
+  int32_t world;
+  int64_t cap;
+  int64_t prefix[DR_MAX_PEERS + 1];
+  const float* gin[DR_MAX_PEERS];
+};
+
+__device__ __forceinline__ int pull_source(const XgmiPullArgs& a, int64_t e) {
+  int s = 0;
+  while (s + 1 < a.world && e >= a.prefix[s + 1]) ++s;
+  return s;
+}
+
+__global__ void xgmi_grad_keys_kernel(XgmiPullArgs a, const int32_t* __restrict__ inbox_slot,
+                                      int T, int64_t TB, int64_t R, uint64_t* __restrict__ kin,
+                                      int32_t* __restrict__ vin) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= R) return;
+  const int s = pull_source(a, e);
+  const int64_t slot = inbox_slot[(int64_t)s * a.cap + (e - a.prefix[s])];
+  const int64_t t = slot % T;
+  kin[e] = (uint64_t)(t * a.world + s) * (uint64_t)TB + (uint64_t)slot;
+  vin[e] = (int32_t)e;
+}
+
+// one 64-lane wave per sorted entry, 4 per block
+__global__ __launch_bounds__(256) void xgmi_grad_pull_kernel(
+    XgmiPullArgs a, const int64_t* __restrict__ inbox_keys, const int32_t* __restrict__ inbox_slot,
+    const int32_t* __restrict__ perm, int64_t R, int dim, int64_t row_stride,
+    int64_t* __restrict__ keys_out, float* __restrict__ grads_out) {
+  const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= R) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t e = perm[p];
+  const int s = pull_source(a, e);
+  const int64_t at = (int64_t)s * a.cap + (e - a.prefix[s]);
+  const int64_t slot = inbox_slot[at];
+  if (lane == 0) keys_out[p] = inbox_keys[at];
+  // slot j = b*T + t of the requester's [B, T*dim] gradient: row b, column t*dim
+  const int64_t T = row_stride / dim;
+  const int64_t b = slot / T, t = slot - b * T;
+  const float* g = a.gin[s] + b * row_stride + t * dim;
+  float* o = grads_out + p * (int64_t)dim;
+  if ((dim & 3) == 0) {
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    float4* o4 = reinterpret_cast<float4*>(o);
+    for (int c = lane; c < dim / 4; c += 64) o4[c] = g4[c];
+  } else {
+    for (int c = lane; c < dim; c += 64) o[c] = g[c];
+  }
+}
+
+// table_start[t] = first sorted position of table t (lower bound), t <= T
+__global__ void xgmi_table_start_kernel(const uint64_t* __restrict__ kout, int64_t R, int T,
+                                        int world, int64_t TB, int64_t* __restrict__ tstart) {
+  const int t = threadIdx.x;
+  if (t > T) return;
+  const uint64_t lo_key = (uint64_t)t * (uint64_t)world * (uint64_t)TB;
+  int64_t lo = 0, hi = R;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (kout[mid] < lo_key)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  tstart[t] = lo;
+}
+
 }  // namespace dr
 
 extern "C" {
@@ -163,6 +239,80 @@ int dr_xgmi_route(const dr_xgmi_peers* peers, const int64_t* keys, int num_table
   }
   hipLaunchKernelGGL(xgmi_counts_kernel, dim3(64), dim3(64), 0, st, a,
                      (const unsigned long long*)cnt_ws);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+
+size_t dr_xgmi_grad_pull_workspace_size(int world, int64_t cap) {
+  using namespace dr;
+  const int64_t n = (int64_t)(world > 0 ? world : 1) * (cap > 0 ? cap : 1);
+  Carver c(nullptr);
+  c.take<uint64_t>(n);
+  c.take<int32_t>(n);
+  c.take<uint64_t>(n);
+  c.take<int32_t>(n);
+  c.take<char>(dr_sort_pairs_workspace_size(n));
+  return c.used + 256;
+}
+
+int dr_xgmi_grad_pull(const dr_xgmi_peers* peers, const float* const* grad_in,
+                      const int64_t* cnt_host, int num_tables, int64_t batch, int dim,
+                      int64_t* keys_out, float* grads_out, int64_t* table_start, void* ws,
+                      size_t ws_bytes, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(peers && grad_in && cnt_host && table_start && num_tables >= 1 && batch >= 0 &&
+                 dim > 0,
+             DR_INVALID_ARGUMENT, "bad argument");
+  const int W = peers->world;
+  DR_REQUIRE(W >= 1 && W <= DR_MAX_PEERS && peers->rank >= 0 && peers->rank < W,
+             DR_INVALID_ARGUMENT, "bad world/rank");
+  DR_REQUIRE(num_tables < 1024, DR_INVALID_ARGUMENT, "too many tables");
+  DR_REQUIRE(ws_bytes >= dr_xgmi_grad_pull_workspace_size(W, peers->cap), DR_INVALID_ARGUMENT,
+             "workspace too small");
+  const int64_t TB = (int64_t)num_tables * batch;
+  XgmiPullArgs a;
+  memset(&a, 0, sizeof(a));
+  a.world = W;
+  a.cap = peers->cap;
+  a.prefix[0] = 0;
+  for (int s = 0; s < W; ++s) {
+    DR_REQUIRE(cnt_host[s] >= 0 && cnt_host[s] <= peers->cap, DR_INVALID_ARGUMENT,
+               "inbox count %lld of source %d out of range", (long long)cnt_host[s], s);
+    DR_REQUIRE(grad_in[s], DR_INVALID_ARGUMENT, "peer %d gradient buffer not mapped", s);
+    a.prefix[s + 1] = a.prefix[s] + cnt_host[s];
+    a.gin[s] = grad_in[s];
+  }
+  const int64_t R = a.prefix[W];
+  DR_REQUIRE(R < (1ll << 31), DR_INVALID_ARGUMENT, "too many entries");
+  hipStream_t st = S(stream);
+  const int me = peers->rank;
+  const int64_t* ikeys = peers->inbox_keys[me];
+  const int32_t* islot = peers->inbox_slot[me];
+  DR_REQUIRE(ikeys && islot, DR_INVALID_ARGUMENT, "own inbox not mapped");
+  Carver c(ws);
+  const int64_t n = (int64_t)W * (peers->cap > 0 ? peers->cap : 1);
+  uint64_t* kin = c.take<uint64_t>(n);
+  int32_t* vin = c.take<int32_t>(n);
+  uint64_t* kout = c.take<uint64_t>(n);
+  int32_t* perm = c.take<int32_t>(n);
+  const size_t sb = dr_sort_pairs_workspace_size(n);
+  void* sws = c.take<char>(sb);
+  if (R > 0) {
+    hipLaunchKernelGGL(xgmi_grad_keys_kernel, dim3((unsigned)ceil_div(R, 256)), dim3(256), 0, st,
+                       a, islot, num_tables, TB, R, kin, vin);
+    DR_LAUNCH_CHECK();
+    int bits = 1;
+    while (bits < 64 && ((uint64_t)num_tables * (uint64_t)W * (uint64_t)TB) >> bits) ++bits;
+    int rc = dr_sort_pairs(kin, vin, kout, perm, R, 0, bits, sws, sb, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(xgmi_grad_pull_kernel, dim3((unsigned)ceil_div(R, 4)), dim3(256), 0, st, a,
+                       ikeys, islot, perm, R, dim, (int64_t)num_tables * dim, keys_out,
+                       grads_out);
+    DR_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(xgmi_table_start_kernel, dim3(1), dim3(1024), 0, st, kout, R, num_tables, W,
+                     TB, table_start);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

@@ -393,8 +393,8 @@ class ReduceScatterShardedLookup(object):
 class XgmiBuffers(object):
     """One rank's exchange buffers for XgmiShardedLookup (torch allocations
     shared with the peers through HIP IPC): the inbox that requesters write
-    (key, slot) pairs into, and the [B, T*D] output that owners write rows
-    into."""
+    (key, slot) pairs into, the [B, T*D] output that owners write rows into,
+    and the [B, T*D] gradient that owners pull rows from in backward()."""
 
     def __init__(self, world, T, batch, dim, device):
         self.cap = T * batch
@@ -402,9 +402,10 @@ class XgmiBuffers(object):
         self.inbox_slot = torch.empty((world, self.cap), dtype=torch.int32, device=device)
         self.inbox_cnt = torch.zeros(world, dtype=torch.int64, device=device)
         self.out = torch.empty((batch, T * dim), dtype=torch.float32, device=device)
+        self.gin = torch.empty((batch, T * dim), dtype=torch.float32, device=device)
 
     def tensors(self):
-        return [self.inbox_keys, self.inbox_slot, self.inbox_cnt, self.out]
+        return [self.inbox_keys, self.inbox_slot, self.inbox_cnt, self.out, self.gin]
 
 
 class XgmiShardedLookup(object):
@@ -447,8 +448,9 @@ class XgmiShardedLookup(object):
         p = _lib.DrXgmiPeers()
         p.world, p.rank, p.cap = world, rank, self.bufs.cap
         for q in range(world):
-            p.inbox_keys[q], p.inbox_slot[q], p.inbox_cnt[q], p.out[q] = peer_ptrs[q]
+            p.inbox_keys[q], p.inbox_slot[q], p.inbox_cnt[q], p.out[q] = peer_ptrs[q][:4]
         self.peers = p
+        self.gin_ptrs = (C.c_void_p * world)(*[peer_ptrs[q][4] for q in range(world)])
         self.cnt_ws = torch.zeros(world, dtype=torch.int64, device=device)
         self.wsb = lib().dr_xgmi_serve_workspace_size(world, self.bufs.cap)
         self.ws = workspace(self.wsb, device)
@@ -491,6 +493,44 @@ class XgmiShardedLookup(object):
         check(lib().dr_xgmi_serve(C.byref(self.peers), self.handles, self.T, self.batch,
                                   ptr(self.ws), self.wsb, stream_handle(self.device)))
         ops._post(self.device)
+
+    def backward(self, grad_out):
+        """grad_out: [B, T*D] gradient of the last forward().
+
+        Requester: the gradient goes into this rank's shared buffer; after a
+        barrier every owner pulls, over xGMI, the rows of the (key, slot)
+        pairs its inbox still holds from the forward, in (table, source,
+        slot) order (dr_xgmi_grad_pull), and queues one IndexedSlices per
+        table on its EVs -- the one-hot counterpart of
+        ShardedLookup.backward, without staging copies.  Returns the
+        per-table (keys, grads) slices."""
+        from .kv_variable_ops import IndexedSlices
+        g = grad_out.contiguous()
+        T, D, B = self.T, self.dim, self.batch
+        if tuple(g.shape) != (B, T * D) or g.dtype != torch.float32:
+            raise ValueError("grad must be fp32 [%d, %d]" % (B, T * D))
+        self.bufs.gin.copy_(g)
+        self._barrier()
+        cnt = self.bufs.inbox_cnt.cpu()                 # this rank's inbox counts (sync)
+        R = int(cnt.sum())
+        keys = torch.empty(max(R, 1), dtype=torch.int64, device=self.device)
+        grads = torch.empty((max(R, 1), D), dtype=torch.float32, device=self.device)
+        tstart = torch.empty(T + 1, dtype=torch.int64, device=self.device)
+        wsb = lib().dr_xgmi_grad_pull_workspace_size(self.world, self.bufs.cap)
+        ws = workspace(wsb, self.device)
+        ch = (C.c_int64 * self.world)(*[int(x) for x in cnt.tolist()])
+        check(lib().dr_xgmi_grad_pull(C.byref(self.peers), self.gin_ptrs, ch, T, B, D, ptr(keys),
+                                      ptr(grads), ptr(tstart), ptr(ws), wsb,
+                                      stream_handle(self.device)))
+        ops._post(self.device)
+        self._barrier()          # no peer's next route() may overwrite the inbox before the pull
+        ts = tstart.cpu().tolist()
+        out = []
+        for t in range(T):
+            k, v = keys[ts[t]:ts[t + 1]], grads[ts[t]:ts[t + 1]]
+            out.append((k, v))
+            self.evs[t].pending_grads.append(IndexedSlices(v, k, unique=False))
+        return out
 
     def forward(self, ids):
         """ids: [T, B] int64 keys (hotness 1) -> [B, T*D] pooled (sum)."""

@@ -455,6 +455,17 @@ int dr_xgmi_route(const dr_xgmi_peers* peers, const int64_t* keys, int num_table
 size_t dr_xgmi_serve_workspace_size(int world, int64_t cap);
 int dr_xgmi_serve(const dr_xgmi_peers* peers, dr_ev* const* evs, int num_tables,
                   int64_t batch, void* ws, size_t ws_bytes, void* stream);
+/* Backward of the peer-write lookup, owner side: this rank's inbox entries  */
+/* (cnt_host[s] of source s, read by the caller from its inbox counts),      */
+/* sorted by (table, source, slot), each pulling the requester's gradient    */
+/* row grad_in[s][slot] ([B, T*dim] per peer, mapped like the outputs) over  */
+/* xGMI: keys_out [R], grads_out [R, dim], table_start [T+1] (DEVICE; table  */
+/* t's entries are [table_start[t], table_start[t+1])).  R = sum cnt_host.   */
+size_t dr_xgmi_grad_pull_workspace_size(int world, int64_t cap);
+int dr_xgmi_grad_pull(const dr_xgmi_peers* peers, const float* const* grad_in,
+                      const int64_t* cnt_host, int num_tables, int64_t batch, int dim,
+                      int64_t* keys_out, float* grads_out, int64_t* table_start, void* ws,
+                      size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Interactions (callers of the path).                                       */

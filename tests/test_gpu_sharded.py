@@ -189,6 +189,39 @@ def _run_xgmi(world, steps=2):
                 ref_ev.insert(allk, _vals(t, allk))
                 ref = orc.embedding_lookup_sparse(ref_ev, ind, ids[r][t], B, combiner="sum")
                 np.testing.assert_array_equal(outs[r][:, t * D:(t + 1) * D], ref)
+        # backward: every owner pulls its keys' gradient rows from the
+        # requesters, in (table, source rank, batch row) order -- exact copies
+        grads = [rng.standard_normal((B, T * D)).astype(np.float32) for _ in range(world)]
+        pulled = [None] * world
+
+        def run_bwd(r):
+            try:
+                got = engines[r].backward(torch.as_tensor(grads[r], device=DEV))
+                pulled[r] = [(k.cpu().numpy(), v.cpu().numpy()) for k, v in got]
+            except Exception as e:
+                errs.append(e)
+                bar.abort()
+
+        th = [threading.Thread(target=run_bwd, args=(r,)) for r in range(world)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(120)
+        if errs:
+            raise errs[0]
+        for r in range(world):
+            for t in range(T):
+                wk, wg = [], []
+                for s in range(world):
+                    sel = np.nonzero(ids[s][t] % world == r)[0]
+                    wk.append(ids[s][t][sel])
+                    wg.append(grads[s][sel, t * D:(t + 1) * D])
+                k, v = pulled[r][t]
+                np.testing.assert_array_equal(k, np.concatenate(wk))
+                np.testing.assert_array_equal(v, np.concatenate(wg).reshape(-1, D))
+                sl = evs_all[r][t].pending_grads.pop()
+                assert sl.indices.numel() == k.shape[0]
+                evs_all[r][t].pending_grads.clear()
     for r in range(world):
         for ev in evs_all[r]:
             k = ev.export()[0].cpu().numpy()
