@@ -2,7 +2,8 @@
 //
 // Scan: reduce-then-scan over 2048-item tiles (256 threads x 8 items), wave64
 // shuffles + LDS across the 4 waves of a block.  Sort: 8-bit digits, per-tile
-// LDS histograms, stable in-tile ranking by wave64 ballot matching (the
+// LDS histograms, stable in-tile ranking by wave64 ballot matching and an
+// LDS regroup so each digit's run leaves the tile as one coalesced store (the
 // CDNA4 replacement for cub::DeviceRadixSort::SortPairs used by
 // FusedEmbeddingSparsePreLookUp, fused_embedding_ops_gpus.cu.cc:192-212).
 #include "dr_common.h"
@@ -110,48 +111,106 @@ int scan_exclusive_i32(const int32_t* in, int32_t* out, int64_t n, const int64_t
 }
 
 // ---------------------------------------------------------------------------
-// Stable LSD radix sort, 8-bit digits.  Tile = 256 threads x 16 rounds.
-// hist layout: [digit][block] so one exclusive scan yields scatter bases.
+// Stable LSD radix sort, 8-bit digits, 3 launches per pass:
+//   hist    per-tile digit counts, layout [digit][tile];
+//   rowscan one block per digit: exclusive scan of its row over the tiles,
+//           and the digit's total;
+//   scatter ranks the tile stably in LDS (wave64 ballot matching, 16 rounds
+//           of 256 keys), regroups the tile by digit in LDS, then writes
+//           every digit's run of the tile to consecutive global positions --
+//           consecutive lanes hit consecutive addresses, so the stores
+//           coalesce instead of landing one 8-byte key per digit per round.
+// Global position = exclusive prefix of the digit totals (scanned in each
+// scatter block, 256 entries) + the digit's row prefix + the tile-local
+// offset inside the digit's run.
 // ---------------------------------------------------------------------------
 static constexpr int kSortThreads = 256;
 static constexpr int kSortRounds = 16;
 static constexpr int kSortTile = kSortThreads * kSortRounds;
 
-__global__ void sort_hist_kernel(const uint64_t* __restrict__ keys, int64_t n, int shift,
-                                 int32_t* __restrict__ hist, int64_t nblocks) {
+__global__ __launch_bounds__(256) void sort_hist_kernel(const uint64_t* __restrict__ keys, int64_t n,
+                                                        int shift, int dmask,
+                                                        int32_t* __restrict__ hist,
+                                                        int64_t nblocks) {
   __shared__ int cnt[256];
   cnt[threadIdx.x] = 0;
-  __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
-  for (int r = 0; r < kSortRounds; ++r) {
-    const int64_t i = base + (int64_t)r * kSortThreads + threadIdx.x;
-    if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & 255], 1);
+  const int c = (int)(n - base < kSortTile ? n - base : kSortTile);
+  int d[kSortRounds];
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {       // all loads in flight before the atomics
+    const int i = r * kSortThreads + threadIdx.x;
+    d[r] = i < c ? (int)((keys[base + i] >> shift) & dmask) : -1;
   }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r)
+    if (d[r] >= 0) atomicAdd(&cnt[d[r]], 1);
   __syncthreads();
   hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
 }
 
-__global__ void sort_scatter_kernel(const uint64_t* __restrict__ kin,
-                                    const int32_t* __restrict__ vin, uint64_t* __restrict__ kout,
-                                    int32_t* __restrict__ vout, int64_t n, int shift,
-                                    const int32_t* __restrict__ hist_scanned, int64_t nblocks) {
-  __shared__ int run[256];
+__global__ __launch_bounds__(256) void sort_rowscan_kernel(int32_t* __restrict__ hist,
+                                                           int64_t nblocks,
+                                                           int32_t* __restrict__ digit_tot) {
+  __shared__ int lds[4];
+  int32_t* row = hist + (int64_t)blockIdx.x * nblocks;
+  int carry = 0;
+  for (int64_t b0 = 0; b0 < nblocks; b0 += kSortThreads) {
+    const int64_t i = b0 + threadIdx.x;
+    const int v = i < nblocks ? row[i] : 0;
+    int tot;
+    const int ex = block_exclusive_scan(v, lds, &tot);
+    if (i < nblocks) row[i] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) digit_tot[blockIdx.x] = carry;
+}
+
+// Each wave ranks its own contiguous quarter of the tile (16 rounds of 64
+// keys) against wave-private LDS digit counters: within one wave the LDS
+// read of a counter and the group leader's update are ordered, so the loop
+// needs no block barrier.  Tile offset of (wave w, digit d) =
+// exclusive-over-digits(total) + sum over w' < w of the wave counts.
+__global__ __launch_bounds__(256) void sort_scatter_kernel(
+    const uint64_t* __restrict__ kin, const int32_t* __restrict__ vin, uint64_t* __restrict__ kout,
+    int32_t* __restrict__ vout, int64_t n, int shift, int dmask,
+    const int32_t* __restrict__ row_scanned, const int32_t* __restrict__ digit_tot,
+    int64_t nblocks) {
+  __shared__ uint64_t sk[kSortTile];
+  __shared__ int32_t sv[kSortTile];
   __shared__ int wcnt[4][256];
-  run[threadIdx.x] = hist_scanned[(int64_t)threadIdx.x * nblocks + blockIdx.x];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  __shared__ int toff[256];
+  __shared__ int gbase[256];
+  __shared__ int lds[4];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  const int cnt = (int)(n - base < kSortTile ? n - base : kSortTile);
+  const int wbase = wave * (kSortTile / 4);
+  uint64_t key[kSortRounds];
+  int32_t val[kSortRounds];
+  int rk[kSortRounds];
+#pragma unroll
   for (int r = 0; r < kSortRounds; ++r) {
-    wcnt[0][threadIdx.x] = 0;
-    wcnt[1][threadIdx.x] = 0;
-    wcnt[2][threadIdx.x] = 0;
-    wcnt[3][threadIdx.x] = 0;
-    __syncthreads();
-    const int64_t i = base + (int64_t)r * kSortThreads + threadIdx.x;
-    const bool valid = i < n;
-    uint64_t key = valid ? kin[i] : 0;
-    int32_t val = valid ? vin[i] : 0;
-    const int d = (int)((key >> shift) & 255);
+    const int i = wbase + r * 64 + lane;
+    const bool valid = i < cnt;
+    key[r] = valid ? kin[base + i] : 0;
+    val[r] = valid ? vin[base + i] : 0;
+  }
+  wcnt[0][tid] = 0;
+  wcnt[1][tid] = 0;
+  wcnt[2][tid] = 0;
+  wcnt[3][tid] = 0;
+  int tot;
+  const int dex = block_exclusive_scan(digit_tot[tid], lds, &tot);   // has barriers
+  gbase[tid] = dex + row_scanned[(int64_t)tid * nblocks + blockIdx.x];
+  int* mycnt = wcnt[wave];
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const bool valid = wbase + r * 64 + lane < cnt;
+    const int d = (int)((key[r] >> shift) & dmask);
     uint64_t peers = __ballot(valid);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -161,25 +220,41 @@ __global__ void sort_scatter_kernel(const uint64_t* __restrict__ kin,
     }
     const int rank = __popcll(peers & lanemask_lt());
     const int gsize = __popcll(peers);
-    if (valid && rank == gsize - 1) wcnt[wave][d] = gsize;
-    __syncthreads();
-    int pos = 0;
-    if (valid) {
-      pos = run[d] + rank;
-      for (int w = 0; w < wave; ++w) pos += wcnt[w][d];
+    const int old = valid ? mycnt[d] : 0;
+    rk[r] = old + rank;
+    if (valid && rank == 0) mycnt[d] = old + gsize;
+  }
+  __syncthreads();
+  const int c0 = wcnt[0][tid], c1 = wcnt[1][tid], c2 = wcnt[2][tid], c3 = wcnt[3][tid];
+  const int dt = block_exclusive_scan(c0 + c1 + c2 + c3, lds, &tot);
+  toff[tid] = dt;
+  wcnt[0][tid] = dt;                 // per-wave tile offsets of digit tid
+  wcnt[1][tid] = dt + c0;
+  wcnt[2][tid] = dt + c0 + c1;
+  wcnt[3][tid] = dt + c0 + c1 + c2;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    if (wbase + r * 64 + lane < cnt) {
+      const int d = (int)((key[r] >> shift) & dmask);
+      const int at = mycnt[d] + rk[r];
+      sk[at] = key[r];
+      sv[at] = val[r];
     }
-    __syncthreads();
-    run[threadIdx.x] += wcnt[0][threadIdx.x] + wcnt[1][threadIdx.x] + wcnt[2][threadIdx.x] +
-                        wcnt[3][threadIdx.x];
-    if (valid) {
-      kout[pos] = key;
-      vout[pos] = val;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int r = 0; r < kSortRounds; ++r) {
+    const int i = r * kSortThreads + tid;
+    if (i < cnt) {
+      const uint64_t k = sk[i];
+      const int d = (int)((k >> shift) & dmask);
+      const int64_t pos = (int64_t)gbase[d] + (i - toff[d]);
+      kout[pos] = k;
+      vout[pos] = sv[i];
     }
-    (void)lane;
   }
 }
-
-static size_t sort_hist_elems(int64_t n) { return (size_t)256 * ceil_div(n > 0 ? n : 1, kSortTile); }
 
 }  // namespace dr
 
@@ -187,10 +262,8 @@ extern "C" size_t dr_sort_pairs_workspace_size(int64_t n) {
   dr::Carver c(nullptr);
   c.take<uint64_t>(n > 0 ? n : 1);
   c.take<int32_t>(n > 0 ? n : 1);
-  size_t he = dr::sort_hist_elems(n);
-  c.take<int32_t>(he);
-  c.take<char>(dr::scan_ws_bytes((int64_t)he));
-  c.take<int64_t>(1);
+  c.take<int32_t>((size_t)256 * dr::ceil_div(n > 0 ? n : 1, dr::kSortTile));
+  c.take<int32_t>(256);
   return c.used + 256;
 }
 
@@ -200,6 +273,7 @@ extern "C" int dr_sort_pairs(const uint64_t* keys_in, const int32_t* vals_in, ui
   using namespace dr;
   DR_REQUIRE(n >= 0 && bit_lo >= 0 && bit_hi <= 64 && bit_lo <= bit_hi, DR_INVALID_ARGUMENT,
              "dr_sort_pairs: bad arguments");
+  DR_REQUIRE(n < ((int64_t)1 << 31), DR_INVALID_ARGUMENT, "dr_sort_pairs: n >= 2^31");
   DR_REQUIRE(ws_bytes >= dr_sort_pairs_workspace_size(n), DR_INVALID_ARGUMENT,
              "dr_sort_pairs: workspace too small");
   hipStream_t st = S(stream);
@@ -207,11 +281,9 @@ extern "C" int dr_sort_pairs(const uint64_t* keys_in, const int32_t* vals_in, ui
   Carver c(ws);
   uint64_t* ktmp = c.take<uint64_t>(n);
   int32_t* vtmp = c.take<int32_t>(n);
-  const size_t he = sort_hist_elems(n);
-  int32_t* hist = c.take<int32_t>(he);
-  void* sws = c.take<char>(scan_ws_bytes((int64_t)he));
-  int64_t* tot = c.take<int64_t>(1);
   const int64_t nblocks = ceil_div(n, kSortTile);
+  int32_t* hist = c.take<int32_t>((size_t)256 * nblocks);
+  int32_t* dtot = c.take<int32_t>(256);
   int passes = (bit_hi - bit_lo + 7) / 8;
   if (passes == 0) {
     DR_HIP(hipMemcpyAsync(keys_out, keys_in, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
@@ -225,12 +297,14 @@ extern "C" int dr_sort_pairs(const uint64_t* keys_in, const int32_t* vals_in, ui
     uint64_t* kd = to_out ? keys_out : ktmp;
     int32_t* vd = to_out ? vals_out : vtmp;
     const int shift = bit_lo + 8 * p;
+    const int dbits = bit_hi - shift < 8 ? bit_hi - shift : 8;   // bits >= bit_hi are ignored
+    const int dmask = (1 << dbits) - 1;
     hipLaunchKernelGGL(sort_hist_kernel, dim3((unsigned)nblocks), dim3(kSortThreads), 0, st, ks,
-                       n, shift, hist, nblocks);
-    int rc = scan_exclusive_i32(hist, hist, (int64_t)he, nullptr, tot, sws, st);
-    if (rc) return rc;
+                       n, shift, dmask, hist, nblocks);
+    hipLaunchKernelGGL(sort_rowscan_kernel, dim3(256), dim3(kSortThreads), 0, st, hist, nblocks,
+                       dtot);
     hipLaunchKernelGGL(sort_scatter_kernel, dim3((unsigned)nblocks), dim3(kSortThreads), 0, st,
-                       ks, vs, kd, vd, n, shift, hist, nblocks);
+                       ks, vs, kd, vd, n, shift, dmask, hist, dtot, nblocks);
     DR_LAUNCH_CHECK();
     ks = kd;
     vs = vd;

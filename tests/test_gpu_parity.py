@@ -285,13 +285,19 @@ def test_onehot_fused_abi_orders_and_slot_column(dr):
         assert neg.all() if order == ORDER_ALI else (~neg).all()
 
 
-def test_sort_pairs_stable(ops):
-    rng = np.random.default_rng(3)
-    n = 100003
-    keys = rng.integers(0, 1 << 20, n).astype(np.int64)
+@pytest.mark.parametrize("n,kmax,bit_lo,bit_hi", [
+    (100003, 1 << 20, 0, 20), (1, 5, 0, 8), (4095, 1 << 12, 0, 12), (4096, 7, 0, 3),
+    (4097, 1 << 40, 0, 40), (2000000, 1 << 21, 0, 21), (300000, 3, 0, 2),
+    (50000, 1 << 40, 9, 34)])
+def test_sort_pairs_stable(ops, n, kmax, bit_lo, bit_hi):
+    """Stable LSD sort on bits [bit_lo, bit_hi): ragged last tile, one key,
+    exactly one tile, few distinct keys (runs spanning many tiles), and a
+    bit window that ignores the low and high bits (ties keep input order)."""
+    rng = np.random.default_rng(n)
+    keys = rng.integers(0, kmax, n).astype(np.int64)
     vals = np.arange(n, dtype=np.int32)
-    ko, vo = ops.sort_pairs(T(keys), T(vals), 20)
-    order = np.argsort(keys, kind="stable")
+    ko, vo = ops.sort_pairs(T(keys), T(vals), bit_hi, bit_lo)
+    order = np.argsort((keys >> bit_lo) & ((1 << (bit_hi - bit_lo)) - 1), kind="stable")
     np.testing.assert_array_equal(H(ko), keys[order])
     np.testing.assert_array_equal(H(vo), vals[order])
 

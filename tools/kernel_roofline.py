@@ -134,6 +134,17 @@ def main():
         report("unsorted_segment_sum", ms, n * (4 + D * 4) + U * D * 4,
                shape="nnz %d, U %d, D %d" % (n, U, D))
 
+    # -- radix sort pairs: per 8-bit pass 8n (hist read) + 12n read + 12n write --
+    if want("sort"):
+        n = N
+        vals = torch.arange(n, device=dev, dtype=torch.int32)
+        for bits in (20, 32):
+            keys = torch.randint(0, 1 << bits, (n,), generator=g, device=dev)
+            ms = timed(lambda: ops.sort_pairs(keys, vals, bits), it)
+            passes = (bits + 7) // 8
+            report("sort_pairs", ms, passes * n * 32,
+                   shape="%d (u64 key, i32 val), %d bits, %d passes" % (n, bits, passes))
+
     # -- Unique (grouped, 26 features): nnz*(8+4) + U*8 ------------------------
     if want("unique"):
         keys = torch.randint(0, 12_500_000, (N,), generator=g, device=dev)
