@@ -7,30 +7,37 @@
 //
 // GPU algorithm (no host sync, integer-exact):
 //   1. open-addressing table per feature (capacity pow2 >= 2 n_t) in the
-//      workspace; each position i CAS-inserts its key and atomicMin's its
-//      position into the slot -> the slot holds the FIRST position of the key;
-//   2. flag[i] = (slot.minpos == i); one exclusive scan over all features;
+//      workspace whose 4-byte slots hold a POSITION, not a key: a slot is
+//      claimed by CAS-ing its first inserter's position in, and a probe
+//      matches when keys[slot value] == k (the input is immutable, so the
+//      position identifies the key).  A later, smaller position of the same
+//      key lowers the slot with atomicMin -- only when it is smaller, which
+//      the roughly ascending launch order makes rare -- so the slot ends
+//      at the key's FIRST position with one returning atomic per key
+//      instead of a key CAS plus a position atomicMin (memory-side atomics
+//      are the insert's bound: one 64-B request per lane);
+//   2. flag[i] = (slot == i); one exclusive scan over all features;
 //      the local unique id is prefix[i] - prefix[first position of table t]
 //      (a table's first position is always a first occurrence);
 //   3. idx[i] = uid(slot(i)); counts by integer atomics (order-free, exact).
-// Key -1 is the hash's empty pattern; each table routes it to a spare slot.
+// Every key value (-1 included) is an ordinary key: the empty pattern is a
+// position (0xFFFFFFFF), never a key.
 // Outputs keep the input layout: table t's uniques / counts sit at
 // [koff[t], koff[t] + U_t) and U_t goes to num_unique[t] (device int64).
 #include "dr_common.h"
 
 namespace dr {
 
-static constexpr uint64_t kEmpty = ~0ull;
+static constexpr uint32_t kEmptyPos = ~0u;
 
 struct UniqGroup {
   int64_t koff[DR_MAX_GROUP + 1];   // input offsets
   int64_t hbase[DR_MAX_GROUP];      // hash region base (slots)
-  int64_t hcap[DR_MAX_GROUP];       // region capacity (pow2), spare slot at hbase + hcap
+  int64_t hcap[DR_MAX_GROUP];       // region capacity (pow2)
 };
 
 struct UniqueWs {
-  uint64_t* tkeys;   // [hash_total]
-  uint32_t* minpos;  // [hash_total]
+  uint32_t* minpos;  // [hash_total] first position of the slot's key
   int32_t* tuid;     // [hash_total]
   int32_t* slot_of;  // [n]
   int32_t* flags;    // [n] scan output
@@ -45,7 +52,7 @@ static int64_t build_group(const int64_t* koff, int T, UniqGroup* g) {
     g->koff[t] = koff[t];
     g->hbase[t] = base;
     g->hcap[t] = next_pow2(2 * (n > 32 ? n : 32));
-    base += g->hcap[t] + 1;
+    base += g->hcap[t];
   }
   g->koff[T] = koff[T];
   return base;
@@ -54,7 +61,6 @@ static int64_t build_group(const int64_t* koff, int T, UniqGroup* g) {
 static UniqueWs carve_unique(void* ws, int64_t n, int64_t hash_total, size_t* used) {
   Carver c(ws);
   UniqueWs u;
-  u.tkeys = c.take<uint64_t>(hash_total);
   u.minpos = c.take<uint32_t>(hash_total);
   u.tuid = c.take<int32_t>(hash_total);
   u.slot_of = c.take<int32_t>(n > 0 ? n : 1);
@@ -71,7 +77,7 @@ __device__ __forceinline__ int group_table(const UniqGroup& g, int T, int64_t i)
 }
 
 __global__ void unique_insert_kernel(UniqGroup g, int T, const int64_t* __restrict__ keys,
-                                     uint64_t* __restrict__ tkeys, uint32_t* __restrict__ minpos,
+                                     uint32_t* __restrict__ minpos,
                                      int32_t* __restrict__ slot_of) {
   __shared__ int64_t shcap[DR_MAX_GROUP], shbase[DR_MAX_GROUP];  // per-lane table: LDS
   if (threadIdx.x < T) {
@@ -82,13 +88,12 @@ __global__ void unique_insert_kernel(UniqGroup g, int T, const int64_t* __restri
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= g.koff[T]) return;  // (exited lanes are the wave's tail: never a run head)
   const int t = group_table(g, T, i);
-  const uint64_t k = (uint64_t)keys[i];
+  const int64_t k = keys[i];
   // Runs of one key in consecutive positions of a wave (a padded history
   // batch, a hot id) insert once: only the run's first lane -- the smallest
-  // position -- touches the slot; the rest take its slot by a shuffle.  The
-  // hot slot then sees one CAS + one atomicMin per wave, not per position.
+  // position -- touches the slot; the rest take its slot by a shuffle.
   const int lane = __lane_id();
-  const uint32_t klo = (uint32_t)k, khi = (uint32_t)(k >> 32);
+  const uint32_t klo = (uint32_t)k, khi = (uint32_t)((uint64_t)k >> 32);
   const uint32_t plo = (uint32_t)__shfl_up((int)klo, 1, 64);
   const uint32_t phi = (uint32_t)__shfl_up((int)khi, 1, 64);
   const int pt = __shfl_up(t, 1, 64);
@@ -97,25 +102,22 @@ __global__ void unique_insert_kernel(UniqGroup g, int T, const int64_t* __restri
   int64_t s = 0;
   if (head) {
     const int64_t cap = shcap[t];
-    uint64_t* tk = tkeys + shbase[t];
-    if (k == kEmpty) {
-      s = cap;
-    } else {
-      const uint64_t mask = (uint64_t)cap - 1;
-      uint64_t h = mix64(k) & mask;
-      // The CAS result (performed at the memory side) is the only truth used
-      // to skip a slot, so a stale cached line can never make the probe run
-      // past every slot (the table holds at most half its capacity).
-      for (int64_t probes = 0; probes <= cap; ++probes) {
-        uint64_t old = atomicCAS((unsigned long long*)&tk[h], (unsigned long long)kEmpty,
-                                 (unsigned long long)k);
-        if (old == kEmpty || old == k) break;
-        h = (h + 1) & mask;
+    uint32_t* mp = minpos + shbase[t];
+    const uint64_t mask = (uint64_t)cap - 1;
+    uint64_t h = mix64((uint64_t)k) & mask;
+    const uint32_t me = (uint32_t)i;
+    // The CAS result (performed at the memory side) is the only truth used
+    // to skip a slot; the table holds at most half its capacity.
+    for (int64_t probes = 0; probes <= cap; ++probes) {
+      const uint32_t old = atomicCAS(&mp[h], kEmptyPos, me);
+      if (old == kEmptyPos) break;
+      if (keys[old] == k) {
+        if (me < old) atomicMin(&mp[h], me);
+        break;
       }
-      s = (int64_t)h;
+      h = (h + 1) & mask;
     }
-    s += shbase[t];
-    atomicMin(&minpos[s], (uint32_t)i);
+    s = (int64_t)h + shbase[t];
   }
   const uint64_t le = heads & (lanemask_lt() | (1ull << lane));
   const int src = 63 - __clzll((long long)le);
@@ -199,18 +201,16 @@ extern "C" int dr_unique_grouped(const int64_t* keys, const int64_t* koff_host, 
   hipStream_t st = S(stream);
   if (n == 0) {
     return fill_bytes(num_unique, 0, T * sizeof(int64_t), st);
-    return DR_OK;
   }
   UniqGroup g;
   const int64_t ht = build_group(koff_host, T, &g);
   UniqueWs u = carve_unique(ws, n, ht, nullptr);
-  int frc = fill_bytes(u.tkeys, 0xFF, ht * sizeof(uint64_t), st);
-  if (!frc) frc = fill_bytes(u.minpos, 0xFF, ht * sizeof(uint32_t), st);
+  int frc = fill_bytes(u.minpos, 0xFF, ht * sizeof(uint32_t), st);
   if (!frc && counts_out) frc = fill_bytes(counts_out, 0, n * sizeof(int32_t), st);
   if (frc) return frc;
   const unsigned blocks = (unsigned)ceil_div(n, 256);
-  hipLaunchKernelGGL(unique_insert_kernel, dim3(blocks), dim3(256), 0, st, g, T, keys, u.tkeys,
-                     u.minpos, u.slot_of);
+  hipLaunchKernelGGL(unique_insert_kernel, dim3(blocks), dim3(256), 0, st, g, T, keys, u.minpos,
+                     u.slot_of);
   hipLaunchKernelGGL(unique_flag_kernel, dim3(blocks), dim3(256), 0, st, n, u.minpos, u.slot_of,
                      u.flags);
   DR_LAUNCH_CHECK();

@@ -131,12 +131,12 @@ def test_segment_reduce_errors_latched(dr, ops):
 
 
 @pytest.mark.parametrize("n,lo,hi", [(0, 0, 1), (1, 0, 1), (1000, 0, 10), (200000, -5, 100000),
-                                     (300000, 0, 1 << 40)])
+                                     (300000, 0, 1 << 40), (500000, -3, 4), (400000, 0, 1000)])
 def test_unique_bitexact(ops, orc, n, lo, hi):
     rng = np.random.default_rng(n)
     x = rng.integers(lo, hi, n).astype(np.int64)
     if n > 10:
-        x[5] = -1                      # the table's empty pattern is handled
+        x[5] = -1                      # all-ones keys are ordinary keys
         x[7] = -1
     y, idx, cnt = ops.unique_with_counts(T(x))
     ry, ridx, rcnt = orc.unique(x, with_counts=True)
