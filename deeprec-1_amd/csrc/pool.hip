@@ -833,7 +833,7 @@ struct GradWs {
   int32_t* longs;
   float* part;
 };
-static constexpr int kGradChain = 8;         // positions of a chunk fetched per step
+static constexpr int kGradChain = 4;         // positions of a chunk fetched per step (80 VGPRs: 6 waves/SIMD)
 static constexpr int kGradFinishChain = 32;  // chunk partials of a long run fetched per step
 
 // run_start[u] = first sorted position of row u; clears the long-run count.
@@ -928,86 +928,106 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
       for (int c = 0; c < CPL; ++c) x[q].v[c] = vzero<V>();
     }
   if (bad) latch(st, DR_INVALID_ARGUMENT);
+  // UnsortedSegmentSum order 0 + x_0 + x_1 ... (sum); x_0 * s + ... (mean/sqrtn);
+  // a later chunk's partial starts at its first element
+  auto scaled = [&](R& y, const dr_pool_grad_desc& d, int mode, int64_t r) {
+    if (mode == 0) return;
+    const int32_t cnt = (r >= 0 && d.bag_off) ? d.bag_off[r + 1] - d.bag_off[r] : 1;
+    if (cnt != 1) {
+      const float sc = mode == 2 ? (float)(1.0 / sqrt((double)cnt)) : (float)(1.0 / (double)cnt);
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) y.v[c] = vmul(y.v[c], sc);
+    }
+  };
+  auto mode_of = [](const dr_pool_grad_desc& d) {
+    return d.combiner == DR_COMBINER_SUM ? 0 : (d.combiner == DR_COMBINER_MEAN ? 1 : 2);
+  };
+  // -- one-position runs (every run of all-distinct ids): the row is loaded --
+  unsigned multi = 0;
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
     if (!head[q]) continue;
+    if (!single[q]) {
+      multi |= 1u << q;
+      continue;
+    }
     const dr_pool_grad_desc& d = sd[tq[q]];
-    const int mode = d.combiner == DR_COMBINER_SUM ? 0 : (d.combiner == DR_COMBINER_MEAN ? 1 : 2);
-    const int64_t u = uq[q];
-    const int64_t c0 = p0 + q;          // chunk's first position
-    const bool first_chunk = c0 == sq[q];
-    auto scaled = [&](R& y, int64_t r) {
-      if (mode == 0) return;
-      const int32_t cnt = (r >= 0 && d.bag_off) ? d.bag_off[r + 1] - d.bag_off[r] : 1;
-      if (cnt != 1) {
-        const float sc = mode == 2 ? (float)(1.0 / sqrt((double)cnt)) : (float)(1.0 / (double)cnt);
+    const int mode = mode_of(d);
+    scaled(x[q], d, mode, rq[q]);
+    R acc;
+    if (mode == 0) {   // 0 + x_0 (a chunk head of a one-position run is its run head)
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) y.v[c] = vmul(y.v[c], sc);
-      }
-    };
+      for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<V>();
+      acc_add(acc, x[q]);
+    } else {
+      acc = x[q];
+    }
+    store_row<VEC, G, CPL>(acc, out + uq[q] * (int64_t)dim, lg, dv);
+  }
+  // -- chunk heads of longer runs: state re-read from memory so that the
+  // per-position arrays above are dead here (register pressure, occupancy) --
+  while (multi) {
+    const int q = __builtin_ctz(multi);
+    multi &= multi - 1;
+    const int64_t c0 = p0 + q;          // chunk's first position
+    const int64_t u = (int64_t)skey[c0];
+    const int t = table_of(g.koff, T, u, ufirst < N ? ufirst : 0);
+    const dr_pool_grad_desc& d = sd[t];
+    const int mode = mode_of(d);
+    const bool first_chunk = c0 == 0 || (int64_t)skey[c0 - 1] != u;
     R acc;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<V>();
-    // UnsortedSegmentSum order 0 + x_0 + x_1 ... (sum); x_0 * s + ... (mean/sqrtn);
-    // a later chunk's partial starts at its first element
     bool fresh = !(first_chunk && mode == 0);
-    if (single[q]) {
-      scaled(x[q], rq[q]);
-      if (fresh)
-        acc = x[q];
-      else
-        acc_add(acc, x[q]);
-    } else {
-      const int64_t lim = c0 + kGradChunk < N ? c0 + kGradChunk : N;
-      const float* tg = d.top_grad;
-      const int64_t ts = d.top_stride;
-      const int64_t* segp = d.seg;
-      const int64_t sst = d.seg_stride;
-      const int64_t kt0 = g.koff[tq[q]];
-      const int64_t nnz_t = d.nnz;
-      bool cbad = false;
-      for (int64_t p = c0; p < lim; p += kGradChain) {
-        R y[kGradChain];
-        int64_t ry[kGradChain];
-        bool ok[kGradChain];
+    const int64_t lim = c0 + kGradChunk < N ? c0 + kGradChunk : N;
+    const float* tg = d.top_grad;
+    const int64_t ts = d.top_stride;
+    const int64_t* segp = d.seg;
+    const int64_t sst = d.seg_stride;
+    const int64_t kt0 = g.koff[t];
+    const int64_t nnz_t = d.nnz;
+    bool cbad = false;
+    for (int64_t p = c0; p < lim; p += kGradChain) {
+      R y[kGradChain];
+      int64_t ry[kGradChain];
+      bool ok[kGradChain];
 #pragma unroll
-        for (int j = 0; j < kGradChain; ++j) {  // keys and sources: unconditional, clamped
-          const int64_t pj = p + j < N ? p + j : N - 1;
-          const int64_t kj = (int64_t)skey[pj];
-          ok[j] = (p + j < lim) & (kj == u);  // monotone: sorted keys
-          const int64_t k = (int64_t)perm[pj] - kt0;
-          ry[j] = ((k >= 0) & (k < nnz_t)) ? k : 0;
-        }
-        if (segp) {
-#pragma unroll
-          for (int j = 0; j < kGradChain; ++j) ry[j] = segp[ry[j] * sst];
-        }
-#pragma unroll
-        for (int j = 0; j < kGradChain; ++j) {
-          const bool okr = (ry[j] >= 0) & (ry[j] < B);
-          cbad |= ok[j] & !okr;
-          ry[j] = okr ? ry[j] : -1;
-          load_row_u<VEC, G, CPL>(y[j], tg + (okr ? ry[j] : 0) * ts, lg, dv);
-        }
-#pragma unroll
-        for (int j = 0; j < kGradChain; ++j) {
-          if (!ok[j]) break;
-          if (ry[j] < 0) {
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) y[j].v[c] = vzero<V>();
-          }
-          scaled(y[j], ry[j]);
-          if (fresh) {
-            acc = y[j];
-            fresh = false;
-          } else {
-            acc_add(acc, y[j]);
-          }
-        }
-        if (!ok[kGradChain - 1]) break;
+      for (int j = 0; j < kGradChain; ++j) {  // keys and sources: unconditional, clamped
+        const int64_t pj = p + j < N ? p + j : N - 1;
+        const int64_t kj = (int64_t)skey[pj];
+        ok[j] = (p + j < lim) & (kj == u);  // monotone: sorted keys
+        const int64_t k = (int64_t)perm[pj] - kt0;
+        ry[j] = ((k >= 0) & (k < nnz_t)) ? k : 0;
       }
-      if (cbad) latch(st, DR_INVALID_ARGUMENT);
+      if (segp) {
+#pragma unroll
+        for (int j = 0; j < kGradChain; ++j) ry[j] = segp[ry[j] * sst];
+      }
+#pragma unroll
+      for (int j = 0; j < kGradChain; ++j) {
+        const bool okr = (ry[j] >= 0) & (ry[j] < B);
+        cbad |= ok[j] & !okr;
+        ry[j] = okr ? ry[j] : -1;
+        load_row_u<VEC, G, CPL>(y[j], tg + (okr ? ry[j] : 0) * ts, lg, dv);
+      }
+#pragma unroll
+      for (int j = 0; j < kGradChain; ++j) {
+        if (!ok[j]) break;
+        if (ry[j] < 0) {
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) y[j].v[c] = vzero<V>();
+        }
+        scaled(y[j], d, mode, ry[j]);
+        if (fresh) {
+          acc = y[j];
+          fresh = false;
+        } else {
+          acc_add(acc, y[j]);
+        }
+      }
+      if (!ok[kGradChain - 1]) break;
     }
+    if (cbad) latch(st, DR_INVALID_ARGUMENT);
     if (first_chunk) {
       store_row<VEC, G, CPL>(acc, out + u * (int64_t)dim, lg, dv);
       // a run longer than one chunk: queue it for grad_finish_kernel
