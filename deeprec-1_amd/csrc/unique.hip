@@ -19,7 +19,9 @@
 //   2. flag[i] = (slot == i); one exclusive scan over all features;
 //      the local unique id is prefix[i] - prefix[first position of table t]
 //      (a table's first position is always a first occurrence);
-//   3. idx[i] = uid(slot(i)); counts by integer atomics (order-free, exact).
+//   3. idx[i] = prefix[slot value] - prefix[table start] in the same pass
+//      that writes the unique keys; counts by integer atomics (order-free,
+//      exact).
 // Every key value (-1 included) is an ordinary key: the empty pattern is a
 // position (0xFFFFFFFF), never a key.
 // Outputs keep the input layout: table t's uniques / counts sit at
@@ -38,7 +40,6 @@ struct UniqGroup {
 
 struct UniqueWs {
   uint32_t* minpos;  // [hash_total] first position of the slot's key
-  int32_t* tuid;     // [hash_total]
   int32_t* slot_of;  // [n]
   int32_t* flags;    // [n] scan output
   int64_t* total;    // [1]
@@ -62,7 +63,6 @@ static UniqueWs carve_unique(void* ws, int64_t n, int64_t hash_total, size_t* us
   Carver c(ws);
   UniqueWs u;
   u.minpos = c.take<uint32_t>(hash_total);
-  u.tuid = c.take<int32_t>(hash_total);
   u.slot_of = c.take<int32_t>(n > 0 ? n : 1);
   u.flags = c.take<int32_t>(n > 0 ? n : 1);
   u.total = c.take<int64_t>(1);
@@ -133,34 +133,23 @@ __global__ void unique_flag_kernel(int64_t n, const uint32_t* __restrict__ minpo
   flags[i] = minpos[slot_of[i]] == (uint32_t)i ? 1 : 0;
 }
 
-// After the scan flags[] holds exclusive prefix sums.
+// After the scan flags[] holds exclusive prefix sums.  One pass writes idx
+// (the uid of the key's first position, read through the slot) and, at first
+// positions, the unique key; no per-slot uid table is written or gathered.
 __global__ void unique_emit_kernel(UniqGroup g, int T, const int64_t* __restrict__ keys,
                                    const uint32_t* __restrict__ minpos,
                                    const int32_t* __restrict__ slot_of,
                                    const int32_t* __restrict__ prefix, int64_t* __restrict__ uniq,
-                                   int32_t* __restrict__ tuid) {
+                                   int32_t* __restrict__ idx, int32_t* __restrict__ counts) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= g.koff[T]) return;
-  const int32_t s = slot_of[i];
-  if (minpos[s] == (uint32_t)i) {
-    const int t = group_table(g, T, i);
-    const int32_t u = prefix[i] - prefix[g.koff[t]];
-    uniq[g.koff[t] + u] = keys[i];
-    tuid[s] = u;
-  }
-}
-
-__global__ void unique_expand_kernel(UniqGroup g, int T, const int32_t* __restrict__ slot_of,
-                                     const int32_t* __restrict__ tuid, int32_t* __restrict__ idx,
-                                     int32_t* __restrict__ counts) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= g.koff[T]) return;
-  const int32_t u = tuid[slot_of[i]];
+  const int t = group_table(g, T, i);
+  const int64_t kt = g.koff[t];
+  const uint32_t m = minpos[slot_of[i]];
+  const int32_t u = prefix[m] - prefix[kt];
   idx[i] = u;
-  if (counts) {
-    const int t = group_table(g, T, i);
-    atomicAdd(&counts[g.koff[t] + u], 1);
-  }
+  if (m == (uint32_t)i) uniq[kt + u] = keys[i];
+  if (counts) atomicAdd(&counts[kt + u], 1);
 }
 
 __global__ void unique_counts_kernel(UniqGroup g, int T, const int32_t* __restrict__ prefix,
@@ -217,9 +206,7 @@ extern "C" int dr_unique_grouped(const int64_t* keys, const int64_t* koff_host, 
   int rc = scan_exclusive_i32(u.flags, u.flags, n, nullptr, u.total, u.scan_ws, st);
   if (rc) return rc;
   hipLaunchKernelGGL(unique_emit_kernel, dim3(blocks), dim3(256), 0, st, g, T, keys, u.minpos,
-                     u.slot_of, u.flags, uniq_out, u.tuid);
-  hipLaunchKernelGGL(unique_expand_kernel, dim3(blocks), dim3(256), 0, st, g, T, u.slot_of, u.tuid,
-                     idx_out, counts_out);
+                     u.slot_of, u.flags, uniq_out, idx_out, counts_out);
   hipLaunchKernelGGL(unique_counts_kernel, dim3(1), dim3(64), 0, st, g, T, u.flags, u.total,
                      num_unique);
   DR_LAUNCH_CHECK();
