@@ -876,11 +876,23 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
     pp = pp < 0 ? 0 : (pp >= N ? N - 1 : pp);
     uk[q + 1] = (int64_t)skey[pp];
   }
+  // run starts are needed only by positions inside a run (chunk alignment);
+  // a wave with none (all-distinct ids, the common case) skips that
+  // dependent load -- the chain key -> start -> source -> row is the
+  // kernel's latency bound
   int64_t rsq[NB];
+  bool inner = false;
 #pragma unroll
-  for (int q = 0; q < NB; ++q) {
-    const int64_t u = uk[q + 1];
-    rsq[q] = run_start[u < N ? u : 0];
+  for (int q = 0; q < NB; ++q) inner |= (p0 + q) > 0 && uk[q] == uk[q + 1];
+  if (__ballot(inner)) {
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int64_t u = uk[q + 1];
+      rsq[q] = run_start[u < N ? u : 0];
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < NB; ++q) rsq[q] = p0 + q;
   }
   bool head[NB], single[NB];
   int64_t uq[NB], sq[NB];
