@@ -954,12 +954,14 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
   auto mode_of = [](const dr_pool_grad_desc& d) {
     return d.combiner == DR_COMBINER_SUM ? 0 : (d.combiner == DR_COMBINER_MEAN ? 1 : 2);
   };
-  // -- one-position runs (every run of all-distinct ids): the row is loaded --
+  // -- one-position runs (every run of all-distinct ids): the row is loaded.
+  // A one-position LAST chunk of a long run is not one of them: it is a
+  // partial, left to the chunk path below --
   unsigned multi = 0;
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
     if (!head[q]) continue;
-    if (!single[q]) {
+    if (!single[q] || sq[q] != p0 + q) {
       multi |= 1u << q;
       continue;
     }
