@@ -63,15 +63,21 @@ __global__ void fused_grad_kernel(const float* __restrict__ top, const float* __
 }
 
 // owner = key mod world (non-negative), sentinel bucket `world` past n_eff.
+// premod > 0: owner = floormod(floormod(key, premod), world) (EV partitions).
 __global__ void owner_keys_kernel(const int64_t* __restrict__ keys, int64_t n, const int64_t* n_dev,
-                                  int world, uint64_t* __restrict__ okey, int32_t* __restrict__ pos,
-                                  unsigned long long* __restrict__ counts) {
+                                  int world, int64_t premod, uint64_t* __restrict__ okey,
+                                  int32_t* __restrict__ pos, unsigned long long* __restrict__ counts) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t ne = eff_n(n, n_dev);
   int64_t o = world;
   if (i < ne) {
-    o = keys[i] % world;
+    int64_t k = keys[i];
+    if (premod > 0) {
+      k %= premod;
+      if (k < 0) k += premod;
+    }
+    o = k % world;
     if (o < 0) o += world;
     atomicAdd(&counts[o], 1ull);
   }
@@ -267,6 +273,13 @@ size_t dr_partition_workspace_size(int64_t n) {
 int dr_partition_by_owner(const int64_t* keys, int64_t n, const int64_t* n_dev, int world,
                           int64_t* keys_out, int32_t* perm_out, int64_t* send_counts, void* ws,
                           size_t ws_bytes, void* stream) {
+  return dr_partition_by_owner_mod(keys, n, n_dev, world, 0, keys_out, perm_out, send_counts, ws,
+                                   ws_bytes, stream);
+}
+
+int dr_partition_by_owner_mod(const int64_t* keys, int64_t n, const int64_t* n_dev, int world,
+                              int64_t premod, int64_t* keys_out, int32_t* perm_out,
+                              int64_t* send_counts, void* ws, size_t ws_bytes, void* stream) {
   using namespace dr;
   DR_REQUIRE(world >= 1 && world <= 4096, DR_INVALID_ARGUMENT, "bad world size");
   DR_REQUIRE(ws_bytes >= dr_partition_workspace_size(n), DR_INVALID_ARGUMENT,
@@ -283,7 +296,7 @@ int dr_partition_by_owner(const int64_t* keys, int64_t n, const int64_t* n_dev, 
   void* sws = c.take<char>(sb);
   const unsigned blocks = (unsigned)ceil_div(n, 256);
   hipLaunchKernelGGL(owner_keys_kernel, dim3(blocks), dim3(256), 0, st, keys, n, n_dev, world,
-                     okey, pos, (unsigned long long*)send_counts);
+                     premod, okey, pos, (unsigned long long*)send_counts);
   DR_LAUNCH_CHECK();
   int bits = 0;
   while ((1 << bits) <= world) ++bits;

@@ -846,7 +846,9 @@ __global__ void grad_run_start_kernel(const uint64_t* __restrict__ skey, int64_t
   if (u < (uint64_t)N && (p == 0 || skey[p - 1] != u)) run_start[u] = (int32_t)p;
 }
 
-template <int VEC, int G, int CPL, int NB>
+// W: some feature of the group is weighted (dr_pool_grad_desc.weights): a
+// separate instantiation, so the unweighted kernel keeps its register budget.
+template <int VEC, int G, int CPL, int NB, bool W>
 __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64_t B,
                                                        const uint64_t* __restrict__ skey,
                                                        const int32_t* __restrict__ perm,
@@ -911,6 +913,7 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
   }
   // -- source rows of the head positions: one batch of unconditional loads --
   int64_t rq[NB];
+  int64_t kq[W ? NB : 1];  // feature-local position (weight index)
   bool bad = false;
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
@@ -918,6 +921,7 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
     pp = pp >= N ? N - 1 : pp;
     const int64_t k = (int64_t)perm[pp] - g.koff[tq[q]];
     rq[q] = head[q] && k >= 0 && k < sd[tq[q]].nnz ? k : 0;
+    if (W) kq[W ? q : 0] = rq[q];
   }
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
@@ -954,6 +958,22 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
   auto mode_of = [](const dr_pool_grad_desc& d) {
     return d.combiner == DR_COMBINER_SUM ? 0 : (d.combiner == DR_COMBINER_MEAN ? 1 : 2);
   };
+  // weighted: (g / bag_scale[bag]) * w[k]  (RealDiv grad, then Mul grad)
+  auto wscaled = [&](R& y, const dr_pool_grad_desc& d, int64_t r, int64_t k) {
+    if (d.bag_scale) {
+      const float q = d.bag_scale[r >= 0 ? r : 0];
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) y.v[c] = vdiv(y.v[c], q);
+    }
+    const float w = d.weights[k];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) y.v[c] = vmul(y.v[c], w);
+  };
+  // the weighted gradient reaches the rows as IndexedSlices -> dense, an
+  // UnsortedSegmentSum (0 + x_0 + ...) whatever the combiner
+  auto zero_start = [&](const dr_pool_grad_desc& d, int mode) {
+    return mode == 0 || (W && d.weights);
+  };
   // -- one-position runs (every run of all-distinct ids): the row is loaded.
   // A one-position LAST chunk of a long run is not one of them: it is a
   // partial, left to the chunk path below --
@@ -967,9 +987,12 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
     }
     const dr_pool_grad_desc& d = sd[tq[q]];
     const int mode = mode_of(d);
-    scaled(x[q], d, mode, rq[q]);
+    if (W && d.weights)
+      wscaled(x[q], d, rq[q], kq[W ? q : 0]);
+    else
+      scaled(x[q], d, mode, rq[q]);
     R acc;
-    if (mode == 0) {   // 0 + x_0 (a chunk head of a one-position run is its run head)
+    if (zero_start(d, mode)) {   // 0 + x_0 (a chunk head of a one-position run is its run head)
 #pragma unroll
       for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<V>();
       acc_add(acc, x[q]);
@@ -992,7 +1015,7 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
     R acc;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<V>();
-    bool fresh = !(first_chunk && mode == 0);
+    bool fresh = !(first_chunk && zero_start(d, mode));
     const int64_t lim = c0 + kGradChunk < N ? c0 + kGradChunk : N;
     const float* tg = d.top_grad;
     const int64_t ts = d.top_stride;
@@ -1004,6 +1027,7 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
     for (int64_t p = c0; p < lim; p += kGradChain) {
       R y[kGradChain];
       int64_t ry[kGradChain];
+      int64_t ky[W ? kGradChain : 1];
       bool ok[kGradChain];
 #pragma unroll
       for (int j = 0; j < kGradChain; ++j) {  // keys and sources: unconditional, clamped
@@ -1012,6 +1036,7 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
         ok[j] = (p + j < lim) & (kj == u);  // monotone: sorted keys
         const int64_t k = (int64_t)perm[pj] - kt0;
         ry[j] = ((k >= 0) & (k < nnz_t)) ? k : 0;
+        if (W) ky[W ? j : 0] = ry[j];
       }
       if (segp) {
 #pragma unroll
@@ -1031,7 +1056,10 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
 #pragma unroll
           for (int c = 0; c < CPL; ++c) y[j].v[c] = vzero<V>();
         }
-        scaled(y[j], d, mode, ry[j]);
+        if (W && d.weights)
+          wscaled(y[j], d, ry[j], ky[W ? j : 0]);
+        else
+          scaled(y[j], d, mode, ry[j]);
         if (fresh) {
           acc = y[j];
           fresh = false;
@@ -1111,11 +1139,92 @@ static void launch_grad_csr(const GradGroup& g, int T, int64_t B, const uint64_t
   hipLaunchKernelGGL(grad_run_start_kernel, dim3((unsigned)ceil_div(N > 0 ? N : 1, 256)),
                      dim3(256), 0, s, skey, N, w.run_start, w.nlong);
   const int64_t blocks = ceil_div(ceil_div(N > 0 ? N : 1, NB), 256 / G);
-  hipLaunchKernelGGL((grad_seg_kernel<VEC, G, CPL, NB>), dim3((unsigned)blocks), dim3(256), 0, s,
-                     g, T, B, skey, perm, w.run_start, dim, out, w.part, w.longs, w.nlong, st);
+  bool weighted = false;
+  for (int t = 0; t < T; ++t) weighted = weighted || g.d[t].weights;
+  if (weighted)
+    hipLaunchKernelGGL((grad_seg_kernel<VEC, G, CPL, NB, true>), dim3((unsigned)blocks), dim3(256),
+                       0, s, g, T, B, skey, perm, w.run_start, dim, out, w.part, w.longs, w.nlong,
+                       st);
+  else
+    hipLaunchKernelGGL((grad_seg_kernel<VEC, G, CPL, NB, false>), dim3((unsigned)blocks),
+                       dim3(256), 0, s, g, T, B, skey, perm, w.run_start, dim, out, w.part,
+                       w.longs, w.nlong, st);
   if (N > kGradChunk)
     hipLaunchKernelGGL((grad_finish_kernel<VEC, G, CPL>), dim3(64), dim3(256), 0, s, skey, N, dim,
                        out, w.part, w.longs, w.nlong, N / kGradChunk + 2);
+}
+
+// ---- weighted-lookup divisor and clip_by_norm backward ----------------------
+// q[b] = 0 + w_0 + w_1 ... (mean) or sqrtf(0 + w_0^2 + ...) (sqrtn), in the
+// weighted forward's order (pool_bag's weighted branch).
+__global__ void bag_weight_scale_kernel(const float* __restrict__ w,
+                                        const int32_t* __restrict__ off, int64_t B, int combiner,
+                                        float* __restrict__ q) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float s = 0.f;
+  for (int64_t k = off[b]; k < off[b + 1]; ++k) {
+    const float x = w[k];
+    s = s + (combiner == DR_COMBINER_SQRTN ? x * x : x);
+  }
+  q[b] = combiner == DR_COMBINER_SQRTN ? sqrtf(s) : s;
+}
+
+// One lane group per row: TF's chain rule through clip_by_norm's ops
+// (clip_ops.py:169-179), see dr_clip_by_norm_grad in the header.
+template <int VEC, int G, int CPL>
+__global__ __launch_bounds__(256) void clip_grad_kernel(const float* __restrict__ pool,
+                                                        int64_t pool_rows,
+                                                        const int64_t* __restrict__ rows,
+                                                        const float* __restrict__ dflt,
+                                                        int64_t dstride, const int64_t* n_dev,
+                                                        int64_t n, int dim, float c,
+                                                        float* __restrict__ grad, int* st) {
+  using R = Row<VEC, G, CPL>;
+  constexpr int GPB = 256 / G;
+  const int64_t i = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+  const bool live = i < eff_n(n, n_dev);
+  const int lg = threadIdx.x % G;
+  const int dv = dim / VEC;
+  const int64_t r = live ? rows[i] : 0;
+  const float* src;
+  if (r < 0) {
+    src = dflt ? dflt + (-r - 1) * dstride : nullptr;
+  } else if (r < pool_rows) {
+    src = pool + r * (int64_t)dim;
+  } else {
+    src = nullptr;
+  }
+  if (live && !src) latch(st, DR_INVALID_ARGUMENT);
+  R v, g;
+  load_row<VEC, G, CPL>(v, live ? src : nullptr, lg, dv);
+  load_row<VEC, G, CPL>(g, live ? grad + i * (int64_t)dim : nullptr, lg, dv);
+  // l2sum = reduce_sum(v * v); l2norm = l2sum > 0 ? sqrt(l2sum) : l2sum
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) s += vdot(v.v[k]);
+  s = group_sum<G>(s);
+  const bool pred = s > 0.f;
+  const float l2 = pred ? sqrtf(s) : s;
+  const float m = l2 > c ? l2 : c;
+  // dL/dm = sum_d g * ((-(v * c)) / m) / m   (RealDiv's grad w.r.t. y)
+  float gm = 0.f;
+  const float* gp = reinterpret_cast<const float*>(&g.v[0]);
+  const float* vp = reinterpret_cast<const float*>(&v.v[0]);
+#pragma unroll
+  for (int k = 0; k < VEC * CPL; ++k) gm += gp[k] * ((-(vp[k] * c) / m) / m);
+  gm = group_sum<G>(gm);
+  const float gl2 = l2 >= c ? gm : 0.f;             // Maximum: x >= y takes the grad
+  const float gs = pred ? (0.5f * gl2) / l2 : 0.f;  // Sqrt grad, where(pred, ...)
+  R o;
+  float* op = reinterpret_cast<float*>(&o.v[0]);
+#pragma unroll
+  for (int k = 0; k < VEC * CPL; ++k) {
+    const float a = (gp[k] / m) * c;  // values * clip_norm path
+    const float b = gs * vp[k];       // values * values path, both factors
+    op[k] = (a + b) + b;
+  }
+  if (live) store_row<VEC, G, CPL>(o, grad + i * (int64_t)dim, lg, dv);
 }
 
 }  // namespace dr
@@ -1325,6 +1434,8 @@ int dr_pool_grad_grouped(const dr_pool_grad_desc* descs_host, int num_tables, in
                "table %d: missing pointers", t);
     DR_REQUIRE(d.combiner == DR_COMBINER_SUM || d.bag_off || !d.seg, DR_INVALID_ARGUMENT,
                "table %d: mean/sqrtn of multi-hot bags need bag_off", t);
+    DR_REQUIRE(!d.weights || d.combiner == DR_COMBINER_SUM || d.bag_scale, DR_INVALID_ARGUMENT,
+               "table %d: weighted mean/sqrtn needs bag_scale (dr_bag_weight_scale)", t);
     g.d[t] = d;
     g.koff[t + 1] = g.koff[t] + d.nnz;
     aligned = aligned && ((uintptr_t)d.top_grad & 15) == 0 && d.top_stride % 4 == 0;
@@ -1404,6 +1515,52 @@ int dr_pool_grad(const float* top_grad, int64_t top_stride, int64_t batch, int d
   return segsum_driver(idx, n, n, num_unique, top_grad, top_stride, batch, seg,
                        combiner == DR_COMBINER_SUM ? nullptr : bag_off, dim, mode, grad_unique,
                        ws, S(stream));
+}
+
+int dr_bag_weight_scale(const float* weights, const int32_t* bag_off, int64_t batch, int combiner,
+                        float* bag_scale, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && (batch == 0 || (weights && bag_off && bag_scale)), DR_INVALID_ARGUMENT,
+             "dr_bag_weight_scale: missing pointers");
+  if (batch == 0) return DR_OK;
+  hipLaunchKernelGGL(bag_weight_scale_kernel, dim3((unsigned)ceil_div(batch, 256)), dim3(256), 0,
+                     S(stream), weights, bag_off, batch, combiner, bag_scale);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_clip_by_norm_grad(const float* pool, int64_t pool_rows, const int64_t* rows,
+                         const float* default_rows, int64_t default_stride, const int64_t* n_dev,
+                         int64_t n, int dim, float max_norm, float* grad, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(n >= 0 && dim > 0 && dim <= 1024 && (n == 0 || (pool && rows && grad)),
+             DR_INVALID_ARGUMENT, "dr_clip_by_norm_grad: bad arguments");
+  if (n == 0) return DR_OK;
+  int* st = status_word();
+  DR_REQUIRE(st, DR_INTERNAL, "status word unavailable");
+  hipStream_t s = S(stream);
+  const bool al = dim % 4 == 0 && ((uintptr_t)grad & 15) == 0 && ((uintptr_t)pool & 15) == 0 &&
+                  (!default_rows || (((uintptr_t)default_rows & 15) == 0 && default_stride % 4 == 0));
+#define DR_CLIPG(V, G, C)                                                                      \
+  do {                                                                                         \
+    hipLaunchKernelGGL((clip_grad_kernel<V, G, C>), dim3((unsigned)ceil_div(n, 256 / G)),    \
+                       dim3(256), 0, s, pool, pool_rows, rows, default_rows, default_stride,  \
+                       n_dev, n, dim, max_norm, grad, st);                                     \
+    DR_LAUNCH_CHECK();                                                                         \
+    return DR_OK;                                                                              \
+  } while (0)
+  if (al) {
+    const int d4 = dim / 4;
+    if (d4 <= 8) DR_CLIPG(4, 8, 1);
+    if (d4 <= 16) DR_CLIPG(4, 16, 1);
+    if (d4 <= 32) DR_CLIPG(4, 32, 1);
+    if (d4 <= 64) DR_CLIPG(4, 64, 1);
+    DR_CLIPG(4, 64, 4);
+  }
+  if (dim <= 64) DR_CLIPG(1, 64, 1);
+  if (dim <= 256) DR_CLIPG(1, 64, 4);
+  DR_CLIPG(1, 64, 16);
+#undef DR_CLIPG
 }
 
 }  // extern "C"

@@ -20,6 +20,7 @@ _CODE_NAMES = {3: "InvalidArgument", 5: "NotFound", 6: "AlreadyExists", 8: "Reso
 COMBINERS = {"sum": 0, "mean": 1, "sqrtn": 2}
 ORDER_ALI, ORDER_SEQ = 0, 1
 MAX_GROUP = 32
+MAX_PARTITIONS = 64
 POOL_ONEHOT = 1
 
 
@@ -50,6 +51,7 @@ class DrPoolGradDesc(C.Structure):
         ("top_grad", C.c_void_p), ("top_stride", C.c_int64), ("bag_off", C.c_void_p),
         ("seg", C.c_void_p), ("seg_stride", C.c_int64), ("idx", C.c_void_p), ("nnz", C.c_int64),
         ("num_unique", C.c_void_p), ("combiner", C.c_int32),
+        ("weights", C.c_void_p), ("bag_scale", C.c_void_p),
     ]
 
 
@@ -146,6 +148,16 @@ SIGNATURES = {
                                      _SZ, _P]),
     "dr_fused_local_lookup_grad": (_I32, [_P, _P, _I64, _I32, _P, _P, _I64, _I64, _I32, _F32, _P,
                                           _P]),
+    "dr_bag_weight_scale": (_I32, [_P, _P, _I64, _I32, _P, _P]),
+    "dr_clip_by_norm_grad": (_I32, [_P, _I64, _P, _P, _I64, _P, _I64, _I32, _F32, _P, _P]),
+    "dr_fused_pre_lookup_workspace_size": (_SZ, [_I64]),
+    "dr_fused_pre_lookup": (_I32, [_P, _P, _I64, _P, _I32, _P, _P, _P, _P, _SZ, _P]),
+    "dr_fused_post_lookup_workspace_size": (_SZ, [_I64, _I64]),
+    "dr_fused_post_lookup": (_I32, [_P, _P, _P, _I32, _I64, _I64, _I32, _I32, _F32, _P, _P, _P,
+                                    _SZ, _P]),
+    "dr_fused_post_lookup_grad": (_I32, [_P, _P, _P, _P, _I32, _I64, _I32, _P, _I32, _F32, _P,
+                                         _P]),
+    "dr_partition_by_owner_mod": (_I32, [_P, _I64, _P, _I32, _I64, _P, _P, _P, _P, _SZ, _P]),
     "dr_partition_workspace_size": (_SZ, [_I64]),
     "dr_partition_by_owner": (_I32, [_P, _I64, _P, _I32, _P, _P, _P, _P, _SZ, _P]),
     "dr_rows_scatter": (_I32, [_P, _P, _I64, _P, _I32, _P, _P]),

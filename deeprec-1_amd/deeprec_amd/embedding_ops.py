@@ -187,38 +187,82 @@ def _grad_to_slices(f, g, col, top_stride):
     floats) -> IndexedSlices over the unique ids, through the grouped
     backward kernel with one feature (chunked runs: a hot id does not
     serialise one wave)."""
-    if f.weights is not None or f.max_norm is not None:
-        raise NotImplementedError("backward of weighted / max_norm lookups is not implemented")
     if f.uniq is None:
         f.uniq, f.idx, _, f.U = ops.unique_device(f.values)
     grp = _UniqueGroup([f], f.uniq, f.U, [0, f.values.numel()])
     return grp.grads(g, [col], top_stride)[0]
 
 
+def _clip_grad(f, gs):
+    """Backward of the max_norm clip (embedding_ops._clip, applied to the
+    unique rows before pooling) on the per-unique grads gs, in place."""
+    p = f.params
+    if isinstance(p, EmbeddingVariable):
+        if f.defaults is not None:
+            dflt, stride = f.defaults, p.dim
+        else:
+            dflt, stride = _ev_default_dev(p), 0
+        ops.clip_by_norm_grad(gs, p.pool(), f.rows, f.max_norm, default_rows=dflt,
+                              default_stride=stride, n_dev=f.U)
+    else:
+        t = p.weight if isinstance(p, DenseTable) else p
+        ops.clip_by_norm_grad(gs, t.detach(), f.uniq, f.max_norm, pool_rows=t.shape[0],
+                              n_dev=f.U)
+
+
+def _trainable_tensors(feats):
+    """Plain torch tables of the features that require grad (each once)."""
+    out = []
+    for f in feats:
+        p = f.params
+        if torch.is_tensor(p) and p.requires_grad and all(p is not q for q in out):
+            out.append(p)
+    return out
+
+
+def _dense_grad(p, sl):
+    """IndexedSlices -> dense [R, D] gradient of a plain tensor table (the
+    reference's IndexedSlices-to-Tensor conversion, an UnsortedSegmentSum in
+    ascending slice order; rows past num_valid are skipped)."""
+    n = sl.indices.numel()
+    seg = sl.indices
+    if sl.num_valid is not None:
+        seg = torch.where(torch.arange(n, device=seg.device) < sl.num_valid, seg,
+                          torch.full_like(seg, -1))
+    return ops.unsorted_segment_sum(sl.values[:n], seg.to(torch.int32), p.shape[0])
+
+
 class _LookupFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, anchor, feats, order):
+    def forward(ctx, anchor, feats, order, *tensors):
         ctx.feats = feats
+        ctx.tensors = tensors
         return _pool_all(feats, order)
 
     @staticmethod
     def backward(ctx, grad_out):
         g = grad_out.contiguous()
-        _queue_grads(ctx.feats, g, 0, g.shape[1])
-        return None, None, None
+        dense = _queue_grads(ctx.feats, g, 0, g.shape[1], ctx.tensors)
+        return (None, None, None) + tuple(dense)
 
 
-def _queue_grads(feats, g, col0, total):
+def _queue_grads(feats, g, col0, total, tensors=()):
     """Per-feature IndexedSlices from the pooled grad g (rows of `total`
-    floats, feature columns starting at col0), queued on the variables."""
+    floats, feature columns starting at col0), queued on the variables;
+    returns the dense grads of the trainable plain tensors `tensors`."""
     cols, col = [], col0
     for f in feats:
         cols.append(col)
         col += f.params.dim if not torch.is_tensor(f.params) else f.params.shape[1]
+    dense = [None] * len(tensors)
     done = set()
     for i, f in enumerate(feats):
         holder = f.params
         if torch.is_tensor(holder):
+            for j, t in enumerate(tensors):
+                if t is holder:
+                    d = _dense_grad(t, _grad_to_slices(f, g, cols[i], total))
+                    dense[j] = d if dense[j] is None else dense[j] + d
             continue
         grp = getattr(f, "group", None)
         if grp is not None:
@@ -231,6 +275,7 @@ def _queue_grads(feats, g, col0, total):
                 x.params.pending_grads.append(sl)
             continue
         holder.pending_grads.append(_grad_to_slices(f, g, cols[i], total))
+    return dense
 
 
 class _StackFn(torch.autograd.Function):
@@ -386,13 +431,20 @@ class _UniqueGroup(object):
         """g: the pooled grad (base tensor), cols[t]: column of feature t.
         Returns one IndexedSlices per feature."""
         dev = g.device
-        D = self.feats[0].params.dim
+        p0 = self.feats[0].params
+        D = p0.shape[1] if torch.is_tensor(p0) else p0.dim
         descs = (_lib.DrPoolGradDesc * len(self.feats))()
+        keep = []   # per-bag weight divisors, alive until the launch is queued
         for t, f in enumerate(self.feats):
-            if f.weights is not None or f.max_norm is not None:
-                raise NotImplementedError("backward of weighted / max_norm lookups is not "
-                                          "implemented")
             d = descs[t]
+            if f.weights is not None:
+                # embedding_ops.py:609-651: (g / weight_sum) * w, unsorted_segment_sum
+                _bag_offsets_all([f])
+                d.weights = ptr(f.weights)
+                if f.combiner != "sum":
+                    q = ops.bag_weight_scale(f.weights, f.bag_off, f.combiner)
+                    keep.append(q)
+                    d.bag_scale = ptr(q)
             d.top_grad = g.data_ptr() + 4 * cols[t]
             d.top_stride = top_stride
             if f.onehot:
@@ -414,6 +466,9 @@ class _UniqueGroup(object):
                                          ptr(ws), wsb, stream_handle(dev)))
         ops._post(dev)
         k = self.koff
+        for t, f in enumerate(self.feats):
+            if f.max_norm is not None and k[t + 1] > k[t]:
+                _clip_grad(f, gu[k[t]:k[t + 1]])
         return [IndexedSlices(gu[k[t]:k[t + 1]], self.uniq[k[t]:k[t + 1]], self.U[t:t + 1], True)
                 for t in range(len(self.feats))]
 
@@ -451,16 +506,18 @@ def _fused_onehot(feats, order):
 
 def _run(feats, order=ORDER_ALI, need_grad=None):
     """Grouped pooled lookup of features sharing the batch -> [B, sum(D_t)]."""
+    tensors = _trainable_tensors(feats) if torch.is_grad_enabled() else []
     if need_grad is None:
-        need_grad = torch.is_grad_enabled() and any(not torch.is_tensor(f.params) for f in feats)
+        need_grad = torch.is_grad_enabled() and (
+            bool(tensors) or any(not torch.is_tensor(f.params) for f in feats))
     if not need_grad and _FUSED_ONEHOT:
         out = _fused_onehot(feats, order)
         if out is not None:
             return out
     _prepare_all(feats, need_grad)
     if need_grad:
-        anchor = [_anchor(f.params) for f in feats if not torch.is_tensor(f.params)][0]
-        return _LookupFn.apply(anchor, feats, order)
+        anchors = [_anchor(f.params) for f in feats if not torch.is_tensor(f.params)]
+        return _LookupFn.apply(anchors[0] if anchors else None, feats, order, *tensors)
     return _pool_all(feats, order)
 
 
@@ -541,28 +598,14 @@ def embedding_lookup(params, ids, partition_strategy="mod", name=None, max_norm=
     if isinstance(params, (list, tuple)) and len(params) == 1:
         params = params[0]
     if isinstance(params, (list, tuple)):
-        flat = ids.reshape(-1).to(torch.int64)
-        np_ = len(params)
-        if isinstance(params[0], EmbeddingVariable):
-            p_assign = flat % 1000 % np_           # embedding_ops.py:207-209
-            new_ids = flat
-        elif partition_strategy == "mod":
-            p_assign = flat % np_
-            new_ids = flat // np_
-        else:  # "div"
-            sizes = [p.get_shape()[0] if not torch.is_tensor(p) else p.shape[0] for p in params]
-            total = sum(sizes)
-            ipp, extras = total // np_, total % np_
-            p_assign = torch.maximum(flat // (ipp + 1), (flat - extras) // ipp)
-            new_ids = torch.where(p_assign < extras, flat % (ipp + 1), (flat - extras) % ipp)
-        D = params[0].dim if not torch.is_tensor(params[0]) else params[0].shape[1]
-        out = torch.empty((flat.numel(), D), dtype=torch.float32, device=flat.device)
-        for p in range(np_):
-            sel = torch.nonzero(p_assign == p).reshape(-1)
-            if sel.numel() == 0:
-                continue
-            out[sel] = embedding_lookup(params[p], new_ids[sel], ev_init_value=None)
-        res = out.reshape(tuple(ids.shape) + (D,))
+        flat = ids.reshape(-1).to(torch.int64).contiguous()
+        init = None
+        if ev_init_value is not None:
+            D = params[0].dim if not torch.is_tensor(params[0]) else params[0].shape[1]
+            init = torch.as_tensor(ev_init_value, dtype=torch.float32, device=flat.device)
+            init = init.expand(flat.numel(), D).contiguous()
+        res = _partitioned_gather(params, flat, None, counts, init, partition_strategy)
+        res = res.reshape(tuple(ids.shape) + (res.shape[1],))
     elif isinstance(params, EmbeddingVariable):
         res = params.sparse_read(ids, counts=counts, ev_init_value=ev_init_value)
     else:
@@ -576,27 +619,147 @@ def embedding_lookup(params, ids, partition_strategy="mod", name=None, max_norm=
     return res
 
 
+def _partition_plan(params, flat, n_dev, partition_strategy):
+    """dynamic_partition of ids over the partitions (embedding_ops.py:207-252):
+    EVs by ids % 1000 % np, dense tables by "mod" (id % np, id // np) or
+    "div" (dim-0 boundaries).  Returns (perm [n] int32, offs host list[np+1],
+    per-partition new ids [n] int64 in partition order); entries past n_dev
+    (device count) fall outside every partition.  One host read of the
+    partition sizes, as dynamic_partition's own output shapes need."""
+    np_ = len(params)
+    n = flat.numel()
+    if isinstance(params[0], EmbeddingVariable):
+        keys, perm, counts = ops.partition_by_owner_mod(flat, np_, 1000, n_dev=n_dev)
+        new_ids = keys
+    else:
+        if partition_strategy == "mod":
+            assign = flat
+        elif partition_strategy == "div":
+            sizes = [p.get_shape()[0] if not torch.is_tensor(p) else p.shape[0] for p in params]
+            total = sum(sizes)
+            ipp, extras = total // np_, total % np_
+            assign = torch.maximum(flat // (ipp + 1), (flat - extras) // max(ipp, 1))
+        else:
+            raise ValueError("Unrecognized partition strategy: " + partition_strategy)
+        _, perm, counts = ops.partition_by_owner(assign, np_, n_dev=n_dev)
+        src = flat.index_select(0, perm.to(torch.int64).clamp_(0, max(n - 1, 0)))
+        if partition_strategy == "mod":
+            new_ids = src // np_
+        else:
+            pa = torch.maximum(src // (ipp + 1), (src - extras) // max(ipp, 1))
+            new_ids = torch.where(pa < extras, src % (ipp + 1), (src - extras) % max(ipp, 1))
+    c = counts.cpu().tolist()
+    offs = [0]
+    for x in c:
+        offs.append(offs[-1] + int(x))
+    return perm, offs, new_ids
+
+
+class _PartitionedGatherFn(torch.autograd.Function):
+    """embedding_lookup over a partitioned variable: dynamic_partition ->
+    per-partition gather (EV KvResourceGather[V1] / dense ResourceGather) ->
+    parallel_dynamic_stitch (embedding_ops.py:207-299).  Backward: the
+    stitch's grad gathered back per partition = IndexedSlices queued on each
+    EV / DenseTable (or a dense grad for a plain tensor partition)."""
+
+    @staticmethod
+    def forward(ctx, anchor, params, flat, n_dev, counts, init, strategy, *tensors):
+        dev = flat.device
+        n = flat.numel()
+        p0 = params[0]
+        D = p0.dim if not torch.is_tensor(p0) else p0.shape[1]
+        perm, offs, new_ids = _partition_plan(params, flat, n_dev, strategy)
+        perm64 = perm.to(torch.int64)
+        emb_part = torch.empty((max(n, 1), D), dtype=torch.float32, device=dev)
+        for p, prm in enumerate(params):
+            a, b = offs[p], offs[p + 1]
+            if b == a:
+                continue
+            ids_p = new_ids[a:b]
+            if isinstance(prm, EmbeddingVariable):
+                sel = perm64[a:b]
+                cnt = None if counts is None else counts.index_select(0, sel)
+                ini = None if init is None else init.index_select(0, sel)
+                dflt = prm._defaults_for(b - a, None) if ini is None else ini
+                emb_part[a:b] = _ev_sparse_read(prm, ids_p, cnt, dflt)
+            else:
+                t = prm.weight if isinstance(prm, DenseTable) else prm
+                emb_part[a:b] = ops.gather(t.detach(), ids_p)
+        out = torch.zeros((n, D), dtype=torch.float32, device=dev)
+        if offs[-1]:
+            ops.rows_scatter(emb_part, perm[:offs[-1]], out)
+        ctx.params, ctx.perm, ctx.offs, ctx.new_ids = params, perm, offs, new_ids
+        ctx.tensors = tensors
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        offs, params = ctx.offs, ctx.params
+        D = g.shape[1]
+        gp = torch.empty((max(offs[-1], 1), D), dtype=torch.float32, device=g.device)
+        if offs[-1]:
+            ops.rows_pack(g, ctx.perm[:offs[-1]], gp)
+        dense = [None] * len(ctx.tensors)
+        for p, prm in enumerate(params):
+            a, b = offs[p], offs[p + 1]
+            if b == a:
+                continue
+            sl = IndexedSlices(gp[a:b], ctx.new_ids[a:b], unique=True)
+            if torch.is_tensor(prm):
+                for j, t in enumerate(ctx.tensors):
+                    if t is prm:
+                        d = _dense_grad(t, sl)
+                        dense[j] = d if dense[j] is None else dense[j] + d
+            else:
+                prm.pending_grads.append(sl)
+        return (None,) * 7 + tuple(dense)
+
+
+def _ev_sparse_read(ev, ids, counts, defaults):
+    """KvResourceGather[V1] of device ids with an explicit [n, D] default
+    block (or None = the EV's default row)."""
+    n = ids.numel()
+    out = torch.empty((n, ev.dim), dtype=torch.float32, device=ev.device)
+    cnt = None if counts is None else counts.to(torch.int32).contiguous()
+    wsb = lib().dr_ev_gather_workspace_size(n)
+    ws = workspace(wsb, ev.device)
+    check(lib().dr_ev_gather(ev.handle, ptr(ids.contiguous()), n, ptr(defaults), ptr(cnt), ptr(out),
+                             ptr(ws), wsb, stream_handle(ev.device)))
+    ops._post(ev.device)
+    return out
+
+
+def _partitioned_gather(params, flat, n_dev, counts, init, strategy):
+    tensors = [p for p in params if torch.is_tensor(p) and p.requires_grad]
+    anchors = [_anchor(p) for p in params if not torch.is_tensor(p)]
+    if torch.is_grad_enabled() and (anchors or tensors):
+        return _PartitionedGatherFn.apply(anchors[0] if anchors else None, params, flat, n_dev,
+                                          counts, init, strategy, *tensors)
+    with torch.no_grad():
+        return _PartitionedGatherFn.forward(_Ctx(), None, params, flat, n_dev, counts, init,
+                                            strategy)
+
+
+class _Ctx(object):
+    pass
+
+
 def _partitioned_lookup_sparse(params, sp_ids, sp_weights, partition_strategy, combiner,
                                max_norm):
-    values = sp_ids.values.to(torch.int64)
-    seg = sp_ids.indices[:, 0].to(torch.int32).contiguous()
+    """embedding_lookup_sparse over a partitioned variable
+    (embedding_ops.py:589-651): unique (with counts when an EV filter needs
+    them) -> partitioned gather of the unique ids -> pooled by idx.  The
+    gathered [U, D] block is the pooling's table, so max_norm / weights /
+    combiner and their backward are the single-table path's."""
+    values = sp_ids.values.to(torch.int64).contiguous()
     B = sp_ids.dense_shape[0]
-    if isinstance(params[0], EmbeddingVariable) and params[0].filter_freq == 0:
-        uniq, idx = ops.unique(values)
-        counts = None
-    else:
-        uniq, idx, counts = ops.unique_with_counts(values)
-    emb = embedding_lookup(params, uniq, partition_strategy, counts=counts)
-    if max_norm is not None:
-        l2 = torch.sqrt((emb * emb).sum(1, keepdim=True))
-        emb = emb * max_norm / torch.maximum(l2, torch.tensor(max_norm, device=emb.device))
-    if sp_weights is None:
-        fn = {"sum": ops.sparse_segment_sum, "mean": ops.sparse_segment_mean,
-              "sqrtn": ops.sparse_segment_sqrt_n}[combiner]
-        return fn(emb, idx, seg, num_segments=B)
-    f = _Feature(emb, idx.to(torch.int64), seg, B, sp_weights.values.to(torch.float32),
-                 combiner, None)
-    return _run([f], need_grad=False)
+    with_counts = isinstance(params[0], EmbeddingVariable) and params[0].filter_freq != 0
+    uniq, idx, cnt, U = ops.unique_device(values, with_counts)
+    emb = _partitioned_gather(params, uniq, U, cnt, None, partition_strategy)
+    w = None if sp_weights is None else sp_weights.values.to(torch.float32).contiguous()
+    f = _Feature(emb, idx.to(torch.int64), _seg_of(sp_ids), B, w, combiner, max_norm)
+    return _run([f])
 
 
 # ---------------------------------------------------------------------------
@@ -684,13 +847,71 @@ class _FusedLocalFn(torch.autograd.Function):
         return dense, None, None, None, None, None
 
 
-def fused_embedding_lookup_sparse(embedding_weights, sparse_ids, combiner="mean", max_norm=None,
-                                  name=None):
-    table = embedding_weights[0] if isinstance(embedding_weights, (list, tuple)) \
-        else embedding_weights
-    if isinstance(table, DenseTable):
-        table = table.weight
-    mn = -1.0 if max_norm is None else float(max_norm)
-    return _FusedLocalFn.apply(table, sparse_ids.values.to(torch.int64).contiguous(),
-                               sparse_ids.indices.to(torch.int64).contiguous(),
-                               sparse_ids.dense_shape[0], combiner, mn)
+class _FusedPartitionedFn(torch.autograd.Function):
+    """fused_embedding_lookup_sparse (python/ops/fused_embedding_ops.py:45-67):
+    PreLookUp -> one Gather per partition -> PostLookUp; backward
+    PostLookUpGrad (:88-98) -> the Gather grads, IndexedSlices(grad_shard,
+    partitioned_values[i]) per partition."""
+
+    @staticmethod
+    def forward(ctx, anchor, parts, sp_values, sp_indices, dense_shape, combiner, max_norm,
+                *tensors):
+        tabs = [p.weight if isinstance(p, DenseTable) else p.detach() for p in parts]
+        pv, pi = ops.fused_embedding_sparse_pre_look_up([t.shape for t in tabs], sp_values,
+                                                        sp_indices)
+        shards = [ops.gather(t, v) for t, v in zip(tabs, pv)]
+        out, fnum = ops.fused_embedding_sparse_post_look_up(shards, pi, dense_shape, pv, combiner,
+                                                            max_norm)
+        ctx.parts, ctx.pv, ctx.pi, ctx.shards, ctx.fnum = parts, pv, pi, shards, fnum
+        ctx.combiner, ctx.max_norm, ctx.tensors = combiner, max_norm, tensors
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        grads = ops.fused_embedding_sparse_post_look_up_grad(
+            g.contiguous(), ctx.shards, ctx.pi, ctx.fnum, ctx.combiner, ctx.max_norm)
+        dense = [None] * len(ctx.tensors)
+        for prm, gs, v in zip(ctx.parts, grads, ctx.pv):
+            sl = IndexedSlices(gs, v)
+            if isinstance(prm, DenseTable):
+                prm.pending_grads.append(sl)
+                continue
+            for j, t in enumerate(ctx.tensors):
+                if t is prm:
+                    d = _dense_grad(t, sl)
+                    dense[j] = d if dense[j] is None else dense[j] + d
+        return (None,) * 7 + tuple(dense)
+
+
+def fused_embedding_lookup_sparse(embedding_weights, sparse_ids, combiner=None, name=None,
+                                  max_norm=None):
+    """python/ops/fused_embedding_ops.py:18-67 over one table or a list of
+    partitions ("div" by partition_shapes[i][0]), dense tables (DenseTable
+    or torch tensors) as in the reference."""
+    if embedding_weights is None:
+        raise ValueError("Missing embedding_weights %s." % embedding_weights)
+    parts = list(embedding_weights) if isinstance(embedding_weights, (list, tuple)) \
+        else [embedding_weights]
+    if not parts:
+        raise ValueError("Missing embedding_weights %s." % embedding_weights)
+    if combiner is None:
+        combiner = "mean"
+    if combiner not in ("mean", "sqrtn", "sum"):
+        raise ValueError("combiner must be one of 'mean', 'sqrtn' or 'sum'")
+    if not isinstance(sparse_ids, SparseTensor):
+        raise TypeError("sparse_ids must be SparseTensor")
+    for p in parts:
+        if isinstance(p, EmbeddingVariable):
+            raise TypeError("fused_embedding_lookup_sparse takes dense tables (the reference's "
+                            "fused ops do not support EmbeddingVariables)")
+    tensors = [p for p in parts if torch.is_tensor(p) and p.requires_grad] \
+        if torch.is_grad_enabled() else []
+    anchors = [_anchor(p) for p in parts if isinstance(p, DenseTable)] \
+        if torch.is_grad_enabled() else []
+    vals = sparse_ids.values.to(torch.int64).contiguous()
+    ind = sparse_ids.indices.to(torch.int64).contiguous()
+    args = (parts, vals, ind, sparse_ids.dense_shape, combiner, max_norm)
+    if anchors or tensors:
+        return _FusedPartitionedFn.apply(anchors[0] if anchors else None, *args, *tensors)
+    with torch.no_grad():
+        return _FusedPartitionedFn.forward(_Ctx(), None, *args)

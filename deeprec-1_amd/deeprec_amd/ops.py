@@ -304,6 +304,133 @@ def fused_embedding_local_sparse_look_up_grad(top_grad, emb_variable, sp_values,
     return out
 
 
+def _combiner(combiner):
+    if combiner not in COMBINERS:
+        raise ValueError("combiner must be one of 'mean', 'sqrtn' or 'sum'")
+    return COMBINERS[combiner]
+
+
+def _max_norm(max_norm):
+    return -1.0 if max_norm is None else float(max_norm)
+
+
+def fused_embedding_sparse_pre_look_up(partition_shapes, sp_values, sp_indices):
+    """FusedEmbeddingSparsePreLookUp (core/ops/fused_embedding_ops.cc:60-107,
+    fused_embedding_ops_gpus.cu.cc:150-283): ids stably sorted and split by
+    the "div" boundaries of partition_shapes[i][0], rebased per partition.
+    Returns (partitioned_values, partitioned_indices) lists.  Like the
+    reference kernel (:228-238) it reads the partition sizes back to the host
+    once to shape its outputs."""
+    dev = _dev(sp_values)
+    rows = [int(s[0]) for s in partition_shapes]
+    P = len(rows)
+    if P < 1 or P > _lib.MAX_PARTITIONS:
+        raise ValueError("num_partitions must be in [1, %d]" % _lib.MAX_PARTITIONS)
+    vals = _c(sp_values.reshape(-1), torch.int64)
+    ind = _c(sp_indices, torch.int64)
+    n = vals.numel()
+    if ind.shape != (n, 2):
+        raise _lib.InvalidArgumentError(_lib.INVALID_ARGUMENT, "sp_indices must be [nnz, 2]")
+    import ctypes as C
+    vout = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    iout = torch.empty((max(n, 1), 2), dtype=torch.int64, device=dev)
+    off = torch.empty(P + 1, dtype=torch.int64, device=dev)
+    wsb = lib().dr_fused_pre_lookup_workspace_size(n)
+    ws = workspace(wsb, dev)
+    check(lib().dr_fused_pre_lookup(ptr(vals), ptr(ind), n, (C.c_int64 * P)(*rows), P, ptr(vout),
+                                    ptr(iout), ptr(off), ptr(ws), wsb, stream_handle(dev)))
+    _post(dev)
+    o = off.cpu().tolist()
+    return ([vout[o[p]:o[p + 1]] for p in range(P)], [iout[o[p]:o[p + 1]] for p in range(P)])
+
+
+def _shard_arrays(emb_shards, partitioned_indices):
+    import ctypes as C
+    P = len(emb_shards)
+    if P < 1 or P > _lib.MAX_PARTITIONS or len(partitioned_indices) != P:
+        raise ValueError("need 1..%d emb_shards with one partitioned_indices each"
+                         % _lib.MAX_PARTITIONS)
+    shards = [_c(s, torch.float32) for s in emb_shards]
+    inds = [_c(i, torch.int64) for i in partitioned_indices]
+    for s, i in zip(shards, inds):
+        if s.shape[0] != i.shape[0]:
+            raise _lib.InvalidArgumentError(
+                _lib.INVALID_ARGUMENT, "emb_shard and partitioned_indice dosn't have the same length")
+    A = C.c_void_p * P
+    sp = A(*[s.data_ptr() if s.numel() else None for s in shards])
+    ip = A(*[i.data_ptr() if i.numel() else None for i in inds])
+    rows = (C.c_int64 * P)(*[s.shape[0] for s in shards])
+    return shards, inds, sp, ip, rows
+
+
+def fused_embedding_sparse_post_look_up(emb_shards, partitioned_indices, sp_dense_shape,
+                                        partitioned_values=None, combiner="mean", max_norm=None):
+    """FusedEmbeddingSparsePostLookUp (core/ops/fused_embedding_ops.cc:109-155,
+    fused_embedding_ops_gpus.cu.cc:285-384) -> (emb_vectors [B, D],
+    feature_nums [B] int32).  Bags are summed in (row, col) order, so the
+    result equals the local fused lookup of the same ids bit for bit."""
+    dev = _dev(emb_shards[0])
+    shards, inds, sp, ip, rows = _shard_arrays(emb_shards, partitioned_indices)
+    P = len(shards)
+    D = shards[0].shape[1]
+    B, cols = int(sp_dense_shape[0]), int(sp_dense_shape[1])
+    out = torch.empty((B, D), dtype=torch.float32, device=dev)
+    fnum = torch.empty(B, dtype=torch.int32, device=dev)
+    N = sum(s.shape[0] for s in shards)
+    wsb = lib().dr_fused_post_lookup_workspace_size(N, B)
+    ws = workspace(wsb, dev)
+    check(lib().dr_fused_post_lookup(sp, ip, rows, P, B, max(cols, 1), D, _combiner(combiner),
+                                     _max_norm(max_norm), ptr(out), ptr(fnum), ptr(ws), wsb,
+                                     stream_handle(dev)))
+    _post(dev)
+    return out, fnum
+
+
+def fused_embedding_sparse_post_look_up_grad(top_grad, emb_shards, partitioned_indices,
+                                             feature_nums, combiner="mean", max_norm=None):
+    """FusedEmbeddingSparsePostLookUpGrad (core/ops/fused_embedding_ops.cc:157-196,
+    fused_embedding_ops_gpus.cu.cc:386-514) -> grad_shards list."""
+    import ctypes as C
+    dev = _dev(top_grad)
+    tg = _c(top_grad, torch.float32)
+    shards, inds, sp, ip, rows = _shard_arrays(emb_shards, partitioned_indices)
+    P = len(shards)
+    D = tg.shape[1]
+    outs = [torch.empty((s.shape[0], D), dtype=torch.float32, device=dev) for s in shards]
+    fn = _c(feature_nums, torch.int32)
+    check(lib().dr_fused_post_lookup_grad(
+        ptr(tg), sp, ip, rows, P, tg.shape[0], D, ptr(fn), _combiner(combiner),
+        _max_norm(max_norm), (C.c_void_p * P)(*[o.data_ptr() if o.numel() else None
+                                               for o in outs]), stream_handle(dev)))
+    _post(dev)
+    return outs
+
+
+def bag_weight_scale(weights, bag_off, combiner):
+    """Per-bag divisor of a weighted lookup: sum(w) (mean) / sqrt(sum(w^2))."""
+    dev = _dev(weights)
+    B = bag_off.numel() - 1
+    q = torch.empty(max(B, 1), dtype=torch.float32, device=dev)
+    check(lib().dr_bag_weight_scale(ptr(weights), ptr(bag_off), B, _combiner(combiner), ptr(q),
+                                    stream_handle(dev)))
+    _post(dev)
+    return q
+
+
+def clip_by_norm_grad(grad, pool, rows, max_norm, pool_rows=None, default_rows=None,
+                      default_stride=0, n_dev=None):
+    """In place: grad [n, D] of clip_by_norm(pool[rows], max_norm) -> grad of
+    the unclipped rows (clip_ops.py:164-184 chain rule)."""
+    dev = _dev(grad)
+    n, D = grad.shape
+    pr = (1 << 62) if pool_rows is None else int(pool_rows)
+    check(lib().dr_clip_by_norm_grad(pool if isinstance(pool, int) else ptr(pool), pr, ptr(rows),
+                                     ptr(default_rows), int(default_stride), ptr(n_dev), n, D,
+                                     float(max_norm), ptr(grad), stream_handle(dev)))
+    _post(dev)
+    return grad
+
+
 # ---------------------------------------------------------------------------
 # Interactions
 # ---------------------------------------------------------------------------
@@ -481,6 +608,25 @@ def partition_by_owner(keys, world, n_dev=None):
     ws = workspace(wsb, dev)
     check(lib().dr_partition_by_owner(ptr(k), n, ptr(n_dev), world, ptr(ko), ptr(perm),
                                       ptr(counts), ptr(ws), wsb, stream_handle(dev)))
+    _post(dev)
+    return ko, perm, counts
+
+
+def partition_by_owner_mod(keys, world, premod, n_dev=None):
+    """partition_by_owner with owner = (key % premod) % world (floor mods):
+    premod = 1000 is the EV partition rule ids % 1000 % np
+    (python/ops/embedding_ops.py:207-209)."""
+    dev = _dev(keys)
+    k = _c(keys, torch.int64)
+    n = k.numel()
+    ko = torch.empty_like(k)
+    perm = torch.empty(n, dtype=torch.int32, device=dev)
+    counts = torch.empty(world, dtype=torch.int64, device=dev)
+    wsb = lib().dr_partition_workspace_size(n)
+    ws = workspace(wsb, dev)
+    check(lib().dr_partition_by_owner_mod(ptr(k), n, ptr(n_dev), world, int(premod), ptr(ko),
+                                          ptr(perm), ptr(counts), ptr(ws), wsb,
+                                          stream_handle(dev)))
     _post(dev)
     return ko, perm, counts
 

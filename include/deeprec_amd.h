@@ -198,7 +198,33 @@ typedef struct {
   int64_t nnz;
   const int64_t* num_unique;  /* DEVICE U_t                                   */
   int32_t combiner;
+  /* Weighted lookups (embedding_ops.py:609-651: gather * w -> segment_sum   */
+  /* -> / weight_sum): NULL, or sp_weights [nnz].  Position k contributes    */
+  /* (top_grad[bag] / bag_scale[bag]) * weights[k] (mean / sqrtn; bag_scale  */
+  /* from dr_bag_weight_scale) or top_grad[bag] * weights[k] (sum), summed    */
+  /* from 0 in ascending k (the IndexedSlices -> dense unsorted_segment_sum). */
+  const float* weights;
+  const float* bag_scale;     /* [B] per-bag divisor, NULL for sum          */
 } dr_pool_grad_desc;
+
+/* bag_scale[b] = sum of weights (mean) or sqrtf(sum of weights^2) (sqrtn)  */
+/* over bag b, accumulated from 0 in ascending position (math_ops.          */
+/* segment_sum(weights) / segment_sum(pow(weights, 2)), embedding_ops.py:    */
+/* 636-645); the divisor of the weighted forward and of its backward.        */
+int dr_bag_weight_scale(const float* weights, const int32_t* bag_off, int64_t batch, int combiner,
+                        float* bag_scale, void* stream);
+
+/* Backward of clip_by_norm (embedding_ops._clip -> clip_ops.py:164-184),    */
+/* in place on grad [n, dim] (n_dev: DEVICE row count or NULL): row i of the */
+/* clipped values came from v = pool[rows[i]] (rows[i] < 0: default_rows +   */
+/* (-rows[i]-1) * default_stride, an EV default).  With m = max(l2, c):      */
+/* grad = (g / m) * c + 2 * (s * v), s = (0.5 * sum_d(g * ((-(v * c)) / m) / */
+/* m)) / l2 when l2 >= c and l2 > 0, else 0 -- TF's op-by-op chain rule     */
+/* (RealDiv, Maximum(x >= y), Sqrt, Mul).  Row sums in wave order: fp32     */
+/* tolerance, not bit-exact.                                                */
+int dr_clip_by_norm_grad(const float* pool, int64_t pool_rows, const int64_t* rows,
+                         const float* default_rows, int64_t default_stride, const int64_t* n_dev,
+                         int64_t n, int dim, float max_norm, float* grad, void* stream);
 size_t dr_pool_grad_grouped_workspace_size(int64_t total_nnz);
 int dr_pool_grad_grouped(const dr_pool_grad_desc* descs_host, int num_tables, int64_t batch,
                          int dim, float* grad_unique, void* ws, size_t ws_bytes, void* stream);
@@ -385,6 +411,58 @@ int dr_fused_local_lookup_grad(const float* top_grad, const float* table, int64_
                                float* grad_out, void* stream);
 
 /* ------------------------------------------------------------------------ */
+/* Partitioned fused lookup: FusedEmbeddingSparsePreLookUp / PostLookUp /    */
+/* PostLookUpGrad (core/ops/fused_embedding_ops.cc:60-198, kernels           */
+/* core/kernels/fused_embedding/fused_embedding_ops_gpus.cu.cc:150-519),     */
+/* the path python/ops/fused_embedding_ops.py:45-67 runs for a list of       */
+/* partitioned dense tables ("div" strategy over partition_shapes[i][0]).    */
+/* At most DR_MAX_PARTITIONS partitions.                                     */
+/* ------------------------------------------------------------------------ */
+#define DR_MAX_PARTITIONS 64
+/* PreLookUp: ids are stably sorted by value (ties keep input order, as the  */
+/* reference's cub radix sort of (value, (row, col)) pairs), partition p     */
+/* holds the ids in [acc[p-1], acc[p]) (acc = prefix sums of partition_rows, */
+/* host int64 [P]) rebased to the partition, with their (row, col) pairs.    */
+/* Outputs are the partitions back to back: values_out [nnz], indices_out    */
+/* [nnz, 2], and part_off (DEVICE int64 [P+1]) partition p = [part_off[p],   */
+/* part_off[p+1]).  Ids outside [0, acc[P-1]) latch DR_INVALID_ARGUMENT and  */
+/* are left out (the reference drops ids >= acc[P-1] silently and hands      */
+/* negative ids to partition 0, where its Gather fails).  Partition          */
+/* boundaries are exact lower bounds (the reference's CalcElementsOffset-    */
+/* PerPartition dichotomy returns a wrong offset when exactly one sorted id  */
+/* lies below a boundary, or when nnz <= 2).                   */
+size_t dr_fused_pre_lookup_workspace_size(int64_t nnz);
+int dr_fused_pre_lookup(const int64_t* sp_values, const int64_t* sp_indices, int64_t nnz,
+                        const int64_t* partition_rows, int num_partitions, int64_t* values_out,
+                        int64_t* indices_out, int64_t* part_off, void* ws, size_t ws_bytes,
+                        void* stream);
+/* PostLookUp: emb_vectors[b] = combiner over the entries (e, p) whose      */
+/* partitioned_indices[p][e] row is b of (clip(emb_shards[p][e])), clip =    */
+/* `*= max_norm / l2` when max_norm >= 0 and l2 > max_norm (SumUpEmbedding-  */
+/* Shard).  The reference adds with float atomics (order unspecified); here  */
+/* a bag is summed from 0 in ascending column order (sp_indices order), so   */
+/* PostLookUp(PreLookUp(x)) equals FusedEmbeddingLocalSparseLookUp bit for   */
+/* bit.  Combiner: sum; mean / n; sqrtn / sqrtf(n) (ApplyCombiner), so an    */
+/* empty bag is 0 for sum and 0/0 (NaN) for mean / sqrtn, as the reference.  */
+/* feature_nums[b] = n (int32).  emb_shards[p] / partitioned_indices[p] are  */
+/* device pointers held in host arrays; shard_rows[p] = entries of p.        */
+/* dense_cols = sp_dense_shape[1] (batch * dense_cols < 2^62).               */
+size_t dr_fused_post_lookup_workspace_size(int64_t total_entries, int64_t batch);
+int dr_fused_post_lookup(const float* const* emb_shards, const int64_t* const* partitioned_indices,
+                         const int64_t* shard_rows, int num_partitions, int64_t batch,
+                         int64_t dense_cols, int dim, int combiner, float max_norm,
+                         float* emb_vectors, int32_t* feature_nums, void* ws, size_t ws_bytes,
+                         void* stream);
+/* PostLookUpGrad (DistributeGradToShard): grad_shards[p][e] =               */
+/* CombineGrad(top_grad[row], feature_nums[row]) scaled by max_norm / l2 of  */
+/* emb_shards[p][e] when max_norm >= 0 and l2 > max_norm.                    */
+int dr_fused_post_lookup_grad(const float* top_grad, const float* const* emb_shards,
+                              const int64_t* const* partitioned_indices,
+                              const int64_t* shard_rows, int num_partitions, int64_t batch,
+                              int dim, const int32_t* feature_nums, int combiner, float max_norm,
+                              float* const* grad_shards, void* stream);
+
+/* ------------------------------------------------------------------------ */
 /* Owner partition for the row-sharded all-to-all (SOK selectKernel,         */
 /* sparse_operation_kit/.../all2all_input_dispatcher.cu:36-126, and the EV   */
 /* partition rule embedding_ops.py:207-209): stable bucket of keys by        */
@@ -395,6 +473,14 @@ size_t dr_partition_workspace_size(int64_t n);
 int dr_partition_by_owner(const int64_t* keys, int64_t n, const int64_t* n_dev, int world,
                           int64_t* keys_out, int32_t* perm_out, int64_t* send_counts,
                           void* ws, size_t ws_bytes, void* stream);
+/* Same with owner = floormod(floormod(key, premod), world) when premod > 0: */
+/* premod = 1000 is the EmbeddingVariable partition rule                     */
+/* `ids % 1000 % np` of embedding_lookup (python/ops/embedding_ops.py:       */
+/* 207-209; TF `%` is FloorMod), which differs from key % np when np does    */
+/* not divide 1000.                                                          */
+int dr_partition_by_owner_mod(const int64_t* keys, int64_t n, const int64_t* n_dev, int world,
+                              int64_t premod, int64_t* keys_out, int32_t* perm_out,
+                              int64_t* send_counts, void* ws, size_t ws_bytes, void* stream);
 /* Request routing of a grouped unique (dr_unique_grouped layout): the      */
 /* valid uniques of all T features are stably ordered by (owner, feature),  */
 /* owner = key % world, giving the [peer][feature]-blocked send buffer of    */

@@ -354,6 +354,157 @@ int orc_fused_local_lookup_grad(const float* top_grad, const float* table,
   return ORC_OK;
 }
 
+/* Stable ascending order of int64 keys (bottom-up merge sort): order[] =   */
+/* positions.                                                                */
+static void stable_order(const int64_t* keys, int64_t n, int64_t* order) {
+  for (int64_t i = 0; i < n; ++i) order[i] = i;
+  int64_t* tmp = (int64_t*)malloc(sizeof(int64_t) * (n > 0 ? n : 1));
+  for (int64_t w = 1; w < n; w *= 2) {
+    for (int64_t lo = 0; lo < n; lo += 2 * w) {
+      int64_t mid = lo + w < n ? lo + w : n;
+      int64_t hi = lo + 2 * w < n ? lo + 2 * w : n;
+      int64_t a = lo, b = mid, o = lo;
+      while (a < mid && b < hi) tmp[o++] = (keys[order[b]] < keys[order[a]]) ? order[b++] : order[a++];
+      while (a < mid) tmp[o++] = order[a++];
+      while (b < hi) tmp[o++] = order[b++];
+    }
+    memcpy(order, tmp, sizeof(int64_t) * n);
+  }
+  free(tmp);
+}
+
+/* FusedEmbeddingSparsePostLookUp (fused_embedding_ops_gpus.cu.cc:285-384):  */
+/* entries = the partitions' (emb row, (row, col)) pairs back to back.  Per  */
+/* bag: out = 0; out += e (e *= max_norm / l2 when max_norm >= 0 and l2 >    */
+/* max_norm, SumUpEmbeddingShard :72-99) over the bag's entries; then        */
+/* ApplyCombiner (:101-107): / sqrtf(n), / n.  The reference's float atomics */
+/* leave the order open; this restatement fixes it to ascending (row, col),  */
+/* the order the engine uses (and FusedEmbeddingLocalSparseLookUp's).       */
+int orc_fused_post_lookup(const float* emb, const int64_t* ind, int64_t N, int64_t B,
+                          int64_t cols, int64_t D, int combiner, float max_norm, float* out,
+                          int32_t* fnum) {
+  int64_t* key = (int64_t*)malloc(sizeof(int64_t) * (N > 0 ? N : 1));
+  int64_t* order = (int64_t*)malloc(sizeof(int64_t) * (N > 0 ? N : 1));
+  float* e = (float*)malloc(sizeof(float) * (D > 0 ? D : 1));
+  for (int64_t i = 0; i < N; ++i) {
+    if (ind[2 * i] < 0 || ind[2 * i] >= B || ind[2 * i + 1] < 0 || ind[2 * i + 1] >= cols) {
+      free(key); free(order); free(e);
+      return ORC_INVALID_ARGUMENT;
+    }
+    key[i] = ind[2 * i] * cols + ind[2 * i + 1];
+  }
+  stable_order(key, N, order);
+  for (int64_t i = 0; i < B * D; ++i) out[i] = 0.0f;
+  for (int64_t b = 0; b < B; ++b) fnum[b] = 0;
+  for (int64_t j = 0; j < N; ++j) {
+    const int64_t s = order[j], b = ind[2 * s];
+    for (int64_t d = 0; d < D; ++d) e[d] = emb[s * D + d];
+    if (max_norm >= 0.0f) {
+      float l2 = 0.0f;
+      for (int64_t d = 0; d < D; ++d) l2 = l2 + e[d] * e[d];
+      l2 = sqrtf(l2);
+      if (l2 > max_norm) {
+        const float f = max_norm / l2;
+        for (int64_t d = 0; d < D; ++d) e[d] = e[d] * f;
+      }
+    }
+    for (int64_t d = 0; d < D; ++d) out[b * D + d] = out[b * D + d] + e[d];
+    fnum[b] += 1;
+  }
+  if (combiner != 0)
+    for (int64_t b = 0; b < B; ++b) {
+      const float q = combiner == 2 ? sqrtf((float)fnum[b]) : (float)fnum[b];
+      for (int64_t d = 0; d < D; ++d) out[b * D + d] = out[b * D + d] / q;
+    }
+  free(key); free(order); free(e);
+  return ORC_OK;
+}
+
+/* FusedEmbeddingSparsePostLookUpGrad, DistributeGradToShard (fused_embedding */
+/* _ops_gpus.cu.cc:109-146): grad[e] = CombineGrad(top[row(e)], fnum[row])   */
+/* then *= max_norm / l2(emb[e]) when max_norm >= 0 and l2 > max_norm.       */
+int orc_fused_post_lookup_grad(const float* top, const float* emb, const int64_t* ind,
+                               int64_t N, int64_t B, int64_t D, const int32_t* fnum,
+                               int combiner, float max_norm, float* out) {
+  for (int64_t i = 0; i < N; ++i) {
+    const int64_t b = ind[2 * i];
+    if (b < 0 || b >= B) return ORC_INVALID_ARGUMENT;
+    float f = 1.0f;
+    int clip = 0;
+    if (max_norm >= 0.0f) {
+      float l2 = 0.0f;
+      for (int64_t d = 0; d < D; ++d) l2 = l2 + emb[i * D + d] * emb[i * D + d];
+      l2 = sqrtf(l2);
+      if (l2 > max_norm) { clip = 1; f = max_norm / l2; }
+    }
+    for (int64_t d = 0; d < D; ++d) {
+      float g = top[b * D + d];
+      if (combiner == 2) g = g / sqrtf((float)fnum[b]);
+      else if (combiner == 1) g = g / (float)fnum[b];
+      if (clip) g = g * f;
+      out[i * D + d] = g;
+    }
+  }
+  return ORC_OK;
+}
+
+/* Backward of the weighted embedding_lookup_sparse composition            */
+/* (python/ops/embedding_ops.py:609-651) w.r.t. the unique rows: TF's        */
+/* gradient chain div (RealDiv: g / weight_sum) -> segment_sum (gather by    */
+/* seg) -> mul (* w) -> gather (IndexedSlices over idx) -> the dense         */
+/* conversion, an UnsortedSegmentSum in ascending position from 0.           */
+/* weight_sum = segment_sum(w) (mean) or sqrt(segment_sum(pow(w, 2)))        */
+/* (sqrtn), accumulated from 0 in ascending position.                        */
+int orc_weighted_segment_grad(const float* g, int64_t B, int64_t D, const int32_t* idx,
+                              const float* w, const int32_t* seg, int64_t n, int64_t U,
+                              int combiner, float* out) {
+  float* q = (float*)calloc((size_t)(B > 0 ? B : 1), sizeof(float));
+  for (int64_t i = 0; i < n; ++i) {
+    if (seg[i] < 0 || seg[i] >= B || idx[i] < 0 || idx[i] >= U) { free(q); return ORC_INVALID_ARGUMENT; }
+    q[seg[i]] = q[seg[i]] + (combiner == 2 ? w[i] * w[i] : w[i]);
+  }
+  if (combiner == 2)
+    for (int64_t b = 0; b < B; ++b) q[b] = sqrtf(q[b]);
+  memset(out, 0, sizeof(float) * U * D);
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t b = seg[i], u = idx[i];
+    for (int64_t d = 0; d < D; ++d) {
+      float t = g[b * D + d];
+      if (combiner != 0) t = t / q[b];
+      t = t * w[i];
+      out[u * D + d] = out[u * D + d] + t;
+    }
+  }
+  free(q);
+  return ORC_OK;
+}
+
+/* Backward of clip_by_norm (clip_ops.py:164-184, applied by embedding_ops. */
+/* _clip to the looked-up rows) by TF's chain rule op by op, in place on g:  */
+/* l2sum = sum v*v; pred = l2sum > 0; l2 = pred ? sqrt(l2sum) : l2sum;       */
+/* m = max(l2, c); gm = sum_d g * ((-(v*c)) / m) / m (RealDiv grad of y);   */
+/* Maximum passes gm to l2 when l2 >= c; Sqrt: gs = (0.5 * gl2) / l2;        */
+/* g' = (g / m) * c + gs * v + v * gs (the three uses of `values`).          */
+void orc_clip_by_norm_grad(const float* v, float* g, int64_t n, int64_t D, float c) {
+  for (int64_t i = 0; i < n; ++i) {
+    const float* r = v + i * D;
+    float* gr = g + i * D;
+    float s = 0.0f;
+    for (int64_t d = 0; d < D; ++d) s = s + r[d] * r[d];
+    const int pred = s > 0.0f;
+    const float l2 = pred ? sqrtf(s) : s;
+    const float m = l2 > c ? l2 : c;
+    float gm = 0.0f;
+    for (int64_t d = 0; d < D; ++d) gm = gm + gr[d] * ((-(r[d] * c) / m) / m);
+    const float gl2 = l2 >= c ? gm : 0.0f;
+    const float gs = pred ? (0.5f * gl2) / l2 : 0.0f;
+    for (int64_t d = 0; d < D; ++d) {
+      const float a = (gr[d] / m) * c, b = gs * r[d];
+      gr[d] = (a + b) + b;
+    }
+  }
+}
+
 /* FusedEmbeddingSparsePreLookUp partition step (fused_embedding_ops_gpus.  */
 /* cu.cc:158-310, "div" over partition_shapes): ids are stably sorted, then  */
 /* split by the cumulative row ranges of the partitions and rebased.  Writes */

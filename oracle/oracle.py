@@ -49,6 +49,10 @@ def lib():
             "orc_fused_local_lookup": (i32, [p, i64, i64, p, p, i64, i64, i32, f32, p, p]),
             "orc_fused_local_lookup_grad": (i32, [p, p, i64, i64, p, p, i64, i64, i32, f32, p]),
             "orc_fused_pre_lookup": (i32, [p, i64, p, i64, p, p, p]),
+            "orc_fused_post_lookup": (i32, [p, p, i64, i64, i64, i64, i32, f32, p, p]),
+            "orc_fused_post_lookup_grad": (i32, [p, p, p, i64, i64, i64, p, i32, f32, p]),
+            "orc_weighted_segment_grad": (i32, [p, i64, i64, p, p, p, i64, i64, i32, p]),
+            "orc_clip_by_norm_grad": (None, [p, p, i64, i64, f32]),
             "orc_ev_create": (p, [i64, p, i64, i64, i64, f32, i32]),
             "orc_ev_create_slot": (p, [p, i32, p]),
             "orc_ev_free": (None, [p]),
@@ -208,6 +212,58 @@ def fused_pre_lookup(values, part_rows):
         res.append((ov[k:k + s].copy(), op[k:k + s].copy()))
         k += s
     return res
+
+
+def fused_post_lookup(shards, indices, batch, cols, combiner, max_norm=-1.0):
+    """FusedEmbeddingSparsePostLookUp over partitions given as lists of
+    [n_p, D] shards and [n_p, 2] indices -> (emb [B, D], feature_nums [B])."""
+    D = np.asarray(shards[0]).shape[1]
+    emb = np.ascontiguousarray(np.concatenate([np.asarray(s, np.float32).reshape(-1, D)
+                                               for s in shards]), np.float32)
+    ind = np.ascontiguousarray(np.concatenate([np.asarray(i, np.int64).reshape(-1, 2)
+                                               for i in indices]), np.int64)
+    out = np.empty((batch, D), np.float32)
+    fnum = np.empty(batch, np.int32)
+    _check(lib().orc_fused_post_lookup(_p(emb), _p(ind), emb.shape[0], batch, cols, D,
+                                       COMBINERS[combiner], max_norm, _p(out), _p(fnum)),
+           "fused_post_lookup")
+    return out, fnum
+
+
+def fused_post_lookup_grad(top_grad, shards, indices, feature_nums, combiner, max_norm=-1.0):
+    top = np.ascontiguousarray(top_grad, np.float32)
+    B, D = top.shape
+    fn = np.ascontiguousarray(feature_nums, np.int32)
+    outs = []
+    for s, i in zip(shards, indices):
+        s = np.ascontiguousarray(s, np.float32).reshape(-1, D)
+        i = np.ascontiguousarray(i, np.int64).reshape(-1, 2)
+        o = np.empty_like(s)
+        _check(lib().orc_fused_post_lookup_grad(_p(top), _p(s), _p(i), s.shape[0], B, D, _p(fn),
+                                                COMBINERS[combiner], max_norm, _p(o)),
+               "fused_post_lookup_grad")
+        outs.append(o)
+    return outs
+
+
+def weighted_segment_grad(g, idx, w, seg, num_unique, combiner):
+    g = np.ascontiguousarray(g, np.float32)
+    B, D = g.shape
+    idx = np.ascontiguousarray(idx, np.int32)
+    w = np.ascontiguousarray(w, np.float32)
+    seg = np.ascontiguousarray(seg, np.int32)
+    out = np.empty((num_unique, D), np.float32)
+    _check(lib().orc_weighted_segment_grad(_p(g), B, D, _p(idx), _p(w), _p(seg), idx.shape[0],
+                                           num_unique, COMBINERS[combiner], _p(out)),
+           "weighted_segment_grad")
+    return out
+
+
+def clip_by_norm_grad(rows, grad, max_norm):
+    rows = np.ascontiguousarray(rows, np.float32)
+    g = np.array(grad, np.float32, copy=True)
+    lib().orc_clip_by_norm_grad(_p(rows), _p(g), g.shape[0], g.shape[1], max_norm)
+    return g
 
 
 def fasthash64(key, seed):
@@ -494,6 +550,27 @@ def embedding_lookup_sparse(params, indices, values, batch, weights=None, combin
                                              _p(np.ascontiguousarray(seg)), idx.shape[0], batch,
                                              COMBINERS[combiner], _p(out)), "weighted")
     return out
+
+
+def embedding_lookup_sparse_grad(params, indices, values, batch, top_grad, weights=None,
+                                 combiner="mean", max_norm=None):
+    """Gradient of embedding_lookup_sparse w.r.t. the looked-up rows, as
+    (unique ids in first-occurrence order, grad [U, D]): the reference's
+    backward (SparseSegment*Grad, or the weighted composition's chain, then
+    clip_by_norm's when max_norm is set).  Call after the forward (EV rows
+    exist)."""
+    seg = np.asarray(indices, np.int64).reshape(-1, 2)[:, 0].astype(np.int32)
+    uids, idx = unique(values)
+    U = uids.shape[0]
+    g = np.ascontiguousarray(top_grad, np.float32)
+    if weights is None:
+        gu = sparse_segment_reduce_grad(g, idx, seg, U, combiner)
+    else:
+        gu = weighted_segment_grad(g, idx, weights, seg, U, combiner)
+    if max_norm is not None:
+        rows = params.gather(uids) if isinstance(params, EV) else gather(params, uids)
+        gu = clip_by_norm_grad(rows, gu, max_norm)
+    return uids, gu
 
 
 def _ev_filter_on(ev):

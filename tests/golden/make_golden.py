@@ -135,6 +135,60 @@ def pre_lookup_partition():
                 ])
 
 
+def post_lookup():
+    # core/kernels/fused_embedding/fused_embedding_ops_test.cc:129-196
+    # (FusedEmbeddingSparsePostLookUp, 3 partitions, sqrtn, max_norm 200, tol 1e-4)
+    # and :217-290 (PostLookUpGrad, 2 partitions, mean, max_norm 100, tol 1e-4)
+    s0 = [8.0, 9.0, 10.0, 11.0, 12.0, 13.0, 14.0, 15.0, 24.0, 25.0,
+          26.0, 27.0, 28.0, 29.0, 30.0, 31.0, 24.0, 25.0, 26.0, 27.0,
+          28.0, 29.0, 30.0, 31.0, 32.0, 33.0, 34.0, 35.0, 36.0, 37.0,
+          38.0, 39.0, 32.0, 33.0, 34.0, 35.0, 36.0, 37.0, 38.0, 39.0,
+          40.0, 41.0, 42.0, 43.0, 44.0, 45.0, 46.0, 47.0]
+    fwd = dict(source="core/kernels/fused_embedding/fused_embedding_ops_test.cc:129-196",
+               combiner="sqrtn", max_norm=200.0, batch=4, cols=8, dim=8,
+               shards=[s0, [56.0, 57.0, 58.0, 59.0, 60.0, 61.0, 62.0, 63.0],
+                       [96.0, 97.0, 98.0, 99.0, 100.0, 101.0, 102.0, 103.0,
+                        96.0, 97.0, 98.0, 99.0, 100.0, 101.0, 102.0, 103.0,
+                        120.0, 121.0, 122.0, 123.0, 124.0, 125.0, 126.0, 127.0]],
+               indices=[[0, 5, 0, 1, 2, 1, 1, 2, 3, 6, 1, 1], [1, 7], [2, 4, 2, 7, 3, 0]],
+               expected=[22.62741661, 24.04163170, 25.45584488, 26.87005806, 28.28427124,
+                         29.69848442, 31.11269951, 32.52691269, 73.90083313, 75.63288879,
+                         77.36493683, 79.09698486, 80.82904053, 82.56108856, 84.29314423,
+                         86.02519226, 92.61308289, 94.01081848, 95.40855408, 96.80628204,
+                         98.20401764, 99.60175323, 100.99948120, 102.39721680, 71.20205688,
+                         72.31395721, 73.42584991, 74.53774261, 75.64963531, 76.76153564,
+                         77.87342834, 78.98532867],
+               feature_nums=[2, 3, 3, 2], tol=1e-4)
+    grad = dict(source="core/kernels/fused_embedding/fused_embedding_ops_test.cc:217-290",
+                combiner="mean", max_norm=100.0, batch=4, dim=8,
+                top_grad=[float(x) for x in range(32)],
+                shards=[s0, [56.0, 57.0, 58.0, 59.0, 60.0, 61.0, 62.0, 63.0,
+                             96.0, 97.0, 98.0, 99.0, 100.0, 101.0, 102.0, 103.0,
+                             96.0, 97.0, 98.0, 99.0, 100.0, 101.0, 102.0, 103.0,
+                             120.0, 121.0, 122.0, 123.0, 124.0, 125.0, 126.0, 127.0]],
+                indices=[[0, 5, 0, 1, 2, 1, 1, 2, 3, 6, 1, 1], [1, 7, 2, 4, 2, 7, 3, 0]],
+                feature_nums=[2, 3, 3, 2],
+                expected=[[0.00000000, 0.50000000, 1.00000000, 1.50000000, 2.00000000,
+                           2.50000000, 3.00000000, 3.50000000, 0.00000000, 0.50000000,
+                           1.00000000, 1.50000000, 2.00000000, 2.50000000, 3.00000000,
+                           3.50000000, 5.33333349, 5.66666651, 6.00000000, 6.33333349,
+                           6.66666651, 7.00000000, 7.33333349, 7.66666651, 2.65028572,
+                           2.98157120, 3.31285667, 3.64414287, 3.97542834, 4.30671406,
+                           4.63799953, 4.96928549, 11.92628479, 12.42321396, 12.92014217,
+                           13.41707039, 13.91399956, 14.41092777, 14.90785599, 15.40478516,
+                           2.16437674, 2.43492365, 2.70547056, 2.97601795, 3.24656487,
+                           3.51711202, 3.78765893, 4.05820608],
+                          [1.58337951, 1.78130186, 1.97922409, 2.17714667, 2.37506914,
+                           2.57299161, 2.77091384, 2.96883631, 1.89459133, 2.01300311,
+                           2.13141513, 2.24982715, 2.36823893, 2.48665094, 2.60506320,
+                           2.72347474, 1.89459133, 2.01300311, 2.13141513, 2.24982715,
+                           2.36823893, 2.48665094, 2.60506320, 2.72347474, 3.43474555,
+                           3.57786012, 3.72097445, 3.86408877, 4.00720310, 4.15031767,
+                           4.29343224, 4.43654633]],
+                tol=1e-4)
+    return dict(forward=fwd, grad=grad)
+
+
 def segment_formula():
     # core/kernels/segment_reduction_ali_ops_test.cc:75-240 (forward) and
     # :299-540 (grads).  input[i] = float(i/6) over 262144 x 6, indices = 2i,
@@ -208,6 +262,7 @@ def fingerprint():
 
 def main():
     out = dict(fused_local=fused_local(), pre_lookup_partition=pre_lookup_partition(),
+               post_lookup=post_lookup(),
                segment_formula=segment_formula(), ev=ev_kats(), fingerprint=fingerprint())
     for k, v in out.items():
         with open(os.path.join(HERE, k + ".json"), "w") as f:

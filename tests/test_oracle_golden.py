@@ -300,3 +300,94 @@ def test_hash_bucket_int64_max_for_ev_columns(orc):
     ids = orc.string_to_hash_bucket_fast(["a", "Hello"], np.iinfo(np.int64).max)
     assert ids[0] == 12917804110809363939 % (2 ** 63 - 1)
     assert ids[1] == 15404698994557526151 % (2 ** 63 - 1)
+
+
+# fused_embedding_ops_test.cc:129-196 / :217-290 (partitioned post-lookup) ----
+def test_post_lookup_kat(orc):
+    c = load("post_lookup")["forward"]
+    D = c["dim"]
+    shards = [np.asarray(s, np.float32).reshape(-1, D) for s in c["shards"]]
+    inds = [np.asarray(i, np.int64).reshape(-1, 2) for i in c["indices"]]
+    out, fnum = orc.fused_post_lookup(shards, inds, c["batch"], c["cols"], c["combiner"],
+                                      c["max_norm"])
+    np.testing.assert_allclose(out.ravel(), c["expected"], atol=c["tol"], rtol=0)
+    assert fnum.tolist() == c["feature_nums"]
+
+
+def test_post_lookup_grad_kat(orc):
+    c = load("post_lookup")["grad"]
+    D = c["dim"]
+    top = np.asarray(c["top_grad"], np.float32).reshape(c["batch"], D)
+    shards = [np.asarray(s, np.float32).reshape(-1, D) for s in c["shards"]]
+    inds = [np.asarray(i, np.int64).reshape(-1, 2) for i in c["indices"]]
+    outs = orc.fused_post_lookup_grad(top, shards, inds, c["feature_nums"], c["combiner"],
+                                      c["max_norm"])
+    for o, e in zip(outs, c["expected"]):
+        np.testing.assert_allclose(o.ravel(), e, atol=c["tol"], rtol=0)
+
+
+def test_pre_post_equals_local_lookup(orc):
+    """PostLookUp(PreLookUp(x)) with per-partition gathers reproduces the
+    local fused lookup on the concatenated table bit for bit (the order the
+    oracle and the engine fix for the reference's atomics)."""
+    rng = np.random.default_rng(5)
+    B, D, M = 40, 8, 6
+    rows = [7, 3, 11]
+    table = rng.standard_normal((sum(rows), D)).astype(np.float32) * 3
+    lens = rng.integers(1, M + 1, B)
+    r = np.repeat(np.arange(B), lens)
+    c = np.concatenate([np.sort(rng.choice(M, n, replace=False)) for n in lens])
+    ind = np.stack([r, c], 1).astype(np.int64)
+    vals = rng.integers(0, sum(rows), r.shape[0]).astype(np.int64)
+    acc = np.cumsum([0] + rows)
+    for comb in ("sum", "mean", "sqrtn"):
+        for mn in (-1.0, 4.0):
+            parts = orc.fused_pre_lookup(vals, rows)
+            shards = [table[acc[p] + v] for p, (v, _) in enumerate(parts)]
+            inds = [ind[pos] for _, pos in parts]
+            out, fnum = orc.fused_post_lookup(shards, inds, B, M, comb, mn)
+            ref, _ = orc.fused_local_lookup(table, vals, r, B, comb, mn)
+            np.testing.assert_array_equal(out, ref)
+            assert fnum.tolist() == lens.tolist()
+
+
+def _torch_lookup_sparse(table, ind, vals, B, w, comb, max_norm):
+    """The reference composition (embedding_ops.py:589-651 + _clip) in torch
+    fp64 autograd: an independent check of the oracle's chain rule."""
+    import torch
+    t = torch.tensor(table, dtype=torch.float64, requires_grad=True)
+    uids, idx = np.unique(vals, return_inverse=True)
+    emb = t[torch.as_tensor(uids)]
+    if max_norm is not None:
+        l2 = torch.sqrt((emb * emb).sum(1, keepdim=True))
+        emb = emb * max_norm / torch.maximum(l2, torch.tensor(max_norm, dtype=torch.float64))
+    seg = torch.as_tensor(ind[:, 0])
+    g = emb[torch.as_tensor(idx)]
+    ww = torch.ones(len(vals), dtype=torch.float64) if w is None else torch.tensor(w, dtype=torch.float64)
+    s = torch.zeros((B, table.shape[1]), dtype=torch.float64).index_add(0, seg, g * ww[:, None])
+    if comb != "sum":
+        q = torch.zeros(B, dtype=torch.float64).index_add(0, seg, ww if comb == "mean" else ww * ww)
+        q = q if comb == "mean" else torch.sqrt(q)
+        s = s / q[:, None]
+    return t, s
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("max_norm", [None, 2.0])
+@pytest.mark.parametrize("comb", ["sum", "mean", "sqrtn"])
+def test_lookup_sparse_grad_oracle_vs_autograd(orc, weighted, max_norm, comb):
+    rng = np.random.default_rng(17)
+    B, D, R = 30, 6, 25
+    table = (rng.standard_normal((R, D)) * 1.5).astype(np.float32)
+    lens = rng.integers(1, 5, B)
+    r = np.repeat(np.arange(B), lens)
+    c = np.concatenate([np.arange(n) for n in lens])
+    ind = np.stack([r, c], 1).astype(np.int64)
+    vals = rng.integers(0, R, r.shape[0]).astype(np.int64)
+    w = rng.uniform(0.2, 2.0, r.shape[0]).astype(np.float32) if weighted else None
+    top = rng.standard_normal((B, D)).astype(np.float32)
+    uids, gu = orc.embedding_lookup_sparse_grad(table, ind, vals, B, top, w, comb, max_norm)
+    t, out = _torch_lookup_sparse(table, ind, vals, B, w, comb, max_norm)
+    out.backward(__import__("torch").tensor(top, dtype=__import__("torch").float64))
+    ref = t.grad.numpy()[uids]
+    np.testing.assert_allclose(gu, ref, rtol=1e-5, atol=1e-6)
