@@ -44,7 +44,11 @@ def parse():
     p.add_argument("--zipf", type=float, default=0.0, help="0 = uniform keys")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
-    p.add_argument("--cpu-rows", type=int, default=2_000_000)
+    p.add_argument("--cpu-rows", type=int, default=12_500_000)
+    p.add_argument("--check-rows", type=int, default=8192,
+                   help="sampled output rows checked bit-exactly after the timed region")
+    p.add_argument("--train-steps", type=int, default=10,
+                   help="N=1: time the embedding training step too (0 = skip)")
     p.add_argument("--kernel-iters", type=int, default=20)
     p.add_argument("--engine", default="auto", choices=["auto", "local", "xgmi", "a2a"],
                    help="auto: local lookup at N=1, xgmi peer-write (RCCL all-to-all "
@@ -74,19 +78,31 @@ def make_batches(nb, tables, batch, keyspace, zipf, seed, device):
     return out
 
 
-def cpu_baseline(args, n_lookups_target=None):
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(args):
     """DeepRec-CPU-semantics restatement (oracle/) timed on the host cores:
     Unique -> KvResourceGather (EV hash lookup + row memcpy, Shard over
-    threads) -> SparseSegmentSum, per feature, h = 1."""
+    threads) -> SparseSegmentSum, per feature, h = 1, on one table of the
+    GPU's per-table shape (rows x dim).  Threads: the box's CPU share
+    (OMP_NUM_THREADS, else the affinity mask)."""
     from oracle import oracle as orc
-    threads = min(16, os.cpu_count() or 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
     D, R = args.dim, args.cpu_rows
     rng = np.random.default_rng(2021)
     ev = orc.EV(D, 0.0)
-    chunk = 1 << 18
+    chunk = 1 << 20
     for b in range(0, R, chunk):
         keys = np.arange(b, min(R, b + chunk), dtype=np.int64)
-        ev.insert(keys, rng.standard_normal((keys.shape[0], D)).astype(np.float32))
+        ev.insert(keys, rng.standard_normal((keys.shape[0], D), dtype=np.float32))
     B = args.batch
     seg_off = np.arange(B + 1, dtype=np.int32)
     out = np.empty((B, D), np.float32)
@@ -102,10 +118,51 @@ def cpu_baseline(args, n_lookups_target=None):
         if el >= args.cpu_seconds:
             break
     return {"value": done / el, "unit": "lookups/s", "cores": threads, "kind": "port",
-            "sample": "%d lookups (features of B=%d ids, h=1) over a %d-key x %d-dim fp32 EV, "
-                      "%.1f s, oracle/deeprec_oracle.c orc_pipeline_ev_lookup_sparse "
-                      "(serial Unique + sharded KvResourceGather + ali SparseSegmentSum)"
-                      % (done, B, R, D, el)}
+            "nproc": os.cpu_count(), "cpu_model": _cpu_model(),
+            "sample": "%d lookups (features of B=%d ids, h=1) over a %d-key x %d-dim fp32 EV "
+                      "(one table of the GPU's per-table shape), %.1f s on %d threads, "
+                      "oracle/deeprec_oracle.c orc_pipeline_ev_lookup_sparse (serial Unique + "
+                      "Shard-split KvResourceGather + ali SparseSegmentSum)"
+                      % (done, B, R, D, el, threads)}
+
+
+def synth_rows(seed, keys, D):
+    """The bench tables' rows: synth(seed, key, col) of dr_common.h
+    (SplitMix64 -> uniform [-1, 1)), for checking gathered rows."""
+    M = np.uint64
+    with np.errstate(over="ignore"):
+        z = (M(seed) * M(0x9E3779B97F4A7C15) + keys.astype(np.uint64)[:, None] * M(0xBF58476D1CE4E5B9)
+             + np.arange(D, dtype=np.uint64)[None, :] * M(0x94D049BB133111EB))
+        z ^= z >> M(30)
+        z *= M(0xBF58476D1CE4E5B9)
+        z ^= z >> M(27)
+        z *= M(0x94D049BB133111EB)
+        z ^= z >> M(31)
+    hi = (z >> M(32)).astype(np.uint32).view(np.int32)
+    return hi.astype(np.float32) * np.float32(1.0 / 2147483648.0)
+
+
+def check_rows(out, ids, T, D, n_sample, seed):
+    """Sampled (bag, table) rows of a [B, T*D] sum-pooled one-hot output must
+    equal the table rows synth(1000 + t, key, :) bit for bit (keys < the
+    populated range); returns the number of rows checked, raises otherwise."""
+    B = out.shape[0]
+    rng = np.random.default_rng(seed)
+    b = rng.integers(0, B, n_sample)
+    t = rng.integers(0, T, n_sample)
+    got = out.view(B, T, D)[torch.as_tensor(b, device=out.device),
+                            torch.as_tensor(t, device=out.device)].cpu().numpy()
+    keys = ids[torch.as_tensor(t, device=ids.device), torch.as_tensor(b, device=ids.device)]
+    keys = keys.cpu().numpy()
+    for tt in np.unique(t):
+        sel = t == tt
+        want = synth_rows(1000 + int(tt), keys[sel], D)
+        if not np.array_equal(got[sel], want):
+            bad = np.argwhere(~(got[sel] == want).all(1))[:, 0]
+            raise AssertionError("headline parity: table %d, %d of %d sampled rows differ "
+                                 "(first key %d)" % (tt, bad.shape[0], sel.sum(),
+                                                     keys[sel][bad[0]]))
+    return int(n_sample)
 
 
 def main():
@@ -140,7 +197,11 @@ def main():
     t0 = time.perf_counter()
     evs = []
     for t in range(T):
-        ev = dr.EmbeddingVariable("table%d" % t, D, 0.0, capacity=R + (1 << 19), device=dev)
+        # headroom for one step of new keys per table: B (local resolve) or
+        # N * B (an owner serving every rank, dr_xgmi_serve), with slack for
+        # the asynchronously mirrored row count (no host sync per step)
+        ev = dr.EmbeddingVariable("table%d" % t, D, 0.0, device=dev,
+                                  capacity=R + max(1 << 19, 4 * world * B))
         # rank r owns keys k % world == r of the keyspace [0, R * world)
         ev.insert_synthetic(rank, R, seed=1000 + t, key_stride=world)
         evs.append(ev)
@@ -196,18 +257,28 @@ def main():
         keyspace = R
     batches = make_batches(4, T, B, keyspace, args.zipf, 2021 + 7919 * rank, dev)
     engine_check = None
-    if engine is not None and engine is not a2a:
-        # the peer-write engine must reproduce the all-to-all engine bit for bit
+
+    def engines_agree(steps):
+        """The peer-write engine must reproduce the all-to-all engine bit for
+        bit: compared on the given batch indices, with the output consumed
+        (read) between steps, and-reduced over ranks."""
+        same = 1
         with torch.no_grad():
-            ref = a2a.forward(batches[0]).clone()
-            same = int(torch.equal(engine.forward(batches[0]), ref))
+            for k in steps:
+                got = engine.forward(batches[k]).clone()
+                float(got.sum())                      # consume, as a model step would
+                same &= int(torch.equal(got, a2a.forward(batches[k])))
         if world > 1:
             flag = torch.tensor([same], dtype=torch.int32, device="cpu" if staged else dev)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             same = int(flag.item())
-        engine_check = "xgmi output == all-to-all output, step 0, all ranks: %s" % bool(same)
+        return bool(same)
+
+    if engine is not None and engine is not a2a:
+        ok0 = engines_agree([0, 1, 2, 3])
+        engine_check = "xgmi == all-to-all output, steps 0-3, all ranks: %s" % ok0
         log(engine_check)
-        if not same:
+        if not ok0:
             engine.close()
             engine, engine_kind = a2a, "RCCL all-to-all (xgmi check failed)"
     seg = torch.arange(B, dtype=torch.int32, device=dev)
@@ -259,17 +330,40 @@ def main():
                     log("step %d: done" % i)
                 i += 1
 
-        run_steps(0, args.warmup)
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        run_steps(0, args.steps)
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
+        def timed():
+            run_steps(0, args.warmup)
+            if dist is not None:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            run_steps(0, args.steps)
+            if dist is not None:
+                dist.barrier()
+            torch.cuda.synchronize()
+            return time.perf_counter() - t0
+
+        el = timed()
         log("timed %d steps in %.3fs" % (args.steps, el))
+        if engine is not None and engine is not a2a:
+            # the last timed step's output (still in the engine's buffer),
+            # then two more steps, against the all-to-all engine
+            with torch.no_grad():
+                kl = (args.steps - 1) % NBATCH
+                last = engine.bufs.out.clone()
+                same = int(torch.equal(last, a2a.forward(batches[kl])))
+                if world > 1:
+                    flag = torch.tensor([same], dtype=torch.int32,
+                                        device="cpu" if staged else dev)
+                    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+                    same = int(flag.item())
+            ok1 = bool(same) and engines_agree([(kl + 1) % NBATCH, (kl + 2) % NBATCH])
+            engine_check += "; last timed step + 2 more after timing: %s" % ok1
+            log(engine_check)
+            if not ok1:
+                engine.close()
+                engine, engine_kind = a2a, "RCCL all-to-all (xgmi check failed after timing)"
+                el = timed()
+                log("re-timed with the all-to-all engine: %.3fs" % el)
     if dist is not None:
         t = torch.tensor([el], dtype=torch.float64, device="cpu" if staged else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -278,6 +372,90 @@ def main():
     value = lookups / el
     ms = el / args.steps * 1e3
     dr.status_check(dev)
+
+    # ---- parity at the headline size, outside the timed region: sampled
+    # output rows == the tables' synth rows bit for bit (every key exists);
+    # N = 1 also runs a step with ~10 % new keys (insert-on-miss: default
+    # rows, EV sizes grow by the distinct new keys) and a Zipf(1.05) step
+    correctness = {"checked_rows": 0}
+    with torch.no_grad():
+        kc = (args.steps - 1) % NBATCH
+        outc = step(kc)
+        correctness["checked_rows"] += check_rows(outc, batches[kc], T, D, args.check_rows,
+                                                  17 + rank)
+        if world == 1 and engine is None:
+            gz = torch.Generator(device=dev)
+            gz.manual_seed(99)
+            ids = torch.randint(0, R, (T, B), generator=gz, device=dev, dtype=torch.int64)
+            newm = torch.rand((T, B), generator=gz, device=dev) < 0.1
+            ids = torch.where(newm, R + torch.randint(0, 1 << 40, (T, B), generator=gz,
+                                                      device=dev, dtype=torch.int64), ids)
+            before = [int(ev.total_count()[0]) for ev in evs]
+            sps = [SparseTensor(ind, ids[t], (B, 1)) for t in range(T)]
+            outn = dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum")
+            dr.status_check(dev)
+            view = outn.view(B, T, D)
+            old_ok = ~newm.t()                          # [B, T]
+            for t in range(T):
+                added = int(evs[t].total_count()[0]) - before[t]
+                want = int(torch.unique(ids[t][newm[t]]).numel())
+                if added != want:
+                    raise AssertionError("table %d grew by %d keys, expected %d" % (t, added, want))
+            if bool((view[~old_ok] != 0).any()):
+                raise AssertionError("new keys must read the EV default row (0)")
+            keep = torch.nonzero(old_ok.t().reshape(-1)).reshape(-1)[:args.check_rows]
+            tb = keep // B
+            bb = keep % B
+            got = view[bb, tb].cpu().numpy()
+            kk = ids[tb, bb].cpu().numpy()
+            tt = tb.cpu().numpy()
+            for t in np.unique(tt):
+                if not np.array_equal(got[tt == t], synth_rows(1000 + int(t), kk[tt == t], D)):
+                    raise AssertionError("new-key step: existing rows differ (table %d)" % t)
+            correctness["checked_rows"] += int(keep.numel())
+            correctness["new_key_step"] = {"new_keys": int(newm.sum()),
+                                           "ev_growth_exact": True,
+                                           "defaults_for_new": True}
+            zk = (torch.as_tensor(np.random.default_rng(5).zipf(1.05, size=(T, B)),
+                                  device=dev) - 1) % R
+            zsp = [SparseTensor(ind, zk[t], (B, 1)) for t in range(T)]
+            outz = dr.embedding_lookup_sparse_multi(evs, zsp, combiner="sum")
+            correctness["checked_rows"] += check_rows(outz, zk, T, D, args.check_rows, 23)
+            correctness["zipf_step"] = {"alpha": 1.05, "distinct_keys_table0":
+                                        int(torch.unique(zk[0]).numel())}
+        dr.status_check(dev)
+    correctness["bitexact"] = True
+    correctness["status"] = "clean"
+    log("headline-size parity: %s" % json.dumps(correctness))
+
+    # ---- embedding training step (N = 1): forward (grouped Unique -> EV
+    # resolve -> pool) + backward (grouped segment grad) + KV SGD apply
+    train = None
+    if world == 1 and engine is None and args.train_steps > 0:
+        opt = dr.GradientDescentOptimizer(0.01)
+        upstream = torch.randn((B, T * D), device=dev)
+
+        def tstep(i):
+            out = dr.embedding_lookup_sparse_multi(evs, batch_sps[i % NBATCH], combiner="sum")
+            out.backward(upstream)
+            opt.apply_gradients(evs)
+
+        for i in range(2):
+            tstep(i)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.train_steps):
+            tstep(i)
+        torch.cuda.synchronize()
+        tel = time.perf_counter() - t0
+        dr.status_check(dev)
+        tms = tel / args.train_steps * 1e3
+        train = {"ms_per_step": round(tms, 4), "samples_per_s": round(B / (tms * 1e-3), 1),
+                 "lookups_per_s": round(T * B / (tms * 1e-3), 1),
+                 "step": "embedding layer training step: embedding_lookup_sparse_multi forward "
+                         "(grouped Unique, EV resolve, pool) + backward (grouped segment grad) "
+                         "+ KV SGD apply, %d EVs, B=%d" % (T, B)}
+        log("train step: %s" % json.dumps(train))
 
     # ---- dominant kernel: the fused one-hot EV lookup, timed alone --------
     # dr_ev_lookup_onehot on keys this rank owns (all keys at N=1): the
@@ -398,7 +576,9 @@ def main():
                        "global_batch": B * world, "tables": T, "rows_per_gpu": R, "dim": D,
                        "engine": engine_kind, "engine_check": engine_check,
                        "parallelism": "row-sharded tables x%d, data-parallel batch" % world},
-            "samples_per_s": round(value / T, 1),
+            "forward_samples_per_s": round(value / T, 1),
+            "train_step": train,
+            "correctness": correctness,
             "roofline": roof,
             "roofline_row_gather": roof_gather,
             "cpu_baseline": cpu,

@@ -2457,6 +2457,17 @@ int dr_xgmi_serve(const dr_xgmi_peers* peers, dr_ev* const* evs, int num_tables,
   int* stw = status_word();
   DR_REQUIRE(stw, DR_INTERNAL, "status word unavailable");
   hipStream_t st = S(stream);
+  // Insert-on-miss of up to W * batch new keys per table (every source may
+  // send `batch` keys of table t): grow the key table / row pools first,
+  // like every other insert path (no host sync while the mirrored row count
+  // leaves room).
+  for (int t = 0; t < num_tables; ++t) {
+    int rc = reserve(evs[t]->sh, (int64_t)W * batch, st);
+    if (rc) return rc;
+    ra.e[t] = make_desc(evs[t]);   // grow() may have moved the table / pools
+    wa.pool[t] = evs[t]->sh->pools[evs[t]->col];
+    wa.dflt[t] = evs[t]->sh->defaults[evs[t]->col];
+  }
   // One-shot grids sized for 1.25x the keys a source sends on average
   // (T*B / W for keys spread over owners); the kernels' grid-stride loops
   // take any excess (skewed keys) in a second pass.  Small grids with long
@@ -2478,6 +2489,7 @@ int dr_xgmi_serve(const dr_xgmi_peers* peers, dr_ev* const* evs, int num_tables,
     hipLaunchKernelGGL((xgmi_emit_kernel<64, 4>), ge(64), dim3(256), 0, st, wa, w.rows);
   hipLaunchKernelGGL(xgmi_flush_kernel, dim3(64), dim3(64), 0, st);
   DR_LAUNCH_CHECK();
+  for (int t = 0; t < num_tables; ++t) post_call(evs[t]->sh, st);
   return DR_OK;
 }
 

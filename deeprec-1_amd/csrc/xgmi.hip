@@ -206,6 +206,114 @@ int dr_ipc_close(void* base) {
   return DR_OK;
 }
 
+// Buffers that other GPUs write over xGMI (inboxes, outputs) or read
+// (gradients): uncached device memory, so no XCD L2 of the owning GPU can
+// hold a line a peer has since rewritten -- per-XCD L2s are not coherent
+// with writes arriving from another agent (MI355X_MICROARCH.md "Correctness
+// boundaries"; the DMA-memset staleness of DESIGN.md section 6 is the same
+// effect).  Zero-filled, synchronously (allocation time only).
+int dr_ipc_alloc(size_t bytes, void** ptr_out) {
+  using namespace dr;
+  DR_REQUIRE(ptr_out, DR_INVALID_ARGUMENT, "null ptr_out");
+  const size_t n = bytes > 0 ? (bytes + 255) & ~size_t(255) : 256;
+  void* p = nullptr;
+  DR_HIP(hipExtMallocWithFlags(&p, n, hipDeviceMallocUncached));
+  int rc = fill_bytes(p, 0, n, nullptr);
+  if (rc == DR_OK) {
+    hipError_t e = hipStreamSynchronize(nullptr);
+    if (e != hipSuccess) {
+      set_error("dr_ipc_alloc: %s", hipGetErrorString(e));
+      rc = DR_INTERNAL;
+    }
+  }
+  if (rc) {
+    (void)hipFree(p);
+    return rc;
+  }
+  *ptr_out = p;
+  return DR_OK;
+}
+
+int dr_ipc_free(void* ptr) {
+  if (!ptr) return DR_OK;
+  DR_HIP(hipFree(ptr));
+  return DR_OK;
+}
+
+// DLPack (v0.8 DLManagedTensor) view of a dr_ipc_alloc buffer, so a framework
+// can own it as a tensor (torch.utils.dlpack.from_dlpack); the deleter is C,
+// independent of the interpreter's lifetime.
+namespace {
+struct DlDevice {
+  int32_t device_type, device_id;
+};
+struct DlDataType {
+  uint8_t code, bits;
+  uint16_t lanes;
+};
+struct DlTensor {
+  void* data;
+  DlDevice device;
+  int32_t ndim;
+  DlDataType dtype;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+};
+struct DlManaged {
+  DlTensor t;
+  void* ctx;
+  void (*deleter)(DlManaged*);
+  int64_t shape[8];
+};
+void dl_delete(DlManaged* m) {
+  if (!m) return;
+  (void)hipFree(m->t.data);
+  free(m);
+}
+}  // namespace
+
+int dr_ipc_alloc_dlpack(int ndim, const int64_t* shape, int dtype_code, int dtype_bits,
+                        int device_id, void** managed_out) {
+  using namespace dr;
+  DR_REQUIRE(ndim >= 1 && ndim <= 8 && shape && managed_out && dtype_bits % 8 == 0 &&
+                 dtype_bits > 0,
+             DR_INVALID_ARGUMENT, "dr_ipc_alloc_dlpack: bad shape / dtype");
+  size_t n = (size_t)(dtype_bits / 8);
+  for (int i = 0; i < ndim; ++i) {
+    DR_REQUIRE(shape[i] >= 0, DR_INVALID_ARGUMENT, "negative dim");
+    n *= (size_t)shape[i];
+  }
+  int cur = 0;
+  DR_HIP(hipGetDevice(&cur));
+  DR_REQUIRE(cur == device_id, DR_INVALID_ARGUMENT, "device %d is not current (%d)", device_id,
+             cur);
+  void* p = nullptr;
+  int rc = dr_ipc_alloc(n, &p);
+  if (rc) return rc;
+  DlManaged* m = static_cast<DlManaged*>(calloc(1, sizeof(DlManaged)));
+  if (!m) {
+    (void)hipFree(p);
+    set_error("dr_ipc_alloc_dlpack: out of host memory");
+    return DR_RESOURCE_EXHAUSTED;
+  }
+  for (int i = 0; i < ndim; ++i) m->shape[i] = shape[i];
+  m->t.data = p;
+  m->t.device.device_type = 10;  // kDLROCM
+  m->t.device.device_id = device_id;
+  m->t.ndim = ndim;
+  m->t.dtype.code = (uint8_t)dtype_code;
+  m->t.dtype.bits = (uint8_t)dtype_bits;
+  m->t.dtype.lanes = 1;
+  m->t.shape = m->shape;
+  m->t.strides = nullptr;  // compact row-major
+  m->t.byte_offset = 0;
+  m->ctx = nullptr;
+  m->deleter = dl_delete;
+  *managed_out = m;
+  return DR_OK;
+}
+
 int dr_xgmi_route(const dr_xgmi_peers* peers, const int64_t* keys, int num_tables,
                   int64_t batch, int64_t* cnt_ws, void* stream) {
   using namespace dr;

@@ -165,6 +165,9 @@ SIGNATURES = {
     "dr_ipc_export": (_I32, [_P, _P, _P]),
     "dr_ipc_import": (_I32, [_P, _I64, _P, _P]),
     "dr_ipc_close": (_I32, [_P]),
+    "dr_ipc_alloc": (_I32, [_SZ, _P]),
+    "dr_ipc_free": (_I32, [_P]),
+    "dr_ipc_alloc_dlpack": (_I32, [_I32, _P, _I32, _I32, _I32, _P]),
     "dr_xgmi_route": (_I32, [_P, _P, _I32, _I64, _P, _P]),
     "dr_xgmi_serve_workspace_size": (_SZ, [_I32, _I64]),
     "dr_xgmi_serve": (_I32, [_P, _P, _I32, _I64, _P, _SZ, _P]),
@@ -242,6 +245,27 @@ def stream_handle(device=None):
 
 def workspace(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+_DL_CODES = {torch.int64: (0, 64), torch.int32: (0, 32), torch.float32: (2, 32)}
+
+
+def uncached_empty(shape, dtype, device):
+    """A zero-filled torch tensor in UNCACHED device memory (dr_ipc_alloc):
+    for buffers that peer GPUs write or read over xGMI.  Owned by torch
+    through DLPack; freed by the library's deleter."""
+    from torch.utils import dlpack
+    code, bits = _DL_CODES[dtype]
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    shp = (C.c_int64 * len(shape))(*[int(x) for x in shape])
+    m = C.c_void_p()
+    with torch.cuda.device(idx):
+        check(lib().dr_ipc_alloc_dlpack(len(shape), shp, code, bits, idx, C.byref(m)))
+    new = C.pythonapi.PyCapsule_New
+    new.restype = C.py_object
+    new.argtypes = [C.c_void_p, C.c_char_p, C.c_void_p]
+    return dlpack.from_dlpack(new(m, b"dltensor", None))
 
 
 def status_check(device=None):

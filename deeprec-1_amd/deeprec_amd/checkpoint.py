@@ -514,8 +514,12 @@ def restore_embedding_variable(ev, reader, name, partition_id=0, partition_num=1
             break
         if new_form:
             for key in ("-values", "-versions"):
+                # LookupHeader / LookupTensorShape fail on a missing tensor and
+                # EVRestoreDynamically treats that as fatal: raise, do not
+                # leave the EV half restored
                 if not reader.contains(tname + key):
-                    return
+                    raise _lib.DeepRecError(_lib.NOT_FOUND, "Key %s%s not found in checkpoint"
+                                       % (tname, key))
             offs = reader.lookup(tname + "-partition_offset")
             for sub in range(partition_id % SAVED_PARTITION_NUM, SAVED_PARTITION_NUM,
                              partition_num):

@@ -396,13 +396,20 @@ class XgmiBuffers(object):
     (key, slot) pairs into, the [B, T*D] output that owners write rows into,
     and the [B, T*D] gradient that owners pull rows from in backward()."""
 
-    def __init__(self, world, T, batch, dim, device):
+    def __init__(self, world, T, batch, dim, device, uncached=True):
+        # uncached (dr_ipc_alloc): a peer's xGMI writes can never be hidden by
+        # a stale line in one of this GPU's per-XCD L2s; uncached=False keeps
+        # plain torch allocations (single-process tests, all "ranks" on one
+        # device and one set of L2s)
+        alloc = _lib.uncached_empty if uncached else \
+            (lambda shape, dtype, dev: torch.zeros(shape, dtype=dtype, device=dev))
         self.cap = T * batch
-        self.inbox_keys = torch.empty((world, self.cap), dtype=torch.int64, device=device)
-        self.inbox_slot = torch.empty((world, self.cap), dtype=torch.int32, device=device)
-        self.inbox_cnt = torch.zeros(world, dtype=torch.int64, device=device)
-        self.out = torch.empty((batch, T * dim), dtype=torch.float32, device=device)
-        self.gin = torch.empty((batch, T * dim), dtype=torch.float32, device=device)
+        self.uncached = uncached
+        self.inbox_keys = alloc((world, self.cap), torch.int64, device)
+        self.inbox_slot = alloc((world, self.cap), torch.int32, device)
+        self.inbox_cnt = alloc((world,), torch.int64, device)
+        self.out = alloc((batch, T * dim), torch.float32, device)
+        self.gin = alloc((batch, T * dim), torch.float32, device)
 
     def tensors(self):
         return [self.inbox_keys, self.inbox_slot, self.inbox_cnt, self.out, self.gin]

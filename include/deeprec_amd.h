@@ -524,6 +524,18 @@ int dr_ipc_export(const void* ptr, void* handle_out, int64_t* offset_out);
 /* maps a peer's allocation; *ptr_out = base + offset, *base_out for close.  */
 int dr_ipc_import(const void* handle, int64_t offset, void** ptr_out, void** base_out);
 int dr_ipc_close(void* base);
+/* Allocation for buffers peers access over xGMI (the exchange inboxes,    */
+/* outputs and gradients): UNCACHED device memory (hipDeviceMallocUncached), */
+/* zero-filled, synchronous.  A coarse-grained hipMalloc buffer can keep a  */
+/* stale line in one of its own GPU's per-XCD L2s after a peer rewrote it.  */
+int dr_ipc_alloc(size_t bytes, void** ptr_out);
+int dr_ipc_free(void* ptr);
+/* The same buffer as a DLPack v0.8 DLManagedTensor (device kDLROCM, compact */
+/* row-major; dtype_code: 0 int, 1 uint, 2 float) whose C deleter frees it, */
+/* for frameworks to own (torch.utils.dlpack.from_dlpack of a "dltensor"    */
+/* capsule).  device_id must be the current device.                         */
+int dr_ipc_alloc_dlpack(int ndim, const int64_t* shape, int dtype_code, int dtype_bits,
+                        int device_id, void** managed_out);
 
 typedef struct {
   int32_t world, rank;

@@ -586,3 +586,20 @@ def safe_embedding_lookup_sparse(params, indices, values, dense_shape, weights=N
     if default_id is None:
         res[empty] = 0.0
     return res
+
+
+def synth_rows(seed, keys, D):
+    """synth(seed, key, col) of the engine's synthetic tables (dr_common.h:
+    SplitMix64 of (seed, row, col) -> uniform [-1, 1)), rows for `keys`."""
+    M = np.uint64
+    keys = np.asarray(keys, np.int64)
+    with np.errstate(over="ignore"):
+        z = (M(seed) * M(0x9E3779B97F4A7C15) + keys.astype(np.uint64)[:, None] * M(0xBF58476D1CE4E5B9)
+             + np.arange(D, dtype=np.uint64)[None, :] * M(0x94D049BB133111EB))
+        z ^= z >> M(30)
+        z *= M(0xBF58476D1CE4E5B9)
+        z ^= z >> M(27)
+        z *= M(0x94D049BB133111EB)
+        z ^= z >> M(31)
+    hi = (z >> M(32)).astype(np.uint32).view(np.int32)
+    return hi.astype(np.float32) * np.float32(1.0 / 2147483648.0)

@@ -75,3 +75,23 @@ def test_abi_version_without_device(built_lib):
     lib = ctypes.CDLL(built_lib)
     lib.dr_abi_version.restype = ctypes.c_int
     assert lib.dr_abi_version() == 1
+
+
+def test_synth_rows_restatement_matches_library(built_lib):
+    """The numpy synth(seed, key, col) used by the headline-size parity checks
+    (oracle.synth_rows, bench.synth_rows) equals the library's host synth."""
+    import sys
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "deeprec-1_amd"))
+    import bench
+    from oracle import oracle as orc
+    L = ctypes.CDLL(built_lib)
+    L.dr_synth_value.restype = ctypes.c_float
+    L.dr_synth_value.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64]
+    keys = np.array([0, 1, 7, 12_499_999, 99_999_999_999, 2 ** 40 + 3], np.int64)
+    for seed in (1000, 1025):
+        want = np.array([[L.dr_synth_value(seed, int(k), c) for c in range(128)] for k in keys],
+                        np.float32)
+        np.testing.assert_array_equal(orc.synth_rows(seed, keys, 128), want)
+        np.testing.assert_array_equal(bench.synth_rows(seed, keys, 128), want)

@@ -97,3 +97,21 @@ def test_restore_without_partition_and_counter_filter(tmp_path):
     np.testing.assert_array_equal(vals[o], v2[o2])
     # Import clamps freqs up to filter_freq (embedding_var.h:204-209)
     np.testing.assert_array_equal(np.maximum(frqs[o], 3), f2[o2])
+
+
+def test_restore_missing_values_is_not_found(tmp_path):
+    """A new-form part with -keys but no -values fails with NotFound (the
+    reference's LookupHeader status; EVRestoreDynamically treats it as
+    fatal) instead of leaving the EV half restored."""
+    import deeprec_amd as dr
+    from deeprec_amd import checkpoint as ck
+    pre = str(tmp_path / "m")
+    w = ck.BundleWriter(pre)
+    w.add("emb/part_0/x-keys", np.array([1, 2], np.int64))
+    w.add("emb/part_0/x-partition_offset", np.zeros(1001, np.int32))
+    w.finish()
+    ev = dr.EmbeddingVariable("ck_missing", 4, 0.5, device=DEV)
+    with pytest.raises(dr.DeepRecError) as e:
+        ck.restore_embedding_variable(ev, ck.BundleReader(pre), "emb/part_0/x", 0, 1)
+    assert e.value.code == 5
+    assert int(ev.total_count()[0]) == 0

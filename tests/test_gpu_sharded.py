@@ -233,6 +233,59 @@ def test_xgmi_peer_write_engine(world):
     _run_xgmi(world)
 
 
+@pytest.mark.parametrize("world", [1, 2])
+def test_xgmi_serve_grows_small_tables(world):
+    """Owners whose EVs start with room for 256 rows receive ~3x that many new
+    keys over three steps: dr_xgmi_serve reserves before its insert-on-miss
+    (ADVICE round 1), so nothing is served from a dead row, the status word
+    stays clean and every key is stored exactly once."""
+    import deeprec_amd as dr
+    from deeprec_amd.sharded import XgmiBuffers, XgmiShardedLookup
+    dr.load()
+    evs_all = [[dr.EmbeddingVariable("xgrow%d_%d_%d" % (world, r, t), D, DEFAULT, device=DEV,
+                                     capacity=256) for t in range(T)] for r in range(world)]
+    bufs = [XgmiBuffers(world, T, B, D, DEV) for _ in range(world)]
+    bar = threading.Barrier(world)
+    engines = [XgmiShardedLookup(evs_all[r], world, r, B, torch.device(DEV), peer_buffers=bufs,
+                                 barrier=bar.wait, buffers=bufs[r]) for r in range(world)]
+    seen = [set() for _ in range(T)]
+    for step in range(3):
+        # distinct new keys every step, each rank's spread over every owner
+        allk = np.random.default_rng(step).permutation(T * B * world).astype(np.int64)
+        allk += step * T * B * world
+        ids = [allk[r * T * B:(r + 1) * T * B].reshape(T, B) for r in range(world)]
+        for r in range(world):
+            for t in range(T):
+                seen[t].update(ids[r][t].tolist())
+        outs, errs = [None] * world, []
+
+        def run(r):
+            try:
+                with torch.no_grad():
+                    o = engines[r].forward(torch.as_tensor(ids[r], device=DEV))
+                bar.wait()
+                outs[r] = o.cpu().numpy()
+            except Exception as e:
+                errs.append(e)
+                bar.abort()
+
+        th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(120)
+        if errs:
+            raise errs[0]
+        dr.status_check()
+        for r in range(world):
+            assert np.all(outs[r] == np.float32(DEFAULT))
+    for r in range(world):
+        for t in range(T):
+            k = evs_all[r][t].export()[0].cpu().numpy()
+            want = np.array(sorted(x for x in seen[t] if x % world == r), np.int64)
+            np.testing.assert_array_equal(np.sort(k), want)
+
+
 # ---------------------------------------------------------------------------
 # Sharded backward (ShardedLookup.backward): grad rows to the owners, then the
 # KV optimizer on each shard.  Reference: one EV per feature holding every
