@@ -5,6 +5,9 @@
 // owner = key % world, exchanges counts, and copies keys through NCCL send /
 // recv buffers.  Here the requester writes every (key, slot) pair straight
 // into the owner's inbox over xGMI: no send buffer, no host read of counts.
+#include <map>
+#include <mutex>
+
 #include "dr_common.h"
 
 namespace dr {
@@ -172,6 +175,18 @@ __global__ void xgmi_table_start_kernel(const uint64_t* __restrict__ kout, int64
 
 }  // namespace dr
 
+namespace {
+struct UcFree {
+  std::mutex mu;
+  std::multimap<std::pair<int, size_t>, void*> free;  // (device, bytes) -> ptr
+  std::map<void*, std::pair<int, size_t>> size_of;
+};
+UcFree& uc_pool() {
+  static UcFree* p = new UcFree();  // never destroyed (process lifetime)
+  return *p;
+}
+}  // namespace
+
 extern "C" {
 
 int dr_ipc_export(const void* ptr, void* handle_out, int64_t* offset_out) {
@@ -212,12 +227,37 @@ int dr_ipc_close(void* base) {
 // with writes arriving from another agent (MI355X_MICROARCH.md "Correctness
 // boundaries"; the DMA-memset staleness of DESIGN.md section 6 is the same
 // effect).  Zero-filled, synchronously (allocation time only).
+//
+// Uncached buffers are never handed back to the HIP allocator: measured on
+// MI355X / ROCm 7.2, a coarse-grained hipMalloc that reuses memory freed
+// from a hipDeviceMallocUncached allocation of the same process returned
+// corrupted rows (tests/test_gpu_sharded.py::test_xgmi_serve_grows_small_
+// tables after the peer-write tests).  Freed buffers go
+// to a per-device free list keyed by size and are reused by the next
+// allocation of that size.
+
 int dr_ipc_alloc(size_t bytes, void** ptr_out) {
   using namespace dr;
   DR_REQUIRE(ptr_out, DR_INVALID_ARGUMENT, "null ptr_out");
   const size_t n = bytes > 0 ? (bytes + 255) & ~size_t(255) : 256;
+  int dev = 0;
+  DR_HIP(hipGetDevice(&dev));
   void* p = nullptr;
-  DR_HIP(hipExtMallocWithFlags(&p, n, hipDeviceMallocUncached));
+  {
+    UcFree& u = uc_pool();
+    std::lock_guard<std::mutex> g(u.mu);
+    auto it = u.free.find({dev, n});
+    if (it != u.free.end()) {
+      p = it->second;
+      u.free.erase(it);
+    }
+  }
+  if (!p) {
+    DR_HIP(hipExtMallocWithFlags(&p, n, hipDeviceMallocUncached));
+    UcFree& u = uc_pool();
+    std::lock_guard<std::mutex> g(u.mu);
+    u.size_of[p] = {dev, n};
+  }
   int rc = fill_bytes(p, 0, n, nullptr);
   if (rc == DR_OK) {
     hipError_t e = hipStreamSynchronize(nullptr);
@@ -227,7 +267,7 @@ int dr_ipc_alloc(size_t bytes, void** ptr_out) {
     }
   }
   if (rc) {
-    (void)hipFree(p);
+    (void)dr_ipc_free(p);
     return rc;
   }
   *ptr_out = p;
@@ -235,8 +275,14 @@ int dr_ipc_alloc(size_t bytes, void** ptr_out) {
 }
 
 int dr_ipc_free(void* ptr) {
+  using namespace dr;
   if (!ptr) return DR_OK;
-  DR_HIP(hipFree(ptr));
+  UcFree& u = uc_pool();
+  std::lock_guard<std::mutex> g(u.mu);
+  auto it = u.size_of.find(ptr);
+  DR_REQUIRE(it != u.size_of.end(), DR_INVALID_ARGUMENT,
+             "dr_ipc_free: %p was not allocated by dr_ipc_alloc", ptr);
+  u.free.insert({it->second, ptr});
   return DR_OK;
 }
 
@@ -268,7 +314,7 @@ struct DlManaged {
 };
 void dl_delete(DlManaged* m) {
   if (!m) return;
-  (void)hipFree(m->t.data);
+  (void)dr_ipc_free(m->t.data);
   free(m);
 }
 }  // namespace

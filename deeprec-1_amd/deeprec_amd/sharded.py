@@ -40,6 +40,7 @@ can be exercised on CPU with world_size-2 gloo (tests/); the product
 backend is HipLocal (HIP kernels through the C ABI).
 """
 import ctypes as C
+import os
 
 import torch
 import torch.distributed as dist
@@ -396,11 +397,13 @@ class XgmiBuffers(object):
     (key, slot) pairs into, the [B, T*D] output that owners write rows into,
     and the [B, T*D] gradient that owners pull rows from in backward()."""
 
-    def __init__(self, world, T, batch, dim, device, uncached=True):
+    def __init__(self, world, T, batch, dim, device, uncached=None):
         # uncached (dr_ipc_alloc): a peer's xGMI writes can never be hidden by
         # a stale line in one of this GPU's per-XCD L2s; uncached=False keeps
         # plain torch allocations (single-process tests, all "ranks" on one
         # device and one set of L2s)
+        if uncached is None:
+            uncached = os.environ.get("DEEPREC_AMD_IPC_UNCACHED", "1") != "0"
         alloc = _lib.uncached_empty if uncached else \
             (lambda shape, dtype, dev: torch.zeros(shape, dtype=dtype, device=dev))
         self.cap = T * batch

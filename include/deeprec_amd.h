@@ -528,6 +528,8 @@ int dr_ipc_close(void* base);
 /* outputs and gradients): UNCACHED device memory (hipDeviceMallocUncached), */
 /* zero-filled, synchronous.  A coarse-grained hipMalloc buffer can keep a  */
 /* stale line in one of its own GPU's per-XCD L2s after a peer rewrote it.  */
+/* dr_ipc_free recycles the buffer for the next dr_ipc_alloc of the same    */
+/* size (uncached memory is never returned to the HIP allocator).           */
 int dr_ipc_alloc(size_t bytes, void** ptr_out);
 int dr_ipc_free(void* ptr);
 /* The same buffer as a DLPack v0.8 DLManagedTensor (device kDLROCM, compact */

@@ -278,7 +278,18 @@ def test_xgmi_serve_grows_small_tables(world):
             raise errs[0]
         dr.status_check()
         for r in range(world):
-            assert np.all(outs[r] == np.float32(DEFAULT))
+            if not np.all(outs[r] == np.float32(DEFAULT)):
+                ob = outs[r].reshape(B, T, D)
+                badbt = np.argwhere(~(ob == np.float32(DEFAULT)).all(2))
+                stored = []
+                for t in range(T):
+                    vals = [evs_all[o][t].export()[1].cpu().numpy() for o in range(world)]
+                    stored.append(int(sum((v != np.float32(DEFAULT)).any(1).sum() for v in vals)))
+                raise AssertionError(
+                    "step %d rank %d: %d (bag, table) outputs differ, first %s (key %d); "
+                    "stored rows != default per table: %s" % (
+                        step, r, badbt.shape[0], badbt[:4].tolist(),
+                        ids[r][badbt[0][1], badbt[0][0]], stored))
     for r in range(world):
         for t in range(T):
             k = evs_all[r][t].export()[0].cpu().numpy()
