@@ -286,6 +286,8 @@ __global__ __launch_bounds__(256) void pool_onehot_kernel(PoolArgs args, int T, 
   __syncthreads();
   constexpr int GPB = 256 / G;
   const int64_t slots = (int64_t)T * B;
+  // (an XCD-contiguous renumbering of the blocks measured 2-3 % slower:
+  // profiles/r02_ab_xcd_swizzle.log)
   const int64_t s0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * NB;
   if (s0 >= slots) return;
   const int lg = threadIdx.x % G;

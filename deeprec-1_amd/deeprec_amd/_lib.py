@@ -10,7 +10,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdeeprec_amd.so")
+# DEEPREC_AMD_LIB: an A/B build of the same library (measurement only)
+LIB_PATH = os.environ.get("DEEPREC_AMD_LIB") or os.path.join(_HERE, "libdeeprec_amd.so")
 
 # TF error::Code values (include/deeprec_amd.h)
 OK, INVALID_ARGUMENT, NOT_FOUND, ALREADY_EXISTS, RESOURCE_EXHAUSTED, INTERNAL = 0, 3, 5, 6, 8, 13
