@@ -8,6 +8,7 @@ safe_embedding_lookup_sparse, fused_embedding_lookup_sparse, the EV sparse
 optimizers) on torch device tensors.
 """
 from . import _lib
+from . import torch_ops  # noqa: F401  (registers torch.ops.deeprec.*)
 from ._lib import DeepRecError, InvalidArgumentError, load
 from .embedding_ops import (DenseTable, SparseTensor, embedding_lookup, embedding_lookup_sparse,
                             embedding_lookup_sparse_multi, fused_embedding_lookup_sparse,

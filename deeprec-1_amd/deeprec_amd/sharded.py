@@ -187,6 +187,17 @@ class ShardedLookup(object):
         vals = ids.reshape(-1)
         koff = [t * nnz for t in range(T + 1)]
         direct = bag_offs is None and not need_grad and not be.filter
+        if G == 1 and direct and isinstance(be, HipLocal):
+            # a single rank owns every key: no exchange with itself, the
+            # local fused lookup (same association order, same EV updates)
+            from .embedding_ops import SparseTensor, embedding_lookup_sparse_multi
+            ind = torch.stack([torch.arange(nnz, device=dev),
+                               torch.zeros(nnz, dtype=torch.int64, device=dev)], 1)
+            sps = [SparseTensor(ind, ids[t], (self.batch, 1)) for t in range(T)]
+            self.last_stats = {"sent_keys": 0, "recv_keys": 0, "direct": True, "local": True}
+            self._saved = None
+            with torch.no_grad():
+                return embedding_lookup_sparse_multi(self.evs, sps, combiner=combiner)
         if direct:
             uniq, idx, U = vals, None, None
         else:

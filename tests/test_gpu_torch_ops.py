@@ -1,0 +1,114 @@
+"""The registered op layer (torch.ops.deeprec.*) on the GPU: results equal the
+package functions / the oracle, torch.library.opcheck passes (schema, fake
+tensor and autograd registration), and a function built from the ops traces
+into an FX graph of deeprec ops (make_fx, fake tensors)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def dr():
+    import deeprec_amd
+    deeprec_amd.load()
+    deeprec_amd.set_validate(True)
+    return deeprec_amd
+
+
+def T(x, dtype=None):
+    return torch.as_tensor(np.asarray(x), device=DEV, dtype=dtype)
+
+
+def H(t):
+    return t.detach().cpu().numpy()
+
+
+def _sparse(rng, B, M, vocab):
+    lens = rng.integers(1, M + 1, B)
+    r = np.repeat(np.arange(B), lens)
+    c = np.concatenate([np.arange(n) for n in lens])
+    return np.stack([r, c], 1).astype(np.int64), rng.integers(0, vocab, r.shape[0]).astype(np.int64)
+
+
+@pytest.mark.parametrize("comb", ["sum", "mean", "sqrtn"])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_embedding_lookup_sparse_op(dr, orc, comb, weighted):
+    rng = np.random.default_rng(7)
+    B, D, R = 90, 16, 60
+    ind, vals = _sparse(rng, B, 5, R)
+    table = rng.standard_normal((R, D)).astype(np.float32)
+    w = rng.uniform(0.2, 2, vals.shape[0]).astype(np.float32) if weighted else None
+    t = T(table).requires_grad_(True)
+    out = torch.ops.deeprec.embedding_lookup_sparse(t, T(ind), T(vals), B,
+                                                    None if w is None else T(w), comb, 2.5)
+    ref = orc.embedding_lookup_sparse(table, ind, vals, B, weights=w, combiner=comb, max_norm=2.5)
+    np.testing.assert_allclose(H(out), ref, rtol=1e-5, atol=1e-6)
+    top = rng.standard_normal((B, D)).astype(np.float32)
+    out.backward(T(top))
+    uids, gu = orc.embedding_lookup_sparse_grad(table, ind, vals, B, top, w, comb, 2.5)
+    np.testing.assert_allclose(H(t.grad)[uids], gu, rtol=1e-5, atol=1e-6)
+
+
+def test_kv_ops_match_package(dr, orc):
+    rng = np.random.default_rng(8)
+    D = 8
+    ev = dr.EmbeddingVariable("tops_kv", D, 0.25)
+    keys = np.arange(0, 400, 3, dtype=np.int64)
+    vals = rng.standard_normal((keys.shape[0], D)).astype(np.float32)
+    torch.ops.deeprec.kv_resource_insert(ev.handle.value, T(keys), T(vals))
+    q = np.concatenate([keys[:50], np.array([1, 2, 1000], np.int64)])
+    got = torch.ops.deeprec.kv_resource_gather(ev.handle.value, T(q), D)
+    np.testing.assert_array_equal(H(got), H(ev.sparse_read(T(q))))
+    acc = ev.slot("Adagrad", 0.1)
+    oev = orc.EV(D, 0.25)
+    oev.insert(keys, vals)
+    oev.gather(np.array([1, 2, 1000], np.int64))
+    oacc = oev.create_slot(1, np.full(D, 0.1, np.float32))
+    uq = np.unique(q)
+    gq = rng.standard_normal((uq.shape[0], D)).astype(np.float32)
+    torch.ops.deeprec.kv_resource_sparse_apply_adagrad(ev.handle.value, acc.handle.value, 0.1,
+                                                       T(gq), T(uq), 3)
+    oev.apply_adagrad(oacc, np.float32(0.1), gq, uq, 3)
+    np.testing.assert_allclose(H(ev.sparse_read(T(uq))), oev.gather(uq), rtol=1e-5, atol=1e-7)
+
+
+def test_opcheck(dr):
+    from torch.library import opcheck
+    rng = np.random.default_rng(9)
+    utils = ("test_schema", "test_faketensor", "test_autograd_registration")
+    data = T(rng.standard_normal((12, 6)).astype(np.float32)).requires_grad_(True)
+    idx = T(np.array([0, 3, 3, 7, 11, 2], np.int32))
+    seg = T(np.array([0, 0, 1, 1, 3, 3], np.int32))
+    opcheck(torch.ops.deeprec.sparse_segment_reduce.default, (data, idx, seg, 4, "mean"),
+            test_utils=utils)
+    opcheck(torch.ops.deeprec.unsorted_segment_sum.default, (data, T(np.arange(12) % 5, torch.int32), 5),
+            test_utils=utils)
+    opcheck(torch.ops.deeprec.resource_gather.default, (data, T(np.array([1, 5, 5, 0]))),
+            test_utils=utils)
+    emb = T(rng.standard_normal((5, 4, 8)).astype(np.float32)).requires_grad_(True)
+    opcheck(torch.ops.deeprec.fm_second_order.default, (emb,), test_utils=utils)
+    opcheck(torch.ops.deeprec.dot_interaction.default, (emb,), test_utils=utils)
+    ind, vals = _sparse(rng, 10, 4, 12)
+    opcheck(torch.ops.deeprec.embedding_lookup_sparse.default,
+            (data, T(ind), T(vals), 10, None, "sqrtn", -1.0), test_utils=utils)
+
+
+def test_trace_to_fx_graph(dr):
+    from torch.fx.experimental.proxy_tensor import make_fx
+    rng = np.random.default_rng(10)
+    ind, vals = _sparse(rng, 16, 3, 40)
+    table = T(rng.standard_normal((40, 8)).astype(np.float32))
+
+    def model(tab, ind, vals):
+        e = torch.ops.deeprec.embedding_lookup_sparse(tab, ind, vals, 16, None, "mean", -1.0)
+        x = torch.stack([e, e * 2.0, e + 1.0], 1)
+        return torch.ops.deeprec.dot_interaction(x)
+
+    gm = make_fx(model, tracing_mode="fake")(table, T(ind), T(vals))
+    targets = [str(n.target) for n in gm.graph.nodes if n.op == "call_function"]
+    assert "deeprec.embedding_lookup_sparse.default" in targets
+    assert "deeprec.dot_interaction.default" in targets
+    np.testing.assert_array_equal(H(gm(table, T(ind), T(vals))), H(model(table, T(ind), T(vals))))
