@@ -70,6 +70,13 @@ struct EvShared {
   hipEvent_t copy_ev = nullptr;
   int64_t* pinned_top = nullptr;
   int64_t removed = 0;  // keys removed by dr_ev_shrink (rows are not recycled)
+  // value dtype: 1 = float, 2 = double (a double row is stored as 2 * dim
+  // float words and moved bitwise; `dim` counts float words)
+  int value_words = 1;
+  // use_locking applies (dr_ev_lock_updates): exclusive updates across
+  // host threads and streams
+  std::mutex update_mu;
+  hipEvent_t update_ev = nullptr;
 };
 
 }  // namespace dr
@@ -987,6 +994,7 @@ static void free_shared(EvShared* s) {
   (void)hipFree(s->bloom);
   (void)hipFree(s->seeds);
   if (s->copy_ev) (void)hipEventDestroy(s->copy_ev);
+  if (s->update_ev) (void)hipEventDestroy(s->update_ev);
   if (s->pinned_top) (void)hipHostFree(s->pinned_top);
   delete s;
 }
@@ -1206,6 +1214,9 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
   for (int t = 0; t < T; ++t) {
     DR_REQUIRE(vars[t] && vars[t]->col == 0, DR_INVALID_ARGUMENT,
                "table %d: var must be a primary EV", t);
+    DR_REQUIRE(vars[t]->sh->value_words == 1, DR_INVALID_ARGUMENT,
+               "table %d: the KvResourceSparseApply* kernels are registered for float values "
+               "only (training_ali_ops.cc)", t);
     if (n_host[t] > 0) {
       int rc = reserve(vars[t]->sh, n_host[t], st);
       if (rc) return rc;
@@ -1582,6 +1593,8 @@ static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t 
   for (int t = 0; t < T; ++t) {
     const EvShared* s = evs[t]->sh;
     DR_REQUIRE(s->dim == dim, DR_INVALID_ARGUMENT, "tables must share dim");
+    DR_REQUIRE(s->value_words == 1, DR_INVALID_ARGUMENT,
+               "table %d: pooled lookups are fp32 (double EVs: dr_ev_gather)", t);
     DR_REQUIRE(s->filter_freq == 0 && s->k_hash == 0, DR_INVALID_ARGUMENT,
                "table %d: the fused lookup is for filter-free EVs", t);
     DR_REQUIRE(((uintptr_t)s->pools[evs[t]->col] & 15) == 0, DR_INVALID_ARGUMENT,
@@ -1674,10 +1687,13 @@ int dr_ev_create(const dr_ev_config* cfg, const float* default_row_host, dr_ev**
   DR_REQUIRE(cfg && out && default_row_host, DR_INVALID_ARGUMENT, "null argument");
   DR_REQUIRE(cfg->dim > 0, DR_INVALID_ARGUMENT, "dim must be > 0");
   DR_REQUIRE(cfg->steps_to_live >= 0, DR_INVALID_ARGUMENT, "steps_to_live must >= 0");
+  DR_REQUIRE(cfg->value_bits == 0 || cfg->value_bits == 32 || cfg->value_bits == 64,
+             DR_INVALID_ARGUMENT, "value_bits must be 32 (float) or 64 (double)");
   EvShared* s = new (std::nothrow) EvShared();
   DR_REQUIRE(s, DR_RESOURCE_EXHAUSTED, "host allocation failed");
   (void)hipGetDevice(&s->device);
-  s->dim = cfg->dim;
+  s->value_words = cfg->value_bits == 64 ? 2 : 1;
+  s->dim = cfg->dim * s->value_words;
   s->filter_freq = cfg->filter_freq < 0 ? 0 : cfg->filter_freq;
   s->steps_to_live = cfg->steps_to_live;
   const int64_t capacity = cfg->capacity > 0 ? cfg->capacity : 1024;
@@ -1720,6 +1736,7 @@ int dr_ev_create(const dr_ev_config* cfg, const float* default_row_host, dr_ev**
                      hipMemcpyHostToDevice));
   }
   DR_TRY(hipEventCreateWithFlags(&s->copy_ev, hipEventDisableTiming));
+  DR_TRY(hipEventCreateWithFlags(&s->update_ev, hipEventDisableTiming));
   DR_TRY(hipHostMalloc(&s->pinned_top, sizeof(int64_t)));
 #undef DR_TRY
   rc = alloc_pool(s, 0, default_row_host);
@@ -1769,7 +1786,49 @@ int dr_ev_release(dr_ev* ev) {
   return DR_OK;
 }
 
-int64_t dr_ev_dim(dr_ev* ev) { return ev ? ev->sh->dim : -1; }
+int64_t dr_ev_dim(dr_ev* ev) { return ev ? ev->sh->dim / ev->sh->value_words : -1; }
+
+int dr_ev_value_bits(dr_ev* ev) { return ev ? 32 * ev->sh->value_words : -1; }
+
+// MaybeLockEmbeddingVariableInputMutexesInOrder (training_ali_op_helpers.h:
+// 85-118) for stream-ordered updates: the host mutexes are taken in address
+// order, and the stream waits for the previous locked update of each EV.
+int dr_ev_lock_updates(dr_ev* const* vars, int n, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(vars && n >= 0, DR_INVALID_ARGUMENT, "bad argument");
+  std::vector<EvShared*> v;
+  for (int i = 0; i < n; ++i)
+    if (vars[i]) v.push_back(vars[i]->sh);
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+  for (EvShared* s : v) s->update_mu.lock();
+  for (EvShared* s : v) {
+    hipError_t e = hipStreamWaitEvent(S(stream), s->update_ev, 0);
+    if (e != hipSuccess) {
+      for (EvShared* u : v) u->update_mu.unlock();
+      set_error("hipStreamWaitEvent: %s", hipGetErrorString(e));
+      return DR_INTERNAL;
+    }
+  }
+  return DR_OK;
+}
+
+int dr_ev_unlock_updates(dr_ev* const* vars, int n, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(vars && n >= 0, DR_INVALID_ARGUMENT, "bad argument");
+  std::vector<EvShared*> v;
+  for (int i = 0; i < n; ++i)
+    if (vars[i]) v.push_back(vars[i]->sh);
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+  int rc = DR_OK;
+  for (EvShared* s : v) {
+    if (hipEventRecord(s->update_ev, S(stream)) != hipSuccess) rc = DR_INTERNAL;
+    s->update_mu.unlock();
+  }
+  if (rc) set_error("dr_ev_unlock_updates: hipEventRecord failed");
+  return rc;
+}
 
 const float* dr_ev_pool(dr_ev* ev) { return ev ? ev->sh->pools[ev->col] : nullptr; }
 
@@ -1790,6 +1849,8 @@ int dr_ev_shrink(dr_ev* ev, int64_t global_step, float l2_weight_threshold,
   const int mode = l2_weight_threshold != -1.0f ? 1 : (s->steps_to_live > 0 ? 2 : 0);
   if (removed_host) *removed_host = 0;
   if (mode == 0) return DR_OK;
+  DR_REQUIRE(mode == 2 || s->value_words == 1, DR_INVALID_ARGUMENT,
+             "l2-weight shrink is for float EVs");
   std::lock_guard<std::mutex> g(s->mu);
   const int64_t n = s->cap + 1;
   uint8_t* keep = nullptr;
@@ -1919,7 +1980,8 @@ int dr_ev_gather_tagged(dr_ev* const* evs, int num_tables, const int32_t* tags,
   memset(&pg, 0, sizeof(pg));
   const int64_t dim = evs[0]->sh->dim;
   for (int t = 0; t < num_tables; ++t) {
-    DR_REQUIRE(evs[t]->sh->dim == dim, DR_INVALID_ARGUMENT, "tables must share dim");
+    DR_REQUIRE(evs[t]->sh->dim == dim && evs[t]->sh->value_words == 1, DR_INVALID_ARGUMENT,
+               "tables must be float EVs sharing dim");
     pg.pool[t] = evs[t]->sh->pools[evs[t]->col];
     pg.dflt[t] = evs[t]->sh->defaults[evs[t]->col];
   }
@@ -2430,8 +2492,8 @@ int dr_xgmi_serve(const dr_xgmi_peers* peers, dr_ev* const* evs, int num_tables,
   for (int t = 0; t < num_tables; ++t) {
     const EvShared* s = evs[t]->sh;
     DR_REQUIRE(s->dim == dim, DR_INVALID_ARGUMENT, "tables must share dim");
-    DR_REQUIRE(s->filter_freq == 0 && s->k_hash == 0, DR_INVALID_ARGUMENT,
-               "table %d: xgmi serve is for filter-free EVs", t);
+    DR_REQUIRE(s->filter_freq == 0 && s->k_hash == 0 && s->value_words == 1,
+               DR_INVALID_ARGUMENT, "table %d: xgmi serve is for filter-free fp32 EVs", t);
     ra.e[t] = make_desc(evs[t]);
     wa.pool[t] = s->pools[evs[t]->col];
     wa.dflt[t] = s->defaults[evs[t]->col];

@@ -61,7 +61,7 @@ class DrEvConfig(C.Structure):
         ("dim", C.c_int64), ("capacity", C.c_int64), ("steps_to_live", C.c_int64),
         ("filter_freq", C.c_int64), ("max_element_size", C.c_int64),
         ("false_positive_probability", C.c_float), ("counter_bits", C.c_int32),
-        ("layout", C.c_int32),
+        ("layout", C.c_int32), ("value_bits", C.c_int32),
     ]
 
 
@@ -117,6 +117,15 @@ SIGNATURES = {
     "dr_ev_release": (_I32, [_P]),
     "dr_ev_size": (_I32, [_P, _P, _P]),
     "dr_ev_dim": (_I64, [_P]),
+    "dr_ev_value_bits": (_I32, [_P]),
+    "dr_ev_lock_updates": (_I32, [_P, _I32, _P]),
+    "dr_ev_unlock_updates": (_I32, [_P, _I32, _P]),
+    "dr_ev_gather_i32_workspace_size": (_SZ, [_I64]),
+    "dr_ev_gather_i32": (_I32, [_P, _P, _I64, _P, _P, _P, _P, _SZ, _P]),
+    "dr_ev_insert_i32": (_I32, [_P, _P, _I64, _P, _P, _P, _I64, _I64, _P]),
+    "dr_ev_export_i32": (_I32, [_P, _P, _P, _P, _P, _I64, _P, _P]),
+    "dr_unique_i32_workspace_size": (_SZ, [_I64]),
+    "dr_unique_i32": (_I32, [_P, _I64, _P, _P, _P, _P, _P, _SZ, _P]),
     "dr_ev_shrink": (_I32, [_P, _I64, _F32, _P, _P]),
     "dr_ev_reserve": (_I32, [_P, _I64, _P]),
     "dr_ev_resolve_workspace_size": (_SZ, [_I64]),

@@ -76,6 +76,12 @@ class _Feature(object):
     sp_ids.indices (read in place, stride 2: no per-step conversion)."""
 
     def __init__(self, params, values, seg, batch, weights, combiner, max_norm, onehot=False):
+        if getattr(params, "value_dtype", torch.float32) != torch.float32:
+            # the pooled lookups are fp32 kernels, as the reference's fused
+            # and GPU EV lookups are (double EVs: sparse_read)
+            raise _lib.DeepRecError(_lib.INVALID_ARGUMENT,
+                                    "embedding lookups pool float32 EVs; %s is %s"
+                                    % (getattr(params, "name", params), params.value_dtype))
         self.params = params
         # one id per row (a valid [B, 1] SparseTensor with nnz == B): bag b is
         # nnz b, so the pool kernel needs no bag offsets (DR_POOL_ONEHOT).

@@ -49,16 +49,20 @@ class EmbeddingVariableOption(object):
         self.filter_option = filter_option
 
 
-def _default_row(initializer, dim, device):
+def _default_row(initializer, dim, device, dtype=torch.float32):
     """EV default_value_ (InitializeKvVariableOp input 2, a [dim] tensor)."""
     if initializer is None:
         initializer = 0.0
     if callable(initializer):
         v = initializer((dim,))
-        v = torch.as_tensor(v, dtype=torch.float32).reshape(dim)
+        v = torch.as_tensor(v, dtype=dtype).reshape(dim)
     else:
-        v = torch.full((dim,), float(initializer), dtype=torch.float32)
+        v = torch.full((dim,), float(initializer), dtype=dtype)
     return v.cpu().contiguous()
+
+
+_KEY_DTYPES = (torch.int64, torch.int32)
+_VALUE_DTYPES = (torch.float32, torch.float64)
 
 
 class IndexedSlices(object):
@@ -82,10 +86,15 @@ class EmbeddingVariable(object):
 
     def __init__(self, name, embedding_dim, initializer=None, steps_to_live=0, ev_option=None,
                  capacity=1 << 16, device=None, _primary=None, _slot_index=0,
-                 l2_weight_threshold=-1.0):
+                 l2_weight_threshold=-1.0, key_dtype=torch.int64, value_dtype=torch.float32):
         _lib.require_gpu()
+        if key_dtype not in _KEY_DTYPES or value_dtype not in _VALUE_DTYPES:
+            raise TypeError("EmbeddingVariable keys are int32 / int64 and values float32 / "
+                            "float64 (the reference's KvResourceGather registrations)")
         self.name = name
         self.dim = int(embedding_dim)
+        self.key_dtype = key_dtype
+        self.value_dtype = value_dtype if _primary is None else _primary.value_dtype
         self.device = torch.device(device) if device is not None else \
             torch.device("cuda", torch.cuda.current_device())
         self.initializer = initializer
@@ -101,7 +110,7 @@ class EmbeddingVariable(object):
         self.steps_to_live = int(steps_to_live or 0)
         # EmbeddingConfig::l2_weight_threshold (embedding_config.h:17,28): -1 = off
         self.l2_weight_threshold = float(l2_weight_threshold)
-        default = _default_row(initializer, self.dim, self.device)
+        default = _default_row(initializer, self.dim, self.device, self.value_dtype)
         self._default_host = default
         h = C.c_void_p()
         with torch.cuda.device(self.device):
@@ -116,6 +125,7 @@ class EmbeddingVariable(object):
                     getattr(f, "false_positive_probability", -1.0))
                 cfg.counter_bits = int(getattr(f, "counter_bits", 64) or 64)
                 cfg.layout = 1 if (self.filter_freq or self.steps_to_live) else 0
+                cfg.value_bits = 64 if self.value_dtype == torch.float64 else 32
                 check(lib().dr_ev_create(C.byref(cfg), default.data_ptr(), C.byref(h)))
             else:
                 check(lib().dr_ev_create_slot(_primary._h, _slot_index, default.data_ptr(),
@@ -147,7 +157,7 @@ class EmbeddingVariable(object):
             self._next_slot += 1
             self._slots[name] = EmbeddingVariable(self.name + "/" + name, self.dim, initializer,
                                                   device=self.device, _primary=self,
-                                                  _slot_index=idx)
+                                                  _slot_index=idx, key_dtype=self.key_dtype)
         return self._slots[name]
 
     def get_shape(self):
@@ -164,27 +174,35 @@ class EmbeddingVariable(object):
     # -- ops -----------------------------------------------------------------
     def _defaults_for(self, n, ev_init_value):
         if ev_init_value is not None:
-            return torch.as_tensor(ev_init_value, dtype=torch.float32,
+            return torch.as_tensor(ev_init_value, dtype=self.value_dtype,
                                    device=self.device).expand(n, self.dim).contiguous()
         if callable(self.initializer):
             v = self.initializer((n, self.dim))
-            return torch.as_tensor(v, dtype=torch.float32, device=self.device).reshape(
+            return torch.as_tensor(v, dtype=self.value_dtype, device=self.device).reshape(
                 n, self.dim).contiguous()
         return None
 
     def sparse_read(self, indices, counts=None, ev_init_value=None, name=None):
-        """KvResourceGather / KvResourceGatherV1 (kv_variable_ops.py:644-664)."""
-        ids = indices.reshape(-1).to(torch.int64).contiguous()
+        """KvResourceGather / KvResourceGatherV1 (kv_variable_ops.py:644-664),
+        int32 or int64 ids, float32 or float64 rows per the EV's dtypes."""
+        i32 = indices.dtype == torch.int32
+        ids = indices.reshape(-1).to(torch.int32 if i32 else torch.int64).contiguous()
         n = ids.numel()
-        out = torch.empty((n, self.dim), dtype=torch.float32, device=self.device)
+        out = torch.empty((n, self.dim), dtype=self.value_dtype, device=self.device)
         if n == 0:
             return out.reshape(tuple(indices.shape) + (self.dim,))
         dflt = self._defaults_for(n, ev_init_value)
         cnt = None if counts is None else counts.reshape(-1).to(torch.int32).contiguous()
-        wsb = lib().dr_ev_gather_workspace_size(n)
-        ws = workspace(wsb, self.device)
-        check(lib().dr_ev_gather(self._h, ptr(ids), n, ptr(dflt), ptr(cnt), ptr(out), ptr(ws), wsb,
-                                 stream_handle(self.device)))
+        if i32:
+            wsb = lib().dr_ev_gather_i32_workspace_size(n)
+            ws = workspace(wsb, self.device)
+            check(lib().dr_ev_gather_i32(self._h, ptr(ids), n, ptr(dflt), ptr(cnt), ptr(out),
+                                         ptr(ws), wsb, stream_handle(self.device)))
+        else:
+            wsb = lib().dr_ev_gather_workspace_size(n)
+            ws = workspace(wsb, self.device)
+            check(lib().dr_ev_gather(self._h, ptr(ids), n, ptr(dflt), ptr(cnt), ptr(out), ptr(ws),
+                                     wsb, stream_handle(self.device)))
         from .ops import _post
         _post(self.device)
         return out.reshape(tuple(indices.shape) + (self.dim,))
@@ -210,14 +228,17 @@ class EmbeddingVariable(object):
         return self._import(keys, values, versions, freqs, partition_id, partition_num)
 
     def _import(self, keys, values, versions, freqs, pid, pnum):
-        k = keys.reshape(-1).to(device=self.device, dtype=torch.int64).contiguous()
+        i32 = keys.dtype == torch.int32
+        k = keys.reshape(-1).to(device=self.device,
+                                dtype=torch.int32 if i32 else torch.int64).contiguous()
         v = values.reshape(k.numel(), self.dim).to(device=self.device,
-                                                   dtype=torch.float32).contiguous()
+                                                   dtype=self.value_dtype).contiguous()
         ver = None if versions is None else versions.to(device=self.device,
                                                         dtype=torch.int64).contiguous()
         fr = None if freqs is None else freqs.to(device=self.device, dtype=torch.int64).contiguous()
-        check(lib().dr_ev_insert(self._h, ptr(k), k.numel(), ptr(v), ptr(ver), ptr(fr), pid, pnum,
-                                 stream_handle(self.device)))
+        fn = lib().dr_ev_insert_i32 if i32 else lib().dr_ev_insert
+        check(fn(self._h, ptr(k), k.numel(), ptr(v), ptr(ver), ptr(fr), pid, pnum,
+                 stream_handle(self.device)))
 
     def insert_synthetic(self, key_begin, n, seed, key_stride=1):
         """Insert keys key_begin + i*key_stride, i < n, rows synth(seed, key, col)."""
@@ -231,17 +252,18 @@ class EmbeddingVariable(object):
         return torch.tensor([n.value, self.dim], dtype=torch.int64)
 
     def export(self):
-        """KvResourceExport -> (keys, values, versions, freqs), keys ascending."""
+        """KvResourceExport -> (keys, values, versions, freqs), keys ascending
+        (keys in the EV's key dtype, values in its value dtype)."""
         m = C.c_int64(0)
         st = stream_handle(self.device)
         check(lib().dr_ev_export(self._h, None, None, None, None, 0, C.byref(m), st))
         M = m.value
-        keys = torch.empty(M, dtype=torch.int64, device=self.device)
-        vals = torch.empty((M, self.dim), dtype=torch.float32, device=self.device)
+        keys = torch.empty(M, dtype=self.key_dtype, device=self.device)
+        vals = torch.empty((M, self.dim), dtype=self.value_dtype, device=self.device)
         vers = torch.empty(M, dtype=torch.int64, device=self.device)
         frqs = torch.empty(M, dtype=torch.int64, device=self.device)
-        check(lib().dr_ev_export(self._h, ptr(keys), ptr(vals), ptr(vers), ptr(frqs), M,
-                                 C.byref(m), st))
+        fn = lib().dr_ev_export_i32 if self.key_dtype == torch.int32 else lib().dr_ev_export
+        check(fn(self._h, ptr(keys), ptr(vals), ptr(vers), ptr(frqs), M, C.byref(m), st))
         n = m.value
         if self.steps_to_live == 0:
             vers = vers[:0]
@@ -280,7 +302,7 @@ _EV_REGISTRY = {}
 
 def get_embedding_variable(name, embedding_dim, key_dtype=torch.int64, initializer=None,
                            steps_to_live=0, ev_option=None, capacity=1 << 16, device=None,
-                           partitioner=None, l2_weight_threshold=-1.0):
+                           partitioner=None, l2_weight_threshold=-1.0, value_dtype=torch.float32):
     """tf.get_embedding_variable (variable_scope.py:2142-2197).
 
     With `partitioner=n` (fixed_size_partitioner(num_shards=n)) returns a list
@@ -289,12 +311,14 @@ def get_embedding_variable(name, embedding_dim, key_dtype=torch.int64, initializ
     if partitioner is not None and int(partitioner) > 1:
         return [get_embedding_variable("%s/part_%d" % (name, p), embedding_dim, key_dtype,
                                        initializer, steps_to_live, ev_option, capacity, device,
-                                       l2_weight_threshold=l2_weight_threshold)
+                                       l2_weight_threshold=l2_weight_threshold,
+                                       value_dtype=value_dtype)
                 for p in range(int(partitioner))]
     if name in _EV_REGISTRY:
         return _EV_REGISTRY[name]
     ev = EmbeddingVariable(name, embedding_dim, initializer, steps_to_live, ev_option, capacity,
-                           device, l2_weight_threshold=l2_weight_threshold)
+                           device, l2_weight_threshold=l2_weight_threshold, key_dtype=key_dtype,
+                           value_dtype=value_dtype)
     _EV_REGISTRY[name] = ev
     return ev
 

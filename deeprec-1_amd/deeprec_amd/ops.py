@@ -57,16 +57,23 @@ def unique_device(x, with_counts=False):
     Returns (y [n], idx [n] int32, counts [n] int32 or None, num_unique int64[1]);
     only y[:num_unique] / counts[:num_unique] are meaningful."""
     dev = _dev(x)
-    x = _c(x.reshape(-1), torch.int64)
+    i32 = x.dtype == torch.int32               # the int32 registration: y stays int32
+    x = _c(x.reshape(-1), torch.int32 if i32 else torch.int64)
     n = x.numel()
-    y = torch.empty(n, dtype=torch.int64, device=dev)
+    y = torch.empty(n, dtype=x.dtype, device=dev)
     idx = torch.empty(n, dtype=torch.int32, device=dev)
     cnt = torch.empty(n, dtype=torch.int32, device=dev) if with_counts else None
     u = torch.empty(1, dtype=torch.int64, device=dev)
-    wsb = lib().dr_unique_workspace_size(n)
-    ws = workspace(wsb, dev)
-    check(lib().dr_unique(ptr(x), n, ptr(y), ptr(idx), ptr(cnt), ptr(u), ptr(ws), wsb,
-                          stream_handle(dev)))
+    if i32:
+        wsb = lib().dr_unique_i32_workspace_size(n)
+        ws = workspace(wsb, dev)
+        check(lib().dr_unique_i32(ptr(x), n, ptr(y), ptr(idx), ptr(cnt), ptr(u), ptr(ws), wsb,
+                                  stream_handle(dev)))
+    else:
+        wsb = lib().dr_unique_workspace_size(n)
+        ws = workspace(wsb, dev)
+        check(lib().dr_unique(ptr(x), n, ptr(y), ptr(idx), ptr(cnt), ptr(u), ptr(ws), wsb,
+                              stream_handle(dev)))
     _post(dev)
     return y, idx, cnt, u
 

@@ -54,7 +54,8 @@ def unique_with_counts(x: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
 @unique_with_counts.register_fake
 def _(x):
     n = x.numel()
-    return (x.new_empty(n, dtype=torch.int64), x.new_empty(n, dtype=torch.int32),
+    kt = torch.int32 if x.dtype == torch.int32 else torch.int64
+    return (x.new_empty(n, dtype=kt), x.new_empty(n, dtype=torch.int32),
             x.new_empty(n, dtype=torch.int32), x.new_empty(1, dtype=torch.int64))
 
 

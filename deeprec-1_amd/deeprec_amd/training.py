@@ -60,11 +60,36 @@ def _rounds(slices):
     return out
 
 
+class _Locked(object):
+    """use_locking=True (optimizer.py Optimizer(use_locking)): the EV applies
+    take each variable's exclusive update lock, as the reference's
+    MaybeLockEmbeddingVariableInputMutexesInOrder does (training_ali_ops.cc:
+    104).  dr_ev_lock_updates serialises host threads on the variables'
+    mutexes (in address order, like the reference) and orders this stream
+    after the last locked apply issued on any other stream."""
+
+    def __init__(self, enabled, handles, stream):
+        import ctypes as C
+        self.enabled, self.stream = enabled, stream
+        self.arr = (C.c_void_p * len(handles))(*handles)
+        self.n = len(handles)
+
+    def __enter__(self):
+        if self.enabled:
+            check(lib().dr_ev_lock_updates(self.arr, self.n, self.stream))
+
+    def __exit__(self, *exc):
+        if self.enabled:
+            check(lib().dr_ev_unlock_updates(self.arr, self.n, self.stream))
+        return False
+
+
 class _Optimizer(object):
     _opt = None   # DR_OPT_* code of the EV apply kernel
 
-    def __init__(self, learning_rate):
+    def __init__(self, learning_rate, use_locking=False):
         self.lr = float(learning_rate)
+        self.use_locking = bool(use_locking)
 
     # How repeated indices reach the EV apply kernel: summed first (the
     # default _resource_apply_sparse_duplicate_indices, optimizer.py:1060-1083)
@@ -118,12 +143,14 @@ class _Optimizer(object):
             P = C.c_void_p * T
             s1 = P(*[a.handle.value if a is not None else None for a, _ in slots])
             s2 = P(*[b.handle.value if b is not None else None for _, b in slots])
-            check(lib().dr_ev_apply_grouped(
-                self._opt, P(*[var.handle.value for var, _ in grp]), s1, s2, T,
-                P(*[v.data_ptr() for v in vals]), P(*[i.data_ptr() for i in idxs]),
-                (C.c_int64 * T)(*[i.numel() for i in idxs]),
-                P(*[ptr(sl.num_valid) for _, sl in grp]), self.lr, b1p, b2p, b1, b2, eps, gs,
-                stream_handle(dev)))
+            st = stream_handle(dev)
+            with _Locked(self.use_locking, [var.handle.value for var, _ in grp], st):
+                check(lib().dr_ev_apply_grouped(
+                    self._opt, P(*[var.handle.value for var, _ in grp]), s1, s2, T,
+                    P(*[v.data_ptr() for v in vals]), P(*[i.data_ptr() for i in idxs]),
+                    (C.c_int64 * T)(*[i.numel() for i in idxs]),
+                    P(*[ptr(sl.num_valid) for _, sl in grp]), self.lr, b1p, b2p, b1, b2, eps, gs,
+                    st))
             ops._post(dev)
 
     def _finish(self):
@@ -149,8 +176,8 @@ class AdagradOptimizer(_Optimizer):
 
     _opt = 1
 
-    def __init__(self, learning_rate, initial_accumulator_value=0.1):
-        super().__init__(learning_rate)
+    def __init__(self, learning_rate, initial_accumulator_value=0.1, use_locking=False):
+        super().__init__(learning_rate, use_locking)
         self.init_acc = float(initial_accumulator_value)
         self._dense_acc = {}
 
@@ -170,9 +197,11 @@ class AdamOptimizer(_Optimizer):
 
     _opt = 2
 
-    def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8):
-        super().__init__(learning_rate)
+    def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8,
+                 use_locking=False):
+        super().__init__(learning_rate, use_locking)
         self.beta1, self.beta2, self.eps = float(beta1), float(beta2), float(epsilon)
+        self._dense_mv = {}
         self.b1p = torch.tensor(self.beta1, dtype=torch.float32).item()
         self.b2p = torch.tensor(self.beta2, dtype=torch.float32).item()
 
@@ -188,7 +217,18 @@ class AdamOptimizer(_Optimizer):
         self.b2p = (f32(self.b2p) * f32(self.beta2)).item()
 
     def _dense_update(self, var, idx, g):
-        raise NotImplementedError("dense-table Adam: use an EmbeddingVariable")
+        """_apply_sparse_shared (adam.py:183-207) on a dense table: m and v
+        decay on every row, the deduplicated gradient is scatter-added, and
+        every row of var moves by lr_t * m / (sqrt(v) + eps) (TF's non-lazy
+        sparse Adam), lr_t = lr * sqrt(1 - beta2^t) / (1 - beta1^t)."""
+        w = var.weight
+        m, v = self._dense_mv.setdefault(id(var), (torch.zeros_like(w), torch.zeros_like(w)))
+        f32 = lambda x: torch.tensor(x, dtype=torch.float32)
+        lr = (f32(self.lr) * torch.sqrt(1 - f32(self.b2p)) / (1 - f32(self.b1p))).item()
+        with torch.no_grad():
+            m.mul_(self.beta1).index_add_(0, idx, g * (1 - self.beta1))
+            v.mul_(self.beta2).index_add_(0, idx, (g * g) * (1 - self.beta2))
+            w.sub_(lr * m / (torch.sqrt(v) + self.eps))
 
 
 class FtrlOptimizer(_Optimizer):
@@ -201,8 +241,8 @@ class FtrlOptimizer(_Optimizer):
 
     def __init__(self, learning_rate, learning_rate_power=-0.5, initial_accumulator_value=0.1,
                  l1_regularization_strength=0.0, l2_regularization_strength=0.0,
-                 l2_shrinkage_regularization_strength=0.0):
-        super().__init__(learning_rate)
+                 l2_shrinkage_regularization_strength=0.0, use_locking=False):
+        super().__init__(learning_rate, use_locking)
         self.lr_power = float(learning_rate_power)
         self.init_acc = float(initial_accumulator_value)
         self.l1 = float(l1_regularization_strength)
@@ -225,12 +265,15 @@ class FtrlOptimizer(_Optimizer):
             idxs = [sl.indices.contiguous() for _, sl in grp]
             slots = [self._slots(var) for var, _ in grp]
             P = C.c_void_p * T
-            check(lib().dr_ev_apply_ftrl_grouped(
-                P(*[var.handle.value for var, _ in grp]), P(*[a.handle.value for a, _ in slots]),
-                P(*[b.handle.value for _, b in slots]), T, P(*[v.data_ptr() for v in vals]),
-                P(*[i.data_ptr() for i in idxs]), (C.c_int64 * T)(*[i.numel() for i in idxs]),
-                P(*[ptr(sl.num_valid) for _, sl in grp]), self.lr, self.l1, self.l2,
-                self.lr_power, self.l2_shrinkage, gs, stream_handle(dev)))
+            st = stream_handle(dev)
+            with _Locked(self.use_locking, [var.handle.value for var, _ in grp], st):
+                check(lib().dr_ev_apply_ftrl_grouped(
+                    P(*[var.handle.value for var, _ in grp]),
+                    P(*[a.handle.value for a, _ in slots]), P(*[b.handle.value for _, b in slots]),
+                    T, P(*[v.data_ptr() for v in vals]), P(*[i.data_ptr() for i in idxs]),
+                    (C.c_int64 * T)(*[i.numel() for i in idxs]),
+                    P(*[ptr(sl.num_valid) for _, sl in grp]), self.lr, self.l1, self.l2,
+                    self.lr_power, self.l2_shrinkage, gs, st))
             ops._post(dev)
 
     def dense_step(self, params):
@@ -254,4 +297,21 @@ class FtrlOptimizer(_Optimizer):
                 acc.add_(g * g)
 
     def _dense_update(self, var, idx, g):
-        raise NotImplementedError("dense-table FTRL: use an EmbeddingVariable")
+        """ResourceSparseApplyFtrl[V2] (training_ops.cc:2587-2614) on the rows
+        idx of a dense table (indices already distinct after _dedup)."""
+        w = var.weight
+        acc_t, lin_t = self._dense.setdefault(
+            id(var), (torch.full_like(w, self.init_acc), torch.zeros_like(w)))
+        with torch.no_grad():
+            x, acc, lin = w[idx], acc_t[idx], lin_t[idx]
+            gs = g + 2.0 * self.l2_shrinkage * x if self.l2_shrinkage > 0 else g
+            na = acc + g * g
+            if self.lr_power == -0.5:
+                pn, po = torch.sqrt(na), torch.sqrt(acc)
+            else:
+                pn, po = na.pow(-self.lr_power), acc.pow(-self.lr_power)
+            lin = lin + (gs - (pn - po) / self.lr * x)
+            y = pn / self.lr + 2.0 * self.l2
+            w[idx] = (lin.clamp(-self.l1, self.l1) - lin) / y
+            lin_t[idx] = lin
+            acc_t[idx] = acc + g * g

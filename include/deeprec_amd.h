@@ -254,6 +254,13 @@ typedef struct {
   float false_positive_probability;  /* -1: Counter filter                  */
   int32_t counter_bits;              /* Bloom counter width 8/16/32/64      */
   int32_t layout;                    /* 0 light, 1 normal (informational)   */
+  int32_t value_bits;                /* 32 (float, default when 0) or 64:    */
+                                     /* double EVs (KvResourceGather's V =   */
+                                     /* double, kv_variable_ops.cc:368-388)  */
+                                     /* support gather / insert / export;   */
+                                     /* default rows / values / outputs are */
+                                     /* doubles; the applies and pooled     */
+                                     /* lookups are float-only (INVALID_ARG) */
 } dr_ev_config;
 
 /* InitializeKvVariableOp primary branch (kernels/kv_variable_ops.cc:173-193). */
@@ -263,6 +270,35 @@ int dr_ev_create_slot(dr_ev* primary, int slot_index, const float* default_row_h
                       dr_ev** out);
 int dr_ev_retain(dr_ev* ev);
 int dr_ev_release(dr_ev* ev);
+/* 32 (float) or 64 (double) */
+int dr_ev_value_bits(dr_ev* ev);
+/* use_locking = true of the KV applies (training_ali_ops.cc:104,141,161,   */
+/* 198,217; MaybeLockEmbeddingVariableInputMutexesInOrder, training_ali_op_ */
+/* helpers.h:85-118): bracket the apply calls.  lock takes the EVs' update  */
+/* mutexes in address order and makes `stream` wait for the previous locked */
+/* update of each EV (on any stream); unlock records this stream's point    */
+/* and releases them.  Without them updates from several streams race, as  */
+/* the reference's use_locking = false.                                     */
+int dr_ev_lock_updates(dr_ev* const* vars, int n, void* stream);
+int dr_ev_unlock_updates(dr_ev* const* vars, int n, void* stream);
+
+/* int32-key forms of the key-taking entry points (the reference registers  */
+/* KvResourceGather / Import / Export and Unique for int32 and int64 keys,  */
+/* kv_variable_ops.cc:368-388, unique_ali_op.cc): keys are widened on the  */
+/* device (the key value is the same), outputs narrowed back.  defaults /   */
+/* values / out are float or double per the EV's value_bits.                */
+size_t dr_ev_gather_i32_workspace_size(int64_t n);
+int dr_ev_gather_i32(dr_ev* ev, const int32_t* keys, int64_t n, const void* defaults,
+                     const int32_t* counts, void* out, void* ws, size_t ws_bytes, void* stream);
+int dr_ev_insert_i32(dr_ev* ev, const int32_t* keys, int64_t n, const void* values,
+                     const int64_t* versions, const int64_t* freqs, int64_t partition_id,
+                     int64_t partition_num, void* stream);
+int dr_ev_export_i32(dr_ev* ev, int32_t* keys_out, void* values_out, int64_t* versions_out,
+                     int64_t* freqs_out, int64_t capacity, int64_t* m_host, void* stream);
+size_t dr_unique_i32_workspace_size(int64_t n);
+int dr_unique_i32(const int32_t* keys, int64_t n, int32_t* uniq_out, int32_t* idx_out,
+                  int32_t* counts_out /* nullable */, int64_t* num_unique, void* ws,
+                  size_t ws_bytes, void* stream);
 /* KvVariableShapeOp (kv_variable_ops.cc:58-75): number of keys.  Syncs.   */
 int dr_ev_size(dr_ev* ev, int64_t* size_host, void* stream);
 /* Save-time eviction EmbeddingVar::Shrink (embedding_var.h:264-313), as     */
