@@ -682,9 +682,23 @@ __device__ __forceinline__ void apply_probe(const ApplyTable& at, int64_t i, int
   *initmask_out = initmask;
 }
 
+// Gradient row of apply entry i: row i of a dense [n, dim] block, or (gind)
+// the address grad_ptr[i] handed on by dr_pool_grad_rows_grouped, whose bit
+// 0 asks for the reference's 0 + x (-0.0f -> +0.0f) before use.
+__device__ __forceinline__ uint64_t apply_grad_addr(const float* grad, int gind, int64_t i,
+                                                    int64_t dim) {
+  return gind ? reinterpret_cast<const uint64_t*>(grad)[i]
+              : (uint64_t)(uintptr_t)(grad + i * dim);
+}
+template <class V>
+__device__ __forceinline__ V apply_grad_load(uint64_t a, int64_t c) {
+  const V g = reinterpret_cast<const V*>((uintptr_t)(a & ~(uint64_t)1))[c];
+  return (a & 1) ? vadd(vzero<V>(), g) : g;
+}
+
 template <int OPT, int VEC, int G>
 __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t dim, int64_t gs,
-                                                       OptScalars sc, int* st) {
+                                                       OptScalars sc, int gind, int* st) {
   const ApplyTable& at = ag.t[blockIdx.y];
   const ApplyCols& cols = at.cols;
   const float* __restrict__ grad = at.grad;
@@ -708,21 +722,22 @@ __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t di
     // cross-lane reads with every lane active (a disabled source lane reads 0)
     int64_t rr[U];
     int imq[U];
+    uint64_t ga[U];
 #pragma unroll
     for (int q = 0; q < U; ++q) {
       const int k = k0 + q * P + sub;
       rr[q] = __shfl(row, k, 64);
       imq[q] = __shfl(initmask, k, 64);
       if (base + k >= ne) rr[q] = -1;
+      ga[q] = rr[q] >= 0 ? apply_grad_addr(grad, gind, base + k, dim) : 0;
     }
     for (int64_t c = lg; c < dv; c += G) {
       V gv[U], w[U], a1[U], a2[U];
 #pragma unroll
       for (int q = 0; q < U; ++q) {  // all loads of U rows first
-        const int k = k0 + q * P + sub;
         const int im = imq[q];
         if (rr[q] < 0) continue;
-        gv[q] = reinterpret_cast<const V*>(grad + (base + k) * dim)[c];
+        gv[q] = apply_grad_load<V>(ga[q], c);
         w[q] = (im & 1) ? d0[c] : reinterpret_cast<const V*>(cols.pool[0] + rr[q] * dim)[c];
         if (OPT != OPT_SGD)
           a1[q] = (im & 2) ? d1[c] : reinterpret_cast<const V*>(cols.pool[1] + rr[q] * dim)[c];
@@ -762,7 +777,8 @@ __device__ __forceinline__ float ftrl_pow(float x, const OptScalars& sc) {
 
 template <int VEC, int G>
 __global__ __launch_bounds__(256) void ev_apply_ftrl_kernel(ApplyGroup ag, int64_t dim,
-                                                            int64_t gs, OptScalars sc, int* st) {
+                                                            int64_t gs, OptScalars sc, int gind,
+                                                            int* st) {
   const ApplyTable& at = ag.t[blockIdx.y];
   const ApplyCols& cols = at.cols;
   const float* __restrict__ grad = at.grad;
@@ -785,8 +801,8 @@ __global__ __launch_bounds__(256) void ev_apply_ftrl_kernel(ApplyGroup ag, int64
     const int im = __shfl(initmask, k, 64);
     if (base + k >= ne) r = -1;
     float ss = 0.f;
+    const uint64_t ga = r >= 0 ? apply_grad_addr(grad, gind, base + k, dim) : 0;
     if (r >= 0) {
-      const V* gp = reinterpret_cast<const V*>(grad + (base + k) * dim);
       V* wp = reinterpret_cast<V*>(cols.pool[0] + r * dim);
       V* ap = reinterpret_cast<V*>(cols.pool[1] + r * dim);
       V* lp = reinterpret_cast<V*>(cols.pool[2] + r * dim);
@@ -794,7 +810,7 @@ __global__ __launch_bounds__(256) void ev_apply_ftrl_kernel(ApplyGroup ag, int64
       const V* d1 = reinterpret_cast<const V*>(cols.dflt[1]);
       const V* d2 = reinterpret_cast<const V*>(cols.dflt[2]);
       for (int64_t c = lg; c < dv; c += G) {
-        const V gv = gp[c];
+        const V gv = apply_grad_load<V>(ga, c);
         const V w = (im & 1) ? d0[c] : wp[c];
         const V a = (im & 2) ? d1[c] : ap[c];
         V l = (im & 4) ? d2[c] : lp[c];
@@ -818,14 +834,13 @@ __global__ __launch_bounds__(256) void ev_apply_ftrl_kernel(ApplyGroup ag, int64
     for (int o = G / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
     if (r < 0) continue;
     const float norm = sqrtf(ss);
-    const V* gp = reinterpret_cast<const V*>(grad + (base + k) * dim);
     V* wp = reinterpret_cast<V*>(cols.pool[0] + r * dim);
     V* ap = reinterpret_cast<V*>(cols.pool[1] + r * dim);
     const V* lp = reinterpret_cast<const V*>(cols.pool[2] + r * dim);
     const V* d0 = reinterpret_cast<const V*>(cols.dflt[0]);
     const V* d1 = reinterpret_cast<const V*>(cols.dflt[1]);
     for (int64_t c = lg; c < dv; c += G) {
-      const V gv = gp[c];
+      const V gv = apply_grad_load<V>(ga, c);
       V w = (im & 1) ? d0[c] : wp[c];
       V a = (im & 2) ? d1[c] : ap[c];
       const V l = lp[c];
@@ -1203,7 +1218,7 @@ static int resolve_grouped(dr_ev* const* evs, int T, const int64_t* keys, const 
 static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* const* s2, int T,
                          OptScalars sc, const float* const* grads, const int64_t* const* keys,
                          const int64_t* n_host, const int64_t* const* n_dev, int64_t gs,
-                         hipStream_t st) {
+                         hipStream_t st, int gind = 0) {
   DR_REQUIRE(T >= 1 && vars && grads && keys && n_host, DR_INVALID_ARGUMENT, "bad argument");
   int* stw = status_word();
   DR_REQUIRE(stw, DR_INTERNAL, "status word unavailable");
@@ -1244,7 +1259,9 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
         a.cols.dflt[c] = s->defaults[cv[c]->col];
         aligned = aligned && ((((uintptr_t)a.cols.pool[c]) | ((uintptr_t)a.cols.dflt[c])) & 15) == 0;
       }
-      aligned = aligned && (((uintptr_t)grads[t]) & 15) == 0;
+      // by-address rows (gind) are 16-byte aligned when dim % 4 == 0
+      // (dr_pool_grad_rows_grouped defers only aligned rows)
+      aligned = aligned && (gind || (((uintptr_t)grads[t]) & 15) == 0);
       a.e = make_desc(var);
       a.keys = keys[t];
       a.grad = grads[t];
@@ -1259,16 +1276,16 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
   do {                                                                                     \
     if (opt == OPT_SGD)                                                                    \
       hipLaunchKernelGGL((ev_apply_kernel<OPT_SGD, VEC, G>), grid, dim3(256), 0, st, ag,    \
-                         dim, gs, sc, stw);                                                 \
+                         dim, gs, sc, gind, stw);                                           \
     else if (opt == OPT_ADAGRAD)                                                           \
       hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAGRAD, VEC, G>), grid, dim3(256), 0, st, ag,\
-                         dim, gs, sc, stw);                                                 \
+                         dim, gs, sc, gind, stw);                                           \
     else if (opt == OPT_FTRL)                                                              \
       hipLaunchKernelGGL((ev_apply_ftrl_kernel<VEC, G>), grid, dim3(256), 0, st, ag, dim,   \
-                         gs, sc, stw);                                                      \
+                         gs, sc, gind, stw);                                                \
     else                                                                                   \
       hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAM, VEC, G>), grid, dim3(256), 0, st, ag,   \
-                         dim, gs, sc, stw);                                                 \
+                         dim, gs, sc, gind, stw);                                           \
   } while (0)
     if (aligned && dim / 4 <= 8)
       DR_APPLY(4, 8);
@@ -1788,6 +1805,8 @@ int dr_ev_release(dr_ev* ev) {
 
 int64_t dr_ev_dim(dr_ev* ev) { return ev ? ev->sh->dim / ev->sh->value_words : -1; }
 
+int64_t dr_ev_row_capacity(dr_ev* ev) { return ev ? ev->sh->row_cap : -1; }
+
 int dr_ev_value_bits(dr_ev* ev) { return ev ? 32 * ev->sh->value_words : -1; }
 
 // MaybeLockEmbeddingVariableInputMutexesInOrder (training_ali_op_helpers.h:
@@ -2249,12 +2268,30 @@ int dr_ev_apply_grouped(int optimizer, dr_ev* const* vars, dr_ev* const* slot1,
                        global_step, S(stream));
 }
 
-int dr_ev_apply_ftrl_grouped(dr_ev* const* vars, dr_ev* const* accums, dr_ev* const* linears,
-                             int num_tables, const float* const* grads,
-                             const int64_t* const* keys, const int64_t* n_host,
-                             const int64_t* const* n_dev, float lr, float l1, float l2,
-                             float lr_power, float l2_shrinkage, int64_t global_step,
-                             void* stream) {
+int dr_ev_apply_grouped_ptr(int optimizer, dr_ev* const* vars, dr_ev* const* slot1,
+                            dr_ev* const* slot2, int num_tables, const uint64_t* const* grad_ptrs,
+                            const int64_t* const* keys, const int64_t* n_host,
+                            const int64_t* const* n_dev, float lr, float beta1_power,
+                            float beta2_power, float beta1, float beta2, float epsilon,
+                            int64_t global_step, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(optimizer >= DR_OPT_SGD && optimizer <= DR_OPT_ADAM, DR_INVALID_ARGUMENT,
+             "unknown optimizer %d", optimizer);
+  DR_REQUIRE(grad_ptrs, DR_INVALID_ARGUMENT, "bad argument");
+  OptScalars sc = {lr, beta1, beta2, epsilon, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (optimizer == DR_OPT_ADAM) sc.alpha = lr * sqrtf(1.0f - beta2_power) / (1.0f - beta1_power);
+  const int opt = optimizer == DR_OPT_SGD ? OPT_SGD
+                                          : (optimizer == DR_OPT_ADAGRAD ? OPT_ADAGRAD : OPT_ADAM);
+  return apply_grouped(opt, vars, slot1, slot2, num_tables, sc,
+                       reinterpret_cast<const float* const*>(grad_ptrs), keys, n_host, n_dev,
+                       global_step, S(stream), 1);
+}
+
+static int ftrl_grouped(dr_ev* const* vars, dr_ev* const* accums, dr_ev* const* linears,
+                        int num_tables, const float* const* grads, const int64_t* const* keys,
+                        const int64_t* n_host, const int64_t* const* n_dev, float lr, float l1,
+                        float l2, float lr_power, float l2_shrinkage, int64_t global_step,
+                        void* stream, int grad_by_address) {
   using namespace dr;
   // the op's OP_REQUIRES (training_ali_ops.cc:189-246)
   DR_REQUIRE(lr > 0.f, DR_INVALID_ARGUMENT, "lr is not a positive scalar");
@@ -2263,7 +2300,29 @@ int dr_ev_apply_ftrl_grouped(dr_ev* const* vars, dr_ev* const* accums, dr_ev* co
   DR_REQUIRE(lr_power <= 0.f, DR_INVALID_ARGUMENT, "lr_power is not a non-positive scalar");
   OptScalars sc = {lr, 0.f, 0.f, 0.f, 0.f, l1, l2, lr_power, l2_shrinkage};
   return apply_grouped(OPT_FTRL, vars, accums, linears, num_tables, sc, grads, keys, n_host,
-                       n_dev, global_step, S(stream));
+                       n_dev, global_step, S(stream), grad_by_address);
+}
+
+int dr_ev_apply_ftrl_grouped(dr_ev* const* vars, dr_ev* const* accums, dr_ev* const* linears,
+                             int num_tables, const float* const* grads,
+                             const int64_t* const* keys, const int64_t* n_host,
+                             const int64_t* const* n_dev, float lr, float l1, float l2,
+                             float lr_power, float l2_shrinkage, int64_t global_step,
+                             void* stream) {
+  return ftrl_grouped(vars, accums, linears, num_tables, grads, keys, n_host, n_dev, lr, l1, l2,
+                      lr_power, l2_shrinkage, global_step, stream, 0);
+}
+
+int dr_ev_apply_ftrl_grouped_ptr(dr_ev* const* vars, dr_ev* const* accums,
+                                 dr_ev* const* linears, int num_tables,
+                                 const uint64_t* const* grad_ptrs, const int64_t* const* keys,
+                                 const int64_t* n_host, const int64_t* const* n_dev, float lr,
+                                 float l1, float l2, float lr_power, float l2_shrinkage,
+                                 int64_t global_step, void* stream) {
+  if (!grad_ptrs) return DR_INVALID_ARGUMENT;
+  return ftrl_grouped(vars, accums, linears, num_tables,
+                      reinterpret_cast<const float* const*>(grad_ptrs), keys, n_host, n_dev, lr,
+                      l1, l2, lr_power, l2_shrinkage, global_step, stream, 1);
 }
 
 int dr_ev_apply_ftrl(dr_ev* var, dr_ev* accum, dr_ev* linear, float lr, float l1, float l2,

@@ -1,0 +1,617 @@
+// grad_rows.hip -- backward of a grouped pooled EV lookup keyed by the rows
+// the forward resolved (dr_pool_grad_rows_grouped).
+//
+// The reference's training lookup is Unique -> gather -> SparseSegmentSum
+// (python/ops/embedding_ops.py:592-675); its gradient is IndexedSlices over
+// the unique ids in first-occurrence order, each value the SparseSegment*Grad
+// sum of that id's positions in ascending order (segment_reduction_ali_ops_
+// util.h:331-458 / math_grad.py:321-368).  For filter-free EVs the forward
+// here skips the Unique (every nnz is resolved straight into the EV: the CAS
+// insert is the dedup), so the backward regroups by the resolved row
+// instead of by a unique index:
+//
+//   1. (row of nnz i, i) pairs, stable radix sort by row.  Positions are
+//      table-major and the sort is stable, so the positions of one (table,
+//      row) are contiguous and ascending: a run.
+//   2. flag[first position of each run] = 1; exclusive scan over positions
+//      -> the first-occurrence rank of every unique id of table t, i.e. the
+//      index Unique would have given it; U_t from the scan.
+//   3. one position pass emits the unique ids in that order.
+//   4. per run, the gradient (rows_classify_kernel, lane per position): a
+//      one-position run whose value needs no arithmetic is handed on BY
+//      ADDRESS (grad_ptr[o] = the pooled-grad row, bit 0 = "add +0.0f", the
+//      0 + x of the reference's unsorted sum), so the optimizer reads the
+//      pooled gradient directly and no [U, D] gradient is written and read
+//      back; every other run goes to a worklist that rows_work_kernel (G
+//      lanes per entry) sums into grad_unique[o] (grad_ptr[o] points there).
+//
+// Runs longer than kRowsChunk positions (a hot id) are cut at multiples of
+// kRowsChunk of the sorted array, summed in parallel and combined in order
+// by rows_finish_kernel: fixed association, deterministic, fp32 tolerance.
+// A run of at most kRowsChunk positions is summed serially in ascending
+// order -- bit-exact to the reference loops.
+#include "dr_rows.h"
+
+namespace dr {
+
+struct RowsGroup {
+  dr_pool_grad_desc d[DR_MAX_GROUP];
+  int64_t koff[DR_MAX_GROUP + 1];
+};
+
+static constexpr int64_t kRowsChunk = 256;
+static constexpr int kRowsChain = 4;        // positions of a chunk fetched per step
+static constexpr int kRowsFinishChain = 16;  // chunk partials fetched per step
+static constexpr int64_t kRowsMaxDim = 1024;
+
+// Table of global position i (lane-varying; koff staged in LDS).
+__device__ __forceinline__ int tab_of(const int64_t* koff, int T, int64_t i) {
+  int lo = 0, hi = T - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (koff[mid] <= i)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ void rows_keys_kernel(const int64_t* __restrict__ rowsel, int64_t N, int64_t row_limit,
+                                 uint64_t sentinel, uint64_t* __restrict__ kin,
+                                 int32_t* __restrict__ vin, int32_t* __restrict__ flags) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const int64_t r = rowsel[i];
+  // a negative row is an EV default served because the pool was exhausted
+  // (RESOURCE_EXHAUSTED already latched by the resolve): no gradient row
+  kin[i] = (r >= 0 && r < row_limit) ? (uint64_t)r : sentinel;
+  vin[i] = (int32_t)i;
+  flags[i] = 0;
+}
+
+__global__ void rows_heads_kernel(RowsGroup g, int T, const uint64_t* __restrict__ skey,
+                                  const int32_t* __restrict__ perm, uint64_t sentinel,
+                                  int32_t* __restrict__ flags) {
+  __shared__ int64_t sk[DR_MAX_GROUP + 1];
+  if (threadIdx.x <= T) sk[threadIdx.x] = g.koff[threadIdx.x];
+  __syncthreads();
+  const int64_t N = sk[T];
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= N) return;
+  const uint64_t u = skey[p];
+  if (u == sentinel) return;
+  const int32_t i = perm[p];
+  bool head = p == 0;
+  if (!head) {
+    const int32_t j = perm[p - 1];
+    head = skey[p - 1] != u || tab_of(sk, T, j) != tab_of(sk, T, i);
+  }
+  if (head) flags[i] = 1;
+}
+
+// Position order: unique ids in first-occurrence order per table, U_t, and
+// the scan base of every table (read by the grad kernel).
+__global__ void rows_emit_kernel(RowsGroup g, int T, const int64_t* __restrict__ keys,
+                                 const int32_t* __restrict__ flags,
+                                 const int32_t* __restrict__ ex, const int64_t* __restrict__ total,
+                                 int64_t* __restrict__ uniq_out, int64_t* __restrict__ num_unique,
+                                 int32_t* __restrict__ base) {
+  const int64_t N = g.koff[T];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i <= T) {   // base[t] = first-occurrence count before table t
+    const int64_t o = g.koff[i];
+    base[i] = o < N ? ex[o] : (int32_t)*total;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < T) {
+    const int t = threadIdx.x;
+    const int64_t a = g.koff[t], b = g.koff[t + 1];
+    const int64_t ba = a < N ? ex[a] : *total;
+    const int64_t bb = b < N ? ex[b] : *total;
+    num_unique[t] = bb - ba;
+  }
+  if (i >= N || !flags[i]) return;
+  const int t = table_of(g.koff, T, i, (int64_t)blockIdx.x * blockDim.x);
+  const int64_t a = g.koff[t];
+  uniq_out[a + ex[i] - ex[a]] = keys[i];
+}
+
+// Is the run (u, t) through inner position m (a multiple of kRowsChunk, not
+// its run's head) longer than kRowsChunk?  Rare path: bounded searches.
+__device__ bool run_is_long(const uint64_t* __restrict__ skey, const int32_t* __restrict__ perm,
+                            const int64_t* sk, int T, int64_t N, int64_t m, uint64_t u, int t) {
+  auto in_run = [&](int64_t q) { return skey[q] == u && tab_of(sk, T, perm[q]) == t; };
+  if (m >= kRowsChunk && in_run(m - kRowsChunk)) return true;
+  if (m + kRowsChunk < N && in_run(m + kRowsChunk)) return true;
+  // start in (m - chunk, m], end in (m, m + chunk]
+  int64_t lo = m - kRowsChunk + 1 < 0 ? 0 : m - kRowsChunk + 1, hi = m;  // first in-run
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (in_run(mid))
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  const int64_t s = lo;
+  lo = m;
+  hi = m + kRowsChunk < N ? m + kRowsChunk : N - 1;  // last in-run
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (in_run(mid))
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo - s + 1 > kRowsChunk;
+}
+
+// Lane per sorted position.  A one-position run whose value needs no
+// arithmetic (sum, or mean/sqrtn of a one-id bag, unweighted) is handed on by
+// address at once; every other run head, and every multiple of the chunk
+// inside a run (a possible later chunk of a long run), goes to the worklist
+// of rows_work_kernel.  All-distinct sum lookups (the Criteo shape) leave
+// the worklist empty: the pass moves no embedding-row bytes at all.
+__global__ __launch_bounds__(256) void rows_classify_kernel(
+    RowsGroup g, int T, int64_t B, const uint64_t* __restrict__ skey,
+    const int32_t* __restrict__ perm, const int32_t* __restrict__ ex,
+    const int32_t* __restrict__ base, uint64_t sentinel, int defer,
+    uint64_t* __restrict__ gptr, int32_t* __restrict__ work, int32_t* __restrict__ nwork,
+    int* st) {
+  __shared__ dr_pool_grad_desc sd[DR_MAX_GROUP];
+  __shared__ int64_t sk[DR_MAX_GROUP + 1];
+  __shared__ int32_t sb[DR_MAX_GROUP + 1];
+  if (threadIdx.x < T) sd[threadIdx.x] = g.d[threadIdx.x];
+  if (threadIdx.x <= T) {
+    sk[threadIdx.x] = g.koff[threadIdx.x];
+    sb[threadIdx.x] = base[threadIdx.x];
+  }
+  __syncthreads();
+  const int64_t N = sk[T];
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool push = false;
+  if (p < N) {
+    const int64_t pm = p > 0 ? p - 1 : 0, pn = p + 1 < N ? p + 1 : N - 1;
+    const uint64_t u = skey[p], um = skey[pm], un = skey[pn];
+    const int32_t i = perm[p], im = perm[pm], in = perm[pn];
+    const int t = tab_of(sk, T, i);
+    const bool valid = u != sentinel;
+    const bool rhead = valid && (p == 0 || um != u || tab_of(sk, T, im) != t);
+    const bool last = p + 1 >= N || un != u || tab_of(sk, T, in) != t;
+    if (rhead && last) {
+      const dr_pool_grad_desc& d = sd[t];
+      const int64_t k = (int64_t)i - sk[t];
+      const int64_t r = d.seg ? d.seg[k * d.seg_stride] : k;
+      const bool okr = r >= 0 && r < B;
+      if (!okr) latch(st, DR_INVALID_ARGUMENT);
+      const int mode = d.combiner == DR_COMBINER_SUM ? 0 : 1;
+      bool dfr = defer && okr && !d.weights;
+      if (dfr && mode != 0) dfr = !d.bag_off || d.bag_off[r + 1] - d.bag_off[r] == 1;
+      if (dfr) {
+        const int64_t o = sk[t] + (int64_t)ex[i] - sb[t];
+        gptr[o] = (uint64_t)(uintptr_t)(d.top_grad + r * d.top_stride) | (mode == 0 ? 1u : 0u);
+      } else {
+        push = true;
+      }
+    } else if (rhead || (valid && p % kRowsChunk == 0)) {
+      push = true;
+    }
+  }
+  const uint64_t m = __ballot(push);
+  if (m) {   // wave-aggregated append
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    int at = 0;
+    if (lane == leader) at = atomicAdd(nwork, __popcll(m));
+    at = __shfl(at, leader, 64);
+    if (push) work[at + __popcll(m & lanemask_lt())] = (int32_t)p;
+  }
+}
+
+// G lanes per worklist entry (a sorted position c0): a run head sums its run
+// (or, for a long run, its first chunk) in ascending position order into
+// grad_unique[o]; an inner multiple of the chunk sums its chunk into
+// part[c0 / chunk] when its run is long, and is dropped otherwise.
+template <int VEC, int G, int CPL, bool W>
+__global__ __launch_bounds__(256) void rows_work_kernel(
+    RowsGroup g, int T, int64_t B, const uint64_t* __restrict__ skey,
+    const int32_t* __restrict__ perm, const int32_t* __restrict__ ex,
+    const int32_t* __restrict__ base, int dim, const int32_t* __restrict__ work,
+    const int32_t* __restrict__ nwork, uint64_t* __restrict__ gptr, float* __restrict__ gu,
+    float* __restrict__ part, int32_t* __restrict__ longs, int32_t* __restrict__ nlong, int* st) {
+  const int nw = *nwork;
+  if ((int64_t)blockIdx.x * (256 / G) >= nw) return;   // block-uniform (empty list: one load)
+  __shared__ dr_pool_grad_desc sd[DR_MAX_GROUP];
+  __shared__ int64_t sk[DR_MAX_GROUP + 1];
+  __shared__ int32_t sb[DR_MAX_GROUP + 1];
+  if (threadIdx.x < T) sd[threadIdx.x] = g.d[threadIdx.x];
+  if (threadIdx.x <= T) {
+    sk[threadIdx.x] = g.koff[threadIdx.x];
+    sb[threadIdx.x] = base[threadIdx.x];
+  }
+  __syncthreads();
+  constexpr int GPB = 256 / G;
+  const int64_t N = sk[T];
+  const int lg = threadIdx.x % G;
+  const int dv = dim / VEC;
+  using R = Row<VEC, G, CPL>;
+  using V = typename VecT<VEC>::T;
+  auto scaled = [&](R& y, const dr_pool_grad_desc& d, int mode, int64_t r) {
+    if (mode == 0) return;
+    const int32_t cnt = (r >= 0 && d.bag_off) ? d.bag_off[r + 1] - d.bag_off[r] : 1;
+    if (cnt != 1) {
+      const float sc = mode == 2 ? (float)(1.0 / sqrt((double)cnt)) : (float)(1.0 / (double)cnt);
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) y.v[c] = vmul(y.v[c], sc);
+    }
+  };
+  auto wscaled = [&](R& y, const dr_pool_grad_desc& d, int64_t r, int64_t k) {
+    if (d.bag_scale) {
+      const float q = d.bag_scale[r >= 0 ? r : 0];
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) y.v[c] = vdiv(y.v[c], q);
+    }
+    const float w = d.weights[k];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) y.v[c] = vmul(y.v[c], w);
+  };
+  for (int64_t e = (int64_t)blockIdx.x * GPB + threadIdx.x / G; e < nw;
+       e += (int64_t)gridDim.x * GPB) {
+    const int64_t c0 = work[e];
+    const uint64_t u = skey[c0];
+    const int32_t pc = perm[c0];
+    const int t = tab_of(sk, T, pc);
+    const bool first = c0 == 0 || skey[c0 - 1] != u || tab_of(sk, T, perm[c0 - 1]) != t;
+    bool islong;
+    int64_t lim;
+    if (first) {
+      islong = c0 + kRowsChunk < N && skey[c0 + kRowsChunk] == u &&
+               tab_of(sk, T, perm[c0 + kRowsChunk]) == t;
+      lim = islong ? (c0 / kRowsChunk + 1) * kRowsChunk : N;
+    } else {
+      if (!run_is_long(skey, perm, sk, T, N, c0, u, t)) continue;  // inside a short run
+      islong = true;
+      lim = c0 + kRowsChunk;
+    }
+    if (lim > N) lim = N;
+    const dr_pool_grad_desc& d = sd[t];
+    const int mode = d.combiner == DR_COMBINER_SUM ? 0 : (d.combiner == DR_COMBINER_MEAN ? 1 : 2);
+    const bool zero_start = mode == 0 || (W && d.weights);
+    R acc;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<V>();
+    bool fresh = !(first && zero_start);
+    const float* tg = d.top_grad;
+    const int64_t ts = d.top_stride;
+    const int64_t* segp = d.seg;
+    const int64_t sst = d.seg_stride;
+    const int64_t kt0 = sk[t];
+    const int64_t nnz_t = d.nnz;
+    bool cbad = false;
+    for (int64_t p = c0; p < lim; p += kRowsChain) {
+      R y[kRowsChain];
+      int64_t ry[kRowsChain];
+      int64_t ky[W ? kRowsChain : 1];
+      bool ok[kRowsChain];
+#pragma unroll
+      for (int j = 0; j < kRowsChain; ++j) {
+        const int64_t pj = p + j < N ? p + j : N - 1;
+        const int64_t k = (int64_t)perm[pj] - kt0;
+        // positions of one (table, row) are contiguous; a position of the same
+        // row in another table has k outside [0, nnz_t)
+        ok[j] = (p + j < lim) & (skey[pj] == u) & (k >= 0) & (k < nnz_t);
+        ry[j] = ok[j] ? k : 0;
+        if (W) ky[W ? j : 0] = ry[j];
+      }
+      if (segp) {
+#pragma unroll
+        for (int j = 0; j < kRowsChain; ++j) ry[j] = segp[ry[j] * sst];
+      }
+#pragma unroll
+      for (int j = 0; j < kRowsChain; ++j) {
+        const bool okr = (ry[j] >= 0) & (ry[j] < B);
+        cbad |= ok[j] & !okr;
+        ry[j] = okr ? ry[j] : -1;
+        load_row_u<VEC, G, CPL>(y[j], tg + (okr ? ry[j] : 0) * ts, lg, dv);
+      }
+#pragma unroll
+      for (int j = 0; j < kRowsChain; ++j) {
+        if (!ok[j]) break;
+        if (ry[j] < 0) {
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) y[j].v[c] = vzero<V>();
+        }
+        if (W && d.weights)
+          wscaled(y[j], d, ry[j], ky[W ? j : 0]);
+        else
+          scaled(y[j], d, mode, ry[j]);
+        if (fresh) {
+          acc = y[j];
+          fresh = false;
+        } else {
+          acc_add(acc, y[j]);
+        }
+      }
+      if (!ok[kRowsChain - 1]) break;
+    }
+    if (cbad) latch(st, DR_INVALID_ARGUMENT);
+    if (first) {
+      const int64_t o = kt0 + (int64_t)ex[pc] - sb[t];
+      float* dst = gu + o * (int64_t)dim;
+      store_row<VEC, G, CPL>(acc, dst, lg, dv);
+      if (lg == 0) {
+        gptr[o] = (uint64_t)(uintptr_t)dst;
+        if (islong) {
+          const int32_t at = atomicAdd(nlong, 1);
+          longs[2 * at] = (int32_t)o;
+          longs[2 * at + 1] = (int32_t)c0;
+        }
+      }
+    } else {
+      store_row<VEC, G, CPL>(acc, part + (c0 / kRowsChunk) * (int64_t)dim, lg, dv);
+    }
+  }
+}
+
+// grad_unique[o] = ((c_0 + c_1) + c_2) + ... for the queued long runs: c_0
+// is in grad_unique[o]; c_k (k >= 1) sits in part[m_k / chunk] for the
+// multiples m_k of the chunk inside the run.
+template <int VEC, int G, int CPL>
+__global__ __launch_bounds__(256) void rows_finish_kernel(
+    RowsGroup g, int T, const uint64_t* __restrict__ skey, const int32_t* __restrict__ perm,
+    int dim, float* __restrict__ gu, const float* __restrict__ part,
+    const int32_t* __restrict__ longs, const int32_t* __restrict__ nlong, int64_t nslots) {
+  __shared__ int64_t sk[DR_MAX_GROUP + 1];
+  if (threadIdx.x <= T) sk[threadIdx.x] = g.koff[threadIdx.x];
+  __syncthreads();
+  constexpr int GPB = 256 / G;
+  const int64_t N = sk[T];
+  const int n = *nlong;
+  const int lg = threadIdx.x % G;
+  const int dv = dim / VEC;
+  using R = Row<VEC, G, CPL>;
+  for (int64_t i = (int64_t)blockIdx.x * GPB + threadIdx.x / G; i < n;
+       i += (int64_t)gridDim.x * GPB) {
+    const int64_t o = longs[2 * i], c0 = longs[2 * i + 1];
+    const uint64_t u = skey[c0];
+    const int t = tab_of(sk, T, perm[c0]);
+    R acc;
+    load_row_u<VEC, G, CPL>(acc, gu + o * (int64_t)dim, lg, dv);
+    for (int64_t m = (c0 / kRowsChunk + 1) * kRowsChunk; m < N;
+         m += kRowsFinishChain * kRowsChunk) {
+      R y[kRowsFinishChain];
+      bool ok[kRowsFinishChain];
+#pragma unroll
+      for (int j = 0; j < kRowsFinishChain; ++j) {
+        const int64_t mj = m + j * kRowsChunk;
+        const int64_t mc = mj < N ? mj : N - 1;
+        ok[j] = (mj < N) && skey[mc] == u && tab_of(sk, T, perm[mc]) == t;
+        int64_t sl = mc / kRowsChunk;
+        sl = sl < nslots ? sl : nslots - 1;
+        load_row_u<VEC, G, CPL>(y[j], part + sl * (int64_t)dim, lg, dv);
+      }
+#pragma unroll
+      for (int j = 0; j < kRowsFinishChain; ++j) {
+        if (!ok[j]) break;
+        acc_add(acc, y[j]);
+      }
+      if (!ok[kRowsFinishChain - 1]) break;
+    }
+    store_row<VEC, G, CPL>(acc, gu + o * (int64_t)dim, lg, dv);
+  }
+}
+
+// out[i] = *grad_ptr[i] (+0.0f first when bit 0 is set), i < min(n, *n_dev):
+// the IndexedSlices values of a by-address gradient, materialised.
+template <int VEC, int G, int CPL>
+__global__ __launch_bounds__(256) void rows_from_ptr_kernel(const uint64_t* __restrict__ gptr,
+                                                            int64_t n, const int64_t* n_dev,
+                                                            int dim, float* __restrict__ out) {
+  constexpr int GPB = 256 / G;
+  const int64_t ne = eff_n(n, n_dev);
+  const int64_t i = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+  if (i >= ne) return;
+  const int lg = threadIdx.x % G;
+  const int dv = dim / VEC;
+  using R = Row<VEC, G, CPL>;
+  using V = typename VecT<VEC>::T;
+  const uint64_t p = gptr[i];
+  R x;
+  load_row_u<VEC, G, CPL>(x, reinterpret_cast<const float*>((uintptr_t)(p & ~(uint64_t)1)), lg,
+                          dv);
+  if (p & 1) {
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) x.v[c] = vadd(vzero<V>(), x.v[c]);
+  }
+  store_row<VEC, G, CPL>(x, out + i * (int64_t)dim, lg, dv);
+}
+
+struct RowsWs {
+  uint64_t* kin;
+  int32_t* vin;
+  uint64_t* kout;
+  int32_t* perm;
+  int32_t* flags;
+  int32_t* ex;
+  int32_t* base;
+  int64_t* total;
+  int32_t* nlong;
+  int32_t* nwork;
+  int32_t* work;
+  int32_t* longs;
+  float* part;
+  void* sort_ws;
+  size_t sort_bytes;
+  void* scan_ws;
+};
+
+static RowsWs carve_rows(void* ws, int64_t n, size_t* used) {
+  Carver c(ws);
+  RowsWs w;
+  const int64_t nn = n > 0 ? n : 1;
+  w.kin = c.take<uint64_t>(nn);
+  w.vin = c.take<int32_t>(nn);
+  w.kout = c.take<uint64_t>(nn);
+  w.perm = c.take<int32_t>(nn);
+  w.flags = c.take<int32_t>(nn);
+  w.ex = c.take<int32_t>(nn);
+  w.base = c.take<int32_t>(DR_MAX_GROUP + 1);
+  w.total = c.take<int64_t>(1);
+  w.nlong = c.take<int32_t>(1);
+  w.nwork = c.take<int32_t>(1);
+  w.work = c.take<int32_t>(nn);
+  const int64_t chunks = nn / kRowsChunk + 2;
+  w.longs = c.take<int32_t>(2 * chunks);
+  w.part = c.take<float>(chunks * kRowsMaxDim);
+  w.sort_bytes = dr_sort_pairs_workspace_size(nn);
+  w.sort_ws = c.take<char>(w.sort_bytes);
+  w.scan_ws = c.take<char>(scan_ws_bytes(nn));
+  if (used) *used = c.used + 256;
+  return w;
+}
+
+template <int VEC, int G, int CPL>
+static void launch_rows(const RowsGroup& g, int T, int64_t B, const RowsWs& w, int dim,
+                        bool weighted, uint64_t* gptr, float* gu, hipStream_t s, int* st) {
+  const int64_t N = g.koff[T];
+  // the worklist is at most N entries; a grid-stride pass over its device
+  // count (an empty list costs one load per block)
+  int64_t blocks = ceil_div(N, 256 / G);
+  if (blocks > 4096) blocks = 4096;
+  if (weighted)
+    hipLaunchKernelGGL((rows_work_kernel<VEC, G, CPL, true>), dim3((unsigned)blocks), dim3(256),
+                       0, s, g, T, B, w.kout, w.perm, w.ex, w.base, dim, w.work, w.nwork, gptr,
+                       gu, w.part, w.longs, w.nlong, st);
+  else
+    hipLaunchKernelGGL((rows_work_kernel<VEC, G, CPL, false>), dim3((unsigned)blocks), dim3(256),
+                       0, s, g, T, B, w.kout, w.perm, w.ex, w.base, dim, w.work, w.nwork, gptr,
+                       gu, w.part, w.longs, w.nlong, st);
+  if (N > kRowsChunk)
+    hipLaunchKernelGGL((rows_finish_kernel<VEC, G, CPL>), dim3(64), dim3(256), 0, s, g, T,
+                       w.kout, w.perm, dim, gu, w.part, w.longs, w.nlong,
+                       N / kRowsChunk + 2);
+}
+
+__global__ void rows_zero_i32(int32_t* p, int32_t* q) {
+  *p = 0;
+  *q = 0;
+}
+
+}  // namespace dr
+
+extern "C" {
+
+size_t dr_pool_grad_rows_workspace_size(int64_t total_nnz) {
+  size_t used = 0;
+  dr::carve_rows(nullptr, total_nnz, &used);
+  return used;
+}
+
+int dr_pool_grad_rows_grouped(const dr_pool_grad_desc* descs_host, int num_tables, int64_t batch,
+                              int dim, const int64_t* rowsel, int64_t row_limit,
+                              const int64_t* keys, int defer, int64_t* uniq_out,
+                              int64_t* num_unique, uint64_t* grad_ptr, float* grad_unique,
+                              void* ws, size_t ws_bytes, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(descs_host && num_tables >= 1 && num_tables <= DR_MAX_GROUP && dim > 0 &&
+                 dim <= kRowsMaxDim && batch >= 0 && row_limit > 0 && rowsel && keys &&
+                 uniq_out && num_unique && grad_ptr && grad_unique,
+             DR_INVALID_ARGUMENT, "bad argument");
+  RowsGroup g;
+  memset(&g, 0, sizeof(g));
+  bool aligned = dim % 4 == 0 && ((uintptr_t)grad_unique & 15) == 0;
+  bool weighted = false;
+  for (int t = 0; t < num_tables; ++t) {
+    const dr_pool_grad_desc& d = descs_host[t];
+    DR_REQUIRE(d.top_grad && d.nnz >= 0, DR_INVALID_ARGUMENT, "table %d: missing pointers", t);
+    DR_REQUIRE(d.combiner == DR_COMBINER_SUM || d.bag_off || !d.seg, DR_INVALID_ARGUMENT,
+               "table %d: mean/sqrtn of multi-hot bags need bag_off", t);
+    DR_REQUIRE(!d.weights || d.combiner == DR_COMBINER_SUM || d.bag_scale, DR_INVALID_ARGUMENT,
+               "table %d: weighted mean/sqrtn needs bag_scale (dr_bag_weight_scale)", t);
+    g.d[t] = d;
+    g.koff[t + 1] = g.koff[t] + d.nnz;
+    aligned = aligned && ((uintptr_t)d.top_grad & 15) == 0 && d.top_stride % 4 == 0;
+    weighted = weighted || d.weights;
+  }
+  const int64_t n = g.koff[num_tables];
+  DR_REQUIRE(n < (1ll << 31), DR_INVALID_ARGUMENT, "too many nnz");
+  DR_REQUIRE(batch > 0 || n == 0, DR_INVALID_ARGUMENT, "nnz without a batch");
+  DR_REQUIRE(ws_bytes >= dr_pool_grad_rows_workspace_size(n), DR_INVALID_ARGUMENT,
+             "workspace too small");
+  hipStream_t s = S(stream);
+  if (n == 0) return fill_bytes(num_unique, 0, sizeof(int64_t) * num_tables, s);
+  int* st = status_word();
+  DR_REQUIRE(st, DR_INTERNAL, "status word unavailable");
+  DR_REQUIRE(dim % 4 != 0 || ((uintptr_t)grad_unique & 15) == 0, DR_INVALID_ARGUMENT,
+             "grad_unique must be 16-byte aligned");
+  if (!aligned) defer = 0;   // by-address rows must share grad_unique's alignment
+  RowsWs w = carve_rows(ws, n, nullptr);
+  int rb = 1;
+  while (rb < 62 && ((int64_t)1 << rb) <= row_limit) ++rb;   // rows < 2^rb - 1
+  const uint64_t sentinel = ((uint64_t)1 << rb) - 1;
+  const unsigned nb = (unsigned)ceil_div(n, 256);
+  hipLaunchKernelGGL(rows_keys_kernel, dim3(nb), dim3(256), 0, s, rowsel, n, row_limit, sentinel,
+                     w.kin, w.vin, w.flags);
+  DR_LAUNCH_CHECK();
+  int rc = dr_sort_pairs(w.kin, w.vin, w.kout, w.perm, n, 0, rb, w.sort_ws, w.sort_bytes, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(rows_heads_kernel, dim3(nb), dim3(256), 0, s, g, num_tables, w.kout, w.perm,
+                     sentinel, w.flags);
+  rc = scan_exclusive_i32(w.flags, w.ex, n, nullptr, w.total, w.scan_ws, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(rows_emit_kernel, dim3(nb), dim3(256), 0, s, g, num_tables, keys, w.flags,
+                     w.ex, w.total, uniq_out, num_unique, w.base);
+  hipLaunchKernelGGL(rows_zero_i32, dim3(1), dim3(1), 0, s, w.nlong, w.nwork);
+  hipLaunchKernelGGL(rows_classify_kernel, dim3(nb), dim3(256), 0, s, g, num_tables, batch,
+                     w.kout, w.perm, w.ex, w.base, sentinel, defer, grad_ptr, w.work, w.nwork, st);
+  DR_LAUNCH_CHECK();
+  if (aligned) {
+    const int d4 = dim / 4;
+    if (d4 <= 8)
+      launch_rows<4, 8, 1>(g, num_tables, batch, w, dim, weighted, grad_ptr, grad_unique, s, st);
+    else if (d4 <= 16)
+      launch_rows<4, 16, 1>(g, num_tables, batch, w, dim, weighted, grad_ptr, grad_unique, s, st);
+    else if (d4 <= 32)
+      launch_rows<4, 32, 1>(g, num_tables, batch, w, dim, weighted, grad_ptr, grad_unique, s, st);
+    else if (d4 <= 64)
+      launch_rows<4, 64, 1>(g, num_tables, batch, w, dim, weighted, grad_ptr, grad_unique, s, st);
+    else
+      launch_rows<4, 64, 4>(g, num_tables, batch, w, dim, weighted, grad_ptr, grad_unique, s, st);
+  } else {
+    if (dim <= 64)
+      launch_rows<1, 64, 1>(g, num_tables, batch, w, dim, weighted, grad_ptr, grad_unique, s, st);
+    else if (dim <= 256)
+      launch_rows<1, 64, 4>(g, num_tables, batch, w, dim, weighted, grad_ptr, grad_unique, s, st);
+    else
+      launch_rows<1, 64, 16>(g, num_tables, batch, w, dim, weighted, grad_ptr, grad_unique, s,
+                             st);
+  }
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_rows_from_ptr(const uint64_t* grad_ptr, int64_t n, const int64_t* n_dev, int dim,
+                     float* out, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(n >= 0 && dim > 0 && dim <= kRowsMaxDim && (n == 0 || (grad_ptr && out)),
+             DR_INVALID_ARGUMENT, "bad argument");
+  if (n == 0) return DR_OK;
+  hipStream_t s = S(stream);
+  // by-address rows are 16-byte aligned whenever dim % 4 == 0 (the producer
+  // only defers when every top_grad slice is)
+  if (dim % 4 == 0 && ((uintptr_t)out & 15) == 0) {
+    const int d4 = dim / 4;
+    if (d4 <= 32)
+      hipLaunchKernelGGL((rows_from_ptr_kernel<4, 32, 1>), dim3((unsigned)ceil_div(n, 8)),
+                         dim3(256), 0, s, grad_ptr, n, n_dev, dim, out);
+    else
+      hipLaunchKernelGGL((rows_from_ptr_kernel<4, 64, 4>), dim3((unsigned)ceil_div(n, 4)),
+                         dim3(256), 0, s, grad_ptr, n, n_dev, dim, out);
+  } else {
+    hipLaunchKernelGGL((rows_from_ptr_kernel<1, 64, 16>), dim3((unsigned)ceil_div(n, 4)),
+                       dim3(256), 0, s, grad_ptr, n, n_dev, dim, out);
+  }
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+}  // extern "C"

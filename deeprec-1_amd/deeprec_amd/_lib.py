@@ -110,6 +110,10 @@ SIGNATURES = {
     "dr_pool_grad_workspace_size": (_SZ, [_I64]),
     "dr_pool_grad_grouped_workspace_size": (_SZ, [_I64]),
     "dr_pool_grad_grouped": (_I32, [_P, _I32, _I64, _I32, _P, _P, _SZ, _P]),
+    "dr_pool_grad_rows_workspace_size": (_SZ, [_I64]),
+    "dr_pool_grad_rows_grouped": (_I32, [_P, _I32, _I64, _I32, _P, _I64, _P, _I32, _P, _P, _P, _P,
+                                         _P, _SZ, _P]),
+    "dr_rows_from_ptr": (_I32, [_P, _I64, _P, _I32, _P, _P]),
     "dr_pool_grad": (_I32, [_P, _I64, _I64, _I32, _P, _P, _P, _I64, _P, _I32, _P, _P, _SZ, _P]),
     "dr_ev_create": (_I32, [_P, _P, _P]),
     "dr_ev_create_slot": (_I32, [_P, _I32, _P, _P]),
@@ -117,6 +121,7 @@ SIGNATURES = {
     "dr_ev_release": (_I32, [_P]),
     "dr_ev_size": (_I32, [_P, _P, _P]),
     "dr_ev_dim": (_I64, [_P]),
+    "dr_ev_row_capacity": (_I64, [_P]),
     "dr_ev_value_bits": (_I32, [_P]),
     "dr_ev_lock_updates": (_I32, [_P, _I32, _P]),
     "dr_ev_unlock_updates": (_I32, [_P, _I32, _P]),
@@ -149,6 +154,10 @@ SIGNATURES = {
                                 _I64, _P]),
     "dr_ev_apply_grouped": (_I32, [_I32, _P, _P, _P, _I32, _P, _P, _P, _P, _F32, _F32, _F32,
                                    _F32, _F32, _F32, _I64, _P]),
+    "dr_ev_apply_grouped_ptr": (_I32, [_I32, _P, _P, _P, _I32, _P, _P, _P, _P, _F32, _F32, _F32,
+                                       _F32, _F32, _F32, _I64, _P]),
+    "dr_ev_apply_ftrl_grouped_ptr": (_I32, [_P, _P, _P, _I32, _P, _P, _P, _P, _F32, _F32, _F32,
+                                            _F32, _F32, _I64, _P]),
     "dr_ev_apply_ftrl": (_I32, [_P, _P, _P, _F32, _F32, _F32, _F32, _F32, _P, _P, _I64, _P, _I64,
                                 _P]),
     "dr_ev_apply_ftrl_grouped": (_I32, [_P, _P, _P, _I32, _P, _P, _P, _P, _F32, _F32, _F32, _F32,

@@ -59,6 +59,9 @@ def _anchor(holder):
 # DEEPREC_AMD_FUSED_ONEHOT=0 selects the resolve -> pool pipeline for
 # forward-only one-hot lookups (A/B measurement; both are HIP paths).
 _FUSED_ONEHOT = os.environ.get("DEEPREC_AMD_FUSED_ONEHOT", "1") != "0"
+# training lookups of filter-free EVs without Unique, backward regrouped by
+# the resolved rows (A/B switch; both are HIP paths)
+_ROWS_GRAD = os.environ.get("DEEPREC_AMD_ROWS_GRAD", "1") != "0"
 
 
 def _ev_default_dev(ev):
@@ -329,7 +332,7 @@ def _prepare_all(feats, need_grad):
     """One grouped Unique + resolve per set of EVs of equal dim (WDL's 64 / 128
     columns: two launches sets instead of 26 per-feature pipelines); other
     parameters one by one."""
-    if _groupable(feats):
+    if _groupable(feats) or (need_grad and len(feats) == 1 and _rows_eligible(feats)):
         _prepare_group(feats, need_grad)
         return
     sets = {}
@@ -385,7 +388,8 @@ def _prepare_group(feats, need_grad=True):
         koff.append(koff[-1] + f.values.numel())
     vals = _concat_values(feats, koff)
     with_counts = any(f.params.filter_freq != 0 for f in feats)
-    if not with_counts and not need_grad:
+    by_rows = need_grad and _rows_eligible(feats)
+    if not with_counts and (not need_grad or by_rows):
         rowsel = torch.empty(koff[-1], dtype=torch.int64, device=dev)
         handles = (C.c_void_p * T)(*[f.params.handle.value for f in feats])
         wsb = lib().dr_ev_resolve_workspace_size(koff[-1])
@@ -397,6 +401,10 @@ def _prepare_group(feats, need_grad=True):
         for t, f in enumerate(feats):
             f.uniq = f.idx = f.rows = f.U = f.defaults = f.group = None
             f.rowsel = rowsel[koff[t]:koff[t + 1]]
+        if by_rows:
+            group = _RowGroup(feats, vals, rowsel, koff)
+            for f in feats:
+                f.group = group
         return
     uniq, idx, cnt, U = ops.unique_grouped(vals, koff, with_counts)
     rows = torch.empty(koff[-1], dtype=torch.int64, device=dev)
@@ -421,6 +429,82 @@ def _prepare_group(feats, need_grad=True):
     group = _UniqueGroup(feats, uniq, U, koff)
     for f in feats:
         f.group = group
+
+
+def _rows_eligible(feats):
+    """The training forward may skip the Unique when every feature is a
+    filter-free EV without max_norm (the clip's backward needs the unique
+    rows): the backward then regroups by the resolved rows
+    (dr_pool_grad_rows_grouped, same IndexedSlices as Unique would give)."""
+    if not _ROWS_GRAD or len(feats) > _lib.MAX_GROUP:
+        return False
+    p0 = feats[0].params
+    return all(isinstance(f.params, EmbeddingVariable) and f.params.filter_freq == 0
+               and not callable(f.params.initializer) and f.max_norm is None
+               and f.params.dim == p0.dim and f.params.device == p0.device
+               and f.batch == feats[0].batch for f in feats)
+
+
+class _RowGroup(object):
+    """Features resolved straight into their EVs (no Unique): the backward is
+    one dr_pool_grad_rows_grouped over the forward's rows.  Unique ids come
+    out in first-occurrence order, gradients by address (kv_variable_ops.
+    IndexedSlices.grad_ptr) so the optimizer reads the pooled gradient in
+    place."""
+
+    def __init__(self, feats, vals, rowsel, koff):
+        self.feats = feats
+        self.vals = vals
+        self.rowsel = rowsel
+        self.koff = koff
+
+    def grads(self, g, cols, top_stride):
+        import ctypes as C
+        dev = g.device
+        D = self.feats[0].params.dim
+        T = len(self.feats)
+        descs = (_lib.DrPoolGradDesc * T)()
+        keep = [g]
+        for t, f in enumerate(self.feats):
+            d = descs[t]
+            if f.weights is not None:
+                _bag_offsets_all([f])
+                d.weights = ptr(f.weights)
+                if f.combiner != "sum":
+                    q = ops.bag_weight_scale(f.weights, f.bag_off, f.combiner)
+                    keep.append(q)
+                    d.bag_scale = ptr(q)
+            d.top_grad = g.data_ptr() + 4 * cols[t]
+            d.top_stride = top_stride
+            if f.onehot:
+                d.bag_off, d.seg, d.seg_stride = None, None, 0
+            else:
+                _bag_offsets_all([f])
+                d.bag_off = ptr(f.bag_off)
+                d.seg = ptr(f.seg64)
+                d.seg_stride = f.seg_stride
+            d.nnz = f.values.numel()
+            d.combiner = COMBINERS[f.combiner]
+        n = self.koff[-1]
+        m = max(n, 1)
+        uniq = torch.empty(m, dtype=torch.int64, device=dev)
+        U = torch.empty(T, dtype=torch.int64, device=dev)
+        gptr = torch.empty(m, dtype=torch.int64, device=dev)
+        gu = torch.empty((m, D), dtype=torch.float32, device=dev)
+        keep.append(gu)
+        limit = max(lib().dr_ev_row_capacity(f.params.handle) for f in self.feats)
+        wsb = lib().dr_pool_grad_rows_workspace_size(n)
+        ws = workspace(wsb, dev)
+        check(lib().dr_pool_grad_rows_grouped(
+            descs, T, self.feats[0].batch, D, ptr(self.rowsel), max(int(limit), 1),
+            ptr(self.vals), 1, ptr(uniq), ptr(U), ptr(gptr), ptr(gu), ptr(ws), wsb,
+            stream_handle(dev)))
+        ops._post(dev)
+        k = self.koff
+        keep = tuple(keep)
+        return [IndexedSlices(None, uniq[k[t]:k[t + 1]], U[t:t + 1], True,
+                              grad_ptr=gptr[k[t]:k[t + 1]], dim=D, keep=keep)
+                for t in range(T)]
 
 
 class _UniqueGroup(object):

@@ -66,13 +66,40 @@ _VALUE_DTYPES = (torch.float32, torch.float64)
 
 
 class IndexedSlices(object):
-    """values [N, D] for rows `indices` [N] (tf.IndexedSlices)."""
+    """values [N, D] for rows `indices` [N] (tf.IndexedSlices).
 
-    def __init__(self, values, indices, num_valid=None, unique=False):
-        self.values = values
+    A lookup backward may hand the values over BY ADDRESS instead
+    (dr_pool_grad_rows_grouped): grad_ptr [N] int64 holds the address of
+    each row (bit 0: use as 0.0f + g) and `keep` the buffers they point into.
+    The EV optimizers read such rows in place (dr_ev_apply_grouped_ptr);
+    `values` materialises them on first access (dr_rows_from_ptr)."""
+
+    def __init__(self, values, indices, num_valid=None, unique=False, grad_ptr=None, dim=None,
+                 keep=()):
+        self._values = values
         self.indices = indices
         self.num_valid = num_valid  # optional device int64[1] (<= N)
         self.unique = unique        # indices known distinct (a lookup's backward)
+        self.grad_ptr = grad_ptr
+        self.dim = dim
+        self._keep = keep
+
+    @property
+    def values(self):
+        if self._values is None and self.grad_ptr is not None:
+            n = self.grad_ptr.numel()
+            out = torch.empty((n, self.dim), dtype=torch.float32, device=self.grad_ptr.device)
+            _lib.check(_lib.lib().dr_rows_from_ptr(
+                _lib.ptr(self.grad_ptr), n, _lib.ptr(self.num_valid), self.dim, _lib.ptr(out),
+                _lib.stream_handle(self.grad_ptr.device)))
+            self._values = out
+        return self._values
+
+    @values.setter
+    def values(self, v):
+        self._values = v
+        self.grad_ptr = None
+        self._keep = ()
 
 
 class EmbeddingVariable(object):

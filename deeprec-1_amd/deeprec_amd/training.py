@@ -60,6 +60,15 @@ def _rounds(slices):
     return out
 
 
+def _grad_rows(grp, fn_name):
+    """The gradient argument of a grouped EV apply: by address when every
+    slice came from a row-grouped lookup backward (no [U, D] gradient copy:
+    the kernel reads the pooled gradient in place), else the value blocks."""
+    if all(sl.grad_ptr is not None and sl._values is None for _, sl in grp):
+        return [sl.grad_ptr for _, sl in grp], getattr(lib(), fn_name + "_ptr")
+    return [sl.values.contiguous() for _, sl in grp], getattr(lib(), fn_name)
+
+
 class _Locked(object):
     """use_locking=True (optimizer.py Optimizer(use_locking)): the EV applies
     take each variable's exclusive update lock, as the reference's
@@ -137,7 +146,7 @@ class _Optimizer(object):
         for (_, _), grp in groups.items():
             T = len(grp)
             dev = grp[0][0].device
-            vals = [sl.values.contiguous() for _, sl in grp]
+            grads, fn = _grad_rows(grp, "dr_ev_apply_grouped")
             idxs = [sl.indices.contiguous() for _, sl in grp]
             slots = [self._slots(var) for var, _ in grp]
             P = C.c_void_p * T
@@ -145,9 +154,9 @@ class _Optimizer(object):
             s2 = P(*[b.handle.value if b is not None else None for _, b in slots])
             st = stream_handle(dev)
             with _Locked(self.use_locking, [var.handle.value for var, _ in grp], st):
-                check(lib().dr_ev_apply_grouped(
+                check(fn(
                     self._opt, P(*[var.handle.value for var, _ in grp]), s1, s2, T,
-                    P(*[v.data_ptr() for v in vals]), P(*[i.data_ptr() for i in idxs]),
+                    P(*[v.data_ptr() for v in grads]), P(*[i.data_ptr() for i in idxs]),
                     (C.c_int64 * T)(*[i.numel() for i in idxs]),
                     P(*[ptr(sl.num_valid) for _, sl in grp]), self.lr, b1p, b2p, b1, b2, eps, gs,
                     st))
@@ -261,16 +270,16 @@ class FtrlOptimizer(_Optimizer):
         for (_, _), grp in groups.items():
             T = len(grp)
             dev = grp[0][0].device
-            vals = [sl.values.contiguous() for _, sl in grp]
+            grads, fn = _grad_rows(grp, "dr_ev_apply_ftrl_grouped")
             idxs = [sl.indices.contiguous() for _, sl in grp]
             slots = [self._slots(var) for var, _ in grp]
             P = C.c_void_p * T
             st = stream_handle(dev)
             with _Locked(self.use_locking, [var.handle.value for var, _ in grp], st):
-                check(lib().dr_ev_apply_ftrl_grouped(
+                check(fn(
                     P(*[var.handle.value for var, _ in grp]),
                     P(*[a.handle.value for a, _ in slots]), P(*[b.handle.value for _, b in slots]),
-                    T, P(*[v.data_ptr() for v in vals]), P(*[i.data_ptr() for i in idxs]),
+                    T, P(*[v.data_ptr() for v in grads]), P(*[i.data_ptr() for i in idxs]),
                     (C.c_int64 * T)(*[i.numel() for i in idxs]),
                     P(*[ptr(sl.num_valid) for _, sl in grp]), self.lr, self.l1, self.l2,
                     self.lr_power, self.l2_shrinkage, gs, st))

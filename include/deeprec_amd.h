@@ -229,6 +229,32 @@ size_t dr_pool_grad_grouped_workspace_size(int64_t total_nnz);
 int dr_pool_grad_grouped(const dr_pool_grad_desc* descs_host, int num_tables, int64_t batch,
                          int dim, float* grad_unique, void* ws, size_t ws_bytes, void* stream);
 
+/* Grouped backward keyed by the forward's rows (filter-free EVs resolved    */
+/* without Unique: dr_ev_resolve_grouped with counts == NULL).  rowsel[i] =  */
+/* the row of nnz i (koff order, every row < row_limit; a negative row -- a  */
+/* default served on an exhausted pool -- gets no gradient), keys[i] its id. */
+/* Same results as dr_unique_grouped -> dr_pool_grad_grouped: uniq_out[koff  */
+/* [t] + u] = table t's unique ids in first-occurrence order (Unique's       */
+/* order), num_unique[t] (DEVICE) = U_t, and the gradient of unique u is     */
+/* the ascending-position SparseSegment*Grad sum (bit-exact for runs of up   */
+/* to 256 positions; longer runs: ordered chunk partials, fp32 tolerance).   */
+/* The gradient is returned BY ADDRESS: grad_ptr[koff[t] + u] = address of   */
+/* its fp32 row, bit 0 = use as 0.0f + g.  defer != 0: an unscaled           */
+/* one-position gradient points straight into top_grad (nothing written);   */
+/* every other row is written to grad_unique[koff[t] + u] and points there.  */
+/* desc.idx / desc.num_unique are unused.  grad_unique 16-byte aligned when  */
+/* dim % 4 == 0.  dr_rows_from_ptr materialises the values.                  */
+size_t dr_pool_grad_rows_workspace_size(int64_t total_nnz);
+int dr_pool_grad_rows_grouped(const dr_pool_grad_desc* descs_host, int num_tables, int64_t batch,
+                              int dim, const int64_t* rowsel, int64_t row_limit,
+                              const int64_t* keys, int defer, int64_t* uniq_out,
+                              int64_t* num_unique, uint64_t* grad_ptr, float* grad_unique,
+                              void* ws, size_t ws_bytes, void* stream);
+/* out[i] = row at grad_ptr[i] (+0.0f first when bit 0 is set) for i <      */
+/* min(n, *n_dev) (n_dev DEVICE or NULL); later rows are not written.        */
+int dr_rows_from_ptr(const uint64_t* grad_ptr, int64_t n, const int64_t* n_dev, int dim,
+                     float* out, void* stream);
+
 /* Backward of the grouped pooling for one table, deterministic:             */
 /* grad_unique[u] = sum over k with idx[k]==u (ascending k) of               */
 /*   top_grad[bag(k)] * scale(bag)  (scale: 1, 1/n, 1/sqrt(n) as the         */
@@ -310,6 +336,10 @@ int dr_ev_size(dr_ev* ev, int64_t* size_host, void* stream);
 int dr_ev_shrink(dr_ev* ev, int64_t global_step, float l2_weight_threshold,
                  int64_t* removed_host, void* stream);
 int64_t dr_ev_dim(dr_ev* ev);
+/* Row-pool capacity of the EV's key space (host value, no sync): every row  */
+/* index the EV has handed out is below it (the row_limit of                 */
+/* dr_pool_grad_rows_grouped).                                               */
+int64_t dr_ev_row_capacity(dr_ev* ev);
 /* Ensures room for `extra` new keys (may rehash/grow; syncs when it must). */
 int dr_ev_reserve(dr_ev* ev, int64_t extra, void* stream);
 
@@ -417,6 +447,18 @@ int dr_ev_apply_grouped(int optimizer, dr_ev* const* vars, dr_ev* const* slot1,
                         const int64_t* const* n_dev, float lr, float beta1_power,
                         float beta2_power, float beta1, float beta2, float epsilon,
                         int64_t global_step, void* stream);
+/* The same with each gradient row given BY ADDRESS: grad_ptrs[t][i] is the */
+/* address of key i's [dim] fp32 gradient row; bit 0 set = the row is used  */
+/* as 0.0f + g (the reference's unsorted segment sum starting from 0).  The  */
+/* grad_ptr output of dr_pool_grad_rows_grouped: the optimizer reads the     */
+/* pooled gradient in place (no [U, dim] gradient written and read back).   */
+/* Rows must be 16-byte aligned when dim % 4 == 0.                           */
+int dr_ev_apply_grouped_ptr(int optimizer, dr_ev* const* vars, dr_ev* const* slot1,
+                            dr_ev* const* slot2, int num_tables, const uint64_t* const* grad_ptrs,
+                            const int64_t* const* keys, const int64_t* n_host,
+                            const int64_t* const* n_dev, float lr, float beta1_power,
+                            float beta2_power, float beta1, float beta2, float epsilon,
+                            int64_t global_step, void* stream);
 /* KvResourceSparseApplyFtrl / FtrlV2 (training_ali_ops.cc:167-331; op defs  */
 /* core/ops/training_ali_ops.cc): accum / linear are slot EVs of var;        */
 /* l2_shrinkage 0 = Ftrl, > 0 = FtrlV2.  The row norm of `linear` is an fp32 */
@@ -430,6 +472,12 @@ int dr_ev_apply_ftrl_grouped(dr_ev* const* vars, dr_ev* const* accums, dr_ev* co
                              const int64_t* const* n_dev, float lr, float l1, float l2,
                              float lr_power, float l2_shrinkage, int64_t global_step,
                              void* stream);
+int dr_ev_apply_ftrl_grouped_ptr(dr_ev* const* vars, dr_ev* const* accums,
+                                 dr_ev* const* linears, int num_tables,
+                                 const uint64_t* const* grad_ptrs, const int64_t* const* keys,
+                                 const int64_t* n_host, const int64_t* const* n_dev, float lr,
+                                 float l1, float l2, float lr_power, float l2_shrinkage,
+                                 int64_t global_step, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* FusedEmbeddingLocalSparseLookUp[Grad]                                     */

@@ -1,0 +1,274 @@
+"""GPU: the row-grouped training backward (dr_pool_grad_rows_grouped) and the
+by-address EV applies (dr_ev_apply_grouped_ptr / _ftrl_grouped_ptr).
+
+The training forward of filter-free EVs skips the Unique and the backward
+regroups by the resolved rows.  It must give the IndexedSlices the Unique
+path gives -- unique ids in first-occurrence order (Unique's order, bit-exact
+vs the oracle), U_t, and the SparseSegment*Grad values (bit-exact for runs of
+<= 256 positions) -- and the optimizer reading the gradient rows by address
+must leave the EVs bit-identical to the value-block apply.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def dr():
+    import deeprec_amd
+    deeprec_amd.load()
+    deeprec_amd.set_validate(True)
+    assert torch.cuda.is_available()
+    return deeprec_amd
+
+
+def T(x, dtype=None):
+    return torch.as_tensor(np.asarray(x), device=DEV, dtype=dtype)
+
+
+def H(t):
+    return t.detach().cpu().numpy()
+
+
+class _Path(object):
+    """Select the training path of embedding_ops for a block."""
+
+    def __init__(self, rows):
+        self.rows = rows
+
+    def __enter__(self):
+        from deeprec_amd import embedding_ops as eo
+        self.old = eo._ROWS_GRAD
+        eo._ROWS_GRAD = self.rows
+
+    def __exit__(self, *a):
+        from deeprec_amd import embedding_ops as eo
+        eo._ROWS_GRAD = self.old
+
+
+def _sparse(rng, B, H_, vocab, allow_empty=False):
+    lo = 0 if allow_empty else 1
+    lens = rng.integers(lo, H_ + 1, B)
+    rows = np.repeat(np.arange(B), lens)
+    cols = np.concatenate([np.arange(n) for n in lens]) if lens.sum() else np.zeros(0, np.int64)
+    ind = np.stack([rows, cols], 1).astype(np.int64)
+    v = rng.integers(0, vocab, rows.shape[0]).astype(np.int64)
+    return ind, v, (B, H_)
+
+
+def _feature_set(dr, rng, tag, F, B, D, onehot, vocab, shared_keys):
+    evs, sps, raw = [], [], []
+    for f in range(F):
+        evs.append(dr.EmbeddingVariable("%s_%d" % (tag, f), D, 0.1 * (f + 1)))
+        if onehot:
+            ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+            v = (shared_keys if shared_keys is not None else
+                 rng.integers(0, vocab, B).astype(np.int64))
+            shape = (B, 1)
+        else:
+            ind, v, shape = _sparse(rng, B, 5, vocab, allow_empty=True)
+        sps.append(dr.SparseTensor(T(ind), T(v), shape))
+        raw.append((ind, v))
+    return evs, sps, raw
+
+
+@pytest.mark.parametrize("onehot", [True, False])
+@pytest.mark.parametrize("comb", ["sum", "mean", "sqrtn"])
+def test_rows_backward_matches_segment_grad(dr, orc, onehot, comb):
+    """Grouped rows path vs the oracle Unique + SparseSegment*Grad: indices
+    (first-occurrence order), U and values bit-exact.  Every feature inserts
+    the same keys in the same order, so equal rows recur across tables (the
+    regrouping must split runs at table boundaries)."""
+    rng = np.random.default_rng(101 + int(onehot))
+    B, D, F = 300, 32, 4
+    shared = rng.integers(0, 90, B).astype(np.int64) if onehot else None
+    evs, sps, raw = _feature_set(dr, rng, "rbw_%d_%s" % (int(onehot), comb), F, B, D, onehot,
+                                 120, shared)
+    out = dr.embedding_lookup_sparse_multi(evs, sps, combiner=comb)
+    g = rng.standard_normal((B, F * D)).astype(np.float32)
+    out.backward(T(g))
+    for f in range(F):
+        sl = evs[f].pending_grads.pop()
+        assert sl.grad_ptr is not None          # the rows path ran
+        U = int(sl.num_valid.item())
+        uids, idx = orc.unique(raw[f][1])
+        assert U == uids.size
+        assert H(sl.indices[:U]).tolist() == uids.tolist()
+        ref = orc.sparse_segment_reduce_grad(np.ascontiguousarray(g[:, f * D:(f + 1) * D]), idx,
+                                             raw[f][0][:, 0].astype(np.int32), U, comb)
+        np.testing.assert_array_equal(H(sl.values[:U]), ref)
+
+
+def test_rows_backward_single_feature_weighted(dr, orc):
+    """One EV feature with weights (embedding_lookup_sparse, not the multi
+    API) through the rows path: the weighted grad is materialised."""
+    rng = np.random.default_rng(7)
+    B, D = 80, 16
+    for comb in ("sum", "mean", "sqrtn"):
+        ev = dr.EmbeddingVariable("rw_" + comb, D, 0.2)
+        ind, v, shape = _sparse(rng, B, 6, 50)
+        w = rng.uniform(0.5, 2.0, v.size).astype(np.float32)
+        out = dr.embedding_lookup_sparse(ev, dr.SparseTensor(T(ind), T(v), shape),
+                                         sp_weights=dr.SparseTensor(T(ind), T(w), shape),
+                                         combiner=comb)
+        g = rng.standard_normal((B, D)).astype(np.float32)
+        out.backward(T(g))
+        sl = ev.pending_grads.pop()
+        U = int(sl.num_valid.item())
+        got = H(sl.values[:U])
+        keys = H(sl.indices[:U])
+        # the same lookup on the Unique path is the reference of this check
+        ev2 = dr.EmbeddingVariable("rw2_" + comb, D, 0.2)
+        with _Path(False):
+            out2 = dr.embedding_lookup_sparse(ev2, dr.SparseTensor(T(ind), T(v), shape),
+                                              sp_weights=dr.SparseTensor(T(ind), T(w), shape),
+                                              combiner=comb)
+            out2.backward(T(g))
+        sl2 = ev2.pending_grads.pop()
+        assert sl2.grad_ptr is None
+        U2 = int(sl2.num_valid.item())
+        assert U == U2 and keys.tolist() == H(sl2.indices[:U]).tolist()
+        np.testing.assert_array_equal(got, H(sl2.values[:U]))
+        np.testing.assert_array_equal(H(out), H(out2))
+
+
+@pytest.mark.parametrize("D", [18, 32])
+def test_rows_backward_long_runs(dr, orc, D):
+    """Hot ids: runs of 5000 / 256 / 257 / 768 / 200 / 511 positions.  Runs of
+    <= 256 positions are bit-exact; longer ones are ordered chunk partials
+    (fp32 tolerance 1e-5 rel / 1e-3 abs, sums of up to 5000 N(0,1) terms)."""
+    rng = np.random.default_rng(41)
+    runs = {0: 5000, 1: 256, 2: 257, 3: 768, 4: 200, 5: 511}
+    v = np.concatenate([np.full(n, k, np.int64) for k, n in runs.items()] +
+                       [rng.integers(6, 400, 3000).astype(np.int64)])
+    rng.shuffle(v)
+    B = v.size
+    evs, sps = [], []
+    for f in range(3):
+        evs.append(dr.EmbeddingVariable("rlong_%d_%d" % (D, f), D, 0.1))
+        ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+        sps.append(dr.SparseTensor(T(ind), T(v), (B, 1)))
+    out = dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum")
+    g = rng.standard_normal((B, 3 * D)).astype(np.float32)
+    out.backward(T(g))
+    uids, idx = orc.unique(v)
+    seg = np.arange(B, dtype=np.int32)
+    long_keys = [k for k, n in runs.items() if n > 256]
+    for f in range(3):
+        sl = evs[f].pending_grads.pop()
+        U = int(sl.num_valid.item())
+        assert H(sl.indices[:U]).tolist() == uids.tolist()
+        ref = orc.sparse_segment_reduce_grad(np.ascontiguousarray(g[:, f * D:(f + 1) * D]), idx,
+                                             seg, U, "sum")
+        got = H(sl.values[:U])
+        pos = {int(k): i for i, k in enumerate(uids)}
+        exact = [i for i in range(U) if int(uids[i]) not in long_keys]
+        np.testing.assert_array_equal(got[exact], ref[exact])
+        for k in long_keys:
+            np.testing.assert_allclose(got[pos[k]], ref[pos[k]], rtol=1e-5, atol=1e-3)
+    dr.status_check()
+
+
+def test_rows_backward_run_straddles_chunk_boundary(dr, orc):
+    """Runs of 2..255 positions land across multiples of 256 of the sorted
+    array (400 ids, ~50 k positions): none may be cut, all bit-exact."""
+    rng = np.random.default_rng(43)
+    lens = rng.integers(2, 256, 400)
+    v = np.repeat(np.arange(400, dtype=np.int64) * 7 + 3, lens)
+    rng.shuffle(v)
+    B = v.size
+    ev = dr.EmbeddingVariable("rstr", 8, 0.1)
+    ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+    out = dr.embedding_lookup_sparse(ev, dr.SparseTensor(T(ind), T(v), (B, 1)), combiner="sum")
+    g = rng.standard_normal((B, 8)).astype(np.float32)
+    out.backward(T(g))
+    sl = ev.pending_grads.pop()
+    U = int(sl.num_valid.item())
+    uids, idx = orc.unique(v)
+    assert H(sl.indices[:U]).tolist() == uids.tolist()
+    ref = orc.sparse_segment_reduce_grad(g, idx, np.arange(B, dtype=np.int32), U, "sum")
+    np.testing.assert_array_equal(H(sl.values[:U]), ref)
+
+
+def _export(ev):
+    k, vals = ev.export()[:2]
+    k, vals = H(k), H(vals)
+    o = np.argsort(k)
+    return k[o], vals[o]
+
+
+@pytest.mark.parametrize("opt_name", ["sgd", "adagrad", "adam", "ftrl"])
+@pytest.mark.parametrize("onehot", [True, False])
+def test_rows_train_step_equals_unique_path(dr, opt_name, onehot):
+    """Three training steps (lookup -> backward -> apply) on the rows path
+    (by-address apply) and on the Unique path (value-block apply): EV
+    contents, slot contents and outputs bit-identical."""
+    rng = np.random.default_rng(53 + int(onehot))
+    B, D, F = 257, 16, 3
+
+    def make_opt():
+        return {"sgd": lambda: dr.GradientDescentOptimizer(0.05),
+                "adagrad": lambda: dr.AdagradOptimizer(0.05),
+                "adam": lambda: dr.AdamOptimizer(0.01),
+                "ftrl": lambda: dr.FtrlOptimizer(0.05, l1_regularization_strength=0.01,
+                                                 l2_regularization_strength=0.02)}[opt_name]()
+
+    batches = []
+    for _ in range(3):
+        sps = []
+        for f in range(F):
+            if onehot:
+                ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+                v = rng.integers(0, 70, B).astype(np.int64)
+                sps.append((ind, v, (B, 1)))
+            else:
+                sps.append(_sparse(rng, B, 4, 70, allow_empty=True))
+        batches.append((sps, rng.standard_normal((B, F * D)).astype(np.float32)))
+    results = []
+    for rows in (True, False):
+        evs = [dr.EmbeddingVariable("rts_%s_%d_%d_%d" % (opt_name, int(onehot), int(rows), f), D,
+                                    0.05) for f in range(F)]
+        opt = make_opt()
+        outs = []
+        with _Path(rows):
+            for step, (sps, g) in enumerate(batches):
+                st = [dr.SparseTensor(T(i), T(v), s) for i, v, s in sps]
+                out = dr.embedding_lookup_sparse_multi(evs, st, combiner="mean")
+                out.backward(T(g))
+                assert (evs[0].pending_grads[-1].grad_ptr is not None) == rows
+                opt.apply_gradients(evs, global_step=step)
+                outs.append(H(out))
+        torch.cuda.synchronize()
+        results.append((outs, [_export(e) for e in evs],
+                        [[_export(s) for s in opt._slots(e) if s is not None] for e in evs]))
+    (o1, e1, s1), (o2, e2, s2) = results
+    for a, b in zip(o1, o2):
+        np.testing.assert_array_equal(a, b)
+    for (k1, v1), (k2, v2) in zip(e1, e2):
+        np.testing.assert_array_equal(k1, k2)
+        np.testing.assert_array_equal(v1, v2)
+    for a, b in zip(s1, s2):
+        for (k1, v1), (k2, v2) in zip(a, b):
+            np.testing.assert_array_equal(k1, k2)
+            np.testing.assert_array_equal(v1, v2)
+    dr.status_check()
+
+
+def test_rows_from_ptr_zero_sign(dr):
+    """Bit 0 of a gradient address = 0.0f + g: -0.0 becomes +0.0 (the
+    reference's unsorted segment sum starts from 0); without it the sign
+    is kept."""
+    from deeprec_amd._lib import lib, ptr, stream_handle
+    src = torch.tensor([[-0.0, 1.0, -2.0, -0.0]], device=DEV)
+    a = src.data_ptr()
+    gp = torch.tensor([a | 1, a], dtype=torch.int64, device=DEV)
+    out = torch.empty((2, 4), device=DEV)
+    assert lib().dr_rows_from_ptr(ptr(gp), 2, None, 4, ptr(out), stream_handle(DEV)) == 0
+    o = H(out)
+    assert not np.signbit(o[0, 0]) and not np.signbit(o[0, 3])
+    assert np.signbit(o[1, 0]) and np.signbit(o[1, 3])
+    np.testing.assert_array_equal(o[:, 1:3], [[1.0, -2.0], [1.0, -2.0]])
