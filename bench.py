@@ -201,7 +201,7 @@ def main():
         # N * B (an owner serving every rank, dr_xgmi_serve), with slack for
         # the asynchronously mirrored row count (no host sync per step)
         ev = dr.EmbeddingVariable("table%d" % t, D, 0.0, device=dev,
-                                  capacity=R + max(1 << 19, 4 * world * B))
+                                  capacity=R + max(1 << 20, 12 * world * B))
         # rank r owns keys k % world == r of the keyspace [0, R * world)
         ev.insert_synthetic(rank, R, seed=1000 + t, key_stride=world)
         evs.append(ev)
@@ -443,18 +443,39 @@ def main():
         for i in range(2):
             tstep(i)
         torch.cuda.synchronize()
+        tgraph = None
+        if not args.no_graph:
+            # NBATCH whole training steps (forward, autograd backward, KV
+            # apply) captured as one hipGraph: every kernel of every step runs
+            # on replay, only the host's per-launch work is gone
+            for ev in evs:   # worst-case adds of the captured steps (resolve + apply)
+                ev.reserve(2 * NBATCH * B)
+            tgraph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(tgraph):
+                for i in range(NBATCH):
+                    tstep(i)
+            tgraph.replay()
+            torch.cuda.synchronize()
+            dr.status_check(dev)
+        nsteps = args.train_steps
         t0 = time.perf_counter()
-        for i in range(args.train_steps):
-            tstep(i)
+        if tgraph is not None:
+            nsteps = -(-nsteps // NBATCH) * NBATCH
+            for i in range(0, nsteps, NBATCH):
+                tgraph.replay()
+        else:
+            for i in range(nsteps):
+                tstep(i)
         torch.cuda.synchronize()
         tel = time.perf_counter() - t0
         dr.status_check(dev)
-        tms = tel / args.train_steps * 1e3
+        tms = tel / nsteps * 1e3
         train = {"ms_per_step": round(tms, 4), "samples_per_s": round(B / (tms * 1e-3), 1),
-                 "lookups_per_s": round(T * B / (tms * 1e-3), 1),
+                 "lookups_per_s": round(T * B / (tms * 1e-3), 1), "steps": nsteps,
+                 "graph": tgraph is not None,
                  "step": "embedding layer training step: embedding_lookup_sparse_multi forward "
-                         "(grouped Unique, EV resolve, pool) + backward (grouped segment grad) "
-                         "+ KV SGD apply, %d EVs, B=%d" % (T, B)}
+                         "(EV resolve of every id, pool) + backward (row-grouped segment grad, "
+                         "gradients by address) + KV SGD apply, %d EVs, B=%d" % (T, B)}
         log("train step: %s" % json.dumps(train))
 
     # ---- dominant kernel: the fused one-hot EV lookup, timed alone --------

@@ -148,5 +148,8 @@ size_t scan_ws_bytes(int64_t n);
 // Exclusive scan of int32 values into int32 out; *total (device int64) = sum.
 int scan_exclusive_i32(const int32_t* in, int32_t* out, int64_t n, const int64_t* n_dev,
                        int64_t* total, void* ws, hipStream_t st);
+// Exclusive scan of the marks (in[i] != -1) of a "-1 = empty" array.
+int scan_exclusive_marks(const int32_t* in, int32_t* out, int64_t n, int64_t* total, void* ws,
+                         hipStream_t st);
 
 }  // namespace dr

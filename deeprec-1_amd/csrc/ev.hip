@@ -1033,6 +1033,14 @@ static int grow(EvShared* s, int64_t need, hipStream_t st) {
   }
   if (need > s->row_cap) {
     int64_t nrc = std::max(need, s->row_cap * 2);
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess &&
+        (size_t)nrc * s->dim * sizeof(float) > fr) {
+      set_error("EV row pool growth %lld -> %lld rows (need %lld) needs %zu bytes, %zu free",
+                (long long)s->row_cap, (long long)nrc, (long long)need,
+                (size_t)nrc * s->dim * sizeof(float), fr);
+      return DR_RESOURCE_EXHAUSTED;
+    }
     for (int c = 0; c < kMaxCols; ++c) {
       if (!s->pools[c]) continue;
       float* np = nullptr;

@@ -13,11 +13,12 @@
 //   1. (row of nnz i, i) pairs, stable radix sort by row.  Positions are
 //      table-major and the sort is stable, so the positions of one (table,
 //      row) are contiguous and ascending: a run.
-//   2. flag[first position of each run] = 1; exclusive scan over positions
+//   2. mark[first position of each run] = its sorted index; exclusive scan
+//      of the marks over positions
 //      -> the first-occurrence rank of every unique id of table t, i.e. the
 //      index Unique would have given it; U_t from the scan.
 //   3. one position pass emits the unique ids in that order.
-//   4. per run, the gradient (rows_classify_kernel, lane per position): a
+//   4. per run, the gradient (rows_emit_kernel, position order): a
 //      one-position run whose value needs no arithmetic is handed on BY
 //      ADDRESS (grad_ptr[o] = the pooled-grad row, bit 0 = "add +0.0f", the
 //      0 + x of the reference's unsorted sum), so the optimizer reads the
@@ -67,36 +68,66 @@ __global__ void rows_keys_kernel(const int64_t* __restrict__ rowsel, int64_t N, 
   // (RESOURCE_EXHAUSTED already latched by the resolve): no gradient row
   kin[i] = (r >= 0 && r < row_limit) ? (uint64_t)r : sentinel;
   vin[i] = (int32_t)i;
-  flags[i] = 0;
+  flags[i] = -1;
 }
 
+// Wave-aggregated append of p to the worklist.
+__device__ __forceinline__ void work_push(bool push, int64_t p, int32_t* __restrict__ work,
+                                          int32_t* __restrict__ nwork) {
+  const uint64_t m = __ballot(push);
+  if (!m) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  int at = 0;
+  if (lane == leader) at = atomicAdd(nwork, __popcll(m));
+  at = __shfl(at, leader, 64);
+  if (push) work[at + __popcll(m & lanemask_lt())] = (int32_t)p;
+}
+
+// Sorted order, lane per position: mark[i] = p (| 1 << 31 for a one-position
+// run) at the run head's original position i; heads of longer runs and
+// every multiple of the chunk inside a run (a possible later chunk of a
+// long run) go straight to the worklist of rows_work_kernel.
 __global__ void rows_heads_kernel(RowsGroup g, int T, const uint64_t* __restrict__ skey,
                                   const int32_t* __restrict__ perm, uint64_t sentinel,
-                                  int32_t* __restrict__ flags) {
+                                  int32_t* __restrict__ mark, int32_t* __restrict__ work,
+                                  int32_t* __restrict__ nwork) {
   __shared__ int64_t sk[DR_MAX_GROUP + 1];
   if (threadIdx.x <= T) sk[threadIdx.x] = g.koff[threadIdx.x];
   __syncthreads();
   const int64_t N = sk[T];
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= N) return;
-  const uint64_t u = skey[p];
-  if (u == sentinel) return;
-  const int32_t i = perm[p];
-  bool head = p == 0;
-  if (!head) {
-    const int32_t j = perm[p - 1];
-    head = skey[p - 1] != u || tab_of(sk, T, j) != tab_of(sk, T, i);
+  bool push = false;
+  if (p < N) {
+    const int64_t pm = p > 0 ? p - 1 : 0, pn = p + 1 < N ? p + 1 : N - 1;
+    const uint64_t u = skey[p], um = skey[pm], un = skey[pn];
+    const int32_t i = perm[p], im = perm[pm], in = perm[pn];
+    const int t = tab_of(sk, T, i);
+    const bool valid = u != sentinel;
+    const bool head = valid && (p == 0 || um != u || tab_of(sk, T, im) != t);
+    const bool last = p + 1 >= N || un != u || tab_of(sk, T, in) != t;
+    if (head) mark[i] = (int32_t)p | (last ? (int32_t)0x80000000 : 0);
+    push = valid && ((head && !last) || (!head && p % kRowsChunk == 0));
   }
-  if (head) flags[i] = 1;
+  work_push(push, p, work, nwork);
 }
 
-// Position order: unique ids in first-occurrence order per table, U_t, and
-// the scan base of every table (read by the grad kernel).
-__global__ void rows_emit_kernel(RowsGroup g, int T, const int64_t* __restrict__ keys,
-                                 const int32_t* __restrict__ flags,
-                                 const int32_t* __restrict__ ex, const int64_t* __restrict__ total,
-                                 int64_t* __restrict__ uniq_out, int64_t* __restrict__ num_unique,
-                                 int32_t* __restrict__ base) {
+// Position order: unique ids in first-occurrence order per table, U_t, the
+// scan base of every table, and the gradient of each one-position run: by
+// address when its value needs no arithmetic (sum, or mean/sqrtn of a
+// one-id bag, unweighted: grad_ptr[o] = the pooled-grad row, bit 0 = "add
+// +0.0f", the 0 + x of the reference's unsorted sum), else a worklist
+// entry.  All-distinct sum lookups (the Criteo shape) leave the worklist
+// empty and the backward moves no embedding-row bytes at all.
+__global__ __launch_bounds__(256) void rows_emit_kernel(
+    RowsGroup g, int T, int64_t B, const int64_t* __restrict__ keys,
+    const int32_t* __restrict__ mark, const int32_t* __restrict__ ex,
+    const int64_t* __restrict__ total, int defer, int64_t* __restrict__ uniq_out,
+    int64_t* __restrict__ num_unique, int32_t* __restrict__ base, uint64_t* __restrict__ gptr,
+    int32_t* __restrict__ work, int32_t* __restrict__ nwork, int* st) {
+  __shared__ dr_pool_grad_desc sd[DR_MAX_GROUP];
+  if (threadIdx.x < T) sd[threadIdx.x] = g.d[threadIdx.x];
+  __syncthreads();
   const int64_t N = g.koff[T];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i <= T) {   // base[t] = first-occurrence count before table t
@@ -110,10 +141,28 @@ __global__ void rows_emit_kernel(RowsGroup g, int T, const int64_t* __restrict__
     const int64_t bb = b < N ? ex[b] : *total;
     num_unique[t] = bb - ba;
   }
-  if (i >= N || !flags[i]) return;
-  const int t = table_of(g.koff, T, i, (int64_t)blockIdx.x * blockDim.x);
-  const int64_t a = g.koff[t];
-  uniq_out[a + ex[i] - ex[a]] = keys[i];
+  const int32_t mk = i < N ? mark[i] : -1;
+  bool push = false;
+  if (mk != -1) {
+    const int t = table_of(g.koff, T, i, (int64_t)blockIdx.x * blockDim.x);
+    const int64_t a = g.koff[t];
+    const int64_t o = a + ex[i] - ex[a];
+    uniq_out[o] = keys[i];
+    if (mk < 0) {   // one-position run
+      const dr_pool_grad_desc& d = sd[t];
+      const int64_t k = i - a;
+      const int64_t r = d.seg ? d.seg[k * d.seg_stride] : k;
+      const bool okr = r >= 0 && r < B;
+      const int mode = d.combiner == DR_COMBINER_SUM ? 0 : 1;
+      bool dfr = defer && okr && !d.weights;
+      if (dfr && mode != 0) dfr = !d.bag_off || d.bag_off[r + 1] - d.bag_off[r] == 1;
+      if (dfr)
+        gptr[o] = (uint64_t)(uintptr_t)(d.top_grad + r * d.top_stride) | (mode == 0 ? 1u : 0u);
+      else
+        push = true;   // (an invalid bag latches there)
+    }
+  }
+  work_push(push, (int64_t)(mk & 0x7FFFFFFF), work, nwork);
 }
 
 // Is the run (u, t) through inner position m (a multiple of kRowsChunk, not
@@ -143,68 +192,6 @@ __device__ bool run_is_long(const uint64_t* __restrict__ skey, const int32_t* __
       hi = mid - 1;
   }
   return lo - s + 1 > kRowsChunk;
-}
-
-// Lane per sorted position.  A one-position run whose value needs no
-// arithmetic (sum, or mean/sqrtn of a one-id bag, unweighted) is handed on by
-// address at once; every other run head, and every multiple of the chunk
-// inside a run (a possible later chunk of a long run), goes to the worklist
-// of rows_work_kernel.  All-distinct sum lookups (the Criteo shape) leave
-// the worklist empty: the pass moves no embedding-row bytes at all.
-__global__ __launch_bounds__(256) void rows_classify_kernel(
-    RowsGroup g, int T, int64_t B, const uint64_t* __restrict__ skey,
-    const int32_t* __restrict__ perm, const int32_t* __restrict__ ex,
-    const int32_t* __restrict__ base, uint64_t sentinel, int defer,
-    uint64_t* __restrict__ gptr, int32_t* __restrict__ work, int32_t* __restrict__ nwork,
-    int* st) {
-  __shared__ dr_pool_grad_desc sd[DR_MAX_GROUP];
-  __shared__ int64_t sk[DR_MAX_GROUP + 1];
-  __shared__ int32_t sb[DR_MAX_GROUP + 1];
-  if (threadIdx.x < T) sd[threadIdx.x] = g.d[threadIdx.x];
-  if (threadIdx.x <= T) {
-    sk[threadIdx.x] = g.koff[threadIdx.x];
-    sb[threadIdx.x] = base[threadIdx.x];
-  }
-  __syncthreads();
-  const int64_t N = sk[T];
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool push = false;
-  if (p < N) {
-    const int64_t pm = p > 0 ? p - 1 : 0, pn = p + 1 < N ? p + 1 : N - 1;
-    const uint64_t u = skey[p], um = skey[pm], un = skey[pn];
-    const int32_t i = perm[p], im = perm[pm], in = perm[pn];
-    const int t = tab_of(sk, T, i);
-    const bool valid = u != sentinel;
-    const bool rhead = valid && (p == 0 || um != u || tab_of(sk, T, im) != t);
-    const bool last = p + 1 >= N || un != u || tab_of(sk, T, in) != t;
-    if (rhead && last) {
-      const dr_pool_grad_desc& d = sd[t];
-      const int64_t k = (int64_t)i - sk[t];
-      const int64_t r = d.seg ? d.seg[k * d.seg_stride] : k;
-      const bool okr = r >= 0 && r < B;
-      if (!okr) latch(st, DR_INVALID_ARGUMENT);
-      const int mode = d.combiner == DR_COMBINER_SUM ? 0 : 1;
-      bool dfr = defer && okr && !d.weights;
-      if (dfr && mode != 0) dfr = !d.bag_off || d.bag_off[r + 1] - d.bag_off[r] == 1;
-      if (dfr) {
-        const int64_t o = sk[t] + (int64_t)ex[i] - sb[t];
-        gptr[o] = (uint64_t)(uintptr_t)(d.top_grad + r * d.top_stride) | (mode == 0 ? 1u : 0u);
-      } else {
-        push = true;
-      }
-    } else if (rhead || (valid && p % kRowsChunk == 0)) {
-      push = true;
-    }
-  }
-  const uint64_t m = __ballot(push);
-  if (m) {   // wave-aggregated append
-    const int lane = threadIdx.x & 63;
-    const int leader = __ffsll((unsigned long long)m) - 1;
-    int at = 0;
-    if (lane == leader) at = atomicAdd(nwork, __popcll(m));
-    at = __shfl(at, leader, 64);
-    if (push) work[at + __popcll(m & lanemask_lt())] = (int32_t)p;
-  }
 }
 
 // G lanes per worklist entry (a sorted position c0): a run head sums its run
@@ -554,15 +541,14 @@ int dr_pool_grad_rows_grouped(const dr_pool_grad_desc* descs_host, int num_table
   DR_LAUNCH_CHECK();
   int rc = dr_sort_pairs(w.kin, w.vin, w.kout, w.perm, n, 0, rb, w.sort_ws, w.sort_bytes, stream);
   if (rc) return rc;
-  hipLaunchKernelGGL(rows_heads_kernel, dim3(nb), dim3(256), 0, s, g, num_tables, w.kout, w.perm,
-                     sentinel, w.flags);
-  rc = scan_exclusive_i32(w.flags, w.ex, n, nullptr, w.total, w.scan_ws, s);
-  if (rc) return rc;
-  hipLaunchKernelGGL(rows_emit_kernel, dim3(nb), dim3(256), 0, s, g, num_tables, keys, w.flags,
-                     w.ex, w.total, uniq_out, num_unique, w.base);
   hipLaunchKernelGGL(rows_zero_i32, dim3(1), dim3(1), 0, s, w.nlong, w.nwork);
-  hipLaunchKernelGGL(rows_classify_kernel, dim3(nb), dim3(256), 0, s, g, num_tables, batch,
-                     w.kout, w.perm, w.ex, w.base, sentinel, defer, grad_ptr, w.work, w.nwork, st);
+  hipLaunchKernelGGL(rows_heads_kernel, dim3(nb), dim3(256), 0, s, g, num_tables, w.kout, w.perm,
+                     sentinel, w.flags, w.work, w.nwork);
+  rc = scan_exclusive_marks(w.flags, w.ex, n, w.total, w.scan_ws, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(rows_emit_kernel, dim3(nb), dim3(256), 0, s, g, num_tables, batch, keys,
+                     w.flags, w.ex, w.total, defer, uniq_out, num_unique, w.base, grad_ptr, w.work,
+                     w.nwork, st);
   DR_LAUNCH_CHECK();
   if (aligned) {
     const int d4 = dim / 4;

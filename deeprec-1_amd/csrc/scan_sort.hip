@@ -38,6 +38,14 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int* lds /*[4]*/, int
   return wprefix + x - v;
 }
 
+// FLAG: the scanned value of element i is (in[i] != -1) -- a count of the
+// set entries of a "-1 = empty" marker array.
+template <bool FLAG>
+__device__ __forceinline__ int scan_val(int32_t v) {
+  return FLAG ? (v != -1) : v;
+}
+
+template <bool FLAG>
 __global__ void scan_reduce_kernel(const int32_t* __restrict__ in, int64_t n,
                                    const int64_t* n_dev, int32_t* __restrict__ bsum) {
   __shared__ int lds[4];
@@ -46,7 +54,7 @@ __global__ void scan_reduce_kernel(const int32_t* __restrict__ in, int64_t n,
   int s = 0;
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k)
-    if (base + k < ne) s += in[base + k];
+    if (base + k < ne) s += scan_val<FLAG>(in[base + k]);
   int tot;
   block_exclusive_scan(s, lds, &tot);
   if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
@@ -67,6 +75,7 @@ __global__ void scan_bsum_kernel(int32_t* __restrict__ bsum, int64_t nb, int64_t
   if (threadIdx.x == 0 && total) *total = carry;
 }
 
+template <bool FLAG>
 __global__ void scan_apply_kernel(const int32_t* __restrict__ in, int32_t* __restrict__ out,
                                   int64_t n, const int64_t* n_dev,
                                   const int32_t* __restrict__ bsum) {
@@ -77,7 +86,7 @@ __global__ void scan_apply_kernel(const int32_t* __restrict__ in, int32_t* __res
   int s = 0;
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
-    v[k] = (base + k < ne) ? in[base + k] : 0;
+    v[k] = (base + k < ne) ? scan_val<FLAG>(in[base + k]) : 0;
     s += v[k];
   }
   int tot;
@@ -93,21 +102,32 @@ size_t scan_ws_bytes(int64_t n) {
   return (size_t)((ceil_div(n > 0 ? n : 1, kScanTile) + 64) * sizeof(int32_t)) + 256;
 }
 
-int scan_exclusive_i32(const int32_t* in, int32_t* out, int64_t n, const int64_t* n_dev,
-                       int64_t* total, void* ws, hipStream_t st) {
+template <bool FLAG>
+static int scan_exclusive(const int32_t* in, int32_t* out, int64_t n, const int64_t* n_dev,
+                          int64_t* total, void* ws, hipStream_t st) {
   if (n <= 0) {
     if (total) return fill_bytes(total, 0, sizeof(int64_t), st);
     return DR_OK;
   }
   const int64_t nb = ceil_div(n, kScanTile);
   int32_t* bsum = static_cast<int32_t*>(ws);
-  hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(kScanThreads), 0, st, in, n,
-                     n_dev, bsum);
-  hipLaunchKernelGGL(scan_bsum_kernel, dim3(1), dim3(kScanThreads), 0, st, bsum, nb, total);
-  hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)nb), dim3(kScanThreads), 0, st, in, out,
+  hipLaunchKernelGGL(scan_reduce_kernel<FLAG>, dim3((unsigned)nb), dim3(kScanThreads), 0, st, in,
                      n, n_dev, bsum);
+  hipLaunchKernelGGL(scan_bsum_kernel, dim3(1), dim3(kScanThreads), 0, st, bsum, nb, total);
+  hipLaunchKernelGGL(scan_apply_kernel<FLAG>, dim3((unsigned)nb), dim3(kScanThreads), 0, st, in,
+                     out, n, n_dev, bsum);
   DR_LAUNCH_CHECK();
   return DR_OK;
+}
+
+int scan_exclusive_i32(const int32_t* in, int32_t* out, int64_t n, const int64_t* n_dev,
+                       int64_t* total, void* ws, hipStream_t st) {
+  return scan_exclusive<false>(in, out, n, n_dev, total, ws, st);
+}
+
+int scan_exclusive_marks(const int32_t* in, int32_t* out, int64_t n, int64_t* total, void* ws,
+                         hipStream_t st) {
+  return scan_exclusive<true>(in, out, n, nullptr, total, ws, st);
 }
 
 // ---------------------------------------------------------------------------

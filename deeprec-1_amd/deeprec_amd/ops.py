@@ -21,7 +21,9 @@ def set_validate(on):
 
 
 def _post(device):
-    if _VALIDATE:
+    # (no validation sync while a hipGraph is being captured: the status word
+    # is checked after the replay instead)
+    if _VALIDATE and not torch.cuda.is_current_stream_capturing():
         _lib.status_check(device)
 
 

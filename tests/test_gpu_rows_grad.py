@@ -272,3 +272,45 @@ def test_rows_from_ptr_zero_sign(dr):
     assert not np.signbit(o[0, 0]) and not np.signbit(o[0, 3])
     assert np.signbit(o[1, 0]) and np.signbit(o[1, 3])
     np.testing.assert_array_equal(o[:, 1:3], [[1.0, -2.0], [1.0, -2.0]])
+
+
+def test_graph_captured_train_steps_equal_eager(dr):
+    """Whole training steps (forward, autograd backward through the rows
+    path, by-address SGD apply) captured as one hipGraph and replayed leave
+    the EVs exactly where the same steps run eagerly leave them (the bench's
+    train_step replays such a graph)."""
+    rng = np.random.default_rng(61)
+    B, D, F, S = 512, 32, 3, 4
+    keys = [T(rng.integers(0, 3000, (F, B)).astype(np.int64)) for _ in range(S + 2)]
+    ind = T(np.stack([np.arange(B), np.zeros(B, np.int64)], 1))
+    ups = [T(rng.standard_normal((B, F * D)).astype(np.float32)) for _ in range(S + 2)]
+    exports = []
+    for graphed in (False, True):
+        evs = [dr.EmbeddingVariable("gts_%d_%d" % (int(graphed), f), D, 0.05, capacity=8192)
+               for f in range(F)]
+        opt = dr.GradientDescentOptimizer(0.1)
+
+        def step(i):
+            sps = [dr.SparseTensor(ind, keys[i][f], (B, 1)) for f in range(F)]
+            out = dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum")
+            out.backward(ups[i])
+            opt.apply_gradients(evs, global_step=i)
+
+        for i in range(2):
+            step(i)
+        torch.cuda.synchronize()
+        if graphed:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for i in range(2, S + 2):
+                    step(i)
+            g.replay()
+        else:
+            for i in range(2, S + 2):
+                step(i)
+        torch.cuda.synchronize()
+        dr.status_check()
+        exports.append([_export(e) for e in evs])
+    for (k1, v1), (k2, v2) in zip(*exports):
+        np.testing.assert_array_equal(k1, k2)
+        np.testing.assert_array_equal(v1, v2)

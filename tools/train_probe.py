@@ -27,7 +27,9 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--opt", default="sgd", choices=["sgd", "adagrad"])
+    ap.add_argument("--opt", default="sgd", choices=["sgd", "adagrad", "adam", "ftrl"])
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the steps as one captured hipGraph (no host launch gaps)")
     args = ap.parse_args()
     import deeprec_amd as dr
     from deeprec_amd.embedding_ops import SparseTensor
@@ -36,10 +38,13 @@ def main():
     T, D, B, R = args.tables, args.dim, args.batch, args.rows
     evs = []
     for t in range(T):
-        ev = dr.EmbeddingVariable("tr%d" % t, D, 0.0, capacity=R + (1 << 19), device=dev)
+        ev = dr.EmbeddingVariable("tr%d" % t, D, 0.0, capacity=R + (1 << 20), device=dev)
         ev.insert_synthetic(0, R, seed=1000 + t)
         evs.append(ev)
-    opt = dr.GradientDescentOptimizer(0.01) if args.opt == "sgd" else dr.AdagradOptimizer(0.01)
+    opt = {"sgd": lambda: dr.GradientDescentOptimizer(0.01),
+           "adagrad": lambda: dr.AdagradOptimizer(0.01),
+           "adam": lambda: dr.AdamOptimizer(0.001),
+           "ftrl": lambda: dr.FtrlOptimizer(0.01)}[args.opt]()
     g = torch.Generator(device=dev)
     g.manual_seed(2021)
     batches = [torch.randint(0, R, (T, B), generator=g, device=dev) for _ in range(4)]
@@ -56,14 +61,31 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    graph = None
+    if args.graph:
+        # the 4 batches' steps in a row, one graph (every kernel of every
+        # step is in it; only the host's launch work disappears)
+        for ev in evs:   # worst-case adds of the captured steps (resolve + apply)
+            ev.reserve(2 * len(batches) * B)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for i in range(len(batches)):
+                step(i)
+        graph.replay()
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
+    if graph is not None:
+        for i in range(0, args.steps, len(batches)):
+            graph.replay()
+        args.steps = (args.steps + len(batches) - 1) // len(batches) * len(batches)
+    else:
+        for i in range(args.steps):
+            step(i)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     dr.status_check(dev)
     ms = el / args.steps * 1e3
-    print(json.dumps({"probe": "train_step", "opt": args.opt, "tables": T, "rows": R, "dim": D,
+    print(json.dumps({"probe": "train_step", "opt": args.opt, "graph": bool(args.graph), "tables": T, "rows": R, "dim": D,
                       "batch": B, "ms_per_step": round(ms, 3),
                       "lookups_per_s": round(T * B / (ms * 1e-3), 1),
                       "samples_per_s": round(B / (ms * 1e-3), 1)}), flush=True)
