@@ -474,8 +474,8 @@ def main():
                  "lookups_per_s": round(T * B / (tms * 1e-3), 1), "steps": nsteps,
                  "graph": tgraph is not None,
                  "step": "embedding layer training step: embedding_lookup_sparse_multi forward "
-                         "(EV resolve of every id, pool) + backward (row-grouped segment grad, "
-                         "gradients by address) + KV SGD apply, %d EVs, B=%d" % (T, B)}
+                         "(fused EV probe + row copy recording each id's row) + backward (row-grouped "
+                         "segment grad, gradients by address) + KV SGD apply, %d EVs, B=%d" % (T, B)}
         log("train step: %s" % json.dumps(train))
 
     # ---- dominant kernel: the fused one-hot EV lookup, timed alone --------

@@ -152,4 +152,9 @@ int scan_exclusive_i32(const int32_t* in, int32_t* out, int64_t n, const int64_t
 int scan_exclusive_marks(const int32_t* in, int32_t* out, int64_t n, int64_t* total, void* ws,
                          hipStream_t st);
 
+// Stable LSD radix sort of (uint32 key, int32 value) pairs on bits [0, bits).
+size_t sort_pairs_u32_ws_bytes(int64_t n);
+int sort_pairs_u32(const uint32_t* keys_in, const int32_t* vals_in, uint32_t* keys_out,
+                   int32_t* vals_out, int64_t n, int bits, void* ws, hipStream_t st);
+
 }  // namespace dr

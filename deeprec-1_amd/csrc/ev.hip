@@ -682,6 +682,38 @@ __device__ __forceinline__ void apply_probe(const ApplyTable& at, int64_t i, int
   *initmask_out = initmask;
 }
 
+// Row traffic of the apply: every gradient / weight / slot row is read once
+// and written once per launch -- nontemporal policy unless DR_APPLY_NO_NT
+// (A/B switch).
+__device__ __forceinline__ float4 apply_ld(const float4* p) {
+#ifdef DR_APPLY_NO_NT
+  return *p;
+#else
+  return nt_load(p);
+#endif
+}
+__device__ __forceinline__ float apply_ld(const float* p) {
+#ifdef DR_APPLY_NO_NT
+  return *p;
+#else
+  return nt_load(p);
+#endif
+}
+__device__ __forceinline__ void apply_st(float4* p, float4 v) {
+#ifdef DR_APPLY_NO_NT
+  *p = v;
+#else
+  nt_store(v, p);
+#endif
+}
+__device__ __forceinline__ void apply_st(float* p, float v) {
+#ifdef DR_APPLY_NO_NT
+  *p = v;
+#else
+  nt_store(v, p);
+#endif
+}
+
 // Gradient row of apply entry i: row i of a dense [n, dim] block, or (gind)
 // the address grad_ptr[i] handed on by dr_pool_grad_rows_grouped, whose bit
 // 0 asks for the reference's 0 + x (-0.0f -> +0.0f) before use.
@@ -721,32 +753,44 @@ __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t di
   for (int k0 = 0; k0 < 64; k0 += P * U) {
     // cross-lane reads with every lane active (a disabled source lane reads 0)
     int64_t rr[U];
-    int imq[U];
-    uint64_t ga[U];
+    // Row pointers chosen once per row, outside the column loop, and always
+    // valid (a skipped row reads the default row): the loads of all U rows
+    // issue back to back.  A "pointer or default" select inside the loop
+    // makes hipcc branch around every load and wait for it.
+    const V* gp[U];
+    const V* wp[U];
+    const V* ap1[U];
+    const V* ap2[U];
+    bool zs[U];
 #pragma unroll
     for (int q = 0; q < U; ++q) {
       const int k = k0 + q * P + sub;
       rr[q] = __shfl(row, k, 64);
-      imq[q] = __shfl(initmask, k, 64);
+      const int im = __shfl(initmask, k, 64);
       if (base + k >= ne) rr[q] = -1;
-      ga[q] = rr[q] >= 0 ? apply_grad_addr(grad, gind, base + k, dim) : 0;
+      const bool ok = rr[q] >= 0;
+      const uint64_t ga = ok ? apply_grad_addr(grad, gind, base + k, dim) : 0;
+      zs[q] = ga & 1;
+      gp[q] = ok ? reinterpret_cast<const V*>((uintptr_t)(ga & ~(uint64_t)1)) : d0;
+      wp[q] = (ok && !(im & 1)) ? reinterpret_cast<const V*>(cols.pool[0] + rr[q] * dim) : d0;
+      ap1[q] = (OPT != OPT_SGD && ok && !(im & 2))
+                   ? reinterpret_cast<const V*>(cols.pool[1] + rr[q] * dim) : d1;
+      ap2[q] = (OPT == OPT_ADAM && ok && !(im & 4))
+                   ? reinterpret_cast<const V*>(cols.pool[2] + rr[q] * dim) : d2;
     }
     for (int64_t c = lg; c < dv; c += G) {
       V gv[U], w[U], a1[U], a2[U];
 #pragma unroll
-      for (int q = 0; q < U; ++q) {  // all loads of U rows first
-        const int im = imq[q];
-        if (rr[q] < 0) continue;
-        gv[q] = apply_grad_load<V>(ga[q], c);
-        w[q] = (im & 1) ? d0[c] : reinterpret_cast<const V*>(cols.pool[0] + rr[q] * dim)[c];
-        if (OPT != OPT_SGD)
-          a1[q] = (im & 2) ? d1[c] : reinterpret_cast<const V*>(cols.pool[1] + rr[q] * dim)[c];
-        if (OPT == OPT_ADAM)
-          a2[q] = (im & 4) ? d2[c] : reinterpret_cast<const V*>(cols.pool[2] + rr[q] * dim)[c];
+      for (int q = 0; q < U; ++q) {  // all loads of U rows first, unconditional
+        gv[q] = apply_ld(gp[q] + c);
+        w[q] = apply_ld(wp[q] + c);
+        if (OPT != OPT_SGD) a1[q] = apply_ld(ap1[q] + c);
+        if (OPT == OPT_ADAM) a2[q] = apply_ld(ap2[q] + c);
       }
 #pragma unroll
       for (int q = 0; q < U; ++q) {
         if (rr[q] < 0) continue;
+        if (zs[q]) gv[q] = vadd(vzero<V>(), gv[q]);
         if constexpr (VEC == 4) {
           w[q].x = apply_one<OPT, VEC, G>(gv[q].x, w[q].x, &a1[q].x, &a2[q].x, sc);
           w[q].y = apply_one<OPT, VEC, G>(gv[q].y, w[q].y, &a1[q].y, &a2[q].y, sc);
@@ -755,9 +799,9 @@ __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t di
         } else {
           w[q] = apply_one<OPT, VEC, G>(gv[q], w[q], &a1[q], &a2[q], sc);
         }
-        if (OPT != OPT_SGD) reinterpret_cast<V*>(cols.pool[1] + rr[q] * dim)[c] = a1[q];
-        if (OPT == OPT_ADAM) reinterpret_cast<V*>(cols.pool[2] + rr[q] * dim)[c] = a2[q];
-        reinterpret_cast<V*>(cols.pool[0] + rr[q] * dim)[c] = w[q];
+        if (OPT != OPT_SGD) apply_st(reinterpret_cast<V*>(cols.pool[1] + rr[q] * dim) + c, a1[q]);
+        if (OPT == OPT_ADAM) apply_st(reinterpret_cast<V*>(cols.pool[2] + rr[q] * dim) + c, a2[q]);
+        apply_st(reinterpret_cast<V*>(cols.pool[0] + rr[q] * dim) + c, w[q]);
       }
     }
   }
@@ -1352,6 +1396,7 @@ struct LookupArgs {
   const int64_t* keys;  // [T, B]
   float* out;
   int64_t out_stride;
+  int64_t* rows;        // [T, B] row served per id (-1: default), or nullptr
 };
 
 // Row of `key` when present with this column initialised, else -1.
@@ -1404,10 +1449,12 @@ __global__ __launch_bounds__(256) void ev_lookup_onehot_kernel(LookupArgs a, int
     const int t = (int)(s - b * T);
     const LkDesc& e = sd[t];
     const int64_t row = ev_probe_row(e, (uint64_t)a.keys[(int64_t)t * B + b]);
-    if (row >= 0)
+    if (row >= 0) {
       mine = e.pool + row * (int64_t)dim;
-    else
+      if (a.rows) a.rows[(int64_t)t * B + b] = row;
+    } else {
       missed = true;
+    }
   }
   // wave-aggregated append of the misses
   const uint64_t mm = __ballot(missed);
@@ -1454,6 +1501,7 @@ struct MissArgs {
   const int64_t* keys;
   float* out;
   int64_t out_stride;
+  int64_t* rows;
 };
 
 // Grid-wide barrier of the miss kernel.  The grid is small enough to be
@@ -1538,6 +1586,7 @@ __global__ __launch_bounds__(256) void ev_miss_kernel(MissArgs a, int T, int64_t
     const int t = (int)(s - b * T);
     const float* src = mrow[i] >= 0 ? a.pool[t] + mrow[i] * dim : a.dflt[t];
     float* dst = a.out + b * a.out_stride + (int64_t)t * dim;
+    if (a.rows && lane == 0) a.rows[(int64_t)t * B + b] = mrow[i] >= 0 ? mrow[i] : -1;
     for (int64_t c = lane; c < dim; c += 64) dst[c] = ORDER == DR_ORDER_SEQ ? 0.f + src[c] : src[c];
   }
 }
@@ -1597,7 +1646,8 @@ static void launch_lookup_onehot(const LookupArgs& a, int T, int64_t B, int dim,
 }
 
 static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t B, float* out,
-                         int64_t out_stride, int order, void* ws, size_t ws_bytes, hipStream_t st) {
+                         int64_t out_stride, int order, int64_t* rows_out, void* ws,
+                         size_t ws_bytes, hipStream_t st) {
   DR_REQUIRE(evs && T >= 1 && T <= DR_MAX_GROUP && B >= 0 && out_stride >= 0, DR_INVALID_ARGUMENT,
              "bad argument");
   DR_REQUIRE(order == DR_ORDER_ALI || order == DR_ORDER_SEQ, DR_INVALID_ARGUMENT, "bad order");
@@ -1648,6 +1698,7 @@ static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t 
     ma.dflt[t] = s->defaults[evs[t]->col];
   }
   la.keys = ma.keys = keys;
+  la.rows = ma.rows = rows_out;
   la.out = ma.out = out;
   la.out_stride = ma.out_stride = out_stride;
   const int d4 = (int)(dim / 4);
@@ -1972,8 +2023,19 @@ size_t dr_ev_lookup_onehot_workspace_size(int num_tables, int64_t batch) {
 int dr_ev_lookup_onehot(dr_ev* const* evs, int num_tables, const int64_t* keys, int64_t batch,
                         float* out, int64_t out_stride, int order, void* ws, size_t ws_bytes,
                         void* stream) {
-  return dr::lookup_onehot(evs, num_tables, keys, batch, out, out_stride, order, ws, ws_bytes,
-                           dr::S(stream));
+  return dr::lookup_onehot(evs, num_tables, keys, batch, out, out_stride, order, nullptr, ws,
+                           ws_bytes, dr::S(stream));
+}
+
+int dr_ev_lookup_onehot_rows(dr_ev* const* evs, int num_tables, const int64_t* keys,
+                             int64_t batch, float* out, int64_t out_stride, int order,
+                             int64_t* rows_out, void* ws, size_t ws_bytes, void* stream) {
+  if (!rows_out) {
+    dr::set_error("rows_out is required");
+    return DR_INVALID_ARGUMENT;
+  }
+  return dr::lookup_onehot(evs, num_tables, keys, batch, out, out_stride, order, rows_out, ws,
+                           ws_bytes, dr::S(stream));
 }
 
 // Tagged resolve: keys of all T tables in one array, table of key i =

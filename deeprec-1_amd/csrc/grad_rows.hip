@@ -59,14 +59,14 @@ __device__ __forceinline__ int tab_of(const int64_t* koff, int T, int64_t i) {
 }
 
 __global__ void rows_keys_kernel(const int64_t* __restrict__ rowsel, int64_t N, int64_t row_limit,
-                                 uint64_t sentinel, uint64_t* __restrict__ kin,
+                                 uint32_t sentinel, uint32_t* __restrict__ kin,
                                  int32_t* __restrict__ vin, int32_t* __restrict__ flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
   const int64_t r = rowsel[i];
   // a negative row is an EV default served because the pool was exhausted
   // (RESOURCE_EXHAUSTED already latched by the resolve): no gradient row
-  kin[i] = (r >= 0 && r < row_limit) ? (uint64_t)r : sentinel;
+  kin[i] = (r >= 0 && r < row_limit) ? (uint32_t)r : sentinel;
   vin[i] = (int32_t)i;
   flags[i] = -1;
 }
@@ -88,8 +88,8 @@ __device__ __forceinline__ void work_push(bool push, int64_t p, int32_t* __restr
 // run) at the run head's original position i; heads of longer runs and
 // every multiple of the chunk inside a run (a possible later chunk of a
 // long run) go straight to the worklist of rows_work_kernel.
-__global__ void rows_heads_kernel(RowsGroup g, int T, const uint64_t* __restrict__ skey,
-                                  const int32_t* __restrict__ perm, uint64_t sentinel,
+__global__ void rows_heads_kernel(RowsGroup g, int T, const uint32_t* __restrict__ skey,
+                                  const int32_t* __restrict__ perm, uint32_t sentinel,
                                   int32_t* __restrict__ mark, int32_t* __restrict__ work,
                                   int32_t* __restrict__ nwork) {
   __shared__ int64_t sk[DR_MAX_GROUP + 1];
@@ -100,7 +100,7 @@ __global__ void rows_heads_kernel(RowsGroup g, int T, const uint64_t* __restrict
   bool push = false;
   if (p < N) {
     const int64_t pm = p > 0 ? p - 1 : 0, pn = p + 1 < N ? p + 1 : N - 1;
-    const uint64_t u = skey[p], um = skey[pm], un = skey[pn];
+    const uint32_t u = skey[p], um = skey[pm], un = skey[pn];
     const int32_t i = perm[p], im = perm[pm], in = perm[pn];
     const int t = tab_of(sk, T, i);
     const bool valid = u != sentinel;
@@ -167,8 +167,8 @@ __global__ __launch_bounds__(256) void rows_emit_kernel(
 
 // Is the run (u, t) through inner position m (a multiple of kRowsChunk, not
 // its run's head) longer than kRowsChunk?  Rare path: bounded searches.
-__device__ bool run_is_long(const uint64_t* __restrict__ skey, const int32_t* __restrict__ perm,
-                            const int64_t* sk, int T, int64_t N, int64_t m, uint64_t u, int t) {
+__device__ bool run_is_long(const uint32_t* __restrict__ skey, const int32_t* __restrict__ perm,
+                            const int64_t* sk, int T, int64_t N, int64_t m, uint32_t u, int t) {
   auto in_run = [&](int64_t q) { return skey[q] == u && tab_of(sk, T, perm[q]) == t; };
   if (m >= kRowsChunk && in_run(m - kRowsChunk)) return true;
   if (m + kRowsChunk < N && in_run(m + kRowsChunk)) return true;
@@ -200,7 +200,7 @@ __device__ bool run_is_long(const uint64_t* __restrict__ skey, const int32_t* __
 // part[c0 / chunk] when its run is long, and is dropped otherwise.
 template <int VEC, int G, int CPL, bool W>
 __global__ __launch_bounds__(256) void rows_work_kernel(
-    RowsGroup g, int T, int64_t B, const uint64_t* __restrict__ skey,
+    RowsGroup g, int T, int64_t B, const uint32_t* __restrict__ skey,
     const int32_t* __restrict__ perm, const int32_t* __restrict__ ex,
     const int32_t* __restrict__ base, int dim, const int32_t* __restrict__ work,
     const int32_t* __restrict__ nwork, uint64_t* __restrict__ gptr, float* __restrict__ gu,
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(256) void rows_work_kernel(
   for (int64_t e = (int64_t)blockIdx.x * GPB + threadIdx.x / G; e < nw;
        e += (int64_t)gridDim.x * GPB) {
     const int64_t c0 = work[e];
-    const uint64_t u = skey[c0];
+    const uint32_t u = skey[c0];
     const int32_t pc = perm[c0];
     const int t = tab_of(sk, T, pc);
     const bool first = c0 == 0 || skey[c0 - 1] != u || tab_of(sk, T, perm[c0 - 1]) != t;
@@ -344,7 +344,7 @@ __global__ __launch_bounds__(256) void rows_work_kernel(
 // multiples m_k of the chunk inside the run.
 template <int VEC, int G, int CPL>
 __global__ __launch_bounds__(256) void rows_finish_kernel(
-    RowsGroup g, int T, const uint64_t* __restrict__ skey, const int32_t* __restrict__ perm,
+    RowsGroup g, int T, const uint32_t* __restrict__ skey, const int32_t* __restrict__ perm,
     int dim, float* __restrict__ gu, const float* __restrict__ part,
     const int32_t* __restrict__ longs, const int32_t* __restrict__ nlong, int64_t nslots) {
   __shared__ int64_t sk[DR_MAX_GROUP + 1];
@@ -359,7 +359,7 @@ __global__ __launch_bounds__(256) void rows_finish_kernel(
   for (int64_t i = (int64_t)blockIdx.x * GPB + threadIdx.x / G; i < n;
        i += (int64_t)gridDim.x * GPB) {
     const int64_t o = longs[2 * i], c0 = longs[2 * i + 1];
-    const uint64_t u = skey[c0];
+    const uint32_t u = skey[c0];
     const int t = tab_of(sk, T, perm[c0]);
     R acc;
     load_row_u<VEC, G, CPL>(acc, gu + o * (int64_t)dim, lg, dv);
@@ -413,9 +413,9 @@ __global__ __launch_bounds__(256) void rows_from_ptr_kernel(const uint64_t* __re
 }
 
 struct RowsWs {
-  uint64_t* kin;
+  uint32_t* kin;
   int32_t* vin;
-  uint64_t* kout;
+  uint32_t* kout;
   int32_t* perm;
   int32_t* flags;
   int32_t* ex;
@@ -435,9 +435,9 @@ static RowsWs carve_rows(void* ws, int64_t n, size_t* used) {
   Carver c(ws);
   RowsWs w;
   const int64_t nn = n > 0 ? n : 1;
-  w.kin = c.take<uint64_t>(nn);
+  w.kin = c.take<uint32_t>(nn);
   w.vin = c.take<int32_t>(nn);
-  w.kout = c.take<uint64_t>(nn);
+  w.kout = c.take<uint32_t>(nn);
   w.perm = c.take<int32_t>(nn);
   w.flags = c.take<int32_t>(nn);
   w.ex = c.take<int32_t>(nn);
@@ -449,7 +449,7 @@ static RowsWs carve_rows(void* ws, int64_t n, size_t* used) {
   const int64_t chunks = nn / kRowsChunk + 2;
   w.longs = c.take<int32_t>(2 * chunks);
   w.part = c.take<float>(chunks * kRowsMaxDim);
-  w.sort_bytes = dr_sort_pairs_workspace_size(nn);
+  w.sort_bytes = sort_pairs_u32_ws_bytes(nn);
   w.sort_ws = c.take<char>(w.sort_bytes);
   w.scan_ws = c.take<char>(scan_ws_bytes(nn));
   if (used) *used = c.used + 256;
@@ -532,14 +532,16 @@ int dr_pool_grad_rows_grouped(const dr_pool_grad_desc* descs_host, int num_table
              "grad_unique must be 16-byte aligned");
   if (!aligned) defer = 0;   // by-address rows must share grad_unique's alignment
   RowsWs w = carve_rows(ws, n, nullptr);
+  DR_REQUIRE(row_limit < ((int64_t)1 << 32) - 1, DR_INVALID_ARGUMENT,
+             "row_limit must be < 2^32 - 1");
   int rb = 1;
-  while (rb < 62 && ((int64_t)1 << rb) <= row_limit) ++rb;   // rows < 2^rb - 1
-  const uint64_t sentinel = ((uint64_t)1 << rb) - 1;
+  while (rb < 32 && ((int64_t)1 << rb) <= row_limit) ++rb;   // rows < 2^rb - 1
+  const uint32_t sentinel = (uint32_t)(((uint64_t)1 << rb) - 1);
   const unsigned nb = (unsigned)ceil_div(n, 256);
   hipLaunchKernelGGL(rows_keys_kernel, dim3(nb), dim3(256), 0, s, rowsel, n, row_limit, sentinel,
                      w.kin, w.vin, w.flags);
   DR_LAUNCH_CHECK();
-  int rc = dr_sort_pairs(w.kin, w.vin, w.kout, w.perm, n, 0, rb, w.sort_ws, w.sort_bytes, stream);
+  int rc = sort_pairs_u32(w.kin, w.vin, w.kout, w.perm, n, rb, w.sort_ws, s);
   if (rc) return rc;
   hipLaunchKernelGGL(rows_zero_i32, dim3(1), dim3(1), 0, s, w.nlong, w.nwork);
   hipLaunchKernelGGL(rows_heads_kernel, dim3(nb), dim3(256), 0, s, g, num_tables, w.kout, w.perm,

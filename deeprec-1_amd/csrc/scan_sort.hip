@@ -148,7 +148,8 @@ static constexpr int kSortThreads = 256;
 static constexpr int kSortRounds = 16;
 static constexpr int kSortTile = kSortThreads * kSortRounds;
 
-__global__ __launch_bounds__(256) void sort_hist_kernel(const uint64_t* __restrict__ keys, int64_t n,
+template <class K>
+__global__ __launch_bounds__(256) void sort_hist_kernel(const K* __restrict__ keys, int64_t n,
                                                         int shift, int dmask,
                                                         int32_t* __restrict__ hist,
                                                         int64_t nblocks) {
@@ -192,12 +193,13 @@ __global__ __launch_bounds__(256) void sort_rowscan_kernel(int32_t* __restrict__
 // read of a counter and the group leader's update are ordered, so the loop
 // needs no block barrier.  Tile offset of (wave w, digit d) =
 // exclusive-over-digits(total) + sum over w' < w of the wave counts.
+template <class K>
 __global__ __launch_bounds__(256) void sort_scatter_kernel(
-    const uint64_t* __restrict__ kin, const int32_t* __restrict__ vin, uint64_t* __restrict__ kout,
+    const K* __restrict__ kin, const int32_t* __restrict__ vin, K* __restrict__ kout,
     int32_t* __restrict__ vout, int64_t n, int shift, int dmask,
     const int32_t* __restrict__ row_scanned, const int32_t* __restrict__ digit_tot,
     int64_t nblocks) {
-  __shared__ uint64_t sk[kSortTile];
+  __shared__ K sk[kSortTile];
   __shared__ int32_t sv[kSortTile];
   __shared__ int wcnt[4][256];
   __shared__ int toff[256];
@@ -209,7 +211,7 @@ __global__ __launch_bounds__(256) void sort_scatter_kernel(
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
   const int cnt = (int)(n - base < kSortTile ? n - base : kSortTile);
   const int wbase = wave * (kSortTile / 4);
-  uint64_t key[kSortRounds];
+  K key[kSortRounds];
   int32_t val[kSortRounds];
   int rk[kSortRounds];
 #pragma unroll
@@ -267,7 +269,7 @@ __global__ __launch_bounds__(256) void sort_scatter_kernel(
   for (int r = 0; r < kSortRounds; ++r) {
     const int i = r * kSortThreads + tid;
     if (i < cnt) {
-      const uint64_t k = sk[i];
+      const K k = sk[i];
       const int d = (int)((k >> shift) & dmask);
       const int64_t pos = (int64_t)gbase[d] + (i - toff[d]);
       kout[pos] = k;
@@ -278,13 +280,69 @@ __global__ __launch_bounds__(256) void sort_scatter_kernel(
 
 }  // namespace dr
 
-extern "C" size_t dr_sort_pairs_workspace_size(int64_t n) {
-  dr::Carver c(nullptr);
-  c.take<uint64_t>(n > 0 ? n : 1);
+namespace dr {
+
+template <class K>
+static size_t sort_ws_bytes(int64_t n) {
+  Carver c(nullptr);
+  c.take<K>(n > 0 ? n : 1);
   c.take<int32_t>(n > 0 ? n : 1);
-  c.take<int32_t>((size_t)256 * dr::ceil_div(n > 0 ? n : 1, dr::kSortTile));
+  c.take<int32_t>((size_t)256 * ceil_div(n > 0 ? n : 1, kSortTile));
   c.take<int32_t>(256);
   return c.used + 256;
+}
+
+template <class K>
+static int sort_pairs(const K* keys_in, const int32_t* vals_in, K* keys_out, int32_t* vals_out,
+                      int64_t n, int bit_lo, int bit_hi, void* ws, hipStream_t st) {
+  if (n == 0) return DR_OK;
+  Carver c(ws);
+  K* ktmp = c.take<K>(n);
+  int32_t* vtmp = c.take<int32_t>(n);
+  const int64_t nblocks = ceil_div(n, kSortTile);
+  int32_t* hist = c.take<int32_t>((size_t)256 * nblocks);
+  int32_t* dtot = c.take<int32_t>(256);
+  int passes = (bit_hi - bit_lo + 7) / 8;
+  if (passes == 0) {
+    DR_HIP(hipMemcpyAsync(keys_out, keys_in, n * sizeof(K), hipMemcpyDeviceToDevice, st));
+    DR_HIP(hipMemcpyAsync(vals_out, vals_in, n * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    return DR_OK;
+  }
+  const K* ks = keys_in;
+  const int32_t* vs = vals_in;
+  for (int p = 0; p < passes; ++p) {
+    const bool to_out = ((passes - 1 - p) % 2) == 0;
+    K* kd = to_out ? keys_out : ktmp;
+    int32_t* vd = to_out ? vals_out : vtmp;
+    const int shift = bit_lo + 8 * p;
+    const int dbits = bit_hi - shift < 8 ? bit_hi - shift : 8;   // bits >= bit_hi are ignored
+    const int dmask = (1 << dbits) - 1;
+    hipLaunchKernelGGL(sort_hist_kernel<K>, dim3((unsigned)nblocks), dim3(kSortThreads), 0, st,
+                       ks, n, shift, dmask, hist, nblocks);
+    hipLaunchKernelGGL(sort_rowscan_kernel, dim3(256), dim3(kSortThreads), 0, st, hist, nblocks,
+                       dtot);
+    hipLaunchKernelGGL(sort_scatter_kernel<K>, dim3((unsigned)nblocks), dim3(kSortThreads), 0, st,
+                       ks, vs, kd, vd, n, shift, dmask, hist, dtot, nblocks);
+    DR_LAUNCH_CHECK();
+    ks = kd;
+    vs = vd;
+  }
+  return DR_OK;
+}
+
+size_t sort_pairs_u32_ws_bytes(int64_t n) { return sort_ws_bytes<uint32_t>(n); }
+
+int sort_pairs_u32(const uint32_t* keys_in, const int32_t* vals_in, uint32_t* keys_out,
+                   int32_t* vals_out, int64_t n, int bits, void* ws, hipStream_t st) {
+  DR_REQUIRE(n >= 0 && n < ((int64_t)1 << 31) && bits >= 0 && bits <= 32, DR_INVALID_ARGUMENT,
+             "sort_pairs_u32: bad arguments");
+  return sort_pairs<uint32_t>(keys_in, vals_in, keys_out, vals_out, n, 0, bits, ws, st);
+}
+
+}  // namespace dr
+
+extern "C" size_t dr_sort_pairs_workspace_size(int64_t n) {
+  return dr::sort_ws_bytes<uint64_t>(n);
 }
 
 extern "C" int dr_sort_pairs(const uint64_t* keys_in, const int32_t* vals_in, uint64_t* keys_out,
@@ -296,38 +354,6 @@ extern "C" int dr_sort_pairs(const uint64_t* keys_in, const int32_t* vals_in, ui
   DR_REQUIRE(n < ((int64_t)1 << 31), DR_INVALID_ARGUMENT, "dr_sort_pairs: n >= 2^31");
   DR_REQUIRE(ws_bytes >= dr_sort_pairs_workspace_size(n), DR_INVALID_ARGUMENT,
              "dr_sort_pairs: workspace too small");
-  hipStream_t st = S(stream);
-  if (n == 0) return DR_OK;
-  Carver c(ws);
-  uint64_t* ktmp = c.take<uint64_t>(n);
-  int32_t* vtmp = c.take<int32_t>(n);
-  const int64_t nblocks = ceil_div(n, kSortTile);
-  int32_t* hist = c.take<int32_t>((size_t)256 * nblocks);
-  int32_t* dtot = c.take<int32_t>(256);
-  int passes = (bit_hi - bit_lo + 7) / 8;
-  if (passes == 0) {
-    DR_HIP(hipMemcpyAsync(keys_out, keys_in, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
-    DR_HIP(hipMemcpyAsync(vals_out, vals_in, n * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
-    return DR_OK;
-  }
-  const uint64_t* ks = keys_in;
-  const int32_t* vs = vals_in;
-  for (int p = 0; p < passes; ++p) {
-    const bool to_out = ((passes - 1 - p) % 2) == 0;
-    uint64_t* kd = to_out ? keys_out : ktmp;
-    int32_t* vd = to_out ? vals_out : vtmp;
-    const int shift = bit_lo + 8 * p;
-    const int dbits = bit_hi - shift < 8 ? bit_hi - shift : 8;   // bits >= bit_hi are ignored
-    const int dmask = (1 << dbits) - 1;
-    hipLaunchKernelGGL(sort_hist_kernel, dim3((unsigned)nblocks), dim3(kSortThreads), 0, st, ks,
-                       n, shift, dmask, hist, nblocks);
-    hipLaunchKernelGGL(sort_rowscan_kernel, dim3(256), dim3(kSortThreads), 0, st, hist, nblocks,
-                       dtot);
-    hipLaunchKernelGGL(sort_scatter_kernel, dim3((unsigned)nblocks), dim3(kSortThreads), 0, st,
-                       ks, vs, kd, vd, n, shift, dmask, hist, dtot, nblocks);
-    DR_LAUNCH_CHECK();
-    ks = kd;
-    vs = vd;
-  }
-  return DR_OK;
+  return sort_pairs<uint64_t>(keys_in, vals_in, keys_out, vals_out, n, bit_lo, bit_hi, ws,
+                              S(stream));
 }

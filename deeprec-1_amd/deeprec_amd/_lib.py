@@ -138,6 +138,7 @@ SIGNATURES = {
     "dr_ev_resolve_grouped": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "dr_ev_lookup_onehot_workspace_size": (_SZ, [_I32, _I64]),
     "dr_ev_lookup_onehot": (_I32, [_P, _I32, _P, _I64, _P, _I64, _I32, _P, _SZ, _P]),
+    "dr_ev_lookup_onehot_rows": (_I32, [_P, _I32, _P, _I64, _P, _I64, _I32, _P, _P, _SZ, _P]),
     "dr_ev_resolve_tagged": (_I32, [_P, _I32, _P, _P, _I64, _P, _P, _P, _P, _P, _SZ, _P]),
     "dr_ev_gather_tagged": (_I32, [_P, _I32, _P, _P, _I64, _P, _P, _P]),
     "dr_ev_pool": (_P, [_P]),

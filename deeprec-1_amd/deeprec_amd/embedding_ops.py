@@ -243,16 +243,18 @@ def _dense_grad(p, sl):
 
 class _LookupFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, anchor, feats, order, *tensors):
+    def forward(ctx, anchor, feats, order, fused_rows, *tensors):
         ctx.feats = feats
         ctx.tensors = tensors
+        if fused_rows:
+            return _fused_onehot(feats, order, with_rows=True)
         return _pool_all(feats, order)
 
     @staticmethod
     def backward(ctx, grad_out):
         g = grad_out.contiguous()
         dense = _queue_grads(ctx.feats, g, 0, g.shape[1], ctx.tensors)
-        return (None, None, None) + tuple(dense)
+        return (None, None, None, None) + tuple(dense)
 
 
 def _queue_grads(feats, g, col0, total, tensors=()):
@@ -563,14 +565,10 @@ class _UniqueGroup(object):
                 for t in range(len(self.feats))]
 
 
-def _fused_onehot(feats, order):
-    """Forward-only one-hot lookup of filter-free EVs in one fused launch
-    (dr_ev_lookup_onehot: probe + row copy, no resolve pass / row array).
-    Returns the [B, T*D] output, or None when the features do not qualify."""
-    import ctypes as C
+def _fused_onehot_ok(feats):
     p0 = feats[0].params
     if not (len(feats) <= _lib.MAX_GROUP and isinstance(p0, EmbeddingVariable)):
-        return None
+        return False
     B = feats[0].batch
     D = p0.dim
     for f in feats:
@@ -578,18 +576,42 @@ def _fused_onehot(feats, order):
         if not (isinstance(p, EmbeddingVariable) and f.onehot and f.batch == B
                 and p.dim == D and p.device == p0.device and p.filter_freq == 0
                 and not callable(p.initializer) and f.values.numel() == B):
-            return None
-    if D % 4 != 0 or D > 256 or len(feats) * B >= (1 << 31):
+            return False
+    return D % 4 == 0 and D <= 256 and len(feats) * B < (1 << 31)
+
+
+def _fused_onehot(feats, order, with_rows=False):
+    """One-hot lookup of filter-free EVs in one fused launch
+    (dr_ev_lookup_onehot: probe + row copy, no resolve pass).  Forward-only,
+    or (with_rows) a training forward that also records the row of every id
+    for the row-grouped backward (_RowGroup).  Returns the [B, T*D] output,
+    or None when the features do not qualify."""
+    import ctypes as C
+    if not _fused_onehot_ok(feats):
         return None
+    p0 = feats[0].params
+    B = feats[0].batch
+    D = p0.dim
     T = len(feats)
     dev = feats[0].values.device
-    vals = _concat_values(feats, [t * B for t in range(T + 1)])
+    koff = [t * B for t in range(T + 1)]
+    vals = _concat_values(feats, koff)
     out = torch.empty((B, T * D), dtype=torch.float32, device=dev)
     handles = (C.c_void_p * T)(*[f.params.handle.value for f in feats])
     wsb = lib().dr_ev_lookup_onehot_workspace_size(T, B)
     ws = workspace(wsb, dev)
-    check(lib().dr_ev_lookup_onehot(handles, T, ptr(vals), B, ptr(out), T * D, order, ptr(ws), wsb,
-                                    stream_handle(dev)))
+    if with_rows:
+        rowsel = torch.empty(T * B, dtype=torch.int64, device=dev)
+        check(lib().dr_ev_lookup_onehot_rows(handles, T, ptr(vals), B, ptr(out), T * D, order,
+                                             ptr(rowsel), ptr(ws), wsb, stream_handle(dev)))
+        group = _RowGroup(feats, vals, rowsel, koff)
+        for t, f in enumerate(feats):
+            f.uniq = f.idx = f.rows = f.U = f.defaults = None
+            f.rowsel = rowsel[koff[t]:koff[t + 1]]
+            f.group = group
+    else:
+        check(lib().dr_ev_lookup_onehot(handles, T, ptr(vals), B, ptr(out), T * D, order, ptr(ws),
+                                        wsb, stream_handle(dev)))
     ops._post(dev)
     return out
 
@@ -604,10 +626,16 @@ def _run(feats, order=ORDER_ALI, need_grad=None):
         out = _fused_onehot(feats, order)
         if out is not None:
             return out
-    _prepare_all(feats, need_grad)
+    # training forward of one-hot filter-free EVs: the fused probe + copy
+    # kernel records the rows for the row-grouped backward
+    fused_rows = (need_grad and _FUSED_ONEHOT and not tensors and _rows_eligible(feats)
+                  and _fused_onehot_ok(feats))
+    if not fused_rows:
+        _prepare_all(feats, need_grad)
     if need_grad:
         anchors = [_anchor(f.params) for f in feats if not torch.is_tensor(f.params)]
-        return _LookupFn.apply(anchors[0] if anchors else None, feats, order, *tensors)
+        return _LookupFn.apply(anchors[0] if anchors else None, feats, order, fused_rows,
+                               *tensors)
     return _pool_all(feats, order)
 
 

@@ -372,6 +372,13 @@ size_t dr_ev_lookup_onehot_workspace_size(int num_tables, int64_t batch);
 int dr_ev_lookup_onehot(dr_ev* const* evs, int num_tables, const int64_t* keys, int64_t batch,
                         float* out, int64_t out_stride, int order, void* ws, size_t ws_bytes,
                         void* stream);
+/* The same, also writing the row each id was served from (rows_out[t*batch */
+/* + b]; -1 = the EV default, served when the pool was exhausted): the       */
+/* training forward of filter-free EVs, whose backward regroups by these     */
+/* rows (dr_pool_grad_rows_grouped) instead of by a Unique.                  */
+int dr_ev_lookup_onehot_rows(dr_ev* const* evs, int num_tables, const int64_t* keys,
+                             int64_t batch, float* out, int64_t out_stride, int order,
+                             int64_t* rows_out, void* ws, size_t ws_bytes, void* stream);
 /* Tagged resolve (owner side of the sharded exchange): keys of all T EVs  */
 /* (equal dim) in one array, table of key i = tags[i]; n_dev: optional      */
 /* DEVICE count.  Filtered keys give -(i+1) (read table t's default row).   */
