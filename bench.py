@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--train-steps", type=int, default=10,
                    help="N=1: time the embedding training step too (0 = skip)")
     p.add_argument("--kernel-iters", type=int, default=20)
+    p.add_argument("--no-deepfm", dest="deepfm", action="store_false",
+                   help="skip the BASELINE configs[1] (DeepFM 26 x 1e7 x 64) leg at N=1")
     p.add_argument("--engine", default="auto", choices=["auto", "local", "xgmi", "a2a"],
                    help="auto: local lookup at N=1, xgmi peer-write (RCCL all-to-all "
                         "fallback) at N>1; xgmi/a2a at N=1 run the sharded engine on itself")
@@ -163,6 +165,95 @@ def check_rows(out, ids, T, D, n_sample, seed):
                                  "(first key %d)" % (tt, bad.shape[0], sel.sum(),
                                                      keys[sel][bad[0]]))
     return int(n_sample)
+
+
+def deepfm_leg(args, dev, log):
+    """BASELINE configs[1] (DeepFM: 26 tables x 1e7 rows x 64 fp32, one
+    MI355X): the fused one-hot EV lookup on its own table shape -- lookups/s,
+    the kernel's HBM roofline (8 key + 16 slot + 256 row + 256 out bytes per
+    lookup) and the embedding-layer training step (SGD), on uniform keys.
+    Runs after the headline's tables are freed (both sets do not fit 288 GB
+    together)."""
+    import deeprec_amd as dr
+    from deeprec_amd import _lib
+    from deeprec_amd.embedding_ops import SparseTensor, _Feature, _fused_onehot
+    T, D, R, B = 26, 64, 10_000_000, args.batch
+    evs = []
+    for t in range(T):
+        ev = dr.EmbeddingVariable("deepfm%d" % t, D, 0.0, device=dev, capacity=R + (1 << 20))
+        ev.insert_synthetic(0, R, seed=5000 + t)
+        evs.append(ev)
+    batches = make_batches(4, T, B, R, 0.0, 77, dev)
+    static_ids = torch.empty((T, B), dtype=torch.int64, device=dev)
+    static_ids.copy_(batches[0])
+    seg = torch.arange(B, dtype=torch.int32, device=dev)
+    with torch.no_grad():
+        feats = [_Feature(evs[t], static_ids[t], seg, B, None, "sum", None, onehot=True)
+                 for t in range(T)]
+        _fused_onehot(feats, _lib.ORDER_ALI)
+        torch.cuda.synchronize()
+        kg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(kg):
+            _fused_onehot(feats, _lib.ORDER_ALI)
+        kg.replay()
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.kernel_iters):
+            kg.replay()
+        e1.record()
+        torch.cuda.synchronize()
+    k_ms = e0.elapsed_time(e1) / args.kernel_iters
+    per = 8 + 16 + 2 * D * 4
+    ach = T * B * per / (k_ms * 1e-3) / 1e9
+    # embedding-layer training step, hipGraph of 4 steps as in main()
+    ind = torch.stack([torch.arange(B, device=dev), torch.zeros(B, dtype=torch.int64, device=dev)],
+                      1)
+    sps = [[SparseTensor(ind, ids[t], (B, 1)) for t in range(T)] for ids in batches]
+    opt = dr.GradientDescentOptimizer(0.01)
+    up = torch.randn((B, T * D), device=dev)
+
+    def tstep(i):
+        out = dr.embedding_lookup_sparse_multi(evs, sps[i % 4], combiner="sum")
+        out.backward(up)
+        opt.apply_gradients(evs)
+
+    for i in range(2):
+        tstep(i)
+    torch.cuda.synchronize()
+    for ev in evs:
+        ev.reserve(8 * B)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for i in range(4):
+            tstep(i)
+    g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    reps = max(1, args.train_steps // 4)
+    for _ in range(reps):
+        g.replay()
+    torch.cuda.synchronize()
+    tms = (time.perf_counter() - t0) / (4 * reps) * 1e3
+    dr.status_check(dev)
+    res = {"workload": "BASELINE configs[1] DeepFM shape: 26 EV tables x %d rows x %d fp32, "
+                       "B=%d, hotness 1, uniform keys, fused one-hot embedding_lookup_sparse(sum)"
+                       % (R, D, B),
+           "lookups_per_s": round(T * B / (k_ms * 1e-3), 1),
+           "samples_per_s": round(B / (k_ms * 1e-3), 1),
+           "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
+                        "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
+                        "kernel": "dr::ev_lookup_onehot_kernel<4,16,1,ALI,4>",
+                        "kernel_ms": round(k_ms, 4), "bytes_per_lookup": per,
+                        "bytes_per_launch": T * B * per},
+           "train_step": {"ms_per_step": round(tms, 4),
+                          "samples_per_s": round(B / (tms * 1e-3), 1),
+                          "step": "fused lookup recording rows + row-grouped backward + "
+                                  "by-address KV SGD, hipGraph of 4 steps"}}
+    log("deepfm leg: %s" % json.dumps(res))
+    del evs, feats, g, kg
+    return res
 
 
 def main():
@@ -570,6 +661,17 @@ def main():
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args)
 
+    deepfm = None
+    if world == 1 and args.deepfm:
+        # drop every holder of the headline EVs so their HBM is released
+        evs = feats = gfeats = batch_sps = None
+        engine = a2a = None
+        import gc
+        gc.collect()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        deepfm = deepfm_leg(args, dev, log)
+
     if rank == 0:
         with open(os.path.join(ROOT, "BASELINE.json")) as f:
             metric = json.load(f)["metric"]
@@ -599,6 +701,7 @@ def main():
                        "parallelism": "row-sharded tables x%d, data-parallel batch" % world},
             "forward_samples_per_s": round(value / T, 1),
             "train_step": train,
+            "deepfm_config": deepfm,
             "correctness": correctness,
             "roofline": roof,
             "roofline_row_gather": roof_gather,
