@@ -157,4 +157,11 @@ size_t sort_pairs_u32_ws_bytes(int64_t n);
 int sort_pairs_u32(const uint32_t* keys_in, const int32_t* vals_in, uint32_t* keys_out,
                    int32_t* vals_out, int64_t n, int bits, void* ws, hipStream_t st);
 
+// The same for uint64 keys over the first *n_dev of n_cap pairs (DEVICE
+// count; the grid is sized for n_cap, no host sync).  Workspace:
+// dr_sort_pairs_workspace_size(n_cap).
+int sort_pairs_u64_dev(const uint64_t* keys_in, const int32_t* vals_in, uint64_t* keys_out,
+                       int32_t* vals_out, int64_t n_cap, const int64_t* n_dev, int bits,
+                       void* ws, hipStream_t st);
+
 }  // namespace dr

@@ -148,15 +148,18 @@ static constexpr int kSortThreads = 256;
 static constexpr int kSortRounds = 16;
 static constexpr int kSortTile = kSortThreads * kSortRounds;
 
+// n_dev (optional DEVICE count <= n): the grid is sized for n, tiles past
+// the device count contribute empty histograms and scatter nothing.
 template <class K>
 __global__ __launch_bounds__(256) void sort_hist_kernel(const K* __restrict__ keys, int64_t n,
-                                                        int shift, int dmask,
-                                                        int32_t* __restrict__ hist,
+                                                        const int64_t* n_dev, int shift,
+                                                        int dmask, int32_t* __restrict__ hist,
                                                         int64_t nblocks) {
   __shared__ int cnt[256];
   cnt[threadIdx.x] = 0;
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
-  const int c = (int)(n - base < kSortTile ? n - base : kSortTile);
+  const int64_t ne = eff_n(n, n_dev);
+  const int c = ne <= base ? 0 : (int)(ne - base < kSortTile ? ne - base : kSortTile);
   int d[kSortRounds];
 #pragma unroll
   for (int r = 0; r < kSortRounds; ++r) {       // all loads in flight before the atomics
@@ -196,7 +199,7 @@ __global__ __launch_bounds__(256) void sort_rowscan_kernel(int32_t* __restrict__
 template <class K>
 __global__ __launch_bounds__(256) void sort_scatter_kernel(
     const K* __restrict__ kin, const int32_t* __restrict__ vin, K* __restrict__ kout,
-    int32_t* __restrict__ vout, int64_t n, int shift, int dmask,
+    int32_t* __restrict__ vout, int64_t n, const int64_t* n_dev, int shift, int dmask,
     const int32_t* __restrict__ row_scanned, const int32_t* __restrict__ digit_tot,
     int64_t nblocks) {
   __shared__ K sk[kSortTile];
@@ -209,7 +212,9 @@ __global__ __launch_bounds__(256) void sort_scatter_kernel(
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
-  const int cnt = (int)(n - base < kSortTile ? n - base : kSortTile);
+  const int64_t ne = eff_n(n, n_dev);
+  if (ne <= base) return;   // block-uniform: a tile past the device count
+  const int cnt = (int)(ne - base < kSortTile ? ne - base : kSortTile);
   const int wbase = wave * (kSortTile / 4);
   K key[kSortRounds];
   int32_t val[kSortRounds];
@@ -294,7 +299,8 @@ static size_t sort_ws_bytes(int64_t n) {
 
 template <class K>
 static int sort_pairs(const K* keys_in, const int32_t* vals_in, K* keys_out, int32_t* vals_out,
-                      int64_t n, int bit_lo, int bit_hi, void* ws, hipStream_t st) {
+                      int64_t n, int bit_lo, int bit_hi, void* ws, hipStream_t st,
+                      const int64_t* n_dev = nullptr) {
   if (n == 0) return DR_OK;
   Carver c(ws);
   K* ktmp = c.take<K>(n);
@@ -318,11 +324,11 @@ static int sort_pairs(const K* keys_in, const int32_t* vals_in, K* keys_out, int
     const int dbits = bit_hi - shift < 8 ? bit_hi - shift : 8;   // bits >= bit_hi are ignored
     const int dmask = (1 << dbits) - 1;
     hipLaunchKernelGGL(sort_hist_kernel<K>, dim3((unsigned)nblocks), dim3(kSortThreads), 0, st,
-                       ks, n, shift, dmask, hist, nblocks);
+                       ks, n, n_dev, shift, dmask, hist, nblocks);
     hipLaunchKernelGGL(sort_rowscan_kernel, dim3(256), dim3(kSortThreads), 0, st, hist, nblocks,
                        dtot);
     hipLaunchKernelGGL(sort_scatter_kernel<K>, dim3((unsigned)nblocks), dim3(kSortThreads), 0, st,
-                       ks, vs, kd, vd, n, shift, dmask, hist, dtot, nblocks);
+                       ks, vs, kd, vd, n, n_dev, shift, dmask, hist, dtot, nblocks);
     DR_LAUNCH_CHECK();
     ks = kd;
     vs = vd;
@@ -331,6 +337,17 @@ static int sort_pairs(const K* keys_in, const int32_t* vals_in, K* keys_out, int
 }
 
 size_t sort_pairs_u32_ws_bytes(int64_t n) { return sort_ws_bytes<uint32_t>(n); }
+
+int sort_pairs_u64_dev(const uint64_t* keys_in, const int32_t* vals_in, uint64_t* keys_out,
+                       int32_t* vals_out, int64_t n_cap, const int64_t* n_dev, int bits,
+                       void* ws, hipStream_t st) {
+  DR_REQUIRE(n_cap >= 0 && n_cap < ((int64_t)1 << 31) && bits >= 0 && bits <= 64 && n_dev,
+             DR_INVALID_ARGUMENT, "sort_pairs_u64_dev: bad arguments");
+  // the pass count is fixed on the host: an even count keeps the result in
+  // keys_out whatever n turns out to be
+  return sort_pairs<uint64_t>(keys_in, vals_in, keys_out, vals_out, n_cap, 0, bits, ws, st,
+                              n_dev);
+}
 
 int sort_pairs_u32(const uint32_t* keys_in, const int32_t* vals_in, uint32_t* keys_out,
                    int32_t* vals_out, int64_t n, int bits, void* ws, hipStream_t st) {

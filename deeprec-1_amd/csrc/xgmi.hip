@@ -173,6 +173,105 @@ __global__ void xgmi_table_start_kernel(const uint64_t* __restrict__ kout, int64
   tstart[t] = lo;
 }
 
+// ---- the same pull with device-side counts (no host read) -------------------
+// prefix[s] = entries of sources < s in this rank's inbox (clamped to cap);
+// prefix[W] = R, the device element count of the sort and the pull.
+__global__ void xgmi_pull_prefix_kernel(const int64_t* __restrict__ inbox_cnt, int world,
+                                        int64_t cap, int64_t* __restrict__ prefix, int* st) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int64_t acc = 0;
+  prefix[0] = 0;
+  for (int s = 0; s < world; ++s) {
+    int64_t c = inbox_cnt[s];
+    if (c < 0 || c > cap) {
+      latch(st, DR_INTERNAL);
+      c = c < 0 ? 0 : cap;
+    }
+    acc += c;
+    prefix[s + 1] = acc;
+  }
+}
+
+__device__ __forceinline__ int pull_source_dev(const int64_t* prefix, int world, int64_t e) {
+  int s = 0;
+  while (s + 1 < world && e >= prefix[s + 1]) ++s;
+  return s;
+}
+
+__global__ void xgmi_grad_keys_dev_kernel(const int64_t* __restrict__ prefix, int world,
+                                          int64_t cap, const int32_t* __restrict__ inbox_slot,
+                                          int T, int64_t TB, uint64_t* __restrict__ kin,
+                                          int32_t* __restrict__ vin) {
+  const int64_t R = prefix[world];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < R;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int s = pull_source_dev(prefix, world, e);
+    const int64_t slot = inbox_slot[(int64_t)s * cap + (e - prefix[s])];
+    const int64_t t = slot % T;
+    kin[e] = (uint64_t)(t * world + s) * (uint64_t)TB + (uint64_t)slot;
+    vin[e] = (int32_t)e;
+  }
+}
+
+// tstart[t] = first sorted position of table t; counts[t] = its entry count
+__global__ void xgmi_table_start_dev_kernel(const uint64_t* __restrict__ kout,
+                                            const int64_t* __restrict__ prefix, int T, int world,
+                                            int64_t TB, int64_t* __restrict__ tstart,
+                                            int64_t* __restrict__ counts) {
+  __shared__ int64_t ts[1025];
+  const int64_t R = prefix[world];
+  for (int t = threadIdx.x; t <= T; t += blockDim.x) {
+    const uint64_t lo_key = (uint64_t)t * (uint64_t)world * (uint64_t)TB;
+    int64_t lo = 0, hi = R;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (kout[mid] < lo_key)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    ts[t] = lo;
+    tstart[t] = lo;
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < T; t += blockDim.x) counts[t] = ts[t + 1] - ts[t];
+}
+
+// one 64-lane wave per sorted entry (grid-stride over the device count):
+// table t's entries land at t * tcap + (p - tstart[t]), tcap = world * batch
+// (every requester sends at most `batch` ids of a table)
+__global__ __launch_bounds__(256) void xgmi_grad_pull_dev_kernel(
+    const int64_t* __restrict__ prefix, int world, int64_t cap, XgmiPullArgs a, const int64_t* __restrict__ inbox_keys,
+    const int32_t* __restrict__ inbox_slot, const uint64_t* __restrict__ kout,
+    const int32_t* __restrict__ perm, const int64_t* __restrict__ tstart, int64_t TB,
+    int64_t tcap, int dim, int64_t row_stride, int64_t* __restrict__ keys_out,
+    float* __restrict__ grads_out) {
+  const int64_t R = prefix[world];
+  const int lane = threadIdx.x & 63;
+  const int64_t T = row_stride / dim;
+  for (int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < R;
+       p += (int64_t)gridDim.x * 4) {
+    const int64_t e = perm[p];
+    const int s = pull_source_dev(prefix, world, e);
+    const int64_t at = (int64_t)s * cap + (e - prefix[s]);
+    const int64_t slot = inbox_slot[at];
+    const int64_t tt = (int64_t)(kout[p] / ((uint64_t)world * (uint64_t)TB));
+    const int64_t q = tt * tcap + (p - tstart[tt]);
+    if (lane == 0) keys_out[q] = inbox_keys[at];
+    // slot j = b*T + t of the requester's [B, T*dim] gradient: row b, column t*dim
+    const int64_t b = slot / T, t = slot - b * T;
+    const float* g = a.gin[s] + b * row_stride + t * dim;
+    float* o = grads_out + q * (int64_t)dim;
+    if ((dim & 3) == 0) {
+      const float4* g4 = reinterpret_cast<const float4*>(g);
+      float4* o4 = reinterpret_cast<float4*>(o);
+      for (int c = lane; c < dim / 4; c += 64) o4[c] = g4[c];
+    } else {
+      for (int c = lane; c < dim; c += 64) o[c] = g[c];
+    }
+  }
+}
+
 }  // namespace dr
 
 namespace {
@@ -467,6 +566,81 @@ int dr_xgmi_grad_pull(const dr_xgmi_peers* peers, const float* const* grad_in,
   }
   hipLaunchKernelGGL(xgmi_table_start_kernel, dim3(1), dim3(1024), 0, st, kout, R, num_tables, W,
                      TB, table_start);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+size_t dr_xgmi_grad_pull_dev_workspace_size(int world, int64_t cap) {
+  using namespace dr;
+  const int64_t n = (int64_t)(world > 0 ? world : 1) * (cap > 0 ? cap : 1);
+  Carver c(nullptr);
+  c.take<int64_t>(DR_MAX_PEERS + 1);
+  c.take<int64_t>(1025);
+  c.take<uint64_t>(n);
+  c.take<int32_t>(n);
+  c.take<uint64_t>(n);
+  c.take<int32_t>(n);
+  c.take<char>(dr_sort_pairs_workspace_size(n));
+  return c.used + 256;
+}
+
+int dr_xgmi_grad_pull_dev(const dr_xgmi_peers* peers, const float* const* grad_in,
+                          int num_tables, int64_t batch, int dim, int64_t* keys_out,
+                          float* grads_out, int64_t* counts_out, void* ws, size_t ws_bytes,
+                          void* stream) {
+  using namespace dr;
+  DR_REQUIRE(peers && grad_in && keys_out && grads_out && counts_out && num_tables >= 1 &&
+                 batch >= 0 && dim > 0,
+             DR_INVALID_ARGUMENT, "bad argument");
+  const int W = peers->world;
+  DR_REQUIRE(W >= 1 && W <= DR_MAX_PEERS && peers->rank >= 0 && peers->rank < W,
+             DR_INVALID_ARGUMENT, "bad world/rank");
+  DR_REQUIRE(num_tables < 1024, DR_INVALID_ARGUMENT, "too many tables");
+  DR_REQUIRE(ws_bytes >= dr_xgmi_grad_pull_dev_workspace_size(W, peers->cap),
+             DR_INVALID_ARGUMENT, "workspace too small");
+  int* st = status_word();
+  DR_REQUIRE(st, DR_INTERNAL, "status word unavailable");
+  const int64_t TB = (int64_t)num_tables * batch;
+  XgmiPullArgs a;
+  memset(&a, 0, sizeof(a));
+  a.world = W;
+  a.cap = peers->cap;
+  for (int q = 0; q < W; ++q) {
+    DR_REQUIRE(grad_in[q], DR_INVALID_ARGUMENT, "peer %d gradient buffer not mapped", q);
+    a.gin[q] = grad_in[q];
+  }
+  hipStream_t s = S(stream);
+  const int me = peers->rank;
+  const int64_t* ikeys = peers->inbox_keys[me];
+  const int32_t* islot = peers->inbox_slot[me];
+  const int64_t* icnt = peers->inbox_cnt[me];
+  DR_REQUIRE(ikeys && islot && icnt, DR_INVALID_ARGUMENT, "own inbox not mapped");
+  const int64_t n = (int64_t)W * (peers->cap > 0 ? peers->cap : 1);
+  DR_REQUIRE(n < (1ll << 31), DR_INVALID_ARGUMENT, "inbox too large");
+  Carver c(ws);
+  int64_t* prefix = c.take<int64_t>(DR_MAX_PEERS + 1);
+  int64_t* tstart = c.take<int64_t>(1025);
+  uint64_t* kin = c.take<uint64_t>(n);
+  int32_t* vin = c.take<int32_t>(n);
+  uint64_t* kout = c.take<uint64_t>(n);
+  int32_t* perm = c.take<int32_t>(n);
+  void* sws = c.take<char>(dr_sort_pairs_workspace_size(n));
+  hipLaunchKernelGGL(xgmi_pull_prefix_kernel, dim3(1), dim3(64), 0, s, icnt, W, peers->cap,
+                     prefix, st);
+  const unsigned kb = (unsigned)std::min<int64_t>(ceil_div(n, 256), 4096);
+  hipLaunchKernelGGL(xgmi_grad_keys_dev_kernel, dim3(kb), dim3(256), 0, s, prefix, W, peers->cap,
+                     islot, num_tables, TB, kin, vin);
+  DR_LAUNCH_CHECK();
+  int bits = 1;
+  while (bits < 64 && ((uint64_t)num_tables * (uint64_t)W * (uint64_t)TB) >> bits) ++bits;
+  int rc = sort_pairs_u64_dev(kin, vin, kout, perm, n, prefix + W, bits, sws, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(xgmi_table_start_dev_kernel, dim3(1), dim3(1024), 0, s, kout, prefix,
+                     num_tables, W, TB, tstart, counts_out);
+  const unsigned pb = (unsigned)std::min<int64_t>(ceil_div(n, 4), 16384);
+  hipLaunchKernelGGL(xgmi_grad_pull_dev_kernel, dim3(pb), dim3(256), 0, s, prefix, W, peers->cap,
+                     a, ikeys, islot, kout, perm, tstart, TB, (int64_t)W * batch, dim,
+                     (int64_t)num_tables * dim, keys_out, grads_out);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

@@ -193,6 +193,8 @@ SIGNATURES = {
     "dr_xgmi_serve": (_I32, [_P, _P, _I32, _I64, _P, _SZ, _P]),
     "dr_xgmi_grad_pull_workspace_size": (_SZ, [_I32, _I64]),
     "dr_xgmi_grad_pull": (_I32, [_P, _P, _P, _I32, _I64, _I32, _P, _P, _P, _P, _SZ, _P]),
+    "dr_xgmi_grad_pull_dev_workspace_size": (_SZ, [_I32, _I64]),
+    "dr_xgmi_grad_pull_dev": (_I32, [_P, _P, _I32, _I64, _I32, _P, _P, _P, _P, _SZ, _P]),
     "dr_fm2": (_I32, [_P, _I64, _I32, _I32, _P, _P]),
     "dr_fm2_grad": (_I32, [_P, _P, _I64, _I32, _I32, _P, _P]),
     "dr_dot_interaction": (_I32, [_P, _I64, _I32, _I32, _P, _P]),

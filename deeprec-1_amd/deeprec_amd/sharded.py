@@ -521,36 +521,37 @@ class XgmiShardedLookup(object):
         Requester: the gradient goes into this rank's shared buffer; after a
         barrier every owner pulls, over xGMI, the rows of the (key, slot)
         pairs its inbox still holds from the forward, in (table, source,
-        slot) order (dr_xgmi_grad_pull), and queues one IndexedSlices per
+        slot) order (dr_xgmi_grad_pull_dev), and queues one IndexedSlices per
         table on its EVs -- the one-hot counterpart of
-        ShardedLookup.backward, without staging copies.  Returns the
-        per-table (keys, grads) slices."""
+        ShardedLookup.backward, without staging copies and without a host
+        read: the inbox counts stay on the device, table t's slice is the
+        fixed region [t*W*B, (t+1)*W*B) with a device count.  Returns the
+        per-table (keys, grads, count) -- count a DEVICE int64[1]; the first
+        count rows of keys / grads are the slice."""
         from .kv_variable_ops import IndexedSlices
         g = grad_out.contiguous()
-        T, D, B = self.T, self.dim, self.batch
+        T, D, B, W = self.T, self.dim, self.batch, self.world
         if tuple(g.shape) != (B, T * D) or g.dtype != torch.float32:
             raise ValueError("grad must be fp32 [%d, %d]" % (B, T * D))
         self.bufs.gin.copy_(g)
         self._barrier()
-        cnt = self.bufs.inbox_cnt.cpu()                 # this rank's inbox counts (sync)
-        R = int(cnt.sum())
-        keys = torch.empty(max(R, 1), dtype=torch.int64, device=self.device)
-        grads = torch.empty((max(R, 1), D), dtype=torch.float32, device=self.device)
-        tstart = torch.empty(T + 1, dtype=torch.int64, device=self.device)
-        wsb = lib().dr_xgmi_grad_pull_workspace_size(self.world, self.bufs.cap)
+        tcap = W * B
+        keys = torch.empty(T * tcap, dtype=torch.int64, device=self.device)
+        grads = torch.empty((T * tcap, D), dtype=torch.float32, device=self.device)
+        counts = torch.empty(T, dtype=torch.int64, device=self.device)
+        wsb = lib().dr_xgmi_grad_pull_dev_workspace_size(W, self.bufs.cap)
         ws = workspace(wsb, self.device)
-        ch = (C.c_int64 * self.world)(*[int(x) for x in cnt.tolist()])
-        check(lib().dr_xgmi_grad_pull(C.byref(self.peers), self.gin_ptrs, ch, T, B, D, ptr(keys),
-                                      ptr(grads), ptr(tstart), ptr(ws), wsb,
-                                      stream_handle(self.device)))
+        check(lib().dr_xgmi_grad_pull_dev(C.byref(self.peers), self.gin_ptrs, T, B, D, ptr(keys),
+                                          ptr(grads), ptr(counts), ptr(ws), wsb,
+                                          stream_handle(self.device)))
         ops._post(self.device)
         self._barrier()          # no peer's next route() may overwrite the inbox before the pull
-        ts = tstart.cpu().tolist()
         out = []
         for t in range(T):
-            k, v = keys[ts[t]:ts[t + 1]], grads[ts[t]:ts[t + 1]]
-            out.append((k, v))
-            self.evs[t].pending_grads.append(IndexedSlices(v, k, unique=False))
+            k, v = keys[t * tcap:(t + 1) * tcap], grads[t * tcap:(t + 1) * tcap]
+            n = counts[t:t + 1]
+            out.append((k, v, n))
+            self.evs[t].pending_grads.append(IndexedSlices(v, k, num_valid=n, unique=False))
         return out
 
     def forward(self, ids):

@@ -657,6 +657,16 @@ int dr_xgmi_grad_pull(const dr_xgmi_peers* peers, const float* const* grad_in,
                       const int64_t* cnt_host, int num_tables, int64_t batch, int dim,
                       int64_t* keys_out, float* grads_out, int64_t* table_start, void* ws,
                       size_t ws_bytes, void* stream);
+/* The same without any host read: the inbox counts are read on the device,  */
+/* and table t's entries (sorted by (source, slot)) land in its fixed region */
+/* keys_out[t*W*batch ...], grads_out[t*W*batch ...] (every requester sends  */
+/* at most `batch` ids of a table); counts_out[t] (DEVICE int64) = how many. */
+/* The optimizer takes the region with counts_out[t] as its device count.    */
+size_t dr_xgmi_grad_pull_dev_workspace_size(int world, int64_t cap);
+int dr_xgmi_grad_pull_dev(const dr_xgmi_peers* peers, const float* const* grad_in,
+                          int num_tables, int64_t batch, int dim, int64_t* keys_out,
+                          float* grads_out, int64_t* counts_out, void* ws, size_t ws_bytes,
+                          void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Interactions (callers of the path).                                       */

@@ -90,9 +90,10 @@ def worker(rank, world, port):
                 sel = np.nonzero(ids_s[t] % world == rank)[0]
                 wk.append(ids_s[t][sel])
                 wg.append(g_s[sel, t * D:(t + 1) * D])
-            k, v = got[t]
-            bwd_ok = bwd_ok and np.array_equal(k.cpu().numpy(), np.concatenate(wk)) and \
-                np.array_equal(v.cpu().numpy(), np.concatenate(wg).reshape(-1, D))
+            k, v, n = got[t]
+            m = int(n.item())
+            bwd_ok = bwd_ok and np.array_equal(k[:m].cpu().numpy(), np.concatenate(wk)) and \
+                np.array_equal(v[:m].cpu().numpy(), np.concatenate(wg).reshape(-1, D))
             evs[t].pending_grads.clear()
     dr.status_check(dev)
     for ev in evs:
