@@ -643,6 +643,306 @@ __global__ __launch_bounds__(512, 1) void crossnet_glds3_kernel(
   }
 }
 
+// The same layer with a 256 x 256 tile: 8 waves as 2 (M) x 4 (N), each
+// wave 128 x 64 (8 x 4 v_mfma_f32_16x16x32_bf16 accumulators), K step 64,
+// both operands staged by global_load_lds_dwordx4 into two 64 KB LDS
+// buffers (tile k+1's DMA in flight while tile k is multiplied; one counted
+// vmcnt + s_barrier before the reads, one s_barrier before a buffer is
+// restaged).  Why 256^2: the 128-wide tiles above read 8 fragments per 16
+// MFMAs from LDS, which at 8 waves per CU is the LDS's whole bandwidth (the
+// 824 TF ceiling measured in round 1); a 128 x 64 wave tile reads 12 per 32.
+static constexpr int C4_BM = 256, C4_BN = 256, C4_BK = 64;
+static constexpr int C4_OP_BYTES = C4_BM * C4_BK * 2;     // 32 KB per operand per buffer
+static constexpr int C4_STAGE = 2 * C4_OP_BYTES;          // 64 KB
+
+__global__ __launch_bounds__(512, 1) void crossnet_256_kernel(
+    const uint16_t* __restrict__ x0, const uint16_t* __restrict__ xl,
+    const uint16_t* __restrict__ W, const float* __restrict__ bias, int64_t M, int d,
+    uint16_t* __restrict__ out, uint16_t* __restrict__ lin_out) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * C4_STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int64_t nwg = (int64_t)gridDim.x;
+  const int64_t orig = blockIdx.x;
+  const int64_t xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t tile = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int ntn = d / C4_BN + (d % C4_BN ? 1 : 0);
+  const int64_t m0 = (tile / ntn) * C4_BM;
+  const int n0 = (int)(tile % ntn) * C4_BN;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = d / C4_BK;
+  cg_stage_n<4>(xl, M, m0, d, 0, lds, wave, lane);
+  cg_stage_n<4>(W, d, n0, d, 0, lds + C4_OP_BYTES, wave, lane);
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = lds + (kt & 1) * C4_STAGE;
+    if (kt + 1 < nk) {
+      char* nxt = lds + ((kt + 1) & 1) * C4_STAGE;
+      cg_stage_n<4>(xl, M, m0, d, (kt + 1) * C4_BK, nxt, wave, lane);
+      cg_stage_n<4>(W, d, n0, d, (kt + 1) * C4_BK, nxt + C4_OP_BYTES, wave, lane);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's tile-kt DMAs landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // ... and every other wave's
+    asm volatile("" ::: "memory");
+    const char* sA = cur;
+    const char* sB = cur + C4_OP_BYTES;
+#ifndef DR_C4_BATCHED_FRAGS
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[8], fb[4];
+      const int lc = kk * 4 + fq;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = cg_frag(sB, wc * 64 + j * 16 + fr, lc);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[i] = cg_frag(sA, wr * 128 + i * 16 + fr, lc);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+#else
+    // all 24 fragment reads of the K step issued up front: the second k
+    // half's reads overlap the first half's MFMAs (224 VGPRs)
+    bf16x8 fa[2][8], fb[2][4];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int lc = kk * 4 + fq;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[kk][j] = cg_frag(sB, wc * 64 + j * 16 + fr, lc);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[kk][i] = cg_frag(sA, wr * 128 + i * 16 + fr, lc);
+    }
+    // keep the reads ahead of the MFMAs: left alone, the scheduler sinks
+    // each read to its first use and waits lgkmcnt(0) every 8 MFMAs
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
+#endif
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // buffer kt&1 is restaged by iteration kt+1's DMA
+    asm volatile("" ::: "memory");
+  }
+  // Epilogue in two row halves of the wave tile (LDS: 8 waves x 16 KB), each
+  // as in crossnet_glds_kernel: accumulators -> swizzled fp32 image -> 8
+  // columns per lane, so x0 / xl / out / lin move as 16-B vectors.
+  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+  float* ct = reinterpret_cast<float*>(lds) + wave * 64 * 64;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();   // this wave's region is free again
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i * 16 + fq * 4 + r;
+          const int col = (j * 16 + fr) ^ (((row >> 2) & 3) << 4);
+          ct[row * 64 + col] = acc[h * 4 + i][j][r];
+        }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int idx = it * 64 + lane;
+      const int row = idx >> 3, cc = (idx & 7) * 8;
+      const int64_t grow = m0 + wr * 128 + h * 64 + row;
+      const int gcol = n0 + wc * 64 + cc;
+      if (grow >= M || gcol >= d) continue;
+      const int pc = cc ^ (((row >> 2) & 3) << 4);
+      const float4 l0 = *reinterpret_cast<const float4*>(ct + row * 64 + pc);
+      const float4 l1 = *reinterpret_cast<const float4*>(ct + row * 64 + pc + 4);
+      float lin[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+      if (bias) {
+        const float4 b0 = *reinterpret_cast<const float4*>(bias + gcol);
+        const float4 b1 = *reinterpret_cast<const float4*>(bias + gcol + 4);
+        lin[0] += b0.x; lin[1] += b0.y; lin[2] += b0.z; lin[3] += b0.w;
+        lin[4] += b1.x; lin[5] += b1.y; lin[6] += b1.z; lin[7] += b1.w;
+      }
+      const int64_t o = grow * d + gcol;
+      const u32x4 a0 = *reinterpret_cast<const u32x4*>(x0 + o);
+      const u32x4 al = *reinterpret_cast<const u32x4*>(xl + o);
+      u32x4 ov, lv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t p0 = a0[e], pl = al[e];
+        const float v0 = bf2f((uint16_t)(p0 & 0xffff)) * lin[2 * e] + bf2f((uint16_t)(pl & 0xffff));
+        const float v1 = bf2f((uint16_t)(p0 >> 16)) * lin[2 * e + 1] + bf2f((uint16_t)(pl >> 16));
+        ov[e] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+        lv[e] = (uint32_t)f2bf(lin[2 * e]) | ((uint32_t)f2bf(lin[2 * e + 1]) << 16);
+      }
+      *reinterpret_cast<u32x4*>(out + o) = ov;
+      if (lin_out) *reinterpret_cast<u32x4*>(lin_out + o) = lv;
+    }
+  }
+}
+
+// The 256 x 256 layer with the two wave groups STAGGERED by one barrier, so
+// that on every SIMD one wave multiplies while its partner stages and waits
+// (waves w and w+4 share a SIMD; group g = w / 4 owns output rows
+// g*128..+127).  Per K step each wave runs  [issue DMAs of tile k+1; counted
+// vmcnt for tile k] barrier [24 fragment reads + 64 MFMAs] barrier,  group 1
+// one barrier behind group 0, so the MFMA windows of the two groups
+// alternate.  The stagger moves a shared buffer's last read one window later,
+// so: the A half-tiles are group-private (each group stages its own 128 rows,
+// 2 buffers), and B -- read by both groups -- is staged by group 0 alone into
+// 3 buffers (2 x 32 KB + 3 x 32 KB = 160 KB).  Ordering, windows n between
+// barriers n and n+1 (group 0 computes tile k in window 2k, group 1 in 2k+1):
+//   RAW  B(k+1), A_top(k+1): issued by group 0 in window 2k-1, vmcnt-retired
+//        before barrier 2k+2, read in windows 2k+2 / 2k+3;  A_bot(k+1): issued
+//        by group 1 in window 2k, retired before barrier 2k+3, read in 2k+3.
+//   WAR  B buffer (k+1)%3 last held tile k-2, whose last reads (group 1, window
+//        2k-3) retired before barrier 2k-2; A buffers: the owner group's last
+//        reads of tile k-1 retired one barrier before its next DMA.
+static constexpr int CS_A_BYTES = 256 * 128;   // one A tile (two 128-row halves)
+static constexpr int CS_B_BYTES = 256 * 128;
+static constexpr int CS_LDS = 2 * CS_A_BYTES + 3 * CS_B_BYTES;  // 160 KB
+
+__global__ __launch_bounds__(512, 1) void crossnet_stag_kernel(
+    const uint16_t* __restrict__ x0, const uint16_t* __restrict__ xl,
+    const uint16_t* __restrict__ W, const float* __restrict__ bias, int64_t M, int d,
+    uint16_t* __restrict__ out, uint16_t* __restrict__ lin_out) {
+  __shared__ __attribute__((aligned(1024))) char lds[CS_LDS];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const bool g1 = wr != 0;
+  const int64_t nwg = (int64_t)gridDim.x;
+  const int64_t orig = blockIdx.x;
+  const int64_t xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t tile = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int ntn = d / 256 + (d % 256 ? 1 : 0);
+  const int64_t m0 = (tile / ntn) * 256;
+  const int n0 = (int)(tile % ntn) * 256;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = d / 64;
+  char* const bbase = lds + 2 * CS_A_BYTES;
+  auto stage = [&](int kt) {
+    const int k0 = kt * 64;
+    char* a = lds + (kt & 1) * CS_A_BYTES;
+    if (!g1) {
+      cg_stage_n<4>(xl, M, m0, d, k0, a, wc, lane);
+      cg_stage_n<8>(W, d, n0, d, k0, bbase + (kt % 3) * CS_B_BYTES, wc, lane);
+    } else {
+      cg_stage_n<4>(xl, M, m0 + 128, d, k0, a + 128 * 128, wc, lane);
+    }
+  };
+  stage(0);
+  if (g1) __builtin_amdgcn_s_barrier();  // the stagger: group 1 one barrier behind
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) {
+      stage(kt + 1);
+      if (!g1)
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // tile kt's 12 DMAs of this wave
+      else
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const char* sA = lds + (kt & 1) * CS_A_BYTES;
+    const char* sB = bbase + (kt % 3) * CS_B_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[8], fb[4];
+      const int lc = kk * 4 + fq;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = cg_frag(sB, wc * 64 + j * 16 + fr, lc);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[i] = cg_frag(sA, wr * 128 + i * 16 + fr, lc);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  if (!g1) __builtin_amdgcn_s_barrier();  // matches group 1's extra barrier
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+  float* ct = reinterpret_cast<float*>(lds) + wave * 64 * 64;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i * 16 + fq * 4 + r;
+          const int col = (j * 16 + fr) ^ (((row >> 2) & 3) << 4);
+          ct[row * 64 + col] = acc[h * 4 + i][j][r];
+        }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int idx = it * 64 + lane;
+      const int row = idx >> 3, cc = (idx & 7) * 8;
+      const int64_t grow = m0 + wr * 128 + h * 64 + row;
+      const int gcol = n0 + wc * 64 + cc;
+      if (grow >= M || gcol >= d) continue;
+      const int pc = cc ^ (((row >> 2) & 3) << 4);
+      const float4 l0 = *reinterpret_cast<const float4*>(ct + row * 64 + pc);
+      const float4 l1 = *reinterpret_cast<const float4*>(ct + row * 64 + pc + 4);
+      float lin[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+      if (bias) {
+        const float4 b0 = *reinterpret_cast<const float4*>(bias + gcol);
+        const float4 b1 = *reinterpret_cast<const float4*>(bias + gcol + 4);
+        lin[0] += b0.x; lin[1] += b0.y; lin[2] += b0.z; lin[3] += b0.w;
+        lin[4] += b1.x; lin[5] += b1.y; lin[6] += b1.z; lin[7] += b1.w;
+      }
+      const int64_t o = grow * d + gcol;
+      const u32x4 a0 = *reinterpret_cast<const u32x4*>(x0 + o);
+      const u32x4 al = *reinterpret_cast<const u32x4*>(xl + o);
+      u32x4 ov, lv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t p0 = a0[e], pl = al[e];
+        const float v0 = bf2f((uint16_t)(p0 & 0xffff)) * lin[2 * e] + bf2f((uint16_t)(pl & 0xffff));
+        const float v1 = bf2f((uint16_t)(p0 >> 16)) * lin[2 * e + 1] + bf2f((uint16_t)(pl >> 16));
+        ov[e] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+        lv[e] = (uint32_t)f2bf(lin[2 * e]) | ((uint32_t)f2bf(lin[2 * e + 1]) << 16);
+      }
+      *reinterpret_cast<u32x4*>(out + o) = ov;
+      if (lin_out) *reinterpret_cast<u32x4*>(lin_out + o) = lv;
+    }
+  }
+}
+
 }  // namespace dr
 
 extern "C" {
@@ -743,7 +1043,23 @@ int dr_crossnet_forward_bf16(const uint16_t* x0, const uint16_t* xl, const uint1
   static const bool legacy = getenv("DR_CROSSNET_LEGACY") != nullptr;
   const bool al16 = (((uintptr_t)bias | (uintptr_t)out | (uintptr_t)lin_out) & 15) == 0;
   static const int variant = getenv("DR_CROSSNET_VARIANT") ? atoi(getenv("DR_CROSSNET_VARIANT"))
-                                                           : 3;
+                                                           : 5;
+  if (d % 64 == 0 && !legacy && al16 && variant == 5) {
+    const int64_t tiles = ceil_div(batch, 256) * ceil_div(d, 256);
+    DR_REQUIRE(tiles < (1ll << 31), DR_INVALID_ARGUMENT, "batch too large");
+    hipLaunchKernelGGL(crossnet_stag_kernel, dim3((unsigned)tiles), dim3(512), 0, S(stream), x0,
+                       xl, W, bias, batch, d, out, lin_out);
+    DR_LAUNCH_CHECK();
+    return DR_OK;
+  }
+  if (d % C4_BK == 0 && !legacy && al16 && variant == 4) {
+    const int64_t tiles = ceil_div(batch, C4_BM) * ceil_div(d, C4_BN);
+    DR_REQUIRE(tiles < (1ll << 31), DR_INVALID_ARGUMENT, "batch too large");
+    hipLaunchKernelGGL(crossnet_256_kernel, dim3((unsigned)tiles), dim3(512), 0, S(stream), x0,
+                       xl, W, bias, batch, d, out, lin_out);
+    DR_LAUNCH_CHECK();
+    return DR_OK;
+  }
   if (d % C3_BK == 0 && !legacy && al16 && variant == 3) {
     const int64_t tiles = ceil_div(batch, C3_BM) * ceil_div(d, C3_BN);
     DR_REQUIRE(tiles < (1ll << 31), DR_INVALID_ARGUMENT, "batch too large");

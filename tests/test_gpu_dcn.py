@@ -117,3 +117,23 @@ def _rows(ev, R):
     out = torch.zeros(R, ev.dim, device=DEV)
     out[k] = v
     return out
+
+
+@pytest.mark.parametrize("B,d", [(4096, 3392), (1000, 512)])
+def test_crossnet_large_tile_repeatable(B, d):
+    """The 256 x 256 glds kernel at the DCN width over many full and partial
+    tiles: within bf16 tolerance of torch, and bit-identical over repeated
+    launches (an LDS staging race would show as launch-to-launch drift)."""
+    from deeprec_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(B ^ d)
+    x0 = torch.randn(B, d, generator=g).to(DEV, torch.bfloat16)
+    xl = torch.randn(B, d, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(d, d, generator=g) / d ** 0.5).to(DEV, torch.bfloat16)
+    b = torch.randn(d, generator=g).to(DEV)
+    out, lin = ops.crossnet_forward(x0, xl, W, b)
+    want, wlin = _ref(x0, xl, W, b)
+    _close(out, want)
+    _close(lin, wlin)
+    for _ in range(6):
+        o2, l2 = ops.crossnet_forward(x0, xl, W, b)
+        assert torch.equal(o2, out) and torch.equal(l2, lin)
