@@ -645,7 +645,7 @@ def main():
             "kernel": "dr::ev_lookup_onehot_kernel<4,32,1,ALI,4> (+ 3 miss-list kernels, empty)",
             "kernel_ms": round(k_ms, 4),
             "bytes_per_launch": bytes_launch, "bytes_per_lookup": per_lookup}
-    for obj, fname, kname in ((roof, "r01_pmc_traffic.json", "ev_lookup_onehot_kernel"),
+    for obj, fname, kname in ((roof, "r02_pmc_traffic.json", "ev_lookup_onehot_kernel"),
                               (roof_gather, "r01_pmc_traffic_row_gather.json",
                                "pool_onehot_kernel")):
         pmc = os.path.join(ROOT, "profiles", fname)

@@ -41,8 +41,11 @@ struct RowsGroup {
 };
 
 static constexpr int64_t kRowsChunk = 256;
-static constexpr int kRowsChain = 4;        // positions of a chunk fetched per step
-static constexpr int kRowsFinishChain = 16;  // chunk partials fetched per step
+#ifndef DR_ROWS_CHAIN
+#define DR_ROWS_CHAIN 8
+#endif
+static constexpr int kRowsChain = DR_ROWS_CHAIN;  // positions of a chunk fetched per step
+static constexpr int kRowsFinishMax = 32;    // chunk partials fetched per step (at most)
 static constexpr int64_t kRowsMaxDim = 1024;
 
 // Table of global position i (lane-varying; koff staged in LDS).
@@ -361,27 +364,41 @@ __global__ __launch_bounds__(256) void rows_finish_kernel(
     const int64_t o = longs[2 * i], c0 = longs[2 * i + 1];
     const uint32_t u = skey[c0];
     const int t = tab_of(sk, T, perm[c0]);
+    const int64_t kt0 = sk[t], nnz_t = sk[t + 1] - sk[t];
     R acc;
     load_row_u<VEC, G, CPL>(acc, gu + o * (int64_t)dim, lg, dv);
-    for (int64_t m = (c0 / kRowsChunk + 1) * kRowsChunk; m < N;
-         m += kRowsFinishChain * kRowsChunk) {
-      R y[kRowsFinishChain];
-      bool ok[kRowsFinishChain];
+    // <= 128 floats of partial rows in flight per lane
+    constexpr int FC = 128 / (VEC * CPL) < 8 ? 8
+                       : (128 / (VEC * CPL) > kRowsFinishMax ? kRowsFinishMax
+                                                             : 128 / (VEC * CPL));
+    for (int64_t m = (c0 / kRowsChunk + 1) * kRowsChunk; m < N; m += FC * kRowsChunk) {
+      R y[FC];
+      bool ok[FC];
+      uint32_t kj[FC];
+      int32_t pj[FC];
+      // unconditional, clamped loads first: a short-circuit test per chunk
+      // would branch around each load and serialise them
 #pragma unroll
-      for (int j = 0; j < kRowsFinishChain; ++j) {
+      for (int j = 0; j < FC; ++j) {
         const int64_t mj = m + j * kRowsChunk;
         const int64_t mc = mj < N ? mj : N - 1;
-        ok[j] = (mj < N) && skey[mc] == u && tab_of(sk, T, perm[mc]) == t;
+        kj[j] = skey[mc];
+        pj[j] = perm[mc];
         int64_t sl = mc / kRowsChunk;
         sl = sl < nslots ? sl : nslots - 1;
         load_row_u<VEC, G, CPL>(y[j], part + sl * (int64_t)dim, lg, dv);
       }
 #pragma unroll
-      for (int j = 0; j < kRowsFinishChain; ++j) {
+      for (int j = 0; j < FC; ++j) {
+        const int64_t k = (int64_t)pj[j] - kt0;   // in table t <=> in [0, nnz_t)
+        ok[j] = (m + j * kRowsChunk < N) & (kj[j] == u) & (k >= 0) & (k < nnz_t);
+      }
+#pragma unroll
+      for (int j = 0; j < FC; ++j) {
         if (!ok[j]) break;
         acc_add(acc, y[j]);
       }
-      if (!ok[kRowsFinishChain - 1]) break;
+      if (!ok[FC - 1]) break;
     }
     store_row<VEC, G, CPL>(acc, gu + o * (int64_t)dim, lg, dv);
   }
