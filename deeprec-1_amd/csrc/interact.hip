@@ -943,6 +943,271 @@ __global__ __launch_bounds__(512, 1) void crossnet_stag_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// The 256 x 256 layer with four phases per K tile (the guide's 8-phase
+// schedule, two K tiles per 8 phases).  Each wave owns 128 x 64 outputs as
+// four 64 x 32 quadrants; a phase multiplies ONE quadrant over K = 64 (16
+// MFMAs).  The LDS tile is cut into half-tiles that each phase reads once:
+//   A_h0 = the first 64 rows of both wave groups' 128-row halves,
+//   A_h1 = their last 64 rows, B_h0 / B_h1 = the first / last 32 of every
+//   wave's 64 output columns (W rows),
+// so phase 1 reads A_h0 + B_h0 (quadrant m0n0), phase 2 B_h1 (m0n1), phase 3
+// A_h1 (m1n0, B_h0 still in registers), phase 4 nothing (m1n1).  One
+// half-tile is staged per phase (2 global_load_lds per thread):
+//   p1: A_h1(t+1)   p2: A_h0(t+2)   p3: B_h0(t+2)   p4: B_h1(t+2)
+// each into a half that was last read at least one phase earlier, and
+// s_waitcnt vmcnt(6) in p4 retires tile t+1 while tile t+2's three halves
+// stay in flight across the barriers.  The two wave groups (waves w, w+4
+// share a SIMD) run staggered by one barrier: between two barriers one group
+// multiplies (s_setprio 1) while the other issues its LDS reads and DMAs.
+// Ordering (window n = between barriers n and n+1; group g reads phase p in
+// window 2p+g and multiplies it in 2p+1+g):
+//   WAR  every wave retires its reads with lgkmcnt(0) BEFORE the barrier
+//        that closes its read window, so a DMA issued one phase later (by
+//        either group) cannot overtake them;
+//   RAW  every wave retires its own DMAs with the counted vmcnt before the
+//        barrier that closes its p4 read window; reads of that tile start in
+//        the next phase, after a barrier every wave passed behind its wait.
+// ---------------------------------------------------------------------------
+static constexpr int C8_HALF = 128 * 128;  // one half-tile image: 128 rows x 64 bf16
+static constexpr int C8_BUF = 4 * C8_HALF;  // [A_h0 | A_h1 | B_h0 | B_h1]
+
+// Stage one half-tile: image row r (0..127) <- global row row0 + map(r),
+// 2 wave instructions of 8 rows x 128 B per wave.  AH: A half (image row r ->
+// tile row (r >> 6) * 128 + h * 64 + (r & 63)); otherwise B half (r -> tile
+// col (r >> 5) * 64 + h * 32 + (r & 31)).
+template <bool AH>
+__device__ __forceinline__ void c8_stage(const uint16_t* __restrict__ X, int64_t rows_valid,
+                                         int64_t row0, int h, int d, int k0, char* img, int wave,
+                                         int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r0 = (wave * 2 + i) * 8;
+    const int r = r0 + (lane >> 3);
+    const int lc = (lane & 7) ^ ((r >> 1) & 7);
+    const int tr = AH ? ((r >> 6) * 128 + h * 64 + (r & 63)) : ((r >> 5) * 64 + h * 32 + (r & 31));
+    int64_t gr = row0 + tr;
+    if (gr >= rows_valid) gr = rows_valid - 1;  // rows past the end feed discarded outputs
+    const uint16_t* src = X + gr * (int64_t)d + k0 + lc * 8;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(img + r0 * 128),
+                                     16, 0, 0);
+  }
+}
+
+template <bool EPI, int GM, bool PIPE>
+__global__ __launch_bounds__(512, 1) void crossnet_8ph_kernel(
+    const uint16_t* __restrict__ x0, const uint16_t* __restrict__ xl,
+    const uint16_t* __restrict__ W, const float* __restrict__ bias, int64_t M, int d,
+    uint16_t* __restrict__ out, uint16_t* __restrict__ lin_out) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * C8_BUF];  // 128 KB
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const bool g1 = wr != 0;
+  const int64_t nwg = (int64_t)gridDim.x;
+  const int64_t orig = blockIdx.x;
+  const int64_t xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t tile = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int ntn = d / 256 + (d % 256 ? 1 : 0);
+  int64_t m0;
+  int n0;
+  if (GM <= 1) {  // row-major: an XCD's running tiles span ~2 row panels x all columns
+    m0 = (tile / ntn) * 256;
+    n0 = (int)(tile % ntn) * 256;
+  } else {  // groups of GM row panels walked column-major: GM x (32 / GM) running tiles
+    const int64_t ntm = (M + 255) / 256;
+    const int64_t g = tile / ((int64_t)GM * ntn), idx = tile % ((int64_t)GM * ntn);
+    const int64_t rows = ntm - g * GM < GM ? ntm - g * GM : GM;
+    m0 = (g * GM + idx % rows) * 256;
+    n0 = (int)(idx / rows) * 256;
+  }
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = d / 64;
+  auto img = [&](int t, int part) -> char* { return lds + (t & 1) * C8_BUF + part * C8_HALF; };
+  auto st_a = [&](int t, int h) { c8_stage<true>(xl, M, m0, h, d, t * 64, img(t, h), wave, lane); };
+  auto st_b = [&](int t, int h) {
+    c8_stage<false>(W, d, n0, h, d, t * 64, img(t, 2 + h), wave, lane);
+  };
+  // prologue: tile 0 whole, tile 1 but its A_h1 (issued in tile 0's p1)
+  st_a(0, 0); st_b(0, 0); st_b(0, 1); st_a(0, 1);
+  if (nk > 1) {
+    st_a(1, 0); st_b(1, 0); st_b(1, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (g1) __builtin_amdgcn_s_barrier();  // the stagger
+  asm volatile("" ::: "memory");
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];  // [frag][kk]
+  auto read_a = [&](const char* s) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = cg_frag(s, wr * 64 + i * 16 + fr, kk * 4 + fq);
+  };
+  auto read_b = [&](const char* s, bf16x8 (&fb)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fb[j][kk] = cg_frag(s, wc * 32 + j * 16 + fr, kk * 4 + fq);
+  };
+  auto close_read = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto mma = [&](int mi, bf16x8 (&fb)[2][2], int nj) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mi + i][nj + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb[j][kk], acc[mi + i][nj + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  for (int t = 0; t < nk; ++t) {
+    const bool pf1 = t + 1 < nk, pf2 = t + 2 < nk;
+    // p1: m0n0
+    read_b(img(t, 2), fb0);
+    read_a(img(t, 0));
+    if (pf1) st_a(t + 1, 1);
+    close_read();
+    mma(0, fb0, 0);
+    // p2: m0n1
+    read_b(img(t, 3), fb1);
+    if (pf2) st_a(t + 2, 0);
+    close_read();
+    mma(0, fb1, 2);
+    // p3: m1n0
+    read_a(img(t, 1));
+    if (pf2) st_b(t + 2, 0);
+    close_read();
+    mma(4, fb0, 0);
+    // p4: m1n1
+    if (pf2) {
+      st_b(t + 2, 1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // tile t+1 landed (this wave's DMAs)
+    } else if (pf1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    close_read();
+    mma(4, fb1, 2);
+  }
+  if (!g1) __builtin_amdgcn_s_barrier();  // matches group 1's extra barrier
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (!EPI) {  // loop-only timing build: keep the MFMAs alive, store nothing
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (sum == 1234.5678f) out[0] = 0;
+    return;
+  }
+  // Epilogue: per 64-row half, this wave's x0 / xl vectors are requested
+  // first (addresses clamped, stores predicated), the accumulators go
+  // through LDS (C/D map -> 8 columns per lane), then out / lin are formed
+  // and stored as 16-B vectors.
+  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+  float* ct = reinterpret_cast<float*>(lds) + wave * 64 * 64;
+  const int cc = (lane & 7) * 8;
+  const int gcol = n0 + wc * 64 + cc;
+  const bool col_ok = gcol < d;
+  const int gcol_c = col_ok ? gcol : d - 8;
+  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(bias + gcol_c);
+    const float4 b1 = *reinterpret_cast<const float4*>(bias + gcol_c + 4);
+    bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
+    bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+  }
+  // x0 / xl vectors of rows [h*64, h*64+64) of this wave's 128 (addresses
+  // clamped; stores are predicated instead)
+  auto load_half = [&](int h, u32x4 (&a0)[8], u32x4 (&al)[8]) {
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      int64_t grow = m0 + wr * 128 + h * 64 + it * 8 + (lane >> 3);
+      if (grow >= M) grow = M - 1;
+      const int64_t o = grow * d + gcol_c;
+      a0[it] = *reinterpret_cast<const u32x4*>(x0 + o);
+      al[it] = *reinterpret_cast<const u32x4*>(xl + o);
+    }
+  };
+  auto acc_to_lds = [&](int h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i * 16 + fq * 4 + r;
+          const int col = (j * 16 + fr) ^ (((row >> 2) & 3) << 4);
+          ct[row * 64 + col] = acc[h * 4 + i][j][r];
+        }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  auto finish_half = [&](int h, const u32x4 (&a0)[8], const u32x4 (&al)[8]) {
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int row = it * 8 + (lane >> 3);
+      const int64_t grow = m0 + wr * 128 + h * 64 + row;
+      const int pc = cc ^ (((row >> 2) & 3) << 4);
+      const float4 l0 = *reinterpret_cast<const float4*>(ct + row * 64 + pc);
+      const float4 l1 = *reinterpret_cast<const float4*>(ct + row * 64 + pc + 4);
+      float lin[8] = {l0.x + bv[0], l0.y + bv[1], l0.z + bv[2], l0.w + bv[3],
+                      l1.x + bv[4], l1.y + bv[5], l1.z + bv[6], l1.w + bv[7]};
+      u32x4 ov, lv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t p0 = a0[it][e], pl = al[it][e];
+        const float v0 = bf2f((uint16_t)(p0 & 0xffff)) * lin[2 * e] + bf2f((uint16_t)(pl & 0xffff));
+        const float v1 = bf2f((uint16_t)(p0 >> 16)) * lin[2 * e + 1] + bf2f((uint16_t)(pl >> 16));
+        ov[e] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+        lv[e] = (uint32_t)f2bf(lin[2 * e]) | ((uint32_t)f2bf(lin[2 * e + 1]) << 16);
+      }
+      if (grow < M && col_ok) {
+        const int64_t o = grow * d + gcol;
+        *reinterpret_cast<u32x4*>(out + o) = ov;
+        if (lin_out) *reinterpret_cast<u32x4*>(lin_out + o) = lv;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ct reads done before it is rewritten
+    __builtin_amdgcn_wave_barrier();
+  };
+  if (PIPE) {  // h = 1's loads in flight while h = 0 is formed and stored
+    u32x4 a00[8], al0[8], a01[8], al1[8];
+    load_half(0, a00, al0);
+    acc_to_lds(0);
+    load_half(1, a01, al1);
+    finish_half(0, a00, al0);
+    acc_to_lds(1);
+    finish_half(1, a01, al1);
+  } else {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      u32x4 a0[8], al[8];
+      load_half(h, a0, al);
+      acc_to_lds(h);
+      finish_half(h, a0, al);
+    }
+  }
+}
+
 }  // namespace dr
 
 extern "C" {
@@ -1042,8 +1307,27 @@ int dr_crossnet_forward_bf16(const uint16_t* x0, const uint16_t* xl, const uint1
   if (batch == 0) return DR_OK;
   static const bool legacy = getenv("DR_CROSSNET_LEGACY") != nullptr;
   const bool al16 = (((uintptr_t)bias | (uintptr_t)out | (uintptr_t)lin_out) & 15) == 0;
+  // 8 = crossnet_8ph_kernel (default); the others are kept for A/B runs
+  // (tools/gpu_crossnet_v.sh): 5 stag, 4 256^2, 3 glds3, 6/9/10 8ph with other
+  // tile orders / epilogue, 7 the 8ph loop alone (no outputs: timing only)
   static const int variant = getenv("DR_CROSSNET_VARIANT") ? atoi(getenv("DR_CROSSNET_VARIANT"))
-                                                           : 5;
+                                                           : 8;
+  if (d % 64 == 0 && !legacy && al16 && (variant >= 6 && variant <= 10)) {
+    const int64_t tiles = ceil_div(batch, 256) * ceil_div(d, 256);
+    DR_REQUIRE(tiles < (1ll << 31), DR_INVALID_ARGUMENT, "batch too large");
+#define DR_C8(E, G, P)                                                                     \
+  hipLaunchKernelGGL((crossnet_8ph_kernel<E, G, P>), dim3((unsigned)tiles), dim3(512), 0,   \
+                     S(stream), x0, xl, W, bias, batch, d, out, lin_out)
+    if (variant == 6) DR_C8(true, 1, false);
+    else if (variant == 8) DR_C8(true, 4, false);
+    else if (variant == 9) DR_C8(true, 8, false);
+    else if (variant == 10) DR_C8(true, 4, true);
+    else DR_C8(false, 4, false);  // 7: loop-only timing build (no outputs; measurement only)
+#undef DR_C8
+    (void)0;
+    DR_LAUNCH_CHECK();
+    return DR_OK;
+  }
   if (d % 64 == 0 && !legacy && al16 && variant == 5) {
     const int64_t tiles = ceil_div(batch, 256) * ceil_div(d, 256);
     DR_REQUIRE(tiles < (1ll << 31), DR_INVALID_ARGUMENT, "batch too large");
