@@ -8,18 +8,56 @@
 
 namespace dr {
 
+// Global-address-space views.  A pointer read from memory (a descriptor in
+// LDS or a kernel-argument struct, a shuffled row address) is generic, and
+// hipcc then emits FLAT loads / stores: those count on lgkmcnt as well as
+// vmcnt and complete out of order, so every later LDS wait (a shuffle's
+// lgkmcnt(0)) also waits for them and a batch of row loads serialises.  Row
+// data always lives in device memory, so the hot helpers cast to
+// address_space(1) and get global_load / global_store.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define DR_GLOBAL __attribute__((address_space(1)))
+#else
+#define DR_GLOBAL  // (host pass: the device-only helpers below are never emitted)
+#endif
+template <class T>
+__device__ __forceinline__ const DR_GLOBAL T* gp(const T* p) {
+  return (const DR_GLOBAL T*)p;
+}
+template <class T>
+__device__ __forceinline__ DR_GLOBAL T* gp(T* p) {
+  return (DR_GLOBAL T*)p;
+}
+template <class T>
+__device__ __forceinline__ T gld(const T* p) {
+  return *gp(p);
+}
+template <class T>
+__device__ __forceinline__ void gst(T* p, const T& v) {
+  *gp(p) = v;
+}
+
+// Every vector-memory load of this wave has returned (s_waitcnt vmcnt(0),
+// expcnt / lgkmcnt left alone).  Placed between a batch of row loads and
+// the conditional stores of those rows: the compiler's own wait before a
+// store inside a branch is vmcnt(0) again, which then also waits for the
+// PREVIOUS store -- the stores of a batch serialise on their write
+// acknowledgements.  After this wait no load is outstanding and the stores
+// issue back to back.
+__device__ __forceinline__ void wait_loads() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // Nontemporal (stream-once) loads / stores of float / float4.
 typedef float nf4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 nt_load(const float4* p) {
-  const nf4 v = __builtin_nontemporal_load(reinterpret_cast<const nf4*>(p));
+  const nf4 v = __builtin_nontemporal_load(gp(reinterpret_cast<const nf4*>(p)));
   return make_float4(v.x, v.y, v.z, v.w);
 }
-__device__ __forceinline__ float nt_load(const float* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ float nt_load(const float* p) { return __builtin_nontemporal_load(gp(p)); }
 __device__ __forceinline__ void nt_store(float4 v, float4* p) {
   nf4 w = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(w, reinterpret_cast<nf4*>(p));
+  __builtin_nontemporal_store(w, gp(reinterpret_cast<nf4*>(p)));
 }
-__device__ __forceinline__ void nt_store(float v, float* p) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ void nt_store(float v, float* p) { __builtin_nontemporal_store(v, gp(p)); }
 
 void set_error(const char* fmt, ...);
 // Device status word of the current device (latched by kernels).

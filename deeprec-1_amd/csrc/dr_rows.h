@@ -54,7 +54,7 @@ __device__ __forceinline__ void load_row(Row<VEC, G, CPL>& x, const float* p, in
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     const int col = lg + c * G;
-    x.v[c] = (p && col < dv) ? reinterpret_cast<const V*>(p)[col] : vzero<V>();
+    x.v[c] = (p && col < dv) ? gld(reinterpret_cast<const V*>(p) + col) : vzero<V>();
   }
 }
 
@@ -85,7 +85,7 @@ __device__ __forceinline__ void store_row(const Row<VEC, G, CPL>& x, float* p, i
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     const int col = lg + c * G;
-    if (col < dv) reinterpret_cast<V*>(p)[col] = x.v[c];
+    if (col < dv) gst(reinterpret_cast<V*>(p) + col, x.v[c]);
   }
 }
 
@@ -106,7 +106,7 @@ __device__ __forceinline__ void load_row_u(Row<VEC, G, CPL>& x, const float* p, 
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     const int col = lg + c * G;
-    x.v[c] = col < dv ? reinterpret_cast<const V*>(p)[col] : vzero<V>();
+    x.v[c] = col < dv ? gld(reinterpret_cast<const V*>(p) + col) : vzero<V>();
   }
 }
 

@@ -1404,7 +1404,7 @@ __device__ __forceinline__ int64_t ev_probe_row(const LkDesc& e, uint64_t key) {
   uint64_t rc;
   typedef unsigned long long slot_v __attribute__((ext_vector_type(2)));
   if (key == kEmptyKey) {
-    const slot_v sv = *reinterpret_cast<const slot_v*>(e.slots + e.cap);
+    const slot_v sv = gld(reinterpret_cast<const slot_v*>(e.slots + e.cap));
     if (sv.x != 0ull) return -1;
     rc = sv.y;
   } else {
@@ -1412,7 +1412,7 @@ __device__ __forceinline__ int64_t ev_probe_row(const LkDesc& e, uint64_t key) {
     uint64_t h = mix64(key) & mask;
     for (int64_t probes = 0;; ++probes) {
       if (probes > e.cap) return -1;
-      const slot_v sv = *reinterpret_cast<const slot_v*>(e.slots + h);
+      const slot_v sv = gld(reinterpret_cast<const slot_v*>(e.slots + h));
       if (sv.x == key) {
         rc = sv.y;
         break;
@@ -1466,22 +1466,29 @@ __global__ __launch_bounds__(256) void ev_lookup_onehot_kernel(LookupArgs a, int
     at = __shfl(at, leader, 64);
     if (missed) mlist[at + __popcll(mm & lanemask_lt())] = (int32_t)(s0 + lg);
   }
-  Row<VEC, G, CPL> x[NB];
-  float* o[NB];
+  // every row address first (the shuffles' LDS waits then precede the row
+  // loads), then the NB row loads back to back as global (not flat) loads
+  const float* p[NB];
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
     const uint64_t u = (uint64_t)(uintptr_t)mine;
     const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)u, base + q, 64);
     const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(u >> 32), base + q, 64);
-    const float* p = reinterpret_cast<const float*>((uintptr_t)(((uint64_t)hi << 32) | lo));
+    p[q] = reinterpret_cast<const float*>((uintptr_t)(((uint64_t)hi << 32) | lo));
+  }
+  Row<VEC, G, CPL> x[NB];
+  float* o[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
     const int64_t s = s0 + q;
     o[q] = nullptr;
-    if (p && s < slots) {
+    if (p[q] && s < slots) {
       const int64_t b = (int64_t)((uint32_t)s / (uint32_t)T);
       o[q] = a.out + b * a.out_stride + (s - b * T) * (int64_t)dim;
     }
-    load_row_nt<VEC, G, CPL>(x[q], p, lg, dv);
+    load_row_nt<VEC, G, CPL>(x[q], p[q], lg, dv);
   }
+  wait_loads();
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
     if (ORDER == DR_ORDER_SEQ) {  // fused op: out = 0 + e (-0.0 -> +0.0)

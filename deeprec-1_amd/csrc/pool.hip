@@ -36,14 +36,15 @@ __device__ __forceinline__ float group_sum(float v) {
 __device__ __forceinline__ const float* select_row(const dr_pool_desc& d, int64_t k, int dim,
                                                    int* st) {
   int64_t r;
+  // (descriptors are read from LDS: gld keeps these global, not flat, loads)
   if (d.ids) {
-    r = d.ids[k];
+    r = gld(d.ids + k);
     // pre-resolved EV rows (dr_rows_per_nnz): negative = filtered -> default
     if (r < 0 && d.default_rows) return d.default_rows + (-r - 1) * d.default_stride;
   } else if (!d.rows) {
-    r = d.idx[k];
+    r = gld(d.idx + k);
   } else {
-    r = d.rows[d.idx[k]];
+    r = gld(d.rows + gld(d.idx + k));
     if (r < 0) return d.default_rows + (-r - 1) * d.default_stride;
     return d.pool + r * (int64_t)dim;
   }
@@ -258,7 +259,7 @@ __device__ __forceinline__ bool chunk_is_fast(const dr_pool_desc& d, int64_t b0,
                                               int (&off)[NB + 1]) {
   if (b0 + NB > B || d.weights || d.max_norm >= 0.f) return false;
 #pragma unroll
-  for (int j = 0; j <= NB; ++j) off[j] = d.bag_off[b0 + j];
+  for (int j = 0; j <= NB; ++j) off[j] = gld(d.bag_off + b0 + j);
   bool fast = true;
 #pragma unroll
   for (int j = 0; j < NB; ++j) fast = fast && (off[j + 1] - off[j] == 1);
@@ -308,6 +309,7 @@ __global__ __launch_bounds__(256) void pool_onehot_kernel(PoolArgs args, int T, 
     }
     load_row_nt<VEC, G, CPL>(x[j], p, lg, dv);
   }
+  wait_loads();
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     seq_zero_add<VEC, G, CPL, ORDER>(x[j]);
