@@ -98,6 +98,70 @@ __global__ void scan_apply_kernel(const int32_t* __restrict__ in, int32_t* __res
   }
 }
 
+// Small inputs (n <= kSmallScan): ONE block of 1024 threads scans the whole
+// array in chunks of 8192 (coalesced loads staged through LDS, each thread
+// scans 8 consecutive items, a carry runs across chunks) -- one launch
+// instead of reduce / block sums / apply, whose cost at this size is the
+// three launch latencies.
+static constexpr int kSmallScanThreads = 1024;
+static constexpr int kSmallScanChunk = kSmallScanThreads * 8;
+static constexpr int64_t kSmallScan = 65536;
+
+template <bool FLAG>
+__global__ __launch_bounds__(1024) void scan_small_kernel(const int32_t* __restrict__ in,
+                                                          int32_t* __restrict__ out, int64_t n,
+                                                          const int64_t* n_dev, int64_t* total) {
+  __shared__ int buf[kSmallScanChunk];
+  __shared__ int wsum[kSmallScanThreads / 64];
+  const int64_t ne = eff_n(n, n_dev);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int carry = 0;
+  for (int64_t c0 = 0; c0 < ne; c0 += kSmallScanChunk) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t i = c0 + k * kSmallScanThreads + threadIdx.x;
+      buf[k * kSmallScanThreads + threadIdx.x] = i < ne ? scan_val<FLAG>(in[i]) : 0;
+    }
+    __syncthreads();
+    int v[8], s = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      v[k] = buf[threadIdx.x * 8 + k];
+      s += v[k];
+    }
+    int x = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kSmallScanThreads / 64; ++w) {
+      const int ws = wsum[w];
+      pre += w < wave ? ws : 0;
+      tot += ws;
+    }
+    int run = carry + pre + x - s;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      buf[threadIdx.x * 8 + k] = run;
+      run += v[k];
+    }
+    carry += tot;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t i = c0 + k * kSmallScanThreads + threadIdx.x;
+      if (i < ne) out[i] = buf[k * kSmallScanThreads + threadIdx.x];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && total) *total = carry;
+}
+
 size_t scan_ws_bytes(int64_t n) {
   return (size_t)((ceil_div(n > 0 ? n : 1, kScanTile) + 64) * sizeof(int32_t)) + 256;
 }
@@ -107,6 +171,12 @@ static int scan_exclusive(const int32_t* in, int32_t* out, int64_t n, const int6
                           int64_t* total, void* ws, hipStream_t st) {
   if (n <= 0) {
     if (total) return fill_bytes(total, 0, sizeof(int64_t), st);
+    return DR_OK;
+  }
+  if (n <= kSmallScan) {
+    hipLaunchKernelGGL(scan_small_kernel<FLAG>, dim3(1), dim3(kSmallScanThreads), 0, st, in, out,
+                       n, n_dev, total);
+    DR_LAUNCH_CHECK();
     return DR_OK;
   }
   const int64_t nb = ceil_div(n, kScanTile);

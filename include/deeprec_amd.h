@@ -74,6 +74,10 @@ size_t dr_unique_grouped_workspace_size(const int64_t* koff_host, int num_tables
 int dr_unique_grouped(const int64_t* keys, const int64_t* koff_host, int num_tables,
                       int64_t* uniq_out, int32_t* idx_out, int32_t* counts_out,
                       int64_t* num_unique, void* ws, size_t ws_bytes, void* stream);
+/* Test hook: bound of the per-bucket LDS hash walk before a key goes to the */
+/* bucket's global overflow region (default and maximum 2048; a smaller     */
+/* value makes small inputs take the overflow path).  Results never change. */
+int dr_unique_set_lds_probes(int probes);
 
 /* ------------------------------------------------------------------------ */
 /* Stable radix sort of (uint64 key, int32 value) pairs on bits [lo, hi).    */

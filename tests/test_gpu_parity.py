@@ -161,6 +161,42 @@ def test_unique_grouped_bitexact(ops, orc):
         np.testing.assert_array_equal(cnt[a:a + U[t]], rcnt)
 
 
+@pytest.mark.parametrize("probes", [2048, 1])
+def test_unique_skewed_and_overflow_bitexact(dr, ops, orc, probes):
+    """LDS-staged Unique on skewed inputs (a padding id holding half of a
+    feature, long runs, a 1.3M-key feature that fills 1024 buckets) and, with
+    the LDS hash walk cut to one probe, through every bucket's global overflow
+    region: outputs stay bit-identical to the oracle's serial Unique."""
+    rng = np.random.default_rng(probes)
+    pad = rng.integers(0, 400000, 200000).astype(np.int64)
+    pad[rng.random(200000) < 0.5] = 0                       # DIN-style padded histories
+    runs = np.repeat(rng.integers(-5, 5000, 3000), rng.integers(1, 90, 3000)).astype(np.int64)
+    big = rng.integers(0, 1 << 40, 1300000).astype(np.int64)
+    parts = [pad, runs, big, np.full(7000, -1, np.int64)]
+    from deeprec_amd import _lib
+    lib = _lib.lib()
+    lib.dr_unique_set_lds_probes(probes)
+    try:
+        for x in parts:
+            y, idx, cnt = ops.unique_with_counts(T(x))
+            ry, ridx, rcnt = orc.unique(x, with_counts=True)
+            np.testing.assert_array_equal(H(y), ry)
+            np.testing.assert_array_equal(H(idx), ridx)
+            np.testing.assert_array_equal(H(cnt), rcnt)
+        koff = np.concatenate([[0], np.cumsum([p.shape[0] for p in parts])]).tolist()
+        y, idx, cnt, U = ops.unique_grouped(T(np.concatenate(parts)), koff, with_counts=True)
+        y, idx, cnt, U = H(y), H(idx), H(cnt), H(U)
+        for t, x in enumerate(parts):
+            ry, ridx, rcnt = orc.unique(x, with_counts=True)
+            a = koff[t]
+            assert U[t] == ry.shape[0]
+            np.testing.assert_array_equal(y[a:a + U[t]], ry)
+            np.testing.assert_array_equal(idx[a:koff[t + 1]], ridx)
+            np.testing.assert_array_equal(cnt[a:a + U[t]], rcnt)
+    finally:
+        lib.dr_unique_set_lds_probes(2048)
+
+
 def test_route_by_owner(ops):
     rng = np.random.default_rng(78)
     sizes = [1000, 0, 2500, 300]
