@@ -3,6 +3,7 @@
 #include <stdio.h>
 
 #include <mutex>
+#include <vector>
 
 #include "dr_common.h"
 
@@ -87,9 +88,70 @@ __global__ void fill_synth_tail_kernel(float* __restrict__ t, int64_t begin, int
   if (e < end) t[e] = synth(seed, e / dim, e % dim);
 }
 
+
+// ---- measurement hook: HIP events around one kernel's launches ------------
+// dr_kernel_timing(which) arms it (DR_TIME_LOOKUP: ev_lookup_onehot_kernel,
+// DR_TIME_POOL_ONEHOT: pool_onehot_kernel); every such launch on any stream
+// is then bracketed by a pair of events recorded on that launch's stream,
+// and dr_kernel_timing_result sums their elapsed times -- the kernel's own
+// duration, not the surrounding helper launches.  Off: one branch per launch.
+static std::mutex g_tmu;
+static int g_time_which = 0;
+static std::vector<std::pair<hipEvent_t, hipEvent_t>> g_tev;
+
+bool timing_on(int which) { return g_time_which == which; }
+
+void timing_mark(int which, hipStream_t st, bool begin) {
+  if (g_time_which != which) return;
+  std::lock_guard<std::mutex> g(g_tmu);
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return;
+  if (hipEventRecord(e, st) != hipSuccess) {
+    (void)hipEventDestroy(e);
+    return;
+  }
+  if (begin)
+    g_tev.push_back({e, nullptr});
+  else if (!g_tev.empty() && g_tev.back().second == nullptr)
+    g_tev.back().second = e;
+  else
+    (void)hipEventDestroy(e);
+}
+
 }  // namespace dr
 
 extern "C" {
+
+int dr_kernel_timing(int which) {
+  using namespace dr;
+  std::lock_guard<std::mutex> g(g_tmu);
+  for (auto& p : g_tev) {
+    if (p.first) (void)hipEventDestroy(p.first);
+    if (p.second) (void)hipEventDestroy(p.second);
+  }
+  g_tev.clear();
+  g_time_which = which;
+  return DR_OK;
+}
+
+int dr_kernel_timing_result(double* total_ms, int64_t* launches) {
+  using namespace dr;
+  DR_REQUIRE(total_ms && launches, DR_INVALID_ARGUMENT, "null output");
+  std::lock_guard<std::mutex> g(g_tmu);
+  double t = 0.0;
+  int64_t n = 0;
+  for (auto& p : g_tev) {
+    if (!p.first || !p.second) continue;
+    DR_HIP(hipEventSynchronize(p.second));
+    float ms = 0.f;
+    DR_HIP(hipEventElapsedTime(&ms, p.first, p.second));
+    t += ms;
+    ++n;
+  }
+  *total_ms = t;
+  *launches = n;
+  return DR_OK;
+}
 
 int dr_abi_version(void) { return 1; }
 

@@ -65,6 +65,10 @@ int* status_word();
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// core.hip: measurement hook (dr_kernel_timing) -- events around one kernel
+enum { DR_TIME_LOOKUP = 1, DR_TIME_POOL_ONEHOT = 2 };
+void timing_mark(int which, hipStream_t st, bool begin);
+
 // pool.hip: EV copy-out, out[i] = rows[i] >= 0 ? pool[rows[i]] : (defaults ?
 // defaults[i] : dflt); the gather-copy kernel (dwordx4, nontemporal).
 int gather_ev_rows(const float* pool, int64_t dim, const int64_t* rows, int64_t n,

@@ -1635,9 +1635,11 @@ template <int VEC, int G, int CPL, int ORDER, int NB>
 static void launch_lookup_nb(const LookupArgs& a, int T, int64_t B, int dim, const LookupWs& w,
                              hipStream_t st) {
   const int64_t items = ceil_div((int64_t)T * B, NB);
+  timing_mark(DR_TIME_LOOKUP, st, true);
   hipLaunchKernelGGL((ev_lookup_onehot_kernel<VEC, G, CPL, ORDER, NB>),
                      dim3((unsigned)ceil_div(items, 256 / G)), dim3(256), 0, st, a, T, B, dim,
                      w.mlist, w.mcnt);
+  timing_mark(DR_TIME_LOOKUP, st, false);
 }
 
 template <int VEC, int G, int CPL, int ORDER>

@@ -378,9 +378,11 @@ static int launch_pool(const PoolArgs& a, int T, int64_t B, int dim, int flags, 
                        int* st) {
   if (flags & POOL_ONEHOT) {
     const int64_t items = ceil_div((int64_t)T * B, kOneHotNB);
+    timing_mark(DR_TIME_POOL_ONEHOT, s, true);
     hipLaunchKernelGGL((pool_onehot_kernel<VEC, G, CPL, ORDER, kOneHotNB>),
                        dim3((unsigned)ceil_div(items, 256 / G)), dim3(256), 0, s, a, T, B, dim,
                        st);
+    timing_mark(DR_TIME_POOL_ONEHOT, s, false);
   } else {
     const int64_t cpt = ceil_div(B, kChunkNB);
     const unsigned blocks = (unsigned)ceil_div((int64_t)T * cpt, 256 / G);

@@ -89,6 +89,8 @@ SIGNATURES = {
     "dr_unique_grouped_workspace_size": (_SZ, [_P, _I32]),
     "dr_unique_grouped": (_I32, [_P, _P, _I32, _P, _P, _P, _P, _P, _SZ, _P]),
     "dr_unique_set_lds_probes": (_I32, [_I32]),
+    "dr_kernel_timing": (_I32, [_I32]),
+    "dr_kernel_timing_result": (_I32, [_P, _P]),
     "dr_route_workspace_size": (_SZ, [_I64, _I32, _I32]),
     "dr_route_by_owner": (_I32, [_P, _P, _I32, _P, _I32, _P, _P, _P, _P, _P, _SZ, _P]),
     "dr_sort_pairs_workspace_size": (_SZ, [_I64]),

@@ -79,6 +79,15 @@ int dr_unique_grouped(const int64_t* keys, const int64_t* koff_host, int num_tab
 /* value makes small inputs take the overflow path).  Results never change. */
 int dr_unique_set_lds_probes(int probes);
 
+/* Measurement hook (bench.py): dr_kernel_timing(which) clears the record and */
+/* brackets every later launch of one kernel with a pair of HIP events on the */
+/* launch's stream (1: the fused lookup kernel of dr_ev_lookup_onehot*, 2: the */
+/* one-hot pooling kernel of dr_pool_grouped_ex; 0: off).  Not for use inside */
+/* graph capture.  dr_kernel_timing_result syncs and returns the summed        */
+/* kernel time (ms) and the number of bracketed launches.                     */
+int dr_kernel_timing(int which);
+int dr_kernel_timing_result(double* total_ms, int64_t* launches);
+
 /* ------------------------------------------------------------------------ */
 /* Stable radix sort of (uint64 key, int32 value) pairs on bits [lo, hi).    */
 /* Replaces cub::DeviceRadixSort::SortPairs in FusedEmbeddingSparsePreLookUp */

@@ -744,7 +744,8 @@ def test_grouped_backward_long_runs(dr, orc, comb, D):
     whole history batch) are summed as ordered chunk partials.  Runs of
     <= 256 positions -- here 256 exactly and 200 -- stay bit-exact to the
     serial reference order; longer ones (257, 5000, 3 x 256) match it to
-    fp32 tolerance 1e-5 rel / 1e-3 abs (sums of up to 5000 N(0,1) terms, |S| ~ 70)."""
+    fp32 tolerance: max |error| <= 1e-5 x max |row| (sums of up to 5000 N(0,1)
+    terms, |S| ~ 70)."""
     rng = np.random.default_rng(37)
     runs = {0: 5000, 1: 256, 2: 257, 3: 768, 4: 200}
     v = np.concatenate([np.full(n, k, np.int64) for k, n in runs.items()] +
@@ -772,7 +773,9 @@ def test_grouped_backward_long_runs(dr, orc, comb, D):
         exact = [i for i in range(U) if int(uids[i]) not in (0, 2, 3)]
         np.testing.assert_array_equal(got[exact], ref[exact])
         for k in (0, 2, 3):
-            np.testing.assert_allclose(got[pos[k]], ref[pos[k]], rtol=1e-5, atol=1e-3)
+            # north_star's 1e-5 rel, relative to the gradient row's magnitude
+            err = np.abs(got[pos[k]] - ref[pos[k]]).max()
+            assert err <= 1e-5 * np.abs(ref[pos[k]]).max(), (k, err)
 
 
 def test_optimizers_with_repeated_indices(dr, orc):
