@@ -1210,6 +1210,91 @@ __global__ __launch_bounds__(512, 1) void crossnet_8ph_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// CrossNet backward, the elementwise part of one layer in ONE pass over HBM
+// (the GEMMs dW = u^T x_l and dx_l = u W + g stay library calls):
+//   u   = bf16(g * x0)                         [B, d] bf16
+//   acc = (acc_in ? acc_in : 0) + g * lin      [B, d] fp32 (dx0 over layers)
+//   dbp[blk][c] = sum over this block's rows of u[r][c]   (fp32 partials)
+// A thread owns 8 consecutive columns (one 16-B bf16 vector) and walks the
+// block's rows; the 4 waves of a block take rows r0 + w, r0 + w + 4, ...
+// and their column partials are added in wave order through LDS, so the
+// partials, and db = crossnet_db_kernel's fixed-order sum of them, are
+// deterministic.
+// ---------------------------------------------------------------------------
+static constexpr int CB_ROWS = 256;  // rows per block
+
+__global__ __launch_bounds__(256) void crossnet_bwd_elem_kernel(
+    const uint16_t* __restrict__ g, const uint16_t* __restrict__ x0,
+    const uint16_t* __restrict__ lin, const float* acc_in, float* acc_out,
+    uint16_t* __restrict__ u, float* __restrict__ dbp, int64_t B, int d) {
+  __shared__ float part[3][64][8 + 1];
+  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = (blockIdx.x * 64 + lane) * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * CB_ROWS;
+  const bool col_ok = c0 < d;
+  float db[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (col_ok) {
+    for (int64_t r = r0 + wave; r < r0 + CB_ROWS && r < B; r += 4) {
+      const int64_t o = r * d + c0;
+      const u32x4 gv = *reinterpret_cast<const u32x4*>(g + o);
+      const u32x4 xv = *reinterpret_cast<const u32x4*>(x0 + o);
+      const u32x4 lv = *reinterpret_cast<const u32x4*>(lin + o);
+      float a[8];
+      if (acc_in) {
+        const float4 a0 = *reinterpret_cast<const float4*>(acc_in + o);
+        const float4 a1 = *reinterpret_cast<const float4*>(acc_in + o + 4);
+        a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w;
+        a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] = 0.f;
+      }
+      u32x4 uv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float g0 = bf2f((uint16_t)(gv[e] & 0xffff)), g1 = bf2f((uint16_t)(gv[e] >> 16));
+        const uint16_t u0 = f2bf(g0 * bf2f((uint16_t)(xv[e] & 0xffff)));
+        const uint16_t u1 = f2bf(g1 * bf2f((uint16_t)(xv[e] >> 16)));
+        uv[e] = (uint32_t)u0 | ((uint32_t)u1 << 16);
+        db[2 * e] += bf2f(u0);
+        db[2 * e + 1] += bf2f(u1);
+        a[2 * e] += g0 * bf2f((uint16_t)(lv[e] & 0xffff));
+        a[2 * e + 1] += g1 * bf2f((uint16_t)(lv[e] >> 16));
+      }
+      *reinterpret_cast<u32x4*>(u + o) = uv;
+      *reinterpret_cast<float4*>(acc_out + o) = make_float4(a[0], a[1], a[2], a[3]);
+      *reinterpret_cast<float4*>(acc_out + o + 4) = make_float4(a[4], a[5], a[6], a[7]);
+    }
+  }
+  // column partials of the 4 waves, added in wave order
+  if (wave > 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part[wave - 1][lane][e] = db[e];
+  }
+  __syncthreads();
+  if (wave == 0 && col_ok) {
+#pragma unroll
+    for (int w = 0; w < 3; ++w)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) db[e] += part[w][lane][e];
+    float* dst = dbp + (int64_t)blockIdx.y * d + c0;
+    *reinterpret_cast<float4*>(dst) = make_float4(db[0], db[1], db[2], db[3]);
+    *reinterpret_cast<float4*>(dst + 4) = make_float4(db[4], db[5], db[6], db[7]);
+  }
+}
+
+// db[c] = sum over row blocks of dbp[blk][c], in block order
+__global__ void crossnet_db_kernel(const float* __restrict__ dbp, int64_t nblk, int d,
+                                   float* __restrict__ db) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d) return;
+  float s = 0.f;
+  for (int64_t k = 0; k < nblk; ++k) s += dbp[k * d + c];
+  db[c] = s;
+}
+
 }  // namespace dr
 
 extern "C" {
@@ -1378,6 +1463,36 @@ int dr_crossnet_forward_bf16(const uint16_t* x0, const uint16_t* xl, const uint1
   dim3 grid((unsigned)ceil_div(d, CN_BN), (unsigned)ceil_div(batch, CN_BM));
   hipLaunchKernelGGL(crossnet_kernel, grid, dim3(256), 0, S(stream), x0, xl, W, bias, batch, d,
                      out);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+size_t dr_crossnet_backward_workspace_size(int64_t batch, int d) {
+  return (size_t)dr::ceil_div(batch > 0 ? batch : 1, dr::CB_ROWS) * (size_t)d * sizeof(float) + 256;
+}
+
+int dr_crossnet_backward_elem_bf16(const uint16_t* g, const uint16_t* x0, const uint16_t* lin,
+                                   const float* acc_in, float* acc_out, uint16_t* u, float* db,
+                                   int64_t batch, int d, void* ws, size_t ws_bytes,
+                                   void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && d > 0 && d % 8 == 0, DR_INVALID_ARGUMENT,
+             "dr_crossnet_backward_elem_bf16: d must be a multiple of 8");
+  DR_REQUIRE(g && x0 && lin && acc_out && u && db, DR_INVALID_ARGUMENT, "null operand");
+  DR_REQUIRE((((uintptr_t)g | (uintptr_t)x0 | (uintptr_t)lin | (uintptr_t)acc_in |
+               (uintptr_t)acc_out | (uintptr_t)u | (uintptr_t)db) & 15) == 0,
+             DR_INVALID_ARGUMENT, "operands must be 16-B aligned");
+  DR_REQUIRE(ws && ws_bytes >= dr_crossnet_backward_workspace_size(batch, d), DR_INVALID_ARGUMENT,
+             "workspace too small");
+  if (batch == 0) return fill_bytes(db, 0, (size_t)d * sizeof(float), S(stream));
+  const int64_t nblk = ceil_div(batch, CB_ROWS);
+  DR_REQUIRE(nblk < 65536, DR_INVALID_ARGUMENT, "batch too large");
+  float* dbp = static_cast<float*>(ws);
+  dim3 grid((unsigned)ceil_div(d, 8 * 64), (unsigned)nblk);
+  hipLaunchKernelGGL(crossnet_bwd_elem_kernel, grid, dim3(256), 0, S(stream), g, x0, lin, acc_in,
+                     acc_out, u, dbp, batch, d);
+  hipLaunchKernelGGL(crossnet_db_kernel, dim3((unsigned)ceil_div(d, 256)), dim3(256), 0, S(stream),
+                     dbp, nblk, d, db);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

@@ -204,6 +204,9 @@ SIGNATURES = {
     "dr_dot_interaction_grad": (_I32, [_P, _P, _I64, _I32, _I32, _P, _P]),
     "dr_crossnet_layer_bf16": (_I32, [_P, _P, _P, _P, _I64, _I32, _P, _P]),
     "dr_crossnet_forward_bf16": (_I32, [_P, _P, _P, _P, _I64, _I32, _P, _P, _P]),
+    "dr_crossnet_backward_workspace_size": (_SZ, [_I64, _I32]),
+    "dr_crossnet_backward_elem_bf16": (_I32, [_P, _P, _P, _P, _P, _P, _P, _I64, _I32, _P, _SZ,
+                                              _P]),
     "dr_din_attention_input": (_I32, [_P, _P, _I64, _I64, _I32, _P, _P]),
     "dr_din_attention_input_grad": (_I32, [_P, _P, _P, _I64, _I64, _I32, _P, _P, _I32, _P]),
     "dr_din_attention_pool": (_I32, [_P, _P, _P, _I64, _I64, _I32, _P, _P, _P, _P]),

@@ -292,6 +292,48 @@ class CrossLayer(torch.autograd.Function):
         return dx0, dxl, dW, db
 
 
+class CrossStack(torch.autograd.Function):
+    """L stacked cross layers x_{l+1} = x0 * (x_l W_l^T + b_l) + x_l as one
+    autograd node.  Forward: the fused MFMA kernel per layer (which hands back
+    lin_l for the backward).  Backward, layer by layer in reverse: ONE
+    elementwise pass (dr_crossnet_backward_elem_bf16) forms u = g * x0, adds
+    g * lin_l into a running fp32 dx0 and the column sums db_l; the two
+    library GEMMs give dW_l = u^T x_l and g <- u W_l + g (= dx_l).  The x0
+    gradient is the running sum plus the first layer's dx_l (x_0 = x0) --
+    what CrossLayer's per-layer autograd adds up in separate bf16 passes."""
+
+    @staticmethod
+    def forward(ctx, x0, *params):
+        L = len(params) // 2
+        ws = [w.to(torch.bfloat16) for w in params[:L]]
+        bs = params[L:]
+        x = x0
+        xs, lins = [], []
+        for w, b in zip(ws, bs):
+            xs.append(x)
+            x, lin = ops.crossnet_forward(x0, x, w, b, with_lin=True)
+            lins.append(lin)
+        ctx.save_for_backward(x0, *ws, *xs, *lins)
+        ctx.L = L
+        return x
+
+    @staticmethod
+    def backward(ctx, g):
+        L = ctx.L
+        saved = ctx.saved_tensors
+        x0, ws, xs, lins = saved[0], saved[1:1 + L], saved[1 + L:1 + 2 * L], saved[1 + 2 * L:]
+        g = g.to(torch.bfloat16).contiguous()
+        acc = None
+        dws, dbs = [None] * L, [None] * L
+        for l in reversed(range(L)):
+            u, acc, db = ops.crossnet_backward_elem(g, x0, lins[l], acc)
+            dws[l] = torch.matmul(u.t(), xs[l]).float()
+            dbs[l] = db
+            g = torch.addmm(g, u, ws[l])
+        dx0 = (acc + g.float()).to(torch.bfloat16)
+        return (dx0, *dws, *dbs)
+
+
 class DCNv2(torch.nn.Module):
     """DCN-v2 (stacked): x0 = [dense | e_1 .. e_T] zero-padded to a multiple
     of 64 features, bf16; L cross layers on the MFMA kernel; a bf16 deep MLP
@@ -325,9 +367,7 @@ class DCNv2(torch.nn.Module):
         emb = self.lookup(ids)                                     # [B, T*D] fp32
         pad = torch.zeros(B, self.dp - self.d, device=dense.device, dtype=dense.dtype)
         x0 = torch.cat([dense, emb, pad], 1).to(torch.bfloat16)
-        x = x0
-        for w, b in zip(self.cross_w, self.cross_b):
-            x = CrossLayer.apply(x0, x, w, b)
+        x = CrossStack.apply(x0, *self.cross_w, *self.cross_b)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             net = self.last(self.deep(x)).float()
         return torch.sigmoid(net).squeeze(1)

@@ -535,6 +535,32 @@ def crossnet_forward(x0, xl, weight, bias, with_lin=True):
     return out, lin
 
 
+def crossnet_backward_elem(g, x0, lin, acc=None):
+    """dr_crossnet_backward_elem_bf16: the elementwise part of a cross
+    layer's backward in one pass.  g, x0, lin [B, d] bf16; acc [B, d] fp32
+    running dx0 (None: start at 0; updated in place).  Returns (u = g * x0
+    bf16, acc + g * lin fp32, db = column sums of u fp32)."""
+    dev = _dev(g)
+    B, d = g.shape
+    for t in (g, x0, lin):
+        if t.dtype != torch.bfloat16 or tuple(t.shape) != (B, d):
+            raise ValueError("crossnet_backward_elem needs bf16 [B, d] operands")
+    g, x0, lin = g.contiguous(), x0.contiguous(), lin.contiguous()
+    out = torch.empty((B, d), dtype=torch.float32, device=dev) if acc is None else acc
+    if acc is not None and (acc.dtype != torch.float32 or not acc.is_contiguous()
+                            or tuple(acc.shape) != (B, d)):
+        raise ValueError("acc must be a contiguous fp32 [B, d] tensor")
+    u = torch.empty((B, d), dtype=torch.bfloat16, device=dev)
+    db = torch.empty(d, dtype=torch.float32, device=dev)
+    wsb = lib().dr_crossnet_backward_workspace_size(B, d)
+    ws = workspace(wsb, dev)
+    check(lib().dr_crossnet_backward_elem_bf16(ptr(g), ptr(x0), ptr(lin), ptr(acc), ptr(out),
+                                               ptr(u), ptr(db), B, d, ptr(ws), wsb,
+                                               stream_handle(dev)))
+    _post(dev)
+    return u, out, db
+
+
 # ---------------------------------------------------------------------------
 # DIN attention (modelzoo/DIN/script/utils.py:264-309, script/model.py:94-98)
 # ---------------------------------------------------------------------------

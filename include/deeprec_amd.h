@@ -701,6 +701,15 @@ int dr_dot_interaction_grad(const float* x, const float* top_grad, int64_t batch
 int dr_crossnet_layer_bf16(const uint16_t* x0, const uint16_t* xl, const uint16_t* W,
                            const float* bias, int64_t batch, int d, uint16_t* out,
                            void* stream);
+/* CrossNet backward, elementwise part of one layer in one pass (the GEMMs   */
+/* dW = u^T x_l, dx_l = u W + g stay library calls): u = bf16(g * x0),       */
+/* acc_out = (acc_in or 0) + g * lin in fp32 (dx0 summed over the layers),  */
+/* db = column sums of u (fixed order).  g, x0, lin, u bf16 [batch, d];     */
+/* acc_in may be NULL or equal acc_out.  Workspace: per-row-block partials.  */
+size_t dr_crossnet_backward_workspace_size(int64_t batch, int d);
+int dr_crossnet_backward_elem_bf16(const uint16_t* g, const uint16_t* x0, const uint16_t* lin,
+                                   const float* acc_in, float* acc_out, uint16_t* u, float* db,
+                                   int64_t batch, int d, void* ws, size_t ws_bytes, void* stream);
 /* Same layer, also writing lin_out = xl W^T + b (bf16, nullable; needs      */
 /* d % 64 == 0) for the backward pass.  d % 64 == 0 selects the pipelined    */
 /* kernel (global_load_lds staging, double-buffered K steps of 64).          */

@@ -70,6 +70,56 @@ def test_cross_layer_backward_matches_autograd():
         _close(got, want, frac=1.0 / 32)
 
 
+@pytest.mark.parametrize("B,d", [(300, 192), (1000, 3392), (64, 64)])
+def test_crossnet_backward_elem_matches_torch(B, d):
+    """dr_crossnet_backward_elem_bf16: u = bf16(g * x0) bit-exact to torch's
+    bf16 multiply, acc + g * lin in fp32 and db = column sums of u against
+    fp64 references (fp32 rounding tolerance); repeated launches are
+    bit-identical (fixed-order column sums)."""
+    from deeprec_amd import ops
+    gen = torch.Generator(device="cpu").manual_seed(B * 7 + d)
+    g, x0, lin = (torch.randn(B, d, generator=gen).to(DEV, torch.bfloat16) for _ in range(3))
+    acc0 = torch.randn(B, d, generator=gen).to(DEV)
+    u, acc, db = ops.crossnet_backward_elem(g, x0, lin, acc0.clone())
+    assert torch.equal(u, g * x0)
+    want = acc0.double() + g.double() * lin.double()
+    assert (acc.double() - want).abs().max().item() <= 1e-6 * want.abs().max().item()
+    wdb = u.double().sum(0)
+    assert (db.double() - wdb).abs().max().item() <= 1e-5 * (u.double().abs().sum(0).max().item())
+    u2, acc2, db2 = ops.crossnet_backward_elem(g, x0, lin, None)
+    assert torch.equal(u2, u) and torch.equal(db2, db)
+    assert torch.equal(acc2, (g.float() * lin.float()))
+
+
+def test_cross_stack_backward_matches_autograd():
+    """CrossStack (3 layers, one fused elementwise pass per layer in the
+    backward) against torch autograd of the fp32 composition from the same
+    bf16 operands: bf16 tolerances as the single layer."""
+    from deeprec_amd.modelzoo import CrossStack
+    gen = torch.Generator(device="cpu").manual_seed(11)
+    B, d, L = 384, 192, 3
+    x0 = torch.randn(B, d, generator=gen).to(DEV, torch.bfloat16)
+    Ws = [(torch.randn(d, d, generator=gen) / d ** 0.5).to(DEV) for _ in range(L)]
+    bs = [(torch.randn(d, generator=gen) * 0.1).to(DEV) for _ in range(L)]
+    G = torch.randn(B, d, generator=gen).to(DEV, torch.bfloat16)
+    a0 = x0.clone().requires_grad_(True)
+    ws = [w.clone().requires_grad_(True) for w in Ws]
+    bb = [b.clone().requires_grad_(True) for b in bs]
+    out = CrossStack.apply(a0, *ws, *bb)
+    out.backward(G)
+    r0 = x0.float().requires_grad_(True)
+    rw = [w.to(torch.bfloat16).float().requires_grad_(True) for w in Ws]
+    rb = [b.clone().requires_grad_(True) for b in bs]
+    x = r0
+    for w, b in zip(rw, rb):
+        x = r0 * (x @ w.t() + b) + x
+    _close(out, x.detach(), frac=1.0 / 32)
+    x.backward(G.float())
+    _close(a0.grad, r0.grad, frac=1.0 / 16)
+    for got, want in zip(ws + bb, rw + rb):
+        _close(got.grad, want.grad, frac=1.0 / 16)
+
+
 def test_dcn_train_step_matches_torch_reference():
     import deeprec_amd as dr
     from deeprec_amd import modelzoo as mz
