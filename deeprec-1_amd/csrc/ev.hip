@@ -632,11 +632,13 @@ struct ApplyTable {
   int64_t n;
   const int64_t* n_dev;
   int64_t steps_to_live;
+  const int64_t* rows;  // known rows of the keys (SGD of a row-grouped backward) or nullptr
 };
 static constexpr int kApplyGroup = 16;  // keeps the kernel arguments < 4 KiB
 struct ApplyGroup {
   ApplyTable t[kApplyGroup];
 };
+static_assert(sizeof(ApplyGroup) + 64 <= 4096, "apply kernel arguments exceed 4 KiB");
 
 // Phase 1 of a sparse apply, lane per key: LookupOrCreate with the global
 // step / filter admission / first-touch column mask (training_ali_ops.cc
@@ -650,7 +652,13 @@ __device__ __forceinline__ void apply_probe(const ApplyTable& at, int64_t i, int
   const int64_t steps_to_live = at.steps_to_live;
   int64_t row = -1;
   int initmask = 0;
-  if (i < ne) {
+  if (i < ne && at.rows) {
+    // Rows known (dr_ev_apply_grouped_ptr_rows: SGD of a filter-free EV whose
+    // forward resolved -- and initialised -- every key's row): what
+    // LookupOrCreate would return, without probing the key table again.
+    row = gld(at.rows + i);
+    if (steps_to_live != 0 && gs != -1 && e.version) e.version[row] = gs;
+  } else if (i < ne) {
     const uint64_t key = (uint64_t)keys[i];
     bool ok = true;
     if (e.k_hash > 0 && bloom_min_freq(e, key) < e.filter_freq) ok = false;
@@ -1270,7 +1278,9 @@ static int resolve_grouped(dr_ev* const* evs, int T, const int64_t* keys, const 
 static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* const* s2, int T,
                          OptScalars sc, const float* const* grads, const int64_t* const* keys,
                          const int64_t* n_host, const int64_t* const* n_dev, int64_t gs,
-                         hipStream_t st, int gind = 0) {
+                         hipStream_t st, int gind = 0, const int64_t* const* rows = nullptr) {
+  DR_REQUIRE(!rows || opt == OPT_SGD, DR_INVALID_ARGUMENT,
+             "known rows skip the slot-column first-touch check: SGD only");
   DR_REQUIRE(T >= 1 && vars && grads && keys && n_host, DR_INVALID_ARGUMENT, "bad argument");
   int* stw = status_word();
   DR_REQUIRE(stw, DR_INTERNAL, "status word unavailable");
@@ -1320,6 +1330,11 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
       a.n = n_host[t];
       a.n_dev = n_dev ? n_dev[t] : nullptr;
       a.steps_to_live = s->steps_to_live;
+      if (rows) {
+        DR_REQUIRE(rows[t] && s->filter_freq == 0 && s->k_hash == 0, DR_INVALID_ARGUMENT,
+                   "table %d: known rows need a filter-free EV and a rows array", t);
+        a.rows = rows[t];
+      }
       nmax = std::max(nmax, a.n);
     }
     if (nmax == 0) continue;
@@ -2364,6 +2379,21 @@ int dr_ev_apply_grouped_ptr(int optimizer, dr_ev* const* vars, dr_ev* const* slo
   return apply_grouped(opt, vars, slot1, slot2, num_tables, sc,
                        reinterpret_cast<const float* const*>(grad_ptrs), keys, n_host, n_dev,
                        global_step, S(stream), 1);
+}
+
+int dr_ev_apply_grouped_ptr_rows(int optimizer, dr_ev* const* vars, int num_tables,
+                                 const uint64_t* const* grad_ptrs, const int64_t* const* keys,
+                                 const int64_t* const* rows, const int64_t* n_host,
+                                 const int64_t* const* n_dev, float lr, int64_t global_step,
+                                 void* stream) {
+  using namespace dr;
+  DR_REQUIRE(optimizer == DR_OPT_SGD, DR_INVALID_ARGUMENT,
+             "dr_ev_apply_grouped_ptr_rows: SGD only (slot columns need the key probe)");
+  DR_REQUIRE(grad_ptrs && rows, DR_INVALID_ARGUMENT, "bad argument");
+  OptScalars sc = {lr, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  return apply_grouped(OPT_SGD, vars, nullptr, nullptr, num_tables, sc,
+                       reinterpret_cast<const float* const*>(grad_ptrs), keys, n_host, n_dev,
+                       global_step, S(stream), 1, rows);
 }
 
 static int ftrl_grouped(dr_ev* const* vars, dr_ev* const* accums, dr_ev* const* linears,

@@ -127,7 +127,8 @@ __global__ __launch_bounds__(256) void rows_emit_kernel(
     const int32_t* __restrict__ mark, const int32_t* __restrict__ ex,
     const int64_t* __restrict__ total, int defer, int64_t* __restrict__ uniq_out,
     int64_t* __restrict__ num_unique, int32_t* __restrict__ base, uint64_t* __restrict__ gptr,
-    int32_t* __restrict__ work, int32_t* __restrict__ nwork, int* st) {
+    int32_t* __restrict__ work, int32_t* __restrict__ nwork, const int64_t* __restrict__ rowsel,
+    int64_t* __restrict__ urows, int* st) {
   __shared__ dr_pool_grad_desc sd[DR_MAX_GROUP];
   if (threadIdx.x < T) sd[threadIdx.x] = g.d[threadIdx.x];
   __syncthreads();
@@ -151,6 +152,7 @@ __global__ __launch_bounds__(256) void rows_emit_kernel(
     const int64_t a = g.koff[t];
     const int64_t o = a + ex[i] - ex[a];
     uniq_out[o] = keys[i];
+    if (urows) urows[o] = rowsel[i];  // the row the forward resolved this id to
     if (mk < 0) {   // one-position run
       const dr_pool_grad_desc& d = sd[t];
       const int64_t k = i - a;
@@ -515,6 +517,16 @@ int dr_pool_grad_rows_grouped(const dr_pool_grad_desc* descs_host, int num_table
                               const int64_t* keys, int defer, int64_t* uniq_out,
                               int64_t* num_unique, uint64_t* grad_ptr, float* grad_unique,
                               void* ws, size_t ws_bytes, void* stream) {
+  return dr_pool_grad_rows_grouped_ex(descs_host, num_tables, batch, dim, rowsel, row_limit, keys,
+                                      defer, uniq_out, nullptr, num_unique, grad_ptr, grad_unique,
+                                      ws, ws_bytes, stream);
+}
+
+int dr_pool_grad_rows_grouped_ex(const dr_pool_grad_desc* descs_host, int num_tables,
+                                 int64_t batch, int dim, const int64_t* rowsel, int64_t row_limit,
+                                 const int64_t* keys, int defer, int64_t* uniq_out,
+                                 int64_t* uniq_rows, int64_t* num_unique, uint64_t* grad_ptr,
+                                 float* grad_unique, void* ws, size_t ws_bytes, void* stream) {
   using namespace dr;
   DR_REQUIRE(descs_host && num_tables >= 1 && num_tables <= DR_MAX_GROUP && dim > 0 &&
                  dim <= kRowsMaxDim && batch >= 0 && row_limit > 0 && rowsel && keys &&
@@ -567,7 +579,7 @@ int dr_pool_grad_rows_grouped(const dr_pool_grad_desc* descs_host, int num_table
   if (rc) return rc;
   hipLaunchKernelGGL(rows_emit_kernel, dim3(nb), dim3(256), 0, s, g, num_tables, batch, keys,
                      w.flags, w.ex, w.total, defer, uniq_out, num_unique, w.base, grad_ptr, w.work,
-                     w.nwork, st);
+                     w.nwork, rowsel, uniq_rows, st);
   DR_LAUNCH_CHECK();
   if (aligned) {
     const int d4 = dim / 4;

@@ -116,6 +116,8 @@ SIGNATURES = {
     "dr_pool_grad_rows_workspace_size": (_SZ, [_I64]),
     "dr_pool_grad_rows_grouped": (_I32, [_P, _I32, _I64, _I32, _P, _I64, _P, _I32, _P, _P, _P, _P,
                                          _P, _SZ, _P]),
+    "dr_pool_grad_rows_grouped_ex": (_I32, [_P, _I32, _I64, _I32, _P, _I64, _P, _I32, _P, _P, _P,
+                                            _P, _P, _P, _SZ, _P]),
     "dr_rows_from_ptr": (_I32, [_P, _I64, _P, _I32, _P, _P]),
     "dr_pool_grad": (_I32, [_P, _I64, _I64, _I32, _P, _P, _P, _I64, _P, _I32, _P, _P, _SZ, _P]),
     "dr_ev_create": (_I32, [_P, _P, _P]),
@@ -160,6 +162,7 @@ SIGNATURES = {
                                    _F32, _F32, _F32, _I64, _P]),
     "dr_ev_apply_grouped_ptr": (_I32, [_I32, _P, _P, _P, _I32, _P, _P, _P, _P, _F32, _F32, _F32,
                                        _F32, _F32, _F32, _I64, _P]),
+    "dr_ev_apply_grouped_ptr_rows": (_I32, [_I32, _P, _I32, _P, _P, _P, _P, _P, _F32, _I64, _P]),
     "dr_ev_apply_ftrl_grouped_ptr": (_I32, [_P, _P, _P, _I32, _P, _P, _P, _P, _F32, _F32, _F32,
                                             _F32, _F32, _I64, _P]),
     "dr_ev_apply_ftrl": (_I32, [_P, _P, _P, _F32, _F32, _F32, _F32, _F32, _P, _P, _I64, _P, _I64,

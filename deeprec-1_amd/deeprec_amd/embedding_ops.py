@@ -492,20 +492,22 @@ class _RowGroup(object):
         uniq = torch.empty(m, dtype=torch.int64, device=dev)
         U = torch.empty(T, dtype=torch.int64, device=dev)
         gptr = torch.empty(m, dtype=torch.int64, device=dev)
+        urows = torch.empty(m, dtype=torch.int64, device=dev)
         gu = torch.empty((m, D), dtype=torch.float32, device=dev)
         keep.append(gu)
         limit = max(lib().dr_ev_row_capacity(f.params.handle) for f in self.feats)
         wsb = lib().dr_pool_grad_rows_workspace_size(n)
         ws = workspace(wsb, dev)
-        check(lib().dr_pool_grad_rows_grouped(
+        check(lib().dr_pool_grad_rows_grouped_ex(
             descs, T, self.feats[0].batch, D, ptr(self.rowsel), max(int(limit), 1),
-            ptr(self.vals), 1, ptr(uniq), ptr(U), ptr(gptr), ptr(gu), ptr(ws), wsb,
+            ptr(self.vals), 1, ptr(uniq), ptr(urows), ptr(U), ptr(gptr), ptr(gu), ptr(ws), wsb,
             stream_handle(dev)))
         ops._post(dev)
         k = self.koff
         keep = tuple(keep)
         return [IndexedSlices(None, uniq[k[t]:k[t + 1]], U[t:t + 1], True,
-                              grad_ptr=gptr[k[t]:k[t + 1]], dim=D, keep=keep)
+                              grad_ptr=gptr[k[t]:k[t + 1]], dim=D, keep=keep,
+                              rows=urows[k[t]:k[t + 1]])
                 for t in range(T)]
 
 

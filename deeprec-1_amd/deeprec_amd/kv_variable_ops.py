@@ -75,9 +75,12 @@ class IndexedSlices(object):
     `values` materialises them on first access (dr_rows_from_ptr)."""
 
     def __init__(self, values, indices, num_valid=None, unique=False, grad_ptr=None, dim=None,
-                 keep=()):
+                 keep=(), rows=None):
         self._values = values
         self.indices = indices
+        # rows [N] int64: the EV row each index was resolved to by the forward
+        # (a row-grouped backward); lets SGD skip the key-table probe
+        self.rows = rows
         self.num_valid = num_valid  # optional device int64[1] (<= N)
         self.unique = unique        # indices known distinct (a lookup's backward)
         self.grad_ptr = grad_ptr

@@ -7,6 +7,8 @@ backward.  Several slices for one variable are deduplicated first with
 unique + unsorted_segment_sum, as _deduplicate_indexed_slices does
 (python/training/optimizer.py:68-83).
 """
+import os
+
 import torch
 
 from . import ops
@@ -58,6 +60,10 @@ def _rounds(slices):
         m = rank == r
         out.append(IndexedSlices(v[m], i[m], unique=True))
     return out
+
+
+# SGD applies of row-grouped backwards use the forward's rows (A/B switch)
+_KNOWN_ROWS = os.environ.get("DR_APPLY_PROBE") != "1"
 
 
 def _grad_rows(grp, fn_name):
@@ -146,6 +152,24 @@ class _Optimizer(object):
         for (_, _), grp in groups.items():
             T = len(grp)
             dev = grp[0][0].device
+            if (self._opt == 0 and _KNOWN_ROWS
+                    and all(sl.grad_ptr is not None and sl._values is None and sl.rows is not None
+                            and var.filter_freq == 0 for var, sl in grp)):
+                # SGD of row-grouped lookup backwards: the forward's rows, no
+                # key-table probe (dr_ev_apply_grouped_ptr_rows)
+                P = C.c_void_p * T
+                st = stream_handle(dev)
+                idxs = [sl.indices.contiguous() for _, sl in grp]
+                with _Locked(self.use_locking, [var.handle.value for var, _ in grp], st):
+                    check(lib().dr_ev_apply_grouped_ptr_rows(
+                        self._opt, P(*[var.handle.value for var, _ in grp]), T,
+                        P(*[sl.grad_ptr.data_ptr() for _, sl in grp]),
+                        P(*[i.data_ptr() for i in idxs]),
+                        P(*[sl.rows.data_ptr() for _, sl in grp]),
+                        (C.c_int64 * T)(*[i.numel() for i in idxs]),
+                        P(*[ptr(sl.num_valid) for _, sl in grp]), self.lr, gs, st))
+                ops._post(dev)
+                continue
             grads, fn = _grad_rows(grp, "dr_ev_apply_grouped")
             idxs = [sl.indices.contiguous() for _, sl in grp]
             slots = [self._slots(var) for var, _ in grp]

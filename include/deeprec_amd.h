@@ -263,6 +263,13 @@ int dr_pool_grad_rows_grouped(const dr_pool_grad_desc* descs_host, int num_table
                               const int64_t* keys, int defer, int64_t* uniq_out,
                               int64_t* num_unique, uint64_t* grad_ptr, float* grad_unique,
                               void* ws, size_t ws_bytes, void* stream);
+/* The same, also writing uniq_rows[o] = the row the forward resolved unique */
+/* id o to (rowsel at its first position; NULL: not written).               */
+int dr_pool_grad_rows_grouped_ex(const dr_pool_grad_desc* descs_host, int num_tables,
+                                 int64_t batch, int dim, const int64_t* rowsel, int64_t row_limit,
+                                 const int64_t* keys, int defer, int64_t* uniq_out,
+                                 int64_t* uniq_rows, int64_t* num_unique, uint64_t* grad_ptr,
+                                 float* grad_unique, void* ws, size_t ws_bytes, void* stream);
 /* out[i] = row at grad_ptr[i] (+0.0f first when bit 0 is set) for i <      */
 /* min(n, *n_dev) (n_dev DEVICE or NULL); later rows are not written.        */
 int dr_rows_from_ptr(const uint64_t* grad_ptr, int64_t n, const int64_t* n_dev, int dim,
@@ -479,6 +486,17 @@ int dr_ev_apply_grouped_ptr(int optimizer, dr_ev* const* vars, dr_ev* const* slo
                             const int64_t* const* n_dev, float lr, float beta1_power,
                             float beta2_power, float beta1, float beta2, float epsilon,
                             int64_t global_step, void* stream);
+/* KvResourceSparseApplyGradientDescent by address with the keys' rows      */
+/* KNOWN (rows[t][i], the uniq_rows output of dr_pool_grad_rows_grouped_ex): */
+/* the forward of a filter-free EV resolved and initialised every key, so   */
+/* LookupOrCreate would return exactly that row -- the key table is not     */
+/* probed again (versions still stamped).  SGD only: the other optimizers   */
+/* need the slot-column first-touch bits of the key's hash slot.            */
+int dr_ev_apply_grouped_ptr_rows(int optimizer, dr_ev* const* vars, int num_tables,
+                                 const uint64_t* const* grad_ptrs, const int64_t* const* keys,
+                                 const int64_t* const* rows, const int64_t* n_host,
+                                 const int64_t* const* n_dev, float lr, int64_t global_step,
+                                 void* stream);
 /* KvResourceSparseApplyFtrl / FtrlV2 (training_ali_ops.cc:167-331; op defs  */
 /* core/ops/training_ali_ops.cc): accum / linear are slot EVs of var;        */
 /* l2_shrinkage 0 = Ftrl, > 0 = FtrlV2.  The row norm of `linear` is an fp32 */

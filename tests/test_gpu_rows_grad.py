@@ -261,6 +261,48 @@ def test_rows_train_step_equals_unique_path(dr, opt_name, onehot):
     dr.status_check()
 
 
+def test_sgd_known_rows_equals_probed_apply(dr):
+    """SGD of a row-grouped backward applies through the forward's rows
+    (dr_ev_apply_grouped_ptr_rows, no key-table probe).  Against the probing
+    by-address apply on the same steps (new keys each step, steps_to_live
+    versions, a shared key space): keys, values and versions identical."""
+    from deeprec_amd import training
+    rng = np.random.default_rng(91)
+    B, D, F = 300, 16, 3
+    batches = [([rng.integers(0, 120, B).astype(np.int64) for _ in range(F)],
+                rng.standard_normal((B, F * D)).astype(np.float32)) for _ in range(4)]
+    res = []
+    for known in (True, False):
+        old = training._KNOWN_ROWS
+        training._KNOWN_ROWS = known
+        try:
+            evs = [dr.EmbeddingVariable("kr_%d_%d" % (int(known), f), D, 0.05, steps_to_live=7)
+                   for f in range(F)]
+            opt = dr.GradientDescentOptimizer(0.05)
+            ind = T(np.stack([np.arange(B), np.zeros(B, np.int64)], 1))
+            with _Path(True):
+                for step, (vs, g) in enumerate(batches):
+                    st = [dr.SparseTensor(ind, T(v), (B, 1)) for v in vs]
+                    out = dr.embedding_lookup_sparse_multi(evs, st, combiner="sum")
+                    out.backward(T(g))
+                    assert evs[0].pending_grads[-1].rows is not None
+                    opt.apply_gradients(evs, global_step=10 + step)
+            torch.cuda.synchronize()
+            ex = []
+            for e in evs:
+                k, v, ver = (H(a) for a in e.export()[:3])
+                o = np.argsort(k)
+                ex.append((k[o], v[o], ver[o]))
+            res.append(ex)
+        finally:
+            training._KNOWN_ROWS = old
+    for a, b in zip(*res):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    assert res[0][0][2].max() == 13          # versions stamped by the last step
+    dr.status_check()
+
+
 def test_rows_from_ptr_zero_sign(dr):
     """Bit 0 of a gradient address = 0.0f + g: -0.0 becomes +0.0 (the
     reference's unsorted segment sum starts from 0); without it the sign
