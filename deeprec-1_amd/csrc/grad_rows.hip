@@ -344,36 +344,47 @@ __global__ __launch_bounds__(256) void rows_work_kernel(
   }
 }
 
-// grad_unique[o] = ((c_0 + c_1) + c_2) + ... for the queued long runs: c_0
-// is in grad_unique[o]; c_k (k >= 1) sits in part[m_k / chunk] for the
-// multiples m_k of the chunk inside the run.
+// grad_unique[o] for the queued long runs: c_0 (in grad_unique[o]) plus the
+// chunk partials c_k (k >= 1, in part[m_k / chunk] for the multiples m_k of
+// the chunk inside the run).  One BLOCK per run: its GPB lane groups take
+// the partials in blocks of FC, group q blocks q, q + GPB, ..., each summed
+// in order; then c_0 + S_0 + S_1 + ... + S_{GPB-1} in group order.  A fixed
+// association (deterministic, fp32 tolerance like every long run), with the
+// serial chain of a hot id cut GPB-fold (a DIN padding id: 800 partials).
 template <int VEC, int G, int CPL>
 __global__ __launch_bounds__(256) void rows_finish_kernel(
     RowsGroup g, int T, const uint32_t* __restrict__ skey, const int32_t* __restrict__ perm,
     int dim, float* __restrict__ gu, const float* __restrict__ part,
     const int32_t* __restrict__ longs, const int32_t* __restrict__ nlong, int64_t nslots) {
+  constexpr int GPB = 256 / G;
   __shared__ int64_t sk[DR_MAX_GROUP + 1];
+  __shared__ __attribute__((aligned(16))) float red[256 * VEC * CPL];  // GPB group sums (dim <= G*VEC*CPL)
+  __shared__ int used[GPB];
   if (threadIdx.x <= T) sk[threadIdx.x] = g.koff[threadIdx.x];
   __syncthreads();
-  constexpr int GPB = 256 / G;
   const int64_t N = sk[T];
   const int n = *nlong;
+  const int q = threadIdx.x / G;
   const int lg = threadIdx.x % G;
   const int dv = dim / VEC;
   using R = Row<VEC, G, CPL>;
-  for (int64_t i = (int64_t)blockIdx.x * GPB + threadIdx.x / G; i < n;
-       i += (int64_t)gridDim.x * GPB) {
+  using V = typename VecT<VEC>::T;
+  // <= 128 floats of partial rows in flight per lane
+  constexpr int FC = 128 / (VEC * CPL) < 8 ? 8
+                     : (128 / (VEC * CPL) > kRowsFinishMax ? kRowsFinishMax
+                                                           : 128 / (VEC * CPL));
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {   // block-uniform
     const int64_t o = longs[2 * i], c0 = longs[2 * i + 1];
     const uint32_t u = skey[c0];
     const int t = tab_of(sk, T, perm[c0]);
     const int64_t kt0 = sk[t], nnz_t = sk[t + 1] - sk[t];
     R acc;
-    load_row_u<VEC, G, CPL>(acc, gu + o * (int64_t)dim, lg, dv);
-    // <= 128 floats of partial rows in flight per lane
-    constexpr int FC = 128 / (VEC * CPL) < 8 ? 8
-                       : (128 / (VEC * CPL) > kRowsFinishMax ? kRowsFinishMax
-                                                             : 128 / (VEC * CPL));
-    for (int64_t m = (c0 / kRowsChunk + 1) * kRowsChunk; m < N; m += FC * kRowsChunk) {
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<V>();
+    bool any = false;
+    const int64_t m1 = (c0 / kRowsChunk + 1) * kRowsChunk;   // first partial of the run
+    for (int64_t m = m1 + (int64_t)q * FC * kRowsChunk; m < N;
+         m += (int64_t)GPB * FC * kRowsChunk) {
       R y[FC];
       bool ok[FC];
       uint32_t kj[FC];
@@ -395,14 +406,43 @@ __global__ __launch_bounds__(256) void rows_finish_kernel(
         const int64_t k = (int64_t)pj[j] - kt0;   // in table t <=> in [0, nnz_t)
         ok[j] = (m + j * kRowsChunk < N) & (kj[j] == u) & (k >= 0) & (k < nnz_t);
       }
-#pragma unroll
-      for (int j = 0; j < FC; ++j) {
-        if (!ok[j]) break;
-        acc_add(acc, y[j]);
+      if (!ok[0]) break;
+      if (any) {
+        acc_add(acc, y[0]);
+      } else {
+        acc = y[0];
+        any = true;
       }
+      // ok[] is a prefix (a run's chunks are contiguous): predicated adds
+#pragma unroll
+      for (int j = 1; j < FC; ++j)
+        if (ok[j]) acc_add(acc, y[j]);
       if (!ok[FC - 1]) break;
     }
-    store_row<VEC, G, CPL>(acc, gu + o * (int64_t)dim, lg, dv);
+    // group sums -> LDS, then group 0 adds them to c_0 in group order
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int col = lg + c * G;
+      if (col < dv) reinterpret_cast<V*>(red + q * dim)[col] = acc.v[c];
+    }
+    if (lg == 0) used[q] = any ? 1 : 0;
+    __syncthreads();
+    if (q == 0) {
+      R tot;
+      load_row_u<VEC, G, CPL>(tot, gu + o * (int64_t)dim, lg, dv);
+      for (int r = 0; r < GPB; ++r) {
+        if (!used[r]) continue;
+        R x;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          const int col = lg + c * G;
+          x.v[c] = col < dv ? reinterpret_cast<const V*>(red + r * dim)[col] : vzero<V>();
+        }
+        acc_add(tot, x);
+      }
+      store_row<VEC, G, CPL>(tot, gu + o * (int64_t)dim, lg, dv);
+    }
+    __syncthreads();   // red / used are rewritten by the next run
   }
 }
 
@@ -491,10 +531,14 @@ static void launch_rows(const RowsGroup& g, int T, int64_t B, const RowsWs& w, i
     hipLaunchKernelGGL((rows_work_kernel<VEC, G, CPL, false>), dim3((unsigned)blocks), dim3(256),
                        0, s, g, T, B, w.kout, w.perm, w.ex, w.base, dim, w.work, w.nwork, gptr,
                        gu, w.part, w.longs, w.nlong, st);
-  if (N > kRowsChunk)
-    hipLaunchKernelGGL((rows_finish_kernel<VEC, G, CPL>), dim3(64), dim3(256), 0, s, g, T,
-                       w.kout, w.perm, dim, gu, w.part, w.longs, w.nlong,
-                       N / kRowsChunk + 2);
+  if (N > kRowsChunk) {
+    // one block per queued run (at most one per chunk); most runs of a
+    // hotness-1 batch hold a single partial, so blocks, not lanes, carry them
+    const int64_t nslots = N / kRowsChunk + 2;
+    const unsigned fb = (unsigned)(nslots < 2048 ? nslots : 2048);
+    hipLaunchKernelGGL((rows_finish_kernel<VEC, G, CPL>), dim3(fb), dim3(256), 0, s, g, T,
+                       w.kout, w.perm, dim, gu, w.part, w.longs, w.nlong, nslots);
+  }
 }
 
 __global__ void rows_zero_i32(int32_t* p, int32_t* q) {

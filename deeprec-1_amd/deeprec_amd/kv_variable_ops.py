@@ -61,6 +61,38 @@ def _default_row(initializer, dim, device, dtype=torch.float32):
     return v.cpu().contiguous()
 
 
+# Handles whose last Python reference died while a hipGraph was being
+# captured.  Releasing one frees device memory (hipFree) and synchronises,
+# which a capture in torch's default global mode turns into a failed capture;
+# the cyclic garbage of an earlier step can be collected at any allocation
+# inside a captured step, so such releases wait for the next uncaptured one.
+_DEFERRED = []
+_DEFERRED_LOCK = threading.Lock()
+
+
+def _capturing():
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
+def _flush_deferred_releases():
+    if not _DEFERRED or _capturing():
+        return
+    with _DEFERRED_LOCK:
+        hs = _DEFERRED[:]
+        del _DEFERRED[:]
+    for h in hs:
+        lib().dr_ev_release(h)
+
+
+def _release_handle(h):
+    if _capturing():
+        with _DEFERRED_LOCK:
+            _DEFERRED.append(h)
+        return
+    _flush_deferred_releases()
+    lib().dr_ev_release(h)
+
+
 _KEY_DTYPES = (torch.int64, torch.int32)
 _VALUE_DTYPES = (torch.float32, torch.float64)
 
@@ -140,6 +172,7 @@ class EmbeddingVariable(object):
         self.steps_to_live = int(steps_to_live or 0)
         # EmbeddingConfig::l2_weight_threshold (embedding_config.h:17,28): -1 = off
         self.l2_weight_threshold = float(l2_weight_threshold)
+        _flush_deferred_releases()
         default = _default_row(initializer, self.dim, self.device, self.value_dtype)
         self._default_host = default
         h = C.c_void_p()
@@ -168,7 +201,7 @@ class EmbeddingVariable(object):
     def __del__(self):
         try:
             if getattr(self, "_h", None):
-                lib().dr_ev_release(self._h)
+                _release_handle(self._h)
                 self._h = None
         except Exception:
             pass
