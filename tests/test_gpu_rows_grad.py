@@ -359,3 +359,28 @@ def test_graph_captured_train_steps_equal_eager(dr):
     for (k1, v1), (k2, v2) in zip(*exports):
         np.testing.assert_array_equal(k1, k2)
         np.testing.assert_array_equal(v1, v2)
+
+
+def test_ev_collected_during_capture_is_released_after(dr):
+    """An EV whose last reference dies inside a hipGraph capture (cyclic
+    garbage collected by an allocation in the captured step) does not free
+    device memory there -- that would invalidate the capture -- but is
+    released by the next uncaptured EV creation."""
+    import gc
+    from deeprec_amd import kv_variable_ops as kvo
+    gc.collect()
+    kvo._flush_deferred_releases()
+    ev = dr.EmbeddingVariable("cap_gc", 8, 0.0, capacity=1024)
+    ev._self_ref = ev                      # a cycle: only the collector frees it
+    del ev
+    x = torch.zeros(16, device="cuda")
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y = x + 1
+        gc.collect()
+    assert len(kvo._DEFERRED) == 1
+    g.replay()
+    torch.cuda.synchronize()
+    assert float(y.sum()) == 16.0
+    dr.EmbeddingVariable("cap_gc2", 8, 0.0, capacity=1024)
+    assert len(kvo._DEFERRED) == 0
