@@ -578,11 +578,26 @@ struct ApplyCols {
   int cols[3];
 };
 
-enum { OPT_SGD = 0, OPT_ADAGRAD = 1, OPT_ADAM = 2, OPT_FTRL = 3 };
+enum {
+  OPT_SGD = 0,
+  OPT_ADAGRAD = 1,
+  OPT_ADAM = 2,
+  OPT_FTRL = 3,
+  OPT_ADAM_ASYNC = 4,     // KvSparseApplyAdamAsync (training_ali_ops.cc:1404-1575)
+  OPT_ADAM_RMSPROP = 5,   //   ... with apply_sparse_rmsprop (:1483-1519)
+  OPT_ADAGRAD_DECAY = 6   // KvSparseApplyAdagradDecay (training_ali_ops.cc:703-823)
+};
+// var + two slot columns (m / v, or accum / accum_decay_power)
+__host__ __device__ constexpr bool opt_three_cols(int opt) {
+  return opt == OPT_ADAM || opt == OPT_ADAM_ASYNC || opt == OPT_ADAM_RMSPROP ||
+         opt == OPT_ADAGRAD_DECAY;
+}
 
 struct OptScalars {
   float lr, beta1, beta2, eps, alpha;
   float l1, l2, lr_power, l2_shrinkage;  // FTRL
+  float decay_rate, decay_baseline;      // AdagradDecay
+  int64_t decay_step;
 };
 
 // Two phases per wave of 64 keys.  Phase 1, lane per key: LookupOrCreate
@@ -605,6 +620,35 @@ __device__ __forceinline__ float apply_one(float gv, float w, float* a1, float* 
     const float up = lg_ * rs;
     *a1 = a;
     return w - up;
+  } else if (OPT == OPT_ADAM_ASYNC) {  // training_ali_ops.cc:1552-1554
+    float m = *a1;
+    float v = *a2;
+    const float mt = m * sc.beta1;
+    const float mg = gv * (1.0f - sc.beta1);
+    m = mt + mg;
+    const float vt = v * sc.beta2;
+    const float g2 = gv * gv;
+    const float vg = g2 * (1.0f - sc.beta2);
+    v = vt + vg;
+    const float num = m * sc.alpha;
+    const float den = sqrtf(v) + sc.eps;
+    *a1 = m;
+    *a2 = v;
+    return w - num / den;
+  } else if (OPT == OPT_ADAM_RMSPROP) {  // training_ali_ops.cc:1506-1513
+    float m = *a1;
+    float v = *a2;
+    const float vt = v * sc.beta2;
+    const float g2 = gv * gv;
+    const float vg = g2 * (1.0f - sc.beta2);
+    v = vt + vg;
+    const float rs = 1.0f / sqrtf(v + sc.eps);
+    const float step = (rs * sc.lr) * gv;
+    const float mt = m * sc.beta1;
+    m = mt + step;
+    *a1 = m;
+    *a2 = v;
+    return w - m;
   } else {  // OPT_ADAM, training_ali_ops.cc:952-958
     float m = *a1;
     float v = *a2;
@@ -621,6 +665,25 @@ __device__ __forceinline__ float apply_one(float gv, float w, float* a1, float* 
     *a2 = v;
     return w - num / den;
   }
+}
+
+// AdagradDecay element (training_ali_ops.cc:802-808): when the row decays
+// this step, a = max(a * rate, baseline) (cwiseMax: a < b ? b : a), then
+// a += g^2; v -= (lr * g) * rsqrt(a).
+__device__ __forceinline__ float adagrad_decay_one(float gv, float w, float* a1, bool dec,
+                                                   const OptScalars& sc) {
+  float a = *a1;
+  if (dec) {
+    a = a * sc.decay_rate;
+    a = a < sc.decay_baseline ? sc.decay_baseline : a;
+  }
+  const float g2 = gv * gv;
+  a = a + g2;
+  const float lg_ = sc.lr * gv;
+  const float rs = 1.0f / sqrtf(a);
+  const float up = lg_ * rs;
+  *a1 = a;
+  return w - up;
 }
 
 // One table of a grouped apply launch (blockIdx.y selects it).
@@ -750,7 +813,8 @@ __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t di
   int initmask;
   apply_probe(at, base + lane, ne, gs, &row, &initmask, st);
   constexpr int P = 64 / G;                          // rows updated together
-  constexpr int U = OPT == OPT_ADAM ? 2 : 4;          // row batches in flight
+  constexpr bool C3 = opt_three_cols(OPT);
+  constexpr int U = C3 ? 2 : 4;                      // row batches in flight
   const int sub = lane / G;
   const int lg = lane % G;
   const int64_t dv = dim / VEC;
@@ -783,8 +847,23 @@ __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t di
       wp[q] = (ok && !(im & 1)) ? reinterpret_cast<const V*>(cols.pool[0] + rr[q] * dim) : d0;
       ap1[q] = (OPT != OPT_SGD && ok && !(im & 2))
                    ? reinterpret_cast<const V*>(cols.pool[1] + rr[q] * dim) : d1;
-      ap2[q] = (OPT == OPT_ADAM && ok && !(im & 4))
+      ap2[q] = (C3 && ok && !(im & 4))
                    ? reinterpret_cast<const V*>(cols.pool[2] + rr[q] * dim) : d2;
+    }
+    // AdagradDecay: the row's decay count is element 0 of its
+    // accum_decay_power row (a var-shaped slot, adagrad_decay.py:104-124);
+    // the row decays when global_step / decay_step > that count (Tstep
+    // division, compared as T)
+    bool dec[U];
+    float pw[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      dec[q] = false;
+      pw[q] = 0.f;
+      if (OPT == OPT_ADAGRAD_DECAY) {
+        pw[q] = gld(reinterpret_cast<const float*>(ap2[q]));
+        dec[q] = (float)(gs / sc.decay_step) > pw[q];
+      }
     }
     for (int64_t c = lg; c < dv; c += G) {
       V gv[U], w[U], a1[U], a2[U];
@@ -793,13 +872,24 @@ __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t di
         gv[q] = apply_ld(gp[q] + c);
         w[q] = apply_ld(wp[q] + c);
         if (OPT != OPT_SGD) a1[q] = apply_ld(ap1[q] + c);
-        if (OPT == OPT_ADAM) a2[q] = apply_ld(ap2[q] + c);
+        if (C3) a2[q] = apply_ld(ap2[q] + c);
       }
 #pragma unroll
       for (int q = 0; q < U; ++q) {
         if (rr[q] < 0) continue;
         if (zs[q]) gv[q] = vadd(vzero<V>(), gv[q]);
-        if constexpr (VEC == 4) {
+        if constexpr (OPT == OPT_ADAGRAD_DECAY) {
+          if constexpr (VEC == 4) {
+            w[q].x = adagrad_decay_one(gv[q].x, w[q].x, &a1[q].x, dec[q], sc);
+            w[q].y = adagrad_decay_one(gv[q].y, w[q].y, &a1[q].y, dec[q], sc);
+            w[q].z = adagrad_decay_one(gv[q].z, w[q].z, &a1[q].z, dec[q], sc);
+            w[q].w = adagrad_decay_one(gv[q].w, w[q].w, &a1[q].w, dec[q], sc);
+            if (c == 0 && dec[q]) a2[q].x = pw[q] + 1.0f;   // accum_decay_power(0) += 1
+          } else {
+            w[q] = adagrad_decay_one(gv[q], w[q], &a1[q], dec[q], sc);
+            if (c == 0 && dec[q]) a2[q] = pw[q] + 1.0f;
+          }
+        } else if constexpr (VEC == 4) {
           w[q].x = apply_one<OPT, VEC, G>(gv[q].x, w[q].x, &a1[q].x, &a2[q].x, sc);
           w[q].y = apply_one<OPT, VEC, G>(gv[q].y, w[q].y, &a1[q].y, &a2[q].y, sc);
           w[q].z = apply_one<OPT, VEC, G>(gv[q].z, w[q].z, &a1[q].z, &a2[q].z, sc);
@@ -808,7 +898,7 @@ __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t di
           w[q] = apply_one<OPT, VEC, G>(gv[q], w[q], &a1[q], &a2[q], sc);
         }
         if (OPT != OPT_SGD) apply_st(reinterpret_cast<V*>(cols.pool[1] + rr[q] * dim) + c, a1[q]);
-        if (OPT == OPT_ADAM) apply_st(reinterpret_cast<V*>(cols.pool[2] + rr[q] * dim) + c, a2[q]);
+        if (C3) apply_st(reinterpret_cast<V*>(cols.pool[2] + rr[q] * dim) + c, a2[q]);
         apply_st(reinterpret_cast<V*>(cols.pool[0] + rr[q] * dim) + c, w[q]);
       }
     }
@@ -1285,7 +1375,7 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
   int* stw = status_word();
   DR_REQUIRE(stw, DR_INTERNAL, "status word unavailable");
   const int64_t dim = vars[0] ? vars[0]->sh->dim : 0;
-  const int ncol = opt == OPT_SGD ? 1 : (opt == OPT_ADAGRAD ? 2 : 3);
+  const int ncol = opt == OPT_SGD ? 1 : (opt_three_cols(opt) || opt == OPT_FTRL ? 3 : 2);
   // Capacity first: a reserve may grow (reallocate) the slot table and the
   // row pools, so no pointer may be read into a descriptor before it.
   for (int t = 0; t < T; ++t) {
@@ -1350,6 +1440,15 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
     else if (opt == OPT_FTRL)                                                              \
       hipLaunchKernelGGL((ev_apply_ftrl_kernel<VEC, G>), grid, dim3(256), 0, st, ag, dim,   \
                          gs, sc, gind, stw);                                                \
+    else if (opt == OPT_ADAM_ASYNC)                                                        \
+      hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAM_ASYNC, VEC, G>), grid, dim3(256), 0, st, \
+                         ag, dim, gs, sc, gind, stw);                                       \
+    else if (opt == OPT_ADAM_RMSPROP)                                                      \
+      hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAM_RMSPROP, VEC, G>), grid, dim3(256), 0,   \
+                         st, ag, dim, gs, sc, gind, stw);                                   \
+    else if (opt == OPT_ADAGRAD_DECAY)                                                     \
+      hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAGRAD_DECAY, VEC, G>), grid, dim3(256), 0,  \
+                         st, ag, dim, gs, sc, gind, stw);                                   \
     else                                                                                   \
       hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAM, VEC, G>), grid, dim3(256), 0, st, ag,   \
                          dim, gs, sc, gind, stw);                                           \
@@ -1368,6 +1467,25 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
     DR_LAUNCH_CHECK();
   }
   // no counter mirror here: the step's next resolve refreshes it
+  return DR_OK;
+}
+
+// DR_OPT_* of dr_ev_apply_grouped[_ptr] -> kernel optimizer + scalars.
+// Adam / AdamAsync: alpha = lr * sqrt(1 - beta2^t) / (1 - beta1^t)
+// (training_ali_ops.cc:935-937, :1529-1531).
+static int grouped_opt(int optimizer, float lr, float beta1_power, float beta2_power, float beta1,
+                       float beta2, float epsilon, int* opt, OptScalars* sc) {
+  DR_REQUIRE(optimizer >= DR_OPT_SGD && optimizer <= DR_OPT_ADAM_ASYNC_RMSPROP,
+             DR_INVALID_ARGUMENT, "unknown optimizer %d", optimizer);
+  *sc = OptScalars{};
+  sc->lr = lr;
+  sc->beta1 = beta1;
+  sc->beta2 = beta2;
+  sc->eps = epsilon;
+  if (optimizer == DR_OPT_ADAM || optimizer == DR_OPT_ADAM_ASYNC)
+    sc->alpha = lr * sqrtf(1.0f - beta2_power) / (1.0f - beta1_power);
+  static const int map[] = {OPT_SGD, OPT_ADAGRAD, OPT_ADAM, OPT_ADAM_ASYNC, OPT_ADAM_RMSPROP};
+  *opt = map[optimizer];
   return DR_OK;
 }
 
@@ -2352,12 +2470,10 @@ int dr_ev_apply_grouped(int optimizer, dr_ev* const* vars, dr_ev* const* slot1,
                         float beta2_power, float beta1, float beta2, float epsilon,
                         int64_t global_step, void* stream) {
   using namespace dr;
-  DR_REQUIRE(optimizer >= DR_OPT_SGD && optimizer <= DR_OPT_ADAM, DR_INVALID_ARGUMENT,
-             "unknown optimizer %d", optimizer);
-  OptScalars sc = {lr, beta1, beta2, epsilon, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (optimizer == DR_OPT_ADAM) sc.alpha = lr * sqrtf(1.0f - beta2_power) / (1.0f - beta1_power);
-  const int opt = optimizer == DR_OPT_SGD ? OPT_SGD
-                                          : (optimizer == DR_OPT_ADAGRAD ? OPT_ADAGRAD : OPT_ADAM);
+  int opt;
+  OptScalars sc;
+  int rc = grouped_opt(optimizer, lr, beta1_power, beta2_power, beta1, beta2, epsilon, &opt, &sc);
+  if (rc) return rc;
   return apply_grouped(opt, vars, slot1, slot2, num_tables, sc, grads, keys, n_host, n_dev,
                        global_step, S(stream));
 }
@@ -2369,13 +2485,11 @@ int dr_ev_apply_grouped_ptr(int optimizer, dr_ev* const* vars, dr_ev* const* slo
                             float beta2_power, float beta1, float beta2, float epsilon,
                             int64_t global_step, void* stream) {
   using namespace dr;
-  DR_REQUIRE(optimizer >= DR_OPT_SGD && optimizer <= DR_OPT_ADAM, DR_INVALID_ARGUMENT,
-             "unknown optimizer %d", optimizer);
   DR_REQUIRE(grad_ptrs, DR_INVALID_ARGUMENT, "bad argument");
-  OptScalars sc = {lr, beta1, beta2, epsilon, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (optimizer == DR_OPT_ADAM) sc.alpha = lr * sqrtf(1.0f - beta2_power) / (1.0f - beta1_power);
-  const int opt = optimizer == DR_OPT_SGD ? OPT_SGD
-                                          : (optimizer == DR_OPT_ADAGRAD ? OPT_ADAGRAD : OPT_ADAM);
+  int opt;
+  OptScalars sc;
+  int rc = grouped_opt(optimizer, lr, beta1_power, beta2_power, beta1, beta2, epsilon, &opt, &sc);
+  if (rc) return rc;
   return apply_grouped(opt, vars, slot1, slot2, num_tables, sc,
                        reinterpret_cast<const float* const*>(grad_ptrs), keys, n_host, n_dev,
                        global_step, S(stream), 1);
@@ -2394,6 +2508,28 @@ int dr_ev_apply_grouped_ptr_rows(int optimizer, dr_ev* const* vars, int num_tabl
   return apply_grouped(OPT_SGD, vars, nullptr, nullptr, num_tables, sc,
                        reinterpret_cast<const float* const*>(grad_ptrs), keys, n_host, n_dev,
                        global_step, S(stream), 1, rows);
+}
+
+int dr_ev_apply_adagrad_decay_grouped(dr_ev* const* vars, dr_ev* const* accums,
+                                      dr_ev* const* decay_powers, int num_tables,
+                                      const void* const* grads, int grad_by_address,
+                                      const int64_t* const* keys, const int64_t* n_host,
+                                      const int64_t* const* n_dev, float lr, int64_t decay_step,
+                                      float decay_rate, float decay_baseline,
+                                      int64_t global_step, void* stream) {
+  using namespace dr;
+  // the op's scalar checks and the optimizer's constructor checks
+  // (adagrad_decay.py:64-72): a zero decay_step would divide by zero
+  DR_REQUIRE(decay_step > 0, DR_INVALID_ARGUMENT, "accumulator_decay_step must be positive");
+  DR_REQUIRE(grads, DR_INVALID_ARGUMENT, "bad argument");
+  OptScalars sc{};
+  sc.lr = lr;
+  sc.decay_step = decay_step;
+  sc.decay_rate = decay_rate;
+  sc.decay_baseline = decay_baseline;
+  return apply_grouped(OPT_ADAGRAD_DECAY, vars, accums, decay_powers, num_tables, sc,
+                       reinterpret_cast<const float* const*>(grads), keys, n_host, n_dev,
+                       global_step, S(stream), grad_by_address ? 1 : 0);
 }
 
 static int ftrl_grouped(dr_ev* const* vars, dr_ev* const* accums, dr_ev* const* linears,

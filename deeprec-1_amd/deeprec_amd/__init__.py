@@ -17,7 +17,8 @@ from .kv_variable_ops import (CBFFilter, CounterFilter, EmbeddingVariable, Embed
                               GlobalStepEvict, IndexedSlices, get_embedding_variable)
 from .ops import set_validate, status_check
 from .string_ops import StringTensor, string_to_hash_bucket_fast
-from .training import AdagradOptimizer, AdamOptimizer, FtrlOptimizer, GradientDescentOptimizer
+from .training import (AdagradDecayOptimizer, AdagradOptimizer, AdamAsyncOptimizer, AdamOptimizer,
+                       FtrlOptimizer, GradientDescentOptimizer)
 
 __all__ = [
     "DeepRecError", "InvalidArgumentError", "load", "DenseTable", "SparseTensor",
@@ -25,6 +26,7 @@ __all__ = [
     "fused_embedding_lookup_sparse", "safe_embedding_lookup_sparse", "CBFFilter",
     "CounterFilter", "EmbeddingVariable", "EmbeddingVariableOption", "GlobalStepEvict",
     "IndexedSlices", "get_embedding_variable", "set_validate", "status_check",
-    "AdagradOptimizer", "AdamOptimizer", "FtrlOptimizer", "GradientDescentOptimizer", "StringTensor",
+    "AdagradOptimizer", "AdagradDecayOptimizer", "AdamAsyncOptimizer", "AdamOptimizer",
+    "FtrlOptimizer", "GradientDescentOptimizer", "StringTensor",
     "string_to_hash_bucket_fast",
 ]

@@ -163,6 +163,8 @@ SIGNATURES = {
     "dr_ev_apply_grouped_ptr": (_I32, [_I32, _P, _P, _P, _I32, _P, _P, _P, _P, _F32, _F32, _F32,
                                        _F32, _F32, _F32, _I64, _P]),
     "dr_ev_apply_grouped_ptr_rows": (_I32, [_I32, _P, _I32, _P, _P, _P, _P, _P, _F32, _I64, _P]),
+    "dr_ev_apply_adagrad_decay_grouped": (_I32, [_P, _P, _P, _I32, _P, _I32, _P, _P, _P, _F32,
+                                                 _I64, _F32, _F32, _I64, _P]),
     "dr_ev_apply_ftrl_grouped_ptr": (_I32, [_P, _P, _P, _I32, _P, _P, _P, _P, _F32, _F32, _F32,
                                             _F32, _F32, _I64, _P]),
     "dr_ev_apply_ftrl": (_I32, [_P, _P, _P, _F32, _F32, _F32, _F32, _F32, _P, _P, _I64, _P, _I64,

@@ -348,3 +348,147 @@ class FtrlOptimizer(_Optimizer):
             w[idx] = (lin.clamp(-self.l1, self.l1) - lin) / y
             lin_t[idx] = lin
             acc_t[idx] = acc + g * g
+
+
+class AdamAsyncOptimizer(_Optimizer):
+    """KvSparseApplyAdamAsync (training_ali_ops.cc:1404-1575) on EVs, the
+    optimizer of python/training/adam_async.py.  Slots m, v (zeros); the beta
+    powers are per variable (adam_async.py:117-141: beta1 / beta2 initial,
+    one pair per EV) and advance after each apply that had gradients
+    (:1558-1559).  The reference multiplies them once per Shard() work chunk
+    of its CPU thread pool, so its count depends on the host's threading for
+    large N; here they advance once per apply, the single-chunk case.
+    apply_sparse_rmsprop: v = b2 v + (1 - b2) g^2, m = b1 m + lr g / sqrt(v +
+    eps), var -= m (:1506-1513); the powers are then not used.  Dense tables
+    take the same two updates on the indexed rows (SparseApplyAdamAsync)."""
+
+    def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8,
+                 use_locking=False, apply_sparse_rmsprop=False):
+        super().__init__(learning_rate, use_locking)
+        self.beta1, self.beta2, self.eps = float(beta1), float(beta2), float(epsilon)
+        self.apply_sparse_rmsprop = bool(apply_sparse_rmsprop)
+        self._opt = 4 if self.apply_sparse_rmsprop else 3
+        self._powers = {}     # id(var) -> [beta1_power, beta2_power] (fp32 values)
+        self._dense_mv = {}
+        self._advanced = []
+
+    def _slots(self, var):
+        return var.slot("AdamAsync", 0.0), var.slot("AdamAsync_1", 0.0)
+
+    def _power(self, var):
+        f32 = lambda x: torch.tensor(x, dtype=torch.float32).item()
+        return self._powers.setdefault(id(var), [f32(self.beta1), f32(self.beta2)])
+
+    def _apply_ev_batch(self, items, gs):
+        # tables with different beta powers cannot share one launch's alpha
+        by_power = {}
+        for var, sl in items:
+            by_power.setdefault(tuple(self._power(var)), []).append((var, sl))
+            self._advanced.append(var)
+        for (b1p, b2p), sub in by_power.items():
+            self._scalars = lambda b1p=b1p, b2p=b2p: (b1p, b2p, self.beta1, self.beta2, self.eps)
+            _Optimizer._apply_ev_batch(self, sub, gs)
+        self._scalars = lambda: (0.0, 0.0, self.beta1, self.beta2, self.eps)
+
+    def _finish(self):
+        f32 = lambda x: torch.tensor(x, dtype=torch.float32)
+        for var in self._advanced:
+            p = self._power(var)
+            p[0] = (f32(p[0]) * f32(self.beta1)).item()
+            p[1] = (f32(p[1]) * f32(self.beta2)).item()
+        self._advanced = []
+
+    def _dense_update(self, var, idx, g):
+        w = var.weight
+        m, v = self._dense_mv.setdefault(id(var), (torch.zeros_like(w), torch.zeros_like(w)))
+        with torch.no_grad():
+            mi, vi = m[idx], v[idx]
+            vi = vi * self.beta2 + (g * g) * (1 - self.beta2)
+            if self.apply_sparse_rmsprop:
+                mi = mi * self.beta1 + torch.rsqrt(vi + self.eps) * self.lr * g
+                w[idx] = w[idx] - mi
+            else:
+                b1p, b2p = self._power(var)
+                f32 = lambda x: torch.tensor(x, dtype=torch.float32)
+                alpha = (f32(self.lr) * torch.sqrt(1 - f32(b2p)) / (1 - f32(b1p))).item()
+                mi = mi * self.beta1 + g * (1 - self.beta1)
+                w[idx] = w[idx] - (mi * alpha) / (torch.sqrt(vi) + self.eps)
+                self._advanced.append(var)
+            m[idx], v[idx] = mi, vi
+
+
+class AdagradDecayOptimizer(_Optimizer):
+    """KvSparseApplyAdagradDecay (training_ali_ops.cc:703-823) on EVs, the
+    optimizer of python/training/adagrad_decay.py.  Slots: accumulator
+    (initial_accumulator_value, also the decay baseline) and
+    accumulator_decay_power (zeros, var-shaped: the count is element 0 of a
+    row, adagrad_decay.py:104-124).  The kernels see global_step + 1 (the
+    optimizer's _global_step_on_worker, :140), which also stamps versions.
+    Dense tables: SparseApplyAdagradDecay (:495-670) with one count per row."""
+
+    def __init__(self, learning_rate, global_step=None, initial_accumulator_value=0.1,
+                 accumulator_decay_step=100000, accumulator_decay_rate=0.9, use_locking=False):
+        if initial_accumulator_value <= 0.0:
+            raise ValueError("initial_accumulator_value must be positive: %s"
+                             % initial_accumulator_value)
+        if accumulator_decay_step <= 0:
+            raise ValueError("accumulator_decay_step must be positive: %s"
+                             % accumulator_decay_step)
+        if accumulator_decay_rate <= 0.0 or accumulator_decay_rate >= 1.0:
+            raise ValueError("accumulator_decay_rate must be in (0.0, 1.0): %s"
+                             % accumulator_decay_rate)
+        super().__init__(learning_rate, use_locking)
+        self.global_step = global_step
+        self.init_acc = float(initial_accumulator_value)
+        self.decay_step = int(accumulator_decay_step)
+        self.decay_rate = float(accumulator_decay_rate)
+        self._dense = {}
+
+    def apply_gradients(self, var_list, global_step=None):
+        gs = self.global_step if global_step is None else global_step
+        if gs is None:
+            raise ValueError("AdagradDecayOptimizer needs a global step")
+        self._gs = int(gs) + 1
+        return _Optimizer.apply_gradients(self, var_list, self._gs)
+
+    def _slots(self, var):
+        return var.slot("AdagradDecay", self.init_acc), var.slot("AdagradDecay_1", 0.0)
+
+    def _apply_ev_batch(self, items, gs):
+        import ctypes as C
+        groups = {}
+        for var, sl in items:
+            groups.setdefault((str(var.device), var.dim), []).append((var, sl))
+        for (_, _), grp in groups.items():
+            T = len(grp)
+            dev = grp[0][0].device
+            grads, _ = _grad_rows(grp, "dr_ev_apply_grouped")
+            by_addr = all(sl.grad_ptr is not None and sl._values is None for _, sl in grp)
+            idxs = [sl.indices.contiguous() for _, sl in grp]
+            slots = [self._slots(var) for var, _ in grp]
+            P = C.c_void_p * T
+            st = stream_handle(dev)
+            with _Locked(self.use_locking, [var.handle.value for var, _ in grp], st):
+                check(lib().dr_ev_apply_adagrad_decay_grouped(
+                    P(*[var.handle.value for var, _ in grp]),
+                    P(*[a.handle.value for a, _ in slots]), P(*[b.handle.value for _, b in slots]),
+                    T, P(*[v.data_ptr() for v in grads]), 1 if by_addr else 0,
+                    P(*[i.data_ptr() for i in idxs]),
+                    (C.c_int64 * T)(*[i.numel() for i in idxs]),
+                    P(*[ptr(sl.num_valid) for _, sl in grp]), self.lr, self.decay_step,
+                    self.decay_rate, self.init_acc, gs, st))
+            ops._post(dev)
+
+    def _dense_update(self, var, idx, g):
+        w = var.weight
+        acc, pw = self._dense.setdefault(
+            id(var), (torch.full_like(w, self.init_acc),
+                      torch.zeros(w.shape[0], dtype=torch.int64, device=w.device)))
+        with torch.no_grad():
+            a = acc[idx]
+            dec = (self._gs // self.decay_step) > pw[idx]
+            a = torch.where(dec[:, None], torch.clamp_min(a * self.decay_rate, self.init_acc), a)
+            pw[idx] = pw[idx] + dec.to(torch.int64)
+            a = a + g * g
+            acc[idx] = a
+            w[idx] = w[idx] - (g * self.lr) * torch.rsqrt(a)

@@ -467,7 +467,17 @@ int dr_ev_apply_adam(dr_ev* var, dr_ev* m, dr_ev* v, float beta1_power, float be
 /* launch): table t gets grads[t] [n_host[t], dim] for keys[t], optional     */
 /* DEVICE count n_dev[t]; slot1/slot2: Adagrad accumulator / Adam m, v (or  */
 /* NULL).  Scalars as in the single-table calls.                             */
-enum { DR_OPT_SGD = 0, DR_OPT_ADAGRAD = 1, DR_OPT_ADAM = 2 };
+/* DR_OPT_ADAM_ASYNC[_RMSPROP]: KvResourceSparseApplyAdamAsync               */
+/* (training_ali_ops.cc:1404-1575; apply_sparse_rmsprop selects the second);  */
+/* beta1_power / beta2_power are the variable's beta power slots (key 0), the */
+/* caller advances them after the apply (:1558-1559).                        */
+enum {
+  DR_OPT_SGD = 0,
+  DR_OPT_ADAGRAD = 1,
+  DR_OPT_ADAM = 2,
+  DR_OPT_ADAM_ASYNC = 3,
+  DR_OPT_ADAM_ASYNC_RMSPROP = 4
+};
 int dr_ev_apply_grouped(int optimizer, dr_ev* const* vars, dr_ev* const* slot1,
                         dr_ev* const* slot2, int num_tables, const float* const* grads,
                         const int64_t* const* keys, const int64_t* n_host,
@@ -497,6 +507,21 @@ int dr_ev_apply_grouped_ptr_rows(int optimizer, dr_ev* const* vars, int num_tabl
                                  const int64_t* const* rows, const int64_t* n_host,
                                  const int64_t* const* n_dev, float lr, int64_t global_step,
                                  void* stream);
+/* KvResourceSparseApplyAdagradDecay (training_ali_ops.cc:703-823; op def    */
+/* core/ops/training_ali_ops.cc): accum and accum_decay_power are slot EVs   */
+/* of var (var-shaped; the decay count is element 0 of a row, as the         */
+/* optimizer's slot, adagrad_decay.py:104-124).  A row whose count is below  */
+/* global_step / decay_step decays first: accum = max(accum * decay_rate,    */
+/* decay_baseline), count += 1; then accum += g^2, var -= lr g rsqrt(accum).  */
+/* grads[t]: a [n, dim] float block, or (grad_by_address) the uint64 row     */
+/* addresses of dr_pool_grad_rows_grouped.  decay_step must be > 0.          */
+int dr_ev_apply_adagrad_decay_grouped(dr_ev* const* vars, dr_ev* const* accums,
+                                      dr_ev* const* decay_powers, int num_tables,
+                                      const void* const* grads, int grad_by_address,
+                                      const int64_t* const* keys, const int64_t* n_host,
+                                      const int64_t* const* n_dev, float lr, int64_t decay_step,
+                                      float decay_rate, float decay_baseline,
+                                      int64_t global_step, void* stream);
 /* KvResourceSparseApplyFtrl / FtrlV2 (training_ali_ops.cc:167-331; op defs  */
 /* core/ops/training_ali_ops.cc): accum / linear are slot EVs of var;        */
 /* l2_shrinkage 0 = Ftrl, > 0 = FtrlV2.  The row norm of `linear` is an fp32 */

@@ -963,6 +963,81 @@ int orc_ev_apply_adam(orc_ev* var, orc_ev* m_ev, orc_ev* v_ev, float beta1_power
   return ORC_OK;
 }
 
+/* KvSparseApplyAdamAsync (training_ali_ops.cc:1404-1575).  rmsprop == 0:  */
+/* alpha = lr*sqrt(1-b2p)/(1-b1p); m = m*b1 + g*(1-b1); v = v*b2 + g^2*(1-b2); */
+/* var -= (m*alpha)/(sqrt(v)+eps) (:1529-1554).  rmsprop != 0 (:1506-1513):  */
+/* v = v*b2 + g^2*(1-b2); m = m*b1 + rsqrt(v+eps)*lr*g; var -= m.  The beta   */
+/* powers are the caller's (advanced after the apply, :1558-1559).           */
+int orc_ev_apply_adam_async(orc_ev* var, orc_ev* m_ev, orc_ev* v_ev, float beta1_power,
+                            float beta2_power, float lr, float beta1, float beta2, float eps,
+                            int rmsprop, const float* grad, const int64_t* keys, int64_t n,
+                            int64_t gs) {
+  const int64_t D = var->dim;
+  const float alpha = lr * sqrtf(1.0f - beta2_power) / (1.0f - beta1_power);
+  for (int64_t i = 0; i < n; ++i) {
+    int64_t e = orc_apply_key(var, keys[i], gs);
+    if (e < 0) continue;
+    float* w = orc_get_or_alloc(var, e, var->default_value);
+    float* m = orc_get_or_alloc(m_ev, e, m_ev->default_value);
+    float* v = orc_get_or_alloc(v_ev, e, v_ev->default_value);
+    for (int64_t d = 0; d < D; ++d) {
+      float g = grad[i * D + d];
+      float vt = v[d] * beta2, g2 = g * g, vg = g2 * (1.0f - beta2);
+      v[d] = vt + vg;
+      if (rmsprop) {
+        float rs = 1.0f / sqrtf(v[d] + eps);
+        float st = (rs * lr) * g;
+        float mt = m[d] * beta1;
+        m[d] = mt + st;
+        w[d] = w[d] - m[d];
+      } else {
+        float mt = m[d] * beta1, mg = g * (1.0f - beta1);
+        m[d] = mt + mg;
+        float num = m[d] * alpha;
+        float den = sqrtf(v[d]) + eps;
+        w[d] = w[d] - num / den;
+      }
+    }
+  }
+  return ORC_OK;
+}
+
+/* KvSparseApplyAdagradDecay (training_ali_ops.cc:703-823): the decay count */
+/* is element 0 of the row of the var-shaped accum_decay_power slot; when   */
+/* gs / decay_step (integer division) > count: a = max(a*rate, baseline),   */
+/* count += 1.  Then a += g^2; v -= (lr*g) * rsqrt(a).                       */
+int orc_ev_apply_adagrad_decay(orc_ev* var, orc_ev* accum, orc_ev* power, float lr,
+                               int64_t decay_step, float decay_rate, float decay_baseline,
+                               const float* grad, const int64_t* keys, int64_t n, int64_t gs) {
+  if (decay_step <= 0) return ORC_INVALID_ARGUMENT;
+  const int64_t D = var->dim;
+  for (int64_t i = 0; i < n; ++i) {
+    int64_t e = orc_apply_key(var, keys[i], gs);
+    if (e < 0) continue;
+    float* a = orc_get_or_alloc(accum, e, accum->default_value);
+    float* p = orc_get_or_alloc(power, e, power->default_value);
+    float* v = orc_get_or_alloc(var, e, var->default_value);
+    const int dec = (float)(gs / decay_step) > p[0];
+    if (dec) p[0] = p[0] + 1.0f;
+    for (int64_t d = 0; d < D; ++d) {
+      float g = grad[i * D + d];
+      float ad = a[d];
+      if (dec) {
+        ad = ad * decay_rate;
+        ad = ad < decay_baseline ? decay_baseline : ad;
+      }
+      float g2 = g * g;
+      ad = ad + g2;
+      a[d] = ad;
+      float lg = lr * g;
+      float rs = 1.0f / sqrtf(ad);
+      float up = lg * rs;
+      v[d] = v[d] - up;
+    }
+  }
+  return ORC_OK;
+}
+
 /* KvResourceSparseApplyFtrl[V2] (training_ali_ops.cc:167-331), the       */
 /* COMPUTE_FTRL macro (:279-307) per key with grad_to_use = g (+ 2 * l2_    */
 /* shrinkage * var for V2, :308-311):                                        */

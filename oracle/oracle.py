@@ -66,6 +66,9 @@ def lib():
             "orc_ev_apply_sgd": (i32, [p, f32, p, p, i64, i64]),
             "orc_ev_apply_adagrad": (i32, [p, p, f32, p, p, i64, i64]),
             "orc_ev_apply_adam": (i32, [p, p, p, f32, f32, f32, f32, f32, f32, p, p, i64, i64]),
+            "orc_ev_apply_adam_async": (i32, [p, p, p, f32, f32, f32, f32, f32, f32, i32, p, p,
+                                              i64, i64]),
+            "orc_ev_apply_adagrad_decay": (i32, [p, p, p, f32, i64, f32, f32, p, p, i64, i64]),
             "orc_ev_apply_ftrl": (i32, [p, p, p, f32, f32, f32, f32, f32, p, p, i64, i64]),
             "orc_dense_apply_sgd": (i32, [p, i64, f32, p, p, i64]),
             "orc_dense_apply_adagrad": (i32, [p, p, i64, f32, p, p, i64]),
@@ -436,6 +439,22 @@ class EV(object):
         _check(lib().orc_ev_apply_adam(self._h, m._h, v._h, beta1_power, beta2_power, lr,
                                        beta1, beta2, eps, _p(grad), _p(keys), keys.shape[0],
                                        gs), "adam")
+
+    def apply_adam_async(self, m, v, beta1_power, beta2_power, lr, beta1, beta2, eps, grad,
+                         keys, rmsprop=False, gs=-1):
+        grad = np.ascontiguousarray(grad, np.float32)
+        keys = np.ascontiguousarray(keys, np.int64)
+        _check(lib().orc_ev_apply_adam_async(self._h, m._h, v._h, beta1_power, beta2_power, lr,
+                                             beta1, beta2, eps, 1 if rmsprop else 0, _p(grad),
+                                             _p(keys), keys.shape[0], gs), "adam_async")
+
+    def apply_adagrad_decay(self, accum, power, lr, decay_step, decay_rate, decay_baseline,
+                            grad, keys, gs):
+        grad = np.ascontiguousarray(grad, np.float32)
+        keys = np.ascontiguousarray(keys, np.int64)
+        _check(lib().orc_ev_apply_adagrad_decay(self._h, accum._h, power._h, lr, decay_step,
+                                                decay_rate, decay_baseline, _p(grad), _p(keys),
+                                                keys.shape[0], gs), "adagrad_decay")
 
     def apply_ftrl(self, accum, linear, lr, l1, l2, lr_power, l2_shrinkage, grad, keys, gs=-1):
         grad = np.ascontiguousarray(grad, np.float32)

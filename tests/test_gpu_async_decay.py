@@ -1,0 +1,121 @@
+"""KvSparseApplyAdamAsync (training_ali_ops.cc:1404-1575, both modes) and
+KvSparseApplyAdagradDecay (:703-823) on the GPU against the oracle's
+restatements (themselves pinned by the reference's KATs,
+tests/test_oracle_async_decay.py): 5 steps over first-touch and repeated
+keys, several dims (VEC = 1 and 4 kernels), decay crossings every 2 steps,
+and the by-address gradients of a row-grouped lookup backward.  The apply
+kernels evaluate the oracle's scalar formulas with separate fp32 roundings:
+weights, slots and decay counts are bit-identical to the oracle's."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def T(x, dtype=None):
+    return torch.as_tensor(np.asarray(x), device=DEV, dtype=dtype)
+
+
+@pytest.fixture(scope="module")
+def dr():
+    import deeprec_amd as dr
+    dr.load()
+    dr.set_validate(True)
+    return dr
+
+
+@pytest.mark.parametrize("D", [1, 3, 16, 64])
+@pytest.mark.parametrize("rmsprop", [False, True])
+def test_adam_async_matches_oracle(dr, orc, D, rmsprop):
+    rng = np.random.default_rng(D * 7 + rmsprop)
+    lr, b1, b2, eps = 0.01, 0.9, 0.999, 1e-8
+    ev = dr.EmbeddingVariable("aa_%d_%d" % (D, rmsprop), D, 0.25)
+    oev = orc.EV(D, 0.25)
+    om, ov = oev.create_slot(1, 0.0), oev.create_slot(2, 0.0)
+    opt = dr.AdamAsyncOptimizer(lr, b1, b2, eps, apply_sparse_rmsprop=rmsprop)
+    b1p, b2p = np.float32(b1), np.float32(b2)
+    for step in range(5):
+        ids = rng.choice(300, 80, replace=False).astype(np.int64)
+        g = (rng.standard_normal((80, D)) * 0.2).astype(np.float32)
+        ev.pending_grads.append(dr.IndexedSlices(T(g), T(ids)))
+        opt.apply_gradients([ev], global_step=step)
+        oev.apply_adam_async(om, ov, float(b1p), float(b2p), lr, b1, b2, eps, g, ids,
+                             rmsprop=rmsprop, gs=step)
+        b1p, b2p = np.float32(b1p * np.float32(b1)), np.float32(b2p * np.float32(b2))
+    keys = np.arange(300, dtype=np.int64)
+    np.testing.assert_array_equal(ev.sparse_read(T(keys)).cpu().numpy(), oev.gather(keys),
+    )
+    np.testing.assert_array_equal(ev.slot("AdamAsync", 0.0).sparse_read(T(keys)).cpu().numpy(),
+                               om.gather(keys))
+    np.testing.assert_array_equal(ev.slot("AdamAsync_1", 0.0).sparse_read(T(keys)).cpu().numpy(),
+                               ov.gather(keys))
+    if not rmsprop:
+        p = opt._power(ev)
+        assert p[0] == float(b1p) and p[1] == float(b2p)
+
+
+@pytest.mark.parametrize("D", [1, 3, 16, 64])
+def test_adagrad_decay_matches_oracle(dr, orc, D):
+    rng = np.random.default_rng(D + 100)
+    lr, init, dstep, rate = 0.3, 0.1, 2, 0.8
+    ev = dr.EmbeddingVariable("ad_%d" % D, D, 0.5)
+    oev = orc.EV(D, 0.5)
+    oacc, opw = oev.create_slot(1, init), oev.create_slot(2, 0.0)
+    opt = dr.AdagradDecayOptimizer(lr, initial_accumulator_value=init,
+                                   accumulator_decay_step=dstep, accumulator_decay_rate=rate)
+    for step in range(6):
+        ids = rng.choice(120, 50, replace=False).astype(np.int64)
+        g = (rng.standard_normal((50, D)) * (0.05 if step % 2 else 0.5)).astype(np.float32)
+        ev.pending_grads.append(dr.IndexedSlices(T(g), T(ids)))
+        opt.apply_gradients([ev], global_step=step)
+        oev.apply_adagrad_decay(oacc, opw, lr, dstep, rate, init, g, ids, step + 1)
+    keys = np.arange(120, dtype=np.int64)
+    np.testing.assert_array_equal(ev.sparse_read(T(keys)).cpu().numpy(), oev.gather(keys),
+    )
+    np.testing.assert_array_equal(ev.slot("AdagradDecay", init).sparse_read(T(keys)).cpu().numpy(),
+                               oacc.gather(keys))
+    pw = ev.slot("AdagradDecay_1", 0.0).sparse_read(T(keys)).cpu().numpy()
+    np.testing.assert_array_equal(pw, opw.gather(keys))
+    assert pw[:, 0].max() >= 2.0            # rows decayed more than once
+
+
+def test_adagrad_decay_needs_global_step(dr):
+    ev = dr.EmbeddingVariable("ad_nogs", 4, 0.5)
+    opt = dr.AdagradDecayOptimizer(0.1)
+    ev.pending_grads.append(dr.IndexedSlices(T(np.ones((1, 4), np.float32)), T([3])))
+    with pytest.raises(ValueError):
+        opt.apply_gradients([ev])
+    with pytest.raises(ValueError):
+        dr.AdagradDecayOptimizer(0.1, accumulator_decay_step=0)
+
+
+@pytest.mark.parametrize("name", ["adam_async", "rmsprop", "adagrad_decay"])
+def test_by_address_grads_equal_value_grads(dr, name):
+    """The lookup's row-grouped backward hands gradients by address; the
+    apply through them equals the apply of the materialised values."""
+    rng = np.random.default_rng(17)
+    B, D = 256, 16
+    keys = T(rng.integers(0, 500, B).astype(np.int64))
+    ind = T(np.stack([np.arange(B), np.zeros(B, np.int64)], 1))
+    up = T(rng.standard_normal((B, D)).astype(np.float32))
+    outs = []
+    for by_addr in (True, False):
+        ev = dr.EmbeddingVariable("ba_%s_%d" % (name, by_addr), D, 0.1)
+        mk = {"adam_async": lambda: dr.AdamAsyncOptimizer(0.01),
+              "rmsprop": lambda: dr.AdamAsyncOptimizer(0.01, apply_sparse_rmsprop=True),
+              "adagrad_decay": lambda: dr.AdagradDecayOptimizer(
+                  0.1, accumulator_decay_step=1, accumulator_decay_rate=0.5)}[name]
+        opt = mk()
+        for step in range(3):
+            out = dr.embedding_lookup_sparse(ev, dr.SparseTensor(ind, keys, (B, 1)),
+                                             combiner="sum")
+            out.backward(up)
+            if not by_addr:
+                for sl in ev.pending_grads:
+                    sl.values = sl.values.clone()     # materialise, drop the addresses
+            opt.apply_gradients([ev], global_step=step)
+        torch.cuda.synchronize()
+        outs.append(ev.sparse_read(T(np.arange(500, dtype=np.int64))).cpu().numpy())
+    np.testing.assert_array_equal(outs[0], outs[1])
