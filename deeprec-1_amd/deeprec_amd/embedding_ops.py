@@ -686,8 +686,11 @@ def embedding_lookup_sparse(params, sp_ids, sp_weights=None, partition_strategy=
     """tf.nn.embedding_lookup_sparse (embedding_ops.py:480-675), 2-D sp_ids."""
     if combiner is None:
         combiner = "mean"
-    if combiner not in ("mean", "sqrtn", "sum"):
-        raise ValueError("combiner must be one of 'mean', 'sqrtn' or 'sum'")
+    if combiner not in ("mean", "sqrtn", "sum", "tile"):
+        raise ValueError("combiner must be one of 'mean', 'sqrtn', 'sum' or 'tile'")
+    if combiner == "tile":
+        return _tile_lookup_sparse(params if isinstance(params, (list, tuple)) else [params],
+                                   sp_ids, sp_weights, partition_strategy, max_norm)
     if isinstance(params, (list, tuple)):
         if len(params) == 1:
             params = params[0]
@@ -863,6 +866,47 @@ def _partitioned_gather(params, flat, n_dev, counts, init, strategy):
 
 class _Ctx(object):
     pass
+
+
+class _TileSumFn(torch.autograd.Function):
+    """unsorted_segment_sum of the gathered rows onto row * C + column
+    (_tile_combine_embedding, embedding_ops.py:468-476): the serial-order
+    HIP segment sum forward; backward gathers the output gradient at each
+    position's segment (UnsortedSegmentSum's gradient, math_grad.py)."""
+
+    @staticmethod
+    def forward(ctx, rows, seg, nseg):
+        ctx.save_for_backward(seg)
+        return ops.unsorted_segment_sum(rows, seg, nseg)
+
+    @staticmethod
+    def backward(ctx, g):
+        (seg,) = ctx.saved_tensors
+        return g.contiguous().index_select(0, seg.to(torch.int64)), None, None
+
+
+def _tile_lookup_sparse(params, sp_ids, sp_weights, partition_strategy, max_norm):
+    """combiner="tile" (embedding_ops.py:646-651,665-671): the embedding of
+    each (row, column) of sp_ids lands in its own D-wide column block of a
+    [B, C * D] output (C = dense_shape[1]); entries sharing a (row, column)
+    are summed.  unique (with counts for EV filters) -> gather of the unique
+    ids (EV / dense / partitioned, with its backward) -> max_norm clip ->
+    gather by idx (x weights) -> segment sum onto row * C + column."""
+    values = sp_ids.values.to(torch.int64).contiguous()
+    B, C = int(sp_ids.dense_shape[0]), int(sp_ids.dense_shape[1])
+    with_counts = isinstance(params[0], EmbeddingVariable) and params[0].filter_freq != 0
+    uniq, idx, cnt, U = ops.unique_device(values, with_counts)
+    emb = _partitioned_gather(list(params), uniq, U, cnt, None, partition_strategy)
+    if max_norm is not None:
+        l2 = torch.sqrt((emb * emb).sum(1, keepdim=True))
+        emb = emb * max_norm / torch.maximum(l2, torch.tensor(max_norm, device=emb.device))
+    rows = emb.index_select(0, idx.to(torch.int64))
+    if sp_weights is not None:
+        rows = rows * sp_weights.values.to(rows.dtype).reshape(-1, 1)
+    ind = sp_ids.indices.to(torch.int64)
+    seg = (ind[:, 0] * C + ind[:, 1]).to(torch.int32).contiguous()
+    out = _TileSumFn.apply(rows.contiguous(), seg, B * C)
+    return out.reshape(B, C * out.shape[1])
 
 
 def _partitioned_lookup_sparse(params, sp_ids, sp_weights, partition_strategy, combiner,
