@@ -79,3 +79,14 @@ def test_oracle_adagrad_decay_baseline_floor(orc):
     np.testing.assert_array_equal(pw.gather(np.array([7]))[0], [1.0, 0.0])
     with pytest.raises(Exception):
         ev.apply_adagrad_decay(acc, pw, 1.0, 0, 0.5, 0.1, g, np.array([7]), 5)
+
+
+def test_adagrad_decay_constructor_checks():
+    """AdagradDecayOptimizer's argument checks (adagrad_decay.py:64-72)."""
+    import deeprec_amd as dr
+    for kw in ({"initial_accumulator_value": 0.0}, {"accumulator_decay_step": 0},
+               {"accumulator_decay_rate": 1.0}, {"accumulator_decay_rate": 0.0}):
+        with pytest.raises(ValueError):
+            dr.AdagradDecayOptimizer(0.1, **kw)
+    o = dr.AdamAsyncOptimizer(apply_sparse_rmsprop=True)
+    assert o._opt == 4 and dr.AdamAsyncOptimizer()._opt == 3
