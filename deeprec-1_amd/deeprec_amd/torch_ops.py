@@ -251,6 +251,45 @@ def kv_resource_sparse_apply_ftrl(var: int, accum: int, linear: int, grad: Tenso
     ops._post(k.device)
 
 
+def _one(x):
+    import ctypes as C
+    return (C.c_void_p * 1)(x)
+
+
+@custom_op(_NS + "::kv_resource_sparse_apply_adam_async", mutates_args=(), device_types="cuda")
+def kv_resource_sparse_apply_adam_async(var: int, m: int, v: int, beta1_power: float,
+                                        beta2_power: float, lr: float, beta1: float,
+                                        beta2: float, epsilon: float, grad: Tensor,
+                                        indices: Tensor, global_step: int = -1,
+                                        apply_sparse_rmsprop: bool = False) -> None:
+    """KvResourceSparseApplyAdamAsync (training_ali_ops.cc:1404-1575); the
+    beta power slots are the caller's scalars (advanced after the call)."""
+    import ctypes as C
+    g, k, n, st = _apply_common(grad, indices)
+    opt = 4 if apply_sparse_rmsprop else 3
+    check(lib().dr_ev_apply_grouped(opt, _one(_h(var)), _one(_h(m)), _one(_h(v)), 1,
+                                    _one(g.data_ptr()), _one(k.data_ptr()), (C.c_int64 * 1)(n),
+                                    _one(None), lr, beta1_power, beta2_power, beta1, beta2,
+                                    epsilon, global_step, st))
+    ops._post(k.device)
+
+
+@custom_op(_NS + "::kv_resource_sparse_apply_adagrad_decay", mutates_args=(),
+           device_types="cuda")
+def kv_resource_sparse_apply_adagrad_decay(var: int, accum: int, accum_decay_power: int,
+                                           lr: float, decay_step: int, decay_rate: float,
+                                           decay_baseline: float, global_step: int,
+                                           grad: Tensor, indices: Tensor) -> None:
+    """KvResourceSparseApplyAdagradDecay (training_ali_ops.cc:703-823)."""
+    import ctypes as C
+    g, k, n, st = _apply_common(grad, indices)
+    check(lib().dr_ev_apply_adagrad_decay_grouped(
+        _one(_h(var)), _one(_h(accum)), _one(_h(accum_decay_power)), 1, _one(g.data_ptr()), 0,
+        _one(k.data_ptr()), (C.c_int64 * 1)(n), _one(None), lr, decay_step, decay_rate,
+        decay_baseline, global_step, st))
+    ops._post(k.device)
+
+
 # ---------------------------------------------------------------------------
 # Fused embedding ops (core/ops/fused_embedding_ops.cc)
 # ---------------------------------------------------------------------------
@@ -418,6 +457,7 @@ OPS = ["unique_with_counts", "sparse_segment_reduce", "sparse_segment_reduce_gra
        "unsorted_segment_sum", "resource_gather", "kv_resource_gather", "kv_resource_insert",
        "kv_resource_sparse_apply_gradient_descent", "kv_resource_sparse_apply_adagrad",
        "kv_resource_sparse_apply_adam", "kv_resource_sparse_apply_ftrl",
+       "kv_resource_sparse_apply_adam_async", "kv_resource_sparse_apply_adagrad_decay",
        "fused_embedding_local_sparse_look_up", "fused_embedding_local_sparse_look_up_grad",
        "fused_embedding_sparse_post_look_up", "fused_embedding_sparse_post_look_up_grad",
        "fm_second_order", "fm_second_order_grad", "dot_interaction", "dot_interaction_grad"]

@@ -119,3 +119,31 @@ def test_by_address_grads_equal_value_grads(dr, name):
         torch.cuda.synchronize()
         outs.append(ev.sparse_read(T(np.arange(500, dtype=np.int64))).cpu().numpy())
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def test_registered_ops_match_optimizers(dr, orc):
+    """torch.ops.deeprec.kv_resource_sparse_apply_{adam_async,adagrad_decay}
+    (the registered op layer) leave the EVs where the oracle does."""
+    import deeprec_amd.torch_ops  # noqa: F401
+    rng = np.random.default_rng(23)
+    D = 8
+    ids = rng.choice(100, 40, replace=False).astype(np.int64)
+    g = (rng.standard_normal((40, D)) * 0.3).astype(np.float32)
+    ev = dr.EmbeddingVariable("op_aa", D, 0.2)
+    m, v = ev.slot("m", 0.0), ev.slot("v", 0.0)
+    oev = orc.EV(D, 0.2)
+    om, ov = oev.create_slot(1, 0.0), oev.create_slot(2, 0.0)
+    torch.ops.deeprec.kv_resource_sparse_apply_adam_async(
+        ev.handle.value, m.handle.value, v.handle.value, 0.9, 0.999, 0.01, 0.9, 0.999, 1e-8,
+        T(g), T(ids), 3)
+    oev.apply_adam_async(om, ov, 0.9, 0.999, 0.01, 0.9, 0.999, 1e-8, g, ids, gs=3)
+    np.testing.assert_array_equal(ev.sparse_read(T(ids)).cpu().numpy(), oev.gather(ids))
+    ev2 = dr.EmbeddingVariable("op_ad", D, 0.2)
+    acc, pw = ev2.slot("acc", 0.1), ev2.slot("pw", 0.0)
+    oev2 = orc.EV(D, 0.2)
+    oacc, opw = oev2.create_slot(1, 0.1), oev2.create_slot(2, 0.0)
+    torch.ops.deeprec.kv_resource_sparse_apply_adagrad_decay(
+        ev2.handle.value, acc.handle.value, pw.handle.value, 0.5, 2, 0.9, 0.1, 5, T(g), T(ids))
+    oev2.apply_adagrad_decay(oacc, opw, 0.5, 2, 0.9, 0.1, g, ids, 5)
+    np.testing.assert_array_equal(ev2.sparse_read(T(ids)).cpu().numpy(), oev2.gather(ids))
+    np.testing.assert_array_equal(pw.sparse_read(T(ids)).cpu().numpy(), opw.gather(ids))
