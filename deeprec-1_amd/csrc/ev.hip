@@ -1851,7 +1851,12 @@ static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t 
     else                                                                        \
       launch_lookup_onehot<4, G, C, DR_ORDER_SEQ>(la, T, B, (int)dim, w, st);   \
   } while (0)
-  if (d4 <= 4) DR_LK(4, 1);
+  // DR_LOOKUP_SPLIT=2 (A/B switch): half the lanes per row, two float4 per
+  // lane -- twice the rows (and probes) per wave in flight
+  static const int split = getenv("DR_LOOKUP_SPLIT") ? atoi(getenv("DR_LOOKUP_SPLIT")) : 1;
+  if (split == 2 && d4 > 8 && d4 <= 16) DR_LK(8, 2);
+  else if (split == 2 && d4 > 16 && d4 <= 32) DR_LK(16, 2);
+  else if (d4 <= 4) DR_LK(4, 1);
   else if (d4 <= 8) DR_LK(8, 1);
   else if (d4 <= 16) DR_LK(16, 1);
   else if (d4 <= 32) DR_LK(32, 1);
