@@ -22,6 +22,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = "ev_lookup_onehot_kernel"  # bench.py's dominant kernel (argv[5] overrides)
+TIMING_LAUNCHES = 20                # bench.py kernel_ms() launches (--kernel-iters default)
 
 
 def per_dispatch(d, counter):
@@ -45,6 +46,16 @@ def main():
     for r in csv.DictReader(open(st)):
         if KERNEL in r["Name"]:
             avg_ns = float(r["AverageNs"])
+    # bench.py's HIP-event timing of the dominant kernel is its last
+    # TIMING_LAUNCHES dispatches (rotating step batches); the CSV average
+    # above also holds the step, check and first-touch launches
+    last_ns = None
+    tr = glob.glob(os.path.join(stats_dir, "*_kernel_trace.csv"))
+    if tr:
+        d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+             for r in csv.DictReader(open(tr[0])) if KERNEL in r["Kernel_Name"]]
+        if len(d) >= TIMING_LAUNCHES:
+            last_ns = sum(d[-TIMING_LAUNCHES:]) / TIMING_LAUNCHES
     fetch = per_dispatch(fetch_dir, "FETCH_SIZE")
     write = per_dispatch(write_dir, "WRITE_SIZE")
     f_b = statistics.median(fetch) * 1024 * 2   # gfx950: FETCH_SIZE = 1/2 of wide reads
@@ -60,6 +71,7 @@ def main():
         "write_bytes": w_b,
         "bytes_per_launch": f_b + w_b,
         "kernel_avg_ns_rocprof": avg_ns,
+        "kernel_avg_ns_rocprof_timing_launches": last_ns,
     }
     json.dump(out, open(os.path.join(prof, "%s_pmc_traffic%s.json" % (rnd, tag)), "w"), indent=1)
     print(json.dumps(out, indent=1))
