@@ -384,7 +384,8 @@ class AdamAsyncOptimizer(_Optimizer):
         by_power = {}
         for var, sl in items:
             by_power.setdefault(tuple(self._power(var)), []).append((var, sl))
-            self._advanced.append(var)
+            if sl.indices.numel() > 0:      # the op's `if (N > 0)` holds the power update
+                self._advanced.append(var)
         for (b1p, b2p), sub in by_power.items():
             self._scalars = lambda b1p=b1p, b2p=b2p: (b1p, b2p, self.beta1, self.beta2, self.eps)
             _Optimizer._apply_ev_batch(self, sub, gs)

@@ -147,3 +147,16 @@ def test_registered_ops_match_optimizers(dr, orc):
     oev2.apply_adagrad_decay(oacc, opw, 0.5, 2, 0.9, 0.1, g, ids, 5)
     np.testing.assert_array_equal(ev2.sparse_read(T(ids)).cpu().numpy(), oev2.gather(ids))
     np.testing.assert_array_equal(pw.sparse_read(T(ids)).cpu().numpy(), opw.gather(ids))
+
+
+def test_adam_async_empty_gradient_keeps_powers(dr):
+    """N == 0: the op does nothing, beta powers included (training_ali_ops.cc
+    :1482 wraps the update and the power advance in `if (N > 0)`)."""
+    ev = dr.EmbeddingVariable("aa_empty", 4, 0.5)
+    opt = dr.AdamAsyncOptimizer(0.01)
+    ev.pending_grads.append(dr.IndexedSlices(T(np.zeros((0, 4), np.float32)),
+                                             T(np.zeros(0, np.int64))))
+    opt.apply_gradients([ev], global_step=0)
+    p = opt._power(ev)
+    assert p[0] == float(np.float32(0.9)) and p[1] == float(np.float32(0.999))
+    assert ev.sparse_read(T([1])).cpu().numpy().tolist() == [[0.5] * 4]
