@@ -160,3 +160,46 @@ def test_adam_async_empty_gradient_keeps_powers(dr):
     p = opt._power(ev)
     assert p[0] == float(np.float32(0.9)) and p[1] == float(np.float32(0.999))
     assert ev.sparse_read(T([1])).cpu().numpy().tolist() == [[0.5] * 4]
+
+
+def test_dense_table_adagrad_decay_and_adam_async(dr):
+    """Dense tables (SparseApplyAdagradDecay, training_ali_ops.cc:495-670,
+    one decay count per row; SparseApplyAdamAsync) against float64 numpy
+    restatements of the same updates on the indexed rows."""
+    rng = np.random.default_rng(31)
+    R, D = 20, 6
+    w0 = rng.standard_normal((R, D)).astype(np.float32)
+    # AdagradDecay, decay_step 2: rows decay on global_step + 1 = 2, 4, ...
+    tab = dr.DenseTable(T(w0.copy()))
+    opt = dr.AdagradDecayOptimizer(0.2, initial_accumulator_value=0.1,
+                                   accumulator_decay_step=2, accumulator_decay_rate=0.5)
+    w, acc, pw = w0.astype(np.float64), np.full((R, D), 0.1), np.zeros(R, np.int64)
+    for step in range(4):
+        idx = np.sort(rng.choice(R, 8, replace=False)).astype(np.int64)
+        g = rng.standard_normal((8, D)).astype(np.float32)
+        tab.pending_grads.append(dr.IndexedSlices(T(g), T(idx)))
+        opt.apply_gradients([tab], global_step=step)
+        gs = step + 1
+        for j, r in enumerate(idx):
+            if gs // 2 > pw[r]:
+                acc[r] = np.maximum(acc[r] * 0.5, 0.1)
+                pw[r] += 1
+            acc[r] = acc[r] + g[j].astype(np.float64) ** 2
+            w[r] = w[r] - 0.2 * g[j] / np.sqrt(acc[r])
+    np.testing.assert_allclose(tab.weight.cpu().numpy(), w, rtol=1e-5, atol=1e-6)
+    # AdamAsync on a dense table
+    tab2 = dr.DenseTable(T(w0.copy()))
+    opt2 = dr.AdamAsyncOptimizer(0.05)
+    w, m, v = w0.astype(np.float64), np.zeros((R, D)), np.zeros((R, D))
+    b1p, b2p = 0.9, 0.999
+    for step in range(3):
+        idx = np.sort(rng.choice(R, 8, replace=False)).astype(np.int64)
+        g = rng.standard_normal((8, D)).astype(np.float32).astype(np.float64)
+        tab2.pending_grads.append(dr.IndexedSlices(T(g.astype(np.float32)), T(idx)))
+        opt2.apply_gradients([tab2], global_step=step)
+        alpha = 0.05 * np.sqrt(1 - b2p) / (1 - b1p)
+        m[idx] = m[idx] * 0.9 + g * 0.1
+        v[idx] = v[idx] * 0.999 + g * g * 0.001
+        w[idx] = w[idx] - alpha * m[idx] / (np.sqrt(v[idx]) + 1e-8)
+        b1p, b2p = b1p * 0.9, b2p * 0.999
+    np.testing.assert_allclose(tab2.weight.cpu().numpy(), w, rtol=1e-4, atol=1e-5)
