@@ -184,13 +184,14 @@ def deepfm_leg(args, dev, log):
         ev.insert_synthetic(0, R, seed=5000 + t)
         evs.append(ev)
     batches = make_batches(4, T, B, R, 0.0, 77, dev)
+    recs = [ids.t().contiguous() for ids in batches]      # record-major [B, T], as main()
     seg = torch.arange(B, dtype=torch.int32, device=dev)
     # the kernel's own launches over the four batches in rotation (as main())
     import ctypes as _C
     L = _lib.lib()
     with torch.no_grad():
-        kfeats = [[_Feature(evs[t], ids[t], seg, B, None, "sum", None, onehot=True)
-                   for t in range(T)] for ids in batches]
+        kfeats = [[_Feature(evs[t], r[:, t], seg, B, None, "sum", None, onehot=True)
+                   for t in range(T)] for r in recs]
         for fs in kfeats:
             _fused_onehot(fs, _lib.ORDER_ALI)
         torch.cuda.synchronize()
@@ -373,13 +374,20 @@ def main():
     ind = torch.stack([torch.arange(B, device=dev), torch.zeros(B, dtype=torch.int64, device=dev)], 1)
     static_ids = torch.empty((T, B), dtype=torch.int64, device=dev)
     # the id batches are resident in HBM (value counts no host->device input
-    # traffic); step k reads batch k % 4 in place
+    # traffic); step k reads batch k % 4 in place.  At N = 1 a batch is a
+    # record-major [B, T] id matrix (one Criteo record of T categorical ids
+    # per row, the SOK/DLRM Criteo-TB input) whose columns are the features'
+    # SparseTensor values: the fused lookup reads it in place
+    # (dr_ev_lookup_onehot_strided).  The training step and the sharded
+    # engines take the feature-major [T, B] form.
+    recs = [ids.t().contiguous() for ids in batches]
     batch_sps = [[SparseTensor(ind, ids[t], (B, 1)) for t in range(T)] for ids in batches]
+    rec_sps = [[SparseTensor(ind, r[:, t], (B, 1)) for t in range(T)] for r in recs]
 
     def step(k):
         if engine is not None:
             return engine.forward(batches[k])
-        return dr.embedding_lookup_sparse_multi(evs, batch_sps[k], combiner="sum")
+        return dr.embedding_lookup_sparse_multi(evs, rec_sps[k], combiner="sum")
 
     NBATCH = len(batches)
     torch.cuda.synchronize()
@@ -591,8 +599,9 @@ def main():
         return tot.value / cnt.value
 
     own = [((batches[k] % R) * world + rank).contiguous() for k in range(len(batches))]
+    own_rec = [o.t().contiguous() for o in own]           # record-major, as the steps
     with torch.no_grad():
-        kfeats = [[_Feature(evs[t], own[k][t], seg, B, None, "sum", None, onehot=True)
+        kfeats = [[_Feature(evs[t], own_rec[k][:, t], seg, B, None, "sum", None, onehot=True)
                    for t in range(T)] for k in range(len(own))]
         for fs in kfeats:
             assert _fused_onehot(fs, _lib.ORDER_ALI) is not None
@@ -633,18 +642,26 @@ def main():
     achieved = bytes_launch / (k_ms * 1e-3) / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
-            "kernel": "dr::ev_lookup_onehot_kernel<4,32,1,ALI,4>",
+            "kernel": "dr::ev_lookup_onehot_kernel<4,32,1,ALI,4> (record-major [B, T] ids)",
             "kernel_ms": round(k_ms, 4),
             "bytes_per_launch": bytes_launch, "bytes_per_lookup": per_lookup}
-    for obj, fname, kname in ((roof, "r02_pmc_traffic.json", "ev_lookup_onehot_kernel"),
-                              (roof_gather, "r02_pmc_traffic_row_gather.json",
+    import glob as _glob
+
+    def _latest(suffix):
+        fs = sorted(_glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_" + suffix)))
+        return fs[-1] if fs else None
+
+    for obj, fname, kname in ((roof, _latest("pmc_traffic.json"), "ev_lookup_onehot_kernel"),
+                              (roof_gather, _latest("pmc_traffic_row_gather.json"),
                                "pool_onehot_kernel")):
-        pmc = os.path.join(ROOT, "profiles", fname)
-        if os.path.exists(pmc):
+        if fname:
             try:
-                j = json.load(open(pmc))
-                if j.get("kernel") == kname:  # PMC of this same kernel only
+                j = json.load(open(fname))
+                # PMC of this same kernel only (rocprof names the template
+                # instantiation, e.g. "ev_lookup_onehot_kernel<4, 32, 1, 0, 4>")
+                if str(j.get("kernel", "")).startswith(kname):
                     obj["traffic"] = j.get("bytes_per_launch")
+                    obj["traffic_source"] = os.path.relpath(fname, ROOT)
             except Exception:
                 pass
 

@@ -696,6 +696,11 @@ struct ApplyTable {
   const int64_t* n_dev;
   int64_t steps_to_live;
   const int64_t* rows;  // known rows of the keys (SGD of a row-grouped backward) or nullptr
+  // AdamAsync: this variable's device-resident {beta1_power, beta2_power}
+  // (the reference keeps them in an EV of their own, training_ali_ops.cc
+  // :1523-1526); alpha is formed from them in the kernel, and
+  // ev_adam_powers_kernel advances them after the apply when N > 0
+  const float* powers;
 };
 static constexpr int kApplyGroup = 16;  // keeps the kernel arguments < 4 KiB
 struct ApplyGroup {
@@ -801,8 +806,15 @@ __device__ __forceinline__ V apply_grad_load(uint64_t a, int64_t c) {
 
 template <int OPT, int VEC, int G>
 __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t dim, int64_t gs,
-                                                       OptScalars sc, int gind, int* st) {
+                                                       OptScalars sc_arg, int gind, int* st) {
   const ApplyTable& at = ag.t[blockIdx.y];
+  OptScalars sc = sc_arg;
+  if (OPT == OPT_ADAM_ASYNC && at.powers) {
+    // alpha = lr * sqrt(1 - beta2_power) / (1 - beta1_power) in T = float
+    // (training_ali_ops.cc:1529-1531), from the powers as they stand
+    const float b1p = gld(at.powers), b2p = gld(at.powers + 1);
+    sc.alpha = sc.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
+  }
   const ApplyCols& cols = at.cols;
   const float* __restrict__ grad = at.grad;
   const int lane = threadIdx.x & 63;
@@ -1363,12 +1375,30 @@ static int resolve_grouped(dr_ev* const* evs, int T, const int64_t* keys, const 
   return DR_OK;
 }
 
+// AdamAsync beta powers, after the apply (training_ali_ops.cc:1558-1559):
+// beta1_power *= beta1, beta2_power *= beta2 -- only for tables whose
+// gradient had rows (the op's `if (N > 0)`, :1482; N = the device count when
+// one is given, so a fixed-capacity slice with no valid row leaves them).
+struct PowersArgs {
+  float* p[DR_MAX_GROUP];
+  int64_t n[DR_MAX_GROUP];
+  const int64_t* n_dev[DR_MAX_GROUP];
+};
+__global__ void ev_adam_powers_kernel(PowersArgs a, int T, float beta1, float beta2) {
+  const int t = threadIdx.x;
+  if (t >= T || !a.p[t]) return;
+  if (eff_n(a.n[t], a.n_dev[t]) <= 0) return;
+  a.p[t][0] = a.p[t][0] * beta1;
+  a.p[t][1] = a.p[t][1] * beta2;
+}
+
 // Grouped sparse apply: T tables (same dim) per launch, blockIdx.y = table,
 // in chunks of kApplyGroup.  A single-table apply is a group of one.
 static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* const* s2, int T,
                          OptScalars sc, const float* const* grads, const int64_t* const* keys,
                          const int64_t* n_host, const int64_t* const* n_dev, int64_t gs,
-                         hipStream_t st, int gind = 0, const int64_t* const* rows = nullptr) {
+                         hipStream_t st, int gind = 0, const int64_t* const* rows = nullptr,
+                         float* const* powers = nullptr) {
   DR_REQUIRE(!rows || opt == OPT_SGD, DR_INVALID_ARGUMENT,
              "known rows skip the slot-column first-touch check: SGD only");
   DR_REQUIRE(T >= 1 && vars && grads && keys && n_host, DR_INVALID_ARGUMENT, "bad argument");
@@ -1425,6 +1455,7 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
                    "table %d: known rows need a filter-free EV and a rows array", t);
         a.rows = rows[t];
       }
+      if (powers) a.powers = powers[t];
       nmax = std::max(nmax, a.n);
     }
     if (nmax == 0) continue;
@@ -1465,6 +1496,21 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
       DR_APPLY(1, 64);
 #undef DR_APPLY
     DR_LAUNCH_CHECK();
+  }
+  if (powers) {
+    for (int c0 = 0; c0 < T; c0 += DR_MAX_GROUP) {
+      const int tn = std::min(DR_MAX_GROUP, T - c0);
+      PowersArgs pa;
+      memset(&pa, 0, sizeof(pa));
+      for (int j = 0; j < tn; ++j) {
+        pa.p[j] = powers[c0 + j];
+        pa.n[j] = n_host[c0 + j];
+        pa.n_dev[j] = n_dev ? n_dev[c0 + j] : nullptr;
+      }
+      hipLaunchKernelGGL(ev_adam_powers_kernel, dim3(1), dim3(64), 0, st, pa, tn, sc.beta1,
+                         sc.beta2);
+      DR_LAUNCH_CHECK();
+    }
   }
   // no counter mirror here: the step's next resolve refreshes it
   return DR_OK;
@@ -1526,7 +1572,8 @@ struct LkDesc {
 
 struct LookupArgs {
   LkDesc d[DR_MAX_GROUP];
-  const int64_t* keys;  // [T, B]
+  const int64_t* keys;  // id of (bag b, table t) = keys[b * ksb + t * kst]
+  int64_t ksb, kst;     // [T, B] feature-major: (1, B); [B, T] record-major: (T, 1)
   float* out;
   int64_t out_stride;
   int64_t* rows;        // [T, B] row served per id (-1: default), or nullptr
@@ -1581,7 +1628,7 @@ __global__ __launch_bounds__(256) void ev_lookup_onehot_kernel(LookupArgs a, int
     const int64_t b = (int64_t)((uint32_t)s / (uint32_t)T);  // slots < 2^31 (host check)
     const int t = (int)(s - b * T);
     const LkDesc& e = sd[t];
-    const int64_t row = ev_probe_row(e, (uint64_t)a.keys[(int64_t)t * B + b]);
+    const int64_t row = ev_probe_row(e, (uint64_t)gld(a.keys + b * a.ksb + (int64_t)t * a.kst));
     if (row >= 0) {
       mine = e.pool + row * (int64_t)dim;
       if (a.rows) a.rows[(int64_t)t * B + b] = row;
@@ -1639,6 +1686,7 @@ struct MissArgs {
   int64_t* mtop[DR_MAX_GROUP];  // row counters to mirror (nullptr: none)
   int64_t* mdst[DR_MAX_GROUP];
   const int64_t* keys;
+  int64_t ksb, kst;
   float* out;
   int64_t out_stride;
   int64_t* rows;
@@ -1690,7 +1738,8 @@ __global__ __launch_bounds__(256) void ev_miss_kernel(MissArgs a, int T, int64_t
     const EvDesc& e = a.e[t];
     bool created;
     uint64_t rc;
-    Slot* sl = ev_find(e, (uint64_t)a.keys[(int64_t)t * B + b], true, &created, &rc, st);
+    Slot* sl = ev_find(e, (uint64_t)a.keys[b * a.ksb + (int64_t)t * a.kst], true, &created, &rc,
+                       st);
     uint8_t claim = 0;
     int64_t row = -1;
     if (sl && (rc & kRowMask) != kRowDead) {
@@ -1787,11 +1836,12 @@ static void launch_lookup_onehot(const LookupArgs& a, int T, int64_t B, int dim,
     launch_lookup_nb<VEC, G, CPL, ORDER, 4>(a, T, B, dim, w, st);
 }
 
-static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t B, float* out,
-                         int64_t out_stride, int order, int64_t* rows_out, void* ws,
-                         size_t ws_bytes, hipStream_t st) {
+static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t ksb, int64_t kst,
+                         int64_t B, float* out, int64_t out_stride, int order, int64_t* rows_out,
+                         void* ws, size_t ws_bytes, hipStream_t st) {
   DR_REQUIRE(evs && T >= 1 && T <= DR_MAX_GROUP && B >= 0 && out_stride >= 0, DR_INVALID_ARGUMENT,
              "bad argument");
+  DR_REQUIRE(ksb >= 0 && kst >= 0, DR_INVALID_ARGUMENT, "key strides must be >= 0");
   DR_REQUIRE(order == DR_ORDER_ALI || order == DR_ORDER_SEQ, DR_INVALID_ARGUMENT, "bad order");
   const int64_t n = (int64_t)T * B;
   DR_REQUIRE(n < (1ll << 31), DR_INVALID_ARGUMENT, "T*B must be < 2^31");
@@ -1840,6 +1890,8 @@ static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t 
     ma.dflt[t] = s->defaults[evs[t]->col];
   }
   la.keys = ma.keys = keys;
+  la.ksb = ma.ksb = ksb;
+  la.kst = ma.kst = kst;
   la.rows = ma.rows = rows_out;
   la.out = ma.out = out;
   la.out_stride = ma.out_stride = out_stride;
@@ -2013,6 +2065,8 @@ int64_t dr_ev_dim(dr_ev* ev) { return ev ? ev->sh->dim / ev->sh->value_words : -
 
 int64_t dr_ev_row_capacity(dr_ev* ev) { return ev ? ev->sh->row_cap : -1; }
 
+int64_t dr_ev_filter_freq(dr_ev* ev) { return ev ? ev->sh->filter_freq : -1; }
+
 int dr_ev_value_bits(dr_ev* ev) { return ev ? 32 * ev->sh->value_words : -1; }
 
 // MaybeLockEmbeddingVariableInputMutexesInOrder (training_ali_op_helpers.h:
@@ -2170,8 +2224,16 @@ size_t dr_ev_lookup_onehot_workspace_size(int num_tables, int64_t batch) {
 int dr_ev_lookup_onehot(dr_ev* const* evs, int num_tables, const int64_t* keys, int64_t batch,
                         float* out, int64_t out_stride, int order, void* ws, size_t ws_bytes,
                         void* stream) {
-  return dr::lookup_onehot(evs, num_tables, keys, batch, out, out_stride, order, nullptr, ws,
-                           ws_bytes, dr::S(stream));
+  return dr::lookup_onehot(evs, num_tables, keys, 1, batch, batch, out, out_stride, order, nullptr,
+                           ws, ws_bytes, dr::S(stream));
+}
+
+int dr_ev_lookup_onehot_strided(dr_ev* const* evs, int num_tables, const int64_t* keys,
+                                int64_t key_stride_bag, int64_t key_stride_table, int64_t batch,
+                                float* out, int64_t out_stride, int order, int64_t* rows_out,
+                                void* ws, size_t ws_bytes, void* stream) {
+  return dr::lookup_onehot(evs, num_tables, keys, key_stride_bag, key_stride_table, batch, out,
+                           out_stride, order, rows_out, ws, ws_bytes, dr::S(stream));
 }
 
 int dr_ev_lookup_onehot_rows(dr_ev* const* evs, int num_tables, const int64_t* keys,
@@ -2181,8 +2243,8 @@ int dr_ev_lookup_onehot_rows(dr_ev* const* evs, int num_tables, const int64_t* k
     dr::set_error("rows_out is required");
     return DR_INVALID_ARGUMENT;
   }
-  return dr::lookup_onehot(evs, num_tables, keys, batch, out, out_stride, order, rows_out, ws,
-                           ws_bytes, dr::S(stream));
+  return dr::lookup_onehot(evs, num_tables, keys, 1, batch, batch, out, out_stride, order,
+                           rows_out, ws, ws_bytes, dr::S(stream));
 }
 
 // Tagged resolve: keys of all T tables in one array, table of key i =
@@ -2481,6 +2543,31 @@ int dr_ev_apply_grouped(int optimizer, dr_ev* const* vars, dr_ev* const* slot1,
   if (rc) return rc;
   return apply_grouped(opt, vars, slot1, slot2, num_tables, sc, grads, keys, n_host, n_dev,
                        global_step, S(stream));
+}
+
+int dr_ev_apply_adam_async_grouped(int rmsprop, int by_address, dr_ev* const* vars,
+                                   dr_ev* const* m, dr_ev* const* v, int num_tables,
+                                   const void* const* grads, const int64_t* const* keys,
+                                   const int64_t* n_host, const int64_t* const* n_dev,
+                                   float* const* powers, float lr, float beta1, float beta2,
+                                   float epsilon, int64_t global_step, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(grads && (rmsprop || powers), DR_INVALID_ARGUMENT,
+             "bad argument (AdamAsync needs the device beta powers)");
+  DR_REQUIRE(num_tables >= 1, DR_INVALID_ARGUMENT, "num_tables must be >= 1");
+  if (!rmsprop)
+    for (int t = 0; t < num_tables; ++t)
+      DR_REQUIRE(powers[t] && ((uintptr_t)powers[t] & 3) == 0, DR_INVALID_ARGUMENT,
+                 "table %d: powers must be a device float[2]", t);
+  int opt;
+  OptScalars sc;
+  int rc = grouped_opt(rmsprop ? DR_OPT_ADAM_ASYNC_RMSPROP : DR_OPT_ADAM_ASYNC, lr, 0.f, 0.f,
+                       beta1, beta2, epsilon, &opt, &sc);
+  if (rc) return rc;
+  return apply_grouped(opt, vars, m, v, num_tables, sc,
+                       reinterpret_cast<const float* const*>(grads), keys, n_host, n_dev,
+                       global_step, S(stream), by_address ? 1 : 0, nullptr,
+                       rmsprop ? nullptr : powers);
 }
 
 int dr_ev_apply_grouped_ptr(int optimizer, dr_ev* const* vars, dr_ev* const* slot1,

@@ -440,10 +440,11 @@ __global__ void bag_offsets_kernel(const TI* __restrict__ seg, int64_t stride, i
   }
   if (k == ne) return;
   int64_t s = (int64_t)seg[k * stride];
-  const int64_t prev = k > 0 ? (int64_t)seg[(k - 1) * stride] : -1;
+  int64_t prev = k > 0 ? (int64_t)seg[(k - 1) * stride] : -1;
   if (s < prev || s < 0 || s >= B) {
     latch(st, DR_INVALID_ARGUMENT);
     s = s < 0 ? 0 : (s >= B ? B - 1 : s);
+    prev = prev < -1 ? -1 : (prev >= B ? B - 1 : prev);  // keep the window in [0, B]
     if (s < prev) return;
   }
   for (int64_t r = prev + 1; r <= s; ++r) off[r] = (int32_t)k;
@@ -473,15 +474,25 @@ __global__ void bag_offsets_grouped_kernel(BagGroup g, int64_t B, int* st) {
   }
   if (k == ne) return;
   int64_t s = seg[k * stride];
-  const int64_t prev = k > 0 ? seg[(k - 1) * stride] : -1;
+  int64_t prev = k > 0 ? seg[(k - 1) * stride] : -1;
   if (s < prev || s < 0 || s >= B) {
     latch(st, DR_INVALID_ARGUMENT);
     s = s < 0 ? 0 : (s >= B ? B - 1 : s);
+    // an out-of-range predecessor must not move the write window outside
+    // [0, B] (seg = [-5, 0] would otherwise write off[-4..0])
+    prev = prev < -1 ? -1 : (prev >= B ? B - 1 : prev);
     if (s < prev) return;
   }
   for (int64_t r = prev + 1; r <= s; ++r) off[r] = (int32_t)k;
   if (k == ne - 1)
     for (int64_t r = s + 1; r <= B; ++r) off[r] = (int32_t)ne;
+}
+
+// Zero-fill of every table's offsets ahead of bag_offsets_grouped_kernel
+// (see launch_bag_offsets: positions skipped for bad input leave no garbage).
+__global__ void bag_zero_grouped_kernel(BagGroup g, int64_t B) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r <= B) g.off[blockIdx.y][r] = 0;
 }
 
 // rowsel[i] = rows[koff[t] + idx[i]] for i in feature t: the EV row of every
@@ -499,11 +510,21 @@ __global__ void rows_per_nnz_kernel(KoffGroup g, int T, const int64_t* __restric
   rowsel[i] = rows[g.koff[t] + idx[i]];
 }
 
+// Caller-supplied segment ids may be unsorted or out of range: the kernel
+// latches INVALID_ARGUMENT, but the positions it skips would leave entries
+// of `off` unwritten, and a pool launched behind it (no host sync in
+// between) would follow garbage offsets.  So `off` is zero-filled first:
+// every entry then lies in [0, n] and a bad bag reads as empty or as a
+// range of valid positions.  Internal, sorted-by-construction keys skip it.
 template <class TI>
 static int launch_bag_offsets(const TI* seg, int64_t stride, int64_t n, const int64_t* n_dev,
-                              int64_t B, int32_t* off, hipStream_t s) {
+                              int64_t B, int32_t* off, hipStream_t s, bool trusted = false) {
   int* st = status_word();
   DR_REQUIRE(st, DR_INTERNAL, "status word unavailable");
+  if (!trusted) {
+    int rc = fill_bytes(off, 0, (size_t)(B + 1) * sizeof(int32_t), s);
+    if (rc) return rc;
+  }
   const unsigned blocks = (unsigned)ceil_div(n + 1, 256);
   hipLaunchKernelGGL(bag_offsets_kernel<TI>, dim3(blocks), dim3(256), 0, s, seg, stride, n, n_dev,
                      B, off, st);
@@ -809,7 +830,7 @@ static int segsum_driver(const int32_t* keyseg, int64_t n, int64_t num_out, cons
                          w.sort_bytes, s);
   if (rc) return rc;
   // offsets over num_out + 1 buckets (the last one collects skipped positions)
-  rc = launch_bag_offsets<uint64_t>(w.kout, 1, n, nullptr, num_out + 1, w.off, s);
+  rc = launch_bag_offsets<uint64_t>(w.kout, 1, n, nullptr, num_out + 1, w.off, s, true);
   if (rc) return rc;
   return dispatch_csr_sum(src, src_stride, src_rows, w.perm, seg_of_pos, w.off, bag_off, num_out,
                           U_dev, dim, mode, out, s, st);
@@ -1339,6 +1360,9 @@ int dr_bag_offsets_grouped(const int64_t* const* seg, const int64_t* stride,
     g.off[t] = bag_off[t];
     mx = n[t] > mx ? n[t] : mx;
   }
+  hipLaunchKernelGGL(bag_zero_grouped_kernel, dim3((unsigned)ceil_div(batch + 1, 256),
+                                                   (unsigned)num_tables), dim3(256), 0,
+                     S(stream), g, batch);
   dim3 grid((unsigned)ceil_div(mx + 1, 256), (unsigned)num_tables);
   hipLaunchKernelGGL(bag_offsets_grouped_kernel, grid, dim3(256), 0, S(stream), g, batch, st);
   DR_LAUNCH_CHECK();
@@ -1364,6 +1388,13 @@ int dr_rows_per_nnz(const int64_t* rows, const int32_t* idx, const int64_t* koff
 int dr_bag_offsets_strided(const int64_t* seg, int64_t stride, int64_t n, int64_t batch,
                            int32_t* bag_off, void* stream) {
   return dr::launch_bag_offsets<int64_t>(seg, stride, n, nullptr, batch, bag_off, dr::S(stream));
+}
+
+int dr_bag_offsets_strided_dev(const int64_t* seg, int64_t stride, int64_t n_cap,
+                               const int64_t* n_dev, int64_t batch, int32_t* bag_off,
+                               void* stream) {
+  return dr::launch_bag_offsets<int64_t>(seg, stride, n_cap, n_dev, batch, bag_off,
+                                         dr::S(stream));
 }
 
 int dr_gather(const float* table, int64_t rows, int64_t dim, const int64_t* ids, int64_t n,

@@ -351,7 +351,22 @@ int dr_ipc_alloc(size_t bytes, void** ptr_out) {
       u.free.erase(it);
     }
   }
-  if (!p) {
+  if (p) {
+    // Reuse is ordered after every stream's work issued before the free:
+    // dr_ipc_free runs from a DLPack deleter as soon as the framework drops
+    // the tensor, while kernels on its (non-blocking) streams may still read
+    // or write the buffer.  A device-wide sync here (allocation time only)
+    // covers all of them.  Peer GPUs' writes are the caller's contract: every
+    // peer closes its IPC mapping (after a barrier) before the owner frees.
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+      UcFree& u = uc_pool();
+      std::lock_guard<std::mutex> g(u.mu);
+      u.free.insert({{dev, n}, p});
+      set_error("dr_ipc_alloc: %s", hipGetErrorString(e));
+      return DR_INTERNAL;
+    }
+  } else {
     DR_HIP(hipExtMallocWithFlags(&p, n, hipDeviceMallocUncached));
     UcFree& u = uc_pool();
     std::lock_guard<std::mutex> g(u.mu);
@@ -373,6 +388,9 @@ int dr_ipc_alloc(size_t bytes, void** ptr_out) {
   return DR_OK;
 }
 
+// Returns the buffer to the uncached free list (never to hipFree, see
+// above).  Cheap and safe to call from a DLPack deleter: the next
+// dr_ipc_alloc that reuses it synchronises the device first.
 int dr_ipc_free(void* ptr) {
   using namespace dr;
   if (!ptr) return DR_OK;
@@ -438,7 +456,7 @@ int dr_ipc_alloc_dlpack(int ndim, const int64_t* shape, int dtype_code, int dtyp
   if (rc) return rc;
   DlManaged* m = static_cast<DlManaged*>(calloc(1, sizeof(DlManaged)));
   if (!m) {
-    (void)hipFree(p);
+    (void)dr_ipc_free(p);  // uncached blocks never go back to hipFree
     set_error("dr_ipc_alloc_dlpack: out of host memory");
     return DR_RESOURCE_EXHAUSTED;
   }

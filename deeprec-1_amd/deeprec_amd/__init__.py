@@ -14,7 +14,8 @@ from .embedding_ops import (DenseTable, SparseTensor, embedding_lookup, embeddin
                             embedding_lookup_sparse_multi, fused_embedding_lookup_sparse,
                             safe_embedding_lookup_sparse)
 from .kv_variable_ops import (CBFFilter, CounterFilter, EmbeddingVariable, EmbeddingVariableOption,
-                              GlobalStepEvict, IndexedSlices, get_embedding_variable)
+                              GlobalStepEvict, IndexedSlices, flush_releases,
+                              get_embedding_variable)
 from .ops import set_validate, status_check
 from .string_ops import StringTensor, string_to_hash_bucket_fast
 from .training import (AdagradDecayOptimizer, AdagradOptimizer, AdamAsyncOptimizer, AdamOptimizer,

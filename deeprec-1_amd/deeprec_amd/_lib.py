@@ -108,6 +108,7 @@ SIGNATURES = {
     "dr_bag_offsets": (_I32, [_P, _I64, _I64, _P, _P]),
     "dr_bag_offsets_i32": (_I32, [_P, _I64, _I64, _P, _P]),
     "dr_bag_offsets_strided": (_I32, [_P, _I64, _I64, _I64, _P, _P]),
+    "dr_bag_offsets_strided_dev": (_I32, [_P, _I64, _I64, _P, _I64, _P, _P]),
     "dr_bag_offsets_grouped": (_I32, [_P, _P, _P, _I32, _I64, _P, _P]),
     "dr_rows_per_nnz": (_I32, [_P, _P, _P, _I32, _P, _P]),
     "dr_pool_grad_workspace_size": (_SZ, [_I64]),
@@ -126,6 +127,10 @@ SIGNATURES = {
     "dr_ev_release": (_I32, [_P]),
     "dr_ev_size": (_I32, [_P, _P, _P]),
     "dr_ev_dim": (_I64, [_P]),
+    "dr_ev_filter_freq": (_I64, [_P]),
+    "dr_embedding_lookup_sparse_workspace_size": (_SZ, [_I64, _I64]),
+    "dr_embedding_lookup_sparse": (_I32, [_P, _P, _I64, _I32, _P, _P, _P, _I64, _I64, _I32, _F32,
+                                          _I32, _I64, _I32, _P, _I64, _P, _SZ, _P]),
     "dr_ev_row_capacity": (_I64, [_P]),
     "dr_ev_value_bits": (_I32, [_P]),
     "dr_ev_lock_updates": (_I32, [_P, _I32, _P]),
@@ -144,6 +149,8 @@ SIGNATURES = {
     "dr_ev_lookup_onehot_workspace_size": (_SZ, [_I32, _I64]),
     "dr_ev_lookup_onehot": (_I32, [_P, _I32, _P, _I64, _P, _I64, _I32, _P, _SZ, _P]),
     "dr_ev_lookup_onehot_rows": (_I32, [_P, _I32, _P, _I64, _P, _I64, _I32, _P, _P, _SZ, _P]),
+    "dr_ev_lookup_onehot_strided": (_I32, [_P, _I32, _P, _I64, _I64, _I64, _P, _I64, _I32, _P, _P,
+                                           _SZ, _P]),
     "dr_ev_resolve_tagged": (_I32, [_P, _I32, _P, _P, _I64, _P, _P, _P, _P, _P, _SZ, _P]),
     "dr_ev_gather_tagged": (_I32, [_P, _I32, _P, _P, _I64, _P, _P, _P]),
     "dr_ev_pool": (_P, [_P]),
@@ -163,6 +170,8 @@ SIGNATURES = {
     "dr_ev_apply_grouped_ptr": (_I32, [_I32, _P, _P, _P, _I32, _P, _P, _P, _P, _F32, _F32, _F32,
                                        _F32, _F32, _F32, _I64, _P]),
     "dr_ev_apply_grouped_ptr_rows": (_I32, [_I32, _P, _I32, _P, _P, _P, _P, _P, _F32, _I64, _P]),
+    "dr_ev_apply_adam_async_grouped": (_I32, [_I32, _I32, _P, _P, _P, _I32, _P, _P, _P, _P, _P,
+                                              _F32, _F32, _F32, _F32, _I64, _P]),
     "dr_ev_apply_adagrad_decay_grouped": (_I32, [_P, _P, _P, _I32, _P, _I32, _P, _P, _P, _F32,
                                                  _I64, _F32, _F32, _I64, _P]),
     "dr_ev_apply_ftrl_grouped_ptr": (_I32, [_P, _P, _P, _I32, _P, _P, _P, _P, _F32, _F32, _F32,

@@ -91,7 +91,11 @@ class _Feature(object):
         self.onehot = bool(onehot) and weights is None and max_norm is None
         self.bag_off = None
         self.group = None
-        self.values = values
+        # ids as given: possibly a strided view (a column of a record-major
+        # [B, T] id matrix), read in place by the fused one-hot lookup;
+        # `values` is the contiguous vector every other kernel takes
+        self.raw_values = values
+        self._values = values if values.is_contiguous() else None
         if seg.dim() == 2:
             self.seg64, self.seg_stride = seg.contiguous(), seg.shape[1]
         elif seg.dtype == torch.int64:
@@ -105,6 +109,12 @@ class _Feature(object):
         self.max_norm = max_norm
         self.uniq = self.idx = self.U = self.rows = self.rowsel = None
         self.defaults = None
+
+    @property
+    def values(self):
+        if self._values is None:
+            self._values = self.raw_values.contiguous()
+        return self._values
 
     @property
     def seg(self):
@@ -577,9 +587,26 @@ def _fused_onehot_ok(feats):
         p = f.params
         if not (isinstance(p, EmbeddingVariable) and f.onehot and f.batch == B
                 and p.dim == D and p.device == p0.device and p.filter_freq == 0
-                and not callable(p.initializer) and f.values.numel() == B):
+                and not callable(p.initializer) and f.raw_values.numel() == B):
             return False
     return D % 4 == 0 and D <= 256 and len(feats) * B < (1 << 31)
+
+
+def _record_major(feats):
+    """Base address of a record-major [B, T] int64 id matrix whose column t
+    is feature t's ids (SparseTensor values = ids[:, t], e.g. a Criteo
+    record batch of 26 categorical ids per sample), else None."""
+    T = len(feats)
+    v0 = feats[0].raw_values
+    if T < 2 or v0.dtype != torch.int64 or v0.dim() != 1 or v0.stride(0) != T:
+        return None
+    st = v0.untyped_storage().data_ptr()
+    for t, f in enumerate(feats):
+        v = f.raw_values
+        if (v.dtype != torch.int64 or v.dim() != 1 or v.stride(0) != T
+                or v.untyped_storage().data_ptr() != st or v.data_ptr() != v0.data_ptr() + 8 * t):
+            return None
+    return v0.data_ptr()
 
 
 def _fused_onehot(feats, order, with_rows=False):
@@ -595,13 +622,21 @@ def _fused_onehot(feats, order, with_rows=False):
     B = feats[0].batch
     D = p0.dim
     T = len(feats)
-    dev = feats[0].values.device
+    dev = feats[0].raw_values.device
     koff = [t * B for t in range(T + 1)]
-    vals = _concat_values(feats, koff)
     out = torch.empty((B, T * D), dtype=torch.float32, device=dev)
     handles = (C.c_void_p * T)(*[f.params.handle.value for f in feats])
     wsb = lib().dr_ev_lookup_onehot_workspace_size(T, B)
     ws = workspace(wsb, dev)
+    rec = None if with_rows else _record_major(feats)
+    if rec is not None:
+        # the features are the columns of one record-major [B, T] id matrix:
+        # read in place, in the kernel's (b, t) visiting order
+        check(lib().dr_ev_lookup_onehot_strided(handles, T, rec, T, 1, B, ptr(out), T * D, order,
+                                                None, ptr(ws), wsb, stream_handle(dev)))
+        ops._post(dev)
+        return out
+    vals = _concat_values(feats, koff)
     if with_rows:
         rowsel = torch.empty(T * B, dtype=torch.int64, device=dev)
         check(lib().dr_ev_lookup_onehot_rows(handles, T, ptr(vals), B, ptr(out), T * D, order,
@@ -709,7 +744,7 @@ def embedding_lookup_sparse_multi(params_list, sp_ids_list, combiner="mean", max
     returns the input_layer concatenation [B, sum(D_t)]."""
     feats = []
     for p, sp in zip(params_list, sp_ids_list):
-        v = sp.values.to(torch.int64).contiguous()
+        v = sp.values.to(torch.int64)      # strided views stay views (_record_major)
         feats.append(_Feature(p, v, _seg_of(sp), sp.dense_shape[0], None, combiner, max_norm,
                               onehot=_is_onehot(sp, v.numel())))
     return _run(feats)

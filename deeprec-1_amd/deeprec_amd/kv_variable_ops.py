@@ -6,6 +6,7 @@ the C ABI (dr_ev_*); this module only holds the handle and the Python-level
 argument semantics.
 """
 import ctypes as C
+import atexit
 import threading
 
 import torch
@@ -61,11 +62,15 @@ def _default_row(initializer, dim, device, dtype=torch.float32):
     return v.cpu().contiguous()
 
 
-# Handles whose last Python reference died while a hipGraph was being
-# captured.  Releasing one frees device memory (hipFree) and synchronises,
-# which a capture in torch's default global mode turns into a failed capture;
-# the cyclic garbage of an earlier step can be collected at any allocation
-# inside a captured step, so such releases wait for the next uncaptured one.
+# Handles whose last Python reference died.  Releasing one frees device
+# memory (hipFree) and synchronises, which breaks a hipGraph capture in
+# torch's default global mode if ANY stream of the process is capturing --
+# and __del__ runs on whatever thread triggers the collection, whose own
+# current stream says nothing about another thread's capture.  So __del__
+# never releases: it queues the handle, and the queue is flushed at points
+# where the library itself runs uncaptured host work (EV creation, the end
+# of an optimizer's apply_gradients when its stream is not capturing), by
+# flush_releases(), and at interpreter exit.
 _DEFERRED = []
 _DEFERRED_LOCK = threading.Lock()
 
@@ -84,13 +89,20 @@ def _flush_deferred_releases():
         lib().dr_ev_release(h)
 
 
-def _release_handle(h):
+def flush_releases():
+    """Release the device memory of every EmbeddingVariable that has been
+    garbage-collected (call outside any hipGraph capture)."""
     if _capturing():
-        with _DEFERRED_LOCK:
-            _DEFERRED.append(h)
-        return
+        raise RuntimeError("flush_releases() inside a stream capture")
     _flush_deferred_releases()
-    lib().dr_ev_release(h)
+
+
+def _release_handle(h):
+    with _DEFERRED_LOCK:
+        _DEFERRED.append(h)
+
+
+atexit.register(lambda: _DEFERRED.clear())   # the process is going away: no frees needed
 
 
 _KEY_DTYPES = (torch.int64, torch.int32)
@@ -209,6 +221,17 @@ class EmbeddingVariable(object):
     @property
     def handle(self):
         return self._h
+
+    @property
+    def resource(self):
+        """The EV as an op input (torch_ops): a host int64[1] tensor holding
+        the library handle, TF's DT_RESOURCE scalar (host memory).  Ops that
+        change the EV list it in mutates_args."""
+        r = getattr(self, "_resource", None)
+        if r is None:
+            r = torch.tensor([self._h.value], dtype=torch.int64)
+            self._resource = r
+        return r
 
     def is_primary(self):
         return self._primary is None

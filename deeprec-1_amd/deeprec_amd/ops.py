@@ -275,6 +275,39 @@ def sort_pairs(keys, vals, bit_hi, bit_lo=0):
 
 
 # ---------------------------------------------------------------------------
+# embedding_lookup_sparse / safe_embedding_lookup_sparse through the single
+# C entry dr_embedding_lookup_sparse (embedding_ops.py:480-675, :1209-1344):
+# what a TF custom-op kernel binds.  Forward only.
+# ---------------------------------------------------------------------------
+def embedding_lookup_sparse_c(params, sp_indices, sp_values, batch, sp_weights=None,
+                              combiner="mean", max_norm=None, safe=False, default_id=None,
+                              prune=True):
+    """params: an EmbeddingVariable (handle / dim attributes) or a dense fp32
+    [rows, dim] tensor.  sp_indices [nnz, 2] int64 rows-sorted, sp_values
+    [nnz] int64, sp_weights [nnz] fp32 or None.  Returns [batch, dim]."""
+    ind = sp_indices.to(torch.int64).contiguous()
+    val = sp_values.to(torch.int64).contiguous()
+    w = None if sp_weights is None else sp_weights.to(torch.float32).contiguous()
+    nnz = val.numel()
+    dev = val.device
+    if torch.is_tensor(params):
+        ev, table = None, params.contiguous()
+        rows, dim = table.shape
+    else:
+        ev, table, rows, dim = params.handle, None, 0, params.dim
+    out = torch.empty((batch, dim), dtype=torch.float32, device=dev)
+    wsb = lib().dr_embedding_lookup_sparse_workspace_size(nnz, batch)
+    ws = workspace(wsb, dev)
+    check(lib().dr_embedding_lookup_sparse(
+        ev, ptr(table), rows, dim, ptr(ind), ptr(val), ptr(w), nnz, batch, COMBINERS[combiner],
+        -1.0 if max_norm is None else float(max_norm), 1 if safe else 0,
+        -1 if default_id is None else int(default_id), 1 if prune else 0, ptr(out), dim,
+        ptr(ws), wsb, stream_handle(dev)))
+    _post(dev)
+    return out
+
+
+# ---------------------------------------------------------------------------
 # Fused embedding ops (core/ops/fused_embedding_ops.cc:12-58)
 # ---------------------------------------------------------------------------
 def fused_embedding_local_sparse_look_up(sp_values, sp_indices, sp_dense_shape, emb_variable,

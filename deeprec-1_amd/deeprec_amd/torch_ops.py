@@ -11,8 +11,9 @@ has a fake (meta) implementation so that graphs can be traced / exported
 reference gradients via torch.library.register_autograd.
 
 EmbeddingVariables are resources in the reference (a `resource` handle
-input); here they are passed as the int handle of the library-owned EV
-(EmbeddingVariable.handle.value).  Data-dependent output sizes (Unique,
+input); here they are passed as their resource tensor
+(EmbeddingVariable.resource, a host int64[1] holding the library handle),
+listed in mutates_args by every op that changes the EV.  Data-dependent output sizes (Unique,
 PreLookUp) are returned at their static upper bound plus a device count, as
 dr_unique does, so no op synchronises the host.
 
@@ -158,10 +159,26 @@ resource_gather.register_autograd(_rg_backward, setup_context=_rg_setup)
 
 
 # ---------------------------------------------------------------------------
-# EmbeddingVariable ops (core/ops/kv_variable_ops.cc): handle = EV handle
+# EmbeddingVariable ops (core/ops/kv_variable_ops.cc, training_ali_ops.cc).
+#
+# An EV enters an op as its RESOURCE tensor (EmbeddingVariable.resource: a
+# host int64[1] holding the library handle -- TF's DT_RESOURCE scalar lives
+# in host memory too).  Every op that changes the EV -- the insert-on-miss
+# gather, insert, the sparse applies -- lists that tensor in mutates_args, so
+# functionalization / torch.compile keep such ops, in program order, against
+# every other op on the same EV (a None-returning op with no mutated input
+# could be dead-code eliminated or reordered).  The tensor's value is never
+# changed; it is the dependency token of the resource.
 # ---------------------------------------------------------------------------
-@custom_op(_NS + "::kv_resource_gather", mutates_args=(), device_types="cuda")
-def kv_resource_gather(handle: int, indices: Tensor, dim: int,
+def _hr(resource):
+    """c_void_p EV handle held by a resource tensor."""
+    if resource.device.type != "cpu" or resource.dtype != torch.int64 or resource.numel() != 1:
+        raise ValueError("an EV resource is a host int64[1] tensor (EmbeddingVariable.resource)")
+    return C.c_void_p(int(resource.item()))
+
+
+@custom_op(_NS + "::kv_resource_gather", mutates_args=("resource",), device_types="cuda")
+def kv_resource_gather(resource: Tensor, indices: Tensor, dim: int,
                        default_value: Optional[Tensor] = None,
                        counts: Optional[Tensor] = None) -> Tensor:
     """KvResourceGather[V1] (kv_variable_ops.cc:314-449): rows of `indices`,
@@ -175,19 +192,19 @@ def kv_resource_gather(handle: int, indices: Tensor, dim: int,
         cnt = None if counts is None else counts.reshape(-1).to(torch.int32).contiguous()
         wsb = lib().dr_ev_gather_workspace_size(n)
         ws = workspace(wsb, ids.device)
-        check(lib().dr_ev_gather(_h(handle), ptr(ids), n, ptr(dflt), ptr(cnt), ptr(out), ptr(ws),
-                                 wsb, stream_handle(ids.device)))
+        check(lib().dr_ev_gather(_hr(resource), ptr(ids), n, ptr(dflt), ptr(cnt), ptr(out),
+                                 ptr(ws), wsb, stream_handle(ids.device)))
         ops._post(ids.device)
     return out.reshape(tuple(indices.shape) + (dim,))
 
 
 @kv_resource_gather.register_fake
-def _(handle, indices, dim, default_value=None, counts=None):
+def _(resource, indices, dim, default_value=None, counts=None):
     return indices.new_empty(tuple(indices.shape) + (dim,), dtype=torch.float32)
 
 
-@custom_op(_NS + "::kv_resource_insert", mutates_args=(), device_types="cuda")
-def kv_resource_insert(handle: int, keys: Tensor, values: Tensor,
+@custom_op(_NS + "::kv_resource_insert", mutates_args=("resource",), device_types="cuda")
+def kv_resource_insert(resource: Tensor, keys: Tensor, values: Tensor,
                        versions: Optional[Tensor] = None, freqs: Optional[Tensor] = None,
                        partition_id: int = 0, partition_num: int = 0) -> None:
     """KvResourceInsert / KvResourceImportV2 (Import semantics, optional
@@ -196,7 +213,7 @@ def kv_resource_insert(handle: int, keys: Tensor, values: Tensor,
     v = values.to(torch.float32).contiguous()
     ver = None if versions is None else versions.to(torch.int64).contiguous()
     fr = None if freqs is None else freqs.to(torch.int64).contiguous()
-    check(lib().dr_ev_insert(_h(handle), ptr(k), k.numel(), ptr(v), ptr(ver), ptr(fr),
+    check(lib().dr_ev_insert(_hr(resource), ptr(k), k.numel(), ptr(v), ptr(ver), ptr(fr),
                              int(partition_id), int(partition_num), stream_handle(k.device)))
     ops._post(k.device)
 
@@ -207,87 +224,169 @@ def _apply_common(grad, indices):
     return g, k, k.numel(), stream_handle(k.device)
 
 
-@custom_op(_NS + "::kv_resource_sparse_apply_gradient_descent", mutates_args=(),
+def _one(x):
+    return (C.c_void_p * 1)(x)
+
+
+@custom_op(_NS + "::kv_resource_sparse_apply_gradient_descent", mutates_args=("var",),
            device_types="cuda")
-def kv_resource_sparse_apply_gradient_descent(var: int, alpha: float, grad: Tensor,
-                                              indices: Tensor, global_step: int = -1) -> None:
-    """KvResourceSparseApplyGradientDescent (training_ali_ops.cc:1597-1678)."""
+def kv_resource_sparse_apply_gradient_descent(var: Tensor, alpha: float, grad: Tensor,
+                                              indices: Tensor, global_step: int = -1,
+                                              num_valid: Optional[Tensor] = None) -> None:
+    """KvResourceSparseApplyGradientDescent (training_ali_ops.cc:1597-1678).
+    num_valid: optional DEVICE int64[1] count of the valid leading rows (the
+    IndexedSlices of a Unique with a data-dependent size)."""
     g, k, n, st = _apply_common(grad, indices)
-    check(lib().dr_ev_apply_sgd(_h(var), alpha, ptr(g), ptr(k), n, None, global_step, st))
+    check(lib().dr_ev_apply_sgd(_hr(var), alpha, ptr(g), ptr(k), n, ptr(num_valid), global_step,
+                                st))
     ops._post(k.device)
 
 
-@custom_op(_NS + "::kv_resource_sparse_apply_adagrad", mutates_args=(), device_types="cuda")
-def kv_resource_sparse_apply_adagrad(var: int, accum: int, lr: float, grad: Tensor,
-                                     indices: Tensor, global_step: int = -1) -> None:
+@custom_op(_NS + "::kv_resource_sparse_apply_adagrad", mutates_args=("var", "accum"),
+           device_types="cuda")
+def kv_resource_sparse_apply_adagrad(var: Tensor, accum: Tensor, lr: float, grad: Tensor,
+                                     indices: Tensor, global_step: int = -1,
+                                     num_valid: Optional[Tensor] = None) -> None:
     """KvResourceSparseApplyAdagrad (training_ali_ops.cc:61-145)."""
     g, k, n, st = _apply_common(grad, indices)
-    check(lib().dr_ev_apply_adagrad(_h(var), _h(accum), lr, ptr(g), ptr(k), n, None,
+    check(lib().dr_ev_apply_adagrad(_hr(var), _hr(accum), lr, ptr(g), ptr(k), n, ptr(num_valid),
                                     global_step, st))
     ops._post(k.device)
 
 
-@custom_op(_NS + "::kv_resource_sparse_apply_adam", mutates_args=(), device_types="cuda")
-def kv_resource_sparse_apply_adam(var: int, m: int, v: int, beta1_power: float,
+@custom_op(_NS + "::kv_resource_sparse_apply_adam", mutates_args=("var", "m", "v"),
+           device_types="cuda")
+def kv_resource_sparse_apply_adam(var: Tensor, m: Tensor, v: Tensor, beta1_power: float,
                                   beta2_power: float, lr: float, beta1: float, beta2: float,
                                   epsilon: float, grad: Tensor, indices: Tensor,
-                                  global_step: int = -1) -> None:
+                                  global_step: int = -1,
+                                  num_valid: Optional[Tensor] = None) -> None:
     """KvResourceSparseApplyAdam (training_ali_ops.cc:848-975)."""
     g, k, n, st = _apply_common(grad, indices)
-    check(lib().dr_ev_apply_adam(_h(var), _h(m), _h(v), beta1_power, beta2_power, lr, beta1,
-                                 beta2, epsilon, ptr(g), ptr(k), n, None, global_step, st))
+    check(lib().dr_ev_apply_adam(_hr(var), _hr(m), _hr(v), beta1_power, beta2_power, lr, beta1,
+                                 beta2, epsilon, ptr(g), ptr(k), n, ptr(num_valid), global_step,
+                                 st))
     ops._post(k.device)
 
 
-@custom_op(_NS + "::kv_resource_sparse_apply_ftrl", mutates_args=(), device_types="cuda")
-def kv_resource_sparse_apply_ftrl(var: int, accum: int, linear: int, grad: Tensor,
+@custom_op(_NS + "::kv_resource_sparse_apply_ftrl", mutates_args=("var", "accum", "linear"),
+           device_types="cuda")
+def kv_resource_sparse_apply_ftrl(var: Tensor, accum: Tensor, linear: Tensor, grad: Tensor,
                                   indices: Tensor, lr: float, l1: float, l2: float,
                                   lr_power: float, l2_shrinkage: float = 0.0,
                                   global_step: int = -1) -> None:
     """KvResourceSparseApplyFtrl[V2] (training_ali_ops.cc:167-331)."""
     g, k, n, st = _apply_common(grad, indices)
-    check(lib().dr_ev_apply_ftrl(_h(var), _h(accum), _h(linear), lr, l1, l2, lr_power,
+    check(lib().dr_ev_apply_ftrl(_hr(var), _hr(accum), _hr(linear), lr, l1, l2, lr_power,
                                  l2_shrinkage, ptr(g), ptr(k), n, None, global_step, st))
     ops._post(k.device)
 
 
-def _one(x):
-    import ctypes as C
-    return (C.c_void_p * 1)(x)
-
-
-@custom_op(_NS + "::kv_resource_sparse_apply_adam_async", mutates_args=(), device_types="cuda")
-def kv_resource_sparse_apply_adam_async(var: int, m: int, v: int, beta1_power: float,
-                                        beta2_power: float, lr: float, beta1: float,
-                                        beta2: float, epsilon: float, grad: Tensor,
-                                        indices: Tensor, global_step: int = -1,
-                                        apply_sparse_rmsprop: bool = False) -> None:
-    """KvResourceSparseApplyAdamAsync (training_ali_ops.cc:1404-1575); the
-    beta power slots are the caller's scalars (advanced after the call)."""
-    import ctypes as C
+@custom_op(_NS + "::kv_resource_sparse_apply_adam_async",
+           mutates_args=("var", "m", "v", "beta_powers"), device_types="cuda")
+def kv_resource_sparse_apply_adam_async(var: Tensor, m: Tensor, v: Tensor, beta_powers: Tensor,
+                                        lr: float, beta1: float, beta2: float, epsilon: float,
+                                        grad: Tensor, indices: Tensor, global_step: int = -1,
+                                        apply_sparse_rmsprop: bool = False,
+                                        num_valid: Optional[Tensor] = None) -> None:
+    """KvResourceSparseApplyAdamAsync (training_ali_ops.cc:1404-1575).
+    beta_powers: DEVICE float32[2] {beta1_power, beta2_power} -- the
+    reference's beta power resources (:1523-1526) -- read for alpha and
+    advanced by the op itself when N > 0 (:1482, :1558-1559)."""
     g, k, n, st = _apply_common(grad, indices)
-    opt = 4 if apply_sparse_rmsprop else 3
-    check(lib().dr_ev_apply_grouped(opt, _one(_h(var)), _one(_h(m)), _one(_h(v)), 1,
-                                    _one(g.data_ptr()), _one(k.data_ptr()), (C.c_int64 * 1)(n),
-                                    _one(None), lr, beta1_power, beta2_power, beta1, beta2,
-                                    epsilon, global_step, st))
+    if not apply_sparse_rmsprop and (beta_powers.dtype != torch.float32
+                                     or beta_powers.numel() != 2 or not beta_powers.is_cuda):
+        raise ValueError("beta_powers must be a device float32[2]")
+    check(lib().dr_ev_apply_adam_async_grouped(
+        1 if apply_sparse_rmsprop else 0, 0, _one(_hr(var)), _one(_hr(m)), _one(_hr(v)), 1,
+        _one(g.data_ptr()), _one(k.data_ptr()), (C.c_int64 * 1)(n), _one(ptr(num_valid)),
+        _one(beta_powers.data_ptr()), lr, beta1, beta2, epsilon, global_step, st))
     ops._post(k.device)
 
 
-@custom_op(_NS + "::kv_resource_sparse_apply_adagrad_decay", mutates_args=(),
-           device_types="cuda")
-def kv_resource_sparse_apply_adagrad_decay(var: int, accum: int, accum_decay_power: int,
+@custom_op(_NS + "::kv_resource_sparse_apply_adagrad_decay",
+           mutates_args=("var", "accum", "accum_decay_power"), device_types="cuda")
+def kv_resource_sparse_apply_adagrad_decay(var: Tensor, accum: Tensor, accum_decay_power: Tensor,
                                            lr: float, decay_step: int, decay_rate: float,
                                            decay_baseline: float, global_step: int,
                                            grad: Tensor, indices: Tensor) -> None:
     """KvResourceSparseApplyAdagradDecay (training_ali_ops.cc:703-823)."""
-    import ctypes as C
     g, k, n, st = _apply_common(grad, indices)
     check(lib().dr_ev_apply_adagrad_decay_grouped(
-        _one(_h(var)), _one(_h(accum)), _one(_h(accum_decay_power)), 1, _one(g.data_ptr()), 0,
+        _one(_hr(var)), _one(_hr(accum)), _one(_hr(accum_decay_power)), 1, _one(g.data_ptr()), 0,
         _one(k.data_ptr()), (C.c_int64 * 1)(n), _one(None), lr, decay_step, decay_rate,
         decay_baseline, global_step, st))
     ops._post(k.device)
+
+
+class _EvRef(object):
+    """(handle, dim) view of a resource for ops.embedding_lookup_sparse_c."""
+
+    def __init__(self, resource, dim):
+        self.handle, self.dim = _hr(resource), dim
+
+
+@custom_op(_NS + "::kv_embedding_lookup_sparse", mutates_args=("resource",),
+           device_types="cuda")
+def kv_embedding_lookup_sparse(resource: Tensor, sp_indices: Tensor, sp_values: Tensor,
+                               batch: int, dim: int, sp_weights: Optional[Tensor] = None,
+                               combiner: str = "mean", max_norm: float = -1.0,
+                               safe: bool = False, default_id: int = -1,
+                               prune: bool = True) -> Tensor:
+    """embedding_lookup_sparse / safe_embedding_lookup_sparse on an EV
+    (python/ops/embedding_ops.py:480-675, :1209-1344; the gather is
+    EmbeddingVariable.sparse_read -> KvResourceGather, kv_variable_ops.py:
+    644-664): the whole composition in ONE C call (dr_embedding_lookup_
+    sparse), insert-on-miss on the EV.  The north_star hot path as one
+    traceable op; its gradient is kv_embedding_lookup_sparse_grad."""
+    if combiner not in _COMB:
+        raise ValueError("combiner must be one of 'mean', 'sqrtn' or 'sum'")
+    return ops.embedding_lookup_sparse_c(_EvRef(resource, dim), sp_indices, sp_values, batch,
+                                         sp_weights, combiner,
+                                         None if max_norm < 0 else max_norm, safe,
+                                         None if default_id < 0 else default_id, prune)
+
+
+@kv_embedding_lookup_sparse.register_fake
+def _(resource, sp_indices, sp_values, batch, dim, sp_weights=None, combiner="mean",
+      max_norm=-1.0, safe=False, default_id=-1, prune=True):
+    return sp_values.new_empty((batch, dim), dtype=torch.float32)
+
+
+@custom_op(_NS + "::kv_embedding_lookup_sparse_grad", mutates_args=(), device_types="cuda")
+def kv_embedding_lookup_sparse_grad(sp_indices: Tensor, sp_values: Tensor, batch: int,
+                                    top_grad: Tensor, sp_weights: Optional[Tensor] = None,
+                                    combiner: str = "mean") -> Tuple[Tensor, Tensor, Tensor]:
+    """The gradient of kv_embedding_lookup_sparse w.r.t. the EV as the
+    reference's IndexedSlices (embedding_ops.py:592-675, math_grad.py:321-368):
+    (unique ids in first-occurrence order [nnz], gradient rows [nnz, dim],
+    num_unique DEVICE int64[1]); rows past num_unique are unused.  Feed to a
+    kv_resource_sparse_apply_* op with num_valid = num_unique."""
+    from .embedding_ops import _Feature, _grad_to_slices
+
+    class _P(object):
+        pass
+
+    p = _P()
+    p.dim = top_grad.shape[1]
+    f = _Feature(p, sp_values.to(torch.int64).contiguous(), sp_indices.to(torch.int64).contiguous(),
+                 batch, None if sp_weights is None else sp_weights.to(torch.float32).contiguous(),
+                 combiner, None)
+    g = top_grad.to(torch.float32).contiguous()
+    sl = _grad_to_slices(f, g, 0, g.shape[1])
+    n = sp_values.numel()
+    vals = sl.values
+    if vals.shape[0] != n:                          # the kernel sizes rows by max(n, 1)
+        vals = vals[:n]
+    return sl.indices[:n].clone(), vals.clone(), sl.num_valid.clone()
+
+
+@kv_embedding_lookup_sparse_grad.register_fake
+def _(sp_indices, sp_values, batch, top_grad, sp_weights=None, combiner="mean"):
+    n = sp_values.numel()
+    return (sp_values.new_empty(n, dtype=torch.int64),
+            top_grad.new_empty((n, top_grad.shape[1]), dtype=torch.float32),
+            sp_values.new_empty(1, dtype=torch.int64))
 
 
 # ---------------------------------------------------------------------------
@@ -460,7 +559,8 @@ OPS = ["unique_with_counts", "sparse_segment_reduce", "sparse_segment_reduce_gra
        "kv_resource_sparse_apply_adam_async", "kv_resource_sparse_apply_adagrad_decay",
        "fused_embedding_local_sparse_look_up", "fused_embedding_local_sparse_look_up_grad",
        "fused_embedding_sparse_post_look_up", "fused_embedding_sparse_post_look_up_grad",
-       "fm_second_order", "fm_second_order_grad", "dot_interaction", "dot_interaction_grad"]
+       "fm_second_order", "fm_second_order_grad", "dot_interaction", "dot_interaction_grad",
+       "kv_embedding_lookup_sparse", "kv_embedding_lookup_sparse_grad"]
 
 
 # ---------------------------------------------------------------------------

@@ -14,7 +14,7 @@ import torch
 from . import ops
 from ._lib import check, lib, ptr, stream_handle
 from .embedding_ops import DenseTable
-from .kv_variable_ops import EmbeddingVariable, IndexedSlices
+from .kv_variable_ops import EmbeddingVariable, IndexedSlices, _flush_deferred_releases
 
 
 def _concat(slices):
@@ -135,6 +135,7 @@ class _Optimizer(object):
         for items in rounds:
             self._apply_ev_batch(items, gs)
         self._finish()
+        _flush_deferred_releases()   # EVs collected meanwhile (no-op while capturing)
 
     def _slots(self, var):
         return None, None
@@ -354,13 +355,18 @@ class AdamAsyncOptimizer(_Optimizer):
     """KvSparseApplyAdamAsync (training_ali_ops.cc:1404-1575) on EVs, the
     optimizer of python/training/adam_async.py.  Slots m, v (zeros); the beta
     powers are per variable (adam_async.py:117-141: beta1 / beta2 initial,
-    one pair per EV) and advance after each apply that had gradients
-    (:1558-1559).  The reference multiplies them once per Shard() work chunk
-    of its CPU thread pool, so its count depends on the host's threading for
-    large N; here they advance once per apply, the single-chunk case.
-    apply_sparse_rmsprop: v = b2 v + (1 - b2) g^2, m = b1 m + lr g / sqrt(v +
-    eps), var -= m (:1506-1513); the powers are then not used.  Dense tables
-    take the same two updates on the indexed rows (SparseApplyAdamAsync)."""
+    one pair per EV) and live on the device, as the reference keeps them in
+    an EV of their own (:1523-1526): the apply kernel forms alpha from them
+    and a follow-up kernel advances them only when the gradient's effective
+    row count -- the device num_valid of a fixed-capacity slice -- is > 0
+    (`if (N > 0)`, :1482; :1558-1559), so no host read is needed and the step
+    can be graph-captured.  The reference multiplies them once per Shard()
+    work chunk of its CPU thread pool, so its count depends on the host's
+    threading for large N; here they advance once per apply, the single-chunk
+    case.  apply_sparse_rmsprop: v = b2 v + (1 - b2) g^2, m = b1 m + lr g /
+    sqrt(v + eps), var -= m (:1506-1513); the powers are then not used.
+    Dense tables take the same two updates on the indexed rows
+    (SparseApplyAdamAsync) with fp32 coefficients (T(1) - beta1 in T)."""
 
     def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8,
                  use_locking=False, apply_sparse_rmsprop=False):
@@ -368,53 +374,71 @@ class AdamAsyncOptimizer(_Optimizer):
         self.beta1, self.beta2, self.eps = float(beta1), float(beta2), float(epsilon)
         self.apply_sparse_rmsprop = bool(apply_sparse_rmsprop)
         self._opt = 4 if self.apply_sparse_rmsprop else 3
-        self._powers = {}     # id(var) -> [beta1_power, beta2_power] (fp32 values)
+        self._powers = {}     # id(var) -> device float32[2] {beta1_power, beta2_power}
         self._dense_mv = {}
-        self._advanced = []
 
     def _slots(self, var):
         return var.slot("AdamAsync", 0.0), var.slot("AdamAsync_1", 0.0)
 
+    def _power_t(self, var):
+        dev = var.weight.device if isinstance(var, DenseTable) else var.device
+        p = self._powers.get(id(var))
+        if p is None:
+            # fill kernels, not a host copy: legal inside a hipGraph capture
+            p = torch.empty(2, dtype=torch.float32, device=dev)
+            p[0].fill_(self.beta1)
+            p[1].fill_(self.beta2)
+            self._powers[id(var)] = p
+        return p
+
     def _power(self, var):
-        f32 = lambda x: torch.tensor(x, dtype=torch.float32).item()
-        return self._powers.setdefault(id(var), [f32(self.beta1), f32(self.beta2)])
+        """(beta1_power, beta2_power) as host floats (reads the device)."""
+        return self._power_t(var).tolist()
 
     def _apply_ev_batch(self, items, gs):
-        # tables with different beta powers cannot share one launch's alpha
-        by_power = {}
+        import ctypes as C
+        groups = {}
         for var, sl in items:
-            by_power.setdefault(tuple(self._power(var)), []).append((var, sl))
-            if sl.indices.numel() > 0:      # the op's `if (N > 0)` holds the power update
-                self._advanced.append(var)
-        for (b1p, b2p), sub in by_power.items():
-            self._scalars = lambda b1p=b1p, b2p=b2p: (b1p, b2p, self.beta1, self.beta2, self.eps)
-            _Optimizer._apply_ev_batch(self, sub, gs)
-        self._scalars = lambda: (0.0, 0.0, self.beta1, self.beta2, self.eps)
-
-    def _finish(self):
-        f32 = lambda x: torch.tensor(x, dtype=torch.float32)
-        for var in self._advanced:
-            p = self._power(var)
-            p[0] = (f32(p[0]) * f32(self.beta1)).item()
-            p[1] = (f32(p[1]) * f32(self.beta2)).item()
-        self._advanced = []
+            groups.setdefault((str(var.device), var.dim), []).append((var, sl))
+        for (_, _), grp in groups.items():
+            T = len(grp)
+            dev = grp[0][0].device
+            grads, _ = _grad_rows(grp, "dr_ev_apply_grouped")
+            by_addr = all(sl.grad_ptr is not None and sl._values is None for _, sl in grp)
+            idxs = [sl.indices.contiguous() for _, sl in grp]
+            slots = [self._slots(var) for var, _ in grp]
+            pw = [self._power_t(var) for var, _ in grp]
+            P = C.c_void_p * T
+            st = stream_handle(dev)
+            with _Locked(self.use_locking, [var.handle.value for var, _ in grp], st):
+                check(lib().dr_ev_apply_adam_async_grouped(
+                    1 if self.apply_sparse_rmsprop else 0, 1 if by_addr else 0,
+                    P(*[var.handle.value for var, _ in grp]),
+                    P(*[a.handle.value for a, _ in slots]), P(*[b.handle.value for _, b in slots]),
+                    T, P(*[v.data_ptr() for v in grads]), P(*[i.data_ptr() for i in idxs]),
+                    (C.c_int64 * T)(*[i.numel() for i in idxs]),
+                    P(*[ptr(sl.num_valid) for _, sl in grp]), P(*[p.data_ptr() for p in pw]),
+                    self.lr, self.beta1, self.beta2, self.eps, gs, st))
+            ops._post(dev)
 
     def _dense_update(self, var, idx, g):
         w = var.weight
         m, v = self._dense_mv.setdefault(id(var), (torch.zeros_like(w), torch.zeros_like(w)))
+        f32 = lambda x: torch.tensor(x, dtype=torch.float32, device=w.device)
+        one, b1, b2 = f32(1.0), f32(self.beta1), f32(self.beta2)
         with torch.no_grad():
             mi, vi = m[idx], v[idx]
-            vi = vi * self.beta2 + (g * g) * (1 - self.beta2)
+            vi = vi * b2 + (g * g) * (one - b2)
             if self.apply_sparse_rmsprop:
-                mi = mi * self.beta1 + torch.rsqrt(vi + self.eps) * self.lr * g
+                mi = mi * b1 + torch.rsqrt(vi + f32(self.eps)) * f32(self.lr) * g
                 w[idx] = w[idx] - mi
             else:
-                b1p, b2p = self._power(var)
-                f32 = lambda x: torch.tensor(x, dtype=torch.float32)
-                alpha = (f32(self.lr) * torch.sqrt(1 - f32(b2p)) / (1 - f32(b1p))).item()
-                mi = mi * self.beta1 + g * (1 - self.beta1)
-                w[idx] = w[idx] - (mi * alpha) / (torch.sqrt(vi) + self.eps)
-                self._advanced.append(var)
+                p = self._power_t(var)
+                alpha = f32(self.lr) * torch.sqrt(one - p[1]) / (one - p[0])
+                mi = mi * b1 + g * (one - b1)
+                w[idx] = w[idx] - (mi * alpha) / (torch.sqrt(vi) + f32(self.eps))
+                if idx.numel() > 0:           # the op's `if (N > 0)`
+                    p.mul_(torch.stack([b1, b2]))
             m[idx], v[idx] = mi, vi
 
 

@@ -193,6 +193,11 @@ int dr_rows_per_nnz(const int64_t* rows, const int32_t* idx, const int64_t* koff
 /* Same over sp_indices[:, 0] read with a stride (2 for [nnz, 2] indices).   */
 int dr_bag_offsets_strided(const int64_t* seg, int64_t stride, int64_t n, int64_t batch,
                            int32_t* bag_off, void* stream);
+/* The same over a DEVICE count n_dev (<= n_cap), e.g. the filled output of */
+/* dr_sparse_prune_fill: no host read of the entry count.                   */
+int dr_bag_offsets_strided_dev(const int64_t* seg, int64_t stride, int64_t n_cap,
+                               const int64_t* n_dev, int64_t batch, int32_t* bag_off,
+                               void* stream);
 
 /* Backward of dr_pool_grouped over T features in one pass (the features of */
 /* one dr_unique_grouped call): grad_unique row koff[t] + u (koff = prefix  */
@@ -356,6 +361,8 @@ int dr_ev_size(dr_ev* ev, int64_t* size_host, void* stream);
 int dr_ev_shrink(dr_ev* ev, int64_t global_step, float l2_weight_threshold,
                  int64_t* removed_host, void* stream);
 int64_t dr_ev_dim(dr_ev* ev);
+/* filter_freq of the EV's Counter / Bloom admission filter (0: none).        */
+int64_t dr_ev_filter_freq(dr_ev* ev);
 /* Row-pool capacity of the EV's key space (host value, no sync): every row  */
 /* index the EV has handed out is below it (the row_limit of                 */
 /* dr_pool_grad_rows_grouped).                                               */
@@ -399,6 +406,18 @@ int dr_ev_lookup_onehot(dr_ev* const* evs, int num_tables, const int64_t* keys, 
 int dr_ev_lookup_onehot_rows(dr_ev* const* evs, int num_tables, const int64_t* keys,
                              int64_t batch, float* out, int64_t out_stride, int order,
                              int64_t* rows_out, void* ws, size_t ws_bytes, void* stream);
+/* The same with the ids read through strides: id of (bag b, table t) =    */
+/* keys[b*key_stride_bag + t*key_stride_table].  (1, batch) is the [T,      */
+/* batch] layout above; (T, 1) reads a record-major [batch, T] id matrix in */
+/* place -- one Criteo record of T categorical ids per row, the input of     */
+/* the SOK/DLRM Criteo-TB pipeline (modelzoo/SOK/DLRM) -- so the kernel,    */
+/* which visits (b, t) in output order, reads its ids as one contiguous run  */
+/* instead of one 128-B line per table.  rows_out (nullable) is written at  */
+/* rows_out[t*batch + b] in either layout.                                   */
+int dr_ev_lookup_onehot_strided(dr_ev* const* evs, int num_tables, const int64_t* keys,
+                                int64_t key_stride_bag, int64_t key_stride_table, int64_t batch,
+                                float* out, int64_t out_stride, int order, int64_t* rows_out,
+                                void* ws, size_t ws_bytes, void* stream);
 /* Tagged resolve (owner side of the sharded exchange): keys of all T EVs  */
 /* (equal dim) in one array, table of key i = tags[i]; n_dev: optional      */
 /* DEVICE count.  Filtered keys give -(i+1) (read table t's default row).   */
@@ -507,6 +526,21 @@ int dr_ev_apply_grouped_ptr_rows(int optimizer, dr_ev* const* vars, int num_tabl
                                  const int64_t* const* rows, const int64_t* n_host,
                                  const int64_t* const* n_dev, float lr, int64_t global_step,
                                  void* stream);
+/* KvResourceSparseApplyAdamAsync (training_ali_ops.cc:1404-1575) with the  */
+/* beta powers DEVICE-resident, as the reference keeps them in an EV (key 0,  */
+/* :1523-1526): powers[t] is table t's float[2] {beta1_power, beta2_power}.   */
+/* The kernel forms alpha = lr sqrt(1 - b2p) / (1 - b1p) from them and a      */
+/* follow-up kernel multiplies them by beta1 / beta2 only for tables whose    */
+/* effective N (min(n_host, *n_dev)) is > 0 (:1482 `if (N > 0)`) -- no host   */
+/* read of a device count, so the step can be graph-captured.  rmsprop != 0:  */
+/* apply_sparse_rmsprop (:1483-1519), powers unused (may be NULL).  grads[t]:  */
+/* a [n, dim] float block, or (by_address) uint64 row addresses.             */
+int dr_ev_apply_adam_async_grouped(int rmsprop, int by_address, dr_ev* const* vars,
+                                   dr_ev* const* m, dr_ev* const* v, int num_tables,
+                                   const void* const* grads, const int64_t* const* keys,
+                                   const int64_t* n_host, const int64_t* const* n_dev,
+                                   float* const* powers, float lr, float beta1, float beta2,
+                                   float epsilon, int64_t global_step, void* stream);
 /* KvResourceSparseApplyAdagradDecay (training_ali_ops.cc:703-823; op def    */
 /* core/ops/training_ali_ops.cc): accum and accum_decay_power are slot EVs   */
 /* of var (var-shaped; the decay count is element 0 of a row, as the         */
@@ -819,6 +853,33 @@ int dr_sparse_prune_fill(const int64_t* indices, int rank, const int64_t* values
                          int64_t* out_values, float* out_weights, int64_t* reverse_index_map,
                          uint8_t* empty_row, int64_t* out_nnz, void* ws, size_t ws_bytes,
                          void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* embedding_lookup_sparse / safe_embedding_lookup_sparse as ONE call        */
+/* (python/ops/embedding_ops.py:480-675 and :1209-1344; the composition a TF */
+/* custom-op kernel binds).  params: exactly one of `ev` (an */
+/* EmbeddingVariable, insert-on-miss; a Counter/Bloom EV goes through         */
+/* UniqueWithCounts -> KvResourceGatherV1 as :592-596 do) or a dense fp32     */
+/* `table` [table_rows, dim] (ids bounds-checked).  sp_indices [nnz, 2]       */
+/* int64 rows-sorted (SparseTensor canonical order), sp_values [nnz] int64,   */
+/* sp_weights [nnz] or NULL.  combiner DR_COMBINER_*; max_norm >= 0 clips     */
+/* each gathered row (clip_by_norm, :183-190), < 0 = None.                    */
+/* safe != 0: safe_embedding_lookup_sparse: prune != 0 drops ids < 0 (and     */
+/* weights <= 0 when weighted and combiner != sum), empty rows get           */
+/* default_id (default_id < 0 = None: filled with id 0, their outputs zeroed */
+/* at the end).  out [batch, out_stride] fp32: row b = bag b (bags past the   */
+/* last non-empty one are 0; the reference's plain embedding_lookup_sparse   */
+/* returns last_row + 1 rows, callers slice).  No host synchronisation        */
+/* except for a filter EV with safe != 0 (the Unique's length).  Errors found */
+/* on the device (unsorted rows, OOB dense ids) latch into dr_status_check.  */
+/* ------------------------------------------------------------------------ */
+size_t dr_embedding_lookup_sparse_workspace_size(int64_t nnz, int64_t batch);
+int dr_embedding_lookup_sparse(dr_ev* ev, const float* table, int64_t table_rows, int dim,
+                               const int64_t* sp_indices, const int64_t* sp_values,
+                               const float* sp_weights, int64_t nnz, int64_t batch, int combiner,
+                               float max_norm, int safe, int64_t default_id, int prune,
+                               float* out, int64_t out_stride, void* ws, size_t ws_bytes,
+                               void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Checkpoint support (host function, no device work): crc32c::Extend of    */

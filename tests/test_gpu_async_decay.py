@@ -133,17 +133,20 @@ def test_registered_ops_match_optimizers(dr, orc):
     m, v = ev.slot("m", 0.0), ev.slot("v", 0.0)
     oev = orc.EV(D, 0.2)
     om, ov = oev.create_slot(1, 0.0), oev.create_slot(2, 0.0)
+    bp = torch.tensor([0.9, 0.999], dtype=torch.float32, device=DEV)
     torch.ops.deeprec.kv_resource_sparse_apply_adam_async(
-        ev.handle.value, m.handle.value, v.handle.value, 0.9, 0.999, 0.01, 0.9, 0.999, 1e-8,
-        T(g), T(ids), 3)
+        ev.resource, m.resource, v.resource, bp, 0.01, 0.9, 0.999, 1e-8, T(g), T(ids), 3)
     oev.apply_adam_async(om, ov, 0.9, 0.999, 0.01, 0.9, 0.999, 1e-8, g, ids, gs=3)
+    # the op advanced its beta power resources (N > 0)
+    assert bp.cpu().tolist() == [float(np.float32(0.9) * np.float32(0.9)),
+                                 float(np.float32(0.999) * np.float32(0.999))]
     np.testing.assert_array_equal(ev.sparse_read(T(ids)).cpu().numpy(), oev.gather(ids))
     ev2 = dr.EmbeddingVariable("op_ad", D, 0.2)
     acc, pw = ev2.slot("acc", 0.1), ev2.slot("pw", 0.0)
     oev2 = orc.EV(D, 0.2)
     oacc, opw = oev2.create_slot(1, 0.1), oev2.create_slot(2, 0.0)
     torch.ops.deeprec.kv_resource_sparse_apply_adagrad_decay(
-        ev2.handle.value, acc.handle.value, pw.handle.value, 0.5, 2, 0.9, 0.1, 5, T(g), T(ids))
+        ev2.resource, acc.resource, pw.resource, 0.5, 2, 0.9, 0.1, 5, T(g), T(ids))
     oev2.apply_adagrad_decay(oacc, opw, 0.5, 2, 0.9, 0.1, g, ids, 5)
     np.testing.assert_array_equal(ev2.sparse_read(T(ids)).cpu().numpy(), oev2.gather(ids))
     np.testing.assert_array_equal(pw.sparse_read(T(ids)).cpu().numpy(), opw.gather(ids))
@@ -160,6 +163,77 @@ def test_adam_async_empty_gradient_keeps_powers(dr):
     p = opt._power(ev)
     assert p[0] == float(np.float32(0.9)) and p[1] == float(np.float32(0.999))
     assert ev.sparse_read(T([1])).cpu().numpy().tolist() == [[0.5] * 4]
+    # a dense table with an empty gradient keeps its powers too
+    tab = dr.DenseTable(T(np.ones((5, 4), np.float32)))
+    tab.pending_grads.append(dr.IndexedSlices(T(np.zeros((0, 4), np.float32)),
+                                              T(np.zeros(0, np.int64))))
+    opt.apply_gradients([tab], global_step=0)
+    p = opt._power(tab)
+    assert p[0] == float(np.float32(0.9)) and p[1] == float(np.float32(0.999))
+
+
+def test_adam_async_device_count_guards_powers(dr, orc):
+    """A fixed-capacity slice whose DEVICE count (num_valid, as the sharded
+    and row-grouped backwards queue them) is 0 is the op's N == 0: no row
+    moves and the beta powers stay (training_ali_ops.cc:1482).  A count of 2
+    of 4 applies exactly the first two rows and advances the powers once --
+    with no host read of the count (the apply can be graph-captured)."""
+    D = 8
+    ev = dr.EmbeddingVariable("aa_devcnt", D, 0.5)
+    oev = orc.EV(D, 0.5)
+    om, ov = oev.create_slot(1, 0.0), oev.create_slot(2, 0.0)
+    opt = dr.AdamAsyncOptimizer(0.01)
+    ids = np.array([3, 7, 11, 19], np.int64)
+    g = (np.random.default_rng(5).standard_normal((4, D)) * 0.3).astype(np.float32)
+    ev.pending_grads.append(dr.IndexedSlices(T(g), T(ids), num_valid=T([0], torch.int64),
+                                             unique=True))
+    opt.apply_gradients([ev], global_step=0)
+    p = opt._power(ev)
+    assert p[0] == float(np.float32(0.9)) and p[1] == float(np.float32(0.999))
+    np.testing.assert_array_equal(ev.sparse_read(T(ids)).cpu().numpy(), np.full((4, D), 0.5,
+                                                                               np.float32))
+    ev2 = dr.EmbeddingVariable("aa_devcnt2", D, 0.5)
+    opt2 = dr.AdamAsyncOptimizer(0.01)
+    ev2.pending_grads.append(dr.IndexedSlices(T(g), T(ids), num_valid=T([2], torch.int64),
+                                              unique=True))
+    opt2._slots(ev2)                  # slot EVs allocate: created before the capture
+    opt2._power_t(ev2)
+    torch.cuda.synchronize()
+    g_cap = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g_cap):
+        opt2.apply_gradients([ev2], global_step=0)
+    g_cap.replay()
+    torch.cuda.synchronize()
+    oev.apply_adam_async(om, ov, 0.9, 0.999, 0.01, 0.9, 0.999, 1e-8, g[:2], ids[:2], gs=0)
+    np.testing.assert_array_equal(ev2.sparse_read(T(ids[:2])).cpu().numpy(), oev.gather(ids[:2]))
+    p = opt2._power(ev2)
+    assert p[0] == float(np.float32(0.9) * np.float32(0.9))
+    assert p[1] == float(np.float32(0.999) * np.float32(0.999))
+
+
+def test_dense_adam_async_fp32_coefficients(dr):
+    """Dense-table AdamAsync computes T(1) - beta in fp32 (1.0f - 0.9f =
+    0.100000024f), as the op does; pinned against an fp32 numpy restatement
+    of the element formula (bit-exact)."""
+    R, D = 6, 4
+    rng = np.random.default_rng(41)
+    w0 = rng.standard_normal((R, D)).astype(np.float32)
+    tab = dr.DenseTable(T(w0.copy()))
+    opt = dr.AdamAsyncOptimizer(0.05)
+    f = np.float32
+    w, m, v = w0.copy(), np.zeros((R, D), f), np.zeros((R, D), f)
+    b1p, b2p = f(0.9), f(0.999)
+    for step in range(3):
+        idx = np.array([0, 2, 5], np.int64)
+        g = rng.standard_normal((3, D)).astype(f)
+        tab.pending_grads.append(dr.IndexedSlices(T(g), T(idx)))
+        opt.apply_gradients([tab], global_step=step)
+        alpha = f(f(0.05) * np.sqrt(f(1) - b2p)) / (f(1) - b1p)
+        m[idx] = m[idx] * f(0.9) + g * (f(1) - f(0.9))
+        v[idx] = v[idx] * f(0.999) + (g * g) * (f(1) - f(0.999))
+        w[idx] = w[idx] - (m[idx] * alpha) / (np.sqrt(v[idx]) + f(1e-8))
+        b1p, b2p = b1p * f(0.9), b2p * f(0.999)
+    np.testing.assert_allclose(tab.weight.cpu().numpy(), w, rtol=2e-7, atol=0)
 
 
 def test_dense_table_adagrad_decay_and_adam_async(dr):

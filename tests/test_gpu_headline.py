@@ -5,7 +5,9 @@ The rows are regenerable (synth(seed, key, col), dr_common.h), so sampled
 output rows are checked bit for bit against the host restatement
 (oracle.synth_rows) at the real load factor and probe-chain lengths, for:
   * a uniform step through the fused one-hot kernel (dr_ev_lookup_onehot) and
-    the resolve -> pool pipeline (whole outputs equal),
+    the resolve -> pool pipeline (whole outputs equal), and with the ids read
+    in place from a record-major [B, T] matrix (dr_ev_lookup_onehot_strided,
+    the bench's layout: whole output equal),
   * a step with ~10 % new keys (insert-on-miss: default rows, every EV grows
     by exactly its distinct new keys, existing rows unchanged),
   * a Zipf(1.05) step (hot keys, long duplicate runs),
@@ -67,14 +69,22 @@ def test_headline_shape_parity(orc):
             dr.status_check()
             assert torch.equal(out, out2)
             assert all(int(ev.total_count()[0]) == R for ev in evs)
+            rec = ids.t().contiguous()                                       # [B, T] records
+            out3 = dr.embedding_lookup_sparse_multi(
+                evs, [SparseTensor(ind, rec[:, t], (B, 1)) for t in range(T)], combiner="sum")
+            dr.status_check()
+            assert torch.equal(out, out3)
 
             # ~10 % new keys: insert-on-miss
             newm = torch.rand((T, B), generator=g, device=DEV) < 0.1
             fresh = R + torch.randint(0, 1 << 40, (T, B), generator=g, device=DEV,
                                       dtype=torch.int64)
             ids_n = torch.where(newm, fresh, ids)
+            rec_n = ids_n.t().contiguous()
+            # the insert-on-miss step reads its ids record-major (strided miss path)
+            outn = dr.embedding_lookup_sparse_multi(
+                evs, [SparseTensor(ind, rec_n[:, t], (B, 1)) for t in range(T)], combiner="sum")
             sps = [SparseTensor(ind, ids_n[t], (B, 1)) for t in range(T)]
-            outn = dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum")
             dr.status_check()
             view = outn.view(B, T, D)
             assert not bool((view[newm.t()] != 0).any())
@@ -105,3 +115,4 @@ def test_headline_shape_parity(orc):
     finally:
         del evs
         gc.collect()
+        dr.flush_releases()

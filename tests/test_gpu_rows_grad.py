@@ -382,5 +382,24 @@ def test_ev_collected_during_capture_is_released_after(dr):
     g.replay()
     torch.cuda.synchronize()
     assert float(y.sum()) == 16.0
-    dr.EmbeddingVariable("cap_gc2", 8, 0.0, capacity=1024)
+    keep = dr.EmbeddingVariable("cap_gc2", 8, 0.0, capacity=1024)
     assert len(kvo._DEFERRED) == 0
+    # collected on ANOTHER thread (whose current stream is not capturing)
+    # while this thread captures: still deferred, released after the capture
+    import threading
+    ev = dr.EmbeddingVariable("cap_gc3", 8, 0.0, capacity=1024)
+    ev._self_ref = ev
+    del ev
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g2):
+        y2 = x + 2
+        th = threading.Thread(target=gc.collect)
+        th.start()
+        th.join()
+    assert len(kvo._DEFERRED) == 1
+    g2.replay()
+    torch.cuda.synchronize()
+    assert float(y2.sum()) == 32.0
+    dr.flush_releases()
+    assert len(kvo._DEFERRED) == 0
+    del keep

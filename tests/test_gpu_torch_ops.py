@@ -58,9 +58,9 @@ def test_kv_ops_match_package(dr, orc):
     ev = dr.EmbeddingVariable("tops_kv", D, 0.25)
     keys = np.arange(0, 400, 3, dtype=np.int64)
     vals = rng.standard_normal((keys.shape[0], D)).astype(np.float32)
-    torch.ops.deeprec.kv_resource_insert(ev.handle.value, T(keys), T(vals))
+    torch.ops.deeprec.kv_resource_insert(ev.resource, T(keys), T(vals))
     q = np.concatenate([keys[:50], np.array([1, 2, 1000], np.int64)])
-    got = torch.ops.deeprec.kv_resource_gather(ev.handle.value, T(q), D)
+    got = torch.ops.deeprec.kv_resource_gather(ev.resource, T(q), D)
     np.testing.assert_array_equal(H(got), H(ev.sparse_read(T(q))))
     acc = ev.slot("Adagrad", 0.1)
     oev = orc.EV(D, 0.25)
@@ -69,7 +69,7 @@ def test_kv_ops_match_package(dr, orc):
     oacc = oev.create_slot(1, np.full(D, 0.1, np.float32))
     uq = np.unique(q)
     gq = rng.standard_normal((uq.shape[0], D)).astype(np.float32)
-    torch.ops.deeprec.kv_resource_sparse_apply_adagrad(ev.handle.value, acc.handle.value, 0.1,
+    torch.ops.deeprec.kv_resource_sparse_apply_adagrad(ev.resource, acc.resource, 0.1,
                                                        T(gq), T(uq), 3)
     oev.apply_adagrad(oacc, np.float32(0.1), gq, uq, 3)
     np.testing.assert_allclose(H(ev.sparse_read(T(uq))), oev.gather(uq), rtol=1e-5, atol=1e-7)
@@ -112,3 +112,74 @@ def test_trace_to_fx_graph(dr):
     assert "deeprec.embedding_lookup_sparse.default" in targets
     assert "deeprec.dot_interaction.default" in targets
     np.testing.assert_array_equal(H(gm(table, T(ind), T(vals))), H(model(table, T(ind), T(vals))))
+
+
+def test_ev_lookup_op_matches_oracle(dr, orc):
+    """torch.ops.deeprec.kv_embedding_lookup_sparse -- the EV-backed hot-path
+    op (EmbeddingVariable.sparse_read -> KvResourceGather inside
+    embedding_lookup_sparse, kv_variable_ops.py:644-664) in one C call --
+    equals the oracle's composition, and its grad op equals the reference
+    SparseSegment*Grad IndexedSlices."""
+    rng = np.random.default_rng(12)
+    B, D = 128, 16
+    ev = dr.EmbeddingVariable("tops_evl", D, 0.25)
+    oev = orc.EV(D, 0.25)
+    keys = np.arange(0, 90, dtype=np.int64)
+    vals0 = rng.standard_normal((90, D)).astype(np.float32)
+    ev.insert(T(keys), T(vals0))
+    oev.insert(keys, vals0)
+    ind, vals = _sparse(rng, B, 4, 120)
+    for comb in ("sum", "mean", "sqrtn"):
+        out = torch.ops.deeprec.kv_embedding_lookup_sparse(ev.resource, T(ind), T(vals), B, D,
+                                                           None, comb)
+        ref = orc.embedding_lookup_sparse(oev, ind, vals, B, None, comb)
+        np.testing.assert_array_equal(H(out), ref)
+        g = rng.standard_normal((B, D)).astype(np.float32)
+        u, gr, nu = torch.ops.deeprec.kv_embedding_lookup_sparse_grad(T(ind), T(vals), B, T(g),
+                                                                      None, comb)
+        U = int(nu.item())
+        uids, gref = orc.embedding_lookup_sparse_grad(oev, ind, vals, B, g, None, comb)
+        assert H(u[:U]).tolist() == uids.tolist()
+        np.testing.assert_array_equal(H(gr[:U]), gref)
+
+
+def test_compile_keeps_stateful_order(dr, orc):
+    """Under torch.compile (aot_eager: functionalization of the custom ops),
+    a lookup -> grad -> SGD apply -> lookup chain on one EV keeps every
+    stateful op, in program order: the second lookup sees the update, bit for
+    bit what eager execution gives, and the traced graph holds one apply
+    between the two lookups."""
+    rng = np.random.default_rng(13)
+    B, D, lr = 64, 8, 0.5
+    ind, vals = _sparse(rng, B, 3, 50)
+    g = T(rng.standard_normal((B, D)).astype(np.float32))
+    def step(res, ind_t, vals_t, g):
+        a = torch.ops.deeprec.kv_embedding_lookup_sparse(res, ind_t, vals_t, B, D, None, "sum")
+        u, gr, nu = torch.ops.deeprec.kv_embedding_lookup_sparse_grad(ind_t, vals_t, B, g, None,
+                                                                      "sum")
+        torch.ops.deeprec.kv_resource_sparse_apply_gradient_descent(res, lr, gr, u, 1, nu)
+        b = torch.ops.deeprec.kv_embedding_lookup_sparse(res, ind_t, vals_t, B, D, None, "sum")
+        return a, b
+
+    outs = []
+    for mode in ("eager", "compiled"):
+        ev = dr.EmbeddingVariable("tops_cmp_" + mode, D, 0.1)
+        ev.insert(T(np.arange(50, dtype=np.int64)),
+                  T(np.random.default_rng(3).standard_normal((50, D)).astype(np.float32)))
+        fn = step if mode == "eager" else torch.compile(step, backend="aot_eager", fullgraph=True)
+        a, b = fn(ev.resource, T(ind), T(vals), g)
+        torch.cuda.synchronize()
+        outs.append((H(a), H(b)))
+        assert not np.array_equal(H(a), H(b))          # the apply ran before the 2nd lookup
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    # the same chain captured by make_fx keeps one apply between two lookups
+    from torch.fx.experimental.proxy_tensor import make_fx
+    ev = dr.EmbeddingVariable("tops_cmp_fx", D, 0.1)
+    gm = make_fx(step, tracing_mode="real")(ev.resource, T(ind), T(vals), g)
+    seq = [str(n.target) for n in gm.graph.nodes if n.op == "call_function"
+           and "deeprec.kv_" in str(n.target)]
+    assert seq == ["deeprec.kv_embedding_lookup_sparse.default",
+                   "deeprec.kv_embedding_lookup_sparse_grad.default",
+                   "deeprec.kv_resource_sparse_apply_gradient_descent.default",
+                   "deeprec.kv_embedding_lookup_sparse.default"], seq

@@ -29,6 +29,25 @@ def test_reference_argument_names(tops):
         assert a in s
 
 
+def test_stateful_ops_declare_mutation(tops):
+    """Ops that change an EV list its resource tensor as mutated (schema
+    `Tensor(a!)`), so functionalization / torch.compile can neither drop nor
+    reorder them; pure ops mutate nothing."""
+    stateful = {"kv_resource_gather": ["resource"], "kv_resource_insert": ["resource"],
+                "kv_embedding_lookup_sparse": ["resource"],
+                "kv_resource_sparse_apply_gradient_descent": ["var"],
+                "kv_resource_sparse_apply_adagrad": ["var", "accum"],
+                "kv_resource_sparse_apply_adam": ["var", "m", "v"],
+                "kv_resource_sparse_apply_ftrl": ["var", "accum", "linear"],
+                "kv_resource_sparse_apply_adam_async": ["var", "m", "v", "beta_powers"],
+                "kv_resource_sparse_apply_adagrad_decay": ["var", "accum", "accum_decay_power"]}
+    for name in tops.OPS:
+        sch = getattr(torch.ops.deeprec, name).default._schema
+        mutated = [a.name for a in sch.arguments if a.alias_info is not None
+                   and a.alias_info.is_write]
+        assert mutated == stateful.get(name, []), (name, mutated)
+
+
 def test_fake_shapes_on_meta(tops):
     m = dict(device="meta")
     x = torch.empty(10, dtype=torch.int64, **m)
@@ -42,7 +61,16 @@ def test_fake_shapes_on_meta(tops):
     e = torch.ops.deeprec.embedding_lookup_sparse(t, torch.empty((20, 2), dtype=torch.int64, **m),
                                                   torch.empty(20, dtype=torch.int64, **m), 6)
     assert e.shape == (6, 8)
-    g = torch.ops.deeprec.kv_resource_gather(0, torch.empty((3, 5), dtype=torch.int64, **m), 16)
+    res = torch.zeros(1, dtype=torch.int64)
+    g = torch.ops.deeprec.kv_resource_gather(res, torch.empty((3, 5), dtype=torch.int64, **m), 16)
     assert g.shape == (3, 5, 16)
+    e = torch.ops.deeprec.kv_embedding_lookup_sparse(
+        res, torch.empty((20, 2), dtype=torch.int64, **m), torch.empty(20, dtype=torch.int64, **m),
+        6, 32)
+    assert e.shape == (6, 32)
+    u, gr, nu = torch.ops.deeprec.kv_embedding_lookup_sparse_grad(
+        torch.empty((20, 2), dtype=torch.int64, **m), torch.empty(20, dtype=torch.int64, **m), 6,
+        torch.empty((6, 32), **m))
+    assert u.shape == (20,) and gr.shape == (20, 32) and nu.shape == (1,)
     d = torch.ops.deeprec.dot_interaction(torch.empty((4, 27, 16), **m))
     assert d.shape == (4, 351)

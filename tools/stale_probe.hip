@@ -100,5 +100,48 @@ int main(int argc, char** argv) {
                realloc_, wname[w], nt ? "nontemporal" : "plain", total, n * 20);
         fflush(stdout);
       }
+  // Uncached round trip (xgmi.hip dr_ipc_alloc history):
+  // cached X warmed into every XCD L2 with pattern A -> hipFree -> an
+  // UNCACHED allocation U (hipDeviceMallocUncached) written B by a kernel
+  // (its stores bypass L2) -> hipFree -> a cached hipMalloc Y written C by
+  // writer w -> every XCD reads Y.  Counts words != C, and how many of those
+  // read A (a stale L2 line of the first cached use) or B.
+  for (int w = 0; w < 2; ++w)
+    for (int nt = 0; nt < 2; ++nt) {
+      unsigned long long total = 0, same_u = 0, same_y = 0;
+      for (int rep = 0; rep < 20; ++rep) {
+        unsigned *x, *u, *y;
+        CK(hipMalloc(&x, bytes));
+        fill_k<<<2048, 256, 0, s>>>(x, n, 0xAAAAAAAAu);
+        for (int k = 0; k < 2; ++k) touch_k<<<2048, 256, 0, s>>>(x, n, sink);
+        CK(hipStreamSynchronize(s));
+        CK(hipFree(x));
+        CK(hipExtMallocWithFlags((void**)&u, bytes, hipDeviceMallocUncached));
+        same_u += u == x;
+        fill_k<<<2048, 256, 0, s>>>(u, n, 0xBBBBBBBBu);
+        for (int k = 0; k < 2; ++k) touch_k<<<2048, 256, 0, s>>>(u, n, sink);
+        CK(hipStreamSynchronize(s));
+        CK(hipFree(u));
+        CK(hipMalloc(&y, bytes));
+        same_y += y == u;
+        if (w == 0) fill_k<<<2048, 256, 0, s>>>(y, n, 0xCCCCCCCCu);
+        if (w == 1) CK(hipMemsetAsync(y, 0xCC, bytes, s));
+        fill_k<<<1, 64, 0, s>>>((unsigned*)bad, 2, 0u);
+        if (nt)
+          check_k<true><<<2048, 256, 0, s>>>(y, n, 0xCCCCCCCCu, bad);
+        else
+          check_k<false><<<2048, 256, 0, s>>>(y, n, 0xCCCCCCCCu, bad);
+        unsigned long long b = 0;
+        CK(hipMemcpyAsync(&b, bad, 8, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        total += b;
+        CK(hipFree(y));
+      }
+      printf("{\"uncached_round_trip\": 1, \"writer\": \"%s\", \"reader\": \"%s\", "
+             "\"stale_words\": %llu, \"words_checked\": %zu, \"u_reused_x_va\": %llu, "
+             "\"y_reused_u_va\": %llu}\n",
+             wname[w], nt ? "nontemporal" : "plain", total, n * 20, same_u, same_y);
+      fflush(stdout);
+    }
   return 0;
 }
