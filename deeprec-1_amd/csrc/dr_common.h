@@ -145,6 +145,31 @@ __host__ __device__ __forceinline__ float synth(uint64_t seed, int64_t row, int6
   return (float)(int32_t)(uint32_t)(z >> 32) * (1.0f / 2147483648.0f);
 }
 
+// ---- bf16 rows (bf16 EVs) --------------------------------------------------
+// fp32 -> bf16 round-to-nearest-even; NaN -> 0x7FC0 (torch's c10::BFloat16
+// conversion, so bf16 results compare bitwise with torch.bfloat16 casts).
+__host__ __device__ __forceinline__ uint16_t bf16_rne(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7FFFFFFFu) > 0x7F800000u) return 0x7FC0;
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+inline uint16_t bf16_rne_host(float f) { return bf16_rne(f); }
+__host__ __device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+  const uint32_t u = (uint32_t)h << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+// two packed bf16 (low half = element 2k) <-> float2
+__device__ __forceinline__ float2 bf16x2_to_f2(uint32_t w) {
+  return make_float2(__uint_as_float(w << 16), __uint_as_float(w & 0xFFFF0000u));
+}
+__device__ __forceinline__ uint32_t f2_to_bf16x2(float a, float b) {
+  return (uint32_t)bf16_rne(a) | ((uint32_t)bf16_rne(b) << 16);
+}
+
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ uint64_t lanemask_lt() {

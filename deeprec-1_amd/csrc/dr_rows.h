@@ -95,6 +95,40 @@ __device__ __forceinline__ void acc_add(Row<VEC, G, CPL>& a, const Row<VEC, G, C
   for (int c = 0; c < CPL; ++c) a.v[c] = vadd(a.v[c], b.v[c]);
 }
 
+// bf16 rows (bf16 EVs): lane chunk c covers VEC consecutive bf16 values
+// (VEC * 2 bytes) of a row whose float-word pointer is p; widened to fp32.
+template <int VEC, int G, int CPL>
+__device__ __forceinline__ void load_row_bf16(Row<VEC, G, CPL>& x, const float* p, int lg, int dv) {
+  static_assert(VEC == 4, "bf16 rows use 4-value chunks");
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = lg + c * G;
+    if (p && col < dv) {
+      const u2 w = gld(reinterpret_cast<const u2*>(p) + col);
+      const float2 a = bf16x2_to_f2(w.x), b = bf16x2_to_f2(w.y);
+      x.v[c] = make_float4(a.x, a.y, b.x, b.y);
+    } else {
+      x.v[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+// fp32 row -> bf16 (round to nearest even) at the float-word pointer p.
+template <int VEC, int G, int CPL>
+__device__ __forceinline__ void store_row_bf16(const Row<VEC, G, CPL>& x, float* p, int lg, int dv) {
+  static_assert(VEC == 4, "bf16 rows use 4-value chunks");
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = lg + c * G;
+    if (col < dv) {
+      const u2 w = {f2_to_bf16x2(x.v[c].x, x.v[c].y), f2_to_bf16x2(x.v[c].z, x.v[c].w)};
+      gst(reinterpret_cast<u2*>(p) + col, w);
+    }
+  }
+}
+
 // Row load with an always-valid pointer (only the lane's column predicate):
 // a per-row "pointer or zero" select makes hipcc branch around every load
 // and wait for it before the next one, so batches of independent loads

@@ -73,11 +73,20 @@ struct EvShared {
   // value dtype: 1 = float, 2 = double (a double row is stored as 2 * dim
   // float words and moved bitwise; `dim` counts float words)
   int value_words = 1;
+  // bf16 EV (value_bits 16): the primary column holds bf16 rows of D values
+  // (D/2 float words, moved bitwise by the copy kernels); `dim` = D counts
+  // the fp32 words of the optimizer slot columns, which stay fp32.
+  int bf16 = 0;
   // use_locking applies (dr_ev_lock_updates): exclusive updates across
   // host threads and streams
   std::mutex update_mu;
   hipEvent_t update_ev = nullptr;
 };
+
+// float words per row of column `col`
+inline int64_t col_words(const EvShared* s, int col) {
+  return (s->bf16 && col == 0) ? s->dim / 2 : s->dim;
+}
 
 }  // namespace dr
 
@@ -543,13 +552,20 @@ __global__ void ev_insert_range_kernel(EvDesc e, int64_t begin, int64_t stride, 
   rows_out[i] = (int64_t)(rc & kRowMask);
 }
 
-__global__ void ev_synth_rows_kernel(float* __restrict__ pool, int64_t dim, int64_t begin,
-                                     int64_t stride, int64_t n, const int64_t* __restrict__ rows,
+__global__ void ev_synth_rows_kernel(float* __restrict__ pool, int64_t dim, int bf16,
+                                     int64_t begin, int64_t stride, int64_t n,
+                                     const int64_t* __restrict__ rows,
                                      const uint8_t* __restrict__ init, uint64_t seed) {
   const int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
   if (i >= n || !init[i]) return;
-  float* dst = pool + rows[i] * dim;
   const int64_t key = begin + i * stride;
+  if (bf16) {  // bf16(synth) pairs, element 2k in the low half
+    uint32_t* dst = reinterpret_cast<uint32_t*>(pool) + rows[i] * (dim / 2);
+    for (int64_t c = threadIdx.x % 64; c < dim / 2; c += 64)
+      dst[c] = f2_to_bf16x2(synth(seed, key, 2 * c), synth(seed, key, 2 * c + 1));
+    return;
+  }
+  float* dst = pool + rows[i] * dim;
   for (int64_t c = threadIdx.x % 64; c < dim; c += 64) dst[c] = synth(seed, key, c);
 }
 
@@ -798,13 +814,38 @@ __device__ __forceinline__ uint64_t apply_grad_addr(const float* grad, int gind,
   return gind ? reinterpret_cast<const uint64_t*>(grad)[i]
               : (uint64_t)(uintptr_t)(grad + i * dim);
 }
+// bf16 var rows of a bf16 EV: 4 values (8 B) per float4 lane chunk, or one
+// value; widened to fp32 for the update and stored rounded to nearest even.
+typedef unsigned int ab_u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 apply_ldw(const ab_u2* p) {
+#ifdef DR_APPLY_NO_NT
+  const ab_u2 v = *gp(p);
+#else
+  const ab_u2 v = __builtin_nontemporal_load(gp(p));
+#endif
+  const float2 a = bf16x2_to_f2(v.x), b = bf16x2_to_f2(v.y);
+  return make_float4(a.x, a.y, b.x, b.y);
+}
+__device__ __forceinline__ float apply_ldw(const uint16_t* p) { return bf16_to_f32(gld(p)); }
+__device__ __forceinline__ void apply_stw(ab_u2* p, float4 w) {
+  const ab_u2 v = {f2_to_bf16x2(w.x, w.y), f2_to_bf16x2(w.z, w.w)};
+#ifdef DR_APPLY_NO_NT
+  *gp(p) = v;
+#else
+  __builtin_nontemporal_store(v, gp(p));
+#endif
+}
+__device__ __forceinline__ void apply_stw(uint16_t* p, float w) { gst(p, bf16_rne(w)); }
+
 template <class V>
 __device__ __forceinline__ V apply_grad_load(uint64_t a, int64_t c) {
   const V g = reinterpret_cast<const V*>((uintptr_t)(a & ~(uint64_t)1))[c];
   return (a & 1) ? vadd(vzero<V>(), g) : g;
 }
 
-template <int OPT, int VEC, int G>
+// WB: the var column holds bf16 values (bf16 EV); gradients and optimizer
+// slots stay fp32, the updated value is rounded to bf16 once per step.
+template <int OPT, int VEC, int G, bool WB = false>
 __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t dim, int64_t gs,
                                                        OptScalars sc_arg, int gind, int* st) {
   const ApplyTable& at = ag.t[blockIdx.y];
@@ -831,7 +872,10 @@ __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t di
   const int lg = lane % G;
   const int64_t dv = dim / VEC;
   using V = typename std::conditional<VEC == 4, float4, float>::type;
-  const V* d0 = reinterpret_cast<const V*>(cols.dflt[0]);
+  using WT = typename std::conditional<WB, typename std::conditional<VEC == 4, ab_u2, uint16_t>::type,
+                                       V>::type;
+  const WT* d0 = reinterpret_cast<const WT*>(cols.dflt[0]);
+  const V* dg = reinterpret_cast<const V*>(cols.dflt[WB ? 1 : 0]);  // any readable row
   const V* d1 = reinterpret_cast<const V*>(cols.dflt[1]);
   const V* d2 = reinterpret_cast<const V*>(cols.dflt[2]);
   for (int k0 = 0; k0 < 64; k0 += P * U) {
@@ -842,7 +886,7 @@ __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t di
     // issue back to back.  A "pointer or default" select inside the loop
     // makes hipcc branch around every load and wait for it.
     const V* gp[U];
-    const V* wp[U];
+    const WT* wp[U];
     const V* ap1[U];
     const V* ap2[U];
     bool zs[U];
@@ -855,8 +899,10 @@ __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t di
       const bool ok = rr[q] >= 0;
       const uint64_t ga = ok ? apply_grad_addr(grad, gind, base + k, dim) : 0;
       zs[q] = ga & 1;
-      gp[q] = ok ? reinterpret_cast<const V*>((uintptr_t)(ga & ~(uint64_t)1)) : d0;
-      wp[q] = (ok && !(im & 1)) ? reinterpret_cast<const V*>(cols.pool[0] + rr[q] * dim) : d0;
+      gp[q] = ok ? reinterpret_cast<const V*>((uintptr_t)(ga & ~(uint64_t)1))
+                 : (WB && OPT == OPT_SGD ? reinterpret_cast<const V*>(cols.dflt[0]) : dg);
+      wp[q] = (ok && !(im & 1)) ? reinterpret_cast<const WT*>(cols.pool[0] + rr[q] * (WB ? dim / 2 : dim))
+                                : d0;
       ap1[q] = (OPT != OPT_SGD && ok && !(im & 2))
                    ? reinterpret_cast<const V*>(cols.pool[1] + rr[q] * dim) : d1;
       ap2[q] = (C3 && ok && !(im & 4))
@@ -881,8 +927,15 @@ __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t di
       V gv[U], w[U], a1[U], a2[U];
 #pragma unroll
       for (int q = 0; q < U; ++q) {  // all loads of U rows first, unconditional
-        gv[q] = apply_ld(gp[q] + c);
-        w[q] = apply_ld(wp[q] + c);
+        if constexpr (WB) {
+          // a skipped row of an SGD apply reads the (bf16) default for its
+          // gradient too: half a row of bytes, always readable
+          gv[q] = (OPT == OPT_SGD && rr[q] < 0) ? V{} : apply_ld(gp[q] + c);
+          w[q] = apply_ldw(wp[q] + c);
+        } else {
+          gv[q] = apply_ld(gp[q] + c);
+          w[q] = apply_ld(wp[q] + c);
+        }
         if (OPT != OPT_SGD) a1[q] = apply_ld(ap1[q] + c);
         if (C3) a2[q] = apply_ld(ap2[q] + c);
       }
@@ -911,7 +964,10 @@ __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t di
         }
         if (OPT != OPT_SGD) apply_st(reinterpret_cast<V*>(cols.pool[1] + rr[q] * dim) + c, a1[q]);
         if (C3) apply_st(reinterpret_cast<V*>(cols.pool[2] + rr[q] * dim) + c, a2[q]);
-        apply_st(reinterpret_cast<V*>(cols.pool[0] + rr[q] * dim) + c, w[q]);
+        if constexpr (WB)
+          apply_stw(reinterpret_cast<WT*>(cols.pool[0] + rr[q] * (dim / 2)) + c, w[q]);
+        else
+          apply_st(reinterpret_cast<V*>(cols.pool[0] + rr[q] * dim) + c, w[q]);
       }
     }
   }
@@ -1033,7 +1089,8 @@ __global__ __launch_bounds__(256) void ev_apply_ftrl_kernel(ApplyGroup ag, int64
 // recycled ("TODO memory recycle" in the reference too).
 // ---------------------------------------------------------------------------
 __global__ void ev_shrink_mark_kernel(Slot* __restrict__ slots, int64_t cap, const float* pool,
-                                      const float* dflt, int64_t dim, int64_t* __restrict__ version,
+                                      const float* dflt, int64_t dim, int bf16,
+                                      int64_t* __restrict__ version,
                                       int mode, float l2_threshold, int64_t gs,
                                       int64_t steps_to_live, uint8_t* __restrict__ keep,
                                       unsigned long long* __restrict__ nremoved) {
@@ -1045,9 +1102,18 @@ __global__ void ev_shrink_mark_kernel(Slot* __restrict__ slots, int64_t cap, con
   if (occupied && sl.rc != kUnset && (sl.rc & kRowMask) != kRowDead) {
     const int64_t row = (int64_t)(sl.rc & kRowMask);
     if (mode == 1) {
-      const float* v = (sl.rc & (1ull << 48)) ? pool + row * dim : dflt;
       float l2 = 0.f;
-      for (int64_t j = 0; j < dim; ++j) l2 += v[j] * v[j];
+      if (bf16) {  // dim bf16 values, widened (fp32 sum in element order)
+        const uint16_t* v = reinterpret_cast<const uint16_t*>(
+            (sl.rc & (1ull << 48)) ? pool + row * (dim / 2) : dflt);
+        for (int64_t j = 0; j < dim; ++j) {
+          const float x = bf16_to_f32(v[j]);
+          l2 += x * x;
+        }
+      } else {
+        const float* v = (sl.rc & (1ull << 48)) ? pool + row * dim : dflt;
+        for (int64_t j = 0; j < dim; ++j) l2 += v[j] * v[j];
+      }
       l2 *= 0.5f;
       if (l2 < l2_threshold) k = 0;
     } else if (mode == 2 && version) {
@@ -1144,10 +1210,19 @@ static void bloom_seeds(int64_t k, std::vector<uint64_t>* out) {
 }
 
 static int alloc_pool(EvShared* s, int col, const float* default_row_host) {
-  DR_HIP(hipMalloc(&s->pools[col], (size_t)s->row_cap * s->dim * sizeof(float)));
-  DR_HIP(hipMalloc(&s->defaults[col], (size_t)s->dim * sizeof(float)));
-  DR_HIP(hipMemcpy(s->defaults[col], default_row_host, s->dim * sizeof(float),
-                   hipMemcpyHostToDevice));
+  const int64_t w = col_words(s, col);
+  DR_HIP(hipMalloc(&s->pools[col], (size_t)s->row_cap * w * sizeof(float)));
+  DR_HIP(hipMalloc(&s->defaults[col], (size_t)w * sizeof(float)));
+  if (w != s->dim) {
+    // bf16 column: the fp32 default row rounded to nearest even
+    std::vector<uint16_t> b((size_t)s->dim);
+    for (int64_t c = 0; c < s->dim; ++c) b[(size_t)c] = bf16_rne_host(default_row_host[c]);
+    DR_HIP(hipMemcpy(s->defaults[col], b.data(), b.size() * sizeof(uint16_t),
+                     hipMemcpyHostToDevice));
+  } else {
+    DR_HIP(hipMemcpy(s->defaults[col], default_row_host, s->dim * sizeof(float),
+                     hipMemcpyHostToDevice));
+  }
   return DR_OK;
 }
 
@@ -1189,17 +1264,18 @@ static int grow(EvShared* s, int64_t need, hipStream_t st) {
     int64_t nrc = std::max(need, s->row_cap * 2);
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess &&
-        (size_t)nrc * s->dim * sizeof(float) > fr) {
+        (size_t)nrc * col_words(s, 0) * sizeof(float) > fr) {
       set_error("EV row pool growth %lld -> %lld rows (need %lld) needs %zu bytes, %zu free",
                 (long long)s->row_cap, (long long)nrc, (long long)need,
-                (size_t)nrc * s->dim * sizeof(float), fr);
+                (size_t)nrc * col_words(s, 0) * sizeof(float), fr);
       return DR_RESOURCE_EXHAUSTED;
     }
     for (int c = 0; c < kMaxCols; ++c) {
       if (!s->pools[c]) continue;
+      const int64_t w = col_words(s, c);
       float* np = nullptr;
-      DR_HIP(hipMalloc(&np, (size_t)nrc * s->dim * sizeof(float)));
-      DR_HIP(hipMemcpyAsync(np, s->pools[c], (size_t)s->row_cap * s->dim * sizeof(float),
+      DR_HIP(hipMalloc(&np, (size_t)nrc * w * sizeof(float)));
+      DR_HIP(hipMemcpyAsync(np, s->pools[c], (size_t)s->row_cap * w * sizeof(float),
                             hipMemcpyDeviceToDevice, st));
       DR_HIP(hipStreamSynchronize(st));
       DR_HIP(hipFree(s->pools[c]));
@@ -1334,8 +1410,8 @@ static int resolve_grouped(dr_ev* const* evs, int T, const int64_t* keys, const 
     ig.koff[t] = g.koff[t];
     ig.n_dev[t] = g.n_dev[t];
     any_bloom |= g.e[t].k_hash > 0;
-    DR_REQUIRE(evs[t]->sh->dim == evs[0]->sh->dim, DR_INVALID_ARGUMENT,
-               "grouped EVs must share dim");
+    DR_REQUIRE(col_words(evs[t]->sh, evs[t]->col) == col_words(evs[0]->sh, evs[0]->col),
+               DR_INVALID_ARGUMENT, "grouped EVs must share dim and value type");
   }
   g.koff[T] = total;
   ig.koff[T] = total;
@@ -1362,7 +1438,7 @@ static int resolve_grouped(dr_ev* const* evs, int T, const int64_t* keys, const 
     }
   }
   hipLaunchKernelGGL(ev_init_rows_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, st, ig,
-                     T, evs[0]->sh->dim, rows_out, w.init);
+                     T, col_words(evs[0]->sh, evs[0]->col), rows_out, w.init);
   const hipError_t le = hipGetLastError();
   for (int q = 0; q < nmir; ++q) {
     if (le == hipSuccess) mirrored(mir[q], st);
@@ -1414,6 +1490,8 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
     DR_REQUIRE(vars[t]->sh->value_words == 1, DR_INVALID_ARGUMENT,
                "table %d: the KvResourceSparseApply* kernels are registered for float values "
                "only (training_ali_ops.cc)", t);
+    DR_REQUIRE(!vars[t]->sh->bf16 || opt != OPT_FTRL, DR_INVALID_ARGUMENT,
+               "table %d: FTRL is not built for bf16 EVs", t);
     if (n_host[t] > 0) {
       int rc = reserve(vars[t]->sh, n_host[t], st);
       if (rc) return rc;
@@ -1429,7 +1507,8 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
       const int t = c0 + j;
       dr_ev* var = vars[t];
       EvShared* s = var->sh;
-      DR_REQUIRE(s->dim == dim, DR_INVALID_ARGUMENT, "grouped apply needs equal dims");
+      DR_REQUIRE(s->dim == dim && s->bf16 == vars[0]->sh->bf16, DR_INVALID_ARGUMENT,
+                 "grouped apply needs equal dims and value types");
       dr_ev* cv[3] = {var, s1 ? s1[t] : nullptr, s2 ? s2[t] : nullptr};
       ApplyTable& a = ag.t[j];
       a.cols.ncol = ncol;
@@ -1460,40 +1539,51 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
     }
     if (nmax == 0) continue;
     const dim3 grid((unsigned)ceil_div(nmax, 256), (unsigned)tn);
-#define DR_APPLY(VEC, G)                                                                    \
+#define DR_APPLY(VEC, G, WB)                                                                    \
   do {                                                                                     \
     if (opt == OPT_SGD)                                                                    \
-      hipLaunchKernelGGL((ev_apply_kernel<OPT_SGD, VEC, G>), grid, dim3(256), 0, st, ag,    \
+      hipLaunchKernelGGL((ev_apply_kernel<OPT_SGD, VEC, G, WB>), grid, dim3(256), 0, st, ag,    \
                          dim, gs, sc, gind, stw);                                           \
     else if (opt == OPT_ADAGRAD)                                                           \
-      hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAGRAD, VEC, G>), grid, dim3(256), 0, st, ag,\
+      hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAGRAD, VEC, G, WB>), grid, dim3(256), 0, st, ag,\
                          dim, gs, sc, gind, stw);                                           \
     else if (opt == OPT_FTRL)                                                              \
       hipLaunchKernelGGL((ev_apply_ftrl_kernel<VEC, G>), grid, dim3(256), 0, st, ag, dim,   \
                          gs, sc, gind, stw);                                                \
     else if (opt == OPT_ADAM_ASYNC)                                                        \
-      hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAM_ASYNC, VEC, G>), grid, dim3(256), 0, st, \
+      hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAM_ASYNC, VEC, G, WB>), grid, dim3(256), 0, st, \
                          ag, dim, gs, sc, gind, stw);                                       \
     else if (opt == OPT_ADAM_RMSPROP)                                                      \
-      hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAM_RMSPROP, VEC, G>), grid, dim3(256), 0,   \
+      hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAM_RMSPROP, VEC, G, WB>), grid, dim3(256), 0,   \
                          st, ag, dim, gs, sc, gind, stw);                                   \
     else if (opt == OPT_ADAGRAD_DECAY)                                                     \
-      hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAGRAD_DECAY, VEC, G>), grid, dim3(256), 0,  \
+      hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAGRAD_DECAY, VEC, G, WB>), grid, dim3(256), 0,  \
                          st, ag, dim, gs, sc, gind, stw);                                   \
     else                                                                                   \
-      hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAM, VEC, G>), grid, dim3(256), 0, st, ag,   \
+      hipLaunchKernelGGL((ev_apply_kernel<OPT_ADAM, VEC, G, WB>), grid, dim3(256), 0, st, ag,   \
                          dim, gs, sc, gind, stw);                                           \
   } while (0)
-    if (aligned && dim / 4 <= 8)
-      DR_APPLY(4, 8);
+    const bool wb = vars[c0]->sh->bf16 != 0;
+    if (wb && aligned && dim / 4 <= 8)
+      DR_APPLY(4, 8, true);
+    else if (wb && aligned && dim / 4 <= 16)
+      DR_APPLY(4, 16, true);
+    else if (wb && aligned && dim / 4 <= 32)
+      DR_APPLY(4, 32, true);
+    else if (wb && aligned)
+      DR_APPLY(4, 64, true);
+    else if (wb)
+      DR_APPLY(1, 64, true);
+    else if (aligned && dim / 4 <= 8)
+      DR_APPLY(4, 8, false);
     else if (aligned && dim / 4 <= 16)
-      DR_APPLY(4, 16);
+      DR_APPLY(4, 16, false);
     else if (aligned && dim / 4 <= 32)
-      DR_APPLY(4, 32);
+      DR_APPLY(4, 32, false);
     else if (aligned)
-      DR_APPLY(4, 64);
+      DR_APPLY(4, 64, false);
     else
-      DR_APPLY(1, 64);
+      DR_APPLY(1, 64, false);
 #undef DR_APPLY
     DR_LAUNCH_CHECK();
   }
@@ -1848,9 +1938,13 @@ static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t 
   size_t need = 0;
   carve_lookup(nullptr, n, &need);
   DR_REQUIRE(ws_bytes >= need, DR_INVALID_ARGUMENT, "lookup workspace too small");
-  const int64_t dim = evs[0]->sh->dim;
+  // float words per row: bf16 EVs are copied bitwise as D / 2 words into a
+  // bf16 output (out_stride counts float words as well)
+  const int64_t dim = col_words(evs[0]->sh, evs[0]->col);
   DR_REQUIRE(dim % 4 == 0 && dim <= 256, DR_INVALID_ARGUMENT,
-             "fused one-hot lookup needs dim %% 4 == 0 and dim <= 256");
+             "fused one-hot lookup needs row words %% 4 == 0 and <= 256");
+  DR_REQUIRE(!evs[0]->sh->bf16 || order == DR_ORDER_ALI, DR_INVALID_ARGUMENT,
+             "bf16 EV lookups pool in the ALI order");
   DR_REQUIRE(out_stride >= (int64_t)T * dim && (out_stride % 4) == 0 &&
                  ((uintptr_t)out & 15) == 0,
              DR_INVALID_ARGUMENT, "out must be 16-B aligned with stride >= T*dim (multiple of 4)");
@@ -1859,9 +1953,10 @@ static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t 
   DR_REQUIRE(stw, DR_INTERNAL, "status word unavailable");
   for (int t = 0; t < T; ++t) {
     const EvShared* s = evs[t]->sh;
-    DR_REQUIRE(s->dim == dim, DR_INVALID_ARGUMENT, "tables must share dim");
+    DR_REQUIRE(col_words(s, evs[t]->col) == dim && s->bf16 == evs[0]->sh->bf16,
+               DR_INVALID_ARGUMENT, "tables must share dim and value type");
     DR_REQUIRE(s->value_words == 1, DR_INVALID_ARGUMENT,
-               "table %d: pooled lookups are fp32 (double EVs: dr_ev_gather)", t);
+               "table %d: pooled lookups are fp32 / bf16 (double EVs: dr_ev_gather)", t);
     DR_REQUIRE(s->filter_freq == 0 && s->k_hash == 0, DR_INVALID_ARGUMENT,
                "table %d: the fused lookup is for filter-free EVs", t);
     DR_REQUIRE(((uintptr_t)s->pools[evs[t]->col] & 15) == 0, DR_INVALID_ARGUMENT,
@@ -1962,12 +2057,16 @@ int dr_ev_create(const dr_ev_config* cfg, const float* default_row_host, dr_ev**
   DR_REQUIRE(cfg && out && default_row_host, DR_INVALID_ARGUMENT, "null argument");
   DR_REQUIRE(cfg->dim > 0, DR_INVALID_ARGUMENT, "dim must be > 0");
   DR_REQUIRE(cfg->steps_to_live >= 0, DR_INVALID_ARGUMENT, "steps_to_live must >= 0");
-  DR_REQUIRE(cfg->value_bits == 0 || cfg->value_bits == 32 || cfg->value_bits == 64,
-             DR_INVALID_ARGUMENT, "value_bits must be 32 (float) or 64 (double)");
+  DR_REQUIRE(cfg->value_bits == 0 || cfg->value_bits == 16 || cfg->value_bits == 32 ||
+                 cfg->value_bits == 64,
+             DR_INVALID_ARGUMENT, "value_bits must be 16 (bf16), 32 (float) or 64 (double)");
+  DR_REQUIRE(cfg->value_bits != 16 || cfg->dim % 2 == 0, DR_INVALID_ARGUMENT,
+             "bf16 EVs need an even dim (rows are moved as float words)");
   EvShared* s = new (std::nothrow) EvShared();
   DR_REQUIRE(s, DR_RESOURCE_EXHAUSTED, "host allocation failed");
   (void)hipGetDevice(&s->device);
   s->value_words = cfg->value_bits == 64 ? 2 : 1;
+  s->bf16 = cfg->value_bits == 16;
   s->dim = cfg->dim * s->value_words;
   s->filter_freq = cfg->filter_freq < 0 ? 0 : cfg->filter_freq;
   s->steps_to_live = cfg->steps_to_live;
@@ -2067,7 +2166,9 @@ int64_t dr_ev_row_capacity(dr_ev* ev) { return ev ? ev->sh->row_cap : -1; }
 
 int64_t dr_ev_filter_freq(dr_ev* ev) { return ev ? ev->sh->filter_freq : -1; }
 
-int dr_ev_value_bits(dr_ev* ev) { return ev ? 32 * ev->sh->value_words : -1; }
+int dr_ev_value_bits(dr_ev* ev) {
+  return ev ? (ev->sh->bf16 && ev->col == 0 ? 16 : 32 * ev->sh->value_words) : -1;
+}
 
 // MaybeLockEmbeddingVariableInputMutexesInOrder (training_ali_op_helpers.h:
 // 85-118) for stream-ordered updates: the host mutexes are taken in address
@@ -2129,7 +2230,7 @@ int dr_ev_shrink(dr_ev* ev, int64_t global_step, float l2_weight_threshold,
   if (removed_host) *removed_host = 0;
   if (mode == 0) return DR_OK;
   DR_REQUIRE(mode == 2 || s->value_words == 1, DR_INVALID_ARGUMENT,
-             "l2-weight shrink is for float EVs");
+             "l2-weight shrink is for float / bf16 EVs");
   std::lock_guard<std::mutex> g(s->mu);
   const int64_t n = s->cap + 1;
   uint8_t* keep = nullptr;
@@ -2151,7 +2252,7 @@ int dr_ev_shrink(dr_ev* ev, int64_t global_step, float l2_weight_threshold,
   if (!rc) {
     const unsigned blocks = (unsigned)ceil_div(n, 256);
     hipLaunchKernelGGL(ev_shrink_mark_kernel, dim3(blocks), dim3(256), 0, st, s->slots, s->cap,
-                       s->pools[0], s->defaults[0], s->dim, s->version, mode,
+                       s->pools[0], s->defaults[0], s->dim, s->bf16, s->version, mode,
                        l2_weight_threshold, global_step, s->steps_to_live, keep, cnt);
     hipLaunchKernelGGL(ev_rehash_kept_kernel, dim3(blocks), dim3(256), 0, st, s->slots, s->cap,
                        keep, ns);
@@ -2276,10 +2377,11 @@ int dr_ev_gather_tagged(dr_ev* const* evs, int num_tables, const int32_t* tags,
   if (n == 0) return DR_OK;
   PoolGroup pg;
   memset(&pg, 0, sizeof(pg));
-  const int64_t dim = evs[0]->sh->dim;
+  const int64_t dim = col_words(evs[0]->sh, evs[0]->col);  // float words (bf16: D / 2)
   for (int t = 0; t < num_tables; ++t) {
-    DR_REQUIRE(evs[t]->sh->dim == dim && evs[t]->sh->value_words == 1, DR_INVALID_ARGUMENT,
-               "tables must be float EVs sharing dim");
+    DR_REQUIRE(col_words(evs[t]->sh, evs[t]->col) == dim && evs[t]->sh->value_words == 1 &&
+                   evs[t]->sh->bf16 == evs[0]->sh->bf16,
+               DR_INVALID_ARGUMENT, "tables must be float (or bf16) EVs sharing dim");
     pg.pool[t] = evs[t]->sh->pools[evs[t]->col];
     pg.dflt[t] = evs[t]->sh->defaults[evs[t]->col];
   }
@@ -2306,7 +2408,7 @@ int dr_ev_gather(dr_ev* ev, const int64_t* keys, int64_t n, const float* default
   DR_REQUIRE(ws_bytes >= c.used, DR_INVALID_ARGUMENT, "workspace too small");
   int rc = dr_ev_resolve(ev, keys, n, nullptr, defaults, counts, rows, rws, rneed, stream);
   if (rc) return rc;
-  return gather_ev_rows(ev->sh->pools[ev->col], ev->sh->dim, rows, n, defaults,
+  return gather_ev_rows(ev->sh->pools[ev->col], col_words(ev->sh, ev->col), rows, n, defaults,
                         ev->sh->defaults[ev->col], out, S(stream));
 }
 
@@ -2343,7 +2445,7 @@ int dr_ev_insert(dr_ev* ev, const int64_t* keys, int64_t n, const float* values,
   ig.koff[0] = 0;
   ig.koff[1] = n;
   hipLaunchKernelGGL(ev_init_rows_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, ig, 1,
-                     ev->sh->dim, rows, init);
+                     col_words(ev->sh, ev->col), rows, init);
   DR_LAUNCH_CHECK();
   DR_HIP(hipFreeAsync(rows, st));
   DR_HIP(hipFreeAsync(init, st));
@@ -2372,7 +2474,8 @@ int dr_ev_insert_synthetic(dr_ev* ev, int64_t key_begin, int64_t key_stride, int
     hipLaunchKernelGGL(ev_insert_range_kernel, dim3((unsigned)ceil_div(m, 256)), dim3(256), 0, st,
                        e, key_begin + b * key_stride, key_stride, m, rows, init, status_word());
     hipLaunchKernelGGL(ev_synth_rows_kernel, dim3((unsigned)ceil_div(m, 4)), dim3(256), 0, st,
-                       ev->sh->pools[ev->col], ev->sh->dim, key_begin + b * key_stride,
+                       ev->sh->pools[ev->col], ev->sh->dim, ev->sh->bf16 && ev->col == 0,
+                       key_begin + b * key_stride,
                        key_stride, m, rows, init, seed);
     DR_LAUNCH_CHECK();
   }
@@ -2467,7 +2570,7 @@ int dr_ev_export(dr_ev* ev, int64_t* keys_out, float* values_out, int64_t* versi
     int64_t* drows = nullptr;
     DR_HIP(hipMalloc(&drows, m * sizeof(int64_t)));
     DR_HIP(hipMemcpy(drows, rows.data(), m * sizeof(int64_t), hipMemcpyHostToDevice));
-    int rc = dr_gather(s->pools[ev->col], top, s->dim, drows, m, values_out, stream);
+    int rc = dr_gather(s->pools[ev->col], top, col_words(s, ev->col), drows, m, values_out, stream);
     (void)hipStreamSynchronize(st);
     (void)hipFree(drows);
     if (rc) return rc;
@@ -2878,18 +2981,21 @@ int dr_xgmi_serve(const dr_xgmi_peers* peers, dr_ev* const* evs, int num_tables,
              DR_INVALID_ARGUMENT, "bad world/rank/cap");
   DR_REQUIRE(ws_bytes >= dr_xgmi_serve_workspace_size(W, peers->cap), DR_INVALID_ARGUMENT,
              "serve workspace too small");
-  const int64_t dim = evs[0]->sh->dim;
+  // float words per row (bf16 EVs: D / 2 words, rows moved bitwise -- the
+  // bf16 wire format halves the link bytes)
+  const int64_t dim = col_words(evs[0]->sh, evs[0]->col);
   DR_REQUIRE(dim % 4 == 0 && dim <= 256, DR_INVALID_ARGUMENT,
-             "xgmi serve needs dim %% 4 == 0 and dim <= 256 (got %lld)", (long long)dim);
+             "xgmi serve needs row words %% 4 == 0 and <= 256 (got %lld)", (long long)dim);
   XgmiResolveArgs ra;
   memset(&ra, 0, sizeof(ra));
   XgmiRowArgs wa;
   memset(&wa, 0, sizeof(wa));
   for (int t = 0; t < num_tables; ++t) {
     const EvShared* s = evs[t]->sh;
-    DR_REQUIRE(s->dim == dim, DR_INVALID_ARGUMENT, "tables must share dim");
+    DR_REQUIRE(col_words(s, evs[t]->col) == dim && s->bf16 == evs[0]->sh->bf16,
+               DR_INVALID_ARGUMENT, "tables must share dim and value type");
     DR_REQUIRE(s->filter_freq == 0 && s->k_hash == 0 && s->value_words == 1,
-               DR_INVALID_ARGUMENT, "table %d: xgmi serve is for filter-free fp32 EVs", t);
+               DR_INVALID_ARGUMENT, "table %d: xgmi serve is for filter-free fp32 / bf16 EVs", t);
     ra.e[t] = make_desc(evs[t]);
     wa.pool[t] = s->pools[evs[t]->col];
     wa.dflt[t] = s->defaults[evs[t]->col];

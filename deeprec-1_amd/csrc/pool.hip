@@ -79,17 +79,34 @@ __device__ __forceinline__ void clip_row(Row<VEC, G, CPL>& x, float max_norm) {
   }
 }
 
-template <int VEC, int G, int CPL, int ORDER>
+// BF: the rows hold bf16 values (bf16 EV / table), widened to fp32 on load;
+// `dim` passed to select_row then counts float words (D / 2).
+template <int VEC, int G, int CPL, bool BF>
+__device__ __forceinline__ void load_any(Row<VEC, G, CPL>& x, const float* p, int lg, int dv) {
+  if constexpr (BF)
+    load_row_bf16<VEC, G, CPL>(x, p, lg, dv);
+  else
+    load_row<VEC, G, CPL>(x, p, lg, dv);
+}
+template <int VEC, int G, int CPL, bool BF>
+__device__ __forceinline__ void store_any(const Row<VEC, G, CPL>& x, float* p, int lg, int dv) {
+  if constexpr (BF)
+    store_row_bf16<VEC, G, CPL>(x, p, lg, dv);
+  else
+    store_row<VEC, G, CPL>(x, p, lg, dv);
+}
+
+template <int VEC, int G, int CPL, int ORDER, bool BF = false>
 __device__ __forceinline__ void fetch(Row<VEC, G, CPL>& x, const dr_pool_desc& d, int64_t k,
                                       int dim, int lg, int dv, int* st) {
-  load_row<VEC, G, CPL>(x, select_row(d, k, dim, st), lg, dv);
+  load_any<VEC, G, CPL, BF>(x, select_row(d, k, dim, st), lg, dv);
   if (d.max_norm >= 0.f) clip_row<VEC, G, CPL, ORDER>(x, d.max_norm);
 }
 
-template <int VEC, int G, int CPL, int ORDER>
+template <int VEC, int G, int CPL, int ORDER, bool BF = false>
 __device__ __forceinline__ void fetch_p(Row<VEC, G, CPL>& x, const float* p, float max_norm,
                                         int lg, int dv) {
-  load_row<VEC, G, CPL>(x, p, lg, dv);
+  load_any<VEC, G, CPL, BF>(x, p, lg, dv);
   if (max_norm >= 0.f) clip_row<VEC, G, CPL, ORDER>(x, max_norm);
 }
 
@@ -113,7 +130,7 @@ struct BagPtrs {
 
 // Unweighted bag of `num` rows, P(k) = row pointer of position k, summed in
 // the reference association order.
-template <int VEC, int G, int CPL, int ORDER, class PtrAt>
+template <int VEC, int G, int CPL, int ORDER, bool BF, class PtrAt>
 __device__ __forceinline__ void pool_bag_rows(const dr_pool_desc& d, int64_t num, float* out,
                                               int lg, int dv, const PtrAt& P) {
   using R = Row<VEC, G, CPL>;
@@ -125,10 +142,10 @@ __device__ __forceinline__ void pool_bag_rows(const dr_pool_desc& d, int64_t num
     int64_t k = 0;
     for (; k + 4 <= num; k += 4) {
       R x0, x1, x2, x3;
-      fetch_p<VEC, G, CPL, ORDER>(x0, P(k), d.max_norm, lg, dv);
-      fetch_p<VEC, G, CPL, ORDER>(x1, P(k + 1), d.max_norm, lg, dv);
-      fetch_p<VEC, G, CPL, ORDER>(x2, P(k + 2), d.max_norm, lg, dv);
-      fetch_p<VEC, G, CPL, ORDER>(x3, P(k + 3), d.max_norm, lg, dv);
+      fetch_p<VEC, G, CPL, ORDER, BF>(x0, P(k), d.max_norm, lg, dv);
+      fetch_p<VEC, G, CPL, ORDER, BF>(x1, P(k + 1), d.max_norm, lg, dv);
+      fetch_p<VEC, G, CPL, ORDER, BF>(x2, P(k + 2), d.max_norm, lg, dv);
+      fetch_p<VEC, G, CPL, ORDER, BF>(x3, P(k + 3), d.max_norm, lg, dv);
       acc_add(acc, x0);
       acc_add(acc, x1);
       acc_add(acc, x2);
@@ -136,7 +153,7 @@ __device__ __forceinline__ void pool_bag_rows(const dr_pool_desc& d, int64_t num
     }
     for (; k < num; ++k) {
       R x;
-      fetch_p<VEC, G, CPL, ORDER>(x, P(k), d.max_norm, lg, dv);
+      fetch_p<VEC, G, CPL, ORDER, BF>(x, P(k), d.max_norm, lg, dv);
       acc_add(acc, x);
     }
     if (d.combiner != DR_COMBINER_SUM) {
@@ -144,13 +161,13 @@ __device__ __forceinline__ void pool_bag_rows(const dr_pool_desc& d, int64_t num
 #pragma unroll
       for (int c = 0; c < CPL; ++c) acc.v[c] = vdiv(acc.v[c], q);
     }
-    store_row<VEC, G, CPL>(acc, out, lg, dv);
+    store_any<VEC, G, CPL, BF>(acc, out, lg, dv);
     return;
   }
   // ORDER_ALI
   if (num == 1) {
-    fetch_p<VEC, G, CPL, ORDER>(acc, P(0), d.max_norm, lg, dv);
-    store_row<VEC, G, CPL>(acc, out, lg, dv);
+    fetch_p<VEC, G, CPL, ORDER, BF>(acc, P(0), d.max_norm, lg, dv);
+    store_any<VEC, G, CPL, BF>(acc, out, lg, dv);
     return;
   }
   int64_t r = num % 8;
@@ -160,7 +177,7 @@ __device__ __forceinline__ void pool_bag_rows(const dr_pool_desc& d, int64_t num
     R x[9];
 #pragma unroll
     for (int j = 0; j < 9; ++j)
-      if (j < r) fetch_p<VEC, G, CPL, ORDER>(x[j], P(j), d.max_norm, lg, dv);
+      if (j < r) fetch_p<VEC, G, CPL, ORDER, BF>(x[j], P(j), d.max_norm, lg, dv);
     acc = x[0];
 #pragma unroll
     for (int j = 1; j < 9; ++j)
@@ -174,7 +191,7 @@ __device__ __forceinline__ void pool_bag_rows(const dr_pool_desc& d, int64_t num
   for (int64_t g = r; g < num; g += 8) {
     R x[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) fetch_p<VEC, G, CPL, ORDER>(x[j], P(g + j), d.max_norm, lg, dv);
+    for (int j = 0; j < 8; ++j) fetch_p<VEC, G, CPL, ORDER, BF>(x[j], P(g + j), d.max_norm, lg, dv);
     R s = x[0];
 #pragma unroll
     for (int j = 1; j < 8; ++j) acc_add(s, x[j]);
@@ -185,12 +202,12 @@ __device__ __forceinline__ void pool_bag_rows(const dr_pool_desc& d, int64_t num
 #pragma unroll
     for (int c = 0; c < CPL; ++c) acc.v[c] = vdiv(acc.v[c], q);
   }
-  store_row<VEC, G, CPL>(acc, out, lg, dv);
+  store_any<VEC, G, CPL, BF>(acc, out, lg, dv);
 }
 
 // One bag, general length, in the reference association order.  Called by
 // every lane of a group together (the shuffles of BagPtrs need that).
-template <int VEC, int G, int CPL, int ORDER>
+template <int VEC, int G, int CPL, int ORDER, bool BF = false>
 __device__ void pool_bag(const dr_pool_desc& d, int64_t b, int dim, int lg, int dv, int* st) {
   using R = Row<VEC, G, CPL>;
   const int64_t k0 = d.bag_off[b];
@@ -200,7 +217,7 @@ __device__ void pool_bag(const dr_pool_desc& d, int64_t b, int dim, int lg, int 
     R z;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) z.v[c] = vzero<typename VecT<VEC>::T>();
-    store_row<VEC, G, CPL>(z, out, lg, dv);
+    store_any<VEC, G, CPL, BF>(z, out, lg, dv);
     return;
   }
   if (d.weights) {
@@ -211,7 +228,7 @@ __device__ void pool_bag(const dr_pool_desc& d, int64_t b, int dim, int lg, int 
     float wsum = 0.f;
     for (int64_t k = 0; k < num; ++k) {
       R x;
-      fetch<VEC, G, CPL, ORDER>(x, d, k0 + k, dim, lg, dv, st);
+      fetch<VEC, G, CPL, ORDER, BF>(x, d, k0 + k, dim, lg, dv, st);
       const float w = d.weights[k0 + k];
 #pragma unroll
       for (int c = 0; c < CPL; ++c) acc.v[c] = vadd(acc.v[c], vmul(x.v[c], w));
@@ -222,7 +239,7 @@ __device__ void pool_bag(const dr_pool_desc& d, int64_t b, int dim, int lg, int 
 #pragma unroll
       for (int c = 0; c < CPL; ++c) acc.v[c] = vdiv(acc.v[c], q);
     }
-    store_row<VEC, G, CPL>(acc, out, lg, dv);
+    store_any<VEC, G, CPL, BF>(acc, out, lg, dv);
     return;
   }
   if (G >= 8 && num <= 4 * G) {
@@ -233,11 +250,11 @@ __device__ void pool_bag(const dr_pool_desc& d, int64_t b, int dim, int lg, int 
       const int64_t k = (int64_t)w * G + lg;
       bp.p[w] = k < num ? select_row(d, k0 + k, dim, st) : nullptr;
     }
-    pool_bag_rows<VEC, G, CPL, ORDER>(d, num, out, lg, dv,
+    pool_bag_rows<VEC, G, CPL, ORDER, BF>(d, num, out, lg, dv,
                                       [&](int64_t k) { return bp.at(k); });
     return;
   }
-  pool_bag_rows<VEC, G, CPL, ORDER>(d, num, out, lg, dv,
+  pool_bag_rows<VEC, G, CPL, ORDER, BF>(d, num, out, lg, dv,
                                     [&](int64_t k) { return select_row(d, k0 + k, dim, st); });
 }
 
@@ -347,7 +364,9 @@ __global__ __launch_bounds__(256) void pool_fast_kernel(PoolArgs args, int T, in
 // chunk of NB bags left most of the chip idle), over a capped grid that
 // strides through the bags so the per-block descriptor staging and the
 // early exits of fast chunks stay cheap.
-template <int VEC, int G, int CPL, int ORDER, int NB>
+// BF: bf16 rows and output; `dim` = float words per row (D / 2), the lane
+// layout covers D values in chunks of VEC (dv = 2 * dim / VEC).
+template <int VEC, int G, int CPL, int ORDER, int NB, bool BF = false>
 __global__ __launch_bounds__(256) void pool_general_kernel(PoolArgs args, int T, int64_t B,
                                                            int dim, int* st) {
   __shared__ dr_pool_desc sd[DR_MAX_GROUP];  // per-group table index: stage in LDS
@@ -355,7 +374,7 @@ __global__ __launch_bounds__(256) void pool_general_kernel(PoolArgs args, int T,
   __syncthreads();
   constexpr int GPB = 256 / G;
   const int lg = threadIdx.x % G;
-  const int dv = dim / VEC;
+  const int dv = (BF ? 2 * dim : dim) / VEC;
   const int64_t total = (int64_t)T * B;
   for (int64_t item = (int64_t)blockIdx.x * GPB + threadIdx.x / G; item < total;
        item += (int64_t)gridDim.x * GPB) {
@@ -364,7 +383,7 @@ __global__ __launch_bounds__(256) void pool_general_kernel(PoolArgs args, int T,
     const dr_pool_desc& d = sd[t];
     int off[NB + 1];
     if (chunk_is_fast<NB>(d, b - b % NB, B, off)) continue;  // taken by pool_fast_kernel
-    pool_bag<VEC, G, CPL, ORDER>(d, b, dim, lg, dv, st);
+    pool_bag<VEC, G, CPL, ORDER, BF>(d, b, dim, lg, dv, st);
   }
 }
 
@@ -388,12 +407,52 @@ static int launch_pool(const PoolArgs& a, int T, int64_t B, int dim, int flags, 
     const unsigned blocks = (unsigned)ceil_div((int64_t)T * cpt, 256 / G);
     hipLaunchKernelGGL((pool_fast_kernel<VEC, G, CPL, ORDER, kChunkNB>), dim3(blocks), dim3(256),
                        0, s, a, T, B, dim, cpt, st);
-    const int64_t gblocks = std::min<int64_t>(ceil_div((int64_t)T * B, 256 / G), kGeneralBlocks);
-    hipLaunchKernelGGL((pool_general_kernel<VEC, G, CPL, ORDER, kChunkNB>), dim3((unsigned)gblocks),
-                       dim3(256), 0, s, a, T, B, dim, st);
+    if (!(flags & 2)) {  // (2: fast kernel only -- the bf16 dispatcher's copies)
+      const int64_t gblocks = std::min<int64_t>(ceil_div((int64_t)T * B, 256 / G), kGeneralBlocks);
+      hipLaunchKernelGGL((pool_general_kernel<VEC, G, CPL, ORDER, kChunkNB>),
+                         dim3((unsigned)gblocks), dim3(256), 0, s, a, T, B, dim, st);
+    }
   }
   DR_LAUNCH_CHECK();
   return DR_OK;
+}
+
+// bf16 rows (DR_POOL_BF16): one-hot copies and single-id chunks are bitwise
+// row copies of D / 2 float words (the fp32 kernels on words); multi-hot
+// bags, weights and max_norm pool in fp32 and round the bag once to bf16.
+template <int G, int CPL>
+static int launch_pool_bf16_general(const PoolArgs& a, int T, int64_t B, int words, hipStream_t s,
+                                    int* st) {
+  const int64_t gblocks = std::min<int64_t>(ceil_div((int64_t)T * B, 256 / G), kGeneralBlocks);
+  hipLaunchKernelGGL((pool_general_kernel<4, G, CPL, DR_ORDER_ALI, kChunkNB, true>),
+                     dim3((unsigned)gblocks), dim3(256), 0, s, a, T, B, words, st);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+template <int ORDER>
+static int dispatch_pool(const PoolArgs& a, int T, int64_t B, int dim, int flags, hipStream_t s,
+                         int* st);
+
+static int dispatch_pool_bf16(const PoolArgs& a, int T, int64_t B, int D, int flags, hipStream_t s,
+                              int* st) {
+  const int words = D / 2;
+  // copies: every one-hot slot, or the single-id chunks of a multi-hot launch
+  // (launch_pool's fast kernel takes exactly those; its general kernel is
+  // replaced by the bf16 one below)
+  if (flags & POOL_ONEHOT) return dispatch_pool<DR_ORDER_ALI>(a, T, B, words, flags, s, st);
+  int rc = dispatch_pool<DR_ORDER_ALI>(a, T, B, words, flags | 2 /* fast only */, s, st);
+  if (rc) return rc;
+  const int d4 = D / 4;
+  if (d4 <= 4) return launch_pool_bf16_general<4, 1>(a, T, B, words, s, st);
+  if (d4 <= 8) return launch_pool_bf16_general<8, 1>(a, T, B, words, s, st);
+  if (d4 <= 16) return launch_pool_bf16_general<16, 1>(a, T, B, words, s, st);
+  if (d4 <= 32) return launch_pool_bf16_general<32, 1>(a, T, B, words, s, st);
+  if (d4 <= 64) return launch_pool_bf16_general<64, 1>(a, T, B, words, s, st);
+  if (d4 <= 128) return launch_pool_bf16_general<64, 2>(a, T, B, words, s, st);
+  if (d4 <= 256) return launch_pool_bf16_general<64, 4>(a, T, B, words, s, st);
+  set_error("bf16 dim %d unsupported (max 1024)", D);
+  return DR_INVALID_ARGUMENT;
 }
 
 template <int ORDER>
@@ -1304,9 +1363,13 @@ int dr_pool_grouped_ex(const dr_pool_desc* descs_host, int num_tables, int64_t b
   DR_REQUIRE(num_tables >= 1 && num_tables <= DR_MAX_GROUP, DR_INVALID_ARGUMENT,
              "num_tables must be in [1, %d]", DR_MAX_GROUP);
   DR_REQUIRE(batch >= 0 && dim > 0, DR_INVALID_ARGUMENT, "bad batch/dim");
-  DR_REQUIRE((flags & ~DR_POOL_ONEHOT) == 0, DR_INVALID_ARGUMENT, "unknown flags 0x%x", flags);
+  DR_REQUIRE((flags & ~(DR_POOL_ONEHOT | DR_POOL_BF16)) == 0, DR_INVALID_ARGUMENT,
+             "unknown flags 0x%x", flags);
   if (batch == 0) return DR_OK;
   const bool onehot = flags & DR_POOL_ONEHOT;
+  const bool bf16 = flags & DR_POOL_BF16;
+  DR_REQUIRE(!bf16 || (dim % 8 == 0 && order == DR_ORDER_ALI), DR_INVALID_ARGUMENT,
+             "DR_POOL_BF16 needs dim %% 8 == 0 and the ALI order");
   DR_REQUIRE(!onehot || (int64_t)num_tables * batch < (1ll << 31), DR_INVALID_ARGUMENT,
              "DR_POOL_ONEHOT: tables x batch must be < 2^31");
   PoolArgs a;
@@ -1327,6 +1390,7 @@ int dr_pool_grouped_ex(const dr_pool_desc* descs_host, int num_tables, int64_t b
   int* st = status_word();
   DR_REQUIRE(st, DR_INTERNAL, "status word unavailable");
   hipStream_t s = S(stream);
+  if (bf16) return dispatch_pool_bf16(a, num_tables, batch, dim, flags & DR_POOL_ONEHOT, s, st);
   if (order == DR_ORDER_SEQ)
     return dispatch_pool<DR_ORDER_SEQ>(a, num_tables, batch, dim, flags, s, st);
   return dispatch_pool<DR_ORDER_ALI>(a, num_tables, batch, dim, flags, s, st);

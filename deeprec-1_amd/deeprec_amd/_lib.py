@@ -23,6 +23,7 @@ ORDER_ALI, ORDER_SEQ = 0, 1
 MAX_GROUP = 32
 MAX_PARTITIONS = 64
 POOL_ONEHOT = 1
+POOL_BF16 = 2
 
 
 class DeepRecError(RuntimeError):
@@ -289,7 +290,8 @@ def workspace(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
 
-_DL_CODES = {torch.int64: (0, 64), torch.int32: (0, 32), torch.float32: (2, 32)}
+_DL_CODES = {torch.int64: (0, 64), torch.int32: (0, 32), torch.float32: (2, 32),
+             torch.bfloat16: (4, 16)}
 
 
 def uncached_empty(shape, dtype, device):

@@ -79,12 +79,20 @@ class _Feature(object):
     sp_ids.indices (read in place, stride 2: no per-step conversion)."""
 
     def __init__(self, params, values, seg, batch, weights, combiner, max_norm, onehot=False):
-        if getattr(params, "value_dtype", torch.float32) != torch.float32:
+        vd = getattr(params, "value_dtype", torch.float32)
+        if vd != torch.float32 and not (vd == torch.bfloat16 and isinstance(params,
+                                                                           EmbeddingVariable)):
             # the pooled lookups are fp32 kernels, as the reference's fused
-            # and GPU EV lookups are (double EVs: sparse_read)
+            # and GPU EV lookups are (double EVs: sparse_read); bf16 EVs pool
+            # in fp32 and hand back bf16 (DR_POOL_BF16)
             raise _lib.DeepRecError(_lib.INVALID_ARGUMENT,
-                                    "embedding lookups pool float32 EVs; %s is %s"
+                                    "embedding lookups pool float32 / bf16 EVs; %s is %s"
                                     % (getattr(params, "name", params), params.value_dtype))
+        self.bf16 = vd == torch.bfloat16
+        if self.bf16 and (params.dim % 8 or max_norm is not None and torch.is_grad_enabled()):
+            raise _lib.DeepRecError(_lib.INVALID_ARGUMENT,
+                                    "bf16 EV lookups need dim % 8 == 0 (and no max_norm "
+                                    "when a gradient is recorded)")
         self.params = params
         # one id per row (a valid [B, 1] SparseTensor with nnz == B): bag b is
         # nnz b, so the pool kernel needs no bag offsets (DR_POOL_ONEHOT).
@@ -183,7 +191,7 @@ def _desc(f, out, out_stride):
         d.rows = ptr(f.rows)
         if f.defaults is not None:
             d.default_rows = ptr(f.defaults)
-            d.default_stride = p.dim
+            d.default_stride = p.row_words
         else:
             d.default_rows = ptr(_ev_default_dev(p))
             d.default_stride = 0
@@ -195,7 +203,7 @@ def _desc(f, out, out_stride):
     d.bag_off = None if f.bag_off is None else ptr(f.bag_off)
     d.weights = ptr(f.weights)
     d.out = out.data_ptr()
-    d.out_stride = out_stride
+    d.out_stride = out_stride   # float words (bf16 outputs: elements / 2)
     d.combiner = COMBINERS[f.combiner]
     d.max_norm = -1.0 if f.max_norm is None else float(f.max_norm)
     return d
@@ -262,7 +270,9 @@ class _LookupFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_out):
-        g = grad_out.contiguous()
+        # gradients are fp32 whatever the table dtype (a bf16 EV's pooled
+        # output hands a bf16 gradient back: widened once here)
+        g = grad_out.float().contiguous()
         dense = _queue_grads(ctx.feats, g, 0, g.shape[1], ctx.tensors)
         return (None, None, None, None) + tuple(dense)
 
@@ -325,6 +335,10 @@ class _StackFn(torch.autograd.Function):
 def embedding_stack(x0, params_list, sp_ids_list, combiner="sum"):
     """torch.stack([x0] + [embedding_lookup_sparse(p, sp) ...], 1) for EVs of
     dim x0.shape[1] (DLRM's interaction input, modelzoo/DLRM/train.py:214-219)."""
+    if any(getattr(p, "value_dtype", None) == torch.bfloat16 for p in params_list):
+        raise _lib.DeepRecError(_lib.INVALID_ARGUMENT,
+                                "embedding_stack builds the fp32 dot-interaction input; "
+                                "bf16 EVs: embedding_lookup_sparse_multi")
     feats = []
     for p, sp in zip(params_list, sp_ids_list):
         v = sp.values.to(torch.int64).contiguous()
@@ -587,9 +601,11 @@ def _fused_onehot_ok(feats):
         p = f.params
         if not (isinstance(p, EmbeddingVariable) and f.onehot and f.batch == B
                 and p.dim == D and p.device == p0.device and p.filter_freq == 0
-                and not callable(p.initializer) and f.raw_values.numel() == B):
+                and not callable(p.initializer) and f.raw_values.numel() == B
+                and p.value_dtype == p0.value_dtype):
             return False
-    return D % 4 == 0 and D <= 256 and len(feats) * B < (1 << 31)
+    W = p0.row_words
+    return W % 4 == 0 and W <= 256 and len(feats) * B < (1 << 31)
 
 
 def _record_major(feats):
@@ -624,7 +640,10 @@ def _fused_onehot(feats, order, with_rows=False):
     T = len(feats)
     dev = feats[0].raw_values.device
     koff = [t * B for t in range(T + 1)]
-    out = torch.empty((B, T * D), dtype=torch.float32, device=dev)
+    # a bf16 EV's rows are copied bitwise into a bf16 output: strides in
+    # float words (row_words = D / 2)
+    out = torch.empty((B, T * D), dtype=p0.value_dtype, device=dev)
+    W = p0.row_words
     handles = (C.c_void_p * T)(*[f.params.handle.value for f in feats])
     wsb = lib().dr_ev_lookup_onehot_workspace_size(T, B)
     ws = workspace(wsb, dev)
@@ -632,14 +651,14 @@ def _fused_onehot(feats, order, with_rows=False):
     if rec is not None:
         # the features are the columns of one record-major [B, T] id matrix:
         # read in place, in the kernel's (b, t) visiting order
-        check(lib().dr_ev_lookup_onehot_strided(handles, T, rec, T, 1, B, ptr(out), T * D, order,
+        check(lib().dr_ev_lookup_onehot_strided(handles, T, rec, T, 1, B, ptr(out), T * W, order,
                                                 None, ptr(ws), wsb, stream_handle(dev)))
         ops._post(dev)
         return out
     vals = _concat_values(feats, koff)
     if with_rows:
         rowsel = torch.empty(T * B, dtype=torch.int64, device=dev)
-        check(lib().dr_ev_lookup_onehot_rows(handles, T, ptr(vals), B, ptr(out), T * D, order,
+        check(lib().dr_ev_lookup_onehot_rows(handles, T, ptr(vals), B, ptr(out), T * W, order,
                                              ptr(rowsel), ptr(ws), wsb, stream_handle(dev)))
         group = _RowGroup(feats, vals, rowsel, koff)
         for t, f in enumerate(feats):
@@ -647,7 +666,7 @@ def _fused_onehot(feats, order, with_rows=False):
             f.rowsel = rowsel[koff[t]:koff[t + 1]]
             f.group = group
     else:
-        check(lib().dr_ev_lookup_onehot(handles, T, ptr(vals), B, ptr(out), T * D, order, ptr(ws),
+        check(lib().dr_ev_lookup_onehot(handles, T, ptr(vals), B, ptr(out), T * W, order, ptr(ws),
                                         wsb, stream_handle(dev)))
     ops._post(dev)
     return out
@@ -681,11 +700,17 @@ def _pool_all(feats, order, out=None):
     B = feats[0].batch
     dims = [f.params.dim if not torch.is_tensor(f.params) else f.params.shape[1] for f in feats]
     total = sum(dims)
+    bf16 = feats[0].bf16
+    if any(f.bf16 != bf16 for f in feats):
+        raise _lib.DeepRecError(_lib.INVALID_ARGUMENT,
+                                "one pooled output: all features bf16 EVs or none")
+    odt = torch.bfloat16 if bf16 else torch.float32
     if out is None:
-        out = torch.empty((B, total), dtype=torch.float32, device=dev)
-    elif out.shape[0] != B or out.stride(1) != 1 or out.shape[1] < total:
-        raise ValueError("out must be a [B, >= %d] view with unit column stride" % total)
-    stride = out.stride(0)
+        out = torch.empty((B, total), dtype=odt, device=dev)
+    elif out.shape[0] != B or out.stride(1) != 1 or out.shape[1] < total or out.dtype != odt:
+        raise ValueError("out must be a [B, >= %d] %s view with unit column stride" % (total, odt))
+    # strides in float words (bf16: two values per word)
+    stride = out.stride(0) // 2 if bf16 else out.stride(0)
     # group consecutive features of equal dim into <= 32-table launches
     col = 0
     i = 0
@@ -701,7 +726,7 @@ def _pool_all(feats, order, out=None):
         for f in feats[i:j]:
             descs.append(_desc(f, out[:, c:], stride))
             c += dims[i]
-        ops.pool_grouped(descs, B, dims[i], order, dev, onehot=onehot)
+        ops.pool_grouped(descs, B, dims[i], order, dev, onehot=onehot, bf16=bf16)
         col = c
         i = j
     return out

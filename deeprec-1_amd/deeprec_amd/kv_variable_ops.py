@@ -106,7 +106,9 @@ atexit.register(lambda: _DEFERRED.clear())   # the process is going away: no fre
 
 
 _KEY_DTYPES = (torch.int64, torch.int32)
-_VALUE_DTYPES = (torch.float32, torch.float64)
+# bfloat16: a build-defined bf16 EV (BASELINE configs[4]; the reference
+# registers float and double): bf16 value rows, fp32 optimizer slots
+_VALUE_DTYPES = (torch.float32, torch.float64, torch.bfloat16)
 
 
 class IndexedSlices(object):
@@ -164,11 +166,19 @@ class EmbeddingVariable(object):
         _lib.require_gpu()
         if key_dtype not in _KEY_DTYPES or value_dtype not in _VALUE_DTYPES:
             raise TypeError("EmbeddingVariable keys are int32 / int64 and values float32 / "
-                            "float64 (the reference's KvResourceGather registrations)")
+                            "float64 (the reference's KvResourceGather registrations) or "
+                            "bfloat16 (bf16 EV)")
         self.name = name
         self.dim = int(embedding_dim)
         self.key_dtype = key_dtype
-        self.value_dtype = value_dtype if _primary is None else _primary.value_dtype
+        if _primary is None:
+            self.value_dtype = value_dtype
+        else:
+            # optimizer slots of a bf16 EV keep fp32 state
+            pv = _primary.value_dtype
+            self.value_dtype = torch.float32 if pv == torch.bfloat16 else pv
+        if self.value_dtype == torch.bfloat16 and self.dim % 2:
+            raise _lib.DeepRecError(_lib.INVALID_ARGUMENT, "bf16 EVs need an even dim")
         self.device = torch.device(device) if device is not None else \
             torch.device("cuda", torch.cuda.current_device())
         self.initializer = initializer
@@ -185,8 +195,12 @@ class EmbeddingVariable(object):
         # EmbeddingConfig::l2_weight_threshold (embedding_config.h:17,28): -1 = off
         self.l2_weight_threshold = float(l2_weight_threshold)
         _flush_deferred_releases()
-        default = _default_row(initializer, self.dim, self.device, self.value_dtype)
-        self._default_host = default
+        bf16 = self.value_dtype == torch.bfloat16
+        # the C ABI takes the default row in fp32 (a bf16 EV rounds it to
+        # nearest even, as the .to(torch.bfloat16) below does)
+        default = _default_row(initializer, self.dim, self.device,
+                               torch.float32 if bf16 else self.value_dtype)
+        self._default_host = default.to(torch.bfloat16) if bf16 else default
         h = C.c_void_p()
         with torch.cuda.device(self.device):
             if _primary is None:
@@ -200,7 +214,7 @@ class EmbeddingVariable(object):
                     getattr(f, "false_positive_probability", -1.0))
                 cfg.counter_bits = int(getattr(f, "counter_bits", 64) or 64)
                 cfg.layout = 1 if (self.filter_freq or self.steps_to_live) else 0
-                cfg.value_bits = 64 if self.value_dtype == torch.float64 else 32
+                cfg.value_bits = {torch.float64: 64, torch.bfloat16: 16}.get(self.value_dtype, 32)
                 check(lib().dr_ev_create(C.byref(cfg), default.data_ptr(), C.byref(h)))
             else:
                 check(lib().dr_ev_create_slot(_primary._h, _slot_index, default.data_ptr(),
@@ -256,6 +270,16 @@ class EmbeddingVariable(object):
     def pool(self):
         """Base pointer of this EV's value rows (device)."""
         return lib().dr_ev_pool(self._h)
+
+    @property
+    def is_bf16(self):
+        return self.value_dtype == torch.bfloat16
+
+    @property
+    def row_words(self):
+        """32-bit words per value row (the kernels' row stride): dim, or
+        dim / 2 for a bf16 EV."""
+        return self.dim // 2 if self.is_bf16 else self.dim
 
     # -- ops -----------------------------------------------------------------
     def _defaults_for(self, n, ev_init_value):

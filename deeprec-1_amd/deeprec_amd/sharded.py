@@ -57,6 +57,10 @@ class HipLocal(object):
         self.device = device
         self.T = len(evs)
         self.dim = evs[0].dim
+        # bf16 EVs exchange bf16 rows (half the link bytes) and pool into a
+        # bf16 output; gradients stay fp32
+        self.value_dtype = evs[0].value_dtype
+        self.bf16 = self.value_dtype == torch.bfloat16
         self.handles = (C.c_void_p * self.T)(*[e.handle.value for e in evs])
         self.filter = any(e.filter_freq != 0 for e in evs)
 
@@ -70,7 +74,7 @@ class HipLocal(object):
         """Owner side: insert-on-miss resolve + row pack of n received keys
         (per_table: host list of how many of them belong to each table)."""
         rows = torch.empty(n, dtype=torch.int64, device=self.device)
-        out = torch.empty((n, self.dim), dtype=torch.float32, device=self.device)
+        out = torch.empty((n, self.dim), dtype=self.value_dtype, device=self.device)
         if n == 0:
             return out
         wsb = lib().dr_ev_resolve_workspace_size(n)
@@ -130,7 +134,8 @@ class HipLocal(object):
         is the received row of unique u (idx given: nnz -> unique) or of nnz
         u directly (idx None, the direct one-hot mode)."""
         T, D = self.T, self.dim
-        out = torch.empty((batch, T * D), dtype=torch.float32, device=self.device)
+        out = torch.empty((batch, T * D), dtype=self.value_dtype, device=self.device)
+        es = out.element_size()
         descs = []
         for t in range(T):
             d = DrPoolDesc()
@@ -144,12 +149,13 @@ class HipLocal(object):
             d.default_rows = rows_recv.data_ptr()
             d.default_stride = 0
             d.bag_off = None if bag_offs is None else bag_offs[t].data_ptr()
-            d.out = out.data_ptr() + 4 * t * D
-            d.out_stride = T * D
+            d.out = out.data_ptr() + es * t * D
+            d.out_stride = T * D * es // 4      # float words
             d.combiner = COMBINERS[combiner]
             d.max_norm = -1.0
             descs.append(d)
-        ops.pool_grouped(descs, batch, D, ORDER_ALI, self.device, onehot=bag_offs is None)
+        ops.pool_grouped(descs, batch, D, ORDER_ALI, self.device, onehot=bag_offs is None,
+                         bf16=self.bf16)
         return out
 
 
@@ -220,7 +226,7 @@ class ShardedLookup(object):
             recv_counts.view(-1), output_size=R)
         # 5. owner resolve + pack, 6. rows all-to-all back
         rows_s = be.resolve_pack(keys_r, tags_r, R, rc.sum(0).tolist())
-        rows_r = torch.empty((S, self.dim), dtype=torch.float32, device=dev)
+        rows_r = torch.empty((S, self.dim), dtype=rows_s.dtype, device=dev)
         self._a2a(rows_r, rows_s, send_splits, recv_splits)
         # 7. requester: (unique | nnz) position -> row in the received buffer
         rowsel = torch.zeros(T * nnz, dtype=torch.int64, device=dev)
@@ -245,7 +251,7 @@ class ShardedLookup(object):
             raise RuntimeError("backward() needs a forward(..., need_grad=True) first")
         self._saved = None
         T, G, D, be = self.T, self.world, self.dim, self.backend
-        g = grad_out.contiguous()
+        g = grad_out.float().contiguous()
         if tuple(g.shape) != (self.batch, T * D):
             raise ValueError("grad must be [%d, %d]" % (self.batch, T * D))
         # 1-2. per-unique grads, packed into the forward's send order
@@ -408,7 +414,7 @@ class XgmiBuffers(object):
     (key, slot) pairs into, the [B, T*D] output that owners write rows into,
     and the [B, T*D] gradient that owners pull rows from in backward()."""
 
-    def __init__(self, world, T, batch, dim, device, uncached=None):
+    def __init__(self, world, T, batch, dim, device, uncached=None, value_dtype=torch.float32):
         # uncached (dr_ipc_alloc): a peer's xGMI writes can never be hidden by
         # a stale line in one of this GPU's per-XCD L2s; uncached=False keeps
         # plain torch allocations (single-process tests, all "ranks" on one
@@ -422,7 +428,7 @@ class XgmiBuffers(object):
         self.inbox_keys = alloc((world, self.cap), torch.int64, device)
         self.inbox_slot = alloc((world, self.cap), torch.int32, device)
         self.inbox_cnt = alloc((world,), torch.int64, device)
-        self.out = alloc((batch, T * dim), torch.float32, device)
+        self.out = alloc((batch, T * dim), value_dtype, device)   # bf16 EVs: bf16 rows
         self.gin = alloc((batch, T * dim), torch.float32, device)
 
     def tensors(self):
@@ -457,7 +463,8 @@ class XgmiShardedLookup(object):
         self.T = len(evs)
         self.dim = evs[0].dim
         self.handles = (C.c_void_p * self.T)(*[e.handle.value for e in evs])
-        self.bufs = buffers or XgmiBuffers(world, self.T, batch, self.dim, device)
+        self.bufs = buffers or XgmiBuffers(world, self.T, batch, self.dim, device,
+                                           value_dtype=evs[0].value_dtype)
         self._bases = []
         if world == 1 and peer_buffers is None:
             peer_buffers = [self.bufs]
@@ -531,8 +538,8 @@ class XgmiShardedLookup(object):
         from .kv_variable_ops import IndexedSlices
         g = grad_out.contiguous()
         T, D, B, W = self.T, self.dim, self.batch, self.world
-        if tuple(g.shape) != (B, T * D) or g.dtype != torch.float32:
-            raise ValueError("grad must be fp32 [%d, %d]" % (B, T * D))
+        if tuple(g.shape) != (B, T * D) or not g.is_floating_point():
+            raise ValueError("grad must be [%d, %d]" % (B, T * D))
         self.bufs.gin.copy_(g)
         self._barrier()
         tcap = W * B

@@ -148,9 +148,9 @@ class _Optimizer(object):
         import ctypes as C
         groups = {}
         for var, sl in items:
-            groups.setdefault((str(var.device), var.dim), []).append((var, sl))
+            groups.setdefault((str(var.device), var.dim, var.value_dtype), []).append((var, sl))
         b1p, b2p, b1, b2, eps = self._scalars()
-        for (_, _), grp in groups.items():
+        for grp in groups.values():
             T = len(grp)
             dev = grp[0][0].device
             if (self._opt == 0 and _KNOWN_ROWS
@@ -291,8 +291,8 @@ class FtrlOptimizer(_Optimizer):
         import ctypes as C
         groups = {}
         for var, sl in items:
-            groups.setdefault((str(var.device), var.dim), []).append((var, sl))
-        for (_, _), grp in groups.items():
+            groups.setdefault((str(var.device), var.dim, var.value_dtype), []).append((var, sl))
+        for grp in groups.values():
             T = len(grp)
             dev = grp[0][0].device
             grads, fn = _grad_rows(grp, "dr_ev_apply_ftrl_grouped")
@@ -399,8 +399,8 @@ class AdamAsyncOptimizer(_Optimizer):
         import ctypes as C
         groups = {}
         for var, sl in items:
-            groups.setdefault((str(var.device), var.dim), []).append((var, sl))
-        for (_, _), grp in groups.items():
+            groups.setdefault((str(var.device), var.dim, var.value_dtype), []).append((var, sl))
+        for grp in groups.values():
             T = len(grp)
             dev = grp[0][0].device
             grads, _ = _grad_rows(grp, "dr_ev_apply_grouped")
@@ -483,8 +483,8 @@ class AdagradDecayOptimizer(_Optimizer):
         import ctypes as C
         groups = {}
         for var, sl in items:
-            groups.setdefault((str(var.device), var.dim), []).append((var, sl))
-        for (_, _), grp in groups.items():
+            groups.setdefault((str(var.device), var.dim, var.value_dtype), []).append((var, sl))
+        for grp in groups.values():
             T = len(grp)
             dev = grp[0][0].device
             grads, _ = _grad_rows(grp, "dr_ev_apply_grouped")

@@ -171,6 +171,12 @@ int dr_pool_grouped(const dr_pool_desc* descs_host, int num_tables, int64_t batc
 /* features); bag_off may be NULL and is not read; weights must be NULL and  */
 /* max_norm < 0.  Results are identical to dr_pool_grouped on such input.    */
 #define DR_POOL_ONEHOT 1
+/* DR_POOL_BF16: the pools (and default rows) hold bf16 values and the output */
+/* is bf16 (a bf16 EV, value_bits 16): `dim` counts values (multiple of 8),  */
+/* pool / out / default strides count float words (2 values each).  Bags of */
+/* one id are bitwise copies; longer bags, weights and max_norm are pooled in */
+/* fp32 in the ALI order and rounded once to bf16 (nearest even).  ALI only. */
+#define DR_POOL_BF16 2
 int dr_pool_grouped_ex(const dr_pool_desc* descs_host, int num_tables, int64_t batch,
                        int dim, int order, int flags, void* stream);
 
@@ -312,6 +318,19 @@ typedef struct {
                                      /* default rows / values / outputs are */
                                      /* doubles; the applies and pooled     */
                                      /* lookups are float-only (INVALID_ARG) */
+                                     /* or 16: bf16 EV (build-defined, the  */
+                                     /* BASELINE configs[4] DCN-v2 tables;  */
+                                     /* the reference registers float and   */
+                                     /* double only): the primary column    */
+                                     /* holds bf16 rows (default_row_host is */
+                                     /* fp32, rounded to nearest even); slot */
+                                     /* columns (optimizer state) stay fp32; */
+                                     /* gather / insert / export values and  */
+                                     /* one-hot lookup outputs are bf16;     */
+                                     /* applies (SGD / Adagrad / Adam /      */
+                                     /* AdamAsync / AdagradDecay, not FTRL)  */
+                                     /* take fp32 gradients and round the    */
+                                     /* updated value once to bf16           */
 } dr_ev_config;
 
 /* InitializeKvVariableOp primary branch (kernels/kv_variable_ops.cc:173-193). */
@@ -321,7 +340,7 @@ int dr_ev_create_slot(dr_ev* primary, int slot_index, const float* default_row_h
                       dr_ev** out);
 int dr_ev_retain(dr_ev* ev);
 int dr_ev_release(dr_ev* ev);
-/* 32 (float) or 64 (double) */
+/* 16 (bf16 primary column), 32 (float) or 64 (double) */
 int dr_ev_value_bits(dr_ev* ev);
 /* use_locking = true of the KV applies (training_ali_ops.cc:104,141,161,   */
 /* 198,217; MaybeLockEmbeddingVariableInputMutexesInOrder, training_ali_op_ */

@@ -584,7 +584,37 @@ typedef struct {
   int counter_bits;
   void* bloom;
   int64_t seeds[64];
+  /* bf16 EV (build-defined, DESIGN "bf16 EVs"): the primary's values are */
+  /* bf16; each apply computes in fp32 on the widened values and rounds    */
+  /* the updated row once to nearest even.  Slots stay fp32.               */
+  int bf16;
 } orc_ev;
+
+/* fp32 -> bf16 (round to nearest even, NaN -> 0x7FC0) -> fp32 */
+float orc_bf16_round(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7FFFFFFFu) > 0x7F800000u) {
+    u = 0x7FC00000u;
+  } else {
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    u &= 0xFFFF0000u;
+  }
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+static void orc_bf16_row(const orc_ev* ev, float* v) {
+  if (!ev->bf16) return;
+  for (int64_t d = 0; d < ev->dim; ++d) v[d] = orc_bf16_round(v[d]);
+}
+
+/* Make a primary EV a bf16 EV: its default row is rounded now, every later */
+/* apply rounds the updated rows.                                            */
+void orc_ev_set_bf16(orc_ev* ev) {
+  ev->bf16 = 1;
+  orc_bf16_row(ev, ev->default_value);
+}
 
 static orc_map* orc_map_new(void) {
   orc_map* m = (orc_map*)calloc(1, sizeof(orc_map));
@@ -909,6 +939,7 @@ int orc_ev_apply_sgd(orc_ev* var, float lr, const float* grad, const int64_t* ke
     if (e < 0) continue;
     float* v = orc_get_or_alloc(var, e, var->default_value);
     for (int64_t d = 0; d < D; ++d) { float p = lr * grad[i * D + d]; v[d] = v[d] - p; }
+    orc_bf16_row(var, v);
   }
   return ORC_OK;
 }
@@ -932,6 +963,7 @@ int orc_ev_apply_adagrad(orc_ev* var, orc_ev* accum, float lr, const float* grad
       float up = lg * rs;
       v[d] = v[d] - up;
     }
+    orc_bf16_row(var, v);
   }
   return ORC_OK;
 }
@@ -959,6 +991,7 @@ int orc_ev_apply_adam(orc_ev* var, orc_ev* m_ev, orc_ev* v_ev, float beta1_power
       float den = sqrtf(v[d]) + eps;
       w[d] = w[d] - num / den;
     }
+    orc_bf16_row(var, w);
   }
   return ORC_OK;
 }
@@ -998,6 +1031,7 @@ int orc_ev_apply_adam_async(orc_ev* var, orc_ev* m_ev, orc_ev* v_ev, float beta1
         w[d] = w[d] - num / den;
       }
     }
+    orc_bf16_row(var, w);
   }
   return ORC_OK;
 }
@@ -1034,6 +1068,7 @@ int orc_ev_apply_adagrad_decay(orc_ev* var, orc_ev* accum, orc_ev* power, float 
       float up = lg * rs;
       v[d] = v[d] - up;
     }
+    orc_bf16_row(var, v);
   }
   return ORC_OK;
 }

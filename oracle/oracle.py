@@ -56,6 +56,8 @@ def lib():
             "orc_ev_create": (p, [i64, p, i64, i64, i64, f32, i32]),
             "orc_ev_create_slot": (p, [p, i32, p]),
             "orc_ev_free": (None, [p]),
+            "orc_ev_set_bf16": (None, [p]),
+            "orc_bf16_round": (f32, [f32]),
             "orc_ev_gather": (i32, [p, p, i64, p, p, p]),
             "orc_ev_import": (i32, [p, p, i64, p, p, p, i64, i64, i64]),
             "orc_ev_size": (i64, [p]),
@@ -344,15 +346,42 @@ def crossnet_layer(x0, xl, W, b):
 # --------------------------------------------------------------------------
 # EmbeddingVariable
 # --------------------------------------------------------------------------
+def bf16_bits(x):
+    """fp32 -> bf16 bit patterns (uint16): round to nearest even, NaN ->
+    0x7FC0 -- torch's c10::BFloat16 conversion, restated."""
+    u = np.ascontiguousarray(x, np.float32).view(np.uint32)
+    nan = (u & np.uint32(0x7FFFFFFF)) > np.uint32(0x7F800000)
+    with np.errstate(over="ignore"):
+        r = ((u + np.uint32(0x7FFF) + ((u >> np.uint32(16)) & np.uint32(1))) >> np.uint32(16))
+    return np.where(nan, np.uint32(0x7FC0), r).astype(np.uint16)
+
+
+def bf16_widen(h):
+    """bf16 bit patterns (uint16) -> fp32."""
+    return (np.asarray(h, np.uint16).astype(np.uint32) << np.uint32(16)).view(np.float32)
+
+
+def bf16_round(x):
+    """fp32 -> the nearest-even bf16 value, as fp32."""
+    return bf16_widen(bf16_bits(x))
+
+
 class EV(object):
-    """CPU EmbeddingVariable (embedding_var.h) -- primary or slot."""
+    """CPU EmbeddingVariable (embedding_var.h) -- primary or slot.
+
+    bf16=True: a bf16 EV (build-defined, the engine's value_bits 16): the
+    default row is rounded to bf16, every apply computes in fp32 on the
+    stored (bf16-valued) rows and rounds the updated row once; rows are kept
+    as fp32 arrays holding bf16 values, so gather / export return them
+    widened (bf16_bits() gives the bit patterns)."""
 
     def __init__(self, dim, default_row, filter_freq=0, steps_to_live=0,
                  max_element_size=0, false_positive_probability=-1.0,
-                 counter_bits=64, _handle=None, _primary=None):
+                 counter_bits=64, _handle=None, _primary=None, bf16=False):
         self.dim = dim
         self._primary = _primary
         self.filter_freq = filter_freq
+        self.bf16 = bool(bf16)
         if _handle is not None:
             self._h = _handle
         else:
@@ -360,6 +389,8 @@ class EV(object):
             self._h = lib().orc_ev_create(dim, _p(d), filter_freq, steps_to_live,
                                           max_element_size, false_positive_probability,
                                           counter_bits)
+            if self.bf16:
+                lib().orc_ev_set_bf16(self._h)
 
     def create_slot(self, slot_index, default_row):
         d = np.ascontiguousarray(np.broadcast_to(np.asarray(default_row, np.float32),
@@ -561,14 +592,15 @@ def embedding_lookup_sparse(params, indices, values, batch, weights=None, combin
     if max_norm is not None:
         emb = clip_rows(emb, max_norm)
     if weights is None:
-        return sparse_segment_reduce(emb, idx, seg, combiner, num_segments=batch)
+        out = sparse_segment_reduce(emb, idx, seg, combiner, num_segments=batch)
+        return bf16_round(out) if getattr(params, "bf16", False) else out
     D = emb.shape[1]
     out = np.empty((batch, D), np.float32)
     w = np.ascontiguousarray(weights, np.float32)
     _check(lib().orc_weighted_segment_reduce(_p(emb), D, _p(np.ascontiguousarray(idx)), _p(w),
                                              _p(np.ascontiguousarray(seg)), idx.shape[0], batch,
                                              COMBINERS[combiner], _p(out)), "weighted")
-    return out
+    return bf16_round(out) if getattr(params, "bf16", False) else out
 
 
 def embedding_lookup_sparse_grad(params, indices, values, batch, top_grad, weights=None,
