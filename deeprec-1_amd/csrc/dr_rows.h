@@ -114,6 +114,34 @@ __device__ __forceinline__ void load_row_bf16(Row<VEC, G, CPL>& x, const float* 
   }
 }
 
+// The same with the nontemporal policy (rows read once per launch).
+template <int VEC, int G, int CPL>
+__device__ __forceinline__ void load_row_bf16_nt(Row<VEC, G, CPL>& x, const float* p, int lg,
+                                                 int dv) {
+  static_assert(VEC == 4, "bf16 rows use 4-value chunks");
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = lg + c * G;
+    if (p && col < dv) {
+      const u2 w = __builtin_nontemporal_load(gp(reinterpret_cast<const u2*>(p) + col));
+      const float2 a = bf16x2_to_f2(w.x), b = bf16x2_to_f2(w.y);
+      x.v[c] = make_float4(a.x, a.y, b.x, b.y);
+    } else {
+      x.v[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+// Row load of a one-hot copy: fp32 rows, or (WIDEN) bf16 rows widened.
+template <int VEC, int G, int CPL, bool WIDEN>
+__device__ __forceinline__ void load_row_copy(Row<VEC, G, CPL>& x, const float* p, int lg, int dv) {
+  if constexpr (WIDEN)
+    load_row_bf16_nt<VEC, G, CPL>(x, p, lg, dv);
+  else
+    load_row_nt<VEC, G, CPL>(x, p, lg, dv);
+}
+
 // fp32 row -> bf16 (round to nearest even) at the float-word pointer p.
 template <int VEC, int G, int CPL>
 __device__ __forceinline__ void store_row_bf16(const Row<VEC, G, CPL>& x, float* p, int lg, int dv) {

@@ -1696,7 +1696,10 @@ __device__ __forceinline__ int64_t ev_probe_row(const LkDesc& e, uint64_t key) {
   return row == (int64_t)kRowDead ? -1 : row;
 }
 
-template <int VEC, int G, int CPL, int ORDER, int NB>
+// WIDEN: bf16 rows (a bf16 EV) widened into an fp32 output -- `dim` counts
+// values, rows are dim / 2 float words apart.  (A bf16 output is the plain
+// kernel on float words.)
+template <int VEC, int G, int CPL, int ORDER, int NB, bool WIDEN = false>
 __global__ __launch_bounds__(256) void ev_lookup_onehot_kernel(LookupArgs a, int T, int64_t B,
                                                                int dim, int32_t* __restrict__ mlist,
                                                                unsigned long long* __restrict__ mcnt) {
@@ -1720,7 +1723,7 @@ __global__ __launch_bounds__(256) void ev_lookup_onehot_kernel(LookupArgs a, int
     const LkDesc& e = sd[t];
     const int64_t row = ev_probe_row(e, (uint64_t)gld(a.keys + b * a.ksb + (int64_t)t * a.kst));
     if (row >= 0) {
-      mine = e.pool + row * (int64_t)dim;
+      mine = e.pool + row * (int64_t)(WIDEN ? dim / 2 : dim);
       if (a.rows) a.rows[(int64_t)t * B + b] = row;
     } else {
       missed = true;
@@ -1756,7 +1759,7 @@ __global__ __launch_bounds__(256) void ev_lookup_onehot_kernel(LookupArgs a, int
       const int64_t b = (int64_t)((uint32_t)s / (uint32_t)T);
       o[q] = a.out + b * a.out_stride + (s - b * T) * (int64_t)dim;
     }
-    load_row_nt<VEC, G, CPL>(x[q], p[q], lg, dv);
+    load_row_copy<VEC, G, CPL, WIDEN>(x[q], p[q], lg, dv);
   }
   wait_loads();
 #pragma unroll
@@ -1813,6 +1816,7 @@ __device__ __forceinline__ void miss_grid_sync(unsigned* bar, unsigned target, i
 // and every block returns after one load.
 template <int ORDER>
 __global__ __launch_bounds__(256) void ev_miss_kernel(MissArgs a, int T, int64_t B, int64_t dim,
+                                                      int widen,
                                                       const int32_t* __restrict__ mlist,
                                                       const unsigned long long* __restrict__ mcnt,
                                                       unsigned* __restrict__ bar,
@@ -1864,8 +1868,14 @@ __global__ __launch_bounds__(256) void ev_miss_kernel(MissArgs a, int T, int64_t
     const int64_t b = s / T;
     const int t = (int)(s - b * T);
     const float* src = mrow[i] >= 0 ? a.pool[t] + mrow[i] * dim : a.dflt[t];
-    float* dst = a.out + b * a.out_stride + (int64_t)t * dim;
     if (a.rows && lane == 0) a.rows[(int64_t)t * B + b] = mrow[i] >= 0 ? mrow[i] : -1;
+    if (widen) {  // bf16 row (dim float words) -> 2 * dim fp32 values
+      const uint16_t* h = reinterpret_cast<const uint16_t*>(src);
+      float* dst = a.out + b * a.out_stride + (int64_t)t * 2 * dim;
+      for (int64_t c = lane; c < 2 * dim; c += 64) dst[c] = bf16_to_f32(h[c]);
+      continue;
+    }
+    float* dst = a.out + b * a.out_stride + (int64_t)t * dim;
     for (int64_t c = lane; c < dim; c += 64) dst[c] = ORDER == DR_ORDER_SEQ ? 0.f + src[c] : src[c];
   }
 }
@@ -1903,12 +1913,12 @@ static LookupWs carve_lookup(void* ws, int64_t n, size_t* used) {
   return w;
 }
 
-template <int VEC, int G, int CPL, int ORDER, int NB>
+template <int VEC, int G, int CPL, int ORDER, int NB, bool WIDEN = false>
 static void launch_lookup_nb(const LookupArgs& a, int T, int64_t B, int dim, const LookupWs& w,
                              hipStream_t st) {
   const int64_t items = ceil_div((int64_t)T * B, NB);
   timing_mark(DR_TIME_LOOKUP, st, true);
-  hipLaunchKernelGGL((ev_lookup_onehot_kernel<VEC, G, CPL, ORDER, NB>),
+  hipLaunchKernelGGL((ev_lookup_onehot_kernel<VEC, G, CPL, ORDER, NB, WIDEN>),
                      dim3((unsigned)ceil_div(items, 256 / G)), dim3(256), 0, st, a, T, B, dim,
                      w.mlist, w.mcnt);
   timing_mark(DR_TIME_LOOKUP, st, false);
@@ -1928,7 +1938,7 @@ static void launch_lookup_onehot(const LookupArgs& a, int T, int64_t B, int dim,
 
 static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t ksb, int64_t kst,
                          int64_t B, float* out, int64_t out_stride, int order, int64_t* rows_out,
-                         void* ws, size_t ws_bytes, hipStream_t st) {
+                         void* ws, size_t ws_bytes, hipStream_t st, int flags = 0) {
   DR_REQUIRE(evs && T >= 1 && T <= DR_MAX_GROUP && B >= 0 && out_stride >= 0, DR_INVALID_ARGUMENT,
              "bad argument");
   DR_REQUIRE(ksb >= 0 && kst >= 0, DR_INVALID_ARGUMENT, "key strides must be >= 0");
@@ -1938,13 +1948,25 @@ static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t 
   size_t need = 0;
   carve_lookup(nullptr, n, &need);
   DR_REQUIRE(ws_bytes >= need, DR_INVALID_ARGUMENT, "lookup workspace too small");
-  // float words per row: bf16 EVs are copied bitwise as D / 2 words into a
-  // bf16 output (out_stride counts float words as well)
-  const int64_t dim = col_words(evs[0]->sh, evs[0]->col);
-  DR_REQUIRE(dim % 4 == 0 && dim <= 256, DR_INVALID_ARGUMENT,
-             "fused one-hot lookup needs row words %% 4 == 0 and <= 256");
-  DR_REQUIRE(!evs[0]->sh->bf16 || order == DR_ORDER_ALI, DR_INVALID_ARGUMENT,
+  // bf16 EVs (value_bits 16): an fp32 output widens each value (the
+  // reference casts bf16 embeddings to float32, embedding_ops.py:606-607);
+  // with DR_LOOKUP_OUT_BF16 the rows are copied bitwise as D / 2 float words
+  // into a bf16 output.  out_stride counts elements of the output type.
+  DR_REQUIRE((flags & ~DR_LOOKUP_OUT_BF16) == 0, DR_INVALID_ARGUMENT, "unknown flags 0x%x", flags);
+  const bool bf16 = evs[0]->sh->bf16 && evs[0]->col == 0;
+  const bool out_bf16 = flags & DR_LOOKUP_OUT_BF16;
+  const bool widen = bf16 && !out_bf16;
+  DR_REQUIRE(!out_bf16 || bf16, DR_INVALID_ARGUMENT, "DR_LOOKUP_OUT_BF16 needs bf16 EVs");
+  DR_REQUIRE(!bf16 || order == DR_ORDER_ALI, DR_INVALID_ARGUMENT,
              "bf16 EV lookups pool in the ALI order");
+  DR_REQUIRE(!out_bf16 || out_stride % 2 == 0, DR_INVALID_ARGUMENT,
+             "bf16 output stride must be even");
+  if (out_bf16) out_stride /= 2;                       // float words from here on
+  // floats per output row segment (and per row, except when widening, where
+  // a row is dim / 2 words)
+  const int64_t dim = bf16 && !widen ? col_words(evs[0]->sh, 0) : evs[0]->sh->dim;
+  DR_REQUIRE(dim % 4 == 0 && dim <= 256, DR_INVALID_ARGUMENT,
+             "fused one-hot lookup needs dim %% 4 == 0 (bf16: %% 8) and <= 256 words");
   DR_REQUIRE(out_stride >= (int64_t)T * dim && (out_stride % 4) == 0 &&
                  ((uintptr_t)out & 15) == 0,
              DR_INVALID_ARGUMENT, "out must be 16-B aligned with stride >= T*dim (multiple of 4)");
@@ -1953,7 +1975,7 @@ static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t 
   DR_REQUIRE(stw, DR_INTERNAL, "status word unavailable");
   for (int t = 0; t < T; ++t) {
     const EvShared* s = evs[t]->sh;
-    DR_REQUIRE(col_words(s, evs[t]->col) == dim && s->bf16 == evs[0]->sh->bf16,
+    DR_REQUIRE(s->dim == evs[0]->sh->dim && (s->bf16 && evs[t]->col == 0) == bf16,
                DR_INVALID_ARGUMENT, "tables must share dim and value type");
     DR_REQUIRE(s->value_words == 1, DR_INVALID_ARGUMENT,
                "table %d: pooled lookups are fp32 / bf16 (double EVs: dr_ev_gather)", t);
@@ -1993,7 +2015,9 @@ static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t 
   const int d4 = (int)(dim / 4);
 #define DR_LK(G, C)                                                             \
   do {                                                                          \
-    if (order == DR_ORDER_ALI)                                                  \
+    if (widen)                                                                  \
+      launch_lookup_nb<4, G, C, DR_ORDER_ALI, 4, true>(la, T, B, (int)dim, w, st); \
+    else if (order == DR_ORDER_ALI)                                             \
       launch_lookup_onehot<4, G, C, DR_ORDER_ALI>(la, T, B, (int)dim, w, st);   \
     else                                                                        \
       launch_lookup_onehot<4, G, C, DR_ORDER_SEQ>(la, T, B, (int)dim, w, st);   \
@@ -2030,10 +2054,11 @@ static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t 
   const unsigned kMissBlocks = miss_blocks();
   if (order == DR_ORDER_ALI)
     hipLaunchKernelGGL(ev_miss_kernel<DR_ORDER_ALI>, dim3(kMissBlocks), dim3(256), 0, st, ma, T, B,
-                       dim, w.mlist, w.mcnt, bar, w.mrow, w.minit, stw);
+                       widen ? dim / 2 : dim, (int)widen, w.mlist, w.mcnt, bar, w.mrow, w.minit,
+                       stw);
   else
     hipLaunchKernelGGL(ev_miss_kernel<DR_ORDER_SEQ>, dim3(kMissBlocks), dim3(256), 0, st, ma, T, B,
-                       dim, w.mlist, w.mcnt, bar, w.mrow, w.minit, stw);
+                       dim, 0, w.mlist, w.mcnt, bar, w.mrow, w.minit, stw);
   const hipError_t le = hipGetLastError();
   for (int q = 0; q < nmir; ++q) {
     if (le == hipSuccess) mirrored(mir[q], st);
@@ -2335,6 +2360,15 @@ int dr_ev_lookup_onehot_strided(dr_ev* const* evs, int num_tables, const int64_t
                                 void* ws, size_t ws_bytes, void* stream) {
   return dr::lookup_onehot(evs, num_tables, keys, key_stride_bag, key_stride_table, batch, out,
                            out_stride, order, rows_out, ws, ws_bytes, dr::S(stream));
+}
+
+int dr_ev_lookup_onehot_ex(dr_ev* const* evs, int num_tables, const int64_t* keys,
+                           int64_t key_stride_bag, int64_t key_stride_table, int64_t batch,
+                           void* out, int64_t out_stride, int order, int flags, int64_t* rows_out,
+                           void* ws, size_t ws_bytes, void* stream) {
+  return dr::lookup_onehot(evs, num_tables, keys, key_stride_bag, key_stride_table, batch,
+                           static_cast<float*>(out), out_stride, order, rows_out, ws, ws_bytes,
+                           dr::S(stream), flags);
 }
 
 int dr_ev_lookup_onehot_rows(dr_ev* const* evs, int num_tables, const int64_t* keys,

@@ -90,7 +90,7 @@ __device__ __forceinline__ void load_any(Row<VEC, G, CPL>& x, const float* p, in
 }
 template <int VEC, int G, int CPL, bool BF>
 __device__ __forceinline__ void store_any(const Row<VEC, G, CPL>& x, float* p, int lg, int dv) {
-  if constexpr (BF)
+  if constexpr (BF)  // (BF here: a bf16 OUTPUT)
     store_row_bf16<VEC, G, CPL>(x, p, lg, dv);
   else
     store_row<VEC, G, CPL>(x, p, lg, dv);
@@ -130,7 +130,7 @@ struct BagPtrs {
 
 // Unweighted bag of `num` rows, P(k) = row pointer of position k, summed in
 // the reference association order.
-template <int VEC, int G, int CPL, int ORDER, bool BF, class PtrAt>
+template <int VEC, int G, int CPL, int ORDER, bool BF, bool OB, class PtrAt>
 __device__ __forceinline__ void pool_bag_rows(const dr_pool_desc& d, int64_t num, float* out,
                                               int lg, int dv, const PtrAt& P) {
   using R = Row<VEC, G, CPL>;
@@ -161,13 +161,13 @@ __device__ __forceinline__ void pool_bag_rows(const dr_pool_desc& d, int64_t num
 #pragma unroll
       for (int c = 0; c < CPL; ++c) acc.v[c] = vdiv(acc.v[c], q);
     }
-    store_any<VEC, G, CPL, BF>(acc, out, lg, dv);
+    store_any<VEC, G, CPL, OB>(acc, out, lg, dv);
     return;
   }
   // ORDER_ALI
   if (num == 1) {
     fetch_p<VEC, G, CPL, ORDER, BF>(acc, P(0), d.max_norm, lg, dv);
-    store_any<VEC, G, CPL, BF>(acc, out, lg, dv);
+    store_any<VEC, G, CPL, OB>(acc, out, lg, dv);
     return;
   }
   int64_t r = num % 8;
@@ -202,22 +202,26 @@ __device__ __forceinline__ void pool_bag_rows(const dr_pool_desc& d, int64_t num
 #pragma unroll
     for (int c = 0; c < CPL; ++c) acc.v[c] = vdiv(acc.v[c], q);
   }
-  store_any<VEC, G, CPL, BF>(acc, out, lg, dv);
+  store_any<VEC, G, CPL, OB>(acc, out, lg, dv);
 }
 
 // One bag, general length, in the reference association order.  Called by
 // every lane of a group together (the shuffles of BagPtrs need that).
-template <int VEC, int G, int CPL, int ORDER, bool BF = false>
+template <int VEC, int G, int CPL, int ORDER, bool BF = false, bool OB = false>
 __device__ void pool_bag(const dr_pool_desc& d, int64_t b, int dim, int lg, int dv, int* st) {
   using R = Row<VEC, G, CPL>;
   const int64_t k0 = d.bag_off[b];
   const int64_t num = (int64_t)d.bag_off[b + 1] - k0;
   float* out = d.out + b * d.out_stride;
-  if (num <= 0) {
+  // an empty bag is a zero row -- except with weights and mean / sqrtn,
+  // where the reference divides the zero segment_sum by a zero weight sum
+  // (embedding_ops.py:636-645): 0 / 0 = NaN, which the weights branch
+  // below reproduces
+  if (num <= 0 && !(d.weights && d.combiner != DR_COMBINER_SUM)) {
     R z;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) z.v[c] = vzero<typename VecT<VEC>::T>();
-    store_any<VEC, G, CPL, BF>(z, out, lg, dv);
+    store_any<VEC, G, CPL, OB>(z, out, lg, dv);
     return;
   }
   if (d.weights) {
@@ -239,7 +243,7 @@ __device__ void pool_bag(const dr_pool_desc& d, int64_t b, int dim, int lg, int 
 #pragma unroll
       for (int c = 0; c < CPL; ++c) acc.v[c] = vdiv(acc.v[c], q);
     }
-    store_any<VEC, G, CPL, BF>(acc, out, lg, dv);
+    store_any<VEC, G, CPL, OB>(acc, out, lg, dv);
     return;
   }
   if (G >= 8 && num <= 4 * G) {
@@ -250,11 +254,11 @@ __device__ void pool_bag(const dr_pool_desc& d, int64_t b, int dim, int lg, int 
       const int64_t k = (int64_t)w * G + lg;
       bp.p[w] = k < num ? select_row(d, k0 + k, dim, st) : nullptr;
     }
-    pool_bag_rows<VEC, G, CPL, ORDER, BF>(d, num, out, lg, dv,
+    pool_bag_rows<VEC, G, CPL, ORDER, BF, OB>(d, num, out, lg, dv,
                                       [&](int64_t k) { return bp.at(k); });
     return;
   }
-  pool_bag_rows<VEC, G, CPL, ORDER, BF>(d, num, out, lg, dv,
+  pool_bag_rows<VEC, G, CPL, ORDER, BF, OB>(d, num, out, lg, dv,
                                     [&](int64_t k) { return select_row(d, k0 + k, dim, st); });
 }
 
@@ -292,7 +296,10 @@ __device__ __forceinline__ void seq_zero_add(Row<VEC, G, CPL>& x) {
   }
 }
 
-template <int VEC, int G, int CPL, int ORDER, int NB>
+// WIDEN: bf16 rows widened into an fp32 output (a bf16 EV's pooled lookup,
+// embedding_ops.py:606-607 casts bf16 embeddings to float32); `dim` counts
+// values, rows are dim / 2 float words apart.
+template <int VEC, int G, int CPL, int ORDER, int NB, bool WIDEN = false>
 __global__ __launch_bounds__(256) void pool_onehot_kernel(PoolArgs args, int T, int64_t B, int dim,
                                                           int* st) {
   // The slot -> table mapping differs per lane, so the descriptors are
@@ -321,10 +328,10 @@ __global__ __launch_bounds__(256) void pool_onehot_kernel(PoolArgs args, int T, 
       // slots < 2^31 (checked on the host): 32-bit division
       const int64_t b = (int64_t)((uint32_t)s / (uint32_t)T);
       const dr_pool_desc& d = sd[(int)(s - b * T)];
-      p = select_row(d, b, dim, st);
+      p = select_row(d, b, WIDEN ? dim / 2 : dim, st);
       o[j] = d.out + b * d.out_stride;
     }
-    load_row_nt<VEC, G, CPL>(x[j], p, lg, dv);
+    load_row_copy<VEC, G, CPL, WIDEN>(x[j], p, lg, dv);
   }
   wait_loads();
 #pragma unroll
@@ -334,7 +341,7 @@ __global__ __launch_bounds__(256) void pool_onehot_kernel(PoolArgs args, int T, 
   }
 }
 
-template <int VEC, int G, int CPL, int ORDER, int NB>
+template <int VEC, int G, int CPL, int ORDER, int NB, bool WIDEN = false>
 __global__ __launch_bounds__(256) void pool_fast_kernel(PoolArgs args, int T, int64_t B, int dim,
                                                         int64_t chunks_per_table, int* st) {
   __shared__ dr_pool_desc sd[DR_MAX_GROUP];  // per-group table index: stage in LDS
@@ -352,7 +359,9 @@ __global__ __launch_bounds__(256) void pool_fast_kernel(PoolArgs args, int T, in
   if (!chunk_is_fast<NB>(d, b0, B, off)) return;
   Row<VEC, G, CPL> x[NB];
 #pragma unroll
-  for (int j = 0; j < NB; ++j) load_row_nt<VEC, G, CPL>(x[j], select_row(d, off[j], dim, st), lg, dv);
+  for (int j = 0; j < NB; ++j)
+    load_row_copy<VEC, G, CPL, WIDEN>(x[j], select_row(d, off[j], WIDEN ? dim / 2 : dim, st), lg,
+                                      dv);
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     seq_zero_add<VEC, G, CPL, ORDER>(x[j]);
@@ -366,7 +375,7 @@ __global__ __launch_bounds__(256) void pool_fast_kernel(PoolArgs args, int T, in
 // early exits of fast chunks stay cheap.
 // BF: bf16 rows and output; `dim` = float words per row (D / 2), the lane
 // layout covers D values in chunks of VEC (dv = 2 * dim / VEC).
-template <int VEC, int G, int CPL, int ORDER, int NB, bool BF = false>
+template <int VEC, int G, int CPL, int ORDER, int NB, bool BF = false, bool OB = false>
 __global__ __launch_bounds__(256) void pool_general_kernel(PoolArgs args, int T, int64_t B,
                                                            int dim, int* st) {
   __shared__ dr_pool_desc sd[DR_MAX_GROUP];  // per-group table index: stage in LDS
@@ -383,7 +392,7 @@ __global__ __launch_bounds__(256) void pool_general_kernel(PoolArgs args, int T,
     const dr_pool_desc& d = sd[t];
     int off[NB + 1];
     if (chunk_is_fast<NB>(d, b - b % NB, B, off)) continue;  // taken by pool_fast_kernel
-    pool_bag<VEC, G, CPL, ORDER, BF>(d, b, dim, lg, dv, st);
+    pool_bag<VEC, G, CPL, ORDER, BF, OB>(d, b, dim, lg, dv, st);
   }
 }
 
@@ -392,21 +401,21 @@ static constexpr int kOneHotNB = 4;  // rows in flight per lane group (probe opt
 static constexpr int kChunkNB = 8;   // bags per chunk, fast/general split
 static constexpr int64_t kGeneralBlocks = 256 * 16;  // general-kernel grid cap (16 per CU)
 
-template <int VEC, int G, int CPL, int ORDER>
+template <int VEC, int G, int CPL, int ORDER, bool WIDEN = false>
 static int launch_pool(const PoolArgs& a, int T, int64_t B, int dim, int flags, hipStream_t s,
                        int* st) {
   if (flags & POOL_ONEHOT) {
     const int64_t items = ceil_div((int64_t)T * B, kOneHotNB);
     timing_mark(DR_TIME_POOL_ONEHOT, s, true);
-    hipLaunchKernelGGL((pool_onehot_kernel<VEC, G, CPL, ORDER, kOneHotNB>),
+    hipLaunchKernelGGL((pool_onehot_kernel<VEC, G, CPL, ORDER, kOneHotNB, WIDEN>),
                        dim3((unsigned)ceil_div(items, 256 / G)), dim3(256), 0, s, a, T, B, dim,
                        st);
     timing_mark(DR_TIME_POOL_ONEHOT, s, false);
   } else {
     const int64_t cpt = ceil_div(B, kChunkNB);
     const unsigned blocks = (unsigned)ceil_div((int64_t)T * cpt, 256 / G);
-    hipLaunchKernelGGL((pool_fast_kernel<VEC, G, CPL, ORDER, kChunkNB>), dim3(blocks), dim3(256),
-                       0, s, a, T, B, dim, cpt, st);
+    hipLaunchKernelGGL((pool_fast_kernel<VEC, G, CPL, ORDER, kChunkNB, WIDEN>), dim3(blocks),
+                       dim3(256), 0, s, a, T, B, dim, cpt, st);
     if (!(flags & 2)) {  // (2: fast kernel only -- the bf16 dispatcher's copies)
       const int64_t gblocks = std::min<int64_t>(ceil_div((int64_t)T * B, 256 / G), kGeneralBlocks);
       hipLaunchKernelGGL((pool_general_kernel<VEC, G, CPL, ORDER, kChunkNB>),
@@ -417,14 +426,17 @@ static int launch_pool(const PoolArgs& a, int T, int64_t B, int dim, int flags, 
   return DR_OK;
 }
 
-// bf16 rows (DR_POOL_BF16): one-hot copies and single-id chunks are bitwise
-// row copies of D / 2 float words (the fp32 kernels on words); multi-hot
-// bags, weights and max_norm pool in fp32 and round the bag once to bf16.
-template <int G, int CPL>
+// bf16 rows (DR_POOL_BF16).  bf16 output (DR_POOL_OUT_BF16): one-hot slots
+// and single-id chunks are bitwise copies of D / 2 float words (the fp32
+// kernels on words), multi-hot bags / weights / max_norm pool in fp32 and
+// round each bag once.  fp32 output (the reference's cast of bf16
+// embeddings to float32 before pooling, embedding_ops.py:606-607): the
+// copies widen each value, bags pool in fp32.
+template <int G, int CPL, bool OB>
 static int launch_pool_bf16_general(const PoolArgs& a, int T, int64_t B, int words, hipStream_t s,
                                     int* st) {
   const int64_t gblocks = std::min<int64_t>(ceil_div((int64_t)T * B, 256 / G), kGeneralBlocks);
-  hipLaunchKernelGGL((pool_general_kernel<4, G, CPL, DR_ORDER_ALI, kChunkNB, true>),
+  hipLaunchKernelGGL((pool_general_kernel<4, G, CPL, DR_ORDER_ALI, kChunkNB, true, OB>),
                      dim3((unsigned)gblocks), dim3(256), 0, s, a, T, B, words, st);
   DR_LAUNCH_CHECK();
   return DR_OK;
@@ -434,23 +446,31 @@ template <int ORDER>
 static int dispatch_pool(const PoolArgs& a, int T, int64_t B, int dim, int flags, hipStream_t s,
                          int* st);
 
-static int dispatch_pool_bf16(const PoolArgs& a, int T, int64_t B, int D, int flags, hipStream_t s,
-                              int* st) {
+template <int G, int CPL>
+static int launch_bf16(const PoolArgs& a, int T, int64_t B, int D, int flags, bool out_bf16,
+                       hipStream_t s, int* st) {
   const int words = D / 2;
-  // copies: every one-hot slot, or the single-id chunks of a multi-hot launch
-  // (launch_pool's fast kernel takes exactly those; its general kernel is
-  // replaced by the bf16 one below)
-  if (flags & POOL_ONEHOT) return dispatch_pool<DR_ORDER_ALI>(a, T, B, words, flags, s, st);
-  int rc = dispatch_pool<DR_ORDER_ALI>(a, T, B, words, flags | 2 /* fast only */, s, st);
-  if (rc) return rc;
+  if (out_bf16) {
+    if (flags & POOL_ONEHOT) return dispatch_pool<DR_ORDER_ALI>(a, T, B, words, flags, s, st);
+    int rc = dispatch_pool<DR_ORDER_ALI>(a, T, B, words, flags | 2 /* fast only */, s, st);
+    if (rc) return rc;
+    return launch_pool_bf16_general<G, CPL, true>(a, T, B, words, s, st);
+  }
+  int rc = launch_pool<4, G, CPL, DR_ORDER_ALI, true>(a, T, B, D, flags | 2, s, st);
+  if (rc || (flags & POOL_ONEHOT)) return rc;
+  return launch_pool_bf16_general<G, CPL, false>(a, T, B, words, s, st);
+}
+
+static int dispatch_pool_bf16(const PoolArgs& a, int T, int64_t B, int D, int flags, bool out_bf16,
+                              hipStream_t s, int* st) {
   const int d4 = D / 4;
-  if (d4 <= 4) return launch_pool_bf16_general<4, 1>(a, T, B, words, s, st);
-  if (d4 <= 8) return launch_pool_bf16_general<8, 1>(a, T, B, words, s, st);
-  if (d4 <= 16) return launch_pool_bf16_general<16, 1>(a, T, B, words, s, st);
-  if (d4 <= 32) return launch_pool_bf16_general<32, 1>(a, T, B, words, s, st);
-  if (d4 <= 64) return launch_pool_bf16_general<64, 1>(a, T, B, words, s, st);
-  if (d4 <= 128) return launch_pool_bf16_general<64, 2>(a, T, B, words, s, st);
-  if (d4 <= 256) return launch_pool_bf16_general<64, 4>(a, T, B, words, s, st);
+  if (d4 <= 4) return launch_bf16<4, 1>(a, T, B, D, flags, out_bf16, s, st);
+  if (d4 <= 8) return launch_bf16<8, 1>(a, T, B, D, flags, out_bf16, s, st);
+  if (d4 <= 16) return launch_bf16<16, 1>(a, T, B, D, flags, out_bf16, s, st);
+  if (d4 <= 32) return launch_bf16<32, 1>(a, T, B, D, flags, out_bf16, s, st);
+  if (d4 <= 64) return launch_bf16<64, 1>(a, T, B, D, flags, out_bf16, s, st);
+  if (d4 <= 128) return launch_bf16<64, 2>(a, T, B, D, flags, out_bf16, s, st);
+  if (d4 <= 256) return launch_bf16<64, 4>(a, T, B, D, flags, out_bf16, s, st);
   set_error("bf16 dim %d unsupported (max 1024)", D);
   return DR_INVALID_ARGUMENT;
 }
@@ -1363,13 +1383,15 @@ int dr_pool_grouped_ex(const dr_pool_desc* descs_host, int num_tables, int64_t b
   DR_REQUIRE(num_tables >= 1 && num_tables <= DR_MAX_GROUP, DR_INVALID_ARGUMENT,
              "num_tables must be in [1, %d]", DR_MAX_GROUP);
   DR_REQUIRE(batch >= 0 && dim > 0, DR_INVALID_ARGUMENT, "bad batch/dim");
-  DR_REQUIRE((flags & ~(DR_POOL_ONEHOT | DR_POOL_BF16)) == 0, DR_INVALID_ARGUMENT,
-             "unknown flags 0x%x", flags);
+  DR_REQUIRE((flags & ~(DR_POOL_ONEHOT | DR_POOL_BF16 | DR_POOL_OUT_BF16)) == 0,
+             DR_INVALID_ARGUMENT, "unknown flags 0x%x", flags);
   if (batch == 0) return DR_OK;
   const bool onehot = flags & DR_POOL_ONEHOT;
   const bool bf16 = flags & DR_POOL_BF16;
+  const bool out_bf16 = flags & DR_POOL_OUT_BF16;
   DR_REQUIRE(!bf16 || (dim % 8 == 0 && order == DR_ORDER_ALI), DR_INVALID_ARGUMENT,
              "DR_POOL_BF16 needs dim %% 8 == 0 and the ALI order");
+  DR_REQUIRE(!out_bf16 || bf16, DR_INVALID_ARGUMENT, "DR_POOL_OUT_BF16 needs DR_POOL_BF16");
   DR_REQUIRE(!onehot || (int64_t)num_tables * batch < (1ll << 31), DR_INVALID_ARGUMENT,
              "DR_POOL_ONEHOT: tables x batch must be < 2^31");
   PoolArgs a;
@@ -1386,11 +1408,19 @@ int dr_pool_grouped_ex(const dr_pool_desc* descs_host, int num_tables, int64_t b
                      (!d.default_rows || ((uintptr_t)d.default_rows & 15) == 0),
                  DR_INVALID_ARGUMENT, "table %d: pool/out must be 16B aligned with stride %% 4", t);
     a.d[t] = d;
+    if (bf16) {
+      // strides arrive in elements of their type; rows move as float words
+      DR_REQUIRE(d.default_stride % 2 == 0 && (!out_bf16 || d.out_stride % 2 == 0),
+                 DR_INVALID_ARGUMENT, "table %d: bf16 strides must be even", t);
+      a.d[t].default_stride = d.default_stride / 2;
+      if (out_bf16) a.d[t].out_stride = d.out_stride / 2;
+    }
   }
   int* st = status_word();
   DR_REQUIRE(st, DR_INTERNAL, "status word unavailable");
   hipStream_t s = S(stream);
-  if (bf16) return dispatch_pool_bf16(a, num_tables, batch, dim, flags & DR_POOL_ONEHOT, s, st);
+  if (bf16)
+    return dispatch_pool_bf16(a, num_tables, batch, dim, flags & DR_POOL_ONEHOT, out_bf16, s, st);
   if (order == DR_ORDER_SEQ)
     return dispatch_pool<DR_ORDER_SEQ>(a, num_tables, batch, dim, flags, s, st);
   return dispatch_pool<DR_ORDER_ALI>(a, num_tables, batch, dim, flags, s, st);

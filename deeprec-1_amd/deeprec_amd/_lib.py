@@ -24,6 +24,8 @@ MAX_GROUP = 32
 MAX_PARTITIONS = 64
 POOL_ONEHOT = 1
 POOL_BF16 = 2
+POOL_OUT_BF16 = 4
+LOOKUP_OUT_BF16 = 1
 
 
 class DeepRecError(RuntimeError):
@@ -150,6 +152,8 @@ SIGNATURES = {
     "dr_ev_lookup_onehot_workspace_size": (_SZ, [_I32, _I64]),
     "dr_ev_lookup_onehot": (_I32, [_P, _I32, _P, _I64, _P, _I64, _I32, _P, _SZ, _P]),
     "dr_ev_lookup_onehot_rows": (_I32, [_P, _I32, _P, _I64, _P, _I64, _I32, _P, _P, _SZ, _P]),
+    "dr_ev_lookup_onehot_ex": (_I32, [_P, _I32, _P, _I64, _I64, _I64, _P, _I64, _I32, _I32, _P,
+                                      _P, _SZ, _P]),
     "dr_ev_lookup_onehot_strided": (_I32, [_P, _I32, _P, _I64, _I64, _I64, _P, _I64, _I32, _P, _P,
                                            _SZ, _P]),
     "dr_ev_resolve_tagged": (_I32, [_P, _I32, _P, _P, _I64, _P, _P, _P, _P, _P, _SZ, _P]),

@@ -191,7 +191,7 @@ def _desc(f, out, out_stride):
         d.rows = ptr(f.rows)
         if f.defaults is not None:
             d.default_rows = ptr(f.defaults)
-            d.default_stride = p.row_words
+            d.default_stride = p.dim
         else:
             d.default_rows = ptr(_ev_default_dev(p))
             d.default_stride = 0
@@ -203,7 +203,7 @@ def _desc(f, out, out_stride):
     d.bag_off = None if f.bag_off is None else ptr(f.bag_off)
     d.weights = ptr(f.weights)
     d.out = out.data_ptr()
-    d.out_stride = out_stride   # float words (bf16 outputs: elements / 2)
+    d.out_stride = out_stride   # elements of the output type
     d.combiner = COMBINERS[f.combiner]
     d.max_norm = -1.0 if f.max_norm is None else float(f.max_norm)
     return d
@@ -261,12 +261,12 @@ def _dense_grad(p, sl):
 
 class _LookupFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, anchor, feats, order, fused_rows, *tensors):
+    def forward(ctx, anchor, feats, order, fused_rows, out_dtype, *tensors):
         ctx.feats = feats
         ctx.tensors = tensors
         if fused_rows:
-            return _fused_onehot(feats, order, with_rows=True)
-        return _pool_all(feats, order)
+            return _fused_onehot(feats, order, with_rows=True, out_dtype=out_dtype)
+        return _pool_all(feats, order, out_dtype=out_dtype)
 
     @staticmethod
     def backward(ctx, grad_out):
@@ -274,7 +274,7 @@ class _LookupFn(torch.autograd.Function):
         # output hands a bf16 gradient back: widened once here)
         g = grad_out.float().contiguous()
         dense = _queue_grads(ctx.feats, g, 0, g.shape[1], ctx.tensors)
-        return (None, None, None, None) + tuple(dense)
+        return (None, None, None, None, None) + tuple(dense)
 
 
 def _queue_grads(feats, g, col0, total, tensors=()):
@@ -625,7 +625,19 @@ def _record_major(feats):
     return v0.data_ptr()
 
 
-def _fused_onehot(feats, order, with_rows=False):
+def _out_dtype(feats, out_dtype):
+    """Pooled output dtype: fp32 (bf16 EVs too: the reference casts bf16
+    embeddings to float32 before pooling, embedding_ops.py:606-607), or bf16
+    when asked for and every feature is a bf16 EV (the DCN-v2 input path)."""
+    if out_dtype in (None, torch.float32):
+        return torch.float32
+    if out_dtype == torch.bfloat16 and all(f.bf16 for f in feats):
+        return torch.bfloat16
+    raise _lib.DeepRecError(_lib.INVALID_ARGUMENT,
+                            "out_dtype %s: float32, or bfloat16 for bf16 EVs" % (out_dtype,))
+
+
+def _fused_onehot(feats, order, with_rows=False, out_dtype=None):
     """One-hot lookup of filter-free EVs in one fused launch
     (dr_ev_lookup_onehot: probe + row copy, no resolve pass).  Forward-only,
     or (with_rows) a training forward that also records the row of every id
@@ -640,10 +652,10 @@ def _fused_onehot(feats, order, with_rows=False):
     T = len(feats)
     dev = feats[0].raw_values.device
     koff = [t * B for t in range(T + 1)]
-    # a bf16 EV's rows are copied bitwise into a bf16 output: strides in
-    # float words (row_words = D / 2)
-    out = torch.empty((B, T * D), dtype=p0.value_dtype, device=dev)
-    W = p0.row_words
+    odt = _out_dtype(feats, out_dtype)
+    # bf16 EVs: widened into an fp32 output, or copied bitwise into a bf16 one
+    flags = _lib.LOOKUP_OUT_BF16 if odt == torch.bfloat16 else 0
+    out = torch.empty((B, T * D), dtype=odt, device=dev)
     handles = (C.c_void_p * T)(*[f.params.handle.value for f in feats])
     wsb = lib().dr_ev_lookup_onehot_workspace_size(T, B)
     ws = workspace(wsb, dev)
@@ -651,35 +663,35 @@ def _fused_onehot(feats, order, with_rows=False):
     if rec is not None:
         # the features are the columns of one record-major [B, T] id matrix:
         # read in place, in the kernel's (b, t) visiting order
-        check(lib().dr_ev_lookup_onehot_strided(handles, T, rec, T, 1, B, ptr(out), T * W, order,
-                                                None, ptr(ws), wsb, stream_handle(dev)))
+        check(lib().dr_ev_lookup_onehot_ex(handles, T, rec, T, 1, B, ptr(out), T * D, order, flags,
+                                           None, ptr(ws), wsb, stream_handle(dev)))
         ops._post(dev)
         return out
     vals = _concat_values(feats, koff)
     if with_rows:
         rowsel = torch.empty(T * B, dtype=torch.int64, device=dev)
-        check(lib().dr_ev_lookup_onehot_rows(handles, T, ptr(vals), B, ptr(out), T * W, order,
-                                             ptr(rowsel), ptr(ws), wsb, stream_handle(dev)))
+        check(lib().dr_ev_lookup_onehot_ex(handles, T, ptr(vals), 1, B, B, ptr(out), T * D, order,
+                                           flags, ptr(rowsel), ptr(ws), wsb, stream_handle(dev)))
         group = _RowGroup(feats, vals, rowsel, koff)
         for t, f in enumerate(feats):
             f.uniq = f.idx = f.rows = f.U = f.defaults = None
             f.rowsel = rowsel[koff[t]:koff[t + 1]]
             f.group = group
     else:
-        check(lib().dr_ev_lookup_onehot(handles, T, ptr(vals), B, ptr(out), T * W, order, ptr(ws),
-                                        wsb, stream_handle(dev)))
+        check(lib().dr_ev_lookup_onehot_ex(handles, T, ptr(vals), 1, B, B, ptr(out), T * D, order,
+                                           flags, None, ptr(ws), wsb, stream_handle(dev)))
     ops._post(dev)
     return out
 
 
-def _run(feats, order=ORDER_ALI, need_grad=None):
+def _run(feats, order=ORDER_ALI, need_grad=None, out_dtype=None):
     """Grouped pooled lookup of features sharing the batch -> [B, sum(D_t)]."""
     tensors = _trainable_tensors(feats) if torch.is_grad_enabled() else []
     if need_grad is None:
         need_grad = torch.is_grad_enabled() and (
             bool(tensors) or any(not torch.is_tensor(f.params) for f in feats))
     if not need_grad and _FUSED_ONEHOT:
-        out = _fused_onehot(feats, order)
+        out = _fused_onehot(feats, order, out_dtype=out_dtype)
         if out is not None:
             return out
     # training forward of one-hot filter-free EVs: the fused probe + copy
@@ -691,11 +703,11 @@ def _run(feats, order=ORDER_ALI, need_grad=None):
     if need_grad:
         anchors = [_anchor(f.params) for f in feats if not torch.is_tensor(f.params)]
         return _LookupFn.apply(anchors[0] if anchors else None, feats, order, fused_rows,
-                               *tensors)
-    return _pool_all(feats, order)
+                               out_dtype, *tensors)
+    return _pool_all(feats, order, out_dtype=out_dtype)
 
 
-def _pool_all(feats, order, out=None):
+def _pool_all(feats, order, out=None, out_dtype=None):
     dev = feats[0].values.device
     B = feats[0].batch
     dims = [f.params.dim if not torch.is_tensor(f.params) else f.params.shape[1] for f in feats]
@@ -704,13 +716,12 @@ def _pool_all(feats, order, out=None):
     if any(f.bf16 != bf16 for f in feats):
         raise _lib.DeepRecError(_lib.INVALID_ARGUMENT,
                                 "one pooled output: all features bf16 EVs or none")
-    odt = torch.bfloat16 if bf16 else torch.float32
+    odt = _out_dtype(feats, out_dtype if out is None else out.dtype)
     if out is None:
         out = torch.empty((B, total), dtype=odt, device=dev)
-    elif out.shape[0] != B or out.stride(1) != 1 or out.shape[1] < total or out.dtype != odt:
-        raise ValueError("out must be a [B, >= %d] %s view with unit column stride" % (total, odt))
-    # strides in float words (bf16: two values per word)
-    stride = out.stride(0) // 2 if bf16 else out.stride(0)
+    elif out.shape[0] != B or out.stride(1) != 1 or out.shape[1] < total:
+        raise ValueError("out must be a [B, >= %d] view with unit column stride" % total)
+    stride = out.stride(0)
     # group consecutive features of equal dim into <= 32-table launches
     col = 0
     i = 0
@@ -726,7 +737,8 @@ def _pool_all(feats, order, out=None):
         for f in feats[i:j]:
             descs.append(_desc(f, out[:, c:], stride))
             c += dims[i]
-        ops.pool_grouped(descs, B, dims[i], order, dev, onehot=onehot, bf16=bf16)
+        ops.pool_grouped(descs, B, dims[i], order, dev, onehot=onehot, bf16=bf16,
+                         out_bf16=odt == torch.bfloat16)
         col = c
         i = j
     return out
@@ -764,15 +776,18 @@ def embedding_lookup_sparse(params, sp_ids, sp_weights=None, partition_strategy=
     return _run([f])
 
 
-def embedding_lookup_sparse_multi(params_list, sp_ids_list, combiner="mean", max_norm=None):
+def embedding_lookup_sparse_multi(params_list, sp_ids_list, combiner="mean", max_norm=None,
+                                  out_dtype=None):
     """Grouped lookup of several features (one pooled launch per 32 tables);
-    returns the input_layer concatenation [B, sum(D_t)]."""
+    returns the input_layer concatenation [B, sum(D_t)], fp32 -- or, for
+    bf16 EVs with out_dtype=torch.bfloat16, bf16 (one-id bags copied
+    bitwise, longer bags pooled in fp32 and rounded once)."""
     feats = []
     for p, sp in zip(params_list, sp_ids_list):
         v = sp.values.to(torch.int64)      # strided views stay views (_record_major)
         feats.append(_Feature(p, v, _seg_of(sp), sp.dense_shape[0], None, combiner, max_norm,
                               onehot=_is_onehot(sp, v.numel())))
-    return _run(feats)
+    return _run(feats, out_dtype=out_dtype)
 
 
 def embedding_lookup(params, ids, partition_strategy="mod", name=None, max_norm=None,

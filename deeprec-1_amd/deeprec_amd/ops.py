@@ -249,12 +249,15 @@ def bag_offsets(segment_ids, batch):
     return off
 
 
-def pool_grouped(descs, batch, dim, order=ORDER_ALI, device=None, onehot=False, bf16=False):
+def pool_grouped(descs, batch, dim, order=ORDER_ALI, device=None, onehot=False, bf16=False,
+                 out_bf16=False):
     """Launch dr_pool_grouped_ex on a list of _lib.DrPoolDesc (<= 32 tables).
     onehot: every bag b holds exactly nnz b (bag_off not read).  bf16: the
-    tables and the output are bf16 (DR_POOL_BF16; strides in float words)."""
+    tables hold bf16 values (DR_POOL_BF16), pooled into fp32 -- or into bf16
+    with out_bf16 (DR_POOL_OUT_BF16); strides in elements of their type."""
     arr = (_lib.DrPoolDesc * len(descs))(*descs)
-    flags = (_lib.POOL_ONEHOT if onehot else 0) | (_lib.POOL_BF16 if bf16 else 0)
+    flags = ((_lib.POOL_ONEHOT if onehot else 0) | (_lib.POOL_BF16 if bf16 else 0)
+             | (_lib.POOL_OUT_BF16 if out_bf16 else 0))
     check(lib().dr_pool_grouped_ex(arr, len(descs), batch, dim, order, flags,
                                    stream_handle(device)))
     _post(device)

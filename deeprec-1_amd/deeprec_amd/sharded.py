@@ -129,12 +129,16 @@ class HipLocal(object):
             ops.rows_pack(src, perm, out)
         return out
 
-    def pool(self, rows_recv, rowsel, idx, koff, bag_offs, batch, combiner):
+    def pool(self, rows_recv, rowsel, idx, koff, bag_offs, batch, combiner, out_dtype=None):
         """Requester: pooled [batch, T*D] from the received rows.  rowsel[u]
         is the received row of unique u (idx given: nnz -> unique) or of nnz
         u directly (idx None, the direct one-hot mode)."""
         T, D = self.T, self.dim
-        out = torch.empty((batch, T * D), dtype=self.value_dtype, device=self.device)
+        # bf16 rows pool into fp32 (the reference's cast, embedding_ops.py:
+        # 606-607) unless a bf16 output is asked for
+        out_bf16 = self.bf16 and out_dtype == torch.bfloat16
+        out = torch.empty((batch, T * D), dtype=torch.bfloat16 if out_bf16 else torch.float32,
+                          device=self.device)
         es = out.element_size()
         descs = []
         for t in range(T):
@@ -150,12 +154,12 @@ class HipLocal(object):
             d.default_stride = 0
             d.bag_off = None if bag_offs is None else bag_offs[t].data_ptr()
             d.out = out.data_ptr() + es * t * D
-            d.out_stride = T * D * es // 4      # float words
+            d.out_stride = T * D
             d.combiner = COMBINERS[combiner]
             d.max_norm = -1.0
             descs.append(d)
         ops.pool_grouped(descs, batch, D, ORDER_ALI, self.device, onehot=bag_offs is None,
-                         bf16=self.bf16)
+                         bf16=self.bf16, out_bf16=out_bf16)
         return out
 
 
@@ -179,7 +183,7 @@ class ShardedLookup(object):
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
         return out
 
-    def forward(self, ids, bag_offs=None, combiner="sum", need_grad=False):
+    def forward(self, ids, bag_offs=None, combiner="sum", need_grad=False, out_dtype=None):
         """ids: [T, nnz] keys (hotness 1 when bag_offs is None: bag b = id b).
 
         Forward-only one-hot lookups of filter-free EVs route the raw ids
@@ -203,7 +207,8 @@ class ShardedLookup(object):
             self.last_stats = {"sent_keys": 0, "recv_keys": 0, "direct": True, "local": True}
             self._saved = None
             with torch.no_grad():
-                return embedding_lookup_sparse_multi(self.evs, sps, combiner=combiner)
+                return embedding_lookup_sparse_multi(self.evs, sps, combiner=combiner,
+                                                     out_dtype=out_dtype)
         if direct:
             uniq, idx, U = vals, None, None
         else:
@@ -231,7 +236,10 @@ class ShardedLookup(object):
         # 7. requester: (unique | nnz) position -> row in the received buffer
         rowsel = torch.zeros(T * nnz, dtype=torch.int64, device=dev)
         rowsel[perm[:S].to(torch.int64)] = torch.arange(S, dtype=torch.int64, device=dev)
-        out = be.pool(rows_r, rowsel, idx, koff, bag_offs, self.batch, combiner)
+        if out_dtype is None:
+            out = be.pool(rows_r, rowsel, idx, koff, bag_offs, self.batch, combiner)
+        else:
+            out = be.pool(rows_r, rowsel, idx, koff, bag_offs, self.batch, combiner, out_dtype)
         self.last_stats = {"sent_keys": S, "recv_keys": R, "direct": direct}
         self._saved = None
         if need_grad:
@@ -561,8 +569,11 @@ class XgmiShardedLookup(object):
             self.evs[t].pending_grads.append(IndexedSlices(v, k, num_valid=n, unique=False))
         return out
 
-    def forward(self, ids):
-        """ids: [T, B] int64 keys (hotness 1) -> [B, T*D] pooled (sum)."""
+    def forward(self, ids, out_dtype=None):
+        """ids: [T, B] int64 keys (hotness 1) -> [B, T*D] pooled (sum).  bf16
+        EVs travel as bf16 rows (half the link bytes); the result is widened
+        to fp32 (the reference's cast) unless out_dtype=torch.bfloat16, which
+        returns the peer-written bf16 buffer itself."""
         if tuple(ids.shape) != (self.T, self.batch) or ids.dtype != torch.int64:
             raise ValueError("ids must be int64 [%d, %d]" % (self.T, self.batch))
         ids = ids.contiguous()
@@ -570,6 +581,8 @@ class XgmiShardedLookup(object):
         self._barrier()
         self.serve()
         self._barrier()
+        if self.bufs.out.dtype == torch.bfloat16 and out_dtype != torch.bfloat16:
+            return self.bufs.out.float()
         return self.bufs.out
 
     def close(self):

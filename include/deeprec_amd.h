@@ -171,12 +171,15 @@ int dr_pool_grouped(const dr_pool_desc* descs_host, int num_tables, int64_t batc
 /* features); bag_off may be NULL and is not read; weights must be NULL and  */
 /* max_norm < 0.  Results are identical to dr_pool_grouped on such input.    */
 #define DR_POOL_ONEHOT 1
-/* DR_POOL_BF16: the pools (and default rows) hold bf16 values and the output */
-/* is bf16 (a bf16 EV, value_bits 16): `dim` counts values (multiple of 8),  */
-/* pool / out / default strides count float words (2 values each).  Bags of */
-/* one id are bitwise copies; longer bags, weights and max_norm are pooled in */
-/* fp32 in the ALI order and rounded once to bf16 (nearest even).  ALI only. */
+/* DR_POOL_BF16: the pools (and default rows) hold bf16 values (a bf16 EV,  */
+/* value_bits 16); `dim` counts values (multiple of 8); default_stride      */
+/* counts bf16 elements.  The output is fp32 (the reference casts bf16      */
+/* embeddings to float32 before pooling, embedding_ops.py:606-607) unless   */
+/* DR_POOL_OUT_BF16, when it is bf16 (out_stride in bf16 elements): bags of */
+/* one id are then bitwise copies, longer bags / weights / max_norm pool in */
+/* fp32 (ALI order) and round once to nearest even.  ALI order only.        */
 #define DR_POOL_BF16 2
+#define DR_POOL_OUT_BF16 4
 int dr_pool_grouped_ex(const dr_pool_desc* descs_host, int num_tables, int64_t batch,
                        int dim, int order, int flags, void* stream);
 
@@ -437,6 +440,18 @@ int dr_ev_lookup_onehot_strided(dr_ev* const* evs, int num_tables, const int64_t
                                 int64_t key_stride_bag, int64_t key_stride_table, int64_t batch,
                                 float* out, int64_t out_stride, int order, int64_t* rows_out,
                                 void* ws, size_t ws_bytes, void* stream);
+/* The strided form with flags.  bf16 EVs (value_bits 16): by default the  */
+/* output is fp32, each value widened (the reference casts bf16 embeddings */
+/* to float32 before pooling, embedding_ops.py:606-607; out_stride in       */
+/* floats); DR_LOOKUP_OUT_BF16 copies the rows bitwise into a bf16 output   */
+/* (out_stride in bf16 elements, even; dim % 8 == 0): 8 + 16 + 2*2*D bytes  */
+/* per lookup.  ALI order only for bf16 EVs.  The entries above are this    */
+/* one with flags 0.                                                         */
+#define DR_LOOKUP_OUT_BF16 1
+int dr_ev_lookup_onehot_ex(dr_ev* const* evs, int num_tables, const int64_t* keys,
+                           int64_t key_stride_bag, int64_t key_stride_table, int64_t batch,
+                           void* out, int64_t out_stride, int order, int flags, int64_t* rows_out,
+                           void* ws, size_t ws_bytes, void* stream);
 /* Tagged resolve (owner side of the sharded exchange): keys of all T EVs  */
 /* (equal dim) in one array, table of key i = tags[i]; n_dev: optional      */
 /* DEVICE count.  Filtered keys give -(i+1) (read table t's default row).   */

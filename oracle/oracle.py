@@ -592,15 +592,16 @@ def embedding_lookup_sparse(params, indices, values, batch, weights=None, combin
     if max_norm is not None:
         emb = clip_rows(emb, max_norm)
     if weights is None:
-        out = sparse_segment_reduce(emb, idx, seg, combiner, num_segments=batch)
-        return bf16_round(out) if getattr(params, "bf16", False) else out
+        # (a bf16 EV pools its widened values into fp32: the reference casts
+        # bf16 embeddings to float32 first, embedding_ops.py:606-607)
+        return sparse_segment_reduce(emb, idx, seg, combiner, num_segments=batch)
     D = emb.shape[1]
     out = np.empty((batch, D), np.float32)
     w = np.ascontiguousarray(weights, np.float32)
     _check(lib().orc_weighted_segment_reduce(_p(emb), D, _p(np.ascontiguousarray(idx)), _p(w),
                                              _p(np.ascontiguousarray(seg)), idx.shape[0], batch,
                                              COMBINERS[combiner], _p(out)), "weighted")
-    return bf16_round(out) if getattr(params, "bf16", False) else out
+    return out
 
 
 def embedding_lookup_sparse_grad(params, indices, values, batch, top_grad, weights=None,

@@ -7,7 +7,10 @@ dr_ev_config.value_bits, DESIGN.md "bf16 EVs") is restated by the oracle
 (oracle.EV(bf16=True), oracle.bf16_round):
   * values are bf16; the fp32 default row is rounded to nearest even;
   * lookups pool the widened values in fp32 in the reference association
-    order and round each bag once (a one-id bag is a bitwise copy);
+    order into an fp32 output (the reference casts bf16 embeddings to
+    float32 before pooling, embedding_ops.py:606-607), or -- out_dtype
+    bfloat16, the DCN-v2 input path -- round each bag once into a bf16
+    output (a one-id bag is then a bitwise copy);
   * gradients are fp32; an apply computes the reference's fp32 formula on
     the widened value and rounds the updated value once; optimizer slots
     stay fp32.
@@ -82,11 +85,12 @@ def test_bf16_synthetic_rows(dr, orc):
     np.testing.assert_array_equal(bits(got), want)
 
 
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("D", [64, 128])
-def test_bf16_onehot_lookup_bitwise(dr, orc, D):
-    """Forward-only fused one-hot lookup (dr_ev_lookup_onehot): a bitwise
-    copy of the bf16 rows into the [B, T*D] bf16 output, misses created with
-    the (rounded) default."""
+def test_bf16_onehot_lookup(dr, orc, D, out_dtype):
+    """Forward-only fused one-hot lookup (dr_ev_lookup_onehot_ex): the bf16
+    rows widened into an fp32 output, or copied bitwise into a bf16 output;
+    misses created with the (rounded) default."""
     rng = np.random.default_rng(D)
     F, B = 5, 700
     evs, oevs = [], []
@@ -99,17 +103,20 @@ def test_bf16_onehot_lookup_bitwise(dr, orc, D):
     ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
     sps = [dr.SparseTensor(T(ind), T(ids[f]), (B, 1)) for f in range(F)]
     with torch.no_grad():
-        out = dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum")
-    assert out.dtype == torch.bfloat16 and tuple(out.shape) == (B, F * D)
+        out = dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum", out_dtype=out_dtype)
+    assert out.dtype == out_dtype and tuple(out.shape) == (B, F * D)
     want = np.concatenate([oevs[f].gather(ids[f]) for f in range(F)], 1)
     np.testing.assert_array_equal(f32(out), want)
 
 
 @pytest.mark.parametrize("comb", ["sum", "mean", "sqrtn"])
-@pytest.mark.parametrize("weighted", [False, True])
-def test_bf16_multihot_pool(dr, orc, comb, weighted):
-    """Multi-hot bags (and weights): fp32 pooling of the widened rows in the
-    ALI order, each bag rounded once (DR_POOL_BF16 general kernel)."""
+@pytest.mark.parametrize("weighted,out_dtype", [(False, torch.float32), (True, torch.float32),
+                                                (False, torch.bfloat16)])
+def test_bf16_multihot_pool(dr, orc, comb, weighted, out_dtype):
+    """Multi-hot bags (and weights, empty bags): fp32 pooling of the widened
+    rows in the ALI order (DR_POOL_BF16 kernels), fp32 out or each bag
+    rounded once to bf16.  Weighted mean / sqrtn of an empty bag is the
+    reference's 0 / 0."""
     rng = np.random.default_rng(3 + int(weighted))
     B, D, H_ = 300, 32, 13
     ev, oev = _ev_pair(dr, orc, "bf_mh_%s_%d" % (comb, weighted), D, 0.1, rng,
@@ -123,9 +130,14 @@ def test_bf16_multihot_pool(dr, orc, comb, weighted):
     sp = dr.SparseTensor(T(ind), T(v), (B, H_))
     spw = dr.SparseTensor(T(ind), T(w), (B, H_)) if weighted else None
     with torch.no_grad():
-        out = dr.embedding_lookup_sparse(ev, sp, sp_weights=spw, combiner=comb)
-    assert out.dtype == torch.bfloat16
+        if out_dtype == torch.bfloat16:       # (the multi-feature API carries no weights)
+            out = dr.embedding_lookup_sparse_multi([ev], [sp], combiner=comb, out_dtype=out_dtype)
+        else:
+            out = dr.embedding_lookup_sparse(ev, sp, sp_weights=spw, combiner=comb)
+    assert out.dtype == out_dtype
     want = orc.embedding_lookup_sparse(oev, ind, v, B, weights=w, combiner=comb)
+    if out_dtype == torch.bfloat16:
+        want = orc.bf16_round(want)
     np.testing.assert_array_equal(f32(out), want)
 
 
@@ -166,13 +178,17 @@ def test_bf16_training_steps_match_oracle(dr, orc, opt):
     for step in range(3):
         ids = rng.integers(0, 160, (F, B)).astype(np.int64)
         sps = [dr.SparseTensor(T(ind), T(ids[f]), (B, 1)) for f in range(F)]
-        out = dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum")
-        assert out.dtype == torch.bfloat16
+        out = dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum",
+                                               out_dtype=torch.bfloat16 if step % 2 else None)
         want = np.concatenate([oevs[f].gather(ids[f]) for f in range(F)], 1)
         np.testing.assert_array_equal(f32(out), want)
         g = rng.standard_normal((B, F * D)).astype(np.float32)
-        out.backward(T(g).to(torch.bfloat16))
-        g16 = orc.bf16_round(g)                       # the bf16 output's gradient, widened
+        if out.dtype == torch.bfloat16:
+            out.backward(T(g).to(torch.bfloat16))
+            g16 = orc.bf16_round(g)                   # the bf16 output's gradient, widened
+        else:
+            out.backward(T(g))
+            g16 = g
         gs = step + 1
         o.apply_gradients(evs, global_step=gs)
         for f in range(F):
@@ -227,12 +243,13 @@ def test_bf16_xgmi_engine_matches_local(dr, orc):
         evs.append(e)
         oevs.append(o)
     eng = XgmiShardedLookup(evs, 1, 0, B, torch.device(DEV))
-    ids = rng.integers(0, 500, (F, B)).astype(np.int64)
-    out = eng.forward(T(ids))
-    torch.cuda.synchronize()
-    assert out.dtype == torch.bfloat16
-    want = np.concatenate([oevs[f].gather(ids[f]) for f in range(F)], 1)
-    np.testing.assert_array_equal(f32(out), want)
+    for step, odt in enumerate((torch.bfloat16, None)):
+        ids = rng.integers(0, 500, (F, B)).astype(np.int64)
+        out = eng.forward(T(ids), out_dtype=odt)
+        torch.cuda.synchronize()
+        assert out.dtype == (odt or torch.float32)
+        want = np.concatenate([oevs[f].gather(ids[f]) for f in range(F)], 1)
+        np.testing.assert_array_equal(f32(out), want)
     eng.close()
 
 
@@ -271,7 +288,8 @@ def test_bf16_alltoall_engine_multihot(dr, orc, world):
         try:
             ids, off = batches[r]
             with torch.no_grad():
-                o = engines[r].forward(T(ids), bag_offs=[T(off)] * F, combiner="mean")
+                o = engines[r].forward(T(ids), bag_offs=[T(off)] * F, combiner="mean",
+                                       out_dtype=torch.bfloat16 if r == 0 else None)
             outs[r] = o
         except Exception as e:
             errs.append(e)
@@ -287,11 +305,13 @@ def test_bf16_alltoall_engine_multihot(dr, orc, world):
     dr.status_check()
     for r in range(world):
         ids, off = batches[r]
-        assert outs[r].dtype == torch.bfloat16
+        assert outs[r].dtype == (torch.bfloat16 if r == 0 else torch.float32)
         seg = np.repeat(np.arange(B), np.diff(off))
         ind = np.stack([seg, np.zeros_like(seg)], 1)
         for f in range(F):
             oev = orc.EV(D, 0.5, bf16=True)
             oev.insert(allk, vals[f])
             want = orc.embedding_lookup_sparse(oev, ind, ids[f], B, combiner="mean")
+            if r == 0:
+                want = orc.bf16_round(want)
             np.testing.assert_array_equal(f32(outs[r][:, f * D:(f + 1) * D]), want)
