@@ -52,6 +52,11 @@ def parse():
     p.add_argument("--kernel-iters", type=int, default=20)
     p.add_argument("--no-deepfm", dest="deepfm", action="store_false",
                    help="skip the BASELINE configs[1] (DeepFM 26 x 1e7 x 64) leg at N=1")
+    p.add_argument("--no-criteo", dest="criteo", action="store_false",
+                   help="skip the real Criteo-TB cardinality legs (one fused table, prefix "
+                        "offsets; B_local 65536 / 8192, uniform / Zipf 1.05) at N=1")
+    p.add_argument("--no-dcn", dest="dcn", action="store_false",
+                   help="skip the BASELINE configs[4] bf16-table leg at N=1")
     p.add_argument("--engine", default="auto", choices=["auto", "local", "xgmi", "a2a"],
                    help="auto: local lookup at N=1, xgmi peer-write (RCCL all-to-all "
                         "fallback) at N>1; xgmi/a2a at N=1 run the sharded engine on itself")
@@ -165,6 +170,196 @@ def check_rows(out, ids, T, D, n_sample, seed):
                                  "(first key %d)" % (tt, bad.shape[0], sel.sum(),
                                                      keys[sel][bad[0]]))
     return int(n_sample)
+
+
+def _onehot_kernel_ms(feat_sets, iters, out_dtype=None):
+    """Average duration of the fused one-hot EV lookup kernel over launches
+    on the given feature sets in rotation (HIP events around the kernel on
+    its stream, dr_kernel_timing(1))."""
+    import ctypes as _C
+    from deeprec_amd import _lib
+    from deeprec_amd.embedding_ops import _fused_onehot
+    L = _lib.lib()
+    with torch.no_grad():
+        for fs in feat_sets:
+            assert _fused_onehot(fs, _lib.ORDER_ALI, out_dtype=out_dtype) is not None
+        torch.cuda.synchronize()
+        L.dr_kernel_timing(1)
+        for i in range(iters):
+            _fused_onehot(feat_sets[i % len(feat_sets)], _lib.ORDER_ALI, out_dtype=out_dtype)
+        torch.cuda.synchronize()
+        tot, cnt = _C.c_double(0.0), _C.c_int64(0)
+        _lib.check(L.dr_kernel_timing_result(_C.byref(tot), _C.byref(cnt)))
+        L.dr_kernel_timing(0)
+    if cnt.value != iters:
+        raise RuntimeError("kernel timing bracketed %d of %d launches" % (cnt.value, iters))
+    return tot.value / cnt.value
+
+
+def _free_hbm():
+    import gc
+    from deeprec_amd.kv_variable_ops import flush_releases
+    gc.collect()
+    torch.cuda.synchronize()
+    flush_releases()           # EV handles queued by __del__ (hipFree now)
+    torch.cuda.empty_cache()
+
+
+# Criteo-Terabyte cardinalities of the reference's SOK DLRM
+# (modelzoo/SOK/DLRM/train_stand.py:242-248), looked up in ONE fused table
+# with per-feature prefix offsets (model/models.py:69-76).
+CRITEO_TB_VOCAB = [39884406, 39043, 17289, 7420, 20263, 3, 7120, 1543, 63, 38532951, 2953546,
+                   403346, 10, 2208, 11938, 155, 4, 976, 14, 39979771, 25641295, 39664984, 585935,
+                   12972, 108, 36]
+
+
+def criteo_legs(args, dev, log):
+    """BASELINE configs[2] with the real Criteo-TB cardinalities (SURVEY 8d
+    #3): the 26 features share one 1.88e8-row x 128 fp32 EV (keys = prefix
+    offset + per-feature id), the fused one-hot lookup at B_local = 65 536
+    and 8 192 (SOK's 65 536 / 8), uniform ids per feature and Zipf(1.05).
+    lookups/s from the kernel's own launches over 4 rotating batches; the
+    algorithmic bytes stay 1048 per lookup (small features hit the same rows
+    again, so the HBM traffic is lower than that)."""
+    import deeprec_amd as dr
+    from deeprec_amd.embedding_ops import _Feature
+    T, D = 26, 128
+    card = np.array(CRITEO_TB_VOCAB, np.int64)
+    pre = np.concatenate([[0], np.cumsum(card)[:-1]])
+    total = int(card.sum())
+    t0 = time.perf_counter()
+    ev = dr.EmbeddingVariable("criteo_fused", D, 0.0, device=dev, capacity=total + (1 << 22))
+    ev.insert_synthetic(0, total, seed=4242)
+    torch.cuda.synchronize()
+    log("criteo fused table: %d rows x %d in %.1fs" % (total, D, time.perf_counter() - t0))
+    cardt = torch.as_tensor(card, device=dev)[None, :]
+    pret = torch.as_tensor(pre, device=dev)[None, :]
+    per = 8 + 16 + 2 * D * 4
+    res = {"table": "one EV of %d rows x %d fp32 (26 Criteo-TB features, prefix offsets; "
+                    "modelzoo/SOK/DLRM/train_stand.py:242-248, model/models.py:69-76)"
+                    % (total, D), "bytes_per_lookup": per}
+    for B in (65536, 8192):
+        seg = torch.arange(B, dtype=torch.int32, device=dev)
+        for dist_name in ("uniform", "zipf1.05"):
+            recs = []
+            for k in range(4):
+                if dist_name == "uniform":
+                    g = torch.Generator(device=dev)
+                    g.manual_seed(300 + k)
+                    u = torch.rand((B, T), generator=g, device=dev, dtype=torch.float64)
+                    ids = (u * cardt).to(torch.int64)
+                else:
+                    z = np.random.default_rng(400 + k).zipf(1.05, size=(B, T)) - 1
+                    ids = torch.as_tensor(z, device=dev) % cardt
+                recs.append((ids + pret).contiguous())          # record-major [B, T]
+            fsets = [[_Feature(ev, r[:, t], seg, B, None, "sum", None, onehot=True)
+                      for t in range(T)] for r in recs]
+            k_ms = _onehot_kernel_ms(fsets, args.kernel_iters)
+            ach = T * B * per / (k_ms * 1e-3) / 1e9
+            res["B%d_%s" % (B, dist_name)] = {
+                "lookups_per_s": round(T * B / (k_ms * 1e-3), 1),
+                "samples_per_s": round(B / (k_ms * 1e-3), 1), "kernel_ms": round(k_ms, 4),
+                "achieved_algorithmic_GBs": round(ach, 1),
+                "frac": round(ach / PEAK_HBM_GBS, 4),
+                "distinct_keys_batch0": int(torch.unique(recs[0]).numel())}
+            log("criteo B=%d %s: %s" % (B, dist_name, json.dumps(res["B%d_%s" % (B, dist_name)])))
+    dr.status_check(dev)
+    del ev, fsets
+    return res
+
+
+def dcn_bf16_leg(args, dev, log):
+    """BASELINE configs[4] per-GPU embedding shape with bf16 tables: 26 bf16
+    EVs x 12.5 M rows x 128, B = 65 536, the fused one-hot lookup writing
+    the bf16 [B, 26*128] CrossNet input bitwise (8 key + 16 slot + 256 row
+    + 256 out bytes per lookup), and the embedding training step on those
+    tables (fp32 gradients, SGD rounding each updated value to bf16)."""
+    import deeprec_amd as dr
+    from deeprec_amd.embedding_ops import SparseTensor, _Feature
+    T, D, R, B = 26, 128, 12_500_000, args.batch
+    evs = []
+    t0 = time.perf_counter()
+    for t in range(T):
+        ev = dr.EmbeddingVariable("dcn%d" % t, D, 0.0, device=dev, capacity=R + (1 << 20),
+                                  value_dtype=torch.bfloat16)
+        ev.insert_synthetic(0, R, seed=6000 + t)
+        evs.append(ev)
+    torch.cuda.synchronize()
+    log("dcn bf16 tables in %.1fs" % (time.perf_counter() - t0))
+    batches = make_batches(4, T, B, R, 0.0, 91, dev)
+    recs = [ids.t().contiguous() for ids in batches]
+    seg = torch.arange(B, dtype=torch.int32, device=dev)
+    fsets = [[_Feature(evs[t], r[:, t], seg, B, None, "sum", None, onehot=True) for t in range(T)]
+             for r in recs]
+    k_ms = _onehot_kernel_ms(fsets, args.kernel_iters, out_dtype=torch.bfloat16)
+    per = 8 + 16 + 2 * D * 2
+    ach = T * B * per / (k_ms * 1e-3) / 1e9
+    # parity at this size: sampled rows of one output == bf16(synth) bitwise
+    from deeprec_amd.embedding_ops import _fused_onehot
+    from deeprec_amd import _lib
+    with torch.no_grad():
+        out = _fused_onehot(fsets[0], _lib.ORDER_ALI, out_dtype=torch.bfloat16)
+    rng = np.random.default_rng(3)
+    bs, ts = rng.integers(0, B, 2048), rng.integers(0, T, 2048)
+    got = out.view(B, T, D)[torch.as_tensor(bs, device=dev), torch.as_tensor(ts, device=dev)]
+    got = got.view(torch.int16).cpu().numpy().view(np.uint16)
+    keys = recs[0][torch.as_tensor(bs, device=dev), torch.as_tensor(ts, device=dev)].cpu().numpy()
+    for tt in np.unique(ts):
+        sel = ts == tt
+        w = synth_rows(6000 + int(tt), keys[sel], D)
+        wb = ((w.view(np.uint32) + np.uint32(0x7FFF) + ((w.view(np.uint32) >> 16) & 1)) >> 16)
+        if not np.array_equal(got[sel], wb.astype(np.uint16)):
+            raise AssertionError("dcn bf16 leg: table %d rows differ from bf16(synth)" % tt)
+    ind = torch.stack([torch.arange(B, device=dev), torch.zeros(B, dtype=torch.int64, device=dev)],
+                      1)
+    sps = [[SparseTensor(ind, ids[t], (B, 1)) for t in range(T)] for ids in batches]
+    opt = dr.GradientDescentOptimizer(0.01)
+    up = torch.randn((B, T * D), device=dev).to(torch.bfloat16)
+
+    def tstep(i):
+        o = dr.embedding_lookup_sparse_multi(evs, sps[i % 4], combiner="sum",
+                                             out_dtype=torch.bfloat16)
+        o.backward(up)
+        opt.apply_gradients(evs)
+
+    for i in range(2):
+        tstep(i)
+    torch.cuda.synchronize()
+    for ev in evs:
+        ev.reserve(8 * B)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for i in range(4):
+            tstep(i)
+    g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    reps = max(1, args.train_steps // 4)
+    for _ in range(reps):
+        g.replay()
+    torch.cuda.synchronize()
+    tms = (time.perf_counter() - t0) / (4 * reps) * 1e3
+    dr.status_check(dev)
+    res = {"workload": "BASELINE configs[4] per-GPU embedding shape: 26 bf16 EV tables x %d rows "
+                       "x %d, B=%d, hotness 1, uniform keys, fused one-hot lookup into the bf16 "
+                       "CrossNet input (DR_LOOKUP_OUT_BF16)" % (R, D, B),
+           "lookups_per_s": round(T * B / (k_ms * 1e-3), 1),
+           "samples_per_s": round(B / (k_ms * 1e-3), 1),
+           "checked_rows": 2048,
+           "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
+                        "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
+                        "kernel": "dr::ev_lookup_onehot_kernel<4,16,1,ALI,4> on bf16 rows "
+                                  "(64 float words)",
+                        "kernel_ms": round(k_ms, 4), "bytes_per_lookup": per,
+                        "bytes_per_launch": T * B * per},
+           "train_step": {"ms_per_step": round(tms, 4),
+                          "samples_per_s": round(B / (tms * 1e-3), 1),
+                          "step": "fused bf16 lookup recording rows + row-grouped backward (fp32 "
+                                  "gradients) + by-address KV SGD rounding to bf16, hipGraph of "
+                                  "4 steps"}}
+    log("dcn bf16 leg: %s" % json.dumps(res))
+    del evs, fsets, g
+    return res
 
 
 def deepfm_leg(args, dev, log):
@@ -669,16 +864,22 @@ def main():
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args)
 
-    deepfm = None
-    if world == 1 and args.deepfm:
-        # drop every holder of the headline EVs so their HBM is released
-        evs = feats = gfeats = batch_sps = None
-        engine = a2a = None
-        import gc
-        gc.collect()
-        torch.cuda.synchronize()
-        torch.cuda.empty_cache()
-        deepfm = deepfm_leg(args, dev, log)
+    deepfm = criteo = dcn = None
+    if world == 1 and (args.deepfm or args.criteo or args.dcn):
+        # drop every holder of the headline EVs so their HBM is released;
+        # each leg below frees its own tables before the next one
+        evs = feats = gfeats = batch_sps = rec_sps = kfeats = gsets = None
+        engine = a2a = outc = graph_all = tgraph = opt = None
+        _free_hbm()
+        if args.deepfm:
+            deepfm = deepfm_leg(args, dev, log)
+            _free_hbm()
+        if args.criteo:
+            criteo = criteo_legs(args, dev, log)
+            _free_hbm()
+        if args.dcn:
+            dcn = dcn_bf16_leg(args, dev, log)
+            _free_hbm()
 
     if rank == 0:
         with open(os.path.join(ROOT, "BASELINE.json")) as f:
@@ -710,6 +911,8 @@ def main():
             "forward_samples_per_s": round(value / T, 1),
             "train_step": train,
             "deepfm_config": deepfm,
+            "criteo_tb_cardinalities": criteo,
+            "dcn_bf16_config": dcn,
             "correctness": correctness,
             "roofline": roof,
             "roofline_row_gather": roof_gather,
