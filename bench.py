@@ -57,6 +57,9 @@ def parse():
                         "offsets; B_local 65536 / 8192, uniform / Zipf 1.05) at N=1")
     p.add_argument("--no-dcn", dest="dcn", action="store_false",
                    help="skip the BASELINE configs[4] bf16-table leg at N=1")
+    p.add_argument("--dedup", action="store_true",
+                   help="xgmi engine: per-destination dedup before the exchange (grouped Unique, "
+                        "unique keys routed, rows expanded locally)")
     p.add_argument("--engine", default="auto", choices=["auto", "local", "xgmi", "a2a"],
                    help="auto: local lookup at N=1, xgmi peer-write (RCCL all-to-all "
                         "fallback) at N>1; xgmi/a2a at N=1 run the sharded engine on itself")
@@ -499,7 +502,7 @@ def main():
         keyspace = R * world
         engine = None
         if want == "xgmi" and world == 1:
-            engine = XgmiShardedLookup(evs, 1, 0, B, dev)
+            engine = XgmiShardedLookup(evs, 1, 0, B, dev, dedup=args.dedup)
             engine_kind = "xgmi peer-write"
         elif want == "xgmi":
             # peer writes over xGMI; every rank must succeed or all fall back
@@ -510,7 +513,8 @@ def main():
                     def barrier():
                         torch.cuda.synchronize()
                         dist.barrier()
-                engine = XgmiShardedLookup(evs, world, rank, B, dev, barrier=barrier)
+                engine = XgmiShardedLookup(evs, world, rank, B, dev, barrier=barrier,
+                                           dedup=args.dedup)
             except Exception as e:  # IPC mapping unavailable
                 ok, err = 0, str(e)
             flag = torch.tensor([ok], dtype=torch.int32, device="cpu" if staged else dev)
@@ -535,6 +539,8 @@ def main():
         if engine is None:
             engine = a2a
             engine_kind = "RCCL all-to-all"
+        if args.dedup and engine is not None and engine is not a2a:
+            engine_kind += " + dedup"
         log("sharded engine: %s" % engine_kind)
     else:
         engine = None
@@ -640,7 +646,7 @@ def main():
             # then two more steps, against the all-to-all engine
             with torch.no_grad():
                 kl = (args.steps - 1) % NBATCH
-                last = engine.bufs.out.clone()
+                last = (engine.forward(batches[kl]) if engine.dedup else engine.bufs.out).clone()
                 same = int(torch.equal(last, a2a.forward(batches[kl])))
                 if world > 1:
                     flag = torch.tensor([same], dtype=torch.int32,

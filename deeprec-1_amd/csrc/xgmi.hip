@@ -28,8 +28,12 @@ struct XgmiArgs {
 // the block's run in the owner's region.
 constexpr int RT_ITEMS = 8;
 
+// n_dev (nullable, DEVICE [T]): only ids b < n_dev[t] of table t are routed
+// -- the deduplicating requester routes each table's first-occurrence unique
+// keys (u = b < U_t) and expands the rows it gets back locally.
 __global__ __launch_bounds__(256) void xgmi_route_kernel(XgmiArgs a, const int64_t* __restrict__ keys,
                                                          int T, int64_t B,
+                                                         const int64_t* __restrict__ n_dev,
                                                          unsigned long long* __restrict__ cnt) {
   __shared__ unsigned int lcnt[DR_MAX_PEERS];
   __shared__ unsigned long long lbase[DR_MAX_PEERS];
@@ -47,9 +51,11 @@ __global__ __launch_bounds__(256) void xgmi_route_kernel(XgmiArgs a, const int64
     if (j < n) {
       const int64_t b = j / T;
       const int t = (int)(j - b * T);
-      int64_t o = keys[(int64_t)t * B + b] % a.world;
-      if (o < 0) o += a.world;
-      owner = (int)o;
+      if (!n_dev || b < n_dev[t]) {
+        int64_t o = keys[(int64_t)t * B + b] % a.world;
+        if (o < 0) o += a.world;
+        owner = (int)o;
+      }
     }
     own[it] = owner;
     off[it] = 0;
@@ -477,8 +483,8 @@ int dr_ipc_alloc_dlpack(int ndim, const int64_t* shape, int dtype_code, int dtyp
   return DR_OK;
 }
 
-int dr_xgmi_route(const dr_xgmi_peers* peers, const int64_t* keys, int num_tables,
-                  int64_t batch, int64_t* cnt_ws, void* stream) {
+int dr_xgmi_route_ex(const dr_xgmi_peers* peers, const int64_t* keys, int num_tables,
+                     int64_t batch, const int64_t* n_dev, int64_t* cnt_ws, void* stream) {
   using namespace dr;
   DR_REQUIRE(peers && cnt_ws && num_tables >= 1 && batch >= 0, DR_INVALID_ARGUMENT,
              "bad argument");
@@ -506,12 +512,17 @@ int dr_xgmi_route(const dr_xgmi_peers* peers, const int64_t* keys, int num_table
   if (n > 0) {
     DR_REQUIRE(keys, DR_INVALID_ARGUMENT, "null keys");
     hipLaunchKernelGGL(xgmi_route_kernel, dim3((unsigned)ceil_div(n, 256 * RT_ITEMS)), dim3(256),
-                       0, st, a, keys, num_tables, batch, (unsigned long long*)cnt_ws);
+                       0, st, a, keys, num_tables, batch, n_dev, (unsigned long long*)cnt_ws);
   }
   hipLaunchKernelGGL(xgmi_counts_kernel, dim3(64), dim3(64), 0, st, a,
                      (const unsigned long long*)cnt_ws);
   DR_LAUNCH_CHECK();
   return DR_OK;
+}
+
+int dr_xgmi_route(const dr_xgmi_peers* peers, const int64_t* keys, int num_tables,
+                  int64_t batch, int64_t* cnt_ws, void* stream) {
+  return dr_xgmi_route_ex(peers, keys, num_tables, batch, nullptr, cnt_ws, stream);
 }
 
 

@@ -211,6 +211,7 @@ SIGNATURES = {
     "dr_ipc_free": (_I32, [_P]),
     "dr_ipc_alloc_dlpack": (_I32, [_I32, _P, _I32, _I32, _I32, _P]),
     "dr_xgmi_route": (_I32, [_P, _P, _I32, _I64, _P, _P]),
+    "dr_xgmi_route_ex": (_I32, [_P, _P, _I32, _I64, _P, _P, _P]),
     "dr_xgmi_serve_workspace_size": (_SZ, [_I32, _I64]),
     "dr_xgmi_serve": (_I32, [_P, _P, _I32, _I64, _P, _SZ, _P]),
     "dr_xgmi_grad_pull_workspace_size": (_SZ, [_I32, _I64]),

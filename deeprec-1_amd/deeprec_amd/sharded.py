@@ -455,10 +455,23 @@ class XgmiShardedLookup(object):
 
     forward() returns this rank's persistent output buffer: it is rewritten
     by the next forward(), so consume it (on the same stream) first.
-    peer_buffers / barrier let tests run several ranks in one process."""
+    peer_buffers / barrier let tests run several ranks in one process.
+
+    dedup=True: per-destination dedup before the exchange (SOK,
+    all2all_input_dispatcher.cu:36-126): the requester runs the grouped
+    first-occurrence Unique over its [T, B] ids, routes each table's unique
+    keys only (dr_xgmi_route_ex), the owners write one row per unique key
+    into the (then staging) peer buffer at slot u*T + t, and the requester
+    expands them over its bags with the one-hot pooling kernel into a local
+    output.  The links carry one row per distinct key instead of one per
+    id -- the lever for skewed (Zipf / real-cardinality) batches; the
+    Unique and the local expansion are the price.  The backward sums each
+    unique key's gradient locally first (dr_pool_grad_grouped, the
+    reference's per-worker IndexedSlices) and the owners pull those rows.
+    Outputs are bit-identical to the non-dedup path and to one GPU."""
 
     def __init__(self, evs, world, rank, batch, device, group=None, peer_buffers=None,
-                 barrier=None, buffers=None):
+                 barrier=None, buffers=None, dedup=False):
         if world > _lib.MAX_PEERS:
             raise ValueError("world %d > %d" % (world, _lib.MAX_PEERS))
         for e in evs:
@@ -492,6 +505,11 @@ class XgmiShardedLookup(object):
         self.ws = workspace(self.wsb, device)
         self.flag = torch.zeros(1, dtype=torch.float32, device=device)
         self._barrier = barrier or self._rccl_barrier
+        self.dedup = bool(dedup)
+        self._local = HipLocal(evs, device)
+        self._koff = [t * batch for t in range(self.T + 1)]
+        self._tcol = torch.arange(self.T, dtype=torch.int64, device=device)[:, None]
+        self._saved = None
 
     def _exchange_ipc(self):
         mine = []
@@ -520,9 +538,9 @@ class XgmiShardedLookup(object):
     def _rccl_barrier(self):
         dist.all_reduce(self.flag, group=self.group)
 
-    def route(self, ids):
-        check(lib().dr_xgmi_route(C.byref(self.peers), ptr(ids), self.T, self.batch,
-                                  ptr(self.cnt_ws), stream_handle(self.device)))
+    def route(self, ids, n_dev=None):
+        check(lib().dr_xgmi_route_ex(C.byref(self.peers), ptr(ids), self.T, self.batch,
+                                     ptr(n_dev), ptr(self.cnt_ws), stream_handle(self.device)))
         ops._post(self.device)
 
     def serve(self):
@@ -548,7 +566,17 @@ class XgmiShardedLookup(object):
         T, D, B, W = self.T, self.dim, self.batch, self.world
         if tuple(g.shape) != (B, T * D) or not g.is_floating_point():
             raise ValueError("grad must be [%d, %d]" % (B, T * D))
-        self.bufs.gin.copy_(g)
+        if self.dedup:
+            # per unique key: the sum of its positions' gradients (ascending
+            # position, SparseSegmentSumGrad), laid out at the forward's slots
+            # u*T + t for the owners' pulls
+            if self._saved is None:
+                raise RuntimeError("backward() needs a dedup forward() first")
+            idx, U = self._saved
+            gu = self._local.pool_grad(g.float(), idx, self._koff, U, None, B, "sum")
+            self.bufs.gin.view(B, T, D).copy_(gu[:T * B].view(T, B, D).transpose(0, 1))
+        else:
+            self.bufs.gin.copy_(g)
         self._barrier()
         tcap = W * B
         keys = torch.empty(T * tcap, dtype=torch.int64, device=self.device)
@@ -577,6 +605,18 @@ class XgmiShardedLookup(object):
         if tuple(ids.shape) != (self.T, self.batch) or ids.dtype != torch.int64:
             raise ValueError("ids must be int64 [%d, %d]" % (self.T, self.batch))
         ids = ids.contiguous()
+        if self.dedup:
+            T, B = self.T, self.batch
+            uniq, idx, _, U = ops.unique_grouped(ids.view(-1), self._koff, False)
+            self.route(uniq, n_dev=U)
+            self._barrier()
+            self.serve()
+            self._barrier()
+            # expand: bag (b, t) reads the staging row of its unique key
+            rowsel = (idx.view(T, B).to(torch.int64) * T + self._tcol).view(-1)
+            self._saved = (idx, U)
+            return self._local.pool(self.bufs.out.view(B * T, self.dim), rowsel, None,
+                                    self._koff, None, B, "sum", out_dtype)
         self.route(ids)
         self._barrier()
         self.serve()

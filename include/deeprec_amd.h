@@ -767,6 +767,14 @@ typedef struct {
 /* cnt_ws: DEVICE int64[world] scratch.  Requires T*B <= cap.                */
 int dr_xgmi_route(const dr_xgmi_peers* peers, const int64_t* keys, int num_tables,
                   int64_t batch, int64_t* cnt_ws, void* stream);
+/* The same routing only ids b < n_dev[t] of each table t (n_dev: DEVICE   */
+/* int64[num_tables], nullable = all): the deduplicating requester routes   */
+/* each table's first-occurrence unique keys (dr_unique_grouped output laid */
+/* out [T, batch], u = b < U_t) -- SOK's per-destination dedup before the   */
+/* key exchange (all2all_input_dispatcher.cu:36-126) -- and expands the     */
+/* rows it gets back (slot u*T + t) over its bags locally.                  */
+int dr_xgmi_route_ex(const dr_xgmi_peers* peers, const int64_t* keys, int num_tables,
+                     int64_t batch, const int64_t* n_dev, int64_t* cnt_ws, void* stream);
 size_t dr_xgmi_serve_workspace_size(int world, int64_t cap);
 int dr_xgmi_serve(const dr_xgmi_peers* peers, dr_ev* const* evs, int num_tables,
                   int64_t batch, void* ws, size_t ws_bytes, void* stream);

@@ -236,6 +236,84 @@ def test_xgmi_peer_write_engine(world):
     _run_xgmi(world)
 
 
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_xgmi_dedup_engine(world):
+    """Peer-write engine with per-destination dedup (dr_xgmi_route_ex over
+    the grouped Unique, local expansion): Zipf-skewed ids with hot keys
+    shared across ranks.  Forward bit-exact vs the oracle (and hence vs the
+    plain engine); backward: each owner pulls, per table and source rank,
+    the source's unique keys in first-occurrence order with their summed
+    gradient (SparseSegmentSumGrad over ascending positions) -- each
+    worker's IndexedSlices, concatenated in rank order."""
+    import deeprec_amd as dr
+    from oracle import oracle as orc
+    from deeprec_amd.sharded import XgmiBuffers, XgmiShardedLookup
+    dr.load()
+    rng = np.random.default_rng(71 + world)
+    evs_all, bufs = [], []
+    for r in range(world):
+        own = np.arange(r, KEYSPACE // 2, world, dtype=np.int64)
+        evs = []
+        for t in range(T):
+            ev = dr.EmbeddingVariable("xgd%d_%d_%d" % (world, r, t), D, DEFAULT, device=DEV)
+            ev.insert(torch.as_tensor(own, device=DEV), torch.as_tensor(_vals(t, own), device=DEV))
+            evs.append(ev)
+        evs_all.append(evs)
+        bufs.append(XgmiBuffers(world, T, B, D, DEV))
+    bar = threading.Barrier(world)
+    engines = [XgmiShardedLookup(evs_all[r], world, r, B, torch.device(DEV), peer_buffers=bufs,
+                                 barrier=bar.wait, buffers=bufs[r], dedup=True)
+               for r in range(world)]
+    allk = np.arange(0, KEYSPACE // 2, dtype=np.int64)
+    ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+    for step in range(2):
+        ids = [((rng.zipf(1.2, size=(T, B)) - 1) % KEYSPACE).astype(np.int64)
+               for _ in range(world)]
+        grads = [rng.standard_normal((B, T * D)).astype(np.float32) for _ in range(world)]
+        outs, pulled, errs = [None] * world, [None] * world, []
+
+        def run(r):
+            try:
+                o = engines[r].forward(torch.as_tensor(ids[r], device=DEV))
+                outs[r] = o.cpu().numpy()
+                got = engines[r].backward(torch.as_tensor(grads[r], device=DEV))
+                pulled[r] = []
+                for k, v, n in got:
+                    m = int(n.item())
+                    pulled[r].append((k[:m].cpu().numpy(), v[:m].cpu().numpy()))
+            except Exception as e:
+                errs.append(e)
+                bar.abort()
+
+        th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(120)
+        if errs:
+            raise errs[0]
+        dr.status_check()
+        for r in range(world):
+            for t in range(T):
+                ref_ev = orc.EV(D, DEFAULT)
+                ref_ev.insert(allk, _vals(t, allk))
+                ref = orc.embedding_lookup_sparse(ref_ev, ind, ids[r][t], B, combiner="sum")
+                np.testing.assert_array_equal(outs[r][:, t * D:(t + 1) * D], ref)
+                wk, wg = [], []
+                for src in range(world):
+                    uids, idx = orc.unique(ids[src][t])
+                    gu = orc.sparse_segment_reduce_grad(
+                        np.ascontiguousarray(grads[src][:, t * D:(t + 1) * D]), idx,
+                        np.arange(B, dtype=np.int32), uids.size, "sum")
+                    sel = uids % world == r
+                    wk.append(uids[sel])
+                    wg.append(gu[sel])
+                k, v = pulled[r][t]
+                np.testing.assert_array_equal(k, np.concatenate(wk))
+                np.testing.assert_array_equal(v, np.concatenate(wg).reshape(-1, D))
+                evs_all[r][t].pending_grads.clear()
+
+
 @pytest.mark.parametrize("world", [1, 2])
 def test_xgmi_serve_grows_small_tables(world):
     """Owners whose EVs start with room for 256 rows receive ~3x that many new
