@@ -1678,17 +1678,31 @@ __device__ __forceinline__ int64_t ev_probe_row(const LkDesc& e, uint64_t key) {
     if (sv.x != 0ull) return -1;
     rc = sv.y;
   } else {
+    // Two slots per step, loaded together: at the tables' load factor a
+    // third of the keys sit past their home slot (linear probing), almost
+    // always in the next one and the same 128-B line.  The pair costs one
+    // memory round trip where slot-at-a-time probing paid a dependent second
+    // one for those keys.
     const uint64_t mask = (uint64_t)e.cap - 1;
     uint64_t h = mix64(key) & mask;
-    for (int64_t probes = 0;; ++probes) {
+    for (int64_t probes = 0;; probes += 2) {
       if (probes > e.cap) return -1;
-      const slot_v sv = gld(reinterpret_cast<const slot_v*>(e.slots + h));
-      if (sv.x == key) {
-        rc = sv.y;
+      const slot_v s0 = gld(reinterpret_cast<const slot_v*>(e.slots + h));
+      const slot_v s1 = gld(reinterpret_cast<const slot_v*>(e.slots + ((h + 1) & mask)));
+      // both loads issue before the first compare (hipcc would otherwise
+      // sink the second into the miss branch, after a wait for the first)
+      __asm__ volatile("" ::"v"(s1));
+      if (s0.x == key) {
+        rc = s0.y;
         break;
       }
-      if (sv.x == kEmptyKey) return -1;  // (a stale empty only sends it to the miss path)
-      h = (h + 1) & mask;
+      if (s0.x == kEmptyKey) return -1;  // (a stale empty only sends it to the miss path)
+      if (s1.x == key) {
+        rc = s1.y;
+        break;
+      }
+      if (s1.x == kEmptyKey) return -1;
+      h = (h + 2) & mask;
     }
   }
   if (rc == kUnset || !(rc & e.colbit)) return -1;
@@ -1704,24 +1718,36 @@ __global__ __launch_bounds__(256) void ev_lookup_onehot_kernel(LookupArgs a, int
                                                                int dim, int32_t* __restrict__ mlist,
                                                                unsigned long long* __restrict__ mcnt) {
   __shared__ LkDesc sd[DR_MAX_GROUP];  // per-lane table index: stage in LDS
-  if (threadIdx.x < T) sd[threadIdx.x] = a.d[threadIdx.x];
-  __syncthreads();
   constexpr int GPB = 256 / G;
   const int64_t slots = (int64_t)T * B;
   const int64_t s0 = ((int64_t)blockIdx.x * GPB + threadIdx.x / G) * NB;
-  if (s0 >= slots) return;
   const int lg = threadIdx.x % G;
+  // The probing lanes' ids are loaded BEFORE the descriptor staging and its
+  // barrier: the id's memory round trip overlaps them (the ids are read
+  // once: nontemporal).
+  const bool prober = lg < NB && s0 + lg < slots;
+  int64_t pb = 0;
+  int pt = 0;
+  uint64_t pkey = 0;
+  if (prober) {
+    const int64_t s = s0 + lg;
+    pb = (int64_t)((uint32_t)s / (uint32_t)T);  // slots < 2^31 (host check)
+    pt = (int)(s - pb * T);
+    pkey = (uint64_t)__builtin_nontemporal_load(gp(a.keys + pb * a.ksb + (int64_t)pt * a.kst));
+  }
+  if (threadIdx.x < T) sd[threadIdx.x] = a.d[threadIdx.x];
+  __syncthreads();
+  if (s0 >= slots) return;
   const int dv = dim / VEC;
   const int base = (int)(threadIdx.x % 64) - lg;
   // lanes 0..NB-1 of the group probe one slot each
   const float* mine = nullptr;
   bool missed = false;
-  if (lg < NB && s0 + lg < slots) {
-    const int64_t s = s0 + lg;
-    const int64_t b = (int64_t)((uint32_t)s / (uint32_t)T);  // slots < 2^31 (host check)
-    const int t = (int)(s - b * T);
+  if (prober) {
+    const int64_t b = pb;
+    const int t = pt;
     const LkDesc& e = sd[t];
-    const int64_t row = ev_probe_row(e, (uint64_t)gld(a.keys + b * a.ksb + (int64_t)t * a.kst));
+    const int64_t row = ev_probe_row(e, pkey);
     if (row >= 0) {
       mine = e.pool + row * (int64_t)(WIDEN ? dim / 2 : dim);
       if (a.rows) a.rows[(int64_t)t * B + b] = row;
