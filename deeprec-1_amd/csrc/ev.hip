@@ -1678,31 +1678,20 @@ __device__ __forceinline__ int64_t ev_probe_row(const LkDesc& e, uint64_t key) {
     if (sv.x != 0ull) return -1;
     rc = sv.y;
   } else {
-    // Two slots per step, loaded together: at the tables' load factor a
-    // third of the keys sit past their home slot (linear probing), almost
-    // always in the next one and the same 128-B line.  The pair costs one
-    // memory round trip where slot-at-a-time probing paid a dependent second
-    // one for those keys.
     const uint64_t mask = (uint64_t)e.cap - 1;
     uint64_t h = mix64(key) & mask;
-    for (int64_t probes = 0;; probes += 2) {
+    // (a two-slots-per-step variant -- home and next slot loaded together,
+    // for the third of the keys past their home slot -- measured no gain:
+    // the dependent second probe mostly hits the line already in L2)
+    for (int64_t probes = 0;; ++probes) {
       if (probes > e.cap) return -1;
-      const slot_v s0 = gld(reinterpret_cast<const slot_v*>(e.slots + h));
-      const slot_v s1 = gld(reinterpret_cast<const slot_v*>(e.slots + ((h + 1) & mask)));
-      // both loads issue before the first compare (hipcc would otherwise
-      // sink the second into the miss branch, after a wait for the first)
-      __asm__ volatile("" ::"v"(s1));
-      if (s0.x == key) {
-        rc = s0.y;
+      const slot_v sv = gld(reinterpret_cast<const slot_v*>(e.slots + h));
+      if (sv.x == key) {
+        rc = sv.y;
         break;
       }
-      if (s0.x == kEmptyKey) return -1;  // (a stale empty only sends it to the miss path)
-      if (s1.x == key) {
-        rc = s1.y;
-        break;
-      }
-      if (s1.x == kEmptyKey) return -1;
-      h = (h + 2) & mask;
+      if (sv.x == kEmptyKey) return -1;  // (a stale empty only sends it to the miss path)
+      h = (h + 1) & mask;
     }
   }
   if (rc == kUnset || !(rc & e.colbit)) return -1;

@@ -214,17 +214,28 @@ int scan_exclusive_marks(const int32_t* in, int32_t* out, int64_t n, int64_t* to
 // scatter block, 256 entries) + the digit's row prefix + the tile-local
 // offset inside the digit's run.
 // ---------------------------------------------------------------------------
+// Tile = 256 threads x R rounds of keys.  R = 16 (4096-key tiles) left a
+// 1.7 M-pair sort with 416 blocks, every one of them resident at once and
+// the pass bound by one block's 16 serial ranking rounds; R = 8 halves that
+// chain at the same residency (DR_SORT_ROUNDS: 16 / 8 / 4 A/B switch).
 static constexpr int kSortThreads = 256;
-static constexpr int kSortRounds = 16;
-static constexpr int kSortTile = kSortThreads * kSortRounds;
+static int sort_rounds() {
+  static const int r = [] {
+    const char* e = getenv("DR_SORT_ROUNDS");
+    const int v = e ? atoi(e) : 8;
+    return (v == 4 || v == 16) ? v : 8;
+  }();
+  return r;
+}
 
 // n_dev (optional DEVICE count <= n): the grid is sized for n, tiles past
 // the device count contribute empty histograms and scatter nothing.
-template <class K>
+template <class K, int kSortRounds>
 __global__ __launch_bounds__(256) void sort_hist_kernel(const K* __restrict__ keys, int64_t n,
                                                         const int64_t* n_dev, int shift,
                                                         int dmask, int32_t* __restrict__ hist,
                                                         int64_t nblocks) {
+  constexpr int kSortTile = kSortThreads * kSortRounds;
   __shared__ int cnt[256];
   cnt[threadIdx.x] = 0;
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
@@ -266,12 +277,13 @@ __global__ __launch_bounds__(256) void sort_rowscan_kernel(int32_t* __restrict__
 // read of a counter and the group leader's update are ordered, so the loop
 // needs no block barrier.  Tile offset of (wave w, digit d) =
 // exclusive-over-digits(total) + sum over w' < w of the wave counts.
-template <class K>
+template <class K, int kSortRounds>
 __global__ __launch_bounds__(256) void sort_scatter_kernel(
     const K* __restrict__ kin, const int32_t* __restrict__ vin, K* __restrict__ kout,
     int32_t* __restrict__ vout, int64_t n, const int64_t* n_dev, int shift, int dmask,
     const int32_t* __restrict__ row_scanned, const int32_t* __restrict__ digit_tot,
     int64_t nblocks) {
+  constexpr int kSortTile = kSortThreads * kSortRounds;
   __shared__ K sk[kSortTile];
   __shared__ int32_t sv[kSortTile];
   __shared__ int wcnt[4][256];
@@ -362,7 +374,8 @@ static size_t sort_ws_bytes(int64_t n) {
   Carver c(nullptr);
   c.take<K>(n > 0 ? n : 1);
   c.take<int32_t>(n > 0 ? n : 1);
-  c.take<int32_t>((size_t)256 * ceil_div(n > 0 ? n : 1, kSortTile));
+  // sized for the smallest tile any switch setting uses
+  c.take<int32_t>((size_t)256 * ceil_div(n > 0 ? n : 1, kSortThreads * 4));
   c.take<int32_t>(256);
   return c.used + 256;
 }
@@ -375,8 +388,9 @@ static int sort_pairs(const K* keys_in, const int32_t* vals_in, K* keys_out, int
   Carver c(ws);
   K* ktmp = c.take<K>(n);
   int32_t* vtmp = c.take<int32_t>(n);
-  const int64_t nblocks = ceil_div(n, kSortTile);
-  int32_t* hist = c.take<int32_t>((size_t)256 * nblocks);
+  const int rounds = sort_rounds();
+  const int64_t nblocks = ceil_div(n, (int64_t)kSortThreads * rounds);
+  int32_t* hist = c.take<int32_t>((size_t)256 * ceil_div(n, (int64_t)kSortThreads * 4));
   int32_t* dtot = c.take<int32_t>(256);
   int passes = (bit_hi - bit_lo + 7) / 8;
   if (passes == 0) {
@@ -393,12 +407,23 @@ static int sort_pairs(const K* keys_in, const int32_t* vals_in, K* keys_out, int
     const int shift = bit_lo + 8 * p;
     const int dbits = bit_hi - shift < 8 ? bit_hi - shift : 8;   // bits >= bit_hi are ignored
     const int dmask = (1 << dbits) - 1;
-    hipLaunchKernelGGL(sort_hist_kernel<K>, dim3((unsigned)nblocks), dim3(kSortThreads), 0, st,
-                       ks, n, n_dev, shift, dmask, hist, nblocks);
-    hipLaunchKernelGGL(sort_rowscan_kernel, dim3(256), dim3(kSortThreads), 0, st, hist, nblocks,
-                       dtot);
-    hipLaunchKernelGGL(sort_scatter_kernel<K>, dim3((unsigned)nblocks), dim3(kSortThreads), 0, st,
-                       ks, vs, kd, vd, n, n_dev, shift, dmask, hist, dtot, nblocks);
+#define DR_SORT_PASS(R)                                                                      \
+  do {                                                                                       \
+    hipLaunchKernelGGL((sort_hist_kernel<K, R>), dim3((unsigned)nblocks), dim3(kSortThreads), \
+                       0, st, ks, n, n_dev, shift, dmask, hist, nblocks);                    \
+    hipLaunchKernelGGL(sort_rowscan_kernel, dim3(256), dim3(kSortThreads), 0, st, hist,      \
+                       nblocks, dtot);                                                       \
+    hipLaunchKernelGGL((sort_scatter_kernel<K, R>), dim3((unsigned)nblocks),                 \
+                       dim3(kSortThreads), 0, st, ks, vs, kd, vd, n, n_dev, shift, dmask, hist, \
+                       dtot, nblocks);                                                       \
+  } while (0)
+    if (rounds == 16)
+      DR_SORT_PASS(16);
+    else if (rounds == 4)
+      DR_SORT_PASS(4);
+    else
+      DR_SORT_PASS(8);
+#undef DR_SORT_PASS
     DR_LAUNCH_CHECK();
     ks = kd;
     vs = vd;
