@@ -1,0 +1,328 @@
+// mlp.hip -- bf16 MFMA GEMMs of the dense towers that sit on the embedding
+// path's output: the DLRM top / bottom MLPs (modelzoo/DLRM/train.py:183-221,
+// the reference's --bf16 switch) -- north_star: "MFMA used only for the
+// dense CrossNet / top-MLP contraction".
+//
+//   C = act(A B^T + bias),  A [M, K], B [N, K] bf16 row-major (lda, ldb),
+//   fp32 accumulate (v_mfma_f32_16x16x32_bf16), C bf16 or fp32.
+//
+// One "NT" form serves a Linear layer's three GEMMs: forward y = x W^T (A =
+// x, B = W), input gradient dx = g W (A = g, B = W^T, a tiny transpose), and
+// weight gradient dW = g^T x (A = g^T, B = x^T: both operands transposed by
+// dr_transpose_bf16, then a GEMM whose K is the batch).  That last GEMM has
+// an output of only N_out x K_in (512 x 512) over K = 65 536: a library GEMM
+// runs it on a few dozen workgroups (DESIGN §6 "Huge-K weight gradients"),
+// here it is split over K (grid.y = split) into fp32 partials that a second
+// kernel sums in split order -- deterministic.
+//
+// Tile: 128 x 128 per block, 4 waves as 2 x 2 of 64 x 64 (4 x 4 MFMA 16x16
+// tiles each), K step 64; operands staged global -> LDS by
+// global_load_lds_dwordx4 into two LDS buffers (the DMA of K tile k+1 in
+// flight while tile k is multiplied), XOR-swizzled image (conflict-free
+// fragment reads), one counted vmcnt + one barrier per K step; blocks remapped
+// so each XCD owns a contiguous range of tiles; 2 blocks per CU.  Epilogue
+// through LDS: 8 columns per lane, bias + ReLU, 16-B (bf16) / 32-B (fp32)
+// stores.
+#include "dr_common.h"
+
+namespace dr {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) short mbf16x8;
+typedef __attribute__((ext_vector_type(4))) float mf32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int mu32x4;
+
+constexpr int GM_BM = 128, GM_BN = 128, GM_BK = 64;
+constexpr int GM_TILE = GM_BM * GM_BK * 2;  // 16 KB per operand per buffer
+
+// 128 rows x 64 bf16 of X starting at (row0, k0): 4 wave instructions of 8
+// rows x 128 B per wave; chunk c of row r lands at c ^ ((r >> 1) & 7).
+__device__ __forceinline__ void gm_stage(const uint16_t* __restrict__ X, int64_t rows_valid,
+                                         int64_t row0, int64_t ld, int64_t k0, char* tile,
+                                         int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r0 = (wave * 4 + i) * 8;
+    const int r = r0 + (lane >> 3);
+    const int lc = (lane & 7) ^ ((r >> 1) & 7);
+    int64_t gr = row0 + r;
+    if (gr >= rows_valid) gr = rows_valid - 1;  // rows past the end feed discarded outputs
+    const uint16_t* src = X + gr * ld + k0 + lc * 8;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(tile + r0 * 128),
+                                     16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ mbf16x8 gm_frag(const char* tile, int r, int lc) {
+  return *reinterpret_cast<const mbf16x8*>(tile + r * 128 + ((lc ^ ((r >> 1) & 7)) << 4));
+}
+
+__device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
+  return (uint32_t)bf16_rne(a) | ((uint32_t)bf16_rne(b) << 16);
+}
+
+// EPI 0: fp32 partial of split z at C + z * M * ldc; 1: bf16 act(acc + bias);
+// 2: fp32 act(acc + bias).
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
+    const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
+    int64_t M, int64_t N, int64_t K, int64_t kchunk, const float* __restrict__ bias, int act,
+    void* __restrict__ C, int64_t ldc) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * 2 * GM_TILE];  // [buf][A|B], 64 KB
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t nwg = (int64_t)gridDim.x;
+  const int64_t orig = blockIdx.x;
+  const int64_t xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t tile = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int64_t ntn = (N + GM_BN - 1) / GM_BN;
+  const int64_t m0 = (tile / ntn) * GM_BM;
+  const int64_t n0 = (tile % ntn) * GM_BN;
+  const int64_t kb = (int64_t)blockIdx.y * kchunk;
+  const int64_t ke = kb + kchunk < K ? kb + kchunk : K;
+  const int nk = ke > kb ? (int)((ke - kb) / GM_BK) : 0;
+  mf32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = mf32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  if (nk > 0) {
+    gm_stage(A, M, m0, lda, kb, lds, wave, lane);
+    gm_stage(B, N, n0, ldb, kb, lds + GM_TILE, wave, lane);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = lds + (kt & 1) * 2 * GM_TILE;
+    if (kt + 1 < nk) {
+      char* nxt = lds + ((kt + 1) & 1) * 2 * GM_TILE;
+      gm_stage(A, M, m0, lda, kb + (int64_t)(kt + 1) * GM_BK, nxt, wave, lane);
+      gm_stage(B, N, n0, ldb, kb + (int64_t)(kt + 1) * GM_BK, nxt + GM_TILE, wave, lane);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's tile-kt DMAs landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // ... and every other wave's
+    asm volatile("" ::: "memory");
+    const char* sA = cur;
+    const char* sB = cur + GM_TILE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      mbf16x8 fa[4], fb[4];
+      const int lc = kk * 4 + fq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = gm_frag(sA, wm * 64 + i * 16 + fr, lc);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = gm_frag(sB, wn * 64 + j * 16 + fr, lc);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // buffer kt&1 is restaged by iteration kt+1's DMA
+    asm volatile("" ::: "memory");
+  }
+  __syncthreads();
+  // accumulators -> this wave's 16 KB LDS region (C/D map: col = lane & 15,
+  // row = (lane >> 4) * 4 + reg; columns XOR-swizzled by (row >> 2) & 3)
+  float* ct = reinterpret_cast<float*>(lds) + wave * 64 * 64;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i * 16 + fq * 4 + r;
+        const int col = (j * 16 + fr) ^ (((row >> 2) & 3) << 4);
+        ct[row * 64 + col] = acc[i][j][r];
+      }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int idx = it * 64 + lane;
+    const int row = idx >> 3, cc = (idx & 7) * 8;
+    const int64_t grow = m0 + wm * 64 + row;
+    const int64_t gcol = n0 + wn * 64 + cc;
+    if (grow >= M || gcol >= N) continue;
+    const int pc = cc ^ (((row >> 2) & 3) << 4);
+    const float4 l0 = *reinterpret_cast<const float4*>(ct + row * 64 + pc);
+    const float4 l1 = *reinterpret_cast<const float4*>(ct + row * 64 + pc + 4);
+    float v[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+    if (EPI == 0) {
+      float* dst = reinterpret_cast<float*>(C) + (int64_t)blockIdx.y * M * ldc + grow * ldc + gcol;
+      reinterpret_cast<float4*>(dst)[0] = make_float4(v[0], v[1], v[2], v[3]);
+      reinterpret_cast<float4*>(dst)[1] = make_float4(v[4], v[5], v[6], v[7]);
+      continue;
+    }
+    if (bias) {
+      const float4 b0 = *reinterpret_cast<const float4*>(bias + gcol);
+      const float4 b1 = *reinterpret_cast<const float4*>(bias + gcol + 4);
+      v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+      v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+    }
+    if (act == DR_ACT_RELU) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+    }
+    if (EPI == 1) {
+      mu32x4 o = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]), pack_bf16(v[4], v[5]),
+                  pack_bf16(v[6], v[7])};
+      *reinterpret_cast<mu32x4*>(reinterpret_cast<uint16_t*>(C) + grow * ldc + gcol) = o;
+    } else {
+      float* dst = reinterpret_cast<float*>(C) + grow * ldc + gcol;
+      reinterpret_cast<float4*>(dst)[0] = make_float4(v[0], v[1], v[2], v[3]);
+      reinterpret_cast<float4*>(dst)[1] = make_float4(v[4], v[5], v[6], v[7]);
+    }
+  }
+}
+
+// Split-K reduction in split order: C = act(sum_z ws[z] + bias), 4 columns
+// per thread.
+__global__ void gemm_splitk_reduce_kernel(const float* __restrict__ ws, int S, int64_t M,
+                                          int64_t N, const float* __restrict__ bias, int act,
+                                          void* __restrict__ C, int64_t ldc, int out_bf16) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nq = N / 4;
+  if (q >= M * nq) return;
+  const int64_t m = q / nq, n = (q - m * nq) * 4;
+  float4 s = reinterpret_cast<const float4*>(ws + m * N + n)[0];
+  for (int z = 1; z < S; ++z) {
+    const float4 p = reinterpret_cast<const float4*>(ws + (int64_t)z * M * N + m * N + n)[0];
+    s.x += p.x;
+    s.y += p.y;
+    s.z += p.z;
+    s.w += p.w;
+  }
+  if (bias) {
+    s.x += bias[n];
+    s.y += bias[n + 1];
+    s.z += bias[n + 2];
+    s.w += bias[n + 3];
+  }
+  if (act == DR_ACT_RELU) {
+    s.x = s.x > 0.f ? s.x : 0.f;
+    s.y = s.y > 0.f ? s.y : 0.f;
+    s.z = s.z > 0.f ? s.z : 0.f;
+    s.w = s.w > 0.f ? s.w : 0.f;
+  }
+  if (out_bf16) {
+    uint2 o = {pack_bf16(s.x, s.y), pack_bf16(s.z, s.w)};
+    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(C) + m * ldc + n) = o;
+  } else {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + m * ldc + n) = s;
+  }
+}
+
+// out[c][r] = in[r][c] (bf16), 64 x 64 tiles through LDS: each thread loads
+// two 16-B row vectors and stores two 16-B column vectors.
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const uint16_t* __restrict__ in,
+                                                             int64_t rows, int64_t cols,
+                                                             int64_t ld_in,
+                                                             uint16_t* __restrict__ out,
+                                                             int64_t ld_out) {
+  __shared__ uint16_t t[64][66];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int v = tid + h * 256;  // 512 vectors of 8: row v / 8, column chunk v % 8
+    const int r = v >> 3, cc = (v & 7) * 8;
+    mu32x4 x = {0u, 0u, 0u, 0u};
+    if (r0 + r < rows && c0 + cc < cols)
+      x = *reinterpret_cast<const mu32x4*>(in + (r0 + r) * ld_in + c0 + cc);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      t[r][cc + 2 * e] = (uint16_t)(x[e] & 0xffff);
+      t[r][cc + 2 * e + 1] = (uint16_t)(x[e] >> 16);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int v = tid + h * 256;  // output row c = v / 8 (an input column), rows chunk v % 8
+    const int c = v >> 3, rc = (v & 7) * 8;
+    if (c0 + c >= cols || r0 + rc >= rows) continue;
+    mu32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      o[e] = (uint32_t)t[rc + 2 * e][c] | ((uint32_t)t[rc + 2 * e + 1][c] << 16);
+    *reinterpret_cast<mu32x4*>(out + (c0 + c) * ld_out + r0 + rc) = o;
+  }
+}
+
+}  // namespace
+}  // namespace dr
+
+extern "C" {
+
+size_t dr_gemm_nt_workspace_size(int64_t M, int64_t N, int split_k) {
+  if (split_k <= 1) return 0;
+  return (size_t)split_k * (size_t)(M > 0 ? M : 1) * (size_t)(N > 0 ? N : 1) * sizeof(float) + 256;
+}
+
+int dr_gemm_nt_bf16(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int64_t M,
+                    int64_t N, int64_t K, const float* bias, int act, void* C, int64_t ldc,
+                    int c_fp32, int split_k, void* ws, size_t ws_bytes, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(A && B && C && M >= 0 && N >= 0 && K >= 0, DR_INVALID_ARGUMENT, "bad argument");
+  DR_REQUIRE(K % 64 == 0 && N % 8 == 0, DR_INVALID_ARGUMENT,
+             "dr_gemm_nt_bf16: K must be a multiple of 64 and N of 8 (pad with zeros)");
+  DR_REQUIRE(lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0 && lda >= K && ldb >= K && ldc >= N,
+             DR_INVALID_ARGUMENT, "dr_gemm_nt_bf16: strides must be multiples of 8 and >= K / N");
+  DR_REQUIRE((((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) == 0 &&
+                 (!bias || ((uintptr_t)bias & 15) == 0),
+             DR_INVALID_ARGUMENT, "dr_gemm_nt_bf16: pointers must be 16-B aligned");
+  DR_REQUIRE(act == DR_ACT_NONE || act == DR_ACT_RELU, DR_INVALID_ARGUMENT, "unknown act %d", act);
+  if (M == 0 || N == 0) return DR_OK;
+  hipStream_t st = S(stream);
+  const int64_t tiles = ((M + GM_BM - 1) / GM_BM) * ((N + GM_BN - 1) / GM_BN);
+  DR_REQUIRE(tiles < (1ll << 31), DR_INVALID_ARGUMENT, "dr_gemm_nt_bf16: too many tiles");
+  const int64_t ksteps = K / GM_BK;
+  int S_ = split_k < 1 ? 1 : split_k;
+  if (S_ > ksteps && ksteps > 0) S_ = (int)ksteps;
+  const int64_t kchunk = (ksteps > 0 ? (ksteps + S_ - 1) / S_ : 1) * GM_BK;
+  if (S_ == 1) {
+    if (c_fp32)
+      hipLaunchKernelGGL(gemm_nt_kernel<2>, dim3((unsigned)tiles, 1), dim3(256), 0, st, A, lda, B,
+                         ldb, M, N, K, kchunk, bias, act, C, ldc);
+    else
+      hipLaunchKernelGGL(gemm_nt_kernel<1>, dim3((unsigned)tiles, 1), dim3(256), 0, st, A, lda, B,
+                         ldb, M, N, K, kchunk, bias, act, C, ldc);
+    DR_LAUNCH_CHECK();
+    return DR_OK;
+  }
+  DR_REQUIRE(ws && ws_bytes >= dr_gemm_nt_workspace_size(M, N, S_), DR_INVALID_ARGUMENT,
+             "dr_gemm_nt_bf16: split-K workspace too small");
+  DR_REQUIRE(((uintptr_t)ws & 15) == 0, DR_INVALID_ARGUMENT, "workspace must be 16-B aligned");
+  hipLaunchKernelGGL(gemm_nt_kernel<0>, dim3((unsigned)tiles, (unsigned)S_), dim3(256), 0, st, A,
+                     lda, B, ldb, M, N, K, kchunk, (const float*)nullptr, 0, ws, N);
+  const int64_t quads = M * (N / 4);
+  hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)ceil_div(quads, 256)), dim3(256),
+                     0, st, (const float*)ws, S_, M, N, bias, act, C, ldc, c_fp32 ? 0 : 1);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_transpose_bf16(const uint16_t* in, int64_t rows, int64_t cols, int64_t ld_in,
+                      uint16_t* out, int64_t ld_out, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(in && out && rows >= 0 && cols >= 0, DR_INVALID_ARGUMENT, "bad argument");
+  DR_REQUIRE(rows % 8 == 0 && cols % 8 == 0 && ld_in % 8 == 0 && ld_out % 8 == 0 &&
+                 ld_in >= cols && ld_out >= rows,
+             DR_INVALID_ARGUMENT, "dr_transpose_bf16: rows, cols and strides multiples of 8");
+  DR_REQUIRE(((((uintptr_t)in) | ((uintptr_t)out)) & 15) == 0, DR_INVALID_ARGUMENT,
+             "dr_transpose_bf16: pointers must be 16-B aligned");
+  if (rows == 0 || cols == 0) return DR_OK;
+  const dim3 grid((unsigned)ceil_div(cols, 64), (unsigned)ceil_div(rows, 64));
+  hipLaunchKernelGGL(transpose_bf16_kernel, grid, dim3(256), 0, S(stream), in, rows, cols, ld_in,
+                     out, ld_out);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+}  // extern "C"

@@ -92,16 +92,83 @@ class _OneHotLookup(object):
         return embedding_stack(x0, self.evs, self._sps(ids), combiner="sum")
 
 
+class _MfmaLinearFn(torch.autograd.Function):
+    """y = act(x W^T + b) on the hand MFMA GEMM (dr_gemm_nt_bf16), bf16
+    operands, fp32 accumulate, bf16 out.  x [B, Kp] bf16 with zero pad
+    columns (Kp % 64 == 0), weight [N, K] fp32 master (the reference's
+    keep_weights), bias [N] fp32.  Backward: g masked by ReLU, dx = g W
+    (one NT GEMM on W^T), dW = g^T x (both operands transposed, then a
+    split-K NT GEMM over the batch: its output is only N x Kp), db = sum g."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu):
+        N, K = weight.shape
+        Kp = x.shape[1]
+        wb = torch.nn.functional.pad(weight.detach(), (0, Kp - K)).to(torch.bfloat16)
+        y = ops.gemm_nt(x, wb, bias.detach(), ops.ACT_RELU if relu else ops.ACT_NONE)
+        ctx.save_for_backward(x, wb, y)
+        ctx.relu, ctx.K = relu, K
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, wb, y = ctx.saved_tensors
+        g = g.to(torch.bfloat16)
+        if ctx.relu:
+            g = g * (y > 0)
+        g = g.contiguous()
+        B, N = g.shape
+        Kp = x.shape[1]
+        dx = ops.gemm_nt(g, wb.t().contiguous())                     # [B, Kp]
+        tiles = ((N + 127) // 128) * ((Kp + 127) // 128)
+        split = max(1, min(64, 512 // tiles, B // (64 * 8)))
+        dW = ops.gemm_nt(ops.transpose_bf16(g), ops.transpose_bf16(x), out_fp32=True,
+                         split_k=split)                              # [N, Kp] fp32
+        db = g.float().sum(0)
+        return dx, dW[:, :ctx.K], db, None
+
+
+class _MfmaMLP(torch.nn.Module):
+    """The bf16 MLP of the reference's --bf16 switch (fp32 master weights,
+    bf16 compute, modelzoo/DLRM/train.py:183-221) on the hand MFMA GEMMs:
+    the same Linear / ReLU stack as _mlp(sizes); the input is zero-padded to
+    a multiple of 64 features.  A layer whose output width is not a multiple
+    of 64 (the contraction of its input gradient), or a batch not a multiple
+    of 512, runs through torch autocast instead."""
+
+    def __init__(self, sizes, last_act=True):
+        super().__init__()
+        self.net = _mlp(sizes, last_act)
+        self.sizes = list(sizes)
+        self.last_act = last_act
+
+    def forward(self, x):
+        lins = [m for m in self.net if isinstance(m, torch.nn.Linear)]
+        B, K = x.shape
+        if B % 512 or any(l.out_features % 64 for l in lins):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                return self.net(x).float()
+        Kp = (K + 63) // 64 * 64
+        h = torch.nn.functional.pad(x.to(torch.bfloat16), (0, Kp - K))
+        for i, lin in enumerate(lins):
+            relu = self.last_act or i < len(lins) - 1
+            h = _MfmaLinearFn.apply(h, lin.weight, lin.bias, relu)
+        return h.float()
+
+
 class _MaybeBF16(object):
     """The reference's bf16 switch: MLPs run in bf16 on fp32 master weights
     (variable_scope(...).keep_weights(), DLRM train.py:183-195), outputs
-    cast back to fp32."""
+    cast back to fp32.  _MfmaMLP towers run on the hand MFMA GEMMs; other
+    modules under torch autocast."""
 
     def __init__(self, on):
         self.on = on
 
     def __call__(self, mlp, x):
         if not self.on:
+            return mlp(x)
+        if isinstance(mlp, _MfmaMLP):
             return mlp(x)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             return mlp(x).float()
@@ -118,9 +185,11 @@ class DLRM(torch.nn.Module):
         self.T = len(self.evs)
         # the bottom MLP ends at the embedding dim so it stacks with the
         # embeddings (the reference: mlp_bot [512, 256, 64, 16] with dim 16)
-        self.bottom = _mlp([num_dense] + list(mlp_bot) + [self.dim])
+        # bf16: the towers run on the hand MFMA GEMMs (dr_gemm_nt_bf16)
+        mlp = _MfmaMLP if bf16 else _mlp
+        self.bottom = mlp([num_dense] + list(mlp_bot) + [self.dim])
         F = self.T + 1
-        self.top = _mlp([self.dim + F * (F - 1) // 2] + list(mlp_top))
+        self.top = mlp([self.dim + F * (F - 1) // 2] + list(mlp_top))
         self.last = torch.nn.Linear(mlp_top[-1], 1)
         self.lookup = _OneHotLookup(self.evs)
 

@@ -572,6 +572,45 @@ def crossnet_forward(x0, xl, weight, bias, with_lin=True):
     return out, lin
 
 
+ACT_NONE, ACT_RELU = 0, 1
+
+
+def gemm_nt(a, b, bias=None, act=ACT_NONE, out_fp32=False, split_k=1, out=None):
+    """dr_gemm_nt_bf16: act(a b^T + bias) with a [M, K], b [N, K] bf16 (row
+    strides free, unit column stride), K % 64 == 0, N % 8 == 0; fp32
+    accumulate; bf16 (or fp32) [M, N] output.  split_k > 1: K cut into
+    chunks summed in chunk order (deterministic)."""
+    dev = _dev(a)
+    M, K = a.shape
+    N = b.shape[0]
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or b.shape[1] != K \
+            or a.stride(1) != 1 or b.stride(1) != 1:
+        raise ValueError("gemm_nt needs bf16 a [M, K], b [N, K] with unit column stride")
+    odt = torch.float32 if out_fp32 else torch.bfloat16
+    if out is None:
+        out = torch.empty((M, N), dtype=odt, device=dev)
+    bb = None if bias is None else bias.to(torch.float32).contiguous()
+    wsb = lib().dr_gemm_nt_workspace_size(M, N, split_k)
+    ws = workspace(wsb, dev) if wsb else None
+    check(lib().dr_gemm_nt_bf16(ptr(a), a.stride(0), ptr(b), b.stride(0), M, N, K, ptr(bb), act,
+                                ptr(out), out.stride(0), 1 if out_fp32 else 0, split_k, ptr(ws),
+                                wsb, stream_handle(dev)))
+    _post(dev)
+    return out
+
+
+def transpose_bf16(x):
+    """dr_transpose_bf16: [R, C] bf16 (unit column stride) -> contiguous [C, R]."""
+    dev = _dev(x)
+    R, Cc = x.shape
+    if x.dtype != torch.bfloat16 or x.stride(1) != 1:
+        raise ValueError("transpose_bf16 needs a bf16 matrix with unit column stride")
+    out = torch.empty((Cc, R), dtype=torch.bfloat16, device=dev)
+    check(lib().dr_transpose_bf16(ptr(x), R, Cc, x.stride(0), ptr(out), R, stream_handle(dev)))
+    _post(dev)
+    return out
+
+
 def crossnet_backward_elem(g, x0, lin, acc=None):
     """dr_crossnet_backward_elem_bf16: the elementwise part of a cross
     layer's backward in one pass.  g, x0, lin [B, d] bf16; acc [B, d] fp32

@@ -829,6 +829,27 @@ size_t dr_crossnet_backward_workspace_size(int64_t batch, int d);
 int dr_crossnet_backward_elem_bf16(const uint16_t* g, const uint16_t* x0, const uint16_t* lin,
                                    const float* acc_in, float* acc_out, uint16_t* u, float* db,
                                    int64_t batch, int d, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Dense towers on the pooled output: bf16 MFMA GEMMs of the DLRM top /     */
+/* bottom MLPs (modelzoo/DLRM/train.py:183-221 with --bf16; north_star:     */
+/* "MFMA ... for the dense CrossNet / top-MLP contraction").                */
+/*   C[M, N] = act(A[M, K] . B[N, K]^T + bias[N])                            */
+/* A, B bf16 row-major with row strides lda, ldb (elements); fp32           */
+/* accumulate; C bf16 (c_fp32 = 0) or fp32, row stride ldc.  K % 64 == 0,    */
+/* N % 8 == 0, strides % 8 == 0, 16-B aligned pointers (pad with zeros).     */
+/* split_k > 1 cuts K into split_k chunks (fp32 partials in ws, summed in    */
+/* chunk order: deterministic) -- for the weight gradient dW = g^T x, whose  */
+/* K is the batch.  bias nullable; act DR_ACT_NONE / DR_ACT_RELU.           */
+#define DR_ACT_NONE 0
+#define DR_ACT_RELU 1
+size_t dr_gemm_nt_workspace_size(int64_t M, int64_t N, int split_k);
+int dr_gemm_nt_bf16(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int64_t M,
+                    int64_t N, int64_t K, const float* bias, int act, void* C, int64_t ldc,
+                    int c_fp32, int split_k, void* ws, size_t ws_bytes, void* stream);
+/* out[c][r] = in[r][c], bf16; rows, cols and strides multiples of 8.        */
+int dr_transpose_bf16(const uint16_t* in, int64_t rows, int64_t cols, int64_t ld_in,
+                      uint16_t* out, int64_t ld_out, void* stream);
 /* Same layer, also writing lin_out = xl W^T + b (bf16, nullable; needs      */
 /* d % 64 == 0) for the backward pass.  d % 64 == 0 selects the pipelined    */
 /* kernel (global_load_lds staging, double-buffered K steps of 64).          */

@@ -1,0 +1,144 @@
+"""GPU: the hand MFMA GEMM of the dense towers (dr_gemm_nt_bf16,
+dr_transpose_bf16) and the bf16 MLP built on it (modelzoo._MfmaMLP, the
+DLRM top / bottom MLPs under the reference's --bf16 switch,
+modelzoo/DLRM/train.py:183-221).
+
+Numerics are checked against plain torch fp32 on the same bf16 operands
+(the reference is the fp32 product of bf16 values): fp32 outputs within
+1e-4 relative (accumulation order only), bf16 outputs within the rounding
+of one bf16 ulp.  Split-K is deterministic: two runs are bit-identical."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def dr():
+    import deeprec_amd
+    deeprec_amd.load()
+    assert torch.cuda.is_available()
+    return deeprec_amd
+
+
+def _ref(a, b, bias, relu):
+    r = a.float() @ b.float().t()
+    if bias is not None:
+        r = r + bias
+    return torch.relu(r) if relu else r
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 128, 64), (300, 72, 192), (1000, 520, 512),
+                                   (4096, 512, 1024), (130, 8, 64)])
+@pytest.mark.parametrize("relu", [False, True])
+def test_gemm_nt_matches_fp32(dr, M, N, K, relu):
+    from deeprec_amd import ops
+    g = torch.Generator(device=DEV)
+    g.manual_seed(M + N + K)
+    a = torch.randn((M, K), generator=g, device=DEV).to(torch.bfloat16)
+    b = torch.randn((N, K), generator=g, device=DEV).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=DEV)
+    act = ops.ACT_RELU if relu else ops.ACT_NONE
+    ref = _ref(a, b, bias, relu)
+    c32 = ops.gemm_nt(a, b, bias, act, out_fp32=True)
+    torch.testing.assert_close(c32, ref, rtol=1e-4, atol=1e-4 * K ** 0.5)
+    c16 = ops.gemm_nt(a, b, bias, act)
+    assert c16.dtype == torch.bfloat16
+    torch.testing.assert_close(c16.float(), ref.to(torch.bfloat16).float(), rtol=8e-3,
+                               atol=1e-3 * K ** 0.5)
+
+
+def test_gemm_nt_strided_operands(dr):
+    """Row strides larger than K (a column window of a wider matrix)."""
+    from deeprec_amd import ops
+    g = torch.Generator(device=DEV)
+    g.manual_seed(3)
+    big_a = torch.randn((512, 640), generator=g, device=DEV).to(torch.bfloat16)
+    big_b = torch.randn((96, 256), generator=g, device=DEV).to(torch.bfloat16)
+    a, b = big_a[:, 64:320], big_b[:, :256]
+    out = torch.zeros((512, 104), device=DEV)
+    ops.gemm_nt(a, b, None, ops.ACT_NONE, out_fp32=True, out=out[:, :96])
+    torch.testing.assert_close(out[:, :96], _ref(a, b, None, False), rtol=1e-4, atol=2e-3)
+    assert bool((out[:, 96:] == 0).all())
+
+
+@pytest.mark.parametrize("split", [2, 7, 32])
+def test_gemm_nt_split_k_deterministic(dr, split):
+    from deeprec_amd import ops
+    g = torch.Generator(device=DEV)
+    g.manual_seed(split)
+    a = torch.randn((256, 16384), generator=g, device=DEV).to(torch.bfloat16)
+    b = torch.randn((192, 16384), generator=g, device=DEV).to(torch.bfloat16)
+    bias = torch.randn(192, generator=g, device=DEV)
+    c1 = ops.gemm_nt(a, b, bias, ops.ACT_RELU, out_fp32=True, split_k=split)
+    c2 = ops.gemm_nt(a, b, bias, ops.ACT_RELU, out_fp32=True, split_k=split)
+    assert torch.equal(c1, c2)
+    torch.testing.assert_close(c1, _ref(a, b, bias, True), rtol=1e-4, atol=2e-2)
+
+
+def test_transpose_bf16_exact(dr):
+    from deeprec_amd import ops
+    x = torch.randn((1000, 520), device=DEV).to(torch.bfloat16)
+    assert torch.equal(ops.transpose_bf16(x), x.t().contiguous())
+    y = x[:, 8:264]
+    assert torch.equal(ops.transpose_bf16(y), y.t().contiguous())
+
+
+def test_gemm_nt_refuses_bad_shapes(dr):
+    from deeprec_amd import ops
+    a = torch.zeros((64, 100), device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(dr.DeepRecError):
+        ops.gemm_nt(a, a)                     # K % 64 != 0
+
+
+@pytest.mark.parametrize("sizes,last_act", [([479, 512, 256], True), ([13, 512, 256, 128], True),
+                                            ([192, 128, 64], False)])
+def test_mfma_mlp_forward_backward(dr, sizes, last_act):
+    """_MfmaMLP (hand GEMMs) against the same Linear stack in fp32 autograd on
+    the bf16-rounded operands: outputs and every gradient within bf16
+    tolerances."""
+    from deeprec_amd import modelzoo as mz
+    torch.manual_seed(sum(sizes))
+    B = 1024
+    mlp = mz._MfmaMLP(sizes, last_act).to(DEV)
+    x = torch.randn((B, sizes[0]), device=DEV, requires_grad=True)
+    y = mlp(x)
+    go = torch.randn_like(y)
+    y.backward(go)
+    # fp32 reference with bf16-rounded weights / input, fp32 math
+    ref = mz._mlp(sizes, last_act).to(DEV)
+    for p, q in zip(ref.parameters(), mlp.net.parameters()):
+        with torch.no_grad():
+            p.copy_(q.to(torch.bfloat16).float() if p.dim() == 2 else q)
+    xr = x.detach().to(torch.bfloat16).float().requires_grad_(True)
+    yr = ref(xr)
+    yr.backward(go)
+    torch.testing.assert_close(y, yr, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=5e-2, atol=5e-2)
+    for p, q in zip(ref.parameters(), mlp.net.parameters()):
+        scale = p.grad.abs().max().item() + 1e-6
+        assert (p.grad - q.grad).abs().max().item() <= 3e-2 * scale
+
+
+def test_dlrm_bf16_step_on_mfma_towers(dr):
+    """DLRM with bf16 towers trains on the MFMA GEMMs (no autocast Linear in
+    the towers) and its loss tracks the fp32 model on the same weights."""
+    from deeprec_amd import modelzoo as mz
+    torch.manual_seed(5)
+    T, D, B = 4, 64, 1024
+    evs = [dr.EmbeddingVariable("mlp_dlrm_%d" % t, D, 0.01, device=DEV) for t in range(T)]
+    model = mz.DLRM(evs, 13, (64,), (128, 64), bf16=True).to(DEV)
+    assert isinstance(model.top, mz._MfmaMLP) and isinstance(model.bottom, mz._MfmaMLP)
+    dense = torch.rand((B, 13), device=DEV)
+    ids = torch.randint(0, 1000, (T, B), device=DEV)
+    labels = (torch.rand(B, device=DEV) > 0.5).float()
+    out = model(dense, ids)
+    loss = torch.nn.functional.binary_cross_entropy(out, labels)
+    loss.backward()
+    assert torch.isfinite(loss)
+    for p in model.parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all()
+    for ev in evs:
+        ev.pending_grads.clear()
