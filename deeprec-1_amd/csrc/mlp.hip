@@ -63,12 +63,14 @@ __device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
 }
 
 // EPI 0: fp32 partial of split z at C + z * M * ldc; 1: bf16 act(acc + bias);
-// 2: fp32 act(acc + bias).
+// 2: fp32 act(acc + bias).  act DR_ACT_MASK: the result is zeroed where the
+// bf16 aux [M, N] (ld_aux) is not > 0 -- the ReLU mask of the layer below
+// applied to its input gradient (dx of the layer above) in the same pass.
 template <int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
     const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
     int64_t M, int64_t N, int64_t K, int64_t kchunk, const float* __restrict__ bias, int act,
-    void* __restrict__ C, int64_t ldc) {
+    void* __restrict__ C, int64_t ldc, const uint16_t* __restrict__ aux, int64_t ld_aux) {
   __shared__ __attribute__((aligned(1024))) char lds[2 * 2 * GM_TILE];  // [buf][A|B], 64 KB
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -168,6 +170,15 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
     if (act == DR_ACT_RELU) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+    } else if (act == DR_ACT_MASK) {
+      const mu32x4 m = *reinterpret_cast<const mu32x4*>(aux + grow * ld_aux + gcol);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        // bf16 > 0: sign bit clear and not +0 (the bits of a positive value)
+        const uint32_t lo = m[e] & 0xffffu, hi = m[e] >> 16;
+        if (!(lo != 0u && lo < 0x8000u && lo <= 0x7f80u)) v[2 * e] = 0.f;
+        if (!(hi != 0u && hi < 0x8000u && hi <= 0x7f80u)) v[2 * e + 1] = 0.f;
+      }
     }
     if (EPI == 1) {
       mu32x4 o = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]), pack_bf16(v[4], v[5]),
@@ -265,9 +276,10 @@ size_t dr_gemm_nt_workspace_size(int64_t M, int64_t N, int split_k) {
   return (size_t)split_k * (size_t)(M > 0 ? M : 1) * (size_t)(N > 0 ? N : 1) * sizeof(float) + 256;
 }
 
-int dr_gemm_nt_bf16(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int64_t M,
-                    int64_t N, int64_t K, const float* bias, int act, void* C, int64_t ldc,
-                    int c_fp32, int split_k, void* ws, size_t ws_bytes, void* stream) {
+int dr_gemm_nt_bf16_ex(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int64_t M,
+                       int64_t N, int64_t K, const float* bias, int act, const uint16_t* aux,
+                       int64_t ld_aux, void* C, int64_t ldc, int c_fp32, int split_k, void* ws,
+                       size_t ws_bytes, void* stream) {
   using namespace dr;
   DR_REQUIRE(A && B && C && M >= 0 && N >= 0 && K >= 0, DR_INVALID_ARGUMENT, "bad argument");
   DR_REQUIRE(K % 64 == 0 && N % 8 == 0, DR_INVALID_ARGUMENT,
@@ -277,7 +289,11 @@ int dr_gemm_nt_bf16(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t l
   DR_REQUIRE((((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) == 0 &&
                  (!bias || ((uintptr_t)bias & 15) == 0),
              DR_INVALID_ARGUMENT, "dr_gemm_nt_bf16: pointers must be 16-B aligned");
-  DR_REQUIRE(act == DR_ACT_NONE || act == DR_ACT_RELU, DR_INVALID_ARGUMENT, "unknown act %d", act);
+  DR_REQUIRE(act == DR_ACT_NONE || act == DR_ACT_RELU || act == DR_ACT_MASK, DR_INVALID_ARGUMENT,
+             "unknown act %d", act);
+  DR_REQUIRE(act != DR_ACT_MASK || (aux && ld_aux >= N && ld_aux % 8 == 0 &&
+                                    ((uintptr_t)aux & 15) == 0),
+             DR_INVALID_ARGUMENT, "DR_ACT_MASK needs a 16-B aligned aux with ld_aux >= N, %% 8");
   if (M == 0 || N == 0) return DR_OK;
   hipStream_t st = S(stream);
   const int64_t tiles = ((M + GM_BM - 1) / GM_BM) * ((N + GM_BN - 1) / GM_BN);
@@ -289,23 +305,32 @@ int dr_gemm_nt_bf16(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t l
   if (S_ == 1) {
     if (c_fp32)
       hipLaunchKernelGGL(gemm_nt_kernel<2>, dim3((unsigned)tiles, 1), dim3(256), 0, st, A, lda, B,
-                         ldb, M, N, K, kchunk, bias, act, C, ldc);
+                         ldb, M, N, K, kchunk, bias, act, C, ldc, aux, ld_aux);
     else
       hipLaunchKernelGGL(gemm_nt_kernel<1>, dim3((unsigned)tiles, 1), dim3(256), 0, st, A, lda, B,
-                         ldb, M, N, K, kchunk, bias, act, C, ldc);
+                         ldb, M, N, K, kchunk, bias, act, C, ldc, aux, ld_aux);
     DR_LAUNCH_CHECK();
     return DR_OK;
   }
+  DR_REQUIRE(act != DR_ACT_MASK, DR_INVALID_ARGUMENT, "DR_ACT_MASK is not built for split-K");
   DR_REQUIRE(ws && ws_bytes >= dr_gemm_nt_workspace_size(M, N, S_), DR_INVALID_ARGUMENT,
              "dr_gemm_nt_bf16: split-K workspace too small");
   DR_REQUIRE(((uintptr_t)ws & 15) == 0, DR_INVALID_ARGUMENT, "workspace must be 16-B aligned");
   hipLaunchKernelGGL(gemm_nt_kernel<0>, dim3((unsigned)tiles, (unsigned)S_), dim3(256), 0, st, A,
-                     lda, B, ldb, M, N, K, kchunk, (const float*)nullptr, 0, ws, N);
+                     lda, B, ldb, M, N, K, kchunk, (const float*)nullptr, 0, ws, N,
+                     (const uint16_t*)nullptr, (int64_t)0);
   const int64_t quads = M * (N / 4);
   hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)ceil_div(quads, 256)), dim3(256),
                      0, st, (const float*)ws, S_, M, N, bias, act, C, ldc, c_fp32 ? 0 : 1);
   DR_LAUNCH_CHECK();
   return DR_OK;
+}
+
+int dr_gemm_nt_bf16(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int64_t M,
+                    int64_t N, int64_t K, const float* bias, int act, void* C, int64_t ldc,
+                    int c_fp32, int split_k, void* ws, size_t ws_bytes, void* stream) {
+  return dr_gemm_nt_bf16_ex(A, lda, B, ldb, M, N, K, bias, act, nullptr, 0, C, ldc, c_fp32,
+                            split_k, ws, ws_bytes, stream);
 }
 
 int dr_transpose_bf16(const uint16_t* in, int64_t rows, int64_t cols, int64_t ld_in,

@@ -228,6 +228,8 @@ SIGNATURES = {
     "dr_gemm_nt_workspace_size": (_SZ, [_I64, _I64, _I32]),
     "dr_gemm_nt_bf16": (_I32, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I32, _P, _I64, _I32,
                                _I32, _P, _SZ, _P]),
+    "dr_gemm_nt_bf16_ex": (_I32, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I32, _P, _I64, _P,
+                                  _I64, _I32, _I32, _P, _SZ, _P]),
     "dr_transpose_bf16": (_I32, [_P, _I64, _I64, _I64, _P, _I64, _P]),
     "dr_crossnet_backward_elem_bf16": (_I32, [_P, _P, _P, _P, _P, _P, _P, _I64, _I32, _P, _SZ,
                                               _P]),

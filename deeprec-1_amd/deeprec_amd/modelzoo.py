@@ -92,49 +92,69 @@ class _OneHotLookup(object):
         return embedding_stack(x0, self.evs, self._sps(ids), combiner="sum")
 
 
-class _MfmaLinearFn(torch.autograd.Function):
-    """y = act(x W^T + b) on the hand MFMA GEMM (dr_gemm_nt_bf16), bf16
-    operands, fp32 accumulate, bf16 out.  x [B, Kp] bf16 with zero pad
-    columns (Kp % 64 == 0), weight [N, K] fp32 master (the reference's
-    keep_weights), bias [N] fp32.  Backward: g masked by ReLU, dx = g W
-    (one NT GEMM on W^T), dW = g^T x (both operands transposed, then a
-    split-K NT GEMM over the batch: its output is only N x Kp), db = sum g."""
+class _MfmaTowerFn(torch.autograd.Function):
+    """A bf16 ReLU MLP tower as ONE autograd node on the hand MFMA GEMM
+    (dr_gemm_nt_bf16[_ex]): layer l computes y_l = act(h_l W_l^T + b_l),
+    bf16 operands, fp32 accumulate, bf16 out, h_0 = the zero-padded input
+    (Kp % 64 == 0), fp32 master weights (the reference's keep_weights).
+    Backward, layer by layer from the top: db_l = sum of g_l (fp32), dW_l =
+    g_l^T h_l (both operands transposed, then a split-K GEMM over the batch:
+    its output is only N_l x K_l), and the input gradient g_{l-1} = g_l W_l
+    with the layer below's ReLU mask applied in the GEMM's epilogue (aux =
+    y_{l-1} = h_l) -- no separate mask / multiply passes."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, relu):
-        N, K = weight.shape
-        Kp = x.shape[1]
-        wb = torch.nn.functional.pad(weight.detach(), (0, Kp - K)).to(torch.bfloat16)
-        y = ops.gemm_nt(x, wb, bias.detach(), ops.ACT_RELU if relu else ops.ACT_NONE)
-        ctx.save_for_backward(x, wb, y)
-        ctx.relu, ctx.K = relu, K
-        return y
+    def forward(ctx, h0, last_act, *params):
+        L = len(params) // 2
+        ws, bs = params[:L], params[L:]
+        hs, wbs = [h0], []
+        h = h0
+        for l in range(L):
+            relu = last_act or l < L - 1
+            wb = torch.nn.functional.pad(ws[l].detach(), (0, h.shape[1] - ws[l].shape[1]))
+            wb = wb.to(torch.bfloat16)
+            h = ops.gemm_nt(h, wb, bs[l].detach(), ops.ACT_RELU if relu else ops.ACT_NONE)
+            hs.append(h)
+            wbs.append(wb)
+        ctx.save_for_backward(*hs, *wbs)
+        ctx.L, ctx.last_act = L, last_act
+        ctx.ks = [w.shape[1] for w in ws]
+        return h
 
     @staticmethod
-    def backward(ctx, g):
-        x, wb, y = ctx.saved_tensors
-        g = g.to(torch.bfloat16)
-        if ctx.relu:
-            g = g * (y > 0)
+    def backward(ctx, go):
+        L = ctx.L
+        saved = ctx.saved_tensors
+        hs, wbs = saved[:L + 1], saved[L + 1:]
+        g = go.to(torch.bfloat16)
+        if ctx.last_act:
+            g = g * (hs[L] > 0)
         g = g.contiguous()
-        B, N = g.shape
-        Kp = x.shape[1]
-        dx = ops.gemm_nt(g, wb.t().contiguous())                     # [B, Kp]
-        tiles = ((N + 127) // 128) * ((Kp + 127) // 128)
-        split = max(1, min(64, 512 // tiles, B // (64 * 8)))
-        dW = ops.gemm_nt(ops.transpose_bf16(g), ops.transpose_bf16(x), out_fp32=True,
-                         split_k=split)                              # [N, Kp] fp32
-        db = g.float().sum(0)
-        return dx, dW[:, :ctx.K], db, None
+        B = g.shape[0]
+        dws, dbs = [None] * L, [None] * L
+        for l in reversed(range(L)):
+            x = hs[l]
+            N, Kp = g.shape[1], x.shape[1]
+            dbs[l] = g.sum(0, dtype=torch.float32)
+            tiles = ((N + 127) // 128) * ((Kp + 127) // 128)
+            split = max(1, min(64, 512 // tiles, B // (64 * 8)))
+            dw = ops.gemm_nt(ops.transpose_bf16(g), ops.transpose_bf16(x), out_fp32=True,
+                             split_k=split)                          # [N, Kp] fp32
+            dws[l] = dw[:, :ctx.ks[l]]
+            if l > 0 or ctx.needs_input_grad[0]:
+                # gradient of h_l; below the top layer h_l = y_{l-1} = ReLU output
+                g = ops.gemm_nt(g, wbs[l].t().contiguous(), mask=x if l > 0 else None)
+        return (g if ctx.needs_input_grad[0] else None, None, *dws, *dbs)
 
 
 class _MfmaMLP(torch.nn.Module):
     """The bf16 MLP of the reference's --bf16 switch (fp32 master weights,
     bf16 compute, modelzoo/DLRM/train.py:183-221) on the hand MFMA GEMMs:
-    the same Linear / ReLU stack as _mlp(sizes); the input is zero-padded to
-    a multiple of 64 features.  A layer whose output width is not a multiple
-    of 64 (the contraction of its input gradient), or a batch not a multiple
-    of 512, runs through torch autocast instead."""
+    the same Linear / ReLU stack as _mlp(sizes), run as one _MfmaTowerFn;
+    the input is zero-padded to a multiple of 64 features.  A tower with an
+    output width not a multiple of 64 (the contraction of its input
+    gradient), or a batch not a multiple of 512, runs through torch autocast
+    instead."""
 
     def __init__(self, sizes, last_act=True):
         super().__init__()
@@ -150,10 +170,9 @@ class _MfmaMLP(torch.nn.Module):
                 return self.net(x).float()
         Kp = (K + 63) // 64 * 64
         h = torch.nn.functional.pad(x.to(torch.bfloat16), (0, Kp - K))
-        for i, lin in enumerate(lins):
-            relu = self.last_act or i < len(lins) - 1
-            h = _MfmaLinearFn.apply(h, lin.weight, lin.bias, relu)
-        return h.float()
+        y = _MfmaTowerFn.apply(h, self.last_act, *[l.weight for l in lins],
+                               *[l.bias for l in lins])
+        return y.float()
 
 
 class _MaybeBF16(object):

@@ -572,14 +572,15 @@ def crossnet_forward(x0, xl, weight, bias, with_lin=True):
     return out, lin
 
 
-ACT_NONE, ACT_RELU = 0, 1
+ACT_NONE, ACT_RELU, ACT_MASK = 0, 1, 2
 
 
-def gemm_nt(a, b, bias=None, act=ACT_NONE, out_fp32=False, split_k=1, out=None):
-    """dr_gemm_nt_bf16: act(a b^T + bias) with a [M, K], b [N, K] bf16 (row
-    strides free, unit column stride), K % 64 == 0, N % 8 == 0; fp32
+def gemm_nt(a, b, bias=None, act=ACT_NONE, out_fp32=False, split_k=1, out=None, mask=None):
+    """dr_gemm_nt_bf16[_ex]: act(a b^T + bias) with a [M, K], b [N, K] bf16
+    (row strides free, unit column stride), K % 64 == 0, N % 8 == 0; fp32
     accumulate; bf16 (or fp32) [M, N] output.  split_k > 1: K cut into
-    chunks summed in chunk order (deterministic)."""
+    chunks summed in chunk order (deterministic).  mask (bf16 [M, N]): the
+    result is zeroed where mask <= 0 (act ACT_MASK, a ReLU's backward)."""
     dev = _dev(a)
     M, K = a.shape
     N = b.shape[0]
@@ -592,9 +593,14 @@ def gemm_nt(a, b, bias=None, act=ACT_NONE, out_fp32=False, split_k=1, out=None):
     bb = None if bias is None else bias.to(torch.float32).contiguous()
     wsb = lib().dr_gemm_nt_workspace_size(M, N, split_k)
     ws = workspace(wsb, dev) if wsb else None
-    check(lib().dr_gemm_nt_bf16(ptr(a), a.stride(0), ptr(b), b.stride(0), M, N, K, ptr(bb), act,
-                                ptr(out), out.stride(0), 1 if out_fp32 else 0, split_k, ptr(ws),
-                                wsb, stream_handle(dev)))
+    if mask is not None:
+        if mask.dtype != torch.bfloat16 or tuple(mask.shape) != (M, N) or mask.stride(1) != 1:
+            raise ValueError("mask must be bf16 [M, N] with unit column stride")
+        act = ACT_MASK
+    check(lib().dr_gemm_nt_bf16_ex(ptr(a), a.stride(0), ptr(b), b.stride(0), M, N, K, ptr(bb), act,
+                                   ptr(mask), mask.stride(0) if mask is not None else 0, ptr(out),
+                                   out.stride(0), 1 if out_fp32 else 0, split_k, ptr(ws), wsb,
+                                   stream_handle(dev)))
     _post(dev)
     return out
 

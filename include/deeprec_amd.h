@@ -843,10 +843,18 @@ int dr_crossnet_backward_elem_bf16(const uint16_t* g, const uint16_t* x0, const 
 /* K is the batch.  bias nullable; act DR_ACT_NONE / DR_ACT_RELU.           */
 #define DR_ACT_NONE 0
 #define DR_ACT_RELU 1
+#define DR_ACT_MASK 2  /* _ex only: C = result where aux > 0, else 0 (no split) */
 size_t dr_gemm_nt_workspace_size(int64_t M, int64_t N, int split_k);
 int dr_gemm_nt_bf16(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int64_t M,
                     int64_t N, int64_t K, const float* bias, int act, void* C, int64_t ldc,
                     int c_fp32, int split_k, void* ws, size_t ws_bytes, void* stream);
+/* With an aux operand: act DR_ACT_MASK zeroes C where the bf16 aux[M, N]  */
+/* (row stride ld_aux) is not > 0 -- the ReLU mask of the layer below,      */
+/* applied to the input gradient of the layer above in the same pass.       */
+int dr_gemm_nt_bf16_ex(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int64_t M,
+                       int64_t N, int64_t K, const float* bias, int act, const uint16_t* aux,
+                       int64_t ld_aux, void* C, int64_t ldc, int c_fp32, int split_k, void* ws,
+                       size_t ws_bytes, void* stream);
 /* out[c][r] = in[r][c], bf16; rows, cols and strides multiples of 8.        */
 int dr_transpose_bf16(const uint16_t* in, int64_t rows, int64_t cols, int64_t ld_in,
                       uint16_t* out, int64_t ld_out, void* stream);

@@ -96,9 +96,11 @@ def test_gemm_nt_refuses_bad_shapes(dr):
 @pytest.mark.parametrize("sizes,last_act", [([479, 512, 256], True), ([13, 512, 256, 128], True),
                                             ([192, 128, 64], False)])
 def test_mfma_mlp_forward_backward(dr, sizes, last_act):
-    """_MfmaMLP (hand GEMMs) against the same Linear stack in fp32 autograd on
-    the bf16-rounded operands: outputs and every gradient within bf16
-    tolerances."""
+    """_MfmaMLP (hand GEMMs) against the same Linear stack under torch
+    autocast bf16 (hipBLASLt: the same bf16 rounding points -- layer outputs,
+    the ReLU-masked gradient, dx -- so the gap is accumulation order and the
+    fp32 dW here), and against fp32 autograd on the bf16-rounded operands
+    (relative Frobenius error)."""
     from deeprec_amd import modelzoo as mz
     torch.manual_seed(sum(sizes))
     B = 1024
@@ -107,7 +109,29 @@ def test_mfma_mlp_forward_backward(dr, sizes, last_act):
     y = mlp(x)
     go = torch.randn_like(y)
     y.backward(go)
-    # fp32 reference with bf16-rounded weights / input, fp32 math
+
+    def close(a, b, tol):
+        return (a - b).abs().max().item() <= tol * (b.abs().max().item() + 1e-6)
+
+    def rel_fro(a, b):
+        return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+    # torch autocast on the same weights
+    ac = mz._mlp(sizes, last_act).to(DEV)
+    ac.load_state_dict({k.split("net.", 1)[1]: v for k, v in mlp.state_dict().items()})
+    xa = x.detach().clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ya = ac(xa).float()
+    ya.backward(go)
+    # (gradients by relative Frobenius error: a pre-activation within rounding
+    # of 0 can flip its ReLU mask between the two paths -- autocast adds a
+    # bf16-rounded bias, this path the fp32 one -- which moves a few entries
+    # by a whole rank-1 term)
+    assert close(y, ya, 2e-2)
+    assert rel_fro(x.grad, xa.grad) < 2e-2
+    for p, q in zip(ac.parameters(), mlp.net.parameters()):
+        assert rel_fro(q.grad, p.grad) < 2e-2
+    # fp32 autograd on the bf16-rounded weights and input
     ref = mz._mlp(sizes, last_act).to(DEV)
     for p, q in zip(ref.parameters(), mlp.net.parameters()):
         with torch.no_grad():
@@ -115,11 +139,10 @@ def test_mfma_mlp_forward_backward(dr, sizes, last_act):
     xr = x.detach().to(torch.bfloat16).float().requires_grad_(True)
     yr = ref(xr)
     yr.backward(go)
-    torch.testing.assert_close(y, yr, rtol=3e-2, atol=3e-2)
-    torch.testing.assert_close(x.grad, xr.grad, rtol=5e-2, atol=5e-2)
+    assert rel_fro(y, yr) < 1e-2
+    assert rel_fro(x.grad, xr.grad) < 2e-2
     for p, q in zip(ref.parameters(), mlp.net.parameters()):
-        scale = p.grad.abs().max().item() + 1e-6
-        assert (p.grad - q.grad).abs().max().item() <= 3e-2 * scale
+        assert rel_fro(q.grad, p.grad) < 2e-2
 
 
 def test_dlrm_bf16_step_on_mfma_towers(dr):
