@@ -123,14 +123,6 @@ def test_mfma_mlp_forward_backward(dr, sizes, last_act):
     with torch.autocast("cuda", dtype=torch.bfloat16):
         ya = ac(xa).float()
     ya.backward(go)
-    # (gradients by relative Frobenius error: a pre-activation within rounding
-    # of 0 can flip its ReLU mask between the two paths -- autocast adds a
-    # bf16-rounded bias, this path the fp32 one -- which moves a few entries
-    # by a whole rank-1 term)
-    assert close(y, ya, 2e-2)
-    assert rel_fro(x.grad, xa.grad) < 2e-2
-    for p, q in zip(ac.parameters(), mlp.net.parameters()):
-        assert rel_fro(q.grad, p.grad) < 2e-2
     # fp32 autograd on the bf16-rounded weights and input
     ref = mz._mlp(sizes, last_act).to(DEV)
     for p, q in zip(ref.parameters(), mlp.net.parameters()):
@@ -139,10 +131,22 @@ def test_mfma_mlp_forward_backward(dr, sizes, last_act):
     xr = x.detach().to(torch.bfloat16).float().requires_grad_(True)
     yr = ref(xr)
     yr.backward(go)
+    # Forward: within bf16 rounding of both.
+    assert close(y, ya, 2e-2)
     assert rel_fro(y, yr) < 1e-2
-    assert rel_fro(x.grad, xr.grad) < 2e-2
-    for p, q in zip(ref.parameters(), mlp.net.parameters()):
-        assert rel_fro(q.grad, p.grad) < 2e-2
+    # Gradients: the bf16 rounding points (layer outputs, the masked gradient)
+    # plus ReLU mask flips of pre-activations within rounding of 0 put BOTH
+    # bf16 paths a few % (relative Frobenius) from fp32 -- ~5 % for the
+    # 13-input bottom tower, measured (profiles/r03_mlp_grad_error.log).  The
+    # bar: this path is no further from fp32 than torch autocast is (+10 %
+    # relative, + a 5e-3 floor), and both stay under 8 %.
+    pairs = [(x.grad, xa.grad, xr.grad)]
+    pairs += [(q.grad, p.grad, r.grad) for p, q, r in
+              zip(ac.parameters(), mlp.net.parameters(), ref.parameters())]
+    for ours, auto, fp32 in pairs:
+        e_ours, e_auto = rel_fro(ours, fp32), rel_fro(auto, fp32)
+        assert e_ours <= 1.1 * e_auto + 5e-3, (e_ours, e_auto)
+        assert e_ours < 8e-2, e_ours
 
 
 def test_dlrm_bf16_step_on_mfma_towers(dr):
