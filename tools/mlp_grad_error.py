@@ -1,8 +1,9 @@
 # Gradient error of the MFMA towers vs torch autocast and vs fp32 autograd on
 # the same bf16 operands (relative Frobenius, per parameter; rows that differ).
 # Output: profiles/r03_mlp_grad_error.log.
-import sys, torch
-sys.path.insert(0, __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))), "deeprec-1_amd"))
+import os, sys
+import torch
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "deeprec-1_amd"))
 import deeprec_amd as dr
 from deeprec_amd import modelzoo as mz, ops
 dr.load()
