@@ -210,6 +210,21 @@ __device__ __forceinline__ int table_of(const int64_t* koff, int T, int64_t i,
 // the next kernel may still see the previous contents in another XCD's L2.
 int fill_bytes(void* p, unsigned char value, size_t bytes, hipStream_t st);
 
+// ---- row-grouped lookup backward fused with KV SGD (grad_rows.hip; the C
+// entry dr_ev_pool_grad_rows_apply_sgd is in ev.hip, which owns the EVs) ----
+// Per table of the group: the var column's rows (fp32, or bf16 pairs when
+// bf16), and the version array to stamp with gs (steps_to_live EVs) or null.
+struct RowsSgd {
+  void* pool[DR_MAX_GROUP];
+  int64_t* version[DR_MAX_GROUP];
+  float lr;
+  int bf16;
+  int64_t gs;
+};
+int rows_apply_sgd(const dr_pool_grad_desc* descs_host, int num_tables, int64_t batch, int dim,
+                   const int64_t* rowsel, int64_t row_limit, const RowsSgd& sg, void* ws,
+                   size_t ws_bytes, hipStream_t s);
+
 // ---- scan / sort primitives (scan_sort.hip) --------------------------------
 size_t scan_ws_bytes(int64_t n);
 // Exclusive scan of int32 values into int32 out; *total (device int64) = sum.

@@ -2754,6 +2754,43 @@ int dr_ev_apply_grouped_ptr_rows(int optimizer, dr_ev* const* vars, int num_tabl
                        global_step, S(stream), 1, rows);
 }
 
+size_t dr_ev_pool_grad_rows_sgd_workspace_size(int64_t total_nnz, int dim) {
+  const int64_t n = total_nnz > 0 ? total_nnz : 1;
+  return dr_pool_grad_rows_workspace_size(total_nnz) + 256 + (size_t)n * (dim > 0 ? dim : 1) * 4;
+}
+
+int dr_ev_pool_grad_rows_apply_sgd(dr_ev* const* vars, const dr_pool_grad_desc* descs,
+                                   int num_tables, int64_t batch, int dim, const int64_t* rowsel,
+                                   float lr, int64_t global_step, void* ws, size_t ws_bytes,
+                                   void* stream) {
+  using namespace dr;
+  DR_REQUIRE(vars && descs && num_tables >= 1 && num_tables <= DR_MAX_GROUP, DR_INVALID_ARGUMENT,
+             "bad argument");
+  RowsSgd sg;
+  memset(&sg, 0, sizeof(sg));
+  sg.lr = lr;
+  sg.gs = global_step;
+  int64_t limit = 1;
+  for (int t = 0; t < num_tables; ++t) {
+    dr_ev* var = vars[t];
+    DR_REQUIRE(var && var->col == 0, DR_INVALID_ARGUMENT, "table %d: var must be a primary EV", t);
+    EvShared* s = var->sh;
+    DR_REQUIRE(s->value_words == 1 && s->dim == dim && s->bf16 == vars[0]->sh->bf16,
+               DR_INVALID_ARGUMENT, "table %d: float / bf16 EVs of one dim and value type", t);
+    DR_REQUIRE(s->filter_freq == 0 && s->k_hash == 0, DR_INVALID_ARGUMENT,
+               "table %d: the forward's rows stand for LookupOrCreate only without a filter", t);
+    for (int j = 0; j < t; ++j)
+      DR_REQUIRE(vars[j]->sh != s, DR_INVALID_ARGUMENT,
+                 "tables %d and %d share an EV (their updates are sequential rounds)", j, t);
+    sg.pool[t] = s->pools[0];
+    sg.version[t] = (s->steps_to_live != 0 && global_step != -1) ? s->version : nullptr;
+    limit = std::max(limit, s->row_cap);
+  }
+  sg.bf16 = vars[0]->sh->bf16;
+  return rows_apply_sgd(descs, num_tables, batch, dim, rowsel, limit, sg, ws, ws_bytes,
+                        S(stream));
+}
+
 int dr_ev_apply_adagrad_decay_grouped(dr_ev* const* vars, dr_ev* const* accums,
                                       dr_ev* const* decay_powers, int num_tables,
                                       const void* const* grads, int grad_by_address,

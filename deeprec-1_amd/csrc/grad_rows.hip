@@ -71,7 +71,49 @@ __global__ void rows_keys_kernel(const int64_t* __restrict__ rowsel, int64_t N, 
   // (RESOURCE_EXHAUSTED already latched by the resolve): no gradient row
   kin[i] = (r >= 0 && r < row_limit) ? (uint32_t)r : sentinel;
   vin[i] = (int32_t)i;
-  flags[i] = -1;
+  if (flags) flags[i] = -1;
+}
+
+// v -= lr * g on one row of a var column (KvResourceSparseApplyGradientDescent,
+// training_ali_ops.cc:1663: one fp32 product, one fp32 difference -- the
+// build keeps -ffp-contract=off, as ev_apply_kernel's apply_one).  bf16 var
+// rows (4 values = 8 B per lane chunk) are widened, updated and rounded to
+// nearest even once, as ev_apply_kernel<OPT_SGD, 4, G, true>.
+__device__ __forceinline__ float4 sgd4(float4 w, float4 g, float lr) {
+  const float4 p = make_float4(lr * g.x, lr * g.y, lr * g.z, lr * g.w);
+  return make_float4(w.x - p.x, w.y - p.y, w.z - p.z, w.w - p.w);
+}
+typedef unsigned int sg_u2 __attribute__((ext_vector_type(2)));
+template <bool WB>
+__device__ __forceinline__ float4 sgd_ld(const float* row, int c) {
+  if constexpr (WB) {
+    const sg_u2 v = __builtin_nontemporal_load(gp(reinterpret_cast<const sg_u2*>(row) + c));
+    const float2 a = bf16x2_to_f2(v.x), b = bf16x2_to_f2(v.y);
+    return make_float4(a.x, a.y, b.x, b.y);
+  } else {
+    return nt_load(reinterpret_cast<const float4*>(row) + c);
+  }
+}
+template <bool WB>
+__device__ __forceinline__ void sgd_st(float* row, int c, float4 w) {
+  if constexpr (WB) {
+    const sg_u2 v = {f2_to_bf16x2(w.x, w.y), f2_to_bf16x2(w.z, w.w)};
+    __builtin_nontemporal_store(v, gp(reinterpret_cast<sg_u2*>(row) + c));
+  } else {
+    nt_store(w, reinterpret_cast<float4*>(row) + c);
+  }
+}
+// Row u of table t += -lr * (the G-lane row gr); version stamped by lane 0.
+template <int G, int CPL, bool WB>
+__device__ __forceinline__ void sgd_row(const Row<4, G, CPL>& gr, void* pool, int64_t* version,
+                                        int64_t u, int dim, float lr, int64_t gs, int lg, int dv) {
+  float* row = static_cast<float*>(pool) + u * (int64_t)(WB ? dim / 2 : dim);
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = lg + c * G;
+    if (col < dv) sgd_st<WB>(row, col, sgd4(sgd_ld<WB>(row, col), gr.v[c], lr));
+  }
+  if (version && lg == 0) version[u] = gs;
 }
 
 // Wave-aggregated append of p to the worklist.
@@ -113,6 +155,112 @@ __global__ void rows_heads_kernel(RowsGroup g, int T, const uint32_t* __restrict
     push = valid && ((head && !last) || (!head && p % kRowsChunk == 0));
   }
   work_push(push, p, work, nwork);
+}
+
+// Fused SGD, sorted order, lane per position (dr_ev_pool_grad_rows_apply_sgd):
+// the run classification of rows_heads_kernel, and a one-position run whose
+// gradient needs no arithmetic -- the rows the unfused backward hands on by
+// address (rows_emit_kernel's rule) -- is applied right here: v -= lr * (0 +
+// g) read from the pooled gradient, the same bytes and roundings as
+// ev_apply_kernel on that address.  Longer runs, inner chunk multiples and
+// the other one-position runs go to rows_work_kernel's worklist.  No mark,
+// scan or emit: the optimizer is the gradient's only consumer, so the
+// IndexedSlices order (first occurrence) is never formed.
+template <int G, bool WB>
+__global__ __launch_bounds__(256) void rows_sgd_kernel(RowsGroup g, RowsSgd sg, int T, int64_t B,
+                                                       const uint32_t* __restrict__ skey,
+                                                       const int32_t* __restrict__ perm,
+                                                       uint32_t sentinel, int dim,
+                                                       int32_t* __restrict__ work,
+                                                       int32_t* __restrict__ nwork) {
+  __shared__ dr_pool_grad_desc sd[DR_MAX_GROUP];
+  __shared__ int64_t sk[DR_MAX_GROUP + 1];
+  __shared__ void* spool[DR_MAX_GROUP];
+  __shared__ int64_t* sver[DR_MAX_GROUP];
+  if (threadIdx.x < T) {
+    sd[threadIdx.x] = g.d[threadIdx.x];
+    spool[threadIdx.x] = sg.pool[threadIdx.x];
+    sver[threadIdx.x] = sg.version[threadIdx.x];
+  }
+  if (threadIdx.x <= T) sk[threadIdx.x] = g.koff[threadIdx.x];
+  __syncthreads();
+  const int64_t N = sk[T];
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool push = false, direct = false;
+  int64_t u = -1;
+  uint64_t ga = 0;
+  int t = 0;
+  if (p < N) {
+    const int64_t pm = p > 0 ? p - 1 : 0, pn = p + 1 < N ? p + 1 : N - 1;
+    const uint32_t uk = skey[p], um = skey[pm], un = skey[pn];
+    const int32_t i = perm[p], im = perm[pm], in = perm[pn];
+    t = tab_of(sk, T, i);
+    const bool valid = uk != sentinel;
+    const bool head = valid && (p == 0 || um != uk || tab_of(sk, T, im) != t);
+    const bool last = p + 1 >= N || un != uk || tab_of(sk, T, in) != t;
+    if (head && last) {
+      const dr_pool_grad_desc& d = sd[t];
+      const int64_t k = i - sk[t];
+      const int64_t r = d.seg ? d.seg[k * d.seg_stride] : k;
+      const bool okr = r >= 0 && r < B;
+      const int mode = d.combiner == DR_COMBINER_SUM ? 0 : 1;
+      bool dfr = okr && !d.weights;
+      if (dfr && mode != 0) dfr = !d.bag_off || d.bag_off[r + 1] - d.bag_off[r] == 1;
+      if (dfr) {
+        direct = true;
+        u = (int64_t)uk;
+        ga = (uint64_t)(uintptr_t)(d.top_grad + r * d.top_stride) | (mode == 0 ? 1u : 0u);
+      } else {
+        push = true;   // (an invalid bag latches in rows_work_kernel)
+      }
+    } else {
+      push = valid && ((head && !last) || (!head && p % kRowsChunk == 0));
+    }
+  }
+  work_push(push, p, work, nwork);
+  if (!__ballot(direct)) return;   // wave-uniform
+  // the wave's direct rows, P at a time, U batches of loads in flight
+  constexpr int P = 64 / G, U = 4;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / G, lg = lane % G;
+  const int dv = dim / 4;
+  const int64_t stride = WB ? dim / 2 : dim;
+  const float lr = sg.lr;
+  for (int k0 = 0; k0 < 64; k0 += P * U) {
+    int64_t rq[U];
+    const float4* gq[U];
+    float* wq[U];
+    bool zq[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int k = k0 + q * P + sub;
+      rq[q] = __shfl(u, k, 64);
+      const uint64_t a = (uint64_t)__shfl((long long)ga, k, 64);
+      const int tq = __shfl(t, k, 64);
+      const bool ok = rq[q] >= 0;
+      zq[q] = a & 1;
+      // always-valid pointers (a skipped row reads table 0's row 0): the
+      // loads of all U rows issue back to back (dr_rows.h load_row_u)
+      gq[q] = reinterpret_cast<const float4*>(ok ? (uintptr_t)(a & ~(uint64_t)1)
+                                                 : (uintptr_t)sd[0].top_grad);
+      wq[q] = static_cast<float*>(spool[ok ? tq : 0]) + (ok ? rq[q] : 0) * stride;
+      if (ok && lg == 0 && sver[tq]) sver[tq][rq[q]] = sg.gs;
+    }
+    for (int c = lg; c < dv; c += G) {
+      float4 gv[U], w[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        gv[q] = nt_load(gq[q] + c);
+        w[q] = sgd_ld<WB>(wq[q], c);
+      }
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        if (rq[q] < 0) continue;
+        if (zq[q]) gv[q] = vadd(vzero<float4>(), gv[q]);
+        sgd_st<WB>(wq[q], c, sgd4(w[q], gv[q], lr));
+      }
+    }
+  }
 }
 
 // Position order: unique ids in first-occurrence order per table, U_t, the
@@ -203,22 +351,36 @@ __device__ bool run_is_long(const uint32_t* __restrict__ skey, const int32_t* __
 // (or, for a long run, its first chunk) in ascending position order into
 // grad_unique[o]; an inner multiple of the chunk sums its chunk into
 // part[c0 / chunk] when its run is long, and is dropped otherwise.
-template <int VEC, int G, int CPL, bool W>
+//
+// SGD (the fused dr_ev_pool_grad_rows_apply_sgd): a run that is not long is
+// applied to its var row (v -= lr * sum) instead of stored; a long run's
+// first chunk goes to grad_unique[c0] (its sorted head), for
+// rows_finish_kernel<SGD> to combine and apply.
+template <int VEC, int G, int CPL, bool W, bool SGD = false, bool WB = false>
 __global__ __launch_bounds__(256) void rows_work_kernel(
     RowsGroup g, int T, int64_t B, const uint32_t* __restrict__ skey,
     const int32_t* __restrict__ perm, const int32_t* __restrict__ ex,
     const int32_t* __restrict__ base, int dim, const int32_t* __restrict__ work,
     const int32_t* __restrict__ nwork, uint64_t* __restrict__ gptr, float* __restrict__ gu,
-    float* __restrict__ part, int32_t* __restrict__ longs, int32_t* __restrict__ nlong, int* st) {
+    float* __restrict__ part, int32_t* __restrict__ longs, int32_t* __restrict__ nlong, int* st,
+    RowsSgd sg) {
   const int nw = *nwork;
   if ((int64_t)blockIdx.x * (256 / G) >= nw) return;   // block-uniform (empty list: one load)
   __shared__ dr_pool_grad_desc sd[DR_MAX_GROUP];
   __shared__ int64_t sk[DR_MAX_GROUP + 1];
   __shared__ int32_t sb[DR_MAX_GROUP + 1];
-  if (threadIdx.x < T) sd[threadIdx.x] = g.d[threadIdx.x];
+  __shared__ void* spool[SGD ? DR_MAX_GROUP : 1];
+  __shared__ int64_t* sver[SGD ? DR_MAX_GROUP : 1];
+  if (threadIdx.x < T) {
+    sd[threadIdx.x] = g.d[threadIdx.x];
+    if constexpr (SGD) {
+      spool[threadIdx.x] = sg.pool[threadIdx.x];
+      sver[threadIdx.x] = sg.version[threadIdx.x];
+    }
+  }
   if (threadIdx.x <= T) {
     sk[threadIdx.x] = g.koff[threadIdx.x];
-    sb[threadIdx.x] = base[threadIdx.x];
+    if constexpr (!SGD) sb[threadIdx.x] = base[threadIdx.x];
   }
   __syncthreads();
   constexpr int GPB = 256 / G;
@@ -327,11 +489,18 @@ __global__ __launch_bounds__(256) void rows_work_kernel(
     }
     if (cbad) latch(st, DR_INVALID_ARGUMENT);
     if (first) {
-      const int64_t o = kt0 + (int64_t)ex[pc] - sb[t];
+      if constexpr (SGD) {
+        static_assert(!SGD || VEC == 4, "fused SGD takes 16-byte rows");
+        if (!islong) {
+          sgd_row<G, CPL, WB>(acc, spool[t], sver[t], (int64_t)u, dim, sg.lr, sg.gs, lg, dv);
+          continue;
+        }
+      }
+      const int64_t o = SGD ? c0 : kt0 + (int64_t)ex[pc] - sb[t];
       float* dst = gu + o * (int64_t)dim;
       store_row<VEC, G, CPL>(acc, dst, lg, dv);
       if (lg == 0) {
-        gptr[o] = (uint64_t)(uintptr_t)dst;
+        if (!SGD) gptr[o] = (uint64_t)(uintptr_t)dst;
         if (islong) {
           const int32_t at = atomicAdd(nlong, 1);
           longs[2 * at] = (int32_t)o;
@@ -351,11 +520,13 @@ __global__ __launch_bounds__(256) void rows_work_kernel(
 // in order; then c_0 + S_0 + S_1 + ... + S_{GPB-1} in group order.  A fixed
 // association (deterministic, fp32 tolerance like every long run), with the
 // serial chain of a hot id cut GPB-fold (a DIN padding id: 800 partials).
-template <int VEC, int G, int CPL>
+// SGD: the combined row is applied to the run's var row instead of stored.
+template <int VEC, int G, int CPL, bool SGD = false, bool WB = false>
 __global__ __launch_bounds__(256) void rows_finish_kernel(
     RowsGroup g, int T, const uint32_t* __restrict__ skey, const int32_t* __restrict__ perm,
     int dim, float* __restrict__ gu, const float* __restrict__ part,
-    const int32_t* __restrict__ longs, const int32_t* __restrict__ nlong, int64_t nslots) {
+    const int32_t* __restrict__ longs, const int32_t* __restrict__ nlong, int64_t nslots,
+    RowsSgd sg) {
   constexpr int GPB = 256 / G;
   __shared__ int64_t sk[DR_MAX_GROUP + 1];
   __shared__ __attribute__((aligned(16))) float red[256 * VEC * CPL];  // GPB group sums (dim <= G*VEC*CPL)
@@ -440,7 +611,12 @@ __global__ __launch_bounds__(256) void rows_finish_kernel(
         }
         acc_add(tot, x);
       }
-      store_row<VEC, G, CPL>(tot, gu + o * (int64_t)dim, lg, dv);
+      if constexpr (SGD) {
+        static_assert(!SGD || VEC == 4, "fused SGD takes 16-byte rows");
+        sgd_row<G, CPL, WB>(tot, sg.pool[t], sg.version[t], (int64_t)u, dim, sg.lr, sg.gs, lg, dv);
+      } else {
+        store_row<VEC, G, CPL>(tot, gu + o * (int64_t)dim, lg, dv);
+      }
     }
     __syncthreads();   // red / used are rewritten by the next run
   }
@@ -526,24 +702,122 @@ static void launch_rows(const RowsGroup& g, int T, int64_t B, const RowsWs& w, i
   if (weighted)
     hipLaunchKernelGGL((rows_work_kernel<VEC, G, CPL, true>), dim3((unsigned)blocks), dim3(256),
                        0, s, g, T, B, w.kout, w.perm, w.ex, w.base, dim, w.work, w.nwork, gptr,
-                       gu, w.part, w.longs, w.nlong, st);
+                       gu, w.part, w.longs, w.nlong, st, RowsSgd{});
   else
     hipLaunchKernelGGL((rows_work_kernel<VEC, G, CPL, false>), dim3((unsigned)blocks), dim3(256),
                        0, s, g, T, B, w.kout, w.perm, w.ex, w.base, dim, w.work, w.nwork, gptr,
-                       gu, w.part, w.longs, w.nlong, st);
+                       gu, w.part, w.longs, w.nlong, st, RowsSgd{});
   if (N > kRowsChunk) {
     // one block per queued run (at most one per chunk); most runs of a
     // hotness-1 batch hold a single partial, so blocks, not lanes, carry them
     const int64_t nslots = N / kRowsChunk + 2;
     const unsigned fb = (unsigned)(nslots < 2048 ? nslots : 2048);
     hipLaunchKernelGGL((rows_finish_kernel<VEC, G, CPL>), dim3(fb), dim3(256), 0, s, g, T,
-                       w.kout, w.perm, dim, gu, w.part, w.longs, w.nlong, nslots);
+                       w.kout, w.perm, dim, gu, w.part, w.longs, w.nlong, nslots, RowsSgd{});
+  }
+}
+
+// The fused SGD tail: direct rows + worklist (rows_sgd_kernel), runs
+// (rows_work_kernel<SGD>), long runs (rows_finish_kernel<SGD>).  gu: [n, dim]
+// scratch for the first chunks of long runs, indexed by sorted head.
+template <int G, int CPL, bool WB>
+static void launch_rows_sgd(const RowsGroup& g, int T, int64_t B, const RowsWs& w, int dim,
+                            bool weighted, uint32_t sentinel, const RowsSgd& sg, float* gu,
+                            hipStream_t s, int* st) {
+  const int64_t N = g.koff[T];
+  hipLaunchKernelGGL((rows_sgd_kernel<G, WB>), dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, s,
+                     g, sg, T, B, w.kout, w.perm, sentinel, dim, w.work, w.nwork);
+  int64_t blocks = ceil_div(N, 256 / G);
+  if (blocks > 4096) blocks = 4096;
+  if (weighted)
+    hipLaunchKernelGGL((rows_work_kernel<4, G, CPL, true, true, WB>), dim3((unsigned)blocks),
+                       dim3(256), 0, s, g, T, B, w.kout, w.perm, nullptr, nullptr, dim, w.work,
+                       w.nwork, nullptr, gu, w.part, w.longs, w.nlong, st, sg);
+  else
+    hipLaunchKernelGGL((rows_work_kernel<4, G, CPL, false, true, WB>), dim3((unsigned)blocks),
+                       dim3(256), 0, s, g, T, B, w.kout, w.perm, nullptr, nullptr, dim, w.work,
+                       w.nwork, nullptr, gu, w.part, w.longs, w.nlong, st, sg);
+  if (N > kRowsChunk) {
+    const int64_t nslots = N / kRowsChunk + 2;
+    const unsigned fb = (unsigned)(nslots < 2048 ? nslots : 2048);
+    hipLaunchKernelGGL((rows_finish_kernel<4, G, CPL, true, WB>), dim3(fb), dim3(256), 0, s, g, T,
+                       w.kout, w.perm, dim, gu, w.part, w.longs, w.nlong, nslots, sg);
   }
 }
 
 __global__ void rows_zero_i32(int32_t* p, int32_t* q) {
   *p = 0;
   *q = 0;
+}
+
+// Fused row-grouped backward + KV SGD (ev.hip dr_ev_pool_grad_rows_apply_sgd
+// validates the EVs and fills sg).  Same sort and run sums as
+// dr_pool_grad_rows_grouped_ex, applied in sorted order.  Needs 16-byte rows
+// (dim % 4 == 0, aligned top_grad slices with top_stride % 4 == 0).
+int rows_apply_sgd(const dr_pool_grad_desc* descs_host, int num_tables, int64_t batch, int dim,
+                   const int64_t* rowsel, int64_t row_limit, const RowsSgd& sg, void* ws,
+                   size_t ws_bytes, hipStream_t s) {
+  DR_REQUIRE(descs_host && num_tables >= 1 && num_tables <= DR_MAX_GROUP && dim > 0 &&
+                 dim <= kRowsMaxDim && dim % 4 == 0 && batch >= 0 && row_limit > 0 && rowsel,
+             DR_INVALID_ARGUMENT, "bad argument (the fused SGD needs dim %% 4 == 0)");
+  RowsGroup g;
+  memset(&g, 0, sizeof(g));
+  bool weighted = false;
+  for (int t = 0; t < num_tables; ++t) {
+    const dr_pool_grad_desc& d = descs_host[t];
+    DR_REQUIRE(d.top_grad && d.nnz >= 0, DR_INVALID_ARGUMENT, "table %d: missing pointers", t);
+    DR_REQUIRE(d.combiner == DR_COMBINER_SUM || d.bag_off || !d.seg, DR_INVALID_ARGUMENT,
+               "table %d: mean/sqrtn of multi-hot bags need bag_off", t);
+    DR_REQUIRE(!d.weights || d.combiner == DR_COMBINER_SUM || d.bag_scale, DR_INVALID_ARGUMENT,
+               "table %d: weighted mean/sqrtn needs bag_scale (dr_bag_weight_scale)", t);
+    DR_REQUIRE(((uintptr_t)d.top_grad & 15) == 0 && d.top_stride % 4 == 0, DR_INVALID_ARGUMENT,
+               "table %d: the fused SGD reads 16-byte gradient rows", t);
+    g.d[t] = d;
+    g.koff[t + 1] = g.koff[t] + d.nnz;
+    weighted = weighted || d.weights;
+  }
+  const int64_t n = g.koff[num_tables];
+  DR_REQUIRE(n < (1ll << 31), DR_INVALID_ARGUMENT, "too many nnz");
+  DR_REQUIRE(batch > 0 || n == 0, DR_INVALID_ARGUMENT, "nnz without a batch");
+  // workspace: the backward's, plus [n, dim] fp32 for long runs' first chunks
+  const size_t wsr = dr_pool_grad_rows_workspace_size(n);
+  const size_t need = wsr + 256 + (size_t)(n > 0 ? n : 1) * dim * sizeof(float);
+  DR_REQUIRE(ws_bytes >= need, DR_INVALID_ARGUMENT, "workspace too small");
+  if (n == 0) return DR_OK;
+  int* st = status_word();
+  DR_REQUIRE(st, DR_INTERNAL, "status word unavailable");
+  RowsWs w = carve_rows(ws, n, nullptr);
+  float* gu = reinterpret_cast<float*>(static_cast<char*>(ws) + ((wsr + 255) & ~size_t(255)));
+  DR_REQUIRE(row_limit < ((int64_t)1 << 32) - 1, DR_INVALID_ARGUMENT,
+             "row_limit must be < 2^32 - 1");
+  int rb = 1;
+  while (rb < 32 && ((int64_t)1 << rb) <= row_limit) ++rb;
+  const uint32_t sentinel = (uint32_t)(((uint64_t)1 << rb) - 1);
+  hipLaunchKernelGGL(rows_keys_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, rowsel,
+                     n, row_limit, sentinel, w.kin, w.vin, (int32_t*)nullptr);
+  DR_LAUNCH_CHECK();
+  int rc = sort_pairs_u32(w.kin, w.vin, w.kout, w.perm, n, rb, w.sort_ws, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(rows_zero_i32, dim3(1), dim3(1), 0, s, w.nlong, w.nwork);
+  const int d4 = dim / 4;
+#define DR_ROWS_SGD(G, CPL)                                                                  \
+  (sg.bf16 ? launch_rows_sgd<G, CPL, true>(g, num_tables, batch, w, dim, weighted, sentinel, sg, \
+                                           gu, s, st)                                          \
+           : launch_rows_sgd<G, CPL, false>(g, num_tables, batch, w, dim, weighted, sentinel, sg, \
+                                            gu, s, st))
+  if (d4 <= 8)
+    DR_ROWS_SGD(8, 1);
+  else if (d4 <= 16)
+    DR_ROWS_SGD(16, 1);
+  else if (d4 <= 32)
+    DR_ROWS_SGD(32, 1);
+  else if (d4 <= 64)
+    DR_ROWS_SGD(64, 1);
+  else
+    DR_ROWS_SGD(64, 4);
+#undef DR_ROWS_SGD
+  DR_LAUNCH_CHECK();
+  return DR_OK;
 }
 
 }  // namespace dr

@@ -175,6 +175,9 @@ SIGNATURES = {
     "dr_ev_apply_grouped_ptr": (_I32, [_I32, _P, _P, _P, _I32, _P, _P, _P, _P, _F32, _F32, _F32,
                                        _F32, _F32, _F32, _I64, _P]),
     "dr_ev_apply_grouped_ptr_rows": (_I32, [_I32, _P, _I32, _P, _P, _P, _P, _P, _F32, _I64, _P]),
+    "dr_ev_pool_grad_rows_sgd_workspace_size": (_SZ, [_I64, _I32]),
+    "dr_ev_pool_grad_rows_apply_sgd": (_I32, [_P, _P, _I32, _I64, _I32, _P, _F32, _I64, _P, _SZ,
+                                              _P]),
     "dr_ev_apply_adam_async_grouped": (_I32, [_I32, _I32, _P, _P, _P, _I32, _P, _P, _P, _P, _P,
                                               _F32, _F32, _F32, _F32, _I64, _P]),
     "dr_ev_apply_adagrad_decay_grouped": (_I32, [_P, _P, _P, _I32, _P, _I32, _P, _P, _P, _F32,

@@ -17,7 +17,7 @@ import torch
 
 from . import _lib, ops
 from ._lib import COMBINERS, ORDER_ALI, ORDER_SEQ, DrPoolDesc, check, lib, ptr, stream_handle, workspace
-from .kv_variable_ops import EmbeddingVariable, IndexedSlices
+from .kv_variable_ops import EmbeddingVariable, IndexedSlices, PendingRowSlices
 
 
 class SparseTensor(object):
@@ -485,7 +485,6 @@ class _RowGroup(object):
         self.koff = koff
 
     def grads(self, g, cols, top_stride):
-        import ctypes as C
         dev = g.device
         D = self.feats[0].params.dim
         T = len(self.feats)
@@ -511,28 +510,82 @@ class _RowGroup(object):
                 d.seg_stride = f.seg_stride
             d.nnz = f.values.numel()
             d.combiner = COMBINERS[f.combiner]
-        n = self.koff[-1]
+        pend = _RowsPending(self, descs, tuple(keep), D, dev)
+        if pend.fusable():
+            return [PendingRowSlices(pend, t, D) for t in range(T)]
+        return pend.materialize()
+
+
+# SGD applies of row-grouped backwards fused with the backward (A/B switch)
+_FUSED_SGD = os.environ.get("DR_ROWS_FUSED_SGD", "1") != "0"
+
+
+class _RowsPending(object):
+    """A row-grouped backward waiting for its consumer (PendingRowSlices):
+    materialize() forms the IndexedSlices (dr_pool_grad_rows_grouped_ex, as
+    the eager backward), apply_sgd() runs the backward fused with the SGD
+    update (dr_ev_pool_grad_rows_apply_sgd).  Holds the pooled gradient and
+    the forward's rows until then."""
+
+    def __init__(self, group, descs, keep, D, dev):
+        self.group, self.descs, self.keep, self.D, self.dev = group, descs, keep, D, dev
+        self.evs = [f.params for f in group.feats]
+        self.slices = None
+        self.applied = False
+
+    def fusable(self):
+        if not _FUSED_SGD or self.slices is not None or self.applied or self.D % 4:
+            return False
+        if len({id(e) for e in self.evs}) != len(self.evs):
+            return False          # one EV twice: sequential rounds, not one fused pass
+        return all(d.top_grad % 16 == 0 and d.top_stride % 4 == 0 for d in self.descs)
+
+    def materialize(self):
+        if self.slices is None:
+            if self.applied:
+                raise RuntimeError("this gradient was already applied (fused SGD)")
+            self.slices = self._form()
+        return self.slices
+
+    def _form(self):
+        grp, dev, D = self.group, self.dev, self.D
+        T = len(grp.feats)
+        n = grp.koff[-1]
         m = max(n, 1)
         uniq = torch.empty(m, dtype=torch.int64, device=dev)
         U = torch.empty(T, dtype=torch.int64, device=dev)
         gptr = torch.empty(m, dtype=torch.int64, device=dev)
         urows = torch.empty(m, dtype=torch.int64, device=dev)
         gu = torch.empty((m, D), dtype=torch.float32, device=dev)
-        keep.append(gu)
-        limit = max(lib().dr_ev_row_capacity(f.params.handle) for f in self.feats)
+        keep = self.keep + (gu,)
+        limit = max(lib().dr_ev_row_capacity(f.params.handle) for f in grp.feats)
         wsb = lib().dr_pool_grad_rows_workspace_size(n)
         ws = workspace(wsb, dev)
         check(lib().dr_pool_grad_rows_grouped_ex(
-            descs, T, self.feats[0].batch, D, ptr(self.rowsel), max(int(limit), 1),
-            ptr(self.vals), 1, ptr(uniq), ptr(urows), ptr(U), ptr(gptr), ptr(gu), ptr(ws), wsb,
+            self.descs, T, grp.feats[0].batch, D, ptr(grp.rowsel), max(int(limit), 1),
+            ptr(grp.vals), 1, ptr(uniq), ptr(urows), ptr(U), ptr(gptr), ptr(gu), ptr(ws), wsb,
             stream_handle(dev)))
         ops._post(dev)
-        k = self.koff
-        keep = tuple(keep)
+        k = grp.koff
         return [IndexedSlices(None, uniq[k[t]:k[t + 1]], U[t:t + 1], True,
                               grad_ptr=gptr[k[t]:k[t + 1]], dim=D, keep=keep,
                               rows=urows[k[t]:k[t + 1]])
                 for t in range(T)]
+
+    def apply_sgd(self, lr, global_step, stream):
+        import ctypes as C
+        grp = self.group
+        T = len(grp.feats)
+        n = grp.koff[-1]
+        wsb = lib().dr_ev_pool_grad_rows_sgd_workspace_size(n, self.D)
+        ws = workspace(wsb, self.dev)
+        P = C.c_void_p * T
+        check(lib().dr_ev_pool_grad_rows_apply_sgd(
+            P(*[e.handle.value for e in self.evs]), self.descs, T, grp.feats[0].batch, self.D,
+            ptr(grp.rowsel), lr, global_step, ptr(ws), wsb, stream))
+        ops._post(self.dev)
+        self.applied = True
+        self.keep = ()
 
 
 class _UniqueGroup(object):

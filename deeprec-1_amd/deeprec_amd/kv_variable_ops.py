@@ -151,6 +151,46 @@ class IndexedSlices(object):
         self._keep = ()
 
 
+class PendingRowSlices(IndexedSlices):
+    """Table t's gradient of a row-grouped lookup backward, not yet formed.
+
+    An SGD apply_gradients over every variable of the group runs the
+    backward fused with the update (dr_ev_pool_grad_rows_apply_sgd: the same
+    run sums and v -= lr * g roundings, no IndexedSlices in between).  Any
+    other use -- indices, values, rows, num_valid, grad_ptr -- first forms the
+    IndexedSlices exactly as the eager backward (dr_pool_grad_rows_grouped_ex)
+    would have, and the object is an ordinary IndexedSlices from then on."""
+
+    _LAZY = ("indices", "rows", "num_valid", "grad_ptr", "_values", "_keep")
+
+    def __init__(self, pending, t, dim):
+        self._pending = pending
+        self._t = t
+        self.unique = True
+        self.dim = dim
+
+    def __getattr__(self, name):
+        # only reached for attributes not yet in __dict__
+        if name in PendingRowSlices._LAZY:
+            real = self._pending.materialize()[self._t]
+            for k in PendingRowSlices._LAZY:
+                self.__dict__.setdefault(k, getattr(real, k))
+            return self.__dict__[name]
+        raise AttributeError(name)
+
+    def fusable(self):
+        return "indices" not in self.__dict__ and self._pending.fusable()
+
+    @property
+    def values(self):
+        return IndexedSlices.values.fget(self)
+
+    @values.setter
+    def values(self, v):
+        self.__getattr__("indices")   # formed first: the indices stay valid
+        IndexedSlices.values.fset(self, v)
+
+
 class EmbeddingVariable(object):
     """Hash-keyed embedding table resident in HBM.
 

@@ -14,7 +14,8 @@ import torch
 from . import ops
 from ._lib import check, lib, ptr, stream_handle
 from .embedding_ops import DenseTable
-from .kv_variable_ops import EmbeddingVariable, IndexedSlices, _flush_deferred_releases
+from .kv_variable_ops import (EmbeddingVariable, IndexedSlices, PendingRowSlices,
+                              _flush_deferred_releases)
 
 
 def _concat(slices):
@@ -115,6 +116,8 @@ class _Optimizer(object):
 
     def apply_gradients(self, var_list, global_step=None):
         gs = -1 if global_step is None else int(global_step)
+        if self._opt == 0 and _KNOWN_ROWS:
+            self._apply_fused_rows(var_list, gs)
         rounds = []   # rounds[r] = [(var, slices)] applied in one grouped launch
         for var in var_list:
             if not var.pending_grads:
@@ -136,6 +139,28 @@ class _Optimizer(object):
             self._apply_ev_batch(items, gs)
         self._finish()
         _flush_deferred_releases()   # EVs collected meanwhile (no-op while capturing)
+
+    def _apply_fused_rows(self, var_list, gs):
+        """SGD over every EV of a row-grouped lookup backward whose gradient
+        is still pending (PendingRowSlices, nothing else read it): one fused
+        backward + update (dr_ev_pool_grad_rows_apply_sgd), the same values as
+        forming the IndexedSlices and applying them.  A group only partly in
+        var_list, or an EV with more than that one pending gradient, takes the
+        ordinary path."""
+        groups = {}
+        for var in var_list:
+            pg = var.pending_grads
+            if (isinstance(var, EmbeddingVariable) and len(pg) == 1
+                    and isinstance(pg[0], PendingRowSlices) and pg[0].fusable()):
+                groups.setdefault(id(pg[0]._pending), (pg[0]._pending, []))[1].append(var)
+        for pend, vs in groups.values():
+            if len(vs) != len(pend.evs) or {id(v) for v in vs} != {id(e) for e in pend.evs}:
+                continue
+            st = stream_handle(pend.dev)
+            with _Locked(self.use_locking, [e.handle.value for e in pend.evs], st):
+                pend.apply_sgd(self.lr, gs, st)
+            for v in vs:
+                v.pending_grads = []
 
     def _slots(self, var):
         return None, None
@@ -259,9 +284,13 @@ class AdamOptimizer(_Optimizer):
         m, v = self._dense_mv.setdefault(id(var), (torch.zeros_like(w), torch.zeros_like(w)))
         f32 = lambda x: torch.tensor(x, dtype=torch.float32)
         lr = (f32(self.lr) * torch.sqrt(1 - f32(self.b2p)) / (1 - f32(self.b1p))).item()
+        # (1 - beta) in fp32, as adam.py's tensors compute it (1.0f - 0.9f =
+        # 0.100000024f, not the double 0.1 rounded)
+        c1 = (f32(1.0) - f32(self.beta1)).item()
+        c2 = (f32(1.0) - f32(self.beta2)).item()
         with torch.no_grad():
-            m.mul_(self.beta1).index_add_(0, idx, g * (1 - self.beta1))
-            v.mul_(self.beta2).index_add_(0, idx, (g * g) * (1 - self.beta2))
+            m.mul_(self.beta1).index_add_(0, idx, g * c1)
+            v.mul_(self.beta2).index_add_(0, idx, (g * g) * c2)
             w.sub_(lr * m / (torch.sqrt(v) + self.eps))
 
 

@@ -560,6 +560,24 @@ int dr_ev_apply_grouped_ptr_rows(int optimizer, dr_ev* const* vars, int num_tabl
                                  const int64_t* const* rows, const int64_t* n_host,
                                  const int64_t* const* n_dev, float lr, int64_t global_step,
                                  void* stream);
+/* The row-grouped lookup backward and KvResourceSparseApplyGradientDescent  */
+/* (training_ali_ops.cc:1597-1678) fused: the composition                    */
+/*   dr_pool_grad_rows_grouped_ex(descs, ..., rowsel, defer = 1) ->          */
+/*   dr_ev_apply_grouped_ptr_rows(DR_OPT_SGD, vars, ...)                     */
+/* when the optimizer is the gradient's only consumer (the training graph   */
+/* of embedding_ops.py:592-675 -> optimizer.apply_gradients).  Every         */
+/* (table, row) run gets the same sum (ascending positions, the same chunk   */
+/* association for runs > 256) and the same v -= lr * g rounding, the same   */
+/* version stamp (steps_to_live EVs, global_step != -1); the runs are        */
+/* applied in row order and the IndexedSlices are never formed.  vars[t]:    */
+/* distinct filter-free primary EVs (fp32 or bf16) of dim `dim`, dim % 4 ==  */
+/* 0, descs' top_grad slices 16-byte aligned with top_stride % 4 == 0.       */
+/* Workspace: dr_ev_pool_grad_rows_sgd_workspace_size(total nnz, dim).       */
+size_t dr_ev_pool_grad_rows_sgd_workspace_size(int64_t total_nnz, int dim);
+int dr_ev_pool_grad_rows_apply_sgd(dr_ev* const* vars, const dr_pool_grad_desc* descs,
+                                   int num_tables, int64_t batch, int dim, const int64_t* rowsel,
+                                   float lr, int64_t global_step, void* ws, size_t ws_bytes,
+                                   void* stream);
 /* KvResourceSparseApplyAdamAsync (training_ali_ops.cc:1404-1575) with the  */
 /* beta powers DEVICE-resident, as the reference keeps them in an EV (key 0,  */
 /* :1523-1526): powers[t] is table t's float[2] {beta1_power, beta2_power}.   */

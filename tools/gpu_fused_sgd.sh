@@ -1,0 +1,24 @@
+# Fused row-grouped backward + SGD: parity tests, then the training-step A/B
+# (DR_ROWS_FUSED_SGD=0 is the unfused path) in fp32 and bf16, and the kernel
+# stats of the fused step.  Tag $1.
+set -o pipefail
+T=${1:-fsgd}
+mkdir -p gpurun_out/$T
+timeout -k 10 300 python -u -m pytest tests/test_gpu_rows_sgd_fused.py tests/test_gpu_rows_grad.py -x -q --timeout 120 --timeout-method thread > gpurun_out/$T/tests.log 2>&1
+rc=$?; tail -3 gpurun_out/$T/tests.log; [ $rc -ne 0 ] && exit $rc
+for X in "" "--bf16"; do
+  for F in 0 1 0 1; do
+    DR_ROWS_FUSED_SGD=$F timeout -k 10 200 python tools/train_probe.py --graph --steps 24 $X > gpurun_out/$T/tp.log 2>&1 || exit 1
+    echo "fused=$F $X $(grep '^{' gpurun_out/$T/tp.log)" | tee -a gpurun_out/$T/ab.log
+  done
+done
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/prof -o run -- python3 tools/train_probe.py --graph --steps 8 > gpurun_out/$T/prof.log 2>&1 || exit 1
+f=$(find gpurun_out/$T/prof -name "*kernel_stats.csv" | head -1)
+python3 - "$f" <<'PY'
+import csv, sys
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
+for r in rows[:22]:
+    print("%-90s %6s %10.1f us avg %8.1f" % (r["Name"][:90], r["Calls"], float(r["TotalDurationNs"]) / 1e3, float(r["AverageNs"]) / 1e3))
+PY

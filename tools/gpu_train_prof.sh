@@ -2,9 +2,10 @@
 # tools/train_probe.py --graph (SGD, bench shape).  Tag $1.
 set -o pipefail
 T=${1:-tp}
+X=${2:-}   # extra train_probe flags, e.g. --bf16
 mkdir -p gpurun_out/$T
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/prof -o run -- python3 tools/train_probe.py --graph --steps 8 > gpurun_out/$T/train.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/prof -o run -- python3 tools/train_probe.py --graph --steps 8 $X > gpurun_out/$T/train.log 2>&1 || exit 1
 tail -2 gpurun_out/$T/train.log
 f=$(find gpurun_out/$T/prof -name "*kernel_stats.csv" | head -1)
 python3 - "$f" <<'PY'

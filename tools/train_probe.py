@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--opt", default="sgd", choices=["sgd", "adagrad", "adam", "ftrl"])
     ap.add_argument("--graph", action="store_true",
                     help="replay the steps as one captured hipGraph (no host launch gaps)")
+    ap.add_argument("--bf16", action="store_true", help="bf16 EV value rows (fp32 slots)")
     args = ap.parse_args()
     import deeprec_amd as dr
     from deeprec_amd.embedding_ops import SparseTensor
@@ -38,7 +39,8 @@ def main():
     T, D, B, R = args.tables, args.dim, args.batch, args.rows
     evs = []
     for t in range(T):
-        ev = dr.EmbeddingVariable("tr%d" % t, D, 0.0, capacity=R + (1 << 20), device=dev)
+        ev = dr.EmbeddingVariable("tr%d" % t, D, 0.0, capacity=R + (1 << 20), device=dev,
+                                  value_dtype=torch.bfloat16 if args.bf16 else torch.float32)
         ev.insert_synthetic(0, R, seed=1000 + t)
         evs.append(ev)
     opt = {"sgd": lambda: dr.GradientDescentOptimizer(0.01),
@@ -85,7 +87,8 @@ def main():
     el = time.perf_counter() - t0
     dr.status_check(dev)
     ms = el / args.steps * 1e3
-    print(json.dumps({"probe": "train_step", "opt": args.opt, "graph": bool(args.graph), "tables": T, "rows": R, "dim": D,
+    print(json.dumps({"probe": "train_step", "opt": args.opt, "graph": bool(args.graph),
+                      "bf16": bool(args.bf16), "tables": T, "rows": R, "dim": D,
                       "batch": B, "ms_per_step": round(ms, 3),
                       "lookups_per_s": round(T * B / (ms * 1e-3), 1),
                       "samples_per_s": round(B / (ms * 1e-3), 1)}), flush=True)
