@@ -324,7 +324,7 @@ def test_onehot_fused_abi_orders_and_slot_column(dr):
 @pytest.mark.parametrize("n,kmax,bit_lo,bit_hi", [
     (100003, 1 << 20, 0, 20), (1, 5, 0, 8), (4095, 1 << 12, 0, 12), (4096, 7, 0, 3),
     (4097, 1 << 40, 0, 40), (2000000, 1 << 21, 0, 21), (300000, 3, 0, 2),
-    (50000, 1 << 40, 9, 34)])
+    (50000, 1 << 40, 9, 34), (300000, 1 << 62, 0, 62)])
 def test_sort_pairs_stable(ops, n, kmax, bit_lo, bit_hi):
     """Stable LSD sort on bits [bit_lo, bit_hi): ragged last tile, one key,
     exactly one tile, few distinct keys (runs spanning many tiles), and a
