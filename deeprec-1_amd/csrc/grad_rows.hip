@@ -61,10 +61,17 @@ __device__ __forceinline__ int tab_of(const int64_t* koff, int T, int64_t i) {
   return lo;
 }
 
+// (also zeroes the worklist / long-run counters: they are first used after
+// the sort, two launches later)
 __global__ void rows_keys_kernel(const int64_t* __restrict__ rowsel, int64_t N, int64_t row_limit,
                                  uint32_t sentinel, uint32_t* __restrict__ kin,
-                                 int32_t* __restrict__ vin, int32_t* __restrict__ flags) {
+                                 int32_t* __restrict__ vin, int32_t* __restrict__ flags,
+                                 int32_t* __restrict__ nlong, int32_t* __restrict__ nwork) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) {
+    *nlong = 0;
+    *nwork = 0;
+  }
   if (i >= N) return;
   const int64_t r = rowsel[i];
   // a negative row is an EV default served because the pool was exhausted
@@ -698,7 +705,7 @@ static void launch_rows(const RowsGroup& g, int T, int64_t B, const RowsWs& w, i
   // the worklist is at most N entries; a grid-stride pass over its device
   // count (an empty list costs one load per block)
   int64_t blocks = ceil_div(N, 256 / G);
-  if (blocks > 4096) blocks = 4096;
+  if (blocks > 1024) blocks = 1024;   // grid-stride: an idle block still costs its dispatch
   if (weighted)
     hipLaunchKernelGGL((rows_work_kernel<VEC, G, CPL, true>), dim3((unsigned)blocks), dim3(256),
                        0, s, g, T, B, w.kout, w.perm, w.ex, w.base, dim, w.work, w.nwork, gptr,
@@ -728,7 +735,7 @@ static void launch_rows_sgd(const RowsGroup& g, int T, int64_t B, const RowsWs& 
   hipLaunchKernelGGL((rows_sgd_kernel<G, WB>), dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, s,
                      g, sg, T, B, w.kout, w.perm, sentinel, dim, w.work, w.nwork);
   int64_t blocks = ceil_div(N, 256 / G);
-  if (blocks > 4096) blocks = 4096;
+  if (blocks > 1024) blocks = 1024;   // grid-stride: an idle block still costs its dispatch
   if (weighted)
     hipLaunchKernelGGL((rows_work_kernel<4, G, CPL, true, true, WB>), dim3((unsigned)blocks),
                        dim3(256), 0, s, g, T, B, w.kout, w.perm, nullptr, nullptr, dim, w.work,
@@ -743,11 +750,6 @@ static void launch_rows_sgd(const RowsGroup& g, int T, int64_t B, const RowsWs& 
     hipLaunchKernelGGL((rows_finish_kernel<4, G, CPL, true, WB>), dim3(fb), dim3(256), 0, s, g, T,
                        w.kout, w.perm, dim, gu, w.part, w.longs, w.nlong, nslots, sg);
   }
-}
-
-__global__ void rows_zero_i32(int32_t* p, int32_t* q) {
-  *p = 0;
-  *q = 0;
 }
 
 // Fused row-grouped backward + KV SGD (ev.hip dr_ev_pool_grad_rows_apply_sgd
@@ -794,11 +796,10 @@ int rows_apply_sgd(const dr_pool_grad_desc* descs_host, int num_tables, int64_t 
   while (rb < 32 && ((int64_t)1 << rb) <= row_limit) ++rb;
   const uint32_t sentinel = (uint32_t)(((uint64_t)1 << rb) - 1);
   hipLaunchKernelGGL(rows_keys_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, rowsel,
-                     n, row_limit, sentinel, w.kin, w.vin, (int32_t*)nullptr);
+                     n, row_limit, sentinel, w.kin, w.vin, (int32_t*)nullptr, w.nlong, w.nwork);
   DR_LAUNCH_CHECK();
   int rc = sort_pairs_u32(w.kin, w.vin, w.kout, w.perm, n, rb, w.sort_ws, s);
   if (rc) return rc;
-  hipLaunchKernelGGL(rows_zero_i32, dim3(1), dim3(1), 0, s, w.nlong, w.nwork);
   const int d4 = dim / 4;
 #define DR_ROWS_SGD(G, CPL)                                                                  \
   (sg.bf16 ? launch_rows_sgd<G, CPL, true>(g, num_tables, batch, w, dim, weighted, sentinel, sg, \
@@ -886,11 +887,10 @@ int dr_pool_grad_rows_grouped_ex(const dr_pool_grad_desc* descs_host, int num_ta
   const uint32_t sentinel = (uint32_t)(((uint64_t)1 << rb) - 1);
   const unsigned nb = (unsigned)ceil_div(n, 256);
   hipLaunchKernelGGL(rows_keys_kernel, dim3(nb), dim3(256), 0, s, rowsel, n, row_limit, sentinel,
-                     w.kin, w.vin, w.flags);
+                     w.kin, w.vin, w.flags, w.nlong, w.nwork);
   DR_LAUNCH_CHECK();
   int rc = sort_pairs_u32(w.kin, w.vin, w.kout, w.perm, n, rb, w.sort_ws, s);
   if (rc) return rc;
-  hipLaunchKernelGGL(rows_zero_i32, dim3(1), dim3(1), 0, s, w.nlong, w.nwork);
   hipLaunchKernelGGL(rows_heads_kernel, dim3(nb), dim3(256), 0, s, g, num_tables, w.kout, w.perm,
                      sentinel, w.flags, w.work, w.nwork);
   rc = scan_exclusive_marks(w.flags, w.ex, n, w.total, w.scan_ws, s);
