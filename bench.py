@@ -358,8 +358,8 @@ def dcn_bf16_leg(args, dev, log):
            "train_step": {"ms_per_step": round(tms, 4),
                           "samples_per_s": round(B / (tms * 1e-3), 1),
                           "step": "fused bf16 lookup recording rows + row-grouped backward (fp32 "
-                                  "gradients) + by-address KV SGD rounding to bf16, hipGraph of "
-                                  "4 steps"}}
+                                  "gradients) fused with the KV SGD update rounding to bf16 "
+                                  "(dr_ev_pool_grad_rows_apply_sgd), hipGraph of 4 steps"}}
     log("dcn bf16 leg: %s" % json.dumps(res))
     del evs, fsets, g
     return res
@@ -445,8 +445,9 @@ def deepfm_leg(args, dev, log):
                         "bytes_per_launch": T * B * per},
            "train_step": {"ms_per_step": round(tms, 4),
                           "samples_per_s": round(B / (tms * 1e-3), 1),
-                          "step": "fused lookup recording rows + row-grouped backward + "
-                                  "by-address KV SGD, hipGraph of 4 steps"}}
+                          "step": "fused lookup recording rows + row-grouped backward fused with "
+                                  "the KV SGD update (dr_ev_pool_grad_rows_apply_sgd), hipGraph "
+                                  "of 4 steps"}}
     log("deepfm leg: %s" % json.dumps(res))
     del evs, kfeats, g
     return res
@@ -772,7 +773,8 @@ def main():
                  "graph": tgraph is not None,
                  "step": "embedding layer training step: embedding_lookup_sparse_multi forward "
                          "(fused EV probe + row copy recording each id's row) + backward (row-grouped "
-                         "segment grad, gradients by address) + KV SGD apply, %d EVs, B=%d" % (T, B)}
+                         "segment grad) fused with the KV SGD update "
+                         "(dr_ev_pool_grad_rows_apply_sgd), %d EVs, B=%d" % (T, B)}
         log("train step: %s" % json.dumps(train))
 
     # ---- dominant kernel: the fused one-hot EV lookup, timed alone --------
