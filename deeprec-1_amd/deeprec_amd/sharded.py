@@ -468,7 +468,17 @@ class XgmiShardedLookup(object):
     Unique and the local expansion are the price.  The backward sums each
     unique key's gradient locally first (dr_pool_grad_grouped, the
     reference's per-worker IndexedSlices) and the owners pull those rows.
-    Outputs are bit-identical to the non-dedup path and to one GPU."""
+    Outputs are bit-identical to the non-dedup path and to one GPU.
+
+    Multi-hot bags (forward(ids, bag_offs=...)): ids [T, nnz] with nnz up to
+    the engine's per-table key capacity `batch`, bag_offs[t] int32 [bags+1]
+    (the same bag count for every table), combiner sum / mean / sqrtn.  They
+    always take the Unique route above (embedding_lookup_sparse's own Unique,
+    embedding_ops.py:592-675): unique keys routed, one row per unique key
+    served into the staging buffer, then the ALI-order segment pooling over
+    the bags (SparseSegmentReduction, segment_reduction_ali_ops_util.h:193-
+    318); backward: each unique key's SparseSegment*Grad sum, pulled by its
+    owner.  No host read in either direction."""
 
     def __init__(self, evs, world, rank, batch, device, group=None, peer_buffers=None,
                  barrier=None, buffers=None, dedup=False):
@@ -564,17 +574,20 @@ class XgmiShardedLookup(object):
         from .kv_variable_ops import IndexedSlices
         g = grad_out.contiguous()
         T, D, B, W = self.T, self.dim, self.batch, self.world
-        if tuple(g.shape) != (B, T * D) or not g.is_floating_point():
-            raise ValueError("grad must be [%d, %d]" % (B, T * D))
-        if self.dedup:
+        if not g.is_floating_point() or (self._saved is None and tuple(g.shape) != (B, T * D)):
+            raise ValueError("grad must be a float [%d, %d]" % (B, T * D))
+        if self._saved is not None:
             # per unique key: the sum of its positions' gradients (ascending
-            # position, SparseSegmentSumGrad), laid out at the forward's slots
+            # position, SparseSegment*Grad), laid out at the forward's slots
             # u*T + t for the owners' pulls
-            if self._saved is None:
-                raise RuntimeError("backward() needs a dedup forward() first")
-            idx, U = self._saved
-            gu = self._local.pool_grad(g.float(), idx, self._koff, U, None, B, "sum")
-            self.bufs.gin.view(B, T, D).copy_(gu[:T * B].view(T, B, D).transpose(0, 1))
+            idx, U, koff, bag_offs, bags, combiner = self._saved
+            nnz = koff[1]
+            if tuple(g.shape) != (bags, T * D):
+                raise ValueError("grad must be [%d, %d]" % (bags, T * D))
+            gu = self._local.pool_grad(g.float(), idx, koff, U, bag_offs, bags, combiner)
+            self.bufs.gin.view(B, T, D)[:nnz].copy_(gu[:T * nnz].view(T, nnz, D).transpose(0, 1))
+        elif self.dedup:
+            raise RuntimeError("backward() needs a dedup forward() first")
         else:
             self.bufs.gin.copy_(g)
         self._barrier()
@@ -597,11 +610,16 @@ class XgmiShardedLookup(object):
             self.evs[t].pending_grads.append(IndexedSlices(v, k, num_valid=n, unique=False))
         return out
 
-    def forward(self, ids, out_dtype=None):
+    def forward(self, ids, out_dtype=None, bag_offs=None, combiner="sum"):
         """ids: [T, B] int64 keys (hotness 1) -> [B, T*D] pooled (sum).  bf16
         EVs travel as bf16 rows (half the link bytes); the result is widened
         to fp32 (the reference's cast) unless out_dtype=torch.bfloat16, which
-        returns the peer-written bf16 buffer itself."""
+        returns the peer-written bf16 buffer itself.
+
+        Multi-hot: ids [T, nnz] (nnz <= batch), bag_offs = T int32 [bags+1]
+        offset arrays -> [bags, T*D] pooled with `combiner` (a new tensor)."""
+        if bag_offs is not None:
+            return self._forward_bags(ids, bag_offs, combiner, out_dtype)
         if tuple(ids.shape) != (self.T, self.batch) or ids.dtype != torch.int64:
             raise ValueError("ids must be int64 [%d, %d]" % (self.T, self.batch))
         ids = ids.contiguous()
@@ -614,9 +632,10 @@ class XgmiShardedLookup(object):
             self._barrier()
             # expand: bag (b, t) reads the staging row of its unique key
             rowsel = (idx.view(T, B).to(torch.int64) * T + self._tcol).view(-1)
-            self._saved = (idx, U)
+            self._saved = (idx, U, self._koff, None, B, "sum")
             return self._local.pool(self.bufs.out.view(B * T, self.dim), rowsel, None,
                                     self._koff, None, B, "sum", out_dtype)
+        self._saved = None
         self.route(ids)
         self._barrier()
         self.serve()
@@ -624,6 +643,36 @@ class XgmiShardedLookup(object):
         if self.bufs.out.dtype == torch.bfloat16 and out_dtype != torch.bfloat16:
             return self.bufs.out.float()
         return self.bufs.out
+
+    def _forward_bags(self, ids, bag_offs, combiner, out_dtype):
+        T, B = self.T, self.batch
+        if ids.dim() != 2 or ids.shape[0] != T or ids.dtype != torch.int64 or ids.shape[1] > B:
+            raise ValueError("multi-hot ids must be int64 [%d, nnz <= %d]" % (T, B))
+        if len(bag_offs) != T or combiner not in ("sum", "mean", "sqrtn"):
+            raise ValueError("bag_offs: %d offset arrays; combiner sum / mean / sqrtn" % T)
+        bags = int(bag_offs[0].numel()) - 1
+        if any(int(o.numel()) - 1 != bags or o.dtype != torch.int32 for o in bag_offs):
+            raise ValueError("bag_offs must be int32 [bags+1] with one bag count")
+        nnz = int(ids.shape[1])
+        koff = [t * nnz for t in range(T + 1)]
+        ids = ids.contiguous()
+        uniq, idx, _, U = ops.unique_grouped(ids.view(-1), koff, False)
+        if nnz == B:
+            keys = uniq
+        else:   # the route layout is [T, batch]: table t's unique keys at t*batch
+            keys = torch.zeros((T, B), dtype=torch.int64, device=self.device)
+            if nnz:
+                keys[:, :nnz] = uniq.view(T, nnz)
+        self.route(keys, n_dev=U)
+        self._barrier()
+        self.serve()
+        self._barrier()
+        # expand: position i of table t reads the staging row u*T + t of its
+        # unique key u, pooled over its bag in the ALI order
+        rowsel = (idx.view(T, nnz).to(torch.int64) * T + self._tcol).view(-1)
+        self._saved = (idx, U, koff, list(bag_offs), bags, combiner)
+        return self._local.pool(self.bufs.out.view(B * T, self.dim), rowsel, None, koff,
+                                bag_offs, bags, combiner, out_dtype)
 
     def close(self):
         for b in self._bases:

@@ -314,6 +314,100 @@ def test_xgmi_dedup_engine(world):
                 evs_all[r][t].pending_grads.clear()
 
 
+@pytest.mark.parametrize("world,combiner", [(1, "sum"), (2, "mean"), (3, "sqrtn"), (2, "sum")])
+def test_xgmi_multihot_engine(world, combiner):
+    """Multi-hot bags on the peer-write engine (Unique -> route unique keys
+    -> owners serve one row per unique key -> ALI-order pooling over the
+    bags): bags of 0..4 Zipf-skewed ids, empty bags, per-table key capacity
+    4 x the bag count.  Forward bit-exact vs the oracle's
+    embedding_lookup_sparse; backward: each owner pulls, per table and
+    source rank, the source's unique keys in first-occurrence order with
+    their SparseSegment{Sum,Mean,SqrtN}Grad rows."""
+    import deeprec_amd as dr
+    from oracle import oracle as orc
+    from deeprec_amd.sharded import XgmiBuffers, XgmiShardedLookup
+    dr.load()
+    rng = np.random.default_rng(97 + world)
+    CAP = 4 * B
+    evs_all, bufs = [], []
+    for r in range(world):
+        own = np.arange(r, KEYSPACE // 2, world, dtype=np.int64)
+        evs = []
+        for t in range(T):
+            ev = dr.EmbeddingVariable("xgm%d_%s_%d_%d" % (world, combiner, r, t), D, DEFAULT,
+                                      device=DEV)
+            ev.insert(torch.as_tensor(own, device=DEV), torch.as_tensor(_vals(t, own), device=DEV))
+            evs.append(ev)
+        evs_all.append(evs)
+        bufs.append(XgmiBuffers(world, T, CAP, D, DEV))
+    bar = threading.Barrier(world)
+    engines = [XgmiShardedLookup(evs_all[r], world, r, CAP, torch.device(DEV), peer_buffers=bufs,
+                                 barrier=bar.wait, buffers=bufs[r]) for r in range(world)]
+    allk = np.arange(0, KEYSPACE // 2, dtype=np.int64)
+    for step in range(2):
+        lens = [rng.integers(0, 5, B) for _ in range(world)]
+        for ln in lens:
+            ln[3] = 0
+        offs = [np.concatenate([[0], np.cumsum(ln)]).astype(np.int32) for ln in lens]
+        ids = [((rng.zipf(1.3, size=(T, int(ln.sum()))) - 1) % KEYSPACE).astype(np.int64)
+               for ln in lens]
+        grads = [rng.standard_normal((B, T * D)).astype(np.float32) for _ in range(world)]
+        outs, pulled, errs = [None] * world, [None] * world, []
+
+        def run(r):
+            try:
+                bo = [torch.as_tensor(offs[r], device=DEV)] * T
+                o = engines[r].forward(torch.as_tensor(ids[r], device=DEV), bag_offs=bo,
+                                       combiner=combiner)
+                outs[r] = o.cpu().numpy()
+                got = engines[r].backward(torch.as_tensor(grads[r], device=DEV))
+                pulled[r] = []
+                for k, v, n in got:
+                    m = int(n.item())
+                    pulled[r].append((k[:m].cpu().numpy(), v[:m].cpu().numpy()))
+            except Exception as e:
+                errs.append(e)
+                bar.abort()
+
+        th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(120)
+        if errs:
+            raise errs[0]
+        dr.status_check()
+        for r in range(world):
+            seg = np.repeat(np.arange(B), lens[r])
+            ind = np.stack([seg, np.zeros_like(seg)], 1)
+            for t in range(T):
+                ref_ev = orc.EV(D, DEFAULT)
+                ref_ev.insert(allk, _vals(t, allk))
+                ref = orc.embedding_lookup_sparse(ref_ev, ind, ids[r][t], B, combiner=combiner)
+                np.testing.assert_array_equal(outs[r][:, t * D:(t + 1) * D], ref)
+                wk, wg, wl = [], [], []
+                for src in range(world):
+                    uids, idx = orc.unique(ids[src][t])
+                    sseg = np.repeat(np.arange(B), lens[src]).astype(np.int32)
+                    gu = orc.sparse_segment_reduce_grad(
+                        np.ascontiguousarray(grads[src][:, t * D:(t + 1) * D]), idx, sseg,
+                        uids.size, combiner)
+                    sel = uids % world == r
+                    wk.append(uids[sel])
+                    wg.append(gu[sel])
+                    # > 256 positions: ordered chunk partials (fp32 tolerance)
+                    wl.append(np.bincount(idx, minlength=uids.size)[sel] > 256)
+                k, v = pulled[r][t]
+                np.testing.assert_array_equal(k, np.concatenate(wk))
+                ref_g = np.concatenate(wg).reshape(-1, D)
+                hot = np.concatenate(wl)
+                np.testing.assert_array_equal(v[~hot], ref_g[~hot])
+                for i in np.where(hot)[0]:
+                    err = np.abs(v[i] - ref_g[i]).max()
+                    assert err <= 1e-5 * np.abs(ref_g[i]).max(), (i, err)
+                evs_all[r][t].pending_grads.clear()
+
+
 @pytest.mark.parametrize("world", [1, 2])
 def test_xgmi_serve_grows_small_tables(world):
     """Owners whose EVs start with room for 256 rows receive ~3x that many new
