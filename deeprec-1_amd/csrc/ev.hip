@@ -1582,6 +1582,10 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
       DR_APPLY(4, 32, false);
     else if (aligned)
       DR_APPLY(4, 64, false);
+    else if (dim <= 4)    // narrow unaligned rows (a linear model's dim 1): 16 rows per pass
+      DR_APPLY(1, 4, false);
+    else if (dim <= 32)   // DIN's D = 18
+      DR_APPLY(1, 32, false);
     else
       DR_APPLY(1, 64, false);
 #undef DR_APPLY

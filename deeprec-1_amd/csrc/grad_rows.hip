@@ -391,6 +391,10 @@ __global__ __launch_bounds__(256) void rows_work_kernel(
   }
   __syncthreads();
   constexpr int GPB = 256 / G;
+  // positions of a run fetched per step: the serial sum's loads are issued
+  // CH at a time -- deeper for scalar rows (one register per row chunk), so
+  // a 256-position chunk of a hot id is 16 dependent steps instead of 32
+  constexpr int CH = VEC * CPL <= 1 ? 16 : kRowsChain;
   const int64_t N = sk[T];
   const int lg = threadIdx.x % G;
   const int dv = dim / VEC;
@@ -448,13 +452,13 @@ __global__ __launch_bounds__(256) void rows_work_kernel(
     const int64_t kt0 = sk[t];
     const int64_t nnz_t = d.nnz;
     bool cbad = false;
-    for (int64_t p = c0; p < lim; p += kRowsChain) {
-      R y[kRowsChain];
-      int64_t ry[kRowsChain];
-      int64_t ky[W ? kRowsChain : 1];
-      bool ok[kRowsChain];
+    for (int64_t p = c0; p < lim; p += CH) {
+      R y[CH];
+      int64_t ry[CH];
+      int64_t ky[W ? CH : 1];
+      bool ok[CH];
 #pragma unroll
-      for (int j = 0; j < kRowsChain; ++j) {
+      for (int j = 0; j < CH; ++j) {
         const int64_t pj = p + j < N ? p + j : N - 1;
         const int64_t k = (int64_t)perm[pj] - kt0;
         // positions of one (table, row) are contiguous; a position of the same
@@ -465,34 +469,37 @@ __global__ __launch_bounds__(256) void rows_work_kernel(
       }
       if (segp) {
 #pragma unroll
-        for (int j = 0; j < kRowsChain; ++j) ry[j] = segp[ry[j] * sst];
+        for (int j = 0; j < CH; ++j) ry[j] = segp[ry[j] * sst];
       }
 #pragma unroll
-      for (int j = 0; j < kRowsChain; ++j) {
+      for (int j = 0; j < CH; ++j) {
         const bool okr = (ry[j] >= 0) & (ry[j] < B);
         cbad |= ok[j] & !okr;
         ry[j] = okr ? ry[j] : -1;
         load_row_u<VEC, G, CPL>(y[j], tg + (okr ? ry[j] : 0) * ts, lg, dv);
       }
+      // ok[] is a prefix (a run's positions are contiguous): predicated, not
+      // an early exit, so the loop unrolls and y[] stays in registers
 #pragma unroll
-      for (int j = 0; j < kRowsChain; ++j) {
-        if (!ok[j]) break;
-        if (ry[j] < 0) {
+      for (int j = 0; j < CH; ++j) {
+        if (ok[j]) {
+          if (ry[j] < 0) {
 #pragma unroll
-          for (int c = 0; c < CPL; ++c) y[j].v[c] = vzero<V>();
-        }
-        if (W && d.weights)
-          wscaled(y[j], d, ry[j], ky[W ? j : 0]);
-        else
-          scaled(y[j], d, mode, ry[j]);
-        if (fresh) {
-          acc = y[j];
-          fresh = false;
-        } else {
-          acc_add(acc, y[j]);
+            for (int c = 0; c < CPL; ++c) y[j].v[c] = vzero<V>();
+          }
+          if (W && d.weights)
+            wscaled(y[j], d, ry[j], ky[W ? j : 0]);
+          else
+            scaled(y[j], d, mode, ry[j]);
+          if (fresh) {
+            acc = y[j];
+            fresh = false;
+          } else {
+            acc_add(acc, y[j]);
+          }
         }
       }
-      if (!ok[kRowsChain - 1]) break;
+      if (!ok[CH - 1]) break;
     }
     if (cbad) latch(st, DR_INVALID_ARGUMENT);
     if (first) {
@@ -912,7 +919,9 @@ int dr_pool_grad_rows_grouped_ex(const dr_pool_grad_desc* descs_host, int num_ta
     else
       launch_rows<4, 64, 4>(g, num_tables, batch, w, dim, weighted, grad_ptr, grad_unique, s, st);
   } else {
-    if (dim <= 64)
+    if (dim <= 32)
+      launch_rows<1, 32, 1>(g, num_tables, batch, w, dim, weighted, grad_ptr, grad_unique, s, st);
+    else if (dim <= 64)
       launch_rows<1, 64, 1>(g, num_tables, batch, w, dim, weighted, grad_ptr, grad_unique, s, st);
     else if (dim <= 256)
       launch_rows<1, 64, 4>(g, num_tables, batch, w, dim, weighted, grad_ptr, grad_unique, s, st);
@@ -941,6 +950,12 @@ int dr_rows_from_ptr(const uint64_t* grad_ptr, int64_t n, const int64_t* n_dev, 
     else
       hipLaunchKernelGGL((rows_from_ptr_kernel<4, 64, 4>), dim3((unsigned)ceil_div(n, 4)),
                          dim3(256), 0, s, grad_ptr, n, n_dev, dim, out);
+  } else if (dim <= 32) {
+    hipLaunchKernelGGL((rows_from_ptr_kernel<1, 32, 1>), dim3((unsigned)ceil_div(n, 8)),
+                       dim3(256), 0, s, grad_ptr, n, n_dev, dim, out);
+  } else if (dim <= 64) {
+    hipLaunchKernelGGL((rows_from_ptr_kernel<1, 64, 1>), dim3((unsigned)ceil_div(n, 4)),
+                       dim3(256), 0, s, grad_ptr, n, n_dev, dim, out);
   } else {
     hipLaunchKernelGGL((rows_from_ptr_kernel<1, 64, 16>), dim3((unsigned)ceil_div(n, 4)),
                        dim3(256), 0, s, grad_ptr, n, n_dev, dim, out);
