@@ -210,6 +210,18 @@ __device__ __forceinline__ int table_of(const int64_t* koff, int T, int64_t i,
 // the next kernel may still see the previous contents in another XCD's L2.
 int fill_bytes(void* p, unsigned char value, size_t bytes, hipStream_t st);
 
+// ev.hip: host-side serialisation of the calls on EVs (EvGuard) for
+// composite entries outside ev.hip that read EV pointers across calls
+void* ev_guard_acquire(dr_ev* const* evs, int64_t n);
+void ev_guard_release(void* g);
+struct EvGuardRef {
+  void* g;
+  explicit EvGuardRef(dr_ev* ev) : g(ev_guard_acquire(&ev, 1)) {}
+  ~EvGuardRef() { ev_guard_release(g); }
+  EvGuardRef(const EvGuardRef&) = delete;
+  EvGuardRef& operator=(const EvGuardRef&) = delete;
+};
+
 // ---- row-grouped lookup backward fused with KV SGD (grad_rows.hip; the C
 // entry dr_ev_pool_grad_rows_apply_sgd is in ev.hip, which owns the EVs) ----
 // Per table of the group: the var column's rows (fp32, or bf16 pairs when

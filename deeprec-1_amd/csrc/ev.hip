@@ -81,6 +81,8 @@ struct EvShared {
   // host threads and streams
   std::mutex update_mu;
   hipEvent_t update_ev = nullptr;
+  // host side of every call on this EV (EvGuard below)
+  std::recursive_mutex api_mu;
 };
 
 // float words per row of column `col`
@@ -97,6 +99,42 @@ struct dr_ev {
 };
 
 namespace dr {
+
+// Host-side serialisation of the calls on one EV.  The reference runs ops on
+// one EmbeddingVar concurrently from inter-op threads; here a call reads the
+// EV's table / pool pointers and enqueues kernels, and a growth (reserve ->
+// grow) rehashes and frees them.  A call holds the api_mu of every EV it
+// touches (distinct shared states, address order: no lock-order cycle) from
+// its first read of an EV pointer to its last launch, and grow() synchronises
+// the device before reading the old buffers, so every kernel another stream
+// enqueued on them earlier has finished.  The kernels of different streams
+// still overlap on the device -- the CAS insert arbitrates there, as the
+// lockless map's CAS does -- and a launch is asynchronous, so the lock costs
+// launch time only.  dr_ev_lock_updates (use_locking) is a separate mutex
+// taken around whole calls and never inside one.
+class EvGuard {
+ public:
+  EvGuard(dr_ev* const* evs, int64_t n) {
+    if (evs)
+      for (int64_t i = 0; i < n; ++i)
+        if (evs[i]) v_.push_back(evs[i]->sh);
+    std::sort(v_.begin(), v_.end());
+    v_.erase(std::unique(v_.begin(), v_.end()), v_.end());
+    for (EvShared* e : v_) e->api_mu.lock();
+  }
+  explicit EvGuard(dr_ev* ev) : EvGuard(&ev, 1) {}
+  ~EvGuard() {
+    for (auto it = v_.rbegin(); it != v_.rend(); ++it) (*it)->api_mu.unlock();
+  }
+  EvGuard(const EvGuard&) = delete;
+  EvGuard& operator=(const EvGuard&) = delete;
+
+ private:
+  std::vector<EvShared*> v_;
+};
+
+void* ev_guard_acquire(dr_ev* const* evs, int64_t n) { return new EvGuard(evs, n); }
+void ev_guard_release(void* g) { delete static_cast<EvGuard*>(g); }
 
 // Per-table view passed to kernels by value.
 struct EvDesc {
@@ -1245,6 +1283,9 @@ static void free_shared(EvShared* s) {
 
 // Grow the slot table and/or the row arrays so that `need` keys fit.
 static int grow(EvShared* s, int64_t need, hipStream_t st) {
+  // kernels other streams enqueued on the old table / pools must be done
+  // before they are copied and freed (EvGuard keeps new ones from starting)
+  DR_HIP(hipDeviceSynchronize());
   if (need > s->cap * 3 / 4) {
     int64_t ncap = next_pow2(need * 2);
     Slot* ns = nullptr;
@@ -1377,6 +1418,7 @@ static int resolve_grouped(dr_ev* const* evs, int T, const int64_t* keys, const 
                            const int32_t* counts, int64_t* rows_out, void* ws, size_t ws_bytes,
                            hipStream_t st, const int32_t* tags = nullptr,
                            const int64_t* per_table_host = nullptr) {
+  EvGuard guard_(evs, T);
   const bool composite = tags != nullptr;
   DR_REQUIRE(T >= 1 && T <= DR_MAX_GROUP, DR_INVALID_ARGUMENT, "bad table count");
   const int64_t total = koff[T];
@@ -1475,6 +1517,7 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
                          const int64_t* n_host, const int64_t* const* n_dev, int64_t gs,
                          hipStream_t st, int gind = 0, const int64_t* const* rows = nullptr,
                          float* const* powers = nullptr) {
+  EvGuard guard_(vars, T);
   DR_REQUIRE(!rows || opt == OPT_SGD, DR_INVALID_ARGUMENT,
              "known rows skip the slot-column first-touch check: SGD only");
   DR_REQUIRE(T >= 1 && vars && grads && keys && n_host, DR_INVALID_ARGUMENT, "bad argument");
@@ -1958,6 +2001,7 @@ static void launch_lookup_onehot(const LookupArgs& a, int T, int64_t B, int dim,
 static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t ksb, int64_t kst,
                          int64_t B, float* out, int64_t out_stride, int order, int64_t* rows_out,
                          void* ws, size_t ws_bytes, hipStream_t st, int flags = 0) {
+  EvGuard guard_(evs, T);
   DR_REQUIRE(evs && T >= 1 && T <= DR_MAX_GROUP && B >= 0 && out_stride >= 0, DR_INVALID_ARGUMENT,
              "bad argument");
   DR_REQUIRE(ksb >= 0 && kst >= 0, DR_INVALID_ARGUMENT, "key strides must be >= 0");
@@ -2257,6 +2301,7 @@ int dr_ev_unlock_updates(dr_ev* const* vars, int n, void* stream) {
 const float* dr_ev_pool(dr_ev* ev) { return ev ? ev->sh->pools[ev->col] : nullptr; }
 
 int dr_ev_size(dr_ev* ev, int64_t* size_host, void* stream) {
+  dr::EvGuard guard_(ev);
   DR_REQUIRE(ev && size_host, DR_INVALID_ARGUMENT, "null argument");
   DR_HIP(hipStreamSynchronize(dr::S(stream)));
   DR_HIP(hipMemcpy(size_host, ev->sh->top, sizeof(int64_t), hipMemcpyDeviceToHost));
@@ -2266,6 +2311,7 @@ int dr_ev_size(dr_ev* ev, int64_t* size_host, void* stream) {
 
 int dr_ev_shrink(dr_ev* ev, int64_t global_step, float l2_weight_threshold,
                  int64_t* removed_host, void* stream) {
+  dr::EvGuard guard_(ev);
   using namespace dr;
   DR_REQUIRE(ev && ev->col == 0, DR_INVALID_ARGUMENT, "shrink needs a primary EV");
   EvShared* s = ev->sh;
@@ -2319,6 +2365,7 @@ int dr_ev_shrink(dr_ev* ev, int64_t global_step, float l2_weight_threshold,
 }
 
 int dr_ev_reserve(dr_ev* ev, int64_t extra, void* stream) {
+  dr::EvGuard guard_(ev);
   DR_REQUIRE(ev && extra >= 0, DR_INVALID_ARGUMENT, "bad argument");
   dr::EvShared* s = ev->sh;
   hipStream_t st = dr::S(stream);
@@ -2408,6 +2455,7 @@ int dr_ev_resolve_tagged(dr_ev* const* evs, int num_tables, const int64_t* keys,
                          const int32_t* tags, int64_t n, const int64_t* n_dev,
                          const int64_t* per_table_host, const int32_t* counts,
                          int64_t* rows_out, void* ws, size_t ws_bytes, void* stream) {
+  dr::EvGuard guard_(evs, num_tables);
   DR_REQUIRE(num_tables >= 1 && num_tables <= DR_MAX_GROUP, DR_INVALID_ARGUMENT,
              "bad table count");
   int64_t koff[DR_MAX_GROUP + 1];
@@ -2424,6 +2472,7 @@ int dr_ev_resolve_tagged(dr_ev* const* evs, int num_tables, const int64_t* keys,
 int dr_ev_gather_tagged(dr_ev* const* evs, int num_tables, const int32_t* tags,
                         const int64_t* rows, int64_t n, const int64_t* n_dev, float* out,
                         void* stream) {
+  dr::EvGuard guard_(evs, num_tables);
   using namespace dr;
   DR_REQUIRE(num_tables >= 1 && num_tables <= DR_MAX_GROUP, DR_INVALID_ARGUMENT,
              "bad table count");
@@ -2451,6 +2500,7 @@ const float* dr_ev_default_row(dr_ev* ev) {
 
 int dr_ev_gather(dr_ev* ev, const int64_t* keys, int64_t n, const float* defaults,
                  const int32_t* counts, float* out, void* ws, size_t ws_bytes, void* stream) {
+  dr::EvGuard guard_(ev);
   using namespace dr;
   DR_REQUIRE(ev && n >= 0, DR_INVALID_ARGUMENT, "bad argument");
   if (n == 0) return DR_OK;
@@ -2475,6 +2525,7 @@ size_t dr_ev_gather_workspace_size(int64_t n) {
 int dr_ev_insert(dr_ev* ev, const int64_t* keys, int64_t n, const float* values,
                  const int64_t* versions, const int64_t* freqs, int64_t partition_id,
                  int64_t partition_num, void* stream) {
+  dr::EvGuard guard_(ev);
   using namespace dr;
   DR_REQUIRE(ev && n >= 0, DR_INVALID_ARGUMENT, "bad argument");
   if (n == 0) return DR_OK;
@@ -2510,6 +2561,7 @@ int dr_ev_insert(dr_ev* ev, const int64_t* keys, int64_t n, const float* values,
 // synth(seed, key, col) -- populates bench/test tables without a host copy.
 int dr_ev_insert_synthetic(dr_ev* ev, int64_t key_begin, int64_t key_stride, int64_t n,
                            uint64_t seed, void* stream) {
+  dr::EvGuard guard_(ev);
   using namespace dr;
   DR_REQUIRE(ev && n >= 0 && key_stride >= 1, DR_INVALID_ARGUMENT, "bad argument");
   if (n == 0) return DR_OK;
@@ -2542,6 +2594,7 @@ int dr_ev_insert_synthetic(dr_ev* ev, int64_t key_begin, int64_t key_stride, int
 // embedding_var.h:221-243), ascending key order.
 int dr_ev_export(dr_ev* ev, int64_t* keys_out, float* values_out, int64_t* versions_out,
                  int64_t* freqs_out, int64_t capacity, int64_t* m_host, void* stream) {
+  dr::EvGuard guard_(ev);
   using namespace dr;
   DR_REQUIRE(ev && m_host, DR_INVALID_ARGUMENT, "null argument");
   hipStream_t st = S(stream);
@@ -2633,6 +2686,7 @@ int dr_ev_export(dr_ev* ev, int64_t* keys_out, float* values_out, int64_t* versi
 
 int dr_ev_key_meta(dr_ev* ev, const int64_t* keys_host, int64_t n, int64_t* freq_host,
                    int64_t* version_host, int32_t* has_row_host, void* stream) {
+  dr::EvGuard guard_(ev);
   using namespace dr;
   DR_REQUIRE(ev && keys_host && n >= 0, DR_INVALID_ARGUMENT, "bad argument");
   if (n == 0) return DR_OK;
@@ -2767,6 +2821,7 @@ int dr_ev_pool_grad_rows_apply_sgd(dr_ev* const* vars, const dr_pool_grad_desc* 
                                    int num_tables, int64_t batch, int dim, const int64_t* rowsel,
                                    float lr, int64_t global_step, void* ws, size_t ws_bytes,
                                    void* stream) {
+  dr::EvGuard guard_(vars, num_tables);
   using namespace dr;
   DR_REQUIRE(vars && descs && num_tables >= 1 && num_tables <= DR_MAX_GROUP, DR_INVALID_ARGUMENT,
              "bad argument");
@@ -3062,6 +3117,7 @@ size_t dr_xgmi_serve_workspace_size(int world, int64_t cap) {
 
 int dr_xgmi_serve(const dr_xgmi_peers* peers, dr_ev* const* evs, int num_tables,
                   int64_t batch, void* ws, size_t ws_bytes, void* stream) {
+  dr::EvGuard guard_(evs, num_tables);
   using namespace dr;
   DR_REQUIRE(peers && evs && num_tables >= 1 && num_tables <= DR_MAX_GROUP && batch >= 0,
              DR_INVALID_ARGUMENT, "bad argument");

@@ -91,6 +91,8 @@ int dr_embedding_lookup_sparse(dr_ev* ev, const float* table, int64_t table_rows
   using namespace dr;
   DR_REQUIRE((ev != nullptr) != (table != nullptr), DR_INVALID_ARGUMENT,
              "exactly one of ev / table must be given");
+  // the resolve and the pooling that reads the EV's pool are one call on it
+  EvGuardRef guard_(ev);
   DR_REQUIRE(nnz >= 0 && batch >= 0 && dim > 0 && out && out_stride >= dim,
              DR_INVALID_ARGUMENT, "bad shape");
   DR_REQUIRE(nnz == 0 || (sp_indices && sp_values), DR_INVALID_ARGUMENT, "null sparse input");

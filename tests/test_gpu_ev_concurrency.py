@@ -1,0 +1,100 @@
+"""GPU: the reference's multi-thread EmbeddingVar invariants
+(core/kernels/embedding_variable_ops_test.cc), restated for the device EV.
+
+TestMultiInsertion (:554-590): THREADNUM threads LookupOrCreate keys 0..4 of
+one EV at once -> Size() == 5, the snapshot holds 5 keys, and every row is
+the initial value (9.0).  TestInsertAndLookup (:920-965): threads insert
+disjoint random key sets concurrently, then every key looks up its own value
+(InsertAndLookup, :892-918) and Size() counts them all.
+
+Here each host thread issues on its own HIP stream (torch's current stream
+is per thread), so the kernels of different threads run concurrently on the
+device: the CAS insert is the only arbitration, as the lockless map's CAS is
+in the reference.
+"""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+THREADNUM = 16
+
+
+@pytest.fixture(scope="module")
+def dr():
+    import deeprec_amd
+    deeprec_amd.load()
+    assert torch.cuda.is_available()
+    return deeprec_amd
+
+
+def _in_threads(fn, n):
+    errs = []
+
+    def run(i):
+        try:
+            s = torch.cuda.Stream(device=DEV)
+            with torch.cuda.stream(s):
+                fn(i)
+            s.synchronize()
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    if errs:
+        raise errs[0]
+    torch.cuda.synchronize()
+
+
+def test_multi_insertion_lookup_or_create(dr):
+    D = 128
+    for rep in range(3):
+        ev = dr.EmbeddingVariable("mtins_%d" % rep, D, 9.0)
+        keys = torch.arange(5, dtype=torch.int64, device=DEV)
+        outs = [None] * THREADNUM
+
+        def work(i):
+            for _ in range(5):
+                outs[i] = ev.sparse_read(keys)
+
+        _in_threads(work, THREADNUM)
+        dr.status_check()
+        assert ev.total_count().tolist() == [5, D]
+        k, v = ev.export()[:2]
+        assert sorted(k.cpu().tolist()) == [0, 1, 2, 3, 4]
+        assert bool((v == 9.0).all())
+        for o in outs:
+            assert bool((o == 9.0).all())
+
+
+def test_insert_and_lookup_disjoint_threads(dr):
+    D = 16
+    rng = np.random.default_rng(7)
+    loops = 1000 * THREADNUM // 16 * 16
+    keys = rng.choice(1 << 40, size=loops, replace=False).astype(np.int64)
+    vals = (keys[:, None] % 9973).astype(np.float32) + np.arange(D, dtype=np.float32)[None, :]
+    ev = dr.EmbeddingVariable("mtlookup", D, 0.0, capacity=1024)   # grows while threads insert
+    per = loops // THREADNUM
+    got = [None] * THREADNUM
+
+    def work(i):
+        k = torch.as_tensor(keys[i * per:(i + 1) * per], device=DEV)
+        ev.insert(k, torch.as_tensor(vals[i * per:(i + 1) * per], device=DEV))
+        got[i] = ev.sparse_read(k).cpu().numpy()
+
+    _in_threads(work, THREADNUM)
+    dr.status_check()
+    assert ev.total_count().tolist() == [loops, D]
+    for i in range(THREADNUM):
+        np.testing.assert_array_equal(got[i], vals[i * per:(i + 1) * per])
+    # and all of them from the default stream afterwards
+    np.testing.assert_array_equal(ev.sparse_read(torch.as_tensor(keys, device=DEV)).cpu().numpy(),
+                                  vals)
