@@ -98,3 +98,53 @@ def test_insert_and_lookup_disjoint_threads(dr):
     # and all of them from the default stream afterwards
     np.testing.assert_array_equal(ev.sparse_read(torch.as_tensor(keys, device=DEV)).cpu().numpy(),
                                   vals)
+
+
+def test_overlapping_lookup_or_create_while_growing(dr):
+    """16 threads LookupOrCreate overlapping key sets (each key drawn by ~4
+    threads, in different orders) on an EV that starts with room for 256
+    keys: every key gets exactly one row (Size = distinct keys, export = the
+    distinct keys).  Then 16 threads Import overlapping sets into a second
+    growing EV, every writer with the same value f(key) -- Import keeps the
+    first row it finds (LookupOrCreateEmb, embedding_var.h:187-219), so
+    whichever insert wins, every key reads f(key) from every thread."""
+    D = 32
+    rng = np.random.default_rng(11)
+    universe = rng.choice(1 << 50, size=8000, replace=False).astype(np.int64)
+    picks = [rng.permutation(universe)[:2000] for _ in range(THREADNUM)]
+    ev = dr.EmbeddingVariable("mtover", D, 0.5, capacity=256)
+
+    def work(i):
+        k = torch.as_tensor(picks[i], device=DEV)
+        for chunk in torch.split(k, 500):
+            out = ev.sparse_read(chunk)
+            assert bool((out == 0.5).all())
+
+    _in_threads(work, THREADNUM)
+    dr.status_check()
+    distinct = np.unique(np.concatenate(picks))
+    assert ev.total_count().tolist() == [distinct.size, D]
+    k = ev.export()[0].cpu().numpy()
+    np.testing.assert_array_equal(np.sort(k), distinct)
+
+    def f(keys):
+        return (keys[:, None] % 997).astype(np.float32) + np.arange(D, dtype=np.float32)[None, :]
+
+    ev2 = dr.EmbeddingVariable("mtover2", D, 0.5, capacity=256)
+
+    def imp(i):
+        for chunk in np.array_split(picks[i], 4):
+            ev2.insert(torch.as_tensor(chunk, device=DEV), torch.as_tensor(f(chunk), device=DEV))
+
+    _in_threads(imp, THREADNUM)
+    dr.status_check()
+    assert ev2.total_count().tolist() == [distinct.size, D]
+    got = [None] * THREADNUM
+
+    def read(i):
+        got[i] = ev2.sparse_read(torch.as_tensor(picks[i], device=DEV)).cpu().numpy()
+
+    _in_threads(read, THREADNUM)
+    for i in range(THREADNUM):
+        np.testing.assert_array_equal(got[i], f(picks[i]))
+    assert ev2.total_count().tolist() == [distinct.size, D]
