@@ -148,3 +148,29 @@ def test_overlapping_lookup_or_create_while_growing(dr):
     for i in range(THREADNUM):
         np.testing.assert_array_equal(got[i], f(picks[i]))
     assert ev2.total_count().tolist() == [distinct.size, D]
+
+
+@pytest.mark.parametrize("threads,reps", [(5, 1)])
+def test_feature_filter_parallel(dr, threads, reps):
+    """TestFeatureFilterParallel (:1012-1037): EmbeddingConfig(steps_to_live 5,
+    filter_freq 7); 5 threads each LookupOrCreate key 20 once -> its
+    frequency counts every one of them (5), and the key, still below the
+    threshold, reads the default row.  (Past the threshold the reference
+    stops counting -- CounterFilter::LookupOrCreate, embedding_filter.h:
+    295-305 -- so more concurrent lookups than filter_freq leave a racy count
+    there: not pinned.)"""
+    ev = dr.EmbeddingVariable(
+        "mtfilter_%d" % threads, 10, 10.0, steps_to_live=5,
+        ev_option=dr.EmbeddingVariableOption(filter_option=dr.CounterFilter(7)))
+    outs = [None] * threads
+
+    def work(i):
+        for _ in range(reps):
+            outs[i] = ev.sparse_read(torch.tensor([20], dtype=torch.int64, device=DEV))
+
+    _in_threads(work, threads)
+    dr.status_check()
+    fr, _, _ = ev.key_meta(np.array([20], np.int64))
+    assert int(fr[0]) == threads * reps
+    for o in outs:
+        assert bool((o == 10.0).all())
