@@ -1714,6 +1714,7 @@ struct LookupArgs {
   float* out;
   int64_t out_stride;
   int64_t* rows;        // [T, B] row served per id (-1: default), or nullptr
+  int tmaj;             // visit slots table by table (s = t * B + b), not in output order
 };
 
 // Row of `key` when present with this column initialised, else -1.
@@ -1767,8 +1768,13 @@ __global__ __launch_bounds__(256) void ev_lookup_onehot_kernel(LookupArgs a, int
   uint64_t pkey = 0;
   if (prober) {
     const int64_t s = s0 + lg;
-    pb = (int64_t)((uint32_t)s / (uint32_t)T);  // slots < 2^31 (host check)
-    pt = (int)(s - pb * T);
+    if (a.tmaj) {   // slots < 2^31 (host check)
+      pt = (int)((uint32_t)s / (uint32_t)B);
+      pb = s - (int64_t)pt * B;
+    } else {
+      pb = (int64_t)((uint32_t)s / (uint32_t)T);
+      pt = (int)(s - pb * T);
+    }
     pkey = (uint64_t)__builtin_nontemporal_load(gp(a.keys + pb * a.ksb + (int64_t)pt * a.kst));
   }
   if (threadIdx.x < T) sd[threadIdx.x] = a.d[threadIdx.x];
@@ -1799,7 +1805,8 @@ __global__ __launch_bounds__(256) void ev_lookup_onehot_kernel(LookupArgs a, int
     unsigned long long at = 0;
     if (lane == leader) at = atomicAdd(mcnt, (unsigned long long)__popcll(mm));
     at = __shfl(at, leader, 64);
-    if (missed) mlist[at + __popcll(mm & lanemask_lt())] = (int32_t)(s0 + lg);
+    // (the miss list holds output-order slots b * T + t in either visiting order)
+    if (missed) mlist[at + __popcll(mm & lanemask_lt())] = (int32_t)(pb * T + pt);
   }
   // every row address first (the shuffles' LDS waits then precede the row
   // loads), then the NB row loads back to back as global (not flat) loads
@@ -1818,8 +1825,15 @@ __global__ __launch_bounds__(256) void ev_lookup_onehot_kernel(LookupArgs a, int
     const int64_t s = s0 + q;
     o[q] = nullptr;
     if (p[q] && s < slots) {
-      const int64_t b = (int64_t)((uint32_t)s / (uint32_t)T);
-      o[q] = a.out + b * a.out_stride + (s - b * T) * (int64_t)dim;
+      int64_t b, t;
+      if (a.tmaj) {
+        t = (int64_t)((uint32_t)s / (uint32_t)B);
+        b = s - t * B;
+      } else {
+        b = (int64_t)((uint32_t)s / (uint32_t)T);
+        t = s - b * T;
+      }
+      o[q] = a.out + b * a.out_stride + t * (int64_t)dim;
     }
     load_row_copy<VEC, G, CPL, WIDEN>(x[q], p[q], lg, dv);
   }
@@ -2015,7 +2029,8 @@ static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t 
   // reference casts bf16 embeddings to float32, embedding_ops.py:606-607);
   // with DR_LOOKUP_OUT_BF16 the rows are copied bitwise as D / 2 float words
   // into a bf16 output.  out_stride counts elements of the output type.
-  DR_REQUIRE((flags & ~DR_LOOKUP_OUT_BF16) == 0, DR_INVALID_ARGUMENT, "unknown flags 0x%x", flags);
+  DR_REQUIRE((flags & ~(DR_LOOKUP_OUT_BF16 | DR_LOOKUP_TABLE_ORDER)) == 0, DR_INVALID_ARGUMENT,
+             "unknown flags 0x%x", flags);
   const bool bf16 = evs[0]->sh->bf16 && evs[0]->col == 0;
   const bool out_bf16 = flags & DR_LOOKUP_OUT_BF16;
   const bool widen = bf16 && !out_bf16;
@@ -2075,6 +2090,7 @@ static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t 
   la.rows = ma.rows = rows_out;
   la.out = ma.out = out;
   la.out_stride = ma.out_stride = out_stride;
+  la.tmaj = (flags & DR_LOOKUP_TABLE_ORDER) ? 1 : 0;
   const int d4 = (int)(dim / 4);
 #define DR_LK(G, C)                                                             \
   do {                                                                          \

@@ -26,6 +26,7 @@ POOL_ONEHOT = 1
 POOL_BF16 = 2
 POOL_OUT_BF16 = 4
 LOOKUP_OUT_BF16 = 1
+LOOKUP_TABLE_ORDER = 2
 
 
 class DeepRecError(RuntimeError):

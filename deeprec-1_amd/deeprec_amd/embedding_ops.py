@@ -644,6 +644,11 @@ class _UniqueGroup(object):
                 for t in range(len(self.feats))]
 
 
+# feature-major one-hot lookups visiting the ids table by table: A/B switch,
+# off -- measured slower than output order (profiles/r03_ab_table_order.log)
+_TABLE_ORDER = os.environ.get("DR_LOOKUP_TABLE_ORDER", "0") == "1"
+
+
 def _fused_onehot_ok(feats):
     p0 = feats[0].params
     if not (len(feats) <= _lib.MAX_GROUP and isinstance(p0, EmbeddingVariable)):
@@ -721,6 +726,10 @@ def _fused_onehot(feats, order, with_rows=False, out_dtype=None):
         ops._post(dev)
         return out
     vals = _concat_values(feats, koff)
+    if _TABLE_ORDER:
+        # feature-major [T, B] ids: visit them table by table so the id reads
+        # and the row records are contiguous (same results)
+        flags |= _lib.LOOKUP_TABLE_ORDER
     if with_rows:
         rowsel = torch.empty(T * B, dtype=torch.int64, device=dev)
         check(lib().dr_ev_lookup_onehot_ex(handles, T, ptr(vals), 1, B, B, ptr(out), T * D, order,

@@ -448,6 +448,11 @@ int dr_ev_lookup_onehot_strided(dr_ev* const* evs, int num_tables, const int64_t
 /* per lookup.  ALI order only for bf16 EVs.  The entries above are this    */
 /* one with flags 0.                                                         */
 #define DR_LOOKUP_OUT_BF16 1
+/* DR_LOOKUP_TABLE_ORDER: visit the ids table by table (t, b) instead of in */
+/* output order (b, t) -- the same results; with feature-major [T, B] ids   */
+/* (key_stride_table = B) the id reads and the rows_out records ([T, B])    */
+/* become contiguous instead of one 8-byte access per 128-byte line.        */
+#define DR_LOOKUP_TABLE_ORDER 2
 int dr_ev_lookup_onehot_ex(dr_ev* const* evs, int num_tables, const int64_t* keys,
                            int64_t key_stride_bag, int64_t key_stride_table, int64_t batch,
                            void* out, int64_t out_stride, int order, int flags, int64_t* rows_out,
