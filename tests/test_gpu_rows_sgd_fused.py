@@ -282,3 +282,36 @@ def test_fused_sgd_graph_captured_equals_eager(dr):
     for p, q in zip(*exports):
         for x, y in zip(p, q):
             np.testing.assert_array_equal(x, y)
+
+
+def test_lookup_table_order_flag_same_results(dr):
+    """DR_LOOKUP_TABLE_ORDER (visit the feature-major ids table by table)
+    gives the output order's outputs and row records bit for bit on the same
+    EVs.  Each order runs first on one EV set (creating the new keys: the
+    miss path) and second on the other (all hits)."""
+    import ctypes as C
+    from deeprec_amd._lib import LOOKUP_TABLE_ORDER, check, lib, ptr, stream_handle
+    rng = np.random.default_rng(3)
+    T_, B, D = 5, 3000, 32
+    ids = T(rng.integers(0, 2600, (T_, B)).astype(np.int64))
+
+    def run(evs, flags):
+        out = torch.empty((B, T_ * D), device=DEV)
+        rows = torch.empty(T_ * B, dtype=torch.int64, device=DEV)
+        handles = (C.c_void_p * T_)(*[e.handle.value for e in evs])
+        wsb = lib().dr_ev_lookup_onehot_workspace_size(T_, B)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=DEV)
+        check(lib().dr_ev_lookup_onehot_ex(handles, T_, ptr(ids), 1, B, B, ptr(out), T_ * D, 0,
+                                           flags, ptr(rows), ptr(ws), wsb, stream_handle(DEV)))
+        torch.cuda.synchronize()
+        dr.status_check()
+        return H(out), H(rows)
+
+    for first in (0, LOOKUP_TABLE_ORDER):
+        evs = [dr.EmbeddingVariable("tord_%d_%d" % (first, t), D, 0.3) for t in range(T_)]
+        for t, e in enumerate(evs):
+            e.insert_synthetic(0, 2000, seed=40 + t)   # ids >= 2000 are new: misses
+        o1, r1 = run(evs, first)
+        o2, r2 = run(evs, LOOKUP_TABLE_ORDER - first)
+        np.testing.assert_array_equal(o1, o2)
+        np.testing.assert_array_equal(r1, r2)
