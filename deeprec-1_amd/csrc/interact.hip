@@ -212,6 +212,125 @@ __global__ __launch_bounds__(256) void dot_tile_kernel(const float* __restrict__
 }
 
 // ---------------------------------------------------------------------------
+// DLRM dot on the f32-input MFMA (v_mfma_f32_16x16x4_f32: exact f32, one
+// rounding per product, a k-ordered fmaf chain per 4-k step).  One wave per
+// sample, no LDS: the Gram matrix X X^T of a sample is at most 32 x 32 =
+// 2 x 2 blocks of 16 rows, of which the lower three are formed:
+// (0,0) = mfma(a0, a0), (1,0) = mfma(a1, a0), (1,1) = mfma(a1, a1).
+// The A and B operand maps of 16x16x4 (A[i = l&15][k = l>>4], B[k = l>>4]
+// [j = l&15]) ask each lane for the SAME value X[l&15 (+16)][k], so one
+// register per row block feeds both operands.  The k order is free as long
+// as A and B agree: lane (r = l&15, q = l>>4) loads float4 i of its rows at
+// columns i*16 + q*4 .. +3 (each row's 64 B per load instruction are
+// contiguous), and MFMA step (i, c) takes component c.
+// Per sample: 2 * KI float4 loads per lane, NT * 4 * KI MFMAs (NT = 1 when
+// F <= 16, 3 otherwise), the strict lower triangle stored from the C/D map
+// (col = l&15, row = (l>>4)*4 + reg).  HBM-bound: X read once, out written
+// once; the LDS-tiled VALU kernel above was LDS-read bound (8 ds_read_b128
+// per 64 FMAs).
+// ---------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(4))) float dot_f4;
+template <int KI, int NT>
+struct DotRows {
+  float4 a0[KI], a1[KI];
+};
+// Rows >= F are loaded from a clamped (valid) address and left as they are:
+// Gram entry (i, j) depends on rows i and j only, and entries with i or j >=
+// F are never stored.  No predicated loads: a branch per load made hipcc
+// fall back to vmcnt(0), which also waited for the prefetched next sample.
+template <int KI, int NT>
+__device__ __forceinline__ void dot_rows_load(DotRows<KI, NT>& v, const float* x, int64_t b, int F,
+                                              int r, int q) {
+  constexpr int D = KI * 16;
+  const float4* base = reinterpret_cast<const float4*>(x + b * F * (int64_t)D) + q;
+  const float4* p0 = base + (r < F ? r : F - 1) * (D / 4);
+#pragma unroll
+  for (int i = 0; i < KI; ++i) v.a0[i] = gld(p0 + i * 4);
+  if (NT > 1) {
+    const float4* p1 = base + (r + 16 < F ? r + 16 : F - 1) * (D / 4);
+#pragma unroll
+    for (int i = 0; i < KI; ++i) v.a1[i] = gld(p1 + i * 4);
+  }
+}
+template <int KI, int NT>
+__device__ __forceinline__ void dot_rows_gram(const DotRows<KI, NT>& v, float* __restrict__ out,
+                                              float* row, int64_t b, int F, int lane) {
+  dot_f4 c00 = {0.f, 0.f, 0.f, 0.f}, c10 = c00, c11 = c00;
+#pragma unroll
+  for (int i = 0; i < KI; ++i) {
+    const float p0[4] = {v.a0[i].x, v.a0[i].y, v.a0[i].z, v.a0[i].w};
+    const float p1[4] = {v.a1[i].x, v.a1[i].y, v.a1[i].z, v.a1[i].w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      c00 = __builtin_amdgcn_mfma_f32_16x16x4f32(p0[c], p0[c], c00, 0, 0, 0);
+      if (NT > 1) {
+        c10 = __builtin_amdgcn_mfma_f32_16x16x4f32(p1[c], p0[c], c10, 0, 0, 0);
+        c11 = __builtin_amdgcn_mfma_f32_16x16x4f32(p1[c], p1[c], c11, 0, 0, 0);
+      }
+    }
+  }
+  float* o = out + b * (int64_t)(F * (F - 1) / 2);
+  const int gj = lane & 15, q = lane >> 4;
+  // the C/D map scatters a lane's results over the sample's output row (4
+  // segments of <= 64 B per store instruction): the row is assembled in
+  // this wave's LDS slice and written out as contiguous 256-B instructions
+  // (the scattered dword stores cost ~25 % of the kernel).  LDS ops of one
+  // wave complete in order, so the reads see the writes and the next
+  // sample's writes land after these reads.
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int gi = q * 4 + e;
+    if (gi < F && gj < gi) row[gi * (gi - 1) / 2 + gj] = c00[e];
+    if (NT > 1) {
+      const int hi = gi + 16;
+      if (hi < F) {
+        row[hi * (hi - 1) / 2 + gj] = c10[e];
+        if (gj + 16 < hi) row[hi * (hi - 1) / 2 + gj + 16] = c11[e];
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  const int P = F * (F - 1) / 2;
+  for (int e = lane; e < P; e += 64) o[e] = row[e];   // (nontemporal: 201-206 vs 195 us)
+}
+// PF = false (default): one sample per wave, 40 VGPRs, so 8 waves per SIMD
+// overlap one another's loads and MFMAs.  PF = true (A/B): persistent waves
+// (grid sized to what is resident), each loading its next sample's rows
+// before the MFMAs of the current one (188 VGPRs, 2 waves per SIMD).
+template <int KI, int NT, bool PF>
+__global__ __launch_bounds__(256) void dot_mfma_kernel(const float* __restrict__ x, int64_t B,
+                                                       int F, float* __restrict__ out) {
+  __shared__ float rows_lds[4][512];   // one output row (<= 496 pairs) per wave
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  float* row = rows_lds[wave];
+  int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  if (b >= B) return;   // wave-uniform; no barriers below
+  DotRows<KI, NT> cur;
+  dot_rows_load<KI, NT>(cur, x, b, F, r, q);
+  if (!PF) {
+    dot_rows_gram<KI, NT>(cur, out, row, b, F, lane);
+    return;
+  }
+  const int64_t step = (int64_t)gridDim.x * 4;
+  for (;;) {
+    const int64_t nb = b + step;
+    if (nb >= B) {
+      dot_rows_gram<KI, NT>(cur, out, row, b, F, lane);
+      return;
+    }
+    DotRows<KI, NT> nxt;
+    dot_rows_load<KI, NT>(nxt, x, nb, F, r, q);
+    // keep the next sample's loads ahead of this sample's MFMAs (the
+    // scheduler otherwise sinks them below the MFMAs to shorten live ranges)
+    __builtin_amdgcn_sched_barrier(0);
+    dot_rows_gram<KI, NT>(cur, out, row, b, F, lane);
+    cur = nxt;
+    b = nb;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Dot interaction backward: dX[b,i,:] = sum_{j != i} S[i,j] X[b,j,:] with S
 // the symmetric completion of the pair grads (S[i,j] = S[j,i] = g[b, p(i,j)],
 // p(i,j) = i(i-1)/2 + j for i > j) -- the autodiff of DLRM's dot_op
@@ -1343,6 +1462,45 @@ int dr_dot_interaction(const float* x, int64_t batch, int fields, int dim, float
   const size_t lds = (size_t)fields * (dim + 1) * sizeof(float);
   DR_REQUIRE(lds <= 64 * 1024, DR_INVALID_ARGUMENT, "fields*dim too large for one block");
   if (batch == 0) return DR_OK;
+  // f32 MFMA path (dot_mfma_kernel): F <= 32, D in {16, 32, 64, 128}
+  static const bool dot_valu = getenv("DR_DOT_VALU") != nullptr;   // A/B: LDS-tiled VALU kernel
+  // DR_DOT_PF=1: persistent prefetching waves (A/B; measured slower in the
+  // DLRM step: 209 vs 196 us, profiles/r03_ab_dot_mfma.log)
+  static const bool dot_pf = getenv("DR_DOT_PF") && atoi(getenv("DR_DOT_PF")) != 0;
+  if (!dot_valu && fields <= 32 && (dim == 16 || dim == 32 || dim == 64 || dim == 128) &&
+      ((uintptr_t)x & 15) == 0) {
+    static const int per_cu = getenv("DR_DOT_BLOCKS_PER_CU") ? atoi(getenv("DR_DOT_BLOCKS_PER_CU")) : 3;
+    const int64_t all = ceil_div(batch, 4);
+    const unsigned grid = (unsigned)(dot_pf ? std::min<int64_t>(all, (int64_t)256 * std::max(1, per_cu)) : all);
+#define DR_DOT_MFMA2(KI, PF)                                                                    \
+  do {                                                                                          \
+    if (fields <= 16)                                                                           \
+      hipLaunchKernelGGL((dot_mfma_kernel<KI, 1, PF>), dim3(grid), dim3(256), 0, S(stream), x,   \
+                         batch, fields, out);                                                   \
+    else                                                                                        \
+      hipLaunchKernelGGL((dot_mfma_kernel<KI, 3, PF>), dim3(grid), dim3(256), 0, S(stream), x,   \
+                         batch, fields, out);                                                   \
+  } while (0)
+#define DR_DOT_MFMA(KI)        \
+  do {                         \
+    if (dot_pf)                \
+      DR_DOT_MFMA2(KI, true);  \
+    else                       \
+      DR_DOT_MFMA2(KI, false); \
+  } while (0)
+    if (dim == 16)
+      DR_DOT_MFMA(1);
+    else if (dim == 32)
+      DR_DOT_MFMA(2);
+    else if (dim == 64)
+      DR_DOT_MFMA(4);
+    else
+      DR_DOT_MFMA(8);
+#undef DR_DOT_MFMA
+#undef DR_DOT_MFMA2
+    DR_LAUNCH_CHECK();
+    return DR_OK;
+  }
   const int nb = (fields + 3) / 4;
   const size_t tlds = (size_t)DOT_WAVES * nb * 4 * (dim + 4) * sizeof(float);
   if (nb * (nb + 1) / 2 <= 32 && dim % 8 == 0 && ((uintptr_t)x & 15) == 0 && tlds <= 64 * 1024 &&

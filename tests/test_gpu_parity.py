@@ -876,9 +876,12 @@ def test_fm2_grad(ops, orc, F, D):
 
 
 @pytest.mark.parametrize("B,F,D", [(50, 27, 128), (9, 5, 16), (7, 2, 8), (5, 30, 64),
-                                   (6, 27, 12)])
+                                   (6, 27, 12), (33, 17, 32), (21, 16, 64), (11, 32, 128),
+                                   (13, 27, 16), (4, 24, 96)])
 def test_dot_interaction(ops, orc, B, F, D):
-    # tiled kernel: nb(nb+1)/2 <= 32 tiles, D % 8 == 0; others: per-pair kernel
+    # f32 MFMA kernel: F <= 32, D in {16, 32, 64, 128} (one or three 16x16
+    # blocks: F = 16 / 17 / 32 are the edges); LDS-tiled kernel: nb(nb+1)/2
+    # <= 32 tiles, D % 8 == 0 (D = 96); others: per-pair kernel
     rng = np.random.default_rng(37)
     x = rng.standard_normal((B, F, D)).astype(np.float32)
     out = H(ops.dot_interaction(T(x)))
