@@ -252,9 +252,31 @@ __device__ __forceinline__ void dot_rows_load(DotRows<KI, NT>& v, const float* x
     for (int i = 0; i < KI; ++i) v.a1[i] = gld(p1 + i * 4);
   }
 }
-template <int KI, int NT>
-__device__ __forceinline__ void dot_rows_gram(const DotRows<KI, NT>& v, float* __restrict__ out,
-                                              float* row, int64_t b, int F, int lane) {
+// One sample per wave, 40 VGPRs, so 8 waves per SIMD overlap one another's
+// loads and MFMAs (persistent waves prefetching their next sample, 188 VGPRs
+// at 2 waves per SIMD, measured slower: 209 vs 196 us in the DLRM step).
+// The C/D map scatters a lane's results over the sample's output row (4
+// segments of <= 64 B per store instruction): the row is assembled in the
+// wave's LDS slice and written out as contiguous 256-B instructions (the
+// scattered dword stores cost ~25 % of the kernel; nontemporal stores 201-206
+// vs 195 us).  LDS ops of one wave complete in order, so the reads see the
+// writes.
+// CAT: the DLRM top-MLP input instead (modelzoo/DLRM/train.py:211-226:
+// concat([dense_inputs, dot], 1), cast to bf16 under --bf16): row b of a
+// bf16 [B, ostride] matrix = bf16(X[b, 0, :]) | bf16(dot) | zeros up to
+// ostride (the MFMA tower's K padding), two values per lane and store.
+template <int KI, int NT, bool CAT>
+__global__ __launch_bounds__(256) void dot_mfma_kernel(const float* __restrict__ x, int64_t B,
+                                                       int F, void* __restrict__ out,
+                                                       int64_t ostride) {
+  constexpr int D = KI * 16;
+  __shared__ float rows_lds[4][CAT ? 640 : 512];   // (x0 |) the pairs (<= 496) per wave
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  if (b >= B) return;   // wave-uniform; no barriers below
+  DotRows<KI, NT> v;
+  dot_rows_load<KI, NT>(v, x, b, F, r, q);
   dot_f4 c00 = {0.f, 0.f, 0.f, 0.f}, c10 = c00, c11 = c00;
 #pragma unroll
   for (int i = 0; i < KI; ++i) {
@@ -269,64 +291,38 @@ __device__ __forceinline__ void dot_rows_gram(const DotRows<KI, NT>& v, float* _
       }
     }
   }
-  float* o = out + b * (int64_t)(F * (F - 1) / 2);
-  const int gj = lane & 15, q = lane >> 4;
-  // the C/D map scatters a lane's results over the sample's output row (4
-  // segments of <= 64 B per store instruction): the row is assembled in
-  // this wave's LDS slice and written out as contiguous 256-B instructions
-  // (the scattered dword stores cost ~25 % of the kernel).  LDS ops of one
-  // wave complete in order, so the reads see the writes and the next
-  // sample's writes land after these reads.
+  float* row = rows_lds[wave];
+  float* pr = row + (CAT ? D : 0);   // the pairs
+  if (CAT && r == 0) {               // lanes 0, 16, 32, 48 hold X[b, 0, :]
+#pragma unroll
+    for (int i = 0; i < KI; ++i) *reinterpret_cast<float4*>(row + i * 16 + q * 4) = v.a0[i];
+  }
+  const int gj = lane & 15;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int gi = q * 4 + e;
-    if (gi < F && gj < gi) row[gi * (gi - 1) / 2 + gj] = c00[e];
+    if (gi < F && gj < gi) pr[gi * (gi - 1) / 2 + gj] = c00[e];
     if (NT > 1) {
       const int hi = gi + 16;
       if (hi < F) {
-        row[hi * (hi - 1) / 2 + gj] = c10[e];
-        if (gj + 16 < hi) row[hi * (hi - 1) / 2 + gj + 16] = c11[e];
+        pr[hi * (hi - 1) / 2 + gj] = c10[e];
+        if (gj + 16 < hi) pr[hi * (hi - 1) / 2 + gj + 16] = c11[e];
       }
     }
   }
   __builtin_amdgcn_wave_barrier();
   const int P = F * (F - 1) / 2;
-  for (int e = lane; e < P; e += 64) o[e] = row[e];   // (nontemporal: 201-206 vs 195 us)
-}
-// PF = false (default): one sample per wave, 40 VGPRs, so 8 waves per SIMD
-// overlap one another's loads and MFMAs.  PF = true (A/B): persistent waves
-// (grid sized to what is resident), each loading its next sample's rows
-// before the MFMAs of the current one (188 VGPRs, 2 waves per SIMD).
-template <int KI, int NT, bool PF>
-__global__ __launch_bounds__(256) void dot_mfma_kernel(const float* __restrict__ x, int64_t B,
-                                                       int F, float* __restrict__ out) {
-  __shared__ float rows_lds[4][512];   // one output row (<= 496 pairs) per wave
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = lane & 15, q = lane >> 4;
-  float* row = rows_lds[wave];
-  int64_t b = (int64_t)blockIdx.x * 4 + wave;
-  if (b >= B) return;   // wave-uniform; no barriers below
-  DotRows<KI, NT> cur;
-  dot_rows_load<KI, NT>(cur, x, b, F, r, q);
-  if (!PF) {
-    dot_rows_gram<KI, NT>(cur, out, row, b, F, lane);
-    return;
-  }
-  const int64_t step = (int64_t)gridDim.x * 4;
-  for (;;) {
-    const int64_t nb = b + step;
-    if (nb >= B) {
-      dot_rows_gram<KI, NT>(cur, out, row, b, F, lane);
-      return;
+  if (!CAT) {
+    float* o = static_cast<float*>(out) + b * (int64_t)P;
+    for (int e = lane; e < P; e += 64) o[e] = row[e];
+  } else {
+    uint32_t* o = reinterpret_cast<uint32_t*>(static_cast<uint16_t*>(out) + b * ostride);
+    const int n = D + P;
+    for (int e2 = lane; e2 < ostride / 2; e2 += 64) {
+      const int e = 2 * e2;
+      const float lo = e < n ? row[e] : 0.f, hi = e + 1 < n ? row[e + 1] : 0.f;
+      o[e2] = (uint32_t)bf16_rne(lo) | ((uint32_t)bf16_rne(hi) << 16);
     }
-    DotRows<KI, NT> nxt;
-    dot_rows_load<KI, NT>(nxt, x, nb, F, r, q);
-    // keep the next sample's loads ahead of this sample's MFMAs (the
-    // scheduler otherwise sinks them below the MFMAs to shorten live ranges)
-    __builtin_amdgcn_sched_barrier(0);
-    dot_rows_gram<KI, NT>(cur, out, row, b, F, lane);
-    cur = nxt;
-    b = nb;
   }
 }
 
@@ -339,10 +335,16 @@ __global__ __launch_bounds__(256) void dot_mfma_kernel(const float* __restrict__
 // the column of X stays in registers (F float4), the sample's S sits in LDS
 // and is read as 16-B broadcasts.  HBM bound: X read + dX written once.
 // ---------------------------------------------------------------------------
-template <int FM>
+// CAT: the gradient arrives as the bf16 top-MLP input gradient [B, gstride]
+// of dot_mfma_kernel<CAT> (x0 | pairs | padding): the pair coefficients are
+// read from columns D.., and columns 0..D-1 (the concat's dense_inputs
+// slot, i.e. X[b, 0, :] itself) are added to dX[b, 0, :] after the sum --
+// the one fp32 add autograd does when the two uses of x0 meet.
+template <int FM, bool CAT = false>
 __global__ __launch_bounds__(256) void dot_grad_kernel(const float* __restrict__ x,
-                                                       const float* __restrict__ g, int64_t B,
-                                                       int F, int D, float* __restrict__ dx) {
+                                                       const void* __restrict__ gv, int64_t B,
+                                                       int F, int D, float* __restrict__ dx,
+                                                       int64_t gstride = 0) {
   // S of the half-wave's sample, zero-padded to FM x FM (row i = the
   // coefficients of dX[i]): no branches in the FMA loop, 16-B LDS reads.
   __shared__ __attribute__((aligned(16))) float ss_all[8][FM * FM];
@@ -351,12 +353,15 @@ __global__ __launch_bounds__(256) void dot_grad_kernel(const float* __restrict__
   float* ss = ss_all[half];
   const int64_t b = (int64_t)blockIdx.x * 8 + half;
   const bool live = b < B;
-  const float* gb = g + b * (int64_t)P;
+  const float* gb = static_cast<const float*>(gv) + b * (int64_t)P;
+  const uint16_t* gh = static_cast<const uint16_t*>(gv) + b * gstride;   // CAT
   for (int e = hl; e < FM * FM; e += 32) {
     const int i = e / FM, j = e - i * FM;
     float v = 0.f;
-    if (live && i < F && j < F && i != j)
-      v = i > j ? gb[i * (i - 1) / 2 + j] : gb[j * (j - 1) / 2 + i];
+    if (live && i < F && j < F && i != j) {
+      const int p = i > j ? i * (i - 1) / 2 + j : j * (j - 1) / 2 + i;
+      v = CAT ? bf16_to_f32(gh[D + p]) : gb[p];
+    }
     ss[e] = v;
   }
   __syncthreads();
@@ -384,6 +389,14 @@ __global__ __launch_bounds__(256) void dot_grad_kernel(const float* __restrict__
           acc.z = fmaf(sj[q], xv.z, acc.z);
           acc.w = fmaf(sj[q], xv.w, acc.w);
         }
+      }
+      if (CAT && i == 0) {
+        const uint2 h = *reinterpret_cast<const uint2*>(gh + c * 4);
+        const float2 a = bf16x2_to_f2(h.x), d = bf16x2_to_f2(h.y);
+        acc.x += a.x;
+        acc.y += a.y;
+        acc.z += d.x;
+        acc.w += d.y;
       }
       nt_store(acc, ob + i * D4 + c);
     }
@@ -1416,6 +1429,37 @@ __global__ void crossnet_db_kernel(const float* __restrict__ dbp, int64_t nblk, 
 
 }  // namespace dr
 
+namespace dr {
+static bool dot_mfma_ok(int fields, int dim) {
+  return fields >= 2 && fields <= 32 && (dim == 16 || dim == 32 || dim == 64 || dim == 128);
+}
+template <bool CAT>
+static int dot_mfma_launch(const float* x, int64_t batch, int fields, int dim, void* out,
+                           int64_t ostride, hipStream_t st) {
+  const unsigned grid = (unsigned)ceil_div(batch, 4);
+#define DR_DOT_MFMA(KI)                                                                         \
+  do {                                                                                          \
+    if (fields <= 16)                                                                           \
+      hipLaunchKernelGGL((dot_mfma_kernel<KI, 1, CAT>), dim3(grid), dim3(256), 0, st, x, batch,  \
+                         fields, out, ostride);                                                 \
+    else                                                                                        \
+      hipLaunchKernelGGL((dot_mfma_kernel<KI, 3, CAT>), dim3(grid), dim3(256), 0, st, x, batch,  \
+                         fields, out, ostride);                                                 \
+  } while (0)
+  if (dim == 16)
+    DR_DOT_MFMA(1);
+  else if (dim == 32)
+    DR_DOT_MFMA(2);
+  else if (dim == 64)
+    DR_DOT_MFMA(4);
+  else
+    DR_DOT_MFMA(8);
+#undef DR_DOT_MFMA
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+}  // namespace dr
+
 extern "C" {
 
 int dr_fm2(const float* emb, int64_t batch, int fields, int dim, float* out, void* stream) {
@@ -1464,43 +1508,8 @@ int dr_dot_interaction(const float* x, int64_t batch, int fields, int dim, float
   if (batch == 0) return DR_OK;
   // f32 MFMA path (dot_mfma_kernel): F <= 32, D in {16, 32, 64, 128}
   static const bool dot_valu = getenv("DR_DOT_VALU") != nullptr;   // A/B: LDS-tiled VALU kernel
-  // DR_DOT_PF=1: persistent prefetching waves (A/B; measured slower in the
-  // DLRM step: 209 vs 196 us, profiles/r03_ab_dot_mfma.log)
-  static const bool dot_pf = getenv("DR_DOT_PF") && atoi(getenv("DR_DOT_PF")) != 0;
-  if (!dot_valu && fields <= 32 && (dim == 16 || dim == 32 || dim == 64 || dim == 128) &&
-      ((uintptr_t)x & 15) == 0) {
-    static const int per_cu = getenv("DR_DOT_BLOCKS_PER_CU") ? atoi(getenv("DR_DOT_BLOCKS_PER_CU")) : 3;
-    const int64_t all = ceil_div(batch, 4);
-    const unsigned grid = (unsigned)(dot_pf ? std::min<int64_t>(all, (int64_t)256 * std::max(1, per_cu)) : all);
-#define DR_DOT_MFMA2(KI, PF)                                                                    \
-  do {                                                                                          \
-    if (fields <= 16)                                                                           \
-      hipLaunchKernelGGL((dot_mfma_kernel<KI, 1, PF>), dim3(grid), dim3(256), 0, S(stream), x,   \
-                         batch, fields, out);                                                   \
-    else                                                                                        \
-      hipLaunchKernelGGL((dot_mfma_kernel<KI, 3, PF>), dim3(grid), dim3(256), 0, S(stream), x,   \
-                         batch, fields, out);                                                   \
-  } while (0)
-#define DR_DOT_MFMA(KI)        \
-  do {                         \
-    if (dot_pf)                \
-      DR_DOT_MFMA2(KI, true);  \
-    else                       \
-      DR_DOT_MFMA2(KI, false); \
-  } while (0)
-    if (dim == 16)
-      DR_DOT_MFMA(1);
-    else if (dim == 32)
-      DR_DOT_MFMA(2);
-    else if (dim == 64)
-      DR_DOT_MFMA(4);
-    else
-      DR_DOT_MFMA(8);
-#undef DR_DOT_MFMA
-#undef DR_DOT_MFMA2
-    DR_LAUNCH_CHECK();
-    return DR_OK;
-  }
+  if (!dot_valu && dot_mfma_ok(fields, dim) && ((uintptr_t)x & 15) == 0)
+    return dot_mfma_launch<false>(x, batch, fields, dim, out, 0, S(stream));
   const int nb = (fields + 3) / 4;
   const size_t tlds = (size_t)DOT_WAVES * nb * 4 * (dim + 4) * sizeof(float);
   if (nb * (nb + 1) / 2 <= 32 && dim % 8 == 0 && ((uintptr_t)x & 15) == 0 && tlds <= 64 * 1024 &&
@@ -1537,6 +1546,45 @@ int dr_dot_interaction_grad(const float* x, const float* top_grad, int64_t batch
   else
     hipLaunchKernelGGL(dot_grad_kernel<32>, dim3(grid), dim3(256), 0, S(stream), x, top_grad,
                        batch, fields, dim, grad_x);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_dot_interaction_concat_bf16(const float* x, int64_t batch, int fields, int dim,
+                                   uint16_t* out, int64_t out_stride, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && dot_mfma_ok(fields, dim), DR_INVALID_ARGUMENT,
+             "dr_dot_interaction_concat_bf16: need 2 <= fields <= 32, dim in {16, 32, 64, 128}");
+  DR_REQUIRE(out_stride % 2 == 0 && out_stride >= dim + (int64_t)fields * (fields - 1) / 2,
+             DR_INVALID_ARGUMENT, "out_stride must be even and >= dim + fields*(fields-1)/2");
+  DR_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 3) == 0, DR_INVALID_ARGUMENT,
+             "x must be 16-B and out 4-B aligned");
+  if (batch == 0) return DR_OK;
+  return dot_mfma_launch<true>(x, batch, fields, dim, out, out_stride, S(stream));
+}
+
+int dr_dot_interaction_concat_grad_bf16(const float* x, const uint16_t* grad, int64_t grad_stride,
+                                        int64_t batch, int fields, int dim, float* grad_x,
+                                        void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && fields > 1 && fields <= 32 && dim > 0 && dim % 4 == 0,
+             DR_INVALID_ARGUMENT,
+             "dr_dot_interaction_concat_grad_bf16: need 2 <= fields <= 32, dim %% 4 == 0");
+  DR_REQUIRE(grad_stride >= dim + (int64_t)fields * (fields - 1) / 2 && grad_stride % 4 == 0,
+             DR_INVALID_ARGUMENT, "grad_stride must be a multiple of 4 and >= dim + pairs");
+  DR_REQUIRE((((uintptr_t)x) | ((uintptr_t)grad_x)) % 16 == 0 && ((uintptr_t)grad & 7) == 0,
+             DR_INVALID_ARGUMENT, "x / grad_x must be 16-B and grad 8-B aligned");
+  if (batch == 0) return DR_OK;
+  const unsigned grid = (unsigned)ceil_div(batch, 8);
+  if (fields <= 16)
+    hipLaunchKernelGGL((dot_grad_kernel<16, true>), dim3(grid), dim3(256), 0, S(stream), x, grad,
+                       batch, fields, dim, grad_x, grad_stride);
+  else if (fields <= 28)
+    hipLaunchKernelGGL((dot_grad_kernel<28, true>), dim3(grid), dim3(256), 0, S(stream), x, grad,
+                       batch, fields, dim, grad_x, grad_stride);
+  else
+    hipLaunchKernelGGL((dot_grad_kernel<32, true>), dim3(grid), dim3(256), 0, S(stream), x, grad,
+                       batch, fields, dim, grad_x, grad_stride);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

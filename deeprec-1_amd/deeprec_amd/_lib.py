@@ -226,6 +226,8 @@ SIGNATURES = {
     "dr_fm2_grad": (_I32, [_P, _P, _I64, _I32, _I32, _P, _P]),
     "dr_dot_interaction": (_I32, [_P, _I64, _I32, _I32, _P, _P]),
     "dr_dot_interaction_grad": (_I32, [_P, _P, _I64, _I32, _I32, _P, _P]),
+    "dr_dot_interaction_concat_bf16": (_I32, [_P, _I64, _I32, _I32, _P, _I64, _P]),
+    "dr_dot_interaction_concat_grad_bf16": (_I32, [_P, _P, _I64, _I64, _I32, _I32, _P, _P]),
     "dr_crossnet_layer_bf16": (_I32, [_P, _P, _P, _P, _I64, _I32, _P, _P]),
     "dr_crossnet_forward_bf16": (_I32, [_P, _P, _P, _P, _I64, _I32, _P, _P, _P]),
     "dr_crossnet_backward_workspace_size": (_SZ, [_I64, _I32]),

@@ -24,6 +24,8 @@ north_star asks.
 Inputs are one-hot ids ([T, B] int64, Criteo hotness 1) and dense features
 [B, 13] fp32.
 """
+import os
+
 import torch
 
 from . import ops
@@ -42,6 +44,24 @@ class DotInteraction(torch.autograd.Function):
     def backward(ctx, g):
         (x,) = ctx.saved_tensors
         return ops.dot_interaction_grad(x, g)
+
+
+class DotConcatBf16(torch.autograd.Function):
+    """DLRM's dot layer, concat and --bf16 cast as one node (train.py:211-226):
+    X [B, F, D] with X[:, 0] = the bottom-MLP output -> the zero-padded bf16
+    top-MLP input [B, cols] (dr_dot_interaction_concat_bf16[_grad])."""
+
+    @staticmethod
+    def forward(ctx, x, cols):
+        ctx.save_for_backward(x)
+        return ops.dot_interaction_concat_bf16(x, cols)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        if g.stride(1) != 1:
+            g = g.contiguous()
+        return ops.dot_interaction_concat_grad_bf16(x, g.to(torch.bfloat16)), None
 
 
 class FMSecondOrder(torch.autograd.Function):
@@ -162,14 +182,26 @@ class _MfmaMLP(torch.nn.Module):
         self.sizes = list(sizes)
         self.last_act = last_act
 
-    def forward(self, x):
+    @property
+    def kp(self):
+        """The zero-padded input width the MFMA tower takes."""
+        return (self.sizes[0] + 63) // 64 * 64
+
+    def mfma_ok(self, batch):
         lins = [m for m in self.net if isinstance(m, torch.nn.Linear)]
+        return batch % 512 == 0 and all(l.out_features % 64 == 0 for l in lins)
+
+    def forward(self, x):
         B, K = x.shape
-        if B % 512 or any(l.out_features % 64 for l in lins):
+        if not self.mfma_ok(B):
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 return self.net(x).float()
-        Kp = (K + 63) // 64 * 64
-        h = torch.nn.functional.pad(x.to(torch.bfloat16), (0, Kp - K))
+        h = torch.nn.functional.pad(x.to(torch.bfloat16), (0, self.kp - K))
+        return self.forward_padded(h)
+
+    def forward_padded(self, h):
+        """The tower on an input already in bf16 and zero-padded to kp columns."""
+        lins = [m for m in self.net if isinstance(m, torch.nn.Linear)]
         y = _MfmaTowerFn.apply(h, self.last_act, *[l.weight for l in lins],
                                *[l.bias for l in lins])
         return y.float()
@@ -212,9 +244,19 @@ class DLRM(torch.nn.Module):
         self.last = torch.nn.Linear(mlp_top[-1], 1)
         self.lookup = _OneHotLookup(self.evs)
 
+    # --bf16 with MFMA towers: dot + concat + cast as one kernel writing the
+    # padded bf16 top-MLP input (DotConcatBf16); False (or the A/B switch
+    # DR_DLRM_FUSE_DOT_CONCAT=0) = the composed dot -> cat -> cast -> pad
+    fuse_dot_concat = os.environ.get("DR_DLRM_FUSE_DOT_CONCAT", "1") != "0"
+
     def forward(self, dense, ids):
         x0 = self.bf16(self.bottom, dense)
         X = self.lookup.stack(x0, ids)                             # [B, 1+T, D], no concat copy
+        if (self.fuse_dot_concat and self.bf16.on and isinstance(self.top, _MfmaMLP)
+                and self.top.mfma_ok(X.shape[0]) and X.shape[1] <= 32
+                and X.shape[2] in (16, 32, 64, 128)):
+            net = self.top.forward_padded(DotConcatBf16.apply(X, self.top.kp))
+            return torch.sigmoid(self.bf16(self.last, net)).squeeze(1)
         z = DotInteraction.apply(X)
         net = self.bf16(self.top, torch.cat([x0, z], 1))
         return torch.sigmoid(self.bf16(self.last, net)).squeeze(1)

@@ -525,6 +525,34 @@ def dot_interaction_grad(x, top_grad):
     return out
 
 
+def dot_interaction_concat_bf16(x, out_cols):
+    """DLRM dot layer + concat + --bf16 cast (modelzoo/DLRM/train.py:211-226):
+    x [B, F, D] fp32 with x[:, 0] = dense_inputs -> bf16 [B, out_cols] =
+    x[:, 0] | dot_interaction(x) | zero padding (dr_dot_interaction_concat_bf16)."""
+    dev = _dev(x)
+    x = _c(x, torch.float32)
+    B, F, D = x.shape
+    out = torch.empty((B, out_cols), dtype=torch.bfloat16, device=dev)
+    check(lib().dr_dot_interaction_concat_bf16(ptr(x), B, F, D, ptr(out), out_cols,
+                                               stream_handle(dev)))
+    _post(dev)
+    return out
+
+
+def dot_interaction_concat_grad_bf16(x, grad):
+    """Backward of dot_interaction_concat_bf16 from the bf16 [B, cols] gradient."""
+    dev = _dev(x)
+    x = _c(x, torch.float32)
+    if grad.dtype != torch.bfloat16 or grad.stride(1) != 1:
+        raise ValueError("grad must be bf16 with unit column stride")
+    B, F, D = x.shape
+    out = torch.empty_like(x)
+    check(lib().dr_dot_interaction_concat_grad_bf16(ptr(x), ptr(grad), grad.stride(0), B, F, D,
+                                                    ptr(out), stream_handle(dev)))
+    _post(dev)
+    return out
+
+
 def crossnet_layer(x0, xl, weight, bias=None):
     """DCN-v2 cross layer x0 * (xl W^T + b) + xl, bf16 MFMA, fp32 accumulate.
 

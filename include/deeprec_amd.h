@@ -837,6 +837,19 @@ int dr_dot_interaction(const float* x, int64_t batch, int fields, int dim, float
 /* top_grad [B, F(F-1)/2] (autodiff of the reference's matmul + mask).       */
 int dr_dot_interaction_grad(const float* x, const float* top_grad, int64_t batch, int fields,
                             int dim, float* grad_x, void* stream);
+/* The DLRM dot layer with its concat and --bf16 cast fused                   */
+/* (modelzoo/DLRM/train.py:211-226: concat([dense_inputs, dot_op(stack)], 1), */
+/* then tf.cast(net, bf16)), X[b, 0, :] = dense_inputs: row b of out [B,      */
+/* out_stride] bf16 = bf16(X[b,0,:]) | bf16(dot) | zeros to out_stride (the   */
+/* top MLP's K padding).  2 <= fields <= 32, dim in {16, 32, 64, 128},        */
+/* out_stride even.  Same fp32 products as dr_dot_interaction, one RNE.      */
+int dr_dot_interaction_concat_bf16(const float* x, int64_t batch, int fields, int dim,
+                                   uint16_t* out, int64_t out_stride, void* stream);
+/* Its backward from the bf16 gradient of that matrix: grad_x = S X + (the     */
+/* dense_inputs columns 0..dim-1 added to row 0), S from columns dim...       */
+int dr_dot_interaction_concat_grad_bf16(const float* x, const uint16_t* grad, int64_t grad_stride,
+                                        int64_t batch, int fields, int dim, float* grad_x,
+                                        void* stream);
 /* DCN-v2 cross layer (absent in the reference): out = x0 * (xl W^T + b) + xl */
 /* x0/xl/out [B,d] bf16 (uint16 storage), W [d,d] bf16 row-major (out,in),   */
 /* b [d] f32; bf16 MFMA with fp32 accumulation.                              */

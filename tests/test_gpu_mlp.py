@@ -169,3 +169,58 @@ def test_dlrm_bf16_step_on_mfma_towers(dr):
         assert p.grad is not None and torch.isfinite(p.grad).all()
     for ev in evs:
         ev.pending_grads.clear()
+
+
+@pytest.mark.parametrize("B,F,D,cols", [(300, 27, 128, 512), (64, 5, 16, 64), (130, 17, 32, 200),
+                                        (77, 32, 64, 640), (9, 16, 128, 256)])
+def test_dot_concat_bf16_equals_composed(dr, B, F, D, cols):
+    """dr_dot_interaction_concat_bf16 = cat([X[:, 0], dot(X)], 1).to(bf16),
+    zero-padded to cols (train.py:211-226), bit for bit; its backward =
+    dot_interaction_grad of the pair columns plus the dense columns added to
+    dX[:, 0] (autograd's sum of x0's two uses), bit for bit."""
+    from deeprec_amd import ops
+    g = torch.Generator(device=DEV)
+    g.manual_seed(B + F + D)
+    x = torch.randn((B, F, D), generator=g, device=DEV)
+    P = F * (F - 1) // 2
+    got = ops.dot_interaction_concat_bf16(x, cols)
+    ref = torch.zeros((B, cols), dtype=torch.bfloat16, device=DEV)
+    ref[:, :D + P] = torch.cat([x[:, 0], ops.dot_interaction(x)], 1).to(torch.bfloat16)
+    assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+    gr = torch.randn((B, cols), generator=g, device=DEV).to(torch.bfloat16)
+    dx = ops.dot_interaction_concat_grad_bf16(x, gr)
+    want = ops.dot_interaction_grad(x, gr[:, D:D + P].float())
+    want[:, 0] = want[:, 0] + gr[:, :D].float()
+    assert torch.equal(dx, want)
+
+
+def test_dlrm_bf16_fused_dot_concat_matches_composed(dr):
+    """DLRM --bf16 with the fused dot + concat + cast node gives the same
+    prediction, dense gradients and queued EV gradients as the composed
+    dot -> cat -> cast -> pad path on the same weights and inputs."""
+    from deeprec_amd import modelzoo as mz
+    torch.manual_seed(9)
+    T, D, B = 26, 128, 1024
+    evs = [dr.EmbeddingVariable("dlrm_fdc_%d" % t, D, 0.01, device=DEV) for t in range(T)]
+    model = mz.DLRM(evs, 13, (64,), (128, 64), bf16=True).to(DEV)
+    dense = torch.rand((B, 13), device=DEV)
+    ids = torch.randint(0, 5000, (T, B), device=DEV)
+    runs = []
+    for fuse in (True, False):
+        model.fuse_dot_concat = fuse
+        model.zero_grad(set_to_none=True)
+        out = model(dense, ids)
+        out.sum().backward()
+        sl = [ev.pending_grads[-1] for ev in evs]
+        nv = [s.indices.numel() if s.num_valid is None else int(s.num_valid.item()) for s in sl]
+        runs.append((out.detach().clone(), [p.grad.clone() for p in model.parameters()],
+                     [s.values[:n].clone() for s, n in zip(sl, nv)],
+                     [s.indices[:n].clone() for s, n in zip(sl, nv)]))
+        for ev in evs:
+            ev.pending_grads.clear()
+    (o1, g1, v1, i1), (o2, g2, v2, i2) = runs
+    assert torch.equal(o1, o2)
+    for a, b in zip(g1, g2):
+        assert torch.equal(a, b)
+    for a, b, c, d in zip(v1, v2, i1, i2):
+        assert torch.equal(c, d) and torch.equal(a, b)
