@@ -235,7 +235,8 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const uint16_t* __r
                                                              int64_t rows, int64_t cols,
                                                              int64_t ld_in,
                                                              uint16_t* __restrict__ out,
-                                                             int64_t ld_out) {
+                                                             int64_t ld_out,
+                                                             float* __restrict__ colsum) {
   __shared__ uint16_t t[64][66];
   const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
   const int tid = threadIdx.x;
@@ -257,11 +258,23 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const uint16_t* __r
   for (int h = 0; h < 2; ++h) {
     const int v = tid + h * 256;  // output row c = v / 8 (an input column), rows chunk v % 8
     const int c = v >> 3, rc = (v & 7) * 8;
-    if (c0 + c >= cols || r0 + rc >= rows) continue;
     mu32x4 o;
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       o[e] = (uint32_t)t[rc + 2 * e][c] | ((uint32_t)t[rc + 2 * e + 1][c] << 16);
+    if (colsum) {
+      // column c's sum over this tile's 64 rows (rows past the end are 0):
+      // 8 rows in order per lane, then the 8 lanes of the column (v & 7 =
+      // consecutive lanes) by a fixed xor butterfly -- deterministic
+      float sum = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sum += bf16_to_f32(t[rc + e][c]);
+      sum += __shfl_xor(sum, 1, 64);
+      sum += __shfl_xor(sum, 2, 64);
+      sum += __shfl_xor(sum, 4, 64);
+      if ((v & 7) == 0 && c0 + c < cols) colsum[(int64_t)blockIdx.y * cols + c0 + c] = sum;
+    }
+    if (c0 + c >= cols || r0 + rc >= rows) continue;
     *reinterpret_cast<mu32x4*>(out + (c0 + c) * ld_out + r0 + rc) = o;
   }
 }
@@ -335,6 +348,11 @@ int dr_gemm_nt_bf16(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t l
 
 int dr_transpose_bf16(const uint16_t* in, int64_t rows, int64_t cols, int64_t ld_in,
                       uint16_t* out, int64_t ld_out, void* stream) {
+  return dr_transpose_bf16_colsum(in, rows, cols, ld_in, out, ld_out, nullptr, stream);
+}
+
+int dr_transpose_bf16_colsum(const uint16_t* in, int64_t rows, int64_t cols, int64_t ld_in,
+                             uint16_t* out, int64_t ld_out, float* col_partials, void* stream) {
   using namespace dr;
   DR_REQUIRE(in && out && rows >= 0 && cols >= 0, DR_INVALID_ARGUMENT, "bad argument");
   DR_REQUIRE(rows % 8 == 0 && cols % 8 == 0 && ld_in % 8 == 0 && ld_out % 8 == 0 &&
@@ -345,7 +363,7 @@ int dr_transpose_bf16(const uint16_t* in, int64_t rows, int64_t cols, int64_t ld
   if (rows == 0 || cols == 0) return DR_OK;
   const dim3 grid((unsigned)ceil_div(cols, 64), (unsigned)ceil_div(rows, 64));
   hipLaunchKernelGGL(transpose_bf16_kernel, grid, dim3(256), 0, S(stream), in, rows, cols, ld_in,
-                     out, ld_out);
+                     out, ld_out, col_partials);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

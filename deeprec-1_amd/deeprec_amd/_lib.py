@@ -237,6 +237,7 @@ SIGNATURES = {
     "dr_gemm_nt_bf16_ex": (_I32, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I32, _P, _I64, _P,
                                   _I64, _I32, _I32, _P, _SZ, _P]),
     "dr_transpose_bf16": (_I32, [_P, _I64, _I64, _I64, _P, _I64, _P]),
+    "dr_transpose_bf16_colsum": (_I32, [_P, _I64, _I64, _I64, _P, _I64, _P, _P]),
     "dr_crossnet_backward_elem_bf16": (_I32, [_P, _P, _P, _P, _P, _P, _P, _I64, _I32, _P, _SZ,
                                               _P]),
     "dr_din_attention_input": (_I32, [_P, _P, _I64, _I64, _I32, _P, _P]),

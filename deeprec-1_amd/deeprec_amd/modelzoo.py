@@ -117,7 +117,8 @@ class _MfmaTowerFn(torch.autograd.Function):
     (dr_gemm_nt_bf16[_ex]): layer l computes y_l = act(h_l W_l^T + b_l),
     bf16 operands, fp32 accumulate, bf16 out, h_0 = the zero-padded input
     (Kp % 64 == 0), fp32 master weights (the reference's keep_weights).
-    Backward, layer by layer from the top: db_l = sum of g_l (fp32), dW_l =
+    Backward, layer by layer from the top: db_l = sum of g_l (fp32, from the
+    per-tile column sums the transpose of g_l writes), dW_l =
     g_l^T h_l (both operands transposed, then a split-K GEMM over the batch:
     its output is only N_l x K_l), and the input gradient g_{l-1} = g_l W_l
     with the layer below's ReLU mask applied in the GEMM's epilogue (aux =
@@ -155,10 +156,11 @@ class _MfmaTowerFn(torch.autograd.Function):
         for l in reversed(range(L)):
             x = hs[l]
             N, Kp = g.shape[1], x.shape[1]
-            dbs[l] = g.sum(0, dtype=torch.float32)
             tiles = ((N + 127) // 128) * ((Kp + 127) // 128)
             split = max(1, min(64, 512 // tiles, B // (64 * 8)))
-            dw = ops.gemm_nt(ops.transpose_bf16(g), ops.transpose_bf16(x), out_fp32=True,
+            # db from the column partials the g transpose writes (no extra pass over g)
+            gt, dbs[l] = ops.transpose_bf16(g, colsum=True)
+            dw = ops.gemm_nt(gt, ops.transpose_bf16(x), out_fp32=True,
                              split_k=split)                          # [N, Kp] fp32
             dws[l] = dw[:, :ctx.ks[l]]
             if l > 0 or ctx.needs_input_grad[0]:

@@ -633,16 +633,25 @@ def gemm_nt(a, b, bias=None, act=ACT_NONE, out_fp32=False, split_k=1, out=None, 
     return out
 
 
-def transpose_bf16(x):
-    """dr_transpose_bf16: [R, C] bf16 (unit column stride) -> contiguous [C, R]."""
+def transpose_bf16(x, colsum=False):
+    """dr_transpose_bf16: [R, C] bf16 (unit column stride) -> contiguous [C, R].
+    colsum=True (dr_transpose_bf16_colsum): also the fp32 column sums of x,
+    from per-64-row-tile partials summed in tile order; returns (out, sums)."""
     dev = _dev(x)
     R, Cc = x.shape
     if x.dtype != torch.bfloat16 or x.stride(1) != 1:
         raise ValueError("transpose_bf16 needs a bf16 matrix with unit column stride")
     out = torch.empty((Cc, R), dtype=torch.bfloat16, device=dev)
-    check(lib().dr_transpose_bf16(ptr(x), R, Cc, x.stride(0), ptr(out), R, stream_handle(dev)))
+    if not colsum:
+        check(lib().dr_transpose_bf16(ptr(x), R, Cc, x.stride(0), ptr(out), R,
+                                      stream_handle(dev)))
+        _post(dev)
+        return out
+    part = torch.empty(((R + 63) // 64, Cc), dtype=torch.float32, device=dev)
+    check(lib().dr_transpose_bf16_colsum(ptr(x), R, Cc, x.stride(0), ptr(out), R, ptr(part),
+                                         stream_handle(dev)))
     _post(dev)
-    return out
+    return out, part.sum(0)
 
 
 def crossnet_backward_elem(g, x0, lin, acc=None):

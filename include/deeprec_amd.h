@@ -894,6 +894,12 @@ int dr_gemm_nt_bf16_ex(const uint16_t* A, int64_t lda, const uint16_t* B, int64_
 /* out[c][r] = in[r][c], bf16; rows, cols and strides multiples of 8.        */
 int dr_transpose_bf16(const uint16_t* in, int64_t rows, int64_t cols, int64_t ld_in,
                       uint16_t* out, int64_t ld_out, void* stream);
+/* Same, also writing col_partials [ceil(rows/64), cols] fp32: each 64-row   */
+/* tile's column sums (8 rows in order, then a fixed butterfly), so a layer's */
+/* bias gradient db = col_partials summed over tiles comes with the dW       */
+/* operand transpose instead of another pass over g.                         */
+int dr_transpose_bf16_colsum(const uint16_t* in, int64_t rows, int64_t cols, int64_t ld_in,
+                             uint16_t* out, int64_t ld_out, float* col_partials, void* stream);
 /* Same layer, also writing lin_out = xl W^T + b (bf16, nullable; needs      */
 /* d % 64 == 0) for the backward pass.  d % 64 == 0 selects the pipelined    */
 /* kernel (global_load_lds staging, double-buffered K steps of 64).          */

@@ -86,6 +86,28 @@ def test_transpose_bf16_exact(dr):
     assert torch.equal(ops.transpose_bf16(y), y.t().contiguous())
 
 
+@pytest.mark.parametrize("R,C", [(1000, 520), (65536, 512), (64, 8), (136, 72)])
+def test_transpose_bf16_colsum(dr, R, C):
+    """The transpose is unchanged and the column sums (per 64-row tile, then
+    over tiles) equal the fp64 sum of the bf16 values within fp32 rounding,
+    and are bit-identical run to run."""
+    from deeprec_amd import ops
+    g = torch.Generator(device=DEV)
+    g.manual_seed(R + C)
+    x = torch.randn((R, C), generator=g, device=DEV).to(torch.bfloat16)
+    t, s = ops.transpose_bf16(x, colsum=True)
+    assert torch.equal(t, x.t().contiguous())
+    ref = x.double().sum(0)
+    tol = 1e-6 * x.double().abs().sum(0) + 1e-6
+    assert ((s.double() - ref).abs() <= tol).all()
+    t2, s2 = ops.transpose_bf16(x, colsum=True)
+    assert torch.equal(s, s2)
+    y = x[:, 8:C] if C > 8 else x
+    ty, sy = ops.transpose_bf16(y, colsum=True)
+    assert torch.equal(ty, y.t().contiguous())
+    assert ((sy.double() - y.double().sum(0)).abs() <= 1e-6 * y.double().abs().sum(0) + 1e-6).all()
+
+
 def test_gemm_nt_refuses_bad_shapes(dr):
     from deeprec_amd import ops
     a = torch.zeros((64, 100), device=DEV, dtype=torch.bfloat16)
