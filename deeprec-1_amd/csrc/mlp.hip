@@ -279,6 +279,107 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const uint16_t* __r
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// The DLRM output layer on top of the bf16 top MLP (modelzoo/DLRM/train.py:
+// 241-249 under --bf16: dense(units=1) in bf16, then sigmoid): a GEMV with
+// N = 1 that a library GEMM runs as three kernels (forward, dx, and a
+// K = 65 536 dW on few workgroups: 15 + 19 + 70 us per DLRM step) plus the
+// casts around them and the top layer's ReLU-mask multiply.
+//   forward  z[b] = bf16( sum_k h[b,k] * bf16(w[k]) + bias )   (fp32 sum)
+//   backward with gz = bf16(dL/dz):
+//            dh[b,k] = h[b,k] > 0 ? bf16(gz[b] * bf16(w[k])) : 0   (the
+//                      top layer's ReLU derivative applied in the same pass)
+//            dw_part[blk][k] = sum over the block's rows of gz[b] * h[b,k]
+//            db_part[blk]    = sum over the block's rows of gz[b]
+// K in {64, 128, 256, 512}: L = K / 8 lanes per row, 8 bf16 per lane; every
+// sum is in a fixed order (8 columns per lane, then an xor butterfly; rows
+// of a block in a fixed lane / LDS order), so results are deterministic.
+// ---------------------------------------------------------------------------
+template <int L>
+__global__ __launch_bounds__(256) void head_fwd_kernel(const uint16_t* __restrict__ h, int64_t ldh,
+                                                       int64_t B, const uint16_t* __restrict__ w,
+                                                       const float* __restrict__ bias,
+                                                       float* __restrict__ z) {
+  constexpr int RPB = 256 / L;  // rows per block
+  const int tid = threadIdx.x;
+  const int lc = tid % L;
+  const int64_t b = (int64_t)blockIdx.x * RPB + tid / L;
+  const bool ok = b < B;
+  const mu32x4 hv = *reinterpret_cast<const mu32x4*>(h + (ok ? b : 0) * ldh + lc * 8);
+  const mu32x4 wv = *reinterpret_cast<const mu32x4*>(w + lc * 8);
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float2 a = bf16x2_to_f2(hv[e]), c = bf16x2_to_f2(wv[e]);
+    s = fmaf(a.x, c.x, s);
+    s = fmaf(a.y, c.y, s);
+  }
+#pragma unroll
+  for (int m = 1; m < L; m <<= 1) s += __shfl_xor(s, m, 64);
+  if (ok && lc == 0) z[b] = bf16_to_f32(bf16_rne(bias ? s + *bias : s));
+}
+
+template <int L>
+__global__ __launch_bounds__(256) void head_bwd_kernel(const uint16_t* __restrict__ h, int64_t ldh,
+                                                       int64_t B, const uint16_t* __restrict__ w,
+                                                       const float* __restrict__ gz,
+                                                       uint16_t* __restrict__ dh, int64_t lddh,
+                                                       int rows_per_block,
+                                                       float* __restrict__ dw_part,
+                                                       float* __restrict__ db_part) {
+  constexpr int RPS = 256 / L;  // rows per sweep of the block
+  constexpr int K = L * 8;
+  __shared__ float red[RPS][K + 4];
+  __shared__ float redb[RPS];
+  const int tid = threadIdx.x;
+  const int lc = tid % L, rs = tid / L;
+  const mu32x4 wv = *reinterpret_cast<const mu32x4*>(w + lc * 8);
+  float wf[8];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float2 c = bf16x2_to_f2(wv[e]);
+    wf[2 * e] = c.x;
+    wf[2 * e + 1] = c.y;
+  }
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float accb = 0.f;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  for (int i = rs; i < rows_per_block; i += RPS) {
+    const int64_t b = r0 + i;
+    if (b >= B) break;
+    const float g = bf16_to_f32(bf16_rne(gz[b]));
+    const mu32x4 hv = *reinterpret_cast<const mu32x4*>(h + b * ldh + lc * 8);
+    mu32x4 ov;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float2 a = bf16x2_to_f2(hv[e]);
+      acc[2 * e] = fmaf(g, a.x, acc[2 * e]);
+      acc[2 * e + 1] = fmaf(g, a.y, acc[2 * e + 1]);
+      const float d0 = a.x > 0.f ? g * wf[2 * e] : 0.f;
+      const float d1 = a.y > 0.f ? g * wf[2 * e + 1] : 0.f;
+      ov[e] = (uint32_t)bf16_rne(d0) | ((uint32_t)bf16_rne(d1) << 16);
+    }
+    *reinterpret_cast<mu32x4*>(dh + b * lddh + lc * 8) = ov;
+    accb += g;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rs][lc * 8 + e] = acc[e];
+  if (lc == 0) redb[rs] = accb;
+  __syncthreads();
+  // column sums over the RPS row sweeps, in sweep order
+  for (int c = tid; c < K; c += 256) {
+    float t = 0.f;
+    for (int r = 0; r < RPS; ++r) t += red[r][c];
+    dw_part[(int64_t)blockIdx.x * K + c] = t;
+  }
+  if (tid == 0) {
+    float t = 0.f;
+    for (int r = 0; r < RPS; ++r) t += redb[r];
+    db_part[blockIdx.x] = t;
+  }
+}
+
 }  // namespace
 }  // namespace dr
 
@@ -364,6 +465,62 @@ int dr_transpose_bf16_colsum(const uint16_t* in, int64_t rows, int64_t cols, int
   const dim3 grid((unsigned)ceil_div(cols, 64), (unsigned)ceil_div(rows, 64));
   hipLaunchKernelGGL(transpose_bf16_kernel, grid, dim3(256), 0, S(stream), in, rows, cols, ld_in,
                      out, ld_out, col_partials);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+
+static constexpr int kHeadRows = 512;   // rows per backward block
+
+size_t dr_mlp_head_grad_partials(int64_t batch) {
+  return (size_t)(batch > 0 ? dr::ceil_div(batch, kHeadRows) : 0);
+}
+
+int dr_mlp_head_forward_bf16(const uint16_t* h, int64_t ldh, int64_t batch, int k,
+                             const uint16_t* w, const float* bias, float* z, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(h && w && z && batch >= 0 && (k == 64 || k == 128 || k == 256 || k == 512) &&
+                 ldh >= k && ldh % 8 == 0,
+             DR_INVALID_ARGUMENT, "dr_mlp_head_forward_bf16: k in {64,128,256,512}, ldh % 8 == 0");
+  DR_REQUIRE(((((uintptr_t)h) | ((uintptr_t)w)) & 15) == 0, DR_INVALID_ARGUMENT,
+             "dr_mlp_head_forward_bf16: h and w must be 16-B aligned");
+  if (batch == 0) return DR_OK;
+  const int L = k / 8;
+  const unsigned grid = (unsigned)ceil_div(batch, 256 / L);
+#define DR_HEAD_F(LL)                                                                          \
+  hipLaunchKernelGGL(head_fwd_kernel<LL>, dim3(grid), dim3(256), 0, S(stream), h, ldh, batch, w, \
+                     bias, z)
+  if (L == 8) DR_HEAD_F(8);
+  else if (L == 16) DR_HEAD_F(16);
+  else if (L == 32) DR_HEAD_F(32);
+  else DR_HEAD_F(64);
+#undef DR_HEAD_F
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_mlp_head_backward_bf16(const uint16_t* h, int64_t ldh, int64_t batch, int k,
+                              const uint16_t* w, const float* grad_z, uint16_t* grad_h,
+                              int64_t ld_grad_h, float* dw_partials, float* db_partials,
+                              void* stream) {
+  using namespace dr;
+  DR_REQUIRE(h && w && grad_z && grad_h && dw_partials && db_partials && batch >= 0 &&
+                 (k == 64 || k == 128 || k == 256 || k == 512) && ldh >= k && ldh % 8 == 0 &&
+                 ld_grad_h >= k && ld_grad_h % 8 == 0,
+             DR_INVALID_ARGUMENT, "dr_mlp_head_backward_bf16: bad shape");
+  DR_REQUIRE(((((uintptr_t)h) | ((uintptr_t)w) | ((uintptr_t)grad_h)) & 15) == 0,
+             DR_INVALID_ARGUMENT, "dr_mlp_head_backward_bf16: h, w, grad_h must be 16-B aligned");
+  if (batch == 0) return DR_OK;
+  const int L = k / 8;
+  const unsigned grid = (unsigned)ceil_div(batch, kHeadRows);
+#define DR_HEAD_B(LL)                                                                          \
+  hipLaunchKernelGGL(head_bwd_kernel<LL>, dim3(grid), dim3(256), 0, S(stream), h, ldh, batch, w, \
+                     grad_z, grad_h, ld_grad_h, kHeadRows, dw_partials, db_partials)
+  if (L == 8) DR_HEAD_B(8);
+  else if (L == 16) DR_HEAD_B(16);
+  else if (L == 32) DR_HEAD_B(32);
+  else DR_HEAD_B(64);
+#undef DR_HEAD_B
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

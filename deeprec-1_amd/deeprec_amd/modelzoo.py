@@ -125,9 +125,13 @@ class _MfmaTowerFn(torch.autograd.Function):
     y_{l-1} = h_l) -- no separate mask / multiply passes."""
 
     @staticmethod
-    def forward(ctx, h0, last_act, *params):
-        L = len(params) // 2
-        ws, bs = params[:L], params[L:]
+    def forward(ctx, h0, last_act, head, *params):
+        # head: the DLRM output layer (N = 1, dr_mlp_head_*) rides on the
+        # tower -- its weight and bias are the last two params, the node
+        # returns the [B, 1] logit, and its backward hands the tower the
+        # ReLU-masked gradient of the last layer directly
+        L = (len(params) - (2 if head else 0)) // 2
+        ws, bs = params[:L], params[L:2 * L]
         hs, wbs = [h0], []
         h = h0
         for l in range(L):
@@ -137,20 +141,32 @@ class _MfmaTowerFn(torch.autograd.Function):
             h = ops.gemm_nt(h, wb, bs[l].detach(), ops.ACT_RELU if relu else ops.ACT_NONE)
             hs.append(h)
             wbs.append(wb)
-        ctx.save_for_backward(*hs, *wbs)
-        ctx.L, ctx.last_act = L, last_act
+        ctx.L, ctx.last_act, ctx.head = L, last_act, head
         ctx.ks = [w.shape[1] for w in ws]
+        if head:
+            wh = params[2 * L].detach().reshape(-1).to(torch.bfloat16)
+            z = ops.mlp_head_forward(h, wh, params[2 * L + 1].detach())
+            ctx.head_shapes = (params[2 * L].shape, params[2 * L + 1].shape)
+            ctx.save_for_backward(*hs, *wbs, wh)
+            return z.view(-1, 1)
+        ctx.save_for_backward(*hs, *wbs)
         return h
 
     @staticmethod
     def backward(ctx, go):
         L = ctx.L
         saved = ctx.saved_tensors
-        hs, wbs = saved[:L + 1], saved[L + 1:]
-        g = go.to(torch.bfloat16)
-        if ctx.last_act:
-            g = g * (hs[L] > 0)
-        g = g.contiguous()
+        hs, wbs = saved[:L + 1], saved[L + 1:2 * L + 1]
+        head_grads = ()
+        if ctx.head:
+            # grad_h = bf16(gz w) masked by the last layer's ReLU, dw / db of the head
+            g, dwh, dbh = ops.mlp_head_backward(hs[L], saved[2 * L + 1], go)
+            head_grads = (dwh.view(ctx.head_shapes[0]), dbh.view(ctx.head_shapes[1]))
+        else:
+            g = go.to(torch.bfloat16)
+            if ctx.last_act:
+                g = g * (hs[L] > 0)
+            g = g.contiguous()
         B = g.shape[0]
         dws, dbs = [None] * L, [None] * L
         for l in reversed(range(L)):
@@ -166,7 +182,7 @@ class _MfmaTowerFn(torch.autograd.Function):
             if l > 0 or ctx.needs_input_grad[0]:
                 # gradient of h_l; below the top layer h_l = y_{l-1} = ReLU output
                 g = ops.gemm_nt(g, wbs[l].t().contiguous(), mask=x if l > 0 else None)
-        return (g if ctx.needs_input_grad[0] else None, None, *dws, *dbs)
+        return (g if ctx.needs_input_grad[0] else None, None, None, *dws, *dbs, *head_grads)
 
 
 class _MfmaMLP(torch.nn.Module):
@@ -204,9 +220,21 @@ class _MfmaMLP(torch.nn.Module):
     def forward_padded(self, h):
         """The tower on an input already in bf16 and zero-padded to kp columns."""
         lins = [m for m in self.net if isinstance(m, torch.nn.Linear)]
-        y = _MfmaTowerFn.apply(h, self.last_act, *[l.weight for l in lins],
+        y = _MfmaTowerFn.apply(h, self.last_act, False, *[l.weight for l in lins],
                                *[l.bias for l in lins])
         return y.float()
+
+    def head_ok(self, head):
+        return (self.last_act and isinstance(head, torch.nn.Linear) and head.out_features == 1
+                and head.bias is not None and self.sizes[-1] in (64, 128, 256, 512))
+
+    def forward_padded_head(self, h, head):
+        """forward_padded followed by the N = 1 Linear `head` (bf16, the
+        reference's dense(units=1) under --bf16) in the same node: [B, 1]
+        fp32 logit (bf16-rounded).  Needs head_ok(head)."""
+        lins = [m for m in self.net if isinstance(m, torch.nn.Linear)]
+        return _MfmaTowerFn.apply(h, self.last_act, True, *[l.weight for l in lins],
+                                  *[l.bias for l in lins], head.weight, head.bias)
 
 
 class _MaybeBF16(object):
@@ -250,6 +278,9 @@ class DLRM(torch.nn.Module):
     # padded bf16 top-MLP input (DotConcatBf16); False (or the A/B switch
     # DR_DLRM_FUSE_DOT_CONCAT=0) = the composed dot -> cat -> cast -> pad
     fuse_dot_concat = os.environ.get("DR_DLRM_FUSE_DOT_CONCAT", "1") != "0"
+    # and the output layer riding on the top tower (dr_mlp_head_*; A/B
+    # switch DR_DLRM_FUSE_HEAD=0 = autocast Linear)
+    fuse_head = os.environ.get("DR_DLRM_FUSE_HEAD", "1") != "0"
 
     def forward(self, dense, ids):
         x0 = self.bf16(self.bottom, dense)
@@ -257,7 +288,10 @@ class DLRM(torch.nn.Module):
         if (self.fuse_dot_concat and self.bf16.on and isinstance(self.top, _MfmaMLP)
                 and self.top.mfma_ok(X.shape[0]) and X.shape[1] <= 32
                 and X.shape[2] in (16, 32, 64, 128)):
-            net = self.top.forward_padded(DotConcatBf16.apply(X, self.top.kp))
+            h0 = DotConcatBf16.apply(X, self.top.kp)
+            if self.fuse_head and self.top.head_ok(self.last):
+                return torch.sigmoid(self.top.forward_padded_head(h0, self.last)).squeeze(1)
+            net = self.top.forward_padded(h0)
             return torch.sigmoid(self.bf16(self.last, net)).squeeze(1)
         z = DotInteraction.apply(X)
         net = self.bf16(self.top, torch.cat([x0, z], 1))

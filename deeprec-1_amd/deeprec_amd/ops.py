@@ -553,6 +553,39 @@ def dot_interaction_concat_grad_bf16(x, grad):
     return out
 
 
+def mlp_head_forward(h, w_bf16, bias=None):
+    """dr_mlp_head_forward_bf16: the N = 1 output layer on the bf16 top-MLP
+    output h [B, K] -> z [B] fp32 (a bf16-rounded logit); bias a 1-element
+    fp32 device tensor or None."""
+    dev = _dev(h)
+    B, K = h.shape
+    if h.dtype != torch.bfloat16 or h.stride(1) != 1 or w_bf16.dtype != torch.bfloat16:
+        raise ValueError("mlp_head_forward needs bf16 h (unit column stride) and bf16 w")
+    z = torch.empty(B, dtype=torch.float32, device=dev)
+    bb = None if bias is None else _c(bias.reshape(1), torch.float32)
+    check(lib().dr_mlp_head_forward_bf16(ptr(h), h.stride(0), B, K, ptr(w_bf16.contiguous()),
+                                         ptr(bb), ptr(z), stream_handle(dev)))
+    _post(dev)
+    return z
+
+
+def mlp_head_backward(h, w_bf16, gz):
+    """dr_mlp_head_backward_bf16 -> (grad_h bf16 [B, K] with h's ReLU mask
+    applied, dw fp32 [K], db fp32 scalar tensor)."""
+    dev = _dev(h)
+    B, K = h.shape
+    gz = _c(gz.reshape(B), torch.float32)
+    P = lib().dr_mlp_head_grad_partials(B)
+    gh = torch.empty((B, K), dtype=torch.bfloat16, device=dev)
+    dwp = torch.empty((max(P, 1), K), dtype=torch.float32, device=dev)
+    dbp = torch.empty(max(P, 1), dtype=torch.float32, device=dev)
+    check(lib().dr_mlp_head_backward_bf16(ptr(h), h.stride(0), B, K, ptr(w_bf16.contiguous()),
+                                          ptr(gz), ptr(gh), K, ptr(dwp), ptr(dbp),
+                                          stream_handle(dev)))
+    _post(dev)
+    return gh, dwp[:P].sum(0), dbp[:P].sum()
+
+
 def crossnet_layer(x0, xl, weight, bias=None):
     """DCN-v2 cross layer x0 * (xl W^T + b) + xl, bf16 MFMA, fp32 accumulate.
 

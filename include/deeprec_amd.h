@@ -900,6 +900,22 @@ int dr_transpose_bf16(const uint16_t* in, int64_t rows, int64_t cols, int64_t ld
 /* operand transpose instead of another pass over g.                         */
 int dr_transpose_bf16_colsum(const uint16_t* in, int64_t rows, int64_t cols, int64_t ld_in,
                              uint16_t* out, int64_t ld_out, float* col_partials, void* stream);
+/* The DLRM output layer under --bf16 (modelzoo/DLRM/train.py:241-249:       */
+/* dense(units=1) on the bf16 top MLP): z[b] = bf16(sum_k h[b,k] w[k] + bias) */
+/* as fp32, h [batch, k] bf16 (row stride ldh), w [k] bf16, bias a device   */
+/* fp32 scalar (nullable), fp32 sum in a fixed order.  k in {64,128,256,512}.*/
+int dr_mlp_head_forward_bf16(const uint16_t* h, int64_t ldh, int64_t batch, int k,
+                             const uint16_t* w, const float* bias, float* z, void* stream);
+/* Its backward from grad_z [batch] fp32 (rounded to bf16 first, as the bf16 */
+/* layer sees it): grad_h = bf16(gz w) where h > 0, else 0 (the top layer's   */
+/* ReLU derivative in the same pass); dw_partials [P, k] and db_partials [P]  */
+/* fp32 = per-block sums of gz h and gz, P = dr_mlp_head_grad_partials(batch) */
+/* (the caller sums them over P: deterministic).                              */
+size_t dr_mlp_head_grad_partials(int64_t batch);
+int dr_mlp_head_backward_bf16(const uint16_t* h, int64_t ldh, int64_t batch, int k,
+                              const uint16_t* w, const float* grad_z, uint16_t* grad_h,
+                              int64_t ld_grad_h, float* dw_partials, float* db_partials,
+                              void* stream);
 /* Same layer, also writing lin_out = xl W^T + b (bf16, nullable; needs      */
 /* d % 64 == 0) for the backward pass.  d % 64 == 0 selects the pipelined    */
 /* kernel (global_load_lds staging, double-buffered K steps of 64).          */

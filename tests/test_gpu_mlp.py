@@ -228,6 +228,7 @@ def test_dlrm_bf16_fused_dot_concat_matches_composed(dr):
     dense = torch.rand((B, 13), device=DEV)
     ids = torch.randint(0, 5000, (T, B), device=DEV)
     runs = []
+    model.fuse_head = False   # both runs through the same output layer
     for fuse in (True, False):
         model.fuse_dot_concat = fuse
         model.zero_grad(set_to_none=True)
@@ -246,3 +247,61 @@ def test_dlrm_bf16_fused_dot_concat_matches_composed(dr):
         assert torch.equal(a, b)
     for a, b, c, d in zip(v1, v2, i1, i2):
         assert torch.equal(c, d) and torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,K", [(1000, 256), (65536, 256), (513, 64), (300, 512), (77, 128)])
+def test_mlp_head_matches_reference(dr, B, K):
+    """dr_mlp_head_*: the N = 1 bf16 output layer.  Forward = the bf16
+    rounding of the fp32 dot product (+ bias), within one bf16 ulp of the
+    fp64 value; backward grad_h bit-exact (one product, one rounding, ReLU
+    mask of h), dw / db within fp32 summation error of fp64."""
+    from deeprec_amd import ops
+    g = torch.Generator(device=DEV)
+    g.manual_seed(B + K)
+    h = torch.relu(torch.randn((B, K), generator=g, device=DEV)).to(torch.bfloat16)
+    w = torch.randn(K, generator=g, device=DEV).to(torch.bfloat16)
+    bias = torch.randn(1, generator=g, device=DEV)
+    z = ops.mlp_head_forward(h, w, bias)
+    ref = h.double() @ w.double() + bias.double()
+    ulp = ref.abs().to(torch.bfloat16).float().double() * 2.0 ** -7 + 1e-30
+    assert ((z.double() - ref).abs() <= ulp + 1e-5 * (h.double().abs() @ w.double().abs())).all()
+    gz = torch.randn(B, generator=g, device=DEV)
+    gh, dw, db = ops.mlp_head_backward(h, w, gz)
+    gzb = gz.to(torch.bfloat16).float()
+    want = torch.where(h.float() > 0, gzb[:, None] * w.float()[None, :],
+                       torch.zeros((), device=DEV)).to(torch.bfloat16)
+    assert torch.equal(gh.view(torch.int16), want.view(torch.int16))
+    dref = (gzb.double()[:, None] * h.double()).sum(0)
+    tol = 1e-5 * (gzb.double().abs()[:, None] * h.double().abs()).sum(0) + 1e-6
+    assert ((dw.double() - dref).abs() <= tol).all()
+    assert abs(float(db) - float(gzb.double().sum())) <= 1e-5 * float(gzb.abs().double().sum())
+    gh2, dw2, db2 = ops.mlp_head_backward(h, w, gz)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+
+
+def test_dlrm_bf16_fused_head_tracks_autocast_head(dr):
+    """DLRM --bf16 with the output layer on dr_mlp_head_* vs the autocast
+    Linear: same prediction up to the bf16 logit rounding, dense gradients
+    within bf16 noise (relative Frobenius)."""
+    from deeprec_amd import modelzoo as mz
+    torch.manual_seed(13)
+    T, D, B = 26, 128, 1024
+    evs = [dr.EmbeddingVariable("dlrm_fh_%d" % t, D, 0.01, device=DEV) for t in range(T)]
+    model = mz.DLRM(evs, 13, (64,), (128, 64), bf16=True).to(DEV)
+    assert model.top.head_ok(model.last)
+    dense = torch.rand((B, 13), device=DEV)
+    ids = torch.randint(0, 5000, (T, B), device=DEV)
+    labels = (torch.rand(B, device=DEV) > 0.5).float()
+    runs = []
+    for fh in (True, False):
+        model.fuse_head = fh
+        model.zero_grad(set_to_none=True)
+        out = model(dense, ids)
+        torch.nn.functional.binary_cross_entropy(out, labels).backward()
+        runs.append((out.detach().clone(), [p.grad.clone() for p in model.parameters()]))
+        for ev in evs:
+            ev.pending_grads.clear()
+    (o1, g1), (o2, g2) = runs
+    assert (o1 - o2).abs().max() <= 1e-2
+    for a, b in zip(g1, g2):
+        assert float((a - b).norm()) <= 5e-2 * float(b.norm()) + 1e-6, (a.shape,)
