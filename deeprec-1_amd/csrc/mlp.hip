@@ -345,6 +345,10 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const uint16_t* __restric
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float accb = 0.f;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  // rows_per_block / RPS rows per thread, all of them loaded before use
+  // (the loads of one thread are independent: unrolled, they are in flight
+  // together instead of one latency per row)
+#pragma unroll 8
   for (int i = rs; i < rows_per_block; i += RPS) {
     const int64_t b = r0 + i;
     if (b >= B) break;
@@ -378,6 +382,37 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const uint16_t* __restric
     for (int r = 0; r < RPS; ++r) t += redb[r];
     db_part[blockIdx.x] = t;
   }
+}
+
+
+// dL/dy of a ReLU layer's bf16 output y, from an fp32 gradient (row stride
+// ldg): out = bf16(g) where y > 0, else 0 -- the MFMA tower's entry when
+// its output was widened to fp32 for the layer above (one pass instead of
+// a cast, a compare and a multiply).  8 columns per thread.
+__global__ __launch_bounds__(256) void relu_grad_bf16_kernel(const float* __restrict__ g,
+                                                             int64_t ldg,
+                                                             const uint16_t* __restrict__ y,
+                                                             int64_t ldy, int64_t rows,
+                                                             int64_t cols,
+                                                             uint16_t* __restrict__ out,
+                                                             int64_t ldo) {
+  const int64_t c8 = cols / 8;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * c8) return;
+  const int64_t r = i / c8, c = (i - r * c8) * 8;
+  const float4 g0 = *reinterpret_cast<const float4*>(g + r * ldg + c);
+  const float4 g1 = *reinterpret_cast<const float4*>(g + r * ldg + c + 4);
+  const mu32x4 yv = *reinterpret_cast<const mu32x4*>(y + r * ldy + c);
+  const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+  mu32x4 ov;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float2 yy = bf16x2_to_f2(yv[e]);
+    const uint32_t lo = yy.x > 0.f ? bf16_rne(gv[2 * e]) : 0u;
+    const uint32_t hi = yy.y > 0.f ? bf16_rne(gv[2 * e + 1]) : 0u;
+    ov[e] = lo | (hi << 16);
+  }
+  *reinterpret_cast<mu32x4*>(out + r * ldo + c) = ov;
 }
 
 }  // namespace
@@ -470,7 +505,7 @@ int dr_transpose_bf16_colsum(const uint16_t* in, int64_t rows, int64_t cols, int
 }
 
 
-static constexpr int kHeadRows = 512;   // rows per backward block
+static constexpr int kHeadRows = 64;    // rows per backward block (1024 blocks at B = 65 536)
 
 size_t dr_mlp_head_grad_partials(int64_t batch) {
   return (size_t)(batch > 0 ? dr::ceil_div(batch, kHeadRows) : 0);
@@ -521,6 +556,24 @@ int dr_mlp_head_backward_bf16(const uint16_t* h, int64_t ldh, int64_t batch, int
   else if (L == 32) DR_HEAD_B(32);
   else DR_HEAD_B(64);
 #undef DR_HEAD_B
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+
+int dr_relu_grad_bf16(const float* grad, int64_t ld_grad, const uint16_t* y, int64_t ld_y,
+                      int64_t rows, int64_t cols, uint16_t* out, int64_t ld_out, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(grad && y && out && rows >= 0 && cols >= 0 && cols % 8 == 0 && ld_grad % 4 == 0 &&
+                 ld_y % 8 == 0 && ld_out % 8 == 0 && ld_grad >= cols && ld_y >= cols &&
+                 ld_out >= cols,
+             DR_INVALID_ARGUMENT, "dr_relu_grad_bf16: cols and strides multiples of 8 (grad: 4)");
+  DR_REQUIRE(((((uintptr_t)grad) | ((uintptr_t)y) | ((uintptr_t)out)) & 15) == 0,
+             DR_INVALID_ARGUMENT, "dr_relu_grad_bf16: pointers must be 16-B aligned");
+  if (rows == 0 || cols == 0) return DR_OK;
+  const int64_t n = rows * (cols / 8);
+  hipLaunchKernelGGL(relu_grad_bf16_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0,
+                     S(stream), grad, ld_grad, y, ld_y, rows, cols, out, ld_out);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

@@ -150,7 +150,9 @@ class _MfmaTowerFn(torch.autograd.Function):
             ctx.save_for_backward(*hs, *wbs, wh)
             return z.view(-1, 1)
         ctx.save_for_backward(*hs, *wbs)
-        return h
+        # widened here rather than by the caller, so the gradient arrives in
+        # fp32 and the ReLU-mask + bf16 cast is one pass (dr_relu_grad_bf16)
+        return h.float()
 
     @staticmethod
     def backward(ctx, go):
@@ -162,6 +164,9 @@ class _MfmaTowerFn(torch.autograd.Function):
             # grad_h = bf16(gz w) masked by the last layer's ReLU, dw / db of the head
             g, dwh, dbh = ops.mlp_head_backward(hs[L], saved[2 * L + 1], go)
             head_grads = (dwh.view(ctx.head_shapes[0]), dbh.view(ctx.head_shapes[1]))
+        elif (ctx.last_act and go.stride(1) == 1 and go.shape[1] % 8 == 0
+              and go.stride(0) % 4 == 0 and go.data_ptr() % 16 == 0):
+            g = ops.relu_grad_bf16(go, hs[L])     # cast + ReLU mask in one pass
         else:
             g = go.to(torch.bfloat16)
             if ctx.last_act:
@@ -220,9 +225,8 @@ class _MfmaMLP(torch.nn.Module):
     def forward_padded(self, h):
         """The tower on an input already in bf16 and zero-padded to kp columns."""
         lins = [m for m in self.net if isinstance(m, torch.nn.Linear)]
-        y = _MfmaTowerFn.apply(h, self.last_act, False, *[l.weight for l in lins],
-                               *[l.bias for l in lins])
-        return y.float()
+        return _MfmaTowerFn.apply(h, self.last_act, False, *[l.weight for l in lins],
+                                  *[l.bias for l in lins])
 
     def head_ok(self, head):
         return (self.last_act and isinstance(head, torch.nn.Linear) and head.out_features == 1

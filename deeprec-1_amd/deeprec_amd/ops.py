@@ -553,6 +553,21 @@ def dot_interaction_concat_grad_bf16(x, grad):
     return out
 
 
+def relu_grad_bf16(g, y):
+    """dr_relu_grad_bf16: bf16(g) masked by y > 0 (y the bf16 ReLU output);
+    g fp32 [R, C] with unit column stride (any row stride)."""
+    dev = _dev(g)
+    R, C = y.shape
+    if g.dtype != torch.float32 or g.stride(1) != 1 or y.dtype != torch.bfloat16 \
+            or y.stride(1) != 1 or tuple(g.shape) != (R, C):
+        raise ValueError("relu_grad_bf16 needs fp32 g and bf16 y of one shape, unit column stride")
+    out = torch.empty((R, C), dtype=torch.bfloat16, device=dev)
+    check(lib().dr_relu_grad_bf16(ptr(g), g.stride(0), ptr(y), y.stride(0), R, C, ptr(out), C,
+                                  stream_handle(dev)))
+    _post(dev)
+    return out
+
+
 def mlp_head_forward(h, w_bf16, bias=None):
     """dr_mlp_head_forward_bf16: the N = 1 output layer on the bf16 top-MLP
     output h [B, K] -> z [B] fp32 (a bf16-rounded logit); bias a 1-element

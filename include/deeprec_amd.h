@@ -900,6 +900,11 @@ int dr_transpose_bf16(const uint16_t* in, int64_t rows, int64_t cols, int64_t ld
 /* operand transpose instead of another pass over g.                         */
 int dr_transpose_bf16_colsum(const uint16_t* in, int64_t rows, int64_t cols, int64_t ld_in,
                              uint16_t* out, int64_t ld_out, float* col_partials, void* stream);
+/* ReLU layer backward entry: out = bf16(grad) where the bf16 ReLU output y */
+/* is > 0, else 0; grad fp32 (row stride ld_grad, a multiple of 4), cols and */
+/* the bf16 strides multiples of 8, pointers 16-B aligned.                   */
+int dr_relu_grad_bf16(const float* grad, int64_t ld_grad, const uint16_t* y, int64_t ld_y,
+                      int64_t rows, int64_t cols, uint16_t* out, int64_t ld_out, void* stream);
 /* The DLRM output layer under --bf16 (modelzoo/DLRM/train.py:241-249:       */
 /* dense(units=1) on the bf16 top MLP): z[b] = bf16(sum_k h[b,k] w[k] + bias) */
 /* as fp32, h [batch, k] bf16 (row stride ldh), w [k] bf16, bias a device   */

@@ -10,7 +10,7 @@ for V in 1 1; do  # fused dot-concat + head
   echo "fuse=$V $(grep '^{' gpurun_out/$T/ms.log)" | tee -a gpurun_out/$T/ab.log
 done
 bash tools/gpu_dlrm_prof.sh $T/prof_fused
-for V in 0 1; do
+for V in 1; do
   DR_DLRM_FUSE_HEAD=$V timeout -k 10 300 python tools/model_step.py --model dlrm --bf16 --steps 10 --warmup 3 > gpurun_out/$T/ms.log 2>&1 || exit 1
   echo "fuse_head=$V $(grep '^{' gpurun_out/$T/ms.log)" | tee -a gpurun_out/$T/ab.log
 done
