@@ -305,3 +305,17 @@ def test_dlrm_bf16_fused_head_tracks_autocast_head(dr):
     assert (o1 - o2).abs().max() <= 1e-2
     for a, b in zip(g1, g2):
         assert float((a - b).norm()) <= 5e-2 * float(b.norm()) + 1e-6, (a.shape,)
+
+
+def test_relu_grad_bf16(dr):
+    """dr_relu_grad_bf16 = g.to(bf16) where y > 0 else 0 (strided fp32 g)."""
+    from deeprec_amd import ops
+    g = torch.Generator(device=DEV)
+    g.manual_seed(21)
+    big = torch.randn((700, 27, 128), generator=g, device=DEV)
+    gr = big[:, 0, :]                                  # row stride 27 * 128
+    y = torch.relu(torch.randn((700, 128), generator=g, device=DEV)).to(torch.bfloat16)
+    got = ops.relu_grad_bf16(gr, y)
+    want = torch.where(y > 0, gr.to(torch.bfloat16), torch.zeros((), dtype=torch.bfloat16,
+                                                                  device=DEV))
+    assert torch.equal(got.view(torch.int16), want.view(torch.int16))
