@@ -192,6 +192,174 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Weight-gradient GEMM in "TN" form, no operand transposes:
+//   C[n][k] = sum_b G[b][n] X[b][k]    (dW = g^T x of a Linear layer)
+// G [rows, N], X [rows, K] bf16 row-major: the contraction runs down the rows
+// of both.  Tile 128 (n) x 128 (k), 4 waves of 64 x 64 (v_mfma_f32_16x16x32_
+// bf16), 64 contraction rows per step.  Each step stages a 64 x 128 chunk of
+// G and of X into LDS as they lie in memory (global_load_lds_dwordx4, 256-B
+// rows, 32-B slots XOR-swizzled by h(r) = (r & 3) | ((r >> 3) & 1) << 2),
+// and the MFMA fragments -- 8 consecutive rows of one column per lane, for
+// the A and the B operand alike -- come from ds_read_b64_tr_b16, the CDNA4
+// transposing LDS read (4 rows x 16 columns per 16-lane group, column i to
+// lane i): the two 8-row halves of a 32-row MFMA step are two such reads.
+// With the swizzle the 8 rows a 32-lane half reads ({0..3, 8..11} + 16 h,
+// {4..7, 12..15} + 16 h) sit in 8 distinct 32-B slots: conflict-free.
+// Split over the rows (grid.y): fp32 partials summed in split order by
+// gemm_splitk_reduce_kernel (deterministic); S = 1 writes C directly.
+// colsum (optional): the column sums of G over each split, from the A
+// fragments already in registers (blocks of the first k tile, waves wn = 0):
+// a layer's bias gradient without another pass over g.
+// Replaces transpose(g) + transpose(x) + an NT GEMM (3 passes).
+// ---------------------------------------------------------------------------
+typedef short tn_v4s __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int tn_h(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+
+// 64 rows x 128 columns of X from (row0, col0) into img (64 x 256 B): 4 wave
+// instructions of 4 rows each per wave.
+__device__ __forceinline__ void tn_stage(const uint16_t* __restrict__ X, int64_t ld, int64_t row0,
+                                         int64_t col0, int64_t cols, char* img, int wave,
+                                         int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rb = (wave * 4 + i) * 4;
+    const int r = rb + (lane >> 4), sl = lane & 15;
+    const int c = (((sl >> 1) ^ tn_h(r)) << 1) | (sl & 1);   // logical 16-B chunk
+    int64_t gc = col0 + c * 8;
+    if (gc >= cols) gc = col0;  // columns past the end feed discarded outputs
+    const uint16_t* src = X + (row0 + r) * ld + gc;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(img + rb * 256),
+                                     16, 0, 0);
+  }
+}
+
+// The fragment of 16 columns starting at slot m (16 bf16 = one 32-B slot)
+// for the 32-row step kk: lane (g, 4q + p) reads rows kk*32 + 8g + q (+ 4).
+__device__ __forceinline__ mbf16x8 tn_frag(const char* img, int kk, int m, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int r1 = kk * 32 + 8 * g + q, r2 = r1 + 4;
+  const tn_v4s a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) tn_v4s*)(img + r1 * 256 + ((m ^ tn_h(r1)) << 5) + 8 * p));
+  const tn_v4s b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) tn_v4s*)(img + r2 * 256 + ((m ^ tn_h(r2)) << 5) + 8 * p));
+  return mbf16x8{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+}
+
+__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
+    const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __restrict__ X, int64_t ldx,
+    int64_t N, int64_t K, int64_t bchunk, int64_t rows, float* __restrict__ C, int64_t ldc,
+    int64_t split_stride, float* __restrict__ colsum) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * 2 * GM_TILE];  // [buf][G|X], 64 KB
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t nwg = (int64_t)gridDim.x;
+  const int64_t orig = blockIdx.x;
+  const int64_t xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
+  const int64_t tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+  const int64_t ntk = (K + 127) / 128;
+  const int64_t m0 = (tile / ntk) * 128;   // n
+  const int64_t n0 = (tile % ntk) * 128;   // k
+  const int64_t b0 = (int64_t)blockIdx.y * bchunk;
+  const int64_t be = b0 + bchunk < rows ? b0 + bchunk : rows;
+  const int nk = be > b0 ? (int)((be - b0) / 64) : 0;
+  const bool sums = colsum && n0 == 0 && wn == 0;
+  mf32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = mf32x4{0.f, 0.f, 0.f, 0.f};
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  if (nk > 0) {
+    tn_stage(G, ldg, b0, m0, N, lds, wave, lane);
+    tn_stage(X, ldx, b0, n0, K, lds + GM_TILE, wave, lane);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = lds + (kt & 1) * 2 * GM_TILE;
+    if (kt + 1 < nk) {
+      char* nxt = lds + ((kt + 1) & 1) * 2 * GM_TILE;
+      tn_stage(G, ldg, b0 + (int64_t)(kt + 1) * 64, m0, N, nxt, wave, lane);
+      tn_stage(X, ldx, b0 + (int64_t)(kt + 1) * 64, n0, K, nxt + GM_TILE, wave, lane);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's step-kt DMAs landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // ... and every other wave's
+    asm volatile("" ::: "memory");
+    const char* sG = cur;
+    const char* sX = cur + GM_TILE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      mbf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = tn_frag(sG, kk, wm * 4 + i, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = tn_frag(sX, kk, wn * 4 + j, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      if (sums) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs[i] += bf16_to_f32((uint16_t)fa[i][e]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // buffer kt&1 is restaged by iteration kt+1's DMA
+    asm volatile("" ::: "memory");
+  }
+  if (sums) {
+    // lane (g, li) summed rows 8g..8g+7 of each 32-row step for column li:
+    // the 4 groups in a fixed butterfly
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      cs[i] += __shfl_xor(cs[i], 16, 64);
+      cs[i] += __shfl_xor(cs[i], 32, 64);
+      const int64_t col = m0 + wm * 64 + i * 16 + (lane & 15);
+      if (lane < 16 && col < N) colsum[(int64_t)blockIdx.y * N + col] = cs[i];
+    }
+  }
+  __syncthreads();
+  // accumulators -> LDS (C/D map: col = lane & 15 = k, row = (lane >> 4) * 4
+  // + reg = n), then 32-B fp32 row stores, as gemm_nt_kernel's epilogue
+  const int fr = lane & 15, fq = lane >> 4;
+  float* ct = reinterpret_cast<float*>(lds) + wave * 64 * 64;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i * 16 + fq * 4 + r;
+        const int col = (j * 16 + fr) ^ (((row >> 2) & 3) << 4);
+        ct[row * 64 + col] = acc[i][j][r];
+      }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  float* Cz = C + (int64_t)blockIdx.y * split_stride;
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int idx = it * 64 + lane;
+    const int row = idx >> 3, cc = (idx & 7) * 8;
+    const int64_t grow = m0 + wm * 64 + row;
+    const int64_t gcol = n0 + wn * 64 + cc;
+    if (grow >= N || gcol >= K) continue;
+    const int pc = cc ^ (((row >> 2) & 3) << 4);
+    const float4 l0 = *reinterpret_cast<const float4*>(ct + row * 64 + pc);
+    const float4 l1 = *reinterpret_cast<const float4*>(ct + row * 64 + pc + 4);
+    float* dst = Cz + grow * ldc + gcol;
+    reinterpret_cast<float4*>(dst)[0] = l0;
+    reinterpret_cast<float4*>(dst)[1] = l1;
+  }
+}
+
 // Split-K reduction in split order: C = act(sum_z ws[z] + bias), 4 columns
 // per thread.
 __global__ void gemm_splitk_reduce_kernel(const float* __restrict__ ws, int S, int64_t M,
@@ -574,6 +742,70 @@ int dr_relu_grad_bf16(const float* grad, int64_t ld_grad, const uint16_t* y, int
   const int64_t n = rows * (cols / 8);
   hipLaunchKernelGGL(relu_grad_bf16_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0,
                      S(stream), grad, ld_grad, y, ld_y, rows, cols, out, ld_out);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+
+size_t dr_gemm_tn_workspace_size(int64_t N, int64_t K, int split_k, int with_colsum) {
+  if (split_k <= 1 && !with_colsum) return 0;
+  const size_t s = (size_t)(split_k > 1 ? split_k : 1);
+  size_t b = split_k > 1 ? s * (size_t)(N > 0 ? N : 1) * (size_t)(K > 0 ? K : 1) * sizeof(float) : 0;
+  b = (b + 255) & ~size_t(255);
+  if (with_colsum) b += s * (size_t)(N > 0 ? N : 1) * sizeof(float);
+  return b + 256;
+}
+
+int dr_gemm_tn_bf16(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, int64_t rows,
+                    int64_t N, int64_t K, float* C, int64_t ldc, float* colsum, int split_k,
+                    void* ws, size_t ws_bytes, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(G && X && C && rows >= 0 && N >= 0 && K >= 0, DR_INVALID_ARGUMENT, "bad argument");
+  DR_REQUIRE(rows % 64 == 0 && N % 8 == 0 && K % 8 == 0, DR_INVALID_ARGUMENT,
+             "dr_gemm_tn_bf16: rows must be a multiple of 64, N and K of 8");
+  DR_REQUIRE(ldg % 8 == 0 && ldx % 8 == 0 && ldc % 4 == 0 && ldg >= N && ldx >= K && ldc >= K,
+             DR_INVALID_ARGUMENT, "dr_gemm_tn_bf16: strides must be multiples of 8 (ldc: 4)");
+  DR_REQUIRE((((uintptr_t)G | (uintptr_t)X | (uintptr_t)C) & 15) == 0 &&
+                 (!colsum || ((uintptr_t)colsum & 15) == 0),
+             DR_INVALID_ARGUMENT, "dr_gemm_tn_bf16: pointers must be 16-B aligned");
+  if (N == 0 || K == 0) return DR_OK;
+  hipStream_t st = S(stream);
+  if (rows == 0) {
+    for (int64_t n = 0; n < N; ++n) {
+      int rc = fill_bytes(C + n * ldc, 0, (size_t)K * sizeof(float), st);
+      if (rc) return rc;
+    }
+    return colsum ? fill_bytes(colsum, 0, (size_t)N * sizeof(float), st) : DR_OK;
+  }
+  const int64_t tiles = ((N + 127) / 128) * ((K + 127) / 128);
+  DR_REQUIRE(tiles < (1ll << 31), DR_INVALID_ARGUMENT, "dr_gemm_tn_bf16: too many tiles");
+  const int64_t steps = rows / 64;
+  int S_ = split_k < 1 ? 1 : split_k;
+  if (S_ > steps) S_ = (int)steps;
+  const int64_t bchunk = ((steps + S_ - 1) / S_) * 64;
+  S_ = (int)((rows + bchunk - 1) / bchunk);
+  const bool direct = S_ == 1;
+  const bool need_ws = !direct || colsum;
+  DR_REQUIRE(!need_ws || (ws && ws_bytes >= dr_gemm_tn_workspace_size(N, K, S_, colsum != nullptr)),
+             DR_INVALID_ARGUMENT, "dr_gemm_tn_bf16: workspace too small");
+  DR_REQUIRE(!need_ws || ((uintptr_t)ws & 15) == 0, DR_INVALID_ARGUMENT,
+             "workspace must be 16-B aligned");
+  float* part = direct ? C : static_cast<float*>(ws);
+  size_t off = direct ? 0 : (((size_t)S_ * N * K * sizeof(float)) + 255) & ~size_t(255);
+  float* csp = colsum ? reinterpret_cast<float*>(static_cast<char*>(ws) + off) : nullptr;
+  hipLaunchKernelGGL(gemm_tn_kernel, dim3((unsigned)tiles, (unsigned)S_), dim3(256), 0, st, G, ldg,
+                     X, ldx, N, K, bchunk, rows, part, direct ? ldc : K,
+                     direct ? (int64_t)0 : N * K, csp);
+  if (!direct) {
+    const int64_t quads = N * (K / 4);
+    hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)ceil_div(quads, 256)), dim3(256),
+                       0, st, (const float*)part, S_, N, K, (const float*)nullptr, 0, (void*)C,
+                       ldc, 0);
+  }
+  if (colsum)   // N % 8 == 0
+    hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)ceil_div(N / 4, 256)), dim3(256),
+                       0, st, (const float*)csp, S_, (int64_t)1, N, (const float*)nullptr, 0,
+                       (void*)colsum, N, 0);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

@@ -112,6 +112,10 @@ class _OneHotLookup(object):
         return embedding_stack(x0, self.evs, self._sps(ids), combiner="sum")
 
 
+# A/B switch: DR_TOWER_TN_DW=0 = transposes + NT GEMM for the weight gradients
+_TN_DW = os.environ.get("DR_TOWER_TN_DW", "1") != "0"
+
+
 class _MfmaTowerFn(torch.autograd.Function):
     """A bf16 ReLU MLP tower as ONE autograd node on the hand MFMA GEMM
     (dr_gemm_nt_bf16[_ex]): layer l computes y_l = act(h_l W_l^T + b_l),
@@ -179,10 +183,15 @@ class _MfmaTowerFn(torch.autograd.Function):
             N, Kp = g.shape[1], x.shape[1]
             tiles = ((N + 127) // 128) * ((Kp + 127) // 128)
             split = max(1, min(64, 512 // tiles, B // (64 * 8)))
-            # db from the column partials the g transpose writes (no extra pass over g)
-            gt, dbs[l] = ops.transpose_bf16(g, colsum=True)
-            dw = ops.gemm_nt(gt, ops.transpose_bf16(x), out_fp32=True,
-                             split_k=split)                          # [N, Kp] fp32
+            if _TN_DW and B % 64 == 0:
+                # dW = g^T x straight from the row-major operands (transposing
+                # LDS reads), db from the same pass's A fragments
+                dw, dbs[l] = ops.gemm_tn(g, x, split_k=split, colsum=True)
+            else:
+                # db from the column partials the g transpose writes
+                gt, dbs[l] = ops.transpose_bf16(g, colsum=True)
+                dw = ops.gemm_nt(gt, ops.transpose_bf16(x), out_fp32=True,
+                                 split_k=split)                      # [N, Kp] fp32
             dws[l] = dw[:, :ctx.ks[l]]
             if l > 0 or ctx.needs_input_grad[0]:
                 # gradient of h_l; below the top layer h_l = y_{l-1} = ReLU output

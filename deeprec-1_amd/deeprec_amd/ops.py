@@ -681,6 +681,26 @@ def gemm_nt(a, b, bias=None, act=ACT_NONE, out_fp32=False, split_k=1, out=None, 
     return out
 
 
+def gemm_tn(g, x, split_k=1, colsum=False):
+    """dr_gemm_tn_bf16: g^T x in fp32 for g [R, N], x [R, K] bf16 (unit column
+    strides, R % 64 == 0): [N, K]; colsum=True also returns g's fp32 column
+    sums (the bias gradient): (dw, db)."""
+    dev = _dev(g)
+    R, N = g.shape
+    K = x.shape[1]
+    if g.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or x.shape[0] != R \
+            or g.stride(1) != 1 or x.stride(1) != 1:
+        raise ValueError("gemm_tn needs bf16 g [R, N], x [R, K] with unit column stride")
+    out = torch.empty((N, K), dtype=torch.float32, device=dev)
+    cs = torch.empty(N, dtype=torch.float32, device=dev) if colsum else None
+    wsb = lib().dr_gemm_tn_workspace_size(N, K, split_k, 1 if colsum else 0)
+    ws = workspace(wsb, dev) if wsb else None
+    check(lib().dr_gemm_tn_bf16(ptr(g), g.stride(0), ptr(x), x.stride(0), R, N, K, ptr(out), K,
+                                ptr(cs), split_k, ptr(ws), wsb, stream_handle(dev)))
+    _post(dev)
+    return (out, cs) if colsum else out
+
+
 def transpose_bf16(x, colsum=False):
     """dr_transpose_bf16: [R, C] bf16 (unit column stride) -> contiguous [C, R].
     colsum=True (dr_transpose_bf16_colsum): also the fp32 column sums of x,

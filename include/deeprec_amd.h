@@ -891,6 +891,17 @@ int dr_gemm_nt_bf16_ex(const uint16_t* A, int64_t lda, const uint16_t* B, int64_
                        int64_t N, int64_t K, const float* bias, int act, const uint16_t* aux,
                        int64_t ld_aux, void* C, int64_t ldc, int c_fp32, int split_k, void* ws,
                        size_t ws_bytes, void* stream);
+/* Weight-gradient GEMM without operand transposes: C[n][k] (fp32, ldc) =    */
+/* sum_b G[b][n] X[b][k] over rows b, G [rows, N] and X [rows, K] bf16       */
+/* row-major (the gradient and the input of a Linear layer: dW = g^T x).     */
+/* rows % 64 == 0, N and K % 8 == 0.  colsum (nullable) [N] fp32 = the       */
+/* column sums of G (the layer's bias gradient).  split_k > 1 splits the     */
+/* rows into fp32 partials summed in split order (deterministic); workspace: */
+/* dr_gemm_tn_workspace_size(N, K, split_k, colsum != NULL).                 */
+size_t dr_gemm_tn_workspace_size(int64_t N, int64_t K, int split_k, int with_colsum);
+int dr_gemm_tn_bf16(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, int64_t rows,
+                    int64_t N, int64_t K, float* C, int64_t ldc, float* colsum, int split_k,
+                    void* ws, size_t ws_bytes, void* stream);
 /* out[c][r] = in[r][c], bf16; rows, cols and strides multiples of 8.        */
 int dr_transpose_bf16(const uint16_t* in, int64_t rows, int64_t cols, int64_t ld_in,
                       uint16_t* out, int64_t ld_out, void* stream);

@@ -319,3 +319,31 @@ def test_relu_grad_bf16(dr):
     want = torch.where(y > 0, gr.to(torch.bfloat16), torch.zeros((), dtype=torch.bfloat16,
                                                                   device=DEV))
     assert torch.equal(got.view(torch.int16), want.view(torch.int16))
+
+
+@pytest.mark.parametrize("R,N,K,split", [(1024, 256, 512, 1), (65536, 512, 512, 16),
+                                         (65536, 128, 256, 64), (640, 72, 200, 3),
+                                         (64, 8, 8, 1), (4096, 512, 64, 8), (192, 136, 520, 2)])
+def test_gemm_tn_matches_fp32(dr, R, N, K, split):
+    """dr_gemm_tn_bf16 (transposing LDS reads): g^T x against fp32 on the same
+    bf16 operands, column sums of g against fp64; split partials summed in
+    order, so two runs are bit-identical."""
+    from deeprec_amd import ops
+    g = torch.Generator(device=DEV)
+    g.manual_seed(R + N + K)
+    a = torch.randn((R, N), generator=g, device=DEV).to(torch.bfloat16)
+    x = torch.randn((R, K), generator=g, device=DEV).to(torch.bfloat16)
+    dw, db = ops.gemm_tn(a, x, split_k=split, colsum=True)
+    ref = a.double().t() @ x.double()
+    scale = a.double().abs().t() @ x.double().abs()
+    assert ((dw.double() - ref).abs() <= 1e-5 * scale + 1e-5).all()
+    cref = a.double().sum(0)
+    assert ((db.double() - cref).abs() <= 1e-5 * a.double().abs().sum(0) + 1e-5).all()
+    dw2, db2 = ops.gemm_tn(a, x, split_k=split, colsum=True)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+    # strided operands (column windows of wider matrices)
+    big = torch.randn((R, N + 16), generator=g, device=DEV).to(torch.bfloat16)
+    a2 = big[:, 8:8 + N]
+    dw3 = ops.gemm_tn(a2, x, split_k=split)
+    ref3 = a2.double().t() @ x.double()
+    assert ((dw3.double() - ref3).abs() <= 1e-5 * (a2.double().abs().t() @ x.double().abs()) + 1e-5).all()
