@@ -312,16 +312,23 @@ class DLRM(torch.nn.Module):
 
 
 class DeepFM(torch.nn.Module):
-    """modelzoo/DeepFM/train.py DeepFM (no batch norm)."""
+    """modelzoo/DeepFM/train.py DeepFM (no batch norm).  bf16=True is the
+    reference's --bf16 (train.py:186-217): the dnn and final_dnn towers in
+    bf16 on fp32 master weights (keep_weights) -- here the hand MFMA towers
+    -- their output cast back to fp32 before the fp32 output layer; the FM
+    and linear parts stay fp32 (their bf16 input cast only rounds values the
+    fp32 kernels then read: kept fp32 here)."""
 
-    def __init__(self, evs, wide_evs, dnn=(256, 128, 64), final=(128, 64)):
+    def __init__(self, evs, wide_evs, dnn=(256, 128, 64), final=(128, 64), bf16=False):
         super().__init__()
+        self.bf16 = _MaybeBF16(bf16)
         self.evs = list(evs)
         self.wide_evs = list(wide_evs)
         self.dim = self.evs[0].dim
         self.T = len(self.evs)
-        self.dnn = _mlp([self.T * self.dim] + list(dnn))
-        self.final = _mlp([dnn[-1] + 1 + self.dim] + list(final))
+        mlp = _MfmaMLP if bf16 else _mlp
+        self.dnn = mlp([self.T * self.dim] + list(dnn))
+        self.final = mlp([dnn[-1] + 1 + self.dim] + list(final))
         self.last = torch.nn.Linear(final[-1], 1)
         self.lookup = _OneHotLookup(self.evs)
         self.wide_lookup = _OneHotLookup(self.wide_evs)
@@ -332,7 +339,7 @@ class DeepFM(torch.nn.Module):
         wide = self.wide_lookup(ids)                               # [B, T]
         linear = wide.sum(1, keepdim=True)
         fm = FMSecondOrder.apply(emb.view(B, self.T, self.dim))
-        net = self.final(torch.cat([self.dnn(emb), linear, fm], 1))
+        net = self.bf16(self.final, torch.cat([self.bf16(self.dnn, emb), linear, fm], 1))
         return torch.sigmoid(self.last(net)).squeeze(1)
 
 

@@ -347,3 +347,31 @@ def test_gemm_tn_matches_fp32(dr, R, N, K, split):
     dw3 = ops.gemm_tn(a2, x, split_k=split)
     ref3 = a2.double().t() @ x.double()
     assert ((dw3.double() - ref3).abs() <= 1e-5 * (a2.double().abs().t() @ x.double().abs()) + 1e-5).all()
+
+
+def test_deepfm_bf16_towers_track_fp32(dr):
+    """DeepFM --bf16 (train.py:186-217): dnn and final_dnn on the MFMA
+    towers; prediction and loss track the fp32 model on the same weights,
+    every dense gradient finite."""
+    from deeprec_amd import modelzoo as mz
+    torch.manual_seed(17)
+    T, D, B = 26, 64, 1024
+    evs = [dr.EmbeddingVariable("dfm_b_%d" % t, D, 0.01, device=DEV) for t in range(T)]
+    wide = [dr.EmbeddingVariable("dfm_bw_%d" % t, 1, 0.0, device=DEV) for t in range(T)]
+    m16 = mz.DeepFM(evs, wide, bf16=True).to(DEV)
+    assert isinstance(m16.dnn, mz._MfmaMLP) and isinstance(m16.final, mz._MfmaMLP)
+    m32 = mz.DeepFM(evs, wide).to(DEV)
+    m32.load_state_dict({k.replace(".net.", "."): v for k, v in m16.state_dict().items()})
+    dense = torch.rand((B, 13), device=DEV)
+    ids = torch.randint(0, 5000, (T, B), device=DEV)
+    labels = (torch.rand(B, device=DEV) > 0.5).float()
+    o16 = m16(dense, ids)
+    l16 = torch.nn.functional.binary_cross_entropy(o16, labels)
+    l16.backward()
+    with torch.no_grad():
+        o32 = m32(dense, ids)
+    for ev in evs + wide:
+        ev.pending_grads.clear()
+    assert (o16 - o32).abs().max() <= 2e-2
+    for p in m16.parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all()

@@ -62,7 +62,7 @@ def main():
             ev = dr.EmbeddingVariable("msw%d" % t, 1, 0.0, capacity=R + (1 << 19), device=dev)
             ev.insert_synthetic(0, R, seed=5000 + t)
             wide.append(ev)
-        model = mz.DeepFM(evs, wide).to(dev)
+        model = mz.DeepFM(evs, wide, bf16=args.bf16).to(dev)
     torch.cuda.synchronize()
     print("[model_step] tables ready in %.1fs" % (time.perf_counter() - t0), file=sys.stderr,
           flush=True)
