@@ -438,6 +438,11 @@ __global__ __launch_bounds__(256) void rows_work_kernel(
       lim = c0 + kRowsChunk;
     }
     if (lim > N) lim = N;
+    // a one-position run (the common case under uniform keys when the
+    // run's value needs arithmetic, e.g. unaligned rows): one row load
+    // instead of a CH-position speculative chunk
+    const bool single = first && !islong &&
+                        (c0 + 1 >= N || skey[c0 + 1] != u || tab_of(sk, T, perm[c0 + 1]) != t);
     const dr_pool_grad_desc& d = sd[t];
     const int mode = d.combiner == DR_COMBINER_SUM ? 0 : (d.combiner == DR_COMBINER_MEAN ? 1 : 2);
     const bool zero_start = mode == 0 || (W && d.weights);
@@ -452,7 +457,28 @@ __global__ __launch_bounds__(256) void rows_work_kernel(
     const int64_t kt0 = sk[t];
     const int64_t nnz_t = d.nnz;
     bool cbad = false;
-    for (int64_t p = c0; p < lim; p += CH) {
+    if (single) {
+      const int64_t k = (int64_t)perm[c0] - kt0;
+      int64_t r = segp ? segp[k * sst] : k;
+      const bool okr = (r >= 0) & (r < B);
+      cbad = !okr;
+      r = okr ? r : -1;
+      R y;
+      load_row_u<VEC, G, CPL>(y, tg + (okr ? r : 0) * ts, lg, dv);
+      if (r < 0) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) y.v[c] = vzero<V>();
+      }
+      if (W && d.weights)
+        wscaled(y, d, r, k);
+      else
+        scaled(y, d, mode, r);
+      if (fresh)
+        acc = y;
+      else
+        acc_add(acc, y);
+    }
+    for (int64_t p = c0; !single && p < lim; p += CH) {
       R y[CH];
       int64_t ry[CH];
       int64_t ky[W ? CH : 1];
@@ -919,7 +945,9 @@ int dr_pool_grad_rows_grouped_ex(const dr_pool_grad_desc* descs_host, int num_ta
     else
       launch_rows<4, 64, 4>(g, num_tables, batch, w, dim, weighted, grad_ptr, grad_unique, s, st);
   } else {
-    if (dim <= 32)
+    if (dim <= 4)   // wide (linear) tables: dim 1
+      launch_rows<1, 4, 1>(g, num_tables, batch, w, dim, weighted, grad_ptr, grad_unique, s, st);
+    else if (dim <= 32)
       launch_rows<1, 32, 1>(g, num_tables, batch, w, dim, weighted, grad_ptr, grad_unique, s, st);
     else if (dim <= 64)
       launch_rows<1, 64, 1>(g, num_tables, batch, w, dim, weighted, grad_ptr, grad_unique, s, st);
@@ -950,6 +978,9 @@ int dr_rows_from_ptr(const uint64_t* grad_ptr, int64_t n, const int64_t* n_dev, 
     else
       hipLaunchKernelGGL((rows_from_ptr_kernel<4, 64, 4>), dim3((unsigned)ceil_div(n, 4)),
                          dim3(256), 0, s, grad_ptr, n, n_dev, dim, out);
+  } else if (dim <= 4) {
+    hipLaunchKernelGGL((rows_from_ptr_kernel<1, 4, 1>), dim3((unsigned)ceil_div(n, 64)),
+                       dim3(256), 0, s, grad_ptr, n, n_dev, dim, out);
   } else if (dim <= 32) {
     hipLaunchKernelGGL((rows_from_ptr_kernel<1, 32, 1>), dim3((unsigned)ceil_div(n, 8)),
                        dim3(256), 0, s, grad_ptr, n, n_dev, dim, out);

@@ -76,18 +76,21 @@ def _feature_set(dr, rng, tag, F, B, D, onehot, vocab, shared_keys):
     return evs, sps, raw
 
 
+@pytest.mark.parametrize("D", [32, 1, 18])
 @pytest.mark.parametrize("onehot", [True, False])
 @pytest.mark.parametrize("comb", ["sum", "mean", "sqrtn"])
-def test_rows_backward_matches_segment_grad(dr, orc, onehot, comb):
+def test_rows_backward_matches_segment_grad(dr, orc, onehot, comb, D):
     """Grouped rows path vs the oracle Unique + SparseSegment*Grad: indices
     (first-occurrence order), U and values bit-exact.  Every feature inserts
     the same keys in the same order, so equal rows recur across tables (the
     regrouping must split runs at table boundaries)."""
+    # D = 1 / 18: unaligned rows (wide tables; every run through the
+    # worklist, one-position runs on its single-row path)
     rng = np.random.default_rng(101 + int(onehot))
-    B, D, F = 300, 32, 4
+    B, F = 300, 4
     shared = rng.integers(0, 90, B).astype(np.int64) if onehot else None
-    evs, sps, raw = _feature_set(dr, rng, "rbw_%d_%s" % (int(onehot), comb), F, B, D, onehot,
-                                 120, shared)
+    evs, sps, raw = _feature_set(dr, rng, "rbw_%d_%s_%d" % (int(onehot), comb, D), F, B, D,
+                                 onehot, 120, shared)
     out = dr.embedding_lookup_sparse_multi(evs, sps, combiner=comb)
     g = rng.standard_normal((B, F * D)).astype(np.float32)
     out.backward(T(g))
@@ -136,7 +139,7 @@ def test_rows_backward_single_feature_weighted(dr, orc):
         np.testing.assert_array_equal(H(out), H(out2))
 
 
-@pytest.mark.parametrize("D", [18, 32])
+@pytest.mark.parametrize("D", [18, 32, 1])
 def test_rows_backward_long_runs(dr, orc, D):
     """Hot ids: runs of 5000 / 256 / 257 / 768 / 200 / 511 positions.  Runs of
     <= 256 positions are bit-exact; longer ones are ordered chunk partials

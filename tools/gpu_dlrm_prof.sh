@@ -3,7 +3,7 @@ set -o pipefail
 T=${1:-dlrmp}
 mkdir -p gpurun_out/$T
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/prof -o run -- python3 tools/model_step.py --model dlrm --bf16 --steps 6 --warmup 3 > gpurun_out/$T/step.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/prof -o run -- python3 tools/model_step.py ${MS_ARGS:---model dlrm --bf16} --steps 6 --warmup 3 > gpurun_out/$T/step.log 2>&1 || exit 1
 f=$(find gpurun_out/$T/prof -name "*kernel_stats.csv" | head -1)
 python3 - "$f" <<'PY'
 import csv, sys
