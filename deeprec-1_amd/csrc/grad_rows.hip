@@ -283,7 +283,7 @@ __global__ __launch_bounds__(256) void rows_emit_kernel(
     const int64_t* __restrict__ total, int defer, int64_t* __restrict__ uniq_out,
     int64_t* __restrict__ num_unique, int32_t* __restrict__ base, uint64_t* __restrict__ gptr,
     int32_t* __restrict__ work, int32_t* __restrict__ nwork, const int64_t* __restrict__ rowsel,
-    int64_t* __restrict__ urows, int* st) {
+    int64_t* __restrict__ urows, int* st, int dim, float* __restrict__ gu) {
   __shared__ dr_pool_grad_desc sd[DR_MAX_GROUP];
   if (threadIdx.x < T) sd[threadIdx.x] = g.d[threadIdx.x];
   __syncthreads();
@@ -316,10 +316,40 @@ __global__ __launch_bounds__(256) void rows_emit_kernel(
       const int mode = d.combiner == DR_COMBINER_SUM ? 0 : 1;
       bool dfr = defer && okr && !d.weights;
       if (dfr && mode != 0) dfr = !d.bag_off || d.bag_off[r + 1] - d.bag_off[r] == 1;
-      if (dfr)
+      if (dfr) {
         gptr[o] = (uint64_t)(uintptr_t)(d.top_grad + r * d.top_stride) | (mode == 0 ? 1u : 0u);
-      else
+      } else if (dim <= 4 && okr) {
+        // narrow rows (wide / linear tables): the run's value formed right
+        // here, with rows_work_kernel's single-row arithmetic (the 0 + x of
+        // a zero-started sum, the mean / sqrtn scale, weights / bag scale),
+        // instead of one worklist entry (one contended counter atomic per
+        // wave and a lane group) per position
+        const int m3 = d.combiner == DR_COMBINER_SUM ? 0 : (d.combiner == DR_COMBINER_MEAN ? 1 : 2);
+        const bool zero_start = m3 == 0 || d.weights;
+        float sc = 1.f, q = 1.f, w = 1.f;
+        if (d.weights) {
+          if (d.bag_scale) q = d.bag_scale[r];
+          w = d.weights[k];
+        } else if (m3 != 0) {
+          const int32_t cnt = d.bag_off ? d.bag_off[r + 1] - d.bag_off[r] : 1;
+          if (cnt != 1)
+            sc = m3 == 2 ? (float)(1.0 / sqrt((double)cnt)) : (float)(1.0 / (double)cnt);
+        }
+        float* dst = gu + o * (int64_t)dim;
+        for (int c = 0; c < dim; ++c) {
+          float y = d.top_grad[r * d.top_stride + c];
+          if (d.weights) {
+            if (d.bag_scale) y = y / q;
+            y = y * w;
+          } else if (m3 != 0 && sc != 1.f) {
+            y = y * sc;
+          }
+          dst[c] = zero_start ? 0.f + y : y;
+        }
+        gptr[o] = (uint64_t)(uintptr_t)dst;
+      } else {
         push = true;   // (an invalid bag latches there)
+      }
     }
   }
   work_push(push, (int64_t)(mk & 0x7FFFFFFF), work, nwork);
@@ -930,7 +960,7 @@ int dr_pool_grad_rows_grouped_ex(const dr_pool_grad_desc* descs_host, int num_ta
   if (rc) return rc;
   hipLaunchKernelGGL(rows_emit_kernel, dim3(nb), dim3(256), 0, s, g, num_tables, batch, keys,
                      w.flags, w.ex, w.total, defer, uniq_out, num_unique, w.base, grad_ptr, w.work,
-                     w.nwork, rowsel, uniq_rows, st);
+                     w.nwork, rowsel, uniq_rows, st, dim, grad_unique);
   DR_LAUNCH_CHECK();
   if (aligned) {
     const int d4 = dim / 4;

@@ -106,13 +106,15 @@ def test_rows_backward_matches_segment_grad(dr, orc, onehot, comb, D):
         np.testing.assert_array_equal(H(sl.values[:U]), ref)
 
 
-def test_rows_backward_single_feature_weighted(dr, orc):
+@pytest.mark.parametrize("D", [16, 1])
+def test_rows_backward_single_feature_weighted(dr, orc, D):
     """One EV feature with weights (embedding_lookup_sparse, not the multi
-    API) through the rows path: the weighted grad is materialised."""
+    API) through the rows path: the weighted grad is materialised (D = 1:
+    formed in the emit pass, no worklist)."""
     rng = np.random.default_rng(7)
-    B, D = 80, 16
+    B = 80
     for comb in ("sum", "mean", "sqrtn"):
-        ev = dr.EmbeddingVariable("rw_" + comb, D, 0.2)
+        ev = dr.EmbeddingVariable("rw_%s_%d" % (comb, D), D, 0.2)
         ind, v, shape = _sparse(rng, B, 6, 50)
         w = rng.uniform(0.5, 2.0, v.size).astype(np.float32)
         out = dr.embedding_lookup_sparse(ev, dr.SparseTensor(T(ind), T(v), shape),
@@ -125,7 +127,7 @@ def test_rows_backward_single_feature_weighted(dr, orc):
         got = H(sl.values[:U])
         keys = H(sl.indices[:U])
         # the same lookup on the Unique path is the reference of this check
-        ev2 = dr.EmbeddingVariable("rw2_" + comb, D, 0.2)
+        ev2 = dr.EmbeddingVariable("rw2_%s_%d" % (comb, D), D, 0.2)
         with _Path(False):
             out2 = dr.embedding_lookup_sparse(ev2, dr.SparseTensor(T(ind), T(v), shape),
                                               sp_weights=dr.SparseTensor(T(ind), T(w), shape),

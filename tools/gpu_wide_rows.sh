@@ -6,7 +6,7 @@ T=${1:-wide}
 mkdir -p gpurun_out/$T
 timeout -k 10 400 python -u -m pytest tests/test_gpu_rows_grad.py tests/test_gpu_rows_sgd_fused.py tests/test_gpu_parity.py tests/test_gpu_modelzoo.py -x -q --timeout 150 --timeout-method thread > gpurun_out/$T/tests.log 2>&1
 rc=$?; tail -3 gpurun_out/$T/tests.log; [ $rc -ne 0 ] && exit $rc
-for F in "--bf16" "--bf16"; do
+for F in "--bf16" "--bf16"; do  # after the emit change
   timeout -k 10 300 python tools/model_step.py --model deepfm --rows 10000000 --dim 64 $F --steps 10 --warmup 3 > gpurun_out/$T/ms.log 2>&1 || exit 1
   echo "$F $(grep '^{' gpurun_out/$T/ms.log)" | tee -a gpurun_out/$T/ab.log
 done
