@@ -10,8 +10,10 @@
 namespace dr {
 
 // out[b, d] = 0.5 * ((sum_f e)^2 - sum_f e^2); thread per (b, 4 columns).
+// ecopy (nullable): also the bf16 copy of emb [B, F*D] -- DeepFM's --bf16
+// dnn input (train.py:186-189) written from the loads the sum already makes.
 __global__ void fm2_kernel(const float* __restrict__ emb, int64_t B, int F, int D,
-                           float* __restrict__ out) {
+                           float* __restrict__ out, uint16_t* __restrict__ ecopy = nullptr) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int D4 = D / 4;
   if (t >= B * D4) return;
@@ -19,10 +21,12 @@ __global__ void fm2_kernel(const float* __restrict__ emb, int64_t B, int F, int 
   const int c = (int)(t % D4);
   const float4* p = reinterpret_cast<const float4*>(emb + b * (int64_t)F * D) + c;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
+  uint2* cp = ecopy ? reinterpret_cast<uint2*>(ecopy + b * (int64_t)F * D) + c : nullptr;
   for (int f = 0; f < F; ++f) {
     const float4 e = p[(int64_t)f * D4];
     s.x += e.x; s.y += e.y; s.z += e.z; s.w += e.w;
     q.x += e.x * e.x; q.y += e.y * e.y; q.z += e.z * e.z; q.w += e.w * e.w;
+    if (cp) cp[(int64_t)f * D4] = make_uint2(f2_to_bf16x2(e.x, e.y), f2_to_bf16x2(e.z, e.w));
   }
   float4 o;
   o.x = 0.5f * (s.x * s.x - q.x);
@@ -35,10 +39,15 @@ __global__ void fm2_kernel(const float* __restrict__ emb, int64_t B, int F, int 
 // d fm / d e_f = (sum_f' e_f' - e_f) * g.  Thread per (b, 4 columns); the F
 // field vectors stay in registers between the sum and the write (a second
 // read pass went back to HBM: the in-flight working set outgrows L2).
+// add (nullable): a bf16 gradient of the same [B, F*D] embedding from its
+// other use (DeepFM's bf16 dnn input), added after the FM term -- the one
+// fp32 add autograd does where the two uses meet.
 template <int FM>
 __global__ __launch_bounds__(256) void fm2_grad_kernel(const float* __restrict__ emb,
                                                        const float* __restrict__ g, int64_t B,
-                                                       int F, int D, float* __restrict__ ge) {
+                                                       int F, int D, float* __restrict__ ge,
+                                                       const uint16_t* __restrict__ add = nullptr,
+                                                       int64_t add_stride = 0) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int D4 = D / 4;
   if (t >= B * D4) return;
@@ -57,6 +66,13 @@ __global__ __launch_bounds__(256) void fm2_grad_kernel(const float* __restrict__
     }
   const float4 gv = reinterpret_cast<const float4*>(g + b * (int64_t)D)[c];
   float4* q = reinterpret_cast<float4*>(ge + b * (int64_t)F * D) + c;
+  const uint2* ap = add ? reinterpret_cast<const uint2*>(add + b * add_stride) + c : nullptr;
+  uint2 av[FM];
+  if (ap) {
+#pragma unroll
+    for (int f = 0; f < FM; ++f)
+      if (f < F) av[f] = ap[(int64_t)f * D4];
+  }
 #pragma unroll
   for (int f = 0; f < FM; ++f)
     if (f < F) {
@@ -65,6 +81,13 @@ __global__ __launch_bounds__(256) void fm2_grad_kernel(const float* __restrict__
       o.y = (s.y - e[f].y) * gv.y;
       o.z = (s.z - e[f].z) * gv.z;
       o.w = (s.w - e[f].w) * gv.w;
+      if (ap) {
+        const float2 a0 = bf16x2_to_f2(av[f].x), a1 = bf16x2_to_f2(av[f].y);
+        o.x = o.x + a0.x;
+        o.y = o.y + a0.y;
+        o.z = o.z + a1.x;
+        o.w = o.w + a1.y;
+      }
       nt_store(o, q + (int64_t)f * D4);
     }
 }
@@ -1469,7 +1492,48 @@ int dr_fm2(const float* emb, int64_t batch, int fields, int dim, float* out, voi
   if (batch == 0) return DR_OK;
   const int64_t n = batch * (dim / 4);
   hipLaunchKernelGGL(fm2_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, S(stream), emb,
-                     batch, fields, dim, out);
+                     batch, fields, dim, out, (uint16_t*)nullptr);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_fm2_bf16_copy(const float* emb, int64_t batch, int fields, int dim, float* out,
+                     uint16_t* emb_bf16, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && fields > 0 && dim > 0 && dim % 4 == 0 && emb_bf16, DR_INVALID_ARGUMENT,
+             "dr_fm2_bf16_copy: dim must be a multiple of 4");
+  DR_REQUIRE(((((uintptr_t)emb) | ((uintptr_t)out)) & 15) == 0 && ((uintptr_t)emb_bf16 & 7) == 0,
+             DR_INVALID_ARGUMENT, "dr_fm2_bf16_copy: emb / out 16-B, emb_bf16 8-B aligned");
+  if (batch == 0) return DR_OK;
+  const int64_t n = batch * (dim / 4);
+  hipLaunchKernelGGL(fm2_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, S(stream), emb,
+                     batch, fields, dim, out, emb_bf16);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_fm2_grad_add_bf16(const float* emb, const float* top_grad, const uint16_t* add,
+                         int64_t add_stride, int64_t batch, int fields, int dim, float* grad_emb,
+                         void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && fields > 0 && fields <= 32 && dim > 0 && dim % 4 == 0 && add &&
+                 add_stride >= (int64_t)fields * dim && add_stride % 4 == 0,
+             DR_INVALID_ARGUMENT,
+             "dr_fm2_grad_add_bf16: fields <= 32, dim %% 4 == 0, add_stride >= fields*dim, %% 4");
+  DR_REQUIRE(((((uintptr_t)emb) | ((uintptr_t)top_grad) | ((uintptr_t)grad_emb)) & 15) == 0 &&
+                 ((uintptr_t)add & 7) == 0,
+             DR_INVALID_ARGUMENT, "dr_fm2_grad_add_bf16: pointers 16-B (add: 8-B) aligned");
+  if (batch == 0) return DR_OK;
+  const unsigned blocks = (unsigned)ceil_div(batch * (dim / 4), 256);
+  if (fields <= 8)
+    hipLaunchKernelGGL(fm2_grad_kernel<8>, dim3(blocks), dim3(256), 0, S(stream), emb, top_grad,
+                       batch, fields, dim, grad_emb, add, add_stride);
+  else if (fields <= 16)
+    hipLaunchKernelGGL(fm2_grad_kernel<16>, dim3(blocks), dim3(256), 0, S(stream), emb, top_grad,
+                       batch, fields, dim, grad_emb, add, add_stride);
+  else
+    hipLaunchKernelGGL(fm2_grad_kernel<32>, dim3(blocks), dim3(256), 0, S(stream), emb, top_grad,
+                       batch, fields, dim, grad_emb, add, add_stride);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }
@@ -1484,13 +1548,15 @@ int dr_fm2_grad(const float* emb, const float* top_grad, int64_t batch, int fiel
     const unsigned blocks = (unsigned)ceil_div(batch * (dim / 4), 256);
     if (fields <= 8)
       hipLaunchKernelGGL(fm2_grad_kernel<8>, dim3(blocks), dim3(256), 0, S(stream), emb, top_grad,
-                         batch, fields, dim, grad_emb);
+                         batch, fields, dim, grad_emb, (const uint16_t*)nullptr, (int64_t)0);
     else if (fields <= 16)
       hipLaunchKernelGGL(fm2_grad_kernel<16>, dim3(blocks), dim3(256), 0, S(stream), emb,
-                         top_grad, batch, fields, dim, grad_emb);
+                         top_grad, batch, fields, dim, grad_emb, (const uint16_t*)nullptr,
+                         (int64_t)0);
     else
       hipLaunchKernelGGL(fm2_grad_kernel<32>, dim3(blocks), dim3(256), 0, S(stream), emb,
-                         top_grad, batch, fields, dim, grad_emb);
+                         top_grad, batch, fields, dim, grad_emb, (const uint16_t*)nullptr,
+                         (int64_t)0);
   } else {
     hipLaunchKernelGGL(fm2_grad_any_kernel, dim3((unsigned)ceil_div(batch * dim, 256)), dim3(256),
                        0, S(stream), emb, top_grad, batch, fields, dim, grad_emb);

@@ -224,6 +224,8 @@ SIGNATURES = {
     "dr_xgmi_grad_pull_dev": (_I32, [_P, _P, _I32, _I64, _I32, _P, _P, _P, _P, _SZ, _P]),
     "dr_fm2": (_I32, [_P, _I64, _I32, _I32, _P, _P]),
     "dr_fm2_grad": (_I32, [_P, _P, _I64, _I32, _I32, _P, _P]),
+    "dr_fm2_bf16_copy": (_I32, [_P, _I64, _I32, _I32, _P, _P, _P]),
+    "dr_fm2_grad_add_bf16": (_I32, [_P, _P, _P, _I64, _I64, _I32, _I32, _P, _P]),
     "dr_dot_interaction": (_I32, [_P, _I64, _I32, _I32, _P, _P]),
     "dr_dot_interaction_grad": (_I32, [_P, _P, _I64, _I32, _I32, _P, _P]),
     "dr_dot_interaction_concat_bf16": (_I32, [_P, _I64, _I32, _I32, _P, _I64, _P]),

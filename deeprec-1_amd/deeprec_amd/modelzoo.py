@@ -64,6 +64,30 @@ class DotConcatBf16(torch.autograd.Function):
         return ops.dot_interaction_concat_grad_bf16(x, g.to(torch.bfloat16)), None
 
 
+class FMSecondOrderBf16Copy(torch.autograd.Function):
+    """DeepFM --bf16 input side as one node: emb [B, F, D] fp32 -> (the FM
+    second-order term, fp32, and the bf16 dnn input [B, F*D]); backward: the
+    FM gradient plus the dnn input's bf16 gradient in one pass
+    (dr_fm2_bf16_copy / dr_fm2_grad_add_bf16)."""
+
+    @staticmethod
+    def forward(ctx, emb):
+        ctx.save_for_backward(emb)
+        return ops.fm_second_order_bf16_copy(emb)
+
+    @staticmethod
+    def backward(ctx, g_fm, g_h):
+        (emb,) = ctx.saved_tensors
+        B, F, D = emb.shape
+        if g_fm is None:
+            g_fm = torch.zeros((B, D), dtype=torch.float32, device=emb.device)
+        if g_h is None:
+            return ops.fm_second_order_grad(emb, g_fm)
+        if g_h.stride(1) != 1:
+            g_h = g_h.contiguous()
+        return ops.fm_second_order_grad_add_bf16(emb, g_fm, g_h.to(torch.bfloat16))
+
+
 class FMSecondOrder(torch.autograd.Function):
     """dr_fm2 / dr_fm2_grad."""
 
@@ -228,8 +252,10 @@ class _MfmaMLP(torch.nn.Module):
         if not self.mfma_ok(B):
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 return self.net(x).float()
-        h = torch.nn.functional.pad(x.to(torch.bfloat16), (0, self.kp - K))
-        return self.forward_padded(h)
+        h = x.to(torch.bfloat16)
+        if self.kp != K:
+            h = torch.nn.functional.pad(h, (0, self.kp - K))
+        return self.forward_padded(h.contiguous())
 
     def forward_padded(self, h):
         """The tower on an input already in bf16 and zero-padded to kp columns."""
@@ -338,9 +364,20 @@ class DeepFM(torch.nn.Module):
         emb = self.lookup(ids)                                     # [B, T*D]
         wide = self.wide_lookup(ids)                               # [B, T]
         linear = wide.sum(1, keepdim=True)
-        fm = FMSecondOrder.apply(emb.view(B, self.T, self.dim))
-        net = self.bf16(self.final, torch.cat([self.bf16(self.dnn, emb), linear, fm], 1))
+        if (self.fuse_fm_copy and isinstance(self.dnn, _MfmaMLP) and self.dnn.mfma_ok(B)
+                and self.dnn.kp == self.T * self.dim and self.dim % 4 == 0 and self.T <= 32):
+            # FM + the dnn input's bf16 cast in one pass (no cast / pad copies,
+            # no separate add of the two embedding gradients)
+            fm, h0 = FMSecondOrderBf16Copy.apply(emb.view(B, self.T, self.dim))
+            dnn_out = self.dnn.forward_padded(h0)
+        else:
+            fm = FMSecondOrder.apply(emb.view(B, self.T, self.dim))
+            dnn_out = self.bf16(self.dnn, emb)
+        net = self.bf16(self.final, torch.cat([dnn_out, linear, fm], 1))
         return torch.sigmoid(self.last(net)).squeeze(1)
+
+    # A/B switch DR_DEEPFM_FUSE_FM_COPY=0 = the composed FM + cast + pad path
+    fuse_fm_copy = os.environ.get("DR_DEEPFM_FUSE_FM_COPY", "1") != "0"
 
 
 class DinAttentionInput(torch.autograd.Function):

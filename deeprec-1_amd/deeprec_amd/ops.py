@@ -502,6 +502,33 @@ def fm_second_order_grad(emb, top_grad):
     return out
 
 
+def fm_second_order_bf16_copy(emb):
+    """dr_fm2_bf16_copy: (fm [B, D] fp32, bf16 copy of emb as [B, F*D])."""
+    dev = _dev(emb)
+    emb = _c(emb, torch.float32)
+    B, F, D = emb.shape
+    out = torch.empty((B, D), dtype=torch.float32, device=dev)
+    cp = torch.empty((B, F * D), dtype=torch.bfloat16, device=dev)
+    check(lib().dr_fm2_bf16_copy(ptr(emb), B, F, D, ptr(out), ptr(cp), stream_handle(dev)))
+    _post(dev)
+    return out, cp
+
+
+def fm_second_order_grad_add_bf16(emb, top_grad, add):
+    """dr_fm2_grad_add_bf16: FM gradient + float(add) (add bf16 [B, F*D])."""
+    dev = _dev(emb)
+    emb = _c(emb, torch.float32)
+    g = _c(top_grad, torch.float32)
+    B, F, D = emb.shape
+    if add.dtype != torch.bfloat16 or add.stride(1) != 1:
+        raise ValueError("add must be bf16 with unit column stride")
+    out = torch.empty_like(emb)
+    check(lib().dr_fm2_grad_add_bf16(ptr(emb), ptr(g), ptr(add), add.stride(0), B, F, D, ptr(out),
+                                     stream_handle(dev)))
+    _post(dev)
+    return out
+
+
 def dot_interaction(x):
     """DLRM dot_op (DLRM train.py:150-163): strictly-lower triangle of X X^T."""
     dev = _dev(x)

@@ -830,6 +830,15 @@ int dr_xgmi_grad_pull_dev(const dr_xgmi_peers* peers, const float* const* grad_i
 int dr_fm2(const float* emb, int64_t batch, int fields, int dim, float* out, void* stream);
 int dr_fm2_grad(const float* emb, const float* top_grad, int64_t batch, int fields, int dim,
                 float* grad_emb, void* stream);
+/* DeepFM --bf16 (train.py:186-189: the dnn input cast to bf16): dr_fm2 that  */
+/* also writes emb_bf16 [B, F*D] = bf16(emb) from the same loads, and the FM  */
+/* backward that adds the bf16 gradient of that copy (row stride add_stride) */
+/* after the FM term -- the single fp32 add where the two uses meet.         */
+int dr_fm2_bf16_copy(const float* emb, int64_t batch, int fields, int dim, float* out,
+                     uint16_t* emb_bf16, void* stream);
+int dr_fm2_grad_add_bf16(const float* emb, const float* top_grad, const uint16_t* add,
+                         int64_t add_stride, int64_t batch, int fields, int dim, float* grad_emb,
+                         void* stream);
 /* DLRM dot (modelzoo/DLRM/train.py:150-163): X [B,F,D] -> [B, F(F-1)/2].   */
 int dr_dot_interaction(const float* x, int64_t batch, int fields, int dim, float* out,
                        void* stream);

@@ -375,3 +375,35 @@ def test_deepfm_bf16_towers_track_fp32(dr):
     assert (o16 - o32).abs().max() <= 2e-2
     for p in m16.parameters():
         assert p.grad is not None and torch.isfinite(p.grad).all()
+
+
+def test_deepfm_bf16_fused_fm_copy_matches_composed(dr):
+    """DeepFM --bf16: FM + dnn-input cast in one node (dr_fm2_bf16_copy /
+    dr_fm2_grad_add_bf16) = the composed FM, cast and gradient add, bit for
+    bit (prediction, dense gradients, queued EV gradients)."""
+    from deeprec_amd import modelzoo as mz
+    torch.manual_seed(23)
+    T, D, B = 26, 64, 1024
+    evs = [dr.EmbeddingVariable("dfm_fc_%d" % t, D, 0.01, device=DEV) for t in range(T)]
+    wide = [dr.EmbeddingVariable("dfm_fcw_%d" % t, 1, 0.0, device=DEV) for t in range(T)]
+    model = mz.DeepFM(evs, wide, bf16=True).to(DEV)
+    dense = torch.rand((B, 13), device=DEV)
+    ids = torch.randint(0, 5000, (T, B), device=DEV)
+    runs = []
+    for fuse in (True, False):
+        model.fuse_fm_copy = fuse
+        model.zero_grad(set_to_none=True)
+        out = model(dense, ids)
+        out.sum().backward()
+        sl = [ev.pending_grads[-1] for ev in evs]
+        nv = [s.indices.numel() if s.num_valid is None else int(s.num_valid.item()) for s in sl]
+        runs.append((out.detach().clone(), [p.grad.clone() for p in model.parameters()],
+                     [s.values[:n].clone() for s, n in zip(sl, nv)]))
+        for ev in evs + wide:
+            ev.pending_grads.clear()
+    (o1, g1, v1), (o2, g2, v2) = runs
+    assert torch.equal(o1, o2)
+    for a, b in zip(g1, g2):
+        assert torch.equal(a, b)
+    for a, b in zip(v1, v2):
+        assert torch.equal(a, b)
