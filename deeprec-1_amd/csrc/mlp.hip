@@ -464,9 +464,31 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const uint16_t* __r
 // sum is in a fixed order (8 columns per lane, then an xor butterfly; rows
 // of a block in a fixed lane / LDS order), so results are deterministic.
 // ---------------------------------------------------------------------------
-template <int L>
+// F32: the fp32 output layer on a bf16-computed tower (DeepFM --bf16,
+// train.py:213-221: the tower output cast to fp32, then dense(units=1) in
+// fp32): w fp32, the logit and gz unrounded.  h is read as bf16 either way
+// (its fp32 widening is exact).
+template <bool F32>
+__device__ __forceinline__ void head_w8(const void* w, int lc, float (&wf)[8]) {
+  if constexpr (F32) {
+    const float4 a = reinterpret_cast<const float4*>(w)[lc * 2];
+    const float4 b = reinterpret_cast<const float4*>(w)[lc * 2 + 1];
+    wf[0] = a.x; wf[1] = a.y; wf[2] = a.z; wf[3] = a.w;
+    wf[4] = b.x; wf[5] = b.y; wf[6] = b.z; wf[7] = b.w;
+  } else {
+    const mu32x4 wv = *reinterpret_cast<const mu32x4*>(static_cast<const uint16_t*>(w) + lc * 8);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float2 c = bf16x2_to_f2(wv[e]);
+      wf[2 * e] = c.x;
+      wf[2 * e + 1] = c.y;
+    }
+  }
+}
+
+template <int L, bool F32>
 __global__ __launch_bounds__(256) void head_fwd_kernel(const uint16_t* __restrict__ h, int64_t ldh,
-                                                       int64_t B, const uint16_t* __restrict__ w,
+                                                       int64_t B, const void* __restrict__ w,
                                                        const float* __restrict__ bias,
                                                        float* __restrict__ z) {
   constexpr int RPB = 256 / L;  // rows per block
@@ -475,22 +497,24 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const uint16_t* __restric
   const int64_t b = (int64_t)blockIdx.x * RPB + tid / L;
   const bool ok = b < B;
   const mu32x4 hv = *reinterpret_cast<const mu32x4*>(h + (ok ? b : 0) * ldh + lc * 8);
-  const mu32x4 wv = *reinterpret_cast<const mu32x4*>(w + lc * 8);
+  float wf[8];
+  head_w8<F32>(w, lc, wf);
   float s = 0.f;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const float2 a = bf16x2_to_f2(hv[e]), c = bf16x2_to_f2(wv[e]);
-    s = fmaf(a.x, c.x, s);
-    s = fmaf(a.y, c.y, s);
+    const float2 a = bf16x2_to_f2(hv[e]);
+    s = fmaf(a.x, wf[2 * e], s);
+    s = fmaf(a.y, wf[2 * e + 1], s);
   }
 #pragma unroll
   for (int m = 1; m < L; m <<= 1) s += __shfl_xor(s, m, 64);
-  if (ok && lc == 0) z[b] = bf16_to_f32(bf16_rne(bias ? s + *bias : s));
+  const float zz = bias ? s + *bias : s;
+  if (ok && lc == 0) z[b] = F32 ? zz : bf16_to_f32(bf16_rne(zz));
 }
 
-template <int L>
+template <int L, bool F32>
 __global__ __launch_bounds__(256) void head_bwd_kernel(const uint16_t* __restrict__ h, int64_t ldh,
-                                                       int64_t B, const uint16_t* __restrict__ w,
+                                                       int64_t B, const void* __restrict__ w,
                                                        const float* __restrict__ gz,
                                                        uint16_t* __restrict__ dh, int64_t lddh,
                                                        int rows_per_block,
@@ -502,14 +526,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const uint16_t* __restric
   __shared__ float redb[RPS];
   const int tid = threadIdx.x;
   const int lc = tid % L, rs = tid / L;
-  const mu32x4 wv = *reinterpret_cast<const mu32x4*>(w + lc * 8);
   float wf[8];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const float2 c = bf16x2_to_f2(wv[e]);
-    wf[2 * e] = c.x;
-    wf[2 * e + 1] = c.y;
-  }
+  head_w8<F32>(w, lc, wf);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float accb = 0.f;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
@@ -520,7 +538,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const uint16_t* __restric
   for (int i = rs; i < rows_per_block; i += RPS) {
     const int64_t b = r0 + i;
     if (b >= B) break;
-    const float g = bf16_to_f32(bf16_rne(gz[b]));
+    const float g = F32 ? gz[b] : bf16_to_f32(bf16_rne(gz[b]));
     const mu32x4 hv = *reinterpret_cast<const mu32x4*>(h + b * ldh + lc * 8);
     mu32x4 ov;
 #pragma unroll
@@ -680,7 +698,8 @@ size_t dr_mlp_head_grad_partials(int64_t batch) {
 }
 
 int dr_mlp_head_forward_bf16(const uint16_t* h, int64_t ldh, int64_t batch, int k,
-                             const uint16_t* w, const float* bias, float* z, void* stream) {
+                             const void* w, int w_fp32, const float* bias, float* z,
+                             void* stream) {
   using namespace dr;
   DR_REQUIRE(h && w && z && batch >= 0 && (k == 64 || k == 128 || k == 256 || k == 512) &&
                  ldh >= k && ldh % 8 == 0,
@@ -691,8 +710,14 @@ int dr_mlp_head_forward_bf16(const uint16_t* h, int64_t ldh, int64_t batch, int 
   const int L = k / 8;
   const unsigned grid = (unsigned)ceil_div(batch, 256 / L);
 #define DR_HEAD_F(LL)                                                                          \
-  hipLaunchKernelGGL(head_fwd_kernel<LL>, dim3(grid), dim3(256), 0, S(stream), h, ldh, batch, w, \
-                     bias, z)
+  do {                                                                                         \
+    if (w_fp32)                                                                                \
+      hipLaunchKernelGGL((head_fwd_kernel<LL, true>), dim3(grid), dim3(256), 0, S(stream), h,   \
+                         ldh, batch, w, bias, z);                                              \
+    else                                                                                       \
+      hipLaunchKernelGGL((head_fwd_kernel<LL, false>), dim3(grid), dim3(256), 0, S(stream), h,  \
+                         ldh, batch, w, bias, z);                                              \
+  } while (0)
   if (L == 8) DR_HEAD_F(8);
   else if (L == 16) DR_HEAD_F(16);
   else if (L == 32) DR_HEAD_F(32);
@@ -703,7 +728,7 @@ int dr_mlp_head_forward_bf16(const uint16_t* h, int64_t ldh, int64_t batch, int 
 }
 
 int dr_mlp_head_backward_bf16(const uint16_t* h, int64_t ldh, int64_t batch, int k,
-                              const uint16_t* w, const float* grad_z, uint16_t* grad_h,
+                              const void* w, int w_fp32, const float* grad_z, uint16_t* grad_h,
                               int64_t ld_grad_h, float* dw_partials, float* db_partials,
                               void* stream) {
   using namespace dr;
@@ -717,8 +742,16 @@ int dr_mlp_head_backward_bf16(const uint16_t* h, int64_t ldh, int64_t batch, int
   const int L = k / 8;
   const unsigned grid = (unsigned)ceil_div(batch, kHeadRows);
 #define DR_HEAD_B(LL)                                                                          \
-  hipLaunchKernelGGL(head_bwd_kernel<LL>, dim3(grid), dim3(256), 0, S(stream), h, ldh, batch, w, \
-                     grad_z, grad_h, ld_grad_h, kHeadRows, dw_partials, db_partials)
+  do {                                                                                         \
+    if (w_fp32)                                                                                \
+      hipLaunchKernelGGL((head_bwd_kernel<LL, true>), dim3(grid), dim3(256), 0, S(stream), h,   \
+                         ldh, batch, w, grad_z, grad_h, ld_grad_h, kHeadRows, dw_partials,     \
+                         db_partials);                                                         \
+    else                                                                                       \
+      hipLaunchKernelGGL((head_bwd_kernel<LL, false>), dim3(grid), dim3(256), 0, S(stream), h,  \
+                         ldh, batch, w, grad_z, grad_h, ld_grad_h, kHeadRows, dw_partials,     \
+                         db_partials);                                                         \
+  } while (0)
   if (L == 8) DR_HEAD_B(8);
   else if (L == 16) DR_HEAD_B(16);
   else if (L == 32) DR_HEAD_B(32);

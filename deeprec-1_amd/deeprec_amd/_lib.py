@@ -240,13 +240,14 @@ SIGNATURES = {
                                   _I64, _I32, _I32, _P, _SZ, _P]),
     "dr_transpose_bf16": (_I32, [_P, _I64, _I64, _I64, _P, _I64, _P]),
     "dr_transpose_bf16_colsum": (_I32, [_P, _I64, _I64, _I64, _P, _I64, _P, _P]),
-    "dr_mlp_head_forward_bf16": (_I32, [_P, _I64, _I64, _I32, _P, _P, _P, _P]),
+    "dr_mlp_head_forward_bf16": (_I32, [_P, _I64, _I64, _I32, _P, _I32, _P, _P, _P]),
     "dr_mlp_head_grad_partials": (_SZ, [_I64]),
     "dr_gemm_tn_workspace_size": (_SZ, [_I64, _I64, _I32, _I32]),
     "dr_gemm_tn_bf16": (_I32, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _I32, _P, _SZ,
                                _P]),
     "dr_relu_grad_bf16": (_I32, [_P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P]),
-    "dr_mlp_head_backward_bf16": (_I32, [_P, _I64, _I64, _I32, _P, _P, _P, _I64, _P, _P, _P]),
+    "dr_mlp_head_backward_bf16": (_I32, [_P, _I64, _I64, _I32, _P, _I32, _P, _P, _I64, _P, _P,
+                                         _P]),
     "dr_crossnet_backward_elem_bf16": (_I32, [_P, _P, _P, _P, _P, _P, _P, _I64, _I32, _P, _SZ,
                                               _P]),
     "dr_din_attention_input": (_I32, [_P, _P, _I64, _I64, _I32, _P, _P]),

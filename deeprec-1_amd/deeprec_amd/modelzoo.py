@@ -172,7 +172,10 @@ class _MfmaTowerFn(torch.autograd.Function):
         ctx.L, ctx.last_act, ctx.head = L, last_act, head
         ctx.ks = [w.shape[1] for w in ws]
         if head:
-            wh = params[2 * L].detach().reshape(-1).to(torch.bfloat16)
+            # head 1: the bf16 output layer (bf16 w, rounded logit); 2: the
+            # fp32 output layer on the widened tower output (fp32 w)
+            wh = params[2 * L].detach().reshape(-1)
+            wh = wh.to(torch.bfloat16) if head == 1 else wh.float().contiguous()
             z = ops.mlp_head_forward(h, wh, params[2 * L + 1].detach())
             ctx.head_shapes = (params[2 * L].shape, params[2 * L + 1].shape)
             ctx.save_for_backward(*hs, *wbs, wh)
@@ -260,20 +263,30 @@ class _MfmaMLP(torch.nn.Module):
     def forward_padded(self, h):
         """The tower on an input already in bf16 and zero-padded to kp columns."""
         lins = [m for m in self.net if isinstance(m, torch.nn.Linear)]
-        return _MfmaTowerFn.apply(h, self.last_act, False, *[l.weight for l in lins],
+        return _MfmaTowerFn.apply(h, self.last_act, 0, *[l.weight for l in lins],
                                   *[l.bias for l in lins])
 
     def head_ok(self, head):
         return (self.last_act and isinstance(head, torch.nn.Linear) and head.out_features == 1
                 and head.bias is not None and self.sizes[-1] in (64, 128, 256, 512))
 
-    def forward_padded_head(self, h, head):
-        """forward_padded followed by the N = 1 Linear `head` (bf16, the
-        reference's dense(units=1) under --bf16) in the same node: [B, 1]
-        fp32 logit (bf16-rounded).  Needs head_ok(head)."""
+    def forward_padded_head(self, h, head, fp32=False):
+        """forward_padded followed by the N = 1 Linear `head` in the same
+        node: [B, 1] fp32 logit.  fp32=False: the bf16 layer (DLRM's
+        dense(units=1) under --bf16, bf16-rounded logit); True: an fp32
+        layer on the widened output (DeepFM's final dense).  Needs
+        head_ok(head)."""
         lins = [m for m in self.net if isinstance(m, torch.nn.Linear)]
-        return _MfmaTowerFn.apply(h, self.last_act, True, *[l.weight for l in lins],
-                                  *[l.bias for l in lins], head.weight, head.bias)
+        return _MfmaTowerFn.apply(h, self.last_act, 2 if fp32 else 1,
+                                  *[l.weight for l in lins], *[l.bias for l in lins],
+                                  head.weight, head.bias)
+
+    def forward_head(self, x, head, fp32=False):
+        """forward() (cast + zero pad of an fp32 input) then the head."""
+        h = x.to(torch.bfloat16)
+        if self.kp != x.shape[1]:
+            h = torch.nn.functional.pad(h, (0, self.kp - x.shape[1]))
+        return self.forward_padded_head(h.contiguous(), head, fp32)
 
 
 class _MaybeBF16(object):
@@ -373,8 +386,16 @@ class DeepFM(torch.nn.Module):
         else:
             fm = FMSecondOrder.apply(emb.view(B, self.T, self.dim))
             dnn_out = self.bf16(self.dnn, emb)
-        net = self.bf16(self.final, torch.cat([dnn_out, linear, fm], 1))
+        cat = torch.cat([dnn_out, linear, fm], 1)
+        if (self.fuse_head and isinstance(self.final, _MfmaMLP) and self.final.mfma_ok(B)
+                and self.final.head_ok(self.last)):
+            # the fp32 output layer (train.py:219) riding on the final tower
+            return torch.sigmoid(self.final.forward_head(cat, self.last, fp32=True)).squeeze(1)
+        net = self.bf16(self.final, cat)
         return torch.sigmoid(self.last(net)).squeeze(1)
+
+    # A/B switch DR_DEEPFM_FUSE_HEAD=0 = torch's fp32 Linear
+    fuse_head = os.environ.get("DR_DEEPFM_FUSE_HEAD", "1") != "0"
 
     # A/B switch DR_DEEPFM_FUSE_FM_COPY=0 = the composed FM + cast + pad path
     fuse_fm_copy = os.environ.get("DR_DEEPFM_FUSE_FM_COPY", "1") != "0"

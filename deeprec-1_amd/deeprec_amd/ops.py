@@ -595,25 +595,28 @@ def relu_grad_bf16(g, y):
     return out
 
 
-def mlp_head_forward(h, w_bf16, bias=None):
-    """dr_mlp_head_forward_bf16: the N = 1 output layer on the bf16 top-MLP
-    output h [B, K] -> z [B] fp32 (a bf16-rounded logit); bias a 1-element
-    fp32 device tensor or None."""
+def mlp_head_forward(h, w, bias=None):
+    """dr_mlp_head_forward_bf16: the N = 1 output layer on the bf16 tower
+    output h [B, K] -> z [B] fp32.  w bf16: the bf16 layer (a bf16-rounded
+    logit); w fp32: the fp32 layer on the widened h.  bias a 1-element fp32
+    device tensor or None."""
     dev = _dev(h)
     B, K = h.shape
-    if h.dtype != torch.bfloat16 or h.stride(1) != 1 or w_bf16.dtype != torch.bfloat16:
-        raise ValueError("mlp_head_forward needs bf16 h (unit column stride) and bf16 w")
+    if h.dtype != torch.bfloat16 or h.stride(1) != 1 or \
+            w.dtype not in (torch.bfloat16, torch.float32):
+        raise ValueError("mlp_head_forward needs bf16 h (unit column stride), bf16 / fp32 w")
     z = torch.empty(B, dtype=torch.float32, device=dev)
     bb = None if bias is None else _c(bias.reshape(1), torch.float32)
-    check(lib().dr_mlp_head_forward_bf16(ptr(h), h.stride(0), B, K, ptr(w_bf16.contiguous()),
-                                         ptr(bb), ptr(z), stream_handle(dev)))
+    check(lib().dr_mlp_head_forward_bf16(ptr(h), h.stride(0), B, K, ptr(w.contiguous()),
+                                         1 if w.dtype == torch.float32 else 0, ptr(bb), ptr(z),
+                                         stream_handle(dev)))
     _post(dev)
     return z
 
 
-def mlp_head_backward(h, w_bf16, gz):
+def mlp_head_backward(h, w, gz):
     """dr_mlp_head_backward_bf16 -> (grad_h bf16 [B, K] with h's ReLU mask
-    applied, dw fp32 [K], db fp32 scalar tensor)."""
+    applied, dw fp32 [K], db fp32 scalar tensor); w as in mlp_head_forward."""
     dev = _dev(h)
     B, K = h.shape
     gz = _c(gz.reshape(B), torch.float32)
@@ -621,9 +624,9 @@ def mlp_head_backward(h, w_bf16, gz):
     gh = torch.empty((B, K), dtype=torch.bfloat16, device=dev)
     dwp = torch.empty((max(P, 1), K), dtype=torch.float32, device=dev)
     dbp = torch.empty(max(P, 1), dtype=torch.float32, device=dev)
-    check(lib().dr_mlp_head_backward_bf16(ptr(h), h.stride(0), B, K, ptr(w_bf16.contiguous()),
-                                          ptr(gz), ptr(gh), K, ptr(dwp), ptr(dbp),
-                                          stream_handle(dev)))
+    check(lib().dr_mlp_head_backward_bf16(ptr(h), h.stride(0), B, K, ptr(w.contiguous()),
+                                          1 if w.dtype == torch.float32 else 0, ptr(gz), ptr(gh),
+                                          K, ptr(dwp), ptr(dbp), stream_handle(dev)))
     _post(dev)
     return gh, dwp[:P].sum(0), dbp[:P].sum()
 

@@ -929,8 +929,11 @@ int dr_relu_grad_bf16(const float* grad, int64_t ld_grad, const uint16_t* y, int
 /* dense(units=1) on the bf16 top MLP): z[b] = bf16(sum_k h[b,k] w[k] + bias) */
 /* as fp32, h [batch, k] bf16 (row stride ldh), w [k] bf16, bias a device   */
 /* fp32 scalar (nullable), fp32 sum in a fixed order.  k in {64,128,256,512}.*/
+/* w_fp32 = 1: the fp32 output layer on a bf16 tower (DeepFM --bf16,        */
+/* train.py:213-221): w fp32, the logit (and, backward, gz) not rounded.     */
 int dr_mlp_head_forward_bf16(const uint16_t* h, int64_t ldh, int64_t batch, int k,
-                             const uint16_t* w, const float* bias, float* z, void* stream);
+                             const void* w, int w_fp32, const float* bias, float* z,
+                             void* stream);
 /* Its backward from grad_z [batch] fp32 (rounded to bf16 first, as the bf16 */
 /* layer sees it): grad_h = bf16(gz w) where h > 0, else 0 (the top layer's   */
 /* ReLU derivative in the same pass); dw_partials [P, k] and db_partials [P]  */
@@ -938,7 +941,7 @@ int dr_mlp_head_forward_bf16(const uint16_t* h, int64_t ldh, int64_t batch, int 
 /* (the caller sums them over P: deterministic).                              */
 size_t dr_mlp_head_grad_partials(int64_t batch);
 int dr_mlp_head_backward_bf16(const uint16_t* h, int64_t ldh, int64_t batch, int k,
-                              const uint16_t* w, const float* grad_z, uint16_t* grad_h,
+                              const void* w, int w_fp32, const float* grad_z, uint16_t* grad_h,
                               int64_t ld_grad_h, float* dw_partials, float* db_partials,
                               void* stream);
 /* Same layer, also writing lin_out = xl W^T + b (bf16, nullable; needs      */

@@ -407,3 +407,32 @@ def test_deepfm_bf16_fused_fm_copy_matches_composed(dr):
         assert torch.equal(a, b)
     for a, b in zip(v1, v2):
         assert torch.equal(a, b)
+
+
+def test_deepfm_bf16_fused_head_matches_fp32_linear(dr):
+    """DeepFM --bf16's fp32 output layer (train.py:219) on dr_mlp_head_*
+    (w_fp32) vs torch's fp32 Linear on the widened tower output: the same
+    products, sums in another order (fp32 tolerance)."""
+    from deeprec_amd import modelzoo as mz
+    torch.manual_seed(29)
+    T, D, B = 26, 64, 1024
+    evs = [dr.EmbeddingVariable("dfm_fh_%d" % t, D, 0.01, device=DEV) for t in range(T)]
+    wide = [dr.EmbeddingVariable("dfm_fhw_%d" % t, 1, 0.0, device=DEV) for t in range(T)]
+    model = mz.DeepFM(evs, wide, bf16=True).to(DEV)
+    assert model.final.head_ok(model.last)
+    dense = torch.rand((B, 13), device=DEV)
+    ids = torch.randint(0, 5000, (T, B), device=DEV)
+    labels = (torch.rand(B, device=DEV) > 0.5).float()
+    runs = []
+    for fh in (True, False):
+        model.fuse_head = fh
+        model.zero_grad(set_to_none=True)
+        out = model(dense, ids)
+        torch.nn.functional.binary_cross_entropy(out, labels).backward()
+        runs.append((out.detach().clone(), [p.grad.clone() for p in model.parameters()]))
+        for ev in evs + wide:
+            ev.pending_grads.clear()
+    (o1, g1), (o2, g2) = runs
+    torch.testing.assert_close(o1, o2, rtol=1e-5, atol=1e-6)
+    for a, b in zip(g1, g2):
+        assert float((a - b).norm()) <= 1e-3 * float(b.norm()) + 1e-7, (a.shape,)
