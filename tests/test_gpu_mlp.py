@@ -436,3 +436,30 @@ def test_deepfm_bf16_fused_head_matches_fp32_linear(dr):
     torch.testing.assert_close(o1, o2, rtol=1e-5, atol=1e-6)
     for a, b in zip(g1, g2):
         assert float((a - b).norm()) <= 1e-3 * float(b.norm()) + 1e-7, (a.shape,)
+
+
+def test_wdl_bf16_tracks_fp32(dr):
+    """WDL --bf16 (train.py:250-266): dnn + logits on the MFMA tower and the
+    bf16 head; the prediction tracks the fp32 model on the same weights and
+    every deep gradient is finite."""
+    from deeprec_amd import modelzoo as mz
+    torch.manual_seed(31)
+    cats, dims, nums, B = ["C1", "C2", "C3"], [8, 16, 32], ["I1", "I2"], 1024
+    deep = [dr.EmbeddingVariable("wdl_b_d%d" % i, d, 0.05, device=DEV) for i, d in enumerate(dims)]
+    wide = [dr.EmbeddingVariable("wdl_b_w%d" % i, 1, 0.0, device=DEV) for i in range(3)]
+    m16 = mz.WDL(cats, deep, wide, nums, hidden=(128, 64), bf16=True).to(DEV)
+    assert isinstance(m16.dnn, mz._MfmaMLP)
+    m32 = mz.WDL(cats, deep, wide, nums, hidden=(128, 64)).to(DEV)
+    m32.load_state_dict({k.replace(".net.", "."): v for k, v in m16.state_dict().items()})
+    dense = torch.rand((B, 2), device=DEV)
+    ids = torch.randint(0, 300, (3, B), device=DEV)
+    labels = (torch.rand(B, device=DEV) > 0.5).float()
+    l16 = m16(dense, ids)
+    torch.nn.functional.binary_cross_entropy_with_logits(l16, labels).backward()
+    with torch.no_grad():
+        l32 = m32(dense, ids)
+    for ev in deep + wide:
+        ev.pending_grads.clear()
+    assert (torch.sigmoid(l16) - torch.sigmoid(l32)).abs().max() <= 2e-2
+    for p in m16.deep_parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all()

@@ -112,7 +112,7 @@ def wdl(args, dr, mz, dev):
         ew = dr.EmbeddingVariable("wdl_w%d" % i, 1, 0.0, capacity=r + (1 << 16), device=dev)
         ew.insert_synthetic(0, r, seed=950 + i)
         wide.append(ew)
-    model = mz.WDL(cats, deep, wide, nums).to(dev)
+    model = mz.WDL(cats, deep, wide, nums, bf16=args.bf16).to(dev)
     deep_opt = torch.optim.Adagrad(model.deep_parameters(), lr=0.01,
                                    initial_accumulator_value=0.1)
     ftrl = dr.FtrlOptimizer(0.2)
@@ -136,7 +136,8 @@ def wdl(args, dr, mz, dev):
     print(json.dumps({"model": "wdl", "samples_per_s": round(B * args.steps / el, 1),
                       "lookups_per_s": round(52 * B * args.steps / el, 1),
                       "ms_per_step": round(el / args.steps * 1e3, 3), "batch": B,
-                      "opt": "adagrad+ftrl", "loss": float(loss.detach())}), flush=True)
+                      "opt": "adagrad+ftrl", "bf16_mlp": args.bf16,
+                      "loss": float(loss.detach())}), flush=True)
 
 
 def din(args, dr, mz, dev):
