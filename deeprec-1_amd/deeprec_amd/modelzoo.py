@@ -136,6 +136,18 @@ class _OneHotLookup(object):
         return embedding_stack(x0, self.evs, self._sps(ids), combiner="sum")
 
 
+def _dw_split(tiles, rows, slots=512):
+    """Row splits of a weight-gradient GEMM: the smallest s within 3 % of the
+    fewest block rounds per unit of rows, ceil(tiles * s / slots) / s (2
+    blocks per CU x 256 CUs = 512 resident blocks), s <= 64 and each split
+    >= 512 rows.  (The old rule, min(64, 512 // tiles), left a 144-tile
+    layer at 3 splits = 432 blocks, one partly filled round.)"""
+    smax = max(1, min(64, rows // 512))
+    cost = {s: -(-tiles * s // slots) / s for s in range(1, smax + 1)}
+    best = min(cost.values())
+    return min(s for s, c in cost.items() if c <= 1.03 * best)
+
+
 # A/B switch: DR_TOWER_TN_DW=0 = transposes + NT GEMM for the weight gradients
 _TN_DW = os.environ.get("DR_TOWER_TN_DW", "1") != "0"
 
@@ -209,7 +221,7 @@ class _MfmaTowerFn(torch.autograd.Function):
             x = hs[l]
             N, Kp = g.shape[1], x.shape[1]
             tiles = ((N + 127) // 128) * ((Kp + 127) // 128)
-            split = max(1, min(64, 512 // tiles, B // (64 * 8)))
+            split = _dw_split(tiles, B)
             if _TN_DW and B % 64 == 0:
                 # dW = g^T x straight from the row-major operands (transposing
                 # LDS reads), db from the same pass's A fragments
