@@ -625,10 +625,17 @@ class DCNv2(torch.nn.Module):
     of 64 features, bf16; L cross layers on the MFMA kernel; a bf16 deep MLP
     over x_L; one logit, sigmoid, BCE (as DLRM / DeepFM here).  Cross weights
     are fp32 master copies cast to bf16 per step (the reference's bf16 +
-    keep_weights convention, modelzoo/DLRM/train.py:183-195)."""
+    keep_weights convention, modelzoo/DLRM/train.py:183-195).
 
-    def __init__(self, evs, num_dense=13, layers=3, deep=(1024, 512)):
+    bf16=False: the deep MLP and the output layer under torch autocast (bf16
+    library GEMMs).  bf16=True: the same bf16 MLP on the hand MFMA towers
+    (_MfmaMLP, the cross output x_L is already the padded bf16 input) with
+    the output layer riding on the tower node (bf16 weight, rounded logit:
+    what autocast's Linear computes), when the batch is a multiple of 512."""
+
+    def __init__(self, evs, num_dense=13, layers=3, deep=(1024, 512), bf16=False):
         super().__init__()
+        self.mfma_deep = bool(bf16)
         self.evs = list(evs)
         self.dim = self.evs[0].dim
         self.T = len(self.evs)
@@ -644,16 +651,26 @@ class DCNv2(torch.nn.Module):
         self.cross_w = torch.nn.ParameterList(ws)
         self.cross_b = torch.nn.ParameterList([torch.nn.Parameter(torch.zeros(dp))
                                                for _ in range(layers)])
-        self.deep = _mlp([dp] + list(deep))
+        self.deep = (_MfmaMLP if self.mfma_deep else _mlp)([dp] + list(deep))
         self.last = torch.nn.Linear(deep[-1], 1)
         self.lookup = _OneHotLookup(self.evs)
 
     def forward(self, dense, ids):
         B = dense.shape[0]
         emb = self.lookup(ids)                                     # [B, T*D] fp32
-        pad = torch.zeros(B, self.dp - self.d, device=dense.device, dtype=dense.dtype)
-        x0 = torch.cat([dense, emb, pad], 1).to(torch.bfloat16)
+        if self.mfma_deep:
+            # x0 cast column block by column block into one bf16 buffer (no
+            # fp32 [B, dp] concat in between); the slice copies keep autograd
+            x0 = torch.zeros(B, self.dp, device=dense.device, dtype=torch.bfloat16)
+            x0[:, :self.num_dense] = dense
+            x0[:, self.num_dense:self.d] = emb
+        else:
+            pad = torch.zeros(B, self.dp - self.d, device=dense.device, dtype=dense.dtype)
+            x0 = torch.cat([dense, emb, pad], 1).to(torch.bfloat16)
         x = CrossStack.apply(x0, *self.cross_w, *self.cross_b)
+        if (self.mfma_deep and self.deep.mfma_ok(B) and self.deep.head_ok(self.last)
+                and x.shape[1] == self.deep.kp):
+            return torch.sigmoid(self.deep.forward_padded_head(x.contiguous(), self.last)).squeeze(1)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             net = self.last(self.deep(x)).float()
         return torch.sigmoid(net).squeeze(1)

@@ -120,11 +120,16 @@ def test_cross_stack_backward_matches_autograd():
         _close(got.grad, want.grad, frac=1.0 / 16)
 
 
-def test_dcn_train_step_matches_torch_reference():
+@pytest.mark.parametrize("bf16", [False, True])
+def test_dcn_train_step_matches_torch_reference(bf16):
+    """bf16=False: deep MLP under autocast; True: the deep MLP and the output
+    layer on the hand MFMA tower node (needs B % 512 == 0 and widths that are
+    multiples of 64), x0 cast straight into its bf16 buffer."""
     import deeprec_amd as dr
     from deeprec_amd import modelzoo as mz
     torch.manual_seed(13)
-    T, R, D, B, lr = 4, 50, 16, 256, 0.05
+    T, R, D, lr = 4, 50, 16, 0.05
+    B, deep = (512, (128, 64)) if bf16 else (256, (64, 32))
     gen = torch.Generator(device="cpu").manual_seed(6)
     tables = [torch.randn(R, D, generator=gen) * 0.1 for _ in range(T)]
     evs = []
@@ -132,11 +137,12 @@ def test_dcn_train_step_matches_torch_reference():
         ev = dr.EmbeddingVariable("dcn_%d" % t, D, 0.0, device=DEV)
         ev.insert(torch.arange(R, device=DEV), w.to(DEV))
         evs.append(ev)
-    model = mz.DCNv2(evs, 13, layers=2, deep=(64, 32)).to(DEV)
+    model = mz.DCNv2(evs, 13, layers=2, deep=deep, bf16=bf16).to(DEV)
     ids = torch.randint(0, R, (T, B), device=DEV)
     dense = torch.randn(B, 13, device=DEV)
     labels = (torch.rand(B, device=DEV) > 0.5).float()
-    P = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    P = {k.replace("deep.net.", "deep."): v.detach().clone()
+         for k, v in model.state_dict().items()}
     # fp32 torch reference of the same model (bf16 rounding of x0 and of the
     # cross weights as in the kernel path; everything else fp32)
     W = [t.to(DEV).clone().requires_grad_(True) for t in tables]

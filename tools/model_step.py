@@ -55,7 +55,7 @@ def main():
     if args.model == "dlrm":
         model = mz.DLRM(evs, 13, (512, 256), (512, 256), bf16=args.bf16).to(dev)
     elif args.model == "dcn":     # BASELINE configs[4]: bf16 CrossNet on MFMA, 3 layers
-        model = mz.DCNv2(evs, 13, layers=3, deep=(1024, 512)).to(dev)
+        model = mz.DCNv2(evs, 13, layers=3, deep=(1024, 512), bf16=args.bf16).to(dev)
     else:
         wide = []
         for t in range(T):
