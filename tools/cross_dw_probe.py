@@ -1,0 +1,49 @@
+"""CrossNet backward weight gradient at the DCN shape (B = 65 536,
+d = 3 392): dW = u^T x as torch.matmul (hipBLASLt) vs the hand TN MFMA GEMM
+(dr_gemm_tn_bf16) over split-K choices; times with HIP events on the current
+stream and the max relative difference between the two."""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "deeprec-1_amd"))
+
+
+def timed(fn, iters=10):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    import deeprec_amd as dr
+    from deeprec_amd import ops
+    from deeprec_amd.modelzoo import _dw_split
+    dr.load()
+    B, d = 65536, 3392
+    g = torch.Generator(device="cuda").manual_seed(1)
+    u = torch.randn(B, d, device="cuda", generator=g).to(torch.bfloat16)
+    x = torch.randn(B, d, device="cuda", generator=g).to(torch.bfloat16)
+    flop = 2.0 * B * d * d
+    ref = torch.matmul(u.t(), x).float()
+    t = timed(lambda: torch.matmul(u.t(), x).float())
+    print("matmul(u.t(), x).float(): %.3f ms  %.0f TF/s" % (t, flop / t / 1e9), flush=True)
+    tiles = ((d + 127) // 128) ** 2
+    for s in sorted({1, 2, 4, _dw_split(tiles, B)}):
+        got = ops.gemm_tn(u, x, split_k=s)
+        err = ((got - ref).abs().max() / ref.abs().max()).item()
+        t = timed(lambda: ops.gemm_tn(u, x, split_k=s))
+        print("gemm_tn split %d: %.3f ms  %.0f TF/s  max rel diff %.2e" % (s, t, flop / t / 1e9, err),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
