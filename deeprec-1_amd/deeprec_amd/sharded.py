@@ -494,8 +494,17 @@ class XgmiShardedLookup(object):
         self.T = len(evs)
         self.dim = evs[0].dim
         self.handles = (C.c_void_p * self.T)(*[e.handle.value for e in evs])
-        self.bufs = buffers or XgmiBuffers(world, self.T, batch, self.dim, device,
-                                           value_dtype=evs[0].value_dtype)
+        # an allocation or export failure on one rank must not leave the others
+        # waiting in the handle exchange: it is carried into the all-gather
+        # and every rank raises together after it
+        self._setup_err = None
+        try:
+            self.bufs = buffers or XgmiBuffers(world, self.T, batch, self.dim, device,
+                                               value_dtype=evs[0].value_dtype)
+        except Exception as e:  # noqa: BLE001 -- re-raised after the exchange
+            if world == 1 or peer_buffers is not None:
+                raise
+            self.bufs, self._setup_err = None, "rank %d: %s" % (rank, e)
         self._bases = []
         if world == 1 and peer_buffers is None:
             peer_buffers = [self.bufs]
@@ -523,13 +532,21 @@ class XgmiShardedLookup(object):
 
     def _exchange_ipc(self):
         mine = []
-        for t in self.bufs.tensors():
-            h = (C.c_char * _lib.IPC_HANDLE_BYTES)()
-            off = C.c_int64(0)
-            check(lib().dr_ipc_export(t.data_ptr(), h, C.byref(off)))
-            mine.append((bytes(h), off.value))
+        try:
+            if self._setup_err is not None:
+                raise RuntimeError(self._setup_err)
+            for t in self.bufs.tensors():
+                h = (C.c_char * _lib.IPC_HANDLE_BYTES)()
+                off = C.c_int64(0)
+                check(lib().dr_ipc_export(t.data_ptr(), h, C.byref(off)))
+                mine.append((bytes(h), off.value))
+        except Exception as e:  # noqa: BLE001 -- every rank raises below
+            mine = "rank %d: %s" % (self.rank, e)
         everyone = [None] * self.world
         dist.all_gather_object(everyone, mine, group=self.group)
+        errs = [m for m in everyone if isinstance(m, str)]
+        if errs:
+            raise RuntimeError("xgmi IPC setup failed: " + "; ".join(errs))
         ptrs = []
         for q in range(self.world):
             if q == self.rank:
