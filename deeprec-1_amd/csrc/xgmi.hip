@@ -7,6 +7,7 @@
 // into the owner's inbox over xGMI: no send buffer, no host read of counts.
 #include <map>
 #include <mutex>
+#include <stdlib.h>
 
 #include "dr_common.h"
 
@@ -394,6 +395,12 @@ int dr_ipc_alloc(size_t bytes, void** ptr_out) {
   return DR_OK;
 }
 
+namespace dr {
+// Diagnostic (DR_IPC_RELEASE=3/4 below): a system-scope fence from blocks on
+// every XCD -- an L2 write-back and invalidate of each XCD's L2.
+__global__ void uc_l2_flush_kernel() { __threadfence_system(); }
+}  // namespace dr
+
 // Returns the buffer to the uncached free list (never to hipFree, see
 // above).  Cheap and safe to call from a DLPack deleter: the next
 // dr_ipc_alloc that reuses it synchronises the device first.
@@ -405,6 +412,29 @@ int dr_ipc_free(void* ptr) {
   auto it = u.size_of.find(ptr);
   DR_REQUIRE(it != u.size_of.end(), DR_INVALID_ARGUMENT,
              "dr_ipc_free: %p was not allocated by dr_ipc_alloc", ptr);
+  // Diagnostic switch for the reuse hazard above (tools/gpu_uc_reuse.sh):
+  // DR_IPC_RELEASE=1 hands the block back to hipFree at once (the round-2
+  // behaviour), =2 after a device-wide synchronisation, =3 / 4 with the L2
+  // flush kernel after (and before) the free.  Unset: free list.
+  static const int release = [] {
+    const char* e = getenv("DR_IPC_RELEASE");
+    return e ? atoi(e) : 0;
+  }();
+  if (release >= 1 && release <= 4) {
+    // 3: L2 flushed on every XCD after the free, 4: before and after
+    u.size_of.erase(it);
+    if (release >= 2) DR_HIP(hipDeviceSynchronize());
+    if (release == 4) {
+      hipLaunchKernelGGL(uc_l2_flush_kernel, dim3(512), dim3(64), 0, nullptr);
+      DR_HIP(hipDeviceSynchronize());
+    }
+    DR_HIP(hipFree(ptr));
+    if (release >= 3) {
+      hipLaunchKernelGGL(uc_l2_flush_kernel, dim3(512), dim3(64), 0, nullptr);
+      DR_HIP(hipDeviceSynchronize());
+    }
+    return DR_OK;
+  }
   u.free.insert({it->second, ptr});
   return DR_OK;
 }

@@ -461,10 +461,11 @@ def test_xgmi_serve_grows_small_tables(world):
                     vals = [evs_all[o][t].export()[1].cpu().numpy() for o in range(world)]
                     stored.append(int(sum((v != np.float32(DEFAULT)).any(1).sum() for v in vals)))
                 raise AssertionError(
-                    "step %d rank %d: %d (bag, table) outputs differ, first %s (key %d); "
-                    "stored rows != default per table: %s" % (
+                    "step %d rank %d: %d (bag, table) outputs differ, first %s (key %d, "
+                    "values %s); stored rows != default per table: %s" % (
                         step, r, badbt.shape[0], badbt[:4].tolist(),
-                        ids[r][badbt[0][1], badbt[0][0]], stored))
+                        ids[r][badbt[0][1], badbt[0][0]],
+                        ob[badbt[0][0], badbt[0][1], :6].tolist(), stored))
     for r in range(world):
         for t in range(T):
             k = evs_all[r][t].export()[0].cpu().numpy()
