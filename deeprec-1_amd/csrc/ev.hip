@@ -1282,6 +1282,26 @@ static void free_shared(EvShared* s) {
 }
 
 // Grow the slot table and/or the row arrays so that `need` keys fit.
+// Diagnostic (tools/gpu_uc_reuse.sh): DR_GROW_KERNEL_COPY=1 copies the
+// pools with a kernel instead of hipMemcpyAsync (the DMA copy path).
+__global__ void grow_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                 int64_t n16) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+static hipError_t grow_copy(void* dst, const void* src, size_t bytes, hipStream_t st) {
+  static const bool kcopy = getenv("DR_GROW_KERNEL_COPY") != nullptr;
+  if (!kcopy || bytes % 16 || ((uintptr_t)dst | (uintptr_t)src) % 16)
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st);
+  const int64_t n16 = (int64_t)(bytes / 16);
+  const int64_t blocks = std::min<int64_t>(std::max<int64_t>(ceil_div(n16, 256), 1), 4096);
+  hipLaunchKernelGGL(grow_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                     static_cast<const uint4*>(src), static_cast<uint4*>(dst), n16);
+  return hipGetLastError();
+}
+
 static int grow(EvShared* s, int64_t need, hipStream_t st) {
   // kernels other streams enqueued on the old table / pools must be done
   // before they are copied and freed (EvGuard keeps new ones from starting)
@@ -1316,8 +1336,7 @@ static int grow(EvShared* s, int64_t need, hipStream_t st) {
       const int64_t w = col_words(s, c);
       float* np = nullptr;
       DR_HIP(hipMalloc(&np, (size_t)nrc * w * sizeof(float)));
-      DR_HIP(hipMemcpyAsync(np, s->pools[c], (size_t)s->row_cap * w * sizeof(float),
-                            hipMemcpyDeviceToDevice, st));
+      DR_HIP(grow_copy(np, s->pools[c], (size_t)s->row_cap * w * sizeof(float), st));
       DR_HIP(hipStreamSynchronize(st));
       DR_HIP(hipFree(s->pools[c]));
       s->pools[c] = np;
@@ -1329,8 +1348,7 @@ static int grow(EvShared* s, int64_t need, hipStream_t st) {
       DR_HIP(hipMalloc(&np, (size_t)nrc * sizeof(int64_t)));
       int frc = fill_bytes(np, 0, (size_t)nrc * sizeof(int64_t), st);
       if (frc) return frc;
-      DR_HIP(hipMemcpyAsync(np, *a, (size_t)s->row_cap * sizeof(int64_t), hipMemcpyDeviceToDevice,
-                            st));
+      DR_HIP(grow_copy(np, *a, (size_t)s->row_cap * sizeof(int64_t), st));
       DR_HIP(hipStreamSynchronize(st));
       DR_HIP(hipFree(*a));
       *a = np;
