@@ -109,7 +109,46 @@ static void trial(int uncached_first, size_t bytes, int t) {
   CK(hipFree(tot));
 }
 
+// Small blocks (sub-allocated): many uncached blocks zero-filled by a kernel
+// and freed, then small hipMalloc blocks written by a HOST-TO-DEVICE copy and
+// read by a kernel ("stale_h2d": words the kernel does not see as written).
+static void small_h2d_trial(size_t bytes, int nblk) {
+  void* u[64];
+  for (int i = 0; i < nblk; ++i) {
+    CK(hipExtMallocWithFlags(&u[i], bytes, hipDeviceMallocUncached));
+    hipLaunchKernelGGL(fill_k, dim3(64), dim3(256), 0, 0, (uint32_t*)u[i], (int64_t)(bytes / 4), 0u);
+  }
+  CK(hipDeviceSynchronize());
+  for (int i = 0; i < nblk; ++i) CK(hipFree(u[i]));
+  const int64_t n = (int64_t)(bytes / 4);
+  uint32_t* h = (uint32_t*)malloc(bytes);
+  for (int64_t i = 0; i < n; ++i) h[i] = (uint32_t)(i * 2654435761u) ^ 0x77u;
+  unsigned long long* bad;
+  CK(hipMalloc(&bad, 8));
+  CK(hipMemset(bad, 0, 8));
+  int reused = 0;
+  void* c[64];
+  for (int i = 0; i < nblk; ++i) {
+    CK(hipMalloc(&c[i], bytes));
+    for (int j = 0; j < nblk; ++j) reused += c[i] == u[j];
+    CK(hipMemcpy(c[i], h, bytes, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(check_k, dim3(64), dim3(256), 0, 0, (const uint32_t*)c[i], n, 0x77u, bad, 0);
+  }
+  unsigned long long hb = 0;
+  CK(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
+  printf("{\"small_h2d\":1,\"bytes\":%zu,\"blocks\":%d,\"same_va\":%d,\"stale_h2d\":%llu}\n",
+         bytes, nblk, reused, hb);
+  for (int i = 0; i < nblk; ++i) CK(hipFree(c[i]));
+  CK(hipFree(bad));
+  free(h);
+}
+
 int main(int argc, char** argv) {
+  if (argc > 2 && atoi(argv[2]) == 1) {
+    const size_t sz[4] = {512, 4096, 65536, 1 << 20};
+    for (int i = 0; i < 4; ++i) small_h2d_trial(sz[i], 32);
+    return 0;
+  }
   const int trials = argc > 1 ? atoi(argv[1]) : 6;
   const size_t sizes[3] = {(size_t)64 << 20, (size_t)1 << 30, (size_t)4 << 30};
   for (int t = 0; t < trials; ++t) {
