@@ -2847,8 +2847,8 @@ int dr_ev_apply_grouped_ptr_rows(int optimizer, dr_ev* const* vars, int num_tabl
 }
 
 size_t dr_ev_pool_grad_rows_sgd_workspace_size(int64_t total_nnz, int dim) {
-  const int64_t n = total_nnz > 0 ? total_nnz : 1;
-  return dr_pool_grad_rows_workspace_size(total_nnz) + 256 + (size_t)n * (dim > 0 ? dim : 1) * 4;
+  (void)dim;   // (the long-run piece partials live in the backward's own workspace)
+  return dr_pool_grad_rows_workspace_size(total_nnz);
 }
 
 int dr_ev_pool_grad_rows_apply_sgd(dr_ev* const* vars, const dr_pool_grad_desc* descs,

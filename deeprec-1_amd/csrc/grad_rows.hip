@@ -26,11 +26,20 @@
 //      back; every other run goes to a worklist that rows_work_kernel (G
 //      lanes per entry) sums into grad_unique[o] (grad_ptr[o] points there).
 //
-// Runs longer than kRowsChunk positions (a hot id) are cut at multiples of
-// kRowsChunk of the sorted array, summed in parallel and combined in order
-// by rows_finish_kernel: fixed association, deterministic, fp32 tolerance.
 // A run of at most kRowsChunk positions is summed serially in ascending
-// order -- bit-exact to the reference loops.
+// order by one lane group (rows_work_kernel) -- bit-exact to the reference
+// loops.  Longer runs (hot ids) go to the long-run kernels: rows_expand_kernel
+// measures each run (two rounds of parallel probes) and cuts it into pieces
+// of kSerialMax positions counted from the RUN's first position; every
+// piece is summed in ascending position order by rows_serial_kernel (one
+// block per piece and column slice: all threads stage the piece's gradient
+// rows through LDS, one wave walks each column's serial chain), and a run of
+// several pieces is the ordered sum of its piece partials
+// (rows_combine_kernel).  So a run of up to kSerialMax positions is the
+// reference's exact serial sum (segment_reduction_ops.cc:391-404), and every
+// association depends only on the run's own position order -- never on the
+// key -> row numbering that racing first-touch inserts assign, nor on where
+// the run lands in the sorted array.
 #include "dr_rows.h"
 
 namespace dr {
@@ -40,13 +49,33 @@ struct RowsGroup {
   int64_t koff[DR_MAX_GROUP + 1];
 };
 
-static constexpr int64_t kRowsChunk = 256;
+static constexpr int64_t kRowsChunk = 256;    // longest run of the lane-group path
+static constexpr int64_t kSerialMax = 8192;   // longest exact-serial piece of a long run
 #ifndef DR_ROWS_CHAIN
 #define DR_ROWS_CHAIN 8
 #endif
-static constexpr int kRowsChain = DR_ROWS_CHAIN;  // positions of a chunk fetched per step
-static constexpr int kRowsFinishMax = 32;    // chunk partials fetched per step (at most)
+static constexpr int kRowsChain = DR_ROWS_CHAIN;  // positions of a run fetched per step
 static constexpr int64_t kRowsMaxDim = 1024;
+
+// Long-run state (the workspace arrays of RowsWs, passed as one argument).
+struct RowsLong {
+  const uint32_t* skey;
+  const int32_t* perm;
+  const int32_t* ex;       // unfused: first-occurrence ranks (output index)
+  const int32_t* base;
+  int32_t* srow;           // per sorted position in a multi-position run: bag row (-1 invalid)
+  float* smul;             //   weight, or the mean / sqrtn scale (1: none)
+  float* sdiv;             //   bag_scale of a weighted mean / sqrtn
+  const int32_t* longs;    // sorted head of each run longer than kRowsChunk
+  const int32_t* nlong;
+  int32_t* rlen;           // its length (rows_expand_kernel)
+  int32_t* rfirst;         // its first piece item
+  int32_t* items;          // pieces: (run, piece index)
+  int32_t* nitems;
+  uint64_t* gptr;
+  float* gu;
+  float* part;             // [item][dim] piece partials of multi-piece runs
+};
 
 // Table of global position i (lane-varying; koff staged in LDS).
 __device__ __forceinline__ int tab_of(const int64_t* koff, int T, int64_t i) {
@@ -66,11 +95,13 @@ __device__ __forceinline__ int tab_of(const int64_t* koff, int T, int64_t i) {
 __global__ void rows_keys_kernel(const int64_t* __restrict__ rowsel, int64_t N, int64_t row_limit,
                                  uint32_t sentinel, uint32_t* __restrict__ kin,
                                  int32_t* __restrict__ vin, int32_t* __restrict__ flags,
-                                 int32_t* __restrict__ nlong, int32_t* __restrict__ nwork) {
+                                 int32_t* __restrict__ nlong, int32_t* __restrict__ nwork,
+                                 int32_t* __restrict__ nitems) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) {
     *nlong = 0;
     *nwork = 0;
+    *nitems = 0;
   }
   if (i >= N) return;
   const int64_t r = rowsel[i];
@@ -147,20 +178,86 @@ __device__ __forceinline__ void work_push_block(bool push, int64_t p, int32_t* _
   }
 }
 
+// Two block-aggregated appends at once (same contract as work_push_block).
+__device__ __forceinline__ void push2_block(bool pa, int32_t va, int32_t* __restrict__ la,
+                                            int32_t* __restrict__ na, bool pb, int32_t vb,
+                                            int32_t* __restrict__ lb, int32_t* __restrict__ nb) {
+  __shared__ int wc[2][4];
+  __shared__ int bb[2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t ma = __ballot(pa), mb = __ballot(pb);
+  if (lane == 0) {
+    wc[0][wv] = __popcll(ma);
+    wc[1][wv] = __popcll(mb);
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const int x = threadIdx.x;
+    const int tot = wc[x][0] + wc[x][1] + wc[x][2] + wc[x][3];
+    bb[x] = tot ? atomicAdd(x ? nb : na, tot) : 0;
+  }
+  __syncthreads();
+  if (pa) {
+    int off = bb[0];
+    for (int w = 0; w < wv; ++w) off += wc[0][w];
+    la[off + __popcll(ma & lanemask_lt())] = va;
+  }
+  if (pb) {
+    int off = bb[1];
+    for (int w = 0; w < wv; ++w) off += wc[1][w];
+    lb[off + __popcll(mb & lanemask_lt())] = vb;
+  }
+}
+
+// The term of sorted position p of a multi-position run (feature-local
+// position k of table descriptor d), for the long-run kernels: its bag row
+// (-1: an invalid bag, a zero term, latched here) and factors -- smul = the
+// weight (weighted) or the mean / sqrtn scale of its bag (1: none), sdiv =
+// the weighted mean / sqrtn divisor -- the arithmetic of rows_work_kernel's
+// scaled / wscaled, precomputed in the fully parallel classification pass so
+// that the serial pass streams one contiguous index per position.
+__device__ __forceinline__ void rows_term(const dr_pool_grad_desc& d, int64_t k, int64_t B,
+                                          int64_t p, const RowsLong& L, int* st) {
+  const int64_t r = d.seg ? d.seg[k * d.seg_stride] : k;
+  const bool okr = r >= 0 && r < B;
+  if (!okr) latch(st, DR_INVALID_ARGUMENT);
+  float m = 1.f, q = 1.f;
+  if (okr && d.weights) {
+    m = d.weights[k];
+    if (d.bag_scale) q = d.bag_scale[r];
+  } else if (okr && d.combiner != DR_COMBINER_SUM && d.bag_off) {
+    const int32_t cnt = d.bag_off[r + 1] - d.bag_off[r];
+    if (cnt != 1)
+      m = d.combiner == DR_COMBINER_SQRTN ? (float)(1.0 / sqrt((double)cnt))
+                                          : (float)(1.0 / (double)cnt);
+  }
+  L.srow[p] = okr ? (int32_t)r : -1;
+  L.smul[p] = m;
+  L.sdiv[p] = q;
+}
+
 // Sorted order, lane per position: mark[i] = p (| 1 << 31 for a one-position
-// run) at the run head's original position i; heads of longer runs and
-// every multiple of the chunk inside a run (a possible later chunk of a
-// long run) go straight to the worklist of rows_work_kernel.
-__global__ void rows_heads_kernel(RowsGroup g, int T, const uint32_t* __restrict__ skey,
-                                  const int32_t* __restrict__ perm, uint32_t sentinel,
-                                  int32_t* __restrict__ mark, int32_t* __restrict__ work,
-                                  int32_t* __restrict__ nwork) {
+// run) at the run head's original position i; heads of runs of 2 ..
+// kRowsChunk positions go to the worklist of rows_work_kernel, heads of
+// longer runs to the long-run list; every position of a multi-position run
+// records its term (rows_term).
+__global__ __launch_bounds__(256) void rows_heads_kernel(RowsGroup g, int T, int64_t B,
+                                                         const uint32_t* __restrict__ skey,
+                                                         const int32_t* __restrict__ perm,
+                                                         uint32_t sentinel,
+                                                         int32_t* __restrict__ mark,
+                                                         int32_t* __restrict__ work,
+                                                         int32_t* __restrict__ nwork, RowsLong L,
+                                                         int32_t* __restrict__ longs,
+                                                         int32_t* __restrict__ nlong, int* st) {
+  __shared__ dr_pool_grad_desc sd[DR_MAX_GROUP];
   __shared__ int64_t sk[DR_MAX_GROUP + 1];
+  if (threadIdx.x < T) sd[threadIdx.x] = g.d[threadIdx.x];
   if (threadIdx.x <= T) sk[threadIdx.x] = g.koff[threadIdx.x];
   __syncthreads();
   const int64_t N = sk[T];
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool push = false;
+  bool push = false, plong = false;
   if (p < N) {
     const int64_t pm = p > 0 ? p - 1 : 0, pn = p + 1 < N ? p + 1 : N - 1;
     const uint32_t u = skey[p], um = skey[pm], un = skey[pn];
@@ -170,9 +267,16 @@ __global__ void rows_heads_kernel(RowsGroup g, int T, const uint32_t* __restrict
     const bool head = valid && (p == 0 || um != u || tab_of(sk, T, im) != t);
     const bool last = p + 1 >= N || un != u || tab_of(sk, T, in) != t;
     if (head) mark[i] = (int32_t)p | (last ? (int32_t)0x80000000 : 0);
-    push = valid && ((head && !last) || (!head && p % kRowsChunk == 0));
+    if (valid && !(head && last)) {
+      rows_term(sd[t], i - sk[t], B, p, L, st);
+      if (head) {
+        const int64_t q = p + kRowsChunk;
+        plong = q < N && skey[q] == u && tab_of(sk, T, perm[q]) == t;
+        push = !plong;
+      }
+    }
   }
-  work_push_block(push, p, work, nwork);
+  push2_block(push, (int32_t)p, work, nwork, plong, (int32_t)p, longs, nlong);
 }
 
 // Fused SGD, sorted order, lane per position (dr_ev_pool_grad_rows_apply_sgd):
@@ -180,17 +284,20 @@ __global__ void rows_heads_kernel(RowsGroup g, int T, const uint32_t* __restrict
 // gradient needs no arithmetic -- the rows the unfused backward hands on by
 // address (rows_emit_kernel's rule) -- is applied right here: v -= lr * (0 +
 // g) read from the pooled gradient, the same bytes and roundings as
-// ev_apply_kernel on that address.  Longer runs, inner chunk multiples and
-// the other one-position runs go to rows_work_kernel's worklist.  No mark,
-// scan or emit: the optimizer is the gradient's only consumer, so the
-// IndexedSlices order (first occurrence) is never formed.
+// ev_apply_kernel on that address.  Runs of 2 .. kRowsChunk positions and
+// the other one-position runs go to rows_work_kernel's worklist, longer runs
+// to the long-run list (rows_heads_kernel's rule).  No mark, scan or emit:
+// the optimizer is the gradient's only consumer, so the IndexedSlices order
+// (first occurrence) is never formed.
 template <int G, bool WB>
 __global__ __launch_bounds__(256) void rows_sgd_kernel(RowsGroup g, RowsSgd sg, int T, int64_t B,
                                                        const uint32_t* __restrict__ skey,
                                                        const int32_t* __restrict__ perm,
                                                        uint32_t sentinel, int dim,
                                                        int32_t* __restrict__ work,
-                                                       int32_t* __restrict__ nwork) {
+                                                       int32_t* __restrict__ nwork, RowsLong L,
+                                                       int32_t* __restrict__ longs,
+                                                       int32_t* __restrict__ nlong, int* st) {
   __shared__ dr_pool_grad_desc sd[DR_MAX_GROUP];
   __shared__ int64_t sk[DR_MAX_GROUP + 1];
   __shared__ void* spool[DR_MAX_GROUP];
@@ -204,7 +311,7 @@ __global__ __launch_bounds__(256) void rows_sgd_kernel(RowsGroup g, RowsSgd sg, 
   __syncthreads();
   const int64_t N = sk[T];
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool push = false, direct = false;
+  bool push = false, plong = false, direct = false;
   int64_t u = -1;
   uint64_t ga = 0;
   int t = 0;
@@ -231,11 +338,16 @@ __global__ __launch_bounds__(256) void rows_sgd_kernel(RowsGroup g, RowsSgd sg, 
       } else {
         push = true;   // (an invalid bag latches in rows_work_kernel)
       }
-    } else {
-      push = valid && ((head && !last) || (!head && p % kRowsChunk == 0));
+    } else if (valid) {
+      rows_term(sd[t], i - sk[t], B, p, L, st);
+      if (head) {
+        const int64_t q = p + kRowsChunk;
+        plong = q < N && skey[q] == uk && tab_of(sk, T, perm[q]) == t;
+        push = !plong;
+      }
     }
   }
-  work_push_block(push, p, work, nwork);
+  push2_block(push, (int32_t)p, work, nwork, plong, (int32_t)p, longs, nlong);
   if (!__ballot(direct)) return;   // wave-uniform
   // the wave's direct rows, P at a time, U batches of loads in flight
   constexpr int P = 64 / G, U = 4;
@@ -366,51 +478,18 @@ __global__ __launch_bounds__(256) void rows_emit_kernel(
   work_push_block(push, (int64_t)(mk & 0x7FFFFFFF), work, nwork);
 }
 
-// Is the run (u, t) through inner position m (a multiple of kRowsChunk, not
-// its run's head) longer than kRowsChunk?  Rare path: bounded searches.
-__device__ bool run_is_long(const uint32_t* __restrict__ skey, const int32_t* __restrict__ perm,
-                            const int64_t* sk, int T, int64_t N, int64_t m, uint32_t u, int t) {
-  auto in_run = [&](int64_t q) { return skey[q] == u && tab_of(sk, T, perm[q]) == t; };
-  if (m >= kRowsChunk && in_run(m - kRowsChunk)) return true;
-  if (m + kRowsChunk < N && in_run(m + kRowsChunk)) return true;
-  // start in (m - chunk, m], end in (m, m + chunk]
-  int64_t lo = m - kRowsChunk + 1 < 0 ? 0 : m - kRowsChunk + 1, hi = m;  // first in-run
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (in_run(mid))
-      hi = mid;
-    else
-      lo = mid + 1;
-  }
-  const int64_t s = lo;
-  lo = m;
-  hi = m + kRowsChunk < N ? m + kRowsChunk : N - 1;  // last in-run
-  while (lo < hi) {
-    const int64_t mid = (lo + hi + 1) >> 1;
-    if (in_run(mid))
-      lo = mid;
-    else
-      hi = mid - 1;
-  }
-  return lo - s + 1 > kRowsChunk;
-}
-
-// G lanes per worklist entry (a sorted position c0): a run head sums its run
-// (or, for a long run, its first chunk) in ascending position order into
-// grad_unique[o]; an inner multiple of the chunk sums its chunk into
-// part[c0 / chunk] when its run is long, and is dropped otherwise.
+// G lanes per worklist entry (a sorted run head c0 of a run of at most
+// kRowsChunk positions, or a one-position run whose value needs arithmetic):
+// the run summed in ascending position order into grad_unique[o].
 //
-// SGD (the fused dr_ev_pool_grad_rows_apply_sgd): a run that is not long is
-// applied to its var row (v -= lr * sum) instead of stored; a long run's
-// first chunk goes to grad_unique[c0] (its sorted head), for
-// rows_finish_kernel<SGD> to combine and apply.
+// SGD (the fused dr_ev_pool_grad_rows_apply_sgd): the run's sum is applied
+// to its var row (v -= lr * sum) instead of stored.
 template <int VEC, int G, int CPL, bool W, bool SGD = false, bool WB = false>
 __global__ __launch_bounds__(256) void rows_work_kernel(
     RowsGroup g, int T, int64_t B, const uint32_t* __restrict__ skey,
     const int32_t* __restrict__ perm, const int32_t* __restrict__ ex,
     const int32_t* __restrict__ base, int dim, const int32_t* __restrict__ work,
-    const int32_t* __restrict__ nwork, uint64_t* __restrict__ gptr, float* __restrict__ gu,
-    float* __restrict__ part, int32_t* __restrict__ longs, int32_t* __restrict__ nlong, int* st,
+    const int32_t* __restrict__ nwork, uint64_t* __restrict__ gptr, float* __restrict__ gu, int* st,
     RowsSgd sg) {
   const int nw = *nwork;
   if ((int64_t)blockIdx.x * (256 / G) >= nw) return;   // block-uniform (empty list: one load)
@@ -434,7 +513,7 @@ __global__ __launch_bounds__(256) void rows_work_kernel(
   constexpr int GPB = 256 / G;
   // positions of a run fetched per step: the serial sum's loads are issued
   // CH at a time -- deeper for scalar rows (one register per row chunk), so
-  // a 256-position chunk of a hot id is 16 dependent steps instead of 32
+  // a 256-position run is 16 dependent steps instead of 32
   constexpr int CH = VEC * CPL <= 1 ? 16 : kRowsChain;
   const int64_t N = sk[T];
   const int lg = threadIdx.x % G;
@@ -466,31 +545,19 @@ __global__ __launch_bounds__(256) void rows_work_kernel(
     const uint32_t u = skey[c0];
     const int32_t pc = perm[c0];
     const int t = tab_of(sk, T, pc);
-    const bool first = c0 == 0 || skey[c0 - 1] != u || tab_of(sk, T, perm[c0 - 1]) != t;
-    bool islong;
-    int64_t lim;
-    if (first) {
-      islong = c0 + kRowsChunk < N && skey[c0 + kRowsChunk] == u &&
-               tab_of(sk, T, perm[c0 + kRowsChunk]) == t;
-      lim = islong ? (c0 / kRowsChunk + 1) * kRowsChunk : N;
-    } else {
-      if (!run_is_long(skey, perm, sk, T, N, c0, u, t)) continue;  // inside a short run
-      islong = true;
-      lim = c0 + kRowsChunk;
-    }
-    if (lim > N) lim = N;
+    const int64_t lim = c0 + kRowsChunk < N ? c0 + kRowsChunk : N;
     // a one-position run (the common case under uniform keys when the
     // run's value needs arithmetic, e.g. unaligned rows): one row load
     // instead of a CH-position speculative chunk
-    const bool single = first && !islong &&
-                        (c0 + 1 >= N || skey[c0 + 1] != u || tab_of(sk, T, perm[c0 + 1]) != t);
+    const bool single =
+        c0 + 1 >= N || skey[c0 + 1] != u || tab_of(sk, T, perm[c0 + 1]) != t;
     const dr_pool_grad_desc& d = sd[t];
     const int mode = d.combiner == DR_COMBINER_SUM ? 0 : (d.combiner == DR_COMBINER_MEAN ? 1 : 2);
     const bool zero_start = mode == 0 || (W && d.weights);
     R acc;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<V>();
-    bool fresh = !(first && zero_start);
+    bool fresh = !zero_start;
     const float* tg = d.top_grad;
     const int64_t ts = d.top_stride;
     const int64_t* segp = d.seg;
@@ -569,137 +636,307 @@ __global__ __launch_bounds__(256) void rows_work_kernel(
       if (!ok[CH - 1]) break;
     }
     if (cbad) latch(st, DR_INVALID_ARGUMENT);
-    if (first) {
-      if constexpr (SGD) {
-        static_assert(!SGD || VEC == 4, "fused SGD takes 16-byte rows");
-        if (!islong) {
-          sgd_row<G, CPL, WB>(acc, spool[t], sver[t], (int64_t)u, dim, sg.lr, sg.gs, lg, dv);
-          continue;
-        }
-      }
-      const int64_t o = SGD ? c0 : kt0 + (int64_t)ex[pc] - sb[t];
+    if constexpr (SGD) {
+      static_assert(!SGD || VEC == 4, "fused SGD takes 16-byte rows");
+      sgd_row<G, CPL, WB>(acc, spool[t], sver[t], (int64_t)u, dim, sg.lr, sg.gs, lg, dv);
+    } else {
+      const int64_t o = kt0 + (int64_t)ex[pc] - sb[t];
       float* dst = gu + o * (int64_t)dim;
       store_row<VEC, G, CPL>(acc, dst, lg, dv);
-      if (lg == 0) {
-        if (!SGD) gptr[o] = (uint64_t)(uintptr_t)dst;
-        if (islong) {
-          const int32_t at = atomicAdd(nlong, 1);
-          longs[2 * at] = (int32_t)o;
-          longs[2 * at + 1] = (int32_t)c0;
-        }
-      }
-    } else {
-      store_row<VEC, G, CPL>(acc, part + (c0 / kRowsChunk) * (int64_t)dim, lg, dv);
+      if (lg == 0) gptr[o] = (uint64_t)(uintptr_t)dst;
     }
   }
 }
 
-// grad_unique[o] for the queued long runs: c_0 (in grad_unique[o]) plus the
-// chunk partials c_k (k >= 1, in part[m_k / chunk] for the multiples m_k of
-// the chunk inside the run).  One BLOCK per run: its GPB lane groups take
-// the partials in blocks of FC, group q blocks q, q + GPB, ..., each summed
-// in order; then c_0 + S_0 + S_1 + ... + S_{GPB-1} in group order.  A fixed
-// association (deterministic, fp32 tolerance like every long run), with the
-// serial chain of a hot id cut GPB-fold (a DIN padding id: 800 partials).
-// SGD: the combined row is applied to the run's var row instead of stored.
-template <int VEC, int G, int CPL, bool SGD = false, bool WB = false>
-__global__ __launch_bounds__(256) void rows_finish_kernel(
-    RowsGroup g, int T, const uint32_t* __restrict__ skey, const int32_t* __restrict__ perm,
-    int dim, float* __restrict__ gu, const float* __restrict__ part,
-    const int32_t* __restrict__ longs, const int32_t* __restrict__ nlong, int64_t nslots,
-    RowsSgd sg) {
-  constexpr int GPB = 256 / G;
+// ---- long runs (more than kRowsChunk positions) ------------------------------
+
+// Columns c, c + 1 (c + 1 < dim or ignored) of a finished run: the
+// IndexedSlices row o (unfused), or v -= lr * sum on the var row u of table
+// t (SGD: one fp32 product, one fp32 difference per value, as sgd4; bf16 rows
+// widened, updated and rounded once per packed pair, as sgd_ld / sgd_st).
+template <bool SGD, bool WB>
+__device__ __forceinline__ void rows_fin_pair(const RowsSgd& sg, int t, uint32_t u, int64_t o,
+                                              int dim, int c, float a, float b, float* gu) {
+  if constexpr (SGD) {
+    if constexpr (WB) {
+      uint32_t* row = static_cast<uint32_t*>(sg.pool[t]) + (int64_t)u * (dim / 2);
+      const float2 w = bf16x2_to_f2(row[c / 2]);
+      const float pa = sg.lr * a, pb = sg.lr * b;
+      row[c / 2] = f2_to_bf16x2(w.x - pa, w.y - pb);
+    } else {
+      float* row = static_cast<float*>(sg.pool[t]) + (int64_t)u * dim;
+      const float pa = sg.lr * a;
+      row[c] = row[c] - pa;
+      if (c + 1 < dim) {
+        const float pb = sg.lr * b;
+        row[c + 1] = row[c + 1] - pb;
+      }
+    }
+  } else {
+    float* dst = gu + o * (int64_t)dim;
+    dst[c] = a;
+    if (c + 1 < dim) dst[c + 1] = b;
+  }
+}
+
+// Once per finished run: the steps_to_live version (SGD) or the by-address
+// gradient pointer of IndexedSlices row o (unfused).
+template <bool SGD>
+__device__ __forceinline__ void rows_fin_run(const RowsSgd& sg, int t, uint32_t u, int64_t o,
+                                             int dim, const RowsLong& L) {
+  if constexpr (SGD) {
+    if (sg.version[t]) sg.version[t][u] = sg.gs;
+  } else {
+    L.gptr[o] = (uint64_t)(uintptr_t)(L.gu + o * (int64_t)dim);
+  }
+}
+
+// Is sorted position q in the run of (u, table slice [lo, hi) of positions)?
+__device__ __forceinline__ bool in_run(const RowsLong& L, int64_t N, int64_t q, uint32_t u,
+                                       int64_t lo, int64_t hi) {
+  const int64_t qc = q < N ? q : N - 1;
+  const uint32_t kq = L.skey[qc];
+  const int32_t pq = L.perm[qc];
+  return (q < N) & (kq == u) & (pq >= lo) & (pq < hi);
+}
+
+// One block per long run: its end (two rounds of parallel probes -- every
+// kRowsChunk-th position past the head, then the 256 positions of the window
+// the run ends in: a run's positions are contiguous, so in_run is a prefix),
+// then its pieces of kSerialMax positions as work items.
+__global__ __launch_bounds__(256) void rows_expand_kernel(RowsGroup g, int T, RowsLong L) {
   __shared__ int64_t sk[DR_MAX_GROUP + 1];
-  __shared__ __attribute__((aligned(16))) float red[256 * VEC * CPL];  // GPB group sums (dim <= G*VEC*CPL)
-  __shared__ int used[GPB];
+  __shared__ int smin;
+  __shared__ int sfirst;
   if (threadIdx.x <= T) sk[threadIdx.x] = g.koff[threadIdx.x];
   __syncthreads();
   const int64_t N = sk[T];
-  const int n = *nlong;
-  const int q = threadIdx.x / G;
-  const int lg = threadIdx.x % G;
-  const int dv = dim / VEC;
-  using R = Row<VEC, G, CPL>;
-  using V = typename VecT<VEC>::T;
-  // <= 128 floats of partial rows in flight per lane
-  constexpr int FC = 128 / (VEC * CPL) < 8 ? 8
-                     : (128 / (VEC * CPL) > kRowsFinishMax ? kRowsFinishMax
-                                                           : 128 / (VEC * CPL));
+  const int n = *L.nlong;
   for (int i = blockIdx.x; i < n; i += gridDim.x) {   // block-uniform
-    const int64_t o = longs[2 * i], c0 = longs[2 * i + 1];
-    const uint32_t u = skey[c0];
-    const int t = tab_of(sk, T, perm[c0]);
-    const int64_t kt0 = sk[t], nnz_t = sk[t + 1] - sk[t];
-    R acc;
+    const int64_t c0 = L.longs[i];
+    const uint32_t u = L.skey[c0];
+    const int t = tab_of(sk, T, L.perm[c0]);
+    const int64_t lo = sk[t], hi = sk[t + 1];
+    int64_t a = c0;   // a position known to be in the run
+    int64_t w0 = 0;   // last in-run probe of the coarse round
+    for (;;) {
+      if (threadIdx.x == 0) smin = 0x7FFFFFFF;
+      __syncthreads();
 #pragma unroll
-    for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<V>();
-    bool any = false;
-    const int64_t m1 = (c0 / kRowsChunk + 1) * kRowsChunk;   // first partial of the run
-    for (int64_t m = m1 + (int64_t)q * FC * kRowsChunk; m < N;
-         m += (int64_t)GPB * FC * kRowsChunk) {
-      R y[FC];
-      bool ok[FC];
-      uint32_t kj[FC];
-      int32_t pj[FC];
-      // unconditional, clamped loads first: a short-circuit test per chunk
-      // would branch around each load and serialise them
-#pragma unroll
-      for (int j = 0; j < FC; ++j) {
-        const int64_t mj = m + j * kRowsChunk;
-        const int64_t mc = mj < N ? mj : N - 1;
-        kj[j] = skey[mc];
-        pj[j] = perm[mc];
-        int64_t sl = mc / kRowsChunk;
-        sl = sl < nslots ? sl : nslots - 1;
-        load_row_u<VEC, G, CPL>(y[j], part + sl * (int64_t)dim, lg, dv);
+      for (int r = 0; r < 8; ++r) {
+        const int m = 1 + threadIdx.x + 256 * r;
+        if (!in_run(L, N, a + kRowsChunk * (int64_t)m, u, lo, hi)) atomicMin(&smin, m);
       }
-#pragma unroll
-      for (int j = 0; j < FC; ++j) {
-        const int64_t k = (int64_t)pj[j] - kt0;   // in table t <=> in [0, nnz_t)
-        ok[j] = (m + j * kRowsChunk < N) & (kj[j] == u) & (k >= 0) & (k < nnz_t);
+      __syncthreads();
+      const int mm = smin;
+      __syncthreads();
+      if (mm != 0x7FFFFFFF) {
+        w0 = a + kRowsChunk * (int64_t)(mm - 1);
+        break;
       }
-      if (!ok[0]) break;
-      if (any) {
-        acc_add(acc, y[0]);
-      } else {
-        acc = y[0];
-        any = true;
-      }
-      // ok[] is a prefix (a run's chunks are contiguous): predicated adds
-#pragma unroll
-      for (int j = 1; j < FC; ++j)
-        if (ok[j]) acc_add(acc, y[j]);
-      if (!ok[FC - 1]) break;
+      a += kRowsChunk * 2048;   // (runs of more than 2^19 positions: another round)
     }
-    // group sums -> LDS, then group 0 adds them to c_0 in group order
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      const int col = lg + c * G;
-      if (col < dv) reinterpret_cast<V*>(red + q * dim)[col] = acc.v[c];
-    }
-    if (lg == 0) used[q] = any ? 1 : 0;
+    if (threadIdx.x == 0) smin = 0x7FFFFFFF;
     __syncthreads();
-    if (q == 0) {
-      R tot;
-      load_row_u<VEC, G, CPL>(tot, gu + o * (int64_t)dim, lg, dv);
-      for (int r = 0; r < GPB; ++r) {
-        if (!used[r]) continue;
-        R x;
+    // the end lies in (w0, w0 + kRowsChunk]: one probe per thread
+    if (!in_run(L, N, w0 + 1 + threadIdx.x, u, lo, hi)) atomicMin(&smin, (int)threadIdx.x);
+    __syncthreads();
+    const int64_t len = w0 + 1 + smin - c0;
+    const int np = (int)((len + kSerialMax - 1) / kSerialMax);
+    if (threadIdx.x == 0) {
+      const int fi = atomicAdd(L.nitems, np);
+      L.rlen[i] = (int32_t)len;
+      L.rfirst[i] = fi;
+      sfirst = fi;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < np; k += 256) {
+      L.items[2 * (sfirst + k)] = i;
+      L.items[2 * (sfirst + k) + 1] = k;
+    }
+    __syncthreads();   // smin / sfirst are rewritten by the next run
+  }
+}
+
+// One block per (piece, column slice of SW columns): the piece's terms in
+// ascending position order.  All 256 threads load the gradient-row slices of
+// S positions at a time (R loads in flight per thread, the next stage's rows
+// issued before this stage is summed) and write them, scaled, into LDS; wave
+// 0 then walks the serial chain of each column (one lane per column) through
+// the stage.  A one-piece run is finished here; a piece of a longer run
+// stores its partial for rows_combine_kernel.
+template <int VEC, int SW, bool SGD, bool WB>
+__global__ __launch_bounds__(256) void rows_serial_kernel(RowsGroup g, int T, int dim, RowsLong L,
+                                                          RowsSgd sg) {
+  using V = typename VecT<VEC>::T;
+  constexpr int SV = SW / VEC;             // vectors of a position's slice
+  constexpr int PI = 256 / SV;             // positions per load instruction
+  constexpr int R = VEC == 4 ? 16 : 32;    // loads in flight per thread
+  constexpr int S = PI * R;                // positions per stage
+  static_assert(SV >= 1 && 256 % SV == 0, "slice shape");
+  __shared__ __attribute__((aligned(16))) float stage[S * SW];
+  __shared__ int64_t sk[DR_MAX_GROUP + 1];
+  if (threadIdx.x <= T) sk[threadIdx.x] = g.koff[threadIdx.x];
+  __syncthreads();
+  const int nsl = (dim + SW - 1) / SW;
+  const int64_t total = (int64_t)(*L.nitems) * nsl;
+  const int tid = threadIdx.x;
+  const int pv = tid / SV, cv = tid % SV;
+  const int lane = tid & 63;
+  const int lc = lane < SW ? lane : 0;
+  for (int64_t wi = blockIdx.x; wi < total; wi += gridDim.x) {   // block-uniform
+    const int j = (int)(wi / nsl), slice = (int)(wi % nsl);
+    const int i = __builtin_amdgcn_readfirstlane(L.items[2 * j]);
+    const int k = __builtin_amdgcn_readfirstlane(L.items[2 * j + 1]);
+    const int64_t c0 = __builtin_amdgcn_readfirstlane(L.longs[i]);
+    const int64_t len = __builtin_amdgcn_readfirstlane(L.rlen[i]);
+    const int np = (int)((len + kSerialMax - 1) / kSerialMax);
+    const int64_t ps = c0 + (int64_t)k * kSerialMax;
+    const int64_t pe = c0 + len < ps + kSerialMax ? c0 + len : ps + kSerialMax;
+    const int32_t pc = __builtin_amdgcn_readfirstlane(L.perm[c0]);
+    const uint32_t u = (uint32_t)__builtin_amdgcn_readfirstlane((int)L.skey[c0]);
+    const int t = __builtin_amdgcn_readfirstlane(tab_of(sk, T, pc));
+    const dr_pool_grad_desc& d = g.d[t];
+    const bool wt = d.weights != nullptr;
+    const bool qs = wt && d.bag_scale;
+    const bool ms = !wt && d.combiner != DR_COMBINER_SUM;
+    const bool zs = d.combiner == DR_COMBINER_SUM || wt;
+    const int colv = slice * SV + cv;                 // this thread's vector column
+    const float* src = d.top_grad + (colv * VEC < dim ? colv * VEC : 0);
+    const int64_t ts = d.top_stride;
+    // bag rows one stage ahead of the row loads; every load is clamped to the
+    // piece, so the batches issue unconditionally (a branch around a batch
+    // would make the compiler wait for it at the join)
+    int32_t rq[R];
+    auto load_idx = [&](int64_t b0) {
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-          const int col = lg + c * G;
-          x.v[c] = col < dv ? reinterpret_cast<const V*>(red + r * dim)[col] : vzero<V>();
-        }
-        acc_add(tot, x);
+      for (int r = 0; r < R; ++r) {
+        int64_t q = b0 + r * PI + pv;
+        q = q < pe ? q : pe - 1;
+        rq[r] = L.srow[q];
       }
-      if constexpr (SGD) {
-        static_assert(!SGD || VEC == 4, "fused SGD takes 16-byte rows");
-        sgd_row<G, CPL, WB>(tot, sg.pool[t], sg.version[t], (int64_t)u, dim, sg.lr, sg.gs, lg, dv);
+    };
+    uint32_t zmask = 0;   // invalid bags among the rows in flight (zero terms)
+    auto take = [&]() {
+      zmask = 0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) zmask |= (rq[r] < 0 ? 1u : 0u) << r;
+    };
+    V y[R];
+    auto load_rows = [&]() {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int64_t rr = rq[r] >= 0 ? rq[r] : 0;
+        y[r] = gld(reinterpret_cast<const V*>(src + rr * ts));
+      }
+    };
+    float acc = 0.f;
+    bool fresh = !(k == 0 && zs);   // first term: 0 + y (zero-started sum) or y
+    load_idx(ps);
+    take();
+    load_rows();
+    load_idx(ps + S);
+    for (int64_t b0 = ps; b0 < pe; b0 += S) {
+      // y: this stage's rows in flight; rq: the next stage's bag rows
+      if (wt || ms) {   // block-uniform: the terms' factors (rows_term), then scaled
+        float mf[R], df[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          int64_t q = b0 + r * PI + pv;
+          q = q < pe ? q : pe - 1;
+          mf[r] = L.smul[q];
+          df[r] = qs ? L.sdiv[q] : 1.f;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          V x = y[r];
+          if ((zmask >> r) & 1u) x = vzero<V>();
+          if (wt) {
+            if (qs) x = vdiv(x, df[r]);
+            x = vmul(x, mf[r]);
+          } else if (mf[r] != 1.f) {
+            x = vmul(x, mf[r]);
+          }
+          *reinterpret_cast<V*>(stage + (r * PI + pv) * SW + cv * VEC) = x;
+        }
       } else {
-        store_row<VEC, G, CPL>(tot, gu + o * (int64_t)dim, lg, dv);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          V x = y[r];
+          if ((zmask >> r) & 1u) x = vzero<V>();
+          *reinterpret_cast<V*>(stage + (r * PI + pv) * SW + cv * VEC) = x;
+        }
+      }
+      __syncthreads();
+      take();
+      load_rows();              // the next stage's rows: in flight while wave 0 sums this one
+      load_idx(b0 + 2 * S);
+      if (tid < 64) {           // wave-uniform
+        const int nv = (int)(pe - b0 < S ? pe - b0 : S);
+        const float* sp = stage + lc;
+        int jj = 0;
+        if (fresh) {
+          acc = sp[0];
+          fresh = false;
+          jj = 1;
+        }
+        for (; jj + 8 <= nv; jj += 8) {
+          float x[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) x[q] = sp[(jj + q) * SW];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc = acc + x[q];
+        }
+        for (; jj < nv; ++jj) acc = acc + sp[jj * SW];
+      }
+      __syncthreads();   // the stage is rewritten next
+    }
+    if (tid < 64) {
+      const int col = slice * SW + lane;
+      const float nxt = __shfl_down(acc, 1, 64);
+      if (np == 1) {
+        const int64_t o = SGD ? 0 : sk[t] + (int64_t)L.ex[pc] - L.base[t];
+        if (lane < SW && (lane & 1) == 0 && col < dim)
+          rows_fin_pair<SGD, WB>(sg, t, u, o, dim, col, acc, nxt, L.gu);
+        if (slice == 0 && lane == 0) rows_fin_run<SGD>(sg, t, u, o, dim, L);
+      } else if (lane < SW && col < dim) {
+        L.part[(int64_t)j * dim + col] = acc;
       }
     }
-    __syncthreads();   // red / used are rewritten by the next run
+  }
+}
+
+// Runs of several pieces: ((p_0 + p_1) + p_2) + ... of the piece partials in
+// piece order (deterministic, independent of which block summed which
+// piece), then finished as in rows_serial_kernel.
+template <bool SGD, bool WB>
+__global__ __launch_bounds__(256) void rows_combine_kernel(RowsGroup g, int T, int dim, RowsLong L,
+                                                           RowsSgd sg) {
+  __shared__ int64_t sk[DR_MAX_GROUP + 1];
+  if (threadIdx.x <= T) sk[threadIdx.x] = g.koff[threadIdx.x];
+  __syncthreads();
+  const int n = *L.nlong;
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {   // block-uniform
+    const int64_t len = L.rlen[i];
+    const int np = (int)((len + kSerialMax - 1) / kSerialMax);
+    if (np <= 1) continue;
+    const int64_t fi = L.rfirst[i];
+    const int64_t c0 = L.longs[i];
+    const int32_t pc = L.perm[c0];
+    const uint32_t u = L.skey[c0];
+    const int t = tab_of(sk, T, pc);
+    const int64_t o = SGD ? 0 : sk[t] + (int64_t)L.ex[pc] - L.base[t];
+    for (int c = 2 * threadIdx.x; c < dim; c += 512) {
+      const bool two = c + 1 < dim;
+      float a = L.part[fi * dim + c];
+      float b = two ? L.part[fi * dim + c + 1] : 0.f;
+      for (int q = 1; q < np; ++q) {
+        a = a + L.part[(fi + q) * dim + c];
+        if (two) b = b + L.part[(fi + q) * dim + c + 1];
+      }
+      rows_fin_pair<SGD, WB>(sg, t, u, o, dim, c, a, b, L.gu);
+    }
+    if (threadIdx.x == 0) rows_fin_run<SGD>(sg, t, u, o, dim, L);
   }
 }
 
@@ -739,12 +976,23 @@ struct RowsWs {
   int64_t* total;
   int32_t* nlong;
   int32_t* nwork;
+  int32_t* nitems;
   int32_t* work;
+  int32_t* srow;
+  float* smul;
+  float* sdiv;
   int32_t* longs;
+  int32_t* rlen;
+  int32_t* rfirst;
+  int32_t* items;
   float* part;
   void* sort_ws;
   size_t sort_bytes;
   void* scan_ws;
+  RowsLong longrun(uint64_t* gptr, float* gu) const {
+    return RowsLong{kout, perm, ex, base, srow, smul, sdiv, longs, nlong, rlen, rfirst, items,
+                    nitems, gptr, gu, part};
+  }
 };
 
 static RowsWs carve_rows(void* ws, int64_t n, size_t* used) {
@@ -761,15 +1009,70 @@ static RowsWs carve_rows(void* ws, int64_t n, size_t* used) {
   w.total = c.take<int64_t>(1);
   w.nlong = c.take<int32_t>(1);
   w.nwork = c.take<int32_t>(1);
+  w.nitems = c.take<int32_t>(1);
   w.work = c.take<int32_t>(nn);
-  const int64_t chunks = nn / kRowsChunk + 2;
-  w.longs = c.take<int32_t>(2 * chunks);
-  w.part = c.take<float>(chunks * kRowsMaxDim);
+  w.srow = c.take<int32_t>(nn);
+  w.smul = c.take<float>(nn);
+  w.sdiv = c.take<float>(nn);
+  // runs longer than kRowsChunk, and their pieces: at most one per
+  // kRowsChunk + 1 positions each
+  const int64_t runs = nn / (kRowsChunk + 1) + 2;
+  w.longs = c.take<int32_t>(runs);
+  w.rlen = c.take<int32_t>(runs);
+  w.rfirst = c.take<int32_t>(runs);
+  w.items = c.take<int32_t>(2 * runs);
+  w.part = c.take<float>(runs * kRowsMaxDim);
   w.sort_bytes = sort_pairs_u32_ws_bytes(nn);
   w.sort_ws = c.take<char>(w.sort_bytes);
   w.scan_ws = c.take<char>(scan_ws_bytes(nn));
   if (used) *used = c.used + 256;
   return w;
+}
+
+// The long-run kernels (expand, serial pieces, combine); empty lists cost one
+// load per block.  Slices of at most 32 columns: a stage of S positions is
+// 64 KiB (fp32 rows) / 32 KiB (unaligned) of LDS.
+template <int VEC, bool SGD, bool WB>
+static void launch_long(const RowsGroup& g, int T, int dim, const RowsLong& L, const RowsSgd& sg,
+                        hipStream_t s) {
+  const int64_t N = g.koff[T];
+  if (N <= kRowsChunk) return;
+  const int64_t runs = N / (kRowsChunk + 1) + 1;
+  hipLaunchKernelGGL(rows_expand_kernel, dim3((unsigned)(runs < 1024 ? runs : 1024)), dim3(256), 0,
+                     s, g, T, L);
+  int sw = 1;
+  while (sw < dim && sw < 32) sw <<= 1;
+  if (VEC == 4 && sw < 4) sw = 4;
+  const int64_t nsl = ceil_div(dim, sw);
+  int64_t sb = runs * nsl;
+  if (sb > 1024) sb = 1024;
+  const dim3 grid((unsigned)sb);
+#define DR_SERIAL(SWC)                                                                         \
+  hipLaunchKernelGGL((rows_serial_kernel<VEC, SWC, SGD, WB>), grid, dim3(256), 0, s, g, T, dim, L, \
+                     sg)
+  if constexpr (VEC == 4) {
+    switch (sw) {
+      case 4: DR_SERIAL(4); break;
+      case 8: DR_SERIAL(8); break;
+      case 16: DR_SERIAL(16); break;
+      default: DR_SERIAL(32); break;
+    }
+  } else {
+    switch (sw) {
+      case 1: DR_SERIAL(1); break;
+      case 2: DR_SERIAL(2); break;
+      case 4: DR_SERIAL(4); break;
+      case 8: DR_SERIAL(8); break;
+      case 16: DR_SERIAL(16); break;
+      default: DR_SERIAL(32); break;
+    }
+  }
+#undef DR_SERIAL
+  if (N > kSerialMax) {
+    const int64_t big = N / (kSerialMax + 1) + 1;
+    hipLaunchKernelGGL((rows_combine_kernel<SGD, WB>), dim3((unsigned)(big < 256 ? big : 256)),
+                       dim3(256), 0, s, g, T, dim, L, sg);
+  }
 }
 
 template <int VEC, int G, int CPL>
@@ -783,47 +1086,36 @@ static void launch_rows(const RowsGroup& g, int T, int64_t B, const RowsWs& w, i
   if (weighted)
     hipLaunchKernelGGL((rows_work_kernel<VEC, G, CPL, true>), dim3((unsigned)blocks), dim3(256),
                        0, s, g, T, B, w.kout, w.perm, w.ex, w.base, dim, w.work, w.nwork, gptr,
-                       gu, w.part, w.longs, w.nlong, st, RowsSgd{});
+                       gu, st, RowsSgd{});
   else
     hipLaunchKernelGGL((rows_work_kernel<VEC, G, CPL, false>), dim3((unsigned)blocks), dim3(256),
                        0, s, g, T, B, w.kout, w.perm, w.ex, w.base, dim, w.work, w.nwork, gptr,
-                       gu, w.part, w.longs, w.nlong, st, RowsSgd{});
-  if (N > kRowsChunk) {
-    // one block per queued run (at most one per chunk); most runs of a
-    // hotness-1 batch hold a single partial, so blocks, not lanes, carry them
-    const int64_t nslots = N / kRowsChunk + 2;
-    const unsigned fb = (unsigned)(nslots < 2048 ? nslots : 2048);
-    hipLaunchKernelGGL((rows_finish_kernel<VEC, G, CPL>), dim3(fb), dim3(256), 0, s, g, T,
-                       w.kout, w.perm, dim, gu, w.part, w.longs, w.nlong, nslots, RowsSgd{});
-  }
+                       gu, st, RowsSgd{});
+  launch_long<VEC, false, false>(g, T, dim, w.longrun(gptr, gu), RowsSgd{}, s);
 }
 
-// The fused SGD tail: direct rows + worklist (rows_sgd_kernel), runs
-// (rows_work_kernel<SGD>), long runs (rows_finish_kernel<SGD>).  gu: [n, dim]
-// scratch for the first chunks of long runs, indexed by sorted head.
+// The fused SGD tail: direct rows + worklist (rows_sgd_kernel), runs of 2 ..
+// kRowsChunk positions (rows_work_kernel<SGD>), long runs (launch_long).
 template <int G, int CPL, bool WB>
 static void launch_rows_sgd(const RowsGroup& g, int T, int64_t B, const RowsWs& w, int dim,
-                            bool weighted, uint32_t sentinel, const RowsSgd& sg, float* gu,
-                            hipStream_t s, int* st) {
+                            bool weighted, uint32_t sentinel, const RowsSgd& sg, hipStream_t s,
+                            int* st) {
   const int64_t N = g.koff[T];
+  const RowsLong L = w.longrun(nullptr, nullptr);
   hipLaunchKernelGGL((rows_sgd_kernel<G, WB>), dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, s,
-                     g, sg, T, B, w.kout, w.perm, sentinel, dim, w.work, w.nwork);
+                     g, sg, T, B, w.kout, w.perm, sentinel, dim, w.work, w.nwork, L, w.longs,
+                     w.nlong, st);
   int64_t blocks = ceil_div(N, 256 / G);
   if (blocks > 1024) blocks = 1024;   // grid-stride: an idle block still costs its dispatch
   if (weighted)
     hipLaunchKernelGGL((rows_work_kernel<4, G, CPL, true, true, WB>), dim3((unsigned)blocks),
                        dim3(256), 0, s, g, T, B, w.kout, w.perm, nullptr, nullptr, dim, w.work,
-                       w.nwork, nullptr, gu, w.part, w.longs, w.nlong, st, sg);
+                       w.nwork, nullptr, nullptr, st, sg);
   else
     hipLaunchKernelGGL((rows_work_kernel<4, G, CPL, false, true, WB>), dim3((unsigned)blocks),
                        dim3(256), 0, s, g, T, B, w.kout, w.perm, nullptr, nullptr, dim, w.work,
-                       w.nwork, nullptr, gu, w.part, w.longs, w.nlong, st, sg);
-  if (N > kRowsChunk) {
-    const int64_t nslots = N / kRowsChunk + 2;
-    const unsigned fb = (unsigned)(nslots < 2048 ? nslots : 2048);
-    hipLaunchKernelGGL((rows_finish_kernel<4, G, CPL, true, WB>), dim3(fb), dim3(256), 0, s, g, T,
-                       w.kout, w.perm, dim, gu, w.part, w.longs, w.nlong, nslots, sg);
-  }
+                       w.nwork, nullptr, nullptr, st, sg);
+  launch_long<4, true, WB>(g, T, dim, L, sg, s);
 }
 
 // Fused row-grouped backward + KV SGD (ev.hip dr_ev_pool_grad_rows_apply_sgd
@@ -855,31 +1147,30 @@ int rows_apply_sgd(const dr_pool_grad_desc* descs_host, int num_tables, int64_t 
   const int64_t n = g.koff[num_tables];
   DR_REQUIRE(n < (1ll << 31), DR_INVALID_ARGUMENT, "too many nnz");
   DR_REQUIRE(batch > 0 || n == 0, DR_INVALID_ARGUMENT, "nnz without a batch");
-  // workspace: the backward's, plus [n, dim] fp32 for long runs' first chunks
-  const size_t wsr = dr_pool_grad_rows_workspace_size(n);
-  const size_t need = wsr + 256 + (size_t)(n > 0 ? n : 1) * dim * sizeof(float);
-  DR_REQUIRE(ws_bytes >= need, DR_INVALID_ARGUMENT, "workspace too small");
+  DR_REQUIRE(batch < (1ll << 31), DR_INVALID_ARGUMENT, "batch must be < 2^31");
+  DR_REQUIRE(ws_bytes >= dr_pool_grad_rows_workspace_size(n), DR_INVALID_ARGUMENT,
+             "workspace too small");
   if (n == 0) return DR_OK;
   int* st = status_word();
   DR_REQUIRE(st, DR_INTERNAL, "status word unavailable");
   RowsWs w = carve_rows(ws, n, nullptr);
-  float* gu = reinterpret_cast<float*>(static_cast<char*>(ws) + ((wsr + 255) & ~size_t(255)));
   DR_REQUIRE(row_limit < ((int64_t)1 << 32) - 1, DR_INVALID_ARGUMENT,
              "row_limit must be < 2^32 - 1");
   int rb = 1;
   while (rb < 32 && ((int64_t)1 << rb) <= row_limit) ++rb;
   const uint32_t sentinel = (uint32_t)(((uint64_t)1 << rb) - 1);
   hipLaunchKernelGGL(rows_keys_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, rowsel,
-                     n, row_limit, sentinel, w.kin, w.vin, (int32_t*)nullptr, w.nlong, w.nwork);
+                     n, row_limit, sentinel, w.kin, w.vin, (int32_t*)nullptr, w.nlong, w.nwork,
+                     w.nitems);
   DR_LAUNCH_CHECK();
   int rc = sort_pairs_u32(w.kin, w.vin, w.kout, w.perm, n, rb, w.sort_ws, s);
   if (rc) return rc;
   const int d4 = dim / 4;
 #define DR_ROWS_SGD(G, CPL)                                                                  \
   (sg.bf16 ? launch_rows_sgd<G, CPL, true>(g, num_tables, batch, w, dim, weighted, sentinel, sg, \
-                                           gu, s, st)                                          \
+                                           s, st)                                              \
            : launch_rows_sgd<G, CPL, false>(g, num_tables, batch, w, dim, weighted, sentinel, sg, \
-                                            gu, s, st))
+                                            s, st))
   if (d4 <= 8)
     DR_ROWS_SGD(8, 1);
   else if (d4 <= 16)
@@ -944,6 +1235,7 @@ int dr_pool_grad_rows_grouped_ex(const dr_pool_grad_desc* descs_host, int num_ta
   const int64_t n = g.koff[num_tables];
   DR_REQUIRE(n < (1ll << 31), DR_INVALID_ARGUMENT, "too many nnz");
   DR_REQUIRE(batch > 0 || n == 0, DR_INVALID_ARGUMENT, "nnz without a batch");
+  DR_REQUIRE(batch < (1ll << 31), DR_INVALID_ARGUMENT, "batch must be < 2^31");
   DR_REQUIRE(ws_bytes >= dr_pool_grad_rows_workspace_size(n), DR_INVALID_ARGUMENT,
              "workspace too small");
   hipStream_t s = S(stream);
@@ -961,12 +1253,13 @@ int dr_pool_grad_rows_grouped_ex(const dr_pool_grad_desc* descs_host, int num_ta
   const uint32_t sentinel = (uint32_t)(((uint64_t)1 << rb) - 1);
   const unsigned nb = (unsigned)ceil_div(n, 256);
   hipLaunchKernelGGL(rows_keys_kernel, dim3(nb), dim3(256), 0, s, rowsel, n, row_limit, sentinel,
-                     w.kin, w.vin, w.flags, w.nlong, w.nwork);
+                     w.kin, w.vin, w.flags, w.nlong, w.nwork, w.nitems);
   DR_LAUNCH_CHECK();
   int rc = sort_pairs_u32(w.kin, w.vin, w.kout, w.perm, n, rb, w.sort_ws, s);
   if (rc) return rc;
-  hipLaunchKernelGGL(rows_heads_kernel, dim3(nb), dim3(256), 0, s, g, num_tables, w.kout, w.perm,
-                     sentinel, w.flags, w.work, w.nwork);
+  hipLaunchKernelGGL(rows_heads_kernel, dim3(nb), dim3(256), 0, s, g, num_tables, batch, w.kout,
+                     w.perm, sentinel, w.flags, w.work, w.nwork, w.longrun(grad_ptr, grad_unique),
+                     w.longs, w.nlong, st);
   rc = scan_exclusive_marks(w.flags, w.ex, n, w.total, w.scan_ws, s);
   if (rc) return rc;
   hipLaunchKernelGGL(rows_emit_kernel, dim3(nb), dim3(256), 0, s, g, num_tables, batch, keys,

@@ -3,8 +3,8 @@
 
 When GradientDescentOptimizer.apply_gradients covers every EV of a lookup
 whose gradient nothing else read, the backward runs fused with the update:
-the same run sums (ascending positions; the same chunk association for runs
-longer than 256 positions) and the same v -= lr * g roundings as forming the
+the same run sums (ascending positions; the same 8192-position pieces for
+runs longer than that) and the same v -= lr * g roundings as forming the
 IndexedSlices (dr_pool_grad_rows_grouped_ex) and applying them
 (dr_ev_apply_grouped_ptr_rows), which is the reference composition
 embedding_ops.py:592-675 -> KvResourceSparseApplyGradientDescent
@@ -81,10 +81,9 @@ def _train(dr, fused, tag, batches, D, combiner, lr=0.05, dtype=torch.float32, s
     F = len(batches[0][0])
     evs = [dr.EmbeddingVariable("%s_%d_%d" % (tag, int(fused), f), D, 0.05 * (f + 1),
                                 steps_to_live=stl, value_dtype=dtype) for f in range(F)]
-    # Runs longer than 256 positions are summed in chunks at multiples of 256
-    # of the row-sorted positions, so their association follows the EV's
-    # key -> row map, which parallel first-touch inserts assign in a racy
-    # order.  Keys inserted one at a time give both EVs the same map.
+    # (preinsert: keys inserted one at a time, rows in key order; without it
+    # parallel first-touch inserts number the rows in a racy order -- the
+    # run sums do not depend on it, test_gpu_rows_deterministic.py)
     for e in evs:
         for k in range(preinsert):
             e.insert_synthetic(k, 1, seed=7)
@@ -127,13 +126,13 @@ def _same(a, b):
 def test_fused_sgd_onehot_sum_equals_unfused(dr, D):
     """One-hot sum over 3 tables, vocab small enough for many duplicate runs
     (and, D = 128, ids that repeat > 256 times: long runs, on EVs whose rows
-    were assigned in key order)."""
+    were numbered by racing first-touch inserts)."""
     rng = np.random.default_rng(D)
     B = 3000 if D < 1024 else 700
     vocab = 8 if D == 128 else 400
     batches = [([_onehot(rng.integers(0, vocab, B).astype(np.int64)) for _ in range(3)],
                 rng.standard_normal((B, 3 * D)).astype(np.float32), None) for _ in range(3)]
-    pre = vocab if D == 128 else 0
+    pre = 0
     _same(_train(dr, True, "fso%d" % D, batches, D, "sum", preinsert=pre),
           _train(dr, False, "fso%d" % D, batches, D, "sum", preinsert=pre))
 

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="replay the steps as one captured hipGraph (no host launch gaps)")
     ap.add_argument("--bf16", action="store_true", help="bf16 EV value rows (fp32 slots)")
+    ap.add_argument("--zipf", type=float, default=0.0,
+                    help="Zipf(a) keys (numpy's zipf, mod rows); 0 = uniform")
     args = ap.parse_args()
     import deeprec_amd as dr
     from deeprec_amd.embedding_ops import SparseTensor
@@ -49,7 +51,13 @@ def main():
            "ftrl": lambda: dr.FtrlOptimizer(0.01)}[args.opt]()
     g = torch.Generator(device=dev)
     g.manual_seed(2021)
-    batches = [torch.randint(0, R, (T, B), generator=g, device=dev) for _ in range(4)]
+    if args.zipf > 0:
+        import numpy as np
+        batches = [torch.as_tensor((np.random.default_rng(77 + i).zipf(args.zipf, size=(T, B)) - 1)
+                                   % R, device=dev) for i in range(4)]
+    else:
+        batches = [torch.randint(0, R, (T, B), generator=g, device=dev) for _ in range(4)]
+    hottest = int(max(torch.unique(b[0], return_counts=True)[1].max() for b in batches))
     ind = torch.stack([torch.arange(B, device=dev), torch.zeros(B, dtype=torch.int64, device=dev)], 1)
     upstream = torch.randn((B, T * D), generator=g, device=dev)
 
@@ -89,6 +97,7 @@ def main():
     ms = el / args.steps * 1e3
     print(json.dumps({"probe": "train_step", "opt": args.opt, "graph": bool(args.graph),
                       "bf16": bool(args.bf16), "tables": T, "rows": R, "dim": D,
+                      "zipf": args.zipf, "hottest_run_table0": hottest,
                       "batch": B, "ms_per_step": round(ms, 3),
                       "lookups_per_s": round(T * B / (ms * 1e-3), 1),
                       "samples_per_s": round(B / (ms * 1e-3), 1)}), flush=True)
