@@ -67,6 +67,24 @@ struct EvShared {
   std::mutex mu;
   int64_t known = 0, adds_since_known = 0, adds_since_copy = 0;
   bool copy_pending = false;
+  // which streams reserved adds since `known` was exact (adds) and since the
+  // pending mirror copy was issued (copy_adds): a copy or a sync on stream X
+  // only covers the adds of other streams once they have run
+  struct Streams {
+    bool any = false, mixed = false;
+    hipStream_t st = nullptr;
+    void note(hipStream_t x) {
+      if (!any) {
+        any = true;
+        st = x;
+      } else if (st != x) {
+        mixed = true;
+      }
+    }
+    bool only(hipStream_t x) const { return !mixed && (!any || st == x); }
+  };
+  Streams adds, copy_adds;
+  bool copy_exact = false;
   hipEvent_t copy_ev = nullptr;
   int64_t* pinned_top = nullptr;
   int64_t removed = 0;  // keys removed by dr_ev_shrink (rows are not recycled)
@@ -1367,19 +1385,32 @@ static int reserve(EvShared* s, int64_t n, hipStream_t st) {
   const bool capturing = cs != hipStreamCaptureStatusNone;
   // (event queries are illegal while a global-mode capture is open)
   if (!capturing && s->copy_pending && hipEventQuery(s->copy_ev) == hipSuccess) {
-    s->known = *s->pinned_top;
-    s->adds_since_known = s->adds_since_copy;
+    // a mirror taken on stream X holds every add reserved before it only if
+    // all of those were issued on X (EvGuard keeps each call's reserve and
+    // launch together); otherwise it is dropped and the count stays an
+    // over-estimate
+    if (s->copy_exact) {
+      s->known = *s->pinned_top;
+      s->adds_since_known = s->adds_since_copy;
+      s->adds = s->copy_adds;
+    }
     s->copy_pending = false;
   }
   const int64_t limit = std::min(s->row_cap, s->cap * 3 / 4);
   if (s->known + s->adds_since_known + n > limit) {
     DR_REQUIRE(!capturing, DR_RESOURCE_EXHAUSTED,
                "EV capacity may be exceeded inside stream capture; dr_ev_reserve first");
-    DR_HIP(hipStreamSynchronize(st));
+    // every reserved add must have run before `top` is read: other streams'
+    // too (no new launch on this EV can start: the caller holds its EvGuard)
+    if (s->adds.only(st))
+      DR_HIP(hipStreamSynchronize(st));
+    else
+      DR_HIP(hipDeviceSynchronize());
     int64_t actual = 0;
     DR_HIP(hipMemcpy(&actual, s->top, sizeof(int64_t), hipMemcpyDeviceToHost));
     s->known = actual;
     s->adds_since_known = 0;
+    s->adds = EvShared::Streams();
     s->copy_pending = false;
     if (actual + n > limit) {
       int rc = grow(s, actual + n, st);
@@ -1387,7 +1418,11 @@ static int reserve(EvShared* s, int64_t n, hipStream_t st) {
     }
   }
   s->adds_since_known += n;
-  if (s->copy_pending) s->adds_since_copy += n;
+  s->adds.note(st);
+  if (s->copy_pending) {
+    s->adds_since_copy += n;
+    s->copy_adds.note(st);
+  }
   return DR_OK;
 }
 
@@ -1406,7 +1441,9 @@ static bool want_mirror(EvShared* s, hipStream_t st) {
 static void mirrored(EvShared* s, hipStream_t st) {
   if (hipEventRecord(s->copy_ev, st) != hipSuccess) return;
   s->copy_pending = true;
+  s->copy_exact = s->adds.only(st);
   s->adds_since_copy = 0;
+  s->copy_adds = EvShared::Streams();
 }
 
 static void post_call(EvShared* s, hipStream_t st) {
@@ -2404,11 +2441,15 @@ int dr_ev_reserve(dr_ev* ev, int64_t extra, void* stream) {
   dr::EvShared* s = ev->sh;
   hipStream_t st = dr::S(stream);
   std::lock_guard<std::mutex> g(s->mu);
-  DR_HIP(hipStreamSynchronize(st));
+  if (s->adds.only(st))
+    DR_HIP(hipStreamSynchronize(st));
+  else
+    DR_HIP(hipDeviceSynchronize());   // adds reserved on other streams must have run
   int64_t actual = 0;
   DR_HIP(hipMemcpy(&actual, s->top, sizeof(int64_t), hipMemcpyDeviceToHost));
   s->known = actual;
   s->adds_since_known = 0;
+  s->adds = dr::EvShared::Streams();
   s->copy_pending = false;
   return dr::grow(s, actual + extra, st);
 }

@@ -150,6 +150,38 @@ def test_overlapping_lookup_or_create_while_growing(dr):
     assert ev2.total_count().tolist() == [distinct.size, D]
 
 
+def test_disjoint_threads_fill_to_growth_limit(dr):
+    """Capacity accounting across streams (the mirror of the device row count
+    is taken on one stream; adds reserved on other streams may not have run
+    yet): 16 threads, one stream each, LookupOrCreate disjoint keys in many
+    small calls, every call bringing the EV to or just past its growth limit,
+    so that a count that forgot another stream's pending adds would skip a
+    growth and latch RESOURCE_EXHAUSTED (the key served the default forever).
+    Every key must get its own row and the status word must stay clean."""
+    D = 16
+    rng = np.random.default_rng(23)
+    per, calls = 96, 24
+    keys = rng.choice(1 << 45, size=THREADNUM * per * calls, replace=False).astype(np.int64)
+    for rep in range(2):
+        ev = dr.EmbeddingVariable("mtfill_%d" % rep, D, 0.25, capacity=512)
+
+        def work(i):
+            mine = keys[i * per * calls:(i + 1) * per * calls]
+            for c in range(calls):
+                k = torch.as_tensor(mine[c * per:(c + 1) * per], device=DEV)
+                out = ev.sparse_read(k)
+                assert out.shape == (per, D)
+
+        _in_threads(work, THREADNUM)
+        dr.status_check()
+        assert ev.total_count().tolist() == [keys.size, D]
+        k = ev.export()[0].cpu().numpy()
+        np.testing.assert_array_equal(np.sort(k), np.sort(keys))
+        got = ev.sparse_read(torch.as_tensor(keys, device=DEV)).cpu().numpy()
+        assert bool((got == 0.25).all())
+        dr.status_check()
+
+
 @pytest.mark.parametrize("threads,reps", [(5, 1)])
 def test_feature_filter_parallel(dr, threads, reps):
     """TestFeatureFilterParallel (:1012-1037): EmbeddingConfig(steps_to_live 5,
