@@ -719,14 +719,11 @@ __global__ __launch_bounds__(256) void rows_expand_kernel(RowsGroup g, int T, Ro
     const int64_t lo = sk[t], hi = sk[t + 1];
     int64_t a = c0;   // a position known to be in the run
     int64_t w0 = 0;   // last in-run probe of the coarse round
-    for (;;) {
+    for (;;) {        // one probe per thread: rounds of 256 x kRowsChunk positions
       if (threadIdx.x == 0) smin = 0x7FFFFFFF;
       __syncthreads();
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int m = 1 + threadIdx.x + 256 * r;
-        if (!in_run(L, N, a + kRowsChunk * (int64_t)m, u, lo, hi)) atomicMin(&smin, m);
-      }
+      const int m = 1 + threadIdx.x;
+      if (!in_run(L, N, a + kRowsChunk * (int64_t)m, u, lo, hi)) atomicMin(&smin, m);
       __syncthreads();
       const int mm = smin;
       __syncthreads();
@@ -734,7 +731,7 @@ __global__ __launch_bounds__(256) void rows_expand_kernel(RowsGroup g, int T, Ro
         w0 = a + kRowsChunk * (int64_t)(mm - 1);
         break;
       }
-      a += kRowsChunk * 2048;   // (runs of more than 2^19 positions: another round)
+      a += kRowsChunk * 256;   // (runs of more than 2^16 positions: another round)
     }
     if (threadIdx.x == 0) smin = 0x7FFFFFFF;
     __syncthreads();
@@ -880,12 +877,23 @@ __global__ __launch_bounds__(256) void rows_serial_kernel(RowsGroup g, int T, in
           fresh = false;
           jj = 1;
         }
-        for (; jj + 8 <= nv; jj += 8) {
-          float x[8];
+        // the LDS reads of the next 8 positions are issued before the adds
+        // of these 8: the chain waits on the adds, not on LDS latency
+        if (jj + 8 <= nv) {
+          float xa[8], xb[8];
 #pragma unroll
-          for (int q = 0; q < 8; ++q) x[q] = sp[(jj + q) * SW];
+          for (int q = 0; q < 8; ++q) xa[q] = sp[(jj + q) * SW];
+          for (; jj + 16 <= nv; jj += 8) {
 #pragma unroll
-          for (int q = 0; q < 8; ++q) acc = acc + x[q];
+            for (int q = 0; q < 8; ++q) xb[q] = sp[(jj + 8 + q) * SW];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc = acc + xa[q];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) xa[q] = xb[q];
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc = acc + xa[q];
+          jj += 8;
         }
         for (; jj < nv; ++jj) acc = acc + sp[jj * SW];
       }

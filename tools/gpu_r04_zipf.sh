@@ -1,0 +1,11 @@
+# round 4: Zipf training-step timing + rocprof (long-run kernels)
+set -o pipefail
+T=${1:-x}
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_rows_grad.py tests/test_gpu_rows_deterministic.py tests/test_gpu_rows_sgd_fused.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r04_rows_tests_$T.log 2>&1
+rc=$?; tail -3 gpurun_out/r04_rows_tests_$T.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 200 python -u tools/train_probe.py --graph --zipf 1.05 > gpurun_out/r04_train_$T.log 2>&1
+rc=$?; cat gpurun_out/r04_train_$T.log; [ $rc -ne 0 ] && exit $rc
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r04_prof_zipf_$T -o run -- python3 tools/train_probe.py --graph --zipf 1.05 > gpurun_out/r04_train_prof_$T.log 2>&1
+exit $?
