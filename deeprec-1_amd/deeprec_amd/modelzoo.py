@@ -456,23 +456,39 @@ class WDL(torch.nn.Module):
     ...) -- then dnn [1024, 512, 256] ReLU and a 1-unit logits layer.  Wide
     part (:283-295): linear_model with sparse_combiner 'sum' over the same
     categorical ids (dim-1 EVs), one weight per numeric column, one bias.
-    logits = dnn_logits + linear_logits."""
+    logits = dnn_logits + linear_logits.
+
+    identity: {name: num_buckets} of numeric inputs the reference reads as
+    categorical_column_with_identity (IDENTITY_NUM_BUCKETS = {'I10': 10},
+    :150-155): an indicator_column ('I10_indicator', num_buckets one-hot
+    columns) in the deep input and a [num_buckets, 1] weight table in the
+    linear model.  num_min / num_range: the numeric columns' min-max scaler
+    (col - min) / range (:141-145, 169-175), applied in fp32 to the
+    non-identity columns."""
 
     def __init__(self, cat_names, deep_evs, wide_evs, num_names, hidden=(1024, 512, 256),
-                 bf16=False):
+                 bf16=False, identity=None, num_min=None, num_range=None):
         super().__init__()
         self.bf16 = _MaybeBF16(bf16)
         self.cat_names, self.num_names = list(cat_names), list(num_names)
         self.deep_evs, self.wide_evs = list(deep_evs), list(wide_evs)
         self.evs = self.deep_evs + self.wide_evs
+        self.identity = dict(identity or {})
         dims = [ev.dim for ev in self.deep_evs]
+        plain = [n for n in self.num_names if n not in self.identity]
+        self.plain_idx = [self.num_names.index(n) for n in plain]
         # input_layer column order: sort by column name, then lay out
         cols, off = {}, 0
         for name, d in zip(self.cat_names, dims):
             cols[name + "_embedding"] = list(range(off, off + d))
             off += d
         for j, name in enumerate(self.num_names):
-            cols[name] = [off + j]
+            if name in self.identity:
+                cols[name + "_indicator"] = list(range(off, off + self.identity[name]))
+                off += self.identity[name]
+            else:
+                cols[name] = [off]
+                off += 1
         perm = [c for name in sorted(cols) for c in cols[name]]
         self.register_buffer("perm", torch.tensor(perm, dtype=torch.int64), persistent=False)
         # the same order without a column gather: the embedding columns are
@@ -482,17 +498,34 @@ class WDL(torch.nn.Module):
         emb_names = [n + "_embedding" for n in self.cat_names]
         self.ev_order = sorted(range(len(emb_names)), key=lambda i: emb_names[i])
         self.block_order = all(n < m for n in emb_names for m in self.num_names)
+        if self.identity and not self.block_order:
+            raise ValueError("identity columns need the embedding columns to sort first")
+        dn = {n if n not in self.identity else n + "_indicator": j
+              for j, n in enumerate(self.num_names)}
+        self.dense_layout = [(dn[k], self.identity.get(self.num_names[dn[k]], 0))
+                             for k in sorted(dn)]
         self.register_buffer("num_perm", torch.tensor(
             sorted(range(len(self.num_names)), key=lambda j: self.num_names[j]),
             dtype=torch.int64), persistent=False)
         self.register_buffer("ev_perm", torch.tensor(self.ev_order, dtype=torch.int64),
                              persistent=False)
+        scale = num_min is not None
+        self.register_buffer("num_min", torch.tensor(
+            num_min if scale else [0.0] * len(self.num_names), dtype=torch.float32),
+            persistent=False)
+        self.register_buffer("num_range", torch.tensor(
+            num_range if scale else [1.0] * len(self.num_names), dtype=torch.float32),
+            persistent=False)
+        self.scale = scale
         # --bf16 (train.py:250-266): dnn and the logits layer in bf16 on fp32
         # master weights (keep_weights), the logit cast back to fp32 -- the
         # MFMA tower with the bf16 head
-        self.dnn = (_MfmaMLP if bf16 else _mlp)([off + len(self.num_names)] + list(hidden))
+        self.dnn = (_MfmaMLP if bf16 else _mlp)([off] + list(hidden))
         self.logits = torch.nn.Linear(hidden[-1], 1)
-        self.linear_num = torch.nn.Parameter(torch.zeros(len(self.num_names), 1))
+        self.linear_num = torch.nn.Parameter(torch.zeros(len(plain), 1))
+        self.linear_ident = torch.nn.ParameterList(
+            [torch.nn.Parameter(torch.zeros(self.identity[n], 1))
+             for n in self.num_names if n in self.identity])
         self.linear_bias = torch.nn.Parameter(torch.zeros(1))
         self.deep_lookup = _OneHotLookup(self.deep_evs)
         self.wide_lookup = _OneHotLookup(self.wide_evs)
@@ -501,18 +534,34 @@ class WDL(torch.nn.Module):
         return list(self.dnn.parameters()) + list(self.logits.parameters())
 
     def wide_parameters(self):
-        return [self.linear_num, self.linear_bias]
+        return [self.linear_num] + list(self.linear_ident) + [self.linear_bias]
+
+    def _scaled(self, dense):
+        if not self.scale:
+            return dense
+        return (dense - self.num_min.view(1, -1)) / self.num_range.view(1, -1)
 
     def forward(self, dense, ids):
+        dn = self._scaled(dense)
+        if self.identity:
+            parts = []
+            for j, nb in self.dense_layout:
+                if nb:
+                    parts.append(torch.nn.functional.one_hot(dense[:, j].long(), nb).float())
+                else:
+                    parts.append(dn[:, j:j + 1])
+            dense_block = torch.cat(parts, 1)
+        elif self.block_order:
+            dense_block = dn.index_select(1, self.num_perm)
         if self.block_order:
             evs = [self.deep_evs[i] for i in self.ev_order]
             emb = embedding_lookup_sparse_multi(evs, self.deep_lookup._sps(ids[self.ev_perm]),
                                                 combiner="mean")
-            net = torch.cat([emb, dense.index_select(1, self.num_perm)], 1)
+            net = torch.cat([emb, dense_block], 1)
         else:
             emb = embedding_lookup_sparse_multi(self.deep_evs, self.deep_lookup._sps(ids),
                                                 combiner="mean")
-            net = torch.cat([emb, dense], 1).index_select(1, self.perm)
+            net = torch.cat([emb, dn], 1).index_select(1, self.perm)
         if (isinstance(self.dnn, _MfmaMLP) and self.dnn.mfma_ok(net.shape[0])
                 and self.dnn.head_ok(self.logits)):
             dnn_logits = self.dnn.forward_head(net, self.logits)   # bf16 logit, as fp32
@@ -521,8 +570,14 @@ class WDL(torch.nn.Module):
         wide = self.wide_lookup(ids)                                # [B, T] (sum of dim-1 rows)
         # dense @ linear_num as a row-wise product sum: the matmul's backward
         # (a [13, B] x [B, 1] GEMM with K = 65 536) ran 0.24 ms on the library
-        num = (dense * self.linear_num.view(1, -1)).sum(1, keepdim=True)
+        plain = dn if not self.identity else dn[:, self.plain_idx]
+        num = (plain * self.linear_num.view(1, -1)).sum(1, keepdim=True)
         linear_logits = wide.sum(1, keepdim=True) + num + self.linear_bias
+        k = 0
+        for j, n in enumerate(self.num_names):
+            if n in self.identity:
+                linear_logits = linear_logits + self.linear_ident[k][dense[:, j].long()]
+                k += 1
         return (dnn_logits + linear_logits).squeeze(1)
 
 
