@@ -15,7 +15,8 @@
 //                 KvResourceGatherV1 with counts (:592-596, kv_variable_ops.cc
 //                 :395-449) -> row of every id
 //   gather + [clip_by_norm(max_norm)] + [* w] + SparseSegment{Sum,Mean,SqrtN}
-//          in the reference's association order          (:600-675)
+//          in the reference's association order          (:600-675);
+//          bf16 EVs: every row widened to float32 first  (:606-607)
 //   safe, default_id None: rows that were empty come out 0   (:1330-1337)
 //
 // Every step takes device counts: no host synchronisation, except the
@@ -104,8 +105,11 @@ int dr_embedding_lookup_sparse(dr_ev* ev, const float* table, int64_t table_rows
   if (ev) {
     DR_REQUIRE(dr_ev_dim(ev) == dim, DR_INVALID_ARGUMENT, "dim %d != the EV's %lld", dim,
                (long long)dr_ev_dim(ev));
-    DR_REQUIRE(dr_ev_value_bits(ev) == 32, DR_INVALID_ARGUMENT,
-               "embedding lookups pool float32 EVs");
+    // bf16 EVs (BASELINE configs[4]): rows widened to float32 before the
+    // pooling, as the reference casts bf16 embeddings (embedding_ops.py:606-607)
+    const int vb = dr_ev_value_bits(ev);
+    DR_REQUIRE(vb == 32 || (vb == 16 && dim % 8 == 0), DR_INVALID_ARGUMENT,
+               "embedding lookups pool float32 EVs, or bf16 EVs with dim %% 8 == 0");
   } else {
     DR_REQUIRE(table_rows >= 0, DR_INVALID_ARGUMENT, "bad table_rows");
   }
@@ -173,7 +177,8 @@ int dr_embedding_lookup_sparse(dr_ev* ev, const float* table, int64_t table_rows
   d.out_stride = out_stride;
   d.combiner = combiner;
   d.max_norm = max_norm >= 0.f ? max_norm : -1.f;
-  rc = dr_pool_grouped(&d, 1, batch, dim, DR_ORDER_ALI, stream);
+  const int flags = (ev && dr_ev_value_bits(ev) == 16) ? DR_POOL_BF16 : 0;
+  rc = dr_pool_grouped_ex(&d, 1, batch, dim, DR_ORDER_ALI, flags, stream);
   if (rc) return rc;
   if (safe && default_id < 0) {
     hipLaunchKernelGGL(zero_empty_rows_kernel, dim3((unsigned)ceil_div(batch, 4)), dim3(256), 0,

@@ -83,6 +83,18 @@ class DrXgmiPeers(C.Structure):
 
 _P, _I64, _I32, _F32, _SZ, _U64 = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_size_t, C.c_uint64
 
+# dr_comm_ops.all_to_all_v (include/deeprec_amd.h)
+COMM_A2A_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_int64), C.c_void_p,
+                          C.POINTER(C.c_int64), C.c_int64, C.c_void_p)
+
+
+class DrCommOps(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("all_to_all_v", COMM_A2A_FN)]
+
+
+RCCL_UNIQUE_ID_BYTES = 128
+SHARDED_OUT_BF16 = 1
+
 # name -> (restype, argtypes); must match include/deeprec_amd.h
 SIGNATURES = {
     "dr_abi_version": (_I32, []),
@@ -222,6 +234,18 @@ SIGNATURES = {
     "dr_xgmi_grad_pull": (_I32, [_P, _P, _P, _I32, _I64, _I32, _P, _P, _P, _P, _SZ, _P]),
     "dr_xgmi_grad_pull_dev_workspace_size": (_SZ, [_I32, _I64]),
     "dr_xgmi_grad_pull_dev": (_I32, [_P, _P, _I32, _I64, _I32, _P, _P, _P, _P, _SZ, _P]),
+    "dr_comm_rccl_unique_id": (_I32, [_P, _I64]),
+    "dr_comm_init": (_I32, [_P, _I32, _I32, _P, _P]),
+    "dr_comm_destroy": (_I32, [_P]),
+    "dr_comm_rank": (_I32, [_P]),
+    "dr_comm_world": (_I32, [_P]),
+    "dr_comm_all_to_all_v": (_I32, [_P, _P, _P, _P, _P, _I64, _P]),
+    "dr_sharded_create": (_I32, [_P, _P, _I32, _P]),
+    "dr_sharded_destroy": (_I32, [_P]),
+    "dr_sharded_forward": (_I32, [_P, _P, _I64, _P, _I64, _I32, _I32, _I32, _P, _P]),
+    "dr_sharded_backward": (_I32, [_P, _P, _P, _P, _P, _P]),
+    "dr_sharded_last_stats": (_I32, [_P, _P, _P]),
+    "dr_memcpy": (_I32, [_P, _P, _I64, _I32, _P]),
     "dr_fm2": (_I32, [_P, _I64, _I32, _I32, _P, _P]),
     "dr_fm2_grad": (_I32, [_P, _P, _I64, _I32, _I32, _P, _P]),
     "dr_fm2_bf16_copy": (_I32, [_P, _I64, _I32, _I32, _P, _P, _P]),

@@ -470,8 +470,9 @@ def clip_by_norm_grad(grad, pool, rows, max_norm, pool_rows=None, default_rows=N
     dev = _dev(grad)
     n, D = grad.shape
     pr = (1 << 62) if pool_rows is None else int(pool_rows)
+    dr_ = default_rows if isinstance(default_rows, int) else ptr(default_rows)
     check(lib().dr_clip_by_norm_grad(pool if isinstance(pool, int) else ptr(pool), pr, ptr(rows),
-                                     ptr(default_rows), int(default_stride), ptr(n_dev), n, D,
+                                     dr_, int(default_stride), ptr(n_dev), n, D,
                                      float(max_norm), ptr(grad), stream_handle(dev)))
     _post(dev)
     return grad

@@ -304,6 +304,160 @@ class ShardedLookup(object):
         return out
 
 
+class Comm(object):
+    """A dr_comm (include/deeprec_amd.h): the collective of the native sharded
+    engine (NativeShardedLookup).
+
+    Comm.rccl(rank, world): RCCL over xGMI -- rank 0 draws the ncclUniqueId
+    (dr_comm_rccl_unique_id) and torch.distributed hands it to every rank.
+    Comm.host_staged(group): the all-to-all of a torch.distributed process
+    group on host copies of the buffers (gloo: CPU collectives) through the
+    callback table -- how a host framework plugs its own collective in, and
+    how the engine is exercised on one GPU with several processes."""
+
+    def __init__(self, handle, world, rank, keep=()):
+        self.h = handle
+        self.world, self.rank = world, rank
+        self._keep = keep
+
+    @classmethod
+    def rccl(cls, rank, world, group=None):
+        uid = (C.c_char * _lib.RCCL_UNIQUE_ID_BYTES)()
+        if rank == 0:
+            check(lib().dr_comm_rccl_unique_id(uid, _lib.RCCL_UNIQUE_ID_BYTES))
+        box = [bytes(uid)]
+        if world > 1:
+            dist.broadcast_object_list(box, src=0, group=group)
+        uid = (C.c_char * _lib.RCCL_UNIQUE_ID_BYTES).from_buffer_copy(box[0])
+        h = C.c_void_p()
+        check(lib().dr_comm_init(uid, rank, world, None, C.byref(h)))
+        return cls(h, world, rank)
+
+    @classmethod
+    def host_staged(cls, group=None):
+        import numpy as np
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        errors = []
+
+        def a2a(user, send, sc, recv, rc, eb, stream):
+            try:
+                scl = [int(sc[i]) * eb for i in range(world)]
+                rcl = [int(rc[i]) * eb for i in range(world)]
+                hs = np.empty(max(sum(scl), 1), np.uint8)
+                hr = np.empty(max(sum(rcl), 1), np.uint8)
+                check(lib().dr_memcpy(hs.ctypes.data, send, sum(scl), 1, stream))
+                dist.all_to_all_single(torch.from_numpy(hr[:sum(rcl)]),
+                                       torch.from_numpy(hs[:sum(scl)]), rcl, scl, group=group)
+                check(lib().dr_memcpy(recv, hr.ctypes.data, sum(rcl), 1, stream))
+                return 0
+            except Exception as e:  # noqa: BLE001 -- reported as the call's status
+                errors.append(e)
+                return 1
+
+        fn = _lib.COMM_A2A_FN(a2a)
+        ops_ = _lib.DrCommOps(None, fn)
+        h = C.c_void_p()
+        check(lib().dr_comm_init(None, rank, world, C.byref(ops_), C.byref(h)))
+        return cls(h, world, rank, keep=(fn, ops_, errors))
+
+    def close(self):
+        if self.h is not None and self.h.value:
+            lib().dr_comm_destroy(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class NativeShardedLookup(object):
+    """The row-sharded embedding_lookup_sparse through the library's own
+    sharded C entries (dr_sharded_forward / dr_sharded_backward over a
+    dr_comm): the same protocol and results as ShardedLookup -- index
+    all-to-all, owner insert-on-miss resolve + row pack, row all-to-all back,
+    ALI-order pooling; the owner's IndexedSlices in the backward -- with the
+    sequence inside the C library, as a TF custom-op kernel would drive it
+    (INTEGRATION.md)."""
+
+    def __init__(self, comm, evs, device):
+        self.comm, self.evs, self.device = comm, list(evs), device
+        self.T = len(self.evs)
+        self.dim = self.evs[0].dim
+        self.bf16 = self.evs[0].value_dtype == torch.bfloat16
+        hs = (C.c_void_p * self.T)(*[e.handle.value for e in self.evs])
+        self.h = C.c_void_p()
+        check(lib().dr_sharded_create(comm.h, hs, self.T, C.byref(self.h)))
+        self._keep = None
+
+    def forward(self, ids, bag_offs=None, combiner="sum", need_grad=False, out_dtype=None):
+        """ids: [T, B] int64 (one-hot, bag_offs None) or T 1-D int64 tensors
+        (table t's ids); bag_offs None or T int32 [bags + 1] offsets covering
+        each table's ids.  Returns [bags, T*D] (fp32; bf16 on request for bf16
+        EVs)."""
+        T = self.T
+        if torch.is_tensor(ids):
+            ids = [ids[t] for t in range(ids.shape[0])]
+        if len(ids) != T:
+            raise ValueError("ids of %d tables expected" % T)
+        lens = [int(x.numel()) for x in ids]
+        koff = [0]
+        for n in lens:
+            koff.append(koff[-1] + n)
+        flat = torch.cat([x.reshape(-1).to(torch.int64) for x in ids]).contiguous()
+        if bag_offs is None:
+            bags, offs = lens[0], None
+        else:
+            bag_offs = [o.to(torch.int32).contiguous() for o in bag_offs]
+            bags = int(bag_offs[0].numel()) - 1
+            offs = (C.c_void_p * T)(*[o.data_ptr() for o in bag_offs])
+        bf = out_dtype == torch.bfloat16
+        out = torch.empty((bags, T * self.dim), dtype=torch.bfloat16 if bf else torch.float32,
+                          device=self.device)
+        ka = (C.c_int64 * (T + 1))(*koff)
+        check(lib().dr_sharded_forward(self.h, ptr(flat), ka, offs, bags, COMBINERS[combiner],
+                                       1 if need_grad else 0, _lib.SHARDED_OUT_BF16 if bf else 0,
+                                       ptr(out), stream_handle(self.device)))
+        ops._post(self.device)
+        self._keep = (flat, bag_offs) if need_grad else None
+        return out
+
+    def stats(self):
+        a, b = C.c_int64(0), C.c_int64(0)
+        check(lib().dr_sharded_last_stats(self.h, C.byref(a), C.byref(b)))
+        return {"sent_keys": a.value, "recv_keys": b.value}
+
+    def backward(self, grad_out):
+        """grad_out [bags, T*D] -> per table the owner's (keys, grads) slice,
+        also queued on evs[t].pending_grads as IndexedSlices."""
+        from .kv_variable_ops import IndexedSlices
+        T, D = self.T, self.dim
+        g = grad_out.float().contiguous()
+        kp, gp, cn = (C.c_void_p * T)(), (C.c_void_p * T)(), (C.c_int64 * T)()
+        st = stream_handle(self.device)
+        check(lib().dr_sharded_backward(self.h, ptr(g), kp, gp, cn, st))
+        out = []
+        for t in range(T):
+            n = int(cn[t])
+            k = torch.empty(n, dtype=torch.int64, device=self.device)
+            v = torch.empty((n, D), dtype=torch.float32, device=self.device)
+            if n:
+                check(lib().dr_memcpy(k.data_ptr(), kp[t], 8 * n, 0, st))
+                check(lib().dr_memcpy(v.data_ptr(), gp[t], 4 * n * D, 0, st))
+            out.append((k, v))
+            self.evs[t].pending_grads.append(IndexedSlices(v, k, unique=False))
+        ops._post(self.device)
+        self._keep = None
+        return out
+
+    def close(self):
+        if self.h is not None and self.h.value:
+            lib().dr_sharded_destroy(self.h)
+        self.h = None
+
+
 class _ReduceScatterFn(torch.autograd.Function):
     """out[B, C] = sum over ranks of their partial[rank's bags]; backward =
     the all-gather of the gradient (every owner needs every rank's rows)."""

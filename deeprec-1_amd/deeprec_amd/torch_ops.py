@@ -356,34 +356,79 @@ def _(resource, sp_indices, sp_values, batch, dim, sp_weights=None, combiner="me
 @custom_op(_NS + "::kv_embedding_lookup_sparse_grad", mutates_args=(), device_types="cuda")
 def kv_embedding_lookup_sparse_grad(sp_indices: Tensor, sp_values: Tensor, batch: int,
                                     top_grad: Tensor, sp_weights: Optional[Tensor] = None,
-                                    combiner: str = "mean") -> Tuple[Tensor, Tensor, Tensor]:
+                                    combiner: str = "mean", resource: Optional[Tensor] = None,
+                                    max_norm: float = -1.0, safe: bool = False,
+                                    default_id: int = -1,
+                                    prune: bool = True) -> Tuple[Tensor, Tensor, Tensor]:
     """The gradient of kv_embedding_lookup_sparse w.r.t. the EV as the
     reference's IndexedSlices (embedding_ops.py:592-675, math_grad.py:321-368):
-    (unique ids in first-occurrence order [nnz], gradient rows [nnz, dim],
-    num_unique DEVICE int64[1]); rows past num_unique are unused.  Feed to a
-    kv_resource_sparse_apply_* op with num_valid = num_unique."""
-    from .embedding_ops import _Feature, _grad_to_slices
+    (unique ids in first-occurrence order, gradient rows, num_unique DEVICE
+    int64[1]); the outputs hold nnz rows (nnz + batch when safe), rows past
+    num_unique are unused.  Feed to a kv_resource_sparse_apply_* op with
+    num_valid = num_unique.
+
+    Takes the forward's safe / default_id / prune / max_norm:
+      * safe: the same _prune_invalid_ids [/ _prune_invalid_weights] +
+        sparse_fill_empty_rows (:1289-1310), so pruned ids get no gradient and
+        the filled default_id (or 0) gets its rows' gradient; with default_id
+        None (-1) the forward zeroes the empty rows (tf.where, :1330-1337), so
+        their gradient is 0;
+      * max_norm: the clip of the gathered unique rows
+        (_embedding_lookup_and_transform -> _clip, :94-190) is differentiated
+        (clip_by_norm's chain rule) at the EV's current rows -- `resource`
+        is then required."""
+    from .embedding_ops import (SparseTensor, _Feature, _grad_to_slices, _prune_and_fill)
+    if combiner not in _COMB:
+        raise ValueError("combiner must be one of 'mean', 'sqrtn' or 'sum'")
+    if max_norm >= 0 and resource is None:
+        raise ValueError("a max_norm gradient needs the EV resource (the clip's rows)")
 
     class _P(object):
         pass
 
     p = _P()
     p.dim = top_grad.shape[1]
-    f = _Feature(p, sp_values.to(torch.int64).contiguous(), sp_indices.to(torch.int64).contiguous(),
-                 batch, None if sp_weights is None else sp_weights.to(torch.float32).contiguous(),
-                 combiner, None)
+    ind = sp_indices.to(torch.int64).contiguous()
+    val = sp_values.to(torch.int64).contiguous()
+    w = None if sp_weights is None else sp_weights.to(torch.float32).contiguous()
     g = top_grad.to(torch.float32).contiguous()
+    n_out = val.numel() + (batch if safe else 0)
+    if safe:
+        sp, spw, empty = _prune_and_fill(
+            SparseTensor(ind, val, (batch, 1)),
+            None if w is None else SparseTensor(ind, w, (batch, 1)), combiner,
+            None if default_id < 0 else default_id, prune)
+        ind, val = sp.indices.contiguous(), sp.values.contiguous()
+        w = None if spw is None else spw.values.contiguous()
+        if default_id < 0:
+            g = torch.where(empty[:, None], torch.zeros_like(g), g)
+    f = _Feature(p, val, ind, batch, w, combiner, None)
     sl = _grad_to_slices(f, g, 0, g.shape[1])
-    n = sp_values.numel()
-    vals = sl.values
-    if vals.shape[0] != n:                          # the kernel sizes rows by max(n, 1)
-        vals = vals[:n]
-    return sl.indices[:n].clone(), vals.clone(), sl.num_valid.clone()
+    n = val.numel()
+    idx = torch.zeros(n_out, dtype=torch.int64, device=g.device)
+    vals = torch.zeros((n_out, g.shape[1]), dtype=torch.float32, device=g.device)
+    idx[:n] = sl.indices[:n]
+    vals[:n] = sl.values[:n]
+    if max_norm >= 0 and n > 0:
+        h = _hr(resource)
+        rows = torch.empty(n, dtype=torch.int64, device=g.device)
+        wsb = lib().dr_ev_resolve_workspace_size(n)
+        ws = workspace(wsb, g.device)
+        st = stream_handle(g.device)
+        check(lib().dr_ev_resolve(h, ptr(idx), n, ptr(sl.num_valid), None, None, ptr(rows),
+                                  ptr(ws), wsb, st))
+        ops._post(g.device)
+        sub = vals[:n]
+        ops.clip_by_norm_grad(sub, int(lib().dr_ev_pool(h)), rows, max_norm,
+                              default_rows=int(lib().dr_ev_default_row(h)), default_stride=0,
+                              n_dev=sl.num_valid)
+    return idx, vals, sl.num_valid.clone()
 
 
 @kv_embedding_lookup_sparse_grad.register_fake
-def _(sp_indices, sp_values, batch, top_grad, sp_weights=None, combiner="mean"):
-    n = sp_values.numel()
+def _(sp_indices, sp_values, batch, top_grad, sp_weights=None, combiner="mean", resource=None,
+      max_norm=-1.0, safe=False, default_id=-1, prune=True):
+    n = sp_values.numel() + (batch if safe else 0)
     return (sp_values.new_empty(n, dtype=torch.int64),
             top_grad.new_empty((n, top_grad.shape[1]), dtype=torch.float32),
             sp_values.new_empty(1, dtype=torch.int64))

@@ -824,6 +824,85 @@ int dr_xgmi_grad_pull_dev(const dr_xgmi_peers* peers, const float* const* grad_i
                           void* stream);
 
 /* ------------------------------------------------------------------------ */
+/* Sharded lookup as C entries (SURVEY 8b "sharded variants taking a         */
+/* dr_comm*"): the index all-to-all -> owner gather -> row all-to-all        */
+/* engine of the reference's multi-GPU embedding plugin, the SOK C++ entry   */
+/* (sparse_operation_kit/kit_cc/framework/kernels/dense_fprop.cc:193-212 ->  */
+/* kit_cc_infra/src/embeddings/embedding_layer.cc:52-72, NCCL send / recv in */
+/* kit_cc_impl/embedding/dispatcher/all2all_input_dispatcher.cu:241-286),    */
+/* and the EV partition rule owner = key % world (embedding_ops.py:207-209;  */
+/* = key % 1000 % world for world | 1000).                                    */
+/*                                                                            */
+/* A dr_comm carries the collective: RCCL over xGMI (dr_comm_init with an    */
+/* ncclUniqueId from dr_comm_rccl_unique_id, distributed by the caller), or  */
+/* a caller-supplied callback table (a host framework's own collectives;     */
+/* tests drive it with gloo).  All device buffers, stream-ordered.           */
+/* ------------------------------------------------------------------------ */
+typedef struct dr_comm dr_comm;
+typedef struct {
+  void* user;
+  /* Variable all-to-all: send_counts[p] elements of elem_bytes from send    */
+  /* (peer-major, consecutive) to rank p; recv_counts[p] from rank p into    */
+  /* recv (peer-major).  Counts are HOST arrays of world entries.  Return 0. */
+  int (*all_to_all_v)(void* user, const void* send, const int64_t* send_counts, void* recv,
+                      const int64_t* recv_counts, int64_t elem_bytes, void* stream);
+} dr_comm_ops;
+#define DR_RCCL_UNIQUE_ID_BYTES 128
+/* ncclGetUniqueId (rank 0 calls it and hands the bytes to every rank).      */
+int dr_comm_rccl_unique_id(void* out, int64_t bytes);
+/* Exactly one of rccl_unique_id / ops.  The RCCL form binds the calling    */
+/* thread's current HIP device (ncclCommInitRank).                           */
+int dr_comm_init(const void* rccl_unique_id, int rank, int world, const dr_comm_ops* ops,
+                 dr_comm** out);
+int dr_comm_destroy(dr_comm* comm);
+int dr_comm_rank(const dr_comm* comm);
+int dr_comm_world(const dr_comm* comm);
+/* The comm's variable all-to-all (exported for callers and tests).          */
+int dr_comm_all_to_all_v(dr_comm* comm, const void* send, const int64_t* send_counts,
+                         void* recv, const int64_t* recv_counts, int64_t elem_bytes,
+                         void* stream);
+
+/* The sharded lookup engine over this rank's T EV shards (filter-free EVs  */
+/* of one dim and value type; rank r holds the keys with key % world == r). */
+/* Buffers are owned by the engine and grown on demand.                      */
+typedef struct dr_sharded dr_sharded;
+int dr_sharded_create(dr_comm* comm, dr_ev* const* evs, int num_tables, dr_sharded** out);
+int dr_sharded_destroy(dr_sharded* s);
+/* Forward: ids int64, this rank's batch in the grouped layout -- table t   */
+/* owns ids[koff_host[t], koff_host[t+1]) (koff_host: HOST T+1 offsets; NULL */
+/* = t * bags, one-hot).  bag_off NULL = one-hot (every table holds `bags`   */
+/* ids, bag b = id b), else T pointers to int32 [bags + 1] CSR offsets over  */
+/* the table's ids (bag_off[t][bags] = its id count: every id is in a bag).  */
+/* out [bags, T*dim]: fp32 (bf16 EVs widened, the                            */
+/* reference's cast, embedding_ops.py:606-607) or bf16 with                  */
+/* DR_SHARDED_OUT_BF16.  Per-bag association = the single-GPU lookup's (ALI  */
+/* order by position), so the output equals one GPU's bit for bit.           */
+/* need_grad keeps the exchange state for dr_sharded_backward; a forward-   */
+/* only one-hot lookup routes the raw ids (the owner's insert-on-miss        */
+/* dedups, SOK's all2all_input_dispatcher), otherwise the grouped Unique     */
+/* runs first (embedding_ops.py:592-596).  One host read of the split sizes */
+/* per direction (SOK syncs there too, all2all_input_dispatcher.cu:256-268). */
+#define DR_SHARDED_OUT_BF16 1
+int dr_sharded_forward(dr_sharded* s, const int64_t* ids, const int64_t* koff_host,
+                       const int32_t* const* bag_off, int64_t bags, int combiner, int need_grad,
+                       int flags, void* out, void* stream);
+/* Backward of the last need_grad forward: grad [bags, T*dim] fp32 -> per   */
+/* local unique id its SparseSegment*Grad row (math_grad.py:321-368) -> the  */
+/* rows all-to-all to the owners -> this rank's IndexedSlices per table,     */
+/* source-rank-major (what the optimizer's _deduplicate_indexed_slices,     */
+/* optimizer.py:68-83, then sums in order).  keys_out[t] / grads_out[t]      */
+/* point into the engine's buffers (valid until its next call); counts_out  */
+/* [t] (HOST) = rows of table t.                                             */
+int dr_sharded_backward(dr_sharded* s, const float* grad, const int64_t** keys_out,
+                        const float** grads_out, int64_t* counts_out, void* stream);
+/* Keys exchanged by the last forward: sent to peers / received from them.  */
+int dr_sharded_last_stats(const dr_sharded* s, int64_t* sent, int64_t* received);
+/* Byte copy between any host / device buffers on `stream` (hipMemcpyDefault); */
+/* sync != 0 waits for it.  For host frameworks' dr_comm callbacks that stage */
+/* device buffers through host memory (e.g. a CPU collective).               */
+int dr_memcpy(void* dst, const void* src, int64_t bytes, int sync, void* stream);
+
+/* ------------------------------------------------------------------------ */
 /* Interactions (callers of the path).                                       */
 /* ------------------------------------------------------------------------ */
 /* FM 2nd order (modelzoo/DeepFM/train.py:205-209): emb [B,F,D] -> [B,D].   */

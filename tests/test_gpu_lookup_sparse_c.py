@@ -61,6 +61,41 @@ def test_ev_lookup_sparse_one_call(dr, orc, comb, weighted, max_norm):
     assert int(ev.total_count()[0]) == oev.size()
 
 
+@pytest.mark.parametrize("comb", ["sum", "mean", "sqrtn"])
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("safe", [False, True])
+def test_bf16_ev_lookup_sparse_one_call(dr, orc, comb, weighted, safe):
+    """bf16 EVs (BASELINE configs[4]) through the single entry: the rows are
+    widened to float32 and pooled in the reference order into an fp32 output
+    (embedding_ops.py:606-607), against oracle.EV(bf16=True)."""
+    from deeprec_amd import ops
+    rng = np.random.default_rng(31 + 3 * weighted + safe + len(comb))
+    B, D = 173, 24
+    ev = dr.EmbeddingVariable("lscbf_%s_%d_%d" % (comb, weighted, safe), D, 0.3,
+                              value_dtype=torch.bfloat16)
+    oev = orc.EV(D, 0.3, bf16=True)
+    keys = np.arange(0, 150, dtype=np.int64)
+    vals = orc.bf16_round(rng.standard_normal((150, D)).astype(np.float32))
+    ev.insert(T(keys), T(vals).to(torch.bfloat16))
+    oev.insert(keys, vals)
+    ind, v = _sparse(rng, B, 5, 200, allow_empty=safe)
+    if safe:
+        v[::9] = -2
+    w = rng.uniform(0.1, 2.0, v.shape[0]).astype(np.float32) if weighted else None
+    out = ops.embedding_lookup_sparse_c(ev, T(ind), T(v), B, None if w is None else T(w), comb,
+                                        None, safe=safe, default_id=None)
+    assert out.dtype == torch.float32
+    if safe:
+        ref = orc.safe_embedding_lookup_sparse(oev, ind, v, (B, 5), w, comb, None)
+    else:
+        ref = orc.embedding_lookup_sparse(oev, ind, v, B, w, comb)
+    if weighted:
+        np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-6)
+    else:
+        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    assert int(ev.total_count()[0]) == oev.size()
+
+
 @pytest.mark.parametrize("default_id", [None, 3])
 @pytest.mark.parametrize("weighted", [False, True])
 def test_safe_lookup_one_call(dr, orc, default_id, weighted):

@@ -143,6 +143,82 @@ def test_ev_lookup_op_matches_oracle(dr, orc):
         np.testing.assert_array_equal(H(gr[:U]), gref)
 
 
+def _np_prune_fill(ind, v, w, B, comb, default_id, prune=True):
+    """_prune_invalid_ids [/ _prune_invalid_weights] + sparse_fill_empty_rows
+    (embedding_ops.py:1289-1310) in numpy: (ind, ids, weights, empty rows)."""
+    keep = v >= 0 if prune else np.ones(v.shape, bool)
+    if prune and w is not None and comb != "sum":
+        keep &= w > 0
+    ind, v = ind[keep], v[keep]
+    w = None if w is None else w[keep]
+    empty = np.ones(B, bool)
+    empty[ind[:, 0]] = False
+    fill = np.nonzero(empty)[0]
+    ind2 = np.concatenate([ind, np.stack([fill, np.zeros_like(fill)], 1)])
+    v2 = np.concatenate([v, np.full(fill.size, default_id or 0, np.int64)])
+    o = np.argsort(ind2[:, 0], kind="stable")
+    w2 = None if w is None else np.concatenate([w, np.ones(fill.size, np.float32)])[o]
+    return ind2[o], v2[o], w2, empty
+
+
+@pytest.mark.parametrize("safe,default_id", [(False, -1), (True, -1), (True, 2)])
+@pytest.mark.parametrize("max_norm", [-1.0, 0.9])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_ev_lookup_grad_op_safe_and_max_norm(dr, orc, safe, default_id, max_norm, weighted):
+    """The registered grad op takes the forward's safe / default_id / prune /
+    max_norm: pruned ids get no gradient, the filled id gets its rows'
+    gradient (zeroed rows when default_id is None), and the max_norm clip's
+    chain rule is applied at the EV's rows -- against the oracle's gradient
+    of the same pruned / filled lookup."""
+    rng = np.random.default_rng(100 + 7 * safe + int(max_norm > 0) + 3 * weighted + default_id)
+    B, D, comb = 96, 8, "mean"
+    ev = dr.EmbeddingVariable("tops_sg_%d_%d_%d_%d" % (safe, default_id, max_norm > 0, weighted),
+                              D, 0.2)
+    oev = orc.EV(D, 0.2)
+    keys = np.arange(0, 60, dtype=np.int64)
+    vals0 = rng.standard_normal((60, D)).astype(np.float32)
+    ev.insert(T(keys), T(vals0))
+    oev.insert(keys, vals0)
+    lens = rng.integers(0 if safe else 1, 5, B)
+    rows = np.repeat(np.arange(B), lens)
+    cols = np.concatenate([np.arange(l) for l in lens])
+    ind = np.stack([rows, cols], 1).astype(np.int64)
+    v = rng.integers(0, 80, rows.shape[0]).astype(np.int64)
+    if safe:
+        v[::6] = -1
+    w = rng.uniform(-0.3, 2.0, v.shape[0]).astype(np.float32) if weighted else None
+    if weighted and not safe:
+        w = np.abs(w) + 0.1
+    Wt = None if w is None else T(w)
+    out = torch.ops.deeprec.kv_embedding_lookup_sparse(ev.resource, T(ind), T(v), B, D, Wt, comb,
+                                                       max_norm, safe, default_id)
+    did = None if default_id < 0 else default_id
+    mn = None if max_norm < 0 else max_norm
+    if safe:
+        ref = orc.safe_embedding_lookup_sparse(oev, ind, v, (B, 5), w, comb, did, mn)
+    else:
+        ref = orc.embedding_lookup_sparse(oev, ind, v, B, w, comb, mn)
+    np.testing.assert_allclose(H(out), ref, rtol=1e-5, atol=1e-6)
+    g = rng.standard_normal((B, D)).astype(np.float32)
+    u, gr, nu = torch.ops.deeprec.kv_embedding_lookup_sparse_grad(
+        T(ind), T(v), B, T(g), Wt, comb, ev.resource, max_norm, safe, default_id)
+    U = int(nu.item())
+    if safe:
+        ind2, v2, w2, empty = _np_prune_fill(ind, v, w, B, comb, did)
+        g2 = g.copy()
+        if did is None:
+            g2[empty] = 0.0
+    else:
+        ind2, v2, w2, g2 = ind, v, w, g
+    uids, gref = orc.embedding_lookup_sparse_grad(oev, ind2, v2, B, g2, w2, comb, mn)
+    assert H(u[:U]).tolist() == uids.tolist()
+    assert (H(u[:U]) >= 0).all()                    # pruned ids never reach the slices
+    if mn is None and not weighted:
+        np.testing.assert_array_equal(H(gr[:U]), gref)
+    else:
+        np.testing.assert_allclose(H(gr[:U]), gref, rtol=1e-5, atol=1e-6)
+
+
 def test_compile_keeps_stateful_order(dr, orc):
     """Under torch.compile (aot_eager: functionalization of the custom ops),
     a lookup -> grad -> SGD apply -> lookup chain on one EV keeps every
