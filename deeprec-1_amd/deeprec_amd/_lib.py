@@ -242,7 +242,7 @@ SIGNATURES = {
     "dr_comm_all_to_all_v": (_I32, [_P, _P, _P, _P, _P, _I64, _P]),
     "dr_sharded_create": (_I32, [_P, _P, _I32, _P]),
     "dr_sharded_destroy": (_I32, [_P]),
-    "dr_sharded_forward": (_I32, [_P, _P, _I64, _P, _I64, _I32, _I32, _I32, _P, _P]),
+    "dr_sharded_forward": (_I32, [_P, _P, _P, _P, _I64, _I32, _I32, _I32, _P, _P]),
     "dr_sharded_backward": (_I32, [_P, _P, _P, _P, _P, _P]),
     "dr_sharded_last_stats": (_I32, [_P, _P, _P]),
     "dr_memcpy": (_I32, [_P, _P, _I64, _I32, _P]),
