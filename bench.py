@@ -57,6 +57,12 @@ def parse():
                         "offsets; B_local 65536 / 8192, uniform / Zipf 1.05) at N=1")
     p.add_argument("--no-dcn", dest="dcn", action="store_false",
                    help="skip the BASELINE configs[4] bf16-table leg at N=1")
+    p.add_argument("--hybrid-cap", type=int, default=0,
+                   help="cap the hybrid leg's large vocabularies at this many rows (rehearsals "
+                        "only; 0 = the real cardinalities)")
+    p.add_argument("--no-hybrid", dest="hybrid", action="store_false",
+                   help="skip the real Criteo-TB cardinality leg with hybrid placement (small "
+                        "features replicated, large ones row-sharded), run at every N")
     p.add_argument("--dedup", action="store_true",
                    help="xgmi engine: per-destination dedup before the exchange (grouped Unique, "
                         "unique keys routed, rows expanded locally)")
@@ -268,6 +274,185 @@ def criteo_legs(args, dev, log):
             log("criteo B=%d %s: %s" % (B, dist_name, json.dumps(res["B%d_%s" % (B, dist_name)])))
     dr.status_check(dev)
     del ev, fsets
+    return res
+
+
+class _LocalOneHot(object):
+    """world 1 stand-in for a sharded engine: the fused one-hot lookup of
+    its EVs (every key is local)."""
+
+    def __init__(self, evs, batch, dev):
+        from deeprec_amd.embedding_ops import SparseTensor
+        self.evs = evs
+        ind = torch.stack([torch.arange(batch, device=dev),
+                           torch.zeros(batch, dtype=torch.int64, device=dev)], 1)
+        self._sp = lambda ids: [SparseTensor(ind, ids[t], (batch, 1)) for t in range(len(evs))]
+
+    def forward(self, ids):
+        import deeprec_amd as dr
+        with torch.no_grad():
+            return dr.embedding_lookup_sparse_multi(self.evs, self._sp(ids), combiner="sum")
+
+    def close(self):
+        pass
+
+
+def criteo_hybrid_leg(args, dev, log, world, rank, dist, staged):
+    """The real Criteo-TB cardinalities at N GPUs with hybrid placement
+    (sharded.HybridShardedLookup): the 20 features of <= 585 935 rows
+    (1.11 M rows, 0.57 GB) are replicated on every rank and looked up
+    locally -- one fused one-hot kernel over their prefix-offset table, on a
+    side stream -- and the 6 large ones (1.87e8 rows) are row-sharded (key %
+    N) and exchanged by the xGMI peer-write engine (RCCL all-to-all
+    fallback).  B_local ids per feature per rank, uniform over the feature's
+    vocabulary.  value = 26 * B_local * N / step time (barrier-bracketed,
+    max over ranks).  At N = 1 both parts are local lookups (the same code
+    path, no exchange)."""
+    import deeprec_amd as dr
+    from deeprec_amd import _lib
+    from deeprec_amd.embedding_ops import _Feature, _fused_onehot
+    from deeprec_amd.sharded import (HybridShardedLookup, ShardedLookup, XgmiShardedLookup,
+                                     hybrid_split)
+    D, B = 128, args.batch
+    card = np.array(CRITEO_TB_VOCAB, np.int64)
+    rep, shard = hybrid_split(CRITEO_TB_VOCAB, 585935)
+    if args.hybrid_cap > 0:
+        card[shard] = np.minimum(card[shard], args.hybrid_cap)
+    rcard = card[rep]
+    rpre = np.concatenate([[0], np.cumsum(rcard)[:-1]])
+    t0 = time.perf_counter()
+    rep_ev = dr.EmbeddingVariable("hyb_rep", D, 0.0, device=dev,
+                                  capacity=int(rcard.sum()) + (1 << 20))
+    rep_ev.insert_synthetic(0, int(rcard.sum()), seed=4242)
+    sh_evs = []
+    for t in shard:
+        n_own = int((card[t] - rank + world - 1) // world)
+        ev = dr.EmbeddingVariable("hyb_sh%d" % t, D, 0.0, device=dev,
+                                  capacity=n_own + max(1 << 20, 12 * world * B))
+        ev.insert_synthetic(rank, n_own, seed=5000 + t, key_stride=world)
+        sh_evs.append(ev)
+    torch.cuda.synchronize()
+    log("hybrid tables: replicated %d features / %d rows, sharded %d features / %d rows "
+        "per rank, in %.1fs" % (len(rep), int(rcard.sum()), len(shard),
+                                sum(int(e.total_count()[0]) for e in sh_evs),
+                                time.perf_counter() - t0))
+    kind = "local (N=1)"
+    a2a = None
+    if world == 1:
+        engine = _LocalOneHot(sh_evs, B, dev)
+    else:
+        engine, ok, err = None, 1, ""
+        try:
+            barrier = None
+            if staged:
+                def barrier():
+                    torch.cuda.synchronize()
+                    dist.barrier()
+            engine = XgmiShardedLookup(sh_evs, world, rank, B, dev, barrier=barrier)
+        except Exception as e:  # noqa: BLE001
+            ok, err = 0, str(e)
+        flag = torch.tensor([ok], dtype=torch.int32, device="cpu" if staged else dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        a2a = ShardedLookup(sh_evs, world, rank, B, dev)
+        if staged:
+            def staged_a2a(out, inp, out_splits=None, in_splits=None):
+                o = torch.empty(out.shape, dtype=out.dtype)
+                dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits)
+                out.copy_(o)
+                return out
+            a2a._a2a = staged_a2a
+        if int(flag.item()) == 1:
+            kind = "xgmi peer-write"
+        else:
+            log("hybrid: xgmi unavailable (%s); RCCL all-to-all" % err)
+            if engine is not None:
+                engine.close()
+            engine, kind = a2a, "RCCL all-to-all"
+    seg = torch.arange(B, dtype=torch.int32, device=dev)
+    cardt = torch.as_tensor(card, device=dev)[:, None]
+    fsets, ishard, idsall = [], [], []
+    for k in range(4):
+        g = torch.Generator(device=dev)
+        g.manual_seed(600 + 7919 * rank + k)
+        u = torch.rand((26, B), generator=g, device=dev, dtype=torch.float64)
+        ids = (u * cardt).to(torch.int64)                     # [26, B] per-feature ids
+        idsall.append(ids)
+        rrec = (ids[rep] + torch.as_tensor(rpre, device=dev)[:, None]).t().contiguous()
+        fsets.append([_Feature(rep_ev, rrec[:, j], seg, B, None, "sum", None, onehot=True)
+                      for j in range(len(rep))])
+        ishard.append(ids[shard].contiguous())
+
+    def local_lookup(fs):
+        return _fused_onehot(fs, _lib.ORDER_ALI)
+
+    hyb = HybridShardedLookup(local_lookup, engine, dev, overlap=True)
+
+    def step(k):
+        return hyb.forward(fsets[k % 4], ishard[k % 4])
+
+    with torch.no_grad():
+        for w in range(max(args.warmup, 2)):
+            out_r, out_s = step(w)
+            torch.cuda.synchronize()
+        # correctness (outside the timing): sampled rows of both blocks are
+        # the tables' synth rows; at N > 1 the exchange equals the all-to-all
+        # engine's output bit for bit
+        checked, ok_rows = 0, True
+        for k in range(2):
+            out_r, out_s = step(k)
+            out_r, out_s = out_r.clone(), out_s.clone()
+            ids = idsall[k].cpu().numpy()
+            rs = np.random.default_rng(31 + k).integers(0, B, 64)
+            for j, t in enumerate(rep):
+                want = synth_rows(4242, ids[t, rs] + rpre[j], D)
+                ok_rows &= np.array_equal(out_r[rs, j * D:(j + 1) * D].cpu().numpy(), want)
+                checked += rs.size
+            for j, t in enumerate(shard):
+                want = synth_rows(5000 + t, ids[t, rs], D)
+                ok_rows &= np.array_equal(out_s[rs, j * D:(j + 1) * D].cpu().numpy(), want)
+                checked += rs.size
+            if a2a is not None and engine is not a2a:
+                ok_rows &= bool(torch.equal(out_s, a2a.forward(ishard[k])))
+        if world > 1:
+            f = torch.tensor([int(ok_rows)], dtype=torch.int32, device="cpu" if staged else dev)
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)
+            ok_rows = bool(f.item())
+        dr.status_check(dev)
+        if not ok_rows:
+            raise AssertionError("hybrid leg: rows differ from the tables' synth rows / a2a")
+        for i in range(args.warmup):
+            step(i)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(i)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    if dist is not None:
+        te = torch.tensor([el], dtype=torch.float64, device="cpu" if staged else dev)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        el = float(te.item())
+    ms = el / args.steps * 1e3
+    res = {"workload": "real Criteo-TB cardinalities (modelzoo/SOK/DLRM/train_stand.py:242-248), "
+                       "hybrid placement: %d features <= 585935 rows replicated (one fused "
+                       "%d-row table, local fused lookup on a side stream), %d large features "
+                       "row-sharded key %% N (%s exchange), B_local=%d, uniform ids per feature, "
+                       "embedding_lookup_sparse(sum) forward" % (len(rep), int(rcard.sum()),
+                                                                 len(shard), kind, B),
+           "n_gpus": world, "ms_per_step": round(ms, 4),
+           "lookups_per_s": round(26 * B * world / (ms * 1e-3), 1),
+           "samples_per_s": round(B * world / (ms * 1e-3), 1),
+           "sharded_lookups_per_gpu_step": len(shard) * B,
+           "remote_rows_per_gpu_step": int(len(shard) * B * (world - 1) / world),
+           "engine": kind, "checked_rows": checked, "bitexact": True,
+           "vocab_cap": args.hybrid_cap or None}
+    log("criteo hybrid leg: %s" % json.dumps(res))
+    if hasattr(engine, "close"):
+        engine.close()
     return res
 
 
@@ -776,6 +961,53 @@ def main():
                          "segment grad) fused with the KV SGD update "
                          "(dr_ev_pool_grad_rows_apply_sgd), %d EVs, B=%d" % (T, B)}
         log("train step: %s" % json.dumps(train))
+    elif world > 1 and engine is not None and args.train_steps > 0:
+        # ---- embedding training step at N > 1: sharded forward (ids to
+        # their owners, owner resolve, rows back), sharded backward (the
+        # owners pull / receive their keys' gradient rows -> IndexedSlices on
+        # their EV shards), owner KV SGD apply.  Eager (the exchange's
+        # barriers are stream-ordered collectives); every rank's own batch.
+        opt = dr.GradientDescentOptimizer(0.01)
+        gu_ = torch.Generator(device=dev)
+        gu_.manual_seed(77 + rank)
+        upstream = torch.randn((B, T * D), generator=gu_, device=dev)
+
+        def tstep(i):
+            ids = batches[i % NBATCH]
+            if engine is a2a:
+                engine.forward(ids, need_grad=True)
+            else:
+                engine.forward(ids)
+            engine.backward(upstream)
+            opt.apply_gradients(evs)
+
+        for i in range(2):
+            tstep(i)
+        torch.cuda.synchronize()
+        dr.status_check(dev)
+        nsteps = args.train_steps
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(nsteps):
+            tstep(i)
+        dist.barrier()
+        torch.cuda.synchronize()
+        tel = time.perf_counter() - t0
+        te = torch.tensor([tel], dtype=torch.float64, device="cpu" if staged else dev)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        tel = float(te.item())
+        dr.status_check(dev)
+        tms = tel / nsteps * 1e3
+        train = {"ms_per_step": round(tms, 4),
+                 "samples_per_s": round(world * B / (tms * 1e-3), 1),
+                 "lookups_per_s": round(world * T * B / (tms * 1e-3), 1), "steps": nsteps,
+                 "graph": False, "engine": engine_kind,
+                 "step": "sharded embedding layer training step: forward (%s exchange) + "
+                         "backward to the owners (IndexedSlices on their EV shards) + owner KV "
+                         "SGD apply, %d EVs, B_local=%d, global batch %d"
+                         % (engine_kind, T, B, world * B)}
+        log("train step: %s" % json.dumps(train))
 
     # ---- dominant kernel: the fused one-hot EV lookup, timed alone --------
     # dr_ev_lookup_onehot on keys this rank owns (all keys at N=1), over the
@@ -872,21 +1104,24 @@ def main():
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args)
 
-    deepfm = criteo = dcn = None
-    if world == 1 and (args.deepfm or args.criteo or args.dcn):
+    deepfm = criteo = dcn = hybrid = None
+    if (world == 1 and (args.deepfm or args.criteo or args.dcn)) or args.hybrid:
         # drop every holder of the headline EVs so their HBM is released;
         # each leg below frees its own tables before the next one
         evs = feats = gfeats = batch_sps = rec_sps = kfeats = gsets = None
         engine = a2a = outc = graph_all = tgraph = opt = None
         _free_hbm()
-        if args.deepfm:
+        if world == 1 and args.deepfm:
             deepfm = deepfm_leg(args, dev, log)
             _free_hbm()
-        if args.criteo:
+        if world == 1 and args.criteo:
             criteo = criteo_legs(args, dev, log)
             _free_hbm()
-        if args.dcn:
+        if world == 1 and args.dcn:
             dcn = dcn_bf16_leg(args, dev, log)
+            _free_hbm()
+        if args.hybrid:
+            hybrid = criteo_hybrid_leg(args, dev, log, world, rank, dist, staged)
             _free_hbm()
 
     if rank == 0:
@@ -920,6 +1155,7 @@ def main():
             "train_step": train,
             "deepfm_config": deepfm,
             "criteo_tb_cardinalities": criteo,
+            "criteo_tb_hybrid": hybrid,
             "dcn_bf16_config": dcn,
             "correctness": correctness,
             "roofline": roof,

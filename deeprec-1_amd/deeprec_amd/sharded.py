@@ -458,6 +458,59 @@ class NativeShardedLookup(object):
         self.h = None
 
 
+def hybrid_split(cardinalities, replicate_max):
+    """Features whose vocabulary is at most `replicate_max` rows are
+    replicated on every rank, the others row-sharded (key % world).  On the
+    real Criteo-TB cardinalities (modelzoo/SOK/DLRM/train_stand.py:242-248)
+    with replicate_max = 585 935, 20 of the 26 features (1.11 M rows, 0.57 GB
+    at D = 128 fp32) are replicated and 6 (1.87e8 rows) sharded."""
+    rep = [t for t, c in enumerate(cardinalities) if c <= replicate_max]
+    shard = [t for t, c in enumerate(cardinalities) if c > replicate_max]
+    return rep, shard
+
+
+class HybridShardedLookup(object):
+    """Hybrid placement for row-sharded one-hot lookups (SURVEY 8e levers):
+    the replicated features are looked up locally -- no link bytes at all --
+    and only the sharded ones go through `engine` (XgmiShardedLookup,
+    ShardedLookup or NativeShardedLookup over those features' EV shards).
+    With overlap, the local lookup runs on a side stream while the exchange
+    runs on the current one (the local part reads HBM, the exchange is
+    link-bound).
+
+    forward(ids_rep [T_r, B], ids_shard [T_s, B]) -> (out_rep [B, T_r*D],
+    out_shard [B, T_s*D]): the replicated and the sharded features' pooled
+    columns as two blocks (a model stacks them behind its dense row, as
+    embedding_stack does).  Results are each feature's single-GPU lookup, bit
+    for bit: the local part IS the single-GPU lookup, the sharded part is
+    position-addressed by the engine.
+
+    local_lookup(ids_rep) -> out_rep is the replicated features' lookup (the
+    fused one-hot kernel over their tables on the GPU; any callable in
+    tests)."""
+
+    def __init__(self, local_lookup, engine, device=None, overlap=True):
+        self.local_lookup = local_lookup
+        self.engine = engine
+        self.device = device
+        use_side = overlap and device is not None and torch.device(device).type == "cuda"
+        self.side = torch.cuda.Stream(device=device) if use_side else None
+
+    def forward(self, ids_rep, ids_shard):
+        if self.side is None:
+            out_r = self.local_lookup(ids_rep)
+            out_s = self.engine.forward(ids_shard)
+            return out_r, out_s
+        cur = torch.cuda.current_stream(self.device)
+        self.side.wait_stream(cur)
+        with torch.cuda.stream(self.side):
+            out_r = self.local_lookup(ids_rep)
+        out_s = self.engine.forward(ids_shard)
+        cur.wait_stream(self.side)
+        out_r.record_stream(cur)
+        return out_r, out_s
+
+
 class _ReduceScatterFn(torch.autograd.Function):
     """out[B, C] = sum over ranks of their partial[rank's bags]; backward =
     the all-gather of the gradient (every owner needs every rank's rows)."""

@@ -7,7 +7,10 @@ peer-write (xGMI IPC) engine's output equals the all-to-all engine's bit for
 bit on steps 0-3 before timing, and on the last timed step plus two more
 after it -- each output consumed by the next step's reads, as in a model
 step -- and the sampled headline rows equal the synthetic tables' rows.
-Never a reported number: the timing of staged steps means nothing."""
+The rehearsal also runs the N > 1 training step (sharded forward + backward
+to the owners + owner SGD) and the hybrid-placement Criteo-TB leg (large
+vocabularies capped for time).  Never a reported number: the timing of
+staged steps means nothing."""
 import json
 import os
 import subprocess
@@ -28,7 +31,8 @@ def test_bench_two_rank_rehearsal(engine):
            "--master-port", {"xgmi": "29531", "xgmi-dedup": "29533", "a2a": "29532"}[engine],
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
            "--rows", "200000", "--batch", "8192", "--tables", "8", "--cpu-seconds", "0",
-           "--check-rows", "4096", "--engine", engine.split("-")[0]]
+           "--check-rows", "4096", "--engine", engine.split("-")[0], "--train-steps", "3",
+           "--hybrid-cap", "1000000"]
     if engine == "xgmi-dedup":
         cmd += ["--dedup", "--zipf", "1.05"]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
@@ -44,3 +48,9 @@ def test_bench_two_rank_rehearsal(engine):
         assert cfg["engine_check"].count("True") == 2 and "False" not in cfg["engine_check"], cfg
     else:
         assert cfg["engine"] == "RCCL all-to-all", cfg
+    # the N > 1 training step (sharded forward + backward + owner SGD) ran
+    assert line["train_step"]["engine"] == cfg["engine"] and line["train_step"]["steps"] == 3
+    # the hybrid-placement leg: replicated small features + sharded large
+    # ones, sampled rows bit-exact and (xgmi) equal to the all-to-all engine
+    hy = line["criteo_tb_hybrid"]
+    assert hy["bitexact"] and hy["n_gpus"] == 2 and hy["checked_rows"] > 0, hy
