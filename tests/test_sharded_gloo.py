@@ -295,3 +295,72 @@ def test_xgmi_setup_failure_is_collective():
         mp.spawn(_setup_fail_worker, args=(2, _free_port(), d), nprocs=2, join=True)
         for r in range(2):
             assert os.path.exists(os.path.join(d, "ok%d" % r))
+
+
+def _hybrid_worker(rank, world, port, outdir):
+    """HybridShardedLookup over gloo: features 0 and 2 replicated (every rank
+    holds the whole table, looked up locally), feature 1 row-sharded through
+    ShardedLookup (oracle backend).  Both output blocks equal the
+    single-process lookup of every feature bit for bit."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                        "deeprec-1_amd"))
+        from oracle import oracle as orc
+        from deeprec_amd.sharded import HybridShardedLookup, ShardedLookup, hybrid_split
+        cards = [30, KEYSPACE, 12]                 # features 0, 2 small; 1 large
+        rep, shard = hybrid_split(cards, 40)
+        assert rep == [0, 2] and shard == [1]
+        allk = [np.arange(c, dtype=np.int64) for c in cards]
+        full = []
+        for t in range(3):
+            ev = orc.EV(D, DEFAULT)
+            ev.insert(allk[t][:cards[t] // 2], _row_values(t, allk[t][:cards[t] // 2]))
+            full.append(ev)
+        own = allk[1][:cards[1] // 2]
+        own = own[own % world == rank]
+        sev = orc.EV(D, DEFAULT)
+        sev.insert(own, _row_values(1, own))
+        be = OracleLocal(orc, [sev])
+        eng = ShardedLookup(None, world, rank, B, torch.device("cpu"), backend=be)
+        rep_evs = [full[t] for t in rep]
+
+        def local_lookup(ids_rep):
+            cols = []
+            for j in range(len(rep)):
+                ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+                cols.append(orc.embedding_lookup_sparse(rep_evs[j], ind, ids_rep[j].numpy(), B,
+                                                        combiner="sum"))
+            return torch.from_numpy(np.concatenate(cols, 1))
+
+        hyb = HybridShardedLookup(local_lookup, eng, device=None)
+        rng = np.random.default_rng(500 + rank)
+        for step in range(2):
+            ids = np.stack([rng.integers(0, c, B) for c in cards]).astype(np.int64)
+            out_r, out_s = hyb.forward(torch.from_numpy(ids[rep]), torch.from_numpy(ids[shard]))
+            ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+            for j, t in enumerate(rep):
+                ref_ev = orc.EV(D, DEFAULT)
+                ref_ev.insert(allk[t][:cards[t] // 2], _row_values(t, allk[t][:cards[t] // 2]))
+                ref = orc.embedding_lookup_sparse(ref_ev, ind, ids[t], B, combiner="sum")
+                np.testing.assert_array_equal(out_r[:, j * D:(j + 1) * D].numpy(), ref)
+            for j, t in enumerate(shard):
+                ref_ev = orc.EV(D, DEFAULT)
+                ref_ev.insert(allk[t][:cards[t] // 2], _row_values(t, allk[t][:cards[t] // 2]))
+                ref = orc.embedding_lookup_sparse(ref_ev, ind, ids[t], B, combiner="sum")
+                np.testing.assert_array_equal(out_s[:, j * D:(j + 1) * D].numpy(), ref)
+        open(os.path.join(outdir, "ok%d" % rank), "w").write("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_hybrid_placement_gloo(world):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_hybrid_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        for r in range(world):
+            assert os.path.exists(os.path.join(d, "ok%d" % r))
