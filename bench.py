@@ -1108,9 +1108,12 @@ def main():
     if (world == 1 and (args.deepfm or args.criteo or args.dcn)) or args.hybrid:
         # drop every holder of the headline EVs so their HBM is released;
         # each leg below frees its own tables before the next one
-        evs = feats = gfeats = batch_sps = rec_sps = kfeats = gsets = None
-        engine = a2a = outc = graph_all = tgraph = opt = None
+        # (loop variables too: `fs` holds a feature list of every table, `ev`
+        # the last table -- either kept 180 GB of headline tables alive)
+        evs = feats = gfeats = batch_sps = rec_sps = kfeats = gsets = fs = ev = None
+        engine = a2a = outc = graph_all = tgraph = opt = step = tstep = None
         _free_hbm()
+        log("HBM free after the headline tables: %.1f GB" % (torch.cuda.mem_get_info(dev)[0] / 1e9))
         if world == 1 and args.deepfm:
             deepfm = deepfm_leg(args, dev, log)
             _free_hbm()
