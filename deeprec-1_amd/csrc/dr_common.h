@@ -237,6 +237,13 @@ int rows_apply_sgd(const dr_pool_grad_desc* descs_host, int num_tables, int64_t 
                    const int64_t* rowsel, int64_t row_limit, const RowsSgd& sg, void* ws,
                    size_t ws_bytes, hipStream_t s);
 
+#ifdef DR_UC_DIAG
+// xgmi.hip, diagnostic build only: uncached blocks freed to hipFree, and a
+// D2H-vs-kernel read check of a buffer against the bytes expected in it
+void uc_diag_freed(void* p, size_t n);
+void uc_diag_check(const char* what, const void* dev, const void* expect, size_t bytes);
+#endif
+
 // ---- scan / sort primitives (scan_sort.hip) --------------------------------
 size_t scan_ws_bytes(int64_t n);
 // Exclusive scan of int32 values into int32 out; *total (device int64) = sum.

@@ -1269,15 +1269,31 @@ static int alloc_pool(EvShared* s, int col, const float* default_row_host) {
   const int64_t w = col_words(s, col);
   DR_HIP(hipMalloc(&s->pools[col], (size_t)s->row_cap * w * sizeof(float)));
   DR_HIP(hipMalloc(&s->defaults[col], (size_t)w * sizeof(float)));
+#ifdef DR_UC_DIAG
+  // poison: a 0xFF word read later was never written by the init / copy;
+  // a 0 word came from stale backing (the uncached blocks were zero-filled)
+  {
+    int frc = fill_bytes(s->pools[col], 0xFF, (size_t)s->row_cap * w * sizeof(float), nullptr);
+    if (!frc) frc = fill_bytes(s->defaults[col], 0xFF, (size_t)w * sizeof(float), nullptr);
+    if (frc) return frc;
+    DR_HIP(hipDeviceSynchronize());
+  }
+#endif
   if (w != s->dim) {
     // bf16 column: the fp32 default row rounded to nearest even
     std::vector<uint16_t> b((size_t)s->dim);
     for (int64_t c = 0; c < s->dim; ++c) b[(size_t)c] = bf16_rne_host(default_row_host[c]);
     DR_HIP(hipMemcpy(s->defaults[col], b.data(), b.size() * sizeof(uint16_t),
                      hipMemcpyHostToDevice));
+#ifdef DR_UC_DIAG
+    uc_diag_check("default row (bf16)", s->defaults[col], b.data(), b.size() * 2);
+#endif
   } else {
     DR_HIP(hipMemcpy(s->defaults[col], default_row_host, s->dim * sizeof(float),
                      hipMemcpyHostToDevice));
+#ifdef DR_UC_DIAG
+    uc_diag_check("default row", s->defaults[col], default_row_host, s->dim * sizeof(float));
+#endif
   }
   return DR_OK;
 }
@@ -1354,8 +1370,22 @@ static int grow(EvShared* s, int64_t need, hipStream_t st) {
       const int64_t w = col_words(s, c);
       float* np = nullptr;
       DR_HIP(hipMalloc(&np, (size_t)nrc * w * sizeof(float)));
+#ifdef DR_UC_DIAG
+      {
+        int frc = fill_bytes(np, 0xFF, (size_t)nrc * w * sizeof(float), st);
+        if (frc) return frc;
+      }
+#endif
       DR_HIP(grow_copy(np, s->pools[c], (size_t)s->row_cap * w * sizeof(float), st));
       DR_HIP(hipStreamSynchronize(st));
+#ifdef DR_UC_DIAG
+      {
+        const size_t cb = (size_t)std::min<int64_t>(s->row_cap * w, 4096) * sizeof(float);
+        std::vector<float> old(cb / 4);
+        DR_HIP(hipMemcpy(old.data(), s->pools[c], cb, hipMemcpyDeviceToHost));
+        uc_diag_check("grown pool (head)", np, old.data(), cb);
+      }
+#endif
       DR_HIP(hipFree(s->pools[c]));
       s->pools[c] = np;
     }

@@ -6,6 +6,8 @@
 // recv buffers.  Here the requester writes every (key, slot) pair straight
 // into the owner's inbox over xGMI: no send buffer, no host read of counts.
 #include <map>
+#include <stdio.h>
+#include <vector>
 #include <mutex>
 #include <stdlib.h>
 
@@ -395,11 +397,62 @@ int dr_ipc_alloc(size_t bytes, void** ptr_out) {
   return DR_OK;
 }
 
+#ifdef DR_UC_DIAG
+}  // extern "C" (the diagnostics have C++ linkage)
 namespace dr {
 // Diagnostic (DR_IPC_RELEASE=3/4 below): a system-scope fence from blocks on
 // every XCD -- an L2 write-back and invalidate of each XCD's L2.
 __global__ void uc_l2_flush_kernel() { __threadfence_system(); }
+
+// Ranges of uncached blocks handed back to hipFree, and a check of a small
+// buffer a later allocation wrote by DMA: the bytes as a D2H copy reads them
+// and as a kernel reads them (plain loads, stored to pinned host memory).
+static std::mutex g_diag_mu;
+static std::vector<std::pair<uintptr_t, size_t>> g_freed;
+
+void uc_diag_freed(void* p, size_t n) {
+  std::lock_guard<std::mutex> g(g_diag_mu);
+  g_freed.push_back({(uintptr_t)p, n});
+  fprintf(stderr, "[uc-diag] hipFree uncached [%p, +%zu)\n", p, n);
+}
+
+__global__ void uc_diag_read_kernel(const uint32_t* __restrict__ src, int64_t n,
+                                    uint32_t* __restrict__ dst) {
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+
+void uc_diag_check(const char* what, const void* dev, const void* expect, size_t bytes) {
+  const size_t nw = bytes / 4;
+  if (nw == 0) return;
+  std::vector<uint32_t> dma(nw);
+  uint32_t* kh = nullptr;
+  if (hipHostMalloc(&kh, nw * 4) != hipSuccess) return;
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpy(dma.data(), dev, nw * 4, hipMemcpyDeviceToHost);
+  hipLaunchKernelGGL(uc_diag_read_kernel, dim3(1), dim3(256), 0, nullptr,
+                     static_cast<const uint32_t*>(dev), (int64_t)nw, kh);
+  (void)hipDeviceSynchronize();
+  const uint32_t* ex = static_cast<const uint32_t*>(expect);
+  size_t bad_dma = 0, bad_k = 0;
+  for (size_t i = 0; i < nw; ++i) {
+    bad_dma += dma[i] != ex[i];
+    bad_k += kh[i] != ex[i];
+  }
+  bool recycled = false;
+  {
+    std::lock_guard<std::mutex> g(g_diag_mu);
+    for (auto& r : g_freed)
+      if ((uintptr_t)dev < r.first + r.second && (uintptr_t)dev + bytes > r.first) recycled = true;
+  }
+  fprintf(stderr,
+          "[uc-diag] %s %p +%zu: on a freed uncached range %d, D2H mismatches %zu, "
+          "kernel-read mismatches %zu (word 0: expect %08x D2H %08x kernel %08x)\n",
+          what, dev, bytes, (int)recycled, bad_dma, bad_k, ex[0], dma[0], kh[0]);
+  (void)hipHostFree(kh);
+}
 }  // namespace dr
+extern "C" {
+#endif
 
 // Returns the buffer to the uncached free list (never to hipFree, see
 // above).  Cheap and safe to call from a DLPack deleter: the next
@@ -412,16 +465,19 @@ int dr_ipc_free(void* ptr) {
   auto it = u.size_of.find(ptr);
   DR_REQUIRE(it != u.size_of.end(), DR_INVALID_ARGUMENT,
              "dr_ipc_free: %p was not allocated by dr_ipc_alloc", ptr);
-  // Diagnostic switch for the reuse hazard above (tools/gpu_uc_reuse.sh):
+#ifdef DR_UC_DIAG
+  // Diagnostic build only (make ab AB_FLAGS=-DDR_UC_DIAG; tools/gpu_uc_reuse.sh):
   // DR_IPC_RELEASE=1 hands the block back to hipFree at once (the round-2
   // behaviour), =2 after a device-wide synchronisation, =3 / 4 with the L2
-  // flush kernel after (and before) the free.  Unset: free list.
+  // flush kernel after (and before) the free.  The product library has no
+  // such switch: freed uncached blocks only ever go to the free list.
   static const int release = [] {
     const char* e = getenv("DR_IPC_RELEASE");
     return e ? atoi(e) : 0;
   }();
   if (release >= 1 && release <= 4) {
     // 3: L2 flushed on every XCD after the free, 4: before and after
+    uc_diag_freed(ptr, it->second.second);
     u.size_of.erase(it);
     if (release >= 2) DR_HIP(hipDeviceSynchronize());
     if (release == 4) {
@@ -435,6 +491,7 @@ int dr_ipc_free(void* ptr) {
     }
     return DR_OK;
   }
+#endif
   u.free.insert({it->second, ptr});
   return DR_OK;
 }

@@ -69,24 +69,66 @@ def _default_row(initializer, dim, device, dtype=torch.float32):
 # current stream says nothing about another thread's capture.  So __del__
 # never releases: it queues the handle, and the queue is flushed at points
 # where the library itself runs uncaptured host work (EV creation, the end
-# of an optimizer's apply_gradients when its stream is not capturing), by
-# flush_releases(), and at interpreter exit.
+# of an optimizer's apply_gradients) and by flush_releases() -- and only when
+# no capture is open anywhere in the process: torch.cuda.CUDAGraph's
+# capture_begin / capture_end are counted process-wide (_CAPTURES), on every
+# thread.  At interpreter exit the queue is dropped (the process's device
+# memory goes with it).
 _DEFERRED = []
 _DEFERRED_LOCK = threading.Lock()
+_CAPTURES = [0]     # torch graph captures open in this process (any thread)
+
+
+def _install_capture_counter():
+    G = getattr(torch.cuda, "CUDAGraph", None)
+    if G is None or getattr(G, "_dr_counted", False):
+        return
+    begin, end = G.capture_begin, G.capture_end
+
+    def capture_begin(self, *a, **k):
+        with _DEFERRED_LOCK:
+            _CAPTURES[0] += 1
+        try:
+            return begin(self, *a, **k)
+        except BaseException:
+            with _DEFERRED_LOCK:
+                _CAPTURES[0] -= 1
+            raise
+
+    def capture_end(self, *a, **k):
+        try:
+            return end(self, *a, **k)
+        finally:
+            with _DEFERRED_LOCK:
+                _CAPTURES[0] -= 1
+
+    G.capture_begin, G.capture_end, G._dr_counted = capture_begin, capture_end, True
+
+
+_install_capture_counter()
 
 
 def _capturing():
+    """A capture is open on this thread's stream or on any thread (torch)."""
+    if _CAPTURES[0] > 0:
+        return True
     return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
 
 
 def _flush_deferred_releases():
-    if not _DEFERRED or _capturing():
+    if not _DEFERRED:
         return
+    # the lock is held across the frees: a capture_begin on another thread
+    # waits for them instead of starting in between
     with _DEFERRED_LOCK:
+        if _CAPTURES[0] > 0:
+            return
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return
         hs = _DEFERRED[:]
         del _DEFERRED[:]
-    for h in hs:
-        lib().dr_ev_release(h)
+        for h in hs:
+            lib().dr_ev_release(h)
 
 
 def flush_releases():
@@ -102,7 +144,7 @@ def _release_handle(h):
         _DEFERRED.append(h)
 
 
-atexit.register(lambda: _DEFERRED.clear())   # the process is going away: no frees needed
+atexit.register(lambda: _DEFERRED.clear())   # dropped: the process's device memory goes too
 
 
 _KEY_DTYPES = (torch.int64, torch.int32)
