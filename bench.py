@@ -328,7 +328,7 @@ def criteo_hybrid_leg(args, dev, log, world, rank, dist, staged):
     for t in shard:
         n_own = int((card[t] - rank + world - 1) // world)
         ev = dr.EmbeddingVariable("hyb_sh%d" % t, D, 0.0, device=dev,
-                                  capacity=n_own + max(1 << 20, 12 * world * B))
+                                  capacity=n_own + max(1 << 20, 4 * world * B))
         ev.insert_synthetic(rank, n_own, seed=5000 + t, key_stride=world)
         sh_evs.append(ev)
     torch.cuda.synchronize()
@@ -670,11 +670,16 @@ def main():
     t0 = time.perf_counter()
     evs = []
     for t in range(T):
-        # headroom for one step of new keys per table: B (local resolve) or
-        # N * B (an owner serving every rank, dr_xgmi_serve), with slack for
-        # the asynchronously mirrored row count (no host sync per step)
+        # headroom for the worst-case new keys of the steps in flight before
+        # the asynchronously mirrored row count catches up: B (local
+        # resolve) or N * B (an owner serving every rank, dr_xgmi_serve) per
+        # step, 4 steps' worth (a lagging mirror past that costs one host
+        # sync, never a growth: every key here exists).  Row pool = capacity
+        # rows, key table next_pow2(2 x capacity) slots: at N = 8 and
+        # B = 65 536 that is 14.6 M rows (7.5 GB) + 33.5 M slots (0.54 GB)
+        # per table, against 18.8 M / 67 M with the earlier 12 x N x B.
         ev = dr.EmbeddingVariable("table%d" % t, D, 0.0, device=dev,
-                                  capacity=R + max(1 << 20, 12 * world * B))
+                                  capacity=R + max(1 << 20, 4 * world * B))
         # rank r owns keys k % world == r of the keyspace [0, R * world)
         ev.insert_synthetic(rank, R, seed=1000 + t, key_stride=world)
         evs.append(ev)

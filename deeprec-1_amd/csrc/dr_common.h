@@ -242,6 +242,8 @@ int rows_apply_sgd(const dr_pool_grad_desc* descs_host, int num_tables, int64_t 
 // D2H-vs-kernel read check of a buffer against the bytes expected in it
 void uc_diag_freed(void* p, size_t n);
 void uc_diag_check(const char* what, const void* dev, const void* expect, size_t bytes);
+bool uc_diag_check_xcd(const char* what, const void* dev, uint32_t fill, size_t bytes);
+void uc_diag_writeback(int system);
 #endif
 
 // ---- scan / sort primitives (scan_sort.hip) --------------------------------

@@ -1277,6 +1277,14 @@ static int alloc_pool(EvShared* s, int col, const float* default_row_host) {
     if (!frc) frc = fill_bytes(s->defaults[col], 0xFF, (size_t)w * sizeof(float), nullptr);
     if (frc) return frc;
     DR_HIP(hipDeviceSynchronize());
+    const size_t cb = (size_t)std::min<int64_t>(s->row_cap * w, 1 << 18) * sizeof(float);
+    if (uc_diag_check_xcd("new pool (poisoned)", s->pools[col], 0xFFFFFFFFu, cb)) {
+      uc_diag_writeback(0);
+      if (uc_diag_check_xcd("  after an agent-scope L2 write-back", s->pools[col], 0xFFFFFFFFu, cb)) {
+        uc_diag_writeback(1);
+        uc_diag_check_xcd("  after a system-scope L2 write-back", s->pools[col], 0xFFFFFFFFu, cb);
+      }
+    }
   }
 #endif
   if (w != s->dim) {
@@ -1537,7 +1545,8 @@ static int resolve_grouped(dr_ev* const* evs, int T, const int64_t* keys, const 
     ig.koff[t] = g.koff[t];
     ig.n_dev[t] = g.n_dev[t];
     any_bloom |= g.e[t].k_hash > 0;
-    DR_REQUIRE(col_words(evs[t]->sh, evs[t]->col) == col_words(evs[0]->sh, evs[0]->col),
+    DR_REQUIRE(col_words(evs[t]->sh, evs[t]->col) == col_words(evs[0]->sh, evs[0]->col) &&
+                   evs[t]->sh->dim == evs[0]->sh->dim && evs[t]->sh->bf16 == evs[0]->sh->bf16,
                DR_INVALID_ARGUMENT, "grouped EVs must share dim and value type");
   }
   g.koff[T] = total;

@@ -450,6 +450,109 @@ void uc_diag_check(const char* what, const void* dev, const void* expect, size_t
           what, dev, bytes, (int)recycled, bad_dma, bad_k, ex[0], dma[0], kh[0]);
   (void)hipHostFree(kh);
 }
+
+// An acquire at system scope on every XCD: invalidates each XCD's L2 lines of
+// memory that is not local-coherent (and the vector L1s).
+__global__ void uc_inv_kernel() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+// L2 write-back of every XCD at agent scope (buffer_wbl2 sc1, what a
+// kernel-end release does for coarse-grained memory) or system scope
+// (buffer_wbl2 sc0 sc1 + buffer_inv sc0 sc1).
+__global__ void uc_wb_agent_kernel() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent"); }
+
+void uc_diag_writeback(int system) {
+  if (system)
+    hipLaunchKernelGGL(uc_l2_flush_kernel, dim3(2048), dim3(64), 0, nullptr);
+  else
+    hipLaunchKernelGGL(uc_wb_agent_kernel, dim3(2048), dim3(64), 0, nullptr);
+  (void)hipDeviceSynchronize();
+}
+
+// The same read from 64 blocks spread over the XCDs: block b records its XCD
+// (HW_REG_XCC_ID) and how many words differ from `expect` -- a stale
+// translation of a recycled VA would show on some XCDs only.
+__global__ void uc_diag_xcd_kernel(const uint32_t* __restrict__ src, int64_t n,
+                                   uint32_t expect_fill, const uint32_t* __restrict__ expect,
+                                   uint32_t* __restrict__ res) {
+  __shared__ uint32_t bad, zeros;
+  if (threadIdx.x == 0) {
+    bad = 0;
+    zeros = 0;
+  }
+  __syncthreads();
+  uint32_t b = 0, z = 0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t v = __builtin_nontemporal_load(src + i);
+    const uint32_t e = expect ? expect[i] : expect_fill;
+    b += v != e;
+    z += v == 0;
+  }
+  atomicAdd(&bad, b);
+  atomicAdd(&zeros, z);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    res[3 * blockIdx.x] = (uint32_t)__builtin_amdgcn_s_getreg(0x1814);   // XCC_ID[3:0]
+    res[3 * blockIdx.x + 1] = bad;
+    res[3 * blockIdx.x + 2] = zeros;
+  }
+}
+
+bool uc_diag_check_xcd(const char* what, const void* dev, uint32_t fill, size_t bytes) {
+  const size_t nw = bytes / 4;
+  if (nw == 0) return false;
+  uint32_t* res = nullptr;
+  if (hipHostMalloc(&res, 64 * 3 * 4) != hipSuccess) return false;
+  (void)hipDeviceSynchronize();
+  hipLaunchKernelGGL(uc_diag_xcd_kernel, dim3(64), dim3(256), 0, nullptr,
+                     static_cast<const uint32_t*>(dev), (int64_t)nw, fill, nullptr, res);
+  (void)hipDeviceSynchronize();
+  // the bytes as DMA reads them (no GPU L2 on the path), and the per-block
+  // view again after an L2 invalidate on every XCD
+  size_t dz = 0, dbad = 0;
+  {
+    std::vector<uint32_t> h(nw);
+    (void)hipMemcpy(h.data(), dev, nw * 4, hipMemcpyDeviceToHost);
+    for (size_t i = 0; i < nw; ++i) {
+      dz += h[i] == 0;
+      dbad += h[i] != fill;
+    }
+  }
+  uint32_t* res2 = nullptr;
+  if (hipHostMalloc(&res2, 64 * 3 * 4) != hipSuccess) return false;
+  hipLaunchKernelGGL(uc_inv_kernel, dim3(2048), dim3(64), 0, nullptr);
+  hipLaunchKernelGGL(uc_diag_xcd_kernel, dim3(64), dim3(256), 0, nullptr,
+                     static_cast<const uint32_t*>(dev), (int64_t)nw, fill, nullptr, res2);
+  (void)hipDeviceSynchronize();
+  bool recycled = false;
+  {
+    std::lock_guard<std::mutex> g(g_diag_mu);
+    for (auto& r : g_freed)
+      if ((uintptr_t)dev < r.first + r.second && (uintptr_t)dev + bytes > r.first) recycled = true;
+  }
+  uint32_t badx[16] = {0}, zx[16] = {0}, seen[16] = {0};
+  for (int b = 0; b < 64; ++b) {
+    const uint32_t x = res[3 * b] & 15;
+    seen[x] = 1;
+    badx[x] += res[3 * b + 1];
+    zx[x] += res[3 * b + 2];
+  }
+  char line[1024];
+  int o = snprintf(line, sizeof(line), "[uc-diag] %s %p +%zu: recycled-uncached %d, per XCD "
+                   "bad/zero words:", what, dev, bytes, (int)recycled);
+  for (int x = 0; x < 16 && o < (int)sizeof(line) - 24; ++x)
+    if (seen[x]) o += snprintf(line + o, sizeof(line) - o, " %d:%u/%u", x, badx[x], zx[x]);
+  if (o < (int)sizeof(line) - 64)
+    o += snprintf(line + o, sizeof(line) - o, "; D2H bad/zero %zu/%zu; blocks 0-7 zero", dbad, dz);
+  for (int b = 0; b < 8 && o < (int)sizeof(line) - 24; ++b)
+    o += snprintf(line + o, sizeof(line) - o, " x%u:%u", res[3 * b] & 15, res[3 * b + 2]);
+  if (o < (int)sizeof(line) - 40)
+    o += snprintf(line + o, sizeof(line) - o, "; after L2 inv blocks 0-7 zero");
+  for (int b = 0; b < 8 && o < (int)sizeof(line) - 24; ++b)
+    o += snprintf(line + o, sizeof(line) - o, " x%u:%u", res2[3 * b] & 15, res2[3 * b + 2]);
+  fprintf(stderr, "%s\n", line);
+  (void)hipHostFree(res);
+  (void)hipHostFree(res2);
+  return dbad != 0;
+}
 }  // namespace dr
 extern "C" {
 #endif
