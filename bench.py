@@ -432,10 +432,25 @@ def criteo_hybrid_leg(args, dev, log, world, rank, dist, staged):
             dist.barrier()
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
+        # each part alone (same batches, same barriers): the replicated
+        # features' local lookup, then the sharded features' lookup with its
+        # exchange -- the inputs of DESIGN section 7's model
+        parts = []
+        for fn in (lambda i: local_lookup(fsets[i % 4]), lambda i: engine.forward(ishard[i % 4])):
+            if dist is not None:
+                dist.barrier()
+            torch.cuda.synchronize()
+            tp = time.perf_counter()
+            for i in range(args.steps):
+                fn(i)
+            if dist is not None:
+                dist.barrier()
+            torch.cuda.synchronize()
+            parts.append(time.perf_counter() - tp)
     if dist is not None:
-        te = torch.tensor([el], dtype=torch.float64, device="cpu" if staged else dev)
+        te = torch.tensor([el] + parts, dtype=torch.float64, device="cpu" if staged else dev)
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
-        el = float(te.item())
+        el, parts = float(te[0].item()), [float(x) for x in te[1:].tolist()]
     ms = el / args.steps * 1e3
     res = {"workload": "real Criteo-TB cardinalities (modelzoo/SOK/DLRM/train_stand.py:242-248), "
                        "hybrid placement: %d features <= 585935 rows replicated (one fused "
@@ -444,6 +459,8 @@ def criteo_hybrid_leg(args, dev, log, world, rank, dist, staged):
                        "embedding_lookup_sparse(sum) forward" % (len(rep), int(rcard.sum()),
                                                                  len(shard), kind, B),
            "n_gpus": world, "ms_per_step": round(ms, 4),
+           "parts_ms_per_step": {"replicated_local": round(parts[0] / args.steps * 1e3, 4),
+                                 "sharded_with_exchange": round(parts[1] / args.steps * 1e3, 4)},
            "lookups_per_s": round(26 * B * world / (ms * 1e-3), 1),
            "samples_per_s": round(B * world / (ms * 1e-3), 1),
            "sharded_lookups_per_gpu_step": len(shard) * B,
@@ -536,7 +553,7 @@ def dcn_bf16_leg(args, dev, log):
            "checked_rows": 2048,
            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
                         "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
-                        "kernel": "dr::ev_lookup_onehot_kernel<4,16,1,ALI,4> on bf16 rows "
+                        "kernel": "dr::ev_lookup_onehot_kernel<4,16,1,ALI,2> on bf16 rows "
                                   "(64 float words)",
                         "kernel_ms": round(k_ms, 4), "bytes_per_lookup": per,
                         "bytes_per_launch": T * B * per},
@@ -625,7 +642,7 @@ def deepfm_leg(args, dev, log):
            "samples_per_s": round(B / (k_ms * 1e-3), 1),
            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
                         "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
-                        "kernel": "dr::ev_lookup_onehot_kernel<4,16,1,ALI,4>",
+                        "kernel": "dr::ev_lookup_onehot_kernel<4,16,1,ALI,2>",
                         "kernel_ms": round(k_ms, 4), "bytes_per_lookup": per,
                         "bytes_per_launch": T * B * per},
            "train_step": {"ms_per_step": round(tms, 4),

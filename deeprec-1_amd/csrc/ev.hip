@@ -2097,7 +2097,12 @@ static void launch_lookup_nb(const LookupArgs& a, int T, int64_t B, int dim, con
 template <int VEC, int G, int CPL, int ORDER>
 static void launch_lookup_onehot(const LookupArgs& a, int T, int64_t B, int dim, const LookupWs& w,
                                  hipStream_t st) {
-  static const int nb = getenv("DR_LOOKUP_NB") ? atoi(getenv("DR_LOOKUP_NB")) : 4;
+  // rows in flight per lane group: 2 for rows of <= 64 floats (D = 64:
+  // 0.194 against 0.200 ms for 4, profiles/r04_lookup_ab_nb2.log -- more,
+  // smaller groups hide the dependent slot probe better), 4 above (D = 128:
+  // the step, not the kernel alone, is 0.7 % slower with 2)
+  static const int nb_env = getenv("DR_LOOKUP_NB") ? atoi(getenv("DR_LOOKUP_NB")) : 0;
+  const int nb = nb_env ? nb_env : (G <= 16 ? 2 : 4);
   if (nb == 8 && G >= 8)
     launch_lookup_nb<VEC, G, CPL, ORDER, 8>(a, T, B, dim, w, st);
   else if (nb == 2)

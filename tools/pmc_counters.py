@@ -1,10 +1,12 @@
 """Per-kernel medians of rocprofv3 --pmc passes (one directory per pass).
 
-  python tools/pmc_counters.py <out.json> <kernel-substring>[,<substring>...] <dir> [<dir> ...]
+  python tools/pmc_counters.py <out.json> <kernel-substring>[|<substring>...] <dir> [<dir> ...]
 
 Reads every <dir>/**/*_counter_collection.csv, keeps the dispatches whose
 kernel name contains a substring, and writes, per substring and counter, the
-median value per dispatch and the number of dispatches."""
+median value per dispatch, the number of dispatches and every dispatch's
+value in launch order (a bench run launches a kernel in several roles: the
+per-dispatch list tells them apart)."""
 import csv
 import glob
 import json
@@ -14,7 +16,7 @@ import sys
 
 
 def main():
-    out, subs, dirs = sys.argv[1], sys.argv[2].split(","), sys.argv[3:]
+    out, subs, dirs = sys.argv[1], sys.argv[2].split("|"), sys.argv[3:]
     res = {}
     for d in dirs:
         for f in glob.glob(os.path.join(d, "**", "*_counter_collection.csv"), recursive=True):
@@ -28,6 +30,7 @@ def main():
             for (s, c), per in vals.items():
                 v = list(per.values())
                 res.setdefault(s, {})[c] = {"median": statistics.median(v), "dispatches": len(v),
+                                            "per_dispatch": v,
                                             "pass": os.path.basename(d.rstrip("/"))}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
