@@ -1151,7 +1151,11 @@ __device__ __forceinline__ void c8_stage(const uint16_t* __restrict__ X, int64_t
   }
 }
 
-template <bool EPI, int GM, bool PIPE>
+// MODE 1: the cross layer, out = x0 * (xl W^T + b) + xl (lin_out = xl W^T + b);
+// MODE 2: the layer's input gradient, out = xl W^T + x0 -- called with A = u,
+// W = the transposed weight and x0 = g, it is dx_l = u W + g (no bias);
+// MODE 0: the loop alone (timing build, no outputs).
+template <int MODE, int GM, bool PIPE>
 __global__ __launch_bounds__(512, 1) void crossnet_8ph_kernel(
     const uint16_t* __restrict__ x0, const uint16_t* __restrict__ xl,
     const uint16_t* __restrict__ W, const float* __restrict__ bias, int64_t M, int d,
@@ -1266,7 +1270,7 @@ __global__ __launch_bounds__(512, 1) void crossnet_8ph_kernel(
   if (!g1) __builtin_amdgcn_s_barrier();  // matches group 1's extra barrier
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  if (!EPI) {  // loop-only timing build: keep the MFMAs alive, store nothing
+  if (MODE == 0) {  // loop-only timing build: keep the MFMAs alive, store nothing
     float sum = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -1301,7 +1305,7 @@ __global__ __launch_bounds__(512, 1) void crossnet_8ph_kernel(
       if (grow >= M) grow = M - 1;
       const int64_t o = grow * d + gcol_c;
       a0[it] = *reinterpret_cast<const u32x4*>(x0 + o);
-      al[it] = *reinterpret_cast<const u32x4*>(xl + o);
+      if (MODE == 1) al[it] = *reinterpret_cast<const u32x4*>(xl + o);
     }
   };
   auto acc_to_lds = [&](int h) {
@@ -1331,16 +1335,23 @@ __global__ __launch_bounds__(512, 1) void crossnet_8ph_kernel(
       u32x4 ov, lv;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const uint32_t p0 = a0[it][e], pl = al[it][e];
-        const float v0 = bf2f((uint16_t)(p0 & 0xffff)) * lin[2 * e] + bf2f((uint16_t)(pl & 0xffff));
-        const float v1 = bf2f((uint16_t)(p0 >> 16)) * lin[2 * e + 1] + bf2f((uint16_t)(pl >> 16));
-        ov[e] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
-        lv[e] = (uint32_t)f2bf(lin[2 * e]) | ((uint32_t)f2bf(lin[2 * e + 1]) << 16);
+        const uint32_t p0 = a0[it][e];
+        if (MODE == 1) {
+          const uint32_t pl = al[it][e];
+          const float v0 = bf2f((uint16_t)(p0 & 0xffff)) * lin[2 * e] + bf2f((uint16_t)(pl & 0xffff));
+          const float v1 = bf2f((uint16_t)(p0 >> 16)) * lin[2 * e + 1] + bf2f((uint16_t)(pl >> 16));
+          ov[e] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+          lv[e] = (uint32_t)f2bf(lin[2 * e]) | ((uint32_t)f2bf(lin[2 * e + 1]) << 16);
+        } else {  // one fp32 sum of the product and the addend, one rounding
+          const float v0 = lin[2 * e] + bf2f((uint16_t)(p0 & 0xffff));
+          const float v1 = lin[2 * e + 1] + bf2f((uint16_t)(p0 >> 16));
+          ov[e] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+        }
       }
       if (grow < M && col_ok) {
         const int64_t o = grow * d + gcol;
         *reinterpret_cast<u32x4*>(out + o) = ov;
-        if (lin_out) *reinterpret_cast<u32x4*>(lin_out + o) = lv;
+        if (MODE == 1 && lin_out) *reinterpret_cast<u32x4*>(lin_out + o) = lv;
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ct reads done before it is rewritten
@@ -1683,12 +1694,12 @@ int dr_crossnet_forward_bf16(const uint16_t* x0, const uint16_t* xl, const uint1
 #define DR_C8(E, G, P)                                                                     \
   hipLaunchKernelGGL((crossnet_8ph_kernel<E, G, P>), dim3((unsigned)tiles), dim3(512), 0,   \
                      S(stream), x0, xl, W, bias, batch, d, ncols, out, lin_out)
-    if (variant == 6) DR_C8(true, 1, false);
-    else if (variant == 8) DR_C8(true, 4, false);
-    else if (variant == 9) DR_C8(true, 8, false);
-    else if (variant == 10) DR_C8(true, 4, true);
-    else if (variant == 11 || variant == 12) DR_C8(true, 4, false);
-    else DR_C8(false, 4, false);  // 7: loop-only timing build (no outputs; measurement only)
+    if (variant == 6) DR_C8(1, 1, false);
+    else if (variant == 8) DR_C8(1, 4, false);
+    else if (variant == 9) DR_C8(1, 8, false);
+    else if (variant == 10) DR_C8(1, 4, true);
+    else if (variant == 11 || variant == 12) DR_C8(1, 4, false);
+    else DR_C8(0, 4, false);  // 7: loop-only timing build (no outputs; measurement only)
 #undef DR_C8
     if (split) {
       const int64_t st = ceil_div(batch, CG_BM) * ceil_div(d - ncols, CG_BN);
@@ -1735,6 +1746,25 @@ int dr_crossnet_forward_bf16(const uint16_t* x0, const uint16_t* xl, const uint1
   dim3 grid((unsigned)ceil_div(d, CN_BN), (unsigned)ceil_div(batch, CN_BM));
   hipLaunchKernelGGL(crossnet_kernel, grid, dim3(256), 0, S(stream), x0, xl, W, bias, batch, d,
                      out);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_crossnet_dx_bf16(const uint16_t* u, const uint16_t* wt, const uint16_t* g, int64_t batch,
+                        int d, uint16_t* dx, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && d > 0 && d % 64 == 0, DR_INVALID_ARGUMENT,
+             "dr_crossnet_dx_bf16: d must be a multiple of 64 (pad features)");
+  DR_REQUIRE(u && wt && g && dx, DR_INVALID_ARGUMENT, "null operand");
+  DR_REQUIRE((((uintptr_t)u | (uintptr_t)wt | (uintptr_t)g | (uintptr_t)dx) & 15) == 0,
+             DR_INVALID_ARGUMENT, "operands must be 16-B aligned");
+  if (batch == 0) return DR_OK;
+  const int64_t tiles = ceil_div(batch, 256) * ceil_div(d, 256);
+  DR_REQUIRE(tiles < (1ll << 31), DR_INVALID_ARGUMENT, "batch too large");
+  // the forward's 256^2 schedule with A = u, B = W^T and the addend g
+  hipLaunchKernelGGL((crossnet_8ph_kernel<2, 4, false>), dim3((unsigned)tiles), dim3(512), 0,
+                     S(stream), g, u, wt, (const float*)nullptr, batch, d, d, dx,
+                     (uint16_t*)nullptr);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

@@ -257,6 +257,7 @@ SIGNATURES = {
     "dr_crossnet_layer_bf16": (_I32, [_P, _P, _P, _P, _I64, _I32, _P, _P]),
     "dr_crossnet_forward_bf16": (_I32, [_P, _P, _P, _P, _I64, _I32, _P, _P, _P]),
     "dr_crossnet_backward_workspace_size": (_SZ, [_I64, _I32]),
+    "dr_crossnet_dx_bf16": (_I32, [_P, _P, _P, _I64, _I32, _P, _P]),
     "dr_gemm_nt_workspace_size": (_SZ, [_I64, _I64, _I32]),
     "dr_gemm_nt_bf16": (_I32, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I32, _P, _I64, _I32,
                                _I32, _P, _SZ, _P]),

@@ -606,13 +606,26 @@ def wdl_train_step(model, dense, ids, labels, deep_opt, deep_ev_opt, wide_opt, w
     return loss
 
 
+# DR_CROSSNET_DX_LIB=1 (A/B switch): the input gradient as the library's addmm
+_CROSS_DX_LIB = os.environ.get("DR_CROSSNET_DX_LIB", "0") == "1"
+
+
+def _cross_dx(u, wb, g):
+    """dx_l = u W + g of a cross layer: the hand 256^2 MFMA kernel
+    (dr_crossnet_dx_bf16, on W^T), one rounding of the fp32 result as
+    torch.addmm(g, u, W) in bf16."""
+    if _CROSS_DX_LIB:
+        return torch.addmm(g, u, wb)
+    return ops.crossnet_dx(u, wb.t().contiguous(), g)
+
+
 class CrossLayer(torch.autograd.Function):
     """DCN-v2 cross layer x_{l+1} = x0 * (x_l W^T + b) + x_l (BASELINE
     configs[4]; absent from the reference).  Forward: the
     fused bf16 MFMA kernel (dr_crossnet_forward_bf16), which also hands back
-    lin = x_l W^T + b for the backward.  Backward (library GEMMs, fp32
-    accumulate): u = g * x0, dW = u^T x_l, db = sum u, dx_l = u W + g,
-    dx0 = g * lin."""
+    lin = x_l W^T + b for the backward.  Backward (fp32 accumulate): u = g *
+    x0, dW = u^T x_l (library GEMM), db = sum u, dx_l = u W + g (the hand
+    MFMA kernel), dx0 = g * lin."""
 
     @staticmethod
     def forward(ctx, x0, xl, weight, bias):
@@ -628,7 +641,7 @@ class CrossLayer(torch.autograd.Function):
         u = g * x0
         dW = torch.matmul(u.t(), xl).float()
         db = u.float().sum(0)
-        dxl = torch.addmm(g, u, wb)
+        dxl = _cross_dx(u, wb, g)
         dx0 = g * lin
         return dx0, dxl, dW, db
 
@@ -638,8 +651,8 @@ class CrossStack(torch.autograd.Function):
     autograd node.  Forward: the fused MFMA kernel per layer (which hands back
     lin_l for the backward).  Backward, layer by layer in reverse: ONE
     elementwise pass (dr_crossnet_backward_elem_bf16) forms u = g * x0, adds
-    g * lin_l into a running fp32 dx0 and the column sums db_l; the two
-    library GEMMs give dW_l = u^T x_l and g <- u W_l + g (= dx_l).  The x0
+    g * lin_l into a running fp32 dx0 and the column sums db_l; dW_l = u^T
+    x_l (library GEMM) and g <- u W_l + g (= dx_l, the hand MFMA kernel).  The x0
     gradient is the running sum plus the first layer's dx_l (x_0 = x0) --
     what CrossLayer's per-layer autograd adds up in separate bf16 passes."""
 
@@ -670,7 +683,7 @@ class CrossStack(torch.autograd.Function):
             u, acc, db = ops.crossnet_backward_elem(g, x0, lins[l], acc)
             dws[l] = torch.matmul(u.t(), xs[l]).float()
             dbs[l] = db
-            g = torch.addmm(g, u, ws[l])
+            g = _cross_dx(u, ws[l], g)
         dx0 = (acc + g.float()).to(torch.bfloat16)
         return (dx0, *dws, *dbs)
 

@@ -753,6 +753,22 @@ def transpose_bf16(x, colsum=False):
     return out, part.sum(0)
 
 
+def crossnet_dx(u, wt, g):
+    """dr_crossnet_dx_bf16: dx = u W + g for a cross layer's input gradient,
+    wt = W^T [d, d] bf16 contiguous; u, g [B, d] bf16, d % 64 == 0.  One
+    rounding of the fp32 u W + g (torch.addmm(g, u, W) in bf16)."""
+    dev = _dev(u)
+    B, d = u.shape
+    if d % 64 or tuple(g.shape) != (B, d) or tuple(wt.shape) != (d, d) or any(
+            t.dtype != torch.bfloat16 for t in (u, wt, g)):
+        raise ValueError("crossnet_dx needs bf16 u, g [B, d] and wt [d, d] with d % 64 == 0")
+    u, wt, g = u.contiguous(), wt.contiguous(), g.contiguous()
+    dx = torch.empty((B, d), dtype=torch.bfloat16, device=dev)
+    check(lib().dr_crossnet_dx_bf16(ptr(u), ptr(wt), ptr(g), B, d, ptr(dx), stream_handle(dev)))
+    _post(dev)
+    return dx
+
+
 def crossnet_backward_elem(g, x0, lin, acc=None):
     """dr_crossnet_backward_elem_bf16: the elementwise part of a cross
     layer's backward in one pass.  g, x0, lin [B, d] bf16; acc [B, d] fp32

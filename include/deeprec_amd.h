@@ -944,11 +944,17 @@ int dr_dot_interaction_concat_grad_bf16(const float* x, const uint16_t* grad, in
 int dr_crossnet_layer_bf16(const uint16_t* x0, const uint16_t* xl, const uint16_t* W,
                            const float* bias, int64_t batch, int d, uint16_t* out,
                            void* stream);
-/* CrossNet backward, elementwise part of one layer in one pass (the GEMMs   */
-/* dW = u^T x_l, dx_l = u W + g stay library calls): u = bf16(g * x0),       */
+/* CrossNet backward, elementwise part of one layer in one pass (dx_l = u W  */
+/* + g: dr_crossnet_dx_bf16; dW = u^T x_l a library GEMM): u = bf16(g * x0), */
 /* acc_out = (acc_in or 0) + g * lin in fp32 (dx0 summed over the layers),  */
 /* db = column sums of u (fixed order).  g, x0, lin, u bf16 [batch, d];     */
 /* acc_in may be NULL or equal acc_out.  Workspace: per-row-block partials.  */
+/* The layer's input gradient on the forward's 256 x 256 MFMA schedule:     */
+/* dx = u W + g = u wt^T + g, wt = W^T [d, d] bf16 (row k = column k of W),   */
+/* u, g, dx [batch, d] bf16; fp32 accumulate, one rounding of (u W + g) --    */
+/* what torch.addmm(g, u, W) computes in bf16.  d % 64 == 0, 16-B aligned.   */
+int dr_crossnet_dx_bf16(const uint16_t* u, const uint16_t* wt, const uint16_t* g, int64_t batch,
+                        int d, uint16_t* dx, void* stream);
 size_t dr_crossnet_backward_workspace_size(int64_t batch, int d);
 int dr_crossnet_backward_elem_bf16(const uint16_t* g, const uint16_t* x0, const uint16_t* lin,
                                    const float* acc_in, float* acc_out, uint16_t* u, float* db,

@@ -91,6 +91,25 @@ def test_crossnet_backward_elem_matches_torch(B, d):
     assert torch.equal(acc2, (g.float() * lin.float()))
 
 
+@pytest.mark.parametrize("B,d", [(300, 192), (1000, 3392), (64, 64), (513, 448)])
+def test_crossnet_dx_matches_torch(B, d):
+    """dr_crossnet_dx_bf16 (dx = u W + g on the 256^2 MFMA schedule, W^T as
+    the B operand) against the fp32 torch product from the same bf16
+    operands (bf16 output tolerance) and the library's bf16 addmm; repeated
+    launches bit-identical."""
+    from deeprec_amd import ops
+    gen = torch.Generator(device="cpu").manual_seed(B * 3 + d)
+    u = torch.randn(B, d, generator=gen).to(DEV, torch.bfloat16)
+    g = torch.randn(B, d, generator=gen).to(DEV, torch.bfloat16)
+    W = (torch.randn(d, d, generator=gen) / d ** 0.5).to(DEV, torch.bfloat16)
+    dx = ops.crossnet_dx(u, W.t().contiguous(), g)
+    want = u.float() @ W.float() + g.float()
+    _close(dx, want)
+    _close(dx, torch.addmm(g, u, W))
+    for _ in range(3):
+        assert torch.equal(ops.crossnet_dx(u, W.t().contiguous(), g), dx)
+
+
 def test_cross_stack_backward_matches_autograd():
     """CrossStack (3 layers, one fused elementwise pass per layer in the
     backward) against torch autograd of the fp32 composition from the same

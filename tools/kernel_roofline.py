@@ -198,6 +198,23 @@ def main():
                                                                   w.t())), it)
             report("torch_crossnet_composed", ms, flops=2 * B * dp * dp,
                    shape="B %d, d %d (hipBLASLt addmm + addcmul)" % (B, dp))
+            # the backward's input gradient dx = u W + g: hand kernel on W^T
+            # vs the library's addmm (the composed CrossStack step used it)
+            wt = w.t().contiguous()
+            dxo = torch.empty((B, dp), dtype=torch.bfloat16, device=dev)
+
+            def dx():
+                check(lib().dr_crossnet_dx_bf16(ptr(xl), ptr(wt), ptr(x0), B, dp, ptr(dxo),
+                                                stream_handle(dev)))
+            ms = timed(dx, it)
+            report("crossnet_dx_bf16", ms, flops=2 * B * dp * dp,
+                   shape="B %d, d %d (dx = u W + g, 256^2 kernel on W^T)" % (B, dp))
+            ms = timed(lambda: torch.addmm(x0, xl, w), it)
+            report("torch_addmm_dx_same_shape", ms, flops=2 * B * dp * dp,
+                   shape="B %d, d %d (hipBLASLt addmm(g, u, W))" % (B, dp))
+            ms = timed(lambda: torch.matmul(xl.t(), x0).float(), it)
+            report("torch_dw_same_shape", ms, flops=2 * B * dp * dp,
+                   shape="B %d, d %d (hipBLASLt u^T x + fp32 cast: the dW GEMM)" % (B, dp))
 
     # -- KV sparse apply: U*(24 + (1+2k)*D*4), k = columns touched -------------
     if want("apply"):
