@@ -16,7 +16,8 @@ callback).  Checks, bit for bit:
     ranks (ascending) of each source's first-occurrence unique keys that
     this rank owns with their SparseSegment*Grad rows (the oracle's Unique +
     sparse_segment_reduce_grad over every rank's batch and gradient).
-Prints one JSON line per rank; exit code != 0 on any mismatch.
+The parent prints one JSON line per rank (sent through a queue, so lines
+never interleave); exit code != 0 on any mismatch.
 """
 import argparse
 import json
@@ -62,7 +63,7 @@ def _grad(step, rank, rows):
         (rows, T * D)).astype(np.float32)
 
 
-def worker(rank, world, port):
+def worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
     sys.path.insert(0, ROOT)
@@ -188,7 +189,7 @@ def worker(rank, world, port):
     eb.close()
     comm.close()
     res["ok"] = ok
-    print(json.dumps(res), flush=True)
+    q.put(json.dumps(res))   # the parent prints: one whole line per rank
     dist.barrier()
     dist.destroy_process_group()
     if not ok:
@@ -205,11 +206,18 @@ def main():
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context("spawn")
-    procs = [ctx.Process(target=worker, args=(r, args.world, port)) for r in range(args.world)]
+    q = ctx.Queue()
+    procs = [ctx.Process(target=worker, args=(r, args.world, port, q)) for r in range(args.world)]
     for p in procs:
         p.start()
+    import queue
+    for _ in procs:
+        try:
+            print(q.get(timeout=300), flush=True)
+        except queue.Empty:
+            break
     for p in procs:
-        p.join(300)
+        p.join(60)
     codes = [p.exitcode for p in procs]
     sys.exit(0 if all(c == 0 for c in codes) else 1)
 

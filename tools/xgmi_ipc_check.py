@@ -39,7 +39,7 @@ def _step_grad(step, rank):
     return rng.standard_normal((B, T * D)).astype(np.float32)
 
 
-def worker(rank, world, port):
+def worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
     sys.path.insert(0, ROOT)
@@ -100,8 +100,9 @@ def worker(rank, world, port):
         k = ev.export()[0].cpu().numpy()
         ok = ok and bool(np.all(k % world == rank))
     eng.close()
-    print(json.dumps({"rank": rank, "world": world, "ipc_peer_write_ok": ok,
-                      "ipc_grad_pull_ok": bool(bwd_ok)}), flush=True)
+    # the parent prints the lines (one whole line per rank, never interleaved)
+    q.put(json.dumps({"rank": rank, "world": world, "ipc_peer_write_ok": ok,
+                      "ipc_grad_pull_ok": bool(bwd_ok)}))
     dist.destroy_process_group()
     if not (ok and bwd_ok):
         raise SystemExit(1)
@@ -116,7 +117,12 @@ def main():
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    mp.spawn(worker, args=(args.world, port), nprocs=args.world, join=True)
+    q = mp.get_context("spawn").SimpleQueue()
+    try:
+        mp.spawn(worker, args=(args.world, port, q), nprocs=args.world, join=True)
+    finally:
+        while not q.empty():
+            print(q.get(), flush=True)
 
 
 if __name__ == "__main__":
