@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--train-steps", type=int, default=10,
                    help="N=1: time the embedding training step too (0 = skip)")
     p.add_argument("--kernel-iters", type=int, default=20)
+    p.add_argument("--model-steps", type=int, default=10,
+                   help="timed DLRM model training steps on the headline tables (0: skip)")
     p.add_argument("--no-deepfm", dest="deepfm", action="store_false",
                    help="skip the BASELINE configs[1] (DeepFM 26 x 1e7 x 64) leg at N=1")
     p.add_argument("--no-criteo", dest="criteo", action="store_false",
@@ -1031,6 +1033,64 @@ def main():
                          % (engine_kind, T, B, world * B)}
         log("train step: %s" % json.dumps(train))
 
+    # ---- DLRM model training step on the headline tables (modelzoo.DLRM,
+    # bf16 MFMA towers): at N > 1 data-parallel with the row-sharded lookup
+    # (train_step_sharded: dense gradients all-reduced, embedding gradient
+    # rows to their owners), at N = 1 the local lookup.  Eager, barrier-
+    # bracketed, max over ranks; samples/s over the global batch.
+    dlrm = None
+    if args.model_steps > 0:
+        from deeprec_amd import modelzoo as mz
+        torch.manual_seed(0)
+        sharded_model = world > 1 and engine is not None
+        model = mz.DLRM(evs, 13, bf16=True, engine=engine if sharded_model else None).to(dev)
+        dopt = torch.optim.SGD(model.parameters(), lr=0.01)
+        eopt = dr.GradientDescentOptimizer(0.01)
+        gd = torch.Generator(device=dev)
+        gd.manual_seed(5 + rank)
+        mdense = [torch.randn((B, 13), generator=gd, device=dev) for _ in range(NBATCH)]
+        mlab = [(torch.rand(B, generator=gd, device=dev) > 0.5).float() for _ in range(NBATCH)]
+
+        def mstep(i):
+            k = i % NBATCH
+            if sharded_model:
+                return mz.train_step_sharded(model, mdense[k], batches[k], mlab[k], dopt, eopt,
+                                             world, staged=staged)
+            return mz.train_step(model, mdense[k], batches[k], mlab[k], dopt, eopt)
+
+        for i in range(2):
+            mstep(i)
+        torch.cuda.synchronize()
+        dr.status_check(dev)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.model_steps):
+            mstep(i)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        mel = time.perf_counter() - t0
+        if dist is not None:
+            te = torch.tensor([mel], dtype=torch.float64, device="cpu" if staged else dev)
+            dist.all_reduce(te, op=dist.ReduceOp.MAX)
+            mel = float(te.item())
+        dr.status_check(dev)
+        mms = mel / args.model_steps * 1e3
+        dlrm = {"ms_per_step": round(mms, 4),
+                "samples_per_s": round(world * B / (mms * 1e-3), 1),
+                "global_batch": world * B, "steps": args.model_steps,
+                "engine": engine_kind if sharded_model else "local",
+                "model": "modelzoo/DLRM/train.py DLRM, dot interaction, bf16 MFMA towers: bottom "
+                         "[13, 512, 256, %d], top [%d, 512, 256] + 1-unit output, BCE; SGD on "
+                         "the dense weights%s, KV SGD on the %d EV%s" % (
+                             D, D + (T + 1) * T // 2,
+                             " (all-reduced gradients)" if sharded_model else "", T,
+                             " shards" if sharded_model else "s")}
+        log("dlrm model step: %s" % json.dumps(dlrm))
+        model = dopt = eopt = mdense = mlab = None
+
     # ---- dominant kernel: the fused one-hot EV lookup, timed alone --------
     # dr_ev_lookup_onehot on keys this rank owns (all keys at N=1), over the
     # timed region's four step batches in rotation (a batch repeated launch
@@ -1133,7 +1193,7 @@ def main():
         # (loop variables too: `fs` holds a feature list of every table, `ev`
         # the last table -- either kept 180 GB of headline tables alive)
         evs = feats = gfeats = batch_sps = rec_sps = kfeats = gsets = fs = ev = None
-        engine = a2a = outc = graph_all = tgraph = opt = step = tstep = None
+        engine = a2a = outc = graph_all = tgraph = opt = step = tstep = mstep = None
         _free_hbm()
         log("HBM free after the headline tables: %.1f GB" % (torch.cuda.mem_get_info(dev)[0] / 1e9))
         if world == 1 and args.deepfm:
@@ -1178,6 +1238,7 @@ def main():
                        "parallelism": "row-sharded tables x%d, data-parallel batch" % world},
             "forward_samples_per_s": round(value / T, 1),
             "train_step": train,
+            "dlrm_train_step": dlrm,
             "deepfm_config": deepfm,
             "criteo_tb_cardinalities": criteo,
             "criteo_tb_hybrid": hybrid,

@@ -319,12 +319,42 @@ class _MaybeBF16(object):
             return mlp(x).float()
 
 
-class DLRM(torch.nn.Module):
-    """modelzoo/DLRM/train.py DLRM with interaction_op='dot'."""
+class _ShardedLookupFn(torch.autograd.Function):
+    """T one-hot features looked up through a multi-GPU row-sharded engine
+    (sharded.ShardedLookup, XgmiShardedLookup or NativeShardedLookup) as one
+    autograd node: forward = the engine's exchange + owner serve + pooling
+    ([B, T*D] fp32); backward hands the [B, T*D] gradient to the engine,
+    which delivers every key's gradient rows to its owner's EV shard as
+    IndexedSlices -- the KV optimizer applies them there (SOK DLRM's sparse
+    path, modelzoo/SOK/DLRM)."""
 
-    def __init__(self, evs, num_dense=13, mlp_bot=(512, 256), mlp_top=(512, 256), bf16=False):
+    @staticmethod
+    def forward(ctx, anchor, engine, ids):
+        ctx.engine = engine
+        if hasattr(engine, "bufs"):            # XgmiShardedLookup: always ready for backward
+            out = engine.forward(ids)
+        else:
+            out = engine.forward(ids, need_grad=True)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        ctx.engine.backward(g.float().contiguous())
+        return None, None, None
+
+
+class DLRM(torch.nn.Module):
+    """modelzoo/DLRM/train.py DLRM with interaction_op='dot'.  engine: a
+    row-sharded multi-GPU lookup over this rank's EV shards (evs = the
+    shards; ids = this rank's [T, B_local] batch) -- the data-parallel DLRM
+    of modelzoo/SOK/DLRM, trained with train_step_sharded."""
+
+    def __init__(self, evs, num_dense=13, mlp_bot=(512, 256), mlp_top=(512, 256), bf16=False,
+                 engine=None):
         super().__init__()
         self.bf16 = _MaybeBF16(bf16)
+        self.engine = engine
+        self._sh_anchor = None
         self.evs = list(evs)
         self.dim = self.evs[0].dim
         self.T = len(self.evs)
@@ -346,9 +376,18 @@ class DLRM(torch.nn.Module):
     # switch DR_DLRM_FUSE_HEAD=0 = autocast Linear)
     fuse_head = os.environ.get("DR_DLRM_FUSE_HEAD", "1") != "0"
 
+    def _stack(self, x0, ids):
+        if self.engine is None:
+            return self.lookup.stack(x0, ids)                      # [B, 1+T, D], no concat copy
+        if self._sh_anchor is None:
+            self._sh_anchor = torch.zeros(1, device=x0.device, requires_grad=True)
+        emb = _ShardedLookupFn.apply(self._sh_anchor, self.engine, ids)
+        B = x0.shape[0]
+        return torch.cat([x0.float().unsqueeze(1), emb.view(B, self.T, self.dim)], 1)
+
     def forward(self, dense, ids):
         x0 = self.bf16(self.bottom, dense)
-        X = self.lookup.stack(x0, ids)                             # [B, 1+T, D], no concat copy
+        X = self._stack(x0, ids)
         if (self.fuse_dot_concat and self.bf16.on and isinstance(self.top, _MfmaMLP)
                 and self.top.mfma_ok(X.shape[0]) and X.shape[1] <= 32
                 and X.shape[2] in (16, 32, 64, 128)):
@@ -861,6 +900,52 @@ def din_train_step(model, batch, dense_opt, ev_opt, global_step=None):
     loss.backward()
     dense_opt.step()
     ev_opt.apply_gradients(model.evs, global_step=global_step)
+    return loss
+
+
+def allreduce_dense_grads(params, group=None, staged=False):
+    """Sum the dense gradients over the ranks in one bucket per dtype (the
+    data-parallel all-reduce; RCCL over xGMI, or host-staged over gloo for a
+    rehearsal of several ranks on one GPU)."""
+    import torch.distributed as dist
+    by = {}
+    for p in params:
+        if p.grad is not None:
+            by.setdefault(p.grad.dtype, []).append(p.grad)
+    for grads in by.values():
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        if staged:
+            h = flat.cpu()
+            dist.all_reduce(h, group=group)
+            flat.copy_(h)
+        else:
+            dist.all_reduce(flat, group=group)
+        off = 0
+        for g in grads:
+            n = g.numel()
+            g.copy_(flat[off:off + n].view_as(g))
+            off += n
+
+
+def train_step_sharded(model, dense, ids, labels, dense_opt, ev_opt, world, group=None,
+                       staged=False, global_step=None):
+    """One data-parallel step of a model whose embeddings are row-sharded
+    (DLRM(engine=...)): every rank's loss is its local mean / world, so the
+    dense gradients summed by allreduce_dense_grads and the sparse gradient
+    rows each owner receives from every rank both come to the gradient of
+    the global-batch mean; then the dense optimizer (identical on every
+    rank) and the KV optimizer on this rank's EV shards.  Returns the local
+    mean loss."""
+    pred = model(dense, ids)
+    eps = 1e-7
+    p = pred.clamp(eps, 1 - eps)
+    loss = -(labels * torch.log(p) + (1 - labels) * torch.log(1 - p)).mean()
+    dense_opt.zero_grad(set_to_none=True)
+    (loss / world).backward()
+    if world > 1:
+        allreduce_dense_grads(list(model.parameters()), group=group, staged=staged)
+    dense_opt.step()
+    ev_opt.apply_gradients(list(model.evs), global_step=global_step)
     return loss
 
 

@@ -8,7 +8,8 @@ bit on steps 0-3 before timing, and on the last timed step plus two more
 after it -- each output consumed by the next step's reads, as in a model
 step -- and the sampled headline rows equal the synthetic tables' rows.
 The rehearsal also runs the N > 1 training step (sharded forward + backward
-to the owners + owner SGD) and the hybrid-placement Criteo-TB leg (large
+to the owners + owner SGD), the data-parallel DLRM model step (dense
+gradients all-reduced) and the hybrid-placement Criteo-TB leg (large
 vocabularies capped for time).  Never a reported number: the timing of
 staged steps means nothing."""
 import json
@@ -32,7 +33,7 @@ def test_bench_two_rank_rehearsal(engine):
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
            "--rows", "200000", "--batch", "8192", "--tables", "8", "--cpu-seconds", "0",
            "--check-rows", "4096", "--engine", engine.split("-")[0], "--train-steps", "3",
-           "--hybrid-cap", "1000000"]
+           "--hybrid-cap", "1000000", "--model-steps", "3"]
     if engine == "xgmi-dedup":
         cmd += ["--dedup", "--zipf", "1.05"]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
@@ -50,6 +51,9 @@ def test_bench_two_rank_rehearsal(engine):
         assert cfg["engine"] == "RCCL all-to-all", cfg
     # the N > 1 training step (sharded forward + backward + owner SGD) ran
     assert line["train_step"]["engine"] == cfg["engine"] and line["train_step"]["steps"] == 3
+    # the data-parallel DLRM model step with the sharded lookup
+    dl = line["dlrm_train_step"]
+    assert dl["global_batch"] == 2 * 8192 and dl["steps"] == 3 and dl["engine"] == cfg["engine"]
     # the hybrid-placement leg: replicated small features + sharded large
     # ones, sampled rows bit-exact and (xgmi) equal to the all-to-all engine
     hy = line["criteo_tb_hybrid"]

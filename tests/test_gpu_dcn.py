@@ -91,7 +91,7 @@ def test_crossnet_backward_elem_matches_torch(B, d):
     assert torch.equal(acc2, (g.float() * lin.float()))
 
 
-@pytest.mark.parametrize("B,d", [(300, 192), (1000, 3392), (64, 64), (513, 448)])
+@pytest.mark.parametrize("B,d", [(300, 192), (1000, 3392), (64, 64), (513, 448), (9472, 3392)])
 def test_crossnet_dx_matches_torch(B, d):
     """dr_crossnet_dx_bf16 (dx = u W + g on the 256^2 MFMA schedule, W^T as
     the B operand) against the fp32 torch product from the same bf16
@@ -194,7 +194,7 @@ def _rows(ev, R):
     return out
 
 
-@pytest.mark.parametrize("B,d", [(4096, 3392), (1000, 512)])
+@pytest.mark.parametrize("B,d", [(4096, 3392), (1000, 512), (9472, 3392)])
 def test_crossnet_large_tile_repeatable(B, d):
     """The 256 x 256 glds kernel at the DCN width over many full and partial
     tiles: within bf16 tolerance of torch, and bit-identical over repeated

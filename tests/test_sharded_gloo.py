@@ -364,3 +364,73 @@ def test_hybrid_placement_gloo(world):
         mp.spawn(_hybrid_worker, args=(world, _free_port(), d), nprocs=world, join=True)
         for r in range(world):
             assert os.path.exists(os.path.join(d, "ok%d" % r))
+
+
+class _TinyDense(torch.nn.Module):
+    """A dense-only stand-in for the model side of train_step_sharded (no
+    EVs: the sharded embedding half is the GPU test
+    tests/test_gpu_dlrm_sharded.py)."""
+
+    def __init__(self):
+        super().__init__()
+        self.evs = []
+        self.l1 = torch.nn.Linear(13, 8)
+        self.l2 = torch.nn.Linear(8, 1)
+
+    def forward(self, dense, ids):
+        return torch.sigmoid(self.l2(torch.relu(self.l1(dense)))).squeeze(1)
+
+
+class _NoKv(object):
+    def apply_gradients(self, evs, global_step=None):
+        assert not evs
+
+
+def _dp_batch():
+    g = torch.Generator().manual_seed(5)
+    return torch.randn(4 * 32, 13, generator=g), (torch.rand(4 * 32, generator=g) > 0.5).float()
+
+
+def _dp_worker(rank, world, port, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "deeprec-1_amd"))
+    from deeprec_amd import modelzoo as mz
+    torch.manual_seed(0)
+    model = _TinyDense()
+    opt = torch.optim.SGD(model.parameters(), lr=0.5)
+    dense, lab = _dp_batch()
+    n = dense.shape[0] // world
+    for _ in range(3):
+        mz.train_step_sharded(model, dense[rank * n:(rank + 1) * n], None,
+                              lab[rank * n:(rank + 1) * n], opt, _NoKv(), world)
+    torch.save({k: v.clone() for k, v in model.state_dict().items()},
+               os.path.join(outdir, "dp%d.pt" % rank))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_data_parallel_dense_step_gloo(world):
+    """train_step_sharded's dense half (loss / world, gradient all-reduce,
+    identical optimizer step on every rank) over gloo equals one process
+    training on the whole global batch (fp32 summation order aside)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "deeprec-1_amd"))
+    from deeprec_amd import modelzoo as mz
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_dp_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        got = [torch.load(os.path.join(d, "dp%d.pt" % r), weights_only=True) for r in range(world)]
+    torch.manual_seed(0)
+    ref = _TinyDense()
+    opt = torch.optim.SGD(ref.parameters(), lr=0.5)
+    dense, lab = _dp_batch()
+    for _ in range(3):
+        mz.train_step(ref, dense, None, lab, opt, _NoKv())
+    for r in range(world):
+        for k, v in ref.state_dict().items():
+            assert torch.equal(got[r][k], got[0][k]), (r, k)        # replicas stay identical
+            assert (got[r][k] - v).abs().max().item() <= 1e-6 * (v.abs().max().item() + 1), k
