@@ -1155,19 +1155,11 @@ __device__ __forceinline__ void c8_stage(const uint16_t* __restrict__ X, int64_t
 // MODE 2: the layer's input gradient, out = xl W^T + x0 -- called with A = u,
 // W = the transposed weight and x0 = g, it is dx_l = u W + g (no bias);
 // MODE 0: the loop alone (timing build, no outputs).
-// nsplit > 0 (desynchronised epilogues): the grid is the nfull tiles plus
-// nsplit blocks.  nsplit of the first 256 blocks (blockIdx < 256 with bit 3
-// set: every other group of 8, i.e. half the CUs of every XCD) take only the
-// top 128 rows of their tile, and blocks nfull.. take the bottom halves at
-// the end.  With one block per CU, those CUs start their second tile half a
-// tile earlier than the others and stay half a tile apart: the epilogues'
-// HBM bursts (x0 / xl in, out / lin out) of the two halves of the chip no
-// longer coincide and overlap the other half's MFMA loop.
 template <int MODE, int GM, bool PIPE>
 __global__ __launch_bounds__(512, 1) void crossnet_8ph_kernel(
     const uint16_t* __restrict__ x0, const uint16_t* __restrict__ xl,
     const uint16_t* __restrict__ W, const float* __restrict__ bias, int64_t M, int d,
-    int ncols, uint16_t* __restrict__ out, uint16_t* __restrict__ lin_out, int nsplit = 0) {
+    int ncols, uint16_t* __restrict__ out, uint16_t* __restrict__ lin_out) {
   // output columns [0, ncols) (ncols <= d; K and the row stride are d)
   __shared__ __attribute__((aligned(1024))) char lds[2 * C8_BUF];  // 128 KB
   const int tid = threadIdx.x;
@@ -1175,19 +1167,8 @@ __global__ __launch_bounds__(512, 1) void crossnet_8ph_kernel(
   const int wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
   const bool g1 = wr != 0;
-  const int64_t nwg = (int64_t)gridDim.x - nsplit;   // the tiles
-  int64_t orig = blockIdx.x;
-  int half = -1;   // -1: whole tile, 0: its top 128 rows, 1: its bottom 128
-  if (nsplit > 0) {
-    if (orig >= nwg) {
-      const int64_t k = orig - nwg;
-      orig = 16 * (k / 8) + 8 + (k % 8);
-      half = 1;
-    } else if (orig < 256 && ((orig >> 3) & 1) && 8 * (orig / 16) + (orig % 8) < nsplit) {
-      half = 0;
-    }
-  }
-  const bool idle = half >= 0 && g1;   // wave group 1 has no rows in a half tile
+  const int64_t nwg = (int64_t)gridDim.x;
+  const int64_t orig = blockIdx.x;
   const int64_t xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
   const int64_t tile = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
   const int ntn = ncols / 256 + (ncols % 256 ? 1 : 0);
@@ -1203,7 +1184,6 @@ __global__ __launch_bounds__(512, 1) void crossnet_8ph_kernel(
     m0 = (g * GM + idx % rows) * 256;
     n0 = (int)(idx / rows) * 256;
   }
-  if (half == 1) m0 += 128;
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -1247,16 +1227,14 @@ __global__ __launch_bounds__(512, 1) void crossnet_8ph_kernel(
   };
   auto mma = [&](int mi, bf16x8 (&fb)[2][2], int nj) {
     __builtin_amdgcn_s_setprio(1);
-    if (!idle) {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[mi + i][nj + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                fa[i][kk], fb[j][kk], acc[mi + i][nj + j], 0, 0, 0);
-    }
+        for (int j = 0; j < 2; ++j)
+          acc[mi + i][nj + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb[j][kk], acc[mi + i][nj + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -1370,7 +1348,7 @@ __global__ __launch_bounds__(512, 1) void crossnet_8ph_kernel(
           ov[e] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
         }
       }
-      if (grow < M && col_ok && !idle) {
+      if (grow < M && col_ok) {
         const int64_t o = grow * d + gcol;
         *reinterpret_cast<u32x4*>(out + o) = ov;
         if (MODE == 1 && lin_out) *reinterpret_cast<u32x4*>(lin_out + o) = lv;
@@ -1701,11 +1679,16 @@ int dr_crossnet_forward_bf16(const uint16_t* x0, const uint16_t* xl, const uint1
   const bool al16 = (((uintptr_t)bias | (uintptr_t)out | (uintptr_t)lin_out) & 15) == 0;
   // 8 = crossnet_8ph_kernel (default); the others are kept for A/B runs
   // (tools/gpu_crossnet_v.sh): 5 stag, 4 256^2, 3 glds3, 6/9/10 8ph with other
-  // tile orders / epilogue, 7 the 8ph loop alone (no outputs: timing only),
-  // 13 8ph with desynchronised epilogues
+  // tile orders / epilogue, 7 the 8ph loop alone (no outputs: timing only).
+  // (Round 4, removed: 13, desynchronised epilogues -- half the CUs starting
+  // with a half tile so the two halves' epilogue bursts alternate --
+  // measured 3-5 % slower, profiles/r04_crossnet_desync_ab.log; a one-wave-
+  // per-SIMD 128 x 128-per-wave form did not compile to a usable loop: with
+  // 256 accumulators the register allocator rotated them through VGPRs,
+  // ~440 accvgpr moves per 128 MFMAs.)
   static const int variant = getenv("DR_CROSSNET_VARIANT") ? atoi(getenv("DR_CROSSNET_VARIANT"))
                                                            : 8;
-  if (d % 64 == 0 && !legacy && al16 && (variant >= 6 && variant <= 13)) {
+  if (d % 64 == 0 && !legacy && al16 && (variant >= 6 && variant <= 12)) {
     // variant 12 (A/B only): the 8-phase kernel covers the whole 256-column
     // tiles and the 128 x 128 glds kernel the d % 256 strip, instead of one
     // ragged 256-column tile -- measured 1.43 vs 1.42 ms at d = 3392, i.e. no
@@ -1714,17 +1697,14 @@ int dr_crossnet_forward_bf16(const uint16_t* x0, const uint16_t* xl, const uint1
     const int ncols = split ? d - d % 256 : d;
     const int64_t tiles = ceil_div(batch, 256) * ceil_div(ncols, 256);
     DR_REQUIRE(tiles < (1ll << 31), DR_INVALID_ARGUMENT, "batch too large");
-    // variant 13 (A/B): desynchronised epilogues (crossnet_8ph_kernel nsplit)
-    const int nsplit = variant == 13 && tiles >= 512 ? 128 : 0;
 #define DR_C8(E, G, P)                                                                     \
-  hipLaunchKernelGGL((crossnet_8ph_kernel<E, G, P>), dim3((unsigned)(tiles + nsplit)),      \
-                     dim3(512), 0, S(stream), x0, xl, W, bias, batch, d, ncols, out, lin_out, \
-                     nsplit)
+  hipLaunchKernelGGL((crossnet_8ph_kernel<E, G, P>), dim3((unsigned)tiles), dim3(512), 0,   \
+                     S(stream), x0, xl, W, bias, batch, d, ncols, out, lin_out)
     if (variant == 6) DR_C8(1, 1, false);
     else if (variant == 8) DR_C8(1, 4, false);
     else if (variant == 9) DR_C8(1, 8, false);
     else if (variant == 10) DR_C8(1, 4, true);
-    else if (variant == 11 || variant == 12 || variant == 13) DR_C8(1, 4, false);
+    else if (variant == 11 || variant == 12) DR_C8(1, 4, false);
     else DR_C8(0, 4, false);  // 7: loop-only timing build (no outputs; measurement only)
 #undef DR_C8
     if (split) {
@@ -1788,12 +1768,9 @@ int dr_crossnet_dx_bf16(const uint16_t* u, const uint16_t* wt, const uint16_t* g
   const int64_t tiles = ceil_div(batch, 256) * ceil_div(d, 256);
   DR_REQUIRE(tiles < (1ll << 31), DR_INVALID_ARGUMENT, "batch too large");
   // the forward's 256^2 schedule with A = u, B = W^T and the addend g
-  static const int variant = getenv("DR_CROSSNET_VARIANT") ? atoi(getenv("DR_CROSSNET_VARIANT"))
-                                                           : 8;
-  const int nsplit = variant == 13 && tiles >= 512 ? 128 : 0;
-  hipLaunchKernelGGL((crossnet_8ph_kernel<2, 4, false>), dim3((unsigned)(tiles + nsplit)),
-                     dim3(512), 0, S(stream), g, u, wt, (const float*)nullptr, batch, d, d, dx,
-                     (uint16_t*)nullptr, nsplit);
+  hipLaunchKernelGGL((crossnet_8ph_kernel<2, 4, false>), dim3((unsigned)tiles), dim3(512), 0,
+                     S(stream), g, u, wt, (const float*)nullptr, batch, d, d, dx,
+                     (uint16_t*)nullptr);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }
