@@ -350,12 +350,18 @@ class DLRM(torch.nn.Module):
     of modelzoo/SOK/DLRM, trained with train_step_sharded."""
 
     def __init__(self, evs, num_dense=13, mlp_bot=(512, 256), mlp_top=(512, 256), bf16=False,
-                 engine=None):
+                 engine=None, replicated=()):
         super().__init__()
         self.bf16 = _MaybeBF16(bf16)
         self.engine = engine
         self._sh_anchor = None
         self.evs = list(evs)
+        # hybrid placement: features in `replicated` hold their whole table on
+        # every rank (looked up locally, gradients synchronised by
+        # train_step_sharded); the engine covers the others, in feature order
+        self.replicated = sorted(replicated)
+        self.replicated_evs = [self.evs[t] for t in self.replicated]
+        self._rep_lookup = _OneHotLookup(self.replicated_evs) if self.replicated else None
         self.dim = self.evs[0].dim
         self.T = len(self.evs)
         # the bottom MLP ends at the embedding dim so it stacks with the
@@ -381,9 +387,20 @@ class DLRM(torch.nn.Module):
             return self.lookup.stack(x0, ids)                      # [B, 1+T, D], no concat copy
         if self._sh_anchor is None:
             self._sh_anchor = torch.zeros(1, device=x0.device, requires_grad=True)
-        emb = _ShardedLookupFn.apply(self._sh_anchor, self.engine, ids)
         B = x0.shape[0]
-        return torch.cat([x0.float().unsqueeze(1), emb.view(B, self.T, self.dim)], 1)
+        if not self.replicated:
+            emb = _ShardedLookupFn.apply(self._sh_anchor, self.engine, ids)
+            return torch.cat([x0.float().unsqueeze(1), emb.view(B, self.T, self.dim)], 1)
+        rep = self.replicated
+        sh = [t for t in range(self.T) if t not in rep]
+        er = self._rep_lookup(ids[rep]).view(B, len(rep), self.dim)
+        es = _ShardedLookupFn.apply(self._sh_anchor, self.engine,
+                                    ids[sh].contiguous()).view(B, len(sh), self.dim)
+        X = x0.new_empty((B, 1 + self.T, self.dim), dtype=torch.float32)
+        X = X.index_copy(1, torch.zeros(1, dtype=torch.int64, device=X.device),
+                         x0.float().unsqueeze(1))
+        X = X.index_copy(1, torch.tensor([1 + t for t in rep], device=X.device), er)
+        return X.index_copy(1, torch.tensor([1 + t for t in sh], device=X.device), es)
 
     def forward(self, dense, ids):
         x0 = self.bf16(self.bottom, dense)
@@ -944,6 +961,10 @@ def train_step_sharded(model, dense, ids, labels, dense_opt, ev_opt, world, grou
     (loss / world).backward()
     if world > 1:
         allreduce_dense_grads(list(model.parameters()), group=group, staged=staged)
+        rep = list(getattr(model, "replicated_evs", []))
+        if rep:
+            from .sharded import sync_replicated_grads
+            sync_replicated_grads(rep, group=group, staged=staged)
     dense_opt.step()
     ev_opt.apply_gradients(list(model.evs), global_step=global_step)
     return loss

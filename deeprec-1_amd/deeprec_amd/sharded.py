@@ -511,6 +511,50 @@ class HybridShardedLookup(object):
         return out_r, out_s
 
 
+def sync_replicated_grads(evs, group=None, staged=False):
+    """Data-parallel gradients of REPLICATED EVs (hybrid placement's small
+    features, every rank holding the whole table): each rank's pending
+    gradient slices of every EV are gathered and every rank queues the same
+    rank-order concatenation (Horovod's allgather of IndexedSlices, in rank
+    order), so the KV optimizer -- which deduplicates a slice by key in
+    position order -- applies identical updates to every replica.  staged:
+    the collectives on host copies (gloo rehearsal on one GPU).  One host
+    read of the slice sizes per EV (the gather is variable-sized)."""
+    from .kv_variable_ops import IndexedSlices
+    world = dist.get_world_size(group)
+    for ev in evs:
+        ks, vs = [], []
+        for sl in ev.pending_grads:
+            k, v = sl.indices, sl.values
+            if sl.num_valid is not None:
+                n = int(sl.num_valid.reshape(-1)[0].item())
+                k, v = k[:n], v[:n]
+            ks.append(k.reshape(-1).to(torch.int64))
+            vs.append(v.reshape(-1, ev.dim).to(torch.float32))
+        dev = ev.device
+        k = torch.cat(ks) if ks else torch.empty(0, dtype=torch.int64, device=dev)
+        v = torch.cat(vs) if vs else torch.empty((0, ev.dim), dtype=torch.float32, device=dev)
+        cdev = torch.device("cpu") if staged else k.device
+        n = torch.tensor([k.numel()], dtype=torch.int64, device=cdev)
+        sizes = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(sizes, n, group=group)
+        sizes = [int(x.item()) for x in sizes]
+        m = max(max(sizes), 1)
+        kp = torch.zeros(m, dtype=torch.int64, device=cdev)
+        vp = torch.zeros((m, ev.dim), dtype=torch.float32, device=cdev)
+        kp[:k.numel()] = k.to(cdev)
+        vp[:k.numel()] = v.to(cdev)
+        kall = [torch.empty_like(kp) for _ in range(world)]
+        vall = [torch.empty_like(vp) for _ in range(world)]
+        dist.all_gather(kall, kp, group=group)
+        dist.all_gather(vall, vp, group=group)
+        kc = torch.cat([kall[r][:sizes[r]] for r in range(world)]).to(dev)
+        vc = torch.cat([vall[r][:sizes[r]] for r in range(world)]).to(dev)
+        ev.pending_grads.clear()
+        if kc.numel():
+            ev.pending_grads.append(IndexedSlices(vc, kc, unique=False))
+
+
 class _ReduceScatterFn(torch.autograd.Function):
     """out[B, C] = sum over ranks of their partial[rank's bags]; backward =
     the all-gather of the gradient (every owner needs every rank's rows)."""

@@ -6,7 +6,10 @@ same DLRM with the full tables on the whole global batch
 (tools/dlrm_sharded_check.py): loss, dense weights and every owned EV row
 within fp32 tolerance (1e-5 relative) after each of three steps.  Engines:
 the RCCL all-to-all form (staged through gloo on one GPU) and the xGMI
-peer-write form (real HIP IPC mappings between the processes)."""
+peer-write form (real HIP IPC mappings between the processes); and hybrid
+placement (two features replicated on every rank, their gradient slices
+gathered by sharded.sync_replicated_grads, every replica equal to the
+reference table)."""
 import json
 import os
 import subprocess
@@ -18,13 +21,15 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("world,engine", [(2, "a2a"), (3, "a2a"), (2, "xgmi")])
-def test_dlrm_sharded_step_matches_one_process(world, engine):
+@pytest.mark.parametrize("world,engine,hybrid", [(2, "a2a", False), (3, "a2a", False),
+                                               (2, "xgmi", False), (2, "a2a", True),
+                                               (3, "xgmi", True)])
+def test_dlrm_sharded_step_matches_one_process(world, engine, hybrid):
     env = dict(os.environ)
     env["MASTER_ADDR"] = "127.0.0.1"
-    p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "dlrm_sharded_check.py"),
-                        "--world", str(world), "--engine", engine], cwd=ROOT, env=env,
-                       capture_output=True, text=True, timeout=170)
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "dlrm_sharded_check.py"),
+           "--world", str(world), "--engine", engine] + (["--hybrid"] if hybrid else [])
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
     lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-4000:]
     assert sorted(x["rank"] for x in lines) == list(range(world))

@@ -14,6 +14,9 @@ with the full tables training the same DLRM on the whole global batch
 (modelzoo.train_step, global mean loss).  After each step every rank checks
 its dense weights and its owned EV rows against the reference (fp32
 tolerance: the towers' GEMMs and the gradient sums associate differently).
+--hybrid: features 0 and 2 replicated on every rank (local lookups, their
+gradient slices gathered by sharded.sync_replicated_grads), 1 and 3 sharded;
+every replica must equal the reference's whole table.
 The parent prints one JSON line per rank (sent through a queue)."""
 import argparse
 import json
@@ -32,7 +35,7 @@ def _vals(t, keys):
     return (0.1 * np.cos(0.017 * k + 0.9 * t + 0.07 * np.arange(D)[None, :])).astype(np.float32)
 
 
-def worker(rank, world, port, engine_kind, q):
+def worker(rank, world, port, engine_kind, hybrid, q):
     import torch
     import torch.distributed as dist
     sys.path.insert(0, os.path.join(ROOT, "deeprec-1_amd"))
@@ -57,8 +60,17 @@ def worker(rank, world, port, engine_kind, q):
         return evs
 
     own = allk[allk % world == rank]
+    # hybrid: features 0 and 2 replicated (the whole table on every rank),
+    # 1 and 3 row-sharded
+    rep = [0, 2] if hybrid else []
     shard = evset("sh", own)
     full = evset("fu", allk)
+    if rep:
+        repl = evset("rp", allk)
+        model_evs = [repl[t] if t in rep else shard[t] for t in range(T)]
+        eng_evs = [shard[t] for t in range(T) if t not in rep]
+    else:
+        model_evs, eng_evs = shard, shard
 
     def staged_a2a(out, inp, out_splits=None, in_splits=None):
         o = torch.empty(out.shape, dtype=out.dtype)
@@ -70,18 +82,19 @@ def worker(rank, world, port, engine_kind, q):
         def barrier():
             torch.cuda.synchronize()
             dist.barrier()
-        engine = XgmiShardedLookup(shard, world, rank, B, dev, barrier=barrier)
+        engine = XgmiShardedLookup(eng_evs, world, rank, B, dev, barrier=barrier)
     else:
-        engine = ShardedLookup(shard, world, rank, B, dev)
+        engine = ShardedLookup(eng_evs, world, rank, B, dev)
         engine._a2a = staged_a2a
     torch.manual_seed(0)
-    model = mz.DLRM(shard, 13, mlp_bot=(64,), mlp_top=(64, 32), engine=engine).to(dev)
+    model = mz.DLRM(model_evs, 13, mlp_bot=(64,), mlp_top=(64, 32), engine=engine,
+                    replicated=rep).to(dev)
     torch.manual_seed(0)
     ref = mz.DLRM(full, 13, mlp_bot=(64,), mlp_top=(64, 32)).to(dev)
     opt = torch.optim.SGD(model.parameters(), lr=LR)
     ropt = torch.optim.SGD(ref.parameters(), lr=LR)
     ev_opt, rev_opt = dr.GradientDescentOptimizer(LR), dr.GradientDescentOptimizer(LR)
-    res = {"rank": rank, "world": world, "engine": engine_kind, "checks": []}
+    res = {"rank": rank, "world": world, "engine": engine_kind, "hybrid": bool(rep), "checks": []}
     ok = True
     for step in range(3):
         rng = np.random.default_rng(100 + step)           # the same global batch on every rank
@@ -108,11 +121,11 @@ def worker(rank, world, port, engine_kind, q):
         c_rows = True
         emax = 0.0
         for t in range(T):
-            k, v = shard[t].export()[:2]
+            k, v = model_evs[t].export()[:2]
             rk, rv = full[t].export()[:2]
             order = torch.argsort(k)
             k, v = k[order], v[order]
-            sel = (rk % world) == rank
+            sel = (rk % world) == rank if t not in rep else torch.ones_like(rk, dtype=torch.bool)
             rk, rv = rk[sel], rv[sel]
             ro = torch.argsort(rk)
             rk, rv = rk[ro], rv[ro]
@@ -139,6 +152,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=2)
     ap.add_argument("--engine", default="a2a", choices=["a2a", "xgmi"])
+    ap.add_argument("--hybrid", action="store_true",
+                    help="features 0 and 2 replicated, 1 and 3 sharded")
     args = ap.parse_args()
     import multiprocessing as mp
     import queue
@@ -148,7 +163,7 @@ def main():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=worker, args=(r, args.world, port, args.engine, q))
+    procs = [ctx.Process(target=worker, args=(r, args.world, port, args.engine, args.hybrid, q))
              for r in range(args.world)]
     for p in procs:
         p.start()
