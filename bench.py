@@ -52,6 +52,9 @@ def parse():
     p.add_argument("--kernel-iters", type=int, default=20)
     p.add_argument("--model-steps", type=int, default=10,
                    help="timed DLRM model training steps on the headline tables (0: skip)")
+    p.add_argument("--din-steps", type=int, default=10,
+                   help="timed DIN (configs[3]) data-parallel training steps (0: skip)")
+    p.add_argument("--din-batch", type=int, default=4096)
     p.add_argument("--no-deepfm", dest="deepfm", action="store_false",
                    help="skip the BASELINE configs[1] (DeepFM 26 x 1e7 x 64) leg at N=1")
     p.add_argument("--no-criteo", dest="criteo", action="store_false",
@@ -472,6 +475,75 @@ def criteo_hybrid_leg(args, dev, log, world, rank, dist, staged):
     log("criteo hybrid leg: %s" % json.dumps(res))
     if hasattr(engine, "close"):
         engine.close()
+    return res
+
+
+def din_leg(args, dev, log, world, rank, dist, staged):
+    """BASELINE configs[3]: DIN (modelzoo/DIN/script/model.py) at B_local =
+    4096, histories U[1, 100] padded to the batch max, dim 18, vocabularies
+    5e5 users / 4e5 items / 2e3 categories, Adam (dense and KV).  At N > 1
+    data parallel over replicated EVs (modelzoo.din_train_step(world=N):
+    dense gradients all-reduced, EV gradient slices gathered in rank order);
+    each rank its own batch.  Eager, barrier-bracketed, max over ranks."""
+    import deeprec_amd as dr
+    from deeprec_amd import modelzoo as mz
+    B, T, D = args.din_batch, 100, 18
+    R = (500_000, 400_000, 2_000)
+    evs = []
+    for i, r in enumerate(R):
+        ev = dr.EmbeddingVariable("din_b%d" % i, D, 0.0, capacity=r + (1 << 16), device=dev)
+        ev.insert_synthetic(0, r, seed=700 + i)
+        evs.append(ev)
+    torch.manual_seed(0)
+    model = mz.DIN(*evs).to(dev)
+    dopt = torch.optim.Adam(model.parameters(), lr=0.001)
+    eopt = dr.AdamOptimizer(0.001)
+    g = torch.Generator(device=dev)
+    g.manual_seed(2021 + 7919 * rank)
+    batches = []
+    for _ in range(4):
+        lens = torch.randint(1, T + 1, (B,), generator=g, device=dev)
+        Tb = int(lens.max())
+        mask = (torch.arange(Tb, device=dev)[None, :] < lens[:, None]).float()
+        mh = torch.randint(1, R[1], (B, Tb), generator=g, device=dev) * mask.long()
+        ch = torch.randint(1, R[2], (B, Tb), generator=g, device=dev) * mask.long()
+        lab = (torch.rand(B, generator=g, device=dev) > 0.5).long()
+        batches.append((torch.randint(0, R[0], (B,), generator=g, device=dev),
+                        torch.randint(0, R[1], (B,), generator=g, device=dev),
+                        torch.randint(0, R[2], (B,), generator=g, device=dev), mh, ch, mask,
+                        torch.stack([lab, 1 - lab], 1).float()))
+
+    def dstep(i):
+        return mz.din_train_step(model, batches[i % 4], dopt, eopt, i, world=world,
+                                 staged=staged)
+
+    for i in range(2):
+        dstep(i)
+    torch.cuda.synchronize()
+    dr.status_check(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.din_steps):
+        dstep(i)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        te = torch.tensor([el], dtype=torch.float64, device="cpu" if staged else dev)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        el = float(te.item())
+    dr.status_check(dev)
+    ms = el / args.din_steps * 1e3
+    res = {"workload": "BASELINE configs[3] DIN: B_local=%d, histories U[1, %d], dim %d, vocab "
+                       "%s, Adam; %s" % (B, T, D, list(R), "data parallel over replicated EVs "
+                                         "(dense all-reduce + EV gradient slices gathered)"
+                                         if world > 1 else "one GPU"),
+           "n_gpus": world, "ms_per_step": round(ms, 4), "global_batch": world * B,
+           "samples_per_s": round(world * B / (ms * 1e-3), 1), "steps": args.din_steps}
+    log("din leg: %s" % json.dumps(res))
     return res
 
 
@@ -1090,6 +1162,9 @@ def main():
                              " shards" if sharded_model else "s")}
         log("dlrm model step: %s" % json.dumps(dlrm))
         model = dopt = eopt = mdense = mlab = None
+    din = None
+    if args.din_steps > 0:
+        din = din_leg(args, dev, log, world, rank, dist, staged)
 
     # ---- dominant kernel: the fused one-hot EV lookup, timed alone --------
     # dr_ev_lookup_onehot on keys this rank owns (all keys at N=1), over the
@@ -1239,6 +1314,7 @@ def main():
             "forward_samples_per_s": round(value / T, 1),
             "train_step": train,
             "dlrm_train_step": dlrm,
+            "din_config": din,
             "deepfm_config": deepfm,
             "criteo_tb_cardinalities": criteo,
             "criteo_tb_hybrid": hybrid,

@@ -907,14 +907,26 @@ class DIN(torch.nn.Module):
         return torch.softmax(self.dnn3(x), -1) + 1e-8
 
 
-def din_train_step(model, batch, dense_opt, ev_opt, global_step=None):
+def din_train_step(model, batch, dense_opt, ev_opt, global_step=None, world=1, group=None,
+                   staged=False):
     """One DIN step: ctr_loss = -mean(log(y_hat) * target) (model.py:137),
-    backward, dense optimizer, KV optimizer on the uid / mid / cat EVs."""
+    backward, dense optimizer, KV optimizer on the uid / mid / cat EVs.
+    world > 1: data parallel over replicated EVs (DIN's tables are small:
+    every rank holds them whole) -- local loss / world, dense gradients
+    all-reduced, every EV's gradient slices gathered in rank order
+    (sharded.sync_replicated_grads), so every replica takes the same update
+    (BASELINE configs[3], 1 -> 8 GPUs)."""
     uids, mids, cats, mid_his, cat_his, mask, target = batch
     y_hat = model(uids, mids, cats, mid_his, cat_his, mask)
     loss = -(torch.log(y_hat) * target).mean()
     dense_opt.zero_grad(set_to_none=True)
-    loss.backward()
+    if world > 1:
+        (loss / world).backward()
+        allreduce_dense_grads(list(model.parameters()), group=group, staged=staged)
+        from .sharded import sync_replicated_grads
+        sync_replicated_grads(list(model.evs), group=group, staged=staged)
+    else:
+        loss.backward()
     dense_opt.step()
     ev_opt.apply_gradients(model.evs, global_step=global_step)
     return loss

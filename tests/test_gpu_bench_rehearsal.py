@@ -33,7 +33,8 @@ def test_bench_two_rank_rehearsal(engine):
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
            "--rows", "200000", "--batch", "8192", "--tables", "8", "--cpu-seconds", "0",
            "--check-rows", "4096", "--engine", engine.split("-")[0], "--train-steps", "3",
-           "--hybrid-cap", "1000000", "--model-steps", "3"]
+           "--hybrid-cap", "1000000", "--model-steps", "3", "--din-steps", "3",
+           "--din-batch", "1024"]
     if engine == "xgmi-dedup":
         cmd += ["--dedup", "--zipf", "1.05"]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
@@ -54,6 +55,8 @@ def test_bench_two_rank_rehearsal(engine):
     # the data-parallel DLRM model step with the sharded lookup
     dl = line["dlrm_train_step"]
     assert dl["global_batch"] == 2 * 8192 and dl["steps"] == 3 and dl["engine"] == cfg["engine"]
+    # the data-parallel DIN leg (replicated EVs)
+    assert line["din_config"]["n_gpus"] == 2 and line["din_config"]["global_batch"] == 2048
     # the hybrid-placement leg: replicated small features + sharded large
     # ones, sampled rows bit-exact and (xgmi) equal to the all-to-all engine
     hy = line["criteo_tb_hybrid"]
