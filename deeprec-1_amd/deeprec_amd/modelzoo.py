@@ -757,9 +757,13 @@ class DCNv2(torch.nn.Module):
     the output layer riding on the tower node (bf16 weight, rounded logit:
     what autocast's Linear computes), when the batch is a multiple of 512."""
 
-    def __init__(self, evs, num_dense=13, layers=3, deep=(1024, 512), bf16=False):
+    def __init__(self, evs, num_dense=13, layers=3, deep=(1024, 512), bf16=False, engine=None):
         super().__init__()
         self.mfma_deep = bool(bf16)
+        # engine: a row-sharded lookup over this rank's EV shards (BASELINE
+        # configs[4] on 8 GPUs; train with train_step_sharded)
+        self.engine = engine
+        self._sh_anchor = None
         self.evs = list(evs)
         self.dim = self.evs[0].dim
         self.T = len(self.evs)
@@ -781,7 +785,12 @@ class DCNv2(torch.nn.Module):
 
     def forward(self, dense, ids):
         B = dense.shape[0]
-        emb = self.lookup(ids)                                     # [B, T*D] fp32
+        if self.engine is None:
+            emb = self.lookup(ids)                                 # [B, T*D] fp32
+        else:
+            if self._sh_anchor is None:
+                self._sh_anchor = torch.zeros(1, device=dense.device, requires_grad=True)
+            emb = _ShardedLookupFn.apply(self._sh_anchor, self.engine, ids)
         if self.mfma_deep:
             # x0 cast column block by column block into one bf16 buffer (no
             # fp32 [B, dp] concat in between); the slice copies keep autograd
