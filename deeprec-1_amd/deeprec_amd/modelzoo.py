@@ -330,8 +330,9 @@ class _ShardedLookupFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, anchor, engine, ids):
+        from .sharded import XgmiShardedLookup
         ctx.engine = engine
-        if hasattr(engine, "bufs"):            # XgmiShardedLookup: always ready for backward
+        if isinstance(engine, XgmiShardedLookup):   # keeps its inbox for the backward
             out = engine.forward(ids)
         else:
             out = engine.forward(ids, need_grad=True)
@@ -393,14 +394,19 @@ class DLRM(torch.nn.Module):
             return torch.cat([x0.float().unsqueeze(1), emb.view(B, self.T, self.dim)], 1)
         rep = self.replicated
         sh = [t for t in range(self.T) if t not in rep]
-        er = self._rep_lookup(ids[rep]).view(B, len(rep), self.dim)
+        key = x0.device
+        if getattr(self, "_hyb_idx", (None,))[0] != key:
+            mk = lambda v: torch.tensor(v, dtype=torch.int64, device=key)  # noqa: E731
+            self._hyb_idx = (key, mk(rep), mk(sh), mk([0]), mk([1 + t for t in rep]),
+                             mk([1 + t for t in sh]))
+        _, irep, ish, i0, xrep, xsh = self._hyb_idx
+        er = self._rep_lookup(ids.index_select(0, irep)).view(B, len(rep), self.dim)
         es = _ShardedLookupFn.apply(self._sh_anchor, self.engine,
-                                    ids[sh].contiguous()).view(B, len(sh), self.dim)
+                                    ids.index_select(0, ish)).view(B, len(sh), self.dim)
         X = x0.new_empty((B, 1 + self.T, self.dim), dtype=torch.float32)
-        X = X.index_copy(1, torch.zeros(1, dtype=torch.int64, device=X.device),
-                         x0.float().unsqueeze(1))
-        X = X.index_copy(1, torch.tensor([1 + t for t in rep], device=X.device), er)
-        return X.index_copy(1, torch.tensor([1 + t for t in sh], device=X.device), es)
+        X = X.index_copy(1, i0, x0.float().unsqueeze(1))
+        X = X.index_copy(1, xrep, er)
+        return X.index_copy(1, xsh, es)
 
     def forward(self, dense, ids):
         x0 = self.bf16(self.bottom, dense)
