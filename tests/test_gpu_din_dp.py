@@ -1,7 +1,8 @@
 """Data-parallel DIN (BASELINE configs[3], 1 -> N GPUs): replicated EVs,
 dense gradients all-reduced, EV gradient slices gathered in rank order
 (modelzoo.din_train_step(world=N)), 2 and 3 processes on one GPU against one
-process training on the whole global batch (tools/din_dp_check.py): loss,
+process running the same step over every rank's slice (tools/din_dp_check.py;
+Dice normalises over a replica's batch, so each slice's forward is its own): loss,
 dense weights and all three tables within 1e-5 relative after each of three
 steps, replicas bit-identical across ranks."""
 import json

@@ -8,7 +8,9 @@ initialisation and its slice of one global batch (each slice padded to the
 same history length).  A step is modelzoo.din_train_step(..., world=N):
 local loss / N, dense gradients all-reduced, every EV's gradient slices
 gathered in rank order (sharded.sync_replicated_grads), SGD + KV SGD.
-Reference: one process training the same model on the whole global batch.
+Reference: one process running the same data-parallel step (every slice's
+forward on its own -- DIN's Dice normalises over the batch a replica sees --
+gradients of all slices accumulated, one optimizer step).
 After each of three steps every rank checks its loss share, dense weights
 and all three tables against the reference (1e-5 relative), and the
 replicas against each other (bit-identical).  The parent prints one JSON
@@ -75,8 +77,24 @@ def worker(rank, world, port, q):
         sl = slice(rank * B, (rank + 1) * B)
         loss = mz.din_train_step(model, [x[sl].contiguous() for x in tg], opt, eo, step,
                                  world=world, staged=True)
-        rloss = mz.din_train_step(ref, tg, ropt, reo, step)
-        lt = torch.tensor([float(loss)], dtype=torch.float64)
+        # reference: the same data-parallel step in one process -- DIN's
+        # Dice activations normalise over the batch a replica sees, so each
+        # slice's forward is its own; the slices' gradients accumulate
+        # (dense: autograd sums, EVs: slices queued in rank order) before one
+        # optimizer step
+        ropt.zero_grad(set_to_none=True)
+        rl = []
+        for r in range(world):
+            rs = slice(r * B, (r + 1) * B)
+            part = [x[rs].contiguous() for x in tg]
+            y = ref(*part[:6])
+            lr_ = -(torch.log(y) * part[6]).mean()
+            (lr_ / world).backward()
+            rl.append(float(lr_.detach()))
+        ropt.step()
+        reo.apply_gradients(ref.evs, global_step=step)
+        rloss = sum(rl) / world
+        lt = torch.tensor([float(loss.detach())], dtype=torch.float64)
         dist.all_reduce(lt)
         gl = lt.item() / world
         c_loss = abs(gl - float(rloss)) <= 1e-5 * abs(float(rloss)) + 1e-7
