@@ -1134,12 +1134,37 @@ def main():
             mstep(i)
         torch.cuda.synchronize()
         dr.status_check(dev)
+        # N = 1: NBATCH whole model steps (forward, backward, dense SGD, KV
+        # SGD) captured as one hipGraph, as the embedding training step; the
+        # eager loop if anything in the step refuses capture
+        mgraph = None
+        if not sharded_model and not args.no_graph:
+            try:
+                for ev in evs:
+                    ev.reserve(2 * NBATCH * B)
+                mgraph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(mgraph):
+                    for i in range(NBATCH):
+                        mstep(i)
+                mgraph.replay()
+                torch.cuda.synchronize()
+                dr.status_check(dev)
+            except Exception as e:  # noqa: BLE001
+                log("dlrm model step: graph capture failed (%s); eager" % str(e)[:200])
+                mgraph = None
+                torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
+        nsteps = args.model_steps
         t0 = time.perf_counter()
-        for i in range(args.model_steps):
-            mstep(i)
+        if mgraph is not None:
+            nsteps = -(-nsteps // NBATCH) * NBATCH
+            for i in range(0, nsteps, NBATCH):
+                mgraph.replay()
+        else:
+            for i in range(nsteps):
+                mstep(i)
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
@@ -1149,10 +1174,10 @@ def main():
             dist.all_reduce(te, op=dist.ReduceOp.MAX)
             mel = float(te.item())
         dr.status_check(dev)
-        mms = mel / args.model_steps * 1e3
+        mms = mel / nsteps * 1e3
         dlrm = {"ms_per_step": round(mms, 4),
                 "samples_per_s": round(world * B / (mms * 1e-3), 1),
-                "global_batch": world * B, "steps": args.model_steps,
+                "global_batch": world * B, "steps": nsteps, "graph": mgraph is not None,
                 "engine": engine_kind if sharded_model else "local",
                 "model": "modelzoo/DLRM/train.py DLRM, dot interaction, bf16 MFMA towers: bottom "
                          "[13, 512, 256, %d], top [%d, 512, 256] + 1-unit output, BCE; SGD on "
@@ -1161,7 +1186,7 @@ def main():
                              " (all-reduced gradients)" if sharded_model else "", T,
                              " shards" if sharded_model else "s")}
         log("dlrm model step: %s" % json.dumps(dlrm))
-        model = dopt = eopt = mdense = mlab = None
+        model = dopt = eopt = mdense = mlab = mgraph = None
     din = None
     if args.din_steps > 0:
         din = din_leg(args, dev, log, world, rank, dist, staged)
