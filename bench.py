@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--kernel-iters", type=int, default=20)
     p.add_argument("--model-steps", type=int, default=10,
                    help="timed DLRM model training steps on the headline tables (0: skip)")
+    p.add_argument("--model-graph", action="store_true",
+                   help="capture the N = 1 DLRM model steps as a hipGraph")
     p.add_argument("--din-steps", type=int, default=10,
                    help="timed DIN (configs[3]) data-parallel training steps (0: skip)")
     p.add_argument("--din-batch", type=int, default=4096)
@@ -1138,7 +1140,7 @@ def main():
         # SGD) captured as one hipGraph, as the embedding training step; the
         # eager loop if anything in the step refuses capture
         mgraph = None
-        if not sharded_model and not args.no_graph:
+        if not sharded_model and not args.no_graph and args.model_graph:
             try:
                 for ev in evs:
                     ev.reserve(2 * NBATCH * B)
