@@ -1191,7 +1191,11 @@ def main():
         model = dopt = eopt = mdense = mlab = mgraph = None
     din = None
     if args.din_steps > 0:
-        din = din_leg(args, dev, log, world, rank, dist, staged)
+        try:
+            din = din_leg(args, dev, log, world, rank, dist, staged)
+        except Exception as e:  # noqa: BLE001 -- an extra leg must not cost the headline line
+            log("din leg failed: %r" % (e,))
+            din = {"error": str(e)[:300]}
 
     # ---- dominant kernel: the fused one-hot EV lookup, timed alone --------
     # dr_ev_lookup_onehot on keys this rank owns (all keys at N=1), over the
