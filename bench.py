@@ -52,8 +52,8 @@ def parse():
     p.add_argument("--kernel-iters", type=int, default=20)
     p.add_argument("--model-steps", type=int, default=10,
                    help="timed DLRM model training steps on the headline tables (0: skip)")
-    p.add_argument("--model-graph", action="store_true",
-                   help="capture the N = 1 DLRM model steps as a hipGraph")
+    p.add_argument("--no-model-graph", dest="model_graph", action="store_false",
+                   help="run the N = 1 DLRM model steps eagerly (default: one hipGraph of 4)")
     p.add_argument("--din-steps", type=int, default=10,
                    help="timed DIN (configs[3]) data-parallel training steps (0: skip)")
     p.add_argument("--din-batch", type=int, default=4096)

@@ -9,7 +9,7 @@ rc=$?; tail -8 $O/tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err
 rc=$?; grep -E "dlrm model step|din leg|train step" $O/bench.err; tail -2 $O/bench.err; [ $rc -ne 0 ] && exit $rc
 S="bench.py --cpu-seconds 0 --no-deepfm --no-criteo --no-dcn --no-hybrid --din-steps 0 --train-steps 0 --model-steps 20"
-timeout -k 10 300 python -u $S --model-graph > $O/graph.json 2> $O/graph.err || { tail -5 $O/graph.err; exit 1; }
+timeout -k 10 300 python -u $S > $O/graph.json 2> $O/graph.err || { tail -5 $O/graph.err; exit 1; }
 grep "dlrm model step" $O/graph.err
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/dlrm_prof -o run -- python3 tools/model_step.py --model dlrm --bf16 --rows 2000000 > $O/dlrm_prof.log 2>&1 || { tail -5 $O/dlrm_prof.log; exit 1; }
