@@ -397,6 +397,42 @@ __global__ void gemm_splitk_reduce_kernel(const float* __restrict__ ws, int S, i
   }
 }
 
+// gemm_tn's two split reductions in ONE launch: threads [0, nq_c) sum the
+// dW partials (C = sum_z part[z], split order), threads [nq_c, nq_c + N/4)
+// the column-sum partials (colsum = sum_z csp[z]) -- one launch per layer
+// instead of two (a DLRM step runs five such layers).
+__global__ void gemm_tn_reduce_kernel(const float* __restrict__ part, int S, int64_t N,
+                                      int64_t K, float* __restrict__ C, int64_t ldc,
+                                      const float* __restrict__ csp, float* __restrict__ colsum,
+                                      int64_t nq_c) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const float* src;
+  float* dst;
+  int64_t stride;
+  if (q < nq_c) {
+    const int64_t kq = K / 4;
+    const int64_t n = q / kq, k = (q - n * kq) * 4;
+    src = part + n * K + k;
+    stride = N * K;
+    dst = C + n * ldc + k;
+  } else {
+    const int64_t c = (q - nq_c) * 4;
+    if (!colsum || c >= N) return;
+    src = csp + c;
+    stride = N;
+    dst = colsum + c;
+  }
+  float4 s = reinterpret_cast<const float4*>(src)[0];
+  for (int z = 1; z < S; ++z) {
+    const float4 p = reinterpret_cast<const float4*>(src + (int64_t)z * stride)[0];
+    s.x += p.x;
+    s.y += p.y;
+    s.z += p.z;
+    s.w += p.w;
+  }
+  *reinterpret_cast<float4*>(dst) = s;
+}
+
 // out[c][r] = in[r][c] (bf16), 64 x 64 tiles through LDS: each thread loads
 // two 16-B row vectors and stores two 16-B column vectors.
 __global__ __launch_bounds__(256) void transpose_bf16_kernel(const uint16_t* __restrict__ in,
@@ -829,16 +865,12 @@ int dr_gemm_tn_bf16(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t l
   hipLaunchKernelGGL(gemm_tn_kernel, dim3((unsigned)tiles, (unsigned)S_), dim3(256), 0, st, G, ldg,
                      X, ldx, N, K, bchunk, rows, part, direct ? ldc : K,
                      direct ? (int64_t)0 : N * K, csp);
-  if (!direct) {
-    const int64_t quads = N * (K / 4);
-    hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)ceil_div(quads, 256)), dim3(256),
-                       0, st, (const float*)part, S_, N, K, (const float*)nullptr, 0, (void*)C,
-                       ldc, 0);
-  }
-  if (colsum)   // N % 8 == 0
-    hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)ceil_div(N / 4, 256)), dim3(256),
-                       0, st, (const float*)csp, S_, (int64_t)1, N, (const float*)nullptr, 0,
-                       (void*)colsum, N, 0);
+  // (K % 8 == 0 and N % 8 == 0: whole float4 quads on both sides)
+  const int64_t nq_c = direct ? 0 : N * (K / 4);
+  const int64_t nq = nq_c + (colsum ? N / 4 : 0);
+  if (nq > 0)
+    hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st,
+                       (const float*)part, S_, N, K, C, ldc, (const float*)csp, colsum, nq_c);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }
