@@ -1239,15 +1239,6 @@ __global__ __launch_bounds__(512, 1) void crossnet_8ph_kernel(
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
-  // Epilogue operands warmed during the last K tiles: one dword per 128-B
-  // line of this wave's x0 (and xl) block is loaded -- 2 (MODE 2) or 4 lines
-  // per lane, one per K tile, issued after that tile's counted wait so the
-  // next wait retires them a tile later -- so the epilogue's reads find the
-  // lines in the caches instead of HBM while the MFMAs run.  The values are
-  // only "used" by an empty asm after the loop.
-  constexpr int NPF = MODE == 1 ? 4 : (MODE == 2 ? 2 : 0);
-  uint32_t pfv[4] = {0u, 0u, 0u, 0u};
-  const int pf_t0 = nk - 2 - NPF;   // tiles [pf_t0, nk - 2) still run the vmcnt(6) wait
   for (int t = 0; t < nk; ++t) {
     const bool pf1 = t + 1 < nk, pf2 = t + 2 < nk;
     // p1: m0n0
@@ -1270,15 +1261,6 @@ __global__ __launch_bounds__(512, 1) void crossnet_8ph_kernel(
     if (pf2) {
       st_b(t + 2, 1);
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // tile t+1 landed (this wave's DMAs)
-      if (NPF > 0 && t >= pf_t0) {
-        const int p = t - pf_t0;                     // 0 .. NPF-1
-        const uint16_t* src = (p >> 1) ? xl : x0;
-        int64_t row = m0 + wr * 128 + (p & 1) * 64 + lane;
-        if (row >= M) row = M - 1;
-        int col = n0 + wc * 64;
-        if (col >= ncols) col = 0;
-        pfv[p & 3] = *reinterpret_cast<const volatile uint32_t*>(src + row * d + col);
-      }
     } else if (pf1) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -1287,7 +1269,6 @@ __global__ __launch_bounds__(512, 1) void crossnet_8ph_kernel(
   }
   if (!g1) __builtin_amdgcn_s_barrier();  // matches group 1's extra barrier
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  if (NPF > 0) asm volatile("" ::"v"(pfv[0]), "v"(pfv[1]), "v"(pfv[2]), "v"(pfv[3]));
   __syncthreads();
   if (MODE == 0) {  // loop-only timing build: keep the MFMAs alive, store nothing
     float sum = 0.f;
