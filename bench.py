@@ -70,6 +70,8 @@ def parse():
     p.add_argument("--no-hybrid", dest="hybrid", action="store_false",
                    help="skip the real Criteo-TB cardinality leg with hybrid placement (small "
                         "features replicated, large ones row-sharded), run at every N")
+    p.add_argument("--native-steps", type=int, default=8,
+                   help="timed forward steps of the native C-ABI engine over RCCL (0: skip)")
     p.add_argument("--dedup", action="store_true",
                    help="xgmi engine: per-destination dedup before the exchange (grouped Unique, "
                         "unique keys routed, rows expanded locally)")
@@ -731,6 +733,97 @@ def deepfm_leg(args, dev, log):
     return res
 
 
+def exchange_phases(ph, batches, world, rank, T, D, dist, staged, dev):
+    """Per-step phase times of the peer-write engine (this rank and the max
+    over ranks) with its link traffic: rows this rank serves to remote
+    requesters (owner side, exact from every rank's id counts per owner),
+    rows it receives, and the achieved xGMI write rate of its serve phase."""
+    if ph is None:
+        return None
+    cnt = torch.zeros(world, dtype=torch.float64, device=dev)
+    for ids in batches:
+        cnt += torch.bincount((ids % world).reshape(-1), minlength=world).double()
+    cnt /= len(batches)                    # ids this rank sends to each owner per step
+    sent = cnt.clone()
+    sent[rank] = 0.0
+    tot = sent.cpu() if staged else sent.clone()
+    dist.all_reduce(tot)                   # tot[d]: remote ids owner d serves per step
+    row_bytes = D * 4
+    out_rows = float(tot[rank])
+    in_rows = float(sent.sum())
+    names = ("route", "wait_route", "serve", "wait_serve")
+    mx = torch.tensor([ph[k] for k in names], dtype=torch.float64,
+                      device="cpu" if staged else dev)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    res = {"ms_rank0" if rank == 0 else "ms_this_rank": {k: round(ph[k], 4) for k in names},
+           "ms_max_over_ranks": {k: round(float(mx[i]), 4) for i, k in enumerate(names)},
+           "steps": ph["steps"],
+           "remote_rows_served_per_step": int(round(out_rows)),
+           "remote_rows_received_per_step": int(round(in_rows)),
+           "link_bytes_out_per_step": int(round(out_rows * row_bytes)),
+           "xgmi_write_GBps_serve_phase": round(out_rows * row_bytes / (ph["serve"] * 1e-3) / 1e9, 1),
+           "xgmi_write_GBps_per_link": round(out_rows * row_bytes / max(world - 1, 1) /
+                                             (ph["serve"] * 1e-3) / 1e9, 1),
+           "note": "serve = owner insert-on-miss resolve + every row written to its requester "
+                   "over xGMI (the link-bound phase); wait_* = stream-ordered barrier (slowest "
+                   "peer + collective latency)"}
+    return res
+
+
+def native_rccl_leg(args, evs, batches, engine, a2a, local_step, world, rank, dist, staged, dev,
+                    log):
+    """NativeShardedLookup over Comm.rccl (the library's sharded C entries on
+    the RCCL transport; Comm.host_staged in a gloo rehearsal): output checked
+    bit for bit against the all-to-all engine (N > 1) or the local fused
+    lookup (N = 1), then timed forward-only."""
+    from deeprec_amd.sharded import Comm, NativeShardedLookup
+    T, B = args.tables, args.batch
+    comm = Comm.host_staged() if staged else Comm.rccl(rank, world)
+    eng = NativeShardedLookup(comm, evs, dev)
+    same = 1
+    with torch.no_grad():
+        for k in range(len(batches)):
+            got = eng.forward(batches[k], combiner="sum").clone()
+            ref = a2a.forward(batches[k]) if a2a is not None else local_step(k)
+            same &= int(torch.equal(got, ref))
+    if world > 1:
+        flag = torch.tensor([same], dtype=torch.int32, device="cpu" if staged else dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        same = int(flag.item())
+    n = args.native_steps
+    with torch.no_grad():
+        for k in range(2):
+            eng.forward(batches[k], combiner="sum")
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(n):
+            eng.forward(batches[i % len(batches)], combiner="sum")
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device="cpu" if staged else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    st = eng.stats()
+    eng.close()
+    comm.close()
+    res = {"transport": "gloo host-staged callback (rehearsal)" if staged else
+           "RCCL (dr_comm_init with an ncclUniqueId)",
+           "engine_check": "native C-ABI engine == %s, %d batches, all ranks: %s" % (
+               "all-to-all engine" if a2a is not None else "local fused lookup",
+               len(batches), bool(same)),
+           "ms_per_step": round(el / n * 1e3, 4), "steps": n,
+           "lookups_per_s": round(T * B * world * n / el, 1),
+           "sent_keys_last_step": st["sent_keys"], "recv_keys_last_step": st["recv_keys"],
+           "note": "forward only; reads the per-peer split sizes on the host once per step"}
+    log("native RCCL engine: %s" % json.dumps(res))
+    return res
+
+
 def main():
     args = parse()
     import deeprec_amd as dr
@@ -831,6 +924,7 @@ def main():
         keyspace = R
     batches = make_batches(4, T, B, keyspace, args.zipf, 2021 + 7919 * rank, dev)
     engine_check = None
+    phases = None
 
     def engines_agree(steps):
         """The peer-write engine must reproduce the all-to-all engine bit for
@@ -911,11 +1005,18 @@ def main():
                     log("step %d: done" % i)
                 i += 1
 
+        # N > 1 peer-write engine: HIP events between its phases during the
+        # timed steps (route / barrier / serve / barrier; phase_summary)
+        phase_engine = (engine if engine is not None and hasattr(engine, "phase_timing")
+                        and not getattr(engine, "dedup", False) and world > 1 else None)
+
         def timed():
             run_steps(0, args.warmup)
             if dist is not None:
                 dist.barrier()
             torch.cuda.synchronize()
+            if phase_engine is not None:
+                phase_engine.phase_timing(True)
             t0 = time.perf_counter()
             run_steps(0, args.steps)
             if dist is not None:
@@ -925,6 +1026,12 @@ def main():
 
         el = timed()
         log("timed %d steps in %.3fs" % (args.steps, el))
+        phases = None
+        if phase_engine is not None:
+            phases = exchange_phases(phase_engine.phase_summary(), batches, world, rank, T, D,
+                                     dist, staged, dev)
+            phase_engine.phase_timing(False)
+            log("exchange phases: %s" % json.dumps(phases))
         if engine is not None and engine is not a2a:
             # the last timed step's output (still in the engine's buffer),
             # then two more steps, against the all-to-all engine
@@ -949,6 +1056,17 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device="cpu" if staged else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    # the library's own sharded C entries (dr_sharded_forward over a dr_comm:
+    # RCCL, ncclUniqueId through torch.distributed; N = 1 too, where every
+    # all-to-all is the self block inside an RCCL group) beside the headline
+    native = None
+    if args.native_steps > 0:
+        try:
+            native = native_rccl_leg(args, evs, batches, engine, a2a if engine is not None else None,
+                                     step, world, rank, dist, staged, dev, log)
+        except Exception as e:  # noqa: BLE001 -- an extra leg must not cost the headline line
+            log("native RCCL leg failed: %r" % (e,))
+            native = {"error": str(e)[:300]}
     lookups = T * B * args.steps * world
     value = lookups / el
     ms = el / args.steps * 1e3
@@ -1263,9 +1381,14 @@ def main():
     per_lookup = 8 + 16 + D * 4 + D * 4
     bytes_launch = T * B * per_lookup
     achieved = bytes_launch / (k_ms * 1e-3) / 1e9
+    # which fused lookup kernel the library launches (DR_LOOKUP_KERNEL, ev.hip)
+    lk_kind = os.environ.get("DR_LOOKUP_KERNEL", "2")
+    lk_name = {"0": "ev_lookup_onehot_kernel", "1": "ev_lookup_line_kernel"}.get(
+        lk_kind, "ev_lookup_pipe_kernel")
+    lk_inst = {"0": "<4,32,1,ALI,4>"}.get(lk_kind, "<4,32,1,ALI>")
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
-            "kernel": "dr::ev_lookup_onehot_kernel<4,32,1,ALI,4> (record-major [B, T] ids)",
+            "kernel": "dr::%s%s (record-major [B, T] ids)" % (lk_name, lk_inst),
             "kernel_ms": round(k_ms, 4),
             "bytes_per_launch": bytes_launch, "bytes_per_lookup": per_lookup}
     import glob as _glob
@@ -1274,7 +1397,7 @@ def main():
         fs = sorted(_glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_" + suffix)))
         return fs[-1] if fs else None
 
-    for obj, fname, kname in ((roof, _latest("pmc_traffic.json"), "ev_lookup_onehot_kernel"),
+    for obj, fname, kname in ((roof, _latest("pmc_traffic.json"), lk_name),
                               (roof_gather, _latest("pmc_traffic_row_gather.json"),
                                "pool_onehot_kernel")):
         if fname:
@@ -1285,6 +1408,9 @@ def main():
                 if str(j.get("kernel", "")).startswith(kname):
                     obj["traffic"] = j.get("bytes_per_launch")
                     obj["traffic_source"] = os.path.relpath(fname, ROOT)
+                    # the profile's round and the instantiation it measured
+                    obj["traffic_round"] = os.path.basename(fname)[:3]
+                    obj["traffic_kernel"] = j.get("kernel")
             except Exception:
                 pass
 
@@ -1349,6 +1475,8 @@ def main():
             "deepfm_config": deepfm,
             "criteo_tb_cardinalities": criteo,
             "criteo_tb_hybrid": hybrid,
+            "exchange_phases": phases,
+            "native_rccl_engine": native,
             "dcn_bf16_config": dcn,
             "correctness": correctness,
             "roofline": roof,

@@ -193,6 +193,18 @@ static EvDesc make_desc(const dr_ev* ev) {
 }
 
 // ---- device helpers --------------------------------------------------------
+// Bucket-local linear probing.  The table is cut into 128-B lines of 8 slots;
+// the i-th probe of a key whose home slot is h0 visits line (h0 / 8 + i / 8)
+// at offset (h0 + i) % 8, i.e. a key's probe sequence wraps inside its home
+// line before it moves on.  At the tables' load (<= 3/4, 3/8 at the bench's
+// sizing) a key is found or ruled out inside its home line ~99.5 % of the
+// time, so one line-wide load of 8 lanes (ev_line_probe) settles a lookup in a
+// single memory round trip.  Every probe / insert / rehash uses this one
+// sequence (cap is a power of two >= 1024, so lines never straddle the end).
+__device__ __forceinline__ uint64_t probe_slot(uint64_t h0, uint64_t i, uint64_t mask) {
+  return (((h0 & ~7ull) + (i & ~7ull)) & mask) | ((h0 + i) & 7ull);
+}
+
 __device__ __forceinline__ uint64_t atomic_read_u64(uint64_t* p) {
   return __hip_atomic_fetch_or(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -218,13 +230,13 @@ __device__ Slot* ev_find(const EvDesc& e, uint64_t key, bool insert, bool* creat
     }
   } else {
     const uint64_t mask = (uint64_t)e.cap - 1;
-    uint64_t h = mix64(key) & mask;
+    const uint64_t h0 = mix64(key) & mask;
     for (int64_t probes = 0;; ++probes) {
       if (probes > e.cap) {
         latch(st, DR_RESOURCE_EXHAUSTED);
         return nullptr;
       }
-      Slot* c = e.slots + h;
+      Slot* c = e.slots + probe_slot(h0, (uint64_t)probes, mask);
       // one 16-byte load brings key and rc: a hit needs no second round trip
       typedef unsigned long long slot_v __attribute__((ext_vector_type(2)));
       const slot_v sv = *reinterpret_cast<const slot_v*>(c);
@@ -257,7 +269,6 @@ __device__ Slot* ev_find(const EvDesc& e, uint64_t key, bool insert, bool* creat
           }
         }
       }
-      h = (h + 1) & mask;
     }
   }
   // The creator publishes the row BEFORE any lane waits for one: with
@@ -1196,15 +1207,15 @@ __global__ void ev_rehash_kept_kernel(const Slot* __restrict__ old_slots, int64_
   }
   if (s.key == kEmptyKey || !keep[i]) return;
   const uint64_t mask = (uint64_t)cap - 1;
-  uint64_t h = mix64(s.key) & mask;
-  for (;;) {
+  const uint64_t h0 = mix64(s.key) & mask;
+  for (uint64_t i = 0;; ++i) {
+    const uint64_t h = probe_slot(h0, i, mask);
     uint64_t old = atomicCAS((unsigned long long*)&new_slots[h].key, (unsigned long long)kEmptyKey,
                              (unsigned long long)s.key);
     if (old == kEmptyKey) {
       new_slots[h].rc = s.rc;
       return;
     }
-    h = (h + 1) & mask;
   }
 }
 
@@ -1218,15 +1229,15 @@ __global__ void ev_rehash_kernel(const Slot* __restrict__ old_slots, int64_t old
   const Slot s = old_slots[i];
   if (s.key == kEmptyKey) return;
   const uint64_t mask = (uint64_t)new_cap - 1;
-  uint64_t h = mix64(s.key) & mask;
-  for (;;) {
+  const uint64_t h0 = mix64(s.key) & mask;
+  for (uint64_t i = 0;; ++i) {
+    const uint64_t h = probe_slot(h0, i, mask);
     uint64_t old = atomicCAS((unsigned long long*)&new_slots[h].key, (unsigned long long)kEmptyKey,
                              (unsigned long long)s.key);
     if (old == kEmptyKey) {
       new_slots[h].rc = s.rc;
       return;
     }
-    h = (h + 1) & mask;
   }
 }
 
@@ -1821,19 +1832,16 @@ __device__ __forceinline__ int64_t ev_probe_row(const LkDesc& e, uint64_t key) {
     rc = sv.y;
   } else {
     const uint64_t mask = (uint64_t)e.cap - 1;
-    uint64_t h = mix64(key) & mask;
-    // (a two-slots-per-step variant -- home and next slot loaded together,
-    // for the third of the keys past their home slot -- measured no gain:
-    // the dependent second probe mostly hits the line already in L2)
+    const uint64_t h0 = mix64(key) & mask;
     for (int64_t probes = 0;; ++probes) {
       if (probes > e.cap) return -1;
-      const slot_v sv = gld(reinterpret_cast<const slot_v*>(e.slots + h));
+      const slot_v sv =
+          gld(reinterpret_cast<const slot_v*>(e.slots + probe_slot(h0, (uint64_t)probes, mask)));
       if (sv.x == key) {
         rc = sv.y;
         break;
       }
       if (sv.x == kEmptyKey) return -1;  // (a stale empty only sends it to the miss path)
-      h = (h + 1) & mask;
     }
   }
   if (rc == kUnset || !(rc & e.colbit)) return -1;
@@ -1939,6 +1947,296 @@ __global__ __launch_bounds__(256) void ev_lookup_onehot_kernel(LookupArgs a, int
       for (int c = 0; c < CPL; ++c) x[q].v[c] = vadd(vzero<typename VecT<VEC>::T>(), x[q].v[c]);
     }
     if (o[q]) store_row_nt<VEC, G, CPL>(x[q], o[q], lg, dv);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Line-wide probes (bucket-local probing, probe_slot): the 8 lanes that share
+// a key load the 8 slots of its home line in one instruction (one 128-B
+// request), and two ballots settle the lookup -- no dependent second probe
+// for the keys displaced from their home slot (a quarter of them at the
+// bench's load), which the slot-by-slot walk paid as an extra L2 round trip
+// in most waves.
+// ---------------------------------------------------------------------------
+typedef unsigned long long slot_v2 __attribute__((ext_vector_type(2)));
+
+// Issue half: lane j (= lane % 8) of the key's 8 lanes loads slot j of the
+// home line (key -1: its special slot, on all 8 lanes).  Branch-free: the
+// address is a select, the load is unconditional.
+__device__ __forceinline__ slot_v2 line_probe_issue(const Slot* slots, int64_t cap, uint64_t key,
+                                                    int j) {
+  const uint64_t line = (mix64(key) & (uint64_t)(cap - 1)) & ~7ull;
+  const uint64_t at = key == kEmptyKey ? (uint64_t)cap : line + (uint64_t)j;
+  return gld(reinterpret_cast<const slot_v2*>(slots + at));
+}
+
+// Resolve half: every lane of the wave calls it (ballots, shuffles).  Each
+// group of 8 lanes gets its key's row, or -1 (absent, column not initialised,
+// dead row: the miss path).  A key neither found nor ruled out in its home
+// line (a full line, ~0.5 % at the bench's load) walks on from probe 8.
+__device__ __forceinline__ int64_t line_probe_resolve(const Slot* slots, int64_t cap,
+                                                      uint64_t colbit, uint64_t key, slot_v2 sv,
+                                                      int lane) {
+  const int j = lane & 7;
+  const bool special = key == kEmptyKey;
+  const uint64_t mask = (uint64_t)cap - 1;
+  const uint64_t h0 = mix64(key) & mask;
+  const int o = special ? 0 : (int)(h0 & 7);
+  // key -1's slot holds 0 when present, -1 when absent; its 8 lanes loaded
+  // the same slot, lane 0 speaks for them (selects, no branches)
+  const bool speaks = !special || j == 0;
+  const bool hit = speaks && sv.x == (special ? 0ull : key);
+  const bool emp = speaks && sv.x == kEmptyKey;
+  const uint64_t hm = __ballot(hit), em = __ballot(emp);
+  const int sh = lane & ~7;
+  const uint32_t h8 = (uint32_t)(hm >> sh) & 0xffu, e8 = (uint32_t)(em >> sh) & 0xffu;
+  // bit i = probe i of the key (offset (o + i) % 8 of the line)
+  const uint32_t rh = ((h8 >> o) | (h8 << (8 - o))) & 0xffu;
+  const uint32_t re = ((e8 >> o) | (e8 << (8 - o))) & 0xffu;
+  const uint32_t any = rh | re;
+  const int f = any ? __builtin_ctz(any) : 0;
+  const int src = sh + ((o + f) & 7);
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)sv.y, src, 64);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(sv.y >> 32), src, 64);
+  uint64_t rc = ((uint64_t)hi << 32) | lo;
+  if (!((rh >> f) & 1u)) rc = kUnset;  // an empty slot comes first, or nothing settled
+  if (!any) {  // the home line holds 8 other keys: continue the sequence
+    for (uint64_t i = 8; i <= (uint64_t)cap; ++i) {
+      const slot_v2 w = gld(reinterpret_cast<const slot_v2*>(slots + probe_slot(h0, i, mask)));
+      if (w.x == key) {
+        rc = w.y;
+        break;
+      }
+      if (w.x == kEmptyKey) break;  // (a stale empty only sends it to the miss path)
+    }
+  }
+  if (rc == kUnset || !(rc & colbit)) return -1;
+  const int64_t row = (int64_t)(rc & kRowMask);
+  return row == (int64_t)kRowDead ? -1 : row;
+}
+
+// One-hot row load / store with no branch around the memory operation: the
+// address is always valid (lanes past the row read its last chunk, rows that
+// are not stored read row 0), the store target a select (rows that must not
+// be written go to a junk line of the workspace).  A branch around a load
+// makes hipcc wait for it right there; a branch around a store makes the
+// counted waits of a software pipeline path-dependent (vmcnt(0)).
+template <int VEC, int G, int CPL, bool WIDEN>
+__device__ __forceinline__ void load_row_copy_u(Row<VEC, G, CPL>& x, const float* p, int lg,
+                                                int dv) {
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    int col = lg + c * G;
+    col = col < dv ? col : dv - 1;
+    if constexpr (WIDEN) {
+      typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+      const u2 w = __builtin_nontemporal_load(gp(reinterpret_cast<const u2*>(p) + col));
+      const float2 a = bf16x2_to_f2(w.x), b = bf16x2_to_f2(w.y);
+      x.v[c] = make_float4(a.x, a.y, b.x, b.y);
+    } else {
+      x.v[c] = nt_load(reinterpret_cast<const typename VecT<VEC>::T*>(p) + col);
+    }
+  }
+}
+
+template <int VEC, int G, int CPL, int ORDER>
+__device__ __forceinline__ void store_row_sel(Row<VEC, G, CPL>& x, float* p, float* junk, int lg,
+                                              int dv) {
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = lg + c * G;
+    if (ORDER == DR_ORDER_SEQ) x.v[c] = vadd(vzero<typename VecT<VEC>::T>(), x.v[c]);  // 0 + e
+    float* dst = col < dv ? p + (int64_t)col * VEC : junk + 2048 + (int64_t)(lg % 64) * VEC;
+    nt_store(x.v[c], reinterpret_cast<typename VecT<VEC>::T*>(dst));
+  }
+}
+
+// Output-order lookup with line-wide probes: a wave owns 8 consecutive
+// output slots (key k of the wave on lanes 8k..8k+7); each group of G = 8 NB
+// lanes then copies NB of the 8 rows (row q of group g = the key on lane
+// g G + 8 q).  One-shot: key -> line -> rows -> stores per wave.
+template <int VEC, int G, int CPL, int ORDER, bool WIDEN = false>
+__global__ __launch_bounds__(256) void ev_lookup_line_kernel(LookupArgs a, int T, int64_t B,
+                                                             int dim, int32_t* __restrict__ mlist,
+                                                             unsigned long long* __restrict__ mcnt,
+                                                             float* __restrict__ junk) {
+  constexpr int NB = G / 8;
+  static_assert(NB * 8 == G, "8 lanes per key, 8 keys per wave");
+  __shared__ LkDesc sd[DR_MAX_GROUP];
+  const int64_t slots = (int64_t)T * B;
+  const int lane = (int)(threadIdx.x & 63);
+  const int64_t ws0 = ((int64_t)blockIdx.x * 4 + threadIdx.x / 64) * 8;  // wave's first slot
+  const int64_t s = ws0 + (lane >> 3);
+  const bool valid = s < slots;
+  const int64_t sc = valid ? s : slots - 1;
+  const int64_t b = (int64_t)((uint32_t)sc / (uint32_t)T);
+  const int t = (int)(sc - b * T);
+  // the id's round trip overlaps the descriptor staging (ids read once)
+  const uint64_t key =
+      (uint64_t)__builtin_nontemporal_load(gp(a.keys + b * a.ksb + (int64_t)t * a.kst));
+  if (threadIdx.x < T) sd[threadIdx.x] = a.d[threadIdx.x];
+  __syncthreads();
+  if (ws0 >= slots) return;  // whole waves
+  const Slot* tsl = sd[t].slots;
+  const int64_t tcap = sd[t].cap;
+  const int64_t row = line_probe_resolve(tsl, tcap, sd[t].colbit, key,
+                                         line_probe_issue(tsl, tcap, key, lane & 7), lane);
+  const bool head = (lane & 7) == 0 && valid;
+  const bool missed = head && row < 0;
+  if (head && row >= 0 && a.rows) a.rows[(int64_t)t * B + b] = row;
+  const uint64_t mm = __ballot(missed);
+  if (mm) {
+    const int leader = __ffsll((unsigned long long)mm) - 1;
+    unsigned long long at = 0;
+    if (lane == leader) at = atomicAdd(mcnt, (unsigned long long)__popcll(mm));
+    at = __shfl(at, leader, 64);
+    if (missed) mlist[at + __popcll(mm & lanemask_lt())] = (int32_t)s;
+  }
+  const int64_t rstride = WIDEN ? dim / 2 : dim;
+  const uint64_t mine = (uint64_t)(uintptr_t)(sd[t].pool + (row >= 0 ? row : 0) * rstride);
+  const uint64_t okm = __ballot(valid && row >= 0);
+  const int lg = lane % G, base = lane - lg;
+  const int dv = dim / VEC;
+  const float* p[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)mine, base + 8 * q, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(mine >> 32), base + 8 * q, 64);
+    p[q] = reinterpret_cast<const float*>((uintptr_t)(((uint64_t)hi << 32) | lo));
+  }
+  Row<VEC, G, CPL> x[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) load_row_copy_u<VEC, G, CPL, WIDEN>(x[q], p[q], lg, dv);
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    const int64_t sq = ws0 + (base / G) * NB + q;
+    const int64_t bq = (int64_t)((uint32_t)sq / (uint32_t)T);
+    const int64_t tq = sq - bq * T;
+    float* dst = ((okm >> (base + 8 * q)) & 1ull) ? a.out + bq * a.out_stride + tq * (int64_t)dim
+                                                  : junk + q * 256;
+    store_row_sel<VEC, G, CPL, ORDER>(x[q], dst, junk, lg, dv);
+  }
+}
+
+// Software-pipelined persistent form of the same lookup: each wave walks its
+// items (8 output slots each) with the keys of item k+2 and the home-line
+// probes of item k+1 in flight while the rows of item k load and the rows of
+// item k-1 are stored -- the probe's dependent round trip leaves the row
+// stream's critical path.  Issue order per iteration: rows(k), probes(k+1),
+// keys(k+2), then the NB stores of k-1; every one of them unconditional, so
+// the wait at the loop top for probes(k+1) is vmcnt(1 + NB stores) on every
+// path and never waits for the stores just issued.  XCD-major item ranges
+// (blocks b, b + 8, ... run on one XCD: speed only, any placement is correct).
+template <int VEC, int G, int CPL, int ORDER, bool WIDEN = false>
+__global__ __launch_bounds__(256) void ev_lookup_pipe_kernel(LookupArgs a, int T, int64_t B,
+                                                             int dim, int32_t* __restrict__ mlist,
+                                                             unsigned long long* __restrict__ mcnt,
+                                                             float* __restrict__ junk) {
+  constexpr int NB = G / 8;
+  static_assert(NB * 8 == G, "8 lanes per key, 8 keys per wave");
+  __shared__ LkDesc sd[DR_MAX_GROUP];
+  if (threadIdx.x < T) sd[threadIdx.x] = a.d[threadIdx.x];
+  __syncthreads();
+  const uint32_t slots = (uint32_t)((int64_t)T * B);  // < 2^31 (host check)
+  const uint32_t items = (slots + 7) / 8;
+  const int lane = (int)(threadIdx.x & 63);
+  const int kq = lane >> 3, j = lane & 7;
+  const int lg = lane % G, base = lane - lg;
+  const int dv = dim / VEC;
+  const int64_t rstride = WIDEN ? dim / 2 : dim;
+  const uint32_t LW = (gridDim.x / 8) * 4;  // waves per XCD (grid % 8 == 0)
+  const uint32_t per = (items + 7) / 8;
+  const uint32_t i0 = (blockIdx.x % 8) * per;
+  const uint32_t i1 = i0 + per < items ? i0 + per : items;
+  uint32_t it = i0 + (blockIdx.x / 8) * 4 + threadIdx.x / 64;
+  if (it >= i1) return;  // whole waves
+  const uint32_t T32 = (uint32_t)T;
+  // slot of this lane's key in item `item` (clamped: reads past the range
+  // are harmless and keep the loop free of branches)
+  auto slot_of = [&](uint32_t item) -> uint32_t {
+    const uint32_t s = item * 8 + kq;
+    return s < slots ? s : slots - 1;
+  };
+  auto key_at = [&](uint32_t s) -> uint64_t {
+    const uint32_t b = s / T32, t = s - b * T32;
+    return (uint64_t)__builtin_nontemporal_load(
+        gp(a.keys + (int64_t)b * a.ksb + (int64_t)t * a.kst));
+  };
+  uint32_t sA = slot_of(it);
+  uint64_t kA = key_at(sA);
+  uint32_t tA = sA % T32;
+  slot_v2 svA = line_probe_issue(sd[tA].slots, sd[tA].cap, kA, j);
+  uint32_t sB = slot_of(it + LW);
+  uint64_t kB = key_at(sB);
+  // rows in flight / being stored ping-pong between X0 and X1 (the loop is
+  // unrolled twice: no register copy of a pending load)
+  Row<VEC, G, CPL> X0[NB], X1[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q)
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) X1[q].v[c] = vzero<typename VecT<VEC>::T>();
+  uint64_t okp = 0;  // which rows of the previous item to store (bit = key lane)
+  uint32_t itp = it;
+  auto store_item = [&](Row<VEC, G, CPL>(&xs)[NB]) {
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const uint32_t sq = itp * 8 + (uint32_t)((base / G) * NB + q);
+      const uint32_t bq = sq / T32, tq = sq - bq * T32;
+      float* dst = ((okp >> (base + 8 * q)) & 1ull)
+                       ? a.out + (int64_t)bq * a.out_stride + (int64_t)tq * dim
+                       : junk + q * 256;  // distinct lines: no store merged away
+      store_row_sel<VEC, G, CPL, ORDER>(xs[q], dst, junk, lg, dv);
+    }
+  };
+  // the loop's shape on entry too: NB (junk) stores after the first probes
+  store_item(X1);
+  // one item: settle its probes, issue its rows into xl, the probes of the
+  // next item and the keys of the one after, then store xs (previous item)
+  auto step = [&](Row<VEC, G, CPL>(&xl)[NB], Row<VEC, G, CPL>(&xs)[NB]) {
+    const int64_t row = line_probe_resolve(sd[tA].slots, sd[tA].cap, sd[tA].colbit, kA, svA, lane);
+    const uint32_t s = it * 8 + kq;
+    const bool valid = s < slots;
+    const bool head = j == 0 && valid;
+    const bool missed = head && row < 0;
+    if (a.rows && head && row >= 0) a.rows[(int64_t)tA * B + s / T32] = row;
+    const uint64_t mm = __ballot(missed);
+    if (mm) {
+      const int leader = __ffsll((unsigned long long)mm) - 1;
+      unsigned long long at = 0;
+      if (lane == leader) at = atomicAdd(mcnt, (unsigned long long)__popcll(mm));
+      at = __shfl(at, leader, 64);
+      if (missed) mlist[at + __popcll(mm & lanemask_lt())] = (int32_t)s;
+    }
+    const uint64_t mine = (uint64_t)(uintptr_t)(sd[tA].pool + (row >= 0 ? row : 0) * rstride);
+    const uint64_t okc = __ballot(valid && row >= 0);
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)mine, base + 8 * q, 64);
+      const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(mine >> 32), base + 8 * q, 64);
+      load_row_copy_u<VEC, G, CPL, WIDEN>(
+          xl[q], reinterpret_cast<const float*>((uintptr_t)(((uint64_t)hi << 32) | lo)), lg, dv);
+    }
+    kA = kB;
+    tA = sB % T32;
+    svA = line_probe_issue(sd[tA].slots, sd[tA].cap, kA, j);
+    sB = slot_of(it + 2 * LW);
+    kB = key_at(sB);
+    store_item(xs);
+    okp = okc;
+    itp = it;
+    it += LW;
+  };
+  for (;;) {
+    step(X0, X1);
+    if (it >= i1) {
+      store_item(X0);
+      break;
+    }
+    step(X1, X0);
+    if (it >= i1) {
+      store_item(X1);
+      break;
+    }
   }
 }
 
@@ -2066,6 +2364,7 @@ static unsigned miss_blocks() {
 }
 
 struct LookupWs {
+  float* junk;  // 16 KB sink of the branch-free stores (line / pipe kernels)
   int32_t* mlist;
   unsigned long long* mcnt;  // [2]: miss count, grid-barrier counter
   int64_t* mrow;
@@ -2075,6 +2374,7 @@ static LookupWs carve_lookup(void* ws, int64_t n, size_t* used) {
   Carver c(ws);
   LookupWs w;
   const int64_t nn = n > 0 ? n : 1;
+  w.junk = c.take<float>(4096);
   w.mlist = c.take<int32_t>(nn);
   w.mcnt = c.take<unsigned long long>(2);
   w.mrow = c.take<int64_t>(nn);
@@ -2094,9 +2394,62 @@ static void launch_lookup_nb(const LookupArgs& a, int T, int64_t B, int dim, con
   timing_mark(DR_TIME_LOOKUP, st, false);
 }
 
+// DR_LOOKUP_KERNEL (A/B switch): 0 = slot-by-slot one-shot kernel (NB rows
+// per lane group), 1 = line probes, one-shot (ev_lookup_line_kernel), 2 =
+// line probes, software-pipelined persistent waves (ev_lookup_pipe_kernel).
+static int lookup_kernel_kind() {
+  static const int v = getenv("DR_LOOKUP_KERNEL") ? atoi(getenv("DR_LOOKUP_KERNEL")) : 2;
+  return v;
+}
+
+// Persistent grid of a 256-thread kernel: resident blocks per CU x CUs,
+// a multiple of 8 (XCD-major item ranges), at most `want`.
+template <class K>
+static unsigned persistent_grid(K kernel, int64_t want) {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess || per <= 0)
+    per = 1;
+  int64_t g = (int64_t)per * cus;
+  want = ceil_div(want, 8) * 8;
+  if (g > want) g = want;
+  g = std::max<int64_t>(8, g / 8 * 8);
+  return (unsigned)g;
+}
+
+// Line-probe lookups (8 lanes per key: G = 8 NB); false when the shape or
+// the switch leaves it to the slot-by-slot kernel.
+template <int VEC, int G, int CPL, int ORDER, bool WIDEN>
+static bool launch_lookup_line(const LookupArgs& a, int T, int64_t B, int dim, const LookupWs& w,
+                               hipStream_t st) {
+  if constexpr (G % 8 != 0) {
+    return false;
+  } else {
+    const int kind = lookup_kernel_kind();
+    if (kind == 0 || a.tmaj) return false;
+    const int64_t waves = ceil_div((int64_t)T * B, 8);
+    timing_mark(DR_TIME_LOOKUP, st, true);
+    if (kind == 1) {
+      hipLaunchKernelGGL((ev_lookup_line_kernel<VEC, G, CPL, ORDER, WIDEN>),
+                         dim3((unsigned)ceil_div(waves, 4)), dim3(256), 0, st, a, T, B, dim,
+                         w.mlist, w.mcnt, w.junk);
+    } else {
+      const unsigned grid =
+          persistent_grid(ev_lookup_pipe_kernel<VEC, G, CPL, ORDER, WIDEN>, ceil_div(waves, 4));
+      hipLaunchKernelGGL((ev_lookup_pipe_kernel<VEC, G, CPL, ORDER, WIDEN>), dim3(grid), dim3(256),
+                         0, st, a, T, B, dim, w.mlist, w.mcnt, w.junk);
+    }
+    timing_mark(DR_TIME_LOOKUP, st, false);
+    return true;
+  }
+}
+
 template <int VEC, int G, int CPL, int ORDER>
 static void launch_lookup_onehot(const LookupArgs& a, int T, int64_t B, int dim, const LookupWs& w,
                                  hipStream_t st) {
+  if (launch_lookup_line<VEC, G, CPL, ORDER, false>(a, T, B, dim, w, st)) return;
   // rows in flight per lane group: 2 for rows of <= 64 floats (D = 64:
   // 0.194 against 0.200 ms for 4, profiles/r04_lookup_ab_nb2.log -- more,
   // smaller groups hide the dependent slot probe better), 4 above (D = 128:
@@ -2193,8 +2546,10 @@ static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t 
   const int d4 = (int)(dim / 4);
 #define DR_LK(G, C)                                                             \
   do {                                                                          \
-    if (widen)                                                                  \
-      launch_lookup_nb<4, G, C, DR_ORDER_ALI, 4, true>(la, T, B, (int)dim, w, st); \
+    if (widen) {                                                                \
+      if (!launch_lookup_line<4, G, C, DR_ORDER_ALI, true>(la, T, B, (int)dim, w, st)) \
+        launch_lookup_nb<4, G, C, DR_ORDER_ALI, 4, true>(la, T, B, (int)dim, w, st); \
+    }                                                                           \
     else if (order == DR_ORDER_ALI)                                             \
       launch_lookup_onehot<4, G, C, DR_ORDER_ALI>(la, T, B, (int)dim, w, st);   \
     else                                                                        \

@@ -30,12 +30,12 @@
 // order by one lane group (rows_work_kernel) -- bit-exact to the reference
 // loops.  Longer runs (hot ids) go to the long-run kernels: rows_expand_kernel
 // measures each run (two rounds of parallel probes) and cuts it into pieces
-// of kSerialMax positions counted from the RUN's first position; every
-// piece is summed in ascending position order by rows_serial_kernel (one
+// of serial_max() positions counted from the RUN's first position (default:
+// unbounded, one piece per run); every piece is summed in ascending position order by rows_serial_kernel (one
 // block per piece and column slice: all threads stage the piece's gradient
 // rows through LDS, one wave walks each column's serial chain), and a run of
 // several pieces is the ordered sum of its piece partials
-// (rows_combine_kernel).  So a run of up to kSerialMax positions is the
+// (rows_combine_kernel).  So every run (any length, by default) is the
 // reference's exact serial sum (segment_reduction_ops.cc:391-404), and every
 // association depends only on the run's own position order -- never on the
 // key -> row numbering that racing first-touch inserts assign, nor on where
@@ -50,12 +50,42 @@ struct RowsGroup {
 };
 
 static constexpr int64_t kRowsChunk = 256;    // longest run of the lane-group path
-static constexpr int64_t kSerialMax = 8192;   // longest exact-serial piece of a long run
+// Longest exact-serial piece of a long run.  Default: unbounded -- every run,
+// however long (a hot id over a whole batch), is ONE serial chain in the
+// reference's ascending order, bit-exact (segment_reduction_ops.cc:391-404).
+// DR_GRAD_SERIAL_MAX=n (A/B switch) cuts runs into pieces of n positions
+// summed in parallel and combined in order (deterministic, fp32-tolerance).
+static int64_t serial_max() {
+  static const int64_t v = [] {
+    const char* e = getenv("DR_GRAD_SERIAL_MAX");
+    const long long n = e ? atoll(e) : 0;
+    // (pieces share the run list's capacity: at least kRowsChunk + 1 long)
+    return n > 0 ? (int64_t)(n > 8192 ? n : 8192) : (int64_t)(1ll << 40);
+  }();
+  return v;
+}
 #ifndef DR_ROWS_CHAIN
 #define DR_ROWS_CHAIN 8
 #endif
 static constexpr int kRowsChain = DR_ROWS_CHAIN;  // positions of a run fetched per step
 static constexpr int64_t kRowsMaxDim = 1024;
+// Zero-term skipping on long serial chains.  A zero-started chain
+// (0 + x_0 + x_1 ..., the sum combiner or a weighted lookup) is never -0.0,
+// so adding a term that is +0.0 or -0.0 leaves it bit-for-bit unchanged
+// (round-to-nearest: s + 0 = s for every s != -0; NaN / Inf terms are not
+// zero and are kept).  Runs longer than zero_scan() positions are first
+// scanned in parallel (rows_nz_kernel: chunks of kRowsChunk positions, each
+// compacted to its nonzero terms in ascending order) and the serial walk
+// visits only those -- e.g. a DIN padding id, whose ~2 x 10^5 history
+// positions all carry exactly zero gradient.  DR_GRAD_ZERO_SKIP=0 (A/B)
+// walks every term.
+static int64_t zero_scan() {
+  static const int64_t v = [] {
+    const char* e = getenv("DR_GRAD_ZERO_SKIP");
+    return (e && atoi(e) == 0) ? (int64_t)0 : (int64_t)2048;
+  }();
+  return v;
+}
 
 // Long-run state (the workspace arrays of RowsWs, passed as one argument).
 struct RowsLong {
@@ -75,6 +105,13 @@ struct RowsLong {
   uint64_t* gptr;
   float* gu;
   float* part;             // [item][dim] piece partials of multi-piece runs
+  int64_t smax;            // piece length (serial_max())
+  int64_t zscan;           // zero-scan runs longer than this (0: never)
+  int32_t* cfirst;         // per long run: its first zero-scan chunk (-1: not scanned)
+  int32_t* crun;           // per chunk: (run, chunk index)
+  int32_t* nchunk;
+  int32_t* ccnt;           // per chunk: its nonzero terms
+  int32_t* kpos;           // [N] chunk k of run c0: nonzero positions at c0 + k*kRowsChunk ..
 };
 
 // Table of global position i (lane-varying; koff staged in LDS).
@@ -96,12 +133,13 @@ __global__ void rows_keys_kernel(const int64_t* __restrict__ rowsel, int64_t N, 
                                  uint32_t sentinel, uint32_t* __restrict__ kin,
                                  int32_t* __restrict__ vin, int32_t* __restrict__ flags,
                                  int32_t* __restrict__ nlong, int32_t* __restrict__ nwork,
-                                 int32_t* __restrict__ nitems) {
+                                 int32_t* __restrict__ nitems, int32_t* __restrict__ nchunk) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) {
     *nlong = 0;
     *nwork = 0;
     *nitems = 0;
+    *nchunk = 0;
   }
   if (i >= N) return;
   const int64_t r = rowsel[i];
@@ -703,7 +741,7 @@ __device__ __forceinline__ bool in_run(const RowsLong& L, int64_t N, int64_t q, 
 // One block per long run: its end (two rounds of parallel probes -- every
 // kRowsChunk-th position past the head, then the 256 positions of the window
 // the run ends in: a run's positions are contiguous, so in_run is a prefix),
-// then its pieces of kSerialMax positions as work items.
+// then its pieces of serial_max() positions as work items.
 __global__ __launch_bounds__(256) void rows_expand_kernel(RowsGroup g, int T, RowsLong L) {
   __shared__ int64_t sk[DR_MAX_GROUP + 1];
   __shared__ int smin;
@@ -739,19 +777,89 @@ __global__ __launch_bounds__(256) void rows_expand_kernel(RowsGroup g, int T, Ro
     if (!in_run(L, N, w0 + 1 + threadIdx.x, u, lo, hi)) atomicMin(&smin, (int)threadIdx.x);
     __syncthreads();
     const int64_t len = w0 + 1 + smin - c0;
-    const int np = (int)((len + kSerialMax - 1) / kSerialMax);
+    const int np = (int)((len + L.smax - 1) / L.smax);
+    // zero-scan chunks: one-piece runs of a zero-started chain (sum combiner
+    // or weighted: rows_serial_kernel's fresh start is then 0 + x_0)
+    const bool zs = g.d[t].combiner == DR_COMBINER_SUM || g.d[t].weights != nullptr;
+    const int nch = (np == 1 && zs && L.zscan > 0 && len > L.zscan)
+                        ? (int)((len + kRowsChunk - 1) / kRowsChunk) : 0;
     if (threadIdx.x == 0) {
       const int fi = atomicAdd(L.nitems, np);
       L.rlen[i] = (int32_t)len;
       L.rfirst[i] = fi;
       sfirst = fi;
+      const int cf = nch ? atomicAdd(L.nchunk, nch) : -1;
+      L.cfirst[i] = cf;
+      smin = cf;
     }
     __syncthreads();
     for (int k = threadIdx.x; k < np; k += 256) {
       L.items[2 * (sfirst + k)] = i;
       L.items[2 * (sfirst + k) + 1] = k;
     }
+    const int cf = smin;
+    for (int k = threadIdx.x; k < nch; k += 256) {
+      L.crun[2 * (cf + k)] = i;
+      L.crun[2 * (cf + k) + 1] = k;
+    }
     __syncthreads();   // smin / sfirst are rewritten by the next run
+  }
+}
+
+// Zero scan of the long runs' chunks (zero_scan()): one block per chunk of
+// kRowsChunk positions, one thread per position computes its term exactly as
+// rows_serial_kernel stages it (bag row or zero, weights / mean scale) and
+// tests every column for != 0; the chunk's nonzero positions are compacted in
+// ascending order into kpos[chunk start ..] and counted in ccnt.
+template <int VEC>
+__global__ __launch_bounds__(256) void rows_nz_kernel(RowsGroup g, int T, int dim, RowsLong L) {
+  __shared__ int64_t sk[DR_MAX_GROUP + 1];
+  __shared__ int wc[4];
+  using V = typename VecT<VEC>::T;
+  if (threadIdx.x <= T) sk[threadIdx.x] = g.koff[threadIdx.x];
+  __syncthreads();
+  const int n = *L.nchunk;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int c = blockIdx.x; c < n; c += gridDim.x) {   // block-uniform
+    const int i = L.crun[2 * c], k = L.crun[2 * c + 1];
+    const int64_t c0 = L.longs[i];
+    const int64_t len = L.rlen[i];
+    const int64_t cs = c0 + (int64_t)k * kRowsChunk;
+    const int64_t ce = c0 + len < cs + kRowsChunk ? c0 + len : cs + kRowsChunk;
+    const int t = tab_of(sk, T, L.perm[c0]);
+    const dr_pool_grad_desc& d = g.d[t];
+    const bool wt = d.weights != nullptr;
+    const bool qs = wt && d.bag_scale;
+    const bool ms = !wt && d.combiner != DR_COMBINER_SUM;
+    const int64_t q = cs + tid;
+    bool nz = false;
+    if (q < ce) {
+      const int32_t rq = L.srow[q];
+      const float mf = (wt || ms) ? L.smul[q] : 1.f;
+      const float df = qs ? L.sdiv[q] : 1.f;
+      const float* row = d.top_grad + (int64_t)(rq >= 0 ? rq : 0) * d.top_stride;
+      for (int cv = 0; cv * VEC < dim; ++cv) {
+        V x = rq >= 0 ? gld(reinterpret_cast<const V*>(row) + cv) : vzero<V>();
+        if (wt) {
+          if (qs) x = vdiv(x, df);
+          x = vmul(x, mf);
+        } else if (ms && mf != 1.f) {
+          x = vmul(x, mf);
+        }
+        if constexpr (VEC == 4)
+          nz |= (x.x != 0.f) | (x.y != 0.f) | (x.z != 0.f) | (x.w != 0.f);
+        else
+          nz |= x != 0.f;
+      }
+    }
+    const uint64_t bm = __ballot(nz);
+    if (lane == 0) wc[wv] = __popcll(bm);
+    __syncthreads();
+    int before = 0;
+    for (int w = 0; w < wv; ++w) before += wc[w];
+    if (nz) L.kpos[cs + before + __popcll(bm & lanemask_lt())] = (int32_t)q;
+    if (tid == 0) L.ccnt[c] = wc[0] + wc[1] + wc[2] + wc[3];
+    __syncthreads();   // wc is rewritten by the next chunk
   }
 }
 
@@ -770,9 +878,12 @@ __global__ __launch_bounds__(256) void rows_serial_kernel(RowsGroup g, int T, in
   constexpr int PI = 256 / SV;             // positions per load instruction
   constexpr int R = VEC == 4 ? 16 : 32;    // loads in flight per thread
   constexpr int S = PI * R;                // positions per stage
+  constexpr int WCH = 1024;                // zero-scan chunks per window (prefix in LDS)
   static_assert(SV >= 1 && 256 % SV == 0, "slice shape");
   __shared__ __attribute__((aligned(16))) float stage[S * SW];
   __shared__ int64_t sk[DR_MAX_GROUP + 1];
+  __shared__ int32_t cpre[WCH + 1];
+  __shared__ int32_t wsum[4];
   if (threadIdx.x <= T) sk[threadIdx.x] = g.koff[threadIdx.x];
   __syncthreads();
   const int nsl = (dim + SW - 1) / SW;
@@ -787,9 +898,10 @@ __global__ __launch_bounds__(256) void rows_serial_kernel(RowsGroup g, int T, in
     const int k = __builtin_amdgcn_readfirstlane(L.items[2 * j + 1]);
     const int64_t c0 = __builtin_amdgcn_readfirstlane(L.longs[i]);
     const int64_t len = __builtin_amdgcn_readfirstlane(L.rlen[i]);
-    const int np = (int)((len + kSerialMax - 1) / kSerialMax);
-    const int64_t ps = c0 + (int64_t)k * kSerialMax;
-    const int64_t pe = c0 + len < ps + kSerialMax ? c0 + len : ps + kSerialMax;
+    const int64_t smax = L.smax;
+    const int np = (int)((len + smax - 1) / smax);
+    const int64_t ps = c0 + (int64_t)k * smax;
+    const int64_t pe = c0 + len < ps + smax ? c0 + len : ps + smax;
     const int32_t pc = __builtin_amdgcn_readfirstlane(L.perm[c0]);
     const uint32_t u = (uint32_t)__builtin_amdgcn_readfirstlane((int)L.skey[c0]);
     const int t = __builtin_amdgcn_readfirstlane(tab_of(sk, T, pc));
@@ -801,103 +913,162 @@ __global__ __launch_bounds__(256) void rows_serial_kernel(RowsGroup g, int T, in
     const int colv = slice * SV + cv;                 // this thread's vector column
     const float* src = d.top_grad + (colv * VEC < dim ? colv * VEC : 0);
     const int64_t ts = d.top_stride;
-    // bag rows one stage ahead of the row loads; every load is clamped to the
-    // piece, so the batches issue unconditionally (a branch around a batch
-    // would make the compiler wait for it at the join)
-    int32_t rq[R];
-    auto load_idx = [&](int64_t b0) {
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        int64_t q = b0 + r * PI + pv;
-        q = q < pe ? q : pe - 1;
-        rq[r] = L.srow[q];
-      }
-    };
-    uint32_t zmask = 0;   // invalid bags among the rows in flight (zero terms)
-    auto take = [&]() {
-      zmask = 0;
-#pragma unroll
-      for (int r = 0; r < R; ++r) zmask |= (rq[r] < 0 ? 1u : 0u) << r;
-    };
-    V y[R];
-    auto load_rows = [&]() {
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int64_t rr = rq[r] >= 0 ? rq[r] : 0;
-        y[r] = gld(reinterpret_cast<const V*>(src + rr * ts));
-      }
-    };
+    // zero-scanned run (rows_nz_kernel): walk only its nonzero terms, chunk by
+    // chunk in ascending order; a zero-started chain is unchanged by the
+    // skipped +-0.0 terms (zero_scan()).  Otherwise entry e = position ps + e.
+    const int cf = np == 1 ? __builtin_amdgcn_readfirstlane(L.cfirst[i]) : -1;
+    const bool zc = cf >= 0;
+    const int64_t nch = zc ? (len + kRowsChunk - 1) / kRowsChunk : 1;
     float acc = 0.f;
     bool fresh = !(k == 0 && zs);   // first term: 0 + y (zero-started sum) or y
-    load_idx(ps);
-    take();
-    load_rows();
-    load_idx(ps + S);
-    for (int64_t b0 = ps; b0 < pe; b0 += S) {
-      // y: this stage's rows in flight; rq: the next stage's bag rows
-      if (wt || ms) {   // block-uniform: the terms' factors (rows_term), then scaled
-        float mf[R], df[R];
+    for (int64_t w0 = 0; w0 < nch; w0 += WCH) {   // windows of chunks (plain: one)
+      int64_t K;
+      int nw = 1;
+      if (zc) {
+        nw = (int)(nch - w0 < WCH ? nch - w0 : WCH);
+        // exclusive prefix of the window's chunk counts: 4 chunks per thread,
+        // wave scan by shuffles, wave totals through LDS
+        int c4[4], tsum = 0;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          int64_t q = b0 + r * PI + pv;
-          q = q < pe ? q : pe - 1;
-          mf[r] = L.smul[q];
-          df[r] = qs ? L.sdiv[q] : 1.f;
+        for (int q = 0; q < 4; ++q) {
+          const int jj = 4 * tid + q;
+          c4[q] = jj < nw ? L.ccnt[cf + w0 + jj] : 0;
+          tsum += c4[q];
         }
+        int incl = tsum;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          V x = y[r];
-          if ((zmask >> r) & 1u) x = vzero<V>();
-          if (wt) {
-            if (qs) x = vdiv(x, df[r]);
-            x = vmul(x, mf[r]);
-          } else if (mf[r] != 1.f) {
-            x = vmul(x, mf[r]);
-          }
-          *reinterpret_cast<V*>(stage + (r * PI + pv) * SW + cv * VEC) = x;
+        for (int o = 1; o < 64; o <<= 1) {
+          const int v = __shfl_up(incl, o, 64);
+          if (lane >= o) incl += v;
         }
+        if (lane == 63) wsum[tid >> 6] = incl;
+        __syncthreads();
+        int before = incl - tsum;
+        for (int w = 0; w < (tid >> 6); ++w) before += wsum[w];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int jj = 4 * tid + q;
+          if (jj <= nw) cpre[jj] = before;   // (jj == nw: the total)
+          before += c4[q];
+        }
+        if (tid == 255 && 4 * 256 <= nw) cpre[nw] = before;
+        __syncthreads();
+        K = cpre[nw];
       } else {
+        K = pe - ps;
+      }
+      // sorted position of entry e (0 <= e < K)
+      auto posmap = [&](int64_t e) -> int64_t {
+        if (!zc) return ps + e;
+        int lo = 0, hi = nw - 1;   // last chunk with cpre <= e
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (cpre[mid] <= e)
+            lo = mid;
+          else
+            hi = mid - 1;
+        }
+        return L.kpos[c0 + (w0 + lo) * kRowsChunk + (e - cpre[lo])];
+      };
+      // bag rows one stage ahead of the row loads; every load is clamped to
+      // the entries, so the batches issue unconditionally (a branch around a
+      // batch would make the compiler wait for it at the join)
+      int32_t rq[R];
+      auto load_idx = [&](int64_t b0) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          V x = y[r];
-          if ((zmask >> r) & 1u) x = vzero<V>();
-          *reinterpret_cast<V*>(stage + (r * PI + pv) * SW + cv * VEC) = x;
+          int64_t e = b0 + r * PI + pv;
+          e = e < K ? e : K - 1;
+          rq[r] = L.srow[posmap(e)];
         }
+      };
+      uint32_t zmask = 0;   // invalid bags among the rows in flight (zero terms)
+      auto take = [&]() {
+        zmask = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) zmask |= (rq[r] < 0 ? 1u : 0u) << r;
+      };
+      V y[R];
+      auto load_rows = [&]() {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int64_t rr = rq[r] >= 0 ? rq[r] : 0;
+          y[r] = gld(reinterpret_cast<const V*>(src + rr * ts));
+        }
+      };
+      if (K > 0) {
+        load_idx(0);
+        take();
+        load_rows();
+        load_idx(S);
       }
-      __syncthreads();
-      take();
-      load_rows();              // the next stage's rows: in flight while wave 0 sums this one
-      load_idx(b0 + 2 * S);
-      if (tid < 64) {           // wave-uniform
-        const int nv = (int)(pe - b0 < S ? pe - b0 : S);
-        const float* sp = stage + lc;
-        int jj = 0;
-        if (fresh) {
-          acc = sp[0];
-          fresh = false;
-          jj = 1;
+      for (int64_t b0 = 0; b0 < K; b0 += S) {
+        // y: this stage's rows in flight; rq: the next stage's bag rows
+        if (wt || ms) {   // block-uniform: the terms' factors (rows_term), then scaled
+          float mf[R], df[R];
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            int64_t e = b0 + r * PI + pv;
+            e = e < K ? e : K - 1;
+            const int64_t q = posmap(e);
+            mf[r] = L.smul[q];
+            df[r] = qs ? L.sdiv[q] : 1.f;
+          }
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            V x = y[r];
+            if ((zmask >> r) & 1u) x = vzero<V>();
+            if (wt) {
+              if (qs) x = vdiv(x, df[r]);
+              x = vmul(x, mf[r]);
+            } else if (mf[r] != 1.f) {
+              x = vmul(x, mf[r]);
+            }
+            *reinterpret_cast<V*>(stage + (r * PI + pv) * SW + cv * VEC) = x;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            V x = y[r];
+            if ((zmask >> r) & 1u) x = vzero<V>();
+            *reinterpret_cast<V*>(stage + (r * PI + pv) * SW + cv * VEC) = x;
+          }
         }
-        // the LDS reads of the next 8 positions are issued before the adds
-        // of these 8: the chain waits on the adds, not on LDS latency
-        if (jj + 8 <= nv) {
-          float xa[8], xb[8];
+        __syncthreads();
+        take();
+        load_rows();              // the next stage's rows: in flight while wave 0 sums this one
+        load_idx(b0 + 2 * S);
+        if (tid < 64) {           // wave-uniform
+          const int nv = (int)(K - b0 < S ? K - b0 : S);
+          const float* sp = stage + lc;
+          int jj = 0;
+          if (fresh) {
+            acc = sp[0];
+            fresh = false;
+            jj = 1;
+          }
+          // the LDS reads of the next 8 positions are issued before the adds
+          // of these 8: the chain waits on the adds, not on LDS latency
+          if (jj + 8 <= nv) {
+            float xa[8], xb[8];
 #pragma unroll
-          for (int q = 0; q < 8; ++q) xa[q] = sp[(jj + q) * SW];
-          for (; jj + 16 <= nv; jj += 8) {
+            for (int q = 0; q < 8; ++q) xa[q] = sp[(jj + q) * SW];
+            for (; jj + 16 <= nv; jj += 8) {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) xb[q] = sp[(jj + 8 + q) * SW];
+              for (int q = 0; q < 8; ++q) xb[q] = sp[(jj + 8 + q) * SW];
+#pragma unroll
+              for (int q = 0; q < 8; ++q) acc = acc + xa[q];
+#pragma unroll
+              for (int q = 0; q < 8; ++q) xa[q] = xb[q];
+            }
 #pragma unroll
             for (int q = 0; q < 8; ++q) acc = acc + xa[q];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) xa[q] = xb[q];
+            jj += 8;
           }
-#pragma unroll
-          for (int q = 0; q < 8; ++q) acc = acc + xa[q];
-          jj += 8;
+          for (; jj < nv; ++jj) acc = acc + sp[jj * SW];
         }
-        for (; jj < nv; ++jj) acc = acc + sp[jj * SW];
+        __syncthreads();   // the stage is rewritten next
       }
-      __syncthreads();   // the stage is rewritten next
     }
     if (tid < 64) {
       const int col = slice * SW + lane;
@@ -926,7 +1097,7 @@ __global__ __launch_bounds__(256) void rows_combine_kernel(RowsGroup g, int T, i
   const int n = *L.nlong;
   for (int i = blockIdx.x; i < n; i += gridDim.x) {   // block-uniform
     const int64_t len = L.rlen[i];
-    const int np = (int)((len + kSerialMax - 1) / kSerialMax);
+    const int np = (int)((len + L.smax - 1) / L.smax);
     if (np <= 1) continue;
     const int64_t fi = L.rfirst[i];
     const int64_t c0 = L.longs[i];
@@ -994,12 +1165,18 @@ struct RowsWs {
   int32_t* rfirst;
   int32_t* items;
   float* part;
+  int32_t* cfirst;
+  int32_t* crun;
+  int32_t* nchunk;
+  int32_t* ccnt;
+  int32_t* kpos;
   void* sort_ws;
   size_t sort_bytes;
   void* scan_ws;
   RowsLong longrun(uint64_t* gptr, float* gu) const {
     return RowsLong{kout, perm, ex, base, srow, smul, sdiv, longs, nlong, rlen, rfirst, items,
-                    nitems, gptr, gu, part};
+                    nitems, gptr, gu, part, serial_max(), zero_scan(), cfirst, crun, nchunk,
+                    ccnt, kpos};
   }
 };
 
@@ -1030,6 +1207,14 @@ static RowsWs carve_rows(void* ws, int64_t n, size_t* used) {
   w.rfirst = c.take<int32_t>(runs);
   w.items = c.take<int32_t>(2 * runs);
   w.part = c.take<float>(runs * kRowsMaxDim);
+  // zero scan: chunks of kRowsChunk positions of the long runs (at most one
+  // per kRowsChunk positions plus one per run), compacted positions [N]
+  const int64_t chunks = nn / kRowsChunk + runs + 1;
+  w.cfirst = c.take<int32_t>(runs);
+  w.crun = c.take<int32_t>(2 * chunks);
+  w.nchunk = c.take<int32_t>(1);
+  w.ccnt = c.take<int32_t>(chunks);
+  w.kpos = c.take<int32_t>(nn);
   w.sort_bytes = sort_pairs_u32_ws_bytes(nn);
   w.sort_ws = c.take<char>(w.sort_bytes);
   w.scan_ws = c.take<char>(scan_ws_bytes(nn));
@@ -1048,6 +1233,11 @@ static void launch_long(const RowsGroup& g, int T, int dim, const RowsLong& L, c
   const int64_t runs = N / (kRowsChunk + 1) + 1;
   hipLaunchKernelGGL(rows_expand_kernel, dim3((unsigned)(runs < 1024 ? runs : 1024)), dim3(256), 0,
                      s, g, T, L);
+  if (L.zscan > 0 && N > L.zscan) {
+    const int64_t chunks = N / kRowsChunk + 1;
+    hipLaunchKernelGGL((rows_nz_kernel<VEC>), dim3((unsigned)(chunks < 2048 ? chunks : 2048)),
+                       dim3(256), 0, s, g, T, dim, L);
+  }
   int sw = 1;
   while (sw < dim && sw < 32) sw <<= 1;
   if (VEC == 4 && sw < 4) sw = 4;
@@ -1076,8 +1266,8 @@ static void launch_long(const RowsGroup& g, int T, int dim, const RowsLong& L, c
     }
   }
 #undef DR_SERIAL
-  if (N > kSerialMax) {
-    const int64_t big = N / (kSerialMax + 1) + 1;
+  if (N > L.smax) {
+    const int64_t big = N / (L.smax + 1) + 1;
     hipLaunchKernelGGL((rows_combine_kernel<SGD, WB>), dim3((unsigned)(big < 256 ? big : 256)),
                        dim3(256), 0, s, g, T, dim, L, sg);
   }
@@ -1169,7 +1359,7 @@ int rows_apply_sgd(const dr_pool_grad_desc* descs_host, int num_tables, int64_t 
   const uint32_t sentinel = (uint32_t)(((uint64_t)1 << rb) - 1);
   hipLaunchKernelGGL(rows_keys_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, rowsel,
                      n, row_limit, sentinel, w.kin, w.vin, (int32_t*)nullptr, w.nlong, w.nwork,
-                     w.nitems);
+                     w.nitems, w.nchunk);
   DR_LAUNCH_CHECK();
   int rc = sort_pairs_u32(w.kin, w.vin, w.kout, w.perm, n, rb, w.sort_ws, s);
   if (rc) return rc;
@@ -1261,7 +1451,7 @@ int dr_pool_grad_rows_grouped_ex(const dr_pool_grad_desc* descs_host, int num_ta
   const uint32_t sentinel = (uint32_t)(((uint64_t)1 << rb) - 1);
   const unsigned nb = (unsigned)ceil_div(n, 256);
   hipLaunchKernelGGL(rows_keys_kernel, dim3(nb), dim3(256), 0, s, rowsel, n, row_limit, sentinel,
-                     w.kin, w.vin, w.flags, w.nlong, w.nwork, w.nitems);
+                     w.kin, w.vin, w.flags, w.nlong, w.nwork, w.nitems, w.nchunk);
   DR_LAUNCH_CHECK();
   int rc = sort_pairs_u32(w.kin, w.vin, w.kout, w.perm, n, rb, w.sort_ws, s);
   if (rc) return rc;

@@ -996,7 +996,8 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
                                                        int dim, float* __restrict__ out,
                                                        float* __restrict__ part,
                                                        int32_t* __restrict__ longs,
-                                                       int32_t* __restrict__ nlong, int* st) {
+                                                       int32_t* __restrict__ nlong, int chunked,
+                                                       int* st) {
   __shared__ dr_pool_grad_desc sd[DR_MAX_GROUP];  // per-lane table index: stage in LDS
   if (threadIdx.x < T) sd[threadIdx.x] = g.d[threadIdx.x];
   __syncthreads();
@@ -1026,7 +1027,7 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
   bool inner = false;
 #pragma unroll
   for (int q = 0; q < NB; ++q) inner |= (p0 + q) > 0 && uk[q] == uk[q + 1];
-  if (__ballot(inner)) {
+  if (chunked && __ballot(inner)) {
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
       const int64_t u = uk[q + 1];
@@ -1046,7 +1047,9 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
     const bool in = p < N && u < N;  // u == N: sentinel for out-of-range idx
     const bool rhead = p == 0 || uk[q] != u;
     sq[q] = rhead ? p : rsq[q];
-    head[q] = in && (rhead || (p - sq[q]) % kGradChunk == 0);
+    // exact (default): only run heads; a run longer than kGradChunk is queued
+    // whole for grad_long_kernel.  chunked (A/B): chunk heads too.
+    head[q] = in && (rhead || (chunked && (p - sq[q]) % kGradChunk == 0));
     single[q] = p + 1 >= N || uk[q + 2] != u;
     uq[q] = u;
     tq[q] = head[q] ? table_of(g.koff, T, u, ufirst < N ? ufirst : 0) : 0;
@@ -1152,6 +1155,17 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
     const dr_pool_grad_desc& d = sd[t];
     const int mode = mode_of(d);
     const bool first_chunk = c0 == 0 || (int64_t)skey[c0 - 1] != u;
+    if (!chunked) {
+      // a run longer than one chunk: one serial chain in grad_long_kernel
+      if (c0 + kGradChunk < N && (int64_t)skey[c0 + kGradChunk] == u) {
+        if (lg == 0) {
+          const int32_t at = atomicAdd(nlong, 1);
+          longs[2 * at] = (int32_t)u;
+          longs[2 * at + 1] = (int32_t)c0;
+        }
+        continue;
+      }
+    }
     R acc;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) acc.v[c] = vzero<V>();
@@ -1212,8 +1226,8 @@ __global__ __launch_bounds__(256) void grad_seg_kernel(GradGroup g, int T, int64
     if (cbad) latch(st, DR_INVALID_ARGUMENT);
     if (first_chunk) {
       store_row<VEC, G, CPL>(acc, out + u * (int64_t)dim, lg, dv);
-      // a run longer than one chunk: queue it for grad_finish_kernel
-      if (lg == 0 && c0 + kGradChunk < N && (int64_t)skey[c0 + kGradChunk] == u) {
+      // (chunked) a run longer than one chunk: queue it for grad_finish_kernel
+      if (chunked && lg == 0 && c0 + kGradChunk < N && (int64_t)skey[c0 + kGradChunk] == u) {
         const int32_t at = atomicAdd(nlong, 1);
         longs[2 * at] = (int32_t)u;
         longs[2 * at + 1] = (int32_t)c0;
@@ -1270,6 +1284,169 @@ __global__ __launch_bounds__(256) void grad_finish_kernel(const uint64_t* __rest
   }
 }
 
+// Exact long runs of the grouped backward (the default): one block per
+// (queued run, column slice of SW columns) sums the WHOLE run in ascending
+// position order -- the reference's serial UnsortedSegmentSum /
+// SparseSegmentReductionGrad chain (segment_reduction_ops.cc:391-404,
+// segment_reduction_ali_ops_util.h:331-458), bit-exact at any length.  The
+// run's end is found by 256-way probing of the sorted keys; then stages of S
+// positions: all 256 threads load the terms' row slices (the next stage's
+// rows in flight while this one is summed), scale them exactly as
+// grad_seg_kernel does (mean / sqrtn bag scale, weights) and write them to
+// LDS; wave 0 walks each column's chain (one lane per column).
+template <int VEC, int SW, bool W>
+__global__ __launch_bounds__(256) void grad_long_kernel(GradGroup g, int T, int64_t B,
+                                                        const uint64_t* __restrict__ skey,
+                                                        const int32_t* __restrict__ perm, int dim,
+                                                        float* __restrict__ out,
+                                                        const int32_t* __restrict__ longs,
+                                                        const int32_t* __restrict__ nlong,
+                                                        int* st) {
+  using V = typename VecT<VEC>::T;
+  constexpr int SV = SW / VEC;             // vectors of a position's slice
+  constexpr int PI = 256 / SV;             // positions per load instruction
+  constexpr int R = VEC == 4 ? 16 : 32;    // loads in flight per thread
+  constexpr int S = PI * R;                // positions per stage
+  static_assert(SV >= 1 && 256 % SV == 0, "slice shape");
+  __shared__ __attribute__((aligned(16))) float stage[S * SW];
+  __shared__ int smin;
+  const int64_t N = g.koff[T];
+  const int nsl = (dim + SW - 1) / SW;
+  const int64_t total = (int64_t)(*nlong) * nsl;
+  const int tid = threadIdx.x;
+  const int pv = tid / SV, cv = tid % SV;
+  const int lane = tid & 63;
+  const int lc = lane < SW ? lane : 0;
+  for (int64_t wi = blockIdx.x; wi < total; wi += gridDim.x) {   // block-uniform
+    const int i = (int)(wi / nsl), slice = (int)(wi % nsl);
+    const int64_t u = __builtin_amdgcn_readfirstlane(longs[2 * i]);
+    const int64_t c0 = __builtin_amdgcn_readfirstlane(longs[2 * i + 1]);
+    // run end: lo in the run, hi = N or a position past it (the run is a
+    // prefix of [c0, N)); 256 probes per round cover (lo, hi]
+    int64_t lo = c0, hi = N;
+    while (hi - lo > 1) {
+      const int64_t step = (hi - lo - 1 + 255) / 256;
+      if (tid == 0) smin = 255;
+      __syncthreads();
+      const int64_t q = lo + step * (int64_t)(tid + 1);
+      if (q >= hi || (int64_t)skey[q] != u) atomicMin(&smin, tid);
+      __syncthreads();
+      const int m = smin;   // first probe past the run (q_255 >= hi: one exists)
+      __syncthreads();
+      const int64_t nh = lo + step * (int64_t)(m + 1);
+      hi = nh < hi ? nh : hi;
+      lo = lo + step * (int64_t)m;
+    }
+    const int64_t pe = lo + 1;   // one past the run's last position
+    const int t = __builtin_amdgcn_readfirstlane(table_of(g.koff, T, u, u));
+    const dr_pool_grad_desc& d = g.d[t];
+    const int mode = d.combiner == DR_COMBINER_SUM ? 0 : (d.combiner == DR_COMBINER_MEAN ? 1 : 2);
+    const bool wt = W && d.weights != nullptr;
+    const bool zs = mode == 0 || wt;                  // 0 + x_0 + x_1 ...
+    const int colv = slice * SV + cv;                 // this thread's vector column
+    const bool colok = colv * VEC < dim;
+    const float* tg = d.top_grad + (colok ? colv * VEC : 0);
+    const int64_t ts = d.top_stride;
+    const int64_t* segp = d.seg;
+    const int64_t sst = d.seg_stride;
+    const int64_t kt0 = g.koff[t];
+    const int64_t nnz_t = d.nnz;
+    // bag rows one stage ahead of the row loads; loads clamped to the run
+    int64_t rq[R];
+    int64_t kk[W ? R : 1];
+    bool bad = false;
+    auto load_idx = [&](int64_t b0) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        int64_t q = b0 + r * PI + pv;
+        q = q < pe ? q : pe - 1;
+        const int64_t k = (int64_t)perm[q] - kt0;
+        rq[r] = ((k >= 0) & (k < nnz_t)) ? k : 0;
+        if (W) kk[W ? r : 0] = rq[r];
+      }
+      if (segp) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) rq[r] = segp[rq[r] * sst];
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const bool okr = (rq[r] >= 0) & (rq[r] < B);
+        bad |= !okr;
+        rq[r] = okr ? rq[r] : -1;
+      }
+    };
+    V y[R];
+    int64_t ry[R];
+    int64_t ky[W ? R : 1];
+    auto load_rows = [&]() {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        ry[r] = rq[r];
+        if (W) ky[W ? r : 0] = kk[W ? r : 0];
+        y[r] = gld(reinterpret_cast<const V*>(tg + (rq[r] >= 0 ? rq[r] : 0) * ts));
+      }
+    };
+    float acc = 0.f;
+    bool fresh = !zs;   // first term: 0 + y (zero-started sum) or y
+    load_idx(c0);
+    load_rows();
+    load_idx(c0 + S);
+    for (int64_t b0 = c0; b0 < pe; b0 += S) {
+      // y: this stage's rows in flight; rq: the next stage's bag rows
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        V x = ry[r] >= 0 ? y[r] : vzero<V>();
+        if (wt) {   // (g / bag_scale[bag]) * w[k]
+          if (d.bag_scale) x = vdiv(x, d.bag_scale[ry[r] >= 0 ? ry[r] : 0]);
+          x = vmul(x, d.weights[ky[W ? r : 0]]);
+        } else if (mode != 0) {   // * 1/cnt or 1/sqrt(cnt), scale computed in double
+          const int64_t rr = ry[r];
+          const int32_t cnt = (rr >= 0 && d.bag_off) ? d.bag_off[rr + 1] - d.bag_off[rr] : 1;
+          if (cnt != 1)
+            x = vmul(x, mode == 2 ? (float)(1.0 / sqrt((double)cnt)) : (float)(1.0 / (double)cnt));
+        }
+        *reinterpret_cast<V*>(stage + (r * PI + pv) * SW + cv * VEC) = x;
+      }
+      __syncthreads();
+      load_rows();              // the next stage's rows: in flight while wave 0 sums this one
+      load_idx(b0 + 2 * S);
+      if (tid < 64) {           // wave-uniform
+        const int nv = (int)(pe - b0 < S ? pe - b0 : S);
+        const float* sp = stage + lc;
+        int jj = 0;
+        if (fresh) {
+          acc = sp[0];
+          fresh = false;
+          jj = 1;
+        }
+        // the LDS reads of the next 8 positions are issued before the adds
+        // of these 8: the chain waits on the adds, not on LDS latency
+        if (jj + 8 <= nv) {
+          float xa[8], xb[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) xa[q] = sp[(jj + q) * SW];
+          for (; jj + 16 <= nv; jj += 8) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) xb[q] = sp[(jj + 8 + q) * SW];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc = acc + xa[q];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) xa[q] = xb[q];
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc = acc + xa[q];
+          jj += 8;
+        }
+        for (; jj < nv; ++jj) acc = acc + sp[jj * SW];
+      }
+      __syncthreads();   // the stage is rewritten next
+    }
+    if (bad) latch(st, DR_INVALID_ARGUMENT);
+    const int col = slice * SW + lane;
+    if (tid < 64 && lane < SW && col < dim) out[u * (int64_t)dim + col] = acc;
+  }
+}
+
 template <int VEC, int G, int CPL>
 static void launch_grad_csr(const GradGroup& g, int T, int64_t B, const uint64_t* skey,
                             const int32_t* perm, int dim, float* out, const GradWs& w,
@@ -1281,17 +1458,34 @@ static void launch_grad_csr(const GradGroup& g, int T, int64_t B, const uint64_t
   const int64_t blocks = ceil_div(ceil_div(N > 0 ? N : 1, NB), 256 / G);
   bool weighted = false;
   for (int t = 0; t < T; ++t) weighted = weighted || g.d[t].weights;
+  // DR_GRAD_CHUNKED=1 (A/B switch): long runs as ordered 256-position chunk
+  // partials (deterministic, fp32 tolerance); default: one exact serial chain
+  static const int chunked = getenv("DR_GRAD_CHUNKED") ? atoi(getenv("DR_GRAD_CHUNKED")) : 0;
   if (weighted)
     hipLaunchKernelGGL((grad_seg_kernel<VEC, G, CPL, NB, true>), dim3((unsigned)blocks), dim3(256),
                        0, s, g, T, B, skey, perm, w.run_start, dim, out, w.part, w.longs, w.nlong,
-                       st);
+                       chunked, st);
   else
     hipLaunchKernelGGL((grad_seg_kernel<VEC, G, CPL, NB, false>), dim3((unsigned)blocks),
                        dim3(256), 0, s, g, T, B, skey, perm, w.run_start, dim, out, w.part,
-                       w.longs, w.nlong, st);
-  if (N > kGradChunk)
+                       w.longs, w.nlong, chunked, st);
+  if (N <= kGradChunk) return;
+  if (chunked) {
     hipLaunchKernelGGL((grad_finish_kernel<VEC, G, CPL>), dim3(64), dim3(256), 0, s, skey, N, dim,
                        out, w.part, w.longs, w.nlong, N / kGradChunk + 2);
+    return;
+  }
+  // one block per (long run, slice); an empty list costs one load per block
+  constexpr int SWC = 32;
+  const int nsl = (dim + SWC - 1) / SWC;
+  int64_t gb = (N / (kGradChunk + 1) + 1) * nsl;
+  if (gb > 512) gb = 512;
+  if (weighted)
+    hipLaunchKernelGGL((grad_long_kernel<VEC, SWC, true>), dim3((unsigned)gb), dim3(256), 0, s, g,
+                       T, B, skey, perm, dim, out, w.longs, w.nlong, st);
+  else
+    hipLaunchKernelGGL((grad_long_kernel<VEC, SWC, false>), dim3((unsigned)gb), dim3(256), 0, s,
+                       g, T, B, skey, perm, dim, out, w.longs, w.nlong, st);
 }
 
 // ---- weighted-lookup divisor and clip_by_norm backward ----------------------

@@ -102,21 +102,36 @@ static int a2a_v(dr_comm* c, const void* send, const int64_t* sc, void* recv, co
   char* rp = static_cast<char*>(recv);
   int64_t so = 0, ro = 0;
   // the self block is a local copy; the others one ncclSend / ncclRecv pair
-  // per peer inside one group (all xGMI links at once)
+  // per peer inside one group (all xGMI links at once).  Any failure inside
+  // the group still closes it (GroupEnd), or every later collective on this
+  // thread's communicator would run inside the dangling group.
   DR_NCCL(api->GroupStart());
-  for (int p = 0; p < c->world; ++p) {
+  int err = DR_OK;
+  for (int p = 0; p < c->world && err == DR_OK; ++p) {
     if (p == c->rank) {
-      if (sc[p])
-        DR_HIP(hipMemcpyAsync(rp + ro * eb, sp + so * eb, (size_t)(sc[p] * eb),
-                              hipMemcpyDeviceToDevice, st));
+      if (sc[p]) {
+        const hipError_t e = hipMemcpyAsync(rp + ro * eb, sp + so * eb, (size_t)(sc[p] * eb),
+                                            hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) {
+          set_error("self block copy failed: %s", hipGetErrorString(e));
+          err = DR_INTERNAL;
+        }
+      }
     } else {
-      if (sc[p]) DR_NCCL(api->Send(sp + so * eb, (size_t)(sc[p] * eb), ncclUint8, p, c->nc, st));
-      if (rc[p]) DR_NCCL(api->Recv(rp + ro * eb, (size_t)(rc[p] * eb), ncclUint8, p, c->nc, st));
+      int r = 0;
+      if (sc[p]) r = api->Send(sp + so * eb, (size_t)(sc[p] * eb), ncclUint8, p, c->nc, st);
+      if (r == 0 && rc[p]) r = api->Recv(rp + ro * eb, (size_t)(rc[p] * eb), ncclUint8, p, c->nc, st);
+      if (r != 0) {
+        set_error("ncclSend/ncclRecv to peer %d failed (%d)", p, r);
+        err = DR_INTERNAL;
+      }
     }
     so += sc[p];
     ro += rc[p];
   }
-  DR_NCCL(api->GroupEnd());
+  const int ge = api->GroupEnd();
+  if (err) return err;
+  DR_REQUIRE(ge == 0, DR_INTERNAL, "ncclGroupEnd failed (%d)", ge);
   return DR_OK;
 }
 

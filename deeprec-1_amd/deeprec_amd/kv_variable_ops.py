@@ -7,6 +7,7 @@ argument semantics.
 """
 import ctypes as C
 import atexit
+import collections
 import threading
 
 import torch
@@ -74,8 +75,11 @@ def _default_row(initializer, dim, device, dtype=torch.float32):
 # capture_begin / capture_end are counted process-wide (_CAPTURES), on every
 # thread.  At interpreter exit the queue is dropped (the process's device
 # memory goes with it).
-_DEFERRED = []
-_DEFERRED_LOCK = threading.Lock()
+# __del__ appends without the lock (deque.append is atomic): a collection
+# that runs inside the locked flush below, on the same thread, must not block
+# on the lock that thread holds.  The lock is reentrant for the same reason.
+_DEFERRED = collections.deque()
+_DEFERRED_LOCK = threading.RLock()
 _CAPTURES = [0]     # torch graph captures open in this process (any thread)
 
 
@@ -125,10 +129,15 @@ def _flush_deferred_releases():
             return
         if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
             return
-        hs = _DEFERRED[:]
-        del _DEFERRED[:]
-        for h in hs:
-            lib().dr_ev_release(h)
+        while True:
+            try:
+                h = _DEFERRED.popleft()
+            except IndexError:
+                break
+            if isinstance(h, tuple):      # (destroy entry name, handle): engines
+                getattr(lib(), h[0])(h[1])
+            else:
+                lib().dr_ev_release(h)
 
 
 def flush_releases():
@@ -140,8 +149,13 @@ def flush_releases():
 
 
 def _release_handle(h):
-    with _DEFERRED_LOCK:
-        _DEFERRED.append(h)
+    _DEFERRED.append(h)   # lock-free: may run from GC inside the flush
+
+
+def _release_engine(destroy, h):
+    """Queue an engine handle (e.g. dr_sharded_destroy, which synchronises the
+    device) on the same capture-safe deferred path as EV handles."""
+    _DEFERRED.append((destroy, h))
 
 
 atexit.register(lambda: _DEFERRED.clear())   # dropped: the process's device memory goes too

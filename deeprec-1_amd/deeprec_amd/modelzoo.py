@@ -328,10 +328,19 @@ class _ShardedLookupFn(torch.autograd.Function):
     IndexedSlices -- the KV optimizer applies them there (SOK DLRM's sparse
     path, modelzoo/SOK/DLRM)."""
 
+    # The engines keep the routing state of ONE gradient-carrying forward
+    # (inbox / send order / unique ids) for the backward.  Each such forward
+    # bumps the engine's generation; a backward whose forward is no longer
+    # the latest (a second forward -- an eval pass, another micro-batch --
+    # ran in between) raises instead of routing gradients by the wrong batch.
+
     @staticmethod
     def forward(ctx, anchor, engine, ids):
         from .sharded import XgmiShardedLookup
         ctx.engine = engine
+        gen = getattr(engine, "_dr_fwd_gen", 0) + 1
+        engine._dr_fwd_gen = gen
+        ctx.gen = gen
         if isinstance(engine, XgmiShardedLookup):   # keeps its inbox for the backward
             out = engine.forward(ids)
         else:
@@ -340,8 +349,28 @@ class _ShardedLookupFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        if getattr(ctx.engine, "_dr_fwd_gen", None) != ctx.gen:
+            raise RuntimeError(
+                "sharded lookup backward: another forward ran on this engine since this "
+                "one (its routing state is gone); run backward before the next forward, "
+                "or run the other forward under torch.no_grad()")
         ctx.engine.backward(g.float().contiguous())
         return None, None, None
+
+
+def _sharded_lookup(anchor, engine, ids):
+    """The engine's lookup as an autograd node when gradients are recorded;
+    under torch.no_grad() (an eval pass) a plain forward that keeps no
+    routing state (need_grad off: the engines' cheaper direct path)."""
+    if torch.is_grad_enabled():
+        return _ShardedLookupFn.apply(anchor, engine, ids)
+    # this forward overwrites the engine's exchange buffers too: a pending
+    # backward of an earlier forward must refuse
+    engine._dr_fwd_gen = getattr(engine, "_dr_fwd_gen", 0) + 1
+    from .sharded import XgmiShardedLookup
+    if isinstance(engine, XgmiShardedLookup):
+        return engine.forward(ids)
+    return engine.forward(ids, need_grad=False)
 
 
 class DLRM(torch.nn.Module):
@@ -390,7 +419,7 @@ class DLRM(torch.nn.Module):
             self._sh_anchor = torch.zeros(1, device=x0.device, requires_grad=True)
         B = x0.shape[0]
         if not self.replicated:
-            emb = _ShardedLookupFn.apply(self._sh_anchor, self.engine, ids)
+            emb = _sharded_lookup(self._sh_anchor, self.engine, ids)
             return torch.cat([x0.float().unsqueeze(1), emb.view(B, self.T, self.dim)], 1)
         rep = self.replicated
         sh = [t for t in range(self.T) if t not in rep]
@@ -401,8 +430,8 @@ class DLRM(torch.nn.Module):
                              mk([1 + t for t in sh]))
         _, irep, ish, i0, xrep, xsh = self._hyb_idx
         er = self._rep_lookup(ids.index_select(0, irep)).view(B, len(rep), self.dim)
-        es = _ShardedLookupFn.apply(self._sh_anchor, self.engine,
-                                    ids.index_select(0, ish)).view(B, len(sh), self.dim)
+        es = _sharded_lookup(self._sh_anchor, self.engine,
+                             ids.index_select(0, ish)).view(B, len(sh), self.dim)
         X = x0.new_empty((B, 1 + self.T, self.dim), dtype=torch.float32)
         X = X.index_copy(1, i0, x0.float().unsqueeze(1))
         X = X.index_copy(1, xrep, er)
@@ -796,7 +825,7 @@ class DCNv2(torch.nn.Module):
         else:
             if self._sh_anchor is None:
                 self._sh_anchor = torch.zeros(1, device=dense.device, requires_grad=True)
-            emb = _ShardedLookupFn.apply(self._sh_anchor, self.engine, ids)
+            emb = _sharded_lookup(self._sh_anchor, self.engine, ids)
         if self.mfma_deep:
             # x0 cast column block by column block into one bf16 buffer (no
             # fp32 [B, dp] concat in between); the slice copies keep autograd
@@ -952,10 +981,13 @@ def allreduce_dense_grads(params, group=None, staged=False):
     data-parallel all-reduce; RCCL over xGMI, or host-staged over gloo for a
     rehearsal of several ranks on one GPU)."""
     import torch.distributed as dist
+    # every parameter in a fixed order, zeros where this rank's batch left no
+    # gradient (as DDP): all ranks reduce buckets of the same size
     by = {}
     for p in params:
-        if p.grad is not None:
-            by.setdefault(p.grad.dtype, []).append(p.grad)
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+        by.setdefault(p.grad.dtype, []).append(p.grad)
     for grads in by.values():
         flat = torch.cat([g.reshape(-1) for g in grads])
         if staged:

@@ -457,6 +457,16 @@ class NativeShardedLookup(object):
             lib().dr_sharded_destroy(self.h)
         self.h = None
 
+    def __del__(self):
+        # dr_sharded_create retained every EV: an engine dropped without
+        # close() must still release them.  dr_sharded_destroy synchronises
+        # the device, so it goes through the EVs' capture-safe deferred path.
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            from .kv_variable_ops import _release_engine
+            _release_engine("dr_sharded_destroy", h)
+            self.h = None
+
 
 def hybrid_split(cardinalities, replicate_max):
     """Features whose vocabulary is at most `replicate_max` rows are
@@ -904,13 +914,52 @@ class XgmiShardedLookup(object):
             return self._local.pool(self.bufs.out.view(B * T, self.dim), rowsel, None,
                                     self._koff, None, B, "sum", out_dtype)
         self._saved = None
+        ph = getattr(self, "_ph", None)
+        if ph is not None:   # phase timing (bench at N > 1): events between the phases
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+            ev[0].record()
         self.route(ids)
+        if ph is not None:
+            ev[1].record()
         self._barrier()
+        if ph is not None:
+            ev[2].record()
         self.serve()
+        if ph is not None:
+            ev[3].record()
         self._barrier()
+        if ph is not None:
+            ev[4].record()
+            ph.append(ev)
         if self.bufs.out.dtype == torch.bfloat16 and out_dtype != torch.bfloat16:
             return self.bufs.out.float()
         return self.bufs.out
+
+    def phase_timing(self, on=True):
+        """Record HIP events around each phase of the one-hot forward (route,
+        barrier, serve = owner resolve + row writes over xGMI, barrier)."""
+        self._ph = [] if on else None
+
+    def phase_summary(self):
+        """Mean ms per forward of each phase since phase_timing(True):
+        route (requester kernel: (key, slot) pairs into the owners' inboxes),
+        wait_route (barrier: the slowest peer's route + the collective's
+        latency), serve (owner resolve + every row written to its requester,
+        the link-bound phase), wait_serve (barrier after the serve)."""
+        ph = getattr(self, "_ph", None) or []
+        if not ph:
+            return None
+        torch.cuda.synchronize()
+        names = ("route", "wait_route", "serve", "wait_serve")
+        acc = [0.0] * 4
+        for ev in ph:
+            for i in range(4):
+                acc[i] += ev[i].elapsed_time(ev[i + 1])
+        n = len(ph)
+        self._ph = []
+        out = {k: acc[i] / n for i, k in enumerate(names)}
+        out["steps"] = n
+        return out
 
     def _forward_bags(self, ids, bag_offs, combiner, out_dtype):
         T, B = self.T, self.batch

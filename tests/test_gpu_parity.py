@@ -740,16 +740,16 @@ def test_grouped_backward_matches_segment_grad(dr, orc, onehot, comb):
 @pytest.mark.parametrize("comb", ["sum", "mean"])
 @pytest.mark.parametrize("D", [18, 32])
 def test_grouped_backward_long_runs(dr, orc, comb, D):
-    """Runs longer than one chunk (256 positions: a DIN padding id over a
-    whole history batch) are summed as ordered chunk partials.  Runs of
-    <= 256 positions -- here 256 exactly and 200 -- stay bit-exact to the
-    serial reference order; longer ones (257, 5000, 3 x 256) match it to
-    fp32 tolerance: max |error| <= 1e-5 x max |row| (sums of up to 5000 N(0,1)
-    terms, |S| ~ 70)."""
+    """Hot ids on the Unique path (dr_pool_grad_grouped; it also serves the
+    sharded backward): runs of 257, 5000, 21846 (a Criteo-TB feature of
+    cardinality 3 at B = 65536) and 65536 positions, besides 256 / 768 / 200.
+    Every run, whatever its length, is ONE serial chain in ascending position
+    order -- bit-equal to the reference's UnsortedSegmentSum /
+    SparseSegmentReductionGrad loops (segment_reduction_ops.cc:391-404)."""
     rng = np.random.default_rng(37)
-    runs = {0: 5000, 1: 256, 2: 257, 3: 768, 4: 200}
+    runs = {0: 5000, 1: 256, 2: 257, 3: 768, 4: 200, 5: 21846, 6: 65536}
     v = np.concatenate([np.full(n, k, np.int64) for k, n in runs.items()] +
-                       [rng.integers(5, 400, 3000).astype(np.int64)])
+                       [rng.integers(7, 400, 3000).astype(np.int64)])
     rng.shuffle(v)
     B = v.size
     evs, sps = [], []
@@ -768,14 +768,33 @@ def test_grouped_backward_long_runs(dr, orc, comb, D):
         assert H(sl.indices[:U]).tolist() == uids.tolist()
         ref = orc.sparse_segment_reduce_grad(np.ascontiguousarray(g[:, f * D:(f + 1) * D]), idx,
                                              seg, U, comb)
-        got = H(sl.values[:U])
-        pos = {int(k): i for i, k in enumerate(uids)}
-        exact = [i for i in range(U) if int(uids[i]) not in (0, 2, 3)]
-        np.testing.assert_array_equal(got[exact], ref[exact])
-        for k in (0, 2, 3):
-            # north_star's 1e-5 rel, relative to the gradient row's magnitude
-            err = np.abs(got[pos[k]] - ref[pos[k]]).max()
-            assert err <= 1e-5 * np.abs(ref[pos[k]]).max(), (k, err)
+        np.testing.assert_array_equal(H(sl.values[:U]), ref)
+    dr.status_check()
+
+
+@pytest.mark.parametrize("comb", ["mean", "sqrtn"])
+def test_grouped_backward_long_runs_multihot(dr, orc, comb):
+    """Multi-hot bags (the per-term 1/cnt or 1/sqrt(cnt) bag scale) with a
+    hot id in 30000 bags and a weighted feature: long runs bit-exact too."""
+    rng = np.random.default_rng(43)
+    B, H_, D = 40000, 4, 16
+    ind, v = _random_sparse(rng, B, H_, 300, allow_empty=False)
+    v = v.copy()
+    hot = rng.random(v.size) < 0.3
+    v[hot] = 7                                  # one id over ~30 % of the positions
+    ev = dr.EmbeddingVariable("lrun_mh_%s" % comb, D, 0.1)
+    sp = dr.SparseTensor(T(ind), T(v), (B, H_))
+    out = dr.embedding_lookup_sparse(ev, sp, combiner=comb)
+    g = rng.standard_normal((B, D)).astype(np.float32)
+    out.backward(T(g))
+    sl = ev.pending_grads.pop()
+    U = int(sl.num_valid.item())
+    uids, idx = orc.unique(v)
+    assert int(np.bincount(idx).max()) > 10000
+    assert H(sl.indices[:U]).tolist() == uids.tolist()
+    ref = orc.sparse_segment_reduce_grad(g, idx, ind[:, 0].astype(np.int32), U, comb)
+    np.testing.assert_array_equal(H(sl.values[:U]), ref)
+    dr.status_check()
 
 
 def test_optimizers_with_repeated_indices(dr, orc):

@@ -143,15 +143,15 @@ def test_rows_backward_single_feature_weighted(dr, orc, D):
 
 @pytest.mark.parametrize("D", [18, 32, 1])
 def test_rows_backward_long_runs(dr, orc, D):
-    """Hot ids: runs of 5000 / 256 / 257 / 768 / 200 / 511 / 8192 / 8193 /
-    20000 positions.  Runs of <= 8192 positions are the serial ascending sum
-    (bit-exact); longer ones are the ordered sum of 8192-position pieces cut
-    from the run start (no further from the exact sum than the serial fp32
-    loop)."""
+    """Hot ids on the rows path: runs of 5000 / 256 / 257 / 768 / 200 / 511 /
+    8192 / 8193 / 20000 / 21846 / 65536 positions.  Every run is ONE serial
+    chain in ascending position order (rows_serial_kernel, one piece per run):
+    bit-equal to the reference's serial sum at any length."""
     rng = np.random.default_rng(41)
-    runs = {0: 5000, 1: 256, 2: 257, 3: 768, 4: 200, 5: 511, 6: 8192, 7: 8193, 8: 20000}
+    runs = {0: 5000, 1: 256, 2: 257, 3: 768, 4: 200, 5: 511, 6: 8192, 7: 8193, 8: 20000,
+            9: 21846, 10: 65536}
     v = np.concatenate([np.full(n, k, np.int64) for k, n in runs.items()] +
-                       [rng.integers(9, 400, 3000).astype(np.int64)])
+                       [rng.integers(11, 400, 3000).astype(np.int64)])
     rng.shuffle(v)
     B = v.size
     evs, sps = [], []
@@ -164,26 +164,54 @@ def test_rows_backward_long_runs(dr, orc, D):
     out.backward(T(g))
     uids, idx = orc.unique(v)
     seg = np.arange(B, dtype=np.int32)
-    pieces = [k for k, n in runs.items() if n > 8192]
     for f in range(3):
         sl = evs[f].pending_grads.pop()
         U = int(sl.num_valid.item())
         assert H(sl.indices[:U]).tolist() == uids.tolist()
         gf = np.ascontiguousarray(g[:, f * D:(f + 1) * D])
         ref = orc.sparse_segment_reduce_grad(gf, idx, seg, U, "sum")
+        np.testing.assert_array_equal(H(sl.values[:U]), ref)
+    dr.status_check()
+
+
+@pytest.mark.parametrize("D", [18, 32])
+def test_rows_backward_long_runs_zero_terms(dr, orc, D):
+    """Long runs whose terms are mostly exact zeros (a DIN padding id: the
+    masked positions' gradients are +-0.0): the serial walk skips the zero
+    terms of a zero-started chain (rows_nz_kernel) -- bit-equal to the full
+    serial sum, signs included: a run of only zero terms (+0.0 and -0.0) is
+    +0.0, as 0 + (-0) + ... is in the reference's loop."""
+    rng = np.random.default_rng(45)
+    runs = {0: 30000, 1: 9000, 2: 40000, 3: 5000}
+    v = np.concatenate([np.full(n, k, np.int64) for k, n in runs.items()] +
+                       [rng.integers(4, 300, 2000).astype(np.int64)])
+    rng.shuffle(v)
+    B = v.size
+    g = rng.standard_normal((B, 2 * D)).astype(np.float32)
+    zero = (v == 0) & (rng.random(B) < 0.9)       # 90 % of run 0: zero rows
+    g[zero] = 0.0
+    g[zero & (rng.random(B) < 0.5)] = -0.0        # half of them -0.0
+    g[v == 2] = np.where(rng.random((int((v == 2).sum()), 2 * D)) < 0.5, -0.0, 0.0)  # only zeros
+    sel = np.flatnonzero(v == 1)[::7]
+    g[sel, :D] = 0.0                                # partly zero rows stay in the walk
+    evs, sps = [], []
+    for f in range(2):
+        evs.append(dr.EmbeddingVariable("rzero_%d_%d" % (D, f), D, 0.1, capacity=1024))
+        ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+        sps.append(dr.SparseTensor(T(ind), T(v), (B, 1)))
+    out = dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum")
+    out.backward(T(g))
+    uids, idx = orc.unique(v)
+    seg = np.arange(B, dtype=np.int32)
+    for f in range(2):
+        sl = evs[f].pending_grads.pop()
+        U = int(sl.num_valid.item())
+        assert H(sl.indices[:U]).tolist() == uids.tolist()
+        gf = np.ascontiguousarray(g[:, f * D:(f + 1) * D])
+        ref = orc.sparse_segment_reduce_grad(gf, idx, seg, U, "sum")
         got = H(sl.values[:U])
-        pos = {int(k): i for i, k in enumerate(uids)}
-        exact = [i for i in range(U) if int(uids[i]) not in pieces]
-        np.testing.assert_array_equal(got[exact], ref[exact])
-        for k in pieces:
-            # first-order bound of fp32 recursive summation: u * sum_k |S_k|
-            # over the serial partial sums (the pieces' partial sums and their
-            # ordered combination are bounded by the same terms, x 2)
-            terms = gf[v == k].astype(np.float64)
-            part = np.cumsum(terms, 0)
-            bound = 2.0 * 2.0 ** -24 * np.abs(part).sum(0)
-            err = np.abs(got[pos[k]] - part[-1])
-            assert np.all(err <= bound), (k, err.max(), bound.min())
+        np.testing.assert_array_equal(got.view(np.int32), ref.view(np.int32))   # bitwise, signs too
+        assert not np.signbit(got[list(uids).index(2)]).any()
     dr.status_check()
 
 

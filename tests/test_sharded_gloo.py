@@ -490,3 +490,37 @@ def test_sync_replicated_grads_gloo(world):
             assert len(out) == (1 if want_k.numel() else 0)
             if out:
                 assert torch.equal(out[0][0], want_k) and torch.equal(out[0][1], want_v)
+
+
+def _unused_param_worker(rank, world, port, outdir):
+    import datetime
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "deeprec-1_amd"))
+    from deeprec_amd import modelzoo as mz
+    a = torch.nn.Parameter(torch.ones(3))
+    b = torch.nn.Parameter(torch.ones(5))
+    loss = (a * (rank + 1)).sum()
+    if rank == 0:                       # b gets a gradient on rank 0 only
+        loss = loss + (b * 2.0).sum()
+    loss.backward()
+    mz.allreduce_dense_grads([a, b])
+    torch.save({"a": a.grad.clone(), "b": b.grad.clone()}, os.path.join(outdir, "u%d.pt" % rank))
+    dist.destroy_process_group()
+
+
+def test_allreduce_dense_grads_param_unused_on_one_rank():
+    """A parameter without a gradient on one rank (unused by its batch after
+    zero_grad(set_to_none=True)) reduces as zeros there: every rank reduces
+    buckets of the same size and ends with the same summed gradients."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_unused_param_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        got = [torch.load(os.path.join(d, "u%d.pt" % r), weights_only=True) for r in range(world)]
+    for g in got:
+        assert torch.equal(g["a"], torch.full((3,), 3.0))
+        assert torch.equal(g["b"], torch.full((5,), 2.0))

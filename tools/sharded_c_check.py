@@ -12,7 +12,8 @@ callback).  Checks, bit for bit:
   * forward (one-hot forward-only, one-hot with gradient, multi-hot mean,
     bf16 EVs) == this rank's batch looked up on one GPU in a full local copy
     of every table (embedding_lookup_sparse_multi);
-  * backward: the owner's IndexedSlices == the concatenation over source
+  * backward (incl. hot keys over 257 / 5000 / 21846 / 65536 positions of
+    a 70000-id batch): the owner's IndexedSlices == the concatenation over source
     ranks (ascending) of each source's first-occurrence unique keys that
     this rank owns with their SparseSegment*Grad rows (the oracle's Unique +
     sparse_segment_reduce_grad over every rank's batch and gradient).
@@ -40,6 +41,20 @@ def _onehot_ids(step, rank):
     ids = np.random.default_rng(31 + 1000 * step + rank).integers(0, KEYSPACE, (T, B))
     ids[:, :9] = 17 + step          # a repeated id in every table
     return ids.astype(np.int64)
+
+
+LONG_RUNS = (257, 5000, 21846, 65536)   # per table (T = 4)
+
+
+def _long_ids(rank, n):
+    """[T, n] one-hot ids; table t's key 4321 + t fills LONG_RUNS[t] shuffled
+    positions (a run of that length in the row-sorted backward)."""
+    rng = np.random.default_rng(913 + rank)
+    ids = rng.integers(0, KEYSPACE, (T, n)).astype(np.int64)
+    for t in range(T):
+        ids[t][ids[t] == 4321 + t] = 0
+        ids[t, rng.permutation(n)[:LONG_RUNS[t]]] = 4321 + t
+    return ids
 
 
 def _bags(step, rank):
@@ -169,6 +184,37 @@ def worker(rank, world, port, q):
             check("bags_bwd_grads_%d_%d" % (step, t), v.cpu().numpy(), np.concatenate(vv))
         for e in shard:
             e.pending_grads.clear()
+    # -- long runs: table t's hot key over LONG_RUNS[t] of BL positions on every
+    # rank (257 .. 65536): each source's SparseSegment*Grad row of it is one
+    # serial chain on the Unique path of the sharded backward --
+    BL = 70000
+    indl = torch.stack([torch.arange(BL, device=dev),
+                        torch.zeros(BL, dtype=torch.int64, device=dev)], 1)
+    ids = _long_ids(rank, BL)
+    it = torch.as_tensor(ids, device=dev)
+    ref = embedding_lookup_sparse_multi(full, [SparseTensor(indl, it[t], (BL, 1))
+                                               for t in range(T)], combiner="sum")
+    out = eng.forward(it, combiner="sum", need_grad=True)
+    torch.cuda.synchronize()
+    check("long_fwd", out.cpu().numpy(), ref.detach().cpu().numpy())
+    g = _grad(200, rank, BL)
+    slices = eng.backward(torch.as_tensor(g, device=dev))
+    for t in range(T):
+        k, v = slices[t]
+        kk, vv = [], []
+        for p in range(world):
+            idp = _long_ids(p, BL)[t]
+            gp = _grad(200, p, BL)[:, t * D:(t + 1) * D]
+            u, idx = orc.unique(idp)
+            gu = orc.sparse_segment_reduce_grad(np.ascontiguousarray(gp), idx,
+                                                np.arange(BL, dtype=np.int32), u.size, "sum")
+            own = u % world == rank
+            kk.append(u[own])
+            vv.append(gu[own])
+        check("long_bwd_keys_%d" % t, k.cpu().numpy(), np.concatenate(kk))
+        check("long_bwd_grads_%d" % t, v.cpu().numpy(), np.concatenate(vv))
+    for e in shard:
+        e.pending_grads.clear()
     # -- bf16 EVs: bf16 rows on the wire, fp32 and bf16 outputs --
     sb = evset("bs", torch.bfloat16)
     fb = evset("bf", torch.bfloat16, full=True)
