@@ -235,7 +235,7 @@ struct RowsSgd {
 };
 int rows_apply_sgd(const dr_pool_grad_desc* descs_host, int num_tables, int64_t batch, int dim,
                    const int64_t* rowsel, int64_t row_limit, const RowsSgd& sg, void* ws,
-                   size_t ws_bytes, hipStream_t s);
+                   size_t ws_bytes, hipStream_t s, int rows_record);
 
 #ifdef DR_UC_DIAG
 // xgmi.hip, diagnostic build only: uncached blocks freed to hipFree, and a

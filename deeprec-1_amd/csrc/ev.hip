@@ -1820,6 +1820,7 @@ struct LookupArgs {
   int64_t out_stride;
   int64_t* rows;        // [T, B] row served per id (-1: default), or nullptr
   int tmaj;             // visit slots table by table (s = t * B + b), not in output order
+  int rrec;             // rows record-major: rows[b * T + t] (DR_LOOKUP_ROWS_RECORD)
 };
 
 // Row of `key` when present with this column initialised, else -1.
@@ -1894,7 +1895,7 @@ __global__ __launch_bounds__(256) void ev_lookup_onehot_kernel(LookupArgs a, int
     const int64_t row = ev_probe_row(e, pkey);
     if (row >= 0) {
       mine = e.pool + row * (int64_t)(WIDEN ? dim / 2 : dim);
-      if (a.rows) a.rows[(int64_t)t * B + b] = row;
+      if (a.rows) a.rows[a.rrec ? b * T + t : (int64_t)t * B + b] = row;
     } else {
       missed = true;
     }
@@ -2083,7 +2084,7 @@ __global__ __launch_bounds__(256) void ev_lookup_line_kernel(LookupArgs a, int T
                                          line_probe_issue(tsl, tcap, key, lane & 7), lane);
   const bool head = (lane & 7) == 0 && valid;
   const bool missed = head && row < 0;
-  if (head && row >= 0 && a.rows) a.rows[(int64_t)t * B + b] = row;
+  if (head && row >= 0 && a.rows) a.rows[a.rrec ? s : (int64_t)t * B + b] = row;
   const uint64_t mm = __ballot(missed);
   if (mm) {
     const int leader = __ffsll((unsigned long long)mm) - 1;
@@ -2198,7 +2199,7 @@ __global__ __launch_bounds__(256) void ev_lookup_pipe_kernel(LookupArgs a, int T
     const bool valid = s < slots;
     const bool head = j == 0 && valid;
     const bool missed = head && row < 0;
-    if (a.rows && head && row >= 0) a.rows[(int64_t)tA * B + s / T32] = row;
+    if (a.rows && head && row >= 0) a.rows[a.rrec ? (int64_t)s : (int64_t)tA * B + s / T32] = row;
     const uint64_t mm = __ballot(missed);
     if (mm) {
       const int leader = __ffsll((unsigned long long)mm) - 1;
@@ -2251,6 +2252,7 @@ struct MissArgs {
   float* out;
   int64_t out_stride;
   int64_t* rows;
+  int rrec;
 };
 
 // Grid-wide barrier of the miss kernel.  The grid is small enough to be
@@ -2336,7 +2338,8 @@ __global__ __launch_bounds__(256) void ev_miss_kernel(MissArgs a, int T, int64_t
     const int64_t b = s / T;
     const int t = (int)(s - b * T);
     const float* src = mrow[i] >= 0 ? a.pool[t] + mrow[i] * dim : a.dflt[t];
-    if (a.rows && lane == 0) a.rows[(int64_t)t * B + b] = mrow[i] >= 0 ? mrow[i] : -1;
+    if (a.rows && lane == 0)
+      a.rows[a.rrec ? b * T + t : (int64_t)t * B + b] = mrow[i] >= 0 ? mrow[i] : -1;
     if (widen) {  // bf16 row (dim float words) -> 2 * dim fp32 values
       const uint16_t* h = reinterpret_cast<const uint16_t*>(src);
       float* dst = a.out + b * a.out_stride + (int64_t)t * 2 * dim;
@@ -2481,8 +2484,8 @@ static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t 
   // reference casts bf16 embeddings to float32, embedding_ops.py:606-607);
   // with DR_LOOKUP_OUT_BF16 the rows are copied bitwise as D / 2 float words
   // into a bf16 output.  out_stride counts elements of the output type.
-  DR_REQUIRE((flags & ~(DR_LOOKUP_OUT_BF16 | DR_LOOKUP_TABLE_ORDER)) == 0, DR_INVALID_ARGUMENT,
-             "unknown flags 0x%x", flags);
+  DR_REQUIRE((flags & ~(DR_LOOKUP_OUT_BF16 | DR_LOOKUP_TABLE_ORDER | DR_LOOKUP_ROWS_RECORD)) == 0,
+             DR_INVALID_ARGUMENT, "unknown flags 0x%x", flags);
   const bool bf16 = evs[0]->sh->bf16 && evs[0]->col == 0;
   const bool out_bf16 = flags & DR_LOOKUP_OUT_BF16;
   const bool widen = bf16 && !out_bf16;
@@ -2543,6 +2546,7 @@ static int lookup_onehot(dr_ev* const* evs, int T, const int64_t* keys, int64_t 
   la.out = ma.out = out;
   la.out_stride = ma.out_stride = out_stride;
   la.tmaj = (flags & DR_LOOKUP_TABLE_ORDER) ? 1 : 0;
+  la.rrec = ma.rrec = (flags & DR_LOOKUP_ROWS_RECORD) ? 1 : 0;
   const int d4 = (int)(dim / 4);
 #define DR_LK(G, C)                                                             \
   do {                                                                          \
@@ -3295,6 +3299,15 @@ int dr_ev_pool_grad_rows_apply_sgd(dr_ev* const* vars, const dr_pool_grad_desc* 
                                    int num_tables, int64_t batch, int dim, const int64_t* rowsel,
                                    float lr, int64_t global_step, void* ws, size_t ws_bytes,
                                    void* stream) {
+  return dr_ev_pool_grad_rows_apply_sgd_ex(vars, descs, num_tables, batch, dim, rowsel, 0, lr,
+                                           global_step, ws, ws_bytes, stream);
+}
+
+int dr_ev_pool_grad_rows_apply_sgd_ex(dr_ev* const* vars, const dr_pool_grad_desc* descs,
+                                      int num_tables, int64_t batch, int dim,
+                                      const int64_t* rowsel, int rows_record, float lr,
+                                      int64_t global_step, void* ws, size_t ws_bytes,
+                                      void* stream) {
   dr::EvGuard guard_(vars, num_tables);
   using namespace dr;
   DR_REQUIRE(vars && descs && num_tables >= 1 && num_tables <= DR_MAX_GROUP, DR_INVALID_ARGUMENT,
@@ -3321,7 +3334,7 @@ int dr_ev_pool_grad_rows_apply_sgd(dr_ev* const* vars, const dr_pool_grad_desc* 
   }
   sg.bf16 = vars[0]->sh->bf16;
   return rows_apply_sgd(descs, num_tables, batch, dim, rowsel, limit, sg, ws, ws_bytes,
-                        S(stream));
+                        S(stream), rows_record);
 }
 
 int dr_ev_apply_adagrad_decay_grouped(dr_ev* const* vars, dr_ev* const* accums,

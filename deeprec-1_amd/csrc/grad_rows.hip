@@ -127,13 +127,25 @@ __device__ __forceinline__ int tab_of(const int64_t* koff, int T, int64_t i) {
   return lo;
 }
 
+// The forward's row of global position i: position order (rec_t == 0), or
+// the record-major [batch, T] rows of a one-hot training lookup
+// (DR_LOOKUP_ROWS_RECORD: rows[b * T + t], written as whole lines in output
+// order) -- position i = t * batch + b.
+__device__ __forceinline__ int64_t rowsel_at(const int64_t* rowsel, int64_t i, int rec_t,
+                                             int64_t rec_b) {
+  if (!rec_t) return rowsel[i];
+  const int64_t t = i / rec_b;
+  return rowsel[(i - t * rec_b) * rec_t + t];
+}
+
 // (also zeroes the worklist / long-run counters: they are first used after
 // the sort, two launches later)
 __global__ void rows_keys_kernel(const int64_t* __restrict__ rowsel, int64_t N, int64_t row_limit,
                                  uint32_t sentinel, uint32_t* __restrict__ kin,
                                  int32_t* __restrict__ vin, int32_t* __restrict__ flags,
                                  int32_t* __restrict__ nlong, int32_t* __restrict__ nwork,
-                                 int32_t* __restrict__ nitems, int32_t* __restrict__ nchunk) {
+                                 int32_t* __restrict__ nitems, int32_t* __restrict__ nchunk,
+                                 int rec_t, int64_t rec_b) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) {
     *nlong = 0;
@@ -142,7 +154,7 @@ __global__ void rows_keys_kernel(const int64_t* __restrict__ rowsel, int64_t N, 
     *nchunk = 0;
   }
   if (i >= N) return;
-  const int64_t r = rowsel[i];
+  const int64_t r = rowsel_at(rowsel, i, rec_t, rec_b);
   // a negative row is an EV default served because the pool was exhausted
   // (RESOURCE_EXHAUSTED already latched by the resolve): no gradient row
   kin[i] = (r >= 0 && r < row_limit) ? (uint32_t)r : sentinel;
@@ -444,7 +456,7 @@ __global__ __launch_bounds__(256) void rows_emit_kernel(
     const int64_t* __restrict__ total, int defer, int64_t* __restrict__ uniq_out,
     int64_t* __restrict__ num_unique, int32_t* __restrict__ base, uint64_t* __restrict__ gptr,
     int32_t* __restrict__ work, int32_t* __restrict__ nwork, const int64_t* __restrict__ rowsel,
-    int64_t* __restrict__ urows, int* st, int dim, float* __restrict__ gu) {
+    int64_t* __restrict__ urows, int* st, int dim, float* __restrict__ gu, int rec_t) {
   __shared__ dr_pool_grad_desc sd[DR_MAX_GROUP];
   if (threadIdx.x < T) sd[threadIdx.x] = g.d[threadIdx.x];
   __syncthreads();
@@ -468,7 +480,7 @@ __global__ __launch_bounds__(256) void rows_emit_kernel(
     const int64_t a = g.koff[t];
     const int64_t o = a + ex[i] - ex[a];
     uniq_out[o] = keys[i];
-    if (urows) urows[o] = rowsel[i];  // the row the forward resolved this id to
+    if (urows) urows[o] = rowsel_at(rowsel, i, rec_t, B);  // the row the forward resolved
     if (mk < 0) {   // one-position run
       const dr_pool_grad_desc& d = sd[t];
       const int64_t k = i - a;
@@ -1316,13 +1328,26 @@ static void launch_rows_sgd(const RowsGroup& g, int T, int64_t B, const RowsWs& 
   launch_long<4, true, WB>(g, T, dim, L, sg, s);
 }
 
+// rows_record: the forward's rows are record-major [batch, T] (every feature
+// one-hot, nnz == batch); validated here
+static int rec_tables(const dr_pool_grad_desc* descs, int T, int64_t batch, int rows_record,
+                      int* rec_t) {
+  *rec_t = 0;
+  if (!rows_record) return DR_OK;
+  for (int t = 0; t < T; ++t)
+    DR_REQUIRE(descs[t].nnz == batch && !descs[t].seg, DR_INVALID_ARGUMENT,
+               "record-major rows need one-hot features of nnz == batch (table %d)", t);
+  *rec_t = T;
+  return DR_OK;
+}
+
 // Fused row-grouped backward + KV SGD (ev.hip dr_ev_pool_grad_rows_apply_sgd
 // validates the EVs and fills sg).  Same sort and run sums as
 // dr_pool_grad_rows_grouped_ex, applied in sorted order.  Needs 16-byte rows
 // (dim % 4 == 0, aligned top_grad slices with top_stride % 4 == 0).
 int rows_apply_sgd(const dr_pool_grad_desc* descs_host, int num_tables, int64_t batch, int dim,
                    const int64_t* rowsel, int64_t row_limit, const RowsSgd& sg, void* ws,
-                   size_t ws_bytes, hipStream_t s) {
+                   size_t ws_bytes, hipStream_t s, int rows_record) {
   DR_REQUIRE(descs_host && num_tables >= 1 && num_tables <= DR_MAX_GROUP && dim > 0 &&
                  dim <= kRowsMaxDim && dim % 4 == 0 && batch >= 0 && row_limit > 0 && rowsel,
              DR_INVALID_ARGUMENT, "bad argument (the fused SGD needs dim %% 4 == 0)");
@@ -1357,9 +1382,12 @@ int rows_apply_sgd(const dr_pool_grad_desc* descs_host, int num_tables, int64_t 
   int rb = 1;
   while (rb < 32 && ((int64_t)1 << rb) <= row_limit) ++rb;
   const uint32_t sentinel = (uint32_t)(((uint64_t)1 << rb) - 1);
+  int rec_t = 0;
+  int rrc = rec_tables(descs_host, num_tables, batch, rows_record, &rec_t);
+  if (rrc) return rrc;
   hipLaunchKernelGGL(rows_keys_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, rowsel,
                      n, row_limit, sentinel, w.kin, w.vin, (int32_t*)nullptr, w.nlong, w.nwork,
-                     w.nitems, w.nchunk);
+                     w.nitems, w.nchunk, rec_t, batch);
   DR_LAUNCH_CHECK();
   int rc = sort_pairs_u32(w.kin, w.vin, w.kout, w.perm, n, rb, w.sort_ws, s);
   if (rc) return rc;
@@ -1409,6 +1437,17 @@ int dr_pool_grad_rows_grouped_ex(const dr_pool_grad_desc* descs_host, int num_ta
                                  const int64_t* keys, int defer, int64_t* uniq_out,
                                  int64_t* uniq_rows, int64_t* num_unique, uint64_t* grad_ptr,
                                  float* grad_unique, void* ws, size_t ws_bytes, void* stream) {
+  return dr_pool_grad_rows_grouped_ex2(descs_host, num_tables, batch, dim, rowsel, 0, row_limit,
+                                       keys, defer, uniq_out, uniq_rows, num_unique, grad_ptr,
+                                       grad_unique, ws, ws_bytes, stream);
+}
+
+int dr_pool_grad_rows_grouped_ex2(const dr_pool_grad_desc* descs_host, int num_tables,
+                                  int64_t batch, int dim, const int64_t* rowsel, int rows_record,
+                                  int64_t row_limit, const int64_t* keys, int defer,
+                                  int64_t* uniq_out, int64_t* uniq_rows, int64_t* num_unique,
+                                  uint64_t* grad_ptr, float* grad_unique, void* ws,
+                                  size_t ws_bytes, void* stream) {
   using namespace dr;
   DR_REQUIRE(descs_host && num_tables >= 1 && num_tables <= DR_MAX_GROUP && dim > 0 &&
                  dim <= kRowsMaxDim && batch >= 0 && row_limit > 0 && rowsel && keys &&
@@ -1450,8 +1489,11 @@ int dr_pool_grad_rows_grouped_ex(const dr_pool_grad_desc* descs_host, int num_ta
   while (rb < 32 && ((int64_t)1 << rb) <= row_limit) ++rb;   // rows < 2^rb - 1
   const uint32_t sentinel = (uint32_t)(((uint64_t)1 << rb) - 1);
   const unsigned nb = (unsigned)ceil_div(n, 256);
+  int rec_t = 0;
+  int rrc = rec_tables(descs_host, num_tables, batch, rows_record, &rec_t);
+  if (rrc) return rrc;
   hipLaunchKernelGGL(rows_keys_kernel, dim3(nb), dim3(256), 0, s, rowsel, n, row_limit, sentinel,
-                     w.kin, w.vin, w.flags, w.nlong, w.nwork, w.nitems, w.nchunk);
+                     w.kin, w.vin, w.flags, w.nlong, w.nwork, w.nitems, w.nchunk, rec_t, batch);
   DR_LAUNCH_CHECK();
   int rc = sort_pairs_u32(w.kin, w.vin, w.kout, w.perm, n, rb, w.sort_ws, s);
   if (rc) return rc;
@@ -1462,7 +1504,7 @@ int dr_pool_grad_rows_grouped_ex(const dr_pool_grad_desc* descs_host, int num_ta
   if (rc) return rc;
   hipLaunchKernelGGL(rows_emit_kernel, dim3(nb), dim3(256), 0, s, g, num_tables, batch, keys,
                      w.flags, w.ex, w.total, defer, uniq_out, num_unique, w.base, grad_ptr, w.work,
-                     w.nwork, rowsel, uniq_rows, st, dim, grad_unique);
+                     w.nwork, rowsel, uniq_rows, st, dim, grad_unique, rec_t);
   DR_LAUNCH_CHECK();
   if (aligned) {
     const int d4 = dim / 4;

@@ -280,6 +280,243 @@ static int seq_vec(int H, uintptr_t ptrs) {
   return 0;
 }
 
+
+// ---------------------------------------------------------------------------
+// DIN attention MLP, fused (utils.py:284-289: din_all -> f1_att 80 sigmoid ->
+// f2_att 40 sigmoid -> f3_att 1).  With W1 = [A | Bm | C | Dm] over din_all =
+// [q, f, q - f, q * f]:
+//   a1 = (A + C) q + b1  +  [Bm - C | Dm] [f ; q * f]
+// the first term is per SAMPLE (cq, computed once), the second per position
+// with the 80 x 2H matrix W1p -- half the multiply-adds of din_all's 4H, and
+// din_all [B, T, 4H] is never written.  Only the valid (mask != 0) history
+// positions run the MLP: a padded position's score is replaced by the
+// padding value before the softmax (utils.py:290-292), so its MLP output and
+// gradient are dead (about half of a batch padded to its longest history).
+// One lane per position, the weights uniform across the wave (scalar loads);
+// activations stored feature-major ([unit][cap]: coalesced) for the
+// backward and the weight-gradient GEMMs.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// W1p = [Bm - C | Dm] [n1][2H], W2T = W2^T [n1][n2], cq = (A + C) q + b1 [B][n1]
+__global__ void din_mlp_prep_kernel(const float* __restrict__ w1, const float* __restrict__ b1,
+                                    const float* __restrict__ w2, const float* __restrict__ q,
+                                    int64_t B, int H, int n1, int n2, float* __restrict__ w1p,
+                                    float* __restrict__ w2t, float* __restrict__ cq) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t np = (int64_t)n1 * 2 * H, nt = (int64_t)n1 * n2;
+  if (i < np) {
+    const int j = (int)(i / (2 * H)), k = (int)(i % (2 * H));
+    const float* r = w1 + (int64_t)j * 4 * H;
+    w1p[i] = k < H ? r[H + k] - r[2 * H + k] : r[3 * H + (k - H)];
+  } else if (i < np + nt) {
+    const int64_t e = i - np;
+    const int j = (int)(e / n2), m = (int)(e % n2);
+    w2t[e] = w2[(int64_t)m * n1 + j];
+  } else if (i < np + nt + B * n1) {
+    const int64_t e = i - np - nt;
+    const int64_t b = e / n1;
+    const int j = (int)(e % n1);
+    const float* r = w1 + (int64_t)j * 4 * H;
+    const float* qb = q + b * H;
+    float acc = b1[j];
+    for (int k = 0; k < H; ++k) acc = fmaf(r[k] + r[2 * H + k], qb[k], acc);
+    cq[e] = acc;
+  }
+}
+
+// valid positions per sample (one wave per sample): cnt[b]
+__global__ void din_mlp_count_kernel(const float* __restrict__ mask, int64_t B, int64_t T,
+                                     int32_t* __restrict__ cnt) {
+  const int64_t b = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
+  const int lane = threadIdx.x & 63;
+  if (b >= B) return;
+  int c = 0;
+  for (int64_t t = lane; t < T; t += 64) c += mask[b * T + t] != 0.f;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if (lane == 0) cnt[b] = c;
+}
+
+// off = exclusive scan of cnt (off[B] = P); one block, serial over its
+// 1024-sample windows (B is a batch: thousands)
+__global__ __launch_bounds__(1024) void din_mlp_scan_kernel(const int32_t* __restrict__ cnt,
+                                                             int64_t B, int32_t* __restrict__ off) {
+  __shared__ int32_t ws[16];
+  __shared__ int32_t carry;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (int64_t b0 = 0; b0 < B; b0 += 1024) {
+    const int64_t b = b0 + tid;
+    const int v = b < B ? cnt[b] : 0;
+    int incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    if (lane == 63) ws[wv] = incl;
+    __syncthreads();
+    int before = carry;
+    for (int w = 0; w < wv; ++w) before += ws[w];
+    if (b < B) off[b] = before + incl - v;
+    __syncthreads();
+    if (tid == 1023) carry = before + incl;
+    __syncthreads();
+  }
+  if (tid == 0) off[B] = carry;
+}
+
+// pos[off[b] + r] = b * T + t for the r-th valid position t of sample b
+__global__ void din_mlp_pos_kernel(const float* __restrict__ mask, int64_t B, int64_t T,
+                                   const int32_t* __restrict__ off, int32_t* __restrict__ pos) {
+  const int64_t b = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
+  const int lane = threadIdx.x & 63;
+  if (b >= B) return;
+  int base = off[b];
+  for (int64_t t0 = 0; t0 < T; t0 += 64) {
+    const int64_t t = t0 + lane;
+    const bool v = t < T && mask[b * T + t] != 0.f;
+    const uint64_t m = __ballot(v);
+    if (v) pos[base + __popcll(m & lanemask_lt())] = (int32_t)(b * T + t);
+    base += __popcll(m);
+  }
+}
+
+// forward: one lane per valid position p < P (= off[B]); lanes past P exit
+template <int H, int N1, int N2>
+__global__ __launch_bounds__(256) void din_mlp_fwd_kernel(
+    const int32_t* __restrict__ pos, const int32_t* __restrict__ off, int64_t B, int64_t T,
+    int64_t cap, const float* __restrict__ facts, const float* __restrict__ q,
+    const float* __restrict__ cq, const float* __restrict__ w1p, const float* __restrict__ w2t,
+    const float* __restrict__ b2, const float* __restrict__ w3, const float* __restrict__ b3,
+    float* __restrict__ scores, float* __restrict__ h1t, float* __restrict__ h2t) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t P = off[B];
+  if ((int64_t)blockIdx.x * blockDim.x >= P) return;   // whole blocks past the count
+  const int64_t pc = p < P ? p : P - 1;                 // (clamped: loads stay valid)
+  const int64_t bt = pos[pc];
+  const int64_t b = bt / T;
+  float x[2 * H];
+  const float* fr = facts + bt * H;
+  const float* qr = q + b * H;
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    const float f = fr[k];
+    x[k] = f;
+    x[H + k] = qr[k] * f;
+  }
+  float a2[N2];
+#pragma unroll
+  for (int m = 0; m < N2; ++m) a2[m] = 0.f;
+  const float* cqb = cq + b * N1;
+  for (int j = 0; j < N1; ++j) {
+    float acc = cqb[j];
+    const float* wr = w1p + j * 2 * H;
+#pragma unroll
+    for (int k = 0; k < 2 * H; ++k) acc = fmaf(wr[k], x[k], acc);
+    const float h = sigm(acc);
+    if (p < P) h1t[(int64_t)j * cap + p] = h;
+    const float* vr = w2t + j * N2;
+#pragma unroll
+    for (int m = 0; m < N2; ++m) a2[m] = fmaf(vr[m], h, a2[m]);
+  }
+  float s = b3[0];
+#pragma unroll
+  for (int m = 0; m < N2; ++m) {
+    const float h = sigm(a2[m] + b2[m]);
+    if (p < P) h2t[(int64_t)m * cap + p] = h;
+    s = fmaf(w3[m], h, s);
+  }
+  if (p < P) scores[bt] = s;
+}
+
+// backward: one lane per position p < cap.  p < P: the MLP backward from the
+// score gradient; the facts gradient (already holding the pool's) gains
+// d f + q * d(q f); per-position buffers for the weight-gradient GEMMs and the
+// per-sample sums.  P <= p < cap: zero columns (the GEMMs run over cap).
+template <int H, int N1, int N2>
+__global__ __launch_bounds__(256) void din_mlp_bwd_kernel(
+    const int32_t* __restrict__ pos, const int32_t* __restrict__ off, int64_t B, int64_t T,
+    int64_t cap, const float* __restrict__ facts, const float* __restrict__ q,
+    const float* __restrict__ w1p, const float* __restrict__ w2t, const float* __restrict__ w3,
+    const float* __restrict__ gscores, const float* __restrict__ h1t,
+    const float* __restrict__ h2t, float* __restrict__ gfacts, float* __restrict__ da1t,
+    float* __restrict__ da2t, float* __restrict__ xt, float* __restrict__ dsc,
+    float* __restrict__ dqp) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= cap) return;
+  const int64_t P = off[B];
+  if (p >= P) {
+#pragma unroll 8
+    for (int j = 0; j < N1; ++j) da1t[(int64_t)j * cap + p] = 0.f;
+#pragma unroll 8
+    for (int m = 0; m < N2; ++m) da2t[(int64_t)m * cap + p] = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < 2 * H; ++k) xt[(int64_t)k * cap + p] = 0.f;
+    dsc[p] = 0.f;
+    return;
+  }
+  const int64_t bt = pos[p];
+  const int64_t b = bt / T;
+  const float ds = gscores[bt];
+  dsc[p] = ds;
+  float da2[N2];
+#pragma unroll
+  for (int m = 0; m < N2; ++m) {
+    const float h = h2t[(int64_t)m * cap + p];
+    da2[m] = ds * w3[m] * (1.f - h) * h;
+    da2t[(int64_t)m * cap + p] = da2[m];
+  }
+  float dx[2 * H];
+#pragma unroll
+  for (int k = 0; k < 2 * H; ++k) dx[k] = 0.f;
+  for (int j = 0; j < N1; ++j) {
+    const float* vr = w2t + j * N2;
+    float dh = 0.f;
+#pragma unroll
+    for (int m = 0; m < N2; ++m) dh = fmaf(vr[m], da2[m], dh);
+    const float h = h1t[(int64_t)j * cap + p];
+    const float da = dh * (1.f - h) * h;
+    da1t[(int64_t)j * cap + p] = da;
+    const float* wr = w1p + j * 2 * H;
+#pragma unroll
+    for (int k = 0; k < 2 * H; ++k) dx[k] = fmaf(wr[k], da, dx[k]);
+  }
+  const float* fr = facts + bt * H;
+  const float* qr = q + b * H;
+  float* gr = gfacts + bt * H;
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    const float f = fr[k], qk = qr[k];
+    xt[(int64_t)k * cap + p] = f;
+    xt[(int64_t)(H + k) * cap + p] = qk * f;
+    gr[k] = gr[k] + (dx[k] + qk * dx[H + k]);
+    dqp[(int64_t)k * cap + p] = f * dx[H + k];
+  }
+}
+
+// per sample b: s1[b] = sum of da1 over its positions, dq2[b] = sum of the
+// q-side terms f * d(q f) (ascending position order); one wave per sample
+template <int H, int N1>
+__global__ void din_mlp_sample_kernel(const int32_t* __restrict__ off, int64_t B, int64_t cap,
+                                      const float* __restrict__ da1t,
+                                      const float* __restrict__ dqp, float* __restrict__ s1,
+                                      float* __restrict__ dq2) {
+  const int64_t b = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
+  const int lane = threadIdx.x & 63;
+  if (b >= B) return;
+  const int64_t p0 = off[b], p1 = off[b + 1];
+  for (int j = lane; j < N1 + H; j += 64) {
+    const float* src = j < N1 ? da1t + (int64_t)j * cap : dqp + (int64_t)(j - N1) * cap;
+    float acc = 0.f;
+    for (int64_t p = p0; p < p1; ++p) acc += src[p];
+    if (j < N1)
+      s1[b * N1 + j] = acc;
+    else
+      dq2[b * H + (j - N1)] = acc;
+  }
+}
+
 }  // namespace dr
 
 extern "C" {
@@ -380,6 +617,78 @@ int dr_din_attention_pool_grad(const float* alphas, const float* mask, const flo
     hipLaunchKernelGGL(din_pool_grad_kernel<1>, dim3((unsigned)batch), dim3(64), lds, S(stream),
                        alphas, mask, facts, grad_att, grad_sum, seq_len, hidden, grad_scores,
                        grad_facts);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+
+// ---- fused DIN attention MLP -------------------------------------------------
+#define DR_DIN_MLP_SHAPES(X) X(16) X(32) X(36) X(64)
+
+int dr_din_mlp_forward(const float* query, const float* facts, const float* mask, int64_t batch,
+                       int64_t seq_len, int hidden, const float* w1, const float* b1, int n1,
+                       const float* w2, const float* b2, int n2, const float* w3, const float* b3,
+                       float* scores, const dr_din_mlp_buf* buf, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && seq_len >= 1 && hidden > 0 && buf, DR_INVALID_ARGUMENT, "bad shape");
+  DR_REQUIRE(n1 == 80 && n2 == 40, DR_INVALID_ARGUMENT,
+             "dr_din_mlp_forward: the reference's 80 / 40 attention units");
+  DR_REQUIRE(hidden == 16 || hidden == 32 || hidden == 36 || hidden == 64, DR_INVALID_ARGUMENT,
+             "dr_din_mlp_forward: hidden %d not built (16, 32, 36, 64)", hidden);
+  DR_REQUIRE(batch * seq_len < (1ll << 31), DR_INVALID_ARGUMENT, "batch * seq_len must be < 2^31");
+  if (batch == 0) return DR_OK;
+  DR_REQUIRE(query && facts && mask && w1 && b1 && w2 && b2 && w3 && b3 && scores && buf->pos &&
+                 buf->off && buf->cnt && buf->w1p && buf->w2t && buf->cq && buf->h1t && buf->h2t,
+             DR_INVALID_ARGUMENT, "null operand");
+  hipStream_t st = S(stream);
+  const int64_t cap = batch * seq_len;
+  const int64_t prep = (int64_t)n1 * 2 * hidden + (int64_t)n1 * n2 + batch * n1;
+  hipLaunchKernelGGL(din_mlp_prep_kernel, dim3((unsigned)ceil_div(prep, 256)), dim3(256), 0, st,
+                     w1, b1, w2, query, batch, hidden, n1, n2, buf->w1p, buf->w2t, buf->cq);
+  const unsigned sb = (unsigned)ceil_div(batch, 4);
+  hipLaunchKernelGGL(din_mlp_count_kernel, dim3(sb), dim3(256), 0, st, mask, batch, seq_len,
+                     buf->cnt);
+  hipLaunchKernelGGL(din_mlp_scan_kernel, dim3(1), dim3(1024), 0, st, buf->cnt, batch, buf->off);
+  hipLaunchKernelGGL(din_mlp_pos_kernel, dim3(sb), dim3(256), 0, st, mask, batch, seq_len,
+                     buf->off, buf->pos);
+  const unsigned pb = (unsigned)ceil_div(cap, 256);
+#define DR_FWD(HH)                                                                            \
+  if (hidden == HH)                                                                           \
+    hipLaunchKernelGGL((din_mlp_fwd_kernel<HH, 80, 40>), dim3(pb), dim3(256), 0, st, buf->pos, \
+                       buf->off, batch, seq_len, cap, facts, query, buf->cq, buf->w1p,        \
+                       buf->w2t, b2, w3, b3, scores, buf->h1t, buf->h2t);
+  DR_DIN_MLP_SHAPES(DR_FWD)
+#undef DR_FWD
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_din_mlp_backward(const float* query, const float* facts, int64_t batch, int64_t seq_len,
+                        int hidden, int n1, int n2, const float* w3, const float* grad_scores,
+                        float* grad_facts, const dr_din_mlp_buf* buf, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && seq_len >= 1 && buf && n1 == 80 && n2 == 40 &&
+                 (hidden == 16 || hidden == 32 || hidden == 36 || hidden == 64),
+             DR_INVALID_ARGUMENT, "bad shape");
+  if (batch == 0) return DR_OK;
+  DR_REQUIRE(query && facts && w3 && grad_scores && grad_facts && buf->da1t && buf->da2t &&
+                 buf->xt && buf->dsc && buf->dqp && buf->s1 && buf->dq2,
+             DR_INVALID_ARGUMENT, "null operand");
+  hipStream_t st = S(stream);
+  const int64_t cap = batch * seq_len;
+  const unsigned pb = (unsigned)ceil_div(cap, 256);
+  const unsigned sb = (unsigned)ceil_div(batch, 4);
+#define DR_BWD(HH)                                                                              \
+  if (hidden == HH) {                                                                           \
+    hipLaunchKernelGGL((din_mlp_bwd_kernel<HH, 80, 40>), dim3(pb), dim3(256), 0, st, buf->pos,   \
+                       buf->off, batch, seq_len, cap, facts, query, buf->w1p, buf->w2t, w3,     \
+                       grad_scores, buf->h1t, buf->h2t, grad_facts, buf->da1t, buf->da2t,       \
+                       buf->xt, buf->dsc, buf->dqp);                                            \
+    hipLaunchKernelGGL((din_mlp_sample_kernel<HH, 80>), dim3(sb), dim3(256), 0, st, buf->off,    \
+                       batch, cap, buf->da1t, buf->dqp, buf->s1, buf->dq2);                     \
+  }
+  DR_DIN_MLP_SHAPES(DR_BWD)
+#undef DR_BWD
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

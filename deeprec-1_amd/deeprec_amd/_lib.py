@@ -27,6 +27,7 @@ POOL_BF16 = 2
 POOL_OUT_BF16 = 4
 LOOKUP_OUT_BF16 = 1
 LOOKUP_TABLE_ORDER = 2
+LOOKUP_ROWS_RECORD = 4
 
 
 class DeepRecError(RuntimeError):
@@ -92,6 +93,13 @@ class DrCommOps(C.Structure):
     _fields_ = [("user", C.c_void_p), ("all_to_all_v", COMM_A2A_FN)]
 
 
+class DrDinMlpBuf(C.Structure):
+    """dr_din_mlp_buf (include/deeprec_amd.h): the fused DIN attention MLP's
+    caller-owned buffers."""
+    _fields_ = [(n, C.c_void_p) for n in ("pos", "cnt", "off", "w1p", "w2t", "cq", "h1t", "h2t",
+                                          "da1t", "da2t", "xt", "dsc", "dqp", "s1", "dq2")]
+
+
 RCCL_UNIQUE_ID_BYTES = 128
 SHARDED_OUT_BF16 = 1
 
@@ -135,6 +143,8 @@ SIGNATURES = {
                                          _P, _SZ, _P]),
     "dr_pool_grad_rows_grouped_ex": (_I32, [_P, _I32, _I64, _I32, _P, _I64, _P, _I32, _P, _P, _P,
                                             _P, _P, _P, _SZ, _P]),
+    "dr_pool_grad_rows_grouped_ex2": (_I32, [_P, _I32, _I64, _I32, _P, _I32, _I64, _P, _I32, _P,
+                                             _P, _P, _P, _P, _P, _SZ, _P]),
     "dr_rows_from_ptr": (_I32, [_P, _I64, _P, _I32, _P, _P]),
     "dr_pool_grad": (_I32, [_P, _I64, _I64, _I32, _P, _P, _P, _I64, _P, _I32, _P, _P, _SZ, _P]),
     "dr_ev_create": (_I32, [_P, _P, _P]),
@@ -191,6 +201,8 @@ SIGNATURES = {
     "dr_ev_pool_grad_rows_sgd_workspace_size": (_SZ, [_I64, _I32]),
     "dr_ev_pool_grad_rows_apply_sgd": (_I32, [_P, _P, _I32, _I64, _I32, _P, _F32, _I64, _P, _SZ,
                                               _P]),
+    "dr_ev_pool_grad_rows_apply_sgd_ex": (_I32, [_P, _P, _I32, _I64, _I32, _P, _I32, _F32, _I64,
+                                                 _P, _SZ, _P]),
     "dr_ev_apply_adam_async_grouped": (_I32, [_I32, _I32, _P, _P, _P, _I32, _P, _P, _P, _P, _P,
                                               _F32, _F32, _F32, _F32, _I64, _P]),
     "dr_ev_apply_adagrad_decay_grouped": (_I32, [_P, _P, _P, _I32, _P, _I32, _P, _P, _P, _F32,
@@ -279,6 +291,9 @@ SIGNATURES = {
     "dr_din_attention_input_grad": (_I32, [_P, _P, _P, _I64, _I64, _I32, _P, _P, _I32, _P]),
     "dr_din_attention_pool": (_I32, [_P, _P, _P, _I64, _I64, _I32, _P, _P, _P, _P]),
     "dr_din_attention_pool_grad": (_I32, [_P, _P, _P, _P, _P, _I64, _I64, _I32, _P, _P, _P]),
+    "dr_din_mlp_forward": (_I32, [_P, _P, _P, _I64, _I64, _I32, _P, _P, _I32, _P, _P, _I32, _P,
+                                  _P, _P, _P, _P]),
+    "dr_din_mlp_backward": (_I32, [_P, _P, _I64, _I64, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "dr_fingerprint64": (_I32, [_P, _P, _I64, _P, _P]),
     "dr_string_to_hash_bucket_fast": (_I32, [_P, _P, _I64, _I64, _P, _P]),
     "dr_crc32c_extend": (C.c_uint32, [C.c_uint32, _P, _SZ]),

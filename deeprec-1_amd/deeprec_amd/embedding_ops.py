@@ -478,11 +478,12 @@ class _RowGroup(object):
     IndexedSlices.grad_ptr) so the optimizer reads the pooled gradient in
     place."""
 
-    def __init__(self, feats, vals, rowsel, koff):
+    def __init__(self, feats, vals, rowsel, koff, rows_record=False):
         self.feats = feats
         self.vals = vals
         self.rowsel = rowsel
         self.koff = koff
+        self.rows_record = rows_record   # rowsel record-major [B, T] (DR_LOOKUP_ROWS_RECORD)
 
     def grads(self, g, cols, top_stride):
         dev = g.device
@@ -515,6 +516,9 @@ class _RowGroup(object):
             return [PendingRowSlices(pend, t, D) for t in range(T)]
         return pend.materialize()
 
+
+# record-major row records of the one-hot training lookup (A/B switch)
+_ROWS_RECORD = os.environ.get("DR_ROWS_RECORD", "1") != "0"
 
 # SGD applies of row-grouped backwards fused with the backward (A/B switch)
 _FUSED_SGD = os.environ.get("DR_ROWS_FUSED_SGD", "1") != "0"
@@ -561,10 +565,10 @@ class _RowsPending(object):
         limit = max(lib().dr_ev_row_capacity(f.params.handle) for f in grp.feats)
         wsb = lib().dr_pool_grad_rows_workspace_size(n)
         ws = workspace(wsb, dev)
-        check(lib().dr_pool_grad_rows_grouped_ex(
-            self.descs, T, grp.feats[0].batch, D, ptr(grp.rowsel), max(int(limit), 1),
-            ptr(grp.vals), 1, ptr(uniq), ptr(urows), ptr(U), ptr(gptr), ptr(gu), ptr(ws), wsb,
-            stream_handle(dev)))
+        check(lib().dr_pool_grad_rows_grouped_ex2(
+            self.descs, T, grp.feats[0].batch, D, ptr(grp.rowsel), int(grp.rows_record),
+            max(int(limit), 1), ptr(grp.vals), 1, ptr(uniq), ptr(urows), ptr(U), ptr(gptr),
+            ptr(gu), ptr(ws), wsb, stream_handle(dev)))
         ops._post(dev)
         k = grp.koff
         return [IndexedSlices(None, uniq[k[t]:k[t + 1]], U[t:t + 1], True,
@@ -580,9 +584,9 @@ class _RowsPending(object):
         wsb = lib().dr_ev_pool_grad_rows_sgd_workspace_size(n, self.D)
         ws = workspace(wsb, self.dev)
         P = C.c_void_p * T
-        check(lib().dr_ev_pool_grad_rows_apply_sgd(
+        check(lib().dr_ev_pool_grad_rows_apply_sgd_ex(
             P(*[e.handle.value for e in self.evs]), self.descs, T, grp.feats[0].batch, self.D,
-            ptr(grp.rowsel), lr, global_step, ptr(ws), wsb, stream))
+            ptr(grp.rowsel), int(grp.rows_record), lr, global_step, ptr(ws), wsb, stream))
         ops._post(self.dev)
         self.applied = True
         self.keep = ()
@@ -732,12 +736,18 @@ def _fused_onehot(feats, order, with_rows=False, out_dtype=None):
         flags |= _lib.LOOKUP_TABLE_ORDER
     if with_rows:
         rowsel = torch.empty(T * B, dtype=torch.int64, device=dev)
+        # the row records record-major [B, T] (whole lines in output order;
+        # the backward reads them strided): A/B switch DR_ROWS_RECORD=0
+        rec = _ROWS_RECORD and not (flags & _lib.LOOKUP_TABLE_ORDER)
+        if rec:
+            flags |= _lib.LOOKUP_ROWS_RECORD
         check(lib().dr_ev_lookup_onehot_ex(handles, T, ptr(vals), 1, B, B, ptr(out), T * D, order,
                                            flags, ptr(rowsel), ptr(ws), wsb, stream_handle(dev)))
-        group = _RowGroup(feats, vals, rowsel, koff)
+        group = _RowGroup(feats, vals, rowsel, koff, rows_record=rec)
         for t, f in enumerate(feats):
             f.uniq = f.idx = f.rows = f.U = f.defaults = None
-            f.rowsel = rowsel[koff[t]:koff[t + 1]]
+            # (a per-feature slice exists only in position order)
+            f.rowsel = None if rec else rowsel[koff[t]:koff[t + 1]]
             f.group = group
     else:
         check(lib().dr_ev_lookup_onehot_ex(handles, T, ptr(vals), 1, B, B, ptr(out), T * D, order,

@@ -537,6 +537,34 @@ class DinAttentionPool(torch.autograd.Function):
         return gs, None, gf
 
 
+class DinAttentionFused(torch.autograd.Function):
+    """The whole attention of din_attention (utils.py:264-309, mode 'SUM')
+    as one node: the fused MLP (dr_din_mlp_forward: din_all never written,
+    only the valid positions) -> masked softmax + weighted sum + history sum
+    (dr_din_attention_pool); backward: pool grad -> dr_din_mlp_backward (the
+    MLP's facts / query gradients and per-position buffers) -> the weight
+    gradients as split-K GEMMs."""
+
+    @staticmethod
+    def forward(ctx, query, facts, mask, w1, b1, w2, b2, w3, b3):
+        scores, buf = ops.din_mlp_forward(query, facts, mask, w1, b1, w2, b2, w3, b3)
+        att, his_sum, alphas = ops.din_attention_pool(scores, mask, facts)
+        ctx.save_for_backward(query, facts, mask, w1, w3, alphas)
+        ctx.buf = buf
+        return att, his_sum
+
+    @staticmethod
+    def backward(ctx, g_att, g_sum):
+        query, facts, mask, w1, w3, alphas = ctx.saved_tensors
+        if g_att is None:
+            g_att = torch.zeros(facts.shape[0], facts.shape[2], device=facts.device)
+        gs, gf = ops.din_attention_pool_grad(alphas, mask, facts, g_att, g_sum)
+        gq, dW1, db1, dW2, db2, dw3, db3 = ops.din_mlp_backward(query, facts, w1, w3, ctx.buf,
+                                                                 gs, gf)
+        ctx.buf = None
+        return gq, gf, None, dW1, db1, dW2, db2, dw3, db3
+
+
 class WDL(torch.nn.Module):
     """modelzoo/WDL/train.py WDL (BASELINE configs[0]) on EVs.
 
@@ -933,17 +961,26 @@ class DIN(torch.nn.Module):
         self.uid_lookup = _OneHotLookup([uid_ev])
         self.item_lookup = _OneHotLookup([mid_ev, cat_ev])
 
+    # the attention as one fused node (DinAttentionFused); A/B switch
+    # DR_DIN_FUSED_ATTENTION=0 = din_all + library GEMMs + elementwise sigmoids
+    fused_attention = os.environ.get("DR_DIN_FUSED_ATTENTION", "1") != "0"
+
     def forward(self, uids, mids, cats, mid_his, cat_his, mask):
         B, T = mid_his.shape
         uid_e = self.uid_lookup(uids.reshape(1, B))
         item_eb = self.item_lookup(torch.stack([mids, cats]))                    # [B, 2D]
         his = torch.stack([mid_his.reshape(-1), cat_his.reshape(-1)])
         facts = self.item_lookup(his).view(B, T, -1)                              # [B, T, 2D]
-        din_all = DinAttentionInput.apply(item_eb, facts)                         # [B, T, 4H]
-        h = torch.sigmoid(self.f1_att(din_all))
-        h = torch.sigmoid(self.f2_att(h))
-        scores = self.f3_att(h).view(B, T)
-        att, his_sum = DinAttentionPool.apply(scores, mask, facts)
+        if self.fused_attention and facts.shape[2] in ops.DIN_MLP_HIDDEN:
+            att, his_sum = DinAttentionFused.apply(
+                item_eb, facts, mask, self.f1_att.weight, self.f1_att.bias, self.f2_att.weight,
+                self.f2_att.bias, self.f3_att.weight, self.f3_att.bias)
+        else:
+            din_all = DinAttentionInput.apply(item_eb, facts)                     # [B, T, 4H]
+            h = torch.sigmoid(self.f1_att(din_all))
+            h = torch.sigmoid(self.f2_att(h))
+            scores = self.f3_att(h).view(B, T)
+            att, his_sum = DinAttentionPool.apply(scores, mask, facts)
         inp = torch.cat([uid_e, item_eb, his_sum, item_eb * his_sum, att], -1)
         bn = inp * (1.0 / (1.0 + 1e-3) ** 0.5) * self.bn1_gamma + self.bn1_beta
         x = self.dice_1(self.dnn1(bn))

@@ -5,6 +5,7 @@ Data-dependent errors (OP_REQUIRES in the reference) are latched on the
 device; call `status_check()` or enable `set_validate(True)` to have every op
 synchronise and raise, which is what the parity tests do.
 """
+import ctypes as C
 import os
 
 import torch
@@ -826,6 +827,98 @@ def din_attention_input_grad(query, facts, top_grad, grad_facts=None):
                                             ptr(grad_facts), int(acc), stream_handle(dev)))
     _post(dev)
     return gq, grad_facts
+
+
+DIN_MLP_HIDDEN = (16, 32, 36, 64)
+
+
+class DinMlpBuffers(object):
+    """The fused DIN attention MLP's buffers (dr_din_mlp_buf) for one step:
+    forward state kept for the backward, backward outputs the weight
+    gradients are formed from.  cap = batch * seq_len (no host read of the
+    valid-position count: columns past it are zero in the backward)."""
+
+    def __init__(self, B, T, H, n1, n2, dev):
+        cap = B * T
+        i32, f32 = torch.int32, torch.float32
+        e = lambda shape, dt=f32: torch.empty(shape, dtype=dt, device=dev)  # noqa: E731
+        self.pos, self.cnt, self.off = e(cap, i32), e(B, i32), e(B + 1, i32)
+        self.w1p, self.w2t, self.cq = e((n1, 2 * H)), e((n1, n2)), e((B, n1))
+        self.h1t, self.h2t = e((n1, cap)), e((n2, cap))
+        self.da1t = self.da2t = self.xt = self.dsc = self.dqp = self.s1 = self.dq2 = None
+        self.B, self.T, self.H, self.n1, self.n2, self.cap = B, T, H, n1, n2, cap
+
+    def alloc_backward(self, dev):
+        B, H, n1, n2, cap = self.B, self.H, self.n1, self.n2, self.cap
+        e = lambda shape: torch.empty(shape, dtype=torch.float32, device=dev)  # noqa: E731
+        self.da1t, self.da2t, self.xt = e((n1, cap)), e((n2, cap)), e((2 * H, cap))
+        self.dsc, self.dqp, self.s1, self.dq2 = e(cap), e((H, cap)), e((B, n1)), e((B, H))
+
+    def struct(self):
+        names = [f[0] for f in _lib.DrDinMlpBuf._fields_]
+        return _lib.DrDinMlpBuf(*[ptr(getattr(self, n)) for n in names])
+
+
+def din_mlp_forward(query, facts, mask, w1, b1, w2, b2, w3, b3):
+    """Fused attention MLP (dr_din_mlp_forward): scores [B, T] at the valid
+    positions (the padded ones are 0 here and masked by the pool), and the
+    buffers its backward needs."""
+    dev = _dev(facts)
+    B, T, H = facts.shape
+    n1, n2 = w1.shape[0], w2.shape[0]
+    q, f, m = _c(query, torch.float32), _c(facts, torch.float32), _c(mask, torch.float32)
+    w1c, b1c, w2c, b2c = (_c(x, torch.float32) for x in (w1, b1, w2, b2))
+    w3c, b3c = _c(w3.reshape(-1), torch.float32), _c(b3.reshape(-1), torch.float32)
+    buf = DinMlpBuffers(B, T, H, n1, n2, dev)
+    scores = torch.zeros((B, T), dtype=torch.float32, device=dev)
+    st = buf.struct()
+    check(lib().dr_din_mlp_forward(ptr(q), ptr(f), ptr(m), B, T, H, ptr(w1c), ptr(b1c), n1,
+                                   ptr(w2c), ptr(b2c), n2, ptr(w3c), ptr(b3c), ptr(scores),
+                                   C.byref(st), stream_handle(dev)))
+    _post(dev)
+    return scores, buf
+
+
+def din_mlp_backward(query, facts, w1, w3, buf, grad_scores, grad_facts):
+    """Backward of din_mlp_forward: adds the MLP's part to grad_facts (in
+    place) and returns (grad_query, dW1, db1, dW2, db2, dw3, db3); the weight
+    gradients are split-K GEMMs over the feature-major per-position buffers
+    (columns past the valid count are zero)."""
+    dev = _dev(facts)
+    B, T, H = facts.shape
+    n1, n2, cap = buf.n1, buf.n2, buf.cap
+    q, f = _c(query, torch.float32), _c(facts, torch.float32)
+    w3c = _c(w3.reshape(-1), torch.float32)
+    gs = _c(grad_scores, torch.float32)
+    if not grad_facts.is_contiguous() or grad_facts.dtype != torch.float32:
+        raise ValueError("grad_facts must be a contiguous fp32 tensor")
+    buf.alloc_backward(dev)
+    st = buf.struct()
+    check(lib().dr_din_mlp_backward(ptr(q), ptr(f), B, T, H, n1, n2, ptr(w3c), ptr(gs),
+                                    ptr(grad_facts), C.byref(st), stream_handle(dev)))
+    _post(dev)
+    S = 64
+    while S > 1 and cap % S:
+        S //= 2
+    L = cap // S
+
+    def kred(a_t, b_t):   # a_t [M, cap], b_t [N, cap] -> a_t b_t^T, split over cap
+        M, N = a_t.shape[0], b_t.shape[0]
+        return torch.bmm(a_t.view(M, S, L).transpose(0, 1),
+                         b_t.view(N, S, L).permute(1, 2, 0)).sum(0)
+    w1f = w1.float()
+    A, Cm = w1f[:, :H], w1f[:, 2 * H:3 * H]
+    gq = buf.s1 @ (A + Cm) + buf.dq2
+    Gq = buf.s1.t() @ q
+    G = kred(buf.da1t, buf.xt)
+    Gf, Gqf = G[:, :H], G[:, H:]
+    dW1 = torch.cat([Gq, Gf, Gq - Gf, Gqf], 1)
+    db1 = buf.s1.sum(0)
+    dW2 = kred(buf.da2t, buf.h1t)
+    db2 = buf.da2t.sum(1)
+    dw3 = (buf.h2t @ buf.dsc).view(1, n2)
+    db3 = buf.dsc.sum().view(1)
+    return gq, dW1, db1, dW2, db2, dw3, db3
 
 
 def din_attention_pool(scores, mask, facts, with_sum=True):

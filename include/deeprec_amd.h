@@ -284,6 +284,14 @@ int dr_pool_grad_rows_grouped_ex(const dr_pool_grad_desc* descs_host, int num_ta
                                  const int64_t* keys, int defer, int64_t* uniq_out,
                                  int64_t* uniq_rows, int64_t* num_unique, uint64_t* grad_ptr,
                                  float* grad_unique, void* ws, size_t ws_bytes, void* stream);
+/* rows_record = 1: rowsel is the record-major [batch, T] of a one-hot      */
+/* training lookup with DR_LOOKUP_ROWS_RECORD (every feature nnz == batch). */
+int dr_pool_grad_rows_grouped_ex2(const dr_pool_grad_desc* descs_host, int num_tables,
+                                  int64_t batch, int dim, const int64_t* rowsel, int rows_record,
+                                  int64_t row_limit, const int64_t* keys, int defer,
+                                  int64_t* uniq_out, int64_t* uniq_rows, int64_t* num_unique,
+                                  uint64_t* grad_ptr, float* grad_unique, void* ws,
+                                  size_t ws_bytes, void* stream);
 /* out[i] = row at grad_ptr[i] (+0.0f first when bit 0 is set) for i <      */
 /* min(n, *n_dev) (n_dev DEVICE or NULL); later rows are not written.        */
 int dr_rows_from_ptr(const uint64_t* grad_ptr, int64_t n, const int64_t* n_dev, int dim,
@@ -453,6 +461,11 @@ int dr_ev_lookup_onehot_strided(dr_ev* const* evs, int num_tables, const int64_t
 /* (key_stride_table = B) the id reads and the rows_out records ([T, B])    */
 /* become contiguous instead of one 8-byte access per 128-byte line.        */
 #define DR_LOOKUP_TABLE_ORDER 2
+/* DR_LOOKUP_ROWS_RECORD: rows_out record-major, rows_out[b*T + t] -- the     */
+/* slots of a wave are consecutive in output order, so the records leave as  */
+/* whole 64-byte writes instead of one partial line per table; pass          */
+/* rows_record = 1 to the row-grouped backward (_ex2 / _sgd_ex) with them.   */
+#define DR_LOOKUP_ROWS_RECORD 4
 int dr_ev_lookup_onehot_ex(dr_ev* const* evs, int num_tables, const int64_t* keys,
                            int64_t key_stride_bag, int64_t key_stride_table, int64_t batch,
                            void* out, int64_t out_stride, int order, int flags, int64_t* rows_out,
@@ -583,6 +596,12 @@ int dr_ev_pool_grad_rows_apply_sgd(dr_ev* const* vars, const dr_pool_grad_desc* 
                                    int num_tables, int64_t batch, int dim, const int64_t* rowsel,
                                    float lr, int64_t global_step, void* ws, size_t ws_bytes,
                                    void* stream);
+/* The same with record-major rows (rows_record = 1, DR_LOOKUP_ROWS_RECORD). */
+int dr_ev_pool_grad_rows_apply_sgd_ex(dr_ev* const* vars, const dr_pool_grad_desc* descs,
+                                      int num_tables, int64_t batch, int dim,
+                                      const int64_t* rowsel, int rows_record, float lr,
+                                      int64_t global_step, void* ws, size_t ws_bytes,
+                                      void* stream);
 /* KvResourceSparseApplyAdamAsync (training_ali_ops.cc:1404-1575) with the  */
 /* beta powers DEVICE-resident, as the reference keeps them in an EV (key 0,  */
 /* :1523-1526): powers[t] is table t's float[2] {beta1_power, beta2_power}.   */
@@ -1061,6 +1080,46 @@ int dr_din_attention_pool_grad(const float* alphas, const float* mask, const flo
                                const float* grad_att, const float* grad_sum, int64_t batch,
                                int64_t seq_len, int hidden, float* grad_scores,
                                float* grad_facts, void* stream);
+
+/* The attention MLP of din_attention (utils.py:284-289: din_all -> 80      */
+/* sigmoid -> 40 sigmoid -> 1 -> scores), fused: din_all is never written    */
+/* (W1 = [A|Bm|C|Dm]: a1 = (A + C) q + b1 + [Bm - C | Dm] [f ; q f]) and only */
+/* the valid (mask != 0) positions run it -- a padded position's score is     */
+/* replaced by the padding value before the softmax.  Weights are the torch  */
+/* Linear layouts: w1 [n1, 4H], w2 [n2, n1], w3 [n2] (f3_att.weight[0]),      */
+/* b3 [1]; n1 = 80, n2 = 40; hidden 16, 32, 36 or 64.  Caller-owned buffers   */
+/* (cap = batch * seq_len); forward fills pos / cnt / off / w1p / w2t / cq /  */
+/* h1t / h2t and writes scores at the valid positions (others untouched);    */
+/* the backward reads them and grad_scores, adds the MLP's part to           */
+/* grad_facts and fills the per-position / per-sample buffers from which the  */
+/* caller forms the weight gradients:                                         */
+/*   dW1 = [Gq | Gf | Gq - Gf | Gqf], Gq = s1^T q, [Gf | Gqf] = da1t xt^T,    */
+/*   db1 = column sums of s1, dW2 = da2t h1t^T, db2 = row sums of da2t,       */
+/*   dw3 = h2t dsc, db3 = sum dsc, grad_query += s1 (A + C) + dq2.            */
+typedef struct dr_din_mlp_buf {
+  int32_t* pos;   /* [cap] valid positions b*T + t, sample-major, ascending   */
+  int32_t* cnt;   /* [batch] valid positions per sample                      */
+  int32_t* off;   /* [batch + 1] exclusive prefix of cnt (off[batch] = P)    */
+  float* w1p;     /* [n1, 2H] = [Bm - C | Dm]                                */
+  float* w2t;     /* [n1, n2] = w2^T                                         */
+  float* cq;      /* [batch, n1] = (A + C) q + b1                            */
+  float* h1t;     /* [n1, cap] sigmoid outputs (columns p < P)               */
+  float* h2t;     /* [n2, cap]                                               */
+  float* da1t;    /* [n1, cap] backward: d a1 (zero columns p >= P)          */
+  float* da2t;    /* [n2, cap] d a2                                          */
+  float* xt;      /* [2H, cap] [f ; q f]                                     */
+  float* dsc;     /* [cap] d score per valid position                        */
+  float* dqp;     /* [H, cap] f * d(q f)                                     */
+  float* s1;      /* [batch, n1] per-sample sum of d a1 (ascending positions) */
+  float* dq2;     /* [batch, H] per-sample sum of f * d(q f)                 */
+} dr_din_mlp_buf;
+int dr_din_mlp_forward(const float* query, const float* facts, const float* mask, int64_t batch,
+                       int64_t seq_len, int hidden, const float* w1, const float* b1, int n1,
+                       const float* w2, const float* b2, int n2, const float* w3, const float* b3,
+                       float* scores, const dr_din_mlp_buf* buf, void* stream);
+int dr_din_mlp_backward(const float* query, const float* facts, int64_t batch, int64_t seq_len,
+                        int hidden, int n1, int n2, const float* w3, const float* grad_scores,
+                        float* grad_facts, const dr_din_mlp_buf* buf, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* String -> id, the step before the lookup.  Strings are one byte buffer    */

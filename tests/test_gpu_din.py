@@ -184,3 +184,57 @@ def test_din_attention_empty_batch():
     gs, gf = ops.din_attention_pool_grad(al, torch.zeros(0, 5, device=DEV), f,
                                          torch.zeros(0, 36, device=DEV))
     assert gs.shape == (0, 5)
+
+
+@pytest.mark.parametrize("B,T,H,prefix", [(64, 100, 36, True), (40, 23, 36, False),
+                                          (8, 1, 36, True), (16, 9, 16, False),
+                                          (12, 30, 64, True), (20, 17, 32, False)])
+def test_din_fused_attention_matches_fp64(B, T, H, prefix):
+    """DinAttentionFused (dr_din_mlp_forward / _backward + the pool kernels):
+    the attention MLP over the valid positions only, din_all never formed
+    (W1 split into its per-sample and per-position parts) -- forward and
+    every gradient (query, facts, the three layers' weights and biases)
+    against torch fp64 autograd of the reference composition (utils.py:
+    264-309), prefix masks (zero-padded histories, a fully masked row) and
+    arbitrary 0/1 masks."""
+    from deeprec_amd import modelzoo as mz
+    g = torch.Generator(device="cpu").manual_seed(B * 1000 + T + H)
+    q = torch.randn(B, H, generator=g, dtype=torch.float64) * 0.5
+    f = torch.randn(B, T, H, generator=g, dtype=torch.float64) * 0.5
+    if prefix:
+        lens = torch.randint(0, T + 1, (B,), generator=g)
+        lens[0] = T
+        if B > 1:
+            lens[1] = 0
+        mask = (torch.arange(T)[None, :] < lens[:, None]).double()
+    else:
+        mask = (torch.rand(B, T, generator=g) < 0.6).double()
+    w1 = torch.randn(80, 4 * H, generator=g, dtype=torch.float64) / (4 * H) ** 0.5
+    b1 = torch.randn(80, generator=g, dtype=torch.float64) * 0.1
+    w2 = torch.randn(40, 80, generator=g, dtype=torch.float64) / 80 ** 0.5
+    b2 = torch.randn(40, generator=g, dtype=torch.float64) * 0.1
+    w3 = torch.randn(1, 40, generator=g, dtype=torch.float64) / 40 ** 0.5
+    b3 = torch.randn(1, generator=g, dtype=torch.float64) * 0.1
+    ga = torch.randn(B, H, generator=g, dtype=torch.float64)
+    gsum = torch.randn(B, H, generator=g, dtype=torch.float64)
+    ins = [x.to(DEV) for x in (q, f, mask, w1, b1, w2, b2, w3, b3)]
+    ref = [x.clone().requires_grad_(x.dim() > 0 and i != 2) for i, x in enumerate(ins)]
+    rq, rf, rm, rw1, rb1, rw2, rb2, rw3, rb3 = ref
+    h = torch.sigmoid(_ref_din_input(rq, rf) @ rw1.t() + rb1)
+    h = torch.sigmoid(h @ rw2.t() + rb2)
+    scores = (h @ rw3.t() + rb3).view(B, T)
+    att, hsum, _ = _ref_pool(scores, rm, rf)
+    (att * ga.to(DEV)).sum().add_((hsum * gsum.to(DEV)).sum()).backward()
+    got = [x.float().clone().requires_grad_(i != 2) for i, x in enumerate(ins)]
+    gatt, ghs = mz.DinAttentionFused.apply(*got)
+    torch.testing.assert_close(gatt.double(), att.detach(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(ghs.double(), hsum.detach(), rtol=1e-5, atol=1e-5)
+    (gatt * ga.to(DEV).float()).sum().add_((ghs * gsum.to(DEV).float()).sum()).backward()
+    for name, a, b in zip(("query", "facts", "mask", "w1", "b1", "w2", "b2", "w3", "b3"), got, ref):
+        if name == "mask":
+            continue
+        # weight gradients sum B*T position terms: fp32 vs fp64 at 2e-5 of the
+        # gradient's scale
+        scale = float(b.grad.abs().max()) + 1e-12
+        err = float((a.grad.double() - b.grad).abs().max())
+        assert err <= 2e-5 * scale + 1e-6, (name, err, scale)
