@@ -2409,13 +2409,30 @@ static int lookup_kernel_kind() {
 // a multiple of 8 (XCD-major item ranges), at most `want`.
 template <class K>
 static unsigned persistent_grid(K kernel, int64_t want) {
-  int dev = 0, cus = 0, per = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-    cus = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess || per <= 0)
-    per = 1;
-  int64_t g = (int64_t)per * cus;
+  // resident blocks of this kernel on this device, asked once
+  static std::mutex mu;
+  static std::vector<std::pair<std::pair<const void*, int>, int64_t>> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  const void* key = reinterpret_cast<const void*>(kernel);
+  int64_t g = 0;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& e : cache)
+      if (e.first.first == key && e.first.second == dev) g = e.second;
+  }
+  if (g == 0) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess ||
+        per <= 0)
+      per = 1;
+    g = (int64_t)per * cus;
+    std::lock_guard<std::mutex> lk(mu);
+    cache.push_back({{key, dev}, g});
+  }
   want = ceil_div(want, 8) * 8;
   if (g > want) g = want;
   g = std::max<int64_t>(8, g / 8 * 8);

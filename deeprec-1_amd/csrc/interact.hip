@@ -1377,6 +1377,217 @@ __global__ __launch_bounds__(512, 1) void crossnet_8ph_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// CrossNet weight gradient dW = u^T x_l (TN: the contraction runs down the
+// rows of both [B, d] operands), on the forward's 256 x 256, four-phase
+// schedule (crossnet_8ph_kernel): the same waves / quadrants / half-tiles,
+// barriers and counted waits, with two changes --
+//   * a half-tile is 64 contraction rows x 128 output columns staged as they
+//     lie in memory (global_load_lds, 256-B image rows, 32-B slots XOR-
+//     swizzled by dw_h(r)), A_h holding columns {wr*128 + h*64 + [0, 64)} of
+//     u and B_h columns {wc*64 + h*32 + [0, 32)} of x_l;
+//   * the MFMA fragments (8 consecutive contraction rows of one column per
+//     lane, for both operands) come from ds_read_b64_tr_b16, the transposing
+//     LDS read (gemm_tn_kernel's fragment, mlp.hip).
+// The 14 x 14 output tiles of d = 3 392 are fewer than the CUs: the batch is
+// split into S slices (grid = tiles x S) whose fp32 partials
+// crossnet_dw_reduce_kernel sums in slice order (deterministic).
+// ---------------------------------------------------------------------------
+typedef short dw_v4s __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int dw_h(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+
+// half-tile h of u (AH) or x_l: 64 rows from k0, 128 logical columns; 2 wave
+// instructions of 4 rows x 256 B per wave
+template <bool AH>
+__device__ __forceinline__ void dw_stage(const uint16_t* __restrict__ X, int d, int64_t k0,
+                                         int c0, int h, char* img, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rb = (wave * 2 + i) * 4;
+    const int r = rb + (lane >> 4), sl = lane & 15;
+    const int c = (((sl >> 1) ^ dw_h(r)) << 1) | (sl & 1);   // logical 16-B chunk
+    const int col = AH ? ((c >> 3) * 128 + h * 64 + (c & 7) * 8)
+                       : ((c >> 2) * 64 + h * 32 + (c & 3) * 8);
+    int gc = c0 + col;
+    if (gc >= d) gc = c0;   // columns past the end feed discarded outputs
+    const uint16_t* src = X + (k0 + r) * (int64_t)d + gc;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(img + rb * 256),
+                                     16, 0, 0);
+  }
+}
+
+// 16 logical columns at slot m (0..7) for the 32-row step kk
+__device__ __forceinline__ bf16x8 dw_frag(const char* img, int kk, int m, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int r1 = kk * 32 + 8 * g + q, r2 = r1 + 4;
+  const dw_v4s a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) dw_v4s*)(img + r1 * 256 + ((m ^ dw_h(r1)) << 5) + 8 * p));
+  const dw_v4s b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) dw_v4s*)(img + r2 * 256 + ((m ^ dw_h(r2)) << 5) + 8 * p));
+  return bf16x8{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+}
+
+__global__ __launch_bounds__(512, 1) void crossnet_dw_kernel(
+    const uint16_t* __restrict__ u, const uint16_t* __restrict__ xl, int64_t K, int d, int S,
+    float* __restrict__ part) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * C8_BUF];  // 128 KB
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const bool g1 = wr != 0;
+  // XCD-contiguous work items, then (output tile, batch slice), slices of a
+  // tile adjacent (they read different rows of the same columns)
+  const int64_t nwg = (int64_t)gridDim.x;
+  const int64_t orig = blockIdx.x;
+  const int64_t xcd = orig % 8, q8 = nwg / 8, rr = nwg % 8;
+  const int64_t item = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + orig / 8;
+  const int64_t tile = item / S;
+  const int z = (int)(item % S);
+  const int nt = d / 256 + (d % 256 ? 1 : 0);
+  const int m0 = (int)(tile / nt) * 256, n0 = (int)(tile % nt) * 256;
+  const int64_t kt = K / 64;                           // 64-row steps (K % 64 == 0)
+  const int64_t ks = (kt * z) / S, ke = (kt * (z + 1)) / S;
+  const int nk = (int)(ke - ks);
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto img = [&](int t, int part_) -> char* { return lds + (t & 1) * C8_BUF + part_ * C8_HALF; };
+  auto st_a = [&](int t, int h) {
+    dw_stage<true>(u, d, (ks + t) * 64, m0, h, img(t, h), wave, lane);
+  };
+  auto st_b = [&](int t, int h) {
+    dw_stage<false>(xl, d, (ks + t) * 64, n0, h, img(t, 2 + h), wave, lane);
+  };
+  if (nk > 0) {
+    st_a(0, 0); st_b(0, 0); st_b(0, 1); st_a(0, 1);
+    if (nk > 1) {
+      st_a(1, 0); st_b(1, 0); st_b(1, 1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __builtin_amdgcn_s_barrier();
+  if (g1) __builtin_amdgcn_s_barrier();  // the stagger
+  asm volatile("" ::: "memory");
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];  // [frag][kk]
+  auto read_a = [&](const char* sm) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = dw_frag(sm, kk, wr * 4 + i, lane);
+  };
+  auto read_b = [&](const char* sm, bf16x8 (&fb)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fb[j][kk] = dw_frag(sm, kk, wc * 2 + j, lane);
+  };
+  auto close_read = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto mma = [&](int mi, bf16x8 (&fb)[2][2], int nj) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mi + i][nj + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb[j][kk], acc[mi + i][nj + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  for (int t = 0; t < nk; ++t) {
+    const bool pf1 = t + 1 < nk, pf2 = t + 2 < nk;
+    read_b(img(t, 2), fb0);
+    read_a(img(t, 0));
+    if (pf1) st_a(t + 1, 1);
+    close_read();
+    mma(0, fb0, 0);
+    read_b(img(t, 3), fb1);
+    if (pf2) st_a(t + 2, 0);
+    close_read();
+    mma(0, fb1, 2);
+    read_a(img(t, 1));
+    if (pf2) st_b(t + 2, 0);
+    close_read();
+    mma(4, fb0, 0);
+    if (pf2) {
+      st_b(t + 2, 1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else if (pf1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    close_read();
+    mma(4, fb1, 2);
+  }
+  if (!g1) __builtin_amdgcn_s_barrier();  // matches group 1's extra barrier
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  // accumulators -> LDS (C/D map), then 2 x 16-B fp32 stores of 8 columns
+  const int fr = lane & 15, fq = lane >> 4;
+  float* ct = reinterpret_cast<float*>(lds) + wave * 64 * 64;
+  float* pz = part + (int64_t)z * d * d;
+  const int cc = (lane & 7) * 8;
+  const int gcol = n0 + wc * 64 + cc;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i * 16 + fq * 4 + r;
+          const int col = (j * 16 + fr) ^ (((row >> 2) & 3) << 4);
+          ct[row * 64 + col] = acc[h * 4 + i][j][r];
+        }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int row = it * 8 + (lane >> 3);
+      const int grow = m0 + wr * 128 + h * 64 + row;
+      const int pc = cc ^ (((row >> 2) & 3) << 4);
+      const float4 l0 = *reinterpret_cast<const float4*>(ct + row * 64 + pc);
+      const float4 l1 = *reinterpret_cast<const float4*>(ct + row * 64 + pc + 4);
+      if (grow < d && gcol < d) {
+        float* dst = pz + (int64_t)grow * d + gcol;
+        reinterpret_cast<float4*>(dst)[0] = l0;
+        reinterpret_cast<float4*>(dst)[1] = l1;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// dW = sum over slices z of part[z], in slice order (deterministic)
+__global__ void crossnet_dw_reduce_kernel(const float* __restrict__ part, int S, int64_t n4,
+                                          int64_t zstride, float* __restrict__ dw) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n4) return;
+  float4 s = reinterpret_cast<const float4*>(part)[q];
+  for (int z = 1; z < S; ++z) {
+    const float4 p = reinterpret_cast<const float4*>(part + (int64_t)z * zstride)[q];
+    s.x += p.x;
+    s.y += p.y;
+    s.z += p.z;
+    s.w += p.w;
+  }
+  reinterpret_cast<float4*>(dw)[q] = s;
+}
+
+// ---------------------------------------------------------------------------
 // CrossNet backward, the elementwise part of one layer in ONE pass over HBM
 // (the GEMMs dW = u^T x_l and dx_l = u W + g stay library calls):
 //   u   = bf16(g * x0)                         [B, d] bf16
@@ -1771,6 +1982,56 @@ int dr_crossnet_dx_bf16(const uint16_t* u, const uint16_t* wt, const uint16_t* g
   hipLaunchKernelGGL((crossnet_8ph_kernel<2, 4, false>), dim3((unsigned)tiles), dim3(512), 0,
                      S(stream), g, u, wt, (const float*)nullptr, batch, d, d, dx,
                      (uint16_t*)nullptr);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+
+// CrossNet weight gradient dW = u^T x_l (fp32 [d, d]); the batch split into
+// crossnet_dw_slices() slices whose partials live in the workspace.
+static int crossnet_dw_slices(int64_t batch, int d) {
+  const int64_t tiles = (int64_t)dr::ceil_div(d, 256) * dr::ceil_div(d, 256);
+  // one block per CU (128 KB of LDS): S slices fill whole rounds of 256 CUs
+  // best; each slice >= 1024 rows
+  int best = 1;
+  double best_eff = 0.0;
+  for (int s = 1; s <= 16; ++s) {
+    if (batch / s < 1024) break;
+    const int64_t items = tiles * s;
+    const int64_t rounds = (items + 255) / 256;
+    const double eff = (double)items / (double)(rounds * 256);
+    if (eff > best_eff + 0.02) {
+      best_eff = eff;
+      best = s;
+    }
+  }
+  return best;
+}
+
+size_t dr_crossnet_dw_workspace_size(int64_t batch, int d) {
+  if (batch <= 0 || d <= 0) return 256;
+  return (size_t)crossnet_dw_slices(batch, d) * (size_t)d * (size_t)d * sizeof(float) + 256;
+}
+
+int dr_crossnet_dw_bf16(const uint16_t* u, const uint16_t* xl, int64_t batch, int d, float* dw,
+                        void* ws, size_t ws_bytes, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && d > 0 && d % 64 == 0 && batch % 64 == 0, DR_INVALID_ARGUMENT,
+             "dr_crossnet_dw_bf16: d and batch must be multiples of 64");
+  DR_REQUIRE(u && xl && dw && ws, DR_INVALID_ARGUMENT, "null operand");
+  DR_REQUIRE((((uintptr_t)u | (uintptr_t)xl | (uintptr_t)dw | (uintptr_t)ws) & 15) == 0,
+             DR_INVALID_ARGUMENT, "operands must be 16-B aligned");
+  DR_REQUIRE(ws_bytes >= dr_crossnet_dw_workspace_size(batch, d), DR_INVALID_ARGUMENT,
+             "workspace too small");
+  const int64_t n4 = (int64_t)d * d / 4;
+  if (batch == 0) return fill_bytes(dw, 0, (size_t)d * d * sizeof(float), S(stream));
+  const int Sl = crossnet_dw_slices(batch, d);
+  const int64_t tiles = (int64_t)ceil_div(d, 256) * ceil_div(d, 256);
+  float* part = static_cast<float*>(ws);
+  hipLaunchKernelGGL(crossnet_dw_kernel, dim3((unsigned)(tiles * Sl)), dim3(512), 0, S(stream),
+                     u, xl, batch, d, Sl, part);
+  hipLaunchKernelGGL(crossnet_dw_reduce_kernel, dim3((unsigned)ceil_div(n4, 256)), dim3(256), 0,
+                     S(stream), part, Sl, n4, (int64_t)d * d, dw);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

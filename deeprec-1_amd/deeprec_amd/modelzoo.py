@@ -738,6 +738,22 @@ def _cross_dx(u, wb, g):
     return ops.crossnet_dx(u, wb.t().contiguous(), g)
 
 
+# A/B switch: DR_CROSSNET_DW_LIB=1 = the library GEMM for the cross layers'
+# weight gradient
+_CROSS_DW_LIB = os.environ.get("DR_CROSSNET_DW_LIB", "0") == "1"
+
+
+def _cross_dw(u, x):
+    """dW = u^T x of a cross layer: the hand TN MFMA kernel (dr_crossnet_dw_bf16,
+    fp32 accumulation and output), or the library GEMM (bf16 result widened)
+    where the shape does not fit it."""
+    if not _CROSS_DW_LIB:
+        dw = ops.crossnet_dw(u, x)
+        if dw is not None:
+            return dw
+    return torch.matmul(u.t(), x).float()
+
+
 class CrossLayer(torch.autograd.Function):
     """DCN-v2 cross layer x_{l+1} = x0 * (x_l W^T + b) + x_l (BASELINE
     configs[4]; absent from the reference).  Forward: the
@@ -758,7 +774,7 @@ class CrossLayer(torch.autograd.Function):
         x0, xl, wb, lin = ctx.saved_tensors
         g = g.to(torch.bfloat16)
         u = g * x0
-        dW = torch.matmul(u.t(), xl).float()
+        dW = _cross_dw(u, xl)
         db = u.float().sum(0)
         dxl = _cross_dx(u, wb, g)
         dx0 = g * lin
@@ -800,7 +816,7 @@ class CrossStack(torch.autograd.Function):
         dws, dbs = [None] * L, [None] * L
         for l in reversed(range(L)):
             u, acc, db = ops.crossnet_backward_elem(g, x0, lins[l], acc)
-            dws[l] = torch.matmul(u.t(), xs[l]).float()
+            dws[l] = _cross_dw(u, xs[l])
             dbs[l] = db
             g = _cross_dx(u, ws[l], g)
         dx0 = (acc + g.float()).to(torch.bfloat16)

@@ -770,6 +770,25 @@ def crossnet_dx(u, wt, g):
     return dx
 
 
+def crossnet_dw(u, xl):
+    """dr_crossnet_dw_bf16: dW = u^T x_l (fp32 [d, d]) for a cross layer's
+    weight gradient; u, xl [B, d] bf16, d and B multiples of 64 (None
+    otherwise: the caller falls back to a library GEMM)."""
+    dev = _dev(u)
+    B, d = u.shape
+    if d % 64 or B % 64 or tuple(xl.shape) != (B, d) or any(
+            t.dtype != torch.bfloat16 for t in (u, xl)):
+        return None
+    u, xl = u.contiguous(), xl.contiguous()
+    dw = torch.empty((d, d), dtype=torch.float32, device=dev)
+    wsb = lib().dr_crossnet_dw_workspace_size(B, d)
+    ws = workspace(wsb, dev)
+    check(lib().dr_crossnet_dw_bf16(ptr(u), ptr(xl), B, d, ptr(dw), ptr(ws), wsb,
+                                    stream_handle(dev)))
+    _post(dev)
+    return dw
+
+
 def crossnet_backward_elem(g, x0, lin, acc=None):
     """dr_crossnet_backward_elem_bf16: the elementwise part of a cross
     layer's backward in one pass.  g, x0, lin [B, d] bf16; acc [B, d] fp32

@@ -1055,6 +1055,15 @@ int dr_crossnet_forward_bf16(const uint16_t* x0, const uint16_t* xl, const uint1
                              const float* bias, int64_t batch, int d, uint16_t* out,
                              uint16_t* lin_out, void* stream);
 
+/* CrossNet weight gradient dW = u^T x_l, fp32 [d, d] (u, x_l [batch, d]    */
+/* bf16 row-major; d and batch multiples of 64): the forward's 256^2         */
+/* four-phase MFMA schedule in TN form (transposing LDS reads), the batch     */
+/* split into slices whose fp32 partials (workspace) are summed in slice     */
+/* order -- deterministic.                                                    */
+size_t dr_crossnet_dw_workspace_size(int64_t batch, int d);
+int dr_crossnet_dw_bf16(const uint16_t* u, const uint16_t* xl, int64_t batch, int d, float* dw,
+                        void* ws, size_t ws_bytes, void* stream);
+
 /* DIN user-behaviour attention (modelzoo/DIN/script/utils.py:264-309,      */
 /* din_attention mode 'SUM'; script/model.py:94-98,381-390).  query [B,H],  */
 /* facts [B,T,H] (the gathered history, H = 2 x EMBEDDING_DIM), fp32.        */

@@ -110,6 +110,34 @@ def test_crossnet_dx_matches_torch(B, d):
         assert torch.equal(ops.crossnet_dx(u, W.t().contiguous(), g), dx)
 
 
+@pytest.mark.parametrize("B,d", [(1024, 192), (4096, 3392), (64, 64), (2048, 448),
+                                 (65536, 3392)])
+def test_crossnet_dw_matches_fp64(B, d):
+    """dr_crossnet_dw_bf16 (dW = u^T x on the 256^2 four-phase schedule in TN
+    form, batch slices summed in order): against the fp64 product of the same
+    bf16 operands, within fp32 accumulation error (each entry a sum of B
+    products: |err| <= 2^-22 sqrt(B) max|row norms|-scale bound, checked as
+    1e-5 of the entry scale), and bit-identical across launches."""
+    from deeprec_amd import ops
+    gen = torch.Generator(device="cpu").manual_seed(B + 7 * d)
+    u = torch.randn(B, d, generator=gen).to(DEV, torch.bfloat16)
+    x = torch.randn(B, d, generator=gen).to(DEV, torch.bfloat16)
+    dw = ops.crossnet_dw(u, x)
+    assert dw is not None and dw.dtype == torch.float32 and dw.shape == (d, d)
+    if B * d * d <= 4096 * 3392 * 3392:
+        want = u.double().t() @ x.double()
+    else:   # sampled rows / columns of the full-size product
+        idx = torch.arange(0, d, 53, device=DEV)
+        want = u.double()[:, idx].t() @ x.double()
+        dw = dw[idx]
+    scale = float(B) ** 0.5
+    err = float((dw.double() - want).abs().max())
+    assert err <= 1e-5 * scale * 4, (err, scale)
+    full = ops.crossnet_dw(u, x)
+    for _ in range(2):
+        assert torch.equal(ops.crossnet_dw(u, x), full)
+
+
 def test_cross_stack_backward_matches_autograd():
     """CrossStack (3 layers, one fused elementwise pass per layer in the
     backward) against torch autograd of the fp32 composition from the same

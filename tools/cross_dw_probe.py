@@ -36,6 +36,14 @@ def main():
     ref = torch.matmul(u.t(), x).float()
     t = timed(lambda: torch.matmul(u.t(), x).float())
     print("matmul(u.t(), x).float(): %.3f ms  %.0f TF/s" % (t, flop / t / 1e9), flush=True)
+    got = ops.crossnet_dw(u, x)
+    err = ((got - ref).abs().max() / ref.abs().max()).item()
+    t = timed(lambda: ops.crossnet_dw(u, x))
+    print("crossnet_dw (256^2 four-phase TN, split %d): %.3f ms  %.0f TF/s  max rel diff %.2e"
+          % (dr._lib.lib().dr_crossnet_dw_workspace_size(B, d) // (4 * d * d), t, flop / t / 1e9,
+             err), flush=True)
+    t = timed(lambda: torch.matmul(u.t(), x).float())
+    print("matmul(u.t(), x).float() again: %.3f ms" % t, flush=True)
     tiles = ((d + 127) // 128) ** 2
     for s in sorted({1, 2, 4, _dw_split(tiles, B)}):
         got = ops.gemm_tn(u, x, split_k=s)

@@ -5,10 +5,10 @@
 set -o pipefail
 T=${1:-r05a}
 mkdir -p gpurun_out/$T
-timeout -k 10 900 python -u -m pytest tests/test_gpu_headline.py tests/test_gpu_record_major.py \
+timeout -k 10 1000 python -u -m pytest tests/test_gpu_headline.py tests/test_gpu_record_major.py \
   tests/test_gpu_parity.py tests/test_gpu_rows_grad.py tests/test_gpu_rows_deterministic.py \
   tests/test_gpu_din.py tests/test_gpu_rccl_comm.py tests/test_gpu_sharded_c.py tests/test_gpu_bf16.py \
-  tests/test_gpu_configs.py -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/$T/tests.log 2>&1
+  tests/test_gpu_configs.py tests/test_gpu_dcn.py -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/$T/tests.log 2>&1
 rc=$?; tail -3 gpurun_out/$T/tests.log; grep -E "^FAILED|^ERROR" gpurun_out/$T/tests.log | head -20
 # a test failure (rc 1) still lets the timings run; a crash / timeout stops here
 [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
@@ -26,3 +26,9 @@ for v in 1 0 1 0; do
 done
 DR_GRAD_SERIAL_MAX=8192 timeout -k 10 300 python -u tools/model_step.py --model din --steps 10 > gpurun_out/$T/din_pieces.log 2>&1 || { tail -5 gpurun_out/$T/din_pieces.log; exit 1; }
 echo "din pieces of 8192 (A/B): $(tail -1 gpurun_out/$T/din_pieces.log)"
+timeout -k 10 200 python -u tools/cross_dw_probe.py > gpurun_out/$T/cross_dw.log 2>&1 || { tail -5 gpurun_out/$T/cross_dw.log; exit 1; }
+cat gpurun_out/$T/cross_dw.log
+timeout -k 10 120 tools/uc_replay_probe 3 0 > gpurun_out/$T/uc_replay.log 2>&1 || { tail -5 gpurun_out/$T/uc_replay.log; exit 1; }
+tail -2 gpurun_out/$T/uc_replay.log
+timeout -k 10 120 tools/uc_replay_probe 3 1 > gpurun_out/$T/uc_replay_control.log 2>&1 || { tail -5 gpurun_out/$T/uc_replay_control.log; exit 1; }
+tail -1 gpurun_out/$T/uc_replay_control.log
