@@ -883,19 +883,24 @@ __global__ __launch_bounds__(256) void rows_nz_kernel(RowsGroup g, int T, int di
 // the stage.  A one-piece run is finished here; a piece of a longer run
 // stores its partial for rows_combine_kernel.
 template <int VEC, int SW, bool SGD, bool WB>
-__global__ __launch_bounds__(256) void rows_serial_kernel(RowsGroup g, int T, int dim, RowsLong L,
-                                                          RowsSgd sg) {
+__global__ __launch_bounds__(1024) void rows_serial_kernel(RowsGroup g, int T, int dim, RowsLong L,
+                                                           RowsSgd sg) {
   using V = typename VecT<VEC>::T;
+  constexpr int NT = 1024;                 // threads: 16 waves load, wave 0 also walks
   constexpr int SV = SW / VEC;             // vectors of a position's slice
-  constexpr int PI = 256 / SV;             // positions per load instruction
-  constexpr int R = VEC == 4 ? 16 : 32;    // loads in flight per thread
-  constexpr int S = PI * R;                // positions per stage
+  constexpr int PI = NT / SV;              // positions per load instruction
+  constexpr int R = VEC == 4 ? 4 : 8;      // loads in flight per thread (<= 128 VGPRs, no spill)
+  constexpr int S = PI * R;                // positions per stage (S * SW = 8 K / 16 K floats)
+  constexpr int SP = S + 4;                // column stride of the transposed stage
   constexpr int WCH = 1024;                // zero-scan chunks per window (prefix in LDS)
-  static_assert(SV >= 1 && 256 % SV == 0, "slice shape");
-  __shared__ __attribute__((aligned(16))) float stage[S * SW];
+  static_assert(SV >= 1 && NT % SV == 0 && S % 4 == 0, "slice shape");
+  // the stage TRANSPOSED, [column][position] (stride S + 4: the loaders'
+  // column writes spread over the banks, the walker's 16-B reads stay
+  // aligned): a lane walks its column 4 positions per LDS read
+  __shared__ __attribute__((aligned(16))) float stage[SW * SP];
   __shared__ int64_t sk[DR_MAX_GROUP + 1];
   __shared__ int32_t cpre[WCH + 1];
-  __shared__ int32_t wsum[4];
+  __shared__ int32_t wsum[NT / 64];
   if (threadIdx.x <= T) sk[threadIdx.x] = g.koff[threadIdx.x];
   __syncthreads();
   const int nsl = (dim + SW - 1) / SW;
@@ -938,16 +943,10 @@ __global__ __launch_bounds__(256) void rows_serial_kernel(RowsGroup g, int T, in
       int nw = 1;
       if (zc) {
         nw = (int)(nch - w0 < WCH ? nch - w0 : WCH);
-        // exclusive prefix of the window's chunk counts: 4 chunks per thread,
-        // wave scan by shuffles, wave totals through LDS
-        int c4[4], tsum = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int jj = 4 * tid + q;
-          c4[q] = jj < nw ? L.ccnt[cf + w0 + jj] : 0;
-          tsum += c4[q];
-        }
-        int incl = tsum;
+        // exclusive prefix of the window's chunk counts (one chunk per
+        // thread): wave scan by shuffles, wave totals through LDS
+        const int cnt = tid < nw ? L.ccnt[cf + w0 + tid] : 0;
+        int incl = cnt;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
           const int v = __shfl_up(incl, o, 64);
@@ -955,15 +954,10 @@ __global__ __launch_bounds__(256) void rows_serial_kernel(RowsGroup g, int T, in
         }
         if (lane == 63) wsum[tid >> 6] = incl;
         __syncthreads();
-        int before = incl - tsum;
+        int before = incl - cnt;
         for (int w = 0; w < (tid >> 6); ++w) before += wsum[w];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int jj = 4 * tid + q;
-          if (jj <= nw) cpre[jj] = before;   // (jj == nw: the total)
-          before += c4[q];
-        }
-        if (tid == 255 && 4 * 256 <= nw) cpre[nw] = before;
+        if (tid < nw) cpre[tid] = before;
+        if (tid == nw - 1) cpre[nw] = before + cnt;
         __syncthreads();
         K = cpre[nw];
       } else {
@@ -1008,6 +1002,18 @@ __global__ __launch_bounds__(256) void rows_serial_kernel(RowsGroup g, int T, in
           y[r] = gld(reinterpret_cast<const V*>(src + rr * ts));
         }
       };
+      auto put = [&](int r, V x) {   // term (r, pv) -> its column rows of the stage
+        const int pos = r * PI + pv;
+        if constexpr (VEC == 4) {
+          float* c = stage + (cv * 4) * SP + pos;
+          c[0] = x.x;
+          c[SP] = x.y;
+          c[2 * SP] = x.z;
+          c[3 * SP] = x.w;
+        } else {
+          stage[cv * SP + pos] = x;
+        }
+      };
       if (K > 0) {
         load_idx(0);
         take();
@@ -1036,48 +1042,47 @@ __global__ __launch_bounds__(256) void rows_serial_kernel(RowsGroup g, int T, in
             } else if (mf[r] != 1.f) {
               x = vmul(x, mf[r]);
             }
-            *reinterpret_cast<V*>(stage + (r * PI + pv) * SW + cv * VEC) = x;
+            put(r, x);
           }
         } else {
 #pragma unroll
           for (int r = 0; r < R; ++r) {
             V x = y[r];
             if ((zmask >> r) & 1u) x = vzero<V>();
-            *reinterpret_cast<V*>(stage + (r * PI + pv) * SW + cv * VEC) = x;
+            put(r, x);
           }
         }
         __syncthreads();
         take();
         load_rows();              // the next stage's rows: in flight while wave 0 sums this one
         load_idx(b0 + 2 * S);
-        if (tid < 64) {           // wave-uniform
+        if (tid < 64) {           // wave-uniform: lane lc walks column lc
           const int nv = (int)(K - b0 < S ? K - b0 : S);
-          const float* sp = stage + lc;
+          const float* sp = stage + lc * SP;
           int jj = 0;
           if (fresh) {
             acc = sp[0];
             fresh = false;
             jj = 1;
           }
-          // the LDS reads of the next 8 positions are issued before the adds
-          // of these 8: the chain waits on the adds, not on LDS latency
+          for (; jj < nv && (jj & 3); ++jj) acc = acc + sp[jj];
+          // 16-B reads, the next 8 positions' issued before these 8 adds
           if (jj + 8 <= nv) {
-            float xa[8], xb[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) xa[q] = sp[(jj + q) * SW];
+            float4 xa0 = *reinterpret_cast<const float4*>(sp + jj);
+            float4 xa1 = *reinterpret_cast<const float4*>(sp + jj + 4);
             for (; jj + 16 <= nv; jj += 8) {
-#pragma unroll
-              for (int q = 0; q < 8; ++q) xb[q] = sp[(jj + 8 + q) * SW];
-#pragma unroll
-              for (int q = 0; q < 8; ++q) acc = acc + xa[q];
-#pragma unroll
-              for (int q = 0; q < 8; ++q) xa[q] = xb[q];
+              const float4 xb0 = *reinterpret_cast<const float4*>(sp + jj + 8);
+              const float4 xb1 = *reinterpret_cast<const float4*>(sp + jj + 12);
+              acc = acc + xa0.x; acc = acc + xa0.y; acc = acc + xa0.z; acc = acc + xa0.w;
+              acc = acc + xa1.x; acc = acc + xa1.y; acc = acc + xa1.z; acc = acc + xa1.w;
+              xa0 = xb0;
+              xa1 = xb1;
             }
-#pragma unroll
-            for (int q = 0; q < 8; ++q) acc = acc + xa[q];
+            acc = acc + xa0.x; acc = acc + xa0.y; acc = acc + xa0.z; acc = acc + xa0.w;
+            acc = acc + xa1.x; acc = acc + xa1.y; acc = acc + xa1.z; acc = acc + xa1.w;
             jj += 8;
           }
-          for (; jj < nv; ++jj) acc = acc + sp[jj * SW];
+          for (; jj < nv; ++jj) acc = acc + sp[jj];
         }
         __syncthreads();   // the stage is rewritten next
       }
@@ -1258,7 +1263,7 @@ static void launch_long(const RowsGroup& g, int T, int dim, const RowsLong& L, c
   if (sb > 1024) sb = 1024;
   const dim3 grid((unsigned)sb);
 #define DR_SERIAL(SWC)                                                                         \
-  hipLaunchKernelGGL((rows_serial_kernel<VEC, SWC, SGD, WB>), grid, dim3(256), 0, s, g, T, dim, L, \
+  hipLaunchKernelGGL((rows_serial_kernel<VEC, SWC, SGD, WB>), grid, dim3(1024), 0, s, g, T, dim, L, \
                      sg)
   if constexpr (VEC == 4) {
     switch (sw) {
