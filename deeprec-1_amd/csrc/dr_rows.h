@@ -14,6 +14,10 @@ struct VecT<4> {
   using T = float4;
 };
 template <>
+struct VecT<2> {
+  using T = float2;
+};
+template <>
 struct VecT<1> {
   using T = float;
 };
@@ -21,7 +25,10 @@ struct VecT<1> {
 __device__ __forceinline__ float4 vadd(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
+__device__ __forceinline__ float2 vadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float vadd(float a, float b) { return a + b; }
+__device__ __forceinline__ float2 vdiv(float2 a, float q) { return make_float2(a.x / q, a.y / q); }
+__device__ __forceinline__ float2 vmul(float2 a, float q) { return make_float2(a.x * q, a.y * q); }
 __device__ __forceinline__ float4 vdiv(float4 a, float q) {
   return make_float4(a.x / q, a.y / q, a.z / q, a.w / q);
 }
@@ -37,6 +44,10 @@ __device__ __forceinline__ V vzero();
 template <>
 __device__ __forceinline__ float4 vzero<float4>() {
   return make_float4(0.f, 0.f, 0.f, 0.f);
+}
+template <>
+__device__ __forceinline__ float2 vzero<float2>() {
+  return make_float2(0.f, 0.f);
 }
 template <>
 __device__ __forceinline__ float vzero<float>() {

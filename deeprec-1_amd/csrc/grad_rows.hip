@@ -890,6 +890,7 @@ __global__ __launch_bounds__(1024) void rows_serial_kernel(RowsGroup g, int T, i
   constexpr int SV = SW / VEC;             // vectors of a position's slice
   constexpr int PI = NT / SV;              // positions per load instruction
   constexpr int R = VEC == 4 ? 4 : 8;      // loads in flight per thread (<= 128 VGPRs, no spill)
+  static_assert(VEC == 1 || VEC == 2 || VEC == 4, "vector width");
   constexpr int S = PI * R;                // positions per stage (S * SW = 8 K / 16 K floats)
   constexpr int SP = S + 4;                // column stride of the transposed stage
   constexpr int WCH = 1024;                // zero-scan chunks per window (prefix in LDS)
@@ -1010,6 +1011,10 @@ __global__ __launch_bounds__(1024) void rows_serial_kernel(RowsGroup g, int T, i
           c[SP] = x.y;
           c[2 * SP] = x.z;
           c[3 * SP] = x.w;
+        } else if constexpr (VEC == 2) {
+          float* c = stage + (cv * 2) * SP + pos;
+          c[0] = x.x;
+          c[SP] = x.y;
         } else {
           stage[cv * SP + pos] = x;
         }
@@ -1244,7 +1249,7 @@ static RowsWs carve_rows(void* ws, int64_t n, size_t* used) {
 // 64 KiB (fp32 rows) / 32 KiB (unaligned) of LDS.
 template <int VEC, bool SGD, bool WB>
 static void launch_long(const RowsGroup& g, int T, int dim, const RowsLong& L, const RowsSgd& sg,
-                        hipStream_t s) {
+                        hipStream_t s, bool aligned2 = false) {
   const int64_t N = g.koff[T];
   if (N <= kRowsChunk) return;
   const int64_t runs = N / (kRowsChunk + 1) + 1;
@@ -1272,6 +1277,20 @@ static void launch_long(const RowsGroup& g, int T, int dim, const RowsLong& L, c
       case 16: DR_SERIAL(16); break;
       default: DR_SERIAL(32); break;
     }
+  } else if (aligned2 && dim % 2 == 0) {
+    // 8-byte rows (an even dim such as DIN's 18 at 8-byte offsets): the
+    // serial walk loads float2 -- twice the bytes per load in flight
+#define DR_SERIAL2(SWC)                                                                       \
+  hipLaunchKernelGGL((rows_serial_kernel<2, SWC, SGD, WB>), grid, dim3(1024), 0, s, g, T, dim, L, \
+                     sg)
+    switch (sw < 2 ? 2 : sw) {
+      case 2: DR_SERIAL2(2); break;
+      case 4: DR_SERIAL2(4); break;
+      case 8: DR_SERIAL2(8); break;
+      case 16: DR_SERIAL2(16); break;
+      default: DR_SERIAL2(32); break;
+    }
+#undef DR_SERIAL2
   } else {
     switch (sw) {
       case 1: DR_SERIAL(1); break;
@@ -1306,7 +1325,10 @@ static void launch_rows(const RowsGroup& g, int T, int64_t B, const RowsWs& w, i
     hipLaunchKernelGGL((rows_work_kernel<VEC, G, CPL, false>), dim3((unsigned)blocks), dim3(256),
                        0, s, g, T, B, w.kout, w.perm, w.ex, w.base, dim, w.work, w.nwork, gptr,
                        gu, st, RowsSgd{});
-  launch_long<VEC, false, false>(g, T, dim, w.longrun(gptr, gu), RowsSgd{}, s);
+  bool aligned2 = dim % 2 == 0;
+  for (int t = 0; t < T; ++t)
+    aligned2 = aligned2 && ((uintptr_t)g.d[t].top_grad & 7) == 0 && g.d[t].top_stride % 2 == 0;
+  launch_long<VEC, false, false>(g, T, dim, w.longrun(gptr, gu), RowsSgd{}, s, aligned2);
 }
 
 // The fused SGD tail: direct rows + worklist (rows_sgd_kernel), runs of 2 ..
