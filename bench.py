@@ -1382,7 +1382,7 @@ def main():
     bytes_launch = T * B * per_lookup
     achieved = bytes_launch / (k_ms * 1e-3) / 1e9
     # which fused lookup kernel the library launches (DR_LOOKUP_KERNEL, ev.hip)
-    lk_kind = os.environ.get("DR_LOOKUP_KERNEL", "2")
+    lk_kind = os.environ.get("DR_LOOKUP_KERNEL", "1")
     lk_name = {"0": "ev_lookup_onehot_kernel", "1": "ev_lookup_line_kernel"}.get(
         lk_kind, "ev_lookup_pipe_kernel")
     lk_inst = {"0": "<4,32,1,ALI,4>"}.get(lk_kind, "<4,32,1,ALI>")

@@ -2401,7 +2401,7 @@ static void launch_lookup_nb(const LookupArgs& a, int T, int64_t B, int dim, con
 // per lane group), 1 = line probes, one-shot (ev_lookup_line_kernel), 2 =
 // line probes, software-pipelined persistent waves (ev_lookup_pipe_kernel).
 static int lookup_kernel_kind() {
-  static const int v = getenv("DR_LOOKUP_KERNEL") ? atoi(getenv("DR_LOOKUP_KERNEL")) : 2;
+  static const int v = getenv("DR_LOOKUP_KERNEL") ? atoi(getenv("DR_LOOKUP_KERNEL")) : 1;
   return v;
 }
 

@@ -76,9 +76,11 @@ static constexpr int64_t kRowsMaxDim = 1024;
 // zero and are kept).  Runs longer than zero_scan() positions are first
 // scanned in parallel (rows_nz_kernel: chunks of kRowsChunk positions, each
 // compacted to its nonzero terms in ascending order) and the serial walk
-// visits only those -- e.g. a DIN padding id, whose ~2 x 10^5 history
-// positions all carry exactly zero gradient.  DR_GRAD_ZERO_SKIP=0 (A/B)
-// walks every term.
+// visits only those -- e.g. a padding id whose positions are masked out
+// downstream.  A window of chunks that is mostly nonzero (DIN's padding id:
+// its history positions feed the unmasked his_sum, model.py:98, so they all
+// carry gradient) is walked whole instead, without the compacted indirection.
+// DR_GRAD_ZERO_SKIP=0 (A/B) walks every term.
 static int64_t zero_scan() {
   static const int64_t v = [] {
     const char* e = getenv("DR_GRAD_ZERO_SKIP");
@@ -942,6 +944,7 @@ __global__ __launch_bounds__(1024) void rows_serial_kernel(RowsGroup g, int T, i
     for (int64_t w0 = 0; w0 < nch; w0 += WCH) {   // windows of chunks (plain: one)
       int64_t K;
       int nw = 1;
+      bool whole = false;
       if (zc) {
         nw = (int)(nch - w0 < WCH ? nch - w0 : WCH);
         // exclusive prefix of the window's chunk counts (one chunk per
@@ -961,12 +964,17 @@ __global__ __launch_bounds__(1024) void rows_serial_kernel(RowsGroup g, int T, i
         if (tid == nw - 1) cpre[nw] = before + cnt;
         __syncthreads();
         K = cpre[nw];
+        // mostly nonzero: walk the window's positions whole (the same chain)
+        const int64_t wend = (w0 + nw) * kRowsChunk < len ? (w0 + nw) * kRowsChunk : len;
+        const int64_t wpos = wend - w0 * kRowsChunk;
+        whole = 2 * K > wpos;
+        if (whole) K = wpos;
       } else {
         K = pe - ps;
       }
       // sorted position of entry e (0 <= e < K)
       auto posmap = [&](int64_t e) -> int64_t {
-        if (!zc) return ps + e;
+        if (!zc || whole) return ps + w0 * kRowsChunk + e;   // (zc: one piece, ps = c0)
         int lo = 0, hi = nw - 1;   // last chunk with cpre <= e
         while (lo < hi) {
           const int mid = (lo + hi + 1) >> 1;
@@ -1071,21 +1079,23 @@ __global__ __launch_bounds__(1024) void rows_serial_kernel(RowsGroup g, int T, i
             jj = 1;
           }
           for (; jj < nv && (jj & 3); ++jj) acc = acc + sp[jj];
-          // 16-B reads, the next 8 positions' issued before these 8 adds
-          if (jj + 8 <= nv) {
-            float4 xa0 = *reinterpret_cast<const float4*>(sp + jj);
-            float4 xa1 = *reinterpret_cast<const float4*>(sp + jj + 4);
-            for (; jj + 16 <= nv; jj += 8) {
-              const float4 xb0 = *reinterpret_cast<const float4*>(sp + jj + 8);
-              const float4 xb1 = *reinterpret_cast<const float4*>(sp + jj + 12);
-              acc = acc + xa0.x; acc = acc + xa0.y; acc = acc + xa0.z; acc = acc + xa0.w;
-              acc = acc + xa1.x; acc = acc + xa1.y; acc = acc + xa1.z; acc = acc + xa1.w;
-              xa0 = xb0;
-              xa1 = xb1;
+          // 16-B reads 16 positions ahead of the chain: four fixed registers,
+          // each reloaded right after its 4 adds (no rotation moves between
+          // the adds), so a read has 12 adds of cover for its latency
+          if (jj + 16 <= nv) {
+            auto ld4 = [&](int o) { return *reinterpret_cast<const float4*>(sp + o); };
+            float4 r0 = ld4(jj), r1 = ld4(jj + 4), r2 = ld4(jj + 8), r3 = ld4(jj + 12);
+            auto add4 = [&](const float4& v) {
+              acc = acc + v.x; acc = acc + v.y; acc = acc + v.z; acc = acc + v.w;
+            };
+            for (; jj + 32 <= nv; jj += 16) {
+              add4(r0); r0 = ld4(jj + 16);
+              add4(r1); r1 = ld4(jj + 20);
+              add4(r2); r2 = ld4(jj + 24);
+              add4(r3); r3 = ld4(jj + 28);
             }
-            acc = acc + xa0.x; acc = acc + xa0.y; acc = acc + xa0.z; acc = acc + xa0.w;
-            acc = acc + xa1.x; acc = acc + xa1.y; acc = acc + xa1.z; acc = acc + xa1.w;
-            jj += 8;
+            add4(r0); add4(r1); add4(r2); add4(r3);
+            jj += 16;
           }
           for (; jj < nv; ++jj) acc = acc + sp[jj];
         }

@@ -433,14 +433,15 @@ __global__ __launch_bounds__(256) void din_mlp_fwd_kernel(
 // backward: one lane per position p < cap.  p < P: the MLP backward from the
 // score gradient; the facts gradient (already holding the pool's) gains
 // d f + q * d(q f); per-position buffers for the weight-gradient GEMMs and the
-// per-sample sums.  P <= p < cap: zero columns (the GEMMs run over cap).
+// per-sample sums.  P <= p < cap: zero columns of every buffer the weight-
+// gradient GEMMs read (they run over cap; the forward wrote only p < P).
 template <int H, int N1, int N2>
 __global__ __launch_bounds__(256) void din_mlp_bwd_kernel(
     const int32_t* __restrict__ pos, const int32_t* __restrict__ off, int64_t B, int64_t T,
     int64_t cap, const float* __restrict__ facts, const float* __restrict__ q,
     const float* __restrict__ w1p, const float* __restrict__ w2t, const float* __restrict__ w3,
-    const float* __restrict__ gscores, const float* __restrict__ h1t,
-    const float* __restrict__ h2t, float* __restrict__ gfacts, float* __restrict__ da1t,
+    const float* __restrict__ gscores, float* __restrict__ h1t,
+    float* __restrict__ h2t, float* __restrict__ gfacts, float* __restrict__ da1t,
     float* __restrict__ da2t, float* __restrict__ xt, float* __restrict__ dsc,
     float* __restrict__ dqp) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -448,9 +449,9 @@ __global__ __launch_bounds__(256) void din_mlp_bwd_kernel(
   const int64_t P = off[B];
   if (p >= P) {
 #pragma unroll 8
-    for (int j = 0; j < N1; ++j) da1t[(int64_t)j * cap + p] = 0.f;
+    for (int j = 0; j < N1; ++j) da1t[(int64_t)j * cap + p] = h1t[(int64_t)j * cap + p] = 0.f;
 #pragma unroll 8
-    for (int m = 0; m < N2; ++m) da2t[(int64_t)m * cap + p] = 0.f;
+    for (int m = 0; m < N2; ++m) da2t[(int64_t)m * cap + p] = h2t[(int64_t)m * cap + p] = 0.f;
 #pragma unroll 8
     for (int k = 0; k < 2 * H; ++k) xt[(int64_t)k * cap + p] = 0.f;
     dsc[p] = 0.f;
