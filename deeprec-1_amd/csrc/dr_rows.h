@@ -183,4 +183,57 @@ __device__ __forceinline__ void load_row_u(Row<VEC, G, CPL>& x, const float* p, 
   }
 }
 
+// One column's serial chain over the LDS stage sp[0, nv) (16-B aligned):
+// acc = acc + sp[0] + sp[1] + ... in order (fresh: the chain starts at
+// sp[0]).  The 16-B reads run 16 positions ahead of the adds in four fixed
+// registers, each reloaded right after its 4 adds, with counted lgkmcnt
+// waits -- as inline asm, because the compiler otherwise re-issued all four
+// reads and waited for them every 4 positions (~20 cycles per position
+// measured, against ~4-8 for the add chain).  The wait takes the register
+// it guards as an operand, so the adds cannot be scheduled above it.
+#define DR_LDS4(R, A, OFF) \
+  asm volatile("ds_read_b128 %0, %1 offset:" #OFF : "=v"(R) : "v"(A))
+#define DR_LGKM(N, R) asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(R))
+__device__ __forceinline__ float chain_walk(const float* sp, int nv, bool& fresh, float acc) {
+  int jj = 0;
+  if (fresh) {
+    acc = sp[0];
+    fresh = false;
+    jj = 1;
+  }
+  for (; jj < nv && (jj & 3); ++jj) acc = acc + sp[jj];
+  if (jj + 16 <= nv) {
+    typedef __attribute__((address_space(3))) const float lds_f;
+    uint32_t a = (uint32_t)(size_t)(lds_f*)(sp + jj);
+    // nothing of the compiler's own in flight: its wait pass then puts no
+    // lgkmcnt(0) inside the loop (it does not see the asm reads)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    f4v r0, r1, r2, r3;
+    DR_LDS4(r0, a, 0);
+    DR_LDS4(r1, a, 16);
+    DR_LDS4(r2, a, 32);
+    DR_LDS4(r3, a, 48);
+    auto add4 = [&](const f4v& v) {
+      acc = acc + v.x; acc = acc + v.y; acc = acc + v.z; acc = acc + v.w;
+    };
+    for (; jj + 32 <= nv; jj += 16) {
+      DR_LGKM(3, r0); add4(r0); DR_LDS4(r0, a, 64);
+      DR_LGKM(3, r1); add4(r1); DR_LDS4(r1, a, 80);
+      DR_LGKM(3, r2); add4(r2); DR_LDS4(r2, a, 96);
+      DR_LGKM(3, r3); add4(r3); DR_LDS4(r3, a, 112);
+      a += 64;
+    }
+    DR_LGKM(3, r0); add4(r0);
+    DR_LGKM(2, r1); add4(r1);
+    DR_LGKM(1, r2); add4(r2);
+    DR_LGKM(0, r3); add4(r3);
+    jj += 16;
+  }
+  for (; jj < nv; ++jj) acc = acc + sp[jj];
+  return acc;
+}
+#undef DR_LDS4
+#undef DR_LGKM
+
 }  // namespace dr

@@ -77,10 +77,21 @@ static constexpr int64_t kRowsMaxDim = 1024;
 // scanned in parallel (rows_nz_kernel: chunks of kRowsChunk positions, each
 // compacted to its nonzero terms in ascending order) and the serial walk
 // visits only those -- e.g. a padding id whose positions are masked out
-// downstream.  A window of chunks that is mostly nonzero (DIN's padding id:
-// its history positions feed the unmasked his_sum, model.py:98, so they all
-// carry gradient) is walked whole instead, without the compacted indirection.
-// DR_GRAD_ZERO_SKIP=0 (A/B) walks every term.
+// downstream.  A run that is mostly nonzero (DIN's padding id: its history
+// positions feed the unmasked his_sum, model.py:98, so they all carry
+// gradient) is walked whole instead (run_sparse()).  DR_GRAD_ZERO_SKIP=0
+// (A/B) walks every term.
+// Plain-sum runs (no weights, no mean / sqrtn scale, not walked compacted)
+// go to rows_serial_dma_kernel; DR_GRAD_SERIAL_DMA=0 (A/B) keeps them in
+// rows_serial_kernel.
+static int serial_dma() {
+  static const int v = [] {
+    const char* e = getenv("DR_GRAD_SERIAL_DMA");
+    return (e && atoi(e) == 0) ? 0 : 1;
+  }();
+  return v;
+}
+
 static int64_t zero_scan() {
   static const int64_t v = [] {
     const char* e = getenv("DR_GRAD_ZERO_SKIP");
@@ -114,7 +125,17 @@ struct RowsLong {
   int32_t* nchunk;
   int32_t* ccnt;           // per chunk: its nonzero terms
   int32_t* kpos;           // [N] chunk k of run c0: nonzero positions at c0 + k*kRowsChunk ..
+  int32_t* rnz;            // per long run: its nonzero terms (zero scan)
+  float* zrow;             // 64 zeros (rows_expand_kernel): the term of an invalid bag
+  int dma;                 // rows_serial_dma_kernel takes the plain-sum runs (serial_dma())
 };
+
+// A zero-scanned run is walked compacted only when at most half its terms
+// are nonzero (the same test in both serial kernels, so they split the runs
+// between them exactly).
+__device__ __forceinline__ bool run_sparse(const RowsLong& L, int i, int np, int64_t len) {
+  return np == 1 && L.cfirst[i] >= 0 && 2 * (int64_t)L.rnz[i] <= len;
+}
 
 // Table of global position i (lane-varying; koff staged in LDS).
 __device__ __forceinline__ int tab_of(const int64_t* koff, int T, int64_t i) {
@@ -757,6 +778,7 @@ __device__ __forceinline__ bool in_run(const RowsLong& L, int64_t N, int64_t q, 
 // the run ends in: a run's positions are contiguous, so in_run is a prefix),
 // then its pieces of serial_max() positions as work items.
 __global__ __launch_bounds__(256) void rows_expand_kernel(RowsGroup g, int T, RowsLong L) {
+  if (blockIdx.x == 0 && threadIdx.x < 64) L.zrow[threadIdx.x] = 0.f;
   __shared__ int64_t sk[DR_MAX_GROUP + 1];
   __shared__ int smin;
   __shared__ int sfirst;
@@ -804,6 +826,7 @@ __global__ __launch_bounds__(256) void rows_expand_kernel(RowsGroup g, int T, Ro
       sfirst = fi;
       const int cf = nch ? atomicAdd(L.nchunk, nch) : -1;
       L.cfirst[i] = cf;
+      L.rnz[i] = 0;
       smin = cf;
     }
     __syncthreads();
@@ -872,35 +895,43 @@ __global__ __launch_bounds__(256) void rows_nz_kernel(RowsGroup g, int T, int di
     int before = 0;
     for (int w = 0; w < wv; ++w) before += wc[w];
     if (nz) L.kpos[cs + before + __popcll(bm & lanemask_lt())] = (int32_t)q;
-    if (tid == 0) L.ccnt[c] = wc[0] + wc[1] + wc[2] + wc[3];
+    if (tid == 0) {
+      const int nzc = wc[0] + wc[1] + wc[2] + wc[3];
+      L.ccnt[c] = nzc;
+      if (nzc) atomicAdd(&L.rnz[i], nzc);
+    }
     __syncthreads();   // wc is rewritten by the next chunk
   }
 }
 
 // One block per (piece, column slice of SW columns): the piece's terms in
-// ascending position order.  All 256 threads load the gradient-row slices of
-// S positions at a time (R loads in flight per thread, the next stage's rows
-// issued before this stage is summed) and write them, scaled, into LDS; wave
-// 0 then walks the serial chain of each column (one lane per column) through
-// the stage.  A one-piece run is finished here; a piece of a longer run
-// stores its partial for rows_combine_kernel.
+// ascending position order.  Wave 0 walks the serial chain of each column
+// (one lane per column, at raised priority); waves 1..15 load the gradient-row
+// slices S positions at a time (R loads in flight per thread, bag rows one
+// stage ahead of the row loads), scale them and write them into LDS.  The
+// stage is double-buffered: while the walker sums stage n out of one buffer
+// the loaders write stage n + 1 into the other and issue the loads of stage
+// n + 2, one barrier per stage -- the walk and the fill overlap.  A one-piece
+// run is finished here; a piece of a longer run stores its partial for
+// rows_combine_kernel.
 template <int VEC, int SW, bool SGD, bool WB>
 __global__ __launch_bounds__(1024) void rows_serial_kernel(RowsGroup g, int T, int dim, RowsLong L,
                                                            RowsSgd sg) {
   using V = typename VecT<VEC>::T;
-  constexpr int NT = 1024;                 // threads: 16 waves load, wave 0 also walks
+  constexpr int NT = 1024;                 // threads: wave 0 walks, waves 1..15 load
+  constexpr int NL = NT - 64;              // loader threads
   constexpr int SV = SW / VEC;             // vectors of a position's slice
-  constexpr int PI = NT / SV;              // positions per load instruction
-  constexpr int R = VEC == 4 ? 4 : 8;      // loads in flight per thread (<= 128 VGPRs, no spill)
+  constexpr int PI = NL / SV;              // positions per load instruction
+  constexpr int R = VEC == 4 ? 4 : 6;      // loads in flight per thread (<= 128 VGPRs, no spill)
   static_assert(VEC == 1 || VEC == 2 || VEC == 4, "vector width");
-  constexpr int S = PI * R;                // positions per stage (S * SW = 8 K / 16 K floats)
+  constexpr int S = PI * R;                // positions per stage (S * SW <= 15 K floats)
   constexpr int SP = S + 4;                // column stride of the transposed stage
   constexpr int WCH = 1024;                // zero-scan chunks per window (prefix in LDS)
-  static_assert(SV >= 1 && NT % SV == 0 && S % 4 == 0, "slice shape");
-  // the stage TRANSPOSED, [column][position] (stride S + 4: the loaders'
-  // column writes spread over the banks, the walker's 16-B reads stay
-  // aligned): a lane walks its column 4 positions per LDS read
-  __shared__ __attribute__((aligned(16))) float stage[SW * SP];
+  static_assert(SV >= 1 && NL % SV == 0 && S % 4 == 0, "slice shape");
+  // two stages, each TRANSPOSED, [column][position] (stride S + 4: the
+  // loaders' column writes spread over the banks, the walker's 16-B reads
+  // stay aligned): a lane walks its column 4 positions per LDS read
+  __shared__ __attribute__((aligned(16))) float stage[2 * SW * SP];
   __shared__ int64_t sk[DR_MAX_GROUP + 1];
   __shared__ int32_t cpre[WCH + 1];
   __shared__ int32_t wsum[NT / 64];
@@ -909,9 +940,14 @@ __global__ __launch_bounds__(1024) void rows_serial_kernel(RowsGroup g, int T, i
   const int nsl = (dim + SW - 1) / SW;
   const int64_t total = (int64_t)(*L.nitems) * nsl;
   const int tid = threadIdx.x;
-  const int pv = tid / SV, cv = tid % SV;
+  // wave-uniform, and known so to the compiler (readfirstlane): the walk
+  // below then compiles as a scalar-controlled loop, not an exec-masked one
+  const bool walker = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;
+  const int lt = walker ? 0 : tid - 64;    // loader index
+  const int pv = lt / SV, cv = lt % SV;
   const int lane = tid & 63;
   const int lc = lane < SW ? lane : 0;
+  if (walker) __builtin_amdgcn_s_setprio(3);   // the chain is the critical path
   for (int64_t wi = blockIdx.x; wi < total; wi += gridDim.x) {   // block-uniform
     const int j = (int)(wi / nsl), slice = (int)(wi % nsl);
     const int i = __builtin_amdgcn_readfirstlane(L.items[2 * j]);
@@ -936,15 +972,15 @@ __global__ __launch_bounds__(1024) void rows_serial_kernel(RowsGroup g, int T, i
     // zero-scanned run (rows_nz_kernel): walk only its nonzero terms, chunk by
     // chunk in ascending order; a zero-started chain is unchanged by the
     // skipped +-0.0 terms (zero_scan()).  Otherwise entry e = position ps + e.
-    const int cf = np == 1 ? __builtin_amdgcn_readfirstlane(L.cfirst[i]) : -1;
-    const bool zc = cf >= 0;
+    const bool zc = run_sparse(L, i, np, len);
+    if (L.dma && !wt && !ms && !zc) continue;   // rows_serial_dma_kernel's run
+    const int cf = zc ? __builtin_amdgcn_readfirstlane(L.cfirst[i]) : -1;
     const int64_t nch = zc ? (len + kRowsChunk - 1) / kRowsChunk : 1;
     float acc = 0.f;
     bool fresh = !(k == 0 && zs);   // first term: 0 + y (zero-started sum) or y
     for (int64_t w0 = 0; w0 < nch; w0 += WCH) {   // windows of chunks (plain: one)
       int64_t K;
       int nw = 1;
-      bool whole = false;
       if (zc) {
         nw = (int)(nch - w0 < WCH ? nch - w0 : WCH);
         // exclusive prefix of the window's chunk counts (one chunk per
@@ -964,17 +1000,12 @@ __global__ __launch_bounds__(1024) void rows_serial_kernel(RowsGroup g, int T, i
         if (tid == nw - 1) cpre[nw] = before + cnt;
         __syncthreads();
         K = cpre[nw];
-        // mostly nonzero: walk the window's positions whole (the same chain)
-        const int64_t wend = (w0 + nw) * kRowsChunk < len ? (w0 + nw) * kRowsChunk : len;
-        const int64_t wpos = wend - w0 * kRowsChunk;
-        whole = 2 * K > wpos;
-        if (whole) K = wpos;
       } else {
         K = pe - ps;
       }
       // sorted position of entry e (0 <= e < K)
       auto posmap = [&](int64_t e) -> int64_t {
-        if (!zc || whole) return ps + w0 * kRowsChunk + e;   // (zc: one piece, ps = c0)
+        if (!zc) return ps + e;
         int lo = 0, hi = nw - 1;   // last chunk with cpre <= e
         while (lo < hi) {
           const int mid = (lo + hi + 1) >> 1;
@@ -1011,30 +1042,24 @@ __global__ __launch_bounds__(1024) void rows_serial_kernel(RowsGroup g, int T, i
           y[r] = gld(reinterpret_cast<const V*>(src + rr * ts));
         }
       };
-      auto put = [&](int r, V x) {   // term (r, pv) -> its column rows of the stage
+      auto put = [&](float* stg, int r, V x) {   // term (r, pv) -> its column rows of the stage
         const int pos = r * PI + pv;
         if constexpr (VEC == 4) {
-          float* c = stage + (cv * 4) * SP + pos;
+          float* c = stg + (cv * 4) * SP + pos;
           c[0] = x.x;
           c[SP] = x.y;
           c[2 * SP] = x.z;
           c[3 * SP] = x.w;
         } else if constexpr (VEC == 2) {
-          float* c = stage + (cv * 2) * SP + pos;
+          float* c = stg + (cv * 2) * SP + pos;
           c[0] = x.x;
           c[SP] = x.y;
         } else {
-          stage[cv * SP + pos] = x;
+          stg[cv * SP + pos] = x;
         }
       };
-      if (K > 0) {
-        load_idx(0);
-        take();
-        load_rows();
-        load_idx(S);
-      }
-      for (int64_t b0 = 0; b0 < K; b0 += S) {
-        // y: this stage's rows in flight; rq: the next stage's bag rows
+      // the rows in flight (y) -> stage buffer stg, scaled (entries from b0)
+      auto fill = [&](float* stg, int64_t b0) {
         if (wt || ms) {   // block-uniform: the terms' factors (rows_term), then scaled
           float mf[R], df[R];
 #pragma unroll
@@ -1055,51 +1080,41 @@ __global__ __launch_bounds__(1024) void rows_serial_kernel(RowsGroup g, int T, i
             } else if (mf[r] != 1.f) {
               x = vmul(x, mf[r]);
             }
-            put(r, x);
+            put(stg, r, x);
           }
         } else {
 #pragma unroll
           for (int r = 0; r < R; ++r) {
             V x = y[r];
             if ((zmask >> r) & 1u) x = vzero<V>();
-            put(r, x);
+            put(stg, r, x);
           }
         }
-        __syncthreads();
+      };
+      if (!walker && K > 0) {   // stage 0 into buffer 0; stage 1's rows in flight
+        load_idx(0);
         take();
-        load_rows();              // the next stage's rows: in flight while wave 0 sums this one
-        load_idx(b0 + 2 * S);
-        if (tid < 64) {           // wave-uniform: lane lc walks column lc
+        load_rows();
+        load_idx(S);
+        fill(stage, 0);
+        take();
+        load_rows();
+        load_idx(2 * S);
+      }
+      __syncthreads();
+      int sb = 0;   // the buffer holding the stage at b0
+      for (int64_t b0 = 0; b0 < K; b0 += S, sb ^= 1) {
+        if (walker) {             // wave-uniform: lane lc walks column lc
           const int nv = (int)(K - b0 < S ? K - b0 : S);
-          const float* sp = stage + lc * SP;
-          int jj = 0;
-          if (fresh) {
-            acc = sp[0];
-            fresh = false;
-            jj = 1;
-          }
-          for (; jj < nv && (jj & 3); ++jj) acc = acc + sp[jj];
-          // 16-B reads 16 positions ahead of the chain: four fixed registers,
-          // each reloaded right after its 4 adds (no rotation moves between
-          // the adds), so a read has 12 adds of cover for its latency
-          if (jj + 16 <= nv) {
-            auto ld4 = [&](int o) { return *reinterpret_cast<const float4*>(sp + o); };
-            float4 r0 = ld4(jj), r1 = ld4(jj + 4), r2 = ld4(jj + 8), r3 = ld4(jj + 12);
-            auto add4 = [&](const float4& v) {
-              acc = acc + v.x; acc = acc + v.y; acc = acc + v.z; acc = acc + v.w;
-            };
-            for (; jj + 32 <= nv; jj += 16) {
-              add4(r0); r0 = ld4(jj + 16);
-              add4(r1); r1 = ld4(jj + 20);
-              add4(r2); r2 = ld4(jj + 24);
-              add4(r3); r3 = ld4(jj + 28);
-            }
-            add4(r0); add4(r1); add4(r2); add4(r3);
-            jj += 16;
-          }
-          for (; jj < nv; ++jj) acc = acc + sp[jj];
+          const float* sp = stage + sb * (SW * SP) + lc * SP;
+          acc = chain_walk(sp, nv, fresh, acc);
+        } else if (b0 + S < K) {  // the next stage into the other buffer, then its successor's loads
+          fill(stage + (sb ^ 1) * (SW * SP), b0 + S);
+          take();
+          load_rows();
+          load_idx(b0 + 3 * S);
         }
-        __syncthreads();   // the stage is rewritten next
+        __syncthreads();   // the next stage is in place; this one may be rewritten
       }
     }
     if (tid < 64) {
@@ -1109,6 +1124,115 @@ __global__ __launch_bounds__(1024) void rows_serial_kernel(RowsGroup g, int T, i
         const int64_t o = SGD ? 0 : sk[t] + (int64_t)L.ex[pc] - L.base[t];
         if (lane < SW && (lane & 1) == 0 && col < dim)
           rows_fin_pair<SGD, WB>(sg, t, u, o, dim, col, acc, nxt, L.gu);
+        if (slice == 0 && lane == 0) rows_fin_run<SGD>(sg, t, u, o, dim, L);
+      } else if (lane < SW && col < dim) {
+        L.part[(int64_t)j * dim + col] = acc;
+      }
+    }
+  }
+}
+
+// The plain-sum runs (rows_serial_kernel's terms with no scale: the sum
+// combiner, unweighted, not walked compacted), one block per (piece, slice of
+// 16 columns).  Waves 1..15 stage the terms by LDS-DMA instead of through
+// registers: loader wave w owns positions [64 w, 64 w + 64) of each stage of
+// 960 and issues, per column, one global_load_lds of 4 B per lane (the term's
+// column c lands at stage[c][position], the walker's transposed layout, with
+// no register round trip and no LDS write instructions); an invalid bag reads
+// the zero row.  Two stages in the ring: stage n + 1 lands while wave 0
+// walks stage n, the loaders' bag rows one stage further ahead; one raw
+// barrier per stage after each loader's counted vmcnt (its DMAs landed).
+template <bool SGD, bool WB>
+__global__ __launch_bounds__(1024) void rows_serial_dma_kernel(RowsGroup g, int T, int dim,
+                                                               RowsLong L, RowsSgd sg) {
+  constexpr int SW = 16;                   // columns per slice
+  constexpr int S = 64 * 15;               // positions per stage: 64 per loader wave
+  constexpr int SP = S + 4;                // column stride (16-B walker reads, banks spread)
+  __shared__ __attribute__((aligned(16))) float stage[2 * SW * SP];
+  __shared__ int64_t sk[DR_MAX_GROUP + 1];
+  if (threadIdx.x <= T) sk[threadIdx.x] = g.koff[threadIdx.x];
+  __syncthreads();
+  const int nsl = (dim + SW - 1) / SW;
+  const int64_t total = (int64_t)(*L.nitems) * nsl;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const bool walker = wave == 0;           // wave-uniform (an SGPR: scalar-controlled walk)
+  const int lw = walker ? 0 : wave - 1;    // loader wave: its 64 positions of a stage
+  const int lc = lane < SW ? lane : 0;
+  if (walker) __builtin_amdgcn_s_setprio(3);   // the chain is the critical path
+  for (int64_t wi = blockIdx.x; wi < total; wi += gridDim.x) {   // block-uniform
+    const int j = (int)(wi / nsl), slice = (int)(wi % nsl);
+    const int i = __builtin_amdgcn_readfirstlane(L.items[2 * j]);
+    const int k = __builtin_amdgcn_readfirstlane(L.items[2 * j + 1]);
+    const int64_t c0 = __builtin_amdgcn_readfirstlane(L.longs[i]);
+    const int64_t len = __builtin_amdgcn_readfirstlane(L.rlen[i]);
+    const int64_t smax = L.smax;
+    const int np = (int)((len + smax - 1) / smax);
+    const int64_t ps = c0 + (int64_t)k * smax;
+    const int64_t pe = c0 + len < ps + smax ? c0 + len : ps + smax;
+    const int32_t pc = __builtin_amdgcn_readfirstlane(L.perm[c0]);
+    const uint32_t u = (uint32_t)__builtin_amdgcn_readfirstlane((int)L.skey[c0]);
+    const int t = __builtin_amdgcn_readfirstlane(tab_of(sk, T, pc));
+    const dr_pool_grad_desc& d = g.d[t];
+    const bool wt = d.weights != nullptr;
+    const bool ms = !wt && d.combiner != DR_COMBINER_SUM;
+    if (wt || ms || run_sparse(L, i, np, len)) continue;   // rows_serial_kernel's run
+    const int64_t K = pe - ps;
+    const int64_t nst = (K + S - 1) / S;
+    const int c0l = slice * SW;
+    const int ncol = dim - c0l < SW ? dim - c0l : SW;
+    const int64_t ts = d.top_stride;
+    // this lane's bag row for the stage at entry b0 (clamped to the piece),
+    // and the term source it gives -- split, so the row load is waited for
+    // only where the next stage's DMAs use it
+    auto rowof = [&](int64_t b0) -> int32_t {
+      int64_t e = b0 + 64 * lw + lane;
+      e = e < K ? e : K - 1;
+      return L.srow[ps + e];
+    };
+    auto srcof = [&](int32_t r) -> const float* {
+      return r >= 0 ? d.top_grad + (int64_t)r * ts + c0l : L.zrow;
+    };
+    auto dma = [&](const float* src, int slot) {
+      char* base = reinterpret_cast<char*>(stage + slot * (SW * SP) + 64 * lw);
+      for (int c = 0; c < ncol; ++c)   // uniform trip count
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + c),
+                                         (__attribute__((address_space(3))) void*)(base + c * SP * 4),
+                                         4, 0, 0);
+    };
+    int32_t nxt = 0;
+    if (!walker) {   // stage 0 into slot 0, stage 1's bag rows in flight
+      dma(srcof(rowof(0)), 0);
+      asm volatile("" ::: "memory");   // the row load below stays behind the DMAs
+      nxt = rowof(S);
+      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");   // this wave's stage-0 DMAs landed
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    float acc = 0.f;
+    bool fresh = !(k == 0);   // first term: 0 + y (the sum combiner is zero-started) or y
+    for (int64_t st = 0; st < nst; ++st) {
+      if (walker) {
+        const int64_t b0 = st * S;
+        const int nv = (int)(K - b0 < S ? K - b0 : S);
+        const float* sp = stage + (st & 1) * (SW * SP) + lc * SP;
+        acc = chain_walk(sp, nv, fresh, acc);
+      } else if (st + 1 < nst) {
+        dma(srcof(nxt), (int)((st + 1) & 1));   // stage st+1 into the slot stage st-1 left
+        asm volatile("" ::: "memory");
+        nxt = rowof((st + 2) * S);       // (clamped past the end: one load, always)
+        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");   // stage st+1's DMAs landed
+      }
+      __builtin_amdgcn_s_barrier();   // stage st+1 in place (all loaders); stage st walked
+      asm volatile("" ::: "memory");
+    }
+    if (walker) {
+      const int col = c0l + lane;
+      const float nx = __shfl_down(acc, 1, 64);
+      if (np == 1) {
+        const int64_t o = SGD ? 0 : sk[t] + (int64_t)L.ex[pc] - L.base[t];
+        if (lane < SW && (lane & 1) == 0 && col < dim)
+          rows_fin_pair<SGD, WB>(sg, t, u, o, dim, col, acc, nx, L.gu);
         if (slice == 0 && lane == 0) rows_fin_run<SGD>(sg, t, u, o, dim, L);
       } else if (lane < SW && col < dim) {
         L.part[(int64_t)j * dim + col] = acc;
@@ -1202,13 +1326,15 @@ struct RowsWs {
   int32_t* nchunk;
   int32_t* ccnt;
   int32_t* kpos;
+  int32_t* rnz;
+  float* zrow;
   void* sort_ws;
   size_t sort_bytes;
   void* scan_ws;
   RowsLong longrun(uint64_t* gptr, float* gu) const {
     return RowsLong{kout, perm, ex, base, srow, smul, sdiv, longs, nlong, rlen, rfirst, items,
                     nitems, gptr, gu, part, serial_max(), zero_scan(), cfirst, crun, nchunk,
-                    ccnt, kpos};
+                    ccnt, kpos, rnz, zrow, serial_dma()};
   }
 };
 
@@ -1247,6 +1373,8 @@ static RowsWs carve_rows(void* ws, int64_t n, size_t* used) {
   w.nchunk = c.take<int32_t>(1);
   w.ccnt = c.take<int32_t>(chunks);
   w.kpos = c.take<int32_t>(nn);
+  w.rnz = c.take<int32_t>(runs);
+  w.zrow = c.take<float>(64);
   w.sort_bytes = sort_pairs_u32_ws_bytes(nn);
   w.sort_ws = c.take<char>(w.sort_bytes);
   w.scan_ws = c.take<char>(scan_ws_bytes(nn));
@@ -1312,6 +1440,13 @@ static void launch_long(const RowsGroup& g, int T, int dim, const RowsLong& L, c
     }
   }
 #undef DR_SERIAL
+  if (L.dma) {
+    const int64_t nsl16 = ceil_div(dim, 16);
+    int64_t db = runs * nsl16;
+    if (db > 1024) db = 1024;
+    hipLaunchKernelGGL((rows_serial_dma_kernel<SGD, WB>), dim3((unsigned)db), dim3(1024), 0, s, g,
+                       T, dim, L, sg);
+  }
   if (N > L.smax) {
     const int64_t big = N / (L.smax + 1) + 1;
     hipLaunchKernelGGL((rows_combine_kernel<SGD, WB>), dim3((unsigned)(big < 256 ? big : 256)),

@@ -1377,6 +1377,301 @@ __global__ __launch_bounds__(512, 1) void crossnet_8ph_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// The 256 x 256 layer at ONE wave per SIMD (crossnet_w4_kernel): 4 waves of
+// 128 x 128 outputs each (8 x 8 v_mfma_f32_16x16x32_bf16 tiles = 256
+// accumulator registers per lane).  The accumulators are pinned in AGPRs by
+// issuing the MFMAs as inline asm with "+a" operands (written with the
+// builtin, the register allocator rotated them through VGPRs: ~440 accvgpr
+// moves per 128 MFMAs, round 4).  No barrier-locked pairing of two waves per
+// SIMD: each wave keeps its matrix pipe busy on its own, 64 MFMAs (1024
+// cycles) per K step of 32 between two barriers.
+//   * LDS: a ring of 4 K-32 stages [A 256 x 64 B | B 256 x 64 B] (128 KB),
+//     filled by global_load_lds three stages ahead; 16-B chunk c of image row
+//     r stored at c ^ (((r >> 2) & 1) << 1) -- the four ds_read_b128 lane
+//     groups of a fragment read hit 16 distinct slots (conflict-free);
+//   * fragments one stage ahead: the 16 reads of stage s + 1 are issued
+//     before the 64 MFMAs of stage s, which use registers filled one
+//     iteration earlier;
+//   * ordering per iteration s: counted vmcnt (this wave's DMAs of stage s+1
+//     landed) then s_barrier (every wave's), then the DMA of stage s+3 into
+//     the slot stage s-1 left -- whose fragments every wave consumed (its
+//     MFMAs waited for them) before it reached this barrier.
+// ---------------------------------------------------------------------------
+static constexpr int W4_IMG = 256 * 64;        // one operand's K-32 stage image
+static constexpr int W4_BUF = 2 * W4_IMG;      // [A | B]
+
+__device__ __forceinline__ int w4_sw(int r) { return ((r >> 2) & 1) << 1; }
+
+// image rows [wave * 64, wave * 64 + 64) <- global rows row0 + r, k0..k0+31:
+// 4 wave instructions of 16 rows x 64 B
+__device__ __forceinline__ void w4_stage(const uint16_t* __restrict__ X, int64_t rows_valid,
+                                         int64_t row0, int d, int k0, char* img, int wave,
+                                         int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r0 = (wave * 4 + i) * 16;
+    const int r = r0 + (lane >> 2);
+    const int c = (lane & 3) ^ w4_sw(r);
+    int64_t gr = row0 + r;
+    if (gr >= rows_valid) gr = rows_valid - 1;  // rows past the end feed discarded outputs
+    const uint16_t* src = X + gr * (int64_t)d + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(img + r0 * 64),
+                                     16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 w4_frag(const char* img, int r, int c) {
+  return *reinterpret_cast<const bf16x8*>(img + r * 64 + ((c ^ w4_sw(r)) << 4));
+}
+
+#define W4_MFMA(C, A, B) \
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(C) : "v"(A), "v"(B))
+
+// MODE 1: out = x0 * (xl W^T + b) + xl (lin_out = xl W^T + b); MODE 2: out =
+// xl W^T + x0 (the input gradient, as crossnet_8ph_kernel); MODE 0: the loop
+// alone (timing build).
+template <int MODE, int GM, bool IL>
+__global__ __launch_bounds__(256, 1) void crossnet_w4_kernel(
+    const uint16_t* __restrict__ x0, const uint16_t* __restrict__ xl,
+    const uint16_t* __restrict__ W, const float* __restrict__ bias, int64_t M, int d,
+    int ncols, uint16_t* __restrict__ out, uint16_t* __restrict__ lin_out) {
+  __shared__ __attribute__((aligned(1024))) char lds[4 * W4_BUF];  // 128 KB
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int64_t nwg = (int64_t)gridDim.x;
+  const int64_t orig = blockIdx.x;
+  const int64_t xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t tile = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int ntn = ncols / 256 + (ncols % 256 ? 1 : 0);
+  int64_t m0;
+  int n0;
+  {  // groups of GM row panels walked column-major (crossnet_8ph_kernel)
+    const int64_t ntm = (M + 255) / 256;
+    const int64_t g = tile / ((int64_t)GM * ntn), idx = tile % ((int64_t)GM * ntn);
+    const int64_t rows = ntm - g * GM < GM ? ntm - g * GM : GM;
+    m0 = (g * GM + idx % rows) * 256;
+    n0 = (int)(idx / rows) * 256;
+  }
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = d / 32;
+  auto img = [&](int s) -> char* { return lds + (s & 3) * W4_BUF; };
+  auto stage = [&](int s) {
+    w4_stage(xl, M, m0, d, s * 32, img(s), wave, lane);
+    w4_stage(W, d, n0, d, s * 32, img(s) + W4_IMG, wave, lane);
+  };
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8 F0[16], F1[16];   // [0, 8): A fragments (rows), [8, 16): B fragments (columns)
+  auto read = [&](int s, bf16x8 (&F)[16]) {
+    const char* a = img(s);
+    const char* b = a + W4_IMG;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) F[i] = w4_frag(a, wr * 128 + i * 16 + fr, fq);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) F[8 + j] = w4_frag(b, wc * 128 + j * 16 + fr, fq);
+  };
+  auto mma = [&](bf16x8 (&F)[16]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) W4_MFMA(acc[i][j], F[i], F[8 + j]);
+  };
+  // IL: the 16 fragment reads (inline asm, so they keep their place) and the
+  // 8 DMA pieces of stage s + 3 spread over the 64 MFMAs -- a read after
+  // every 4th MFMA, a DMA piece after every 8th -- instead of issued in a
+  // block in front of them.  The DMAs are unconditional (past the last stage
+  // they reload stage nk - 1 into the slot stage s - 1 left: dead data), so
+  // vmcnt(8) always means "stage s + 1 landed".
+  typedef __attribute__((address_space(3))) char lds_t;
+  const uint32_t lb = (uint32_t)(fr * 64 + ((fq ^ w4_sw(fr)) << 4));
+  auto dma_piece = [&](int s3, int p) {
+    const int k0 = s3 * 32;
+    const int i = p & 3;
+    const int r0 = (wave * 4 + i) * 16;
+    const int r = r0 + (lane >> 2);
+    const int c = (lane & 3) ^ w4_sw(r);
+    char* dst = img(s3) + (p >> 2) * W4_IMG + r0 * 64;
+    const uint16_t* X = (p >> 2) ? W : xl;
+    const int64_t rv = (p >> 2) ? (int64_t)d : M;
+    int64_t gr = ((p >> 2) ? (int64_t)n0 : m0) + r;
+    if (gr >= rv) gr = rv - 1;
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(X + gr * (int64_t)d + k0 + c * 8),
+        (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  };
+  auto iter_il = [&](int s, bf16x8 (&Fc)[16], bf16x8 (&Fn)[16]) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): Fc complete
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // stage s+1 landed (this wave's DMAs)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int s1 = s + 1 < nk ? s + 1 : s;
+    const int s3 = s + 3 < nk ? s + 3 : nk - 1;
+    const uint32_t ra = (uint32_t)(size_t)(lds_t*)img(s1) + lb + wr * 8192;
+    const uint32_t rb = (uint32_t)(size_t)(lds_t*)img(s1) + W4_IMG + lb + wc * 8192;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        W4_MFMA(acc[i][j], Fc[i], Fc[8 + j]);
+        const int m = i * 8 + j;
+        if ((m & 3) == 3) {
+          const int k = m >> 2;   // 0..15
+          if (k < 8)
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(Fn[k]) : "v"(ra), "i"(k * 1024));
+          else
+            asm volatile("ds_read_b128 %0, %1 offset:%2"
+                         : "=v"(Fn[k]) : "v"(rb), "i"((k - 8) * 1024));
+        }
+        if ((m & 7) == 1) dma_piece(s3, m >> 3);
+      }
+  };
+  auto iter = [&](int s, bf16x8 (&Fc)[16], bf16x8 (&Fn)[16]) {
+    // Fc (read one iteration ago) complete -- as a real s_waitcnt the
+    // compiler's wait pass sees, so it puts no lgkmcnt(0) behind this
+    // iteration's reads in front of the MFMAs
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+    if (s + 2 < nk)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // stage s+1 landed (this wave's DMAs)
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + 3 < nk) stage(s + 3);
+    read(s + 1 < nk ? s + 1 : s, Fn);   // unconditional (a branch would end in a wait)
+    mma(Fc);
+  };
+  if (IL) {   // prologue: stages 0..2 (clamped), stage 0 landed
+    for (int p = 0; p < 8; ++p) dma_piece(0, p);
+    for (int p = 0; p < 8; ++p) dma_piece(1 < nk ? 1 : nk - 1, p);
+    for (int p = 0; p < 8; ++p) dma_piece(2 < nk ? 2 : nk - 1, p);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+  stage(0);
+  if (nk > 1) stage(1);
+  if (nk > 2) stage(2);
+  if (nk > 2)
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (nk > 1)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  read(0, F0);
+  int s = 0;
+  if (IL) {
+    for (; s + 1 < nk; s += 2) {
+      iter_il(s, F0, F1);
+      iter_il(s + 1, F1, F0);
+    }
+    if (s < nk) iter_il(s, F0, F1);
+  } else {
+    for (; s + 1 < nk; s += 2) {
+      iter(s, F0, F1);
+      iter(s + 1, F1, F0);
+    }
+    if (s < nk) iter(s, F0, F1);
+  }
+  // the last MFMAs' results are read below (AGPR -> VGPR): cover their latency
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();   // every wave's last fragment reads done: the ring is reused below
+  if (MODE == 0) {
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (sum == 1234.5678f) out[0] = 0;
+    return;
+  }
+  // Epilogue by 64 x 64 quarters (row half h, column half g): this wave's x0
+  // / xl vectors requested first, the accumulators through LDS (C/D map -> 8
+  // columns per lane), then out / lin formed and stored as 16-B vectors.
+  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+  float* ct = reinterpret_cast<float*>(lds) + wave * 64 * 64;
+  const int cc = (lane & 7) * 8;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int gcol = n0 + wc * 128 + g * 64 + cc;
+    const bool col_ok = gcol < ncols;
+    const int gcol_c = col_ok ? gcol : d - 8;
+    float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (MODE == 1 && bias) {
+      const float4 b0 = *reinterpret_cast<const float4*>(bias + gcol_c);
+      const float4 b1 = *reinterpret_cast<const float4*>(bias + gcol_c + 4);
+      bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
+      bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      u32x4 a0[8], al[8];
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        int64_t grow = m0 + wr * 128 + h * 64 + it * 8 + (lane >> 3);
+        if (grow >= M) grow = M - 1;
+        const int64_t o = grow * d + gcol_c;
+        a0[it] = *reinterpret_cast<const u32x4*>(x0 + o);
+        if (MODE == 1) al[it] = *reinterpret_cast<const u32x4*>(xl + o);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = i * 16 + fq * 4 + r;
+            const int col = (j * 16 + fr) ^ (((row >> 2) & 3) << 4);
+            ct[row * 64 + col] = acc[h * 4 + i][g * 4 + j][r];
+          }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int row = it * 8 + (lane >> 3);
+        const int64_t grow = m0 + wr * 128 + h * 64 + row;
+        const int pc = cc ^ (((row >> 2) & 3) << 4);
+        const float4 l0 = *reinterpret_cast<const float4*>(ct + row * 64 + pc);
+        const float4 l1 = *reinterpret_cast<const float4*>(ct + row * 64 + pc + 4);
+        float lin[8] = {l0.x + bv[0], l0.y + bv[1], l0.z + bv[2], l0.w + bv[3],
+                        l1.x + bv[4], l1.y + bv[5], l1.z + bv[6], l1.w + bv[7]};
+        u32x4 ov, lv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t p0 = a0[it][e];
+          if (MODE == 1) {
+            const uint32_t pl = al[it][e];
+            const float v0 = bf2f((uint16_t)(p0 & 0xffff)) * lin[2 * e] + bf2f((uint16_t)(pl & 0xffff));
+            const float v1 = bf2f((uint16_t)(p0 >> 16)) * lin[2 * e + 1] + bf2f((uint16_t)(pl >> 16));
+            ov[e] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+            lv[e] = (uint32_t)f2bf(lin[2 * e]) | ((uint32_t)f2bf(lin[2 * e + 1]) << 16);
+          } else {  // one fp32 sum of the product and the addend, one rounding
+            const float v0 = lin[2 * e] + bf2f((uint16_t)(p0 & 0xffff));
+            const float v1 = lin[2 * e + 1] + bf2f((uint16_t)(p0 >> 16));
+            ov[e] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+          }
+        }
+        if (grow < M && col_ok) {
+          const int64_t o = grow * d + gcol;
+          *reinterpret_cast<u32x4*>(out + o) = ov;
+          if (MODE == 1 && lin_out) *reinterpret_cast<u32x4*>(lin_out + o) = lv;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ct reads done before it is rewritten
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+#undef W4_MFMA
+
+// ---------------------------------------------------------------------------
 // CrossNet weight gradient dW = u^T x_l (TN: the contraction runs down the
 // rows of both [B, d] operands), on the forward's 256 x 256, four-phase
 // schedule (crossnet_8ph_kernel): the same waves / quadrants / half-tiles,
@@ -1899,6 +2194,23 @@ int dr_crossnet_forward_bf16(const uint16_t* x0, const uint16_t* xl, const uint1
   // ~440 accvgpr moves per 128 MFMAs.)
   static const int variant = getenv("DR_CROSSNET_VARIANT") ? atoi(getenv("DR_CROSSNET_VARIANT"))
                                                            : 8;
+  if (d % 64 == 0 && !legacy && al16 && variant >= 14 && variant <= 17) {
+    // 14: crossnet_w4_kernel (one wave per SIMD, AGPR accumulators); 15 its
+    // loop alone (timing only); 16 / 17 the same with reads and DMAs
+    // interleaved with the MFMAs
+    const int64_t tiles = ceil_div(batch, 256) * ceil_div(d, 256);
+    DR_REQUIRE(tiles < (1ll << 31), DR_INVALID_ARGUMENT, "batch too large");
+#define DR_W4(E, IL)                                                                        \
+  hipLaunchKernelGGL((crossnet_w4_kernel<E, 4, IL>), dim3((unsigned)tiles), dim3(256), 0,      \
+                     S(stream), x0, xl, W, bias, batch, d, d, out, lin_out)
+    if (variant == 14) DR_W4(1, false);
+    else if (variant == 15) DR_W4(0, false);
+    else if (variant == 16) DR_W4(1, true);
+    else DR_W4(0, true);
+#undef DR_W4
+    DR_LAUNCH_CHECK();
+    return DR_OK;
+  }
   if (d % 64 == 0 && !legacy && al16 && (variant >= 6 && variant <= 12)) {
     // variant 12 (A/B only): the 8-phase kernel covers the whole 256-column
     // tiles and the 128 x 128 glds kernel the d % 256 strip, instead of one
@@ -1979,9 +2291,20 @@ int dr_crossnet_dx_bf16(const uint16_t* u, const uint16_t* wt, const uint16_t* g
   const int64_t tiles = ceil_div(batch, 256) * ceil_div(d, 256);
   DR_REQUIRE(tiles < (1ll << 31), DR_INVALID_ARGUMENT, "batch too large");
   // the forward's 256^2 schedule with A = u, B = W^T and the addend g
-  hipLaunchKernelGGL((crossnet_8ph_kernel<2, 4, false>), dim3((unsigned)tiles), dim3(512), 0,
-                     S(stream), g, u, wt, (const float*)nullptr, batch, d, d, dx,
-                     (uint16_t*)nullptr);
+  static const int variant = getenv("DR_CROSSNET_VARIANT") ? atoi(getenv("DR_CROSSNET_VARIANT"))
+                                                           : 8;
+  if (variant == 14 || variant == 15)
+    hipLaunchKernelGGL((crossnet_w4_kernel<2, 4, false>), dim3((unsigned)tiles), dim3(256), 0,
+                       S(stream), g, u, wt, (const float*)nullptr, batch, d, d, dx,
+                       (uint16_t*)nullptr);
+  else if (variant >= 16 && variant <= 17)
+    hipLaunchKernelGGL((crossnet_w4_kernel<2, 4, true>), dim3((unsigned)tiles), dim3(256), 0,
+                       S(stream), g, u, wt, (const float*)nullptr, batch, d, d, dx,
+                       (uint16_t*)nullptr);
+  else
+    hipLaunchKernelGGL((crossnet_8ph_kernel<2, 4, false>), dim3((unsigned)tiles), dim3(512), 0,
+                       S(stream), g, u, wt, (const float*)nullptr, batch, d, d, dx,
+                       (uint16_t*)nullptr);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

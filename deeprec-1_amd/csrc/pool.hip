@@ -1293,7 +1293,8 @@ __global__ __launch_bounds__(256) void grad_finish_kernel(const uint64_t* __rest
 // positions: all 256 threads load the terms' row slices (the next stage's
 // rows in flight while this one is summed), scale them exactly as
 // grad_seg_kernel does (mean / sqrtn bag scale, weights) and write them to
-// LDS; wave 0 walks each column's chain (one lane per column).
+// LDS transposed ([column][position]); wave 0 walks each column's chain (one
+// lane per column, chain_walk).
 template <int VEC, int SW, bool W>
 __global__ __launch_bounds__(256) void grad_long_kernel(GradGroup g, int T, int64_t B,
                                                         const uint64_t* __restrict__ skey,
@@ -1307,8 +1308,9 @@ __global__ __launch_bounds__(256) void grad_long_kernel(GradGroup g, int T, int6
   constexpr int PI = 256 / SV;             // positions per load instruction
   constexpr int R = VEC == 4 ? 16 : 32;    // loads in flight per thread
   constexpr int S = PI * R;                // positions per stage
-  static_assert(SV >= 1 && 256 % SV == 0, "slice shape");
-  __shared__ __attribute__((aligned(16))) float stage[S * SW];
+  constexpr int SP = S + 4;                // column stride of the transposed stage
+  static_assert(SV >= 1 && 256 % SV == 0 && S % 4 == 0, "slice shape");
+  __shared__ __attribute__((aligned(16))) float stage[SW * SP];
   __shared__ int smin;
   const int64_t N = g.koff[T];
   const int nsl = (dim + SW - 1) / SW;
@@ -1317,6 +1319,7 @@ __global__ __launch_bounds__(256) void grad_long_kernel(GradGroup g, int T, int6
   const int pv = tid / SV, cv = tid % SV;
   const int lane = tid & 63;
   const int lc = lane < SW ? lane : 0;
+  const bool walker = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;
   for (int64_t wi = blockIdx.x; wi < total; wi += gridDim.x) {   // block-uniform
     const int i = (int)(wi / nsl), slice = (int)(wi % nsl);
     const int64_t u = __builtin_amdgcn_readfirstlane(longs[2 * i]);
@@ -1405,39 +1408,26 @@ __global__ __launch_bounds__(256) void grad_long_kernel(GradGroup g, int T, int6
           if (cnt != 1)
             x = vmul(x, mode == 2 ? (float)(1.0 / sqrt((double)cnt)) : (float)(1.0 / (double)cnt));
         }
-        *reinterpret_cast<V*>(stage + (r * PI + pv) * SW + cv * VEC) = x;
+        // transposed, [column][position]: the walker's column is contiguous
+        float* c = stage + (cv * VEC) * SP + r * PI + pv;
+        if constexpr (VEC == 4) {
+          c[0] = x.x;
+          c[SP] = x.y;
+          c[2 * SP] = x.z;
+          c[3 * SP] = x.w;
+        } else if constexpr (VEC == 2) {
+          c[0] = x.x;
+          c[SP] = x.y;
+        } else {
+          c[0] = x;
+        }
       }
       __syncthreads();
       load_rows();              // the next stage's rows: in flight while wave 0 sums this one
       load_idx(b0 + 2 * S);
-      if (tid < 64) {           // wave-uniform
+      if (walker) {             // wave 0 (an SGPR test: a scalar-controlled walk)
         const int nv = (int)(pe - b0 < S ? pe - b0 : S);
-        const float* sp = stage + lc;
-        int jj = 0;
-        if (fresh) {
-          acc = sp[0];
-          fresh = false;
-          jj = 1;
-        }
-        // the LDS reads of the next 8 positions are issued before the adds
-        // of these 8: the chain waits on the adds, not on LDS latency
-        if (jj + 8 <= nv) {
-          float xa[8], xb[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) xa[q] = sp[(jj + q) * SW];
-          for (; jj + 16 <= nv; jj += 8) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) xb[q] = sp[(jj + 8 + q) * SW];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) acc = acc + xa[q];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) xa[q] = xb[q];
-          }
-#pragma unroll
-          for (int q = 0; q < 8; ++q) acc = acc + xa[q];
-          jj += 8;
-        }
-        for (; jj < nv; ++jj) acc = acc + sp[jj * SW];
+        acc = chain_walk(stage + lc * SP, nv, fresh, acc);
       }
       __syncthreads();   // the stage is rewritten next
     }

@@ -497,7 +497,11 @@ __global__ __launch_bounds__(256) void din_mlp_bwd_kernel(
 }
 
 // per sample b: s1[b] = sum of da1 over its positions, dq2[b] = sum of the
-// q-side terms f * d(q f) (ascending position order); one wave per sample
+// q-side terms f * d(q f); one wave per sample, lanes over its positions (a
+// coalesced 256-B load per unit and 64 positions), each lane's partial over
+// the position chunks then a fixed xor-shuffle tree (deterministic).  (The
+// per-lane-unit form -- 64 units' rows per load instruction, 64 lines each --
+// took 173 us at configs[3].)
 template <int H, int N1>
 __global__ void din_mlp_sample_kernel(const int32_t* __restrict__ off, int64_t B, int64_t cap,
                                       const float* __restrict__ da1t,
@@ -505,16 +509,20 @@ __global__ void din_mlp_sample_kernel(const int32_t* __restrict__ off, int64_t B
                                       float* __restrict__ dq2) {
   const int64_t b = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
   const int lane = threadIdx.x & 63;
-  if (b >= B) return;
+  if (b >= B) return;   // wave-uniform
   const int64_t p0 = off[b], p1 = off[b + 1];
-  for (int j = lane; j < N1 + H; j += 64) {
+  for (int j = 0; j < N1 + H; ++j) {
     const float* src = j < N1 ? da1t + (int64_t)j * cap : dqp + (int64_t)(j - N1) * cap;
     float acc = 0.f;
-    for (int64_t p = p0; p < p1; ++p) acc += src[p];
-    if (j < N1)
-      s1[b * N1 + j] = acc;
-    else
-      dq2[b * H + (j - N1)] = acc;
+    for (int64_t p = p0 + lane; p < p1; p += 64) acc += src[p];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane == 0) {
+      if (j < N1)
+        s1[b * N1 + j] = acc;
+      else
+        dq2[b * H + (j - N1)] = acc;
+    }
   }
 }
 
