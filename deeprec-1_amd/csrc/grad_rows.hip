@@ -79,25 +79,26 @@ static constexpr int64_t kRowsMaxDim = 1024;
 // visits only those -- e.g. a padding id whose positions are masked out
 // downstream.  A run that is mostly nonzero (DIN's padding id: its history
 // positions feed the unmasked his_sum, model.py:98, so they all carry
-// gradient) is walked whole instead (run_sparse()).  DR_GRAD_ZERO_SKIP=0
-// (A/B) walks every term.
+// gradient) is walked whole instead (run_sparse()).  Opt-in:
+// DR_GRAD_ZERO_SKIP=1 (zero_scan()).
 // Plain-sum runs (no weights, no mean / sqrtn scale, not walked compacted)
-// go to rows_serial_dma_kernel; DR_GRAD_SERIAL_DMA=0 (A/B) keeps them in
-// rows_serial_kernel.
+// go to rows_serial_plain_kernel (1, default) or rows_serial_dma_kernel (2,
+// A/B); DR_GRAD_SERIAL_PLAIN=0 keeps them in rows_serial_kernel.
 static int serial_dma() {
   static const int v = [] {
-    const char* e = getenv("DR_GRAD_SERIAL_DMA");
-    return (e && atoi(e) == 0) ? 0 : 1;
+    const char* e = getenv("DR_GRAD_SERIAL_PLAIN");
+    return e ? atoi(e) : 1;
   }();
   return v;
 }
 
 static int64_t zero_scan() {
-  static const int64_t v = [] {
-    const char* e = getenv("DR_GRAD_ZERO_SKIP");
-    return (e && atoi(e) == 0) ? (int64_t)0 : (int64_t)2048;
-  }();
-  return v;
+  // read per call (host only, once per backward): tests switch it on around
+  // one call.  Off by default: none of the measured workloads has exact-zero
+  // terms (DIN's padding positions carry his_sum's gradient), where the scan
+  // only adds a pass over every long run's terms (127 us at configs[3])
+  const char* e = getenv("DR_GRAD_ZERO_SKIP");
+  return (e && atoi(e) != 0) ? (int64_t)2048 : (int64_t)0;
 }
 
 // Long-run state (the workspace arrays of RowsWs, passed as one argument).
@@ -127,7 +128,7 @@ struct RowsLong {
   int32_t* kpos;           // [N] chunk k of run c0: nonzero positions at c0 + k*kRowsChunk ..
   int32_t* rnz;            // per long run: its nonzero terms (zero scan)
   float* zrow;             // 64 zeros (rows_expand_kernel): the term of an invalid bag
-  int dma;                 // rows_serial_dma_kernel takes the plain-sum runs (serial_dma())
+  int dma;                 // who takes the plain-sum runs (serial_dma()): 1 plain, 2 dma
 };
 
 // A zero-scanned run is walked compacted only when at most half its terms
@@ -973,7 +974,7 @@ __global__ __launch_bounds__(1024) void rows_serial_kernel(RowsGroup g, int T, i
     // chunk in ascending order; a zero-started chain is unchanged by the
     // skipped +-0.0 terms (zero_scan()).  Otherwise entry e = position ps + e.
     const bool zc = run_sparse(L, i, np, len);
-    if (L.dma && !wt && !ms && !zc) continue;   // rows_serial_dma_kernel's run
+    if (L.dma && !wt && !ms && !zc) continue;   // the plain / dma kernel's run
     const int cf = zc ? __builtin_amdgcn_readfirstlane(L.cfirst[i]) : -1;
     const int64_t nch = zc ? (len + kRowsChunk - 1) / kRowsChunk : 1;
     float acc = 0.f;
@@ -1124,6 +1125,143 @@ __global__ __launch_bounds__(1024) void rows_serial_kernel(RowsGroup g, int T, i
         const int64_t o = SGD ? 0 : sk[t] + (int64_t)L.ex[pc] - L.base[t];
         if (lane < SW && (lane & 1) == 0 && col < dim)
           rows_fin_pair<SGD, WB>(sg, t, u, o, dim, col, acc, nxt, L.gu);
+        if (slice == 0 && lane == 0) rows_fin_run<SGD>(sg, t, u, o, dim, L);
+      } else if (lane < SW && col < dim) {
+        L.part[(int64_t)j * dim + col] = acc;
+      }
+    }
+  }
+}
+
+// The plain-sum runs (rows_serial_kernel's terms with no scale: the sum
+// combiner, unweighted, not walked compacted), one block per (piece, slice of
+// 16 columns): rows_serial_kernel's double-buffered walk without the scaling,
+// compaction and window machinery, whose registers capped it at 6 loads in
+// flight per thread -- here 8 (float2 / float) or 4 (float4) with a 16-column
+// slice, so a stage is 960 positions (2.7 x the general kernel's 360 at DIN's
+// dim 18): the loads of a stage have the walk of a whole stage to land.
+template <int VEC, bool SGD, bool WB>
+__global__ __launch_bounds__(1024) void rows_serial_plain_kernel(RowsGroup g, int T, int dim,
+                                                                 RowsLong L, RowsSgd sg) {
+  using V = typename VecT<VEC>::T;
+  constexpr int SW = 16;                   // columns per slice
+  constexpr int NL = 960;                  // loader threads (waves 1..15)
+  constexpr int SV = SW / VEC;             // vectors of a position's slice
+  constexpr int PI = NL / SV;              // positions per load instruction
+  constexpr int R = VEC == 4 ? 4 : 8;      // loads in flight per thread
+  constexpr int S = PI * R;                // positions per stage (480 / 960)
+  constexpr int SP = S + 4;                // column stride of the transposed stage
+  static_assert(NL % SV == 0 && S % 4 == 0, "slice shape");
+  __shared__ __attribute__((aligned(16))) float stage[2 * SW * SP];
+  __shared__ int64_t sk[DR_MAX_GROUP + 1];
+  if (threadIdx.x <= T) sk[threadIdx.x] = g.koff[threadIdx.x];
+  __syncthreads();
+  const int nsl = (dim + SW - 1) / SW;
+  const int64_t total = (int64_t)(*L.nitems) * nsl;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const bool walker = wave == 0;           // wave-uniform (an SGPR: scalar-controlled walk)
+  const int lt = walker ? 0 : tid - 64;
+  const int pv = lt / SV, cv = lt % SV;
+  const int lc = lane < SW ? lane : 0;
+  if (walker) __builtin_amdgcn_s_setprio(3);   // the chain is the critical path
+  for (int64_t wi = blockIdx.x; wi < total; wi += gridDim.x) {   // block-uniform
+    const int j = (int)(wi / nsl), slice = (int)(wi % nsl);
+    const int i = __builtin_amdgcn_readfirstlane(L.items[2 * j]);
+    const int k = __builtin_amdgcn_readfirstlane(L.items[2 * j + 1]);
+    const int64_t c0 = __builtin_amdgcn_readfirstlane(L.longs[i]);
+    const int64_t len = __builtin_amdgcn_readfirstlane(L.rlen[i]);
+    const int64_t smax = L.smax;
+    const int np = (int)((len + smax - 1) / smax);
+    const int64_t ps = c0 + (int64_t)k * smax;
+    const int64_t pe = c0 + len < ps + smax ? c0 + len : ps + smax;
+    const int32_t pc = __builtin_amdgcn_readfirstlane(L.perm[c0]);
+    const uint32_t u = (uint32_t)__builtin_amdgcn_readfirstlane((int)L.skey[c0]);
+    const int t = __builtin_amdgcn_readfirstlane(tab_of(sk, T, pc));
+    const dr_pool_grad_desc& d = g.d[t];
+    const bool wt = d.weights != nullptr;
+    const bool ms = !wt && d.combiner != DR_COMBINER_SUM;
+    if (wt || ms || run_sparse(L, i, np, len)) continue;   // rows_serial_kernel's run
+    const int64_t K = pe - ps;
+    const int colv = slice * SV + cv;
+    const float* src = d.top_grad + (colv * VEC < dim ? colv * VEC : 0);
+    const int64_t ts = d.top_stride;
+    const int32_t* srow = L.srow + ps;
+    int32_t rq[R];
+    auto load_idx = [&](int64_t b0) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        int64_t e = b0 + r * PI + pv;
+        e = e < K ? e : K - 1;
+        rq[r] = srow[e];
+      }
+    };
+    V y[R];
+    auto load_rows = [&]() {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int64_t rr = rq[r] >= 0 ? rq[r] : 0;
+        y[r] = gld(reinterpret_cast<const V*>(src + rr * ts));
+      }
+    };
+    uint32_t zmask = 0;
+    auto take = [&]() {
+      zmask = 0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) zmask |= (rq[r] < 0 ? 1u : 0u) << r;
+    };
+    auto fill = [&](float* stg) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        V x = y[r];
+        if ((zmask >> r) & 1u) x = vzero<V>();
+        float* c = stg + (cv * VEC) * SP + r * PI + pv;
+        if constexpr (VEC == 4) {
+          c[0] = x.x;
+          c[SP] = x.y;
+          c[2 * SP] = x.z;
+          c[3 * SP] = x.w;
+        } else if constexpr (VEC == 2) {
+          c[0] = x.x;
+          c[SP] = x.y;
+        } else {
+          c[0] = x;
+        }
+      }
+    };
+    if (!walker) {   // stage 0 into buffer 0; stage 1's rows in flight
+      load_idx(0);
+      take();
+      load_rows();
+      load_idx(S);
+      fill(stage);
+      take();
+      load_rows();
+      load_idx(2 * S);
+    }
+    __syncthreads();
+    float acc = 0.f;
+    bool fresh = !(k == 0);   // first term: 0 + y (the sum combiner is zero-started) or y
+    int sb = 0;
+    for (int64_t b0 = 0; b0 < K; b0 += S, sb ^= 1) {
+      if (walker) {
+        const int nv = (int)(K - b0 < S ? K - b0 : S);
+        acc = chain_walk(stage + sb * (SW * SP) + lc * SP, nv, fresh, acc);
+      } else if (b0 + S < K) {
+        fill(stage + (sb ^ 1) * (SW * SP));
+        take();
+        load_rows();
+        load_idx(b0 + 3 * S);
+      }
+      __syncthreads();
+    }
+    if (walker) {
+      const int col = slice * SW + lane;
+      const float nx = __shfl_down(acc, 1, 64);
+      if (np == 1) {
+        const int64_t o = SGD ? 0 : sk[t] + (int64_t)L.ex[pc] - L.base[t];
+        if (lane < SW && (lane & 1) == 0 && col < dim)
+          rows_fin_pair<SGD, WB>(sg, t, u, o, dim, col, acc, nx, L.gu);
         if (slice == 0 && lane == 0) rows_fin_run<SGD>(sg, t, u, o, dim, L);
       } else if (lane < SW && col < dim) {
         L.part[(int64_t)j * dim + col] = acc;
@@ -1444,8 +1582,18 @@ static void launch_long(const RowsGroup& g, int T, int dim, const RowsLong& L, c
     const int64_t nsl16 = ceil_div(dim, 16);
     int64_t db = runs * nsl16;
     if (db > 1024) db = 1024;
-    hipLaunchKernelGGL((rows_serial_dma_kernel<SGD, WB>), dim3((unsigned)db), dim3(1024), 0, s, g,
-                       T, dim, L, sg);
+    if (L.dma == 2)
+      hipLaunchKernelGGL((rows_serial_dma_kernel<SGD, WB>), dim3((unsigned)db), dim3(1024), 0, s,
+                         g, T, dim, L, sg);
+    else if (VEC == 4)
+      hipLaunchKernelGGL((rows_serial_plain_kernel<VEC, SGD, WB>), dim3((unsigned)db), dim3(1024),
+                         0, s, g, T, dim, L, sg);
+    else if (aligned2 && dim % 2 == 0)
+      hipLaunchKernelGGL((rows_serial_plain_kernel<2, SGD, WB>), dim3((unsigned)db), dim3(1024), 0,
+                         s, g, T, dim, L, sg);
+    else
+      hipLaunchKernelGGL((rows_serial_plain_kernel<1, SGD, WB>), dim3((unsigned)db), dim3(1024), 0,
+                         s, g, T, dim, L, sg);
   }
   if (N > L.smax) {
     const int64_t big = N / (L.smax + 1) + 1;

@@ -409,16 +409,26 @@ __global__ __launch_bounds__(256) void din_mlp_fwd_kernel(
 #pragma unroll
   for (int m = 0; m < N2; ++m) a2[m] = 0.f;
   const float* cqb = cq + b * N1;
-  for (int j = 0; j < N1; ++j) {
-    float acc = cqb[j];
-    const float* wr = w1p + j * 2 * H;
+  // two hidden units per pass: two independent 72-term chains interleave
+  static_assert(N1 % 2 == 0, "unit pairs");
+  for (int j = 0; j < N1; j += 2) {
+    float acc0 = cqb[j], acc1 = cqb[j + 1];
+    const float* wr0 = w1p + j * 2 * H;
+    const float* wr1 = wr0 + 2 * H;
 #pragma unroll
-    for (int k = 0; k < 2 * H; ++k) acc = fmaf(wr[k], x[k], acc);
-    const float h = sigm(acc);
-    if (p < P) h1t[(int64_t)j * cap + p] = h;
-    const float* vr = w2t + j * N2;
+    for (int k = 0; k < 2 * H; ++k) {
+      acc0 = fmaf(wr0[k], x[k], acc0);
+      acc1 = fmaf(wr1[k], x[k], acc1);
+    }
+    const float h0 = sigm(acc0), h1 = sigm(acc1);
+    if (p < P) {
+      h1t[(int64_t)j * cap + p] = h0;
+      h1t[(int64_t)(j + 1) * cap + p] = h1;
+    }
+    const float* vr0 = w2t + j * N2;
+    const float* vr1 = vr0 + N2;
 #pragma unroll
-    for (int m = 0; m < N2; ++m) a2[m] = fmaf(vr[m], h, a2[m]);
+    for (int m = 0; m < N2; ++m) a2[m] = fmaf(vr1[m], h1, fmaf(vr0[m], h0, a2[m]));
   }
   float s = b3[0];
 #pragma unroll
@@ -471,17 +481,35 @@ __global__ __launch_bounds__(256) void din_mlp_bwd_kernel(
   float dx[2 * H];
 #pragma unroll
   for (int k = 0; k < 2 * H; ++k) dx[k] = 0.f;
-  for (int j = 0; j < N1; ++j) {
-    const float* vr = w2t + j * N2;
-    float dh = 0.f;
+  // the h1 activations four units ahead of their use: a load per unit inside
+  // the loop was waited for right away, ~80 exposed global-load latencies
+  // per position (the kernel took 280-300 us at configs[3])
+  static_assert(N1 % 4 == 0, "unit groups of 4");
+  float hn[4];
 #pragma unroll
-    for (int m = 0; m < N2; ++m) dh = fmaf(vr[m], da2[m], dh);
-    const float h = h1t[(int64_t)j * cap + p];
-    const float da = dh * (1.f - h) * h;
-    da1t[(int64_t)j * cap + p] = da;
-    const float* wr = w1p + j * 2 * H;
+  for (int q = 0; q < 4; ++q) hn[q] = h1t[(int64_t)q * cap + p];
+  for (int j0 = 0; j0 < N1; j0 += 4) {
+    float hc[4];
 #pragma unroll
-    for (int k = 0; k < 2 * H; ++k) dx[k] = fmaf(wr[k], da, dx[k]);
+    for (int q = 0; q < 4; ++q) {
+      hc[q] = hn[q];
+      const int jn = j0 + 4 + q < N1 ? j0 + 4 + q : N1 - 1;
+      hn[q] = h1t[(int64_t)jn * cap + p];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = j0 + q;
+      const float* vr = w2t + j * N2;
+      float dh = 0.f;
+#pragma unroll
+      for (int m = 0; m < N2; ++m) dh = fmaf(vr[m], da2[m], dh);
+      const float h = hc[q];
+      const float da = dh * (1.f - h) * h;
+      da1t[(int64_t)j * cap + p] = da;
+      const float* wr = w1p + j * 2 * H;
+#pragma unroll
+      for (int k = 0; k < 2 * H; ++k) dx[k] = fmaf(wr[k], da, dx[k]);
+    }
   }
   const float* fr = facts + bt * H;
   const float* qr = q + b * H;
@@ -511,17 +539,33 @@ __global__ void din_mlp_sample_kernel(const int32_t* __restrict__ off, int64_t B
   const int lane = threadIdx.x & 63;
   if (b >= B) return;   // wave-uniform
   const int64_t p0 = off[b], p1 = off[b + 1];
-  for (int j = 0; j < N1 + H; ++j) {
-    const float* src = j < N1 ? da1t + (int64_t)j * cap : dqp + (int64_t)(j - N1) * cap;
-    float acc = 0.f;
-    for (int64_t p = p0 + lane; p < p1; p += 64) acc += src[p];
+  constexpr int NU = N1 + H;
+  for (int jb = 0; jb < NU; jb += 8) {   // 8 units' loads in flight together
+    float acc[8];
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if (lane == 0) {
+    for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+    for (int64_t p = p0 + lane; p < p1; p += 64) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int j = jb + q < NU ? jb + q : NU - 1;
+        const float* src = j < N1 ? da1t + (int64_t)j * cap : dqp + (int64_t)(j - N1) * cap;
+        acc[q] += src[p];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) acc[q] += __shfl_xor(acc[q], o, 64);
+    }
+    if (lane < 8 && jb + lane < NU) {
+      float v = acc[0];
+#pragma unroll
+      for (int q = 1; q < 8; ++q) v = lane == q ? acc[q] : v;
+      const int j = jb + lane;
       if (j < N1)
-        s1[b * N1 + j] = acc;
+        s1[b * N1 + j] = v;
       else
-        dq2[b * H + (j - N1)] = acc;
+        dq2[b * H + (j - N1)] = v;
     }
   }
 }

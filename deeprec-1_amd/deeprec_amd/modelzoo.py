@@ -738,20 +738,25 @@ def _cross_dx(u, wb, g):
     return ops.crossnet_dx(u, wb.t().contiguous(), g)
 
 
-# A/B switch: DR_CROSSNET_DW_LIB=1 = the library GEMM for the cross layers'
-# weight gradient
-_CROSS_DW_LIB = os.environ.get("DR_CROSSNET_DW_LIB", "0") == "1"
+# The cross layers' weight gradient: the library GEMM writing fp32 (default;
+# 1.43-1.63 ms at B = 65 536, d = 3 392) or, DR_CROSSNET_DW=hand, the hand TN
+# MFMA kernel (dr_crossnet_dw_bf16: 2.16 ms there, profiles/r05_cross_dw.log)
+_CROSS_DW_HAND = os.environ.get("DR_CROSSNET_DW", "lib") == "hand"
 
 
 def _cross_dw(u, x):
-    """dW = u^T x of a cross layer: the hand TN MFMA kernel (dr_crossnet_dw_bf16,
-    fp32 accumulation and output), or the library GEMM (bf16 result widened)
-    where the shape does not fit it."""
-    if not _CROSS_DW_LIB:
+    """dW = u^T x of a cross layer in fp32 (fp32 accumulation, no bf16
+    rounding of the result): torch.mm with out_dtype=float32 (hipBLASLt), the
+    bf16 product widened where that overload is absent, or the hand kernel
+    (A/B)."""
+    if _CROSS_DW_HAND:
         dw = ops.crossnet_dw(u, x)
         if dw is not None:
             return dw
-    return torch.matmul(u.t(), x).float()
+    try:
+        return torch.mm(u.t(), x, out_dtype=torch.float32)
+    except (TypeError, RuntimeError):
+        return torch.matmul(u.t(), x).float()
 
 
 class CrossLayer(torch.autograd.Function):

@@ -176,11 +176,21 @@ def test_rows_backward_long_runs(dr, orc, D):
 
 @pytest.mark.parametrize("D", [18, 32])
 def test_rows_backward_long_runs_zero_terms(dr, orc, D):
-    """Long runs whose terms are mostly exact zeros (a DIN padding id: the
-    masked positions' gradients are +-0.0): the serial walk skips the zero
+    """Long runs whose terms are mostly exact zeros (a padding id whose
+    positions are masked out downstream: their gradients are +-0.0): with the
+    zero scan on (DR_GRAD_ZERO_SKIP=1, opt-in) the serial walk skips the zero
     terms of a zero-started chain (rows_nz_kernel) -- bit-equal to the full
     serial sum, signs included: a run of only zero terms (+0.0 and -0.0) is
     +0.0, as 0 + (-0) + ... is in the reference's loop."""
+    import os
+    os.environ["DR_GRAD_ZERO_SKIP"] = "1"
+    try:
+        _zero_terms_case(dr, orc, D)
+    finally:
+        del os.environ["DR_GRAD_ZERO_SKIP"]
+
+
+def _zero_terms_case(dr, orc, D):
     rng = np.random.default_rng(45)
     runs = {0: 30000, 1: 9000, 2: 40000, 3: 5000}
     v = np.concatenate([np.full(n, k, np.int64) for k, n in runs.items()] +

@@ -44,6 +44,14 @@ def main():
              err), flush=True)
     t = timed(lambda: torch.matmul(u.t(), x).float())
     print("matmul(u.t(), x).float() again: %.3f ms" % t, flush=True)
+    try:   # the library GEMM writing fp32 directly (aten::mm.dtype)
+        got = torch.mm(u.t(), x, out_dtype=torch.float32)
+        err = ((got - ref).abs().max() / ref.abs().max()).item()
+        t = timed(lambda: torch.mm(u.t(), x, out_dtype=torch.float32))
+        print("mm(u.t(), x, out_dtype=fp32): %.3f ms  %.0f TF/s  max rel diff %.2e"
+              % (t, flop / t / 1e9, err), flush=True)
+    except Exception as e:  # not in this torch build
+        print("mm out_dtype unavailable: %s" % str(e)[:120], flush=True)
     tiles = ((d + 127) // 128) ** 2
     for s in sorted({1, 2, 4, _dw_split(tiles, B)}):
         got = ops.gemm_tn(u, x, split_k=s)

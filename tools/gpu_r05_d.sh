@@ -9,7 +9,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_rows_grad.py tests/test_gpu
   tests/test_gpu_parity.py tests/test_gpu_din.py tests/test_gpu_rows_sgd_fused.py tests/test_gpu_configs.py tests/test_gpu_sharded_c.py -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/$T/tests.log 2>&1
 rc=$?; tail -2 gpurun_out/$T/tests.log; grep -E "^FAILED|^ERROR" gpurun_out/$T/tests.log | head -20
 [ $rc -ne 0 ] && exit $rc
-for e in "X=1" "DR_GRAD_SERIAL_DMA=0" "DR_GRAD_SERIAL_MAX=8192" "X=1"; do
+for e in "X=1" "DR_GRAD_SERIAL_PLAIN=0" "DR_GRAD_SERIAL_PLAIN=2" "DR_GRAD_SERIAL_MAX=8192" "X=1"; do
   env $e timeout -k 10 300 python -u tools/model_step.py --model din --steps 10 > gpurun_out/$T/din.log 2>&1 || { tail -5 gpurun_out/$T/din.log; exit 1; }
   echo "din $e: $(tail -1 gpurun_out/$T/din.log | cut -c1-120)"
 done

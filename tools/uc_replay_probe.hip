@@ -16,7 +16,10 @@
 //     acquire.  The r04 library run showed 4 of 92 pools with stale words
 //     (per-XCD views disagreeing).
 //   hipcc -O3 --offload-arch=gfx950 tools/uc_replay_probe.hip -o tools/uc_replay_probe
-//   tools/uc_replay_probe [rounds] [control]   (control: coarse hipMalloc for the IPC buffers)
+//   tools/uc_replay_probe [rounds] [control] [ipc]   (control: coarse hipMalloc for the IPC
+//   buffers; ipc: export every buffer with hipIpcGetMemHandle, open it again in this same
+//   process -- as the ranks-as-threads engines of test_gpu_sharded.py do for their peers --
+//   write through that second mapping, close it before hipFree)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -79,6 +82,7 @@ __global__ void view_k(const uint32_t* p, int64_t n, uint32_t expect, uint32_t* 
 int main(int argc, char** argv) {
   const int rounds = argc > 1 ? atoi(argv[1]) : 3;
   const int control = argc > 2 ? atoi(argv[2]) : 0;
+  const int ipc = argc > 3 ? atoi(argv[3]) : 0;
   const size_t nfree = sizeof(kFree) / sizeof(kFree[0]);
   uint32_t* res;
   CK(hipMalloc(&res, 64 * 3 * sizeof(uint32_t)));
@@ -88,6 +92,7 @@ int main(int argc, char** argv) {
     // groups of 5 (one engine's IPC buffers): alloc, zero, use, then free
     for (size_t g = 0; g + 5 <= nfree; g += 5) {
       void* u[5];
+      void* m[5];   // the buffer written by the engine: u, or its IPC mapping
       for (int k = 0; k < 5; ++k) {
         if (control)
           CK(hipMalloc(&u[k], kFree[g + k]));
@@ -96,6 +101,12 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(fill_k, dim3(64), dim3(256), 0, 0, (uint32_t*)u[k],
                            (int64_t)(kFree[g + k] / 4), 0u);
         CK(hipStreamSynchronize(nullptr));
+        m[k] = u[k];
+        if (ipc) {
+          hipIpcMemHandle_t h;
+          CK(hipIpcGetMemHandle(&h, u[k]));
+          CK(hipIpcOpenMemHandle(&m[k], h, hipIpcMemLazyEnablePeerAccess));
+        }
       }
       // the engine's cached neighbours: EV pools / torch segments
       void* c = nullptr;
@@ -104,10 +115,13 @@ int main(int argc, char** argv) {
       for (int k = 0; k < 5; ++k) {
         const int64_t n = (int64_t)(kFree[g + k] / 4);
         hipLaunchKernelGGL(scatter_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0,
-                           (uint32_t*)u[k], n, 0x1234u + (uint32_t)k);
+                           (uint32_t*)m[k], n, 0x1234u + (uint32_t)k);
       }
       CK(hipDeviceSynchronize());
-      for (int k = 0; k < 5; ++k) CK(hipFree(u[k]));
+      for (int k = 0; k < 5; ++k) {
+        if (ipc) CK(hipIpcCloseMemHandle(m[k]));
+        CK(hipFree(u[k]));
+      }
     }
     // the EV pools of the next test: poison, sync, three views
     for (int pidx = 0; pidx < 92; ++pidx) {
@@ -143,8 +157,8 @@ int main(int argc, char** argv) {
     printf("round %d done: %d / %d pools stale so far\n", r, bad_pools, pools);
     fflush(stdout);
   }
-  printf("{\"probe\":\"uc_replay\",\"control\":%d,\"rounds\":%d,\"pools\":%d,\"stale_pools\":%d}\n",
-         control, rounds, pools, bad_pools);
+  printf("{\"probe\":\"uc_replay\",\"control\":%d,\"ipc\":%d,\"rounds\":%d,\"pools\":%d,"
+         "\"stale_pools\":%d}\n", control, ipc, rounds, pools, bad_pools);
   CK(hipFree(res));
   return 0;
 }
