@@ -551,6 +551,16 @@ def din_leg(args, dev, log, world, rank, dist, staged):
     return res
 
 
+def lookup_kernel_label(G):
+    """The fused one-hot lookup the library launches for G lanes per row
+    (DR_LOOKUP_KERNEL, ev.hip lookup_kernel_kind(); default 1 = line probes)."""
+    kind = os.environ.get("DR_LOOKUP_KERNEL", "1")
+    if kind == "0":
+        return "dr::ev_lookup_onehot_kernel<4,%d,1,ALI,%d>" % (G, 2 if G <= 16 else 4)
+    name = "ev_lookup_line_kernel" if kind == "1" else "ev_lookup_pipe_kernel"
+    return "dr::%s<4,%d,1,ALI>" % (name, G)
+
+
 def dcn_bf16_leg(args, dev, log):
     """BASELINE configs[4] per-GPU embedding shape with bf16 tables: 26 bf16
     EVs x 12.5 M rows x 128, B = 65 536, the fused one-hot lookup writing
@@ -631,8 +641,7 @@ def dcn_bf16_leg(args, dev, log):
            "checked_rows": 2048,
            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
                         "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
-                        "kernel": "dr::ev_lookup_onehot_kernel<4,16,1,ALI,2> on bf16 rows "
-                                  "(64 float words)",
+                        "kernel": lookup_kernel_label(16) + " on bf16 rows (64 float words)",
                         "kernel_ms": round(k_ms, 4), "bytes_per_lookup": per,
                         "bytes_per_launch": T * B * per},
            "train_step": {"ms_per_step": round(tms, 4),
@@ -720,7 +729,7 @@ def deepfm_leg(args, dev, log):
            "samples_per_s": round(B / (k_ms * 1e-3), 1),
            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
                         "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
-                        "kernel": "dr::ev_lookup_onehot_kernel<4,16,1,ALI,2>",
+                        "kernel": lookup_kernel_label(16),
                         "kernel_ms": round(k_ms, 4), "bytes_per_lookup": per,
                         "bytes_per_launch": T * B * per},
            "train_step": {"ms_per_step": round(tms, 4),
