@@ -382,6 +382,24 @@ __global__ void din_mlp_pos_kernel(const float* __restrict__ mask, int64_t B, in
   }
 }
 
+// The attention MLP's weights (W1p [N1][2H] then W2^T [N1][N2], 36 KB at H =
+// 36) staged in LDS once per block: every lane reads the same word, so the
+// reads broadcast.  Read through scalar loads instead, the 35 KB stream
+// overflowed the scalar cache and every unit pair waited on an L2 round
+// trip (SQ_WAIT_ANY 62 % of the forward's wave cycles, profiles/r05_din_pmc.json).
+template <int H, int N1, int N2>
+__device__ __forceinline__ void din_stage_weights(float* sw, const float* __restrict__ w1p,
+                                                  const float* __restrict__ w2t) {
+  constexpr int A = N1 * 2 * H, Bn = N1 * N2;
+  for (int i = threadIdx.x; i < (A + Bn) / 4; i += blockDim.x) {
+    const int e = 4 * i;
+    const float4 v = e < A ? *reinterpret_cast<const float4*>(w1p + e)
+                           : *reinterpret_cast<const float4*>(w2t + (e - A));
+    *reinterpret_cast<float4*>(sw + e) = v;
+  }
+  __syncthreads();
+}
+
 // forward: one lane per valid position p < P (= off[B]); lanes past P exit
 template <int H, int N1, int N2>
 __global__ __launch_bounds__(256) void din_mlp_fwd_kernel(
@@ -393,6 +411,9 @@ __global__ __launch_bounds__(256) void din_mlp_fwd_kernel(
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t P = off[B];
   if ((int64_t)blockIdx.x * blockDim.x >= P) return;   // whole blocks past the count
+  static_assert((N1 * 2 * H) % 4 == 0 && N2 % 4 == 0, "16-B weight rows");
+  __shared__ __attribute__((aligned(16))) float sw[N1 * 2 * H + N1 * N2];
+  din_stage_weights<H, N1, N2>(sw, w1p, w2t);
   const int64_t pc = p < P ? p : P - 1;                 // (clamped: loads stay valid)
   const int64_t bt = pos[pc];
   const int64_t b = bt / T;
@@ -413,7 +434,7 @@ __global__ __launch_bounds__(256) void din_mlp_fwd_kernel(
   static_assert(N1 % 2 == 0, "unit pairs");
   for (int j = 0; j < N1; j += 2) {
     float acc0 = cqb[j], acc1 = cqb[j + 1];
-    const float* wr0 = w1p + j * 2 * H;
+    const float* wr0 = sw + j * 2 * H;
     const float* wr1 = wr0 + 2 * H;
 #pragma unroll
     for (int k = 0; k < 2 * H; ++k) {
@@ -425,7 +446,7 @@ __global__ __launch_bounds__(256) void din_mlp_fwd_kernel(
       h1t[(int64_t)j * cap + p] = h0;
       h1t[(int64_t)(j + 1) * cap + p] = h1;
     }
-    const float* vr0 = w2t + j * N2;
+    const float* vr0 = sw + N1 * 2 * H + j * N2;
     const float* vr1 = vr0 + N2;
 #pragma unroll
     for (int m = 0; m < N2; ++m) a2[m] = fmaf(vr1[m], h1, fmaf(vr0[m], h0, a2[m]));
@@ -455,8 +476,11 @@ __global__ __launch_bounds__(256) void din_mlp_bwd_kernel(
     float* __restrict__ da2t, float* __restrict__ xt, float* __restrict__ dsc,
     float* __restrict__ dqp) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= cap) return;
   const int64_t P = off[B];
+  __shared__ __attribute__((aligned(16))) float sw[N1 * 2 * H + N1 * N2];
+  if ((int64_t)blockIdx.x * blockDim.x < P)   // block-uniform: the block has valid positions
+    din_stage_weights<H, N1, N2>(sw, w1p, w2t);
+  if (p >= cap) return;
   if (p >= P) {
 #pragma unroll 8
     for (int j = 0; j < N1; ++j) da1t[(int64_t)j * cap + p] = h1t[(int64_t)j * cap + p] = 0.f;
@@ -499,14 +523,14 @@ __global__ __launch_bounds__(256) void din_mlp_bwd_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int j = j0 + q;
-      const float* vr = w2t + j * N2;
+      const float* vr = sw + N1 * 2 * H + j * N2;
       float dh = 0.f;
 #pragma unroll
       for (int m = 0; m < N2; ++m) dh = fmaf(vr[m], da2[m], dh);
       const float h = hc[q];
       const float da = dh * (1.f - h) * h;
       da1t[(int64_t)j * cap + p] = da;
-      const float* wr = w1p + j * 2 * H;
+      const float* wr = sw + j * 2 * H;
 #pragma unroll
       for (int k = 0; k < 2 * H; ++k) dx[k] = fmaf(wr[k], da, dx[k]);
     }
