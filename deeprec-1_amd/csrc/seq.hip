@@ -320,6 +320,8 @@ __global__ void din_mlp_prep_kernel(const float* __restrict__ w1, const float* _
     const float* r = w1 + (int64_t)j * 4 * H;
     const float* qb = q + b * H;
     float acc = b1[j];
+    // the loads run ahead of the chain (a rolled loop waited for each pair)
+#pragma unroll 12
     for (int k = 0; k < H; ++k) acc = fmaf(r[k] + r[2 * H + k], qb[k], acc);
     cq[e] = acc;
   }
