@@ -434,8 +434,14 @@ __global__ __launch_bounds__(256) void din_mlp_fwd_kernel(
   const float* cqb = cq + b * N1;
   // two hidden units per pass: two independent 72-term chains interleave
   static_assert(N1 % 2 == 0, "unit pairs");
+  // the per-sample bias pair one iteration ahead (a load per pair waited
+  // for at once was most of the forward's SQ_WAIT_ANY, r05_din_pmc.json)
+  float cn0 = cqb[0], cn1 = cqb[1];
   for (int j = 0; j < N1; j += 2) {
-    float acc0 = cqb[j], acc1 = cqb[j + 1];
+    float acc0 = cn0, acc1 = cn1;
+    const int jn = j + 2 < N1 ? j + 2 : N1 - 2;
+    cn0 = cqb[jn];
+    cn1 = cqb[jn + 1];
     const float* wr0 = sw + j * 2 * H;
     const float* wr1 = wr0 + 2 * H;
 #pragma unroll
