@@ -2400,9 +2400,9 @@ static void launch_lookup_nb(const LookupArgs& a, int T, int64_t B, int dim, con
 // DR_LOOKUP_KERNEL (A/B switch): 0 = slot-by-slot one-shot kernel (NB rows
 // per lane group), 1 = line probes, one-shot (ev_lookup_line_kernel), 2 =
 // line probes, software-pipelined persistent waves (ev_lookup_pipe_kernel).
-static int lookup_kernel_kind() {
-  static const int v = getenv("DR_LOOKUP_KERNEL") ? atoi(getenv("DR_LOOKUP_KERNEL")) : 1;
-  return v;
+static int lookup_kernel_kind() {   // read per launch (host only): tests cover each kernel
+  const char* e = getenv("DR_LOOKUP_KERNEL");
+  return e ? atoi(e) : 1;
 }
 
 // Persistent grid of a 256-thread kernel: resident blocks per CU x CUs,

@@ -84,12 +84,9 @@ static constexpr int64_t kRowsMaxDim = 1024;
 // Plain-sum runs (no weights, no mean / sqrtn scale, not walked compacted)
 // go to rows_serial_plain_kernel (1, default) or rows_serial_dma_kernel (2,
 // A/B); DR_GRAD_SERIAL_PLAIN=0 keeps them in rows_serial_kernel.
-static int serial_dma() {
-  static const int v = [] {
-    const char* e = getenv("DR_GRAD_SERIAL_PLAIN");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
+static int serial_dma() {   // read per call (host, once per backward): tests cover each walker
+  const char* e = getenv("DR_GRAD_SERIAL_PLAIN");
+  return e ? atoi(e) : 1;
 }
 
 static int64_t zero_scan() {

@@ -250,23 +250,30 @@ def test_multi_feature_grouped_lookup(dr, orc, grad):
         np.testing.assert_array_equal(H(v), ov)
 
 
+@pytest.mark.parametrize("kernel", ["1", "2", "0"])
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("D", [8, 128])
-def test_onehot_forward_lookup(dr, orc, fused, D):
+def test_onehot_forward_lookup(dr, orc, fused, D, kernel):
     """Forward-only one-hot lookup of filter-free EVs: the fused probe+copy
-    kernel (dr_ev_lookup_onehot) and the resolve -> pool pipeline must both
-    equal the oracle's unique -> gather -> pool, including misses (inserted
-    with the default row), duplicate new keys in one batch, key -1, and a
-    slot EV column whose rows exist but whose column was never touched."""
+    kernel (dr_ev_lookup_onehot: DR_LOOKUP_KERNEL 1 line probes, the default;
+    2 the pipelined persistent kernel; 0 the slot walk) and the resolve ->
+    pool pipeline must all equal the oracle's unique -> gather -> pool,
+    including misses (inserted with the default row), duplicate new keys in
+    one batch, key -1, and a slot EV column whose rows exist but whose column
+    was never touched."""
+    import os
     from deeprec_amd import embedding_ops as eo
+    if not fused and kernel != "1":
+        pytest.skip("the kernel switch only selects the fused lookup")
     rng = np.random.default_rng(83 + D)
     B, F = 777, 3
     saved = eo._FUSED_ONEHOT
     eo._FUSED_ONEHOT = fused
+    os.environ["DR_LOOKUP_KERNEL"] = kernel
     try:
         evs, oevs = [], []
         for f in range(F):
-            evs.append(dr.EmbeddingVariable("oh%d_%d_%d" % (f, D, fused), D, 0.5 - f,
+            evs.append(dr.EmbeddingVariable("oh%d_%d_%d_%s" % (f, D, fused, kernel), D, 0.5 - f,
                                             capacity=300))
             oevs.append(orc.EV(D, 0.5 - f))
             keys = np.arange(0, 400, 2, dtype=np.int64) + f
@@ -291,6 +298,7 @@ def test_onehot_forward_lookup(dr, orc, fused, D):
             np.testing.assert_array_equal(H(v), ov)
     finally:
         eo._FUSED_ONEHOT = saved
+        del os.environ["DR_LOOKUP_KERNEL"]
 
 
 def test_onehot_fused_abi_orders_and_slot_column(dr):

@@ -141,12 +141,24 @@ def test_rows_backward_single_feature_weighted(dr, orc, D):
         np.testing.assert_array_equal(H(out), H(out2))
 
 
+@pytest.mark.parametrize("walker", ["1", "0", "2"])
 @pytest.mark.parametrize("D", [18, 32, 1])
-def test_rows_backward_long_runs(dr, orc, D):
+def test_rows_backward_long_runs(dr, orc, D, walker):
     """Hot ids on the rows path: runs of 5000 / 256 / 257 / 768 / 200 / 511 /
     8192 / 8193 / 20000 / 21846 / 65536 positions.  Every run is ONE serial
-    chain in ascending position order (rows_serial_kernel, one piece per run):
-    bit-equal to the reference's serial sum at any length."""
+    chain in ascending position order, one piece per run, through each
+    walker (DR_GRAD_SERIAL_PLAIN 1: rows_serial_plain_kernel, the default;
+    0: rows_serial_kernel; 2: rows_serial_dma_kernel): bit-equal to the
+    reference's serial sum at any length."""
+    import os
+    os.environ["DR_GRAD_SERIAL_PLAIN"] = walker
+    try:
+        _long_runs_case(dr, orc, D, walker)
+    finally:
+        del os.environ["DR_GRAD_SERIAL_PLAIN"]
+
+
+def _long_runs_case(dr, orc, D, walker):
     rng = np.random.default_rng(41)
     runs = {0: 5000, 1: 256, 2: 257, 3: 768, 4: 200, 5: 511, 6: 8192, 7: 8193, 8: 20000,
             9: 21846, 10: 65536}
@@ -156,7 +168,8 @@ def test_rows_backward_long_runs(dr, orc, D):
     B = v.size
     evs, sps = [], []
     for f in range(3):
-        evs.append(dr.EmbeddingVariable("rlong_%d_%d" % (D, f), D, 0.1, capacity=1024))
+        evs.append(dr.EmbeddingVariable("rlong_%d_%d_%s" % (D, f, walker), D, 0.1,
+                                        capacity=1024))
         ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
         sps.append(dr.SparseTensor(T(ind), T(v), (B, 1)))
     out = dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum")
