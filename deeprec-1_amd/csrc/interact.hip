@@ -1505,8 +1505,22 @@ __global__ __launch_bounds__(256, 1) void crossnet_w4_kernel(
         (const __attribute__((address_space(1))) void*)(X + gr * (int64_t)d + k0 + c * 8),
         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
   };
+  // The fragment reads are inline asm, so the compiler takes their
+  // registers as written at issue: a read whose result it deems dead (the
+  // last iteration's Fn) or copies early lets it recycle the register while
+  // the LDS return is in flight.  Every wait on them therefore names them
+  // ("+v"), keeping them live and in place up to it.
+  auto tie16 = [&](bf16x8 (&F)[16]) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(F[0]), "+v"(F[1]), "+v"(F[2]), "+v"(F[3]), "+v"(F[4]), "+v"(F[5]),
+                   "+v"(F[6]), "+v"(F[7])::"memory");
+    asm volatile(""
+                 : "+v"(F[8]), "+v"(F[9]), "+v"(F[10]), "+v"(F[11]), "+v"(F[12]), "+v"(F[13]),
+                   "+v"(F[14]), "+v"(F[15])::"memory");
+  };
   auto iter_il = [&](int s, bf16x8 (&Fc)[16], bf16x8 (&Fn)[16]) {
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): Fc complete
+    tie16(Fc);
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // stage s+1 landed (this wave's DMAs)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -1536,6 +1550,7 @@ __global__ __launch_bounds__(256, 1) void crossnet_w4_kernel(
     // compiler's wait pass sees, so it puts no lgkmcnt(0) behind this
     // iteration's reads in front of the MFMAs
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+    tie16(Fc);
     if (s + 2 < nk)
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // stage s+1 landed (this wave's DMAs)
     else
@@ -1579,6 +1594,8 @@ __global__ __launch_bounds__(256, 1) void crossnet_w4_kernel(
     }
     if (s < nk) iter(s, F0, F1);
   }
+  tie16(F0);
+  tie16(F1);
   // the last MFMAs' results are read below (AGPR -> VGPR): cover their latency
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1865,6 +1882,212 @@ __global__ __launch_bounds__(512, 1) void crossnet_dw_kernel(
     __builtin_amdgcn_wave_barrier();
   }
 }
+
+// dW = u^T x_l on the one-wave-per-SIMD schedule (crossnet_w4_kernel) in TN
+// form (the default; DR_CROSSNET_DW_KERNEL=8ph the A/B): 4 waves of 128 x 128 outputs, the 64
+// accumulators per lane pinned in AGPRs by inline-asm MFMAs; a 4-deep ring
+// of K-32 stages, each operand 32 contraction rows x 256 output columns as
+// they lie in memory (512-B image rows, 32-B slots XOR-swizzled by dw_h(r),
+// global_load_lds three stages ahead, unconditional: past the slice's last
+// stage the pieces reload it into the dead slot); fragments by
+// ds_read_b64_tr_b16 (two per fragment, one stage ahead); batch slices as
+// crossnet_dw_kernel, fp32 partials stored straight from the accumulators.
+static constexpr int W4D_IMG = 32 * 512;   // one operand's K-32 stage: 32 rows x 256 bf16
+
+#define W4D_MFMA(C, A, B) \
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(C) : "v"(A), "v"(B))
+
+// LDS ring [u slots 0..3 | x_l slots 0..3]; the stage loop is unrolled 4x so
+// a stage's ring slot is a compile-time offset on per-lane fragment
+// addresses computed once (16 VGPRs): with the slot at run time the
+// compiler held 32 live addresses and spilled.
+__global__ __launch_bounds__(256, 1) void crossnet_dw_w4_kernel(
+    const uint16_t* __restrict__ u, const uint16_t* __restrict__ xl, int64_t K, int d, int S,
+    float* __restrict__ part, int grp) {
+  __shared__ __attribute__((aligned(1024))) char lds[8 * W4D_IMG];  // 128 KB
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int64_t nwg = (int64_t)gridDim.x;
+  const int64_t orig = blockIdx.x;
+  const int64_t xcd = orig % 8, q8 = nwg / 8, rr = nwg % 8;
+  const int64_t item = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + orig / 8;
+  const int nt = d / 256 + (d % 256 ? 1 : 0);
+  int z, m0, n0;
+  if (grp > 0) {
+    // slice-major, tiles in groups of grp tile rows walked column by column:
+    // the ~32 work-groups an XCD runs at once share one K slice and cover a
+    // grp x (32 / grp) block of tiles, so its L2 fetches each operand block
+    // once for grp (or 32 / grp) tiles instead of once per tile
+    const int64_t tiles = (int64_t)nt * nt;
+    z = (int)(item / tiles);
+    const int t = (int)(item % tiles);
+    const int g0 = (t / (grp * nt)) * grp;
+    const int gm = nt - g0 < grp ? nt - g0 : grp;
+    const int tr = t - g0 * nt;
+    m0 = (g0 + tr % gm) * 256;
+    n0 = (tr / gm) * 256;
+  } else {
+    const int64_t tile = item / S;
+    z = (int)(item % S);
+    m0 = (int)(tile / nt) * 256;
+    n0 = (int)(tile % nt) * 256;
+  }
+  const int64_t kt = K / 32;                           // 32-row stages (K % 64 == 0)
+  const int64_t ks = (kt * z) / S, ke = (kt * (z + 1)) / S;
+  const int nk = (int)(ke - ks);
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // DMA piece p of a stage: operand p >> 2 (u / x_l), image rows r0, r0 + 1
+  const uint16_t* psrc[8];
+  int pdst[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int r0 = (wave * 4 + (p & 3)) * 2;
+    const int r = r0 + (lane >> 5), sl = lane & 31;
+    const int c = (((sl >> 1) ^ dw_h(r)) << 1) | (sl & 1);   // logical 16-B chunk
+    const int cb = (p >> 2) ? n0 : m0;
+    int gc = cb + c * 8;
+    if (gc >= d) gc = cb;   // columns past the end feed discarded outputs
+    psrc[p] = ((p >> 2) ? xl : u) + (ks * 32 + r) * (int64_t)d + gc;
+    pdst[p] = (p >> 2) * 4 * W4D_IMG + r0 * 512;
+  }
+  auto dma = [&](int stage, int slot) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(psrc[p] + (int64_t)stage * 32 * d),
+          (__attribute__((address_space(3))) void*)(lds + pdst[p] + slot * W4D_IMG), 16, 0, 0);
+  };
+  // fragment f (0..7 u rows, 8..15 x_l columns): its first row's address in
+  // slot 0; the second read is 4 rows (2048 B) on (same swizzle)
+  const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int r1 = 8 * g + qq;
+  int fa[16];
+#pragma unroll
+  for (int f = 0; f < 16; ++f) {
+    const int slot = f < 8 ? wr * 8 + f : wc * 8 + (f - 8);
+    fa[f] = (f < 8 ? 0 : 4 * W4D_IMG) + r1 * 512 + ((slot ^ dw_h(r1)) << 5) + 8 * pp;
+  }
+  bf16x8 F0[16], F1[16];
+  // the transposing reads as inline asm: written with the builtin, the
+  // compiler (which cannot tell the ring slots apart) put a vmcnt(0) in
+  // front of them for the LDS-DMA pieces just issued -- a wait for stage
+  // s + 3 in every stage.  Completion is the lgkmcnt(0) at the next stage's
+  // top, before any MFMA reads these registers.
+  typedef __attribute__((address_space(3))) char lds_c;
+  const uint32_t lbase = (uint32_t)(size_t)(lds_c*)lds;
+  auto tie_compose = [&](dw_v4s (&hx)[16], dw_v4s (&hy)[16], bf16x8 (&F)[16]) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(hx[0]), "+v"(hx[1]), "+v"(hx[2]), "+v"(hx[3]), "+v"(hx[4]), "+v"(hx[5]),
+                   "+v"(hx[6]), "+v"(hx[7]), "+v"(hy[0]), "+v"(hy[1]), "+v"(hy[2]), "+v"(hy[3]),
+                   "+v"(hy[4]), "+v"(hy[5]), "+v"(hy[6]), "+v"(hy[7])::"memory");
+    asm volatile(""
+                 : "+v"(hx[8]), "+v"(hx[9]), "+v"(hx[10]), "+v"(hx[11]), "+v"(hx[12]),
+                   "+v"(hx[13]), "+v"(hx[14]), "+v"(hx[15]), "+v"(hy[8]), "+v"(hy[9]),
+                   "+v"(hy[10]), "+v"(hy[11]), "+v"(hy[12]), "+v"(hy[13]), "+v"(hy[14]),
+                   "+v"(hy[15])::"memory");
+#pragma unroll
+    for (int f = 0; f < 16; ++f)
+      F[f] = bf16x8{hx[f].x, hx[f].y, hx[f].z, hx[f].w, hy[f].x, hy[f].y, hy[f].z, hy[f].w};
+  };
+  auto read = [&](int slot, bf16x8 (&F)[16]) {
+    dw_v4s hx[16], hy[16];
+#pragma unroll
+    for (int f = 0; f < 16; ++f) {
+      const uint32_t a = lbase + (uint32_t)(fa[f] + slot * W4D_IMG);
+      asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hx[f]) : "v"(a));
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:2048" : "=v"(hy[f]) : "v"(a));
+    }
+    tie_compose(hx, hy, F);
+  };
+  // one stage: s at ring slot Q (compile time); the next stage's fragments
+  // from slot Q + 1, stage s + 3's pieces into slot Q + 3 (= the slot stage
+  // s - 1 left), clamped to the slice's last stage
+  // interleaved form: the 32 transposing reads after the stage's first 32
+  // MFMAs, the 8 DMA pieces after every 4th of the last 32; the halves are
+  // tied through the closing lgkmcnt(0) ("+v") so the compiler neither
+  // copies nor reuses their registers while the LDS returns are in flight
+  // (without the tie it recycled one for an address: an illegal access)
+  auto stage_il = [&](int Q, int s, bf16x8 (&FC)[16], bf16x8 (&FN)[16]) {
+    const int s3 = s + 3 < nk ? s + 3 : nk - 1;
+    const int rslot = s + 1 < nk ? ((Q + 1) & 3) : Q;
+    const int dslot = (Q + 3) & 3;
+    dw_v4s hx[16], hy[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        W4D_MFMA(acc[i][j], FC[i], FC[8 + j]);
+        const int m = i * 8 + j;
+        if (m < 32) {
+          const int f = m >> 1;
+          const uint32_t a = lbase + (uint32_t)(fa[f] + rslot * W4D_IMG);
+          if (m & 1)
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:2048" : "=v"(hy[f]) : "v"(a));
+          else
+            asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hx[f]) : "v"(a));
+        } else if ((m & 3) == 2) {
+          const int p = (m - 34) >> 2;
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(psrc[p] + (int64_t)s3 * 32 * d),
+              (__attribute__((address_space(3))) void*)(lds + pdst[p] + dslot * W4D_IMG), 16, 0, 0);
+        }
+      }
+    tie_compose(hx, hy, FN);
+  };
+#define W4D_ITER(Q, FC, FN)                                                               \
+  do {                                                                                    \
+    __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): FC complete */                    \
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); /* stage s+1 landed (this wave) */  \
+    __builtin_amdgcn_s_barrier();                                                         \
+    asm volatile("" ::: "memory");                                                        \
+    stage_il((Q), s, FC, FN);                                                             \
+    ++s;                                                                                  \
+  } while (0)
+  if (nk > 0) {
+    dma(0, 0);
+    dma(1 < nk ? 1 : nk - 1, 1);
+    dma(2 < nk ? 2 : nk - 1, 2);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read(0, F0);
+    int s = 0;
+    while (s + 4 <= nk) {
+      W4D_ITER(0, F0, F1);
+      W4D_ITER(1, F1, F0);
+      W4D_ITER(2, F0, F1);
+      W4D_ITER(3, F1, F0);
+    }
+    if (s < nk) W4D_ITER(0, F0, F1);
+    if (s < nk) W4D_ITER(1, F1, F0);
+    if (s < nk) W4D_ITER(2, F0, F1);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  }
+#undef W4D_ITER
+  // fp32 partials straight from the accumulators (C/D map: row fq * 4 + r,
+  // column fr of each 16 x 16 tile; 16 lanes write 64 contiguous bytes)
+  const int fr = lane & 15, fq = lane >> 4;
+  float* pz = part + (int64_t)z * d * d;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = n0 + wc * 128 + j * 16 + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr * 128 + i * 16 + fq * 4 + r;
+        if (m < d && n < d) pz[(int64_t)m * d + n] = acc[i][j][r];
+      }
+    }
+}
+#undef W4D_MFMA
 
 // dW = sum over slices z of part[z], in slice order (deterministic)
 __global__ void crossnet_dw_reduce_kernel(const float* __restrict__ part, int S, int64_t n4,
@@ -2351,8 +2574,23 @@ int dr_crossnet_dw_bf16(const uint16_t* u, const uint16_t* xl, int64_t batch, in
   const int Sl = crossnet_dw_slices(batch, d);
   const int64_t tiles = (int64_t)ceil_div(d, 256) * ceil_div(d, 256);
   float* part = static_cast<float*>(ws);
-  hipLaunchKernelGGL(crossnet_dw_kernel, dim3((unsigned)(tiles * Sl)), dim3(512), 0, S(stream),
-                     u, xl, batch, d, Sl, part);
+  // the one-wave-per-SIMD form by default (1.35-1.37 ms at B = 65536, d =
+  // 3392 against 2.16 for the 8-phase kernel and 1.43-1.64 for hipBLASLt,
+  // profiles/r05_cross_dw_w4.log); DR_CROSSNET_DW_KERNEL=8ph (read per call)
+  // selects the 8-phase kernel (A/B)
+  const char* kern = getenv("DR_CROSSNET_DW_KERNEL");
+  const bool w4 = !(kern && strcmp(kern, "8ph") == 0);
+  // DR_CROSSNET_DW_ORDER (read per call): the w4 work order, 0 = tile-major
+  // (an XCD's concurrent work-groups are the slices of a few tiles), g > 0 =
+  // slice-major in groups of g tile rows (default 4)
+  const char* ord = getenv("DR_CROSSNET_DW_ORDER");
+  const int grp = ord ? atoi(ord) : 4;
+  if (w4)
+    hipLaunchKernelGGL(crossnet_dw_w4_kernel, dim3((unsigned)(tiles * Sl)), dim3(256), 0,
+                       S(stream), u, xl, batch, d, Sl, part, grp < 0 ? 0 : grp);
+  else
+    hipLaunchKernelGGL(crossnet_dw_kernel, dim3((unsigned)(tiles * Sl)), dim3(512), 0, S(stream),
+                       u, xl, batch, d, Sl, part);
   hipLaunchKernelGGL(crossnet_dw_reduce_kernel, dim3((unsigned)ceil_div(n4, 256)), dim3(256), 0,
                      S(stream), part, Sl, n4, (int64_t)d * d, dw);
   DR_LAUNCH_CHECK();

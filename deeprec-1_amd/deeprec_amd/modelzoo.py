@@ -738,17 +738,20 @@ def _cross_dx(u, wb, g):
     return ops.crossnet_dx(u, wb.t().contiguous(), g)
 
 
-# The cross layers' weight gradient: the library GEMM writing fp32 (default;
-# 1.43-1.63 ms at B = 65 536, d = 3 392) or, DR_CROSSNET_DW=hand, the hand TN
-# MFMA kernel (dr_crossnet_dw_bf16: 2.16 ms there, profiles/r05_cross_dw.log)
-_CROSS_DW_HAND = os.environ.get("DR_CROSSNET_DW", "lib") == "hand"
+# The cross layers' weight gradient: the hand TN MFMA kernel (default;
+# dr_crossnet_dw_bf16, 1.35-1.37 ms at B = 65 536, d = 3 392,
+# profiles/r05_cross_dw_w4.log) or, DR_CROSSNET_DW=lib, the library GEMM
+# writing fp32 (1.43-1.64 ms there)
+_CROSS_DW_HAND = os.environ.get("DR_CROSSNET_DW", "hand") == "hand"
 
 
 def _cross_dw(u, x):
     """dW = u^T x of a cross layer in fp32 (fp32 accumulation, no bf16
-    rounding of the result): torch.mm with out_dtype=float32 (hipBLASLt), the
-    bf16 product widened where that overload is absent, or the hand kernel
-    (A/B)."""
+    rounding of the result): the hand kernel (dr_crossnet_dw_bf16, 1.35 ms
+    at B = 65536, d = 3392 against 1.43-1.64 ms for hipBLASLt); for shapes it
+    does not take, or with DR_CROSSNET_DW=lib (A/B), torch.mm with
+    out_dtype=float32, the bf16 product widened where that overload is
+    absent."""
     if _CROSS_DW_HAND:
         dw = ops.crossnet_dw(u, x)
         if dw is not None:

@@ -110,15 +110,20 @@ def test_crossnet_dx_matches_torch(B, d):
         assert torch.equal(ops.crossnet_dx(u, W.t().contiguous(), g), dx)
 
 
+@pytest.mark.parametrize("kernel,order", [("w4", "4"), ("w4", "0"), ("w4", "14"), ("8ph", "4")])
 @pytest.mark.parametrize("B,d", [(1024, 192), (4096, 3392), (64, 64), (2048, 448),
                                  (65536, 3392)])
-def test_crossnet_dw_matches_fp64(B, d):
-    """dr_crossnet_dw_bf16 (dW = u^T x on the 256^2 four-phase schedule in TN
-    form, batch slices summed in order): against the fp64 product of the same
-    bf16 operands, within fp32 accumulation error (each entry a sum of B
-    products: |err| <= 2^-22 sqrt(B) max|row norms|-scale bound, checked as
-    1e-5 of the entry scale), and bit-identical across launches."""
+def test_crossnet_dw_matches_fp64(B, d, kernel, order, monkeypatch):
+    """dr_crossnet_dw_bf16 (dW = u^T x in TN form, batch slices summed in
+    order) on each kernel (w4 = one wave per SIMD, the default, in tile-major
+    and slice-major work orders; 8ph = the 256^2 eight-phase A/B): against the
+    fp64 product of the same bf16 operands, within fp32 accumulation error
+    (each entry a sum of B products: |err| <= 2^-22 sqrt(B) max|row
+    norms|-scale bound, checked as 1e-5 of the entry scale), and
+    bit-identical across launches."""
     from deeprec_amd import ops
+    monkeypatch.setenv("DR_CROSSNET_DW_KERNEL", kernel)
+    monkeypatch.setenv("DR_CROSSNET_DW_ORDER", order)
     gen = torch.Generator(device="cpu").manual_seed(B + 7 * d)
     u = torch.randn(B, d, generator=gen).to(DEV, torch.bfloat16)
     x = torch.randn(B, d, generator=gen).to(DEV, torch.bfloat16)

@@ -33,6 +33,12 @@ def main():
     u = torch.randn(B, d, device="cuda", generator=g).to(torch.bfloat16)
     x = torch.randn(B, d, device="cuda", generator=g).to(torch.bfloat16)
     flop = 2.0 * B * d * d
+    if "--hand-only" in sys.argv:   # counter passes: the hand kernel alone, 5 calls
+        for _ in range(5):
+            ops.crossnet_dw(u, x)
+        torch.cuda.synchronize()
+        print("hand dW x5 done", flush=True)
+        return
     ref = torch.matmul(u.t(), x).float()
     t = timed(lambda: torch.matmul(u.t(), x).float())
     print("matmul(u.t(), x).float(): %.3f ms  %.0f TF/s" % (t, flop / t / 1e9), flush=True)
@@ -42,6 +48,15 @@ def main():
     print("crossnet_dw (256^2 four-phase TN, split %d): %.3f ms  %.0f TF/s  max rel diff %.2e"
           % (dr._lib.lib().dr_crossnet_dw_workspace_size(B, d) // (4 * d * d), t, flop / t / 1e9,
              err), flush=True)
+    if os.environ.get("DR_CROSSNET_DW_KERNEL", "w4") == "w4":   # work orders (read per call)
+        for o in ("0", "2", "4", "8", "14"):
+            os.environ["DR_CROSSNET_DW_ORDER"] = o
+            got = ops.crossnet_dw(u, x)
+            err = ((got - ref).abs().max() / ref.abs().max()).item()
+            t = timed(lambda: ops.crossnet_dw(u, x))
+            print("crossnet_dw w4 order %s: %.3f ms  %.0f TF/s  max rel diff %.2e"
+                  % (o, t, flop / t / 1e9, err), flush=True)
+        del os.environ["DR_CROSSNET_DW_ORDER"]
     t = timed(lambda: torch.matmul(u.t(), x).float())
     print("matmul(u.t(), x).float() again: %.3f ms" % t, flush=True)
     try:   # the library GEMM writing fp32 directly (aten::mm.dtype)
