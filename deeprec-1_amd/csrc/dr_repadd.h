@@ -1,0 +1,122 @@
+// dr_repadd.h -- k in-order fp32 additions of one term, exactly, in O(log)
+// steps: rep_add(s, x, k) == fl(...fl(fl(s + x) + x)... + x) (k additions,
+// round-to-nearest-even after each), bit for bit.
+//
+// A long run's serial gradient sum (segment_reduction_ops.cc:391-404: one
+// fp32 add per position, ascending) often adds the same term many times in
+// a row -- DIN's padding id: every padded history position of a sample
+// carries that sample's his_sum gradient, ~50 identical terms per sample.
+// Within one binade of the running sum the grid is fixed (ulp u), and while
+// the exact sums stay in it every add moves the sum by the same whole number
+// of ulps, rint(x / u) -- for a rounding tie (x / u = m + 1/2) only from an
+// even sum, which every tie leaves.  So after one plain add, the next n adds
+// are s1 + n * rint(x / u) ulps, computed exactly in double, n as far as the
+// binade allows; an add that leaves the sum unchanged (x = 0, x below half an
+// ulp, NaN, Inf) ends the walk.  The steps near a binade edge or a sign
+// change, a tie from an odd sum, zero and subnormal sums are plain adds.
+//
+// Header-only and host-compilable (tests/test_repadd_host.py checks it
+// against the plain loop on the CPU).
+#pragma once
+#include <math.h>
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define DR_HD __host__ __device__
+#else
+#define DR_HD
+#endif
+
+namespace dr {
+
+DR_HD inline uint32_t f32_bits(float f) {
+  uint32_t b;
+  __builtin_memcpy(&b, &f, 4);
+  return b;
+}
+
+// The common case in integer arithmetic, no branches but the verdict: all k
+// adds round on s's own grid (s normal, x normal and at most 2^25 ulps below
+// s's, the exact sums inside s's binade, no tie from an odd s).  With a = s
+// in ulps (2^23 + mantissa) and x = xu ulps along s's sign, each add moves a
+// by D = rint(xu) (ties to even); the exact sum a + j D + xu is checked as
+// A' + f with A' = a + (j + 1) D and f = xu - D in [-1/2, 1/2] (only its
+// sign matters against the integer bounds).  Returns false to leave it to
+// the general walk.
+DR_HD inline bool rep_add_grid(float s, float x, int64_t k, float* out) {
+  const uint32_t bs = f32_bits(s), bx = f32_bits(x);
+  const int es = (int)((bs >> 23) & 0xFF), ex = (int)((bx >> 23) & 0xFF);
+  const int sh = es - ex;   // xu = mx / 2^sh
+  if (es == 0 || es == 0xFF || ex == 0 || sh < 1 || sh > 25) return false;
+  const int64_t mx = (int64_t)((bx & 0x7FFFFFu) | 0x800000u);
+  const int64_t ip = mx >> sh, fr = mx & (((int64_t)1 << sh) - 1), half = (int64_t)1 << (sh - 1);
+  const bool up = fr > half || (fr == half && (ip & 1));   // |xu| rounded up
+  const bool tie = fr == half;
+  const int64_t a = (int64_t)(bs & 0x7FFFFFu) | 0x800000;
+  if (tie && (a & 1)) return false;
+  const int64_t dabs = ip + (up ? 1 : 0);
+  const bool grow = ((bs ^ bx) >> 31) == 0;   // x along s's sign
+  const int64_t D = grow ? dabs : -dabs;
+  // sign of f = xu - D along the magnitude: |xu| - dabs is < 0 when rounded
+  // up with a fraction, > 0 when rounded down with one, 0 when exact
+  int fs = fr == 0 ? 0 : (up ? -1 : 1);
+  if (!grow) fs = -fs;
+  const int64_t lo = 0x800000, hi = 0x1000000;
+  const int64_t a1 = a + D, ak = a + k * D;   // A' of the first and the last add
+  auto in_grid = [&](int64_t ap) {
+    const bool below_hi = fs < 0 ? ap <= hi : ap < hi;
+    const bool above_lo = fs < 0 ? ap >= lo + 1 : ap >= lo;
+    return below_hi && above_lo;
+  };
+  if (!in_grid(a1) || !in_grid(ak)) return false;
+  *out = __builtin_bit_cast(float, (bs & 0x80000000u) + ((uint32_t)es << 23) + (uint32_t)(ak - lo));
+  return true;
+}
+
+DR_HD inline float rep_add(float s, float x, int64_t k) {
+  float r;
+  if (k > 1 && rep_add_grid(s, x, k, &r)) return r;
+  const double lo = 8388608.0, hi = 16777216.0;   // a binade in ulps: [2^23, 2^24)
+  while (k > 0) {
+    const float s1 = s + x;   // one plain add, then the rest in closed form if it may
+    const uint32_t b1 = f32_bits(s1);
+    const bool fixed = b1 == f32_bits(s);   // s + x rounded back to s: so does every later add
+    s = s1;
+    if (--k == 0 || fixed) break;
+    const int ex = (int)((b1 >> 23) & 0xFF);
+    if (ex == 0 || ex == 0xFF) continue;   // zero, subnormal, Inf, NaN: plain adds
+    // s1's magnitude in ulps of its binade, x along the magnitude in ulps
+    // (both exact in double)
+    const double inv_u = ldexp(1.0, 150 - ex);
+    const double xu = (b1 >> 31) ? -(double)x * inv_u : (double)x * inv_u;
+    const double a1 = lo + (double)(b1 & 0x7FFFFFu);
+    const double dd = rint(xu);   // the in-grid step: nearest, ties to even
+    // a tie (xu = m + 1/2) adds rint(xu) only from an even sum: from an odd
+    // one the first add goes to the other neighbour (then all are even)
+    if (xu - floor(xu) == 0.5 && (b1 & 1u)) continue;
+    // add j (0-based, from a1) rounds on this grid while a1 + j dd + xu is in
+    // [lo, hi): monotone in j
+    auto in_grid = [&](int64_t j) {
+      const double v = a1 + (double)j * dd + xu;
+      return v >= lo && v < hi;
+    };
+    if (dd == 0) {   // s1 + x rounds back to s1: a fixed point
+      if (in_grid(0)) break;
+      continue;
+    }
+    int64_t n = k;
+    if (!in_grid(n - 1)) {
+      const double lim = dd > 0 ? (hi - a1 - xu) / dd : (a1 + xu - lo) / -dd;
+      n = lim > 0 ? (lim < (double)k ? (int64_t)lim : k) : 0;
+      while (n > 0 && !in_grid(n - 1)) --n;
+      while (n < k && in_grid(n)) ++n;
+    }
+    if (n == 0) continue;
+    const double a = (a1 + (double)n * dd) * ldexp(1.0, ex - 150);   // exact (<= the next power of 2)
+    s = (float)((b1 >> 31) ? -a : a);
+    k -= n;
+  }
+  return s;
+}
+
+}  // namespace dr

@@ -40,6 +40,7 @@
 // association depends only on the run's own position order -- never on the
 // key -> row numbering that racing first-touch inserts assign, nor on where
 // the run lands in the sorted array.
+#include "dr_repadd.h"
 #include "dr_rows.h"
 
 namespace dr {
@@ -89,6 +90,24 @@ static int serial_dma() {   // read per call (host, once per backward): tests co
   return e ? atoi(e) : 1;
 }
 
+// Segment scan of the plain long runs (A/B, opt-in): a one-piece plain-sum
+// run longer than seg_scan() positions is first split (rows_seg_kernel, in
+// parallel) into segments of bitwise-identical consecutive terms -- DIN's
+// padding id: each sample's padded history positions all carry that
+// sample's his_sum gradient -- and, when its segments average at least
+// kSegMin terms, walked one segment at a time (rows_serial_seg_kernel): k
+// additions of one term in closed form (rep_add, dr_repadd.h), bit-equal to
+// k plain adds.  Off by default: a closed-form segment costs ~600 cycles
+// of branchy integer work against 8.5 per position for the plain chain, so
+// it only pays for segments of ~70+ terms; DIN's average 50 (4 050 segments
+// over 203 800 padding positions) walked 4x slower (profiles/r05_seg_walk.log).
+// Read per call (DR_GRAD_SEG_SCAN=n positions; 0, the default, = off).
+static constexpr int64_t kSegMin = 64;
+static int64_t seg_scan() {
+  const char* e = getenv("DR_GRAD_SEG_SCAN");
+  return e ? (int64_t)atoll(e) : (int64_t)0;
+}
+
 static int64_t zero_scan() {
   // read per call (host only, once per backward): tests switch it on around
   // one call.  Off by default: none of the measured workloads has exact-zero
@@ -126,13 +145,21 @@ struct RowsLong {
   int32_t* rnz;            // per long run: its nonzero terms (zero scan)
   float* zrow;             // 64 zeros (rows_expand_kernel): the term of an invalid bag
   int dma;                 // who takes the plain-sum runs (serial_dma()): 1 plain, 2 dma
+  int32_t* rseg;           // per long run: its segment count (seg scan; -1: not scanned)
+  int64_t sscan;           // seg-scan plain runs longer than this (0: never)
 };
 
 // A zero-scanned run is walked compacted only when at most half its terms
 // are nonzero (the same test in both serial kernels, so they split the runs
 // between them exactly).
 __device__ __forceinline__ bool run_sparse(const RowsLong& L, int i, int np, int64_t len) {
-  return np == 1 && L.cfirst[i] >= 0 && 2 * (int64_t)L.rnz[i] <= len;
+  return np == 1 && L.cfirst[i] >= 0 && L.rseg[i] < 0 && 2 * (int64_t)L.rnz[i] <= len;
+}
+
+// A seg-scanned run is walked by segments when they average at least kSegMin
+// terms (every walker applies the same test, so they split the runs exactly).
+__device__ __forceinline__ bool run_seg(const RowsLong& L, int i, int np, int64_t len) {
+  return np == 1 && L.cfirst[i] >= 0 && L.rseg[i] >= 0 && kSegMin * (int64_t)L.rseg[i] <= len;
 }
 
 // Table of global position i (lane-varying; koff staged in LDS).
@@ -815,8 +842,11 @@ __global__ __launch_bounds__(256) void rows_expand_kernel(RowsGroup g, int T, Ro
     // zero-scan chunks: one-piece runs of a zero-started chain (sum combiner
     // or weighted: rows_serial_kernel's fresh start is then 0 + x_0)
     const bool zs = g.d[t].combiner == DR_COMBINER_SUM || g.d[t].weights != nullptr;
-    const int nch = (np == 1 && zs && L.zscan > 0 && len > L.zscan)
-                        ? (int)((len + kRowsChunk - 1) / kRowsChunk) : 0;
+    const bool zscan = np == 1 && zs && L.zscan > 0 && len > L.zscan;
+    // plain-sum runs not zero-scanned: segment scan (seg_scan())
+    const bool plain = g.d[t].combiner == DR_COMBINER_SUM && g.d[t].weights == nullptr;
+    const bool sscan = !zscan && np == 1 && plain && L.sscan > 0 && len > L.sscan;
+    const int nch = (zscan || sscan) ? (int)((len + kRowsChunk - 1) / kRowsChunk) : 0;
     if (threadIdx.x == 0) {
       const int fi = atomicAdd(L.nitems, np);
       L.rlen[i] = (int32_t)len;
@@ -825,6 +855,7 @@ __global__ __launch_bounds__(256) void rows_expand_kernel(RowsGroup g, int T, Ro
       const int cf = nch ? atomicAdd(L.nchunk, nch) : -1;
       L.cfirst[i] = cf;
       L.rnz[i] = 0;
+      L.rseg[i] = sscan ? 0 : -1;
       smin = cf;
     }
     __syncthreads();
@@ -857,6 +888,7 @@ __global__ __launch_bounds__(256) void rows_nz_kernel(RowsGroup g, int T, int di
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int c = blockIdx.x; c < n; c += gridDim.x) {   // block-uniform
     const int i = L.crun[2 * c], k = L.crun[2 * c + 1];
+    if (L.rseg[i] >= 0) continue;   // a seg-scanned run's chunk (rows_seg_kernel)
     const int64_t c0 = L.longs[i];
     const int64_t len = L.rlen[i];
     const int64_t cs = c0 + (int64_t)k * kRowsChunk;
@@ -899,6 +931,201 @@ __global__ __launch_bounds__(256) void rows_nz_kernel(RowsGroup g, int T, int di
       if (nzc) atomicAdd(&L.rnz[i], nzc);
     }
     __syncthreads();   // wc is rewritten by the next chunk
+  }
+}
+
+// Segment scan of the seg-scanned runs' chunks (seg_scan()): one block per
+// chunk of kRowsChunk positions, one thread per position q: q ends a segment
+// when it is the run's last position or its term differs, bitwise in any
+// column, from position q + 1's (the same bag row always gives the same
+// term; an invalid bag's term is the zero row).  The chunk's segment ends are
+// compacted in ascending order into kpos[chunk start ..], counted in ccnt
+// and summed per run into rseg.
+template <int VEC>
+__global__ __launch_bounds__(256) void rows_seg_kernel(RowsGroup g, int T, int dim, RowsLong L) {
+  __shared__ int64_t sk[DR_MAX_GROUP + 1];
+  __shared__ int wc[4];
+  using V = typename VecT<VEC>::T;
+  if (threadIdx.x <= T) sk[threadIdx.x] = g.koff[threadIdx.x];
+  __syncthreads();
+  const int n = *L.nchunk;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int c = blockIdx.x; c < n; c += gridDim.x) {   // block-uniform
+    const int i = L.crun[2 * c], k = L.crun[2 * c + 1];
+    if (L.rseg[i] < 0) continue;   // a zero-scanned run's chunk (rows_nz_kernel)
+    const int64_t c0 = L.longs[i];
+    const int64_t len = L.rlen[i];
+    const int64_t cs = c0 + (int64_t)k * kRowsChunk;
+    const int64_t ce = c0 + len < cs + kRowsChunk ? c0 + len : cs + kRowsChunk;
+    const int t = tab_of(sk, T, L.perm[c0]);
+    const dr_pool_grad_desc& d = g.d[t];
+    const int64_t q = cs + tid;
+    bool end = false;
+    if (q < ce) {
+      end = q + 1 >= c0 + len;
+      if (!end) {
+        const int32_t r0 = L.srow[q], r1 = L.srow[q + 1];
+        if (r0 != r1) {
+          const float* p0 = d.top_grad + (int64_t)(r0 >= 0 ? r0 : 0) * d.top_stride;
+          const float* p1 = d.top_grad + (int64_t)(r1 >= 0 ? r1 : 0) * d.top_stride;
+          for (int cv = 0; cv * VEC < dim && !end; ++cv) {
+            const V x0 = r0 >= 0 ? gld(reinterpret_cast<const V*>(p0) + cv) : vzero<V>();
+            const V x1 = r1 >= 0 ? gld(reinterpret_cast<const V*>(p1) + cv) : vzero<V>();
+            if constexpr (VEC == 4)
+              end = (__float_as_uint(x0.x) != __float_as_uint(x1.x)) ||
+                    (__float_as_uint(x0.y) != __float_as_uint(x1.y)) ||
+                    (__float_as_uint(x0.z) != __float_as_uint(x1.z)) ||
+                    (__float_as_uint(x0.w) != __float_as_uint(x1.w));
+            else if constexpr (VEC == 2)
+              end = (__float_as_uint(x0.x) != __float_as_uint(x1.x)) ||
+                    (__float_as_uint(x0.y) != __float_as_uint(x1.y));
+            else
+              end = __float_as_uint(x0) != __float_as_uint(x1);
+          }
+        }
+      }
+    }
+    const uint64_t bm = __ballot(end);
+    if (lane == 0) wc[wv] = __popcll(bm);
+    __syncthreads();
+    int before = 0;
+    for (int w = 0; w < wv; ++w) before += wc[w];
+    if (end) L.kpos[cs + before + __popcll(bm & lanemask_lt())] = (int32_t)q;
+    if (tid == 0) {
+      const int ns = wc[0] + wc[1] + wc[2] + wc[3];
+      L.ccnt[c] = ns;
+      if (ns) atomicAdd(&L.rseg[i], ns);
+    }
+    __syncthreads();   // wc is rewritten by the next chunk
+  }
+}
+
+// The runs walked by segments (run_seg()): one block per (run, slice of 16
+// columns).  Windows of up to 256 chunks: the chunks' segment ends (kpos)
+// in ascending order, prefix of their counts in LDS; stages of up to 1024
+// segments: every thread stages segments' terms (the term at the segment's
+// end, = every term of it) transposed [column][segment] and their lengths
+// (end - previous end); then lanes 0..15 of wave 0 each walk one column:
+// acc = rep_add(acc, term, length) per segment, in order.  The chain starts
+// at 0 (the sum combiner), so the first segment's first add is 0 + x, as in
+// the plain walk.
+template <int VEC, bool SGD, bool WB>
+__global__ __launch_bounds__(1024) void rows_serial_seg_kernel(RowsGroup g, int T, int dim,
+                                                               RowsLong L, RowsSgd sg) {
+  using V = typename VecT<VEC>::T;
+  constexpr int SW = 16;           // columns per slice
+  constexpr int SV = SW / VEC;     // vectors of a term's slice
+  constexpr int S = 1024;          // segments per stage
+  constexpr int NT = 1024;
+  constexpr int WCH = NT;          // chunks per window (one per thread)
+  __shared__ __attribute__((aligned(16))) float stage[SW * S];
+  __shared__ int32_t qend[S];
+  __shared__ int64_t sk[DR_MAX_GROUP + 1];
+  __shared__ int32_t cpre[WCH + 1];
+  __shared__ int32_t wsum[NT / 64];
+  __shared__ float accs[SW];
+  if (threadIdx.x <= T) sk[threadIdx.x] = g.koff[threadIdx.x];
+  __syncthreads();
+  const int nsl = (dim + SW - 1) / SW;
+  const int64_t total = (int64_t)(*L.nitems) * nsl;
+  const int tid = threadIdx.x, lane = tid & 63;
+  // wave w walks column w of the slice, all 64 lanes on the same values:
+  // the closed form branches per column, and one column per wave keeps each
+  // wave on its own path (16 columns on the lanes of one wave ran the union
+  // of their paths: 2-3x slower than the plain walk, profiles/r05_seg_walk.log)
+  const int wcol = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int64_t wi = blockIdx.x; wi < total; wi += gridDim.x) {   // block-uniform
+    const int j = (int)(wi / nsl), slice = (int)(wi % nsl);
+    const int i = L.items[2 * j];
+    const int64_t len = L.rlen[i];
+    const int np = (int)((len + L.smax - 1) / L.smax);
+    if (!run_seg(L, i, np, len)) continue;
+    const int64_t c0 = L.longs[i];
+    const int32_t pc = L.perm[c0];
+    const uint32_t u = L.skey[c0];
+    const int t = tab_of(sk, T, pc);
+    const dr_pool_grad_desc& d = g.d[t];
+    const int cf = L.cfirst[i];
+    const int64_t nch = (len + kRowsChunk - 1) / kRowsChunk;
+    const int64_t ts = d.top_stride;
+    float acc = 0.f;
+    int64_t prev = c0 - 1;   // the end of the segment before the stage's first
+    for (int64_t w0 = 0; w0 < nch; w0 += WCH) {
+      const int nw = (int)(nch - w0 < WCH ? nch - w0 : WCH);
+      // exclusive prefix of the window's chunk counts (one chunk per thread)
+      const int cnt = tid < nw ? L.ccnt[cf + w0 + tid] : 0;
+      int incl = cnt;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+      }
+      if (lane == 63) wsum[tid >> 6] = incl;
+      __syncthreads();
+      int before = incl - cnt;
+      for (int w = 0; w < (tid >> 6); ++w) before += wsum[w];
+      if (tid < nw) cpre[tid] = before;
+      if (tid == nw - 1) cpre[nw] = before + cnt;
+      __syncthreads();
+      const int K = cpre[nw];
+      for (int b0 = 0; b0 < K; b0 += S) {
+        const int nv = K - b0 < S ? K - b0 : S;
+        for (int e = tid; e < nv; e += NT) {
+          int lo = 0, hi = nw - 1;   // last chunk with cpre <= b0 + e
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (cpre[mid] <= b0 + e)
+              lo = mid;
+            else
+              hi = mid - 1;
+          }
+          const int32_t q = L.kpos[c0 + (w0 + lo) * kRowsChunk + (b0 + e - cpre[lo])];
+          qend[e] = q;
+          const int32_t rq = L.srow[q];
+          const float* row = d.top_grad + (int64_t)(rq >= 0 ? rq : 0) * ts;
+#pragma unroll
+          for (int cv = 0; cv < SV; ++cv) {
+            const int col = slice * SW + cv * VEC;
+            V x = (rq >= 0 && col < dim) ? gld(reinterpret_cast<const V*>(row + col)) : vzero<V>();
+            if constexpr (VEC == 4) {
+              stage[(cv * 4 + 0) * S + e] = x.x;
+              stage[(cv * 4 + 1) * S + e] = x.y;
+              stage[(cv * 4 + 2) * S + e] = x.z;
+              stage[(cv * 4 + 3) * S + e] = x.w;
+            } else if constexpr (VEC == 2) {
+              stage[(cv * 2 + 0) * S + e] = x.x;
+              stage[(cv * 2 + 1) * S + e] = x.y;
+            } else {
+              stage[cv * S + e] = x;
+            }
+          }
+        }
+        __syncthreads();
+        if (wcol < SW && slice * SW + wcol < dim) {   // (columns past dim: idle)
+          const float* sp = stage + wcol * S;
+          int64_t pe = prev;
+          for (int e = 0; e < nv; ++e) {
+            const int32_t q = qend[e];
+            acc = rep_add(acc, sp[e], (int64_t)q - pe);
+            pe = q;
+          }
+        }
+        prev = qend[nv - 1];
+        __syncthreads();   // the stage and qend are rewritten next
+      }
+    }
+    if (wcol < SW && lane == 0) accs[wcol] = acc;
+    __syncthreads();
+    if (wcol == 0) {
+      const int col = slice * SW + lane;
+      const float a0 = accs[lane < SW ? lane : 0];
+      const float nx = __shfl_down(a0, 1, 64);
+      const int64_t o = SGD ? 0 : sk[t] + (int64_t)L.ex[pc] - L.base[t];
+      if (lane < SW && (lane & 1) == 0 && col < dim)
+        rows_fin_pair<SGD, WB>(sg, t, u, o, dim, col, a0, nx, L.gu);
+      if (slice == 0 && lane == 0) rows_fin_run<SGD>(sg, t, u, o, dim, L);
+    }
+    __syncthreads();   // accs is rewritten by the next item
   }
 }
 
@@ -970,6 +1197,7 @@ __global__ __launch_bounds__(1024) void rows_serial_kernel(RowsGroup g, int T, i
     // zero-scanned run (rows_nz_kernel): walk only its nonzero terms, chunk by
     // chunk in ascending order; a zero-started chain is unchanged by the
     // skipped +-0.0 terms (zero_scan()).  Otherwise entry e = position ps + e.
+    if (run_seg(L, i, np, len)) continue;       // rows_serial_seg_kernel's run
     const bool zc = run_sparse(L, i, np, len);
     if (L.dma && !wt && !ms && !zc) continue;   // the plain / dma kernel's run
     const int cf = zc ? __builtin_amdgcn_readfirstlane(L.cfirst[i]) : -1;
@@ -1179,6 +1407,7 @@ __global__ __launch_bounds__(1024) void rows_serial_plain_kernel(RowsGroup g, in
     const bool wt = d.weights != nullptr;
     const bool ms = !wt && d.combiner != DR_COMBINER_SUM;
     if (wt || ms || run_sparse(L, i, np, len)) continue;   // rows_serial_kernel's run
+    if (run_seg(L, i, np, len)) continue;                  // rows_serial_seg_kernel's run
     const int64_t K = pe - ps;
     const int colv = slice * SV + cv;
     const float* src = d.top_grad + (colv * VEC < dim ? colv * VEC : 0);
@@ -1312,6 +1541,7 @@ __global__ __launch_bounds__(1024) void rows_serial_dma_kernel(RowsGroup g, int 
     const bool wt = d.weights != nullptr;
     const bool ms = !wt && d.combiner != DR_COMBINER_SUM;
     if (wt || ms || run_sparse(L, i, np, len)) continue;   // rows_serial_kernel's run
+    if (run_seg(L, i, np, len)) continue;                  // rows_serial_seg_kernel's run
     const int64_t K = pe - ps;
     const int64_t nst = (K + S - 1) / S;
     const int c0l = slice * SW;
@@ -1462,6 +1692,7 @@ struct RowsWs {
   int32_t* ccnt;
   int32_t* kpos;
   int32_t* rnz;
+  int32_t* rseg;
   float* zrow;
   void* sort_ws;
   size_t sort_bytes;
@@ -1469,7 +1700,7 @@ struct RowsWs {
   RowsLong longrun(uint64_t* gptr, float* gu) const {
     return RowsLong{kout, perm, ex, base, srow, smul, sdiv, longs, nlong, rlen, rfirst, items,
                     nitems, gptr, gu, part, serial_max(), zero_scan(), cfirst, crun, nchunk,
-                    ccnt, kpos, rnz, zrow, serial_dma()};
+                    ccnt, kpos, rnz, zrow, serial_dma(), rseg, seg_scan()};
   }
 };
 
@@ -1509,6 +1740,7 @@ static RowsWs carve_rows(void* ws, int64_t n, size_t* used) {
   w.ccnt = c.take<int32_t>(chunks);
   w.kpos = c.take<int32_t>(nn);
   w.rnz = c.take<int32_t>(runs);
+  w.rseg = c.take<int32_t>(runs);
   w.zrow = c.take<float>(64);
   w.sort_bytes = sort_pairs_u32_ws_bytes(nn);
   w.sort_ws = c.take<char>(w.sort_bytes);
@@ -1532,6 +1764,17 @@ static void launch_long(const RowsGroup& g, int T, int dim, const RowsLong& L, c
     const int64_t chunks = N / kRowsChunk + 1;
     hipLaunchKernelGGL((rows_nz_kernel<VEC>), dim3((unsigned)(chunks < 2048 ? chunks : 2048)),
                        dim3(256), 0, s, g, T, dim, L);
+  }
+  const bool segs = L.sscan > 0 && N > L.sscan;
+  if (segs) {
+    const int64_t chunks = N / kRowsChunk + 1;
+    // (8-byte rows when every slice is: as the walk below)
+    if (VEC == 1 && aligned2 && dim % 2 == 0)
+      hipLaunchKernelGGL((rows_seg_kernel<2>), dim3((unsigned)(chunks < 2048 ? chunks : 2048)),
+                         dim3(256), 0, s, g, T, dim, L);
+    else
+      hipLaunchKernelGGL((rows_seg_kernel<VEC>), dim3((unsigned)(chunks < 2048 ? chunks : 2048)),
+                         dim3(256), 0, s, g, T, dim, L);
   }
   int sw = 1;
   while (sw < dim && sw < 32) sw <<= 1;
@@ -1590,6 +1833,20 @@ static void launch_long(const RowsGroup& g, int T, int dim, const RowsLong& L, c
                          s, g, T, dim, L, sg);
     else
       hipLaunchKernelGGL((rows_serial_plain_kernel<1, SGD, WB>), dim3((unsigned)db), dim3(1024), 0,
+                         s, g, T, dim, L, sg);
+  }
+  if (segs) {
+    const int64_t nsl16 = ceil_div(dim, 16);
+    int64_t sb2 = runs * nsl16;
+    if (sb2 > 1024) sb2 = 1024;
+    if (VEC == 4)
+      hipLaunchKernelGGL((rows_serial_seg_kernel<VEC, SGD, WB>), dim3((unsigned)sb2), dim3(1024), 0,
+                         s, g, T, dim, L, sg);
+    else if (aligned2 && dim % 2 == 0)
+      hipLaunchKernelGGL((rows_serial_seg_kernel<2, SGD, WB>), dim3((unsigned)sb2), dim3(1024), 0,
+                         s, g, T, dim, L, sg);
+    else
+      hipLaunchKernelGGL((rows_serial_seg_kernel<1, SGD, WB>), dim3((unsigned)sb2), dim3(1024), 0,
                          s, g, T, dim, L, sg);
   }
   if (N > L.smax) {

@@ -512,7 +512,7 @@ class _RowGroup(object):
             d.nnz = f.values.numel()
             d.combiner = COMBINERS[f.combiner]
         pend = _RowsPending(self, descs, tuple(keep), D, dev)
-        if pend.fusable():
+        if pend.fusable() or pend.launch_side():
             return [PendingRowSlices(pend, t, D) for t in range(T)]
         return pend.materialize()
 
@@ -522,6 +522,26 @@ _ROWS_RECORD = os.environ.get("DR_ROWS_RECORD", "1") != "0"
 
 # SGD applies of row-grouped backwards fused with the backward (A/B switch)
 _FUSED_SGD = os.environ.get("DR_ROWS_FUSED_SGD", "1") != "0"
+
+# Row-grouped backwards that are not fused into an SGD apply run on a side
+# stream, joined when their IndexedSlices are first used (A/B switch
+# DR_ROWS_SIDE_STREAM=0): the serial walk of a long run (DIN's padding id, a
+# popular category) keeps a few CUs for hundreds of microseconds, and the
+# lookups of one step (DIN's uid, target and history) then walk at once,
+# beside the dense backward, instead of one after another.
+_SIDE_STREAM = os.environ.get("DR_ROWS_SIDE_STREAM", "1") != "0"
+_SIDE_STREAMS = {}
+_N_SIDE = 4
+
+
+def _side_stream(dev):
+    pool = _SIDE_STREAMS.get(dev.index)
+    if pool is None:
+        pool = _SIDE_STREAMS[dev.index] = [[torch.cuda.Stream(device=dev)
+                                            for _ in range(_N_SIDE)], 0]
+    s = pool[0][pool[1] % _N_SIDE]
+    pool[1] += 1
+    return s
 
 
 class _RowsPending(object):
@@ -536,22 +556,50 @@ class _RowsPending(object):
         self.evs = [f.params for f in group.feats]
         self.slices = None
         self.applied = False
+        self.done = None   # side-stream launch: the event its consumer waits on
 
     def fusable(self):
-        if not _FUSED_SGD or self.slices is not None or self.applied or self.D % 4:
+        if (not _FUSED_SGD or self.slices is not None or self.applied or self.D % 4
+                or self.done is not None):
             return False
         if len({id(e) for e in self.evs}) != len(self.evs):
             return False          # one EV twice: sequential rounds, not one fused pass
         return all(d.top_grad % 16 == 0 and d.top_stride % 4 == 0 for d in self.descs)
 
     def materialize(self):
+        if self.done is not None:   # formed on a side stream: the consumer waits for it
+            torch.cuda.current_stream(self.dev).wait_event(self.done)
+            self.done = None
+            ops._post(self.dev)
         if self.slices is None:
             if self.applied:
                 raise RuntimeError("this gradient was already applied (fused SGD)")
             self.slices = self._form()
         return self.slices
 
-    def _form(self):
+    def launch_side(self):
+        """Form the IndexedSlices now on a side stream (after everything the
+        current stream has queued, the pooled gradient included); the first
+        use of any of them makes its stream wait for the result.  Every
+        buffer the launch touches is recorded on the side stream, so the
+        caching allocator does not hand it out again before the launch ends.
+        Not while a graph is being captured (an unjoined fork)."""
+        if (not _SIDE_STREAM or self.dev.type != "cuda" or self.slices is not None
+                or torch.cuda.is_current_stream_capturing()):
+            return False
+        main = torch.cuda.current_stream(self.dev)
+        side = _side_stream(self.dev)
+        side.wait_stream(main)
+        used = []
+        self.slices = self._form(side, used)
+        for t in used + [self.group.rowsel, self.group.vals] + list(self.keep):
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                t.record_stream(side)
+        self.done = torch.cuda.Event()
+        self.done.record(side)
+        return True
+
+    def _form(self, side=None, used=None):
         grp, dev, D = self.group, self.dev, self.D
         T = len(grp.feats)
         n = grp.koff[-1]
@@ -565,11 +613,14 @@ class _RowsPending(object):
         limit = max(lib().dr_ev_row_capacity(f.params.handle) for f in grp.feats)
         wsb = lib().dr_pool_grad_rows_workspace_size(n)
         ws = workspace(wsb, dev)
+        if used is not None:
+            used += [uniq, U, gptr, urows, gu, ws]
         check(lib().dr_pool_grad_rows_grouped_ex2(
             self.descs, T, grp.feats[0].batch, D, ptr(grp.rowsel), int(grp.rows_record),
             max(int(limit), 1), ptr(grp.vals), 1, ptr(uniq), ptr(urows), ptr(U), ptr(gptr),
-            ptr(gu), ptr(ws), wsb, stream_handle(dev)))
-        ops._post(dev)
+            ptr(gu), ptr(ws), wsb, side.cuda_stream if side is not None else stream_handle(dev)))
+        if side is None:
+            ops._post(dev)
         k = grp.koff
         return [IndexedSlices(None, uniq[k[t]:k[t + 1]], U[t:t + 1], True,
                               grad_ptr=gptr[k[t]:k[t + 1]], dim=D, keep=keep,

@@ -187,6 +187,149 @@ def _long_runs_case(dr, orc, D, walker):
     dr.status_check()
 
 
+def _repeated_terms(rng, n, D):
+    """n gradient rows in blocks of identical rows (lengths 1..259) whose
+    values stress the closed-form walk: normals over six decades, dyadic
+    integers (exact sums, rounding ties later), odd multiples of 2^(e-24)
+    (ties against sums of binade e), tiny and huge values, zeros of both
+    signs, and sign flips that drive the sum through zero."""
+    rows = np.empty((n, D), np.float32)
+    i = 0
+    prev = np.zeros(D, np.float32)
+    while i < n:
+        m = min(int(rng.integers(1, 260)), n - i)
+        kind = int(rng.integers(0, 8))
+        if kind == 0:
+            r = rng.standard_normal(D) * 10.0 ** rng.uniform(-3, 3)
+        elif kind == 1:
+            r = rng.integers(-64, 65, D) * 2.0 ** -12
+        elif kind == 2:
+            r = (2 * rng.integers(-40, 40, D) + 1) * 2.0 ** (rng.integers(-10, 10, D) - 24)
+        elif kind == 3:
+            r = rng.choice([1e-30, -1e-30, 0.0, -0.0, 1e6, -1e6], D)
+        elif kind == 4:
+            r = -prev * rng.integers(1, 4, D)
+        else:
+            r = rng.standard_normal(D).astype(np.float32)
+        prev = np.asarray(r, np.float32)
+        rows[i:i + m] = prev
+        i += m
+    return rows
+
+
+@pytest.mark.parametrize("seg", ["4096", "0"])
+@pytest.mark.parametrize("D", [18, 32, 1])
+def test_rows_backward_repeated_terms(dr, orc, D, seg, monkeypatch):
+    """Long runs whose terms come in blocks of identical rows (DIN's padding
+    id: every padded position of a sample carries that sample's his_sum
+    gradient).  With the segment scan on (DR_GRAD_SEG_SCAN=4096, opt-in) a
+    run of such blocks is walked one block at a time in closed form
+    (rows_serial_seg_kernel + rep_add); off (0, the default), position by
+    position.
+    Both bit-equal to the reference's serial sum; a long run without
+    repeats rides along (scanned, then walked plainly)."""
+    monkeypatch.setenv("DR_GRAD_SEG_SCAN", seg)
+    rng = np.random.default_rng(61 + D)
+    v = np.concatenate([np.zeros(60000, np.int64), np.ones(5000, np.int64),
+                        rng.integers(2, 300, 4000).astype(np.int64)])
+    rng.shuffle(v)
+    B = v.size
+    g = rng.standard_normal((B, 3 * D)).astype(np.float32)
+    pos0 = np.nonzero(v == 0)[0]
+    for f in range(3):
+        g[pos0, f * D:(f + 1) * D] = _repeated_terms(rng, pos0.size, D)
+    evs, sps = [], []
+    ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+    for f in range(3):
+        evs.append(dr.EmbeddingVariable("rrep_%d_%d_%s" % (D, f, seg), D, 0.1, capacity=1024))
+        sps.append(dr.SparseTensor(T(ind), T(v), (B, 1)))
+    out = dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum")
+    out.backward(T(g))
+    uids, idx = orc.unique(v)
+    segs = np.arange(B, dtype=np.int32)
+    for f in range(3):
+        sl = evs[f].pending_grads.pop()
+        U = int(sl.num_valid.item())
+        assert H(sl.indices[:U]).tolist() == uids.tolist()
+        gf = np.ascontiguousarray(g[:, f * D:(f + 1) * D])
+        ref = orc.sparse_segment_reduce_grad(gf, idx, segs, U, "sum")
+        np.testing.assert_array_equal(H(sl.values[:U]).view(np.uint32), ref.view(np.uint32))
+    dr.status_check()
+
+
+def test_rows_sgd_repeated_terms_seg_equals_plain(dr, monkeypatch):
+    """The fused SGD backward (dr_ev_pool_grad_rows_apply_sgd, 16-B rows)
+    over blocks of repeated terms: the segment walk and the plain walk leave
+    bit-identical EVs after two steps."""
+    rng = np.random.default_rng(67)
+    D, B = 32, 40000
+    v = np.concatenate([np.zeros(36000, np.int64), rng.integers(1, 200, B - 36000)])
+    rng.shuffle(v)
+    gs = []
+    for _ in range(2):
+        g = rng.standard_normal((B, D)).astype(np.float32)
+        g[np.nonzero(v == 0)[0]] = _repeated_terms(rng, int((v == 0).sum()), D)
+        gs.append(g)
+    ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+    res = []
+    for seg in ("4096", "0"):
+        monkeypatch.setenv("DR_GRAD_SEG_SCAN", seg)
+        ev = dr.EmbeddingVariable("rrep_sgd_%s" % seg, D, 0.1, capacity=1024)
+        opt = dr.GradientDescentOptimizer(0.05)
+        for step, g in enumerate(gs):
+            out = dr.embedding_lookup_sparse(ev, dr.SparseTensor(T(ind), T(v), (B, 1)),
+                                             combiner="sum")
+            out.backward(T(g))
+            opt.apply_gradients([ev], global_step=step)
+        torch.cuda.synchronize()
+        res.append(_export(ev))
+    (k1, v1), (k2, v2) = res
+    np.testing.assert_array_equal(k1, k2)
+    np.testing.assert_array_equal(v1.view(np.uint32), v2.view(np.uint32))
+
+
+@pytest.mark.parametrize("side", [True, False])
+def test_rows_backward_side_stream(dr, orc, side, monkeypatch):
+    """Row-grouped backwards not fused into an SGD apply run on a side stream
+    (DR_ROWS_SIDE_STREAM, default on), joined when their slices are first
+    read: three separate lookups with long runs (D = 18, so no fused SGD),
+    their backwards in flight together, the top gradient dropped and the
+    allocator churned on the main stream before the slices are read --
+    bit-equal to the reference's serial sums either way."""
+    from deeprec_amd import embedding_ops
+    monkeypatch.setattr(embedding_ops, "_SIDE_STREAM", side)
+    rng = np.random.default_rng(43)
+    D = 18
+    runs = {0: 30000, 1: 257, 2: 9000, 3: 65536}
+    v = np.concatenate([np.full(n, k, np.int64) for k, n in runs.items()] +
+                       [rng.integers(4, 300, 5000).astype(np.int64)])
+    rng.shuffle(v)
+    B = v.size
+    evs, outs = [], []
+    ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+    for f in range(3):
+        ev = dr.EmbeddingVariable("rside_%d_%d" % (f, side), D, 0.1, capacity=1024)
+        evs.append(ev)
+        outs.append(dr.embedding_lookup_sparse(ev, dr.SparseTensor(T(ind), T(v), (B, 1)),
+                                               combiner="sum"))
+    g = rng.standard_normal((B, 3 * D)).astype(np.float32)
+    gt = T(g)
+    torch.cat(outs, 1).backward(gt)
+    del gt, outs
+    for _ in range(4):   # main-stream allocations that would reuse freed buffers
+        torch.full((B, 3 * D), float("nan"), device="cuda").mul_(2.0)
+    uids, idx = orc.unique(v)
+    seg = np.arange(B, dtype=np.int32)
+    for f in range(3):
+        sl = evs[f].pending_grads.pop()
+        U = int(sl.num_valid.item())
+        assert H(sl.indices[:U]).tolist() == uids.tolist()
+        gf = np.ascontiguousarray(g[:, f * D:(f + 1) * D])
+        ref = orc.sparse_segment_reduce_grad(gf, idx, seg, U, "sum")
+        np.testing.assert_array_equal(H(sl.values[:U]), ref)
+    dr.status_check()
+
+
 @pytest.mark.parametrize("D", [18, 32])
 def test_rows_backward_long_runs_zero_terms(dr, orc, D):
     """Long runs whose terms are mostly exact zeros (a padding id whose
