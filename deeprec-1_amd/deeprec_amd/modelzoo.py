@@ -989,12 +989,29 @@ class DIN(torch.nn.Module):
     # DR_DIN_FUSED_ATTENTION=0 = din_all + library GEMMs + elementwise sigmoids
     fused_attention = os.environ.get("DR_DIN_FUSED_ATTENTION", "1") != "0"
 
+    # the target item and the history in ONE lookup of the mid / cat EVs
+    # (A/B switch DR_DIN_ONE_ITEM_LOOKUP=0: two lookups): each EV then gets
+    # one gradient whose per-id sums are single serial chains in the order
+    # [target positions, history positions] -- the reference's two
+    # embedding_lookup gradients concatenated and summed per id by the
+    # optimizer's unsorted_segment_sum (optimizer.py _deduplicate_indexed_
+    # slices) -- instead of two per-lookup sums added afterwards (a
+    # different rounding, and a unique + sort + segment-sum pass per step)
+    one_item_lookup = os.environ.get("DR_DIN_ONE_ITEM_LOOKUP", "1") != "0"
+
     def forward(self, uids, mids, cats, mid_his, cat_his, mask):
         B, T = mid_his.shape
         uid_e = self.uid_lookup(uids.reshape(1, B))
-        item_eb = self.item_lookup(torch.stack([mids, cats]))                    # [B, 2D]
-        his = torch.stack([mid_his.reshape(-1), cat_his.reshape(-1)])
-        facts = self.item_lookup(his).view(B, T, -1)                              # [B, T, 2D]
+        if self.one_item_lookup:
+            ids = torch.stack([torch.cat([mids, mid_his.reshape(-1)]),
+                               torch.cat([cats, cat_his.reshape(-1)])])
+            allv = self.item_lookup(ids)                                           # [B + B T, 2D]
+            item_eb = allv[:B]                                                     # [B, 2D]
+            facts = allv[B:].view(B, T, -1)                                        # [B, T, 2D]
+        else:
+            item_eb = self.item_lookup(torch.stack([mids, cats]))                 # [B, 2D]
+            his = torch.stack([mid_his.reshape(-1), cat_his.reshape(-1)])
+            facts = self.item_lookup(his).view(B, T, -1)                           # [B, T, 2D]
         if self.fused_attention and facts.shape[2] in ops.DIN_MLP_HIDDEN:
             att, his_sum = DinAttentionFused.apply(
                 item_eb, facts, mask, self.f1_att.weight, self.f1_att.bias, self.f2_att.weight,
