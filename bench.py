@@ -500,7 +500,11 @@ def din_leg(args, dev, log, world, rank, dist, staged):
         evs.append(ev)
     torch.manual_seed(0)
     model = mz.DIN(*evs).to(dev)
-    dopt = torch.optim.Adam(model.parameters(), lr=0.001)
+    # one GPU: the step as hipGraphs (one per batch shape) when --model-graph;
+    # capturable dense Adam (step counts on the device), KV Adam's beta powers
+    # in HBM (training.AdamOptimizer._device_powers)
+    use_graph = world == 1 and getattr(args, "model_graph", True)
+    dopt = torch.optim.Adam(model.parameters(), lr=0.001, capturable=use_graph)
     eopt = dr.AdamOptimizer(0.001)
     g = torch.Generator(device=dev)
     g.manual_seed(2021 + 7919 * rank)
@@ -521,16 +525,41 @@ def din_leg(args, dev, log, world, rank, dist, staged):
         return mz.din_train_step(model, batches[i % 4], dopt, eopt, i, world=world,
                                  staged=staged)
 
-    for i in range(2):
+    for i in range(4 if use_graph else 2):   # graphs: every batch shape once first
         dstep(i)
     torch.cuda.synchronize()
     dr.status_check(dev)
+    graphs, graph_err, eager_ms = None, None, None
+    if use_graph:
+        t0 = time.perf_counter()
+        for i in range(4, 4 + args.din_steps):
+            dstep(i)
+        torch.cuda.synchronize()
+        eager_ms = (time.perf_counter() - t0) / args.din_steps * 1e3
+        try:
+            graphs = []
+            pool = torch.cuda.graph_pool_handle()
+            for j in range(4):
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr, pool=pool):
+                    dstep(j)
+                graphs.append(gr)
+            for gr in graphs:
+                gr.replay()
+            torch.cuda.synchronize()
+            dr.status_check(dev)
+        except Exception as e:   # report the eager step instead
+            graphs, graph_err = None, "%s: %s" % (type(e).__name__, str(e)[:200])
+            torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.din_steps):
-        dstep(i)
+        if graphs is not None:
+            graphs[i % 4].replay()
+        else:
+            dstep(i)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -546,7 +575,12 @@ def din_leg(args, dev, log, world, rank, dist, staged):
                                          "(dense all-reduce + EV gradient slices gathered)"
                                          if world > 1 else "one GPU"),
            "n_gpus": world, "ms_per_step": round(ms, 4), "global_batch": world * B,
-           "samples_per_s": round(world * B / (ms * 1e-3), 1), "steps": args.din_steps}
+           "samples_per_s": round(world * B / (ms * 1e-3), 1), "steps": args.din_steps,
+           "hipgraph": graphs is not None}
+    if eager_ms is not None:
+        res["ms_per_step_eager"] = round(eager_ms, 4)
+    if graph_err:
+        res["graph_error"] = graph_err
     log("din leg: %s" % json.dumps(res))
     return res
 

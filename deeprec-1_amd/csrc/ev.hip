@@ -917,9 +917,10 @@ __global__ __launch_bounds__(256) void ev_apply_kernel(ApplyGroup ag, int64_t di
                                                        OptScalars sc_arg, int gind, int* st) {
   const ApplyTable& at = ag.t[blockIdx.y];
   OptScalars sc = sc_arg;
-  if (OPT == OPT_ADAM_ASYNC && at.powers) {
+  if ((OPT == OPT_ADAM_ASYNC || OPT == OPT_ADAM) && at.powers) {
     // alpha = lr * sqrt(1 - beta2_power) / (1 - beta1_power) in T = float
-    // (training_ali_ops.cc:1529-1531), from the powers as they stand
+    // (training_ali_ops.cc:1529-1531; Adam :935-937), from the powers as they
+    // stand in HBM
     const float b1p = gld(at.powers), b2p = gld(at.powers + 1);
     sc.alpha = sc.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
   }
@@ -1621,7 +1622,7 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
                          OptScalars sc, const float* const* grads, const int64_t* const* keys,
                          const int64_t* n_host, const int64_t* const* n_dev, int64_t gs,
                          hipStream_t st, int gind = 0, const int64_t* const* rows = nullptr,
-                         float* const* powers = nullptr) {
+                         float* const* powers = nullptr, bool advance_powers = true) {
   EvGuard guard_(vars, T);
   DR_REQUIRE(!rows || opt == OPT_SGD, DR_INVALID_ARGUMENT,
              "known rows skip the slot-column first-touch check: SGD only");
@@ -1739,7 +1740,7 @@ static int apply_grouped(int opt, dr_ev* const* vars, dr_ev* const* s1, dr_ev* c
 #undef DR_APPLY
     DR_LAUNCH_CHECK();
   }
-  if (powers) {
+  if (powers && advance_powers) {
     for (int c0 = 0; c0 < T; c0 += DR_MAX_GROUP) {
       const int tn = std::min(DR_MAX_GROUP, T - c0);
       PowersArgs pa;
@@ -3273,6 +3274,27 @@ int dr_ev_apply_adam_async_grouped(int rmsprop, int by_address, dr_ev* const* va
                        reinterpret_cast<const float* const*>(grads), keys, n_host, n_dev,
                        global_step, S(stream), by_address ? 1 : 0, nullptr,
                        rmsprop ? nullptr : powers);
+}
+
+int dr_ev_apply_adam_grouped_dev(int by_address, dr_ev* const* vars, dr_ev* const* m,
+                                 dr_ev* const* v, int num_tables, const void* const* grads,
+                                 const int64_t* const* keys, const int64_t* n_host,
+                                 const int64_t* const* n_dev, const float* powers, float lr,
+                                 float beta1, float beta2, float epsilon, int64_t global_step,
+                                 void* stream) {
+  using namespace dr;
+  DR_REQUIRE(grads && powers && ((uintptr_t)powers & 3) == 0 && num_tables >= 1,
+             DR_INVALID_ARGUMENT, "bad argument (powers: a device float[2])");
+  DR_REQUIRE(num_tables <= 4096, DR_INVALID_ARGUMENT, "too many tables");
+  int opt;
+  OptScalars sc;
+  int rc = grouped_opt(DR_OPT_ADAM, lr, 0.f, 0.f, beta1, beta2, epsilon, &opt, &sc);
+  if (rc) return rc;
+  float* pw[4096];
+  for (int t = 0; t < num_tables; ++t) pw[t] = const_cast<float*>(powers);
+  return apply_grouped(opt, vars, m, v, num_tables, sc,
+                       reinterpret_cast<const float* const*>(grads), keys, n_host, n_dev,
+                       global_step, S(stream), by_address ? 1 : 0, nullptr, pw, false);
 }
 
 int dr_ev_apply_grouped_ptr(int optimizer, dr_ev* const* vars, dr_ev* const* slot1,

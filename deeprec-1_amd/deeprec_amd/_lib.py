@@ -205,6 +205,8 @@ SIGNATURES = {
                                                  _P, _SZ, _P]),
     "dr_ev_apply_adam_async_grouped": (_I32, [_I32, _I32, _P, _P, _P, _I32, _P, _P, _P, _P, _P,
                                               _F32, _F32, _F32, _F32, _I64, _P]),
+    "dr_ev_apply_adam_grouped_dev": (_I32, [_I32, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _F32,
+                                            _F32, _F32, _F32, _I64, _P]),
     "dr_ev_apply_adagrad_decay_grouped": (_I32, [_P, _P, _P, _I32, _P, _I32, _P, _P, _P, _F32,
                                                  _I64, _F32, _F32, _I64, _P]),
     "dr_ev_apply_ftrl_grouped_ptr": (_I32, [_P, _P, _P, _I32, _P, _P, _P, _P, _F32, _F32, _F32,

@@ -66,6 +66,9 @@ def _rounds(slices):
 # SGD applies of row-grouped backwards use the forward's rows (A/B switch)
 _KNOWN_ROWS = os.environ.get("DR_APPLY_PROBE") != "1"
 
+# KV Adam with its beta powers in HBM (A/B switch DR_KV_ADAM_DEVICE_POWERS=0)
+_ADAM_DEVICE_POWERS = os.environ.get("DR_KV_ADAM_DEVICE_POWERS", "1") != "0"
+
 
 def _grad_rows(grp, fn_name):
     """The gradient argument of a grouped EV apply: by address when every
@@ -263,6 +266,7 @@ class AdamOptimizer(_Optimizer):
         self._dense_mv = {}
         self.b1p = torch.tensor(self.beta1, dtype=torch.float32).item()
         self.b2p = torch.tensor(self.beta2, dtype=torch.float32).item()
+        self._pw = {}   # device -> (float[2] beta powers in HBM, float[2] betas)
 
     def _slots(self, var):
         return var.slot("Adam", 0.0), var.slot("Adam_1", 0.0)
@@ -270,10 +274,54 @@ class AdamOptimizer(_Optimizer):
     def _scalars(self):
         return (self.b1p, self.b2p, self.beta1, self.beta2, self.eps)
 
+    def _device_powers(self, dev):
+        """The beta powers as a device float[2] (created from the host values
+        on first use -- before any graph capture), advanced in _finish by an
+        fp32 multiply on the device: the same roundings as the host values,
+        and no per-step host scalar in the EV apply (capturable)."""
+        key = str(dev)
+        if key not in self._pw:
+            self._pw[key] = (torch.tensor([self.b1p, self.b2p], dtype=torch.float32, device=dev),
+                             torch.tensor([self.beta1, self.beta2], dtype=torch.float32,
+                                          device=dev))
+        return self._pw[key][0]
+
+    def _apply_ev_batch(self, items, gs):
+        """dr_ev_apply_adam_grouped_dev per (device, dim, dtype) group: alpha
+        formed in the kernel from the HBM beta powers (A/B switch
+        DR_KV_ADAM_DEVICE_POWERS=0: host powers, dr_ev_apply_grouped)."""
+        if not _ADAM_DEVICE_POWERS:
+            return _Optimizer._apply_ev_batch(self, items, gs)
+        import ctypes as C
+        groups = {}
+        for var, sl in items:
+            groups.setdefault((str(var.device), var.dim, var.value_dtype), []).append((var, sl))
+        for grp in groups.values():
+            T = len(grp)
+            dev = grp[0][0].device
+            by_addr = all(sl.grad_ptr is not None and sl._values is None for _, sl in grp)
+            grads = [sl.grad_ptr if by_addr else sl.values.contiguous() for _, sl in grp]
+            idxs = [sl.indices.contiguous() for _, sl in grp]
+            slots = [self._slots(var) for var, _ in grp]
+            pw = self._device_powers(dev)
+            P = C.c_void_p * T
+            st = stream_handle(dev)
+            with _Locked(self.use_locking, [var.handle.value for var, _ in grp], st):
+                check(lib().dr_ev_apply_adam_grouped_dev(
+                    int(by_addr), P(*[var.handle.value for var, _ in grp]),
+                    P(*[a.handle.value for a, _ in slots]), P(*[b.handle.value for _, b in slots]),
+                    T, P(*[g.data_ptr() for g in grads]), P(*[i.data_ptr() for i in idxs]),
+                    (C.c_int64 * T)(*[i.numel() for i in idxs]),
+                    P(*[ptr(sl.num_valid) for _, sl in grp]), pw.data_ptr(), self.lr, self.beta1,
+                    self.beta2, self.eps, gs, st))
+            ops._post(dev)
+
     def _finish(self):
         f32 = lambda x: torch.tensor(x, dtype=torch.float32)
         self.b1p = (f32(self.b1p) * f32(self.beta1)).item()
         self.b2p = (f32(self.b2p) * f32(self.beta2)).item()
+        for pw, betas in self._pw.values():   # the device copies, on their streams
+            pw.mul_(betas)
 
     def _dense_update(self, var, idx, g):
         """_apply_sparse_shared (adam.py:183-207) on a dense table: m and v

@@ -617,6 +617,21 @@ int dr_ev_apply_adam_async_grouped(int rmsprop, int by_address, dr_ev* const* va
                                    const int64_t* n_host, const int64_t* const* n_dev,
                                    float* const* powers, float lr, float beta1, float beta2,
                                    float epsilon, int64_t global_step, void* stream);
+/* KvSparseApplyAdam (training_ali_ops.cc:848-975) with the beta powers     */
+/* read from HBM: powers is ONE device float[2] {beta1_power, beta2_power}   */
+/* shared by the tables (the optimizer's non-slot variables, adam.py          */
+/* _create_slots); every table's kernel forms alpha = lr sqrt(1 - b2p) /     */
+/* (1 - b1p) in float from it, as dr_ev_apply_grouped does on the host.      */
+/* The powers are NOT advanced here (the optimizer's _finish does it once    */
+/* per apply_gradients, after every table): with no host scalar that        */
+/* changes per step, the apply can sit in a captured hipGraph.  grads[t]: a  */
+/* [n, dim] float block, or (by_address) uint64 row addresses.               */
+int dr_ev_apply_adam_grouped_dev(int by_address, dr_ev* const* vars, dr_ev* const* m,
+                                 dr_ev* const* v, int num_tables, const void* const* grads,
+                                 const int64_t* const* keys, const int64_t* n_host,
+                                 const int64_t* const* n_dev, const float* powers, float lr,
+                                 float beta1, float beta2, float epsilon, int64_t global_step,
+                                 void* stream);
 /* KvResourceSparseApplyAdagradDecay (training_ali_ops.cc:703-823; op def    */
 /* core/ops/training_ali_ops.cc): accum and accum_decay_power are slot EVs   */
 /* of var (var-shaped; the decay count is element 0 of a row, as the         */

@@ -1,0 +1,128 @@
+"""The DIN training step (BASELINE configs[3] shape, tools/model_step.py din)
+captured as hipGraphs, one per batch (the history length differs per batch):
+two identical models from the same seeds, A stepped eagerly, B by graph
+replays after the same warmup; losses, dense parameters and EV contents
+compared bit for bit after every step, then both timed.
+
+usage: python tools/din_graph_probe.py [--steps 20]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "deeprec-1_amd"))
+
+
+def build(dr, mz, dev, tag, B, T, D, R):
+    evs = []
+    for i, r in enumerate(R):
+        ev = dr.EmbeddingVariable("dgp_%s%d" % (tag, i), D, 0.0, capacity=r + (1 << 16), device=dev)
+        ev.insert_synthetic(0, r, seed=700 + i)
+        evs.append(ev)
+    torch.manual_seed(11)
+    model = mz.DIN(*evs).to(dev)
+    dopt = torch.optim.Adam(model.parameters(), lr=0.001, capturable=True)
+    eopt = dr.AdamOptimizer(0.001)
+    return evs, model, dopt, eopt
+
+
+def batches_for(dev, B, T, R):
+    g = torch.Generator(device=dev)
+    g.manual_seed(2021)
+    out = []
+    for _ in range(4):
+        lens = torch.randint(1, T + 1, (B,), generator=g, device=dev)
+        Tb = int(lens.max())
+        mask = (torch.arange(Tb, device=dev)[None, :] < lens[:, None]).float()
+        mh = torch.randint(1, R[1], (B, Tb), generator=g, device=dev) * mask.long()
+        ch = torch.randint(1, R[2], (B, Tb), generator=g, device=dev) * mask.long()
+        lab = (torch.rand(B, generator=g, device=dev) > 0.5).long()
+        out.append((torch.randint(0, R[0], (B,), generator=g, device=dev),
+                    torch.randint(0, R[1], (B,), generator=g, device=dev),
+                    torch.randint(0, R[2], (B,), generator=g, device=dev), mh, ch, mask,
+                    torch.stack([lab, 1 - lab], 1).float()))
+    return out
+
+
+def snapshot(model, evs):
+    ps = [p.detach().clone() for p in model.parameters()]
+    es = []
+    for ev in evs:
+        k, v = ev.export()[:2]
+        o = torch.argsort(k)
+        es.append((k[o].clone(), v[o].clone()))
+    return ps, es
+
+
+def same(a, b):
+    (pa, ea), (pb, eb) = a, b
+    ok = all(torch.equal(x.view(torch.int32), y.view(torch.int32)) for x, y in zip(pa, pb))
+    for (ka, va), (kb, vb) in zip(ea, eb):
+        ok = ok and torch.equal(ka, kb) and torch.equal(va.view(torch.int32), vb.view(torch.int32))
+    return ok
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=4096)
+    args = ap.parse_args()
+    import deeprec_amd as dr
+    from deeprec_amd import modelzoo as mz
+    dr.load()
+    dev = torch.device("cuda:0")
+    B, T, D = args.batch, 100, 18
+    R = (500_000, 400_000, 2_000)
+    bat = batches_for(dev, B, T, R)
+    A = build(dr, mz, dev, "a", B, T, D, R)
+    Bm = build(dr, mz, dev, "b", B, T, D, R)
+    warm = 4   # every batch once: per-shape caches, slots, device beta powers
+    for m in (A, Bm):
+        evs, model, dopt, eopt = m
+        for i in range(warm):
+            mz.din_train_step(model, bat[i % 4], dopt, eopt, i)
+    torch.cuda.synchronize()
+    assert same(snapshot(A[1], A[0]), snapshot(Bm[1], Bm[0])), "warmup diverged"
+    evs, model, dopt, eopt = Bm
+    graphs = []
+    pool = torch.cuda.graph_pool_handle()
+    for j in range(4):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=pool):
+            loss = mz.din_train_step(model, bat[(warm + j) % 4], dopt, eopt, warm + j)
+        graphs.append((g, loss))
+    torch.cuda.synchronize()
+    print("captured 4 graphs", flush=True)
+    equal = True
+    for i in range(warm, warm + args.steps):
+        la = mz.din_train_step(A[1], bat[i % 4], A[2], A[3], i)
+        g, lb = graphs[(i - warm) % 4]
+        g.replay()
+        torch.cuda.synchronize()
+        ok = torch.equal(la.view(torch.int32), lb.view(torch.int32)) and \
+            same(snapshot(A[1], A[0]), snapshot(model, evs))
+        equal = equal and ok
+        if not ok:
+            print("step %d differs: loss %r vs %r" % (i, float(la), float(lb)), flush=True)
+            break
+    print("eager == graph over %d steps: %s" % (args.steps, equal), flush=True)
+    n = args.steps
+    for name, fn in (("eager", lambda i: mz.din_train_step(A[1], bat[i % 4], A[2], A[3], i)),
+                     ("graph", lambda i: graphs[i % 4][0].replay())):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(n):
+            fn(i)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / n * 1e3
+        print(json.dumps({"din_step": name, "ms_per_step": round(ms, 3), "batch": B,
+                          "samples_per_s": round(B / ms * 1e3, 1)}), flush=True)
+    dr.status_check(dev)
+
+
+if __name__ == "__main__":
+    main()
