@@ -537,6 +537,9 @@ def din_leg(args, dev, log, world, rank, dist, staged):
         torch.cuda.synchronize()
         eager_ms = (time.perf_counter() - t0) / args.din_steps * 1e3
         try:
+            for ev in evs:   # a captured resolve must not be able to outgrow the table
+                ev.reserve(8 * B * (T + 1))   # 4 graphs x (lookup + apply) adds, counted conservatively
+            torch.cuda.synchronize()
             graphs = []
             pool = torch.cuda.graph_pool_handle()
             for j in range(4):

@@ -102,7 +102,9 @@ def _train(dr, fused, tag, batches, D, combiner, lr=0.05, dtype=torch.float32, s
                 out = dr.embedding_lookup_sparse_multi(evs, st, combiner=combiner)
             out.backward(T(g[:, :out.shape[1]]))
             pend = [e.pending_grads[-1] for e in evs]
-            assert all(isinstance(p, PendingRowSlices) for p in pend) == fused
+            # (unfused: formed eagerly, or launched on a side stream -- a
+            # PendingRowSlices that is no longer fusable)
+            assert all(isinstance(p, PendingRowSlices) and p.fusable() for p in pend) == fused
             opt.apply_gradients(evs, global_step=10 + step)
             if fused:   # ran fused: the IndexedSlices were never formed
                 assert all(p._pending.applied and "indices" not in p.__dict__ for p in pend)

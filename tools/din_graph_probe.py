@@ -58,11 +58,28 @@ def snapshot(model, evs):
     return ps, es
 
 
-def same(a, b):
+def same(a, b, names=None, report=False):
     (pa, ea), (pb, eb) = a, b
-    ok = all(torch.equal(x.view(torch.int32), y.view(torch.int32)) for x, y in zip(pa, pb))
-    for (ka, va), (kb, vb) in zip(ea, eb):
-        ok = ok and torch.equal(ka, kb) and torch.equal(va.view(torch.int32), vb.view(torch.int32))
+    ok = True
+    for n, (x, y) in enumerate(zip(pa, pb)):
+        if not torch.equal(x.view(torch.int32), y.view(torch.int32)):
+            ok = False
+            if report:
+                d = (x - y).abs()
+                print("  param %s differs: %d elements, max |diff| %.3g (max |x| %.3g)"
+                      % (names[n] if names else n, int((d > 0).sum()), float(d.max()),
+                         float(x.abs().max())), flush=True)
+    for t, ((ka, va), (kb, vb)) in enumerate(zip(ea, eb)):
+        if not (torch.equal(ka, kb) and torch.equal(va.view(torch.int32), vb.view(torch.int32))):
+            ok = False
+            if report:
+                if torch.equal(ka, kb):
+                    d = (va - vb).abs()
+                    print("  EV %d differs: %d rows, max |diff| %.3g" % (
+                        t, int((d.amax(1) > 0).sum()), float(d.max())), flush=True)
+                else:
+                    print("  EV %d key sets differ (%d vs %d)" % (t, ka.numel(), kb.numel()),
+                          flush=True)
     return ok
 
 
@@ -87,7 +104,12 @@ def main():
             mz.din_train_step(model, bat[i % 4], dopt, eopt, i)
     torch.cuda.synchronize()
     assert same(snapshot(A[1], A[0]), snapshot(Bm[1], Bm[0])), "warmup diverged"
+    for ev in A[0]:   # the eager twin grows its tables the same way
+        ev.reserve(8 * B * (T + 1))
     evs, model, dopt, eopt = Bm
+    for ev in evs:   # a captured resolve must not be able to outgrow the table
+        ev.reserve(8 * B * (T + 1))   # 4 graphs x (lookup + apply) adds, counted conservatively
+    torch.cuda.synchronize()
     graphs = []
     pool = torch.cuda.graph_pool_handle()
     for j in range(4):
@@ -103,11 +125,13 @@ def main():
         g, lb = graphs[(i - warm) % 4]
         g.replay()
         torch.cuda.synchronize()
-        ok = torch.equal(la.view(torch.int32), lb.view(torch.int32)) and \
-            same(snapshot(A[1], A[0]), snapshot(model, evs))
+        okl = torch.equal(la.view(torch.int32), lb.view(torch.int32))
+        names = [n for n, _ in model.named_parameters()]
+        ok = same(snapshot(A[1], A[0]), snapshot(model, evs), names, report=True) and okl
         equal = equal and ok
         if not ok:
-            print("step %d differs: loss %r vs %r" % (i, float(la), float(lb)), flush=True)
+            print("step %d differs: loss %r vs %r" % (i, float(la.detach()), float(lb.detach())),
+                  flush=True)
             break
     print("eager == graph over %d steps: %s" % (args.steps, equal), flush=True)
     n = args.steps
