@@ -27,6 +27,16 @@ def build(dr, mz, dev, tag, B, T, D, R):
     model = mz.DIN(*evs).to(dev)
     dopt = torch.optim.Adam(model.parameters(), lr=0.001, capturable=True)
     eopt = dr.AdamOptimizer(0.001)
+    skip = os.environ.get("DGP_SKIP", "")   # bisection: "ev" / "dense" updates left out
+    if skip == "ev":
+        def drop(var_list, global_step=None):
+            for v in var_list:
+                for sl in v.pending_grads:
+                    getattr(sl, "indices", None)   # formed, then dropped
+                v.pending_grads = []
+        eopt.apply_gradients = drop
+    elif skip == "dense":
+        dopt.step = lambda *a, **k: None
     return evs, model, dopt, eopt
 
 
@@ -111,18 +121,24 @@ def main():
         ev.reserve(8 * B * (T + 1))   # 4 graphs x (lookup + apply) adds, counted conservatively
     torch.cuda.synchronize()
     graphs = []
-    pool = torch.cuda.graph_pool_handle()
-    for j in range(4):
+    shared = os.environ.get("DGP_SHARED_POOL", "0") == "1"
+    pool = torch.cuda.graph_pool_handle() if shared else None
+    # capture order (DGP_ORDER, e.g. "1,0,3,2"): graph k replays batch order[k]
+    order = [int(x) for x in os.environ.get("DGP_ORDER", "0,1,2,3").split(",")]
+    for j in order:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=pool):
-            loss = mz.din_train_step(model, bat[(warm + j) % 4], dopt, eopt, warm + j)
+            loss = mz.din_train_step(model, bat[j], dopt, eopt, warm + j)
         graphs.append((g, loss))
     torch.cuda.synchronize()
-    print("captured 4 graphs", flush=True)
+    print("captured %d graphs, batch order %s, skip %r, powers %s" % (
+        len(order), order, os.environ.get("DGP_SKIP", ""), list(eopt._pw.keys())), flush=True)
     equal = True
     for i in range(warm, warm + args.steps):
-        la = mz.din_train_step(A[1], bat[i % 4], A[2], A[3], i)
-        g, lb = graphs[(i - warm) % 4]
+        k = (i - warm) % len(order)
+        la = mz.din_train_step(A[1], bat[order[k]], A[2], A[3], warm + order[k])
+        g, lb = graphs[k]
+        print("step %d: graph %d (batch %d)" % (i, k, order[k]), flush=True)
         g.replay()
         torch.cuda.synchronize()
         okl = torch.equal(la.view(torch.int32), lb.view(torch.int32))
@@ -135,8 +151,9 @@ def main():
             break
     print("eager == graph over %d steps: %s" % (args.steps, equal), flush=True)
     n = args.steps
-    for name, fn in (("eager", lambda i: mz.din_train_step(A[1], bat[i % 4], A[2], A[3], i)),
-                     ("graph", lambda i: graphs[i % 4][0].replay())):
+    for name, fn in (("eager", lambda i: mz.din_train_step(A[1], bat[order[i % len(order)]],
+                                                           A[2], A[3], i)),
+                     ("graph", lambda i: graphs[i % len(order)][0].replay())):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(n):
