@@ -51,8 +51,22 @@ def main():
             ev.pending_grads = []
         return (loss, model.f1_att.weight.grad, model.dnn1.weight.grad)
 
-    for name, fn in (("lookups", lookups), ("attention", attention), ("forward", full),
-                     ("forward+backward", loss_bwd)):
+    sgd = torch.optim.SGD(model.parameters(), lr=0.01)
+
+    def with_opt(opt):
+        def f():
+            out = loss_bwd()
+            opt.step()
+            return out
+        return f
+
+    pieces = (("lookups", lookups), ("attention", attention), ("forward", full),
+              ("forward+backward", loss_bwd), ("+ dense SGD", with_opt(sgd)),
+              ("+ dense Adam", with_opt(dopt)))
+    only = os.environ.get("DFP_ONLY")
+    for name, fn in pieces:
+        if only and name not in only.split(","):
+            continue
         for _ in range(2):
             fn()
         for ev in evs:
@@ -75,7 +89,25 @@ def main():
             graphs[k].replay()
             torch.cuda.synchronize()
             res.append(all(torch.equal(a.detach(), b) for a, b in zip(outs[k], want)))
-        print("%-18s graph replays equal eager: %s" % (name, res), flush=True)
+        # then the state moves (in place, eagerly) and the graphs replay again
+        with torch.no_grad():
+            for prm in model.parameters():
+                prm.mul_(1.01)
+            for ev in evs:
+                k_, v_ = ev.export()[:2]
+                ev.insert(k_, v_ * 1.01)
+        for ev in evs:   # (insert counts as adds: headroom again for the next capture)
+            ev.reserve(8 * B * (T + 1))
+        torch.cuda.synchronize()
+        want2 = [t.detach().clone() for t in fn()]
+        for ev in evs:
+            ev.pending_grads = []
+        for k in range(2):
+            graphs[k].replay()
+            torch.cuda.synchronize()
+            res.append(all(torch.equal(a.detach(), b) for a, b in zip(outs[k], want2)))
+        print("%-18s graph replays equal eager (before / after a state change): %s"
+              % (name, res), flush=True)
     dr.status_check(dev)
 
 

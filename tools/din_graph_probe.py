@@ -125,17 +125,46 @@ def main():
     pool = torch.cuda.graph_pool_handle() if shared else None
     # capture order (DGP_ORDER, e.g. "1,0,3,2"): graph k replays batch order[k]
     order = [int(x) for x in os.environ.get("DGP_ORDER", "0,1,2,3").split(",")]
-    for j in order:
+    # DGP_ZERO_OUTSIDE=1: zero_grad(set_to_none) before each capture and a
+    # no-op inside it (torch's documented whole-network pattern)
+    zero_out = os.environ.get("DGP_ZERO_OUTSIDE", "0") == "1"
+    real_zero = dopt.zero_grad
+    if os.environ.get("DGP_CAPTURE_ONLY") == "1":
+        # kernels that run while a capture is open ran eagerly, not into the
+        # graph: a kernel trace of this window shows them (gaps mark it)
+        torch.cuda.synchronize()
+        time.sleep(0.3)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=pool):
+            mz.din_train_step(model, bat[order[0]], dopt, eopt, warm)
+        torch.cuda.synchronize()
+        time.sleep(0.3)
+        print("captured one graph (capture-only mode)", flush=True)
+        return
+    for j in order:
+        g = torch.cuda.CUDAGraph()
+        if zero_out:
+            real_zero(set_to_none=True)
+            dopt.zero_grad = lambda *a, **k: None
+        with torch.cuda.graph(g, pool=pool):
             loss = mz.din_train_step(model, bat[j], dopt, eopt, warm + j)
+        dopt.zero_grad = real_zero
         graphs.append((g, loss))
     torch.cuda.synchronize()
     print("captured %d graphs, batch order %s, skip %r, powers %s" % (
         len(order), order, os.environ.get("DGP_SKIP", ""), list(eopt._pw.keys())), flush=True)
     equal = True
+    def ptrs():
+        out = [p.data_ptr() for p in model.parameters()]
+        for st in dopt.state.values():
+            out += [v.data_ptr() for v in st.values() if torch.is_tensor(v)]
+        return out
+    ptrs0 = ptrs()
+    # replay sequence (DGP_REPLAY, indices into the captured graphs)
+    rep = [int(x) for x in os.environ.get("DGP_REPLAY", ",".join(
+        str(k) for k in range(len(order)))).split(",")]
     for i in range(warm, warm + args.steps):
-        k = (i - warm) % len(order)
+        k = rep[(i - warm) % len(rep)]
         la = mz.din_train_step(A[1], bat[order[k]], A[2], A[3], warm + order[k])
         g, lb = graphs[k]
         print("step %d: graph %d (batch %d)" % (i, k, order[k]), flush=True)
@@ -150,6 +179,8 @@ def main():
                   flush=True)
             break
     print("eager == graph over %d steps: %s" % (args.steps, equal), flush=True)
+    print("parameter / optimizer-state storage unchanged since capture: %s" % (ptrs() == ptrs0),
+          flush=True)
     n = args.steps
     for name, fn in (("eager", lambda i: mz.din_train_step(A[1], bat[order[i % len(order)]],
                                                            A[2], A[3], i)),
