@@ -49,7 +49,7 @@ def main():
         loss.backward()
         for ev in evs:
             ev.pending_grads = []
-        return (loss, model.f1_att.weight.grad, model.dnn1.weight.grad)
+        return (loss,) + tuple(p.grad for p in model.parameters())
 
     sgd = torch.optim.SGD(model.parameters(), lr=0.01)
 
@@ -106,6 +106,11 @@ def main():
             graphs[k].replay()
             torch.cuda.synchronize()
             res.append(all(torch.equal(a.detach(), b) for a, b in zip(outs[k], want2)))
+            if name == "forward+backward" and not res[-1]:
+                names = ["loss"] + [n for n, _ in model.named_parameters()]
+                bad = [names[i] for i, (a, b) in enumerate(zip(outs[k], want2))
+                       if not torch.equal(a.detach(), b)]
+                print("  replay %d after the change: differs in %s" % (k, bad[:8]), flush=True)
         print("%-18s graph replays equal eager (before / after a state change): %s"
               % (name, res), flush=True)
     dr.status_check(dev)

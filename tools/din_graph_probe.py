@@ -163,13 +163,42 @@ def main():
     # replay sequence (DGP_REPLAY, indices into the captured graphs)
     rep = [int(x) for x in os.environ.get("DGP_REPLAY", ",".join(
         str(k) for k in range(len(order)))).split(",")]
+    # DGP_SEQUENTIAL=1: the eager twin runs all its steps first (snapshots
+    # kept), then the graphs replay -- no eager allocation between replays
+    seq = os.environ.get("DGP_SEQUENTIAL", "0") == "1"
+    pre = {}
+    if os.environ.get("DGP_CHURN") == "1":
+        # no eager step at all: only allocations filled with NaN, then freed
+        for _ in range(8):
+            junk = [torch.full((1 << 22,), float("nan"), device=dev) for _ in range(64)]
+            del junk
+        torch.cuda.synchronize()
+        print("churned the default pool with NaN-filled blocks", flush=True)
+    if seq:
+        for i in range(warm, warm + args.steps):
+            k = rep[(i - warm) % len(rep)]
+            la = mz.din_train_step(A[1], bat[order[k]], A[2], A[3], warm + order[k])
+            pre[i] = (la.detach().clone(), snapshot(A[1], A[0]))
+        torch.cuda.synchronize()
     for i in range(warm, warm + args.steps):
         k = rep[(i - warm) % len(rep)]
-        la = mz.din_train_step(A[1], bat[order[k]], A[2], A[3], warm + order[k])
+        if not seq:
+            la = mz.din_train_step(A[1], bat[order[k]], A[2], A[3], warm + order[k])
         g, lb = graphs[k]
         print("step %d: graph %d (batch %d)" % (i, k, order[k]), flush=True)
         g.replay()
         torch.cuda.synchronize()
+        if seq:
+            la, snapA = pre[i]
+            okl = torch.equal(la.view(torch.int32), lb.detach().view(torch.int32))
+            names = [n for n, _ in model.named_parameters()]
+            ok = same(snapA, snapshot(model, evs), names, report=True) and okl
+            equal = equal and ok
+            if not ok:
+                print("step %d differs: loss %r vs %r" % (i, float(la), float(lb.detach())),
+                      flush=True)
+                break
+            continue
         okl = torch.equal(la.view(torch.int32), lb.view(torch.int32))
         names = [n for n, _ in model.named_parameters()]
         ok = same(snapshot(A[1], A[0]), snapshot(model, evs), names, report=True) and okl
