@@ -500,13 +500,14 @@ def din_leg(args, dev, log, world, rank, dist, staged):
         evs.append(ev)
     torch.manual_seed(0)
     model = mz.DIN(*evs).to(dev)
-    # one GPU, DR_DIN_GRAPH=1: the step as hipGraphs (one per batch shape);
-    # capturable dense Adam (step counts on the device), KV Adam's beta powers
-    # in HBM (training.AdamOptimizer._device_powers).  Off by default: the
-    # second and later captured graphs diverge from the eager step
-    # (tools/din_graph_probe.py), so the reported step is eager
+    # one GPU: the step as hipGraphs, one per batch shape (DR_DIN_GRAPH=0:
+    # eager); capturable dense Adam (step counts on the device), KV Adam's
+    # beta powers in HBM (training.AdamOptimizer._device_powers).  The
+    # replays are bit-equal to the eager steps when nothing else runs between
+    # them (tests/test_gpu_din_graph.py, profiles/r05_din_graph_probe.log);
+    # the eager step is timed and reported beside them
     use_graph = (world == 1 and getattr(args, "model_graph", True)
-                 and os.environ.get("DR_DIN_GRAPH", "0") == "1")
+                 and os.environ.get("DR_DIN_GRAPH", "1") == "1")
     dopt = torch.optim.Adam(model.parameters(), lr=0.001, capturable=use_graph)
     eopt = dr.AdamOptimizer(0.001)
     g = torch.Generator(device=dev)

@@ -93,6 +93,60 @@ def same(a, b, names=None, report=False):
     return ok
 
 
+def one_model(dr, mz, dev, bat, B, T, D, R, steps, mode):
+    """One model in this process: DGP_MODE=eager saves every step's loss and
+    the final state to gpurun_out/dgp_eager.pt; DGP_MODE=graph replays the
+    captured steps and compares with that file -- no second model's eager
+    calls between the replays."""
+    path = os.environ.get("DGP_FILE", os.path.join("/tmp", "dgp_eager_%d.pt" % B))
+    evs, model, dopt, eopt = build(dr, mz, dev, "m", B, T, D, R)
+    warm = 4
+    for i in range(warm):
+        mz.din_train_step(model, bat[i % 4], dopt, eopt, i)
+    for ev in evs:
+        ev.reserve(8 * B * (T + 1))
+    torch.cuda.synchronize()
+    losses = []
+    if mode == "eager":
+        for i in range(warm, warm + steps):
+            losses.append(mz.din_train_step(model, bat[i % 4], dopt, eopt, i).detach().clone())
+        torch.cuda.synchronize()
+        ps, es = snapshot(model, evs)
+        torch.save({"losses": [l.cpu() for l in losses], "ps": [p.cpu() for p in ps],
+                    "es": [(k.cpu(), v.cpu()) for k, v in es]}, path)
+        print("eager run saved (%d steps)" % steps, flush=True)
+        return
+    ref = torch.load(path, weights_only=True)
+    graphs = []
+    for j in range(4):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            loss = mz.din_train_step(model, bat[(warm + j) % 4], dopt, eopt, warm + j)
+        graphs.append((g, loss))
+    ok = True
+    for n, i in enumerate(range(warm, warm + steps)):
+        g, lb = graphs[(i - warm) % 4]
+        g.replay()
+        torch.cuda.synchronize()
+        same_l = torch.equal(ref["losses"][n].view(torch.int32), lb.detach().cpu().view(torch.int32))
+        if not same_l:
+            print("step %d loss differs: %r vs %r" % (i, float(ref["losses"][n]),
+                                                       float(lb.detach())), flush=True)
+            ok = False
+            break
+    if ok:
+        ps, es = snapshot(model, evs)
+        ok = all(torch.equal(a.view(torch.int32), b.cpu().view(torch.int32))
+                 for a, b in zip(ref["ps"], ps))
+        for (ka, va), (kb, vb) in zip(ref["es"], es):
+            ok = ok and torch.equal(ka, kb.cpu()) and torch.equal(va.view(torch.int32),
+                                                                    vb.cpu().view(torch.int32))
+    print("graph replays (alone in their process) == eager run: %s over %d steps" % (ok, steps),
+          flush=True)
+    if not ok:
+        sys.exit(1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
@@ -105,6 +159,9 @@ def main():
     B, T, D = args.batch, 100, 18
     R = (500_000, 400_000, 2_000)
     bat = batches_for(dev, B, T, R)
+    mode = os.environ.get("DGP_MODE", "")   # "eager" / "graph": one model per process
+    if mode:
+        return one_model(dr, mz, dev, bat, B, T, D, R, args.steps, mode)
     A = build(dr, mz, dev, "a", B, T, D, R)
     Bm = build(dr, mz, dev, "b", B, T, D, R)
     warm = 4   # every batch once: per-shape caches, slots, device beta powers

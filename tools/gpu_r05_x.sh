@@ -1,0 +1,13 @@
+# Round 5, batch X: the DIN hipGraph step -- the two-process bit-equality
+# test, then the bench DIN leg (graphs by default).  Tag $1.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+T=${1:-r05x}
+mkdir -p gpurun_out/$T
+timeout -k 10 600 python -u -m pytest tests/test_gpu_din_graph.py tests/test_gpu_din.py -m gpu -q --timeout 500 --timeout-method thread > gpurun_out/$T/tests.log 2>&1
+rc=$?; tail -2 gpurun_out/$T/tests.log; grep -E "^FAILED|^ERROR|assert" gpurun_out/$T/tests.log | head -10
+[ $rc -ne 0 ] && exit $rc
+DGP_MODE=eager DGP_FILE=/tmp/dgp_full.pt timeout -k 10 200 python -u tools/din_graph_probe.py --steps 12 > gpurun_out/$T/e.log 2>&1 && DGP_MODE=graph DGP_FILE=/tmp/dgp_full.pt timeout -k 10 200 python -u tools/din_graph_probe.py --steps 12 > gpurun_out/$T/g.log 2>&1; rc=$?; grep -E "==" gpurun_out/$T/g.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 400 python -u bench.py --cpu-seconds 0 --steps 3 --warmup 1 --train-steps 0 --no-criteo --no-dcn --no-hybrid --no-deepfm --model-steps 0 --native-steps 0 --din-steps 20 > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err; rc=$?; grep "din leg" gpurun_out/$T/bench.err | cut -c1-500
+exit $rc
