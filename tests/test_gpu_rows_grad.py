@@ -608,3 +608,35 @@ def test_ev_collected_during_capture_is_released_after(dr):
     dr.flush_releases()
     assert len(kvo._DEFERRED) == 0
     del keep
+
+
+def test_kv_adam_device_powers_equal_host_powers(dr, monkeypatch):
+    """KV Adam with its beta powers in HBM (dr_ev_apply_adam_grouped_dev:
+    alpha formed by the kernel, powers advanced by an fp32 multiply on the
+    device) leaves the EVs and both slots bit-identical to the host-powers
+    apply (dr_ev_apply_grouped, alpha formed on the host) over three steps,
+    by-address and value-block gradients both."""
+    from deeprec_amd import training
+    rng = np.random.default_rng(71)
+    B, D = 3000, 16
+    batches = []
+    for _ in range(3):
+        v = rng.integers(0, 500, B).astype(np.int64)
+        batches.append((v, rng.standard_normal((B, D)).astype(np.float32)))
+    ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+    res = []
+    for dev_powers in (True, False):
+        monkeypatch.setattr(training, "_ADAM_DEVICE_POWERS", dev_powers)
+        ev = dr.EmbeddingVariable("adam_pw_%d" % int(dev_powers), D, 0.1, capacity=2048)
+        opt = dr.AdamOptimizer(0.01)
+        for step, (v, g) in enumerate(batches):
+            out = dr.embedding_lookup_sparse(ev, dr.SparseTensor(T(ind), T(v), (B, 1)),
+                                             combiner="mean")
+            out.backward(T(g))
+            opt.apply_gradients([ev], global_step=step)
+        torch.cuda.synchronize()
+        m, s = opt._slots(ev)
+        res.append([_export(ev), _export(m), _export(s)])
+    for (k1, v1), (k2, v2) in zip(res[0], res[1]):
+        np.testing.assert_array_equal(k1, k2)
+        np.testing.assert_array_equal(v1.view(np.uint32), v2.view(np.uint32))
