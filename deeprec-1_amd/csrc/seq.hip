@@ -602,6 +602,159 @@ __global__ void din_mlp_sample_kernel(const int32_t* __restrict__ off, int64_t B
   }
 }
 
+// The attention MLP's weight gradients in one pass over the per-position
+// buffers (dr_din_mlp_wgrad): G = da1 x^T [N1 x H2] (dW1's four blocks are
+// formed from it), dW2 = da2 h1^T [N2 x N1], db2 = sum da2, dw3 = h2 dsc,
+// db3 = sum dsc -- reductions over the cap positions, which the library did
+// as two batched split-K GEMMs, a GEMV and three reductions (≈ 0.25-0.3 ms at
+// DIN's cap = 409 600).  Split-K: block b sums positions [b*per, (b+1)*per)
+// in chunks of 64 staged through LDS position-major ([p][row]: a thread's 4
+// or CW rows at one position are contiguous), fp32 partials per block;
+// din_wgrad_reduce_kernel sums them in block order (deterministic).
+// Threads 0..20*(H2/CW)-1: a 4 x CW tile of G; threads 0..199: a 4 x 4 tile
+// of dW2; threads 200..239: db2 / dw3 of one row; thread 240: db3.
+static constexpr int DW_CH = 64;
+template <int H2, int CW, int N1, int N2>
+__global__ __launch_bounds__(256) void din_wgrad_kernel(
+    const float* __restrict__ da1t, const float* __restrict__ xt, const float* __restrict__ da2t,
+    const float* __restrict__ h1t, const float* __restrict__ h2t, const float* __restrict__ dsc,
+    int64_t cap, int64_t per, float* __restrict__ part) {
+  static_assert(N1 == 80 && N2 == 40 && H2 % CW == 0 && 20 * (H2 / CW) <= 256, "tile shape");
+  constexpr int GOUT = N1 * H2, WOUT = N2 * N1, OUT = GOUT + WOUT + 2 * N2 + 1;
+  constexpr int RA = N1, RX = H2, RD = N2, RH = N1, RG = N2;     // rows per position
+  constexpr int OA = 0, OX = OA + RA, OD = OX + RX, OH = OD + RD, OG = OH + RH, OS = OG + RG;
+  constexpr int ROW = (OS + 1 + 3) / 4 * 4;                       // floats per staged position (16-B rows)
+  __shared__ __attribute__((aligned(16))) float st[DW_CH * ROW];
+  const int tid = threadIdx.x;
+  const int64_t p0 = (int64_t)blockIdx.x * per;
+  const int64_t p1 = p0 + per < cap ? p0 + per : cap;
+  constexpr int NG = 20 * (H2 / CW);
+  const bool tg = tid < NG;
+  const int gi = (tid / (H2 / CW)) * 4, gj = (tid % (H2 / CW)) * CW;
+  const bool tw = tid < 200;
+  const int wi = (tid / 20) * 4, wj = (tid % 20) * 4;
+  const bool tb = tid >= 200 && tid < 200 + N2;
+  const int bk = tid - 200;
+  float g[4][CW], w[4][4], db2 = 0.f, dw3 = 0.f, db3 = 0.f;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+#pragma unroll
+    for (int c = 0; c < CW; ++c) g[a][c] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[a][c] = 0.f;
+  }
+  for (int64_t c0 = p0; c0 < p1; c0 += DW_CH) {
+    const int nc = (int)(p1 - c0 < DW_CH ? p1 - c0 : DW_CH);
+    // stage: row r of matrix M, positions c0 .. c0 + 63 as 16-B vectors
+    // (coalesced along p), into st[p][offset + r]; positions past nc are
+    // zero.  Four vector loads in flight per thread, from clamped (always
+    // valid) addresses, so none is branched around (rows are 16-B aligned:
+    // cap % 4 == 0, c0 % 64 == 0)
+    auto stage_mat = [&](const float* __restrict__ M, int R, int off) {
+      const int nv = R * (DW_CH / 4);
+      for (int e0 = 0; e0 < nv; e0 += 256 * 4) {
+        float4 v[4];
+        int ee[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          int e = e0 + u * 256 + tid;
+          ee[u] = e;
+          e = e < nv ? e : nv - 1;
+          const int r = e / (DW_CH / 4), p4 = (e % (DW_CH / 4)) * 4;
+          const int pc = p4 < nc ? p4 : 0;
+          v[u] = *reinterpret_cast<const float4*>(M + (int64_t)r * cap + c0 + pc);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e = ee[u];
+          if (e < nv) {
+            const int r = e / (DW_CH / 4), p4 = (e % (DW_CH / 4)) * 4;
+            float* d = st + p4 * ROW + off + r;
+            d[0] = p4 < nc ? v[u].x : 0.f;
+            d[ROW] = p4 + 1 < nc ? v[u].y : 0.f;
+            d[2 * ROW] = p4 + 2 < nc ? v[u].z : 0.f;
+            d[3 * ROW] = p4 + 3 < nc ? v[u].w : 0.f;
+          }
+        }
+      }
+    };
+    stage_mat(da1t, RA, OA);
+    stage_mat(xt, RX, OX);
+    stage_mat(da2t, RD, OD);
+    stage_mat(h1t, RH, OH);
+    stage_mat(h2t, RG, OG);
+    if (tid < DW_CH) st[tid * ROW + OS] = tid < nc ? dsc[c0 + tid] : 0.f;
+    __syncthreads();
+    for (int p = 0; p < nc; ++p) {
+      const float* sp = st + p * ROW;
+      if (tg) {
+        float a[4], x[CW];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] = sp[OA + gi + k];
+#pragma unroll
+        for (int k = 0; k < CW; ++k) x[k] = sp[OX + gj + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int c = 0; c < CW; ++c) g[k][c] = fmaf(a[k], x[c], g[k][c]);
+      }
+      if (tw) {
+        float a[4], h[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] = sp[OD + wi + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) h[k] = sp[OH + wj + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) w[k][c] = fmaf(a[k], h[c], w[k][c]);
+      } else if (tb) {
+        db2 += sp[OD + bk];
+        dw3 = fmaf(sp[OG + bk], sp[OS], dw3);
+      } else if (tid == 240) {
+        db3 += sp[OS];
+      }
+    }
+    __syncthreads();   // the stage is rewritten next
+  }
+  float* pb = part + (int64_t)blockIdx.x * OUT;
+  if (tg)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int c = 0; c < CW; ++c) pb[(gi + k) * H2 + gj + c] = g[k][c];
+  if (tw)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) pb[GOUT + (wi + k) * N1 + wj + c] = w[k][c];
+  if (tb) {
+    pb[GOUT + WOUT + bk] = db2;
+    pb[GOUT + WOUT + N2 + bk] = dw3;
+  }
+  if (tid == 240) pb[GOUT + WOUT + 2 * N2] = db3;
+}
+
+__global__ __launch_bounds__(256) void din_wgrad_reduce_kernel(const float* __restrict__ part,
+                                                               int nb, int out_n,
+                                                               float* __restrict__ out) {
+  // 64 outputs per block; wave w sums blocks [w*q, (w+1)*q) in order, then
+  // the four wave sums are added in wave order (deterministic)
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int o = blockIdx.x * 64 + lane;
+  const int q = (nb + 3) / 4;
+  const int b0 = w * q, b1 = b0 + q < nb ? b0 + q : nb;
+  float a = 0.f;
+  if (o < out_n)
+    for (int b = b0; b < b1; ++b) a += part[(int64_t)b * out_n + o];
+  red[w][lane] = a;
+  __syncthreads();
+  if (w == 0 && o < out_n) out[o] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+static constexpr int kWgradBlocks = 512;
+
 }  // namespace dr
 
 extern "C" {
@@ -744,6 +897,45 @@ int dr_din_mlp_forward(const float* query, const float* facts, const float* mask
                        buf->w2t, b2, w3, b3, scores, buf->h1t, buf->h2t);
   DR_DIN_MLP_SHAPES(DR_FWD)
 #undef DR_FWD
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+size_t dr_din_mlp_wgrad_workspace_size(int n1, int hidden2, int n2) {
+  return (size_t)dr::kWgradBlocks * (size_t)(n1 * hidden2 + n2 * n1 + 2 * n2 + 1) * sizeof(float) +
+         256;
+}
+
+int dr_din_mlp_wgrad(const float* da1t, const float* xt, const float* da2t, const float* h1t,
+                     const float* h2t, const float* dsc, int64_t cap, int n1, int hidden2, int n2,
+                     float* out, void* ws, size_t ws_bytes, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(cap >= 1 && n1 == 80 && n2 == 40 &&
+                 (hidden2 == 32 || hidden2 == 64 || hidden2 == 72 || hidden2 == 128),
+             DR_INVALID_ARGUMENT, "dr_din_mlp_wgrad: n1 = 80, n2 = 40, 2H in {32, 64, 72, 128}");
+  DR_REQUIRE(da1t && xt && da2t && h1t && h2t && dsc && out && ws, DR_INVALID_ARGUMENT,
+             "null operand");
+  DR_REQUIRE(ws_bytes >= dr_din_mlp_wgrad_workspace_size(n1, hidden2, n2), DR_INVALID_ARGUMENT,
+             "workspace too small");
+  DR_REQUIRE(cap % 4 == 0 && ((uintptr_t)da1t | (uintptr_t)xt | (uintptr_t)da2t | (uintptr_t)h1t |
+                              (uintptr_t)h2t) % 16 == 0,
+             DR_INVALID_ARGUMENT, "dr_din_mlp_wgrad: cap % 4 == 0 and 16-B aligned buffers");
+  const int out_n = n1 * hidden2 + n2 * n1 + 2 * n2 + 1;
+  int64_t per = (cap + kWgradBlocks - 1) / kWgradBlocks;
+  per = (per + DW_CH - 1) / DW_CH * DW_CH;
+  const int nb = (int)((cap + per - 1) / per);
+  float* part = static_cast<float*>(ws);
+  hipStream_t s = S(stream);
+#define DR_WG(H2, CW)                                                                         \
+  hipLaunchKernelGGL((din_wgrad_kernel<H2, CW, 80, 40>), dim3((unsigned)nb), dim3(256), 0, s,  \
+                     da1t, xt, da2t, h1t, h2t, dsc, cap, per, part)
+  if (hidden2 == 72) DR_WG(72, 6);
+  else if (hidden2 == 64) DR_WG(64, 8);
+  else if (hidden2 == 32) DR_WG(32, 4);
+  else DR_WG(128, 16);
+#undef DR_WG
+  hipLaunchKernelGGL(din_wgrad_reduce_kernel, dim3((unsigned)ceil_div((int64_t)out_n, 64)),
+                     dim3(256), 0, s, part, nb, out_n, out);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

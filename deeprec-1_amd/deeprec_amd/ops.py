@@ -898,6 +898,13 @@ def din_mlp_forward(query, facts, mask, w1, b1, w2, b2, w3, b3):
     return scores, buf
 
 
+# the attention MLP's weight gradients: library GEMMs + reductions (default)
+# or DR_DIN_WGRAD=hand, one hand split-K pass (dr_din_mlp_wgrad: correct, but
+# 0.38 + 0.035 ms against the library's ≈ 0.25 at DIN's cap = 409 600 -- its
+# per-position LDS reads bound it; profiles/r05_din_wgrad.log)
+_DIN_WGRAD_HAND = os.environ.get("DR_DIN_WGRAD", "lib") == "hand"
+
+
 def din_mlp_backward(query, facts, w1, w3, buf, grad_scores, grad_facts):
     """Backward of din_mlp_forward: adds the MLP's part to grad_facts (in
     place) and returns (grad_query, dW1, db1, dW2, db2, dw3, db3); the weight
@@ -929,14 +936,30 @@ def din_mlp_backward(query, facts, w1, w3, buf, grad_scores, grad_facts):
     A, Cm = w1f[:, :H], w1f[:, 2 * H:3 * H]
     gq = buf.s1 @ (A + Cm) + buf.dq2
     Gq = buf.s1.t() @ q
-    G = kred(buf.da1t, buf.xt)
+    db1 = buf.s1.sum(0)
+    if _DIN_WGRAD_HAND and 2 * H in (32, 64, 72, 128) and (n1, n2) == (80, 40) and cap % 4 == 0:
+        # one split-K pass for G, dW2, db2, dw3, db3 (dr_din_mlp_wgrad)
+        gout, wout = n1 * 2 * H, n2 * n1
+        out = torch.empty(gout + wout + 2 * n2 + 1, dtype=torch.float32, device=dev)
+        wsb = lib().dr_din_mlp_wgrad_workspace_size(n1, 2 * H, n2)
+        ws = workspace(wsb, dev)
+        check(lib().dr_din_mlp_wgrad(ptr(buf.da1t), ptr(buf.xt), ptr(buf.da2t), ptr(buf.h1t),
+                                     ptr(buf.h2t), ptr(buf.dsc), cap, n1, 2 * H, n2, ptr(out),
+                                     ptr(ws), wsb, stream_handle(dev)))
+        _post(dev)
+        G = out[:gout].view(n1, 2 * H)
+        dW2 = out[gout:gout + wout].view(n2, n1)
+        db2 = out[gout + wout:gout + wout + n2]
+        dw3 = out[gout + wout + n2:gout + wout + 2 * n2].view(1, n2)
+        db3 = out[gout + wout + 2 * n2:].view(1)
+    else:
+        G = kred(buf.da1t, buf.xt)
+        dW2 = kred(buf.da2t, buf.h1t)
+        db2 = buf.da2t.sum(1)
+        dw3 = (buf.h2t @ buf.dsc).view(1, n2)
+        db3 = buf.dsc.sum().view(1)
     Gf, Gqf = G[:, :H], G[:, H:]
     dW1 = torch.cat([Gq, Gf, Gq - Gf, Gqf], 1)
-    db1 = buf.s1.sum(0)
-    dW2 = kred(buf.da2t, buf.h1t)
-    db2 = buf.da2t.sum(1)
-    dw3 = (buf.h2t @ buf.dsc).view(1, n2)
-    db3 = buf.dsc.sum().view(1)
     return gq, dW1, db1, dW2, db2, dw3, db3
 
 

@@ -1141,6 +1141,16 @@ int dr_din_mlp_forward(const float* query, const float* facts, const float* mask
                        int64_t seq_len, int hidden, const float* w1, const float* b1, int n1,
                        const float* w2, const float* b2, int n2, const float* w3, const float* b3,
                        float* scores, const dr_din_mlp_buf* buf, void* stream);
+/* The attention MLP's weight gradients from dr_din_mlp_backward's buffers   */
+/* in one split-K pass over the cap positions: out = [G = da1 x^T (n1 x 2H),  */
+/* dW2 = da2 h1^T (n2 x n1), db2 = sum da2 (n2), dw3 = h2 dsc (n2), db3 =     */
+/* sum dsc (1)], fp32 partials summed in block order (deterministic).  The    */
+/* buffers are the dr_din_mlp_buf fields da1t, xt, da2t, h1t, h2t, dsc        */
+/* (feature-major, columns past the valid count zero).  n1 = 80, n2 = 40.     */
+size_t dr_din_mlp_wgrad_workspace_size(int n1, int hidden2, int n2);
+int dr_din_mlp_wgrad(const float* da1t, const float* xt, const float* da2t, const float* h1t,
+                     const float* h2t, const float* dsc, int64_t cap, int n1, int hidden2, int n2,
+                     float* out, void* ws, size_t ws_bytes, void* stream);
 int dr_din_mlp_backward(const float* query, const float* facts, int64_t batch, int64_t seq_len,
                         int hidden, int n1, int n2, const float* w3, const float* grad_scores,
                         float* grad_facts, const dr_din_mlp_buf* buf, void* stream);
