@@ -25,7 +25,9 @@ def build(dr, mz, dev, tag, B, T, D, R):
         evs.append(ev)
     torch.manual_seed(11)
     model = mz.DIN(*evs).to(dev)
-    dopt = torch.optim.Adam(model.parameters(), lr=0.001, capturable=True)
+    # DGP_FOREACH=0: the per-parameter Adam (no multi-tensor address lists)
+    fe = {"0": False, "1": True}.get(os.environ.get("DGP_FOREACH", ""), None)
+    dopt = torch.optim.Adam(model.parameters(), lr=0.001, capturable=True, foreach=fe)
     eopt = dr.AdamOptimizer(0.001)
     skip = os.environ.get("DGP_SKIP", "")   # bisection: "ev" / "dense" updates left out
     if skip == "ev":
@@ -231,6 +233,43 @@ def main():
             del junk
         torch.cuda.synchronize()
         print("churned the default pool with NaN-filled blocks", flush=True)
+    twin = os.environ.get("DGP_TWIN_OP", "")
+    if twin:
+        if twin == "none":
+            twin = "-"
+        # bisecting the interference: only part of a step on the twin model
+        # A between capture and replay, then B's replays are checked for NaN
+        for i in range(8):
+            bt = bat[i % 4]
+            if twin == "fwd":
+                with torch.no_grad():
+                    A[1](*bt[:6])
+            elif twin == "fwdbwd":
+                y = A[1](*bt[:6])
+                (-(torch.log(y) * bt[6]).mean()).backward()
+                for ev in A[0]:
+                    ev.pending_grads = []
+            elif twin == "lookup":
+                with torch.no_grad():
+                    A[1].item_lookup(torch.stack([bt[1], bt[2]]))
+            elif twin == "apply":
+                y = A[1](*bt[:6])
+                (-(torch.log(y) * bt[6]).mean()).backward()
+                A[3].apply_gradients(A[0], global_step=i)
+            elif twin == "dense":
+                y = A[1](*bt[:6])
+                A[2].zero_grad(set_to_none=True)
+                (-(torch.log(y) * bt[6]).mean()).backward()
+                A[2].step()
+                for ev in A[0]:
+                    ev.pending_grads = []
+        torch.cuda.synchronize()
+        for k, (g, lb) in enumerate(graphs[:2]):
+            g.replay()
+            torch.cuda.synchronize()
+            print("twin op %r then graph %d replay: loss %r" % (twin, k, float(lb.detach())),
+                  flush=True)
+        return
     if seq:
         for i in range(warm, warm + args.steps):
             k = rep[(i - warm) % len(rep)]
