@@ -753,6 +753,137 @@ __global__ __launch_bounds__(256) void din_wgrad_reduce_kernel(const float* __re
   if (w == 0 && o < out_n) out[o] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
+// The same reductions on the matrix cores (the default of DR_DIN_WGRAD=hand;
+// DR_DIN_WGRAD_VALU=1 the kernel above): every output is a 16 x 16 tile of
+// v_mfma_f32_16x16x4f32 over K = 4 positions at a time -- G (5 x NT tiles,
+// columns past H2 discarded), dW2 (3 x 5, rows past N2 discarded) and 5
+// tiles whose B operand is [dsc, 1, 0, ...] over the rows [da2 ; h2]
+// (column 1 of the da2 rows = db2, column 0 of the h2 rows = dw3); db3 by
+// wave 0's lanes.  Tiles dealt round-robin to the 4 waves; fragments read
+// from the same position-major LDS stage (lane l: row l % 16 of the tile at
+// position p + l / 16).
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+template <int H2, int N1, int N2>
+__global__ __launch_bounds__(256) void din_wgrad_mfma_kernel(
+    const float* __restrict__ da1t, const float* __restrict__ xt, const float* __restrict__ da2t,
+    const float* __restrict__ h1t, const float* __restrict__ h2t, const float* __restrict__ dsc,
+    int64_t cap, int64_t per, float* __restrict__ part) {
+  static_assert(N1 == 80 && N2 == 40, "tile shape");
+  constexpr int NT = (H2 + 15) / 16;
+  constexpr int GT = 5 * NT, WT = 15, XT = 5, TT = GT + WT + XT;
+  constexpr int TPW = (TT + 3) / 4;                                // tiles per wave
+  constexpr int GOUT = N1 * H2, WOUT = N2 * N1, OUT = GOUT + WOUT + 2 * N2 + 1;
+  constexpr int RA = N1, RX = H2, RD = N2, RH = N1, RG = N2;
+  constexpr int OA = 0, OX = OA + RA, OD = OX + RX, OH = OD + RD, OG = OH + RH, OS = OG + RG;
+  constexpr int ROW = (OS + 1 + 3) / 4 * 4;
+  static_assert(OX + 16 * NT <= ROW && OD + 48 <= ROW, "padded fragment reads stay in the row");
+  __shared__ __attribute__((aligned(16))) float st[DW_CH * ROW];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t p0 = (int64_t)blockIdx.x * per;
+  const int64_t p1 = p0 + per < cap ? p0 + per : cap;
+  const int li = lane & 15, lk = lane >> 4;
+  f32x4v acc[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  float db3 = 0.f;
+  for (int64_t c0 = p0; c0 < p1; c0 += DW_CH) {
+    const int nc = (int)(p1 - c0 < DW_CH ? p1 - c0 : DW_CH);
+    // stage: row r of matrix M, positions c0 .. c0 + 63 as 16-B vectors
+    // (coalesced along p), into st[p][offset + r]; positions past nc are
+    // zero.  Four vector loads in flight per thread, from clamped (always
+    // valid) addresses, so none is branched around (rows are 16-B aligned:
+    // cap % 4 == 0, c0 % 64 == 0)
+    auto stage_mat = [&](const float* __restrict__ M, int R, int off) {
+      const int nv = R * (DW_CH / 4);
+      for (int e0 = 0; e0 < nv; e0 += 256 * 4) {
+        float4 v[4];
+        int ee[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          int e = e0 + u * 256 + tid;
+          ee[u] = e;
+          e = e < nv ? e : nv - 1;
+          const int r = e / (DW_CH / 4), p4 = (e % (DW_CH / 4)) * 4;
+          const int pc = p4 < nc ? p4 : 0;
+          v[u] = *reinterpret_cast<const float4*>(M + (int64_t)r * cap + c0 + pc);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e = ee[u];
+          if (e < nv) {
+            const int r = e / (DW_CH / 4), p4 = (e % (DW_CH / 4)) * 4;
+            float* d = st + p4 * ROW + off + r;
+            d[0] = p4 < nc ? v[u].x : 0.f;
+            d[ROW] = p4 + 1 < nc ? v[u].y : 0.f;
+            d[2 * ROW] = p4 + 2 < nc ? v[u].z : 0.f;
+            d[3 * ROW] = p4 + 3 < nc ? v[u].w : 0.f;
+          }
+        }
+      }
+    };
+    stage_mat(da1t, RA, OA);
+    stage_mat(xt, RX, OX);
+    stage_mat(da2t, RD, OD);
+    stage_mat(h1t, RH, OH);
+    stage_mat(h2t, RG, OG);
+    if (tid < DW_CH) st[tid * ROW + OS] = tid < nc ? dsc[c0 + tid] : 0.f;
+    __syncthreads();
+    if (wave == 0) db3 += st[lane * ROW + OS];   // (zero past nc)
+    for (int p = 0; p < DW_CH; p += 4) {         // zero-padded past nc: a full chunk
+      const float* sp = st + (p + lk) * ROW;
+      const float ds = sp[OS];
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) {
+        const int t = wave + 4 * j;              // wave-uniform
+        if (t >= TT) break;
+        float a, b;
+        if (t < GT) {
+          a = sp[OA + (t / NT) * 16 + li];
+          b = sp[OX + (t % NT) * 16 + li];
+        } else if (t < GT + WT) {
+          const int q = t - GT;
+          a = sp[OD + (q / 5) * 16 + li];
+          b = sp[OH + (q % 5) * 16 + li];
+        } else {
+          const int r = (t - GT - WT) * 16 + li;      // virtual rows [da2 ; h2]
+          a = r < N2 ? sp[OD + r] : sp[OG + (r - N2)];
+          b = li == 0 ? ds : (li == 1 ? 1.f : 0.f);
+        }
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
+      }
+    }
+    __syncthreads();   // the stage is rewritten next
+  }
+  float* pb = part + (int64_t)blockIdx.x * OUT;
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int t = wave + 4 * j;
+    if (t >= TT) break;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * lk + r, col = li;      // C/D map: rows 4 (l / 16) + r, column l % 16
+      const float v = acc[j][r];
+      if (t < GT) {
+        const int gi = (t / NT) * 16 + row, gj = (t % NT) * 16 + col;
+        if (gj < H2) pb[gi * H2 + gj] = v;
+      } else if (t < GT + WT) {
+        const int q = t - GT;
+        const int wi = (q / 5) * 16 + row, wj = (q % 5) * 16 + col;
+        if (wi < N2) pb[GOUT + wi * N1 + wj] = v;
+      } else {
+        const int vr = (t - GT - WT) * 16 + row;
+        if (vr < N2 && col == 1) pb[GOUT + WOUT + vr] = v;                 // db2
+        if (vr >= N2 && vr < 2 * N2 && col == 0) pb[GOUT + WOUT + vr] = v;  // dw3 (N2 + k)
+      }
+    }
+  }
+  if (wave == 0) {
+    for (int o = 32; o > 0; o >>= 1) db3 += __shfl_down(db3, o, 64);
+    if (lane == 0) pb[GOUT + WOUT + 2 * N2] = db3;
+  }
+}
+
 static constexpr int kWgradBlocks = 512;
 
 }  // namespace dr
@@ -910,6 +1041,9 @@ int dr_din_mlp_wgrad(const float* da1t, const float* xt, const float* da2t, cons
                      const float* h2t, const float* dsc, int64_t cap, int n1, int hidden2, int n2,
                      float* out, void* ws, size_t ws_bytes, void* stream) {
   using namespace dr;
+  // the matrix-core form unless DR_DIN_WGRAD_VALU=1 (read per call)
+  const char* ve = getenv("DR_DIN_WGRAD_VALU");
+  const bool mfma = !(ve && atoi(ve) != 0);
   DR_REQUIRE(cap >= 1 && n1 == 80 && n2 == 40 &&
                  (hidden2 == 32 || hidden2 == 64 || hidden2 == 72 || hidden2 == 128),
              DR_INVALID_ARGUMENT, "dr_din_mlp_wgrad: n1 = 80, n2 = 40, 2H in {32, 64, 72, 128}");
@@ -927,8 +1061,14 @@ int dr_din_mlp_wgrad(const float* da1t, const float* xt, const float* da2t, cons
   float* part = static_cast<float*>(ws);
   hipStream_t s = S(stream);
 #define DR_WG(H2, CW)                                                                         \
-  hipLaunchKernelGGL((din_wgrad_kernel<H2, CW, 80, 40>), dim3((unsigned)nb), dim3(256), 0, s,  \
-                     da1t, xt, da2t, h1t, h2t, dsc, cap, per, part)
+  do {                                                                                        \
+    if (mfma)                                                                                 \
+      hipLaunchKernelGGL((din_wgrad_mfma_kernel<H2, 80, 40>), dim3((unsigned)nb), dim3(256), 0, \
+                         s, da1t, xt, da2t, h1t, h2t, dsc, cap, per, part);                   \
+    else                                                                                      \
+      hipLaunchKernelGGL((din_wgrad_kernel<H2, CW, 80, 40>), dim3((unsigned)nb), dim3(256), 0, \
+                         s, da1t, xt, da2t, h1t, h2t, dsc, cap, per, part);                   \
+  } while (0)
   if (hidden2 == 72) DR_WG(72, 6);
   else if (hidden2 == 64) DR_WG(64, 8);
   else if (hidden2 == 32) DR_WG(32, 4);

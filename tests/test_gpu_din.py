@@ -186,7 +186,7 @@ def test_din_attention_empty_batch():
     assert gs.shape == (0, 5)
 
 
-@pytest.mark.parametrize("wgrad", ["lib", "hand"])
+@pytest.mark.parametrize("wgrad", ["lib", "mfma", "valu"])
 @pytest.mark.parametrize("B,T,H,prefix", [(64, 100, 36, True), (40, 23, 36, False),
                                           (8, 1, 36, True), (16, 9, 16, False),
                                           (12, 30, 64, True), (20, 17, 32, False)])
@@ -198,11 +198,13 @@ def test_din_fused_attention_matches_fp64(B, T, H, prefix, wgrad, monkeypatch):
     against torch fp64 autograd of the reference composition (utils.py:
     264-309), prefix masks (zero-padded histories, a fully masked row) and
     arbitrary 0/1 masks.  Weight gradients both ways: library GEMMs (the
-    default) and the hand split-K pass (dr_din_mlp_wgrad, DR_DIN_WGRAD=hand;
-    used when cap % 4 == 0)."""
+    default) and the hand split-K pass (dr_din_mlp_wgrad, DR_DIN_WGRAD=hand,
+    on the matrix cores or, DR_DIN_WGRAD_VALU=1, the VALU; used when cap % 4
+    == 0)."""
     from deeprec_amd import modelzoo as mz
     from deeprec_amd import ops
-    monkeypatch.setattr(ops, "_DIN_WGRAD_HAND", wgrad == "hand")
+    monkeypatch.setattr(ops, "_DIN_WGRAD_HAND", wgrad != "lib")
+    monkeypatch.setenv("DR_DIN_WGRAD_VALU", "1" if wgrad == "valu" else "0")
     g = torch.Generator(device="cpu").manual_seed(B * 1000 + T + H)
     q = torch.randn(B, H, generator=g, dtype=torch.float64) * 0.5
     f = torch.randn(B, T, H, generator=g, dtype=torch.float64) * 0.5
