@@ -18,6 +18,8 @@
 
 #include <math.h>
 
+#include <type_traits>
+
 namespace dr {
 
 // tf.ones_like(scores) * (-2 ** 32 + 1) in float32 (utils.py:291)
@@ -735,22 +737,28 @@ __global__ __launch_bounds__(256) void din_wgrad_kernel(
   if (tid == 240) pb[GOUT + WOUT + 2 * N2] = db3;
 }
 
-__global__ __launch_bounds__(256) void din_wgrad_reduce_kernel(const float* __restrict__ part,
-                                                               int nb, int out_n,
-                                                               float* __restrict__ out) {
-  // 64 outputs per block; wave w sums blocks [w*q, (w+1)*q) in order, then
-  // the four wave sums are added in wave order (deterministic)
-  __shared__ float red[4][64];
+__global__ __launch_bounds__(1024) void din_wgrad_reduce_kernel(const float* __restrict__ part,
+                                                                int nb, int out_n,
+                                                                float* __restrict__ out) {
+  // 64 outputs per block; wave w of 16 sums blocks [w*q, (w+1)*q) in order,
+  // then the sixteen wave sums are added in wave order (deterministic)
+  __shared__ float red[16][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int o = blockIdx.x * 64 + lane;
-  const int q = (nb + 3) / 4;
+  const int q = (nb + 15) / 16;
   const int b0 = w * q, b1 = b0 + q < nb ? b0 + q : nb;
   float a = 0.f;
   if (o < out_n)
+#pragma unroll 8
     for (int b = b0; b < b1; ++b) a += part[(int64_t)b * out_n + o];
   red[w][lane] = a;
   __syncthreads();
-  if (w == 0 && o < out_n) out[o] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  if (w == 0 && o < out_n) {
+    float t = red[0][lane];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) t += red[k][lane];
+    out[o] = t;
+  }
 }
 
 // The same reductions on the matrix cores (the default of DR_DIN_WGRAD=hand;
@@ -763,7 +771,7 @@ __global__ __launch_bounds__(256) void din_wgrad_reduce_kernel(const float* __re
 // from the same position-major LDS stage (lane l: row l % 16 of the tile at
 // position p + l / 16).
 typedef float f32x4v __attribute__((ext_vector_type(4)));
-template <int H2, int N1, int N2>
+template <int H2, int N1, int N2, int CH>
 __global__ __launch_bounds__(256) void din_wgrad_mfma_kernel(
     const float* __restrict__ da1t, const float* __restrict__ xt, const float* __restrict__ da2t,
     const float* __restrict__ h1t, const float* __restrict__ h2t, const float* __restrict__ dsc,
@@ -775,9 +783,12 @@ __global__ __launch_bounds__(256) void din_wgrad_mfma_kernel(
   constexpr int GOUT = N1 * H2, WOUT = N2 * N1, OUT = GOUT + WOUT + 2 * N2 + 1;
   constexpr int RA = N1, RX = H2, RD = N2, RH = N1, RG = N2;
   constexpr int OA = 0, OX = OA + RA, OD = OX + RX, OH = OD + RD, OG = OH + RH, OS = OG + RG;
-  constexpr int ROW = (OS + 1 + 3) / 4 * 4;
+  // floats per staged position: ROW = 17 (mod 64), so the stage's transposing
+  // stores (16 positions 4 apart x 4 rows per wave) hit 64 distinct banks and
+  // the fragment reads (4 positions x 16 rows) overlap in at most 3 banks
+  constexpr int ROW = OS + 1 + ((17 - (OS + 1) % 64) % 64 + 64) % 64;
   static_assert(OX + 16 * NT <= ROW && OD + 48 <= ROW, "padded fragment reads stay in the row");
-  __shared__ __attribute__((aligned(16))) float st[DW_CH * ROW];
+  __shared__ __attribute__((aligned(16))) float st[CH * ROW];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t p0 = (int64_t)blockIdx.x * per;
@@ -787,33 +798,39 @@ __global__ __launch_bounds__(256) void din_wgrad_mfma_kernel(
 #pragma unroll
   for (int j = 0; j < TPW; ++j) acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
   float db3 = 0.f;
-  for (int64_t c0 = p0; c0 < p1; c0 += DW_CH) {
-    const int nc = (int)(p1 - c0 < DW_CH ? p1 - c0 : DW_CH);
-    // stage: row r of matrix M, positions c0 .. c0 + 63 as 16-B vectors
-    // (coalesced along p), into st[p][offset + r]; positions past nc are
-    // zero.  Four vector loads in flight per thread, from clamped (always
-    // valid) addresses, so none is branched around (rows are 16-B aligned:
-    // cap % 4 == 0, c0 % 64 == 0)
-    auto stage_mat = [&](const float* __restrict__ M, int R, int off) {
-      const int nv = R * (DW_CH / 4);
-      for (int e0 = 0; e0 < nv; e0 += 256 * 4) {
-        float4 v[4];
-        int ee[4];
+  for (int64_t c0 = p0; c0 < p1; c0 += CH) {
+    const int nc = (int)(p1 - c0 < CH ? p1 - c0 : CH);
+    // stage: the six operands as one list of rows (da1, x, da2, h1, h2, dsc:
+    // row q lands at st[p][q], the LDS offsets OA.. OS follow the same
+    // order), positions c0 .. c0 + CH - 1 as 16-B vectors coalesced along p;
+    // positions past nc are zero.  SU vector loads in flight per thread, from
+    // clamped (always valid) addresses, so none is branched around (rows are
+    // 16-B aligned: cap % 4 == 0, c0 % 4 == 0) -- two round trips to HBM per
+    // 64-position chunk, not one per operand and 1024 vectors
+    {
+      constexpr int NQ = OS + 1, NV = NQ * (CH / 4), SU = 8;
+      for (int e0 = 0; e0 < NV; e0 += 256 * SU) {
+        float4 v[SU];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < SU; ++u) {
           int e = e0 + u * 256 + tid;
-          ee[u] = e;
-          e = e < nv ? e : nv - 1;
-          const int r = e / (DW_CH / 4), p4 = (e % (DW_CH / 4)) * 4;
+          e = e < NV ? e : NV - 1;
+          const int q = e / (CH / 4), p4 = (e % (CH / 4)) * 4;
           const int pc = p4 < nc ? p4 : 0;
-          v[u] = *reinterpret_cast<const float4*>(M + (int64_t)r * cap + c0 + pc);
+          const float* M = q < OX ? da1t + (int64_t)q * cap
+                         : q < OD ? xt + (int64_t)(q - OX) * cap
+                         : q < OH ? da2t + (int64_t)(q - OD) * cap
+                         : q < OG ? h1t + (int64_t)(q - OH) * cap
+                         : q < OS ? h2t + (int64_t)(q - OG) * cap
+                                  : dsc;
+          v[u] = *reinterpret_cast<const float4*>(M + c0 + pc);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int e = ee[u];
-          if (e < nv) {
-            const int r = e / (DW_CH / 4), p4 = (e % (DW_CH / 4)) * 4;
-            float* d = st + p4 * ROW + off + r;
+        for (int u = 0; u < SU; ++u) {
+          const int e = e0 + u * 256 + tid;
+          if (e < NV) {
+            const int q = e / (CH / 4), p4 = (e % (CH / 4)) * 4;
+            float* d = st + p4 * ROW + q;
             d[0] = p4 < nc ? v[u].x : 0.f;
             d[ROW] = p4 + 1 < nc ? v[u].y : 0.f;
             d[2 * ROW] = p4 + 2 < nc ? v[u].z : 0.f;
@@ -821,38 +838,43 @@ __global__ __launch_bounds__(256) void din_wgrad_mfma_kernel(
           }
         }
       }
-    };
-    stage_mat(da1t, RA, OA);
-    stage_mat(xt, RX, OX);
-    stage_mat(da2t, RD, OD);
-    stage_mat(h1t, RH, OH);
-    stage_mat(h2t, RG, OG);
-    if (tid < DW_CH) st[tid * ROW + OS] = tid < nc ? dsc[c0 + tid] : 0.f;
-    __syncthreads();
-    if (wave == 0) db3 += st[lane * ROW + OS];   // (zero past nc)
-    for (int p = 0; p < DW_CH; p += 4) {         // zero-padded past nc: a full chunk
-      const float* sp = st + (p + lk) * ROW;
-      const float ds = sp[OS];
-#pragma unroll
-      for (int j = 0; j < TPW; ++j) {
-        const int t = wave + 4 * j;              // wave-uniform
-        if (t >= TT) break;
-        float a, b;
-        if (t < GT) {
-          a = sp[OA + (t / NT) * 16 + li];
-          b = sp[OX + (t % NT) * 16 + li];
-        } else if (t < GT + WT) {
-          const int q = t - GT;
-          a = sp[OD + (q / 5) * 16 + li];
-          b = sp[OH + (q % 5) * 16 + li];
-        } else {
-          const int r = (t - GT - WT) * 16 + li;      // virtual rows [da2 ; h2]
-          a = r < N2 ? sp[OD + r] : sp[OG + (r - N2)];
-          b = li == 0 ? ds : (li == 1 ? 1.f : 0.f);
-        }
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
-      }
     }
+    __syncthreads();
+    if (wave == 0 && lane < CH) db3 += st[lane * ROW + OS];   // (zero past nc)
+    // the wave's tiles as compile-time indices (one instantiation per wave),
+    // so the fragment reads of all its tiles are issued together and shared
+    // reads are merged, rather than a branch and a read-wait before each MFMA
+    auto mma = [&](auto w_) {
+      constexpr int W = decltype(w_)::value;
+#pragma unroll 2
+      for (int p = 0; p < CH; p += 4) {        // zero-padded past nc: a full chunk
+        const float* sp = st + (p + lk) * ROW;
+        const float ds = sp[OS];
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+          const int t = W + 4 * j;
+          if (t >= TT) break;
+          float a, b;
+          if (t < GT) {
+            a = sp[OA + (t / NT) * 16 + li];
+            b = sp[OX + (t % NT) * 16 + li];
+          } else if (t < GT + WT) {
+            const int q = t - GT;
+            a = sp[OD + (q / 5) * 16 + li];
+            b = sp[OH + (q % 5) * 16 + li];
+          } else {
+            const int r = (t - GT - WT) * 16 + li;    // virtual rows [da2 ; h2]
+            a = r < N2 ? sp[OD + r] : sp[OG + (r - N2)];
+            b = li == 0 ? ds : (li == 1 ? 1.f : 0.f);
+          }
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
+        }
+      }
+    };
+    if (wave == 0) mma(std::integral_constant<int, 0>{});
+    else if (wave == 1) mma(std::integral_constant<int, 1>{});
+    else if (wave == 2) mma(std::integral_constant<int, 2>{});
+    else mma(std::integral_constant<int, 3>{});
     __syncthreads();   // the stage is rewritten next
   }
   float* pb = part + (int64_t)blockIdx.x * OUT;
@@ -884,7 +906,7 @@ __global__ __launch_bounds__(256) void din_wgrad_mfma_kernel(
   }
 }
 
-static constexpr int kWgradBlocks = 512;
+static constexpr int kWgradBlocks = 1024;
 
 }  // namespace dr
 
@@ -1044,6 +1066,10 @@ int dr_din_mlp_wgrad(const float* da1t, const float* xt, const float* da2t, cons
   // the matrix-core form unless DR_DIN_WGRAD_VALU=1 (read per call)
   const char* ve = getenv("DR_DIN_WGRAD_VALU");
   const bool mfma = !(ve && atoi(ve) != 0);
+  // positions staged per chunk by the matrix-core form: 32 (three blocks per
+  // CU, so one block's loads overlap the others' MFMAs) or 64
+  const char* ce = getenv("DR_DIN_WGRAD_CH");
+  const int ch = ce && atoi(ce) == 64 ? 64 : 32;
   DR_REQUIRE(cap >= 1 && n1 == 80 && n2 == 40 &&
                  (hidden2 == 32 || hidden2 == 64 || hidden2 == 72 || hidden2 == 128),
              DR_INVALID_ARGUMENT, "dr_din_mlp_wgrad: n1 = 80, n2 = 40, 2H in {32, 64, 72, 128}");
@@ -1055,16 +1081,24 @@ int dr_din_mlp_wgrad(const float* da1t, const float* xt, const float* da2t, cons
                               (uintptr_t)h2t) % 16 == 0,
              DR_INVALID_ARGUMENT, "dr_din_mlp_wgrad: cap % 4 == 0 and 16-B aligned buffers");
   const int out_n = n1 * hidden2 + n2 * n1 + 2 * n2 + 1;
-  int64_t per = (cap + kWgradBlocks - 1) / kWgradBlocks;
+  // split-K blocks: kWgradBlocks (1024, the workspace's size) for the VALU
+  // form; the matrix-core form runs 3 blocks per CU (DR_DIN_WGRAD_BLOCKS)
+  const char* be = getenv("DR_DIN_WGRAD_BLOCKS");
+  int nbk = mfma ? 768 : 512;
+  if (be && atoi(be) > 0) nbk = atoi(be) < kWgradBlocks ? atoi(be) : kWgradBlocks;
+  int64_t per = (cap + nbk - 1) / nbk;
   per = (per + DW_CH - 1) / DW_CH * DW_CH;
   const int nb = (int)((cap + per - 1) / per);
   float* part = static_cast<float*>(ws);
   hipStream_t s = S(stream);
 #define DR_WG(H2, CW)                                                                         \
   do {                                                                                        \
-    if (mfma)                                                                                 \
-      hipLaunchKernelGGL((din_wgrad_mfma_kernel<H2, 80, 40>), dim3((unsigned)nb), dim3(256), 0, \
-                         s, da1t, xt, da2t, h1t, h2t, dsc, cap, per, part);                   \
+    if (mfma && ch == 32)                                                                     \
+      hipLaunchKernelGGL((din_wgrad_mfma_kernel<H2, 80, 40, 32>), dim3((unsigned)nb), dim3(256),  \
+                         0, s, da1t, xt, da2t, h1t, h2t, dsc, cap, per, part);                \
+    else if (mfma)                                                                            \
+      hipLaunchKernelGGL((din_wgrad_mfma_kernel<H2, 80, 40, 64>), dim3((unsigned)nb), dim3(256),  \
+                         0, s, da1t, xt, da2t, h1t, h2t, dsc, cap, per, part);                \
     else                                                                                      \
       hipLaunchKernelGGL((din_wgrad_kernel<H2, CW, 80, 40>), dim3((unsigned)nb), dim3(256), 0, \
                          s, da1t, xt, da2t, h1t, h2t, dsc, cap, per, part);                   \
@@ -1075,7 +1109,7 @@ int dr_din_mlp_wgrad(const float* da1t, const float* xt, const float* da2t, cons
   else DR_WG(128, 16);
 #undef DR_WG
   hipLaunchKernelGGL(din_wgrad_reduce_kernel, dim3((unsigned)ceil_div((int64_t)out_n, 64)),
-                     dim3(256), 0, s, part, nb, out_n, out);
+                     dim3(1024), 0, s, part, nb, out_n, out);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

@@ -898,11 +898,11 @@ def din_mlp_forward(query, facts, mask, w1, b1, w2, b2, w3, b3):
     return scores, buf
 
 
-# the attention MLP's weight gradients: library GEMMs + reductions (default)
-# or DR_DIN_WGRAD=hand, one hand split-K pass (dr_din_mlp_wgrad: correct, but
-# 0.38 + 0.035 ms against the library's ≈ 0.25 at DIN's cap = 409 600 -- its
-# per-position LDS reads bound it; profiles/r05_din_wgrad.log)
-_DIN_WGRAD_HAND = os.environ.get("DR_DIN_WGRAD", "lib") == "hand"
+# the attention MLP's weight gradients: one hand split-K pass on the matrix
+# cores (dr_din_mlp_wgrad, default: 0.18 + 0.009 ms at DIN's cap = 409 600)
+# or, DR_DIN_WGRAD=lib, library GEMMs + reductions (≈ 0.25 ms;
+# profiles/r05_din_wgrad.log)
+_DIN_WGRAD_HAND = os.environ.get("DR_DIN_WGRAD", "hand") == "hand"
 
 
 def din_mlp_backward(query, facts, w1, w3, buf, grad_scores, grad_facts):

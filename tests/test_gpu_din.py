@@ -197,10 +197,9 @@ def test_din_fused_attention_matches_fp64(B, T, H, prefix, wgrad, monkeypatch):
     every gradient (query, facts, the three layers' weights and biases)
     against torch fp64 autograd of the reference composition (utils.py:
     264-309), prefix masks (zero-padded histories, a fully masked row) and
-    arbitrary 0/1 masks.  Weight gradients both ways: library GEMMs (the
-    default) and the hand split-K pass (dr_din_mlp_wgrad, DR_DIN_WGRAD=hand,
-    on the matrix cores or, DR_DIN_WGRAD_VALU=1, the VALU; used when cap % 4
-    == 0)."""
+    arbitrary 0/1 masks.  Weight gradients every way: the hand split-K pass
+    (dr_din_mlp_wgrad, the default when cap % 4 == 0) on the matrix cores or,
+    DR_DIN_WGRAD_VALU=1, the VALU, and library GEMMs (DR_DIN_WGRAD=lib)."""
     from deeprec_amd import modelzoo as mz
     from deeprec_amd import ops
     monkeypatch.setattr(ops, "_DIN_WGRAD_HAND", wgrad != "lib")
