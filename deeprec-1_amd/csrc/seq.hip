@@ -1087,7 +1087,8 @@ int dr_din_mlp_wgrad(const float* da1t, const float* xt, const float* da2t, cons
   int nbk = mfma ? 768 : 512;
   if (be && atoi(be) > 0) nbk = atoi(be) < kWgradBlocks ? atoi(be) : kWgradBlocks;
   int64_t per = (cap + nbk - 1) / nbk;
-  per = (per + DW_CH - 1) / DW_CH * DW_CH;
+  const int pr = mfma ? ch : DW_CH;   // whole chunks per block
+  per = (per + pr - 1) / pr * pr;
   const int nb = (int)((cap + per - 1) / per);
   float* part = static_cast<float*>(ws);
   hipStream_t s = S(stream);
