@@ -772,7 +772,7 @@ __global__ __launch_bounds__(1024) void din_wgrad_reduce_kernel(const float* __r
 // position p + l / 16).
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 template <int H2, int N1, int N2, int CH>
-__global__ __launch_bounds__(256) void din_wgrad_mfma_kernel(
+__global__ __launch_bounds__(256, 3) void din_wgrad_mfma_kernel(
     const float* __restrict__ da1t, const float* __restrict__ xt, const float* __restrict__ da2t,
     const float* __restrict__ h1t, const float* __restrict__ h2t, const float* __restrict__ dsc,
     int64_t cap, int64_t per, float* __restrict__ part) {
@@ -808,7 +808,7 @@ __global__ __launch_bounds__(256) void din_wgrad_mfma_kernel(
     // 16-B aligned: cap % 4 == 0, c0 % 4 == 0) -- two round trips to HBM per
     // 64-position chunk, not one per operand and 1024 vectors
     {
-      constexpr int NQ = OS + 1, NV = NQ * (CH / 4), SU = 8;
+      constexpr int NQ = OS + 1, NV = NQ * (CH / 4), SU = CH == 32 ? 10 : 8;
       for (int e0 = 0; e0 < NV; e0 += 256 * SU) {
         float4 v[SU];
 #pragma unroll
@@ -1067,7 +1067,8 @@ int dr_din_mlp_wgrad(const float* da1t, const float* xt, const float* da2t, cons
   const char* ve = getenv("DR_DIN_WGRAD_VALU");
   const bool mfma = !(ve && atoi(ve) != 0);
   // positions staged per chunk by the matrix-core form: 32 (three blocks per
-  // CU, so one block's loads overlap the others' MFMAs) or 64
+  // CU, so one block's loads overlap the others' MFMAs) or 64 (24: 0.184 ms
+  // against 32's 0.160, profiles/r05_din_wgrad.log)
   const char* ce = getenv("DR_DIN_WGRAD_CH");
   const int ch = ce && atoi(ce) == 64 ? 64 : 32;
   DR_REQUIRE(cap >= 1 && n1 == 80 && n2 == 40 &&

@@ -899,7 +899,7 @@ def din_mlp_forward(query, facts, mask, w1, b1, w2, b2, w3, b3):
 
 
 # the attention MLP's weight gradients: one hand split-K pass on the matrix
-# cores (dr_din_mlp_wgrad, default: 0.18 + 0.009 ms at DIN's cap = 409 600)
+# cores (dr_din_mlp_wgrad, default: 0.16 + 0.008 ms at DIN's cap = 409 600)
 # or, DR_DIN_WGRAD=lib, library GEMMs + reductions (≈ 0.25 ms;
 # profiles/r05_din_wgrad.log)
 _DIN_WGRAD_HAND = os.environ.get("DR_DIN_WGRAD", "hand") == "hand"
