@@ -474,8 +474,9 @@ __global__ __launch_bounds__(256) void din_mlp_fwd_kernel(
 // backward: one lane per position p < cap.  p < P: the MLP backward from the
 // score gradient; the facts gradient (already holding the pool's) gains
 // d f + q * d(q f); per-position buffers for the weight-gradient GEMMs and the
-// per-sample sums.  P <= p < cap: zero columns of every buffer the weight-
-// gradient GEMMs read (they run over cap; the forward wrote only p < P).
+// per-sample sums.  P <= p < cap, when zero_tail: zero columns of every buffer
+// the library weight-gradient GEMMs read (they run over cap; the forward wrote
+// only p < P) -- 1.25 KB per position the hand pass (bounded by P) skips.
 template <int H, int N1, int N2>
 __global__ __launch_bounds__(256) void din_mlp_bwd_kernel(
     const int32_t* __restrict__ pos, const int32_t* __restrict__ off, int64_t B, int64_t T,
@@ -484,7 +485,7 @@ __global__ __launch_bounds__(256) void din_mlp_bwd_kernel(
     const float* __restrict__ gscores, float* __restrict__ h1t,
     float* __restrict__ h2t, float* __restrict__ gfacts, float* __restrict__ da1t,
     float* __restrict__ da2t, float* __restrict__ xt, float* __restrict__ dsc,
-    float* __restrict__ dqp) {
+    float* __restrict__ dqp, int zero_tail) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t P = off[B];
   __shared__ __attribute__((aligned(16))) float sw[N1 * 2 * H + N1 * N2];
@@ -492,6 +493,7 @@ __global__ __launch_bounds__(256) void din_mlp_bwd_kernel(
     din_stage_weights<H, N1, N2>(sw, w1p, w2t);
   if (p >= cap) return;
   if (p >= P) {
+    if (!zero_tail) return;   // the hand weight-gradient pass stops at P itself
 #pragma unroll 8
     for (int j = 0; j < N1; ++j) da1t[(int64_t)j * cap + p] = h1t[(int64_t)j * cap + p] = 0.f;
 #pragma unroll 8
@@ -620,7 +622,7 @@ template <int H2, int CW, int N1, int N2>
 __global__ __launch_bounds__(256) void din_wgrad_kernel(
     const float* __restrict__ da1t, const float* __restrict__ xt, const float* __restrict__ da2t,
     const float* __restrict__ h1t, const float* __restrict__ h2t, const float* __restrict__ dsc,
-    int64_t cap, int64_t per, float* __restrict__ part) {
+    int64_t cap, int64_t per, const int32_t* __restrict__ valid, float* __restrict__ part) {
   static_assert(N1 == 80 && N2 == 40 && H2 % CW == 0 && 20 * (H2 / CW) <= 256, "tile shape");
   constexpr int GOUT = N1 * H2, WOUT = N2 * N1, OUT = GOUT + WOUT + 2 * N2 + 1;
   constexpr int RA = N1, RX = H2, RD = N2, RH = N1, RG = N2;     // rows per position
@@ -628,8 +630,15 @@ __global__ __launch_bounds__(256) void din_wgrad_kernel(
   constexpr int ROW = (OS + 1 + 3) / 4 * 4;                       // floats per staged position (16-B rows)
   __shared__ __attribute__((aligned(16))) float st[DW_CH * ROW];
   const int tid = threadIdx.x;
+  // positions [0, lim): cap, or the valid count P read on the device (the
+  // blocks then split P in whole chunks; no host read, capturable)
+  int64_t lim = cap;
+  if (valid) {
+    lim = *valid;
+    per = ((lim + gridDim.x - 1) / gridDim.x + DW_CH - 1) / DW_CH * DW_CH;
+  }
   const int64_t p0 = (int64_t)blockIdx.x * per;
-  const int64_t p1 = p0 + per < cap ? p0 + per : cap;
+  const int64_t p1 = p0 + per < lim ? p0 + per : lim;
   constexpr int NG = 20 * (H2 / CW);
   const bool tg = tid < NG;
   const int gi = (tid / (H2 / CW)) * 4, gj = (tid % (H2 / CW)) * CW;
@@ -775,7 +784,7 @@ template <int H2, int N1, int N2, int CH>
 __global__ __launch_bounds__(256, 3) void din_wgrad_mfma_kernel(
     const float* __restrict__ da1t, const float* __restrict__ xt, const float* __restrict__ da2t,
     const float* __restrict__ h1t, const float* __restrict__ h2t, const float* __restrict__ dsc,
-    int64_t cap, int64_t per, float* __restrict__ part) {
+    int64_t cap, int64_t per, const int32_t* __restrict__ valid, float* __restrict__ part) {
   static_assert(N1 == 80 && N2 == 40, "tile shape");
   constexpr int NT = (H2 + 15) / 16;
   constexpr int GT = 5 * NT, WT = 15, XT = 5, TT = GT + WT + XT;
@@ -791,8 +800,15 @@ __global__ __launch_bounds__(256, 3) void din_wgrad_mfma_kernel(
   __shared__ __attribute__((aligned(16))) float st[CH * ROW];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // positions [0, lim): cap, or the valid count P read on the device (the
+  // blocks then split P in whole chunks; no host read, capturable)
+  int64_t lim = cap;
+  if (valid) {
+    lim = *valid;
+    per = ((lim + gridDim.x - 1) / gridDim.x + CH - 1) / CH * CH;
+  }
   const int64_t p0 = (int64_t)blockIdx.x * per;
-  const int64_t p1 = p0 + per < cap ? p0 + per : cap;
+  const int64_t p1 = p0 + per < lim ? p0 + per : lim;
   const int li = lane & 15, lk = lane >> 4;
   f32x4v acc[TPW];
 #pragma unroll
@@ -1062,6 +1078,14 @@ size_t dr_din_mlp_wgrad_workspace_size(int n1, int hidden2, int n2) {
 int dr_din_mlp_wgrad(const float* da1t, const float* xt, const float* da2t, const float* h1t,
                      const float* h2t, const float* dsc, int64_t cap, int n1, int hidden2, int n2,
                      float* out, void* ws, size_t ws_bytes, void* stream) {
+  return dr_din_mlp_wgrad_valid(da1t, xt, da2t, h1t, h2t, dsc, cap, nullptr, n1, hidden2, n2, out,
+                                ws, ws_bytes, stream);
+}
+
+int dr_din_mlp_wgrad_valid(const float* da1t, const float* xt, const float* da2t,
+                           const float* h1t, const float* h2t, const float* dsc, int64_t cap,
+                           const int32_t* valid, int n1, int hidden2, int n2, float* out, void* ws,
+                           size_t ws_bytes, void* stream) {
   using namespace dr;
   // the matrix-core form unless DR_DIN_WGRAD_VALU=1 (read per call)
   const char* ve = getenv("DR_DIN_WGRAD_VALU");
@@ -1097,13 +1121,13 @@ int dr_din_mlp_wgrad(const float* da1t, const float* xt, const float* da2t, cons
   do {                                                                                        \
     if (mfma && ch == 32)                                                                     \
       hipLaunchKernelGGL((din_wgrad_mfma_kernel<H2, 80, 40, 32>), dim3((unsigned)nb), dim3(256),  \
-                         0, s, da1t, xt, da2t, h1t, h2t, dsc, cap, per, part);                \
+                         0, s, da1t, xt, da2t, h1t, h2t, dsc, cap, per, valid, part);                \
     else if (mfma)                                                                            \
       hipLaunchKernelGGL((din_wgrad_mfma_kernel<H2, 80, 40, 64>), dim3((unsigned)nb), dim3(256),  \
-                         0, s, da1t, xt, da2t, h1t, h2t, dsc, cap, per, part);                \
+                         0, s, da1t, xt, da2t, h1t, h2t, dsc, cap, per, valid, part);                \
     else                                                                                      \
       hipLaunchKernelGGL((din_wgrad_kernel<H2, CW, 80, 40>), dim3((unsigned)nb), dim3(256), 0, \
-                         s, da1t, xt, da2t, h1t, h2t, dsc, cap, per, part);                   \
+                         s, da1t, xt, da2t, h1t, h2t, dsc, cap, per, valid, part);                   \
   } while (0)
   if (hidden2 == 72) DR_WG(72, 6);
   else if (hidden2 == 64) DR_WG(64, 8);
@@ -1119,6 +1143,14 @@ int dr_din_mlp_wgrad(const float* da1t, const float* xt, const float* da2t, cons
 int dr_din_mlp_backward(const float* query, const float* facts, int64_t batch, int64_t seq_len,
                         int hidden, int n1, int n2, const float* w3, const float* grad_scores,
                         float* grad_facts, const dr_din_mlp_buf* buf, void* stream) {
+  return dr_din_mlp_backward_tail(query, facts, batch, seq_len, hidden, n1, n2, w3, grad_scores,
+                                  grad_facts, buf, 1, stream);
+}
+
+int dr_din_mlp_backward_tail(const float* query, const float* facts, int64_t batch,
+                             int64_t seq_len, int hidden, int n1, int n2, const float* w3,
+                             const float* grad_scores, float* grad_facts,
+                             const dr_din_mlp_buf* buf, int zero_tail, void* stream) {
   using namespace dr;
   DR_REQUIRE(batch >= 0 && seq_len >= 1 && buf && n1 == 80 && n2 == 40 &&
                  (hidden == 16 || hidden == 32 || hidden == 36 || hidden == 64),
@@ -1136,7 +1168,7 @@ int dr_din_mlp_backward(const float* query, const float* facts, int64_t batch, i
     hipLaunchKernelGGL((din_mlp_bwd_kernel<HH, 80, 40>), dim3(pb), dim3(256), 0, st, buf->pos,   \
                        buf->off, batch, seq_len, cap, facts, query, buf->w1p, buf->w2t, w3,     \
                        grad_scores, buf->h1t, buf->h2t, grad_facts, buf->da1t, buf->da2t,       \
-                       buf->xt, buf->dsc, buf->dqp);                                            \
+                       buf->xt, buf->dsc, buf->dqp, zero_tail);                                 \
     hipLaunchKernelGGL((din_mlp_sample_kernel<HH, 80>), dim3(sb), dim3(256), 0, st, buf->off,    \
                        batch, cap, buf->da1t, buf->dqp, buf->s1, buf->dq2);                     \
   }

@@ -298,8 +298,12 @@ SIGNATURES = {
     "dr_din_mlp_forward": (_I32, [_P, _P, _P, _I64, _I64, _I32, _P, _P, _I32, _P, _P, _I32, _P,
                                   _P, _P, _P, _P]),
     "dr_din_mlp_backward": (_I32, [_P, _P, _I64, _I64, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
+    "dr_din_mlp_backward_tail": (_I32, [_P, _P, _I64, _I64, _I32, _I32, _I32, _P, _P, _P, _P,
+                                        _I32, _P]),
     "dr_din_mlp_wgrad_workspace_size": (_SZ, [_I32, _I32, _I32]),
     "dr_din_mlp_wgrad": (_I32, [_P, _P, _P, _P, _P, _P, _I64, _I32, _I32, _I32, _P, _P, _SZ, _P]),
+    "dr_din_mlp_wgrad_valid": (_I32, [_P, _P, _P, _P, _P, _P, _I64, _P, _I32, _I32, _I32, _P, _P,
+                                      _SZ, _P]),
     "dr_fingerprint64": (_I32, [_P, _P, _I64, _P, _P]),
     "dr_string_to_hash_bucket_fast": (_I32, [_P, _P, _I64, _I64, _P, _P]),
     "dr_crc32c_extend": (C.c_uint32, [C.c_uint32, _P, _SZ]),

@@ -899,7 +899,8 @@ def din_mlp_forward(query, facts, mask, w1, b1, w2, b2, w3, b3):
 
 
 # the attention MLP's weight gradients: one hand split-K pass on the matrix
-# cores (dr_din_mlp_wgrad, default: 0.16 + 0.008 ms at DIN's cap = 409 600)
+# cores (dr_din_mlp_wgrad_valid over the valid positions, default: 0.085 + 0.008
+# ms at DIN's configs[3])
 # or, DR_DIN_WGRAD=lib, library GEMMs + reductions (≈ 0.25 ms;
 # profiles/r05_din_wgrad.log)
 _DIN_WGRAD_HAND = os.environ.get("DR_DIN_WGRAD", "hand") == "hand"
@@ -908,8 +909,9 @@ _DIN_WGRAD_HAND = os.environ.get("DR_DIN_WGRAD", "hand") == "hand"
 def din_mlp_backward(query, facts, w1, w3, buf, grad_scores, grad_facts):
     """Backward of din_mlp_forward: adds the MLP's part to grad_facts (in
     place) and returns (grad_query, dW1, db1, dW2, db2, dw3, db3); the weight
-    gradients are split-K GEMMs over the feature-major per-position buffers
-    (columns past the valid count are zero)."""
+    gradients come from the feature-major per-position buffers: one hand pass
+    bounded by the valid count, or library split-K GEMMs over cap (for which
+    the backward zeroes the columns past the valid count)."""
     dev = _dev(facts)
     B, T, H = facts.shape
     n1, n2, cap = buf.n1, buf.n2, buf.cap
@@ -920,8 +922,12 @@ def din_mlp_backward(query, facts, w1, w3, buf, grad_scores, grad_facts):
         raise ValueError("grad_facts must be a contiguous fp32 tensor")
     buf.alloc_backward(dev)
     st = buf.struct()
-    check(lib().dr_din_mlp_backward(ptr(q), ptr(f), B, T, H, n1, n2, ptr(w3c), ptr(gs),
-                                    ptr(grad_facts), C.byref(st), stream_handle(dev)))
+    hand = _DIN_WGRAD_HAND and 2 * H in (32, 64, 72, 128) and (n1, n2) == (80, 40) and cap % 4 == 0
+    # the hand pass stops at the valid count P itself: the columns p >= P of
+    # the per-position buffers stay unwritten (1.25 KB per position less)
+    check(lib().dr_din_mlp_backward_tail(ptr(q), ptr(f), B, T, H, n1, n2, ptr(w3c), ptr(gs),
+                                         ptr(grad_facts), C.byref(st), 0 if hand else 1,
+                                         stream_handle(dev)))
     _post(dev)
     S = 64
     while S > 1 and cap % S:
@@ -937,15 +943,16 @@ def din_mlp_backward(query, facts, w1, w3, buf, grad_scores, grad_facts):
     gq = buf.s1 @ (A + Cm) + buf.dq2
     Gq = buf.s1.t() @ q
     db1 = buf.s1.sum(0)
-    if _DIN_WGRAD_HAND and 2 * H in (32, 64, 72, 128) and (n1, n2) == (80, 40) and cap % 4 == 0:
+    if hand:
         # one split-K pass for G, dW2, db2, dw3, db3 (dr_din_mlp_wgrad)
         gout, wout = n1 * 2 * H, n2 * n1
         out = torch.empty(gout + wout + 2 * n2 + 1, dtype=torch.float32, device=dev)
         wsb = lib().dr_din_mlp_wgrad_workspace_size(n1, 2 * H, n2)
         ws = workspace(wsb, dev)
-        check(lib().dr_din_mlp_wgrad(ptr(buf.da1t), ptr(buf.xt), ptr(buf.da2t), ptr(buf.h1t),
-                                     ptr(buf.h2t), ptr(buf.dsc), cap, n1, 2 * H, n2, ptr(out),
-                                     ptr(ws), wsb, stream_handle(dev)))
+        check(lib().dr_din_mlp_wgrad_valid(ptr(buf.da1t), ptr(buf.xt), ptr(buf.da2t),
+                                           ptr(buf.h1t), ptr(buf.h2t), ptr(buf.dsc), cap,
+                                           ptr(buf.off[B:]), n1, 2 * H, n2, ptr(out), ptr(ws), wsb,
+                                           stream_handle(dev)))
         _post(dev)
         G = out[:gout].view(n1, 2 * H)
         dW2 = out[gout:gout + wout].view(n2, n1)

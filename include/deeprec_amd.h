@@ -1151,9 +1151,22 @@ size_t dr_din_mlp_wgrad_workspace_size(int n1, int hidden2, int n2);
 int dr_din_mlp_wgrad(const float* da1t, const float* xt, const float* da2t, const float* h1t,
                      const float* h2t, const float* dsc, int64_t cap, int n1, int hidden2, int n2,
                      float* out, void* ws, size_t ws_bytes, void* stream);
+/* The same over the valid positions only: valid = a device int32 (the       */
+/* buffer's off[batch] = P), read on the device, so the columns p >= P need  */
+/* not be zero (dr_din_mlp_backward_tail with zero_tail = 0 skips them).      */
+int dr_din_mlp_wgrad_valid(const float* da1t, const float* xt, const float* da2t,
+                           const float* h1t, const float* h2t, const float* dsc, int64_t cap,
+                           const int32_t* valid, int n1, int hidden2, int n2, float* out, void* ws,
+                           size_t ws_bytes, void* stream);
 int dr_din_mlp_backward(const float* query, const float* facts, int64_t batch, int64_t seq_len,
                         int hidden, int n1, int n2, const float* w3, const float* grad_scores,
                         float* grad_facts, const dr_din_mlp_buf* buf, void* stream);
+/* dr_din_mlp_backward with the zeroing of the buffers' columns p >= P       */
+/* optional (zero_tail = 0: only dr_din_mlp_wgrad_valid reads them after).    */
+int dr_din_mlp_backward_tail(const float* query, const float* facts, int64_t batch,
+                             int64_t seq_len, int hidden, int n1, int n2, const float* w3,
+                             const float* grad_scores, float* grad_facts,
+                             const dr_din_mlp_buf* buf, int zero_tail, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* String -> id, the step before the lookup.  Strings are one byte buffer    */
