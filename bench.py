@@ -43,7 +43,7 @@ def parse():
     p.add_argument("--batch", type=int, default=65536, help="per-GPU batch (B_local)")
     p.add_argument("--zipf", type=float, default=0.0, help="0 = uniform keys")
     p.add_argument("--no-graph", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-seconds", type=float, default=18.0)
     p.add_argument("--cpu-rows", type=int, default=12_500_000)
     p.add_argument("--check-rows", type=int, default=8192,
                    help="sampled output rows checked bit-exactly after the timed region")
@@ -117,8 +117,12 @@ def cpu_baseline(args):
     """DeepRec-CPU-semantics restatement (oracle/) timed on the host cores:
     Unique -> KvResourceGather (EV hash lookup + row memcpy, Shard over
     threads) -> SparseSegmentSum, per feature, h = 1, on one table of the
-    GPU's per-table shape (rows x dim).  Threads: the box's CPU share
-    (OMP_NUM_THREADS, else the affinity mask)."""
+    GPU's per-table shape (rows x dim), on a persistent worker pool (TF's
+    CPU worker threads).  Unique is UniqueAliOp's default: ParallelComputeV1
+    for N >= 14336 (unique_ali_op_util.h:651-657; serial_ = false,
+    unique_ali_op.cc:55-56); the serial-Unique variant is timed beside it.
+    Three timed repeats each (median reported, min / max as the spread).
+    Threads: the box's CPU share (OMP_NUM_THREADS, else the affinity mask)."""
     from oracle import oracle as orc
     threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
     D, R = args.dim, args.cpu_rows
@@ -132,23 +136,49 @@ def cpu_baseline(args):
     seg_off = np.arange(B + 1, dtype=np.int32)
     out = np.empty((B, D), np.float32)
     L = orc.lib()
-    done, t0 = 0, time.perf_counter()
-    while True:
-        ids = rng.integers(0, R, B).astype(np.int64)
-        rc = L.orc_pipeline_ev_lookup_sparse(ev._h, orc._p(ids), B, orc._p(seg_off), B, 0,
-                                             threads, orc._p(out))
-        assert rc == 0
-        done += B
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds:
-            break
-    return {"value": done / el, "unit": "lookups/s", "cores": threads, "kind": "port",
+    pool = orc.Pool(threads)
+    reps = 3
+    per = args.cpu_seconds / (2 * reps)
+
+    def timed(serial):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            ids = rng.integers(0, R, B).astype(np.int64)
+            rc = L.orc_pipeline_ev_lookup_sparse_pool(pool._h, ev._h, orc._p(ids), B,
+                                                      orc._p(seg_off), B, 0, int(serial),
+                                                      orc._p(out))
+            assert rc == 0
+            done += B
+            el = time.perf_counter() - t0
+            if el >= per:
+                return done / el, done
+    per0 = per
+    per = min(0.5, per0)
+    timed(False)   # warm-up: first touch of the pool's and the maps' pages
+    timed(True)
+    per = per0
+    runs = {False: [], True: []}
+    total = 0
+    for _ in range(reps):   # interleaved, so drift hits both variants alike
+        for serial in (False, True):
+            v, n = timed(serial)
+            runs[serial].append(v)
+            total += n
+    pool.close()
+    med = {k: float(np.median(v)) for k, v in runs.items()}
+    return {"value": med[False], "unit": "lookups/s", "cores": pool.threads, "kind": "port",
+            "repeats": [round(v, 1) for v in runs[False]],
+            "spread": round((max(runs[False]) - min(runs[False])) / med[False], 4),
+            "serial_unique_value": med[True],
+            "serial_unique_repeats": [round(v, 1) for v in runs[True]],
             "nproc": os.cpu_count(), "cpu_model": _cpu_model(),
             "sample": "%d lookups (features of B=%d ids, h=1) over a %d-key x %d-dim fp32 EV "
-                      "(one table of the GPU's per-table shape), %.1f s on %d threads, "
-                      "oracle/deeprec_oracle.c orc_pipeline_ev_lookup_sparse (serial Unique + "
-                      "Shard-split KvResourceGather + ali SparseSegmentSum)"
-                      % (done, B, R, D, el, threads)}
+                      "(one table of the GPU's per-table shape), %d x %.1f s per variant on a "
+                      "persistent %d-thread pool, oracle/deeprec_oracle.c "
+                      "orc_pipeline_ev_lookup_sparse_pool (UniqueAliOp's default parallel "
+                      "Unique + Shard-split KvResourceGather + ali SparseSegmentSum; value = "
+                      "median of the repeats, spread = (max - min) / median)"
+                      % (total, B, R, D, reps, per, pool.threads)}
 
 
 def synth_rows(seed, keys, D):

@@ -1293,6 +1293,321 @@ int orc_pipeline_dense_lookup_sparse(const float* table, int64_t D, const int64_
 }
 
 /* ------------------------------------------------------------------------ */
+/* Persistent worker pool: TF's per-device CPU worker threads               */
+/* (tensorflow_cpu_worker_threads()->workers, the pool Shard and the Unique  */
+/* op's TaskRunner hand their tasks to), created once, not per call.         */
+/* orc_pool_run(pool, fn, arg, ntasks) runs fn(arg, id, ntasks) for every    */
+/* id in [0, ntasks) on the workers and returns when all have finished.      */
+/* ------------------------------------------------------------------------ */
+typedef void (*orc_task_fn)(void* arg, int id, int ntasks);
+typedef struct {
+  int n;
+  pthread_t th[256];
+  pthread_mutex_t mu;
+  pthread_cond_t cv_work, cv_done;
+  orc_task_fn fn;
+  void* arg;
+  int ntasks, next, pending, quit;
+} orc_pool;
+
+static void* orc_pool_main(void* p) {
+  orc_pool* pl = (orc_pool*)p;
+  pthread_mutex_lock(&pl->mu);
+  for (;;) {
+    while (!pl->quit && pl->next >= pl->ntasks) pthread_cond_wait(&pl->cv_work, &pl->mu);
+    if (pl->quit) break;
+    const int id = pl->next++;
+    orc_task_fn fn = pl->fn;
+    void* arg = pl->arg;
+    const int nt = pl->ntasks;
+    pthread_mutex_unlock(&pl->mu);
+    fn(arg, id, nt);
+    pthread_mutex_lock(&pl->mu);
+    if (--pl->pending == 0) pthread_cond_signal(&pl->cv_done);
+  }
+  pthread_mutex_unlock(&pl->mu);
+  return NULL;
+}
+
+orc_pool* orc_pool_create(int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  orc_pool* pl = (orc_pool*)calloc(1, sizeof(orc_pool));
+  if (!pl) return NULL;
+  pthread_mutex_init(&pl->mu, NULL);
+  pthread_cond_init(&pl->cv_work, NULL);
+  pthread_cond_init(&pl->cv_done, NULL);
+  for (int t = 0; t < threads; ++t) {
+    if (pthread_create(&pl->th[t], NULL, orc_pool_main, pl) != 0) break;
+    pl->n = t + 1;
+  }
+  return pl;
+}
+
+int orc_pool_threads(const orc_pool* pl) { return pl ? pl->n : 0; }
+
+void orc_pool_free(orc_pool* pl) {
+  if (!pl) return;
+  pthread_mutex_lock(&pl->mu);
+  pl->quit = 1;
+  pthread_cond_broadcast(&pl->cv_work);
+  pthread_mutex_unlock(&pl->mu);
+  for (int t = 0; t < pl->n; ++t) pthread_join(pl->th[t], NULL);
+  pthread_cond_destroy(&pl->cv_work);
+  pthread_cond_destroy(&pl->cv_done);
+  pthread_mutex_destroy(&pl->mu);
+  free(pl);
+}
+
+static void orc_pool_run(orc_pool* pl, orc_task_fn fn, void* arg, int ntasks) {
+  if (ntasks <= 0) return;
+  if (ntasks == 1 || pl->n <= 0) {   /* one task: inline, as Shard does below its cost cut */
+    for (int i = 0; i < ntasks; ++i) fn(arg, i, ntasks);
+    return;
+  }
+  pthread_mutex_lock(&pl->mu);
+  pl->fn = fn;
+  pl->arg = arg;
+  pl->next = 0;
+  pl->pending = ntasks;
+  pl->ntasks = ntasks;
+  pthread_cond_broadcast(&pl->cv_work);
+  while (pl->pending > 0) pthread_cond_wait(&pl->cv_done, &pl->mu);
+  pl->ntasks = pl->next = 0;
+  pthread_mutex_unlock(&pl->mu);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Parallel first-occurrence Unique: ParallelComputeV1                       */
+/* (unique_ali_op_util.h:226-445), the default of UniqueAliOp (serial_ =     */
+/* false, unique_ali_op.cc:55-56) for N >= kPartitionLimit = 14336           */
+/* (unique_ali_op_util.h:48, :651-657).  Four steps:                          */
+/*  1. T1 = max(min(threads, cbrt(10 threads) + 1), 1) sections, one local    */
+/*     hash map (key -> local position, insertion order) per section;       */
+/*  2. T2 = max(min(threads, ceil(sum_i size_i * i / 8192)), 1) tasks mark    */
+/*     each key of map l that an earlier map p < l holds (prior maps in      */
+/*     ascending order, so the owner is always the earliest map's node) and  */
+/*     count the duplicates;                                                 */
+/*  3. per map, global indices from the prefix of the non-duplicate counts,  */
+/*     the keys written at them;                                             */
+/*  4. idx[i] = the global index of the node (or its owner) of x[i] in its   */
+/*     section's map, T4 = max(min(threads, ceil(N / 8192)), 1) tasks.       */
+/* The result equals SerialComputeV1's (first occurrence over the whole     */
+/* input), which tests/test_oracle_golden.py checks against orc_unique.      */
+/* ------------------------------------------------------------------------ */
+typedef struct {         /* INode (unique_ali_op_util.h:230-237) */
+  int64_t key;
+  int64_t index;         /* local, then global index */
+  int64_t owner;         /* -1, or (map << 32) | position of the earliest map's node */
+} orc_inode;
+
+typedef struct {
+  int64_t lo, hi;        /* section of the input */
+  int64_t cap;           /* open-addressing table: slot -> local position or -1 */
+  int64_t* slot;
+  orc_inode* node;       /* in insertion order */
+  int64_t size;
+} orc_submap;
+
+static int64_t orc_submap_find(const orc_submap* m, int64_t k) {
+  uint64_t h = orc_mix64((uint64_t)k) & (uint64_t)(m->cap - 1);
+  for (;;) {
+    const int64_t j = m->slot[h];
+    if (j < 0) return -1;
+    if (m->node[j].key == k) return j;
+    h = (h + 1) & (uint64_t)(m->cap - 1);
+  }
+}
+
+typedef struct {
+  const int64_t* x;
+  int64_t n;
+  orc_submap* maps;
+  int t1, t2;
+  int64_t* dups;         /* [T1 * T2] */
+  int64_t* goff;         /* [T1] */
+  int64_t* y;
+  int32_t* idx;
+} orc_punique;
+
+static void orc_pu_build(void* a, int id, int nt) {
+  orc_punique* u = (orc_punique*)a;
+  orc_submap* m = &u->maps[id];
+  (void)nt;
+  const int64_t n = m->hi - m->lo;
+  m->cap = 16;
+  while (m->cap < 2 * n) m->cap <<= 1;
+  m->slot = (int64_t*)malloc(sizeof(int64_t) * m->cap);
+  m->node = (orc_inode*)malloc(sizeof(orc_inode) * (n > 0 ? n : 1));
+  for (int64_t s = 0; s < m->cap; ++s) m->slot[s] = -1;
+  m->size = 0;
+  for (int64_t i = m->lo; i < m->hi; ++i) {
+    const int64_t k = u->x[i];
+    uint64_t h = orc_mix64((uint64_t)k) & (uint64_t)(m->cap - 1);
+    for (;;) {
+      const int64_t j = m->slot[h];
+      if (j < 0) {
+        m->slot[h] = m->size;
+        m->node[m->size].key = k;
+        m->node[m->size].index = m->size;
+        m->node[m->size].owner = -1;
+        m->size++;
+        break;
+      }
+      if (m->node[j].key == k) break;
+      h = (h + 1) & (uint64_t)(m->cap - 1);
+    }
+  }
+}
+
+/* Partitioner (unique_ali_op_util.h:103-116): part i = (work + i) / parts   */
+static void orc_part(int64_t work, int parts, int i, int64_t* lo, int64_t* hi) {
+  int64_t s = 0;
+  for (int j = 0; j < i; ++j) s += (work + j) / parts;
+  *lo = s;
+  *hi = s + (work + i) / parts;
+}
+
+static void orc_pu_dedup(void* a, int task, int nt) {
+  orc_punique* u = (orc_punique*)a;
+  for (int p = 0; p < u->t1 - 1; ++p) {
+    const orc_submap* prior = &u->maps[p];
+    for (int l = p + 1; l < u->t1; ++l) {
+      orc_submap* lat = &u->maps[l];
+      int64_t lo, hi, d = 0;
+      orc_part(lat->size, nt, task, &lo, &hi);
+      for (int64_t i = lo; i < hi; ++i) {
+        if (lat->node[i].owner >= 0) continue;
+        const int64_t j = orc_submap_find(prior, lat->node[i].key);
+        if (j < 0) continue;
+        /* GetINodeByPos: the prior node, or the node it defers to */
+        lat->node[i].owner = prior->node[j].owner >= 0 ? prior->node[j].owner
+                                                       : ((int64_t)p << 32) | j;
+        ++d;
+      }
+      u->dups[l * nt + task] += d;   /* one store per (map, task): no shared line in the loop */
+    }
+  }
+}
+
+static void orc_pu_index(void* a, int id, int nt) {
+  orc_punique* u = (orc_punique*)a;
+  orc_submap* m = &u->maps[id];
+  (void)nt;
+  int64_t cur = u->goff[id];
+  for (int64_t i = 0; i < m->size; ++i) {
+    if (m->node[i].owner >= 0) continue;
+    m->node[i].index = cur;
+    u->y[cur] = m->node[i].key;
+    ++cur;
+  }
+}
+
+static void orc_pu_output(void* a, int task, int nt) {
+  orc_punique* u = (orc_punique*)a;
+  int64_t lo, hi;
+  orc_part(u->n, nt, task, &lo, &hi);
+  int mi = 0;
+  for (int64_t i = lo; i < hi; ++i) {
+    while (i >= u->maps[mi].hi) ++mi;
+    const orc_submap* m = &u->maps[mi];
+    const int64_t j = orc_submap_find(m, u->x[i]);
+    const int64_t o = m->node[j].owner;
+    u->idx[i] = (int32_t)(o < 0 ? m->node[j].index : u->maps[o >> 32].node[o & 0xffffffff].index);
+  }
+}
+
+int64_t orc_unique_parallel(orc_pool* pool, const int64_t* x, int64_t n, int64_t* y,
+                            int32_t* idx) {
+  if (n <= 0) return 0;
+  const int threads = pool ? pool->n : 1;
+  int t1 = (int)(cbrt(10.0 * threads) + 1);
+  if (t1 > threads) t1 = threads;
+  if (t1 < 1) t1 = 1;
+  orc_punique u;
+  memset(&u, 0, sizeof(u));
+  u.x = x;
+  u.n = n;
+  u.y = y;
+  u.idx = idx;
+  u.t1 = t1;
+  u.maps = (orc_submap*)calloc((size_t)t1, sizeof(orc_submap));
+  for (int i = 0; i < t1; ++i) orc_part(n, t1, i, &u.maps[i].lo, &u.maps[i].hi);
+  orc_pool_run(pool, orc_pu_build, &u, t1);
+  int64_t cost = 0;
+  for (int i = 0; i < t1; ++i) cost += u.maps[i].size * i;
+  int t2 = (int)((cost + 8191) / 8192);
+  if (t2 > threads) t2 = threads;
+  if (t2 < 1) t2 = 1;
+  u.t2 = t2;
+  u.dups = (int64_t*)calloc((size_t)t1 * t2, sizeof(int64_t));
+  orc_pool_run(pool, orc_pu_dedup, &u, t2);
+  u.goff = (int64_t*)calloc((size_t)t1, sizeof(int64_t));
+  for (int i = 0; i + 1 < t1; ++i) {
+    u.goff[i + 1] = u.goff[i] + u.maps[i].size;
+    for (int j = 0; j < t2; ++j) u.goff[i + 1] -= u.dups[i * t2 + j];
+  }
+  int64_t total = u.goff[t1 - 1] + u.maps[t1 - 1].size;
+  for (int j = 0; j < t2; ++j) total -= u.dups[(t1 - 1) * t2 + j];
+  orc_pool_run(pool, orc_pu_index, &u, t1);
+  int t4 = (int)((n + 8191) / 8192);
+  if (t4 > threads) t4 = threads;
+  if (t4 < 1) t4 = 1;
+  orc_pool_run(pool, orc_pu_output, &u, t4);
+  for (int i = 0; i < t1; ++i) {
+    free(u.maps[i].slot); free(u.maps[i].node);
+  }
+  free(u.maps); free(u.dups); free(u.goff);
+  return total;
+}
+
+/* The cpu_baseline pipeline on the persistent pool: UniqueAliOp's dispatch  */
+/* (parallel for N >= 14336 unless serial, unique_ali_op_util.h:651-657) ->  */
+/* KvResourceGather (Shard over the workers, kv_variable_ops.cc:360-362) ->  */
+/* SparseSegmentReduction (threads - 1 shards over the output rows,          */
+/* segment_reduction_ali_ops_util.h:173-174).                                 */
+typedef struct {
+  orc_task proto;
+  int64_t total;
+  void* (*fn)(void*);
+} orc_shard;
+
+static void orc_shard_task(void* a, int id, int nt) {
+  orc_shard* s = (orc_shard*)a;
+  orc_task t = s->proto;
+  t.lo = s->total * id / nt;
+  t.hi = s->total * (id + 1) / nt;
+  s->fn(&t);
+}
+
+int orc_pipeline_ev_lookup_sparse_pool(orc_pool* pool, orc_ev* ev, const int64_t* ids,
+                                       int64_t nnz, const int32_t* seg_off, int64_t B,
+                                       int combiner, int serial_unique, float* out) {
+  if (!pool || !ev) return ORC_INVALID_ARGUMENT;
+  const int64_t D = ev->dim;
+  const int threads = pool->n;
+  int64_t* uniq = (int64_t*)malloc(sizeof(int64_t) * (nnz > 0 ? nnz : 1));
+  int32_t* idx = (int32_t*)malloc(sizeof(int32_t) * (nnz > 0 ? nnz : 1));
+  const int64_t U = (nnz >= 14336 && !serial_unique) ? orc_unique_parallel(pool, ids, nnz, uniq, idx)
+                                                      : orc_unique(ids, nnz, uniq, idx, NULL);
+  float* emb = (float*)malloc(sizeof(float) * (U > 0 ? U : 1) * D);
+  orc_shard s;
+  memset(&s, 0, sizeof(s));
+  s.proto.ev = ev; s.proto.keys = uniq; s.proto.out = emb;
+  s.total = U;
+  s.fn = orc_gather_worker;
+  orc_pool_run(pool, orc_shard_task, &s, U > 0 ? threads : 0);
+  memset(&s, 0, sizeof(s));
+  s.proto.ev = ev; s.proto.data = emb; s.proto.idx = idx; s.proto.seg_off = seg_off;
+  s.proto.combiner = combiner; s.proto.out = out;
+  s.total = B;
+  s.fn = orc_reduce_worker;
+  orc_pool_run(pool, orc_shard_task, &s, B > 0 ? (threads > 1 ? threads - 1 : 1) : 0);
+  free(uniq); free(idx); free(emb);
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------ */
 /* String -> id: StringToHashBucketFast (string_to_hash_bucket_ali_op.h:     */
 /* 33-63: bucket = Fingerprint64(s) % num_buckets) and the EV column's       */
 /* num_buckets = INT64_MAX (feature_column_v2.py:5954-5957).                 */

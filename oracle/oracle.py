@@ -82,6 +82,11 @@ def lib():
             "orc_string_to_hash_bucket_fast": (None, [p, p, i64, i64, p]),
             "orc_pipeline_ev_lookup_sparse": (i32, [p, p, i64, p, i64, i32, i32, p]),
             "orc_pipeline_dense_lookup_sparse": (i32, [p, i64, p, i64, p, i64, i32, i32, p]),
+            "orc_pool_create": (p, [i32]),
+            "orc_pool_threads": (i32, [p]),
+            "orc_pool_free": (None, [p]),
+            "orc_unique_parallel": (i64, [p, p, i64, p, p]),
+            "orc_pipeline_ev_lookup_sparse_pool": (i32, [p, p, p, i64, p, i64, i32, i32, p]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -115,6 +120,33 @@ def unique(x, with_counts=False):
     u = lib().orc_unique(_p(x), x.shape[0], _p(y), _p(idx), _p(cnt))
     if with_counts:
         return y[:u].copy(), idx, cnt[:u].copy()
+    return y[:u].copy(), idx
+
+
+class Pool(object):
+    """The persistent worker pool (orc_pool_create): TF's CPU worker threads."""
+
+    def __init__(self, threads):
+        self._h = lib().orc_pool_create(int(threads))
+        if not self._h:
+            raise OracleError("orc_pool_create failed")
+        self.threads = int(lib().orc_pool_threads(self._h))
+
+    def close(self):
+        if self._h:
+            lib().orc_pool_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+def unique_parallel(x, pool):
+    """ParallelComputeV1 (unique_ali_op_util.h:226-445) on the pool's threads."""
+    x = np.ascontiguousarray(x, dtype=np.int64)
+    y = np.empty_like(x)
+    idx = np.empty(x.shape[0], np.int32)
+    u = lib().orc_unique_parallel(pool._h, _p(x), x.shape[0], _p(y), _p(idx))
     return y[:u].copy(), idx
 
 

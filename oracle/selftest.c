@@ -45,6 +45,14 @@ int orc_pipeline_ev_lookup_sparse(orc_ev* ev, const int64_t* ids, int64_t nnz,
 int orc_pipeline_dense_lookup_sparse(const float* table, int64_t D, const int64_t* ids,
                                      int64_t nnz, const int32_t* seg_off, int64_t B, int combiner,
                                      int threads, float* out);
+typedef struct orc_pool orc_pool;
+orc_pool* orc_pool_create(int threads);
+void orc_pool_free(orc_pool* pl);
+int64_t orc_unique_parallel(orc_pool* pool, const int64_t* x, int64_t n, int64_t* y,
+                            int32_t* idx);
+int orc_pipeline_ev_lookup_sparse_pool(orc_pool* pool, orc_ev* ev, const int64_t* ids,
+                                       int64_t nnz, const int32_t* seg_off, int64_t B,
+                                       int combiner, int serial_unique, float* out);
 
 static uint64_t rs = 0x9E3779B97F4A7C15ULL;
 static uint64_t rnd(void) {
@@ -87,6 +95,19 @@ static void test_unique(void) {
     if (first[idx[i]] < 0) first[idx[i]] = i;
   for (int64_t u = 1; u < U; ++u) CHECK(first[u] > first[u - 1], "unique order at %lld", (long long)u);
   free(first);
+  /* the parallel Unique (four threaded steps) gives the serial result */
+  int64_t* y2 = malloc(sizeof(int64_t) * n);
+  int32_t* idx2 = malloc(sizeof(int32_t) * n);
+  for (int th = 1; th <= 8; th += 3) {
+    orc_pool* pl = orc_pool_create(th);
+    const int64_t U2 = orc_unique_parallel(pl, x, n, y2, idx2);
+    CHECK(U2 == U && memcmp(y, y2, sizeof(int64_t) * U) == 0 &&
+              memcmp(idx, idx2, sizeof(int32_t) * n) == 0,
+          "parallel unique, %d threads", th);
+    orc_pool_free(pl);
+  }
+  free(y2);
+  free(idx2);
   free(x);
   free(y);
   free(idx);
@@ -124,6 +145,12 @@ static void test_ev_and_pipelines(void) {
     orc_pipeline_ev_lookup_sparse(ev, ids, nnz, off, B, comb, 1, o1);
     orc_pipeline_ev_lookup_sparse(ev, ids, nnz, off, B, comb, 8, o8);
     CHECK(memcmp(o1, o8, sizeof(float) * B * D) == 0, "ev pipeline threads, combiner %d", comb);
+    for (int serial = 0; serial < 2; ++serial) {   /* the pooled pipeline, both Uniques */
+      orc_pool* pl = orc_pool_create(6);
+      orc_pipeline_ev_lookup_sparse_pool(pl, ev, ids, nnz, off, B, comb, serial, o8);
+      CHECK(memcmp(o1, o8, sizeof(float) * B * D) == 0, "pooled pipeline, combiner %d", comb);
+      orc_pool_free(pl);
+    }
     free(o1);
     free(o8);
   }

@@ -18,6 +18,8 @@ sys.path.insert(0, os.path.join(ROOT, "deeprec-1_amd"))
 
 
 def build(dr, mz, dev, tag, B, T, D, R):
+    if os.environ.get("GMP_BLAS"):   # graph_mem_probe bisection: rocblas / hipblaslt
+        torch.backends.cuda.preferred_blas_library(os.environ["GMP_BLAS"])
     evs = []
     for i, r in enumerate(R):
         ev = dr.EmbeddingVariable("dgp_%s%d" % (tag, i), D, 0.0, capacity=r + (1 << 16), device=dev)
