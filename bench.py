@@ -26,6 +26,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "deeprec-1_amd"))
 
+# before HIP initialises: graph replays without the runtime's packet capture
+# (deeprec_amd/_lib.py GRAPH_PACKET_CAPTURE_ENV)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -308,7 +311,10 @@ def criteo_legs(args, dev, log):
                 "lookups_per_s": round(T * B / (k_ms * 1e-3), 1),
                 "samples_per_s": round(B / (k_ms * 1e-3), 1), "kernel_ms": round(k_ms, 4),
                 "achieved_algorithmic_GBs": round(ach, 1),
-                "frac": round(ach / PEAK_HBM_GBS, 4),
+                # NOT an HBM roofline fraction: the small features' rows are
+                # re-read from L2 / MALL, so the HBM bytes are below the
+                # algorithmic 1 048 per lookup (no PMC traffic behind it)
+                "frac_cache_inclusive": round(ach / PEAK_HBM_GBS, 4),
                 "distinct_keys_batch0": int(torch.unique(recs[0]).numel())}
             log("criteo B=%d %s: %s" % (B, dist_name, json.dumps(res["B%d_%s" % (B, dist_name)])))
     dr.status_check(dev)
@@ -512,6 +518,103 @@ def criteo_hybrid_leg(args, dev, log, world, rank, dist, staged):
     return res
 
 
+def _state(model, evs):
+    """Parameters and EV contents (sorted by key) of a model, for bit compares."""
+    ps = [p.detach().clone() for p in model.parameters()]
+    es = []
+    for ev in evs:
+        k, v = ev.export()[:2]
+        o = torch.argsort(k)
+        es.append((k[o], v[o]))
+    return ps, es
+
+
+def _same_state(a, b):
+    (pa, ea), (pb, eb) = a, b
+    return (all(torch.equal(x.view(torch.int32), y.view(torch.int32)) for x, y in zip(pa, pb))
+            and all(torch.equal(ka, kb) and torch.equal(va.view(torch.int32), vb.view(torch.int32))
+                    for (ka, va), (kb, vb) in zip(ea, eb)))
+
+
+def _ev_rows_io(evs, rowsets, D, saved=None):
+    """Copy the given rows (int32 row indices) of fp32 EVs out of their pools
+    (saved=None: returns the copies) or back in (dr_rows_pack / _scatter on
+    the pool pointer)."""
+    import ctypes as _C
+    from deeprec_amd._lib import check, lib, ptr, stream_handle
+    out = []
+    for i, (ev, r) in enumerate(zip(evs, rowsets)):
+        pool, st = _C.c_void_p(ev.pool()), stream_handle(r.device)
+        if saved is None:
+            o = torch.empty((r.numel(), D), dtype=torch.float32, device=r.device)
+            check(lib().dr_rows_pack(pool, ptr(r), r.numel(), None, D, ptr(o), st))
+            out.append(o)
+        else:
+            check(lib().dr_rows_scatter(ptr(saved[i]), ptr(r), r.numel(), None, D, pool, st))
+    return out
+
+
+def _dlrm_graph_check(mgraph, glosses, mstep, model, evs, idlist, D, n, rounds=2):
+    """The captured n DLRM steps (SGD dense + KV) against n eager steps from
+    the same state: parameters and the EV rows of every key the batches touch
+    are saved, the eager steps run, their losses / parameters / rows are kept,
+    the state is put back and the graph replayed -- `rounds` times, eager work
+    in between -- each replay bit-compared with the eager result."""
+    keys = [torch.unique(torch.cat([ids[t] for ids in idlist])) for t in range(len(evs))]
+    rows = [ev.resolve(k).to(torch.int32) for ev, k in zip(evs, keys)]
+    params = list(model.parameters())
+    p0 = [p.detach().clone() for p in params]
+    r0 = _ev_rows_io(evs, rows, D)
+    le = [mstep(i).detach().clone() for i in range(n)]
+    pe = [p.detach().clone() for p in params]
+    re_ = _ev_rows_io(evs, rows, D)
+    eq = lambda a, b: torch.equal(a.view(torch.int32), b.view(torch.int32))  # noqa: E731
+    for rep in range(rounds):
+        with torch.no_grad():
+            for p, v in zip(params, p0):
+                p.copy_(v)
+        _ev_rows_io(evs, rows, D, r0)
+        mgraph.replay()
+        torch.cuda.synchronize()
+        bad = [i for i in range(n) if not eq(glosses[i].detach(), le[i])]
+        if bad:
+            return "replay %d: step %d loss %r != eager %r" % (rep, bad[0], float(glosses[bad[0]]),
+                                                                float(le[bad[0]]))
+        if not all(eq(p.detach(), v) for p, v in zip(params, pe)):
+            return "replay %d: parameters differ from the eager steps" % rep
+        if not all(eq(a, b) for a, b in zip(_ev_rows_io(evs, rows, D), re_)):
+            return "replay %d: EV rows differ from the eager steps" % rep
+        # eager work between the replays (what the runtime bug needed)
+        junk = [torch.full((int(k),), float("nan"), device=p0[0].device)
+                for k in torch.randint(1, 1 << 18, (500,)).tolist()]
+        del junk
+    return "equal: %d replays of %d steps from a restored state, losses + parameters + %d " \
+           "touched EV rows bit-equal to the eager steps" % (rounds, n,
+                                                              sum(int(r.numel()) for r in rows))
+
+
+def _din_graph_check(graphs, glosses, shadow_step, cur, shadow, dev, rounds=2):
+    """Replay the captured steps `rounds` times over, an eager shadow step of
+    the same batch before each replay; returns "equal ..." when every loss
+    and, at the end, every parameter and EV row agree bit for bit."""
+    n = 0
+    for _ in range(rounds):
+        for j, gr in enumerate(graphs):
+            le = shadow_step(j).detach()
+            gr.replay()
+            torch.cuda.synchronize()
+            if not torch.equal(le.view(torch.int32), glosses[j].detach().view(torch.int32)):
+                return "replay %d (graph %d) loss %r != eager shadow %r" % (
+                    n, j, float(glosses[j]), float(le))
+            n += 1
+    evs_c, model_c = cur
+    evs_s, model_s = shadow
+    if not _same_state(_state(model_c, evs_c), _state(model_s, evs_s)):
+        return "parameters / EV rows differ from the eager shadow after %d replays" % n
+    return "equal: %d replays interleaved with eager shadow steps, losses + parameters + EV " \
+           "rows bit-equal" % n
+
+
 def din_leg(args, dev, log, world, rank, dist, staged):
     """BASELINE configs[3]: DIN (modelzoo/DIN/script/model.py) at B_local =
     4096, histories U[1, 100] padded to the batch max, dim 18, vocabularies
@@ -523,23 +626,30 @@ def din_leg(args, dev, log, world, rank, dist, staged):
     from deeprec_amd import modelzoo as mz
     B, T, D = args.din_batch, 100, 18
     R = (500_000, 400_000, 2_000)
-    evs = []
-    for i, r in enumerate(R):
-        ev = dr.EmbeddingVariable("din_b%d" % i, D, 0.0, capacity=r + (1 << 16), device=dev)
-        ev.insert_synthetic(0, r, seed=700 + i)
-        evs.append(ev)
-    torch.manual_seed(0)
-    model = mz.DIN(*evs).to(dev)
     # one GPU: the step as hipGraphs, one per batch shape (DR_DIN_GRAPH=0:
     # eager); capturable dense Adam (step counts on the device), KV Adam's
-    # beta powers in HBM (training.AdamOptimizer._device_powers).  The
-    # replays are bit-equal to the eager steps when nothing else runs between
-    # them (tests/test_gpu_din_graph.py, profiles/r05_din_graph_probe.log);
-    # the eager step is timed and reported beside them
+    # beta powers in HBM (training.AdamOptimizer._device_powers).  Before the
+    # graphs are timed they are checked against an eager shadow model (same
+    # seeds, same steps) stepped BETWEEN the replays in this process -- the
+    # interleaving that broke round 5's replays (the runtime's graph packet
+    # capture, deeprec_amd/_lib.py) -- over two rounds of the four graphs;
+    # any bit that differs and the eager step is timed instead
     use_graph = (world == 1 and getattr(args, "model_graph", True)
                  and os.environ.get("DR_DIN_GRAPH", "1") == "1")
-    dopt = torch.optim.Adam(model.parameters(), lr=0.001, capturable=use_graph)
-    eopt = dr.AdamOptimizer(0.001)
+
+    def make(tag):
+        evs = []
+        for i, r in enumerate(R):
+            ev = dr.EmbeddingVariable("din_%s%d" % (tag, i), D, 0.0, capacity=r + (1 << 16),
+                                      device=dev)
+            ev.insert_synthetic(0, r, seed=700 + i)
+            evs.append(ev)
+        torch.manual_seed(0)
+        model = mz.DIN(*evs).to(dev)
+        dopt = torch.optim.Adam(model.parameters(), lr=0.001, capturable=use_graph)
+        return evs, model, dopt, dr.AdamOptimizer(0.001)
+    evs, model, dopt, eopt = make("b")
+    shadow = make("s") if use_graph else None
     g = torch.Generator(device=dev)
     g.manual_seed(2021 + 7919 * rank)
     batches = []
@@ -555,39 +665,46 @@ def din_leg(args, dev, log, world, rank, dist, staged):
                         torch.randint(0, R[2], (B,), generator=g, device=dev), mh, ch, mask,
                         torch.stack([lab, 1 - lab], 1).float()))
 
-    def dstep(i):
-        return mz.din_train_step(model, batches[i % 4], dopt, eopt, i, world=world,
-                                 staged=staged)
+    def dstep(i, m=None):
+        e_, md, do, eo = m or (evs, model, dopt, eopt)
+        return mz.din_train_step(md, batches[i % 4], do, eo, i, world=world, staged=staged)
 
     for i in range(4 if use_graph else 2):   # graphs: every batch shape once first
         dstep(i)
+        if shadow is not None:
+            dstep(i, shadow)
     torch.cuda.synchronize()
     dr.status_check(dev)
-    graphs, graph_err, eager_ms = None, None, None
+    graphs, graph_err, eager_ms, graph_check = None, None, None, None
     if use_graph:
         t0 = time.perf_counter()
         for i in range(4, 4 + args.din_steps):
             dstep(i)
         torch.cuda.synchronize()
         eager_ms = (time.perf_counter() - t0) / args.din_steps * 1e3
+        for i in range(4, 4 + args.din_steps):
+            dstep(i, shadow)
         try:
-            for ev in evs:   # a captured resolve must not be able to outgrow the table
-                ev.reserve(8 * B * (T + 1))   # 4 graphs x (lookup + apply) adds, counted conservatively
+            for m in (evs, shadow[0]):   # a captured resolve must not be able to outgrow the table
+                for ev in m:
+                    ev.reserve(8 * B * (T + 1))   # 4 graphs x (lookup + apply) adds, counted conservatively
             torch.cuda.synchronize()
-            graphs = []
+            graphs, glosses = [], []
             pool = torch.cuda.graph_pool_handle()
             for j in range(4):
                 gr = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gr, pool=pool):
-                    dstep(j)
+                    glosses.append(dstep(j))
                 graphs.append(gr)
-            for gr in graphs:
-                gr.replay()
-            torch.cuda.synchronize()
+            graph_check = _din_graph_check(graphs, glosses, lambda j: dstep(j, shadow),
+                                           (evs, model), shadow[:2], dev)
             dr.status_check(dev)
+            if not graph_check.startswith("equal"):
+                graph_err, graphs = graph_check, None
         except Exception as e:   # report the eager step instead
             graphs, graph_err = None, "%s: %s" % (type(e).__name__, str(e)[:200])
             torch.cuda.synchronize()
+        shadow = None
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -616,6 +733,8 @@ def din_leg(args, dev, log, world, rank, dist, staged):
            "hipgraph": graphs is not None}
     if eager_ms is not None:
         res["ms_per_step_eager"] = round(eager_ms, 4)
+    if graph_check:
+        res["graph_check"] = graph_check
     if graph_err:
         res["graph_error"] = graph_err
     log("din leg: %s" % json.dumps(res))
@@ -1337,18 +1456,24 @@ def main():
         # N = 1: NBATCH whole model steps (forward, backward, dense SGD, KV
         # SGD) captured as one hipGraph, as the embedding training step; the
         # eager loop if anything in the step refuses capture
-        mgraph = None
+        # Before it is timed, the graph is checked against the eager steps
+        # from the same state (parameters and every touched EV row saved and
+        # restored; SGD keeps no other state), replayed twice with eager work
+        # between: any bit that differs and the eager loop is timed instead
+        mgraph, mcheck, mlosses = None, None, None
         if not sharded_model and not args.no_graph and args.model_graph:
             try:
                 for ev in evs:
                     ev.reserve(2 * NBATCH * B)
                 mgraph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(mgraph):
-                    for i in range(NBATCH):
-                        mstep(i)
-                mgraph.replay()
-                torch.cuda.synchronize()
+                    mlosses = [mstep(i) for i in range(NBATCH)]
+                mcheck = _dlrm_graph_check(mgraph, mlosses, mstep, model, evs,
+                                           [batches[k] for k in range(NBATCH)], D, NBATCH)
                 dr.status_check(dev)
+                if not mcheck.startswith("equal"):
+                    log("dlrm model step: graph check failed (%s); eager" % mcheck)
+                    mgraph = None
             except Exception as e:  # noqa: BLE001
                 log("dlrm model step: graph capture failed (%s); eager" % str(e)[:200])
                 mgraph = None
@@ -1378,6 +1503,7 @@ def main():
         dlrm = {"ms_per_step": round(mms, 4),
                 "samples_per_s": round(world * B / (mms * 1e-3), 1),
                 "global_batch": world * B, "steps": nsteps, "graph": mgraph is not None,
+                "graph_check": mcheck,
                 "engine": engine_kind if sharded_model else "local",
                 "model": "modelzoo/DLRM/train.py DLRM, dot interaction, bf16 MFMA towers: bottom "
                          "[13, 512, 256, %d], top [%d, 512, 256] + 1-unit output, BCE; SGD on "
@@ -1386,7 +1512,8 @@ def main():
                              " (all-reduced gradients)" if sharded_model else "", T,
                              " shards" if sharded_model else "s")}
         log("dlrm model step: %s" % json.dumps(dlrm))
-        model = dopt = eopt = mdense = mlab = mgraph = None
+        # (the captured losses live in the graph's private pool: drop them too)
+        model = dopt = eopt = mdense = mlab = mgraph = mlosses = None
     din = None
     if args.din_steps > 0:
         try:

@@ -7,7 +7,24 @@ library is missing, or no GPU is visible, every op raises.
 import ctypes as C
 import os
 
-import torch
+# hipGraph replays and the ROCm runtime's graph packet capture
+# (DEBUG_CLR_GRAPH_PACKET_CAPTURE, on by default in this ROCm): with it on,
+# a captured graph is right on its first replay and can be wrong from the
+# second on once other kernels and allocations ran in the process between
+# replays -- reproduced with plain torch ops, no engine code involved
+# (tools/torch_graph_churn_probe.py: a.sum() + b.sum() in a graph, replayed
+# after allocator churn, changes value; profiles/r06_graph_replay_bisect.log).
+# The runtime reads the flag once, when HIP initialises: it is set here, before
+# this module touches the GPU, unless the caller set it.  GRAPH_REPLAY_SAFE
+# says whether that happened before HIP was up (a process that initialised the
+# GPU before importing deeprec_amd must export the variable itself).
+GRAPH_PACKET_CAPTURE_ENV = "DEBUG_CLR_GRAPH_PACKET_CAPTURE"
+os.environ.setdefault(GRAPH_PACKET_CAPTURE_ENV, "0")
+
+import torch  # noqa: E402
+
+GRAPH_REPLAY_SAFE = (os.environ.get(GRAPH_PACKET_CAPTURE_ENV) == "0"
+                     and not torch.cuda.is_initialized())
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # DEEPREC_AMD_LIB: an A/B build of the same library (measurement only)

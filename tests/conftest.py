@@ -3,6 +3,10 @@ import sys
 
 import pytest
 
+# before any test initialises HIP: hipGraph replays without the runtime's
+# graph packet capture (deeprec-1_amd/deeprec_amd/_lib.py)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "deeprec-1_amd")):
     if p not in sys.path:
