@@ -247,6 +247,27 @@ def _onehot_kernel_ms(feat_sets, iters, out_dtype=None):
     return tot.value / cnt.value
 
 
+def _pmc_traffic(roof, suffix, kname):
+    """roofline["traffic"] (HBM bytes per launch) from the newest committed
+    rocprofv3 PMC summary profiles/rNN_<suffix> of the same kernel
+    (tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE, separate passes)."""
+    import glob as _glob
+    fs = sorted(_glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_" + suffix)))
+    if not fs:
+        return roof
+    try:
+        j = json.load(open(fs[-1]))
+    except (OSError, ValueError):
+        return roof
+    if str(j.get("kernel", "")).startswith(kname):
+        roof["traffic"] = j.get("bytes_per_launch")
+        roof["traffic_source"] = os.path.relpath(fs[-1], ROOT)
+        roof["traffic_round"] = os.path.basename(fs[-1])[:3]
+        if roof.get("bytes_per_launch"):
+            roof["traffic_ratio"] = round(j["bytes_per_launch"] / roof["bytes_per_launch"], 4)
+    return roof
+
+
 def _free_hbm():
     import gc
     from deeprec_amd.kv_variable_ops import flush_releases
@@ -839,6 +860,7 @@ def dcn_bf16_leg(args, dev, log):
                           "step": "fused bf16 lookup recording rows + row-grouped backward (fp32 "
                                   "gradients) fused with the KV SGD update rounding to bf16 "
                                   "(dr_ev_pool_grad_rows_apply_sgd), hipGraph of 4 steps"}}
+    _pmc_traffic(res["roofline"], "pmc_traffic_dcn.json", "ev_lookup_line_kernel")
     log("dcn bf16 leg: %s" % json.dumps(res))
     del evs, fsets, g
     return res
@@ -927,6 +949,7 @@ def deepfm_leg(args, dev, log):
                           "step": "fused lookup recording rows + row-grouped backward fused with "
                                   "the KV SGD update (dr_ev_pool_grad_rows_apply_sgd), hipGraph "
                                   "of 4 steps"}}
+    _pmc_traffic(res["roofline"], "pmc_traffic_deepfm.json", "ev_lookup_line_kernel")
     log("deepfm leg: %s" % json.dumps(res))
     del evs, kfeats, g
     return res

@@ -41,7 +41,7 @@ def main():
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     st = glob.glob(os.path.join(stats_dir, "*_kernel_stats.csv"))[0]
-    shutil.copy(st, os.path.join(prof, "%s_bench_kernel_stats.csv" % rnd))
+    shutil.copy(st, os.path.join(prof, "%s_%s_kernel_stats.csv" % (rnd, tag[1:] or "bench")))
     avg_ns = None
     for r in csv.DictReader(open(st)):
         if KERNEL in r["Name"]:
@@ -62,7 +62,8 @@ def main():
     w_b = statistics.median(write) * 1024
     out = {
         "kernel": KERNEL,
-        "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes, "
+        "source": os.environ.get("PMC_SOURCE") or
+                  "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes, "
                   "bench.py --no-graph --steps 2 --kernel-iters 3; median over dispatches",
         "fetch_size_kib_raw_median": statistics.median(fetch),
         "write_size_kib_raw_median": statistics.median(write),
