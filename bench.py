@@ -995,55 +995,73 @@ def exchange_phases(ph, batches, world, rank, T, D, dist, staged, dev):
 def native_rccl_leg(args, evs, batches, engine, a2a, local_step, world, rank, dist, staged, dev,
                     log):
     """NativeShardedLookup over Comm.rccl (the library's sharded C entries on
-    the RCCL transport; Comm.host_staged in a gloo rehearsal): output checked
+    the RCCL transport; Comm.host_staged in a gloo rehearsal), each engine
+    kind of dr_sharded_create_ex: "rccl" (exact-size all-to-alls, the split
+    sizes read on the host), "xgmi" (peer writes into IPC-mapped buffers,
+    barriers through the comm, the result left in the engine's buffer -- no
+    host read) and, at N = 1, "fixed" (all-to-alls at fixed capacity, no
+    host read; it moves N x the keys at N > 1).  Each kind's output checked
     bit for bit against the all-to-all engine (N > 1) or the local fused
     lookup (N = 1), then timed forward-only."""
     from deeprec_amd.sharded import Comm, NativeShardedLookup
     T, B = args.tables, args.batch
     comm = Comm.host_staged() if staged else Comm.rccl(rank, world)
-    eng = NativeShardedLookup(comm, evs, dev)
-    same = 1
-    with torch.no_grad():
-        for k in range(len(batches)):
-            got = eng.forward(batches[k], combiner="sum").clone()
-            ref = a2a.forward(batches[k]) if a2a is not None else local_step(k)
-            same &= int(torch.equal(got, ref))
-    if world > 1:
-        flag = torch.tensor([same], dtype=torch.int32, device="cpu" if staged else dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        same = int(flag.item())
+    kinds = ["xgmi", "rccl"] + (["fixed"] if world == 1 else [])
+    out = {"transport": "gloo host-staged callback (rehearsal)" if staged else
+           "RCCL (dr_comm_init with an ncclUniqueId)"}
     n = args.native_steps
-    with torch.no_grad():
-        for k in range(2):
-            eng.forward(batches[k], combiner="sum")
+    for kind in kinds:
+        try:
+            eng = NativeShardedLookup(comm, evs, dev, kind=kind, batch=B, max_ids=B)
+        except Exception as e:  # noqa: BLE001 -- one kind must not cost the others
+            out[kind] = {"error": str(e)[:200]}
+            continue
+        copy = kind != "xgmi"   # xgmi: the result stays in the engine buffer
+        same = 1
+        with torch.no_grad():
+            for k in range(len(batches)):
+                got = eng.forward(batches[k], combiner="sum", copy=copy).clone()
+                ref = a2a.forward(batches[k]) if a2a is not None else local_step(k)
+                same &= int(torch.equal(got, ref))
+        if world > 1:
+            flag = torch.tensor([same], dtype=torch.int32, device="cpu" if staged else dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            same = int(flag.item())
+        with torch.no_grad():
+            for k in range(2):
+                eng.forward(batches[k], combiner="sum", copy=copy)
+            if dist is not None:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(n):
+                eng.forward(batches[i % len(batches)], combiner="sum", copy=copy)
+            if dist is not None:
+                dist.barrier()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
         if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(n):
-            eng.forward(batches[i % len(batches)], combiner="sum")
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([el], dtype=torch.float64, device="cpu" if staged else dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    st = eng.stats()
-    eng.close()
+            t = torch.tensor([el], dtype=torch.float64, device="cpu" if staged else dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        st = eng.stats()
+        eng.close()
+        res = {"engine_check": "native C-ABI engine (%s) == %s, %d batches, all ranks: %s" % (
+                   kind, "all-to-all engine" if a2a is not None else "local fused lookup",
+                   len(batches), bool(same)),
+               "ms_per_step": round(el / n * 1e3, 4), "steps": n,
+               "lookups_per_s": round(T * B * world * n / el, 1),
+               "note": {"rccl": "reads the per-peer split sizes on the host once per step",
+                        "xgmi": "route -> barrier -> owner serve (peer writes) -> barrier, "
+                                "no host read; output left in the engine buffer",
+                        "fixed": "fixed-capacity all-to-alls, device counts, no host read"}[kind]}
+        if kind == "rccl":
+            res["sent_keys_last_step"] = st["sent_keys"]
+            res["recv_keys_last_step"] = st["recv_keys"]
+        out[kind] = res
+        log("native engine %s: %s" % (kind, json.dumps(res)))
     comm.close()
-    res = {"transport": "gloo host-staged callback (rehearsal)" if staged else
-           "RCCL (dr_comm_init with an ncclUniqueId)",
-           "engine_check": "native C-ABI engine == %s, %d batches, all ranks: %s" % (
-               "all-to-all engine" if a2a is not None else "local fused lookup",
-               len(batches), bool(same)),
-           "ms_per_step": round(el / n * 1e3, 4), "steps": n,
-           "lookups_per_s": round(T * B * world * n / el, 1),
-           "sent_keys_last_step": st["sent_keys"], "recv_keys_last_step": st["recv_keys"],
-           "note": "forward only; reads the per-peer split sizes on the host once per step"}
-    log("native RCCL engine: %s" % json.dumps(res))
-    return res
+    return out
 
 
 def main():
@@ -1706,7 +1724,7 @@ def main():
             "criteo_tb_cardinalities": criteo,
             "criteo_tb_hybrid": hybrid,
             "exchange_phases": phases,
-            "native_rccl_engine": native,
+            "native_engine": native,
             "dcn_bf16_config": dcn,
             "correctness": correctness,
             "roofline": roof,

@@ -153,7 +153,7 @@ int dr_kernel_timing_result(double* total_ms, int64_t* launches) {
   return DR_OK;
 }
 
-int dr_abi_version(void) { return 1; }
+int dr_abi_version(void) { return 2; }
 
 const char* dr_last_error(void) { return dr::t_err; }
 

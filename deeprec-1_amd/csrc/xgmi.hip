@@ -630,7 +630,32 @@ void dl_delete(DlManaged* m) {
   (void)dr_ipc_free(m->t.data);
   free(m);
 }
+void dl_delete_view(DlManaged* m) { free(m); }   // a view: the memory is not ours
 }  // namespace
+
+int dr_dlpack_view(void* data, int ndim, const int64_t* shape, int dtype_code, int dtype_bits,
+                   int device_id, void** managed_out) {
+  using namespace dr;
+  DR_REQUIRE(data && ndim >= 1 && ndim <= 8 && shape && managed_out && dtype_bits % 8 == 0 &&
+                 dtype_bits > 0,
+             DR_INVALID_ARGUMENT, "dr_dlpack_view: bad argument");
+  DlManaged* m = static_cast<DlManaged*>(calloc(1, sizeof(DlManaged)));
+  DR_REQUIRE(m, DR_RESOURCE_EXHAUSTED, "dr_dlpack_view: out of host memory");
+  for (int i = 0; i < ndim; ++i) m->shape[i] = shape[i];
+  m->t.data = data;
+  m->t.device.device_type = 10;  // kDLROCM
+  m->t.device.device_id = device_id;
+  m->t.ndim = ndim;
+  m->t.dtype.code = (uint8_t)dtype_code;
+  m->t.dtype.bits = (uint8_t)dtype_bits;
+  m->t.dtype.lanes = 1;
+  m->t.shape = m->shape;
+  m->t.strides = nullptr;
+  m->t.byte_offset = 0;
+  m->deleter = dl_delete_view;
+  *managed_out = m;
+  return DR_OK;
+}
 
 int dr_ipc_alloc_dlpack(int ndim, const int64_t* shape, int dtype_code, int dtype_bits,
                         int device_id, void** managed_out) {

@@ -106,8 +106,23 @@ COMM_A2A_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_int64),
                           C.POINTER(C.c_int64), C.c_int64, C.c_void_p)
 
 
+# dr_comm_ops.all_gather / .barrier
+COMM_GATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p)
+COMM_BARRIER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p)
+
+
 class DrCommOps(C.Structure):
-    _fields_ = [("user", C.c_void_p), ("all_to_all_v", COMM_A2A_FN)]
+    _fields_ = [("user", C.c_void_p), ("all_to_all_v", COMM_A2A_FN),
+                ("all_gather", COMM_GATHER_FN), ("barrier", COMM_BARRIER_FN)]
+
+
+# dr_sharded_create_ex kinds and config (include/deeprec_amd.h)
+SHARDED_RCCL, SHARDED_XGMI, SHARDED_RCCL_FIXED = 0, 1, 2
+
+
+class DrShardedConfig(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("reserved", C.c_int32), ("batch", C.c_int64),
+                ("max_ids", C.c_int64)]
 
 
 class DrDinMlpBuf(C.Structure):
@@ -276,6 +291,10 @@ SIGNATURES = {
     "dr_sharded_forward": (_I32, [_P, _P, _P, _P, _I64, _I32, _I32, _I32, _P, _P]),
     "dr_sharded_backward": (_I32, [_P, _P, _P, _P, _P, _P]),
     "dr_sharded_last_stats": (_I32, [_P, _P, _P]),
+    "dr_sharded_create_ex": (_I32, [_P, _P, _I32, _P, _P]),
+    "dr_dlpack_view": (_I32, [_P, _I32, _P, _I32, _I32, _I32, _P]),
+    "dr_sharded_output": (_I32, [_P, _P]),
+    "dr_sharded_backward_dev": (_I32, [_P, _P, _P, _P, _P, _P, _P]),
     "dr_memcpy": (_I32, [_P, _P, _I64, _I32, _P]),
     "dr_fm2": (_I32, [_P, _I64, _I32, _I32, _P, _P]),
     "dr_fm2_grad": (_I32, [_P, _P, _I64, _I32, _I32, _P, _P]),
@@ -401,6 +420,23 @@ def uncached_empty(shape, dtype, device):
     m = C.c_void_p()
     with torch.cuda.device(idx):
         check(lib().dr_ipc_alloc_dlpack(len(shape), shp, code, bits, idx, C.byref(m)))
+    new = C.pythonapi.PyCapsule_New
+    new.restype = C.py_object
+    new.argtypes = [C.c_void_p, C.c_char_p, C.c_void_p]
+    return dlpack.from_dlpack(new(m, b"dltensor", None))
+
+
+def device_view(address, shape, dtype, device):
+    """A torch tensor viewing library-owned device memory (dr_dlpack_view; it
+    owns nothing: keep the owner alive while the view is used)."""
+    from torch.utils import dlpack
+    code, bits = _DL_CODES[dtype]
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    shp = (C.c_int64 * len(shape))(*[int(x) for x in shape])
+    m = C.c_void_p()
+    check(lib().dr_dlpack_view(C.c_void_p(address), len(shape), shp, code, bits, idx,
+                               C.byref(m)))
     new = C.pythonapi.PyCapsule_New
     new.restype = C.py_object
     new.argtypes = [C.c_void_p, C.c_char_p, C.c_void_p]

@@ -355,11 +355,38 @@ class Comm(object):
                 errors.append(e)
                 return 1
 
+        def gather(user, send, nbytes, recv):
+            # the XGMI engine's IPC handle exchange (setup only)
+            try:
+                mine = C.string_at(send, nbytes)
+                allb = [None] * world
+                dist.all_gather_object(allb, mine, group=group)
+                C.memmove(recv, b"".join(allb), nbytes * world)
+                return 0
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+                return 1
+
+        def barrier(user, stream):
+            # host-blocking: the stream's work first, then every rank
+            try:
+                if stream:
+                    torch.cuda.ExternalStream(stream).synchronize()
+                else:
+                    torch.cuda.synchronize()
+                dist.barrier(group=group)
+                return 0
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+                return 1
+
         fn = _lib.COMM_A2A_FN(a2a)
-        ops_ = _lib.DrCommOps(None, fn)
+        gfn = _lib.COMM_GATHER_FN(gather)
+        bfn = _lib.COMM_BARRIER_FN(barrier)
+        ops_ = _lib.DrCommOps(None, fn, gfn, bfn)
         h = C.c_void_p()
         check(lib().dr_comm_init(None, rank, world, C.byref(ops_), C.byref(h)))
-        return cls(h, world, rank, keep=(fn, ops_, errors))
+        return cls(h, world, rank, keep=(fn, gfn, bfn, ops_, errors))
 
     def close(self):
         if self.h is not None and self.h.value:
@@ -382,17 +409,40 @@ class NativeShardedLookup(object):
     sequence inside the C library, as a TF custom-op kernel would drive it
     (INTEGRATION.md)."""
 
-    def __init__(self, comm, evs, device):
+    def __init__(self, comm, evs, device, kind="rccl", batch=0, max_ids=0):
+        """kind: "rccl" (dr_sharded_create: exact-size all-to-alls, host reads
+        of the split sizes), "xgmi" (peer writes over IPC-mapped buffers;
+        one-hot sum over `batch` bags; no host read) or "fixed" (the
+        all-to-alls at fixed capacity, `max_ids` ids per table per rank;
+        no host read) -- dr_sharded_create_ex."""
         self.comm, self.evs, self.device = comm, list(evs), device
         self.T = len(self.evs)
         self.dim = self.evs[0].dim
         self.bf16 = self.evs[0].value_dtype == torch.bfloat16
+        self.kind = kind
+        self.batch = int(batch)
         hs = (C.c_void_p * self.T)(*[e.handle.value for e in self.evs])
         self.h = C.c_void_p()
-        check(lib().dr_sharded_create(comm.h, hs, self.T, C.byref(self.h)))
+        if kind == "rccl":
+            check(lib().dr_sharded_create(comm.h, hs, self.T, C.byref(self.h)))
+        else:
+            k = {"xgmi": _lib.SHARDED_XGMI, "fixed": _lib.SHARDED_RCCL_FIXED}[kind]
+            cfg = _lib.DrShardedConfig(k, 0, int(batch), int(max_ids))
+            with torch.cuda.device(device):
+                check(lib().dr_sharded_create_ex(comm.h, hs, self.T, C.byref(cfg),
+                                                 C.byref(self.h)))
         self._keep = None
 
-    def forward(self, ids, bag_offs=None, combiner="sum", need_grad=False, out_dtype=None):
+    def output(self, out_dtype=None):
+        """XGMI kind: the engine buffer with the last forward's result (the
+        EVs' value type) as a tensor view -- forward(..., copy=False)."""
+        p = C.c_void_p()
+        check(lib().dr_sharded_output(self.h, C.byref(p)))
+        dt = torch.bfloat16 if self.bf16 else torch.float32
+        return _lib.device_view(p.value, (self.batch, self.T * self.dim), dt, self.device)
+
+    def forward(self, ids, bag_offs=None, combiner="sum", need_grad=False, out_dtype=None,
+                copy=True):
         """ids: [T, B] int64 (one-hot, bag_offs None) or T 1-D int64 tensors
         (table t's ids); bag_offs None or T int32 [bags + 1] offsets covering
         each table's ids.  Returns [bags, T*D] (fp32; bf16 on request for bf16
@@ -414,12 +464,16 @@ class NativeShardedLookup(object):
             bags = int(bag_offs[0].numel()) - 1
             offs = (C.c_void_p * T)(*[o.data_ptr() for o in bag_offs])
         bf = out_dtype == torch.bfloat16
-        out = torch.empty((bags, T * self.dim), dtype=torch.bfloat16 if bf else torch.float32,
-                          device=self.device)
+        out = None
+        if copy:
+            out = torch.empty((bags, T * self.dim), dtype=torch.bfloat16 if bf else torch.float32,
+                              device=self.device)
         ka = (C.c_int64 * (T + 1))(*koff)
         check(lib().dr_sharded_forward(self.h, ptr(flat), ka, offs, bags, COMBINERS[combiner],
                                        1 if need_grad else 0, _lib.SHARDED_OUT_BF16 if bf else 0,
                                        ptr(out), stream_handle(self.device)))
+        if out is None:
+            out = self.output()
         ops._post(self.device)
         self._keep = (flat, bag_offs) if need_grad else None
         return out
@@ -435,6 +489,8 @@ class NativeShardedLookup(object):
         from .kv_variable_ops import IndexedSlices
         T, D = self.T, self.dim
         g = grad_out.float().contiguous()
+        if self.kind != "rccl":
+            return self._backward_dev(g)
         kp, gp, cn = (C.c_void_p * T)(), (C.c_void_p * T)(), (C.c_int64 * T)()
         st = stream_handle(self.device)
         check(lib().dr_sharded_backward(self.h, ptr(g), kp, gp, cn, st))
@@ -448,6 +504,34 @@ class NativeShardedLookup(object):
                 check(lib().dr_memcpy(v.data_ptr(), gp[t], 4 * n * D, 0, st))
             out.append((k, v))
             self.evs[t].pending_grads.append(IndexedSlices(v, k, unique=False))
+        ops._post(self.device)
+        self._keep = None
+        return out
+
+    def _backward_dev(self, g):
+        """XGMI / fixed kinds: no host read -- each table's IndexedSlices is a
+        fixed region of the engine's buffers with a DEVICE count (copied out
+        here, so the slices outlive the next call)."""
+        from .kv_variable_ops import IndexedSlices
+        T, D = self.T, self.dim
+        kp, gp, cp = (C.c_void_p * T)(), (C.c_void_p * T)(), (C.c_void_p * T)()
+        region = C.c_int64(0)
+        st = stream_handle(self.device)
+        check(lib().dr_sharded_backward_dev(self.h, ptr(g), kp, gp, cp, C.byref(region), st))
+        R = region.value
+        keys = torch.empty((T, R), dtype=torch.int64, device=self.device)
+        grads = torch.empty((T, R, D), dtype=torch.float32, device=self.device)
+        cnt = torch.empty(T, dtype=torch.int64, device=self.device)
+        for t in range(T):
+            keys[t].copy_(_lib.device_view(kp[t], (R,), torch.int64, self.device))
+            grads[t].copy_(_lib.device_view(gp[t], (R, D), torch.float32, self.device))
+        cnt.copy_(_lib.device_view(cp[0], (T,), torch.int64, self.device))
+        out = []
+        for t in range(T):
+            n = cnt[t:t + 1]
+            out.append((keys[t], grads[t], n))
+            self.evs[t].pending_grads.append(IndexedSlices(grads[t], keys[t], num_valid=n,
+                                                           unique=False))
         ops._post(self.device)
         self._keep = None
         return out

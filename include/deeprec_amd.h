@@ -810,6 +810,10 @@ int dr_ipc_free(void* ptr);
 /* capsule).  device_id must be the current device.                         */
 int dr_ipc_alloc_dlpack(int ndim, const int64_t* shape, int dtype_code, int dtype_bits,
                         int device_id, void** managed_out);
+/* A DLPack view (no ownership: the deleter frees the descriptor only) of   */
+/* device memory the library owns, e.g. an engine buffer (dr_sharded_output). */
+int dr_dlpack_view(void* data, int ndim, const int64_t* shape, int dtype_code, int dtype_bits,
+                   int device_id, void** managed_out);
 
 typedef struct {
   int32_t world, rank;
@@ -880,6 +884,14 @@ typedef struct {
   /* recv (peer-major).  Counts are HOST arrays of world entries.  Return 0. */
   int (*all_to_all_v)(void* user, const void* send, const int64_t* send_counts, void* recv,
                       const int64_t* recv_counts, int64_t elem_bytes, void* stream);
+  /* All-gather of `bytes` HOST bytes from every rank into recv, rank-major  */
+  /* (world * bytes).  Engine setup only (the IPC handle exchange of the     */
+  /* XGMI kind).  NULL: no XGMI engine on this comm.                         */
+  int (*all_gather)(void* user, const void* send, int64_t bytes, void* recv);
+  /* Stream-ordered cross-rank barrier: all work queued on `stream` before it */
+  /* on every rank completes before work queued after it on any rank.  The   */
+  /* XGMI kind calls it twice per step.  NULL: no XGMI engine on this comm.  */
+  int (*barrier)(void* user, void* stream);
 } dr_comm_ops;
 #define DR_RCCL_UNIQUE_ID_BYTES 128
 /* ncclGetUniqueId (rank 0 calls it and hands the bytes to every rank).      */
@@ -929,8 +941,53 @@ int dr_sharded_forward(dr_sharded* s, const int64_t* ids, const int64_t* koff_ho
 /* [t] (HOST) = rows of table t.                                             */
 int dr_sharded_backward(dr_sharded* s, const float* grad, const int64_t** keys_out,
                         const float** grads_out, int64_t* counts_out, void* stream);
-/* Keys exchanged by the last forward: sent to peers / received from them.  */
+/* Keys exchanged by the last forward: sent to peers / received from them   */
+/* (-1 for the kinds below, which keep the counts on the device).            */
 int dr_sharded_last_stats(const dr_sharded* s, int64_t* sent, int64_t* received);
+
+/* Engine kinds (dr_sharded_create_ex).                                      */
+/* DR_SHARDED_RCCL: the engine above (dr_sharded_create): exact-size         */
+/*   all-to-alls, one host read of the split sizes per direction.            */
+/* DR_SHARDED_XGMI: the peer-write exchange (dr_xgmi_* above) run inside the */
+/*   library -- route -> barrier -> serve -> barrier; backward: the gradient */
+/*   into the shared buffer -> barrier -> owner pull -> barrier.  Buffers    */
+/*   (uncached, dr_ipc_alloc) are mapped across ranks once at create time    */
+/*   through the comm's all_gather (IPC handles); the barriers are the       */
+/*   comm's (RCCL: a one-float all-reduce).  One-hot sum over `batch` bags;  */
+/*   no host read, so a step captures into a hipGraph.                       */
+/* DR_SHARDED_RCCL_FIXED: the all-to-all engine at fixed capacity: every     */
+/*   rank sends each peer a region of tables * max_ids keys (and the rows   */
+/*   back in the same layout), the [world, tables] counts in a header; every */
+/*   size after the exchange is a device count, so no host read and the step */
+/*   captures into a hipGraph.  It moves world x the keys of the variable    */
+/*   exchange at worst -- the price of the capture.  A block past its region */
+/*   latches DR_RESOURCE_EXHAUSTED (dr_status_check).                        */
+/* Outputs of every kind equal the single-GPU lookup bit for bit.            */
+#define DR_SHARDED_RCCL 0
+#define DR_SHARDED_XGMI 1
+#define DR_SHARDED_RCCL_FIXED 2
+typedef struct {
+  int32_t kind;
+  int32_t reserved;  /* 0 */
+  int64_t batch;     /* XGMI: bags per table (one-hot), the same on every rank */
+  int64_t max_ids;   /* RCCL_FIXED: most ids one table holds on one rank in a step */
+} dr_sharded_config;
+int dr_sharded_create_ex(dr_comm* comm, dr_ev* const* evs, int num_tables,
+                         const dr_sharded_config* cfg, dr_sharded** out);
+/* XGMI: the engine buffer holding the last forward's [batch, T*dim] result  */
+/* (the EVs' value type; valid until the next forward).  dr_sharded_forward  */
+/* with out == NULL leaves it there instead of copying it out.               */
+int dr_sharded_output(dr_sharded* s, void** out);
+/* Backward of the XGMI / RCCL_FIXED kinds with device counts: table t's    */
+/* IndexedSlices are keys_out[t][0, n_t) / grads_out[t][0, n_t) with n_t =   */
+/* *counts_dev_out[t] (DEVICE int64), inside a fixed region of *region_rows */
+/* rows (world x batch, or world x max_ids).  Order: table-major, source-   */
+/* rank-major (source-slot order within a source for XGMI, the source's     */
+/* first-occurrence Unique order for RCCL_FIXED).  Valid until the next     */
+/* call.  dr_sharded_backward works for these kinds too (one host read).    */
+int dr_sharded_backward_dev(dr_sharded* s, const float* grad, const int64_t** keys_out,
+                            const float** grads_out, const int64_t** counts_dev_out,
+                            int64_t* region_rows, void* stream);
 /* Byte copy between any host / device buffers on `stream` (hipMemcpyDefault); */
 /* sync != 0 waits for it.  For host frameworks' dr_comm callbacks that stage */
 /* device buffers through host memory (e.g. a CPU collective).               */

@@ -74,7 +74,7 @@ def test_ops_refuse_without_gpu():
 def test_abi_version_without_device(built_lib):
     lib = ctypes.CDLL(built_lib)
     lib.dr_abi_version.restype = ctypes.c_int
-    assert lib.dr_abi_version() == 1
+    assert lib.dr_abi_version() == 2
 
 
 def test_synth_rows_restatement_matches_library(built_lib):

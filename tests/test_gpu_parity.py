@@ -51,7 +51,7 @@ def H(t):
 # ---------------------------------------------------------------------------
 def test_native_library_is_loaded(dr):
     from deeprec_amd import _lib
-    assert _lib.lib().dr_abi_version() == 1
+    assert _lib.lib().dr_abi_version() == 2
     maps = open("/proc/self/maps").read()
     assert "libdeeprec_amd.so" in maps
 

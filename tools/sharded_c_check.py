@@ -17,6 +17,12 @@ callback).  Checks, bit for bit:
     ranks (ascending) of each source's first-occurrence unique keys that
     this rank owns with their SparseSegment*Grad rows (the oracle's Unique +
     sparse_segment_reduce_grad over every rank's batch and gradient).
+  * the host-read-free kinds (dr_sharded_create_ex, round 6): XGMI (peer
+    writes into IPC-mapped buffers; backward: every position's gradient row,
+    source-rank-major, source-slot order) and the fixed-capacity all-to-all
+    (the same slices as the variable engine) -- one-hot forward / backward,
+    fixed-kind multi-hot mean bags, bf16 EVs -- through the comm's
+    all_gather / barrier callbacks.
 The parent prints one JSON line per rank (sent through a queue, so lines
 never interleave); exit code != 0 on any mismatch.
 """
@@ -233,6 +239,93 @@ def worker(rank, world, port, q):
     dr.status_check()
     eng.close()
     eb.close()
+    # -- the host-read-free kinds (dr_sharded_create_ex): XGMI peer writes and
+    # the fixed-capacity all-to-all, on the same shards and batches --
+    for kind in ("xgmi", "fixed"):
+        ek = NativeShardedLookup(comm, shard, dev, kind=kind, batch=B, max_ids=70000)
+        for step in range(2):
+            ids = _onehot_ids(step, rank)
+            it = torch.as_tensor(ids, device=dev)
+            ref = embedding_lookup_sparse_multi(full, [SparseTensor(ind1, it[t], (B, 1))
+                                                       for t in range(T)], combiner="sum")
+            out = ek.forward(it, combiner="sum", need_grad=False)
+            torch.cuda.synchronize()
+            check("%s_onehot_fwd_%d" % (kind, step), out.cpu().numpy(), ref.detach().cpu().numpy())
+            out = ek.forward(it, combiner="sum", need_grad=True)
+            check("%s_onehot_fwd_grad_%d" % (kind, step), out.cpu().numpy(),
+                  ref.detach().cpu().numpy())
+            g = _grad(step, rank, B)
+            slices = ek.backward(torch.as_tensor(g, device=dev))
+            for t in range(T):
+                k, v, n = slices[t]
+                n = int(n.item())
+                kk, vv = [], []
+                for p in range(world):
+                    idp = _onehot_ids(step, p)[t]
+                    gp = _grad(step, p, B)[:, t * D:(t + 1) * D]
+                    if kind == "xgmi":   # every position, in source-slot order
+                        own = idp % world == rank
+                        kk.append(idp[own])
+                        vv.append(gp[own])
+                        continue
+                    u, idx = orc.unique(idp)
+                    gu = orc.sparse_segment_reduce_grad(np.ascontiguousarray(gp), idx,
+                                                        np.arange(B, dtype=np.int32), u.size, "sum")
+                    own = u % world == rank
+                    kk.append(u[own])
+                    vv.append(gu[own])
+                check("%s_onehot_bwd_keys_%d_%d" % (kind, step, t), k[:n].cpu().numpy(),
+                      np.concatenate(kk))
+                check("%s_onehot_bwd_grads_%d_%d" % (kind, step, t), v[:n].cpu().numpy(),
+                      np.concatenate(vv))
+            for e in shard:
+                e.pending_grads.clear()
+        if kind == "fixed":
+            # multi-hot mean bags through the fixed regions
+            ids, offs, lens = _bags(0, rank)
+            it = [torch.as_tensor(x, device=dev) for x in ids]
+            ot = [torch.as_tensor(o, device=dev) for o in offs]
+            sps = []
+            for t in range(T):
+                rows = np.repeat(np.arange(B), lens[t])
+                ind = np.stack([rows, np.zeros_like(rows)], 1).astype(np.int64)
+                sps.append(SparseTensor(torch.as_tensor(ind, device=dev), it[t], (B, 5)))
+            ref = embedding_lookup_sparse_multi(full, sps, combiner="mean")
+            out = ek.forward(it, bag_offs=ot, combiner="mean", need_grad=True)
+            torch.cuda.synchronize()
+            check("fixed_bags_fwd", out.cpu().numpy(), ref.detach().cpu().numpy())
+            g = _grad(100, rank, B)
+            slices = ek.backward(torch.as_tensor(g, device=dev))
+            for t in range(T):
+                k, v, n = slices[t]
+                n = int(n.item())
+                kk, vv = [], []
+                for p in range(world):
+                    idp, offp, lenp = _bags(0, p)
+                    u, idx = orc.unique(idp[t])
+                    seg = np.repeat(np.arange(B), lenp[t]).astype(np.int32)
+                    gp = _grad(100, p, B)[:, t * D:(t + 1) * D]
+                    gu = orc.sparse_segment_reduce_grad(np.ascontiguousarray(gp), idx, seg, u.size,
+                                                        "mean")
+                    own = u % world == rank
+                    kk.append(u[own])
+                    vv.append(gu[own])
+                check("fixed_bags_bwd_keys_%d" % t, k[:n].cpu().numpy(), np.concatenate(kk))
+                check("fixed_bags_bwd_grads_%d" % t, v[:n].cpu().numpy(), np.concatenate(vv))
+            for e in shard:
+                e.pending_grads.clear()
+        ek.close()
+        # bf16 EVs: fp32 and bf16 outputs
+        ekb = NativeShardedLookup(comm, sb, dev, kind=kind, batch=B, max_ids=B)
+        ids = _onehot_ids(9, rank)
+        it = torch.as_tensor(ids, device=dev)
+        o32 = ekb.forward(it, combiner="sum")
+        check("%s_bf16_fwd_fp32" % kind, o32.cpu().numpy(), ref32.float().cpu().numpy())
+        o16 = ekb.forward(it, combiner="sum", out_dtype=torch.bfloat16)
+        check("%s_bf16_fwd_bf16" % kind, o16.view(torch.int16).cpu().numpy(),
+              ref16.view(torch.int16).cpu().numpy())
+        ekb.close()
+    dr.status_check()
     comm.close()
     res["ok"] = ok
     q.put(json.dumps(res))   # the parent prints: one whole line per rank
