@@ -140,7 +140,7 @@ def cpu_baseline(args):
     out = np.empty((B, D), np.float32)
     L = orc.lib()
     pool = orc.Pool(threads)
-    reps = 3
+    reps = 5
     per = args.cpu_seconds / (2 * reps)
 
     def timed(serial):

@@ -1066,13 +1066,15 @@ int dr_sharded_forward(dr_sharded* s, const int64_t* ids, const int64_t* koff_ho
                        const int32_t* const* bag_off, int64_t bags, int combiner, int need_grad,
                        int flags, void* out, void* stream) {
   using namespace dr;
-  DR_REQUIRE(s && out && bags >= 0, DR_INVALID_ARGUMENT, "bad argument");
+  DR_REQUIRE(s && bags >= 0, DR_INVALID_ARGUMENT, "bad argument");
   DR_REQUIRE(combiner >= DR_COMBINER_SUM && combiner <= DR_COMBINER_SQRTN, DR_INVALID_ARGUMENT,
              "combiner must be sum, mean or sqrtn");
   DR_REQUIRE(!(flags & DR_SHARDED_OUT_BF16) || s->bf16, DR_INVALID_ARGUMENT,
              "a bf16 output needs bf16 EVs");
+  // (XGMI: out may be NULL -- the result stays in the engine buffer)
   if (s->kind == DR_SHARDED_XGMI)
     return xgmi_forward(s, ids, koff_host, bag_off, bags, combiner, need_grad, flags, out, stream);
+  DR_REQUIRE(out, DR_INVALID_ARGUMENT, "null output");
   if (s->kind == DR_SHARDED_RCCL_FIXED)
     return fixed_forward(s, ids, koff_host, bag_off, bags, combiner, need_grad, flags, out, stream);
   const int T = s->T, G = s->comm->world, GT = G * T;
