@@ -119,4 +119,93 @@ DR_HD inline float rep_add(float s, float x, int64_t k) {
   return s;
 }
 
+// ---- many segments at once ------------------------------------------------
+// A chain of segments (term x_j added k_j times, j ascending) taken in
+// parallel: while the running sum stays in one binade of one sign (grid
+// fixed), segment j moves it by exactly k_j * D_j ulps (rep_add_grid's step),
+// so the sum after any prefix of segments is the start plus an integer
+// prefix sum -- the sequential dependence is only through the grid, which
+// changes rarely (binade edges, sign changes).  A walker takes a window of
+// segments: every segment's step on the current grid (seg_grid_term), an
+// exclusive prefix of k_j * D_j, a test that each segment's sums stay on the
+// grid from its prefix (seg_grid_fits: both ends inside the binade, no tie
+// from an odd sum), and takes the segments before the first that fails in
+// one step; the failing one is added by rep_add (exact), and the next round
+// starts on its new grid.  Bit-equal to the plain loop (tools/repadd_check.cpp
+// "rounds" mode checks it against sum-by-sum adds; rows_rounds_seg_kernel
+// runs it on the device).
+
+// The grid of a normal nonzero sum s: its sign / exponent bits and its
+// magnitude in ulps a in [2^23, 2^24).
+struct SegGrid {
+  uint32_t se;   // sign | exponent bits of s (mantissa 0)
+  int es;        // exponent field
+  bool neg;
+};
+DR_HD inline bool seg_grid_of(float s, SegGrid* g, int64_t* a) {
+  const uint32_t bs = f32_bits(s);
+  const int es = (int)((bs >> 23) & 0xFF);
+  if (es == 0 || es == 0xFF) return false;
+  g->se = bs & 0xFF800000u;
+  g->es = es;
+  g->neg = (bs >> 31) != 0;
+  *a = (int64_t)(bs & 0x7FFFFFu) | 0x800000;
+  return true;
+}
+DR_HD inline float seg_grid_value(const SegGrid& g, int64_t a) {   // a in [2^23, 2^24)
+  return __builtin_bit_cast(float, g.se + (uint32_t)(a - 0x800000));
+}
+
+// One term on a grid: D = its step in ulps along the magnitude, fs the sign
+// of (x in ulps - D) along the magnitude (0: exact), tie: x is an odd
+// multiple of half an ulp.  ok = false: not expressible as a grid step
+// (x within 2 binades of s, a non-finite or subnormal x) -- a plain add.
+struct SegTerm {
+  int64_t D;
+  int fs;
+  bool tie, ok;
+};
+DR_HD inline SegTerm seg_grid_term(const SegGrid& g, float x) {
+  SegTerm r{0, 0, false, true};
+  const uint32_t bx = f32_bits(x);
+  const int ex = (int)((bx >> 23) & 0xFF);
+  if ((bx & 0x7FFFFFFFu) == 0) return r;          // +-0: the sum is unchanged
+  if (ex == 0 || ex == 0xFF) {
+    r.ok = false;
+    return r;
+  }
+  const int sh = g.es - ex;
+  if (sh < 1) {
+    r.ok = false;
+    return r;
+  }
+  const bool grow = ((bx >> 31) != 0) == g.neg;   // x along s's sign
+  if (sh > 25) {   // |x| < 2^-2 ulps: every add rounds back to s (never a tie)
+    r.fs = grow ? 1 : -1;
+    return r;
+  }
+  const int64_t mx = (int64_t)((bx & 0x7FFFFFu) | 0x800000u);
+  const int64_t ip = mx >> sh, fr = mx & (((int64_t)1 << sh) - 1), half = (int64_t)1 << (sh - 1);
+  const bool up = fr > half || (fr == half && (ip & 1));
+  r.tie = fr == half;
+  const int64_t dabs = ip + (up ? 1 : 0);
+  r.D = grow ? dabs : -dabs;
+  int fs = fr == 0 ? 0 : (up ? -1 : 1);
+  r.fs = grow ? fs : -fs;
+  return r;
+}
+
+// k adds of the term from a (the running sum in ulps) all round on the grid
+DR_HD inline bool seg_grid_fits(int64_t a, int64_t k, const SegTerm& t) {
+  if (!t.ok || (t.tie && (a & 1))) return false;
+  const int64_t lo = 0x800000, hi = 0x1000000;
+  const int64_t a1 = a + t.D, ak = a + k * t.D;
+  auto in_grid = [&](int64_t ap) {
+    const bool below_hi = t.fs < 0 ? ap <= hi : ap < hi;
+    const bool above_lo = t.fs < 0 ? ap >= lo + 1 : ap >= lo;
+    return below_hi && above_lo;
+  };
+  return in_grid(a1) && in_grid(ak);
+}
+
 }  // namespace dr

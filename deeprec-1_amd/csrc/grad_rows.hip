@@ -101,12 +101,28 @@ static int serial_dma() {   // read per call (host, once per backward): tests co
 // of branchy integer work against 8.5 per position for the plain chain, so
 // it only pays for segments of ~70+ terms; DIN's average 50 (4 050 segments
 // over 203 800 padding positions) walked 4x slower (profiles/r05_seg_walk.log).
-// Read per call (DR_GRAD_SEG_SCAN=n positions; 0, the default, = off).
-static constexpr int64_t kSegMin = 64;
+// Read per call (DR_GRAD_SEG_SCAN=n positions; 0 = off).
+// Round 6: DR_GRAD_SEG_ROUNDS=1 (opt-in) walks the segments by a whole wave
+// in rounds (wave_rounds_walk: every segment of a window on the running
+// sum's grid at once, an integer prefix over the lanes, the segment where the
+// grid changes added exactly by seg_add), scanning runs longer than 4 096
+// positions and walking them by segments when they average >= 8 terms.  Its
+// cost is data-dependent: a round per grid change.  DIN's padding chain at
+// the first step (sums growing steadily to ~0.06) takes ~100 rounds per
+// column, 0.48 ms against the plain walk's 1.0; after training the column
+// sums wander around 1e-5, every few segments change the grid (200-350
+// rounds per column, tools/din_term_probe.py DTP_STEPS + tools/
+// repadd_check.cpp file mode) and the walk takes 0.3-1.6 ms per step, 1.0 on
+// average -- no better than the plain walk, which stays the default
+// (profiles/r06_seg_rounds_walk.log).
+static bool seg_rounds_host();
+static constexpr int64_t kSegPlainMax = 256;   // seg_add: plain adds up to this many
 static int64_t seg_scan() {
   const char* e = getenv("DR_GRAD_SEG_SCAN");
-  return e ? (int64_t)atoll(e) : (int64_t)0;
+  if (e) return (int64_t)atoll(e);
+  return seg_rounds_host() ? (int64_t)4096 : (int64_t)0;
 }
+static int32_t seg_min() { return seg_rounds_host() ? 8 : 64; }
 
 static int64_t zero_scan() {
   // read per call (host only, once per backward): tests switch it on around
@@ -147,6 +163,8 @@ struct RowsLong {
   int dma;                 // who takes the plain-sum runs (serial_dma()): 1 plain, 2 dma
   int32_t* rseg;           // per long run: its segment count (seg scan; -1: not scanned)
   int64_t sscan;           // seg-scan plain runs longer than this (0: never)
+  int32_t segmin;          // walk a seg-scanned run by segments from this mean length
+  int32_t srounds;         // segment walk in wave rounds (wave_rounds_walk)
 };
 
 // A zero-scanned run is walked compacted only when at most half its terms
@@ -159,7 +177,7 @@ __device__ __forceinline__ bool run_sparse(const RowsLong& L, int i, int np, int
 // A seg-scanned run is walked by segments when they average at least kSegMin
 // terms (every walker applies the same test, so they split the runs exactly).
 __device__ __forceinline__ bool run_seg(const RowsLong& L, int i, int np, int64_t len) {
-  return np == 1 && L.cfirst[i] >= 0 && L.rseg[i] >= 0 && kSegMin * (int64_t)L.rseg[i] <= len;
+  return np == 1 && L.cfirst[i] >= 0 && L.rseg[i] >= 0 && (int64_t)L.segmin * L.rseg[i] <= len;
 }
 
 // Table of global position i (lane-varying; koff staged in LDS).
@@ -1000,6 +1018,121 @@ __global__ __launch_bounds__(256) void rows_seg_kernel(RowsGroup g, int T, int d
   }
 }
 
+// Inclusive prefix sum over the 64 lanes of a wave: DPP row shifts inside
+// each 16-lane row (out-of-row sources read 0), then the row totals added
+// from lanes 15 / 31 / 47 by readlane (VALU + SALU, no LDS permute).
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);   // row_shr:8
+  const int r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31),
+            r2 = __builtin_amdgcn_readlane(v, 47);
+  const int row = lane >> 4;
+  return v + (row >= 1 ? r0 : 0) + (row >= 2 ? r1 : 0) + (row >= 3 ? r2 : 0);
+}
+
+// One column's segments [0, nv) walked by a whole wave in rounds
+// (dr_repadd.h "many segments at once"): each round, lane l takes segment
+// i + l -- its term's step on the current sum's grid, an exclusive prefix of
+// k * D over the lanes, whether its adds stay on the grid from there -- and
+// the wave moves the sum past every segment before the first lane that does
+// not fit in one step; that segment is added exactly by rep_add and the next
+// round starts on the new grid.  A zero / subnormal sum: one rep_add.
+// sp: the column's terms, qe: segment end positions (LDS), pe0: the end of
+// the segment before the first.  Bit-equal to rep_add segment by segment.
+// k adds of x to acc, exactly: the plain adds themselves for a short
+// segment (one dependent v_add_f32 each, ~8.5 cycles -- a DIN segment's ~50
+// cost less than rep_add's double-precision closed form, ~2-4 k cycles of
+// dependent instructions), rep_add for a long one.
+__device__ __forceinline__ float seg_add(float acc, float x, int64_t k) {
+  if (k > kSegPlainMax) return rep_add(acc, x, k);
+  for (int q = 0; q < (int)k; ++q) acc = acc + x;
+  return acc;
+}
+
+#ifdef DR_SEG_DEBUG
+__device__ unsigned long long g_dbg[4096][3];   // (measurement build) per wave: rounds, rep_add, walk cycles
+#endif
+__device__ __noinline__ float wave_rounds_walk(float acc, const float* sp, const int32_t* qe, int nv,
+                                               int64_t pe0, int lane) {
+  int i = 0;
+  int64_t pe = pe0;
+#ifdef DR_SEG_DEBUG
+  int nr = 0;
+  uint64_t t_rep = 0;
+  const uint64_t t_all = clock64();
+#endif
+  while (i < nv) {   // wave-uniform
+#ifdef DR_SEG_DEBUG
+    ++nr;
+#endif
+    SegGrid g;
+    int64_t a;
+    if (!seg_grid_of(acc, &g, &a)) {
+      const int64_t q = qe[i];
+      acc = seg_add(acc, sp[i], q - pe);
+      pe = q;
+      ++i;
+      continue;
+    }
+    const int j = i + lane;
+    const bool in = j < nv;
+    const float x = in ? sp[j] : 0.f;
+    const int32_t q = in ? qe[j] : 0;
+    const int32_t qp = lane == 0 ? (int32_t)pe : (in ? qe[j - 1] : 0);
+    const int32_t k = in ? q - qp : 0;
+    const SegTerm t = seg_grid_term(g, x);
+    // the lane's move k * D, clamped to +-(2^24 + 1) ulps: a clamped lane
+    // leaves the binade itself (its own fits test below uses k * D
+    // unclamped), so it or an earlier lane is the first stop and every prefix
+    // before it is exact; 64 clamped values cannot overflow int32
+    int64_t c64 = (in && t.ok) ? (int64_t)k * t.D : 0;
+    c64 = c64 > 0x1000001 ? 0x1000001 : (c64 < -0x1000001 ? -0x1000001 : c64);
+    const int c = (int)c64;
+    const int incl = wave_incl_scan(c, lane);
+    const int excl = incl - c;
+    const bool stop = !in || !seg_grid_fits(a + excl, k, t);
+    const uint64_t sm = __ballot(stop);
+    const int f = sm ? __builtin_ctzll(sm) : 64;   // segments i .. i + f - 1 fit (wave-uniform)
+    const int64_t af = a + (f < 64 ? __builtin_amdgcn_readlane(excl, f)
+                                   : __builtin_amdgcn_readlane(incl, 63));
+    acc = seg_grid_value(g, af);
+    if (f < 64 && i + f < nv) {   // segment i + f: one exact rep_add
+      const int32_t kf = __builtin_amdgcn_readlane(k, f);
+      const float xf = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), f));
+#ifdef DR_SEG_DEBUG
+      const uint64_t t0 = clock64();
+#endif
+      acc = seg_add(acc, xf, kf);
+#ifdef DR_SEG_DEBUG
+      t_rep += clock64() - t0;
+#endif
+      i += f + 1;
+    } else {
+      i += f < 64 ? f : 64;
+    }
+    pe = qe[i - 1];
+  }
+#ifdef DR_SEG_DEBUG
+  if (lane == 0) {
+    const int slot = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    g_dbg[slot][0] += nr;
+    g_dbg[slot][1] += t_rep;
+    g_dbg[slot][2] += clock64() - t_all;
+  }
+#endif
+  return acc;
+}
+
+// DR_GRAD_SEG_ROUNDS (default 0): 1 = the segment walk takes segments in
+// rounds of a wave (wave_rounds_walk, and the scan on from 4 096 positions);
+// 0 = one rep_add per segment where DR_GRAD_SEG_SCAN asks for a scan
+static bool seg_rounds_host() {
+  const char* e = getenv("DR_GRAD_SEG_ROUNDS");
+  return e && atoi(e) != 0;
+}
+
 // The runs walked by segments (run_seg()): one block per (run, slice of 16
 // columns).  Windows of up to 256 chunks: the chunks' segment ends (kpos)
 // in ascending order, prefix of their counts in LDS; stages of up to 1024
@@ -1009,15 +1142,18 @@ __global__ __launch_bounds__(256) void rows_seg_kernel(RowsGroup g, int T, int d
 // acc = rep_add(acc, term, length) per segment, in order.  The chain starts
 // at 0 (the sum combiner), so the first segment's first add is 0 + x, as in
 // the plain walk.
-template <int VEC, bool SGD, bool WB>
-__global__ __launch_bounds__(1024) void rows_serial_seg_kernel(RowsGroup g, int T, int dim,
-                                                               RowsLong L, RowsSgd sg) {
+// SW columns per slice, NT threads: (16, 1024) for the one-wave-per-column
+// rep_add walk (16 walker waves on one CU); (4, 256) for the wave-rounds
+// walk, whose whole-wave rounds are VALU work: one column per SIMD, the
+// slices spread over CUs.
+template <int VEC, bool SGD, bool WB, int SW, int NT>
+__global__ __launch_bounds__(NT) void rows_serial_seg_kernel(RowsGroup g, int T, int dim,
+                                                             RowsLong L, RowsSgd sg) {
   using V = typename VecT<VEC>::T;
-  constexpr int SW = 16;           // columns per slice
   constexpr int SV = SW / VEC;     // vectors of a term's slice
   constexpr int S = 1024;          // segments per stage
-  constexpr int NT = 1024;
   constexpr int WCH = NT;          // chunks per window (one per thread)
+  static_assert(SW % VEC == 0 && SW % 2 == 0 && SW <= NT / 64, "slice shape");
   __shared__ __attribute__((aligned(16))) float stage[SW * S];
   __shared__ int32_t qend[S];
   __shared__ int64_t sk[DR_MAX_GROUP + 1];
@@ -1034,6 +1170,9 @@ __global__ __launch_bounds__(1024) void rows_serial_seg_kernel(RowsGroup g, int 
   // wave on its own path (16 columns on the lanes of one wave ran the union
   // of their paths: 2-3x slower than the plain walk, profiles/r05_seg_walk.log)
   const int wcol = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // the chains are the backward's critical path: ahead of co-resident waves
+  // of other kernels (the DIN step runs this on a side stream beside them)
+  __builtin_amdgcn_s_setprio(3);
   for (int64_t wi = blockIdx.x; wi < total; wi += gridDim.x) {   // block-uniform
     const int j = (int)(wi / nsl), slice = (int)(wi % nsl);
     const int i = L.items[2 * j];
@@ -1050,6 +1189,10 @@ __global__ __launch_bounds__(1024) void rows_serial_seg_kernel(RowsGroup g, int 
     const int64_t ts = d.top_stride;
     float acc = 0.f;
     int64_t prev = c0 - 1;   // the end of the segment before the stage's first
+#ifdef DR_SEG_DEBUG
+    uint64_t t_pre = 0, t_stage = 0, t_walk = 0, tc = clock64();
+    int nseg = 0;
+#endif
     for (int64_t w0 = 0; w0 < nch; w0 += WCH) {
       const int nw = (int)(nch - w0 < WCH ? nch - w0 : WCH);
       // exclusive prefix of the window's chunk counts (one chunk per thread)
@@ -1068,6 +1211,9 @@ __global__ __launch_bounds__(1024) void rows_serial_seg_kernel(RowsGroup g, int 
       if (tid == nw - 1) cpre[nw] = before + cnt;
       __syncthreads();
       const int K = cpre[nw];
+#ifdef DR_SEG_DEBUG
+      { const uint64_t t = clock64(); t_pre += t - tc; tc = t; }
+#endif
       for (int b0 = 0; b0 < K; b0 += S) {
         const int nv = K - b0 < S ? K - b0 : S;
         for (int e = tid; e < nv; e += NT) {
@@ -1101,19 +1247,41 @@ __global__ __launch_bounds__(1024) void rows_serial_seg_kernel(RowsGroup g, int 
           }
         }
         __syncthreads();
+#ifdef DR_SEG_DEBUG
+        { const uint64_t t = clock64(); t_stage += t - tc; tc = t; nseg += nv; }
+#endif
         if (wcol < SW && slice * SW + wcol < dim) {   // (columns past dim: idle)
           const float* sp = stage + wcol * S;
-          int64_t pe = prev;
-          for (int e = 0; e < nv; ++e) {
-            const int32_t q = qend[e];
-            acc = rep_add(acc, sp[e], (int64_t)q - pe);
-            pe = q;
+          if (L.srounds)
+            acc = wave_rounds_walk(acc, sp, qend, nv, prev, lane);
+          else {
+            int64_t pe = prev;
+            for (int e = 0; e < nv; ++e) {
+              const int32_t q = qend[e];
+              acc = rep_add(acc, sp[e], (int64_t)q - pe);
+              pe = q;
+            }
           }
         }
         prev = qend[nv - 1];
         __syncthreads();   // the stage and qend are rewritten next
+#ifdef DR_SEG_DEBUG
+        { const uint64_t t = clock64(); t_walk += t - tc; tc = t; }
+#endif
       }
     }
+#ifdef DR_SEG_DEBUG
+    if (lane == 0 && wcol == 0)
+      printf("segwalk run %d slice %d: segs %d chunks %lld pre %llu stage %llu walk %llu cycles\n",
+             i, slice, nseg, (long long)nch, (unsigned long long)t_pre, (unsigned long long)t_stage,
+             (unsigned long long)t_walk);
+    if (lane == 0 && L.srounds) {
+      const int slot = blockIdx.x * 4 + wcol;
+      printf("roundswalk run %d slice %d col %d: rounds %llu rep_add %llu walk %llu cycles\n", i,
+             slice, wcol, g_dbg[slot][0], g_dbg[slot][1], g_dbg[slot][2]);
+      g_dbg[slot][0] = g_dbg[slot][1] = g_dbg[slot][2] = 0;
+    }
+#endif
     if (wcol < SW && lane == 0) accs[wcol] = acc;
     __syncthreads();
     if (wcol == 0) {
@@ -1700,7 +1868,8 @@ struct RowsWs {
   RowsLong longrun(uint64_t* gptr, float* gu) const {
     return RowsLong{kout, perm, ex, base, srow, smul, sdiv, longs, nlong, rlen, rfirst, items,
                     nitems, gptr, gu, part, serial_max(), zero_scan(), cfirst, crun, nchunk,
-                    ccnt, kpos, rnz, zrow, serial_dma(), rseg, seg_scan()};
+                    ccnt, kpos, rnz, zrow, serial_dma(), rseg, seg_scan(), seg_min(),
+                    (int32_t)seg_rounds_host()};
   }
 };
 
@@ -1835,19 +2004,31 @@ static void launch_long(const RowsGroup& g, int T, int dim, const RowsLong& L, c
       hipLaunchKernelGGL((rows_serial_plain_kernel<1, SGD, WB>), dim3((unsigned)db), dim3(1024), 0,
                          s, g, T, dim, L, sg);
   }
-  if (segs) {
+  if (segs && L.srounds) {   // wave rounds: 4 columns per 256-thread block
+    int64_t sb2 = runs * ceil_div(dim, 4);
+    if (sb2 > 1024) sb2 = 1024;
+    if (VEC == 4)
+      hipLaunchKernelGGL((rows_serial_seg_kernel<VEC, SGD, WB, 4, 256>), dim3((unsigned)sb2),
+                         dim3(256), 0, s, g, T, dim, L, sg);
+    else if (aligned2 && dim % 2 == 0)
+      hipLaunchKernelGGL((rows_serial_seg_kernel<2, SGD, WB, 4, 256>), dim3((unsigned)sb2),
+                         dim3(256), 0, s, g, T, dim, L, sg);
+    else
+      hipLaunchKernelGGL((rows_serial_seg_kernel<1, SGD, WB, 4, 256>), dim3((unsigned)sb2),
+                         dim3(256), 0, s, g, T, dim, L, sg);
+  } else if (segs) {
     const int64_t nsl16 = ceil_div(dim, 16);
     int64_t sb2 = runs * nsl16;
     if (sb2 > 1024) sb2 = 1024;
     if (VEC == 4)
-      hipLaunchKernelGGL((rows_serial_seg_kernel<VEC, SGD, WB>), dim3((unsigned)sb2), dim3(1024), 0,
-                         s, g, T, dim, L, sg);
+      hipLaunchKernelGGL((rows_serial_seg_kernel<VEC, SGD, WB, 16, 1024>), dim3((unsigned)sb2),
+                         dim3(1024), 0, s, g, T, dim, L, sg);
     else if (aligned2 && dim % 2 == 0)
-      hipLaunchKernelGGL((rows_serial_seg_kernel<2, SGD, WB>), dim3((unsigned)sb2), dim3(1024), 0,
-                         s, g, T, dim, L, sg);
+      hipLaunchKernelGGL((rows_serial_seg_kernel<2, SGD, WB, 16, 1024>), dim3((unsigned)sb2),
+                         dim3(1024), 0, s, g, T, dim, L, sg);
     else
-      hipLaunchKernelGGL((rows_serial_seg_kernel<1, SGD, WB>), dim3((unsigned)sb2), dim3(1024), 0,
-                         s, g, T, dim, L, sg);
+      hipLaunchKernelGGL((rows_serial_seg_kernel<1, SGD, WB, 16, 1024>), dim3((unsigned)sb2),
+                         dim3(1024), 0, s, g, T, dim, L, sg);
   }
   if (N > L.smax) {
     const int64_t big = N / (L.smax + 1) + 1;

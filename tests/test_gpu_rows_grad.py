@@ -217,7 +217,16 @@ def _repeated_terms(rng, n, D):
     return rows
 
 
-@pytest.mark.parametrize("seg", ["4096", "0"])
+def _seg_env(monkeypatch, seg):
+    """"4096": segment scan, wave-rounds walk (DR_GRAD_SEG_ROUNDS=1, opt-in);
+    "4096/r0": segment scan, one rep_add per segment (round 5's walk); "0": no
+    scan, the plain walk (the default)."""
+    s, _, r = seg.partition("/")
+    monkeypatch.setenv("DR_GRAD_SEG_SCAN", s)
+    monkeypatch.setenv("DR_GRAD_SEG_ROUNDS", "0" if r == "r0" else "1")
+
+
+@pytest.mark.parametrize("seg", ["4096", "4096/r0", "0"])
 @pytest.mark.parametrize("D", [18, 32, 1])
 def test_rows_backward_repeated_terms(dr, orc, D, seg, monkeypatch):
     """Long runs whose terms come in blocks of identical rows (DIN's padding
@@ -227,8 +236,10 @@ def test_rows_backward_repeated_terms(dr, orc, D, seg, monkeypatch):
     (rows_serial_seg_kernel + rep_add); off (0, the default), position by
     position.
     Both bit-equal to the reference's serial sum; a long run without
-    repeats rides along (scanned, then walked plainly)."""
-    monkeypatch.setenv("DR_GRAD_SEG_SCAN", seg)
+    repeats rides along (scanned, then walked plainly).  Round 6: the
+    segments walked by a whole wave in rounds (wave_rounds_walk, DR_GRAD_SEG_ROUNDS=1),
+    the round-5 walk one segment at a time ("4096/r0")."""
+    _seg_env(monkeypatch, seg)
     rng = np.random.default_rng(61 + D)
     v = np.concatenate([np.zeros(60000, np.int64), np.ones(5000, np.int64),
                         rng.integers(2, 300, 4000).astype(np.int64)])
@@ -241,7 +252,8 @@ def test_rows_backward_repeated_terms(dr, orc, D, seg, monkeypatch):
     evs, sps = [], []
     ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
     for f in range(3):
-        evs.append(dr.EmbeddingVariable("rrep_%d_%d_%s" % (D, f, seg), D, 0.1, capacity=1024))
+        evs.append(dr.EmbeddingVariable("rrep_%d_%d_%s" % (D, f, seg.replace("/", "")), D, 0.1,
+                                        capacity=1024))
         sps.append(dr.SparseTensor(T(ind), T(v), (B, 1)))
     out = dr.embedding_lookup_sparse_multi(evs, sps, combiner="sum")
     out.backward(T(g))
@@ -272,9 +284,9 @@ def test_rows_sgd_repeated_terms_seg_equals_plain(dr, monkeypatch):
         gs.append(g)
     ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
     res = []
-    for seg in ("4096", "0"):
-        monkeypatch.setenv("DR_GRAD_SEG_SCAN", seg)
-        ev = dr.EmbeddingVariable("rrep_sgd_%s" % seg, D, 0.1, capacity=1024)
+    for seg in ("4096", "4096/r0", "0"):
+        _seg_env(monkeypatch, seg)
+        ev = dr.EmbeddingVariable("rrep_sgd_%s" % seg.replace("/", ""), D, 0.1, capacity=1024)
         opt = dr.GradientDescentOptimizer(0.05)
         for step, g in enumerate(gs):
             out = dr.embedding_lookup_sparse(ev, dr.SparseTensor(T(ind), T(v), (B, 1)),
@@ -283,9 +295,47 @@ def test_rows_sgd_repeated_terms_seg_equals_plain(dr, monkeypatch):
             opt.apply_gradients([ev], global_step=step)
         torch.cuda.synchronize()
         res.append(_export(ev))
-    (k1, v1), (k2, v2) = res
-    np.testing.assert_array_equal(k1, k2)
-    np.testing.assert_array_equal(v1.view(np.uint32), v2.view(np.uint32))
+    (k1, v1) = res[0]
+    for k2, v2 in res[1:]:
+        np.testing.assert_array_equal(k1, k2)
+        np.testing.assert_array_equal(v1.view(np.uint32), v2.view(np.uint32))
+
+
+@pytest.mark.parametrize("seg", ["4096", "0"])
+def test_rows_backward_din_padding_chain(dr, orc, seg, monkeypatch):
+    """DIN's padding id at configs[3]'s size: ~4 000 samples, each adding its
+    his_sum gradient row at every padded position (1..99 identical terms,
+    normal values of both signs -- the running sum walks through zero and
+    across binades), 2 x 10^5 positions in one run, D = 18: the wave-rounds
+    segment walk (opt-in) and the plain walk bit-equal to the reference's
+    serial sum."""
+    _seg_env(monkeypatch, seg)
+    rng = np.random.default_rng(2024)
+    D, S = 18, 4000
+    k = rng.integers(1, 100, S)
+    terms = (rng.standard_normal((S, D)) * 10.0 ** rng.uniform(-6, -3, (S, 1))).astype(np.float32)
+    n0 = int(k.sum())
+    g0 = np.repeat(terms, k, axis=0)
+    other = rng.integers(1, 5000, 30000).astype(np.int64)
+    v = np.concatenate([np.zeros(n0, np.int64), other])
+    g = np.concatenate([g0, rng.standard_normal((other.size, D)).astype(np.float32)])
+    B = v.size
+    ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+    # the mid / cat pair of DIN's item lookup: two EVs, one grouped lookup
+    evs = [dr.EmbeddingVariable("rdin_%s_%d" % (seg, f), D, 0.1, capacity=8192) for f in range(2)]
+    gg = np.concatenate([g, g[::-1].copy()], 1)
+    out = dr.embedding_lookup_sparse_multi(
+        evs, [dr.SparseTensor(T(ind), T(v), (B, 1)) for _ in range(2)], combiner="sum")
+    out.backward(T(gg))
+    uids, idx = orc.unique(v)
+    for f in range(2):
+        sl = evs[f].pending_grads.pop()
+        U = int(sl.num_valid.item())
+        assert H(sl.indices[:U]).tolist() == uids.tolist()
+        gf = np.ascontiguousarray(gg[:, f * D:(f + 1) * D])
+        ref = orc.sparse_segment_reduce_grad(gf, idx, np.arange(B, dtype=np.int32), U, "sum")
+        np.testing.assert_array_equal(H(sl.values[:U]).view(np.uint32), ref.view(np.uint32))
+    dr.status_check()
 
 
 @pytest.mark.parametrize("side", [True, False])

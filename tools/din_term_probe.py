@@ -37,13 +37,22 @@ def main():
              torch.randint(0, R[1], (B,), generator=g, device=dev),
              torch.randint(0, R[2], (B,), generator=g, device=dev), mh, ch, mask,
              torch.stack([lab, 1 - lab], 1).float())
+    # DTP_STEPS: train this many steps first (Adam, the bench's optimizers),
+    # so the terms are a trained model's rather than the first step's
+    nsteps = int(os.environ.get("DTP_STEPS", "0"))
+    if nsteps:
+        dopt = torch.optim.Adam(model.parameters(), lr=0.001)
+        eopt = dr.AdamOptimizer(0.001)
+        for i in range(nsteps):
+            mz.din_train_step(model, batch, dopt, eopt, i)
+        torch.cuda.synchronize()
     grads = []
     inner = model.item_lookup
 
     class Hooked(object):
         def __call__(self, ids):
             out = inner(ids)
-            if ids.shape[1] == B * Tb:
+            if ids.shape[1] in (B * Tb, B + B * Tb):   # history-only or one item lookup
                 out.register_hook(lambda gr: grads.append(gr.detach().clone()))
             return out
     model.item_lookup = Hooked()
@@ -51,8 +60,9 @@ def main():
     loss = -(torch.log(y) * batch[6]).mean()
     loss.backward()
     torch.cuda.synchronize()
-    gh = grads[0].reshape(B * Tb, 2, D)               # [positions, table, D]
+    gh = grads[0][-B * Tb:].reshape(B * Tb, 2, D)     # [positions, table, D]
     pad = (mask.reshape(-1) == 0).nonzero().squeeze(1)  # ascending positions of id 0
+    segs = {}
     for t, name in ((0, "mid"), (1, "cat")):
         rows = gh[pad, t].contiguous().view(torch.int32)
         n = rows.shape[0]
@@ -64,10 +74,18 @@ def main():
                             diff_row.nonzero().squeeze(1) + 1,
                             torch.tensor([n], device=dev)])
         longest = int((bounds[1:] - bounds[:-1]).max())
+        if os.environ.get("DTP_SAVE"):   # segment terms + lengths, for host replays
+            import numpy as np
+            segs[name] = (rows[bounds[:-1]].view(torch.float32).cpu().numpy(),
+                          (bounds[1:] - bounds[:-1]).cpu().numpy())
         print("%s: padding run %d positions, %d row segments (mean %.1f, longest %d), "
               "per-column segments %d..%d; samples with padding %d"
               % (name, n, seg, n / seg, longest, int(seg_col.min()), int(seg_col.max()),
                  int((lens < Tb).sum())), flush=True)
+    if segs:
+        import numpy as np
+        np.savez(os.environ["DTP_SAVE"], **{"%s_terms" % k: v[0] for k, v in segs.items()},
+                 **{"%s_len" % k: v[1] for k, v in segs.items()})
 
 
 if __name__ == "__main__":

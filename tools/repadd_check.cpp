@@ -45,7 +45,140 @@ static float pick_x(float s) {
   }
 }
 
+static long g_prefix_bad = 0;
+static void SegGrid_check(const dr::SegGrid& g, float acc, int64_t a, int32_t pre) {
+  dr::SegGrid g0;
+  int64_t a0;
+  dr::seg_grid_of(acc, &g0, &a0);
+  if (a0 + pre != a) ++g_prefix_bad;
+  (void)g;
+}
+
+// The windowed rounds walk (dr_repadd.h "many segments at once"), as the
+// device kernel runs it, emulated sequentially: per round a window of W
+// segments on the current grid, exclusive prefix of k*D, first segment that
+// does not fit, the fitting ones taken at once, the failing one by rep_add.
+static float rounds_walk(float acc, const float* x, const int64_t* k, int n, int W,
+                         long* rounds) {
+  int i = 0;
+  while (i < n) {
+    ++*rounds;
+    dr::SegGrid g;
+    int64_t a;
+    if (!dr::seg_grid_of(acc, &g, &a)) {   // zero / subnormal / non-finite sum
+      acc = dr::rep_add(acc, x[i], k[i]);
+      ++i;
+      continue;
+    }
+    const int e = i + W < n ? i + W : n;
+    int j = i;
+    int32_t pre = 0;   // the device's clamped int32 prefix (wave_incl_scan)
+    for (; j < e; ++j) {
+      const dr::SegTerm t = dr::seg_grid_term(g, x[j]);
+      if (!dr::seg_grid_fits(a, k[j], t)) break;
+      a += k[j] * t.D;
+      int64_t c = t.ok ? k[j] * t.D : 0;
+      c = c > 0x1000001 ? 0x1000001 : (c < -0x1000001 ? -0x1000001 : c);
+      pre += (int32_t)c;
+    }
+    {   // the fitting prefix, as the device forms it: start + clamped int32 sum
+      SegGrid_check(g, acc, a, pre);
+    }
+    acc = dr::seg_grid_value(g, a);
+    if (j < e) {
+      acc = dr::rep_add(acc, x[j], k[j]);
+      ++j;
+    }
+    i = j;
+  }
+  return acc;
+}
+
+// chains of segments: DIN-like (normal terms, 1..99 repeats, signs mixed),
+// narrow-range terms, ties (terms at half-ulp multiples of a running sum),
+// zeros and tiny / huge terms mixed in
+static int rounds_mode(long chains, int W) {
+  long bad = 0, segs = 0, rounds = 0;
+  for (long c = 0; c < chains; ++c) {
+    const int n = 1 + (int)(rnd() % 5000);
+    float* x = (float*)malloc(sizeof(float) * n);
+    int64_t* k = (int64_t*)malloc(sizeof(int64_t) * n);
+    const int regime = (int)(rnd() % 4);
+    const float scale = ldexpf(1.f, (int)(rnd() % 40) - 30);
+    for (int j = 0; j < n; ++j) {
+      float v;
+      const double u = ((double)(rnd() >> 11) / 9007199254740992.0) * 2.0 - 1.0;
+      switch (regime) {
+        case 0: v = (float)(u * scale); break;                                   // DIN-like
+        case 1: v = (float)((0.5 + 0.25 * u) * scale); break;                    // one sign
+        case 2: v = ldexpf((float)((int)(rnd() % 64) - 32), (int)(rnd() % 6) - 30); break;  // ties
+        default: v = (rnd() % 16 == 0) ? 0.f : (rnd() % 32 == 0 ? (float)(u * 1e6) : (float)(u * scale));
+      }
+      x[j] = v;
+      k[j] = 1 + (int64_t)(rnd() % (regime == 2 ? 8 : 99));
+    }
+    float ref = 0.f;
+    for (int j = 0; j < n; ++j)
+      for (int64_t q = 0; q < k[j]; ++q) ref = ref + x[j];
+    long r = 0;
+    const float got = rounds_walk(0.f, x, k, n, W, &r);
+    if (dr::f32_bits(ref) != dr::f32_bits(got) && !(isnan(ref) && isnan(got))) {
+      if (bad < 20) printf("MISMATCH chain %ld regime %d n %d ref=%a got=%a\n", c, regime, n, ref, got);
+      ++bad;
+    }
+    segs += n;
+    rounds += r;
+    free(x);
+    free(k);
+  }
+  printf("rounds mode: chains %ld segments %ld rounds %ld (%.3f per segment) mismatches %ld "
+         "int32-prefix mismatches %ld\n", chains, segs, rounds, (double)rounds / (double)segs, bad,
+         g_prefix_bad);
+  bad += g_prefix_bad;
+  return bad ? 1 : 0;
+}
+
+// Real chains from a file (tools/din_term_probe.py DTP_SAVE, converted to
+// int64 n, int64 D, float terms[n][D], int64 lengths[n]): every column
+// walked, the rounds counted, the result checked against the plain loop.
+static int file_mode(const char* path, int W) {
+  FILE* f = fopen(path, "rb");
+  if (!f) { perror(path); return 2; }
+  int64_t n = 0, D = 0;
+  if (fread(&n, 8, 1, f) != 1 || fread(&D, 8, 1, f) != 1) return 2;
+  float* t = (float*)malloc(sizeof(float) * n * D);
+  int64_t* k = (int64_t*)malloc(sizeof(int64_t) * n);
+  float* x = (float*)malloc(sizeof(float) * n);
+  if (fread(t, sizeof(float), n * D, f) != (size_t)(n * D) || fread(k, 8, n, f) != (size_t)n) return 2;
+  fclose(f);
+  long bad = 0, rounds = 0, zero_runs = 0;
+  for (int64_t c = 0; c < D; ++c) {
+    for (int64_t j = 0; j < n; ++j) x[j] = t[j * D + c];
+    float ref = 0.f;
+    for (int64_t j = 0; j < n; ++j)
+      for (int64_t q = 0; q < k[j]; ++q) ref = ref + x[j];
+    long r = 0;
+    const float got = rounds_walk(0.f, x, k, (int)n, W, &r);
+    bad += dr::f32_bits(ref) != dr::f32_bits(got);
+    rounds += r;
+    int64_t z = 0;
+    while (z < n && x[z] == 0.f) ++z;
+    zero_runs += z;
+    printf("col %2lld: rounds %5ld  leading zero segments %lld  sum %a\n", (long long)c, r,
+           (long long)z, got);
+  }
+  printf("file %s: segments %lld x %lld columns, rounds %ld (%.3f per segment) mismatches %ld\n",
+         path, (long long)n, (long long)D, rounds, (double)rounds / (double)(n * D), bad);
+  return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 2 && !strcmp(argv[1], "file"))
+    return file_mode(argv[2], argc > 3 ? atoi(argv[3]) : 256);
+  if (argc > 1 && !strcmp(argv[1], "rounds")) {
+    st = argc > 3 ? strtoull(argv[3], 0, 10) : 88172645463325252ull;
+    return rounds_mode(argc > 2 ? atol(argv[2]) : 2000, argc > 4 ? atoi(argv[4]) : 256);
+  }
   const long cases = argc > 1 ? atol(argv[1]) : 200000;
   st = argc > 2 ? strtoull(argv[2], 0, 10) : 88172645463325252ull;
   long bad = 0, jumps = 0;
