@@ -124,7 +124,8 @@ def cpu_baseline(args):
     CPU worker threads).  Unique is UniqueAliOp's default: ParallelComputeV1
     for N >= 14336 (unique_ali_op_util.h:651-657; serial_ = false,
     unique_ali_op.cc:55-56); the serial-Unique variant is timed beside it.
-    Three timed repeats each (median reported, min / max as the spread).
+    Five timed repeats each, interleaved (median reported, (max - min) /
+    median as the spread); the id batches are drawn before timing.
     Threads: the box's CPU share (OMP_NUM_THREADS, else the affinity mask)."""
     from oracle import oracle as orc
     threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
@@ -143,10 +144,13 @@ def cpu_baseline(args):
     reps = 5
     per = args.cpu_seconds / (2 * reps)
 
+    batches = [rng.integers(0, R, B).astype(np.int64) for _ in range(16)]
+
     def timed(serial):
-        done, t0 = 0, time.perf_counter()
+        done, t0, it = 0, time.perf_counter(), 0
         while True:
-            ids = rng.integers(0, R, B).astype(np.int64)
+            ids = batches[it % len(batches)]
+            it += 1
             rc = L.orc_pipeline_ev_lookup_sparse_pool(pool._h, ev._h, orc._p(ids), B,
                                                       orc._p(seg_off), B, 0, int(serial),
                                                       orc._p(out))
@@ -686,9 +690,13 @@ def din_leg(args, dev, log, world, rank, dist, staged):
                         torch.randint(0, R[2], (B,), generator=g, device=dev), mh, ch, mask,
                         torch.stack([lab, 1 - lab], 1).float()))
 
-    def dstep(i, m=None):
+    def dstep(i, m=None, stamp=True):
+        # stamp=False: no global step reaches the EV apply (a captured graph
+        # would replay its capture-time step as every row's version; these
+        # EVs have steps_to_live = 0, so no version is kept either way)
         e_, md, do, eo = m or (evs, model, dopt, eopt)
-        return mz.din_train_step(md, batches[i % 4], do, eo, i, world=world, staged=staged)
+        return mz.din_train_step(md, batches[i % 4], do, eo, i if stamp else None, world=world,
+                                 staged=staged)
 
     for i in range(4 if use_graph else 2):   # graphs: every batch shape once first
         dstep(i)
@@ -715,9 +723,9 @@ def din_leg(args, dev, log, world, rank, dist, staged):
             for j in range(4):
                 gr = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gr, pool=pool):
-                    glosses.append(dstep(j))
+                    glosses.append(dstep(j, stamp=False))
                 graphs.append(gr)
-            graph_check = _din_graph_check(graphs, glosses, lambda j: dstep(j, shadow),
+            graph_check = _din_graph_check(graphs, glosses, lambda j: dstep(j, shadow, False),
                                            (evs, model), shadow[:2], dev)
             dr.status_check(dev)
             if not graph_check.startswith("equal"):

@@ -855,7 +855,17 @@ class DinMlpBuffers(object):
     """The fused DIN attention MLP's buffers (dr_din_mlp_buf) for one step:
     forward state kept for the backward, backward outputs the weight
     gradients are formed from.  cap = batch * seq_len (no host read of the
-    valid-position count: columns past it are zero in the backward)."""
+    valid-position count P).  The per-position buffers (h1t, h2t, da1t, da2t,
+    xt, dsc) hold positions [0, P) only: with the hand weight-gradient pass
+    their columns p >= P stay unwritten (uninitialised memory) and that pass
+    stops at P itself; the library GEMM path asks the backward to zero the
+    backward buffers' columns past P (zero_tail = 1).
+
+    fill (test hook, None in use): a value every per-position buffer is
+    filled with when allocated, so a test can show the hand pass never reads
+    past P (NaN there must not reach a gradient)."""
+
+    fill = None
 
     def __init__(self, B, T, H, n1, n2, dev):
         cap = B * T
@@ -863,13 +873,16 @@ class DinMlpBuffers(object):
         e = lambda shape, dt=f32: torch.empty(shape, dtype=dt, device=dev)  # noqa: E731
         self.pos, self.cnt, self.off = e(cap, i32), e(B, i32), e(B + 1, i32)
         self.w1p, self.w2t, self.cq = e((n1, 2 * H)), e((n1, n2)), e((B, n1))
-        self.h1t, self.h2t = e((n1, cap)), e((n2, cap))
+        self.h1t, self.h2t = self._filled(e((n1, cap))), self._filled(e((n2, cap)))
         self.da1t = self.da2t = self.xt = self.dsc = self.dqp = self.s1 = self.dq2 = None
         self.B, self.T, self.H, self.n1, self.n2, self.cap = B, T, H, n1, n2, cap
 
+    def _filled(self, t):
+        return t if self.fill is None else t.fill_(self.fill)
+
     def alloc_backward(self, dev):
         B, H, n1, n2, cap = self.B, self.H, self.n1, self.n2, self.cap
-        e = lambda shape: torch.empty(shape, dtype=torch.float32, device=dev)  # noqa: E731
+        e = lambda shape: self._filled(torch.empty(shape, dtype=torch.float32, device=dev))  # noqa: E731
         self.da1t, self.da2t, self.xt = e((n1, cap)), e((n2, cap)), e((2 * H, cap))
         self.dsc, self.dqp, self.s1, self.dq2 = e(cap), e((H, cap)), e((B, n1)), e((B, H))
 

@@ -253,6 +253,16 @@ class AdagradOptimizer(_Optimizer):
         var.weight[idx] = var.weight[idx] - (g * self.lr) * torch.rsqrt(a)
 
 
+def _capturing():
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
+def _not_capturing(what):
+    if _capturing():
+        raise RuntimeError("%s is not graph-safe: its per-step host scalars would be frozen "
+                           "at their capture-time values in every replay" % what)
+
+
 class AdamOptimizer(_Optimizer):
     """KvSparseApplyAdam (training_ali_ops.cc:848-975); beta powers advance
     once per apply_gradients like the optimizer's non-slot variables."""
@@ -274,13 +284,35 @@ class AdamOptimizer(_Optimizer):
     def _scalars(self):
         return (self.b1p, self.b2p, self.beta1, self.beta2, self.eps)
 
+    def prepare(self, device):
+        """Create the device beta powers for `device` now (eagerly): a graph
+        that captures the first EV apply then finds them in place."""
+        self._device_powers(torch.device(device))
+
+    def sync_host_powers(self):
+        """The device powers are the source of truth once steps replay from a
+        hipGraph (a replay advances only them): copy them back into the host
+        b1p / b2p (one device sync; not under capture)."""
+        if not self._pw:
+            return
+        _not_capturing("AdamOptimizer.sync_host_powers")
+        b1p, b2p = next(iter(self._pw.values()))[0].tolist()
+        self.b1p, self.b2p = b1p, b2p
+
     def _device_powers(self, dev):
         """The beta powers as a device float[2] (created from the host values
-        on first use -- before any graph capture), advanced in _finish by an
-        fp32 multiply on the device: the same roundings as the host values,
-        and no per-step host scalar in the EV apply (capturable)."""
+        on first use, or by prepare() -- never under a graph capture), advanced
+        in _finish by an fp32 multiply on the device: the same roundings as the
+        host values, and no per-step host scalar in the EV apply (capturable).
+        Under replays only these advance; sync_host_powers() brings the host
+        copies (used by dense tables and the DR_KV_ADAM_DEVICE_POWERS=0 A/B
+        path, neither graph-safe) up to date."""
         key = str(dev)
         if key not in self._pw:
+            if _capturing():
+                raise RuntimeError("AdamOptimizer: the device beta powers are created on the "
+                                   "first EV apply, which is under a graph capture here; run one "
+                                   "eager step or call prepare(device) before capturing")
             self._pw[key] = (torch.tensor([self.b1p, self.b2p], dtype=torch.float32, device=dev),
                              torch.tensor([self.beta1, self.beta2], dtype=torch.float32,
                                           device=dev))
@@ -291,6 +323,7 @@ class AdamOptimizer(_Optimizer):
         formed in the kernel from the HBM beta powers (A/B switch
         DR_KV_ADAM_DEVICE_POWERS=0: host powers, dr_ev_apply_grouped)."""
         if not _ADAM_DEVICE_POWERS:
+            _not_capturing("AdamOptimizer with DR_KV_ADAM_DEVICE_POWERS=0 (host beta powers)")
             return _Optimizer._apply_ev_batch(self, items, gs)
         import ctypes as C
         groups = {}
@@ -328,6 +361,7 @@ class AdamOptimizer(_Optimizer):
         decay on every row, the deduplicated gradient is scatter-added, and
         every row of var moves by lr_t * m / (sqrt(v) + eps) (TF's non-lazy
         sparse Adam), lr_t = lr * sqrt(1 - beta2^t) / (1 - beta1^t)."""
+        _not_capturing("AdamOptimizer on a dense table (lr_t from host beta powers)")
         w = var.weight
         m, v = self._dense_mv.setdefault(id(var), (torch.zeros_like(w), torch.zeros_like(w)))
         f32 = lambda x: torch.tensor(x, dtype=torch.float32)

@@ -199,10 +199,15 @@ def test_din_fused_attention_matches_fp64(B, T, H, prefix, wgrad, monkeypatch):
     264-309), prefix masks (zero-padded histories, a fully masked row) and
     arbitrary 0/1 masks.  Weight gradients every way: the hand split-K pass
     (dr_din_mlp_wgrad, the default when cap % 4 == 0) on the matrix cores or,
-    DR_DIN_WGRAD_VALU=1, the VALU, and library GEMMs (DR_DIN_WGRAD=lib)."""
+    DR_DIN_WGRAD_VALU=1, the VALU, and library GEMMs (DR_DIN_WGRAD=lib).
+    The hand passes run with every per-position buffer NaN-filled first
+    (DinMlpBuffers.fill): their columns past the valid count stay unwritten
+    and must never be read."""
     from deeprec_amd import modelzoo as mz
     from deeprec_amd import ops
     monkeypatch.setattr(ops, "_DIN_WGRAD_HAND", wgrad != "lib")
+    if wgrad != "lib":
+        monkeypatch.setattr(ops.DinMlpBuffers, "fill", float("nan"))
     monkeypatch.setenv("DR_DIN_WGRAD_VALU", "1" if wgrad == "valu" else "0")
     g = torch.Generator(device="cpu").manual_seed(B * 1000 + T + H)
     q = torch.randn(B, H, generator=g, dtype=torch.float64) * 0.5
