@@ -3531,12 +3531,21 @@ struct XgmiRowArgs {
   int64_t dim;
   int T;
   int world;
+  int64_t* mtop[DR_MAX_GROUP];   // row counters to mirror (nullptr: none)
+  int64_t* mdst[DR_MAX_GROUP];   // their pinned host mirrors
 };
 
-// Wave-cooperative first-touch copy (steady state: one byte per key).
+// Wave-cooperative first-touch copy (steady state: one byte per key); block
+// (0, 0) also mirrors the tables' row counters to the host (the resolve
+// before it has finished: the counters are final) -- no per-table copy launch.
 __global__ __launch_bounds__(256) void xgmi_init_kernel(XgmiRowArgs a,
                                                         const int64_t* __restrict__ rows,
                                                         const uint8_t* __restrict__ init) {
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < a.T && a.mdst[threadIdx.x]) {
+    const int64_t top = __hip_atomic_load(a.mtop[threadIdx.x], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.mdst[threadIdx.x], top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   const int src = blockIdx.y;
   const int64_t n = inbox_count(a.cnt, src);
   const int lane = threadIdx.x & 63;
@@ -3712,7 +3721,36 @@ int dr_xgmi_serve(const dr_xgmi_peers* peers, dr_ev* const* evs, int num_tables,
   const int64_t expect = per_src + per_src / 4 + 256;
   const unsigned gx = (unsigned)ceil_div(expect, 256);
   hipLaunchKernelGGL(xgmi_resolve_kernel, dim3(gx, W), dim3(256), 0, st, ra, w.rows, w.init, stw);
+  // counter mirrors ride on the init kernel (as resolve_grouped's)
+  EvShared* mir[DR_MAX_GROUP];
+  int nmir = 0;
+  for (int t = 0; t < num_tables; ++t) {
+    EvShared* sh = evs[t]->sh;
+    bool seen = false;
+    for (int q = 0; q < nmir; ++q) seen = seen || mir[q] == sh;
+    if (seen) continue;
+    sh->mu.lock();
+    if (want_mirror(sh, st)) {
+      wa.mtop[t] = sh->top;
+      wa.mdst[t] = sh->pinned_top;
+      mir[nmir++] = sh;
+    } else {
+      sh->mu.unlock();
+    }
+  }
   hipLaunchKernelGGL(xgmi_init_kernel, dim3(gx, W), dim3(256), 0, st, wa, w.rows, w.init);
+  {
+    const hipError_t le = hipGetLastError();
+    for (int q = 0; q < nmir; ++q) {
+      if (le == hipSuccess) mirrored(mir[q], st);
+      mir[q]->mu.unlock();
+    }
+    if (le != hipSuccess) {
+      set_error("kernel launch failed: %s", hipGetErrorString(le));
+      return DR_INTERNAL;
+    }
+  }
+  for (int t = 0; t < num_tables; ++t) wa.mtop[t] = wa.mdst[t] = nullptr;   // (emit: unused)
   const int dv = (int)(dim / 4);
   auto ge = [&](int G) { return dim3((unsigned)(ceil_div(expect, (256 / G) * 4) * W)); };
   if (dv <= 8)
@@ -3725,7 +3763,6 @@ int dr_xgmi_serve(const dr_xgmi_peers* peers, dr_ev* const* evs, int num_tables,
     hipLaunchKernelGGL((xgmi_emit_kernel<64, 4>), ge(64), dim3(256), 0, st, wa, w.rows);
   hipLaunchKernelGGL(xgmi_flush_kernel, dim3(64), dim3(64), 0, st);
   DR_LAUNCH_CHECK();
-  for (int t = 0; t < num_tables; ++t) post_call(evs[t]->sh, st);
   return DR_OK;
 }
 

@@ -448,7 +448,10 @@ class NativeShardedLookup(object):
         each table's ids.  Returns [bags, T*D] (fp32; bf16 on request for bf16
         EVs)."""
         T = self.T
+        flat = None
         if torch.is_tensor(ids):
+            if ids.dim() == 2 and ids.dtype == torch.int64 and ids.is_contiguous():
+                flat = ids.reshape(-1)   # [T, B] table-major already: no copy
             ids = [ids[t] for t in range(ids.shape[0])]
         if len(ids) != T:
             raise ValueError("ids of %d tables expected" % T)
@@ -456,7 +459,8 @@ class NativeShardedLookup(object):
         koff = [0]
         for n in lens:
             koff.append(koff[-1] + n)
-        flat = torch.cat([x.reshape(-1).to(torch.int64) for x in ids]).contiguous()
+        if flat is None:
+            flat = torch.cat([x.reshape(-1).to(torch.int64) for x in ids]).contiguous()
         if bag_offs is None:
             bags, offs = lens[0], None
         else:
