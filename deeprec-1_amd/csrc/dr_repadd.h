@@ -73,6 +73,69 @@ DR_HD inline bool rep_add_grid(float s, float x, int64_t k, float* out) {
   return true;
 }
 
+// rep_add_grid in 32-bit integer arithmetic for a short segment (1 < k <
+// 128: |k D| <= 2^30, no overflow) -- the form a serial device walk takes
+// per segment: ~25 dependent 32-bit ops instead of rep_add's 64-bit and
+// double-precision ones.  Same verdict and result as rep_add_grid.
+DR_HD inline bool rep_add_grid32(float s, float x, int32_t k, float* out) {
+  const uint32_t bs = f32_bits(s), bx = f32_bits(x);
+  const int es = (int)((bs >> 23) & 0xFF), ex = (int)((bx >> 23) & 0xFF);
+  const int sh = es - ex;
+  if (k < 2 || k > 127 || es == 0 || es == 0xFF || ex == 0 || sh < 1 || sh > 25) return false;
+  const uint32_t mx = (bx & 0x7FFFFFu) | 0x800000u;
+  const uint32_t ip = mx >> sh, fr = mx & ((1u << sh) - 1u), half = 1u << (sh - 1);
+  const bool up = fr > half || (fr == half && (ip & 1u));
+  const int32_t a = (int32_t)((bs & 0x7FFFFFu) | 0x800000u);
+  if (fr == half && (a & 1)) return false;
+  const int32_t dabs = (int32_t)ip + (up ? 1 : 0);
+  const bool grow = ((bs ^ bx) >> 31) == 0;
+  const int32_t D = grow ? dabs : -dabs;
+  int fs = fr == 0 ? 0 : (up ? -1 : 1);
+  if (!grow) fs = -fs;
+  const int32_t lo = 0x800000, hi = 0x1000000;
+  const int32_t a1 = a + D, ak = a + k * D;
+  const bool ok1 = fs < 0 ? (a1 <= hi && a1 >= lo + 1) : (a1 < hi && a1 >= lo);
+  const bool okk = fs < 0 ? (ak <= hi && ak >= lo + 1) : (ak < hi && ak >= lo);
+  if (!ok1 || !okk) return false;
+  *out = __builtin_bit_cast(float, (bs & 0xFF800000u) + (uint32_t)(ak - lo));
+  return true;
+}
+
+// k adds of x from s with the first two done by the fp32 adder itself: a1 =
+// s + x, a2 = a1 + x.  When s, a1 and a2 share sign and exponent (one grid,
+// ulp u), every later add moves the sum by the same D = bits(a2) - bits(a1)
+// ulps: the rounding of a_j + x depends only on x's fraction of an ulp --
+// and, for a tie, on the sum's parity, which the first add (made on this
+// grid) left even and an even D keeps even -- as long as the sums stay
+// strictly inside the binade: bits(a2) + (k - 2) D keeps the sign / exponent
+// and a nonzero mantissa (one ulp above the lower edge).  Otherwise the
+// remaining adds are plain.  A few integer ops after two adds instead of k
+// adds; bit-equal to the loop.  (The device walk, grad_rows.hip
+// serial_seg_walk, is this with every value wave-uniform;
+// tools/repadd_check.cpp checks it here.)
+DR_HD inline bool seg_tail_fits(uint32_t b0, uint32_t b1, uint32_t b2, int32_t k, uint32_t* bk) {
+  const int32_t D = (int32_t)(b2 - b1);
+  const uint32_t e2 = (b2 >> 23) & 0xFF;
+  const uint32_t r = b2 + (uint32_t)(k * D);
+  *bk = r;
+  return k < 128 && ((b0 ^ b2) >> 23) == 0 && ((b1 ^ b2) >> 23) == 0 && ((b2 ^ r) >> 23) == 0 &&
+         (r & 0x7FFFFFu) != 0 && e2 != 0 && e2 != 0xFF;
+}
+DR_HD inline float seg_walk2(float s, float x, int64_t k) {
+  if (k <= 0) return s;
+  const float a1 = s + x;
+  if (--k == 0) return a1;
+  const float a2 = a1 + x;
+  --k;
+  uint32_t bk;
+  if (k == 0) return a2;
+  if (seg_tail_fits(f32_bits(s), f32_bits(a1), f32_bits(a2), (int32_t)(k < 128 ? k : 128), &bk))
+    return __builtin_bit_cast(float, bk);
+  s = a2;
+  for (int64_t j = 0; j < k; ++j) s = s + x;
+  return s;
+}
+
 DR_HD inline float rep_add(float s, float x, int64_t k) {
   float r;
   if (k > 1 && rep_add_grid(s, x, k, &r)) return r;

@@ -101,7 +101,13 @@ static int serial_dma() {   // read per call (host, once per backward): tests co
 // of branchy integer work against 8.5 per position for the plain chain, so
 // it only pays for segments of ~70+ terms; DIN's average 50 (4 050 segments
 // over 203 800 padding positions) walked 4x slower (profiles/r05_seg_walk.log).
-// Read per call (DR_GRAD_SEG_SCAN=n positions; 0 = off).
+// Read per call (DR_GRAD_SEG_SCAN=n positions; 0 = off).  Round 6: the
+// segment step is two fp32 adds then the rest in closed form on the sum's
+// grid (serial_seg_walk, dr_repadd.h seg_walk2: 93-97 % of DIN's segments),
+// every value wave-uniform, one walker wave per SIMD, segments of >= 16
+// terms on average: ~450 cycles per segment measured (clock64, ~10 cycles
+// per dependent instruction of a lone wave), 0.83-1.19 ms for DIN's chain
+// against the plain walk's 1.0 -- still opt-in (profiles/r06_seg_rounds_walk.log).
 // Round 6: DR_GRAD_SEG_ROUNDS=1 (opt-in) walks the segments by a whole wave
 // in rounds (wave_rounds_walk: every segment of a window on the running
 // sum's grid at once, an integer prefix over the lanes, the segment where the
@@ -122,7 +128,7 @@ static int64_t seg_scan() {
   if (e) return (int64_t)atoll(e);
   return seg_rounds_host() ? (int64_t)4096 : (int64_t)0;
 }
-static int32_t seg_min() { return seg_rounds_host() ? 8 : 64; }
+static int32_t seg_min() { return seg_rounds_host() ? 8 : 16; }
 
 static int64_t zero_scan() {
   // read per call (host only, once per backward): tests switch it on around
@@ -1032,15 +1038,6 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
   return v + (row >= 1 ? r0 : 0) + (row >= 2 ? r1 : 0) + (row >= 3 ? r2 : 0);
 }
 
-// One column's segments [0, nv) walked by a whole wave in rounds
-// (dr_repadd.h "many segments at once"): each round, lane l takes segment
-// i + l -- its term's step on the current sum's grid, an exclusive prefix of
-// k * D over the lanes, whether its adds stay on the grid from there -- and
-// the wave moves the sum past every segment before the first lane that does
-// not fit in one step; that segment is added exactly by rep_add and the next
-// round starts on the new grid.  A zero / subnormal sum: one rep_add.
-// sp: the column's terms, qe: segment end positions (LDS), pe0: the end of
-// the segment before the first.  Bit-equal to rep_add segment by segment.
 // k adds of x to acc, exactly: the plain adds themselves for a short
 // segment (one dependent v_add_f32 each, ~8.5 cycles -- a DIN segment's ~50
 // cost less than rep_add's double-precision closed form, ~2-4 k cycles of
@@ -1051,6 +1048,64 @@ __device__ __forceinline__ float seg_add(float acc, float x, int64_t k) {
   return acc;
 }
 
+// One column's segments [0, nv) walked one at a time by a wave, every value
+// wave-uniform (readfirstlane): per segment of k terms the first two adds
+// on the fp32 adder, then the other k - 2 in closed form when the sum stays
+// on one grid (dr_repadd.h seg_walk2 / seg_tail_fits: a few scalar integer
+// ops; 93-97 % of DIN's padding segments), else plainly.  The next
+// segment's term and end are read from LDS while this one is added.
+__device__ __forceinline__ float serial_seg_walk(float acc, const float* sp, const int32_t* qe,
+                                                int nv_, int64_t pe0) {
+  const int nv = __builtin_amdgcn_readfirstlane(nv_);
+  int32_t pe = __builtin_amdgcn_readfirstlane((int32_t)pe0);
+  float a = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(acc)));
+  float xv = sp[0];
+  int32_t qv = qe[0];
+  for (int e = 0; e < nv; ++e) {
+    const float x = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(xv)));
+    const int32_t q = __builtin_amdgcn_readfirstlane(qv);
+    if (e + 1 < nv) {
+      xv = sp[e + 1];
+      qv = qe[e + 1];
+    }
+    const int32_t k = q - pe;
+    pe = q;
+    const float a1 = a + x;
+    if (k == 1) {
+      a = a1;
+      continue;
+    }
+    const float a2 = a1 + x;
+    if (k == 2) {
+      a = a2;
+      continue;
+    }
+    uint32_t bk;
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane(__float_as_uint(a));
+    const uint32_t b1 = __builtin_amdgcn_readfirstlane(__float_as_uint(a1));
+    const uint32_t b2 = __builtin_amdgcn_readfirstlane(__float_as_uint(a2));
+    if (seg_tail_fits(b0, b1, b2, k - 2, &bk)) {
+      a = __uint_as_float(bk);
+      continue;
+    }
+    a = a2;
+    if (k - 2 > kSegPlainMax)
+      a = rep_add(a, x, k - 2);
+    else
+      for (int j = 0; j < k - 2; ++j) a = a + x;
+  }
+  return a;
+}
+
+// One column's segments [0, nv) walked by a whole wave in rounds
+// (dr_repadd.h "many segments at once"): each round, lane l takes segment
+// i + l -- its term's step on the current sum's grid, an exclusive prefix of
+// k * D over the lanes, whether its adds stay on the grid from there -- and
+// the wave moves the sum past every segment before the first lane that does
+// not fit in one step; that segment is added exactly by rep_add and the next
+// round starts on the new grid.  A zero / subnormal sum: one rep_add.
+// sp: the column's terms, qe: segment end positions (LDS), pe0: the end of
+// the segment before the first.  Bit-equal to rep_add segment by segment.
 #ifdef DR_SEG_DEBUG
 __device__ unsigned long long g_dbg[4096][3];   // (measurement build) per wave: rounds, rep_add, walk cycles
 #endif
@@ -1254,14 +1309,8 @@ __global__ __launch_bounds__(NT) void rows_serial_seg_kernel(RowsGroup g, int T,
           const float* sp = stage + wcol * S;
           if (L.srounds)
             acc = wave_rounds_walk(acc, sp, qend, nv, prev, lane);
-          else {
-            int64_t pe = prev;
-            for (int e = 0; e < nv; ++e) {
-              const int32_t q = qend[e];
-              acc = rep_add(acc, sp[e], (int64_t)q - pe);
-              pe = q;
-            }
-          }
+          else
+            acc = serial_seg_walk(acc, sp, qend, nv, prev);
         }
         prev = qend[nv - 1];
         __syncthreads();   // the stage and qend are rewritten next
@@ -2004,7 +2053,7 @@ static void launch_long(const RowsGroup& g, int T, int dim, const RowsLong& L, c
       hipLaunchKernelGGL((rows_serial_plain_kernel<1, SGD, WB>), dim3((unsigned)db), dim3(1024), 0,
                          s, g, T, dim, L, sg);
   }
-  if (segs && L.srounds) {   // wave rounds: 4 columns per 256-thread block
+  if (segs) {   // 4 columns per 256-thread block: one walker wave per SIMD
     int64_t sb2 = runs * ceil_div(dim, 4);
     if (sb2 > 1024) sb2 = 1024;
     if (VEC == 4)
@@ -2016,19 +2065,6 @@ static void launch_long(const RowsGroup& g, int T, int dim, const RowsLong& L, c
     else
       hipLaunchKernelGGL((rows_serial_seg_kernel<1, SGD, WB, 4, 256>), dim3((unsigned)sb2),
                          dim3(256), 0, s, g, T, dim, L, sg);
-  } else if (segs) {
-    const int64_t nsl16 = ceil_div(dim, 16);
-    int64_t sb2 = runs * nsl16;
-    if (sb2 > 1024) sb2 = 1024;
-    if (VEC == 4)
-      hipLaunchKernelGGL((rows_serial_seg_kernel<VEC, SGD, WB, 16, 1024>), dim3((unsigned)sb2),
-                         dim3(1024), 0, s, g, T, dim, L, sg);
-    else if (aligned2 && dim % 2 == 0)
-      hipLaunchKernelGGL((rows_serial_seg_kernel<2, SGD, WB, 16, 1024>), dim3((unsigned)sb2),
-                         dim3(1024), 0, s, g, T, dim, L, sg);
-    else
-      hipLaunchKernelGGL((rows_serial_seg_kernel<1, SGD, WB, 16, 1024>), dim3((unsigned)sb2),
-                         dim3(1024), 0, s, g, T, dim, L, sg);
   }
   if (N > L.smax) {
     const int64_t big = N / (L.smax + 1) + 1;

@@ -151,7 +151,7 @@ static int file_mode(const char* path, int W) {
   float* x = (float*)malloc(sizeof(float) * n);
   if (fread(t, sizeof(float), n * D, f) != (size_t)(n * D) || fread(k, 8, n, f) != (size_t)n) return 2;
   fclose(f);
-  long bad = 0, rounds = 0, zero_runs = 0;
+  long bad = 0, rounds = 0, zero_runs = 0, w2fast = 0;
   for (int64_t c = 0; c < D; ++c) {
     for (int64_t j = 0; j < n; ++j) x[j] = t[j * D + c];
     float ref = 0.f;
@@ -160,6 +160,16 @@ static int file_mode(const char* path, int W) {
     long r = 0;
     const float got = rounds_walk(0.f, x, k, (int)n, W, &r);
     bad += dr::f32_bits(ref) != dr::f32_bits(got);
+    float w2 = 0.f;
+    for (int64_t j = 0; j < n; ++j) {
+      float b1 = w2 + x[j], b2 = b1 + x[j];
+      uint32_t bk;
+      if (k[j] > 2 && dr::seg_tail_fits(dr::f32_bits(w2), dr::f32_bits(b1), dr::f32_bits(b2),
+                                        (int32_t)(k[j] - 2), &bk))
+        ++w2fast;
+      w2 = dr::seg_walk2(w2, x[j], k[j]);
+    }
+    bad += dr::f32_bits(ref) != dr::f32_bits(w2);
     rounds += r;
     int64_t z = 0;
     while (z < n && x[z] == 0.f) ++z;
@@ -167,8 +177,9 @@ static int file_mode(const char* path, int W) {
     printf("col %2lld: rounds %5ld  leading zero segments %lld  sum %a\n", (long long)c, r,
            (long long)z, got);
   }
-  printf("file %s: segments %lld x %lld columns, rounds %ld (%.3f per segment) mismatches %ld\n",
-         path, (long long)n, (long long)D, rounds, (double)rounds / (double)(n * D), bad);
+  printf("file %s: segments %lld x %lld columns, rounds %ld (%.3f per segment), two-add closed "
+         "form %.1f%% of segments, mismatches %ld\n", path, (long long)n, (long long)D, rounds,
+         (double)rounds / (double)(n * D), 100.0 * w2fast / (double)(n * D), bad);
   return bad ? 1 : 0;
 }
 
@@ -181,7 +192,7 @@ int main(int argc, char** argv) {
   }
   const long cases = argc > 1 ? atol(argv[1]) : 200000;
   st = argc > 2 ? strtoull(argv[2], 0, 10) : 88172645463325252ull;
-  long bad = 0, jumps = 0;
+  long bad = 0, jumps = 0, g32hit = 0;
   for (long c = 0; c < cases; ++c) {
     const float s = pick_s(), x = pick_x(s);
     const int64_t k = (rnd() % 3 == 0) ? (int64_t)(rnd() % 8) : (int64_t)(rnd() % 20000);
@@ -195,8 +206,31 @@ int main(int argc, char** argv) {
         printf("MISMATCH s=%a x=%a k=%lld ref=%a got=%a\n", s, x, (long long)k, ref, got);
       ++bad;
     }
+    {   // the two-adds-then-closed-form segment step
+      const float w2 = dr::seg_walk2(s, x, k < 4096 ? k : 4096);
+      float r2 = s;
+      for (int64_t j = 0; j < (k < 4096 ? k : 4096); ++j) r2 = r2 + x;
+      if (dr::f32_bits(w2) != dr::f32_bits(r2) && !(isnan(w2) && isnan(r2))) {
+        if (bad < 20)
+          printf("WALK2 s=%a x=%a k=%lld ref=%a got=%a\n", s, x, (long long)k, r2, w2);
+        ++bad;
+      }
+    }
+    if (k > 1 && k < 128) {   // the 32-bit fast path: same verdict, same result
+      float g64 = 0.f, g32 = 0.f;
+      const bool v64 = dr::rep_add_grid(s, x, k, &g64);
+      const bool v32 = dr::rep_add_grid32(s, x, (int32_t)k, &g32);
+      if (v64 != v32 || (v32 && dr::f32_bits(g32) != rb)) {
+        if (bad < 20)
+          printf("GRID32 s=%a x=%a k=%lld v64=%d v32=%d ref=%a got=%a\n", s, x, (long long)k, v64,
+                 v32, ref, g32);
+        ++bad;
+      }
+      g32hit += v32;
+    }
     jumps += k >= 4;
   }
-  printf("cases %ld (k >= 4: %ld) mismatches %ld\n", cases, jumps, bad);
+  printf("cases %ld (k >= 4: %ld, grid32 fast path: %ld) mismatches %ld\n", cases, jumps, g32hit,
+         bad);
   return bad ? 1 : 0;
 }

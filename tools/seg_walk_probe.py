@@ -26,10 +26,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--modes", default=",".join(MODES))
+    ap.add_argument("--terms", default="din_pad_terms.npz",
+                    help="tools/data file: din_pad_terms.npz (first step) or "
+                         "din_pad_terms_s200.npz (after 200 Adam steps)")
     args = ap.parse_args()
     import deeprec_amd as dr
     dev = torch.device("cuda:0")
-    z = np.load(os.path.join(ROOT, "tools", "data", "din_pad_terms.npz"))
+    z = np.load(os.path.join(ROOT, "tools", "data", args.terms))
     terms, k = z["terms"].astype(np.float32), z["lens"].astype(np.int64)
     D = terms.shape[1]
     rng = np.random.default_rng(5)
