@@ -1901,9 +1901,20 @@ static constexpr int W4D_IMG = 32 * 512;   // one operand's K-32 stage: 32 rows 
 // a stage's ring slot is a compile-time offset on per-lane fragment
 // addresses computed once (16 VGPRs): with the slot at run time the
 // compiler held 32 live addresses and spilled.
+// XCD-region work order (grp == -2): the nt x nt tiles in Hilbert-curve
+// order cut into 8 compact regions, region x the tiles of XCD x; XCD x walks
+// slice 0's region, then slice 1's, ...  All 8 XCDs thus work on the same
+// slice at once (its operands, K / S rows of u and x_l, fit the MALL: fetched
+// from HBM about once), each on a compact block of tiles (its L2 shares the
+// block's operand columns).
+struct DwOrder {
+  int16_t tile[256];   // tile ids (row * nt + col) in region order
+  int16_t start[9];    // region x = tile[start[x] .. start[x + 1])
+};
+
 __global__ __launch_bounds__(256, 1) void crossnet_dw_w4_kernel(
     const uint16_t* __restrict__ u, const uint16_t* __restrict__ xl, int64_t K, int d, int S,
-    float* __restrict__ part, int grp) {
+    float* __restrict__ part, int grp, DwOrder ord) {
   __shared__ __attribute__((aligned(1024))) char lds[8 * W4D_IMG];  // 128 KB
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1915,7 +1926,16 @@ __global__ __launch_bounds__(256, 1) void crossnet_dw_w4_kernel(
   const int64_t item = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + orig / 8;
   const int nt = d / 256 + (d % 256 ? 1 : 0);
   int z, m0, n0;
-  if (grp > 0) {
+  if (grp == -2) {
+    const int x = (int)(orig % 8);
+    const int64_t k = orig / 8;
+    const int n = ord.start[x + 1] - ord.start[x];
+    if (k >= (int64_t)S * n) return;   // (XCDs with a smaller region: idle blocks)
+    z = (int)(k / n);
+    const int t = ord.tile[ord.start[x] + (int)(k % n)];
+    m0 = (t / nt) * 256;
+    n0 = (t % nt) * 256;
+  } else if (grp > 0) {
     // slice-major, tiles in groups of grp tile rows walked column by column:
     // the ~32 work-groups an XCD runs at once share one K slice and cover a
     // grp x (32 / grp) block of tiles, so its L2 fetches each operand block
@@ -2583,11 +2603,43 @@ int dr_crossnet_dw_bf16(const uint16_t* u, const uint16_t* xl, int64_t batch, in
   // DR_CROSSNET_DW_ORDER (read per call): the w4 work order, 0 = tile-major
   // (an XCD's concurrent work-groups are the slices of a few tiles), g > 0 =
   // slice-major in groups of g tile rows (default 4)
+  // ("xcd": the XCD-region order, DwOrder)
   const char* ord = getenv("DR_CROSSNET_DW_ORDER");
-  const int grp = ord ? atoi(ord) : 4;
+  const bool xcd = ord && strcmp(ord, "xcd") == 0;
+  const int grp = xcd ? -2 : (ord ? atoi(ord) : 4);
+  DwOrder wo;
+  memset(&wo, 0, sizeof(wo));
+  int64_t blocks = tiles * Sl;
+  if (xcd) {
+    const int nt = (int)ceil_div(d, 256);
+    DR_REQUIRE(nt <= 16, DR_INVALID_ARGUMENT, "xcd dW order: d <= 4096");
+    int n = 0;
+    for (int h = 0; h < 256; ++h) {   // Hilbert curve over a 16 x 16 grid
+      int x = 0, y = 0, t = h;
+      for (int sq = 1; sq < 16; sq *= 2) {
+        const int rx = 1 & (t / 2), ry = 1 & (t ^ rx);
+        if (ry == 0) {
+          if (rx == 1) {
+            x = sq - 1 - x;
+            y = sq - 1 - y;
+          }
+          std::swap(x, y);
+        }
+        x += sq * rx;
+        y += sq * ry;
+        t /= 4;
+      }
+      if (x < nt && y < nt) wo.tile[n++] = (int16_t)(y * nt + x);
+    }
+    int most = 0;
+    for (int r = 0; r <= 8; ++r) wo.start[r] = (int16_t)((int64_t)n * r / 8);
+    for (int r = 0; r < 8; ++r) most = std::max(most, wo.start[r + 1] - wo.start[r]);
+    blocks = 8ll * Sl * most;
+  }
   if (w4)
-    hipLaunchKernelGGL(crossnet_dw_w4_kernel, dim3((unsigned)(tiles * Sl)), dim3(256), 0,
-                       S(stream), u, xl, batch, d, Sl, part, grp < 0 ? 0 : grp);
+    hipLaunchKernelGGL(crossnet_dw_w4_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                       S(stream), u, xl, batch, d, Sl, part, grp == -2 ? -2 : (grp < 0 ? 0 : grp),
+                       wo);
   else
     hipLaunchKernelGGL(crossnet_dw_kernel, dim3((unsigned)(tiles * Sl)), dim3(512), 0, S(stream),
                        u, xl, batch, d, Sl, part);

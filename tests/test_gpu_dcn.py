@@ -110,7 +110,8 @@ def test_crossnet_dx_matches_torch(B, d):
         assert torch.equal(ops.crossnet_dx(u, W.t().contiguous(), g), dx)
 
 
-@pytest.mark.parametrize("kernel,order", [("w4", "4"), ("w4", "0"), ("w4", "14"), ("8ph", "4")])
+@pytest.mark.parametrize("kernel,order", [("w4", "4"), ("w4", "0"), ("w4", "14"), ("w4", "xcd"),
+                                          ("8ph", "4")])
 @pytest.mark.parametrize("B,d", [(1024, 192), (4096, 3392), (64, 64), (2048, 448),
                                  (65536, 3392)])
 def test_crossnet_dw_matches_fp64(B, d, kernel, order, monkeypatch):

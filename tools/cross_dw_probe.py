@@ -49,7 +49,7 @@ def main():
           % (dr._lib.lib().dr_crossnet_dw_workspace_size(B, d) // (4 * d * d), t, flop / t / 1e9,
              err), flush=True)
     if os.environ.get("DR_CROSSNET_DW_KERNEL", "w4") == "w4":   # work orders (read per call)
-        for o in ("0", "2", "4", "8", "14"):
+        for o in ("0", "2", "4", "8", "14", "xcd"):
             os.environ["DR_CROSSNET_DW_ORDER"] = o
             got = ops.crossnet_dw(u, x)
             err = ((got - ref).abs().max() / ref.abs().max()).item()
