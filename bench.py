@@ -671,7 +671,11 @@ def din_leg(args, dev, log, world, rank, dist, staged):
             evs.append(ev)
         torch.manual_seed(0)
         model = mz.DIN(*evs).to(dev)
-        dopt = torch.optim.Adam(model.parameters(), lr=0.001, capturable=use_graph)
+        # the dense Adam as torch's fused kernel (one launch per step instead
+        # of ~15 multi-tensor launches; DR_BENCH_DENSE_ADAM=foreach: A/B)
+        fused = os.environ.get("DR_BENCH_DENSE_ADAM", "fused") == "fused"
+        dopt = torch.optim.Adam(model.parameters(), lr=0.001, capturable=use_graph,
+                                fused=fused or None)
         return evs, model, dopt, dr.AdamOptimizer(0.001)
     evs, model, dopt, eopt = make("b")
     shadow = make("s") if use_graph else None

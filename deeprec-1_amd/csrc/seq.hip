@@ -924,6 +924,117 @@ __global__ __launch_bounds__(256, 3) void din_wgrad_mfma_kernel(
 
 static constexpr int kWgradBlocks = 1024;
 
+// ---- Dice (modelzoo/DIN/script/utils.py:12-35, batch statistics) ----------
+// One block per 16 columns, 64 row groups of 16 lanes (1024 threads, the
+// row loops unrolled 8 deep: the loads of a pass are in flight together --
+// a column's few thousand rows would otherwise be one dependent load chain
+// per thread): the column sums in a fixed order (per-thread partials over
+// rows rg, rg + 64, ..., then the 64 groups in order), so a column's
+// statistics do not depend on timing.
+static constexpr int kDiceCols = 16, kDiceRg = 64;
+
+__device__ __forceinline__ float dice_col_sum(float v, float (*red)[kDiceCols], int rg, int cl) {
+  red[rg][cl] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int r = 0; r < kDiceRg; ++r) t += red[r][cl];
+  __syncthreads();
+  return t;
+}
+
+// y = alpha (1 - p) x + p x, p = sigmoid((x - mean) / (std + eps)), mean and
+// std = sqrt(mean((x - mean)^2 + eps)) over the batch; stats [2, n] = mean,
+// std for the backward.
+__global__ __launch_bounds__(1024) void dice_fwd_kernel(const float* __restrict__ x,
+                                                       const float* __restrict__ alpha, int64_t B,
+                                                       int n, float eps, float* __restrict__ y,
+                                                       float* __restrict__ stats) {
+  __shared__ float red[kDiceRg][kDiceCols];
+  const int cl = threadIdx.x % kDiceCols, rg = threadIdx.x / kDiceCols;
+  const int col = blockIdx.x * kDiceCols + cl;
+  const bool ok = col < n;
+  const float inv = 1.f / (float)B;
+  float s = 0.f;
+  if (ok)
+#pragma unroll 8
+    for (int i = rg; i < (int)B; i += kDiceRg) s += x[(int64_t)i * n + col];
+  const float mean = dice_col_sum(s, red, rg, cl) * inv;
+  float v = 0.f;
+  if (ok)
+#pragma unroll 8
+    for (int i = rg; i < (int)B; i += kDiceRg) {
+      const float c = x[(int64_t)i * n + col] - mean;
+      v += c * c + eps;
+    }
+  const float sd = sqrtf(dice_col_sum(v, red, rg, cl) * inv);
+  if (!ok) return;
+  const float a = alpha[col], den = sd + eps;
+#pragma unroll 8
+  for (int i = rg; i < (int)B; i += kDiceRg) {
+    const float xv = x[(int64_t)i * n + col];
+    const float p = 1.f / (1.f + expf(-((xv - mean) / den)));
+    y[(int64_t)i * n + col] = a * (1.f - p) * xv + p * xv;
+  }
+  if (rg == 0) {
+    stats[col] = mean;
+    stats[n + col] = sd;
+  }
+}
+
+// Its backward: with c = x - mean, s = std + eps, p = sigmoid(c / s),
+// gz = gy (1 - alpha) x p (1 - p), g_std = -sum(gz c) / s^2, g_var =
+// g_std / (2 std), gc = gz / s + g_var 2 c / B:  gx = gy (alpha + (1 - alpha)
+// p) + gc - mean(gc);  g_alpha = sum gy (1 - p) x.
+__global__ __launch_bounds__(1024) void dice_bwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ gy, const float* __restrict__ alpha,
+    const float* __restrict__ stats, int64_t B, int n, float eps, float* __restrict__ gx,
+    float* __restrict__ galpha) {
+  __shared__ float red[kDiceRg][kDiceCols];
+  const int cl = threadIdx.x % kDiceCols, rg = threadIdx.x / kDiceCols;
+  const int col = blockIdx.x * kDiceCols + cl;
+  const bool ok = col < n;
+  const float inv = 1.f / (float)B;
+  const float mean = ok ? stats[col] : 0.f, sd = ok ? stats[n + col] : 1.f;
+  const float a = ok ? alpha[col] : 0.f, den = sd + eps;
+  float sgc = 0.f, sga = 0.f;
+  if (ok)
+#pragma unroll 8
+    for (int i = rg; i < (int)B; i += kDiceRg) {
+      const float xv = x[(int64_t)i * n + col], g = gy[(int64_t)i * n + col];
+      const float c = xv - mean;
+      const float p = 1.f / (1.f + expf(-(c / den)));
+      const float gz = g * (1.f - a) * xv * (p * (1.f - p));
+      sgc += gz * c;
+      sga += g * (1.f - p) * xv;
+    }
+  const float gs = -dice_col_sum(sgc, red, rg, cl) / (den * den);
+  const float ga = dice_col_sum(sga, red, rg, cl);
+  const float gv2 = gs / (2.f * sd) * 2.f * inv;   // g_var * 2 / B
+  float sc = 0.f;
+  if (ok)
+#pragma unroll 8
+    for (int i = rg; i < (int)B; i += kDiceRg) {
+      const float xv = x[(int64_t)i * n + col], g = gy[(int64_t)i * n + col];
+      const float c = xv - mean;
+      const float p = 1.f / (1.f + expf(-(c / den)));
+      const float gz = g * (1.f - a) * xv * (p * (1.f - p));
+      sc += gz / den + gv2 * c;
+    }
+  const float mgc = dice_col_sum(sc, red, rg, cl) * inv;
+  if (!ok) return;
+#pragma unroll 8
+  for (int i = rg; i < (int)B; i += kDiceRg) {
+    const float xv = x[(int64_t)i * n + col], g = gy[(int64_t)i * n + col];
+    const float c = xv - mean;
+    const float p = 1.f / (1.f + expf(-(c / den)));
+    const float gz = g * (1.f - a) * xv * (p * (1.f - p));
+    // (the centring first: gc and its mean can be far larger than the
+    // direct term when std is tiny, e.g. a batch of one)
+    gx[(int64_t)i * n + col] = g * (a + (1.f - a) * p) + ((gz / den + gv2 * c) - mgc);
+  }
+  if (rg == 0) galpha[col] = ga;
+}
+
 }  // namespace dr
 
 extern "C" {
@@ -1174,6 +1285,34 @@ int dr_din_mlp_backward_tail(const float* query, const float* facts, int64_t bat
   }
   DR_DIN_MLP_SHAPES(DR_BWD)
 #undef DR_BWD
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_din_dice_forward(const float* x, const float* alpha, int64_t batch, int n, float epsilon,
+                        float* y, float* stats, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 1 && n >= 0, DR_INVALID_ARGUMENT, "bad shape (batch >= 1)");
+  if (n == 0) return DR_OK;
+  DR_REQUIRE(x && alpha && y && stats, DR_INVALID_ARGUMENT, "null operand");
+  DR_REQUIRE(batch < (1ll << 31), DR_INVALID_ARGUMENT, "batch must be < 2^31");
+  hipLaunchKernelGGL(dice_fwd_kernel, dim3((unsigned)ceil_div(n, kDiceCols)), dim3(1024), 0,
+                     S(stream), x, alpha, batch, n, epsilon, y, stats);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_din_dice_backward(const float* x, const float* grad_y, const float* alpha,
+                         const float* stats, int64_t batch, int n, float epsilon, float* grad_x,
+                         float* grad_alpha, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 1 && n >= 0, DR_INVALID_ARGUMENT, "bad shape (batch >= 1)");
+  if (n == 0) return DR_OK;
+  DR_REQUIRE(x && grad_y && alpha && stats && grad_x && grad_alpha, DR_INVALID_ARGUMENT,
+             "null operand");
+  DR_REQUIRE(batch < (1ll << 31), DR_INVALID_ARGUMENT, "batch must be < 2^31");
+  hipLaunchKernelGGL(dice_bwd_kernel, dim3((unsigned)ceil_div(n, kDiceCols)), dim3(1024), 0,
+                     S(stream), x, grad_y, alpha, stats, batch, n, epsilon, grad_x, grad_alpha);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

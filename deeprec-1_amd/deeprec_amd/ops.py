@@ -983,6 +983,33 @@ def din_mlp_backward(query, facts, w1, w3, buf, grad_scores, grad_facts):
     return gq, dW1, db1, dW2, db2, dw3, db3
 
 
+def din_dice_forward(x, alpha, epsilon):
+    """Dice (utils.py:12-35) over a [B, n] fp32 batch in one kernel
+    (dr_din_dice_forward) -> (y [B, n], stats [2, n] = column mean, std)."""
+    dev = _dev(x)
+    B, n = x.shape
+    xc, a = _c(x, torch.float32), _c(alpha, torch.float32)
+    y = torch.empty((B, n), dtype=torch.float32, device=dev)
+    st = torch.empty((2, n), dtype=torch.float32, device=dev)
+    check(lib().dr_din_dice_forward(ptr(xc), ptr(a), B, n, float(epsilon), ptr(y), ptr(st),
+                                    stream_handle(dev)))
+    _post(dev)
+    return y, st
+
+
+def din_dice_backward(x, grad_y, alpha, stats, epsilon):
+    """-> (grad_x [B, n], grad_alpha [n]) through the batch statistics."""
+    dev = _dev(x)
+    B, n = x.shape
+    xc, g, a = _c(x, torch.float32), _c(grad_y, torch.float32), _c(alpha, torch.float32)
+    gx = torch.empty((B, n), dtype=torch.float32, device=dev)
+    ga = torch.empty(n, dtype=torch.float32, device=dev)
+    check(lib().dr_din_dice_backward(ptr(xc), ptr(g), ptr(a), ptr(_c(stats, torch.float32)), B, n,
+                                     float(epsilon), ptr(gx), ptr(ga), stream_handle(dev)))
+    _post(dev)
+    return gx, ga
+
+
 def din_attention_pool(scores, mask, facts, with_sum=True):
     """Masked softmax over the history + weighted sum (din_attention, mode
     'SUM', utils.py:286-303) and the history sum (model.py:98) in one pass.

@@ -1225,6 +1225,20 @@ int dr_din_mlp_backward_tail(const float* query, const float* facts, int64_t bat
                              const float* grad_scores, float* grad_facts,
                              const dr_din_mlp_buf* buf, int zero_tail, void* stream);
 
+/* DIN's Dice activation (modelzoo/DIN/script/utils.py:12-35, the batch      */
+/* statistics form Model_DIN's fcn uses, model.py:130-134), fp32 x [batch, n] */
+/* row-major: mean and std = sqrt(mean((x - mean)^2 + eps)) per column over   */
+/* the batch, p = sigmoid((x - mean) / (std + eps)), y = alpha (1 - p) x +   */
+/* p x.  stats [2, n] (mean, std) is written for the backward.  Column sums   */
+/* in a fixed order (deterministic).                                          */
+int dr_din_dice_forward(const float* x, const float* alpha, int64_t batch, int n, float epsilon,
+                        float* y, float* stats, void* stream);
+/* Its backward through the batch statistics: grad_x [batch, n], grad_alpha  */
+/* [n] (written).                                                             */
+int dr_din_dice_backward(const float* x, const float* grad_y, const float* alpha,
+                         const float* stats, int64_t batch, int n, float epsilon, float* grad_x,
+                         float* grad_alpha, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* String -> id, the step before the lookup.  Strings are one byte buffer    */
 /* plus int64 offsets[n+1] (string i = bytes[offsets[i] .. offsets[i+1])).   */

@@ -249,3 +249,37 @@ def test_din_fused_attention_matches_fp64(B, T, H, prefix, wgrad, monkeypatch):
         scale = float(b.grad.abs().max()) + 1e-12
         err = float((a.grad.double() - b.grad).abs().max())
         assert err <= 2e-5 * scale + 1e-6, (name, err, scale)
+
+
+@pytest.mark.parametrize("B,n", [(4096, 200), (4096, 80), (37, 19), (1, 5), (300, 1)])
+def test_din_dice_fused_matches_fp64(B, n):
+    """dr_din_dice_forward / _backward (one kernel each way) against torch
+    fp64 autograd of dice() (modelzoo/DIN/script/utils.py:12-35: batch mean,
+    std = sqrt(mean((x - mean)^2 + eps)), p = sigmoid((x - mean) / (std +
+    eps)), alpha (1 - p) x + p x): output, grad_x and grad_alpha within fp32
+    accumulation error; bit-identical across launches."""
+    from deeprec_amd import modelzoo as mz
+    g = torch.Generator(device="cpu").manual_seed(B * 7 + n)
+    x = (torch.randn(B, n, generator=g, dtype=torch.float64) * 2.0 + 0.5)
+    alpha = torch.randn(n, generator=g, dtype=torch.float64) * 0.3
+    gy = torch.randn(B, n, generator=g, dtype=torch.float64)
+    eps = 1e-9
+    rx, ra = x.clone().requires_grad_(True), alpha.clone().requires_grad_(True)
+    mean = rx.mean(0, keepdim=True)
+    std = torch.sqrt(((rx - mean) ** 2 + eps).mean(0, keepdim=True))
+    p = torch.sigmoid((rx - mean) / (std + eps))
+    ry = ra * (1.0 - p) * rx + p * rx
+    (ry * gy).sum().backward()
+    dice = mz.Dice(n, epsilon=eps).to(DEV)
+    with torch.no_grad():
+        dice.alpha.copy_(alpha.float())
+    gx_in = x.float().to(DEV).requires_grad_(True)
+    y = dice(gx_in)
+    y.backward(gy.float().to(DEV))
+    torch.testing.assert_close(y.double().cpu(), ry.detach(), rtol=1e-5, atol=1e-5)
+    scale = float(rx.grad.abs().max()) + 1e-12
+    assert float((gx_in.grad.double().cpu() - rx.grad).abs().max()) <= 1e-4 * scale + 1e-6
+    scale = float(ra.grad.abs().max()) + 1e-12
+    assert float((dice.alpha.grad.double().cpu() - ra.grad).abs().max()) <= 1e-4 * scale + 1e-5
+    y2 = dice(gx_in.detach())
+    assert torch.equal(y2, y.detach())
