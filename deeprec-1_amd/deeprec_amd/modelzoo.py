@@ -565,6 +565,47 @@ class DinAttentionFused(torch.autograd.Function):
         return gq, gf, None, dW1, db1, dW2, db2, dw3, db3
 
 
+class DinAttentionFusedAll(torch.autograd.Function):
+    """DinAttentionFused over the merged item lookup's output allv [B + B T,
+    H] (target rows, then the history rows): returns (item_eb, att, his_sum)
+    and, in the backward, writes the gradient of allv in one buffer -- the
+    history rows by the pool / MLP backward kernels in place, the target rows
+    as the attention's query gradient plus item_eb's downstream gradient --
+    instead of autograd's zero fill + slice copies + add for two views of
+    allv."""
+
+    @staticmethod
+    def forward(ctx, allv, mask, w1, b1, w2, b2, w3, b3):
+        B, T = mask.shape
+        query = allv[:B]
+        facts = allv[B:].view(B, T, -1)
+        scores, buf = ops.din_mlp_forward(query, facts, mask, w1, b1, w2, b2, w3, b3)
+        att, his_sum, alphas = ops.din_attention_pool(scores, mask, facts)
+        ctx.save_for_backward(allv, mask, w1, w3, alphas)
+        ctx.buf = buf
+        return query.clone(), att, his_sum
+
+    @staticmethod
+    def backward(ctx, g_item, g_att, g_sum):
+        allv, mask, w1, w3, alphas = ctx.saved_tensors
+        B, T = mask.shape
+        query = allv[:B]
+        facts = allv[B:].view(B, T, -1)
+        if g_att is None:
+            g_att = torch.zeros(B, facts.shape[2], device=facts.device)
+        g_all = torch.empty_like(allv)
+        gf = g_all[B:].view(B, T, -1)
+        gs, _ = ops.din_attention_pool_grad(alphas, mask, facts, g_att, g_sum, out=gf)
+        gq, dW1, db1, dW2, db2, dw3, db3 = ops.din_mlp_backward(query, facts, w1, w3, ctx.buf,
+                                                                 gs, gf)
+        ctx.buf = None
+        if g_item is None:
+            g_all[:B].copy_(gq)
+        else:
+            torch.add(gq, g_item, out=g_all[:B])
+        return g_all, None, dW1, db1, dW2, db2, dw3, db3
+
+
 class WDL(torch.nn.Module):
     """modelzoo/WDL/train.py WDL (BASELINE configs[0]) on EVs.
 
@@ -1023,9 +1064,14 @@ class DIN(torch.nn.Module):
     # different rounding, and a unique + sort + segment-sum pass per step)
     one_item_lookup = os.environ.get("DR_DIN_ONE_ITEM_LOOKUP", "1") != "0"
 
+    # with the merged lookup, the attention takes allv whole and forms its
+    # gradient in one buffer (DinAttentionFusedAll; A/B DR_DIN_FUSED_ALLV=0)
+    fused_allv = os.environ.get("DR_DIN_FUSED_ALLV", "1") != "0"
+
     def forward(self, uids, mids, cats, mid_his, cat_his, mask):
         B, T = mid_his.shape
         uid_e = self.uid_lookup(uids.reshape(1, B))
+        allv = None
         if self.one_item_lookup:
             ids = torch.stack([torch.cat([mids, mid_his.reshape(-1)]),
                                torch.cat([cats, cat_his.reshape(-1)])])
@@ -1036,7 +1082,12 @@ class DIN(torch.nn.Module):
             item_eb = self.item_lookup(torch.stack([mids, cats]))                 # [B, 2D]
             his = torch.stack([mid_his.reshape(-1), cat_his.reshape(-1)])
             facts = self.item_lookup(his).view(B, T, -1)                           # [B, T, 2D]
-        if self.fused_attention and facts.shape[2] in ops.DIN_MLP_HIDDEN:
+        if (self.fused_attention and facts.shape[2] in ops.DIN_MLP_HIDDEN and allv is not None
+                and self.fused_allv and allv.is_contiguous()):
+            item_eb, att, his_sum = DinAttentionFusedAll.apply(
+                allv, mask, self.f1_att.weight, self.f1_att.bias, self.f2_att.weight,
+                self.f2_att.bias, self.f3_att.weight, self.f3_att.bias)
+        elif self.fused_attention and facts.shape[2] in ops.DIN_MLP_HIDDEN:
             att, his_sum = DinAttentionFused.apply(
                 item_eb, facts, mask, self.f1_att.weight, self.f1_att.bias, self.f2_att.weight,
                 self.f2_att.bias, self.f3_att.weight, self.f3_att.bias)

@@ -1027,15 +1027,22 @@ def din_attention_pool(scores, mask, facts, with_sum=True):
     return att, hs, al
 
 
-def din_attention_pool_grad(alphas, mask, facts, grad_att, grad_sum=None):
-    """-> (grad_scores [B, T], grad_facts [B, T, H])."""
+def din_attention_pool_grad(alphas, mask, facts, grad_att, grad_sum=None, out=None):
+    """-> (grad_scores [B, T], grad_facts [B, T, H]); out: a contiguous fp32
+    [B, T, H] buffer to write grad_facts into (e.g. a slice of the lookup's
+    gradient)."""
     dev = _dev(facts)
     B, T, H = facts.shape
     a, m, f = _c(alphas, torch.float32), _c(mask, torch.float32), _c(facts, torch.float32)
     ga = _c(grad_att, torch.float32)
     gs = None if grad_sum is None else _c(grad_sum, torch.float32)
     gsc = torch.empty((B, T), dtype=torch.float32, device=dev)
-    gf = torch.empty((B, T, H), dtype=torch.float32, device=dev)
+    if out is not None:
+        if out.shape != (B, T, H) or out.dtype != torch.float32 or not out.is_contiguous():
+            raise ValueError("out must be a contiguous fp32 [B, T, H] tensor")
+        gf = out
+    else:
+        gf = torch.empty((B, T, H), dtype=torch.float32, device=dev)
     check(lib().dr_din_attention_pool_grad(ptr(a), ptr(m), ptr(f), ptr(ga), ptr(gs), B, T, H,
                                            ptr(gsc), ptr(gf), stream_handle(dev)))
     _post(dev)
