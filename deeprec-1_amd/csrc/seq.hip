@@ -1035,6 +1035,91 @@ __global__ __launch_bounds__(1024) void dice_bwd_kernel(
   if (rg == 0) galpha[col] = ga;
 }
 
+
+// ---- the fcn input of Model_DIN (model.py:118-124) -----------------------
+// inp = [uid, item, his_sum, item * his_sum, att] ([B, Du + 4H]), then the
+// inference-form batch_normalization bn = (inp * c) * gamma + beta (c =
+// 1 / sqrt(1 + 1e-3)): one elementwise pass instead of a concat and three
+// broadcast ops.
+__device__ __forceinline__ float fcn_in(const float* uid, const float* item, const float* hs,
+                                        const float* att, int64_t b, int j, int Du, int H) {
+  if (j < Du) return uid[b * Du + j];
+  const int k = j - Du, piece = k / H, h = k - piece * H;
+  const int64_t o = b * H + h;
+  switch (piece) {
+    case 0: return item[o];
+    case 1: return hs[o];
+    case 2: return item[o] * hs[o];
+    default: return att[o];
+  }
+}
+
+__global__ __launch_bounds__(256) void fcn_input_fwd_kernel(
+    const float* __restrict__ uid, const float* __restrict__ item, const float* __restrict__ hs,
+    const float* __restrict__ att, const float* __restrict__ gamma, const float* __restrict__ beta,
+    int64_t B, int Du, int H, float c, float* __restrict__ out) {
+  const int n = Du + 4 * H;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * n) return;
+  const int64_t b = e / n;
+  const int j = (int)(e - b * n);
+  const float v = fcn_in(uid, item, hs, att, b, j, Du, H);
+  out[e] = (v * c) * gamma[j] + beta[j];
+}
+
+// Its backward, per (sample, column of a piece): gi = (g gamma) c for each
+// inp column; g_uid = gi_uid, g_item = gi_item + gi_prod his_sum, g_his_sum
+// = gi_hs + gi_prod item, g_att = gi_att.
+__global__ __launch_bounds__(256) void fcn_input_bwd_kernel(
+    const float* __restrict__ g, const float* __restrict__ item, const float* __restrict__ hs,
+    const float* __restrict__ gamma, int64_t B, int Du, int H, float c, float* __restrict__ g_uid,
+    float* __restrict__ g_item, float* __restrict__ g_hs, float* __restrict__ g_att) {
+  const int n = Du + 4 * H, w = Du + H;   // per sample: Du uid columns, H (item, hs, prod, att)
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * w) return;
+  const int64_t b = e / w;
+  const int j = (int)(e - b * w);
+  const float* gr = g + b * n;
+  if (j < Du) {
+    g_uid[b * Du + j] = (gr[j] * gamma[j]) * c;
+    return;
+  }
+  const int h = j - Du;
+  const int ji = Du + h, jh = Du + H + h, jp = Du + 2 * H + h, ja = Du + 3 * H + h;
+  const float gi = (gr[ji] * gamma[ji]) * c, gh = (gr[jh] * gamma[jh]) * c;
+  const float gp = (gr[jp] * gamma[jp]) * c, ga = (gr[ja] * gamma[ja]) * c;
+  const int64_t o = b * H + h;
+  g_item[o] = gi + gp * hs[o];
+  g_hs[o] = gh + gp * item[o];
+  g_att[o] = ga;
+}
+
+// g_gamma[j] = sum_b g (inp c), g_beta[j] = sum_b g: one block per 16
+// columns, fixed-order sums (dice_col_sum).
+__global__ __launch_bounds__(1024) void fcn_input_param_grad_kernel(
+    const float* __restrict__ g, const float* __restrict__ uid, const float* __restrict__ item,
+    const float* __restrict__ hs, const float* __restrict__ att, int64_t B, int Du, int H, float c,
+    float* __restrict__ g_gamma, float* __restrict__ g_beta) {
+  __shared__ float red[kDiceRg][kDiceCols];
+  const int n = Du + 4 * H;
+  const int cl = threadIdx.x % kDiceCols, rg = threadIdx.x / kDiceCols;
+  const int col = blockIdx.x * kDiceCols + cl;
+  const bool ok = col < n;
+  float sg = 0.f, sb = 0.f;
+  if (ok)
+#pragma unroll 8
+    for (int i = rg; i < (int)B; i += kDiceRg) {
+      const float gv = g[(int64_t)i * n + col];
+      sg += gv * (fcn_in(uid, item, hs, att, i, col, Du, H) * c);
+      sb += gv;
+    }
+  const float tg = dice_col_sum(sg, red, rg, cl);
+  const float tb = dice_col_sum(sb, red, rg, cl);
+  if (ok && rg == 0) {
+    g_gamma[col] = tg;
+    g_beta[col] = tb;
+  }
+}
 }  // namespace dr
 
 extern "C" {
@@ -1313,6 +1398,50 @@ int dr_din_dice_backward(const float* x, const float* grad_y, const float* alpha
   DR_REQUIRE(batch < (1ll << 31), DR_INVALID_ARGUMENT, "batch must be < 2^31");
   hipLaunchKernelGGL(dice_bwd_kernel, dim3((unsigned)ceil_div(n, kDiceCols)), dim3(1024), 0,
                      S(stream), x, grad_y, alpha, stats, batch, n, epsilon, grad_x, grad_alpha);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_din_fcn_input_forward(const float* uid, const float* item, const float* his_sum,
+                             const float* att, const float* gamma, const float* beta,
+                             int64_t batch, int uid_dim, int hidden, float scale, float* out,
+                             void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && uid_dim >= 0 && hidden > 0, DR_INVALID_ARGUMENT, "bad shape");
+  const int64_t total = batch * (uid_dim + 4 * (int64_t)hidden);
+  if (total == 0) return DR_OK;
+  DR_REQUIRE(item && his_sum && att && gamma && beta && out && (uid || !uid_dim),
+             DR_INVALID_ARGUMENT, "null operand");
+  hipLaunchKernelGGL(fcn_input_fwd_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0,
+                     S(stream), uid, item, his_sum, att, gamma, beta, batch, uid_dim, hidden, scale,
+                     out);
+  DR_LAUNCH_CHECK();
+  return DR_OK;
+}
+
+int dr_din_fcn_input_backward(const float* grad, const float* uid, const float* item,
+                              const float* his_sum, const float* att, const float* gamma,
+                              int64_t batch, int uid_dim, int hidden, float scale, float* g_uid,
+                              float* g_item, float* g_his_sum, float* g_att, float* g_gamma,
+                              float* g_beta, void* stream) {
+  using namespace dr;
+  DR_REQUIRE(batch >= 0 && uid_dim >= 0 && hidden > 0, DR_INVALID_ARGUMENT, "bad shape");
+  DR_REQUIRE(batch < (1ll << 31), DR_INVALID_ARGUMENT, "batch must be < 2^31");
+  const int n = uid_dim + 4 * hidden;
+  DR_REQUIRE(grad && item && his_sum && att && gamma && g_item && g_his_sum && g_att && g_gamma &&
+                 g_beta && (!uid_dim || (uid && g_uid)),
+             DR_INVALID_ARGUMENT, "null operand");
+  if (batch == 0) {
+    int rc = fill_bytes(g_gamma, 0, (size_t)n * 4, S(stream));
+    return rc ? rc : fill_bytes(g_beta, 0, (size_t)n * 4, S(stream));
+  }
+  const int64_t rows = batch * (uid_dim + (int64_t)hidden);
+  hipLaunchKernelGGL(fcn_input_bwd_kernel, dim3((unsigned)ceil_div(rows, 256)), dim3(256), 0,
+                     S(stream), grad, item, his_sum, gamma, batch, uid_dim, hidden, scale, g_uid,
+                     g_item, g_his_sum, g_att);
+  hipLaunchKernelGGL(fcn_input_param_grad_kernel, dim3((unsigned)ceil_div(n, kDiceCols)),
+                     dim3(1024), 0, S(stream), grad, uid, item, his_sum, att, batch, uid_dim,
+                     hidden, scale, g_gamma, g_beta);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

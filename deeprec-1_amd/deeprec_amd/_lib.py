@@ -329,6 +329,9 @@ SIGNATURES = {
     "dr_din_attention_input_grad": (_I32, [_P, _P, _P, _I64, _I64, _I32, _P, _P, _I32, _P]),
     "dr_din_attention_pool": (_I32, [_P, _P, _P, _I64, _I64, _I32, _P, _P, _P, _P]),
     "dr_din_dice_forward": (_I32, [_P, _P, _I64, _I32, _F32, _P, _P, _P]),
+    "dr_din_fcn_input_forward": (_I32, [_P, _P, _P, _P, _P, _P, _I64, _I32, _I32, _F32, _P, _P]),
+    "dr_din_fcn_input_backward": (_I32, [_P, _P, _P, _P, _P, _P, _I64, _I32, _I32, _F32, _P, _P,
+                                         _P, _P, _P, _P, _P]),
     "dr_din_dice_backward": (_I32, [_P, _P, _P, _P, _I64, _I32, _F32, _P, _P, _P]),
     "dr_din_attention_pool_grad": (_I32, [_P, _P, _P, _P, _P, _I64, _I64, _I32, _P, _P, _P]),
     "dr_crossnet_dw_workspace_size": (_SZ, [_I64, _I32]),

@@ -997,6 +997,25 @@ class _DiceFn(torch.autograd.Function):
         return gx, ga, None
 
 
+class _DinFcnInputFn(torch.autograd.Function):
+    """inp = [uid, item, his_sum, item * his_sum, att] and the inference
+    batch_normalization (model.py:118-124) as one kernel each way
+    (dr_din_fcn_input_forward / _backward)."""
+
+    @staticmethod
+    def forward(ctx, uid, item, his_sum, att, gamma, beta, scale):
+        ctx.save_for_backward(uid, item, his_sum, att, gamma)
+        ctx.scale = scale
+        return ops.din_fcn_input_forward(uid, item, his_sum, att, gamma, beta, scale)
+
+    @staticmethod
+    def backward(ctx, g):
+        uid, item, his_sum, att, gamma = ctx.saved_tensors
+        gu, gi, gh, ga, gg, gb = ops.din_fcn_input_backward(g, uid, item, his_sum, att, gamma,
+                                                            ctx.scale)
+        return gu, gi, gh, ga, gg, gb, None
+
+
 class Dice(torch.nn.Module):
     """dice() of modelzoo/DIN/script/utils.py:12-35 (batch statistics).  On
     the GPU one fused kernel each way (_DiceFn; DR_DIN_DICE_FUSED=0: the
@@ -1068,6 +1087,10 @@ class DIN(torch.nn.Module):
     # gradient in one buffer (DinAttentionFusedAll; A/B DR_DIN_FUSED_ALLV=0)
     fused_allv = os.environ.get("DR_DIN_FUSED_ALLV", "1") != "0"
 
+    # the fcn input (concat + inference batch_normalization) as one kernel
+    # each way (_DinFcnInputFn; A/B DR_DIN_FUSED_FCN_INPUT=0)
+    fused_fcn_input = os.environ.get("DR_DIN_FUSED_FCN_INPUT", "1") != "0"
+
     def forward(self, uids, mids, cats, mid_his, cat_his, mask):
         B, T = mid_his.shape
         uid_e = self.uid_lookup(uids.reshape(1, B))
@@ -1097,8 +1120,13 @@ class DIN(torch.nn.Module):
             h = torch.sigmoid(self.f2_att(h))
             scores = self.f3_att(h).view(B, T)
             att, his_sum = DinAttentionPool.apply(scores, mask, facts)
-        inp = torch.cat([uid_e, item_eb, his_sum, item_eb * his_sum, att], -1)
-        bn = inp * (1.0 / (1.0 + 1e-3) ** 0.5) * self.bn1_gamma + self.bn1_beta
+        bn_scale = 1.0 / (1.0 + 1e-3) ** 0.5   # moving variance 1, epsilon 1e-3
+        if self.fused_fcn_input and item_eb.is_cuda and item_eb.dtype == torch.float32:
+            bn = _DinFcnInputFn.apply(uid_e, item_eb, his_sum, att, self.bn1_gamma,
+                                      self.bn1_beta, bn_scale)
+        else:
+            inp = torch.cat([uid_e, item_eb, his_sum, item_eb * his_sum, att], -1)
+            bn = inp * bn_scale * self.bn1_gamma + self.bn1_beta
         x = self.dice_1(self.dnn1(bn))
         x = self.dice_2(self.dnn2(x))
         return torch.softmax(self.dnn3(x), -1) + 1e-8

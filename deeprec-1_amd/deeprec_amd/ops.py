@@ -1010,6 +1010,38 @@ def din_dice_backward(x, grad_y, alpha, stats, epsilon):
     return gx, ga
 
 
+def din_fcn_input_forward(uid, item, his_sum, att, gamma, beta, scale):
+    """Model_DIN's fcn input + inference batch_normalization in one pass
+    (dr_din_fcn_input_forward) -> [B, Du + 4H]."""
+    dev = _dev(item)
+    B, H = item.shape
+    Du = uid.shape[1]
+    u, i, h, a = (_c(t, torch.float32) for t in (uid, item, his_sum, att))
+    gm, bt = _c(gamma, torch.float32), _c(beta, torch.float32)
+    out = torch.empty((B, Du + 4 * H), dtype=torch.float32, device=dev)
+    check(lib().dr_din_fcn_input_forward(ptr(u), ptr(i), ptr(h), ptr(a), ptr(gm), ptr(bt), B, Du,
+                                         H, float(scale), ptr(out), stream_handle(dev)))
+    _post(dev)
+    return out
+
+
+def din_fcn_input_backward(grad, uid, item, his_sum, att, gamma, scale):
+    """-> (g_uid, g_item, g_his_sum, g_att, g_gamma, g_beta)."""
+    dev = _dev(item)
+    B, H = item.shape
+    Du = uid.shape[1]
+    g = _c(grad, torch.float32)
+    u, i, h, a = (_c(t, torch.float32) for t in (uid, item, his_sum, att))
+    gm = _c(gamma, torch.float32)
+    e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)  # noqa: E731
+    gu, gi, gh, ga, gg, gb = e(B, Du), e(B, H), e(B, H), e(B, H), e(Du + 4 * H), e(Du + 4 * H)
+    check(lib().dr_din_fcn_input_backward(ptr(g), ptr(u), ptr(i), ptr(h), ptr(a), ptr(gm), B, Du,
+                                          H, float(scale), ptr(gu), ptr(gi), ptr(gh), ptr(ga),
+                                          ptr(gg), ptr(gb), stream_handle(dev)))
+    _post(dev)
+    return gu, gi, gh, ga, gg, gb
+
+
 def din_attention_pool(scores, mask, facts, with_sum=True):
     """Masked softmax over the history + weighted sum (din_attention, mode
     'SUM', utils.py:286-303) and the history sum (model.py:98) in one pass.

@@ -1239,6 +1239,22 @@ int dr_din_dice_backward(const float* x, const float* grad_y, const float* alpha
                          const float* stats, int64_t batch, int n, float epsilon, float* grad_x,
                          float* grad_alpha, void* stream);
 
+/* Model_DIN's fcn input (model.py:118-124): inp = [uid (uid_dim), item,    */
+/* his_sum, item * his_sum, att (hidden each)] per sample, then the           */
+/* inference-form batch_normalization out = (inp * scale) * gamma + beta     */
+/* (scale = 1 / sqrt(1 + 1e-3); gamma / beta [uid_dim + 4 hidden]); fp32,    */
+/* out [batch, uid_dim + 4 hidden].  The backward writes the four inputs'    */
+/* gradients and gamma / beta's (batch sums in a fixed order).               */
+int dr_din_fcn_input_forward(const float* uid, const float* item, const float* his_sum,
+                             const float* att, const float* gamma, const float* beta,
+                             int64_t batch, int uid_dim, int hidden, float scale, float* out,
+                             void* stream);
+int dr_din_fcn_input_backward(const float* grad, const float* uid, const float* item,
+                              const float* his_sum, const float* att, const float* gamma,
+                              int64_t batch, int uid_dim, int hidden, float scale, float* g_uid,
+                              float* g_item, float* g_his_sum, float* g_att, float* g_gamma,
+                              float* g_beta, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* String -> id, the step before the lookup.  Strings are one byte buffer    */
 /* plus int64 offsets[n+1] (string i = bytes[offsets[i] .. offsets[i+1])).   */

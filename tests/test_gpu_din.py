@@ -283,3 +283,29 @@ def test_din_dice_fused_matches_fp64(B, n):
     assert float((dice.alpha.grad.double().cpu() - ra.grad).abs().max()) <= 1e-4 * scale + 1e-5
     y2 = dice(gx_in.detach())
     assert torch.equal(y2, y.detach())
+
+
+@pytest.mark.parametrize("B,Du,H", [(4096, 18, 36), (7, 5, 16), (1, 0, 4)])
+def test_din_fcn_input_fused_matches_torch(B, Du, H):
+    """dr_din_fcn_input_forward / _backward (model.py:118-124: inp = [uid,
+    item, his_sum, item * his_sum, att], bn = inp * c * gamma + beta) against
+    the torch composition in fp64: output and all six gradients."""
+    from deeprec_amd import modelzoo as mz
+    g = torch.Generator(device="cpu").manual_seed(B + Du + H)
+    ts = [torch.randn(B, k, generator=g, dtype=torch.float64) for k in (Du, H, H, H)]
+    gamma = torch.randn(Du + 4 * H, generator=g, dtype=torch.float64)
+    beta = torch.randn(Du + 4 * H, generator=g, dtype=torch.float64)
+    gout = torch.randn(B, Du + 4 * H, generator=g, dtype=torch.float64)
+    c = 1.0 / (1.0 + 1e-3) ** 0.5
+    ref = [t.clone().requires_grad_(True) for t in ts + [gamma, beta]]
+    u, i, h, a, gm, bt = ref
+    (torch.cat([u, i, h, i * h, a], -1) * c * gm + bt).mul(gout).sum().backward()
+    got = [t.float().to(DEV).requires_grad_(True) for t in ts + [gamma, beta]]
+    out = mz._DinFcnInputFn.apply(*got, c)
+    want = torch.cat([u, i, h, i * h, a], -1) * c * gm + bt
+    torch.testing.assert_close(out.double().cpu(), want.detach(), rtol=1e-5, atol=1e-5)
+    out.backward(gout.float().to(DEV))
+    for name, x, r in zip(("uid", "item", "his_sum", "att", "gamma", "beta"), got, ref):
+        scale = float(r.grad.abs().max()) + 1e-12 if r.grad.numel() else 1.0
+        err = float((x.grad.double().cpu() - r.grad).abs().max()) if r.grad.numel() else 0.0
+        assert err <= 1e-5 * scale * max(1.0, B ** 0.5) + 1e-6, (name, err, scale)
