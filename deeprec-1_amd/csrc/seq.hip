@@ -925,19 +925,22 @@ __global__ __launch_bounds__(256, 3) void din_wgrad_mfma_kernel(
 static constexpr int kWgradBlocks = 1024;
 
 // ---- Dice (modelzoo/DIN/script/utils.py:12-35, batch statistics) ----------
-// One block per 16 columns, 64 row groups of 16 lanes (1024 threads, the
-// row loops unrolled 8 deep: the loads of a pass are in flight together --
-// a column's few thousand rows would otherwise be one dependent load chain
-// per thread): the column sums in a fixed order (per-thread partials over
-// rows rg, rg + 64, ..., then the 64 groups in order), so a column's
+// One block per 4 columns, 256 row groups (1024 threads; 50 blocks for a
+// 200-wide layer -- with 16 columns per block the 13 blocks' dependent load
+// chains set the time): each thread sums its rows rg, rg + 256, ... (loops
+// unrolled 8 deep), then a fixed LDS tree over the row groups -- a column's
 // statistics do not depend on timing.
-static constexpr int kDiceCols = 16, kDiceRg = 64;
+static constexpr int kDiceCols = 4, kDiceRg = 256;
 
 __device__ __forceinline__ float dice_col_sum(float v, float (*red)[kDiceCols], int rg, int cl) {
   red[rg][cl] = v;
   __syncthreads();
-  float t = 0.f;
-  for (int r = 0; r < kDiceRg; ++r) t += red[r][cl];
+#pragma unroll
+  for (int st = kDiceRg / 2; st > 0; st >>= 1) {
+    if (rg < st) red[rg][cl] += red[rg + st][cl];
+    __syncthreads();
+  }
+  const float t = red[0][cl];
   __syncthreads();
   return t;
 }
