@@ -3761,7 +3761,9 @@ int dr_xgmi_serve(const dr_xgmi_peers* peers, dr_ev* const* evs, int num_tables,
     hipLaunchKernelGGL((xgmi_emit_kernel<32, 4>), ge(32), dim3(256), 0, st, wa, w.rows);
   else
     hipLaunchKernelGGL((xgmi_emit_kernel<64, 4>), ge(64), dim3(256), 0, st, wa, w.rows);
-  hipLaunchKernelGGL(xgmi_flush_kernel, dim3(64), dim3(64), 0, st);
+  // (one rank: the rows stay on this device, whose next kernels see them
+  // after the kernel boundary -- no system-scope release needed)
+  if (W > 1) hipLaunchKernelGGL(xgmi_flush_kernel, dim3(64), dim3(64), 0, st);
   DR_LAUNCH_CHECK();
   return DR_OK;
 }

@@ -439,7 +439,11 @@ class NativeShardedLookup(object):
         p = C.c_void_p()
         check(lib().dr_sharded_output(self.h, C.byref(p)))
         dt = torch.bfloat16 if self.bf16 else torch.float32
-        return _lib.device_view(p.value, (self.batch, self.T * self.dim), dt, self.device)
+        v = getattr(self, "_out_view", None)
+        if v is None or v[0] != p.value or v[1] != dt:   # the engine's buffer is fixed: one view
+            self._out_view = (p.value, dt, _lib.device_view(p.value, (self.batch, self.T * self.dim),
+                                                            dt, self.device))
+        return self._out_view[2]
 
     def forward(self, ids, bag_offs=None, combiner="sum", need_grad=False, out_dtype=None,
                 copy=True):
@@ -541,6 +545,7 @@ class NativeShardedLookup(object):
         return out
 
     def close(self):
+        self._out_view = None
         if self.h is not None and self.h.value:
             lib().dr_sharded_destroy(self.h)
         self.h = None
