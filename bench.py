@@ -73,7 +73,7 @@ def parse():
     p.add_argument("--no-hybrid", dest="hybrid", action="store_false",
                    help="skip the real Criteo-TB cardinality leg with hybrid placement (small "
                         "features replicated, large ones row-sharded), run at every N")
-    p.add_argument("--native-steps", type=int, default=8,
+    p.add_argument("--native-steps", type=int, default=32,
                    help="timed forward steps of the native C-ABI engine over RCCL (0: skip)")
     p.add_argument("--dedup", action="store_true",
                    help="xgmi engine: per-destination dedup before the exchange (grouped Unique, "
@@ -176,6 +176,7 @@ def cpu_baseline(args):
     return {"value": med[False], "unit": "lookups/s", "cores": pool.threads, "kind": "port",
             "repeats": [round(v, 1) for v in runs[False]],
             "spread": round((max(runs[False]) - min(runs[False])) / med[False], 4),
+            "best": max(runs[False]),
             "serial_unique_value": med[True],
             "serial_unique_repeats": [round(v, 1) for v in runs[True]],
             "nproc": os.cpu_count(), "cpu_model": _cpu_model(),
@@ -184,7 +185,9 @@ def cpu_baseline(args):
                       "persistent %d-thread pool, oracle/deeprec_oracle.c "
                       "orc_pipeline_ev_lookup_sparse_pool (UniqueAliOp's default parallel "
                       "Unique + Shard-split KvResourceGather + ali SparseSegmentSum; value = "
-                      "median of the repeats, spread = (max - min) / median)"
+                      "median of the repeats, spread = (max - min) / median, best = the least "
+                      "disturbed repeat; the host is shared, so run-to-run differences are the "
+                      "box's load)"
                       % (total, B, R, D, reps, per, pool.threads)}
 
 
