@@ -690,3 +690,61 @@ def test_kv_adam_device_powers_equal_host_powers(dr, monkeypatch):
     for (k1, v1), (k2, v2) in zip(res[0], res[1]):
         np.testing.assert_array_equal(k1, k2)
         np.testing.assert_array_equal(v1.view(np.uint32), v2.view(np.uint32))
+
+
+def test_din_item_gradient_order_matches_oracle(dr, orc):
+    """Pins the order DIN's merged item lookup sums its gradient in: the
+    reference looks up the target items and the history separately
+    (model.py:61-98) and the optimizer sums the two IndexedSlices per id with
+    unsorted_segment_sum over their concatenation (optimizer.py
+    _deduplicate_indexed_slices; the CPU functor adds the rows in order) --
+    one serial chain per id over [target positions, history positions].
+    modelzoo.DIN's single lookup of [mids, mid_his] must give exactly that:
+    for the mid and cat EVs, the unique ids in first-occurrence order and
+    every per-id sum bit-equal to the oracle's serial segment sum of the same
+    allv gradient rows (hooked), padding id 0 included."""
+    from deeprec_amd import modelzoo as mz
+    B, T_, D = 64, 20, 18
+    R = (500, 300, 40)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(77)
+    evs = []
+    for i, r in enumerate(R):
+        ev = dr.EmbeddingVariable("dgo_%d" % i, D, 0.0, capacity=r + 4096, device=DEV)
+        ev.insert_synthetic(0, r, seed=900 + i)
+        evs.append(ev)
+    model = mz.DIN(*evs).to(DEV)
+    lens = torch.randint(1, T_ + 1, (B,), generator=g, device=DEV)
+    mask = (torch.arange(T_, device=DEV)[None, :] < lens[:, None]).float()
+    mh = torch.randint(1, R[1], (B, T_), generator=g, device=DEV) * mask.long()
+    ch = torch.randint(1, R[2], (B, T_), generator=g, device=DEV) * mask.long()
+    uids = torch.randint(0, R[0], (B,), generator=g, device=DEV)
+    mids = torch.randint(0, R[1], (B,), generator=g, device=DEV)
+    cats = torch.randint(0, R[2], (B,), generator=g, device=DEV)
+    lab = (torch.rand(B, generator=g, device=DEV) > 0.5).long()
+    target = torch.stack([lab, 1 - lab], 1).float()
+    grads = []
+    inner = model.item_lookup
+
+    class Hooked(object):
+        def __call__(self, ids):
+            out = inner(ids)
+            out.register_hook(lambda gr: grads.append(gr.detach().clone()))
+            return out
+    model.item_lookup = Hooked()
+    y = model(uids, mids, cats, mh, ch, mask)
+    (-(torch.log(y) * target).mean()).backward()
+    torch.cuda.synchronize()
+    assert len(grads) == 1
+    gall = H(grads[0])                                      # [B + B T, 2D]
+    for f, (tgt, his) in enumerate(((mids, mh), (cats, ch))):
+        ids = np.concatenate([H(tgt), H(his).reshape(-1)]).astype(np.int64)
+        uids_ref, idx = orc.unique(ids)
+        sl = evs[1 + f].pending_grads.pop()
+        U = int(sl.num_valid.item())
+        assert H(sl.indices[:U]).tolist() == uids_ref.tolist()
+        gf = np.ascontiguousarray(gall[:, f * D:(f + 1) * D])
+        ref = orc.sparse_segment_reduce_grad(gf, idx, np.arange(ids.size, dtype=np.int32), U,
+                                             "sum")
+        np.testing.assert_array_equal(H(sl.values[:U]).view(np.uint32), ref.view(np.uint32))
+    dr.status_check()
