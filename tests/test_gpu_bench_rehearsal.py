@@ -34,7 +34,7 @@ def test_bench_two_rank_rehearsal(engine):
            "--rows", "200000", "--batch", "8192", "--tables", "8", "--cpu-seconds", "0",
            "--check-rows", "4096", "--engine", engine.split("-")[0], "--train-steps", "3",
            "--hybrid-cap", "1000000", "--model-steps", "3", "--din-steps", "3",
-           "--din-batch", "1024"]
+           "--din-batch", "1024", "--native-steps", "4"]
     if engine == "xgmi-dedup":
         cmd += ["--dedup", "--zipf", "1.05"]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
