@@ -124,7 +124,7 @@ def cpu_baseline(args):
     CPU worker threads).  Unique is UniqueAliOp's default: ParallelComputeV1
     for N >= 14336 (unique_ali_op_util.h:651-657; serial_ = false,
     unique_ali_op.cc:55-56); the serial-Unique variant is timed beside it.
-    Five timed repeats each, interleaved (median reported, (max - min) /
+    Nine timed repeats each, interleaved (median reported, (max - min) /
     median as the spread); the id batches are drawn before timing.
     Threads: the box's CPU share (OMP_NUM_THREADS, else the affinity mask)."""
     from oracle import oracle as orc
@@ -141,7 +141,7 @@ def cpu_baseline(args):
     out = np.empty((B, D), np.float32)
     L = orc.lib()
     pool = orc.Pool(threads)
-    reps = 5
+    reps = 9   # short interleaved repeats: the median rides out bursts of host load
     per = args.cpu_seconds / (2 * reps)
 
     batches = [rng.integers(0, R, B).astype(np.int64) for _ in range(16)]
