@@ -195,3 +195,24 @@ def test_dlrm_graph_replays_interleaved_with_eager_model():
             assert _bits_equal(la[k], gl[k].detach()), (r, k, float(la[k]), float(gl[k]))
     _assert_same_state(_state(A[1], A[0]), _state(Bm[1], Bm[0]))
     dr.status_check(DEV)
+
+
+def test_adam_device_powers_prepare_and_sync():
+    """KV Adam's beta powers: prepare() creates the device copy eagerly (a
+    capture may then hold the first EV apply), _finish advances host and
+    device copies with the same fp32 roundings, and sync_host_powers() --
+    what a caller runs after graph replays, which advance only the device
+    copy -- reads them back unchanged."""
+    import deeprec_amd as dr
+    opt = dr.AdamOptimizer(0.001, beta1=0.9, beta2=0.999)
+    opt.prepare(DEV)
+    assert str(DEV) in opt._pw
+    for _ in range(3):
+        opt._finish()
+    h1, h2 = opt.b1p, opt.b2p
+    dev_pw = opt._pw[str(DEV)][0].tolist()
+    assert dev_pw == [h1, h2]
+    opt._pw[str(DEV)][0].mul_(opt._pw[str(DEV)][1])   # a replay's device-only advance
+    opt.sync_host_powers()
+    f32 = lambda x: torch.tensor(x, dtype=torch.float32)  # noqa: E731
+    assert opt.b1p == (f32(h1) * f32(0.9)).item() and opt.b2p == (f32(h2) * f32(0.999)).item()
