@@ -185,12 +185,15 @@ __device__ __forceinline__ void load_row_u(Row<VEC, G, CPL>& x, const float* p, 
 
 // One column's serial chain over the LDS stage sp[0, nv) (16-B aligned):
 // acc = acc + sp[0] + sp[1] + ... in order (fresh: the chain starts at
-// sp[0]).  The 16-B reads run 16 positions ahead of the adds in four fixed
+// sp[0]).  The 16-B reads run 32 positions ahead of the adds in eight fixed
 // registers, each reloaded right after its 4 adds, with counted lgkmcnt
-// waits -- as inline asm, because the compiler otherwise re-issued all four
+// waits -- as inline asm, because the compiler otherwise re-issued all the
 // reads and waited for them every 4 positions (~20 cycles per position
 // measured, against ~4-8 for the add chain).  The wait takes the register
-// it guards as an operand, so the adds cannot be scheduled above it.
+// it guards as an operand, so the adds cannot be scheduled above it.  (Four
+// registers / 16 positions ahead left the walk at ~11.8 cycles per position
+// in the DIN step, where 15 loader waves write the next stage into the same
+// LDS: the deeper window covers the longer read latency under that load.)
 #define DR_LDS4(R, A, OFF) \
   asm volatile("ds_read_b128 %0, %1 offset:" #OFF : "=v"(R) : "v"(A))
 #define DR_LGKM(N, R) asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(R))
@@ -202,33 +205,45 @@ __device__ __forceinline__ float chain_walk(const float* sp, int nv, bool& fresh
     jj = 1;
   }
   for (; jj < nv && (jj & 3); ++jj) acc = acc + sp[jj];
-  if (jj + 16 <= nv) {
+  if (jj + 32 <= nv) {
     typedef __attribute__((address_space(3))) const float lds_f;
     uint32_t a = (uint32_t)(size_t)(lds_f*)(sp + jj);
     // nothing of the compiler's own in flight: its wait pass then puts no
     // lgkmcnt(0) inside the loop (it does not see the asm reads)
     __builtin_amdgcn_s_waitcnt(0xC07F);
     typedef float f4v __attribute__((ext_vector_type(4)));
-    f4v r0, r1, r2, r3;
+    f4v r0, r1, r2, r3, r4, r5, r6, r7;
     DR_LDS4(r0, a, 0);
     DR_LDS4(r1, a, 16);
     DR_LDS4(r2, a, 32);
     DR_LDS4(r3, a, 48);
+    DR_LDS4(r4, a, 64);
+    DR_LDS4(r5, a, 80);
+    DR_LDS4(r6, a, 96);
+    DR_LDS4(r7, a, 112);
     auto add4 = [&](const f4v& v) {
       acc = acc + v.x; acc = acc + v.y; acc = acc + v.z; acc = acc + v.w;
     };
-    for (; jj + 32 <= nv; jj += 16) {
-      DR_LGKM(3, r0); add4(r0); DR_LDS4(r0, a, 64);
-      DR_LGKM(3, r1); add4(r1); DR_LDS4(r1, a, 80);
-      DR_LGKM(3, r2); add4(r2); DR_LDS4(r2, a, 96);
-      DR_LGKM(3, r3); add4(r3); DR_LDS4(r3, a, 112);
-      a += 64;
+    for (; jj + 64 <= nv; jj += 32) {
+      DR_LGKM(7, r0); add4(r0); DR_LDS4(r0, a, 128);
+      DR_LGKM(7, r1); add4(r1); DR_LDS4(r1, a, 144);
+      DR_LGKM(7, r2); add4(r2); DR_LDS4(r2, a, 160);
+      DR_LGKM(7, r3); add4(r3); DR_LDS4(r3, a, 176);
+      DR_LGKM(7, r4); add4(r4); DR_LDS4(r4, a, 192);
+      DR_LGKM(7, r5); add4(r5); DR_LDS4(r5, a, 208);
+      DR_LGKM(7, r6); add4(r6); DR_LDS4(r6, a, 224);
+      DR_LGKM(7, r7); add4(r7); DR_LDS4(r7, a, 240);
+      a += 128;
     }
-    DR_LGKM(3, r0); add4(r0);
-    DR_LGKM(2, r1); add4(r1);
-    DR_LGKM(1, r2); add4(r2);
-    DR_LGKM(0, r3); add4(r3);
-    jj += 16;
+    DR_LGKM(7, r0); add4(r0);
+    DR_LGKM(6, r1); add4(r1);
+    DR_LGKM(5, r2); add4(r2);
+    DR_LGKM(4, r3); add4(r3);
+    DR_LGKM(3, r4); add4(r4);
+    DR_LGKM(2, r5); add4(r5);
+    DR_LGKM(1, r6); add4(r6);
+    DR_LGKM(0, r7); add4(r7);
+    jj += 32;
   }
   for (; jj < nv; ++jj) acc = acc + sp[jj];
   return acc;
