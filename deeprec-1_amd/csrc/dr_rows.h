@@ -185,7 +185,7 @@ __device__ __forceinline__ void load_row_u(Row<VEC, G, CPL>& x, const float* p, 
 
 // One column's serial chain over the LDS stage sp[0, nv) (16-B aligned):
 // acc = acc + sp[0] + sp[1] + ... in order (fresh: the chain starts at
-// sp[0]).  The 16-B reads run 32 positions ahead of the adds in eight fixed
+// sp[0]).  The 16-B reads run 64 positions ahead of the adds in 16 fixed
 // registers, each reloaded right after its 4 adds, with counted lgkmcnt
 // waits -- as inline asm, because the compiler otherwise re-issued all the
 // reads and waited for them every 4 positions (~20 cycles per position
@@ -193,7 +193,10 @@ __device__ __forceinline__ void load_row_u(Row<VEC, G, CPL>& x, const float* p, 
 // it guards as an operand, so the adds cannot be scheduled above it.  (Four
 // registers / 16 positions ahead left the walk at ~11.8 cycles per position
 // in the DIN step, where 15 loader waves write the next stage into the same
-// LDS: the deeper window covers the longer read latency under that load.)
+// LDS: the deeper window covers the longer read latency under that load.
+// DIN's padding chain: 4 registers 1.00-1.01 ms, 8 0.92, 16 (the lgkmcnt
+// limit) 0.89 ms -- the 64 extra VGPRs spill a few loader registers in the
+// 1024-thread kernels, still the fastest; profiles/r06_seg_rounds_walk.log.)
 #define DR_LDS4(R, A, OFF) \
   asm volatile("ds_read_b128 %0, %1 offset:" #OFF : "=v"(R) : "v"(A))
 #define DR_LGKM(N, R) asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(R))
@@ -205,14 +208,14 @@ __device__ __forceinline__ float chain_walk(const float* sp, int nv, bool& fresh
     jj = 1;
   }
   for (; jj < nv && (jj & 3); ++jj) acc = acc + sp[jj];
-  if (jj + 32 <= nv) {
+  if (jj + 64 <= nv) {
     typedef __attribute__((address_space(3))) const float lds_f;
     uint32_t a = (uint32_t)(size_t)(lds_f*)(sp + jj);
     // nothing of the compiler's own in flight: its wait pass then puts no
     // lgkmcnt(0) inside the loop (it does not see the asm reads)
     __builtin_amdgcn_s_waitcnt(0xC07F);
     typedef float f4v __attribute__((ext_vector_type(4)));
-    f4v r0, r1, r2, r3, r4, r5, r6, r7;
+    f4v r0, r1, r2, r3, r4, r5, r6, r7, r8, r9, r10, r11, r12, r13, r14, r15;
     DR_LDS4(r0, a, 0);
     DR_LDS4(r1, a, 16);
     DR_LDS4(r2, a, 32);
@@ -221,29 +224,53 @@ __device__ __forceinline__ float chain_walk(const float* sp, int nv, bool& fresh
     DR_LDS4(r5, a, 80);
     DR_LDS4(r6, a, 96);
     DR_LDS4(r7, a, 112);
+    DR_LDS4(r8, a, 128);
+    DR_LDS4(r9, a, 144);
+    DR_LDS4(r10, a, 160);
+    DR_LDS4(r11, a, 176);
+    DR_LDS4(r12, a, 192);
+    DR_LDS4(r13, a, 208);
+    DR_LDS4(r14, a, 224);
+    DR_LDS4(r15, a, 240);
     auto add4 = [&](const f4v& v) {
       acc = acc + v.x; acc = acc + v.y; acc = acc + v.z; acc = acc + v.w;
     };
-    for (; jj + 64 <= nv; jj += 32) {
-      DR_LGKM(7, r0); add4(r0); DR_LDS4(r0, a, 128);
-      DR_LGKM(7, r1); add4(r1); DR_LDS4(r1, a, 144);
-      DR_LGKM(7, r2); add4(r2); DR_LDS4(r2, a, 160);
-      DR_LGKM(7, r3); add4(r3); DR_LDS4(r3, a, 176);
-      DR_LGKM(7, r4); add4(r4); DR_LDS4(r4, a, 192);
-      DR_LGKM(7, r5); add4(r5); DR_LDS4(r5, a, 208);
-      DR_LGKM(7, r6); add4(r6); DR_LDS4(r6, a, 224);
-      DR_LGKM(7, r7); add4(r7); DR_LDS4(r7, a, 240);
-      a += 128;
+    for (; jj + 128 <= nv; jj += 64) {
+      DR_LGKM(15, r0); add4(r0); DR_LDS4(r0, a, 256);
+      DR_LGKM(15, r1); add4(r1); DR_LDS4(r1, a, 272);
+      DR_LGKM(15, r2); add4(r2); DR_LDS4(r2, a, 288);
+      DR_LGKM(15, r3); add4(r3); DR_LDS4(r3, a, 304);
+      DR_LGKM(15, r4); add4(r4); DR_LDS4(r4, a, 320);
+      DR_LGKM(15, r5); add4(r5); DR_LDS4(r5, a, 336);
+      DR_LGKM(15, r6); add4(r6); DR_LDS4(r6, a, 352);
+      DR_LGKM(15, r7); add4(r7); DR_LDS4(r7, a, 368);
+      DR_LGKM(15, r8); add4(r8); DR_LDS4(r8, a, 384);
+      DR_LGKM(15, r9); add4(r9); DR_LDS4(r9, a, 400);
+      DR_LGKM(15, r10); add4(r10); DR_LDS4(r10, a, 416);
+      DR_LGKM(15, r11); add4(r11); DR_LDS4(r11, a, 432);
+      DR_LGKM(15, r12); add4(r12); DR_LDS4(r12, a, 448);
+      DR_LGKM(15, r13); add4(r13); DR_LDS4(r13, a, 464);
+      DR_LGKM(15, r14); add4(r14); DR_LDS4(r14, a, 480);
+      DR_LGKM(15, r15); add4(r15); DR_LDS4(r15, a, 496);
+      a += 256;
     }
-    DR_LGKM(7, r0); add4(r0);
-    DR_LGKM(6, r1); add4(r1);
-    DR_LGKM(5, r2); add4(r2);
-    DR_LGKM(4, r3); add4(r3);
-    DR_LGKM(3, r4); add4(r4);
-    DR_LGKM(2, r5); add4(r5);
-    DR_LGKM(1, r6); add4(r6);
-    DR_LGKM(0, r7); add4(r7);
-    jj += 32;
+    DR_LGKM(15, r0); add4(r0);
+    DR_LGKM(14, r1); add4(r1);
+    DR_LGKM(13, r2); add4(r2);
+    DR_LGKM(12, r3); add4(r3);
+    DR_LGKM(11, r4); add4(r4);
+    DR_LGKM(10, r5); add4(r5);
+    DR_LGKM(9, r6); add4(r6);
+    DR_LGKM(8, r7); add4(r7);
+    DR_LGKM(7, r8); add4(r8);
+    DR_LGKM(6, r9); add4(r9);
+    DR_LGKM(5, r10); add4(r10);
+    DR_LGKM(4, r11); add4(r11);
+    DR_LGKM(3, r12); add4(r12);
+    DR_LGKM(2, r13); add4(r13);
+    DR_LGKM(1, r14); add4(r14);
+    DR_LGKM(0, r15); add4(r15);
+    jj += 64;
   }
   for (; jj < nv; ++jj) acc = acc + sp[jj];
   return acc;
