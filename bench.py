@@ -1042,15 +1042,55 @@ def native_rccl_leg(args, evs, batches, engine, a2a, local_step, world, rank, di
             flag = torch.tensor([same], dtype=torch.int32, device="cpu" if staged else dev)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             same = int(flag.item())
+        # one GPU, host-read-free kinds: the forward as a hipGraph (as the
+        # headline step), kept only if every batch's replay equals the local
+        # lookup bit for bit (DR_NATIVE_GRAPH=0: eager)
+        graph, static, graph_note = None, None, None
+        if (world == 1 and not staged and kind in ("xgmi", "fixed")
+                and os.environ.get("DR_NATIVE_GRAPH", "1") == "1"):
+            try:
+                with torch.no_grad():
+                    for e_ in evs:   # a captured serve must not be able to grow a table
+                        e_.reserve(2 * B * world)
+                    torch.cuda.synchronize()
+                    static = batches[0].clone()
+                    s = torch.cuda.Stream()
+                    s.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(s):
+                        eng.forward(static, combiner="sum", copy=copy)
+                    torch.cuda.current_stream().wait_stream(s)
+                    gr = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gr):
+                        gout = eng.forward(static, combiner="sum", copy=copy)
+                    ok = True
+                    for k in range(len(batches)):
+                        static.copy_(batches[k])
+                        gr.replay()
+                        torch.cuda.synchronize()
+                        ok = ok and torch.equal(gout, local_step(k))
+                    graph = gr if ok else None
+                    graph_note = None if ok else "replay != local lookup: eager timed"
+            except Exception as e:  # noqa: BLE001 -- time the eager forward instead
+                graph, graph_note = None, "capture failed (%s: %s): eager timed" % (
+                    type(e).__name__, str(e)[:160])
+                torch.cuda.synchronize()
         with torch.no_grad():
             for k in range(2):
-                eng.forward(batches[k], combiner="sum", copy=copy)
+                if graph is not None:
+                    static.copy_(batches[k])
+                    graph.replay()
+                else:
+                    eng.forward(batches[k], combiner="sum", copy=copy)
             if dist is not None:
                 dist.barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for i in range(n):
-                eng.forward(batches[i % len(batches)], combiner="sum", copy=copy)
+                if graph is not None:
+                    static.copy_(batches[i % len(batches)])
+                    graph.replay()
+                else:
+                    eng.forward(batches[i % len(batches)], combiner="sum", copy=copy)
             if dist is not None:
                 dist.barrier()
             torch.cuda.synchronize()
@@ -1060,11 +1100,15 @@ def native_rccl_leg(args, evs, batches, engine, a2a, local_step, world, rank, di
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         st = eng.stats()
+        graphed = graph is not None
+        graph = static = None   # the graph holds the engine's buffers: drop it first
+        torch.cuda.synchronize()
         eng.close()
         res = {"engine_check": "native C-ABI engine (%s) == %s, %d batches, all ranks: %s" % (
                    kind, "all-to-all engine" if a2a is not None else "local fused lookup",
                    len(batches), bool(same)),
-               "ms_per_step": round(el / n * 1e3, 4), "steps": n,
+               "ms_per_step": round(el / n * 1e3, 4), "steps": n, "graph": graphed,
+               "graph_note": graph_note,
                "lookups_per_s": round(T * B * world * n / el, 1),
                "note": {"rccl": "reads the per-peer split sizes on the host once per step",
                         "xgmi": "route -> barrier -> owner serve (peer writes) -> barrier, "
