@@ -200,6 +200,7 @@ __device__ __forceinline__ void load_row_u(Row<VEC, G, CPL>& x, const float* p, 
 #define DR_LDS4(R, A, OFF) \
   asm volatile("ds_read_b128 %0, %1 offset:" #OFF : "=v"(R) : "v"(A))
 #define DR_LGKM(N, R) asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(R))
+#define DR_LGKM2(N, R, Q) asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(R), "+v"(Q))
 __device__ __forceinline__ float chain_walk(const float* sp, int nv, bool& fresh, float acc) {
   int jj = 0;
   if (fresh) {
@@ -236,22 +237,14 @@ __device__ __forceinline__ float chain_walk(const float* sp, int nv, bool& fresh
       acc = acc + v.x; acc = acc + v.y; acc = acc + v.z; acc = acc + v.w;
     };
     for (; jj + 128 <= nv; jj += 64) {
-      DR_LGKM(15, r0); add4(r0); DR_LDS4(r0, a, 256);
-      DR_LGKM(15, r1); add4(r1); DR_LDS4(r1, a, 272);
-      DR_LGKM(15, r2); add4(r2); DR_LDS4(r2, a, 288);
-      DR_LGKM(15, r3); add4(r3); DR_LDS4(r3, a, 304);
-      DR_LGKM(15, r4); add4(r4); DR_LDS4(r4, a, 320);
-      DR_LGKM(15, r5); add4(r5); DR_LDS4(r5, a, 336);
-      DR_LGKM(15, r6); add4(r6); DR_LDS4(r6, a, 352);
-      DR_LGKM(15, r7); add4(r7); DR_LDS4(r7, a, 368);
-      DR_LGKM(15, r8); add4(r8); DR_LDS4(r8, a, 384);
-      DR_LGKM(15, r9); add4(r9); DR_LDS4(r9, a, 400);
-      DR_LGKM(15, r10); add4(r10); DR_LDS4(r10, a, 416);
-      DR_LGKM(15, r11); add4(r11); DR_LDS4(r11, a, 432);
-      DR_LGKM(15, r12); add4(r12); DR_LDS4(r12, a, 448);
-      DR_LGKM(15, r13); add4(r13); DR_LDS4(r13, a, 464);
-      DR_LGKM(15, r14); add4(r14); DR_LDS4(r14, a, 480);
-      DR_LGKM(15, r15); add4(r15); DR_LDS4(r15, a, 496);
+      DR_LGKM2(14, r0, r1); add4(r0); add4(r1); DR_LDS4(r0, a, 256); DR_LDS4(r1, a, 272);
+      DR_LGKM2(14, r2, r3); add4(r2); add4(r3); DR_LDS4(r2, a, 288); DR_LDS4(r3, a, 304);
+      DR_LGKM2(14, r4, r5); add4(r4); add4(r5); DR_LDS4(r4, a, 320); DR_LDS4(r5, a, 336);
+      DR_LGKM2(14, r6, r7); add4(r6); add4(r7); DR_LDS4(r6, a, 352); DR_LDS4(r7, a, 368);
+      DR_LGKM2(14, r8, r9); add4(r8); add4(r9); DR_LDS4(r8, a, 384); DR_LDS4(r9, a, 400);
+      DR_LGKM2(14, r10, r11); add4(r10); add4(r11); DR_LDS4(r10, a, 416); DR_LDS4(r11, a, 432);
+      DR_LGKM2(14, r12, r13); add4(r12); add4(r13); DR_LDS4(r12, a, 448); DR_LDS4(r13, a, 464);
+      DR_LGKM2(14, r14, r15); add4(r14); add4(r15); DR_LDS4(r14, a, 480); DR_LDS4(r15, a, 496);
       a += 256;
     }
     DR_LGKM(15, r0); add4(r0);
@@ -277,5 +270,6 @@ __device__ __forceinline__ float chain_walk(const float* sp, int nv, bool& fresh
 }
 #undef DR_LDS4
 #undef DR_LGKM
+#undef DR_LGKM2
 
 }  // namespace dr
