@@ -237,32 +237,28 @@ __device__ __forceinline__ float chain_walk(const float* sp, int nv, bool& fresh
       acc = acc + v.x; acc = acc + v.y; acc = acc + v.z; acc = acc + v.w;
     };
     for (; jj + 128 <= nv; jj += 64) {
-      DR_LGKM2(14, r0, r1); add4(r0); add4(r1); DR_LDS4(r0, a, 256); DR_LDS4(r1, a, 272);
-      DR_LGKM2(14, r2, r3); add4(r2); add4(r3); DR_LDS4(r2, a, 288); DR_LDS4(r3, a, 304);
-      DR_LGKM2(14, r4, r5); add4(r4); add4(r5); DR_LDS4(r4, a, 320); DR_LDS4(r5, a, 336);
-      DR_LGKM2(14, r6, r7); add4(r6); add4(r7); DR_LDS4(r6, a, 352); DR_LDS4(r7, a, 368);
-      DR_LGKM2(14, r8, r9); add4(r8); add4(r9); DR_LDS4(r8, a, 384); DR_LDS4(r9, a, 400);
-      DR_LGKM2(14, r10, r11); add4(r10); add4(r11); DR_LDS4(r10, a, 416); DR_LDS4(r11, a, 432);
-      DR_LGKM2(14, r12, r13); add4(r12); add4(r13); DR_LDS4(r12, a, 448); DR_LDS4(r13, a, 464);
-      DR_LGKM2(14, r14, r15); add4(r14); add4(r15); DR_LDS4(r14, a, 480); DR_LDS4(r15, a, 496);
+      asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3)); add4(r0); add4(r1); add4(r2); add4(r3); DR_LDS4(r0, a, 256); DR_LDS4(r1, a, 272); DR_LDS4(r2, a, 288); DR_LDS4(r3, a, 304);
+      asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7)); add4(r4); add4(r5); add4(r6); add4(r7); DR_LDS4(r4, a, 320); DR_LDS4(r5, a, 336); DR_LDS4(r6, a, 352); DR_LDS4(r7, a, 368);
+      asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(r8), "+v"(r9), "+v"(r10), "+v"(r11)); add4(r8); add4(r9); add4(r10); add4(r11); DR_LDS4(r8, a, 384); DR_LDS4(r9, a, 400); DR_LDS4(r10, a, 416); DR_LDS4(r11, a, 432);
+      asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(r12), "+v"(r13), "+v"(r14), "+v"(r15)); add4(r12); add4(r13); add4(r14); add4(r15); DR_LDS4(r12, a, 448); DR_LDS4(r13, a, 464); DR_LDS4(r14, a, 480); DR_LDS4(r15, a, 496);
       a += 256;
     }
-    DR_LGKM(15, r0); add4(r0);
-    DR_LGKM(14, r1); add4(r1);
-    DR_LGKM(13, r2); add4(r2);
-    DR_LGKM(12, r3); add4(r3);
-    DR_LGKM(11, r4); add4(r4);
-    DR_LGKM(10, r5); add4(r5);
-    DR_LGKM(9, r6); add4(r6);
-    DR_LGKM(8, r7); add4(r7);
-    DR_LGKM(7, r8); add4(r8);
-    DR_LGKM(6, r9); add4(r9);
-    DR_LGKM(5, r10); add4(r10);
-    DR_LGKM(4, r11); add4(r11);
-    DR_LGKM(3, r12); add4(r12);
-    DR_LGKM(2, r13); add4(r13);
-    DR_LGKM(1, r14); add4(r14);
-    DR_LGKM(0, r15); add4(r15);
+    asm volatile("s_waitcnt lgkmcnt(15)" : "+v"(r0)); add4(r0);
+    asm volatile("s_waitcnt lgkmcnt(14)" : "+v"(r1)); add4(r1);
+    asm volatile("s_waitcnt lgkmcnt(13)" : "+v"(r2)); add4(r2);
+    asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(r3)); add4(r3);
+    asm volatile("s_waitcnt lgkmcnt(11)" : "+v"(r4)); add4(r4);
+    asm volatile("s_waitcnt lgkmcnt(10)" : "+v"(r5)); add4(r5);
+    asm volatile("s_waitcnt lgkmcnt(9)" : "+v"(r6)); add4(r6);
+    asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(r7)); add4(r7);
+    asm volatile("s_waitcnt lgkmcnt(7)" : "+v"(r8)); add4(r8);
+    asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(r9)); add4(r9);
+    asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(r10)); add4(r10);
+    asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(r11)); add4(r11);
+    asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(r12)); add4(r12);
+    asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(r13)); add4(r13);
+    asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(r14)); add4(r14);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r15)); add4(r15);
     jj += 64;
   }
   for (; jj < nv; ++jj) acc = acc + sp[jj];
