@@ -186,17 +186,15 @@ __device__ __forceinline__ void load_row_u(Row<VEC, G, CPL>& x, const float* p, 
 // One column's serial chain over the LDS stage sp[0, nv) (16-B aligned):
 // acc = acc + sp[0] + sp[1] + ... in order (fresh: the chain starts at
 // sp[0]).  The 16-B reads run 64 positions ahead of the adds in 16 fixed
-// registers, each reloaded right after its 4 adds, with counted lgkmcnt
-// waits -- as inline asm, because the compiler otherwise re-issued all the
-// reads and waited for them every 4 positions (~20 cycles per position
-// measured, against ~4-8 for the add chain).  The wait takes the register
-// it guards as an operand, so the adds cannot be scheduled above it.  (Four
-// registers / 16 positions ahead left the walk at ~11.8 cycles per position
-// in the DIN step, where 15 loader waves write the next stage into the same
-// LDS: the deeper window covers the longer read latency under that load.
-// DIN's padding chain: 4 registers 1.00-1.01 ms, 8 0.92, 16 (the lgkmcnt
-// limit) 0.89 ms -- the 64 extra VGPRs spill a few loader registers in the
-// 1024-thread kernels, still the fastest; profiles/r06_seg_rounds_walk.log.)
+// registers (the lgkmcnt limit), one counted wait per 8 registers (32
+// positions), each group reloaded right after its adds -- as inline asm,
+// because the compiler otherwise re-issued the reads and waited for them
+// every 4 positions.  The wait takes the registers it guards as operands, so
+// the adds cannot be scheduled above it.  The s_waitcnt itself was the cost:
+// DIN's padding chain (2 x 10^5 positions) took 1.00 ms with a wait per 4
+// positions and 4 registers, 0.90 with 16 registers, 0.74 / 0.65 / 0.62 ms
+// with a wait per 8 / 16 / 32 positions (7.4 cycles per position;
+// profiles/r06_seg_rounds_walk.log).
 #define DR_LDS4(R, A, OFF) \
   asm volatile("ds_read_b128 %0, %1 offset:" #OFF : "=v"(R) : "v"(A))
 #define DR_LGKM(N, R) asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(R))
@@ -237,10 +235,8 @@ __device__ __forceinline__ float chain_walk(const float* sp, int nv, bool& fresh
       acc = acc + v.x; acc = acc + v.y; acc = acc + v.z; acc = acc + v.w;
     };
     for (; jj + 128 <= nv; jj += 64) {
-      asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3)); add4(r0); add4(r1); add4(r2); add4(r3); DR_LDS4(r0, a, 256); DR_LDS4(r1, a, 272); DR_LDS4(r2, a, 288); DR_LDS4(r3, a, 304);
-      asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7)); add4(r4); add4(r5); add4(r6); add4(r7); DR_LDS4(r4, a, 320); DR_LDS4(r5, a, 336); DR_LDS4(r6, a, 352); DR_LDS4(r7, a, 368);
-      asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(r8), "+v"(r9), "+v"(r10), "+v"(r11)); add4(r8); add4(r9); add4(r10); add4(r11); DR_LDS4(r8, a, 384); DR_LDS4(r9, a, 400); DR_LDS4(r10, a, 416); DR_LDS4(r11, a, 432);
-      asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(r12), "+v"(r13), "+v"(r14), "+v"(r15)); add4(r12); add4(r13); add4(r14); add4(r15); DR_LDS4(r12, a, 448); DR_LDS4(r13, a, 464); DR_LDS4(r14, a, 480); DR_LDS4(r15, a, 496);
+      asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7)); add4(r0); add4(r1); add4(r2); add4(r3); add4(r4); add4(r5); add4(r6); add4(r7); DR_LDS4(r0, a, 256); DR_LDS4(r1, a, 272); DR_LDS4(r2, a, 288); DR_LDS4(r3, a, 304); DR_LDS4(r4, a, 320); DR_LDS4(r5, a, 336); DR_LDS4(r6, a, 352); DR_LDS4(r7, a, 368);
+      asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(r8), "+v"(r9), "+v"(r10), "+v"(r11), "+v"(r12), "+v"(r13), "+v"(r14), "+v"(r15)); add4(r8); add4(r9); add4(r10); add4(r11); add4(r12); add4(r13); add4(r14); add4(r15); DR_LDS4(r8, a, 384); DR_LDS4(r9, a, 400); DR_LDS4(r10, a, 416); DR_LDS4(r11, a, 432); DR_LDS4(r12, a, 448); DR_LDS4(r13, a, 464); DR_LDS4(r14, a, 480); DR_LDS4(r15, a, 496);
       a += 256;
     }
     asm volatile("s_waitcnt lgkmcnt(15)" : "+v"(r0)); add4(r0);
