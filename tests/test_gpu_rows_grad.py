@@ -748,3 +748,35 @@ def test_din_item_gradient_order_matches_oracle(dr, orc):
                                              "sum")
         np.testing.assert_array_equal(H(sl.values[:U]).view(np.uint32), ref.view(np.uint32))
     dr.status_check()
+
+
+@pytest.mark.parametrize("terms", ["din_pad_terms.npz", "din_pad_terms_s200.npz"])
+def test_rows_backward_real_din_padding_chain(dr, orc, terms):
+    """The padding id's chain with DIN's REAL gradient terms (tools/data:
+    one step of configs[3] at the first step and after 200 Adam steps,
+    dumped by tools/din_term_probe.py -- 4 050 segments, 203 800 positions,
+    D = 18), beside 30 000 positions on other ids, through the default walk
+    (64 positions read ahead, one counted LDS wait per 32): every per-id sum
+    bit-equal to the oracle's serial sum."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                             "tools", "data", terms))
+    tv, k = z["terms"].astype(np.float32), z["lens"].astype(np.int64)
+    D = tv.shape[1]
+    rng = np.random.default_rng(5)
+    other = rng.integers(1, 5000, 30000).astype(np.int64)
+    v = np.concatenate([np.zeros(int(k.sum()), np.int64), other])
+    g = np.concatenate([np.repeat(tv, k, axis=0),
+                        (rng.standard_normal((other.size, D)) * 1e-6).astype(np.float32)])
+    B = v.size
+    ind = np.stack([np.arange(B), np.zeros(B, np.int64)], 1)
+    ev = dr.EmbeddingVariable("rdinreal_%s" % terms[:-4], D, 0.1, capacity=8192)
+    out = dr.embedding_lookup_sparse(ev, dr.SparseTensor(T(ind), T(v), (B, 1)), combiner="sum")
+    out.backward(T(g))
+    uids, idx = orc.unique(v)
+    sl = ev.pending_grads.pop()
+    U = int(sl.num_valid.item())
+    assert H(sl.indices[:U]).tolist() == uids.tolist()
+    ref = orc.sparse_segment_reduce_grad(g, idx, np.arange(B, dtype=np.int32), U, "sum")
+    np.testing.assert_array_equal(H(sl.values[:U]).view(np.uint32), ref.view(np.uint32))
+    dr.status_check()
